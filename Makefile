@@ -1,0 +1,43 @@
+# Build: the HIP product library (gfx950) and the CPU oracle (test infrastructure).
+#   make            -> both
+#   make product    -> crdt-enc_amd/libcrdtenc.so
+#   make oracle     -> oracle/libce_oracle.so
+HIPCC      ?= /opt/rocm/bin/hipcc
+ARCH       ?= gfx950
+PKG        := crdt-enc_amd
+CSRC       := $(PKG)/csrc
+PRODUCT    := $(PKG)/libcrdtenc.so
+ORACLE     := oracle/libce_oracle.so
+
+HIP_SRCS   := $(wildcard $(CSRC)/*.hip)
+CPP_SRCS   := $(wildcard $(CSRC)/*.cpp)
+HDRS       := $(wildcard $(CSRC)/*.h) $(wildcard include/*.h)
+HIP_OBJS   := $(patsubst $(CSRC)/%.hip,$(PKG)/build/%.o,$(HIP_SRCS))
+CPP_OBJS   := $(patsubst $(CSRC)/%.cpp,$(PKG)/build/%.o,$(CPP_SRCS))
+
+HIPFLAGS   := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -I$(CSRC) -Wall -Wno-unused-function
+CXXFLAGS   := -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wall -Wno-unused-function -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include
+
+all: product oracle
+
+product: $(PRODUCT)
+oracle: $(ORACLE)
+
+$(PKG)/build/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(PKG)/build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(PKG)/build/%.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p $(PKG)/build
+	$(HIPCC) $(CXXFLAGS) -c $< -o $@
+
+$(PRODUCT): $(HIP_OBJS) $(CPP_OBJS)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread
+
+$(ORACLE): oracle/ce_oracle.c oracle/ce_oracle.h
+	gcc -O3 -march=x86-64-v3 -fPIC -shared -Wall -Wextra -o $@ oracle/ce_oracle.c -lpthread
+
+clean:
+	rm -rf $(PKG)/build $(PRODUCT) $(ORACLE)
+
+.PHONY: all product oracle clean
