@@ -16,7 +16,7 @@ HIP_OBJS   := $(patsubst $(CSRC)/%.hip,$(PKG)/build/%.o,$(HIP_SRCS))
 CPP_OBJS   := $(patsubst $(CSRC)/%.cpp,$(PKG)/build/%.o,$(CPP_SRCS))
 
 HIPFLAGS   := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -I$(CSRC) -Wall -Wno-unused-function
-CXXFLAGS   := -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wall -Wno-unused-function -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include
+CXXFLAGS   := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -I$(CSRC) -Wall -Wno-unused-function
 
 all: product oracle
 

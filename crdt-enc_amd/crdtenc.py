@@ -1,0 +1,421 @@
+"""ctypes binding of libcrdtenc.so (include/crdtenc.h) -- the MI355X hot path of crdt-enc.
+
+Mirrors the reference's plugin/Core interface (Rust, chpio/crdt-enc):
+  Cryptor  crdt-enc/src/cryptor.rs:11-27, EncHandler crdt-enc-xchacha20poly1305/src/lib.rs
+  Storage  crdt-enc/src/storage.rs:8-43,  tokio local dir crdt-enc-tokio/src/lib.rs
+  Core     crdt-enc/src/lib.rs (open, read_remote, compact, apply_ops, state bytes)
+
+There is no CPU fallback: loading fails loudly when the library is missing, and every
+cipher/fold call runs the gfx950 kernels (CE_ERR_DEVICE without a GPU).
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcrdtenc.so")
+
+OK = 0
+STATUS_NAMES = {
+    0: "OK", 1: "OUTER_LEN", 2: "OUTER_VERSION", 3: "KEY_VERSION", 4: "KEY_LEN",
+    5: "PARSE_VBOX", 6: "DATA_VERSION", 7: "PARSE_ENCBOX", 8: "NONCE_LEN", 9: "AUTH",
+    10: "PT_LEN", 11: "PT_VERSION", 12: "DECODE", 13: "OP_VERSION", 64: "INVALID_ARG",
+    65: "DEVICE", 66: "NO_KEY", 67: "IO", 68: "NO_LOCAL_META",
+}
+STATE_VCLOCK, STATE_GCOUNTER = 0, 1
+OPEN_CREATE, COMPACT_INGEST_FORMAT = 1, 2
+
+CORE_VERSION = bytes.fromhex("e834d789101b463498239de990a9051f")   # crdt-enc/src/lib.rs:26
+KEY_VERSION = bytes.fromhex("5df28591439a4cef8ca68433276cc9ed")    # xchacha lib.rs:13
+
+# symbols declared in include/crdtenc.h (checked by tests/test_abi.py)
+EXPORTS = [
+    "ce_buf_free", "ce_status_str", "ce_ctx_create", "ce_ctx_destroy", "ce_ctx_set_stream",
+    "ce_ctx_synchronize", "ce_ctx_last_error", "ce_cryptor_gen_key", "ce_cryptor_encrypt",
+    "ce_cryptor_decrypt", "ce_cryptor_sealed_len", "ce_cryptor_decrypt_batch",
+    "ce_cryptor_encrypt_batch", "ce_cryptor_decrypt_batch_device",
+    "ce_cryptor_encrypt_batch_device", "ce_storage_open", "ce_storage_close",
+    "ce_storage_list_op_actors", "ce_storage_load_ops", "ce_storage_store_ops",
+    "ce_storage_remove_ops", "ce_storage_list_state_names", "ce_storage_store_state",
+    "ce_storage_load_state", "ce_storage_remove_state", "ce_content_name", "ce_core_open",
+    "ce_core_close", "ce_core_set_latest_key", "ce_core_info_actor", "ce_core_read_remote",
+    "ce_core_compact", "ce_core_apply_ops", "ce_core_state_bytes", "ce_core_ingest_ops",
+    "ce_core_ingest_ops_device", "ce_core_ingest_states", "ce_core_compact_to_buffer",
+    "ce_core_register_actors", "ce_core_dense_capacity", "ce_core_export_dense",
+    "ce_core_import_dense", "ce_vbuf_init", "ce_vbuf_remaining", "ce_vbuf_chunk",
+    "ce_vbuf_advance", "ce_vbuf_chunks_vectored",
+]
+
+
+class CeError(RuntimeError):
+    def __init__(self, code, detail=""):
+        self.code = code
+        super().__init__("%s (%d)%s" % (STATUS_NAMES.get(code, "?"), code,
+                                        (": " + detail) if detail else ""))
+
+
+class Buf(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("len", ctypes.c_size_t)]
+
+
+class OpenOptions(ctypes.Structure):
+    _fields_ = [("state_kind", ctypes.c_int), ("supported_data_versions", ctypes.c_char_p),
+                ("n_supported", ctypes.c_size_t), ("current_data_version", ctypes.c_char_p),
+                ("local_path", ctypes.c_char_p), ("remote_path", ctypes.c_char_p),
+                ("flags", ctypes.c_uint32)]
+
+
+class VBuf(ctypes.Structure):
+    _fields_ = [("pos", ctypes.c_size_t), ("version", ctypes.c_uint8 * 16),
+                ("content", ctypes.c_void_p), ("content_len", ctypes.c_size_t)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("libcrdtenc.so not built (run `make -C %s product`); the product "
+                               "has no CPU fallback" % os.path.dirname(HERE))
+        L = ctypes.CDLL(LIB_PATH)
+        L.ce_status_str.restype = ctypes.c_char_p
+        L.ce_ctx_last_error.restype = ctypes.c_char_p
+        L.ce_cryptor_sealed_len.restype = ctypes.c_size_t
+        L.ce_cryptor_sealed_len.argtypes = [ctypes.c_size_t]
+        L.ce_core_dense_capacity.restype = ctypes.c_uint32
+        L.ce_vbuf_remaining.restype = ctypes.c_size_t
+        L.ce_vbuf_chunk.restype = ctypes.c_size_t
+        L.ce_vbuf_chunks_vectored.restype = ctypes.c_size_t
+        _lib = L
+    return _lib
+
+
+def _take(b):
+    data = ctypes.string_at(b.data, b.len) if b.len else b""
+    lib().ce_buf_free(ctypes.byref(b))
+    return data
+
+
+def _cbuf(b):
+    return ctypes.create_string_buffer(bytes(b), max(len(b), 1))
+
+
+def sealed_len(n):
+    return lib().ce_cryptor_sealed_len(n)
+
+
+def content_name(data):
+    out = ctypes.create_string_buffer(64)
+    rc = lib().ce_content_name(_cbuf(data), ctypes.c_size_t(len(data)), out)
+    if rc:
+        raise CeError(rc)
+    return out.value.decode()
+
+
+class Context:
+    """One per GPU (one process per GPU)."""
+
+    def __init__(self, device=0):
+        import weakref
+        self.p = ctypes.c_void_p()
+        self._cores = weakref.WeakSet()  # cores hold the context: close them first
+        rc = lib().ce_ctx_create(device, ctypes.byref(self.p))
+        if rc:
+            raise CeError(rc, "ce_ctx_create(device=%d)" % device)
+
+    def close(self):
+        if self.p:
+            for c in list(self._cores):
+                c.close()
+            lib().ce_ctx_destroy(self.p)
+            self.p = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def last_error(self):
+        return lib().ce_ctx_last_error(self.p).decode(errors="replace")
+
+    def check(self, rc, what=""):
+        if rc:
+            raise CeError(rc, "%s %s" % (what, self.last_error()))
+
+    def set_stream(self, stream_ptr):
+        self.check(lib().ce_ctx_set_stream(self.p, ctypes.c_void_p(stream_ptr)), "set_stream")
+
+    def synchronize(self):
+        lib().ce_ctx_synchronize(self.p)
+
+    # ---- Cryptor ----
+    def gen_key(self):
+        b = Buf()
+        self.check(lib().ce_cryptor_gen_key(self.p, ctypes.byref(b)), "gen_key")
+        vb = _take(b)
+        return vb[:16], vb[16:]
+
+    def encrypt(self, key, clear, nonce=None, key_version=KEY_VERSION):
+        b = Buf()
+        rc = lib().ce_cryptor_encrypt(self.p, _cbuf(key_version), _cbuf(key),
+                                      ctypes.c_size_t(len(key)),
+                                      _cbuf(nonce) if nonce is not None else None,
+                                      _cbuf(clear), ctypes.c_size_t(len(clear)), ctypes.byref(b))
+        self.check(rc, "encrypt")
+        return _take(b)
+
+    def decrypt(self, key, enc, key_version=KEY_VERSION):
+        """Returns (status, plaintext or None)."""
+        b = Buf()
+        rc = lib().ce_cryptor_decrypt(self.p, _cbuf(key_version), _cbuf(key),
+                                      ctypes.c_size_t(len(key)), _cbuf(enc),
+                                      ctypes.c_size_t(len(enc)), ctypes.byref(b))
+        if rc:
+            return rc, None
+        return 0, _take(b)
+
+    def decrypt_batch(self, key, items, key_version=KEY_VERSION):
+        """items: list of enc boxes.  Returns (rc, [status], [plaintext or None], out_blob)."""
+        n = len(items)
+        blob = b"".join(items)
+        offs = (ctypes.c_uint64 * (n + 1))()
+        o = 0
+        for i, it in enumerate(items):
+            offs[i] = o
+            o += len(it)
+        offs[n] = o
+        out = ctypes.create_string_buffer(o + 16 * n + 64)
+        oo = (ctypes.c_uint64 * max(n, 1))()
+        ol = (ctypes.c_uint64 * max(n, 1))()
+        st = (ctypes.c_int32 * max(n, 1))()
+        rc = lib().ce_cryptor_decrypt_batch(self.p, _cbuf(key_version), _cbuf(key),
+                                            ctypes.c_size_t(len(key)), _cbuf(blob), offs,
+                                            ctypes.c_uint32(n), out, oo, ol, st)
+        raw = out.raw
+        pts = [raw[oo[i]:oo[i] + ol[i]] if st[i] == 0 else None for i in range(n)]
+        return rc, list(st)[:n], pts, raw, [oo[i] for i in range(n)]
+
+    def encrypt_batch(self, key, clears, nonces=None, key_version=KEY_VERSION):
+        n = len(clears)
+        blob = b"".join(clears)
+        offs = (ctypes.c_uint64 * (n + 1))()
+        o = 0
+        for i, c in enumerate(clears):
+            offs[i] = o
+            o += len(c)
+        offs[n] = o
+        cap = sum(sealed_len(len(c)) for c in clears)
+        out = ctypes.create_string_buffer(max(cap, 1))
+        oo = (ctypes.c_uint64 * (n + 1))()
+        nb = _cbuf(b"".join(nonces)) if nonces is not None else None
+        rc = lib().ce_cryptor_encrypt_batch(self.p, _cbuf(key_version), _cbuf(key),
+                                            ctypes.c_size_t(len(key)), _cbuf(blob), offs,
+                                            ctypes.c_uint32(n), nb, out, ctypes.c_size_t(cap), oo)
+        self.check(rc, "encrypt_batch")
+        raw = out.raw
+        return [raw[oo[i]:oo[i + 1]] for i in range(n)]
+
+    def decrypt_batch_device(self, key, d_blob, d_offs, n, d_out, d_status=0,
+                             key_version=KEY_VERSION):
+        nf = ctypes.c_uint32(0)
+        rc = lib().ce_cryptor_decrypt_batch_device(
+            self.p, _cbuf(key_version), _cbuf(key), ctypes.c_size_t(len(key)),
+            ctypes.c_void_p(d_blob), ctypes.c_void_p(d_offs), ctypes.c_uint32(n),
+            ctypes.c_void_p(d_out), ctypes.c_void_p(d_status or None), ctypes.byref(nf))
+        self.check(rc, "decrypt_batch_device")
+        return nf.value
+
+    def encrypt_batch_device(self, key, d_clear, d_offs, n, d_nonces, d_out, d_out_offs,
+                             outer_version=None, key_version=KEY_VERSION):
+        rc = lib().ce_cryptor_encrypt_batch_device(
+            self.p, _cbuf(key_version), _cbuf(key), ctypes.c_size_t(len(key)),
+            _cbuf(outer_version) if outer_version is not None else None,
+            ctypes.c_void_p(d_clear), ctypes.c_void_p(d_offs), ctypes.c_uint32(n),
+            ctypes.c_void_p(d_nonces), ctypes.c_void_p(d_out), ctypes.c_void_p(d_out_offs))
+        self.check(rc, "encrypt_batch_device")
+
+
+class Storage:
+    """crdt-enc-tokio Storage (local dir)."""
+
+    def __init__(self, local_path, remote_path):
+        self.p = ctypes.c_void_p()
+        rc = lib().ce_storage_open(local_path.encode(), remote_path.encode(), ctypes.byref(self.p))
+        if rc:
+            raise CeError(rc, "ce_storage_open")
+
+    def __del__(self):
+        try:
+            lib().ce_storage_close(self.p)
+        except Exception:
+            pass
+
+    def list_op_actors(self):
+        b = Buf()
+        rc = lib().ce_storage_list_op_actors(self.p, ctypes.byref(b))
+        if rc:
+            raise CeError(rc)
+        d = _take(b)
+        return [d[i:i + 16] for i in range(0, len(d), 16)]
+
+    def load_ops(self, actor_first):
+        actors = b"".join(a for a, _ in actor_first)
+        m = len(actor_first)
+        first = (ctypes.c_uint64 * max(m, 1))(*[f for _, f in actor_first])
+        bufs = [Buf() for _ in range(4)]
+        rc = lib().ce_storage_load_ops(self.p, _cbuf(actors), first, ctypes.c_uint32(m),
+                                       *[ctypes.byref(x) for x in bufs])
+        if rc:
+            raise CeError(rc)
+        blob, offs, aidx, vers = [_take(x) for x in bufs]
+        import struct
+        o = struct.unpack("<%dQ" % (len(offs) // 8), offs)
+        ai = struct.unpack("<%dI" % (len(aidx) // 4), aidx)
+        vv = struct.unpack("<%dQ" % (len(vers) // 8), vers)
+        return [(actor_first[ai[i]][0], vv[i], blob[o[i]:o[i + 1]]) for i in range(len(ai))]
+
+    def store_ops(self, actor, version, data):
+        rc = lib().ce_storage_store_ops(self.p, _cbuf(actor), ctypes.c_uint64(version),
+                                        _cbuf(data), ctypes.c_size_t(len(data)))
+        if rc:
+            raise CeError(rc)
+
+    def list_state_names(self):
+        b = Buf()
+        rc = lib().ce_storage_list_state_names(self.p, ctypes.byref(b))
+        if rc:
+            raise CeError(rc)
+        d = _take(b)
+        return [x.decode() for x in d.split(b"\0") if x]
+
+    def store_state(self, data):
+        out = ctypes.create_string_buffer(64)
+        rc = lib().ce_storage_store_state(self.p, _cbuf(data), ctypes.c_size_t(len(data)), out)
+        if rc:
+            raise CeError(rc)
+        return out.value.decode()
+
+    def load_state(self, name):
+        b = Buf()
+        rc = lib().ce_storage_load_state(self.p, name.encode(), ctypes.byref(b))
+        if rc:
+            raise CeError(rc)
+        return _take(b)
+
+
+class Core:
+    """Core<S> for S in {VClock<Uuid>, GCounter<Uuid>} (crdt-enc/src/lib.rs)."""
+
+    def __init__(self, ctx, kind=STATE_GCOUNTER, supported=(), current_data_version=None,
+                 local_path=None, remote_path=None, flags=0):
+        self.ctx = ctx
+        sup = b"".join(supported)
+        cdv = current_data_version or (supported[0] if supported else bytes(16))
+        self._keep = [sup, cdv]
+        o = OpenOptions(kind, sup, len(supported), cdv,
+                        local_path.encode() if local_path else None,
+                        remote_path.encode() if remote_path else None, flags)
+        self.p = ctypes.c_void_p()
+        rc = lib().ce_core_open(ctx.p, ctypes.byref(o), ctypes.byref(self.p))
+        if rc:
+            raise CeError(rc, "ce_core_open " + ctx.last_error())
+        ctx._cores.add(self)
+
+    def close(self):
+        if self.p:
+            lib().ce_core_close(self.p)
+            self.p = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_latest_key(self, key, key_version=KEY_VERSION):
+        self.ctx.check(lib().ce_core_set_latest_key(self.p, _cbuf(key_version), _cbuf(key),
+                                                    ctypes.c_size_t(len(key))), "set_latest_key")
+
+    def info_actor(self):
+        out = ctypes.create_string_buffer(16)
+        self.ctx.check(lib().ce_core_info_actor(self.p, out), "info")
+        return out.raw
+
+    def state_bytes(self):
+        b = Buf()
+        self.ctx.check(lib().ce_core_state_bytes(self.p, ctypes.byref(b)), "state_bytes")
+        return _take(b)
+
+    def ingest_ops(self, files, actors, file_actor, versions, want_status=True):
+        n = len(files)
+        blob = b"".join(files)
+        offs = (ctypes.c_uint64 * (n + 1))()
+        o = 0
+        for i, f in enumerate(files):
+            offs[i] = o
+            o += len(f)
+        offs[n] = o
+        st = (ctypes.c_int32 * max(n, 1))() if want_status else None
+        fa = (ctypes.c_uint32 * max(n, 1))(*file_actor)
+        fv = (ctypes.c_uint64 * max(n, 1))(*versions)
+        rc = lib().ce_core_ingest_ops(self.p, _cbuf(blob), offs, ctypes.c_uint32(n),
+                                      _cbuf(b"".join(actors)), ctypes.c_uint32(len(actors)), fa,
+                                      fv, st)
+        return rc, (list(st)[:n] if want_status else None)
+
+    def ingest_ops_device(self, d_blob, d_offs, n, blob_len, actors, file_actor_arr,
+                          file_version_arr):
+        """file_actor_arr / file_version_arr: ctypes arrays (host)."""
+        return lib().ce_core_ingest_ops_device(
+            self.p, ctypes.c_void_p(d_blob), ctypes.c_void_p(d_offs), ctypes.c_uint32(n),
+            ctypes.c_uint64(blob_len), actors, ctypes.c_uint32(len(actors) // 16),
+            file_actor_arr, file_version_arr, None)
+
+    def ingest_states(self, files):
+        n = len(files)
+        blob = b"".join(files)
+        offs = (ctypes.c_uint64 * (n + 1))()
+        o = 0
+        for i, f in enumerate(files):
+            offs[i] = o
+            o += len(f)
+        offs[n] = o
+        st = (ctypes.c_int32 * max(n, 1))()
+        rc = lib().ce_core_ingest_states(self.p, _cbuf(blob), offs, ctypes.c_uint32(n), st)
+        return rc, list(st)[:n]
+
+    def read_remote(self):
+        return lib().ce_core_read_remote(self.p)
+
+    def compact(self):
+        name = ctypes.create_string_buffer(64)
+        rc = lib().ce_core_compact(self.p, name)
+        return rc, name.value.decode()
+
+    def compact_to_buffer(self, nonce=None):
+        b = Buf()
+        name = ctypes.create_string_buffer(64)
+        rc = lib().ce_core_compact_to_buffer(self.p, _cbuf(nonce) if nonce is not None else None,
+                                             ctypes.byref(b), name)
+        self.ctx.check(rc, "compact_to_buffer")
+        return _take(b), name.value.decode()
+
+    def apply_ops(self, ops_msgpack):
+        return lib().ce_core_apply_ops(self.p, _cbuf(ops_msgpack), ctypes.c_size_t(len(ops_msgpack)))
+
+    def register_actors(self, actors):
+        self.ctx.check(lib().ce_core_register_actors(self.p, _cbuf(b"".join(actors)),
+                                                     ctypes.c_uint32(len(actors))), "register")
+
+    def dense_capacity(self):
+        return lib().ce_core_dense_capacity(self.p)
+
+    def export_dense(self, d_state, d_nov):
+        self.ctx.check(lib().ce_core_export_dense(self.p, ctypes.c_void_p(d_state),
+                                                  ctypes.c_void_p(d_nov)), "export_dense")
+
+    def import_dense(self, d_state, d_nov):
+        self.ctx.check(lib().ce_core_import_dense(self.p, ctypes.c_void_p(d_state),
+                                                  ctypes.c_void_p(d_nov)), "import_dense")

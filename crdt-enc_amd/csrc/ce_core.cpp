@@ -1,0 +1,1111 @@
+// ce_core.cpp -- Core<S, Storage, Cryptor, _> (crdt-enc/src/lib.rs:188-723) for S in
+// {VClock<Uuid>, GCounter<Uuid>}, driving the GPU batch engine.
+//
+// State layout: a host-built open-addressing actor table (UUID -> dense slot) mirrored in HBM;
+// the CRDT state (VClock dots / GCounter.inner) is a dense u64[cap] max-register array in HBM;
+// next_op_versions (lib.rs:741) is a dense u64[cap] on the host (the version gate runs there
+// while the GPU decrypts).  Serialization sorts slots by UUID bytes = BTreeMap order.
+#include <algorithm>
+#include <cstdio>
+#include <functional>
+#include <set>
+
+#include "ce_internal.h"
+
+namespace ce {
+int storage_load_ops_vec(ce_storage* s, const std::vector<Uuid>& actors,
+                         const std::vector<uint64_t>& first, std::vector<uint8_t>* blob,
+                         std::vector<uint64_t>* offs, std::vector<uint32_t>* aidx,
+                         std::vector<uint64_t>* vers);
+int storage_list_op_actors_vec(ce_storage* s, std::vector<Uuid>* out);
+int storage_list_states_vec(ce_storage* s, std::vector<std::string>* out);
+int storage_read_state(ce_storage* s, const std::string& name, std::vector<uint8_t>* out);
+int storage_store_content(ce_storage* s, const char* sub, const uint8_t* d, size_t n,
+                          std::string* name);
+int storage_remove_state(ce_storage* s, const std::string& name);
+int storage_store_op(ce_storage* s, const Uuid& actor, uint64_t version, const uint8_t* d,
+                     size_t n);
+int storage_remove_op(ce_storage* s, const Uuid& actor, uint64_t version);
+int storage_load_local_meta(ce_storage* s, std::vector<uint8_t>* out, bool* missing);
+int storage_store_local_meta(ce_storage* s, const uint8_t* d, size_t n);
+ce_storage* storage_new(const std::string& local, const std::string& remote);
+}  // namespace ce
+
+using namespace ce;
+
+struct ce_core {
+  ce_ctx* ctx = nullptr;
+  int kind = CE_STATE_GCOUNTER;
+  std::vector<Uuid> supported;  // sorted (lib.rs:227-228)
+  Uuid current_data_version{};
+  ce_storage* storage = nullptr;
+  uint32_t flags = 0;
+  Uuid local_actor{};
+  bool has_key = false;
+  uint8_t key_version[16] = {0};
+  std::vector<uint8_t> key;
+  // actor table
+  uint32_t cap = 0, size = 0, registered = 0;
+  std::vector<ActorSlot> h_table;
+  std::vector<Uuid> slot_actor;
+  std::vector<uint64_t> nov;  // next_op_versions by slot
+  std::unordered_map<Uuid, uint32_t, UuidHash> slot_of;
+  bool table_dirty = true;
+  DevBuf d_table, d_state, d_batch, d_supported, d_refold2, d_tmp;
+  std::set<std::string> read_states;  // lib.rs:205
+  ce_ctx* aux = nullptr;              // single-file work during a batch (exotic envelopes)
+};
+
+namespace {
+
+// ---------------------------------------------------------------------------------------
+// msgpack writer (rmp-serde to_vec_named)
+// ---------------------------------------------------------------------------------------
+struct Wr {
+  std::vector<uint8_t> b;
+  void u8(uint8_t v) { b.push_back(v); }
+  void be(uint64_t v, int k) {
+    for (int j = k - 1; j >= 0; j--) b.push_back((uint8_t)(v >> (8 * j)));
+  }
+  void uint(uint64_t v) {
+    if (v <= 0x7f) u8((uint8_t)v);
+    else if (v <= 0xff) { u8(0xcc); be(v, 1); }
+    else if (v <= 0xffff) { u8(0xcd); be(v, 2); }
+    else if (v <= 0xffffffffull) { u8(0xce); be(v, 4); }
+    else { u8(0xcf); be(v, 8); }
+  }
+  void str(const char* s) {
+    const size_t l = std::strlen(s);
+    u8((uint8_t)(0xa0 | l));
+    b.insert(b.end(), s, s + l);
+  }
+  void bin(const uint8_t* d, size_t l) {
+    if (l <= 0xff) { u8(0xc4); be(l, 1); }
+    else if (l <= 0xffff) { u8(0xc5); be(l, 2); }
+    else { u8(0xc6); be(l, 4); }
+    b.insert(b.end(), d, d + l);
+  }
+  void map(size_t n) {
+    if (n <= 15) u8((uint8_t)(0x80 | n));
+    else if (n <= 0xffff) { u8(0xde); be(n, 2); }
+    else { u8(0xdf); be(n, 4); }
+  }
+};
+
+// ---------------------------------------------------------------------------------------
+// host-side msgpack reading (states, local ops, local meta, exotic envelopes)
+// ---------------------------------------------------------------------------------------
+// skip one value, recursion depth bounded like rmp-serde's default (1024)
+bool skip_any(Rd& r, int depth = 0) {
+  if (depth > 1024) return false;
+  uint64_t at, cnt = 0;
+  if (r.i >= r.n) return false;
+  const uint8_t m = r.p[r.i];
+  bool cont = false;
+  if ((m & 0xf0) == 0x80) { r.i++; cnt = 2ull * (m & 15); cont = true; }
+  else if ((m & 0xf0) == 0x90) { r.i++; cnt = m & 15; cont = true; }
+  else if (m == 0xdc || m == 0xdd || m == 0xde || m == 0xdf) {
+    r.i++;
+    if (!rd_be(r, (m == 0xdc || m == 0xde) ? 2 : 4, &cnt)) return false;
+    if (m >= 0xde) cnt *= 2;
+    cont = true;
+  }
+  if (cont) {
+    for (uint64_t k = 0; k < cnt; k++)
+      if (!skip_any(r, depth + 1)) return false;
+    return true;
+  }
+  Rd q = r;
+  int s = rd_skip(q);  // scalar / bin / str / ext: no recursion needed
+  if (s != 1) return false;
+  r = q;
+  (void)at;
+  return true;
+}
+
+// serde_bytes Cow<[u8]> in any accepted form (bin, str, array of u8)
+bool bytes_any(Rd& r, std::vector<uint8_t>* out) {
+  if (r.i >= r.n) return false;
+  if (is_array_marker(r.p[r.i])) {
+    uint64_t cnt, v;
+    if (!rd_array_hdr(r, &cnt) || cnt > r.n) return false;
+    out->clear();
+    for (uint64_t k = 0; k < cnt; k++) {
+      if (!rd_u64(r, &v) || v > 255) return false;
+      out->push_back((uint8_t)v);
+    }
+    return true;
+  }
+  int kind;
+  uint64_t off, len;
+  if (!rd_binstr(r, &kind, &off, &len)) return false;
+  out->assign(r.p + off, r.p + off + len);
+  return true;
+}
+
+// derive(Deserialize) struct: map (any key order; unknown ignored; duplicates rejected) or
+// array of exactly nf.  cb(field, rd) reads a value.
+bool read_struct(Rd& r, const std::vector<const char*>& names,
+                 const std::function<bool(int, Rd&)>& cb) {
+  const int nf = (int)names.size();
+  if (r.i >= r.n) return false;
+  uint64_t cnt;
+  if (is_array_marker(r.p[r.i])) {
+    if (!rd_array_hdr(r, &cnt) || cnt != (uint64_t)nf) return false;
+    for (int f = 0; f < nf; f++)
+      if (!cb(f, r)) return false;
+    return true;
+  }
+  if (!rd_map_hdr(r, &cnt)) return false;
+  unsigned seen = 0;
+  for (uint64_t k = 0; k < cnt; k++) {
+    int f;
+    const uint8_t m = r.i < r.n ? r.p[r.i] : 0xc1;
+    if (is_binstr_marker(m)) {
+      int kind;
+      uint64_t off, l;
+      if (!rd_binstr(r, &kind, &off, &l)) return false;
+      f = nf;
+      for (int j = 0; j < nf; j++)
+        if (std::strlen(names[j]) == l && std::memcmp(names[j], r.p + off, l) == 0) f = j;
+    } else {
+      uint64_t v;
+      if (!rd_u64(r, &v)) return false;
+      f = v < (uint64_t)nf ? (int)v : nf;
+    }
+    if (f == nf) {
+      if (!skip_any(r)) return false;
+      continue;
+    }
+    if (seen & (1u << f)) return false;
+    seen |= 1u << f;
+    if (!cb(f, r)) return false;
+  }
+  return seen == (1u << nf) - 1;
+}
+
+using Dots = std::vector<std::pair<Uuid, uint64_t>>;
+
+// VClock { dots: BTreeMap<Uuid, u64> }: later duplicate keys overwrite earlier ones
+bool read_vclock(Rd& r, Dots* out) {
+  return read_struct(r, {"dots"}, [&](int, Rd& q) {
+    uint64_t cnt;
+    if (!rd_map_hdr(q, &cnt)) return false;
+    std::unordered_map<Uuid, size_t, UuidHash> idx;
+    for (uint64_t k = 0; k < cnt; k++) {
+      uint64_t off, c;
+      if (!rd_uuid(q, &off) || !rd_u64(q, &c)) return false;
+      Uuid u;
+      std::memcpy(u.data(), q.p + off, 16);
+      auto it = idx.find(u);
+      if (it != idx.end()) out->at(it->second).second = c;
+      else { idx[u] = out->size(); out->push_back({u, c}); }
+    }
+    return true;
+  });
+}
+
+// StateWrapper<S> { next_op_versions: VClock, state: S } (lib.rs:739-743)
+bool read_state_wrapper(const uint8_t* p, size_t n, int kind, Dots* nov, Dots* st) {
+  Rd r{p, n, 0};
+  return read_struct(r, {"next_op_versions", "state"}, [&](int f, Rd& q) {
+    if (f == 0) return read_vclock(q, nov);
+    if (kind == CE_STATE_GCOUNTER)
+      return read_struct(q, {"inner"}, [&](int, Rd& q2) { return read_vclock(q2, st); });
+    return read_vclock(q, st);
+  });
+}
+
+// Vec<Dot<Uuid>> (lib.rs:507)
+bool read_dots(const uint8_t* p, size_t n, Dots* out) {
+  Rd r{p, n, 0};
+  uint64_t cnt;
+  if (!rd_array_hdr(r, &cnt) || cnt > n) return false;
+  for (uint64_t k = 0; k < cnt; k++) {
+    uint64_t aoff = 0, c = 0;
+    Rd q = r;
+    int ok = parse_dot(q, &aoff, &c);
+    if (ok < 0) {
+      // too deep for the shared parser's bounded stack: host recursion
+      bool has_a = false, has_c = false;
+      Uuid a{};
+      if (!read_struct(r, {"actor", "counter"}, [&](int f, Rd& s) {
+            if (f == 0) {
+              uint64_t o;
+              if (!rd_uuid(s, &o)) return false;
+              std::memcpy(a.data(), s.p + o, 16);
+              has_a = true;
+              return true;
+            }
+            has_c = true;
+            return rd_u64(s, &c);
+          }) || !has_a || !has_c)
+        return false;
+      out->push_back({a, c});
+      continue;
+    }
+    if (ok == 0) return false;
+    Uuid a;
+    std::memcpy(a.data(), q.p + aoff, 16);
+    out->push_back({a, c});
+    r = q;
+  }
+  return true;
+}
+
+// Cryptor envelope in any accepted encoding -> canonical bytes (device decodes only the
+// in-place forms; an array-of-u8 byte string or deep nesting comes here).
+int32_t normalize_envelope(const uint8_t* enc, size_t len, std::vector<uint8_t>* canon) {
+  Rd r{enc, len, 0};
+  uint64_t cnt;
+  if (r.n == 0 || !is_array_marker(r.p[0]) || !rd_array_hdr(r, &cnt) || cnt != 2)
+    return CE_ERR_PARSE_VBOX;
+  uint64_t voff;
+  std::vector<uint8_t> box;
+  if (!rd_uuid(r, &voff) || !bytes_any(r, &box)) return CE_ERR_PARSE_VBOX;
+  if (std::memcmp(enc + voff, kBoxVersion, 16) != 0) return CE_ERR_DATA_VERSION;
+  std::vector<uint8_t> nonce, ed;
+  Rd q{box.data(), box.size(), 0};
+  if (!read_struct(q, {"nonce", "enc_data"},
+                   [&](int f, Rd& s) { return bytes_any(s, f == 0 ? &nonce : &ed); }))
+    return CE_ERR_PARSE_ENCBOX;
+  if (nonce.size() != 24) return CE_ERR_NONCE_LEN;
+  if (ed.size() < 16) return CE_ERR_AUTH;
+  canon->resize(128);
+  const uint64_t h = put_envelope_header(canon->data(), ed.size() - 16, nonce.data());
+  canon->resize(h);
+  canon->insert(canon->end(), ed.begin(), ed.end());
+  return CE_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// actor table
+// ---------------------------------------------------------------------------------------
+uint32_t probe_slot(const std::vector<ActorSlot>& t, uint32_t mask, const Uuid& u, bool* found) {
+  uint32_t w[4];
+  std::memcpy(w, u.data(), 16);
+  uint32_t h = actor_hash(w[0], w[1], w[2], w[3]) & mask;
+  for (;;) {
+    if (!t[h].used) { *found = false; return h; }
+    if (std::memcmp(t[h].k, w, 16) == 0) { *found = true; return h; }
+    h = (h + 1) & mask;
+  }
+}
+
+int table_init(ce_core* c, uint32_t cap) {
+  c->cap = cap;
+  c->size = 0;
+  c->h_table.assign(cap, ActorSlot{});
+  c->slot_actor.assign(cap, Uuid{});
+  c->nov.assign(cap, 0);
+  c->slot_of.clear();
+  c->table_dirty = true;
+  hipError_t e;
+  if ((e = c->d_table.reserve(cap * sizeof(ActorSlot))) || (e = c->d_state.reserve(cap * 8ull)) ||
+      (e = c->d_batch.reserve(cap * 8ull)) || (e = c->d_tmp.reserve(cap * 8ull)))
+    return c->ctx->hip_fail(e, "actor table");
+  if ((e = hipMemsetAsync(c->d_state.p, 0, cap * 8ull, c->ctx->stream)))
+    return c->ctx->hip_fail(e, "actor table");
+  return CE_OK;
+}
+
+int table_upload(ce_core* c) {
+  if (!c->table_dirty) return CE_OK;
+  hipError_t e = hipMemcpyAsync(c->d_table.p, c->h_table.data(), c->cap * sizeof(ActorSlot),
+                                hipMemcpyHostToDevice, c->ctx->stream);
+  if (e) return c->ctx->hip_fail(e, "table upload");
+  // the host vector may be rewritten before the copy runs: wait (table changes are rare)
+  if ((e = hipStreamSynchronize(c->ctx->stream))) return c->ctx->hip_fail(e, "table upload");
+  c->table_dirty = false;
+  return CE_OK;
+}
+
+int table_grow(ce_core* c) {
+  // rehash into 2x capacity; move the dense state (device) and nov (host) with it
+  const uint32_t old_cap = c->cap;
+  std::vector<uint64_t> st(old_cap);
+  hipError_t e;
+  if ((e = hipMemcpyAsync(st.data(), c->d_state.p, old_cap * 8ull, hipMemcpyDeviceToHost,
+                          c->ctx->stream)) ||
+      (e = hipStreamSynchronize(c->ctx->stream)))
+    return c->ctx->hip_fail(e, "grow");
+  std::vector<Uuid> actors;
+  std::vector<uint64_t> nov, sv;
+  for (uint32_t s = 0; s < old_cap; s++)
+    if (c->h_table[s].used) { actors.push_back(c->slot_actor[s]); nov.push_back(c->nov[s]); sv.push_back(st[s]); }
+  // keep insertion order stable: re-insert in the old slot order
+  const uint32_t reg = c->registered;
+  DevBuf keep_state;
+  int rc = table_init(c, old_cap * 2);
+  if (rc) return rc;
+  std::vector<uint64_t> nst(c->cap, 0);
+  for (size_t i = 0; i < actors.size(); i++) {
+    bool found;
+    const uint32_t s = probe_slot(c->h_table, c->cap - 1, actors[i], &found);
+    std::memcpy(c->h_table[s].k, actors[i].data(), 16);
+    c->h_table[s].used = 1;
+    c->slot_actor[s] = actors[i];
+    c->slot_of[actors[i]] = s;
+    c->nov[s] = nov[i];
+    nst[s] = sv[i];
+    c->size++;
+  }
+  c->registered = reg;
+  if ((e = hipMemcpyAsync(c->d_state.p, nst.data(), c->cap * 8ull, hipMemcpyHostToDevice,
+                          c->ctx->stream)) ||
+      (e = hipStreamSynchronize(c->ctx->stream)))
+    return c->ctx->hip_fail(e, "grow");
+  return CE_OK;
+}
+
+int insert_actor(ce_core* c, const Uuid& u, uint32_t* slot) {
+  auto it = c->slot_of.find(u);
+  if (it != c->slot_of.end()) { *slot = it->second; return CE_OK; }
+  if ((c->size + 1) * 2 > c->cap) {
+    int rc = table_grow(c);
+    if (rc) return rc;
+  }
+  bool found;
+  const uint32_t s = probe_slot(c->h_table, c->cap - 1, u, &found);
+  std::memcpy(c->h_table[s].k, u.data(), 16);
+  c->h_table[s].used = 1;
+  c->slot_actor[s] = u;
+  c->slot_of[u] = s;
+  c->size++;
+  c->table_dirty = true;
+  *slot = s;
+  return CE_OK;
+}
+
+int download_state(ce_core* c, std::vector<uint64_t>* st) {
+  st->resize(c->cap);
+  hipError_t e;
+  if ((e = hipMemcpyAsync(st->data(), c->d_state.p, c->cap * 8ull, hipMemcpyDeviceToHost,
+                          c->ctx->stream)) ||
+      (e = hipStreamSynchronize(c->ctx->stream)))
+    return c->ctx->hip_fail(e, "state download");
+  return CE_OK;
+}
+
+// max-merge host dots into the device state (VClock::merge / apply)
+int merge_dots_host(ce_core* c, const Dots& dots) {
+  if (dots.empty()) return CE_OK;
+  std::vector<std::pair<uint32_t, uint64_t>> sv;
+  for (auto& d : dots) {
+    uint32_t s;
+    int rc = insert_actor(c, d.first, &s);
+    if (rc) return rc;
+    sv.push_back({s, d.second});
+  }
+  std::vector<uint64_t> dense(c->cap, 0);
+  for (auto& p : sv) dense[p.first] = std::max(dense[p.first], p.second);
+  hipError_t e;
+  if ((e = hipMemcpyAsync(c->d_tmp.p, dense.data(), c->cap * 8ull, hipMemcpyHostToDevice,
+                          c->ctx->stream)) ||
+      (e = launch_merge_max(c->ctx->stream, c->d_state.as<unsigned long long>(),
+                            c->d_tmp.as<unsigned long long>(), c->cap)) ||
+      (e = hipStreamSynchronize(c->ctx->stream)))
+    return c->ctx->hip_fail(e, "merge dots");
+  return CE_OK;
+}
+
+int serialize_state(ce_core* c, std::vector<uint8_t>* out) {
+  std::vector<uint64_t> st;
+  int rc = download_state(c, &st);
+  if (rc) return rc;
+  std::vector<uint32_t> slots;
+  for (uint32_t s = 0; s < c->cap; s++)
+    if (c->h_table[s].used) slots.push_back(s);
+  std::sort(slots.begin(), slots.end(),
+            [&](uint32_t a, uint32_t b) { return c->slot_actor[a] < c->slot_actor[b]; });
+  size_t n_nov = 0, n_st = 0;
+  for (uint32_t s : slots) { n_nov += c->nov[s] != 0; n_st += st[s] != 0; }
+  Wr w;
+  w.map(2);
+  w.str("next_op_versions");
+  w.map(1);
+  w.str("dots");
+  w.map(n_nov);
+  for (uint32_t s : slots)
+    if (c->nov[s]) { w.bin(c->slot_actor[s].data(), 16); w.uint(c->nov[s]); }
+  w.str("state");
+  if (c->kind == CE_STATE_GCOUNTER) { w.map(1); w.str("inner"); }
+  w.map(1);
+  w.str("dots");
+  w.map(n_st);
+  for (uint32_t s : slots)
+    if (st[s]) { w.bin(c->slot_actor[s].data(), 16); w.uint(st[s]); }
+  *out = std::move(w.b);
+  return CE_OK;
+}
+
+KeyRef key_of(ce_core* c) { return KeyRef{c->key_version, c->key.data(), c->key.size()}; }
+
+ce_ctx* aux_ctx(ce_core* c) {
+  if (!c->aux) {
+    c->aux = new ce_ctx();
+    c->aux->device = c->ctx->device;
+    c->aux->stream = c->ctx->stream;
+    c->aux->own_stream = false;
+  }
+  return c->aux;
+}
+
+// Open one file (host bytes) with the aux context: returns status, plaintext.
+int open_one(ce_core* c, const uint8_t* file, size_t flen, bool outer, int32_t* st,
+             std::vector<uint8_t>* pt) {
+  ce_ctx* a = aux_ctx(c);
+  const uint64_t offs[2] = {0, flen};
+  hipError_t e;
+  if ((e = a->blob.reserve(flen + 64)) || (e = a->offs.reserve(64)) ||
+      (e = a->out.reserve(flen + 128)) || (e = a->status.reserve(64)))
+    return a->hip_fail(e, "open_one");
+  if ((e = hipMemcpyAsync(a->blob.p, file, flen, hipMemcpyHostToDevice, a->stream)) ||
+      (e = hipMemcpyAsync(a->offs.p, offs, 16, hipMemcpyHostToDevice, a->stream)))
+    return a->hip_fail(e, "open_one");
+  int rc = device_open(a, a->blob.as<uint8_t>(), a->offs.as<uint64_t>(), 1, flen, outer, key_of(c),
+                       a->out.as<uint8_t>(), a->status.as<int32_t>(), false);
+  if (rc) return rc;
+  FileParams P;
+  if ((e = hipMemcpyAsync(&P, a->params.p, sizeof P, hipMemcpyDeviceToHost, a->stream)) ||
+      (e = hipMemcpyAsync(st, a->status.p, 4, hipMemcpyDeviceToHost, a->stream)) ||
+      (e = hipStreamSynchronize(a->stream)))
+    return a->hip_fail(e, "open_one");
+  if (*st == CE_OK) {
+    pt->resize(P.len);
+    if (P.len && ((e = hipMemcpyAsync(pt->data(), a->out.as<uint8_t>() + P.out_off, P.len,
+                                      hipMemcpyDeviceToHost, a->stream)) ||
+                  (e = hipStreamSynchronize(a->stream))))
+      return a->hip_fail(e, "open_one");
+  }
+  return CE_OK;
+}
+
+// Files whose envelope the device left to the host: normalize, open the canonical form on the
+// GPU, and patch the batch (plaintext into ctx->out at the file's slot, params.len, status).
+int resolve_host_parse(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
+                       bool outer) {
+  ce_ctx* ctx = c->ctx;
+  std::vector<int32_t> st(n);
+  hipError_t e;
+  if ((e = hipMemcpyAsync(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
+      (e = hipStreamSynchronize(ctx->stream)))
+    return ctx->hip_fail(e, "host parse");
+  for (uint32_t i = 0; i < n; i++) {
+    if (st[i] != kStatusHostParse) continue;
+    uint64_t o[2];
+    FileParams P;
+    if ((e = hipMemcpy(o, d_offs + i, 16, hipMemcpyDeviceToHost)) ||
+        (e = hipMemcpy(&P, ctx->params.as<FileParams>() + i, sizeof P, hipMemcpyDeviceToHost)))
+      return ctx->hip_fail(e, "host parse");
+    std::vector<uint8_t> file(o[1] - o[0]);
+    if ((e = hipMemcpy(file.data(), d_blob + o[0], file.size(), hipMemcpyDeviceToHost)))
+      return ctx->hip_fail(e, "host parse");
+    const size_t pre = outer ? 16 : 0;
+    std::vector<uint8_t> canon;
+    int32_t s = normalize_envelope(file.data() + pre, file.size() - pre, &canon);
+    std::vector<uint8_t> pt;
+    if (s == CE_OK) {
+      std::vector<uint8_t> nf(file.begin(), file.begin() + pre);
+      nf.insert(nf.end(), canon.begin(), canon.end());
+      int rc = open_one(c, nf.data(), nf.size(), outer, &s, &pt);
+      if (rc) return rc;
+    }
+    FileParams NP = P;
+    NP.status = s;
+    NP.len = s == CE_OK ? (uint32_t)pt.size() : 0;
+    if ((s == CE_OK && !pt.empty() &&
+         (e = hipMemcpy(ctx->out.as<uint8_t>() + P.out_off, pt.data(), pt.size(), hipMemcpyHostToDevice))) ||
+        (e = hipMemcpy(ctx->params.as<FileParams>() + i, &NP, sizeof NP, hipMemcpyHostToDevice)) ||
+        (e = hipMemcpy(ctx->status.as<int32_t>() + i, &s, 4, hipMemcpyHostToDevice)))
+      return ctx->hip_fail(e, "host parse");
+  }
+  return CE_OK;
+}
+
+int ensure_supported(ce_core* c) {
+  const size_t bytes = c->supported.size() * 16;
+  hipError_t e;
+  if ((e = c->d_supported.reserve(bytes + 16))) return c->ctx->hip_fail(e, "supported");
+  if (bytes && (e = hipMemcpyAsync(c->d_supported.p, c->supported.data(), bytes,
+                                   hipMemcpyHostToDevice, c->ctx->stream)))
+    return c->ctx->hip_fail(e, "supported");
+  return CE_OK;
+}
+
+// Core::read_remote_ops after Storage::load_ops (lib.rs:495-546), files resident in HBM.
+int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
+                   uint64_t blob_len, const uint8_t* actors, uint32_t m,
+                   const uint32_t* file_actor, const uint64_t* file_version, int32_t* status_out) {
+  ce_ctx* ctx = c->ctx;
+  if (!c->has_key) return ctx->fail(CE_ERR_NO_KEY, "no latest key");
+  if (n == 0) return CE_OK;
+  for (uint32_t i = 0; i < n; i++)
+    if (file_actor[i] >= m) return ctx->fail(CE_ERR_INVALID_ARG, "file_actor out of range");
+  hipError_t e;
+  const KeyRef key = key_of(c);
+  // writer actors (the op directories) get slots first: the version gate is keyed by them
+  std::vector<uint32_t> wslot(m);
+  for (uint32_t a = 0; a < m; a++) {
+    Uuid u;
+    std::memcpy(u.data(), actors + 16ull * a, 16);
+    int rc = insert_actor(c, u, &wslot[a]);
+    if (rc) return rc;
+  }
+  int rc = table_upload(c);
+  if (rc) return rc;
+  if ((rc = ensure_supported(c))) return rc;
+  if ((e = ctx->out.reserve(blob_len + 16ull * n + 128)) || (e = ctx->status.reserve(n * 4ull + 64)) ||
+      (e = ctx->apply.reserve(n + 64)) || (e = ctx->h_apply.reserve(n + 64)) ||
+      (e = ctx->refold.reserve(n + 64)) || (e = c->d_refold2.reserve(n + 64)) ||
+      (e = ctx->miss.reserve(65536 * 16)))
+    return ctx->hip_fail(e, "ingest reserve");
+
+  // 1) GPU: outer version, envelope, XChaCha20-Poly1305 open (verify-before-release)
+  rc = device_open(ctx, d_blob, d_offs, n, blob_len, true, key, ctx->out.as<uint8_t>(),
+                   ctx->status.as<int32_t>(), false);
+  if (rc) return rc;
+
+  // 2) host, overlapped: the per-actor version gate (lib.rs:519-538)
+  uint8_t* ap = ctx->h_apply.as<uint8_t>();
+  std::vector<uint64_t> expect(m);
+  for (uint32_t a = 0; a < m; a++) expect[a] = c->nov[wslot[a]];
+  uint32_t first_gap = n;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t a = file_actor[i];
+    const uint64_t v = file_version[i];
+    if (v < expect[a]) { ap[i] = 0; continue; }       // already read
+    if (v > expect[a]) { first_gap = i; break; }      // "Unexpected op version"
+    ap[i] = 1;
+    expect[a] = v + 1;
+  }
+  if (first_gap < n) std::memset(ap + first_gap, 0, n - first_gap);
+
+  // 3) exotic envelopes (none in the canonical case): normalize on the host, AEAD on the GPU
+  if ((e = hipMemcpyAsync(ctx->h_counters.p, ctx->counters.p, 64, hipMemcpyDeviceToHost,
+                          ctx->stream)))
+    return ctx->hip_fail(e, "counters");
+  if ((e = hipMemcpyAsync(ctx->apply.p, ap, n, hipMemcpyHostToDevice, ctx->stream)) ||
+      (e = hipMemsetAsync(c->d_batch.p, 0, c->cap * 8ull, ctx->stream)) ||
+      (e = hipMemsetAsync(ctx->refold.p, 0, n, ctx->stream)))
+    return ctx->hip_fail(e, "ingest upload");
+
+  DecodeArgs da{};
+  da.pt = ctx->out.as<uint8_t>();
+  da.params = ctx->params.as<FileParams>();
+  da.status = ctx->status.as<int32_t>();
+  da.n = n;
+  da.supported = c->d_supported.as<uint8_t>();
+  da.n_supported = (uint32_t)c->supported.size();
+  da.apply = ctx->apply.as<uint8_t>();
+  da.counters = ctx->counters.as<uint32_t>();
+  da.miss_list = ctx->miss.as<uint4>();
+  da.miss_cap = 65536;
+  da.refold = ctx->refold.as<uint8_t>();
+  da.only = nullptr;
+
+  // 4) GPU: decode Vec<Dot> of every opened file, fold applied files into the batch state
+  da.table = c->d_table.as<ActorSlot>();
+  da.mask = c->cap - 1;
+  da.batch = c->d_batch.as<unsigned long long>();
+  if ((e = launch_decode_dots(ctx->stream, da, grid_waves_for(n)))) return ctx->hip_fail(e, "decode");
+  uint32_t* hc = ctx->h_counters.as<uint32_t>();
+  if ((e = hipMemcpyAsync(hc, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->stream)) ||
+      (e = hipStreamSynchronize(ctx->stream)))
+    return ctx->hip_fail(e, "decode sync");
+
+  // misses: actors not in the table -> insert, upload, re-fold the files that missed
+  for (int round = 0; hc[4] != 0 && hc[3] == 0 && hc[2] == 0 && hc[8] == 0; round++) {
+    const uint32_t nm = std::min<uint32_t>(hc[4], 65536);
+    std::vector<uint4> ml(nm);
+    if ((e = hipMemcpyAsync(ml.data(), ctx->miss.p, nm * 16ull, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (e = hipMemcpyAsync(c->d_refold2.p, ctx->refold.p, n, hipMemcpyDeviceToDevice, ctx->stream)) ||
+        (e = hipMemsetAsync(ctx->refold.p, 0, n, ctx->stream)) ||
+        (e = hipMemsetAsync(ctx->counters.as<uint32_t>() + 4, 0, 4, ctx->stream)) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+      return ctx->hip_fail(e, "miss");
+    const uint32_t old_cap = c->cap;
+    for (auto& x : ml) {
+      Uuid u;
+      std::memcpy(u.data(), &x, 16);
+      uint32_t s;
+      if ((rc = insert_actor(c, u, &s))) return rc;
+    }
+    if (c->cap != old_cap) {
+      // slots moved: the partial batch state is stale -> re-fold everything
+      if ((e = hipMemsetAsync(c->d_batch.p, 0, c->cap * 8ull, ctx->stream)) ||
+          (e = hipMemsetAsync(c->d_refold2.p, 1, n, ctx->stream)))
+        return ctx->hip_fail(e, "miss");
+    }
+    if ((rc = table_upload(c))) return rc;
+    for (uint32_t a = 0; a < m; a++) {
+      Uuid u;
+      std::memcpy(u.data(), actors + 16ull * a, 16);
+      wslot[a] = c->slot_of[u];
+    }
+    da.table = c->d_table.as<ActorSlot>();
+    da.mask = c->cap - 1;
+    da.batch = c->d_batch.as<unsigned long long>();
+    da.only = c->d_refold2.as<uint8_t>();
+    if ((e = launch_decode_dots(ctx->stream, da, grid_waves_for(n))) ||
+        (e = hipMemcpyAsync(hc, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+      return ctx->hip_fail(e, "refold");
+    if (round > 64) return ctx->fail(CE_ERR_DEVICE, "actor table did not converge");
+  }
+
+  // statuses: needed for the caller, for host-parse files, and to name the first failure
+  std::vector<int32_t> st;
+  auto fetch_status = [&]() -> int {
+    st.resize(n);
+    if ((e = hipMemcpyAsync(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+      return ctx->hip_fail(e, "status");
+    return CE_OK;
+  };
+  // counters: [2] auth failures, [3] decode failures, [7] host-parse envelopes,
+  // [8] setup failures (outer version, key, envelope)
+  const bool failed = hc[2] || hc[3] || hc[8];
+  if (status_out || failed || hc[7]) {
+    if ((rc = fetch_status())) return rc;
+  }
+  if (hc[7]) {
+    if ((rc = resolve_host_parse(c, d_blob, d_offs, n, true))) return rc;
+    // decode only the resolved files
+    std::vector<uint8_t> only(n, 0);
+    for (uint32_t i = 0; i < n; i++) only[i] = st[i] == kStatusHostParse;
+    if ((e = hipMemcpy(c->d_refold2.p, only.data(), n, hipMemcpyHostToDevice))) return ctx->hip_fail(e, "x");
+    da.only = c->d_refold2.as<uint8_t>();
+    da.table = c->d_table.as<ActorSlot>();
+    da.mask = c->cap - 1;
+    da.batch = c->d_batch.as<unsigned long long>();
+    if ((e = launch_decode_dots(ctx->stream, da, grid_waves_for(n))) ||
+        (e = hipMemcpyAsync(hc, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+      return ctx->hip_fail(e, "exotic decode");
+    if (hc[4]) return ctx->fail(CE_ERR_DEVICE, "unregistered actor in an exotic file");
+    if ((rc = fetch_status())) return rc;
+  }
+  int first = CE_OK;
+  if (st.size() == n) {
+    for (uint32_t i = 0; i < n && first == CE_OK; i++)
+      if (st[i] != CE_OK) first = st[i];
+    if (status_out) std::memcpy(status_out, st.data(), n * 4ull);
+  }
+  if (first != CE_OK) return first;  // all-or-nothing: batch state discarded (lib.rs:497-514)
+
+  // 5) commit: state = max(state, batch); next_op_versions from the gate
+  if ((e = launch_merge_max(ctx->stream, c->d_state.as<unsigned long long>(),
+                            c->d_batch.as<unsigned long long>(), c->cap)) ||
+      (e = hipStreamSynchronize(ctx->stream)))
+    return ctx->hip_fail(e, "merge");
+  for (uint32_t a = 0; a < m; a++) c->nov[wslot[a]] = std::max(c->nov[wslot[a]], expect[a]);
+  if (first_gap < n) {
+    if (status_out) status_out[first_gap] = CE_ERR_OP_VERSION;
+    return CE_ERR_OP_VERSION;
+  }
+  return CE_OK;
+}
+
+// Core::read_remote_states after Storage::load_states (lib.rs:425-466)
+int ingest_states_host(ce_core* c, const uint8_t* blob, const uint64_t* offs, uint32_t n,
+                       int32_t* status_out) {
+  ce_ctx* ctx = c->ctx;
+  if (!c->has_key) return ctx->fail(CE_ERR_NO_KEY, "no latest key");
+  if (n == 0) return CE_OK;
+  const uint64_t blen = offs[n];
+  hipError_t e;
+  if ((e = ctx->blob.reserve(blen + 64)) || (e = ctx->offs.reserve((n + 1) * 8ull)) ||
+      (e = ctx->out.reserve(blen + 16ull * n + 128)) || (e = ctx->status.reserve(n * 4ull + 64)))
+    return ctx->hip_fail(e, "states reserve");
+  if ((e = hipMemcpyAsync(ctx->blob.p, blob, blen, hipMemcpyHostToDevice, ctx->stream)) ||
+      (e = hipMemcpyAsync(ctx->offs.p, offs, (n + 1) * 8ull, hipMemcpyHostToDevice, ctx->stream)))
+    return ctx->hip_fail(e, "states upload");
+  int rc = device_open(ctx, ctx->blob.as<uint8_t>(), ctx->offs.as<uint64_t>(), n, blen, true,
+                       key_of(c), ctx->out.as<uint8_t>(), ctx->status.as<int32_t>(), false);
+  if (rc) return rc;
+  std::vector<int32_t> st(n);
+  if ((e = hipMemcpyAsync(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
+      (e = hipStreamSynchronize(ctx->stream)))
+    return ctx->hip_fail(e, "states status");
+  for (uint32_t i = 0; i < n; i++)
+    if (st[i] == kStatusHostParse) {
+      if ((rc = resolve_host_parse(c, ctx->blob.as<uint8_t>(), ctx->offs.as<uint64_t>(), n, true)))
+        return rc;
+      if ((e = hipMemcpy(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost)))
+        return ctx->hip_fail(e, "states status");
+      break;
+    }
+  std::vector<FileParams> P(n);
+  std::vector<uint8_t> out(blen + 16ull * n + 64);
+  if ((e = hipMemcpyAsync(P.data(), ctx->params.p, n * sizeof(FileParams), hipMemcpyDeviceToHost,
+                          ctx->stream)) ||
+      (e = hipMemcpyAsync(out.data(), ctx->out.p, blen + 16ull * n, hipMemcpyDeviceToHost, ctx->stream)) ||
+      (e = hipStreamSynchronize(ctx->stream)))
+    return ctx->hip_fail(e, "states download");
+  // host pass: StateWrapper msgpack -> dots (north star: "host pass that flattens decoded
+  // ops/states into columnar arrays")
+  std::vector<Dots> novs(n), sts(n);
+  int first = CE_OK;
+  for (uint32_t i = 0; i < n; i++) {
+    if (st[i] == CE_OK) {
+      const uint8_t* pt = out.data() + P[i].out_off;
+      const uint32_t len = P[i].len;
+      if (len < 16) st[i] = CE_ERR_PT_LEN;
+      else {
+        Uuid v;
+        std::memcpy(v.data(), pt, 16);
+        if (!std::binary_search(c->supported.begin(), c->supported.end(), v)) st[i] = CE_ERR_PT_VERSION;
+        else if (!read_state_wrapper(pt + 16, len - 16, c->kind, &novs[i], &sts[i]))
+          st[i] = CE_ERR_DECODE;
+      }
+    }
+    if (st[i] != CE_OK && first == CE_OK) first = st[i];
+  }
+  if (status_out) std::memcpy(status_out, st.data(), n * 4ull);
+  if (first != CE_OK) return first;
+  // fold (lib.rs:458-466): state.merge(sw.state); next_op_versions.merge(sw.next_op_versions)
+  Dots all;
+  for (uint32_t i = 0; i < n; i++) all.insert(all.end(), sts[i].begin(), sts[i].end());
+  if ((rc = merge_dots_host(c, all))) return rc;
+  for (uint32_t i = 0; i < n; i++)
+    for (auto& d : novs[i]) {
+      uint32_t s;
+      if ((rc = insert_actor(c, d.first, &s))) return rc;
+      c->nov[s] = std::max(c->nov[s], d.second);
+    }
+  return table_upload(c);
+}
+
+int read_remote(ce_core* c) {
+  if (!c->storage) return c->ctx->fail(CE_ERR_INVALID_ARG, "core opened without storage");
+  // read_remote_states (lib.rs:401-469)
+  std::vector<std::string> names;
+  int rc = storage_list_states_vec(c->storage, &names);
+  if (rc) return c->ctx->fail(rc, "failed getting state entry names while reading remote states");
+  std::vector<std::string> to_read;
+  for (auto& nm : names)
+    if (!c->read_states.count(nm)) to_read.push_back(nm);
+  if (!to_read.empty()) {
+    if (!c->has_key) return c->ctx->fail(CE_ERR_NO_KEY, "no latest key");
+    std::vector<uint8_t> blob;
+    std::vector<uint64_t> offs{0};
+    for (auto& nm : to_read) {
+      std::vector<uint8_t> f;
+      if ((rc = storage_read_state(c->storage, nm, &f))) return c->ctx->fail(rc, "failed loading state content");
+      blob.insert(blob.end(), f.begin(), f.end());
+      offs.push_back(blob.size());
+    }
+    rc = ingest_states_host(c, blob.data(), offs.data(), (uint32_t)to_read.size(), nullptr);
+    if (rc) return rc;
+    for (auto& nm : to_read) c->read_states.insert(nm);
+  }
+  // read_remote_ops (lib.rs:471-547)
+  std::vector<Uuid> actors;
+  if ((rc = storage_list_op_actors_vec(c->storage, &actors))) return c->ctx->fail(rc, "failed getting op actor entries");
+  if (actors.empty()) return CE_OK;
+  if (!c->has_key) return c->ctx->fail(CE_ERR_NO_KEY, "no latest key");
+  std::vector<uint64_t> first(actors.size());
+  for (size_t a = 0; a < actors.size(); a++) {
+    auto it = c->slot_of.find(actors[a]);
+    first[a] = it == c->slot_of.end() ? 0 : c->nov[it->second];
+  }
+  std::vector<uint8_t> blob;
+  std::vector<uint64_t> offs, vers;
+  std::vector<uint32_t> aidx;
+  if ((rc = storage_load_ops_vec(c->storage, actors, first, &blob, &offs, &aidx, &vers)))
+    return c->ctx->fail(rc, "failed loading ops");
+  const uint32_t n = (uint32_t)aidx.size();
+  if (n == 0) return CE_OK;
+  ce_ctx* ctx = c->ctx;
+  hipError_t e;
+  if ((e = ctx->blob.reserve(blob.size() + 64)) || (e = ctx->offs.reserve((n + 1) * 8ull)))
+    return ctx->hip_fail(e, "ops reserve");
+  if ((e = hipMemcpyAsync(ctx->blob.p, blob.data(), blob.size(), hipMemcpyHostToDevice, ctx->stream)) ||
+      (e = hipMemcpyAsync(ctx->offs.p, offs.data(), (n + 1) * 8ull, hipMemcpyHostToDevice, ctx->stream)) ||
+      (e = hipStreamSynchronize(ctx->stream)))
+    return ctx->hip_fail(e, "ops upload");
+  std::vector<uint8_t> ab(actors.size() * 16);
+  for (size_t a = 0; a < actors.size(); a++) std::memcpy(ab.data() + 16 * a, actors[a].data(), 16);
+  return ingest_ops_dev(c, ctx->blob.as<uint8_t>(), ctx->offs.as<uint64_t>(), n, blob.size(),
+                        ab.data(), (uint32_t)actors.size(), aidx.data(), vers.data(), nullptr);
+}
+
+// clear text + file of a compaction (lib.rs:335-360)
+int compact_bytes(ce_core* c, const uint8_t* nonce, std::vector<uint8_t>* file) {
+  if (!c->has_key) return c->ctx->fail(CE_ERR_NO_KEY, "no latest key");
+  std::vector<uint8_t> clear;
+  int rc = serialize_state(c, &clear);
+  if (rc) return rc;
+  if (c->flags & CE_COMPACT_INGEST_FORMAT) {
+    // readable by read_remote_states: CURRENT_VERSION || encrypt(data_version || state)
+    std::vector<uint8_t> vb(c->current_data_version.begin(), c->current_data_version.end());
+    vb.insert(vb.end(), clear.begin(), clear.end());
+    return seal_one(c->ctx, key_of(c), kCoreVersion, nonce, vb.data(), vb.size(), file);
+  }
+  // exactly what Core::compact writes: VersionBytes(current_data_version, encrypt(state))
+  return seal_one(c->ctx, key_of(c), c->current_data_version.data(), nonce, clear.data(),
+                  clear.size(), file);
+}
+
+}  // namespace
+
+extern "C" {
+
+int ce_core_open(ce_ctx* ctx, const ce_open_options* o, ce_core** out) {
+  if (!ctx || !o || !out || !o->current_data_version || (o->n_supported && !o->supported_data_versions))
+    return CE_ERR_INVALID_ARG;
+  if (o->state_kind != CE_STATE_VCLOCK && o->state_kind != CE_STATE_GCOUNTER) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  (void)hipSetDevice(ctx->device);
+  ce_core* c = new ce_core();
+  c->ctx = ctx;
+  c->kind = o->state_kind;
+  c->flags = o->flags;
+  std::memcpy(c->current_data_version.data(), o->current_data_version, 16);
+  for (size_t i = 0; i < o->n_supported; i++) {
+    Uuid u;
+    std::memcpy(u.data(), o->supported_data_versions + 16 * i, 16);
+    c->supported.push_back(u);
+  }
+  std::sort(c->supported.begin(), c->supported.end());
+  int rc = table_init(c, 8192);
+  if (rc) { delete c; return rc; }
+  if (o->local_path || o->remote_path) {
+    if (!o->local_path || !o->remote_path || o->local_path[0] != '/' || o->remote_path[0] != '/') {
+      delete c;
+      return CE_ERR_INVALID_ARG;
+    }
+    c->storage = storage_new(o->local_path, o->remote_path);
+    // load_local_meta (lib.rs:250-278)
+    std::vector<uint8_t> lm;
+    bool missing = false;
+    if ((rc = storage_load_local_meta(c->storage, &lm, &missing))) { ce_core_close(c); return rc; }
+    if (!missing) {
+      if (lm.size() < 16 || std::memcmp(lm.data(), kCoreVersion, 16) != 0) {
+        ce_core_close(c);
+        return lm.size() < 16 ? CE_ERR_OUTER_LEN : CE_ERR_OUTER_VERSION;
+      }
+      Rd r{lm.data() + 16, lm.size() - 16, 0};
+      bool ok = read_struct(r, {"local_actor_id"}, [&](int, Rd& q) {
+        uint64_t off;
+        if (!rd_uuid(q, &off)) return false;
+        std::memcpy(c->local_actor.data(), q.p + off, 16);
+        return true;
+      });
+      if (!ok) { ce_core_close(c); return CE_ERR_DECODE; }
+    } else {
+      if (!(o->flags & CE_OPEN_CREATE)) { ce_core_close(c); return CE_ERR_NO_LOCAL_META; }
+      c->local_actor = uuid_v4();
+      Wr w;
+      w.b.assign(kCoreVersion, kCoreVersion + 16);  // VersionBytes(CURRENT_VERSION, ..)
+      w.map(1);
+      w.str("local_actor_id");
+      w.bin(c->local_actor.data(), 16);
+      if ((rc = storage_store_local_meta(c->storage, w.b.data(), w.b.size()))) { ce_core_close(c); return rc; }
+    }
+  } else {
+    c->local_actor = uuid_v4();
+  }
+  if ((rc = table_upload(c))) { ce_core_close(c); return rc; }
+  *out = c;
+  return CE_OK;
+}
+
+void ce_core_close(ce_core* c) {
+  if (!c) return;
+  if (c->ctx) (void)hipStreamSynchronize(c->ctx->stream);
+  delete c->storage;
+  delete c->aux;
+  delete c;
+}
+
+int ce_core_set_latest_key(ce_core* c, const uint8_t key_version[16], const uint8_t* key,
+                           size_t key_len) {
+  if (!c || !key_version || (key_len && !key)) return CE_ERR_INVALID_ARG;
+  std::memcpy(c->key_version, key_version, 16);
+  c->key.assign(key, key + key_len);
+  c->has_key = true;
+  return CE_OK;
+}
+
+int ce_core_info_actor(ce_core* c, uint8_t out[16]) {
+  if (!c || !out) return CE_ERR_INVALID_ARG;
+  std::memcpy(out, c->local_actor.data(), 16);
+  return CE_OK;
+}
+
+int ce_core_state_bytes(ce_core* c, ce_buf* out) {
+  if (!c || !out) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  std::vector<uint8_t> b;
+  int rc = serialize_state(c, &b);
+  if (rc) return rc;
+  out->data = (uint8_t*)malloc(b.size() ? b.size() : 1);
+  std::memcpy(out->data, b.data(), b.size());
+  out->len = b.size();
+  return CE_OK;
+}
+
+int ce_core_ingest_ops(ce_core* c, const uint8_t* blob, const uint64_t* offs, uint32_t n,
+                       const uint8_t* actors, uint32_t m, const uint32_t* file_actor,
+                       const uint64_t* file_version, int32_t* status) {
+  if (!c || (n && (!blob || !offs || !actors || !file_actor || !file_version))) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  (void)hipSetDevice(c->ctx->device);
+  if (n == 0) return CE_OK;
+  ce_ctx* ctx = c->ctx;
+  hipError_t e;
+  const uint64_t blen = offs[n];
+  if ((e = ctx->blob.reserve(blen + 64)) || (e = ctx->offs.reserve((n + 1) * 8ull)))
+    return ctx->hip_fail(e, "ingest reserve");
+  if ((e = hipMemcpyAsync(ctx->blob.p, blob, blen, hipMemcpyHostToDevice, ctx->stream)) ||
+      (e = hipMemcpyAsync(ctx->offs.p, offs, (n + 1) * 8ull, hipMemcpyHostToDevice, ctx->stream)) ||
+      (e = hipStreamSynchronize(ctx->stream)))
+    return ctx->hip_fail(e, "ingest upload");
+  return ingest_ops_dev(c, ctx->blob.as<uint8_t>(), ctx->offs.as<uint64_t>(), n, blen, actors, m,
+                        file_actor, file_version, status);
+}
+
+int ce_core_ingest_ops_device(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs,
+                              uint32_t n, uint64_t blob_len, const uint8_t* actors, uint32_t m,
+                              const uint32_t* file_actor, const uint64_t* file_version,
+                              int32_t* status) {
+  if (!c || (n && (!d_blob || !d_offs || !actors || !file_actor || !file_version)))
+    return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  (void)hipSetDevice(c->ctx->device);
+  return ingest_ops_dev(c, d_blob, d_offs, n, blob_len, actors, m, file_actor, file_version, status);
+}
+
+int ce_core_ingest_states(ce_core* c, const uint8_t* blob, const uint64_t* offs, uint32_t n,
+                          int32_t* status) {
+  if (!c || (n && (!blob || !offs))) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  (void)hipSetDevice(c->ctx->device);
+  return ingest_states_host(c, blob, offs, n, status);
+}
+
+int ce_core_read_remote(ce_core* c) {
+  if (!c) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  (void)hipSetDevice(c->ctx->device);
+  return read_remote(c);
+}
+
+int ce_core_compact_to_buffer(ce_core* c, const uint8_t* nonce, ce_buf* file, char name_out[64]) {
+  if (!c || !file) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  (void)hipSetDevice(c->ctx->device);
+  std::vector<uint8_t> f;
+  int rc = compact_bytes(c, nonce, &f);
+  if (rc) return rc;
+  if (name_out) {
+    uint8_t h[32];
+    sha3_256(f.data(), f.size(), h);
+    std::snprintf(name_out, 64, "%s", base32_nopad(h, 32).c_str());
+  }
+  file->data = (uint8_t*)malloc(f.size() ? f.size() : 1);
+  std::memcpy(file->data, f.data(), f.size());
+  file->len = f.size();
+  return CE_OK;
+}
+
+int ce_core_compact(ce_core* c, char name_out[64]) {
+  if (!c) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  (void)hipSetDevice(c->ctx->device);
+  if (!c->storage) return c->ctx->fail(CE_ERR_INVALID_ARG, "core opened without storage");
+  int rc = read_remote(c);
+  if (rc) return rc;
+  std::vector<uint8_t> f;
+  if ((rc = compact_bytes(c, nullptr, &f))) return rc;
+  const std::vector<std::string> states_to_remove(c->read_states.begin(), c->read_states.end());
+  std::vector<std::pair<Uuid, uint64_t>> ops_to_remove;  // (actor, counter - 1) (lib.rs:340-345)
+  for (uint32_t s = 0; s < c->cap; s++)
+    if (c->h_table[s].used && c->nov[s]) ops_to_remove.push_back({c->slot_actor[s], c->nov[s] - 1});
+  std::string name;
+  if ((rc = storage_store_content(c->storage, "states", f.data(), f.size(), &name)))
+    return c->ctx->fail(rc, "failed writing state file");
+  for (auto& s : states_to_remove)
+    if ((rc = storage_remove_state(c->storage, s))) return c->ctx->fail(rc, "failed removing state file");
+  for (auto& o : ops_to_remove)
+    if ((rc = storage_remove_op(c->storage, o.first, o.second))) return c->ctx->fail(rc, "failed removing ops file");
+  for (auto& s : states_to_remove) c->read_states.erase(s);
+  c->read_states.insert(name);
+  if (name_out) std::snprintf(name_out, 64, "%s", name.c_str());
+  return CE_OK;
+}
+
+int ce_core_apply_ops(ce_core* c, const uint8_t* ops, size_t len) {
+  if (!c || (len && !ops)) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  (void)hipSetDevice(c->ctx->device);
+  if (!c->has_key) return c->ctx->fail(CE_ERR_NO_KEY, "no latest key");
+  Dots dots;
+  if (!read_dots(ops, len, &dots)) return c->ctx->fail(CE_ERR_DECODE, "ops are not a Vec<Dot<Uuid>>");
+  // clear_text = VersionBytes(current_data_version, msgpack(ops)).serialize() (lib.rs:670-671)
+  std::vector<uint8_t> clear(c->current_data_version.begin(), c->current_data_version.end());
+  clear.insert(clear.end(), ops, ops + len);
+  std::vector<uint8_t> file;
+  int rc = seal_one(c->ctx, key_of(c), kCoreVersion, nullptr, clear.data(), clear.size(), &file);
+  if (rc) return rc;
+  uint32_t s;
+  if ((rc = insert_actor(c, c->local_actor, &s))) return rc;
+  const uint64_t version = c->nov[s];  // next_op_versions.get(actor) (lib.rs:703)
+  if (c->storage && (rc = storage_store_op(c->storage, c->local_actor, version, file.data(), file.size())))
+    return c->ctx->fail(rc, "failed writing ops file");
+  if ((rc = merge_dots_host(c, dots))) return rc;  // state.apply(op) for op in ops (lib.rs:710-712)
+  c->nov[s] = version + 1;                         // next_op_versions.inc(actor) (lib.rs:714-715)
+  return table_upload(c);
+}
+
+int ce_core_register_actors(ce_core* c, const uint8_t* actors, uint32_t m) {
+  if (!c || (m && !actors)) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  if (c->registered != c->size) return CE_ERR_INVALID_ARG;
+  while ((c->size + m) * 2 > c->cap) {
+    int rc = table_grow(c);
+    if (rc) return rc;
+  }
+  for (uint32_t i = 0; i < m; i++) {
+    Uuid u;
+    std::memcpy(u.data(), actors + 16ull * i, 16);
+    uint32_t s;
+    int rc = insert_actor(c, u, &s);
+    if (rc) return rc;
+  }
+  c->registered = c->size;
+  return table_upload(c);
+}
+
+uint32_t ce_core_dense_capacity(ce_core* c) { return c ? c->cap : 0; }
+
+int ce_core_export_dense(ce_core* c, uint64_t* d_state, uint64_t* d_nov) {
+  if (!c || !d_state || !d_nov) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  if (c->registered != c->size) return c->ctx->fail(CE_ERR_INVALID_ARG, "actors outside the registered set");
+  hipError_t e;
+  if ((e = hipMemcpyAsync(d_state, c->d_state.p, c->cap * 8ull, hipMemcpyDeviceToDevice, c->ctx->stream)) ||
+      (e = hipMemcpyAsync(d_nov, c->nov.data(), c->cap * 8ull, hipMemcpyHostToDevice, c->ctx->stream)) ||
+      (e = hipStreamSynchronize(c->ctx->stream)))
+    return c->ctx->hip_fail(e, "export");
+  return CE_OK;
+}
+
+int ce_core_import_dense(ce_core* c, const uint64_t* d_state, const uint64_t* d_nov) {
+  if (!c || !d_state || !d_nov) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  if (c->registered != c->size) return c->ctx->fail(CE_ERR_INVALID_ARG, "actors outside the registered set");
+  std::vector<uint64_t> nv(c->cap);
+  hipError_t e;
+  if ((e = launch_merge_max(c->ctx->stream, c->d_state.as<unsigned long long>(),
+                            reinterpret_cast<const unsigned long long*>(d_state), c->cap)) ||
+      (e = hipMemcpyAsync(nv.data(), d_nov, c->cap * 8ull, hipMemcpyDeviceToHost, c->ctx->stream)) ||
+      (e = hipStreamSynchronize(c->ctx->stream)))
+    return c->ctx->hip_fail(e, "import");
+  for (uint32_t s = 0; s < c->cap; s++) c->nov[s] = std::max(c->nov[s], nv[s]);
+  return CE_OK;
+}
+
+}  // extern "C"

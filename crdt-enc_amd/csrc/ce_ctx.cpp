@@ -1,0 +1,460 @@
+// ce_ctx.cpp -- context, device batch engine (open / seal) and the Cryptor C ABI.
+//
+// Cryptor trait: crdt-enc/src/cryptor.rs:11-27.  EncHandler (XChaCha20-Poly1305):
+// crdt-enc-xchacha20poly1305/src/lib.rs:28-101.  Every AEAD in this library runs on the GPU;
+// there is no CPU implementation of the cipher in the product.
+#include <sys/random.h>
+
+#include <algorithm>
+#include <cstdio>
+
+#include "ce_internal.h"
+
+namespace ce {
+
+hipError_t DevBuf::reserve(size_t bytes) {
+  if (bytes <= cap) return hipSuccess;
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+  size_t want = std::max<size_t>(bytes, 256);
+  want = (want + 4095) & ~size_t(4095);
+  hipError_t e = hipMalloc(&p, want);
+  if (e == hipSuccess) cap = want;
+  return e;
+}
+DevBuf::~DevBuf() {
+  if (p) (void)hipFree(p);
+}
+hipError_t HostBuf::reserve(size_t bytes) {
+  if (bytes <= cap) return hipSuccess;
+  if (p) (void)hipHostFree(p);
+  p = nullptr;
+  cap = 0;
+  size_t want = std::max<size_t>(bytes, 256);
+  want = (want + 4095) & ~size_t(4095);
+  hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+  if (e == hipSuccess) cap = want;
+  return e;
+}
+HostBuf::~HostBuf() {
+  if (p) (void)hipHostFree(p);
+}
+
+void os_random(uint8_t* out, size_t n) {
+  size_t got = 0;
+  while (got < n) {
+    ssize_t r = getrandom(out + got, n - got, 0);
+    if (r > 0) got += (size_t)r;
+  }
+}
+
+int32_t key_status(const KeyRef& k) {
+  // xchacha lib.rs:74-78: key.ensure_version(KEY_VERSION), key.len() == KEY_LEN
+  if (std::memcmp(k.version, kKeyVersion, 16) != 0) return CE_ERR_KEY_VERSION;
+  if (k.len != 32) return CE_ERR_KEY_LEN;
+  return CE_OK;
+}
+
+DevKey dev_key(const KeyRef& k) {
+  DevKey d{};
+  if (k.len == 32) std::memcpy(d.k, k.key, 32);
+  return d;
+}
+
+uint32_t grid_waves_for(uint32_t work) {
+  // 256 CUs x 32 resident waves (segment kernel: <= 64 VGPRs -> 8 waves / SIMD)
+  const uint32_t full = 256u * 32u;
+  return std::max<uint32_t>(1, std::min<uint32_t>(work, full));
+}
+
+static int reserve_batch(ce_ctx* ctx, uint32_t n, uint64_t blob_len, uint32_t* extra_cap) {
+  const uint64_t ec = blob_len / (kSegBlocks * 16) + 16;
+  if (ec > 0xffffffffull) return ctx->fail(CE_ERR_INVALID_ARG, "batch too large");
+  *extra_cap = (uint32_t)ec;
+  hipError_t e;
+  if ((e = ctx->params.reserve((size_t)n * sizeof(FileParams))) != hipSuccess ||
+      (e = ctx->status.reserve((size_t)n * 4 + 64)) != hipSuccess ||
+      (e = ctx->counters.reserve(256)) != hipSuccess ||
+      (e = ctx->extra.reserve(ec * 8)) != hipSuccess ||
+      (e = ctx->multi.reserve(ec * 4)) != hipSuccess ||
+      (e = ctx->partials.reserve(ec * 2 * 5 * 4)) != hipSuccess ||
+      (e = ctx->h_counters.reserve(256)) != hipSuccess)
+    return ctx->hip_fail(e, "reserve batch scratch");
+  return CE_OK;
+}
+
+static SegScratch scratch_of(ce_ctx* ctx, uint32_t extra_cap) {
+  SegScratch sc;
+  sc.counters = ctx->counters.as<uint32_t>();
+  sc.extra_list = ctx->extra.as<uint2>();
+  sc.extra_cap = extra_cap;
+  sc.multi_files = ctx->multi.as<uint32_t>();
+  sc.partials = ctx->partials.as<uint32_t>();
+  return sc;
+}
+
+static hipError_t reset_counters(ce_ctx* ctx) {
+  hipError_t e = hipMemsetAsync(ctx->counters.p, 0, 64, ctx->stream);
+  if (e != hipSuccess) return e;
+  // counters[5] = first failing index (atomicMin) starts at UINT32_MAX
+  return hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ctx->counters.as<uint32_t>() + 5),
+                           0xffffffffu, 1, ctx->stream);
+}
+
+int device_open(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
+                uint64_t blob_len, bool outer, const KeyRef& key, uint8_t* d_out,
+                int32_t* d_status, bool sync_counters) {
+  uint32_t ec;
+  int rc = reserve_batch(ctx, n, blob_len, &ec);
+  if (rc) return rc;
+  hipError_t e;
+  if ((e = reset_counters(ctx)) != hipSuccess) return ctx->hip_fail(e, "memset counters");
+  SegScratch sc = scratch_of(ctx, ec);
+  FileParams* P = ctx->params.as<FileParams>();
+  if ((e = launch_open_setup(ctx->stream, d_blob, d_offs, n, outer, dev_key(key), key_status(key),
+                             P, d_status, sc)) != hipSuccess)
+    return ctx->hip_fail(e, "open setup");
+  if ((e = launch_segments(ctx->stream, false, d_blob, d_out, P, n, d_status, sc,
+                           grid_waves_for(n))) != hipSuccess)
+    return ctx->hip_fail(e, "open segments");
+  if ((e = launch_finalize_multi(ctx->stream, false, d_out, P, d_status, sc)) != hipSuccess)
+    return ctx->hip_fail(e, "open finalize");
+  if (sync_counters) {
+    if ((e = hipMemcpyAsync(ctx->h_counters.p, ctx->counters.p, 64, hipMemcpyDeviceToHost,
+                            ctx->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(ctx->stream)) != hipSuccess)
+      return ctx->hip_fail(e, "open sync");
+  }
+  return CE_OK;
+}
+
+int device_seal(ce_ctx* ctx, const uint8_t* d_clear, const uint64_t* d_offs, uint32_t n,
+                uint64_t clear_len_total, const uint8_t* d_outer_version, const uint8_t* d_nonces,
+                uint8_t* d_out, const uint64_t* d_out_offs, const KeyRef& key) {
+  if (int32_t ks = key_status(key)) return ctx->fail(ks, "key rejected");
+  uint32_t ec;
+  int rc = reserve_batch(ctx, n, clear_len_total + 16ull * n, &ec);
+  if (rc) return rc;
+  hipError_t e;
+  if ((e = reset_counters(ctx)) != hipSuccess) return ctx->hip_fail(e, "memset counters");
+  SegScratch sc = scratch_of(ctx, ec);
+  FileParams* P = ctx->params.as<FileParams>();
+  if ((e = launch_seal_setup(ctx->stream, d_clear, d_offs, n, d_outer_version, d_nonces, d_out,
+                             d_out_offs, dev_key(key), P, sc)) != hipSuccess)
+    return ctx->hip_fail(e, "seal setup");
+  if ((e = launch_segments(ctx->stream, true, d_clear, d_out, P, n, ctx->status.as<int32_t>(), sc,
+                           grid_waves_for(n))) != hipSuccess)
+    return ctx->hip_fail(e, "seal segments");
+  if ((e = launch_finalize_multi(ctx->stream, true, d_out, P, ctx->status.as<int32_t>(), sc)) !=
+      hipSuccess)
+    return ctx->hip_fail(e, "seal finalize");
+  return CE_OK;
+}
+
+int seal_one(ce_ctx* ctx, const KeyRef& key, const uint8_t* outer_version, const uint8_t* nonce,
+             const uint8_t* clear, size_t clear_len, std::vector<uint8_t>* file) {
+  if (int32_t ks = key_status(key)) return ctx->fail(ks, "key rejected");
+  const uint64_t pre = outer_version ? 16 : 0;
+  const uint64_t total = pre + sealed_len(clear_len);
+  uint8_t nb[24];
+  if (nonce) std::memcpy(nb, nonce, 24);
+  else os_random(nb, 24);
+  hipError_t e;
+  // staging: [offs(2) | out_offs(1) | outer(16) | nonce(24)] small args, clear text, output
+  if ((e = ctx->offs.reserve(64)) != hipSuccess || (e = ctx->out_offs.reserve(64)) != hipSuccess ||
+      (e = ctx->outer_ver.reserve(64)) != hipSuccess || (e = ctx->nonces.reserve(64)) != hipSuccess ||
+      (e = ctx->blob.reserve(clear_len + 64)) != hipSuccess ||
+      (e = ctx->out.reserve(total + 64)) != hipSuccess ||
+      (e = ctx->h_stage.reserve(std::max<uint64_t>(clear_len, total) + 256)) != hipSuccess)
+    return ctx->hip_fail(e, "seal_one reserve");
+  uint8_t* hs = ctx->h_stage.as<uint8_t>();
+  const uint64_t offs[2] = {0, clear_len};
+  const uint64_t oo[1] = {0};
+  std::memcpy(hs, clear, clear_len);
+  if ((e = hipMemcpyAsync(ctx->blob.p, hs, clear_len, hipMemcpyHostToDevice, ctx->stream)) ||
+      (e = hipMemcpyAsync(ctx->offs.p, offs, 16, hipMemcpyHostToDevice, ctx->stream)) ||
+      (e = hipMemcpyAsync(ctx->out_offs.p, oo, 8, hipMemcpyHostToDevice, ctx->stream)) ||
+      (e = hipMemcpyAsync(ctx->nonces.p, nb, 24, hipMemcpyHostToDevice, ctx->stream)))
+    return ctx->hip_fail(e, "seal_one upload");
+  if (outer_version &&
+      (e = hipMemcpyAsync(ctx->outer_ver.p, outer_version, 16, hipMemcpyHostToDevice, ctx->stream)))
+    return ctx->hip_fail(e, "seal_one upload");
+  int rc = device_seal(ctx, ctx->blob.as<uint8_t>(), ctx->offs.as<uint64_t>(), 1, clear_len,
+                       outer_version ? ctx->outer_ver.as<uint8_t>() : nullptr,
+                       ctx->nonces.as<uint8_t>(), ctx->out.as<uint8_t>(),
+                       ctx->out_offs.as<uint64_t>(), key);
+  if (rc) return rc;
+  if ((e = hipMemcpyAsync(hs, ctx->out.p, total, hipMemcpyDeviceToHost, ctx->stream)) ||
+      (e = hipStreamSynchronize(ctx->stream)))
+    return ctx->hip_fail(e, "seal_one download");
+  file->assign(hs, hs + total);
+  return CE_OK;
+}
+
+}  // namespace ce
+
+using namespace ce;
+
+extern "C" {
+
+const char* ce_status_str(int s) {
+  switch (s) {
+    case CE_OK: return "ok";
+    case CE_ERR_OUTER_LEN: return "invalid length";
+    case CE_ERR_OUTER_VERSION: return "version check failed";
+    case CE_ERR_KEY_VERSION: return "not matching key version";
+    case CE_ERR_KEY_LEN: return "Invalid key length";
+    case CE_ERR_PARSE_VBOX: return "failed to parse version box";
+    case CE_ERR_DATA_VERSION: return "not matching version of encryption box";
+    case CE_ERR_PARSE_ENCBOX: return "failed to parse encryption box";
+    case CE_ERR_NONCE_LEN: return "Invalid nonce length";
+    case CE_ERR_AUTH: return "Decryption failed";
+    case CE_ERR_PT_LEN: return "invalid length";
+    case CE_ERR_PT_VERSION: return "version check failed";
+    case CE_ERR_DECODE: return "failed to decode msgpack";
+    case CE_ERR_OP_VERSION: return "Unexpected op version. Got ops in the wrong order? Bug in storage?";
+    case CE_ERR_INVALID_ARG: return "invalid argument";
+    case CE_ERR_DEVICE: return "HIP device error";
+    case CE_ERR_NO_KEY: return "no latest key";
+    case CE_ERR_IO: return "io error";
+    case CE_ERR_NO_LOCAL_META: return "local meta does not exist, and `create` option is not set";
+    default: return "unknown";
+  }
+}
+
+void ce_buf_free(ce_buf* b) {
+  if (b && b->data) free(b->data);
+  if (b) { b->data = nullptr; b->len = 0; }
+}
+
+static int buf_set(ce_buf* out, const uint8_t* d, size_t n) {
+  out->data = (uint8_t*)malloc(n ? n : 1);
+  if (!out->data) return CE_ERR_INVALID_ARG;
+  if (n) std::memcpy(out->data, d, n);
+  out->len = n;
+  return CE_OK;
+}
+
+int ce_ctx_create(int device, ce_ctx** out) {
+  if (!out) return CE_ERR_INVALID_ARG;
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= device || device < 0)
+    return CE_ERR_DEVICE;  // no GPU: the product has no CPU path
+  if (hipSetDevice(device) != hipSuccess) return CE_ERR_DEVICE;
+  ce_ctx* c = new ce_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return CE_ERR_DEVICE;
+  }
+  c->own_stream = true;
+  *out = c;
+  return CE_OK;
+}
+
+void ce_ctx_destroy(ce_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int ce_ctx_set_stream(ce_ctx* c, void* s) {
+  if (!c) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  (void)hipStreamSynchronize(c->stream);
+  if (c->own_stream) (void)hipStreamDestroy(c->stream);
+  if (s) {
+    c->stream = (hipStream_t)s;
+    c->own_stream = false;
+  } else {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return CE_ERR_DEVICE;
+    c->own_stream = true;
+  }
+  return CE_OK;
+}
+
+void ce_ctx_synchronize(ce_ctx* c) {
+  if (c) (void)hipStreamSynchronize(c->stream);
+}
+
+const char* ce_ctx_last_error(ce_ctx* c) { return c ? c->last_error.c_str() : ""; }
+
+size_t ce_cryptor_sealed_len(size_t clear_len) { return (size_t)sealed_len(clear_len); }
+
+int ce_cryptor_gen_key(ce_ctx* c, ce_buf* out) {
+  (void)c;
+  if (!out) return CE_ERR_INVALID_ARG;
+  uint8_t vb[48];
+  std::memcpy(vb, kKeyVersion, 16);
+  os_random(vb + 16, 32);  // xchacha lib.rs:29-38 (rand::rng)
+  return buf_set(out, vb, 48);
+}
+
+int ce_cryptor_encrypt(ce_ctx* c, const uint8_t key_version[16], const uint8_t* key,
+                       size_t key_len, const uint8_t* nonce, const uint8_t* clear,
+                       size_t clear_len, ce_buf* out) {
+  if (!c || !key_version || !out || (clear_len && !clear)) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
+  KeyRef k{key_version, key, key_len};
+  std::vector<uint8_t> file;
+  int rc = seal_one(c, k, nullptr, nonce, clear, clear_len, &file);
+  if (rc) return rc;
+  return buf_set(out, file.data(), file.size());
+}
+
+int ce_cryptor_decrypt_batch(ce_ctx* c, const uint8_t key_version[16], const uint8_t* key,
+                             size_t key_len, const uint8_t* blob, const uint64_t* offs, uint32_t n,
+                             uint8_t* out_blob, uint64_t* out_offs, uint64_t* out_lens,
+                             int32_t* status) {
+  if (!c || !key_version || !offs || !out_blob || !out_offs || !out_lens || !status)
+    return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
+  KeyRef k{key_version, key, key_len};
+  // Cryptor::decrypt checks the key before anything else (xchacha lib.rs:74-78)
+  if (int32_t ks = key_status(k)) {
+    for (uint32_t i = 0; i < n; i++) { status[i] = ks; out_lens[i] = 0; out_offs[i] = 0; }
+    return n ? ks : CE_OK;
+  }
+  if (n == 0) return CE_OK;
+  const uint64_t blen = offs[n];
+  hipError_t e;
+  if ((e = c->blob.reserve(blen + 64)) || (e = c->offs.reserve((n + 1) * 8ull)) ||
+      (e = c->out.reserve(blen + 16ull * n + 128)))
+    return c->hip_fail(e, "decrypt_batch reserve");
+  if ((e = hipMemcpyAsync(c->blob.p, blob, blen, hipMemcpyHostToDevice, c->stream)) ||
+      (e = hipMemcpyAsync(c->offs.p, offs, (n + 1) * 8ull, hipMemcpyHostToDevice, c->stream)))
+    return c->hip_fail(e, "decrypt_batch upload");
+  int rc = device_open(c, c->blob.as<uint8_t>(), c->offs.as<uint64_t>(), n, blen, false, k,
+                       c->out.as<uint8_t>(), c->status.as<int32_t>(), false);
+  if (rc) return rc;
+  std::vector<FileParams> P(n);
+  if ((e = hipMemcpyAsync(status, c->status.p, n * 4ull, hipMemcpyDeviceToHost, c->stream)) ||
+      (e = hipMemcpyAsync(P.data(), c->params.p, n * sizeof(FileParams), hipMemcpyDeviceToHost,
+                          c->stream)) ||
+      (e = hipMemcpyAsync(out_blob, c->out.p, blen + 16ull * n, hipMemcpyDeviceToHost, c->stream)) ||
+      (e = hipStreamSynchronize(c->stream)))
+    return c->hip_fail(e, "decrypt_batch download");
+  int first = CE_OK;
+  for (uint32_t i = 0; i < n; i++) {
+    out_offs[i] = P[i].out_off;
+    out_lens[i] = status[i] == CE_OK ? P[i].len : 0;
+    if (status[i] == kStatusHostParse) {
+      // exotic byte-string encoding: not decoded in place on the device
+      status[i] = CE_ERR_PARSE_ENCBOX;
+    }
+    if (status[i] != CE_OK && first == CE_OK) first = status[i];
+  }
+  return first;
+}
+
+int ce_cryptor_decrypt(ce_ctx* c, const uint8_t key_version[16], const uint8_t* key,
+                       size_t key_len, const uint8_t* enc, size_t enc_len, ce_buf* out) {
+  if (!c || !out || (enc_len && !enc)) return CE_ERR_INVALID_ARG;
+  const uint64_t offs[2] = {0, enc_len};
+  std::vector<uint8_t> ob(enc_len + 16 + 64);
+  uint64_t oo = 0, ol = 0;
+  int32_t st = 0;
+  int rc = ce_cryptor_decrypt_batch(c, key_version, key, key_len, enc, offs, 1, ob.data(), &oo,
+                                    &ol, &st);
+  if (rc) return rc;
+  return buf_set(out, ob.data() + oo, ol);
+}
+
+int ce_cryptor_encrypt_batch(ce_ctx* c, const uint8_t key_version[16], const uint8_t* key,
+                             size_t key_len, const uint8_t* blob, const uint64_t* offs, uint32_t n,
+                             const uint8_t* nonces, uint8_t* out_blob, size_t out_cap,
+                             uint64_t* out_offs) {
+  if (!c || !key_version || !offs || !out_offs) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
+  KeyRef k{key_version, key, key_len};
+  if (int32_t ks = key_status(k)) return ks;
+  out_offs[0] = 0;
+  for (uint32_t i = 0; i < n; i++) out_offs[i + 1] = out_offs[i] + sealed_len(offs[i + 1] - offs[i]);
+  if (n == 0) return CE_OK;
+  if (out_offs[n] > out_cap || !out_blob) return CE_ERR_INVALID_ARG;
+  const uint64_t blen = offs[n];
+  std::vector<uint8_t> nb;
+  if (!nonces) {
+    nb.resize(24ull * n);
+    os_random(nb.data(), nb.size());
+    nonces = nb.data();
+  }
+  hipError_t e;
+  if ((e = c->blob.reserve(blen + 64)) || (e = c->offs.reserve((n + 1) * 8ull)) ||
+      (e = c->out_offs.reserve((n + 1) * 8ull)) || (e = c->nonces.reserve(24ull * n)) ||
+      (e = c->out.reserve(out_offs[n] + 64)))
+    return c->hip_fail(e, "encrypt_batch reserve");
+  if ((e = hipMemcpyAsync(c->blob.p, blob, blen, hipMemcpyHostToDevice, c->stream)) ||
+      (e = hipMemcpyAsync(c->offs.p, offs, (n + 1) * 8ull, hipMemcpyHostToDevice, c->stream)) ||
+      (e = hipMemcpyAsync(c->out_offs.p, out_offs, (n + 1) * 8ull, hipMemcpyHostToDevice, c->stream)) ||
+      (e = hipMemcpyAsync(c->nonces.p, nonces, 24ull * n, hipMemcpyHostToDevice, c->stream)))
+    return c->hip_fail(e, "encrypt_batch upload");
+  int rc = device_seal(c, c->blob.as<uint8_t>(), c->offs.as<uint64_t>(), n, blen, nullptr,
+                       c->nonces.as<uint8_t>(), c->out.as<uint8_t>(), c->out_offs.as<uint64_t>(), k);
+  if (rc) return rc;
+  if ((e = hipMemcpyAsync(out_blob, c->out.p, out_offs[n], hipMemcpyDeviceToHost, c->stream)) ||
+      (e = hipStreamSynchronize(c->stream)))
+    return c->hip_fail(e, "encrypt_batch download");
+  return CE_OK;
+}
+
+int ce_cryptor_decrypt_batch_device(ce_ctx* c, const uint8_t key_version[16], const uint8_t* key,
+                                    size_t key_len, const uint8_t* d_blob, const uint64_t* d_offs,
+                                    uint32_t n, uint8_t* d_out, int32_t* d_status,
+                                    uint32_t* n_failed) {
+  if (!c || !key_version || !d_blob || !d_offs || !d_out) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
+  KeyRef k{key_version, key, key_len};
+  uint64_t blen = 0;
+  hipError_t e;
+  if (n && ((e = hipMemcpyAsync(&blen, d_offs + n, 8, hipMemcpyDeviceToHost, c->stream)) ||
+            (e = hipStreamSynchronize(c->stream))))
+    return c->hip_fail(e, "decrypt_batch_device offs");
+  int32_t* st = d_status;
+  if (!st) {
+    if ((e = c->status.reserve(n * 4ull + 64))) return c->hip_fail(e, "status");
+    st = c->status.as<int32_t>();
+  }
+  int rc = device_open(c, d_blob, d_offs, n, blen, false, k, d_out, st, n_failed != nullptr);
+  if (rc) return rc;
+  if (n_failed) {
+    const uint32_t* hc = c->h_counters.as<uint32_t>();
+    *n_failed = hc[2];
+  }
+  return CE_OK;
+}
+
+int ce_cryptor_encrypt_batch_device(ce_ctx* c, const uint8_t key_version[16], const uint8_t* key,
+                                    size_t key_len, const uint8_t* outer_version,
+                                    const uint8_t* d_clear, const uint64_t* d_offs, uint32_t n,
+                                    const uint8_t* d_nonces, uint8_t* d_out,
+                                    const uint64_t* d_out_offs) {
+  if (!c || !key_version || !d_clear || !d_offs || !d_nonces || !d_out || !d_out_offs)
+    return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
+  KeyRef k{key_version, key, key_len};
+  uint64_t blen = 0;
+  hipError_t e;
+  if (n && ((e = hipMemcpyAsync(&blen, d_offs + n, 8, hipMemcpyDeviceToHost, c->stream)) ||
+            (e = hipStreamSynchronize(c->stream))))
+    return c->hip_fail(e, "encrypt_batch_device offs");
+  const uint8_t* dov = nullptr;
+  if (outer_version) {
+    if ((e = c->outer_ver.reserve(64)) ||
+        (e = hipMemcpyAsync(c->outer_ver.p, outer_version, 16, hipMemcpyHostToDevice, c->stream)))
+      return c->hip_fail(e, "outer version");
+    dov = c->outer_ver.as<uint8_t>();
+  }
+  return device_seal(c, d_clear, d_offs, n, blen, dov, d_nonces, d_out, d_out_offs, k);
+}
+
+}  // extern "C"

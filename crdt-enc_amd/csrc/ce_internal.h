@@ -1,0 +1,117 @@
+// ce_internal.h -- host-side internals shared by ce_ctx.cpp, ce_storage.cpp, ce_core.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "ce_common.h"
+#include "ce_kernels.h"
+#include "crdtenc.h"
+
+namespace ce {
+
+using Uuid = std::array<uint8_t, 16>;
+
+struct UuidHash {
+  size_t operator()(const Uuid& u) const {
+    uint32_t w[4];
+    std::memcpy(w, u.data(), 16);
+    return actor_hash(w[0], w[1], w[2], w[3]);
+  }
+};
+
+std::string uuid_to_string(const Uuid& u);              // lowercase hyphenated
+bool uuid_parse(const std::string& s, Uuid* out);       // Uuid::from_str formats
+void os_random(uint8_t* out, size_t n);                 // getrandom(2)
+Uuid uuid_v4();
+void sha3_256(const uint8_t* msg, size_t len, uint8_t out[32]);
+std::string base32_nopad(const uint8_t* in, size_t len);
+
+// growable device buffer
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t reserve(size_t bytes);
+  ~DevBuf();
+  template <typename T>
+  T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+// growable pinned host buffer
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t reserve(size_t bytes);
+  ~HostBuf();
+  template <typename T>
+  T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+struct KeyRef {
+  const uint8_t* version;  // 16
+  const uint8_t* key;
+  size_t len;
+};
+
+// Result of a device open pass.
+struct OpenResult {
+  uint32_t auth_failed = 0;
+  uint32_t first_fail = 0xffffffffu;
+};
+
+}  // namespace ce
+
+struct ce_storage {
+  std::string local, remote;  // crdt-enc-tokio Storage{local_path, remote_path} (lib.rs:22-26)
+};
+
+struct ce_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  std::recursive_mutex mu;
+  std::string last_error;
+  // batch scratch (device)
+  ce::DevBuf params, status, counters, extra, multi, partials, out, apply, refold, miss,
+      supported, blob, offs, nonces, out_offs, outer_ver, batch_counters;
+  ce::HostBuf h_counters, h_apply, h_stage, h_stage2;
+
+  int fail(int code, const std::string& msg) {
+    last_error = msg;
+    return code;
+  }
+  int hip_fail(hipError_t e, const char* where) {
+    last_error = std::string(where) + ": " + hipGetErrorString(e);
+    return CE_ERR_DEVICE;
+  }
+};
+
+namespace ce {
+
+int32_t key_status(const KeyRef& k);
+DevKey dev_key(const KeyRef& k);
+
+// Open n files resident in HBM (d_blob/d_offs) on ctx's stream; plaintexts land in ctx->out.
+// outer: files carry the core's 16-byte version prefix.  After the call ctx->status holds the
+// per-file statuses and ctx->params the FileParams; counters are copied to h_counters.
+int device_open(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
+                uint64_t blob_len, bool outer, const KeyRef& key, uint8_t* d_out,
+                int32_t* d_status, bool sync_counters);
+
+// Seal n clear texts resident in HBM.  d_out_offs[i] = output start of file i.
+int device_seal(ce_ctx* ctx, const uint8_t* d_clear, const uint64_t* d_offs, uint32_t n,
+                uint64_t clear_len_total, const uint8_t* d_outer_version, const uint8_t* d_nonces,
+                uint8_t* d_out, const uint64_t* d_out_offs, const KeyRef& key);
+
+// Seal one host clear text into a host file: [outer(16)] || Cryptor::encrypt(clear).
+int seal_one(ce_ctx* ctx, const KeyRef& key, const uint8_t* outer_version, const uint8_t* nonce,
+             const uint8_t* clear, size_t clear_len, std::vector<uint8_t>* file);
+
+uint32_t grid_waves_for(uint32_t work);
+
+}  // namespace ce

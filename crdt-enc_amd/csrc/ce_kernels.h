@@ -1,0 +1,90 @@
+// ce_kernels.h -- host-side launch interface of the gfx950 kernels (ce_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ce_common.h"
+
+namespace ce {
+
+// Segment = up to kSegPages pages of 4 KiB of ciphertext processed by one wavefront.
+static constexpr uint32_t kPageBytes = 4096;
+static constexpr uint32_t kSegPages = 4;
+static constexpr uint32_t kSegBlocks = kSegPages * kPageBytes / 16;  // Poly1305 blocks
+
+// Per-file AEAD parameters written by the setup kernels (256 B, read with scalar loads).
+struct alignas(16) FileParams {
+  uint32_t subkey[8];    // HChaCha20(key, nonce[0:16])
+  uint32_t n2[2];        // nonce[16:24] (ChaCha20 nonce words 14, 15; word 13 = 0)
+  uint32_t pad0[2];
+  uint32_t s[4];         // Poly1305 s
+  uint32_t tag[4];       // expected tag (open)
+  uint32_t rpow[7][5];   // r^(2^k), k = 0..6, radix-2^26 limbs
+  uint32_t pad1;
+  uint64_t in_off;       // open: ciphertext offset in the input blob; seal: clear text offset
+  uint64_t out_off;      // open: plaintext offset in the output; seal: ciphertext offset
+  uint32_t len;          // ciphertext length without tag (== plaintext length)
+  int32_t status;
+  uint32_t nseg;
+  uint32_t extra_base;   // first entry of this file's extra segments (nseg > 1)
+};
+static_assert(sizeof(FileParams) == 256, "FileParams layout");
+
+struct DevKey {
+  uint32_t k[8];
+};
+
+// device scratch shared by one batch
+struct SegScratch {
+  uint32_t* counters;     // [0] extra segments, [1] multi-segment files, [2] auth failures,
+                          // [3] decode failures, [4] misses, [5] first failing index (min),
+                          // [6] partial slots, [7] host-parse envelopes, [8] setup failures
+  uint2* extra_list;      // (file, seg) for segments j >= 1
+  uint32_t extra_cap;
+  uint32_t* multi_files;  // files with nseg > 1
+  uint32_t* partials;     // 5 limbs per segment: [file-major] base = extra index
+};
+
+// file-level open: outer version check (when outer), envelope parse, key schedule.
+hipError_t launch_open_setup(hipStream_t s, const uint8_t* blob, const uint64_t* offs,
+                             uint32_t n, bool outer, DevKey key, int32_t key_status,
+                             FileParams* params, int32_t* status, SegScratch sc);
+// seal setup: header write + key schedule; out_offs[i] = start of output i.
+hipError_t launch_seal_setup(hipStream_t s, const uint8_t* clear, const uint64_t* offs,
+                             uint32_t n, const uint8_t* outer_version /* device, or null */,
+                             const uint8_t* nonces, uint8_t* out, const uint64_t* out_offs,
+                             DevKey key, FileParams* params, SegScratch sc);
+// one wavefront per segment (grid-stride); seal selects encrypt.
+hipError_t launch_segments(hipStream_t s, bool seal, const uint8_t* in, uint8_t* out,
+                           const FileParams* params, uint32_t n, int32_t* status, SegScratch sc,
+                           uint32_t grid_waves);
+// multi-segment files: combine partial Poly1305 sums, emit/compare tag (one lane per file).
+hipError_t launch_finalize_multi(hipStream_t s, bool seal, uint8_t* out, const FileParams* params,
+                                 int32_t* status, SegScratch sc);
+
+// decode Vec<Dot<Uuid>> of every opened file and max-fold the dots of applied files into
+// batch_counters (dense by actor slot).  One wavefront per file.
+struct DecodeArgs {
+  const uint8_t* pt;            // plaintext blob (FileParams.out_off / len)
+  const FileParams* params;
+  int32_t* status;
+  uint32_t n;
+  const uint8_t* supported;     // n_supported * 16 bytes (device)
+  uint32_t n_supported;
+  const uint8_t* apply;         // 1 = fold this file (version gate), null = all
+  const ActorSlot* table;       // open addressing, capacity = mask + 1
+  uint32_t mask;
+  unsigned long long* batch;    // [capacity] max counters
+  uint32_t* counters;           // SegScratch counters
+  uint4* miss_list;             // actors not in the table
+  uint32_t miss_cap;
+  uint8_t* refold;              // per file: had a miss
+  const uint8_t* only;          // null, or per-file: process only files with only[i] != 0
+};
+hipError_t launch_decode_dots(hipStream_t s, const DecodeArgs& a, uint32_t grid_waves);
+
+// dst[i] = max(dst[i], src[i])
+hipError_t launch_merge_max(hipStream_t s, unsigned long long* dst,
+                            const unsigned long long* src, uint32_t n);
+
+}  // namespace ce

@@ -1,0 +1,256 @@
+/*
+ * crdtenc.h -- C ABI of the MI355X-native crdt-enc compaction/ingest hot path.
+ *
+ * Every entry point replaces one reference interface (Rust, chpio/crdt-enc @ /root/reference):
+ *   Cryptor  trait   crdt-enc/src/cryptor.rs:11-27         -> ce_cryptor_*
+ *            impl    crdt-enc-xchacha20poly1305/src/lib.rs:28-101 (EncHandler)
+ *   Storage  trait   crdt-enc/src/storage.rs:8-43          -> ce_storage_*
+ *            impl    crdt-enc-tokio/src/lib.rs:48-316       (local-dir layout)
+ *   Core     API     crdt-enc/src/lib.rs:226 open, :332 compact, :390 read_remote,
+ *                    :666 apply_ops, :325 with_state        -> ce_core_*
+ * INTEGRATION.md shows the Rust FFI binding a maintainer would add on the reference side.
+ *
+ * Conventions: plain pointers and sizes; no torch/HIP types.  Functions return a ce_status
+ * (0 = CE_OK).  Buffers returned in a ce_buf are owned by the caller and released with
+ * ce_buf_free.  All entry points are thread-safe per ce_ctx (internally serialized; the
+ * reference issues <= 16 concurrent decrypts, crdt-enc/src/lib.rs:452,512).
+ */
+#ifndef CRDTENC_H
+#define CRDTENC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Per-file / per-call status, numbered in the reference's check order. */
+enum ce_status {
+  CE_OK = 0,
+  CE_ERR_OUTER_LEN = 1,     /* VersionBytes::deserialize InvalidLength (version_bytes.rs:187)  */
+  CE_ERR_OUTER_VERSION = 2, /* ensure_versions_phf(SUPPORTED_VERSIONS) (lib.rs:435,501)        */
+  CE_ERR_KEY_VERSION = 3,   /* "not matching key version" (xchacha lib.rs:74-75)               */
+  CE_ERR_KEY_LEN = 4,       /* "Invalid key length" (xchacha lib.rs:76-78)                     */
+  CE_ERR_PARSE_VBOX = 5,    /* "failed to parse version box" (xchacha lib.rs:82-83)            */
+  CE_ERR_DATA_VERSION = 6,  /* "not matching version of encryption box" (xchacha lib.rs:84-86) */
+  CE_ERR_PARSE_ENCBOX = 7,  /* "failed to parse encryption box" (xchacha lib.rs:87-88)         */
+  CE_ERR_NONCE_LEN = 8,     /* "Invalid nonce length" (xchacha lib.rs:89-91)                   */
+  CE_ERR_AUTH = 9,          /* "Decryption failed" (xchacha lib.rs:92-97)                      */
+  CE_ERR_PT_LEN = 10,       /* clear text VersionBytesRef::deserialize (lib.rs:443,504)        */
+  CE_ERR_PT_VERSION = 11,   /* ensure_versions(supported_data_versions) (lib.rs:444,505)       */
+  CE_ERR_DECODE = 12,       /* rmp_serde::from_slice of ops / StateWrapper (lib.rs:447,507)    */
+  CE_ERR_OP_VERSION = 13,   /* "Unexpected op version" (lib.rs:527-531)                        */
+  CE_ERR_INVALID_ARG = 64,
+  CE_ERR_DEVICE = 65,       /* HIP runtime failure / no GPU: the product has no CPU path       */
+  CE_ERR_NO_KEY = 66,       /* "no latest key" (lib.rs:420,490)                                */
+  CE_ERR_IO = 67,
+  CE_ERR_NO_LOCAL_META = 68 /* "local meta does not exist, and `create` option is not set"     */
+};
+
+typedef struct ce_buf {
+  uint8_t *data;
+  size_t len;
+} ce_buf;
+
+void ce_buf_free(ce_buf *b);
+const char *ce_status_str(int status);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Context: one per GPU (one process per GPU).                                               */
+/* ---------------------------------------------------------------------------------------- */
+typedef struct ce_ctx ce_ctx;
+
+int ce_ctx_create(int device, ce_ctx **out);
+void ce_ctx_destroy(ce_ctx *ctx);
+/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL = own. */
+int ce_ctx_set_stream(ce_ctx *ctx, void *hip_stream);
+void ce_ctx_synchronize(ce_ctx *ctx);
+/* Human readable detail of the last failure on this context. */
+const char *ce_ctx_last_error(ce_ctx *ctx);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Cryptor: XChaCha20-Poly1305 EncHandler on the GPU                                          */
+/*   (trait crdt-enc/src/cryptor.rs:11-27; impl crdt-enc-xchacha20poly1305/src/lib.rs:28-101) */
+/* ---------------------------------------------------------------------------------------- */
+/* Cryptor::gen_key (xchacha lib.rs:29-38): out = VersionBytes(KEY_VERSION, 32 random bytes)
+ * in the raw framing (16-byte version || 32-byte key; version_bytes.rs:198-208). */
+int ce_cryptor_gen_key(ce_ctx *ctx, ce_buf *out);
+
+/* Cryptor::encrypt (xchacha lib.rs:40-71): out = msgpack(VersionBytesRef(DATA_VERSION,
+ * msgpack(EncBox{nonce, enc_data}))).  nonce: 24 bytes, or NULL to draw from the OS RNG
+ * (the reference uses rand::rng(), lib.rs:51-54). */
+int ce_cryptor_encrypt(ce_ctx *ctx, const uint8_t key_version[16], const uint8_t *key,
+                       size_t key_len, const uint8_t *nonce, const uint8_t *clear,
+                       size_t clear_len, ce_buf *out);
+
+/* Cryptor::decrypt (xchacha lib.rs:73-101): enc = VersionBytes content (the outer 16-byte
+ * version already stripped by the caller, lib.rs:502).  No plaintext is returned for a file
+ * whose tag fails. */
+int ce_cryptor_decrypt(ce_ctx *ctx, const uint8_t key_version[16], const uint8_t *key,
+                       size_t key_len, const uint8_t *enc, size_t enc_len, ce_buf *out);
+
+/* Length of Cryptor::encrypt's output for a clear text of clear_len bytes. */
+size_t ce_cryptor_sealed_len(size_t clear_len);
+
+/* Batched Cryptor::decrypt over host buffers: input i = blob[offs[i], offs[i+1]).
+ * out_blob must hold offs[n] + 16*n bytes; plaintext i is written at out_offs[i] with length
+ * out_lens[i] (both outputs, n entries).  status[i] receives the per-file status; the call
+ * returns CE_OK when every file opened, else the status of the lowest failing index.  A file
+ * whose tag fails has its output region zeroed (verify-before-release). */
+int ce_cryptor_decrypt_batch(ce_ctx *ctx, const uint8_t key_version[16], const uint8_t *key,
+                             size_t key_len, const uint8_t *blob, const uint64_t *offs,
+                             uint32_t n, uint8_t *out_blob, uint64_t *out_offs,
+                             uint64_t *out_lens, int32_t *status);
+
+/* Batched Cryptor::encrypt: clear text i = blob[offs[i], offs[i+1]); nonces = n*24 bytes or
+ * NULL (OS RNG).  Output i is written at out_offs[i] (n+1 entries, computed by the call; size
+ * out_offs[n] = sum of ce_cryptor_sealed_len) into out_blob (capacity out_cap). */
+int ce_cryptor_encrypt_batch(ce_ctx *ctx, const uint8_t key_version[16], const uint8_t *key,
+                             size_t key_len, const uint8_t *blob, const uint64_t *offs,
+                             uint32_t n, const uint8_t *nonces, uint8_t *out_blob,
+                             size_t out_cap, uint64_t *out_offs);
+
+/* Device-resident variants: every pointer is a device pointer (hipMalloc / torch tensor);
+ * the work is enqueued on the context stream and the call returns after enqueueing unless
+ * noted.  d_offs has n+1 entries.  d_out must hold offs[n] + 16*n + 64 bytes; plaintext i
+ * lands at align16(offs[i]) (see DESIGN.md "HBM layout").  d_status may be NULL. */
+int ce_cryptor_decrypt_batch_device(ce_ctx *ctx, const uint8_t key_version[16],
+                                    const uint8_t *key, size_t key_len, const uint8_t *d_blob,
+                                    const uint64_t *d_offs, uint32_t n, uint8_t *d_out,
+                                    int32_t *d_status, uint32_t *n_failed);
+/* Seal n clear texts of d_clear[d_offs[i], d_offs[i+1]) into op files
+ * CURRENT_VERSION || Cryptor::encrypt(...) at d_out[d_out_offs[i], ...).  d_nonces = n*24
+ * device bytes.  outer_version: 16 bytes or NULL (no outer prefix). */
+int ce_cryptor_encrypt_batch_device(ce_ctx *ctx, const uint8_t key_version[16],
+                                    const uint8_t *key, size_t key_len,
+                                    const uint8_t *outer_version, const uint8_t *d_clear,
+                                    const uint64_t *d_offs, uint32_t n, const uint8_t *d_nonces,
+                                    uint8_t *d_out, const uint64_t *d_out_offs);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Storage: crdt-enc-tokio local-dir layout (crdt-enc-tokio/src/lib.rs)                        */
+/*   local/meta-data.msgpack, remote/{meta,states}/<BASE32_NOPAD(SHA3-256)>,                   */
+/*   remote/ops/<uuid>/<version>                                                              */
+/* ---------------------------------------------------------------------------------------- */
+typedef struct ce_storage ce_storage;
+
+/* Storage::new (tokio lib.rs:29-45): both paths must be absolute. */
+int ce_storage_open(const char *local_path, const char *remote_path, ce_storage **out);
+void ce_storage_close(ce_storage *s);
+/* list_op_actors (tokio lib.rs:204-220): out = m*16 bytes of actor UUIDs */
+int ce_storage_list_op_actors(ce_storage *s, ce_buf *out);
+/* load_ops (tokio lib.rs:222-278): for each (actor, first) read ops/<actor>/<v> for
+ * v = first.. until the first missing file.  Outputs (caller frees with ce_buf_free):
+ * blob = concatenated files, offs = (k+1) u64, actor_idx = k u32 (index into actors),
+ * versions = k u64. */
+int ce_storage_load_ops(ce_storage *s, const uint8_t *actors, const uint64_t *first, uint32_t m,
+                        ce_buf *blob, ce_buf *offs, ce_buf *actor_idx, ce_buf *versions);
+/* store_ops (tokio lib.rs:280-293): create-new + fsync */
+int ce_storage_store_ops(ce_storage *s, const uint8_t actor[16], uint64_t version,
+                         const uint8_t *data, size_t len);
+/* remove_ops (tokio lib.rs:295-315): NotFound is not an error */
+int ce_storage_remove_ops(ce_storage *s, const uint8_t *actors, const uint64_t *versions,
+                          uint32_t m);
+/* list_state_names (tokio lib.rs:138-153): out = NUL-separated names */
+int ce_storage_list_state_names(ce_storage *s, ce_buf *out);
+/* store_state (tokio lib.rs:174-179): name = BASE32_NOPAD(SHA3-256(bytes)), 52 chars + NUL */
+int ce_storage_store_state(ce_storage *s, const uint8_t *data, size_t len, char name_out[64]);
+int ce_storage_load_state(ce_storage *s, const char *name, ce_buf *out);
+int ce_storage_remove_state(ce_storage *s, const char *name);
+/* content address of a blob: BASE32_NOPAD(SHA3-256(data)) (tokio lib.rs:403-417) */
+int ce_content_name(const uint8_t *data, size_t len, char name_out[64]);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Core (crdt-enc/src/lib.rs)                                                                */
+/* ---------------------------------------------------------------------------------------- */
+typedef struct ce_core ce_core;
+
+/* StateWrapper<S> state type S */
+enum ce_state_kind { CE_STATE_VCLOCK = 0, CE_STATE_GCOUNTER = 1 };
+
+enum ce_open_flags {
+  CE_OPEN_CREATE = 1,            /* OpenOptions.create (lib.rs:729)                          */
+  CE_COMPACT_INGEST_FORMAT = 2   /* write compacted states in the format read_remote_states
+                                    reads (outer CURRENT_VERSION + inner data-version prefix)
+                                    instead of the reference's compact() bytes   */
+};
+
+typedef struct ce_open_options {
+  int state_kind;                        /* ce_state_kind                                  */
+  const uint8_t *supported_data_versions; /* n_supported * 16 bytes (lib.rs:730)             */
+  size_t n_supported;
+  const uint8_t *current_data_version;   /* 16 bytes (lib.rs:731)                          */
+  const char *local_path;                /* NULL: no storage (ingest API only)             */
+  const char *remote_path;
+  uint32_t flags;                        /* ce_open_flags                                  */
+} ce_open_options;
+
+/* Core::open (lib.rs:226-311) minus the key-cryptor handshake: the latest data key is
+ * supplied with ce_core_set_latest_key (Keys::latest_key, key_cryptor.rs:59-70). */
+int ce_core_open(ce_ctx *ctx, const ce_open_options *opts, ce_core **out);
+void ce_core_close(ce_core *c);
+int ce_core_set_latest_key(ce_core *c, const uint8_t key_version[16], const uint8_t *key,
+                           size_t key_len);
+/* Core::info().actor() (lib.rs:313-322) */
+int ce_core_info_actor(ce_core *c, uint8_t out[16]);
+/* Core::read_remote (lib.rs:390-399): read_remote_states then read_remote_ops via Storage */
+int ce_core_read_remote(ce_core *c);
+/* Core::compact (lib.rs:332-380).  name_out (may be NULL) receives the new state's name. */
+int ce_core_compact(ce_core *c, char name_out[64]);
+/* Core::apply_ops (lib.rs:666-722): ops = rmp-serde msgpack of Vec<S::Op> (Vec<Dot<Uuid>>). */
+int ce_core_apply_ops(ce_core *c, const uint8_t *ops, size_t len);
+/* rmp_serde::to_vec_named(&StateWrapper) (lib.rs:336, 739-743) */
+int ce_core_state_bytes(ce_core *c, ce_buf *out);
+
+/* Storage-less ingest: what read_remote_ops does after Storage::load_ops (lib.rs:495-546).
+ * files i = blob[offs[i], offs[i+1]) (outer version || cryptor box); the writer of file i is
+ * actors[file_actor[i]] (m actors, 16 bytes each) with version file_version[i].  status may
+ * be NULL.  Returns CE_OK, the lowest failing file's status (nothing folded), or
+ * CE_ERR_OP_VERSION (fold stopped at the gap, as the reference's loop). */
+int ce_core_ingest_ops(ce_core *c, const uint8_t *blob, const uint64_t *offs, uint32_t n,
+                       const uint8_t *actors, uint32_t m, const uint32_t *file_actor,
+                       const uint64_t *file_version, int32_t *status);
+/* Same with the files already resident in HBM (d_blob/d_offs device pointers, d_offs has n+1
+ * entries and blob_len = offs[n]); actor metadata stays on the host. */
+int ce_core_ingest_ops_device(ce_core *c, const uint8_t *d_blob, const uint64_t *d_offs,
+                              uint32_t n, uint64_t blob_len, const uint8_t *actors, uint32_t m,
+                              const uint32_t *file_actor, const uint64_t *file_version,
+                              int32_t *status);
+/* What read_remote_states does after Storage::load_states (lib.rs:425-466). */
+int ce_core_ingest_states(ce_core *c, const uint8_t *blob, const uint64_t *offs, uint32_t n,
+                          int32_t *status);
+/* compact() without storage: serialize the state, seal it on the GPU with the latest key and
+ * return the state file bytes and its content name.  nonce: 24 bytes or NULL (OS RNG). */
+int ce_core_compact_to_buffer(ce_core *c, const uint8_t *nonce, ce_buf *file, char name_out[64]);
+
+/* Dense state exchange for multi-GPU merges (one process per GPU): actors registered in the
+ * same order on every rank get the same dense index.  export copies the dense state counters
+ * (u64[cap]) and next_op_versions (u64[cap]) into device buffers; import max-merges them back.
+ * cap = ce_core_dense_capacity(). */
+int ce_core_register_actors(ce_core *c, const uint8_t *actors, uint32_t m);
+uint32_t ce_core_dense_capacity(ce_core *c);
+int ce_core_export_dense(ce_core *c, uint64_t *d_state, uint64_t *d_nov);
+int ce_core_import_dense(ce_core *c, const uint64_t *d_state, const uint64_t *d_nov);
+
+/* Framing helpers (crdt-enc/src/utils/version_bytes.rs): VersionBytesBuf chunk/advance. */
+typedef struct ce_vbuf {
+  size_t pos;
+  uint8_t version[16];
+  const uint8_t *content;
+  size_t content_len;
+} ce_vbuf;
+void ce_vbuf_init(ce_vbuf *b, const uint8_t version[16], const uint8_t *content, size_t len);
+size_t ce_vbuf_remaining(const ce_vbuf *b);
+/* current chunk; returns its length */
+size_t ce_vbuf_chunk(const ce_vbuf *b, const uint8_t **chunk);
+/* returns 0, or -1 when cnt > remaining (the reference panics, version_bytes.rs:281) */
+int ce_vbuf_advance(ce_vbuf *b, size_t cnt);
+/* chunks_vectored (version_bytes.rs:285-308): fills up to n_dst (ptr,len) pairs */
+size_t ce_vbuf_chunks_vectored(const ce_vbuf *b, const uint8_t **dst_ptr, size_t *dst_len,
+                               size_t n_dst);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,347 @@
+"""GPU parity: the HIP path through the C ABI vs the oracle and the golden fixtures.
+
+Bit-exact everywhere (integer / byte work): plaintexts, ciphertexts, tags, per-file statuses,
+serialized StateWrapper bytes and content names.
+"""
+import os
+import random
+import struct
+
+import msgpack
+import pytest
+
+import crdtenc
+
+pytestmark = pytest.mark.gpu
+H = bytes.fromhex
+APP = H("aadfd5a66e194b24a8024fa27c72f20c")
+CORE = crdtenc.CORE_VERSION
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = crdtenc.Context(0)
+    yield c
+    c.close()
+
+
+def box(nonce, ct):
+    return msgpack.packb([H("c7f269be0ff54a7799c37c23c96d5cb4"),
+                          msgpack.packb({"nonce": nonce, "enc_data": ct}, use_bin_type=True)],
+                         use_bin_type=True)
+
+
+# ------------------------------------------------------------------ cryptor (EncHandler)
+def test_encrypt_matches_oracle_every_length(ctx, oracle, kats):
+    for v in kats["xchacha"]:
+        key, nonce, pt = H(v["key"]), H(v["nonce"]), v["pt_bytes"]
+        enc = ctx.encrypt(key, pt, nonce=nonce)
+        st, want = oracle.cryptor_encrypt(key, nonce, pt)
+        assert st == 0 and enc == want, v["len"]
+        assert enc.endswith(v["ct_bytes"])                 # OpenSSL-generated ct || tag
+
+
+def test_decrypt_kat_vectors(ctx, kats):
+    for v in kats["xchacha"]:
+        key, nonce = H(v["key"]), H(v["nonce"])
+        st, pt = ctx.decrypt(key, box(nonce, v["ct_bytes"]))
+        assert st == 0 and pt == v["pt_bytes"], v["len"]
+
+
+def test_decrypt_batch_tamper_scrubs(ctx, kats):
+    items, want = [], []
+    key = H(kats["xchacha"][0]["key"])
+    rng = random.Random(5)
+    # one key for the whole batch: re-seal every vector's plaintext under `key`
+    for i, v in enumerate(kats["xchacha"]):
+        nonce = rng.randbytes(24)
+        enc = ctx.encrypt(key, v["pt_bytes"], nonce=nonce)
+        if i % 3 == 1 and v["len"] > 0:
+            b = bytearray(enc)
+            b[-1 - rng.randrange(16 + v["len"])] ^= 1 << rng.randrange(8)
+            enc = bytes(b)
+            want.append((9, None))
+        else:
+            want.append((0, v["pt_bytes"]))
+        items.append(enc)
+    rc, st, pts, raw, offs = ctx.decrypt_batch(key, items)
+    assert [s for s in st] == [w[0] for w in want]
+    assert rc == next(w[0] for w in want if w[0] != 0)
+    for i, (s, p) in enumerate(want):
+        if s == 0:
+            assert pts[i] == p
+        else:
+            # verify-before-release: the failed file's region holds no plaintext
+            n = len(kats["xchacha"][i]["pt_bytes"])
+            assert raw[offs[i]:offs[i] + n] == bytes(n)
+
+
+def test_key_checks_come_first(ctx, repo_fx):
+    key = H(repo_fx["key"])
+    f = H(repo_fx["files"][0]["file"])[16:]
+    assert ctx.decrypt(key, f, key_version=bytes(16))[0] == 3
+    assert ctx.decrypt(key[:31], f)[0] == 4
+    assert ctx.decrypt(key, b"\xc0")[0] == 5
+
+
+def test_encrypt_batch_random_nonces_roundtrip(ctx, oracle):
+    key = os.urandom(32)
+    clears = [os.urandom(n) for n in [0, 5, 4096, 16384 - 16, 16384 + 1, 70000]]
+    encs = ctx.encrypt_batch(key, clears)
+    for c, e in zip(clears, encs):
+        st, pt = oracle.cryptor_decrypt(key, e)
+        assert st == 0 and pt == c
+
+
+# ------------------------------------------------------------------ core ingest
+def files_of(repo_fx):
+    files = [H(f["file"]) for f in repo_fx["files"]]
+    actors = [H(a) for a in repo_fx["actors"]]
+    idx = {a: i for i, a in enumerate(actors)}
+    fa = [idx[H(f["actor"])] for f in repo_fx["files"]]
+    vers = [f["version"] for f in repo_fx["files"]]
+    return files, actors, fa, vers
+
+
+def new_core(ctx, repo_fx, kind, **kw):
+    c = crdtenc.Core(ctx, kind=kind, supported=[APP], current_data_version=APP, **kw)
+    c.set_latest_key(H(repo_fx["key"]))
+    return c
+
+
+@pytest.mark.parametrize("kind", ["gcounter", "vclock"])
+def test_ingest_ops_golden(ctx, repo_fx, kind):
+    k = crdtenc.STATE_GCOUNTER if kind == "gcounter" else crdtenc.STATE_VCLOCK
+    core = new_core(ctx, repo_fx, k)
+    files, actors, fa, vers = files_of(repo_fx)
+    rc, st = core.ingest_ops(files, actors, fa, vers)
+    assert rc == 0 and st == [0] * len(files)
+    assert core.state_bytes().hex() == repo_fx["expected_state"][kind]
+    # idempotent re-read: every file is below next_op_versions and skipped
+    rc, st = core.ingest_ops(files, actors, fa, vers)
+    assert rc == 0 and core.state_bytes().hex() == repo_fx["expected_state"][kind]
+
+
+@pytest.mark.parametrize("kind", ["gcounter", "vclock"])
+def test_ingest_states_then_ops(ctx, repo_fx, kind):
+    k = crdtenc.STATE_GCOUNTER if kind == "gcounter" else crdtenc.STATE_VCLOCK
+    core = new_core(ctx, repo_fx, k)
+    rc, st = core.ingest_states([H(repo_fx["state_files"][kind])])
+    assert rc == 0, st
+    files, actors, fa, vers = files_of(repo_fx)
+    rc, st = core.ingest_ops(files, actors, fa, vers)
+    assert rc == 0
+    assert core.state_bytes().hex() == repo_fx["expected_after_state_then_ops"][kind]
+
+
+def test_negative_statuses_match_fixture(ctx, repo_fx, oracle):
+    for case in repo_fx["negatives"]:
+        core = new_core(ctx, repo_fx, crdtenc.STATE_GCOUNTER)
+        empty = core.state_bytes()
+        rc, st = core.ingest_ops([H(case["file"])], [bytes(16)], [0], [0])
+        assert st[0] == case["status"], (case["name"], st[0], case["status"])
+        if case["status"]:
+            assert rc == case["status"] and core.state_bytes() == empty
+        # and the oracle agrees
+        oc = oracle.Core()
+        _, ost = oc.read_remote_ops(H(repo_fx["key"]), [APP], [H(case["file"])], [bytes(16)], [0])
+        assert ost == st
+
+
+def test_batch_reject_leaves_state(ctx, repo_fx):
+    core = new_core(ctx, repo_fx, crdtenc.STATE_GCOUNTER)
+    files, actors, fa, vers = files_of(repo_fx)
+    empty = core.state_bytes()
+    bad = bytearray(files[7])
+    bad[-3] ^= 1
+    files[7] = bytes(bad)
+    rc, st = core.ingest_ops(files, actors, fa, vers)
+    assert rc == 9 and st[7] == 9 and sum(s != 0 for s in st) == 1
+    assert core.state_bytes() == empty
+
+
+def test_version_gate_matches_oracle(ctx, repo_fx, oracle):
+    files, actors, fa, vers = files_of(repo_fx)
+    keep = [i for i in range(len(files)) if not (fa[i] == 1 and vers[i] == 3)]
+    sel = lambda xs: [xs[i] for i in keep]
+    core = new_core(ctx, repo_fx, crdtenc.STATE_GCOUNTER)
+    rc, st = core.ingest_ops(sel(files), actors, sel(fa), sel(vers))
+    oc = oracle.Core()
+    orc, ost = oc.read_remote_ops(H(repo_fx["key"]), [APP], sel(files), [actors[i] for i in sel(fa)],
+                                  sel(vers))
+    assert rc == orc == 13
+    assert st == ost
+    assert core.state_bytes() == oc.serialize()
+
+
+def test_compact_to_buffer_matches_fixture(ctx, repo_fx):
+    for kind, k in (("gcounter", crdtenc.STATE_GCOUNTER), ("vclock", crdtenc.STATE_VCLOCK)):
+        core = new_core(ctx, repo_fx, k)
+        files, actors, fa, vers = files_of(repo_fx)
+        assert core.ingest_ops(files, actors, fa, vers)[0] == 0
+        c = repo_fx["compact"][kind]
+        f, name = core.compact_to_buffer(nonce=H(c["nonce"]))
+        assert f.hex() == c["file"] and name == c["name"]
+
+
+# ------------------------------------------------------------------ larger random batches
+def make_ops_batch(ctx, key, n_actors, n_versions, dots_per_file, seed, stress=False):
+    rng = random.Random(seed)
+    actors = sorted(rng.randbytes(16) for _ in range(n_actors))
+    clears, fa, vers = [], [], []
+    for v in range(n_versions):
+        for a in range(n_actors):
+            dots = []
+            for d in range(dots_per_file):
+                if stress:
+                    dots.append({"actor": rng.choice(actors), "counter": rng.getrandbits(rng.choice([7, 8, 16, 32, 64]))})
+                else:
+                    dots.append({"actor": actors[a], "counter": v * dots_per_file + d + 1})
+            clears.append(APP + msgpack.packb(dots, use_bin_type=True))
+            fa.append(a)
+            vers.append(v)
+    # order files per actor (load_ops order): actor-major
+    order = sorted(range(len(clears)), key=lambda i: (fa[i], vers[i]))
+    clears = [clears[i] for i in order]
+    fa = [fa[i] for i in order]
+    vers = [vers[i] for i in order]
+    encs = ctx.encrypt_batch(key, clears)
+    files = [CORE + e for e in encs]
+    return files, actors, fa, vers
+
+
+@pytest.mark.parametrize("stress", [False, True])
+def test_random_batch_matches_oracle(ctx, oracle, stress):
+    key = os.urandom(32)
+    files, actors, fa, vers = make_ops_batch(ctx, key, 37, 9, 23, seed=11 + stress, stress=stress)
+    core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+    core.set_latest_key(key)
+    rc, st = core.ingest_ops(files, actors, fa, vers)
+    assert rc == 0 and set(st) == {0}
+    oc = oracle.Core()
+    orc, ost = oc.read_remote_ops(key, [APP], files, [actors[i] for i in fa], vers)
+    assert orc == 0
+    assert core.state_bytes() == oc.serialize()
+
+
+def test_unknown_dot_actors_grow_table(ctx, oracle):
+    """Dots naming actors that are not op writers (table misses -> refold)."""
+    key = os.urandom(32)
+    rng = random.Random(3)
+    writers = [rng.randbytes(16) for _ in range(3)]
+    others = [rng.randbytes(16) for _ in range(9000)]   # forces table growth past 8192 slots
+    clears = []
+    for i in range(30):
+        dots = [{"actor": rng.choice(others), "counter": rng.getrandbits(20)} for _ in range(400)]
+        clears.append(APP + msgpack.packb(dots, use_bin_type=True))
+    files = [CORE + e for e in ctx.encrypt_batch(key, clears)]
+    fa = [i % 3 for i in range(30)]
+    order = sorted(range(30), key=lambda i: (fa[i], i))
+    files = [files[i] for i in order]
+    fa = [fa[i] for i in order]
+    vers = []
+    cnt = {}
+    for a in fa:
+        vers.append(cnt.get(a, 0))
+        cnt[a] = cnt.get(a, 0) + 1
+    core = crdtenc.Core(ctx, kind=crdtenc.STATE_VCLOCK, supported=[APP], current_data_version=APP)
+    core.set_latest_key(key)
+    rc, st = core.ingest_ops(files, writers, fa, vers)
+    assert rc == 0
+    oc = oracle.Core(oracle.STATE_VCLOCK)
+    assert oc.read_remote_ops(key, [APP], files, [writers[i] for i in fa], vers)[0] == 0
+    assert core.state_bytes() == oc.serialize()
+
+
+def test_skewed_sizes_multi_segment(ctx, oracle):
+    """Files from 256 B to 1 MiB: multi-wave segments + partial Poly1305 combine."""
+    key = os.urandom(32)
+    rng = random.Random(9)
+    actor = rng.randbytes(16)
+    clears, ctr = [], 0
+    for i in range(12):
+        target = int(256 * (4096 ** (i / 11)))     # 256 B .. 1 MiB, log-spaced
+        ndots = max(1, target // 36)
+        dots = []
+        for _ in range(ndots):
+            ctr += rng.choice([1, 300, 70000])
+            dots.append({"actor": actor, "counter": ctr})
+        clears.append(APP + msgpack.packb(dots, use_bin_type=True))
+    files = [CORE + e for e in ctx.encrypt_batch(key, clears)]
+    core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+    core.set_latest_key(key)
+    rc, st = core.ingest_ops(files, [actor], [0] * 12, list(range(12)))
+    assert rc == 0
+    oc = oracle.Core()
+    assert oc.read_remote_ops(key, [APP], files, [actor] * 12, list(range(12)))[0] == 0
+    assert core.state_bytes() == oc.serialize()
+    # and a tamper in the middle of the biggest file is caught by the segment combine
+    bad = bytearray(files[-1])
+    bad[len(bad) // 2] ^= 2
+    core2 = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+    core2.set_latest_key(key)
+    rc, st = core2.ingest_ops(files[:-1] + [bytes(bad)], [actor], [0] * 12, list(range(12)))
+    assert rc == 9 and st[-1] == 9
+
+
+# ------------------------------------------------------------------ storage end to end
+def test_storage_apply_read_compact(ctx, tmp_path, oracle):
+    """Two replicas share a remote dir (syncthing-style, README.md:3-4)."""
+    key = os.urandom(32)
+    remote = str(tmp_path / "remote")
+    c1 = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP,
+                      local_path=str(tmp_path / "l1"), remote_path=remote, flags=crdtenc.OPEN_CREATE)
+    c2 = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP,
+                      local_path=str(tmp_path / "l2"), remote_path=remote,
+                      flags=crdtenc.OPEN_CREATE | crdtenc.COMPACT_INGEST_FORMAT)
+    for c in (c1, c2):
+        c.set_latest_key(key)
+    a1, a2 = c1.info_actor(), c2.info_actor()
+    for i in range(5):
+        assert c1.apply_ops(msgpack.packb([{"actor": a1, "counter": i + 1}], use_bin_type=True)) == 0
+    for i in range(3):
+        assert c2.apply_ops(msgpack.packb([{"actor": a2, "counter": 10 * (i + 1)}], use_bin_type=True)) == 0
+    assert c1.read_remote() == 0 and c2.read_remote() == 0
+    assert c1.state_bytes() == c2.state_bytes()
+    # the state equals the oracle fold of the stored op files
+    st = crdtenc.Storage(str(tmp_path / "l1"), remote)
+    loaded = st.load_ops([(a1, 0), (a2, 0)])
+    oc = oracle.Core()
+    assert oc.read_remote_ops(key, [APP], [x[2] for x in loaded], [x[0] for x in loaded],
+                              [x[1] for x in loaded])[0] == 0
+    assert c1.state_bytes() == oc.serialize()
+    # local meta survives a reopen (lib.rs:250-259)
+    c1b = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP,
+                       local_path=str(tmp_path / "l1"), remote_path=remote)
+    assert c1b.info_actor() == a1
+    # compact (ingest format) on c2: one state file, the last op of each actor removed
+    rc, name = c2.compact()
+    assert rc == 0 and st.list_state_names() == [name]
+    left = st.load_ops([(a1, 0), (a2, 0)])
+    assert [(x[0], x[1]) for x in left] == [(a1, v) for v in range(4)] + [(a2, v) for v in range(2)]
+    # a fresh replica reads the compacted state + skips the ops it already covers
+    c3 = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP,
+                      local_path=str(tmp_path / "l3"), remote_path=remote, flags=crdtenc.OPEN_CREATE)
+    c3.set_latest_key(key)
+    assert c3.read_remote() == 0
+    assert c3.state_bytes() == c2.state_bytes()
+
+
+def test_reference_compact_format_is_unreadable_by_read_remote(ctx, tmp_path):
+    """Core::compact writes VersionBytes(current_data_version, encrypt(state)),
+    which read_remote_states rejects (outer version != CURRENT_VERSION)."""
+    key = os.urandom(32)
+    remote = str(tmp_path / "remote")
+    c1 = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP,
+                      local_path=str(tmp_path / "l1"), remote_path=remote, flags=crdtenc.OPEN_CREATE)
+    c1.set_latest_key(key)
+    a1 = c1.info_actor()
+    assert c1.apply_ops(msgpack.packb([{"actor": a1, "counter": 7}], use_bin_type=True)) == 0
+    rc, name = c1.compact()
+    assert rc == 0
+    f = crdtenc.Storage(str(tmp_path / "l1"), remote).load_state(name)
+    assert f[:16] == APP
+    c2 = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP,
+                      local_path=str(tmp_path / "l2"), remote_path=remote, flags=crdtenc.OPEN_CREATE)
+    c2.set_latest_key(key)
+    assert c2.read_remote() == 2     # "version check failed" (lib.rs:435)
