@@ -42,7 +42,8 @@ EXPORTS = [
     "ce_core_ingest_ops_device", "ce_core_ingest_states", "ce_core_compact_to_buffer",
     "ce_core_register_actors", "ce_core_dense_capacity", "ce_core_export_dense",
     "ce_core_import_dense", "ce_vbuf_init", "ce_vbuf_remaining", "ce_vbuf_chunk",
-    "ce_vbuf_advance", "ce_vbuf_chunks_vectored",
+    "ce_vbuf_advance", "ce_vbuf_chunks_vectored", "ce_ctx_set_timing", "ce_ctx_timing_read",
+    "ce_ctx_timing_reset", "ce_core_reset",
 ]
 
 
@@ -149,6 +150,20 @@ class Context:
 
     def synchronize(self):
         lib().ce_ctx_synchronize(self.p)
+
+    def set_timing(self, enable=True):
+        self.check(lib().ce_ctx_set_timing(self.p, 1 if enable else 0), "set_timing")
+
+    def timing(self, kernel):
+        """(total_ms, launches) of one kernel since the last reset (HIP events on our stream)."""
+        ms = ctypes.c_double(0)
+        cnt = ctypes.c_uint64(0)
+        self.check(lib().ce_ctx_timing_read(self.p, kernel.encode(), ctypes.byref(ms),
+                                            ctypes.byref(cnt)), "timing")
+        return ms.value, cnt.value
+
+    def timing_reset(self):
+        lib().ce_ctx_timing_reset(self.p)
 
     # ---- Cryptor ----
     def gen_key(self):
@@ -404,6 +419,9 @@ class Core:
 
     def apply_ops(self, ops_msgpack):
         return lib().ce_core_apply_ops(self.p, _cbuf(ops_msgpack), ctypes.c_size_t(len(ops_msgpack)))
+
+    def reset(self):
+        self.ctx.check(lib().ce_core_reset(self.p), "reset")
 
     def register_actors(self, actors):
         self.ctx.check(lib().ce_core_register_actors(self.p, _cbuf(b"".join(actors)),

@@ -608,7 +608,11 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
   da.table = c->d_table.as<ActorSlot>();
   da.mask = c->cap - 1;
   da.batch = c->d_batch.as<unsigned long long>();
-  if ((e = launch_decode_dots(ctx->stream, da, grid_waves_for(n)))) return ctx->hip_fail(e, "decode");
+  {
+    const int t = ctx->tbegin("decode");
+    if ((e = launch_decode_dots(ctx->stream, da, grid_waves_for(n)))) return ctx->hip_fail(e, "decode");
+    ctx->tend(t);
+  }
   uint32_t* hc = ctx->h_counters.as<uint32_t>();
   if ((e = hipMemcpyAsync(hc, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->stream)) ||
       (e = hipStreamSynchronize(ctx->stream)))
@@ -695,10 +699,14 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
   if (first != CE_OK) return first;  // all-or-nothing: batch state discarded (lib.rs:497-514)
 
   // 5) commit: state = max(state, batch); next_op_versions from the gate
-  if ((e = launch_merge_max(ctx->stream, c->d_state.as<unsigned long long>(),
-                            c->d_batch.as<unsigned long long>(), c->cap)) ||
-      (e = hipStreamSynchronize(ctx->stream)))
-    return ctx->hip_fail(e, "merge");
+  {
+    const int t = ctx->tbegin("merge");
+    if ((e = launch_merge_max(ctx->stream, c->d_state.as<unsigned long long>(),
+                              c->d_batch.as<unsigned long long>(), c->cap)))
+      return ctx->hip_fail(e, "merge");
+    ctx->tend(t);
+    if ((e = hipStreamSynchronize(ctx->stream))) return ctx->hip_fail(e, "merge");
+  }
   for (uint32_t a = 0; a < m; a++) c->nov[wslot[a]] = std::max(c->nov[wslot[a]], expect[a]);
   if (first_gap < n) {
     if (status_out) status_out[first_gap] = CE_ERR_OP_VERSION;
@@ -1058,6 +1066,16 @@ int ce_core_apply_ops(ce_core* c, const uint8_t* ops, size_t len) {
   if ((rc = merge_dots_host(c, dots))) return rc;  // state.apply(op) for op in ops (lib.rs:710-712)
   c->nov[s] = version + 1;                         // next_op_versions.inc(actor) (lib.rs:714-715)
   return table_upload(c);
+}
+
+int ce_core_reset(ce_core* c) {
+  if (!c) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  std::fill(c->nov.begin(), c->nov.end(), 0);
+  c->read_states.clear();
+  hipError_t e = hipMemsetAsync(c->d_state.p, 0, c->cap * 8ull, c->ctx->stream);
+  if (e) return c->ctx->hip_fail(e, "reset");
+  return CE_OK;
 }
 
 int ce_core_register_actors(ce_core* c, const uint8_t* actors, uint32_t m) {

@@ -112,14 +112,20 @@ int device_open(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint
   if ((e = reset_counters(ctx)) != hipSuccess) return ctx->hip_fail(e, "memset counters");
   SegScratch sc = scratch_of(ctx, ec);
   FileParams* P = ctx->params.as<FileParams>();
+  int t = ctx->tbegin("open_setup");
   if ((e = launch_open_setup(ctx->stream, d_blob, d_offs, n, outer, dev_key(key), key_status(key),
                              P, d_status, sc)) != hipSuccess)
     return ctx->hip_fail(e, "open setup");
+  ctx->tend(t);
+  t = ctx->tbegin("segments_open");
   if ((e = launch_segments(ctx->stream, false, d_blob, d_out, P, n, d_status, sc,
                            grid_waves_for(n))) != hipSuccess)
     return ctx->hip_fail(e, "open segments");
+  ctx->tend(t);
+  t = ctx->tbegin("finalize_open");
   if ((e = launch_finalize_multi(ctx->stream, false, d_out, P, d_status, sc)) != hipSuccess)
     return ctx->hip_fail(e, "open finalize");
+  ctx->tend(t);
   if (sync_counters) {
     if ((e = hipMemcpyAsync(ctx->h_counters.p, ctx->counters.p, 64, hipMemcpyDeviceToHost,
                             ctx->stream)) != hipSuccess ||
@@ -140,15 +146,21 @@ int device_seal(ce_ctx* ctx, const uint8_t* d_clear, const uint64_t* d_offs, uin
   if ((e = reset_counters(ctx)) != hipSuccess) return ctx->hip_fail(e, "memset counters");
   SegScratch sc = scratch_of(ctx, ec);
   FileParams* P = ctx->params.as<FileParams>();
+  int t = ctx->tbegin("seal_setup");
   if ((e = launch_seal_setup(ctx->stream, d_clear, d_offs, n, d_outer_version, d_nonces, d_out,
                              d_out_offs, dev_key(key), P, sc)) != hipSuccess)
     return ctx->hip_fail(e, "seal setup");
+  ctx->tend(t);
+  t = ctx->tbegin("segments_seal");
   if ((e = launch_segments(ctx->stream, true, d_clear, d_out, P, n, ctx->status.as<int32_t>(), sc,
                            grid_waves_for(n))) != hipSuccess)
     return ctx->hip_fail(e, "seal segments");
+  ctx->tend(t);
+  t = ctx->tbegin("finalize_seal");
   if ((e = launch_finalize_multi(ctx->stream, true, d_out, P, ctx->status.as<int32_t>(), sc)) !=
       hipSuccess)
     return ctx->hip_fail(e, "seal finalize");
+  ctx->tend(t);
   return CE_OK;
 }
 
@@ -258,6 +270,8 @@ void ce_ctx_destroy(ce_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto& t : c->timed) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
+  for (auto e : c->event_pool) (void)hipEventDestroy(e);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -282,6 +296,37 @@ void ce_ctx_synchronize(ce_ctx* c) {
 }
 
 const char* ce_ctx_last_error(ce_ctx* c) { return c ? c->last_error.c_str() : ""; }
+
+int ce_ctx_set_timing(ce_ctx* c, int enable) {
+  if (!c) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  c->timing = enable != 0;
+  return CE_OK;
+}
+
+int ce_ctx_timing_read(ce_ctx* c, const char* kernel, double* total_ms, uint64_t* launches) {
+  if (!c || !kernel || !total_ms || !launches) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  (void)hipStreamSynchronize(c->stream);
+  double tot = 0;
+  uint64_t cnt = 0;
+  for (auto& t : c->timed) {
+    if (std::strcmp(t.name, kernel) != 0) continue;
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) { tot += ms; cnt++; }
+  }
+  *total_ms = tot;
+  *launches = cnt;
+  return CE_OK;
+}
+
+void ce_ctx_timing_reset(ce_ctx* c) {
+  if (!c) return;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  (void)hipStreamSynchronize(c->stream);
+  for (auto& t : c->timed) { c->event_pool.push_back(t.a); c->event_pool.push_back(t.b); }
+  c->timed.clear();
+}
 
 size_t ce_cryptor_sealed_len(size_t clear_len) { return (size_t)sealed_len(clear_len); }
 

@@ -80,6 +80,35 @@ struct ce_ctx {
   ce::DevBuf params, status, counters, extra, multi, partials, out, apply, refold, miss,
       supported, blob, offs, nonces, out_offs, outer_ver, batch_counters;
   ce::HostBuf h_counters, h_apply, h_stage, h_stage2;
+  // kernel timing (ce_ctx_set_timing)
+  bool timing = false;
+  struct TimedLaunch {
+    const char* name;
+    hipEvent_t a, b;
+  };
+  std::vector<TimedLaunch> timed;
+  std::vector<hipEvent_t> event_pool;
+  hipEvent_t take_event() {
+    if (!event_pool.empty()) {
+      hipEvent_t e = event_pool.back();
+      event_pool.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+  }
+  // brackets one launch: t0 = begin(name) ... end(t0)
+  int tbegin(const char* name) {
+    if (!timing) return -1;
+    TimedLaunch t{name, take_event(), take_event()};
+    (void)hipEventRecord(t.a, stream);
+    timed.push_back(t);
+    return (int)timed.size() - 1;
+  }
+  void tend(int idx) {
+    if (idx >= 0) (void)hipEventRecord(timed[idx].b, stream);
+  }
 
   int fail(int code, const std::string& msg) {
     last_error = msg;

@@ -68,6 +68,13 @@ int ce_ctx_set_stream(ce_ctx *ctx, void *hip_stream);
 void ce_ctx_synchronize(ce_ctx *ctx);
 /* Human readable detail of the last failure on this context. */
 const char *ce_ctx_last_error(ce_ctx *ctx);
+/* Kernel timing with HIP events recorded on the context stream around every launch (off by
+ * default).  ce_ctx_timing_read synchronizes and returns the summed milliseconds and launch
+ * count of one kernel ("open_setup", "segments_open", "finalize_open", "decode", "merge",
+ * "seal_setup", "segments_seal", "finalize_seal"). */
+int ce_ctx_set_timing(ce_ctx *ctx, int enable);
+int ce_ctx_timing_read(ce_ctx *ctx, const char *kernel, double *total_ms, uint64_t *launches);
+void ce_ctx_timing_reset(ce_ctx *ctx);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Cryptor: XChaCha20-Poly1305 EncHandler on the GPU                                          */
@@ -202,6 +209,9 @@ int ce_core_compact(ce_core *c, char name_out[64]);
 int ce_core_apply_ops(ce_core *c, const uint8_t *ops, size_t len);
 /* rmp_serde::to_vec_named(&StateWrapper) (lib.rs:336, 739-743) */
 int ce_core_state_bytes(ce_core *c, ce_buf *out);
+/* Back to the empty StateWrapper (Default, lib.rs:240-243), keeping registered actors and the
+ * read key; used to compact the same batch repeatedly in benchmarks. */
+int ce_core_reset(ce_core *c);
 
 /* Storage-less ingest: what read_remote_ops does after Storage::load_ops (lib.rs:495-546).
  * files i = blob[offs[i], offs[i+1]) (outer version || cryptor box); the writer of file i is

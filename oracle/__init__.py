@@ -172,11 +172,17 @@ class Core:
         return rc, list(st)[:n]
 
 
+_out_buf = None
+
+
 def compact_ops_baseline(kind, key, data_version, blob, offs, file_actor, file_version,
                          n_files, n_threads):
     """CPU baseline over numpy/ctypes buffers (blob: bytes-like, offs: uint64[n+1])."""
-    cap = 64 << 20
-    out = ctypes.create_string_buffer(cap)
+    global _out_buf
+    cap = 8 << 20
+    if _out_buf is None:
+        _out_buf = ctypes.create_string_buffer(cap)
+    out = _out_buf
     err = ctypes.c_int(0)
     n = lib().oc_compact_ops_baseline(kind, _buf(key), _buf(data_version), blob, offs, file_actor,
                                       file_version, ctypes.c_size_t(n_files), n_threads, out,

@@ -796,19 +796,20 @@ int oc_decode_apply_dots(oc_core *c, const uint8_t *buf, size_t len, int dry_run
   rd_t r = {buf, len, 0};
   uint64_t cnt;
   if (rd_array_hdr(&r, &cnt)) return OC_ERR_DECODE;
-  /* decode everything first (rmp_serde::from_slice returns the whole Vec or an error) */
-  size_t start = r.i;
+  if (cnt > len) return OC_ERR_DECODE;
+  /* decode everything first (rmp_serde::from_slice returns the whole Vec or an error),
+   * then apply in order */
+  dot_t stackbuf[256];
+  dot_t *dots = cnt <= 256 ? stackbuf : (dot_t *)malloc(cnt * sizeof(dot_t));
   for (uint64_t k = 0; k < cnt; k++) {
-    dot_t d;
-    if (rd_struct(&r, F, 2, dot_cb, &d)) return OC_ERR_DECODE;
+    if (rd_struct(&r, F, 2, dot_cb, &dots[k])) {
+      if (dots != stackbuf) free(dots);
+      return OC_ERR_DECODE;
+    }
   }
-  if (dry_run) return OC_OK;
-  r.i = start;
-  for (uint64_t k = 0; k < cnt; k++) {
-    dot_t d;
-    rd_struct(&r, F, 2, dot_cb, &d);
-    oc_vclock_apply(&c->state, d.actor, d.counter);
-  }
+  if (!dry_run)
+    for (uint64_t k = 0; k < cnt; k++) oc_vclock_apply(&c->state, dots[k].actor, dots[k].counter);
+  if (dots != stackbuf) free(dots);
   return OC_OK;
 }
 
