@@ -79,6 +79,14 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise RuntimeError("libcrdtenc.so not built (run `make -C %s product`); the product "
                                "has no CPU fallback" % os.path.dirname(HERE))
+        # One HIP runtime per process: torch bundles libamdhip64 with the same SONAME
+        # (libamdhip64.so.7) but is linked by file name, so it must be loaded first; our
+        # DT_NEEDED then binds to it and torch tensors / streams and our kernels share it.
+        if not os.environ.get("CRDTENC_NO_TORCH"):
+            try:
+                import torch  # noqa: F401
+            except Exception:
+                pass
         L = ctypes.CDLL(LIB_PATH)
         L.ce_status_str.restype = ctypes.c_char_p
         L.ce_ctx_last_error.restype = ctypes.c_char_p
@@ -380,13 +388,16 @@ class Core:
                                       fv, st)
         return rc, (list(st)[:n] if want_status else None)
 
-    def ingest_ops_device(self, d_blob, d_offs, n, blob_len, actors, file_actor_arr,
-                          file_version_arr):
-        """file_actor_arr / file_version_arr: ctypes arrays (host)."""
-        return lib().ce_core_ingest_ops_device(
+    def ingest_ops_device(self, d_blob, d_offs, n, blob_len, actors, d_file_actor,
+                          d_file_version, want_status=False):
+        """Batch resident in HBM: d_* are device pointers (u8 files, u64 offs[n+1],
+        u32 file_actor[n], u64 file_version[n]); actors = host bytes (16 per writer)."""
+        st = (ctypes.c_int32 * max(n, 1))() if want_status else None
+        rc = lib().ce_core_ingest_ops_device(
             self.p, ctypes.c_void_p(d_blob), ctypes.c_void_p(d_offs), ctypes.c_uint32(n),
-            ctypes.c_uint64(blob_len), actors, ctypes.c_uint32(len(actors) // 16),
-            file_actor_arr, file_version_arr, None)
+            ctypes.c_uint64(blob_len), _cbuf(actors), ctypes.c_uint32(len(actors) // 16),
+            ctypes.c_void_p(d_file_actor), ctypes.c_void_p(d_file_version), st)
+        return (rc, list(st)[:n]) if want_status else rc
 
     def ingest_states(self, files):
         n = len(files)

@@ -51,7 +51,8 @@ struct ce_core {
   std::vector<uint64_t> nov;  // next_op_versions by slot
   std::unordered_map<Uuid, uint32_t, UuidHash> slot_of;
   bool table_dirty = true;
-  DevBuf d_table, d_state, d_batch, d_supported, d_refold2, d_tmp;
+  DevBuf d_table, d_state, d_batch, d_supported, d_refold2, d_tmp, d_gate, d_meta;
+  int files_per_wave = 4;  // fused kernel geometry (CE_FILES_PER_WAVE overrides)
   std::set<std::string> read_states;  // lib.rs:205
   ce_ctx* aux = nullptr;              // single-file work during a batch (exotic envelopes)
 };
@@ -533,15 +534,31 @@ int ensure_supported(ce_core* c) {
   return CE_OK;
 }
 
-// Core::read_remote_ops after Storage::load_ops (lib.rs:495-546), files resident in HBM.
+// Host version gate (lib.rs:519-538) for batches the device gate does not cover (actors split
+// into several runs, non-consecutive versions).  Returns the first gap index (n if none).
+uint32_t host_gate(const uint32_t* fa, const uint64_t* fv, uint32_t n, std::vector<uint64_t>* expect,
+                   uint8_t* apply) {
+  uint32_t first_gap = n;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t a = fa[i];
+    const uint64_t v = fv[i];
+    if (v < (*expect)[a]) { apply[i] = 0; continue; }   // already read
+    if (v > (*expect)[a]) { first_gap = i; break; }     // "Unexpected op version"
+    apply[i] = 1;
+    (*expect)[a] = v + 1;
+  }
+  for (uint32_t i = first_gap; i < n; i++) apply[i] = 0;
+  return first_gap;
+}
+
+// Core::read_remote_ops after Storage::load_ops (lib.rs:495-546), files and per-file metadata
+// resident in HBM (d_fa = local actor index per file, d_fv = version per file).
 int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
-                   uint64_t blob_len, const uint8_t* actors, uint32_t m,
-                   const uint32_t* file_actor, const uint64_t* file_version, int32_t* status_out) {
+                   uint64_t blob_len, const uint8_t* actors, uint32_t m, const uint32_t* d_fa,
+                   const uint64_t* d_fv, int32_t* status_out) {
   ce_ctx* ctx = c->ctx;
   if (!c->has_key) return ctx->fail(CE_ERR_NO_KEY, "no latest key");
   if (n == 0) return CE_OK;
-  for (uint32_t i = 0; i < n; i++)
-    if (file_actor[i] >= m) return ctx->fail(CE_ERR_INVALID_ARG, "file_actor out of range");
   hipError_t e;
   const KeyRef key = key_of(c);
   // writer actors (the op directories) get slots first: the version gate is keyed by them
@@ -556,42 +573,50 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
   if (rc) return rc;
   if ((rc = ensure_supported(c))) return rc;
   if ((e = ctx->out.reserve(blob_len + 16ull * n + 128)) || (e = ctx->status.reserve(n * 4ull + 64)) ||
-      (e = ctx->apply.reserve(n + 64)) || (e = ctx->h_apply.reserve(n + 64)) ||
-      (e = ctx->refold.reserve(n + 64)) || (e = c->d_refold2.reserve(n + 64)) ||
-      (e = ctx->miss.reserve(65536 * 16)))
+      (e = ctx->apply.reserve(n + 64)) || (e = ctx->refold.reserve(n + 64)) ||
+      (e = c->d_refold2.reserve(n + 64)) || (e = ctx->miss.reserve(65536 * 16)) ||
+      (e = c->d_gate.reserve(m * 24ull + 64)) || (e = ctx->h_stage2.reserve(m * 16ull + 64)))
     return ctx->hip_fail(e, "ingest reserve");
 
-  // 1) GPU: outer version, envelope, XChaCha20-Poly1305 open (verify-before-release)
-  rc = device_open(ctx, d_blob, d_offs, n, blob_len, true, key, ctx->out.as<uint8_t>(),
-                   ctx->status.as<int32_t>(), false);
-  if (rc) return rc;
+  // expected versions per writer (next_op_versions.get, lib.rs:481) -> device
+  uint64_t* he0 = ctx->h_stage2.as<uint64_t>();
+  for (uint32_t a = 0; a < m; a++) he0[a] = c->nov[wslot[a]];
+  GateArgs ga{};
+  ga.fa = d_fa;
+  ga.fv = d_fv;
+  ga.n = n;
+  ga.m = m;
+  uint8_t* gbase = c->d_gate.as<uint8_t>();
+  ga.e0 = reinterpret_cast<const uint64_t*>(gbase);
+  ga.newnov = reinterpret_cast<unsigned long long*>(gbase + 8ull * m);
+  ga.run_count = reinterpret_cast<uint32_t*>(gbase + 16ull * m);
+  ga.run_first = reinterpret_cast<uint32_t*>(gbase + 20ull * m);
+  ga.flags = ctx->counters.as<uint32_t>() + 12;  // [12] not grouped, [13] first gap
+  ga.apply = ctx->apply.as<uint8_t>();
 
-  // 2) host, overlapped: the per-actor version gate (lib.rs:519-538)
-  uint8_t* ap = ctx->h_apply.as<uint8_t>();
-  std::vector<uint64_t> expect(m);
-  for (uint32_t a = 0; a < m; a++) expect[a] = c->nov[wslot[a]];
-  uint32_t first_gap = n;
-  for (uint32_t i = 0; i < n; i++) {
-    const uint32_t a = file_actor[i];
-    const uint64_t v = file_version[i];
-    if (v < expect[a]) { ap[i] = 0; continue; }       // already read
-    if (v > expect[a]) { first_gap = i; break; }      // "Unexpected op version"
-    ap[i] = 1;
-    expect[a] = v + 1;
+  // 1) GPU: setup (outer version, envelope, key schedule) + device gate
+  uint32_t ec;
+  {
+    // device_open's setup only; the fused kernel replaces its segment pass for small files
+    int rr = device_open_setup(ctx, d_blob, d_offs, n, blob_len, true, key, ctx->status.as<int32_t>(), &ec);
+    if (rr) return rr;
   }
-  if (first_gap < n) std::memset(ap + first_gap, 0, n - first_gap);
-
-  // 3) exotic envelopes (none in the canonical case): normalize on the host, AEAD on the GPU
-  if ((e = hipMemcpyAsync(ctx->h_counters.p, ctx->counters.p, 64, hipMemcpyDeviceToHost,
-                          ctx->stream)))
-    return ctx->hip_fail(e, "counters");
-  if ((e = hipMemcpyAsync(ctx->apply.p, ap, n, hipMemcpyHostToDevice, ctx->stream)) ||
-      (e = hipMemsetAsync(c->d_batch.p, 0, c->cap * 8ull, ctx->stream)) ||
+  if ((e = hipMemcpyAsync(gbase, he0, m * 8ull, hipMemcpyHostToDevice, ctx->stream)) ||
+      (e = hipMemsetAsync(gbase + 8ull * m, 0, 16ull * m, ctx->stream)) ||
+      (e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ga.flags + 1), 0xffffffffu, 1, ctx->stream)))
+    return ctx->hip_fail(e, "gate upload");
+  {
+    const int t = ctx->tbegin("gate");
+    if ((e = launch_gate(ctx->stream, ga))) return ctx->hip_fail(e, "gate");
+    ctx->tend(t);
+  }
+  if ((e = hipMemsetAsync(c->d_batch.p, 0, c->cap * 8ull, ctx->stream)) ||
       (e = hipMemsetAsync(ctx->refold.p, 0, n, ctx->stream)))
-    return ctx->hip_fail(e, "ingest upload");
+    return ctx->hip_fail(e, "ingest memset");
 
   DecodeArgs da{};
   da.pt = ctx->out.as<uint8_t>();
+  da.blob = d_blob;
   da.params = ctx->params.as<FileParams>();
   da.status = ctx->status.as<int32_t>();
   da.n = n;
@@ -602,24 +627,72 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
   da.miss_list = ctx->miss.as<uint4>();
   da.miss_cap = 65536;
   da.refold = ctx->refold.as<uint8_t>();
-  da.only = nullptr;
-
-  // 4) GPU: decode Vec<Dot> of every opened file, fold applied files into the batch state
   da.table = c->d_table.as<ActorSlot>();
   da.mask = c->cap - 1;
   da.batch = c->d_batch.as<unsigned long long>();
-  {
+
+  // 2) GPU: single-page files: open + decode + fold fused; larger files: segments + decode
+  auto run_fold = [&](const uint8_t* only) -> int {
+    da.only = only;
+    da.large_only = 1;
+    {
+      const int t = ctx->tbegin("open_fold_small");
+      if ((e = launch_open_fold_small(ctx->stream, da, c->files_per_wave))) return ctx->hip_fail(e, "fused");
+      ctx->tend(t);
+    }
+    if (!only) {
+      SegScratch sc = segscratch(ctx, ec);
+      int t = ctx->tbegin("segments_open");
+      if ((e = launch_segments(ctx->stream, false, d_blob, ctx->out.as<uint8_t>(), da.params, n,
+                               da.status, sc, grid_waves_for(n), true)))
+        return ctx->hip_fail(e, "segments");
+      ctx->tend(t);
+      t = ctx->tbegin("finalize_open");
+      if ((e = launch_finalize_multi(ctx->stream, false, ctx->out.as<uint8_t>(), da.params, da.status, sc)))
+        return ctx->hip_fail(e, "finalize");
+      ctx->tend(t);
+    }
     const int t = ctx->tbegin("decode");
     if ((e = launch_decode_dots(ctx->stream, da, grid_waves_for(n)))) return ctx->hip_fail(e, "decode");
     ctx->tend(t);
-  }
+    return CE_OK;
+  };
+  if ((rc = run_fold(nullptr))) return rc;
   uint32_t* hc = ctx->h_counters.as<uint32_t>();
   if ((e = hipMemcpyAsync(hc, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->stream)) ||
       (e = hipStreamSynchronize(ctx->stream)))
-    return ctx->hip_fail(e, "decode sync");
+    return ctx->hip_fail(e, "fold sync");
 
-  // misses: actors not in the table -> insert, upload, re-fold the files that missed
-  for (int round = 0; hc[4] != 0 && hc[3] == 0 && hc[2] == 0 && hc[8] == 0; round++) {
+  // 3) batches outside the device gate's shape: host gate, fold again with its flags
+  std::vector<uint64_t> expect(he0, he0 + m);
+  uint32_t first_gap = hc[13] == 0xffffffffu ? n : hc[13];
+  bool host_gated = false;
+  if (hc[12]) {
+    std::vector<uint32_t> fa(n);
+    std::vector<uint64_t> fv(n);
+    std::vector<uint8_t> ap(n);
+    if ((e = hipMemcpyAsync(fa.data(), d_fa, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (e = hipMemcpyAsync(fv.data(), d_fv, n * 8ull, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+      return ctx->hip_fail(e, "host gate");
+    for (uint32_t i = 0; i < n; i++)
+      if (fa[i] >= m) return ctx->fail(CE_ERR_INVALID_ARG, "file_actor out of range");
+    first_gap = host_gate(fa.data(), fv.data(), n, &expect, ap.data());
+    host_gated = true;
+    if ((e = hipMemcpyAsync(ctx->apply.p, ap.data(), n, hipMemcpyHostToDevice, ctx->stream)) ||
+        (e = hipMemsetAsync(c->d_batch.p, 0, c->cap * 8ull, ctx->stream)) ||
+        (e = hipMemsetAsync(c->d_refold2.p, 1, n, ctx->stream)) ||
+        (e = hipMemsetAsync(ctx->refold.p, 0, n, ctx->stream)) ||
+        (e = hipMemsetAsync(ctx->counters.as<uint32_t>() + 4, 0, 4, ctx->stream)))
+      return ctx->hip_fail(e, "host gate");
+    if ((rc = run_fold(c->d_refold2.as<uint8_t>()))) return rc;
+    if ((e = hipMemcpyAsync(hc, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+      return ctx->hip_fail(e, "fold sync");
+  }
+
+  // 4) misses: actors not in the table -> insert, upload, fold again the files that missed
+  for (int round = 0; hc[4] != 0 && hc[2] == 0 && hc[3] == 0 && hc[8] == 0; round++) {
     const uint32_t nm = std::min<uint32_t>(hc[4], 65536);
     std::vector<uint4> ml(nm);
     if ((e = hipMemcpyAsync(ml.data(), ctx->miss.p, nm * 16ull, hipMemcpyDeviceToHost, ctx->stream)) ||
@@ -636,7 +709,7 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
       if ((rc = insert_actor(c, u, &s))) return rc;
     }
     if (c->cap != old_cap) {
-      // slots moved: the partial batch state is stale -> re-fold everything
+      // slots moved: the partial batch state is stale -> fold everything again
       if ((e = hipMemsetAsync(c->d_batch.p, 0, c->cap * 8ull, ctx->stream)) ||
           (e = hipMemsetAsync(c->d_refold2.p, 1, n, ctx->stream)))
         return ctx->hip_fail(e, "miss");
@@ -650,15 +723,15 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
     da.table = c->d_table.as<ActorSlot>();
     da.mask = c->cap - 1;
     da.batch = c->d_batch.as<unsigned long long>();
-    da.only = c->d_refold2.as<uint8_t>();
-    if ((e = launch_decode_dots(ctx->stream, da, grid_waves_for(n))) ||
-        (e = hipMemcpyAsync(hc, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->stream)) ||
+    if ((rc = run_fold(c->d_refold2.as<uint8_t>()))) return rc;
+    if ((e = hipMemcpyAsync(hc, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->stream)) ||
         (e = hipStreamSynchronize(ctx->stream)))
       return ctx->hip_fail(e, "refold");
     if (round > 64) return ctx->fail(CE_ERR_DEVICE, "actor table did not converge");
   }
 
-  // statuses: needed for the caller, for host-parse files, and to name the first failure
+  // statuses: needed by the caller, for host-parse envelopes and to name the first failure
+  // counters: [2] auth, [3] decode, [7] host-parse envelopes, [8] setup failures
   std::vector<int32_t> st;
   auto fetch_status = [&]() -> int {
     st.resize(n);
@@ -667,19 +740,17 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
       return ctx->hip_fail(e, "status");
     return CE_OK;
   };
-  // counters: [2] auth failures, [3] decode failures, [7] host-parse envelopes,
-  // [8] setup failures (outer version, key, envelope)
   const bool failed = hc[2] || hc[3] || hc[8];
   if (status_out || failed || hc[7]) {
     if ((rc = fetch_status())) return rc;
   }
   if (hc[7]) {
     if ((rc = resolve_host_parse(c, d_blob, d_offs, n, true))) return rc;
-    // decode only the resolved files
     std::vector<uint8_t> only(n, 0);
     for (uint32_t i = 0; i < n; i++) only[i] = st[i] == kStatusHostParse;
     if ((e = hipMemcpy(c->d_refold2.p, only.data(), n, hipMemcpyHostToDevice))) return ctx->hip_fail(e, "x");
     da.only = c->d_refold2.as<uint8_t>();
+    da.large_only = 0;
     da.table = c->d_table.as<ActorSlot>();
     da.mask = c->cap - 1;
     da.batch = c->d_batch.as<unsigned long long>();
@@ -705,7 +776,15 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
                               c->d_batch.as<unsigned long long>(), c->cap)))
       return ctx->hip_fail(e, "merge");
     ctx->tend(t);
-    if ((e = hipStreamSynchronize(ctx->stream))) return ctx->hip_fail(e, "merge");
+  }
+  if (!host_gated) {
+    std::vector<uint64_t> nn(m);
+    if ((e = hipMemcpyAsync(nn.data(), gbase + 8ull * m, m * 8ull, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+      return ctx->hip_fail(e, "nov");
+    for (uint32_t a = 0; a < m; a++) expect[a] = std::max(expect[a], nn[a]);
+  } else if ((e = hipStreamSynchronize(ctx->stream))) {
+    return ctx->hip_fail(e, "merge");
   }
   for (uint32_t a = 0; a < m; a++) c->nov[wslot[a]] = std::max(c->nov[wslot[a]], expect[a]);
   if (first_gap < n) {
@@ -713,6 +792,26 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
     return CE_ERR_OP_VERSION;
   }
   return CE_OK;
+}
+
+// host metadata -> device, then ingest_ops_dev
+int ingest_ops_hostmeta(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
+                        uint64_t blob_len, const uint8_t* actors, uint32_t m,
+                        const uint32_t* file_actor, const uint64_t* file_version,
+                        int32_t* status_out) {
+  ce_ctx* ctx = c->ctx;
+  for (uint32_t i = 0; i < n; i++)
+    if (file_actor[i] >= m) return ctx->fail(CE_ERR_INVALID_ARG, "file_actor out of range");
+  hipError_t e;
+  if ((e = c->d_meta.reserve(n * 12ull + 64))) return ctx->hip_fail(e, "meta");
+  uint8_t* mb = c->d_meta.as<uint8_t>();
+  if ((e = hipMemcpyAsync(mb, file_version, n * 8ull, hipMemcpyHostToDevice, ctx->stream)) ||
+      (e = hipMemcpyAsync(mb + 8ull * n, file_actor, n * 4ull, hipMemcpyHostToDevice, ctx->stream)) ||
+      (e = hipStreamSynchronize(ctx->stream)))
+    return ctx->hip_fail(e, "meta upload");
+  return ingest_ops_dev(c, d_blob, d_offs, n, blob_len, actors, m,
+                        reinterpret_cast<const uint32_t*>(mb + 8ull * n),
+                        reinterpret_cast<const uint64_t*>(mb), status_out);
 }
 
 // Core::read_remote_states after Storage::load_states (lib.rs:425-466)
@@ -835,8 +934,8 @@ int read_remote(ce_core* c) {
     return ctx->hip_fail(e, "ops upload");
   std::vector<uint8_t> ab(actors.size() * 16);
   for (size_t a = 0; a < actors.size(); a++) std::memcpy(ab.data() + 16 * a, actors[a].data(), 16);
-  return ingest_ops_dev(c, ctx->blob.as<uint8_t>(), ctx->offs.as<uint64_t>(), n, blob.size(),
-                        ab.data(), (uint32_t)actors.size(), aidx.data(), vers.data(), nullptr);
+  return ingest_ops_hostmeta(c, ctx->blob.as<uint8_t>(), ctx->offs.as<uint64_t>(), n, blob.size(),
+                             ab.data(), (uint32_t)actors.size(), aidx.data(), vers.data(), nullptr);
 }
 
 // clear text + file of a compaction (lib.rs:335-360)
@@ -869,6 +968,10 @@ int ce_core_open(ce_ctx* ctx, const ce_open_options* o, ce_core** out) {
   ce_core* c = new ce_core();
   c->ctx = ctx;
   c->kind = o->state_kind;
+  if (const char* fw = getenv("CE_FILES_PER_WAVE")) {
+    const int v = atoi(fw);
+    if (v == 1 || v == 2 || v == 4) c->files_per_wave = v;
+  }
   c->flags = o->flags;
   std::memcpy(c->current_data_version.data(), o->current_data_version, 16);
   for (size_t i = 0; i < o->n_supported; i++) {
@@ -971,19 +1074,20 @@ int ce_core_ingest_ops(ce_core* c, const uint8_t* blob, const uint64_t* offs, ui
       (e = hipMemcpyAsync(ctx->offs.p, offs, (n + 1) * 8ull, hipMemcpyHostToDevice, ctx->stream)) ||
       (e = hipStreamSynchronize(ctx->stream)))
     return ctx->hip_fail(e, "ingest upload");
-  return ingest_ops_dev(c, ctx->blob.as<uint8_t>(), ctx->offs.as<uint64_t>(), n, blen, actors, m,
-                        file_actor, file_version, status);
+  return ingest_ops_hostmeta(c, ctx->blob.as<uint8_t>(), ctx->offs.as<uint64_t>(), n, blen, actors,
+                             m, file_actor, file_version, status);
 }
 
 int ce_core_ingest_ops_device(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs,
                               uint32_t n, uint64_t blob_len, const uint8_t* actors, uint32_t m,
-                              const uint32_t* file_actor, const uint64_t* file_version,
+                              const uint32_t* d_file_actor, const uint64_t* d_file_version,
                               int32_t* status) {
-  if (!c || (n && (!d_blob || !d_offs || !actors || !file_actor || !file_version)))
+  if (!c || (n && (!d_blob || !d_offs || !actors || !d_file_actor || !d_file_version)))
     return CE_ERR_INVALID_ARG;
   std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
   (void)hipSetDevice(c->ctx->device);
-  return ingest_ops_dev(c, d_blob, d_offs, n, blob_len, actors, m, file_actor, file_version, status);
+  return ingest_ops_dev(c, d_blob, d_offs, n, blob_len, actors, m, d_file_actor, d_file_version,
+                        status);
 }
 
 int ce_core_ingest_states(ce_core* c, const uint8_t* blob, const uint64_t* offs, uint32_t n,

@@ -84,7 +84,7 @@ static int reserve_batch(ce_ctx* ctx, uint32_t n, uint64_t blob_len, uint32_t* e
   return CE_OK;
 }
 
-static SegScratch scratch_of(ce_ctx* ctx, uint32_t extra_cap) {
+SegScratch segscratch(ce_ctx* ctx, uint32_t extra_cap) {
   SegScratch sc;
   sc.counters = ctx->counters.as<uint32_t>();
   sc.extra_list = ctx->extra.as<uint2>();
@@ -102,6 +102,22 @@ static hipError_t reset_counters(ce_ctx* ctx) {
                            0xffffffffu, 1, ctx->stream);
 }
 
+int device_open_setup(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
+                      uint64_t blob_len, bool outer, const KeyRef& key, int32_t* d_status,
+                      uint32_t* extra_cap) {
+  int rc = reserve_batch(ctx, n, blob_len, extra_cap);
+  if (rc) return rc;
+  hipError_t e;
+  if ((e = reset_counters(ctx)) != hipSuccess) return ctx->hip_fail(e, "memset counters");
+  SegScratch sc = segscratch(ctx, *extra_cap);
+  const int t = ctx->tbegin("open_setup");
+  if ((e = launch_open_setup(ctx->stream, d_blob, d_offs, n, outer, dev_key(key), key_status(key),
+                             ctx->params.as<FileParams>(), d_status, sc)) != hipSuccess)
+    return ctx->hip_fail(e, "open setup");
+  ctx->tend(t);
+  return CE_OK;
+}
+
 int device_open(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
                 uint64_t blob_len, bool outer, const KeyRef& key, uint8_t* d_out,
                 int32_t* d_status, bool sync_counters) {
@@ -110,7 +126,7 @@ int device_open(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint
   if (rc) return rc;
   hipError_t e;
   if ((e = reset_counters(ctx)) != hipSuccess) return ctx->hip_fail(e, "memset counters");
-  SegScratch sc = scratch_of(ctx, ec);
+  SegScratch sc = segscratch(ctx, ec);
   FileParams* P = ctx->params.as<FileParams>();
   int t = ctx->tbegin("open_setup");
   if ((e = launch_open_setup(ctx->stream, d_blob, d_offs, n, outer, dev_key(key), key_status(key),
@@ -144,7 +160,7 @@ int device_seal(ce_ctx* ctx, const uint8_t* d_clear, const uint64_t* d_offs, uin
   if (rc) return rc;
   hipError_t e;
   if ((e = reset_counters(ctx)) != hipSuccess) return ctx->hip_fail(e, "memset counters");
-  SegScratch sc = scratch_of(ctx, ec);
+  SegScratch sc = segscratch(ctx, ec);
   FileParams* P = ctx->params.as<FileParams>();
   int t = ctx->tbegin("seal_setup");
   if ((e = launch_seal_setup(ctx->stream, d_clear, d_offs, n, d_outer_version, d_nonces, d_out,

@@ -128,6 +128,10 @@ DevKey dev_key(const KeyRef& k);
 // Open n files resident in HBM (d_blob/d_offs) on ctx's stream; plaintexts land in ctx->out.
 // outer: files carry the core's 16-byte version prefix.  After the call ctx->status holds the
 // per-file statuses and ctx->params the FileParams; counters are copied to h_counters.
+int device_open_setup(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
+                      uint64_t blob_len, bool outer, const KeyRef& key, int32_t* d_status,
+                      uint32_t* extra_cap);
+SegScratch segscratch(ce_ctx* ctx, uint32_t extra_cap);
 int device_open(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
                 uint64_t blob_len, bool outer, const KeyRef& key, uint8_t* d_out,
                 int32_t* d_status, bool sync_counters);

@@ -11,6 +11,8 @@ namespace ce {
 static constexpr uint32_t kPageBytes = 4096;
 static constexpr uint32_t kSegPages = 4;
 static constexpr uint32_t kSegBlocks = kSegPages * kPageBytes / 16;  // Poly1305 blocks
+// files with at most one page of ciphertext are opened, decoded and folded in one kernel
+static constexpr uint32_t kSmallMax = kPageBytes;
 
 // Per-file AEAD parameters written by the setup kernels (256 B, read with scalar loads).
 struct alignas(16) FileParams {
@@ -38,7 +40,8 @@ struct DevKey {
 struct SegScratch {
   uint32_t* counters;     // [0] extra segments, [1] multi-segment files, [2] auth failures,
                           // [3] decode failures, [4] misses, [5] first failing index (min),
-                          // [6] partial slots, [7] host-parse envelopes, [8] setup failures
+                          // [6] partial slots, [7] host-parse envelopes, [8] setup failures,
+                          // [12] gate: batch not in load_ops shape, [13] gate: first gap
   uint2* extra_list;      // (file, seg) for segments j >= 1
   uint32_t extra_cap;
   uint32_t* multi_files;  // files with nseg > 1
@@ -57,7 +60,7 @@ hipError_t launch_seal_setup(hipStream_t s, const uint8_t* clear, const uint64_t
 // one wavefront per segment (grid-stride); seal selects encrypt.
 hipError_t launch_segments(hipStream_t s, bool seal, const uint8_t* in, uint8_t* out,
                            const FileParams* params, uint32_t n, int32_t* status, SegScratch sc,
-                           uint32_t grid_waves);
+                           uint32_t grid_waves, bool skip_small = false);
 // multi-segment files: combine partial Poly1305 sums, emit/compare tag (one lane per file).
 hipError_t launch_finalize_multi(hipStream_t s, bool seal, uint8_t* out, const FileParams* params,
                                  int32_t* status, SegScratch sc);
@@ -80,8 +83,28 @@ struct DecodeArgs {
   uint32_t miss_cap;
   uint8_t* refold;              // per file: had a miss
   const uint8_t* only;          // null, or per-file: process only files with only[i] != 0
+  int large_only;               // with only == null: skip files the fused kernel handles
+  const uint8_t* blob;          // fused kernel: input files (ciphertext at FileParams.in_off)
 };
 hipError_t launch_decode_dots(hipStream_t s, const DecodeArgs& a, uint32_t grid_waves);
+
+// fused open + decode + fold of single-page files (ce_fused.hip); files_per_wave in {1, 2, 4}
+hipError_t launch_open_fold_small(hipStream_t s, const DecodeArgs& a, int files_per_wave);
+
+// version gate on the device (ce_fused.hip): files grouped by actor with consecutive versions
+// (Storage::load_ops order, storage.rs:36-40) -> apply flags, first gap, next versions.
+struct GateArgs {
+  const uint32_t* fa;      // file -> local actor index
+  const uint64_t* fv;      // file version
+  uint32_t n, m;
+  const uint64_t* e0;      // expected version per local actor (next_op_versions.get)
+  uint32_t* run_count;     // [m]
+  uint32_t* run_first;     // [m]
+  uint32_t* flags;         // [0] not grouped/consecutive, [1] first gap (min file index)
+  unsigned long long* newnov;  // [m] max(v + 1) over applied files
+  uint8_t* apply;          // [n]
+};
+hipError_t launch_gate(hipStream_t s, const GateArgs& g);
 
 // dst[i] = max(dst[i], src[i])
 hipError_t launch_merge_max(hipStream_t s, unsigned long long* dst,

@@ -14,203 +14,9 @@
 //                   decoded 64 dots at a time by speculating on the canonical encoding, general
 //                   grammar by lane 0 otherwise; dots of applied files max-folded
 //                   (VClock::apply) into a dense batch state.
-#include "ce_kernels.h"
+#include "ce_device.h"
 
 namespace ce {
-
-// ----------------------------------------------------------------------------------------
-// ChaCha20 (RFC 8439 §2.3) / HChaCha20 (draft-irtf-cfrg-xchacha-03 §2.2)
-// ----------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t rotl32(uint32_t x, int c) {
-  return __builtin_amdgcn_alignbit(x, x, 32 - c);
-}
-
-#define CE_QR(a, b, c, d)                                                                   \
-  a += b; d ^= a; d = rotl32(d, 16); c += d; b ^= c; b = rotl32(b, 12);                    \
-  a += b; d ^= a; d = rotl32(d, 8);  c += d; b ^= c; b = rotl32(b, 7);
-
-__device__ __forceinline__ void chacha_rounds(uint32_t (&x)[16]) {
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-    CE_QR(x[0], x[4], x[8], x[12]); CE_QR(x[1], x[5], x[9], x[13]);
-    CE_QR(x[2], x[6], x[10], x[14]); CE_QR(x[3], x[7], x[11], x[15]);
-    CE_QR(x[0], x[5], x[10], x[15]); CE_QR(x[1], x[6], x[11], x[12]);
-    CE_QR(x[2], x[7], x[8], x[13]); CE_QR(x[3], x[4], x[9], x[14]);
-  }
-}
-
-__device__ __forceinline__ void chacha_block(const uint32_t (&k)[8], uint32_t ctr, uint32_t n0,
-                                             uint32_t n1, uint32_t n2, uint32_t (&out)[16]) {
-  uint32_t x[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, k[0], k[1], k[2], k[3],
-                    k[4], k[5], k[6], k[7], ctr, n0, n1, n2};
-  chacha_rounds(x);
-  out[0] = x[0] + 0x61707865u; out[1] = x[1] + 0x3320646eu;
-  out[2] = x[2] + 0x79622d32u; out[3] = x[3] + 0x6b206574u;
-#pragma unroll
-  for (int i = 0; i < 8; i++) out[4 + i] = x[4 + i] + k[i];
-  out[12] = x[12] + ctr; out[13] = x[13] + n0; out[14] = x[14] + n1; out[15] = x[15] + n2;
-}
-
-__device__ __forceinline__ void hchacha20(const uint32_t (&k)[8], const uint32_t (&n)[4],
-                                          uint32_t (&sub)[8]) {
-  uint32_t x[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, k[0], k[1], k[2], k[3],
-                    k[4], k[5], k[6], k[7], n[0], n[1], n[2], n[3]};
-  chacha_rounds(x);
-  sub[0] = x[0]; sub[1] = x[1]; sub[2] = x[2]; sub[3] = x[3];
-  sub[4] = x[12]; sub[5] = x[13]; sub[6] = x[14]; sub[7] = x[15];
-}
-
-// ----------------------------------------------------------------------------------------
-// Poly1305 over GF(2^130 - 5), radix 2^26 (5 limbs), v_mad_u64_u32 products
-// ----------------------------------------------------------------------------------------
-static constexpr uint32_t M26 = 0x3ffffffu;
-
-struct L5 {
-  uint32_t v[5];
-};
-
-// h * r mod p; h limbs < 2^28, r limbs < 2^26 + 2^9  ->  result limbs < 2^26 (v[1] < 2^26+2^9)
-__device__ __forceinline__ L5 mulmod(const L5& h, const L5& r) {
-  const uint32_t s1 = r.v[1] * 5, s2 = r.v[2] * 5, s3 = r.v[3] * 5, s4 = r.v[4] * 5;
-  uint64_t d0 = (uint64_t)h.v[0] * r.v[0] + (uint64_t)h.v[1] * s4 + (uint64_t)h.v[2] * s3 +
-                (uint64_t)h.v[3] * s2 + (uint64_t)h.v[4] * s1;
-  uint64_t d1 = (uint64_t)h.v[0] * r.v[1] + (uint64_t)h.v[1] * r.v[0] + (uint64_t)h.v[2] * s4 +
-                (uint64_t)h.v[3] * s3 + (uint64_t)h.v[4] * s2;
-  uint64_t d2 = (uint64_t)h.v[0] * r.v[2] + (uint64_t)h.v[1] * r.v[1] + (uint64_t)h.v[2] * r.v[0] +
-                (uint64_t)h.v[3] * s4 + (uint64_t)h.v[4] * s3;
-  uint64_t d3 = (uint64_t)h.v[0] * r.v[3] + (uint64_t)h.v[1] * r.v[2] + (uint64_t)h.v[2] * r.v[1] +
-                (uint64_t)h.v[3] * r.v[0] + (uint64_t)h.v[4] * s4;
-  uint64_t d4 = (uint64_t)h.v[0] * r.v[4] + (uint64_t)h.v[1] * r.v[3] + (uint64_t)h.v[2] * r.v[2] +
-                (uint64_t)h.v[3] * r.v[1] + (uint64_t)h.v[4] * r.v[0];
-  L5 o;
-  d1 += d0 >> 26; o.v[0] = (uint32_t)d0 & M26;
-  d2 += d1 >> 26; o.v[1] = (uint32_t)d1 & M26;
-  d3 += d2 >> 26; o.v[2] = (uint32_t)d2 & M26;
-  d4 += d3 >> 26; o.v[3] = (uint32_t)d3 & M26;
-  const uint64_t c = d4 >> 26; o.v[4] = (uint32_t)d4 & M26;
-  const uint64_t t0 = (uint64_t)o.v[0] + c * 5;
-  o.v[0] = (uint32_t)t0 & M26;
-  o.v[1] += (uint32_t)(t0 >> 26);
-  return o;
-}
-
-__device__ __forceinline__ L5 add5(const L5& a, const L5& b) {
-  L5 o;
-#pragma unroll
-  for (int i = 0; i < 5; i++) o.v[i] = a.v[i] + b.v[i];
-  return o;
-}
-
-// partial carry: limbs back under 2^26 (+ small in v[1])
-__device__ __forceinline__ L5 carry5(L5 h) {
-  uint32_t c;
-  c = h.v[0] >> 26; h.v[0] &= M26; h.v[1] += c;
-  c = h.v[1] >> 26; h.v[1] &= M26; h.v[2] += c;
-  c = h.v[2] >> 26; h.v[2] &= M26; h.v[3] += c;
-  c = h.v[3] >> 26; h.v[3] &= M26; h.v[4] += c;
-  c = h.v[4] >> 26; h.v[4] &= M26; h.v[0] += c * 5;
-  c = h.v[0] >> 26; h.v[0] &= M26; h.v[1] += c;
-  return h;
-}
-
-// 16-byte little-endian block (+2^128 pad bit) -> limbs
-__device__ __forceinline__ L5 block_limbs(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
-  L5 m;
-  m.v[0] = w0 & M26;
-  m.v[1] = __builtin_amdgcn_alignbit(w1, w0, 26) & M26;
-  m.v[2] = __builtin_amdgcn_alignbit(w2, w1, 20) & M26;
-  m.v[3] = __builtin_amdgcn_alignbit(w3, w2, 14) & M26;
-  m.v[4] = (w3 >> 8) | (1u << 24);
-  return m;
-}
-
-// full reduction mod p, then (h + s) mod 2^128 -> 4 LE words
-__device__ __forceinline__ void poly_tag(L5 h, const uint32_t (&s)[4], uint32_t (&tag)[4]) {
-  h = carry5(h);
-  uint32_t c;
-  // limbs 0..3 < 2^26, h4 <= 2^26 (+small): value < 2^130 + 2^104
-  c = h.v[1] >> 26; h.v[1] &= M26; h.v[2] += c;
-  c = h.v[2] >> 26; h.v[2] &= M26; h.v[3] += c;
-  c = h.v[3] >> 26; h.v[3] &= M26; h.v[4] += c;
-  // g = h + 5 - 2^130 ; select g when non-negative (h >= p)
-  uint32_t g[5];
-  g[0] = h.v[0] + 5; c = g[0] >> 26; g[0] &= M26;
-  g[1] = h.v[1] + c; c = g[1] >> 26; g[1] &= M26;
-  g[2] = h.v[2] + c; c = g[2] >> 26; g[2] &= M26;
-  g[3] = h.v[3] + c; c = g[3] >> 26; g[3] &= M26;
-  g[4] = h.v[4] + c - (1u << 26);
-  const uint32_t mask = (g[4] >> 31) - 1;  // all ones when g >= 0
-#pragma unroll
-  for (int i = 0; i < 5; i++) h.v[i] = (h.v[i] & ~mask) | (g[i] & mask);
-  const uint32_t w0 = h.v[0] | (h.v[1] << 26);
-  const uint32_t w1 = (h.v[1] >> 6) | (h.v[2] << 20);
-  const uint32_t w2 = (h.v[2] >> 12) | (h.v[3] << 14);
-  const uint32_t w3 = (h.v[3] >> 18) | (h.v[4] << 8);
-  uint64_t f = (uint64_t)w0 + s[0]; tag[0] = (uint32_t)f;
-  f = (uint64_t)w1 + s[1] + (f >> 32); tag[1] = (uint32_t)f;
-  f = (uint64_t)w2 + s[2] + (f >> 32); tag[2] = (uint32_t)f;
-  f = (uint64_t)w3 + s[3] + (f >> 32); tag[3] = (uint32_t)f;
-}
-
-__device__ __forceinline__ L5 load_l5(const uint32_t* p) {
-  L5 o;
-#pragma unroll
-  for (int i = 0; i < 5; i++) o.v[i] = p[i];
-  return o;
-}
-
-__device__ __forceinline__ uint32_t ld_le32(const uint8_t* p) {
-  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
-}
-
-// key schedule shared by open/seal setup: subkey, (r, s), r^(2^k)
-__device__ void key_schedule(const DevKey& key, const uint8_t* nonce, FileParams& P) {
-  uint32_t k[8], n16[4], sub[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) k[i] = key.k[i];
-#pragma unroll
-  for (int i = 0; i < 4; i++) n16[i] = ld_le32(nonce + 4 * i);
-  hchacha20(k, n16, sub);
-  const uint32_t n2a = ld_le32(nonce + 16), n2b = ld_le32(nonce + 20);
-  uint32_t b0[16];
-  chacha_block(sub, 0, 0, n2a, n2b, b0);
-#pragma unroll
-  for (int i = 0; i < 8; i++) P.subkey[i] = sub[i];
-  P.n2[0] = n2a; P.n2[1] = n2b;
-  // r = le128(b0[0..4]) clamped
-  const uint32_t r0 = b0[0] & 0x0fffffffu, r1 = b0[1] & 0x0ffffffcu, r2 = b0[2] & 0x0ffffffcu,
-                 r3 = b0[3] & 0x0ffffffcu;
-  L5 r;
-  r.v[0] = r0 & M26;
-  r.v[1] = __builtin_amdgcn_alignbit(r1, r0, 26) & M26;
-  r.v[2] = __builtin_amdgcn_alignbit(r2, r1, 20) & M26;
-  r.v[3] = __builtin_amdgcn_alignbit(r3, r2, 14) & M26;
-  r.v[4] = r3 >> 8;
-  P.s[0] = b0[4]; P.s[1] = b0[5]; P.s[2] = b0[6]; P.s[3] = b0[7];
-#pragma unroll
-  for (int i = 0; i < 5; i++) P.rpow[0][i] = r.v[i];
-  L5 p = r;
-  for (int kk = 1; kk < 7; kk++) {
-    p = mulmod(p, p);
-#pragma unroll
-    for (int i = 0; i < 5; i++) P.rpow[kk][i] = p.v[i];
-  }
-}
-
-__device__ __forceinline__ void reserve_segments(FileParams& P, uint32_t f, SegScratch sc) {
-  const uint64_t nblk = ((uint64_t)P.len + 15) / 16 + 1;
-  const uint32_t nseg = (uint32_t)((nblk + kSegBlocks - 1) / kSegBlocks);
-  P.nseg = nseg;
-  P.extra_base = 0;
-  if (nseg > 1) {
-    const uint32_t e = atomicAdd(&sc.counters[0], nseg - 1);
-    const uint32_t pb = atomicAdd(&sc.counters[6], nseg);
-    const uint32_t mf = atomicAdd(&sc.counters[1], 1u);
-    P.extra_base = pb;
-    sc.multi_files[mf] = f;
-    for (uint32_t j = 1; j < nseg; j++) sc.extra_list[e + j - 1] = make_uint2(f, j);
-  }
-}
 
 // ----------------------------------------------------------------------------------------
 // setup kernels
@@ -240,7 +46,35 @@ __global__ __launch_bounds__(256) void k_open_setup(const uint8_t* __restrict__ 
   }
   if (st == CE_OK) st = key_status;  // key version / length (xchacha lib.rs:74-78)
   Envelope e{};
-  if (st == CE_OK) st = parse_envelope(enc, enc_len, &e);
+  bool fast = false;
+  if (st == CE_OK && enc_len >= 67 + 16) {
+    // canonical EncHandler::encrypt box with a bin16 EncBox (clear text ~190 B .. 64 KiB),
+    // checked from registers: 92 c4 10 <box16> c5 EE EE 82 a5"nonce" c4 18 <24> a8"enc_data"
+    // c5 LL LL <ct||tag>  (xchacha lib.rs:59-67)
+    uint32_t w[17];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint4 v = *reinterpret_cast<const uint4*>(enc + 16 * i);
+      w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+    }
+    w[16] = ld_le32(enc + 64);
+    auto byte = [&](int i) -> uint32_t { return (w[i >> 2] >> (8 * (i & 3))) & 0xffu; };
+    bool ok = byte(0) == 0x92 && byte(1) == 0xc4 && byte(2) == 0x10 && byte(19) == 0xc5 &&
+              byte(22) == 0x82 && byte(23) == 0xa5 && byte(24) == 'n' && byte(25) == 'o' &&
+              byte(26) == 'n' && byte(27) == 'c' && byte(28) == 'e' && byte(29) == 0xc4 &&
+              byte(30) == 0x18 && byte(55) == 0xa8 && byte(56) == 'e' && byte(57) == 'n' &&
+              byte(58) == 'c' && byte(59) == '_' && byte(60) == 'd' && byte(61) == 'a' &&
+              byte(62) == 't' && byte(63) == 'a' && byte(64) == 0xc5;
+#pragma unroll
+    for (int i = 0; i < 16; i++) ok = ok && byte(3 + i) == kBoxVersion[i];
+    const uint32_t eb = (byte(20) << 8) | byte(21);
+    const uint32_t l2 = (byte(65) << 8) | byte(66);
+    if (ok && eb == 45 + l2 && 22ull + eb <= enc_len && l2 >= 16) {
+      e.nonce_off = 31; e.nonce_len = 24; e.enc_off = 67; e.enc_len = l2;
+      fast = true;
+    }
+  }
+  if (st == CE_OK && !fast) st = parse_envelope(enc, enc_len, &e);
   FileParams P;
   P.status = st;
   P.len = 0;
@@ -304,15 +138,12 @@ __global__ __launch_bounds__(256) void k_seal_setup(const uint8_t* __restrict__ 
 // segment kernel: one wavefront per (file, 16 KiB segment)
 // ----------------------------------------------------------------------------------------
 static constexpr int kWavesPerBlock = 4;
-static constexpr int kKsStride = 80;  // LDS bytes per keystream block (64 + 16 pad: no conflicts)
-
-__device__ __forceinline__ uint32_t bcast(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-
 template <bool SEAL>
 __global__ __launch_bounds__(256) void k_segments(const uint8_t* __restrict__ in,
                                                   uint8_t* __restrict__ out,
                                                   const FileParams* __restrict__ params, uint32_t n,
-                                                  int32_t* __restrict__ status, SegScratch sc) {
+                                                  int32_t* __restrict__ status, SegScratch sc,
+                                                  int skip_small) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWavesPerBlock * 64 * kKsStride];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wib = threadIdx.x >> 6;
@@ -327,6 +158,7 @@ __global__ __launch_bounds__(256) void k_segments(const uint8_t* __restrict__ in
     const FileParams* Pp = params + f;
     if (Pp->status != CE_OK) continue;  // setup status (never rewritten: read-only here)
     const uint32_t len = Pp->len;
+    if (skip_small && len <= kSmallMax) continue;  // k_open_fold_small handles these
     const uint32_t nseg = Pp->nseg;
     uint32_t key[8];
 #pragma unroll
@@ -509,29 +341,6 @@ __global__ __launch_bounds__(256) void k_finalize_multi(uint8_t* __restrict__ ou
 // ----------------------------------------------------------------------------------------
 // decode + fold: one wavefront per file
 // ----------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t lookup_slot(const ActorSlot* __restrict__ tab, uint32_t mask,
-                                                uint32_t k0, uint32_t k1, uint32_t k2,
-                                                uint32_t k3) {
-  uint32_t h = actor_hash(k0, k1, k2, k3) & mask;
-  for (uint32_t probe = 0; probe <= mask; probe++) {
-    const uint4 a = *reinterpret_cast<const uint4*>(tab[h].k);
-    const uint32_t used = tab[h].used;
-    if (!used) return 0xffffffffu;
-    if (a.x == k0 && a.y == k1 && a.z == k2 && a.w == k3) return h;
-    h = (h + 1) & mask;
-  }
-  return 0xffffffffu;
-}
-
-__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
-
-// bytes [b, b+4) of a 48-byte window held as 12 LE words (b compile-time or uniform small)
-__device__ __forceinline__ uint32_t win_word(const uint32_t (&w)[12], int b) {
-  const int i = b >> 2, s = b & 3;
-  if (s == 0) return w[i];
-  return __builtin_amdgcn_alignbyte(w[i + 1], w[i], s);
-}
-
 struct FoldState {
   uint32_t slot;             // wave-uniform pending slot (0xffffffff = none)
   unsigned long long best;   // pending max
@@ -583,8 +392,8 @@ __global__ __launch_bounds__(256) void k_decode_dots(DecodeArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t stride = gridDim.x * kWavesPerBlock;
   for (uint32_t f = bcast(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)); f < a.n; f += stride) {
-    if (a.only && !a.only[f]) continue;
     const FileParams* Pp = a.params + f;
+    if ((a.only && !a.only[f]) || (a.large_only && Pp->len <= kSmallMax)) continue;
     if (a.status[f] != CE_OK) continue;
     const uint8_t* pt = a.pt + Pp->out_off;
     const uint32_t len = Pp->len;
@@ -613,11 +422,7 @@ __global__ __launch_bounds__(256) void k_decode_dots(DecodeArgs a) {
       if (remaining > blen) st = CE_ERR_DECODE, remaining = 0;  // each Dot takes >= 1 byte
       while (remaining > 0 && st == CE_OK) {
         // canonical rmp-serde Dot: 82 a5"actor" c4 10 <16> a7"counter" <uint>  (33 + 1..9 bytes)
-        uint32_t L = 0;
-        if (pos + 34 <= blen) {
-          const uint8_t mk = body[pos + 33];
-          L = mk <= 0x7f ? 34 : mk == 0xcc ? 35 : mk == 0xcd ? 36 : mk == 0xce ? 38 : mk == 0xcf ? 42 : 0;
-        }
+        const uint32_t L = pos + 34 <= blen ? dot_len_of_marker(body[pos + 33]) : 0;
         bool valid = false;
         uint32_t k0 = 0, k1 = 0, k2 = 0, k3 = 0;
         unsigned long long ctr = 0;
@@ -631,17 +436,7 @@ __global__ __launch_bounds__(256) void k_decode_dots(DecodeArgs a) {
             w[0] = A.x; w[1] = A.y; w[2] = A.z; w[3] = A.w;
             w[4] = B.x; w[5] = B.y; w[6] = B.z; w[7] = B.w;
             w[8] = C.x; w[9] = C.y; w[10] = C.z; w[11] = C.w;
-            const uint32_t mk = (w[8] >> 8) & 0xff;
-            const uint32_t Lc = mk <= 0x7f ? 34 : mk == 0xcc ? 35 : mk == 0xcd ? 36 : mk == 0xce ? 38 : mk == 0xcf ? 42 : 0;
-            valid = w[0] == 0x6361a582u && w[1] == 0xc4726f74u && (w[2] & 0xffu) == 0x10u &&
-                    win_word(w, 25) == 0x756f63a7u && win_word(w, 29) == 0x7265746eu && Lc == L;
-            k0 = win_word(w, 9); k1 = win_word(w, 13); k2 = win_word(w, 17); k3 = win_word(w, 21);
-            const uint32_t hi = bswap32(win_word(w, 34)), lo = bswap32(win_word(w, 38));
-            ctr = L == 34 ? mk
-                : L == 35 ? (hi >> 24)
-                : L == 36 ? (hi >> 16)
-                : L == 38 ? hi
-                : (((unsigned long long)hi << 32) | lo);
+            valid = canon_dot(w, L, k0, k1, k2, k3, ctr);
           }
         }
         const unsigned long long vm = __ballot(valid);
@@ -718,15 +513,15 @@ hipError_t launch_seal_setup(hipStream_t s, const uint8_t* clear, const uint64_t
 
 hipError_t launch_segments(hipStream_t s, bool seal, const uint8_t* in, uint8_t* out,
                            const FileParams* params, uint32_t n, int32_t* status, SegScratch sc,
-                           uint32_t grid_waves) {
+                           uint32_t grid_waves, bool skip_small) {
   if (n == 0) return hipSuccess;
   const uint32_t blocks = (grid_waves + kWavesPerBlock - 1) / kWavesPerBlock;
   if (seal)
     hipLaunchKernelGGL(k_segments<true>, dim3(blocks), dim3(256), 0, s, in, out, params, n,
-                       status, sc);
+                       status, sc, 0);
   else
     hipLaunchKernelGGL(k_segments<false>, dim3(blocks), dim3(256), 0, s, in, out, params, n,
-                       status, sc);
+                       status, sc, skip_small ? 1 : 0);
   return hipGetLastError();
 }
 

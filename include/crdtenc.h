@@ -221,11 +221,14 @@ int ce_core_reset(ce_core *c);
 int ce_core_ingest_ops(ce_core *c, const uint8_t *blob, const uint64_t *offs, uint32_t n,
                        const uint8_t *actors, uint32_t m, const uint32_t *file_actor,
                        const uint64_t *file_version, int32_t *status);
-/* Same with the files already resident in HBM (d_blob/d_offs device pointers, d_offs has n+1
- * entries and blob_len = offs[n]); actor metadata stays on the host. */
+/* Same with the batch resident in HBM: d_blob/d_offs (n+1 entries, blob_len = offs[n]) and
+ * the per-file metadata d_file_actor (u32) / d_file_version (u64) are device pointers; the m
+ * writer actors (16 bytes each) and status (may be NULL) are host memory.  Batches in
+ * Storage::load_ops order (each actor's files contiguous with consecutive versions) are gated
+ * on the GPU; any other order is gated on the host with identical results. */
 int ce_core_ingest_ops_device(ce_core *c, const uint8_t *d_blob, const uint64_t *d_offs,
                               uint32_t n, uint64_t blob_len, const uint8_t *actors, uint32_t m,
-                              const uint32_t *file_actor, const uint64_t *file_version,
+                              const uint32_t *d_file_actor, const uint64_t *d_file_version,
                               int32_t *status);
 /* What read_remote_states does after Storage::load_states (lib.rs:425-466). */
 int ce_core_ingest_states(ce_core *c, const uint8_t *blob, const uint64_t *offs, uint32_t n,

@@ -345,3 +345,91 @@ def test_reference_compact_format_is_unreadable_by_read_remote(ctx, tmp_path):
                       local_path=str(tmp_path / "l2"), remote_path=remote, flags=crdtenc.OPEN_CREATE)
     c2.set_latest_key(key)
     assert c2.read_remote() == 2     # "version check failed" (lib.rs:435)
+
+
+@pytest.mark.parametrize("fpw", ["1", "2", "4"])
+def test_fused_geometries_match_oracle(ctx, oracle, fpw, monkeypatch):
+    """k_open_fold_small with 1, 2 and 4 files per wavefront; mixed single-page sizes."""
+    monkeypatch.setenv("CE_FILES_PER_WAVE", fpw)
+    key = os.urandom(32)
+    rng = random.Random(int(fpw))
+    actors = sorted(rng.randbytes(16) for _ in range(13))
+    clears, fa, vers = [], [], []
+    for a in range(13):
+        for v in range(11):
+            nd = rng.choice([0, 1, 3, 15, 16, 17, 63, 64, 65, 100, 107])
+            dots = [{"actor": actors[a] if rng.random() < 0.7 else rng.choice(actors),
+                     "counter": rng.getrandbits(rng.choice([5, 7, 8, 16, 32, 63]))} for _ in range(nd)]
+            clears.append(APP + msgpack.packb(dots, use_bin_type=True))
+            fa.append(a)
+            vers.append(v)
+    files = [CORE + e for e in ctx.encrypt_batch(key, clears)]
+    assert max(len(c) for c in clears) <= 4096
+    core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+    core.set_latest_key(key)
+    rc, st = core.ingest_ops(files, actors, fa, vers)
+    oc = oracle.Core()
+    orc, ost = oc.read_remote_ops(key, [APP], files, [actors[i] for i in fa], vers)
+    assert rc == orc == 0 and st == ost
+    assert core.state_bytes() == oc.serialize()
+    # one tampered file in the middle of a 4-file wave group: whole batch rejected
+    bad = bytearray(files[50])
+    bad[-20] ^= 8
+    files2 = files[:50] + [bytes(bad)] + files[51:]
+    core2 = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+    core2.set_latest_key(key)
+    empty = core2.state_bytes()
+    rc, st = core2.ingest_ops(files2, actors, fa, vers)
+    assert rc == 9 and st[50] == 9 and core2.state_bytes() == empty
+
+
+def test_unordered_batch_uses_host_gate(ctx, oracle):
+    """Files not in load_ops order (actors interleaved, versions shuffled): the device gate
+    declines and the host gate reproduces the reference loop exactly."""
+    key = os.urandom(32)
+    files, actors, fa, vers = make_ops_batch(ctx, key, 5, 6, 4, seed=99)
+    rng = random.Random(1)
+    order = list(range(len(files)))
+    rng.shuffle(order)
+    sel = lambda xs: [xs[i] for i in order]
+    core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+    core.set_latest_key(key)
+    rc, st = core.ingest_ops(sel(files), actors, sel(fa), sel(vers))
+    oc = oracle.Core()
+    orc, ost = oc.read_remote_ops(key, [APP], sel(files), [actors[i] for i in sel(fa)], sel(vers))
+    assert rc == orc and st == ost
+    assert core.state_bytes() == oc.serialize()
+    # interleaved but per-actor ordered (round-robin) -> no gap, everything applies
+    rr = sorted(range(len(files)), key=lambda i: (vers[i], fa[i]))
+    sel2 = lambda xs: [xs[i] for i in rr]
+    core2 = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+    core2.set_latest_key(key)
+    assert core2.ingest_ops(sel2(files), actors, sel2(fa), sel2(vers))[0] == 0
+    oc2 = oracle.Core()
+    assert oc2.read_remote_ops(key, [APP], files, [actors[i] for i in fa], vers)[0] == 0
+    assert core2.state_bytes() == oc2.serialize()
+
+
+def test_device_metadata_api(ctx, oracle):
+    """ce_core_ingest_ops_device with files + per-file metadata in HBM (torch tensors)."""
+    torch = pytest.importorskip("torch")
+    import numpy as np
+    key = os.urandom(32)
+    files, actors, fa, vers = make_ops_batch(ctx, key, 9, 7, 30, seed=5)
+    blob = b"".join(files)
+    offs = np.zeros(len(files) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum([len(f) for f in files])
+    d_blob = torch.tensor(list(blob) + [0] * 64, dtype=torch.uint8, device="cuda")
+    d_offs = torch.tensor(offs, device="cuda")
+    d_fa = torch.tensor(np.array(fa, dtype=np.int32), device="cuda")
+    d_fv = torch.tensor(np.array(vers, dtype=np.int64), device="cuda")
+    torch.cuda.synchronize()
+    core = crdtenc.Core(ctx, kind=crdtenc.STATE_VCLOCK, supported=[APP], current_data_version=APP)
+    core.set_latest_key(key)
+    rc, st = core.ingest_ops_device(d_blob.data_ptr(), d_offs.data_ptr(), len(files), len(blob),
+                                    b"".join(actors), d_fa.data_ptr(), d_fv.data_ptr(),
+                                    want_status=True)
+    assert rc == 0 and set(st) == {0}
+    oc = oracle.Core(oracle.STATE_VCLOCK)
+    assert oc.read_remote_ops(key, [APP], files, [actors[i] for i in fa], vers)[0] == 0
+    assert core.state_bytes() == oc.serialize()
