@@ -630,6 +630,15 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
   da.table = c->d_table.as<ActorSlot>();
   da.mask = c->cap - 1;
   da.batch = c->d_batch.as<unsigned long long>();
+  da.large_list = ctx->large.as<uint32_t>();
+  if (const char* ab = getenv("CE_ABLATE")) da.ablate = atoi(ab);
+  static DevBuf& prof_buf = *new DevBuf;  // CE_PROF diagnostics (never freed): per-wave phase cycles
+  const bool prof = getenv("CE_PROF") != nullptr;
+  if (prof) {
+    if ((e = prof_buf.reserve(8ull * 8 * 65536)) || (e = hipMemsetAsync(prof_buf.p, 0, 8ull * 8 * 65536, ctx->stream)))
+      return ctx->hip_fail(e, "prof");
+    da.prof = prof_buf.as<unsigned long long>();
+  }
 
   // 2) GPU: single-page files: open + decode + fold fused; larger files: segments + decode
   auto run_fold = [&](const uint8_t* only) -> int {
@@ -658,6 +667,23 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
     return CE_OK;
   };
   if ((rc = run_fold(nullptr))) return rc;
+  if (prof) {
+    std::vector<unsigned long long> hp(8ull * 65536);
+    if ((e = hipMemcpyAsync(hp.data(), prof_buf.p, hp.size() * 8, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+      return ctx->hip_fail(e, "prof");
+    double sum[7] = {0, 0, 0, 0, 0, 0, 0};
+    uint32_t waves = 0;
+    for (size_t w = 0; w < 65536; w++)
+      if (hp[8 * w + 6]) {
+        waves++;
+        for (int i = 0; i < 7; i++) sum[i] += (double)hp[8 * w + i];
+      }
+    if (waves)
+      fprintf(stderr, "CE_PROF waves %u iters/wave %.1f cycles/iter: params %.0f chacha %.0f xor_horner %.0f "
+              "tree_tag %.0f decode_prelude %.0f decode_rounds %.0f\n", waves, sum[6] / waves,
+              sum[0] / sum[6], sum[1] / sum[6], sum[2] / sum[6], sum[3] / sum[6], sum[4] / sum[6], sum[5] / sum[6]);
+  }
   uint32_t* hc = ctx->h_counters.as<uint32_t>();
   if ((e = hipMemcpyAsync(hc, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->stream)) ||
       (e = hipStreamSynchronize(ctx->stream)))

@@ -79,6 +79,7 @@ static int reserve_batch(ce_ctx* ctx, uint32_t n, uint64_t blob_len, uint32_t* e
       (e = ctx->extra.reserve(ec * 8)) != hipSuccess ||
       (e = ctx->multi.reserve(ec * 4)) != hipSuccess ||
       (e = ctx->partials.reserve(ec * 2 * 5 * 4)) != hipSuccess ||
+      (e = ctx->large.reserve((size_t)n * 4 + 64)) != hipSuccess ||
       (e = ctx->h_counters.reserve(256)) != hipSuccess)
     return ctx->hip_fail(e, "reserve batch scratch");
   return CE_OK;
@@ -91,6 +92,7 @@ SegScratch segscratch(ce_ctx* ctx, uint32_t extra_cap) {
   sc.extra_cap = extra_cap;
   sc.multi_files = ctx->multi.as<uint32_t>();
   sc.partials = ctx->partials.as<uint32_t>();
+  sc.large_list = ctx->large.as<uint32_t>();
   return sc;
 }
 

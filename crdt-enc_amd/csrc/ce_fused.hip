@@ -21,7 +21,9 @@
 
 namespace ce {
 
-static constexpr uint32_t kRegion = 64 * kKsStride;  // 5120 B of LDS per file in flight
+// LDS per file in flight: 64 keystream blocks at an 80-byte stride (5120 B).  Any padding
+// beyond this costs resident blocks: 4 x (2 waves x 4 files x 5120 B) is exactly 160 KiB.
+static constexpr uint32_t kRegion = 64 * kKsStride;
 
 template <int LPF>
 struct FusedCfg {
@@ -29,51 +31,91 @@ struct FusedCfg {
   static constexpr int WPB = LPF == 16 ? 2 : 4;            // waves per block
   static constexpr int LOG = LPF == 16 ? 4 : LPF == 32 ? 5 : 6;
   static constexpr int ROWS = (256 + 1 + LPF - 1) / LPF;   // Horner steps for a full page
-  static constexpr int WAVES_PER_SIMD = LPF == 16 ? 2 : LPF == 32 ? 4 : 8;  // LDS-limited
+  static constexpr int WAVES_PER_SIMD = LPF == 16 ? 2 : LPF == 32 ? 3 : 4;  // LDS-limited
 };
 
-struct GroupFold {
-  uint32_t slot;
-  unsigned long long best;
-};
-
+// ---- lane-group collectives (a group = the LPF lanes of one file) --------------------------
+// DPP inside a row of 16 lanes (no LDS round trip); wider groups add xor-shuffles.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+}
+// lane i <- lane i + d inside the row (0 past the row's end), d in {1, 2, 4, 8}
+__device__ __forceinline__ uint32_t row_down(uint32_t v, int d) {
+  switch (d) {
+    case 1: return dpp<0x101>(v);
+    case 2: return dpp<0x102>(v);
+    case 4: return dpp<0x104>(v);
+    default: return dpp<0x108>(v);
+  }
+}
+template <int LPF, typename Op>
+__device__ __forceinline__ uint32_t grp_reduce(uint32_t v, Op op) {
+  v = op(v, dpp<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = op(v, dpp<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = op(v, dpp<0x141>(v));  // row_half_mirror
+  v = op(v, dpp<0x140>(v));  // row_mirror
+  if (LPF >= 32) v = op(v, (uint32_t)__shfl_xor((int)v, 16));
+  if (LPF >= 64) v = op(v, (uint32_t)__shfl_xor((int)v, 32));
+  return v;
+}
 template <int LPF>
-__device__ __forceinline__ void fold_group(const DecodeArgs& a, uint32_t f, bool active,
-                                           uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3,
-                                           unsigned long long ctr, GroupFold& gf, uint32_t grp,
-                                           uint32_t sub) {
+__device__ __forceinline__ unsigned long long grp_max64(unsigned long long v) {
+  auto step = [&](uint32_t lo, uint32_t hi) {
+    const unsigned long long o = ((unsigned long long)hi << 32) | lo;
+    v = o > v ? o : v;
+  };
+  step(dpp<0xB1>((uint32_t)v), dpp<0xB1>((uint32_t)(v >> 32)));
+  step(dpp<0x4E>((uint32_t)v), dpp<0x4E>((uint32_t)(v >> 32)));
+  step(dpp<0x141>((uint32_t)v), dpp<0x141>((uint32_t)(v >> 32)));
+  step(dpp<0x140>((uint32_t)v), dpp<0x140>((uint32_t)(v >> 32)));
+  if (LPF >= 32) step((uint32_t)__shfl_xor((int)(uint32_t)v, 16), (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), 16));
+  if (LPF >= 64) step((uint32_t)__shfl_xor((int)(uint32_t)v, 32), (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), 32));
+  return v;
+}
+// this lane's group bit of a wave ballot
+template <int LPF>
+__device__ __forceinline__ unsigned long long grp_bits(bool p, uint32_t grp) {
   constexpr unsigned long long GM = LPF == 64 ? ~0ull : ((1ull << LPF) - 1);
-  uint32_t slot = 0xffffffffu;
-  if (active) {
-    slot = lookup_slot(a.table, a.mask, k0, k1, k2, k3);
-    if (slot == 0xffffffffu) {
-      const uint32_t mi = atomicAdd(&a.counters[4], 1u);
-      if (mi < a.miss_cap) a.miss_list[mi] = make_uint4(k0, k1, k2, k3);
-      a.refold[f] = 1;
-    }
-  }
-  const bool live = active && slot != 0xffffffffu;
-  const unsigned long long gb = (__ballot(live) >> (grp * LPF)) & GM;
-  const uint32_t first = grp * LPF + (uint32_t)__builtin_ctzll(gb | (1ull << (LPF - 1)));
-  const uint32_t s0 = __shfl(slot, first);
-  const bool same = ((__ballot(live && slot != s0) >> (grp * LPF)) & GM) == 0;
-  if (same && gb != 0) {
-    unsigned long long v = live ? ctr : 0ull;
+  return (__ballot(p) >> (grp * LPF)) & GM;
+}
+
+// canonical Dot lengths <-> 3-bit codes (ballot transport of the next Dot's length)
+__device__ __forceinline__ uint32_t len_code(uint32_t L) {
+  return L == 34 ? 1u : L == 35 ? 2u : L == 36 ? 3u : L == 38 ? 4u : L == 42 ? 5u : 0u;
+}
+__device__ __forceinline__ uint32_t code_len(uint32_t c) {
+  return c == 1 ? 34u : c == 2 ? 35u : c == 3 ? 36u : c == 4 ? 38u : 42u;
+}
+
+// per-iteration inputs of one file, prefetched one grid-stride iteration ahead
+struct FilePre {
+  uint32_t ok;      // file exists, selected, setup status OK
+  uint32_t apply;   // version gate lets this file fold
+  uint32_t len;
+  uint32_t in_off;  // ciphertext offset in the blob (lo, hi)
+  uint32_t in_hi;
+  uint32_t key[8];
+  uint32_t n2a, n2b;
+};
+
+__device__ __forceinline__ FilePre load_pre(const DecodeArgs& a, uint32_t f) {
+  FilePre p;
+  const bool in = f < a.n;
+  const uint32_t fi = in ? f : 0u;
+  const FileParams* Pp = a.params + fi;
+  bool ok = in && a.status[fi] == CE_OK;
+  if (a.only) ok = ok && a.only[fi] != 0;
+  p.ok = ok;
+  p.apply = a.apply == nullptr || a.apply[fi] != 0;
+  p.len = Pp->len;
+  p.in_off = (uint32_t)Pp->in_off;
+  p.in_hi = (uint32_t)(Pp->in_off >> 32);
 #pragma unroll
-    for (int d = LPF / 2; d >= 1; d >>= 1) {
-      const unsigned long long o = __shfl_xor(v, d);
-      v = o > v ? o : v;
-    }
-    if (gf.slot != s0) {
-      if (gf.slot != 0xffffffffu && sub == 0) atomicMax(&a.batch[gf.slot], gf.best);
-      gf.slot = s0;
-      gf.best = v;
-    } else if (v > gf.best) {
-      gf.best = v;
-    }
-  } else if (live) {
-    atomicMax(&a.batch[slot], ctr);
-  }
+  for (int i = 0; i < 8; i++) p.key[i] = Pp->subkey[i];
+  p.n2a = Pp->n2[0];
+  p.n2b = Pp->n2[1];
+  return p;
 }
 
 template <int LPF>
@@ -89,17 +131,32 @@ void k_open_fold_small(DecodeArgs a) {
   uint8_t* fl = lds + (wib * F + grp) * kRegion;
   const uint32_t ngroups = (a.n + F - 1) / F;
   const uint32_t stride = gridDim.x * C::WPB;
+  // CE_PROF: s_memtime at phase boundaries, summed per wave (params+loads, ChaCha20,
+  // XOR+Horner, tree+tag, decode prelude, decode rounds+flush, iterations)
+  unsigned long long pc[7] = {0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tp = a.prof ? __builtin_amdgcn_s_memtime() : 0;
+#define CE_PHASE(i)                                            \
+  if (a.prof) {                                                \
+    const unsigned long long tn = __builtin_amdgcn_s_memtime(); \
+    pc[i] += tn - tp;                                          \
+    tp = tn;                                                   \
+  }
 
-  for (uint32_t g = bcast(blockIdx.x * C::WPB + wib); g < ngroups; g += stride) {
+  uint32_t g = bcast(blockIdx.x * C::WPB + wib);
+  FilePre nx = load_pre(a, g * F + grp);
+  // decode state carried across files: speculated Dot length, per-lane actor cache
+  uint32_t Ls = 38;
+  uint32_t ck0 = 0, ck1 = 0, ck2 = 0, ck3 = 0, cslot = 0xffffffffu;
+
+  for (; g < ngroups; g += stride) {
     const uint32_t f = g * F + grp;
-    bool act = f < a.n;
-    if (act && a.only) act = a.only[f] != 0;
-    const FileParams* Pp = a.params + (act ? f : 0);
-    if (act) act = a.status[f] == CE_OK && Pp->len <= kSmallMax;
-    const uint32_t len = act ? Pp->len : 0u;
+    const FilePre cur = nx;
+    const uint32_t len = cur.ok && cur.len <= kSmallMax ? cur.len : 0u;
+    const bool act = cur.ok && cur.len <= kSmallMax;
     const uint32_t nblk_ct = (len + 15) >> 4;
     const uint32_t nb = nblk_ct + 1;
-    const uint8_t* src = a.blob + (act ? Pp->in_off : 0);
+    const uint8_t* src = a.blob + (act ? (((uint64_t)cur.in_hi << 32) | cur.in_off) : 0);
+    const FileParams* Pp = a.params + (act ? f : 0);
 
     // 1) ciphertext pieces -> registers (issued first: latency hides under the ChaCha20)
     uint4 ct[PPL];
@@ -107,26 +164,25 @@ void k_open_fold_small(DecodeArgs a) {
     for (int j = 0; j < PPL; j++) {
       const uint32_t blk = sub + LPF * j;
       const uint32_t boff = blk * 16;
-      if (act && boff + 16 <= len) ct[j] = *reinterpret_cast<const uint4*>(src + boff);
-      else if (act && boff < len) {
-        uint32_t wv[4] = {0, 0, 0, 0};
-        for (uint32_t b = 0; b < len - boff; b++) wv[b >> 2] |= (uint32_t)src[boff + b] << (8 * (b & 3));
-        ct[j] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-      } else ct[j] = make_uint4(0, 0, 0, 0);
+      if (a.ablate & 8) ct[j] = make_uint4(boff, len, sub, 0);
+      // the 16-byte tag follows the ciphertext, so a 16-byte load at any boff < len stays
+      // inside the file; bytes past len are zeroed below (Poly1305 pad16, plaintext tail)
+      else if (act && boff < len) ct[j] = *reinterpret_cast<const uint4*>(src + boff);
+      else ct[j] = make_uint4(0, 0, 0, 0);
     }
+    __builtin_amdgcn_wave_barrier();
+    CE_PHASE(0)
 
     // 2) keystream: lane computes blocks sub + LPF*k (ChaCha20 counter 1 + block)
-    uint32_t key[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) key[i] = act ? Pp->subkey[i] : 0u;
-    const uint32_t n2a = act ? Pp->n2[0] : 0u, n2b = act ? Pp->n2[1] : 0u;
-    __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int k = 0; k < F; k++) {
       const uint32_t b = sub + LPF * k;
       if (act && b * 64 < len) {
         uint32_t kb[16];
-        chacha_block(key, 1u + b, 0u, n2a, n2b, kb);
+        if (a.ablate & 4) {
+#pragma unroll
+          for (int i = 0; i < 16; i++) kb[i] = cur.key[i & 7] + b;
+        } else chacha_block(cur.key, 1u + b, 0u, cur.n2a, cur.n2b, kb);
         uint4* kd = reinterpret_cast<uint4*>(fl + b * kKsStride);
         kd[0] = make_uint4(kb[0], kb[1], kb[2], kb[3]);
         kd[1] = make_uint4(kb[4], kb[5], kb[6], kb[7]);
@@ -135,6 +191,7 @@ void k_open_fold_small(DecodeArgs a) {
       }
     }
     __builtin_amdgcn_wave_barrier();
+    CE_PHASE(1)
 
     // 3) XOR, plaintext into LDS (over consumed keystream), strided Horner in r^LPF
     L5 R;
@@ -145,33 +202,39 @@ void k_open_fold_small(DecodeArgs a) {
     for (int j = 0; j < C::ROWS; j++) {
       const uint32_t blk = sub + LPF * j;
       if (act && blk < nblk_ct) {
+        uint32_t kw_mask[4] = {~0u, ~0u, ~0u, ~0u};
         const uint32_t q = blk;  // piece index within the page
         const uint4 k4 = *reinterpret_cast<const uint4*>(fl + (q >> 2) * kKsStride + (q & 3) * 16);
-        const uint4 x = j < PPL ? ct[j < PPL ? j : 0] : make_uint4(0, 0, 0, 0);
-        uint4 y = make_uint4(x.x ^ k4.x, x.y ^ k4.y, x.z ^ k4.z, x.w ^ k4.w);
+        uint4 x = j < PPL ? ct[j < PPL ? j : 0] : make_uint4(0, 0, 0, 0);
         const uint32_t boff = blk * 16;
-        if (boff + 16 > len) {  // tail: zero the bytes past the plaintext
+        if (boff + 16 > len) {  // tail piece: zero the bytes past the ciphertext
           const uint32_t rem = len - boff;
-          uint32_t yw[4] = {y.x, y.y, y.z, y.w};
+          uint32_t xw[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
           for (int i = 0; i < 4; i++) {
             const uint32_t lo = 4 * i;
             const uint32_t keep = rem >= lo + 4 ? 0xffffffffu
                                   : (rem <= lo ? 0u : ((1u << (8 * (rem - lo))) - 1));
-            yw[i] &= keep;
+            xw[i] &= keep;
+            kw_mask[i] = keep;
           }
-          y = make_uint4(yw[0], yw[1], yw[2], yw[3]);
+          x = make_uint4(xw[0], xw[1], xw[2], xw[3]);
         }
+        uint4 y = make_uint4(x.x ^ (k4.x & kw_mask[0]), x.y ^ (k4.y & kw_mask[1]),
+                             x.z ^ (k4.z & kw_mask[2]), x.w ^ (k4.w & kw_mask[3]));
         *reinterpret_cast<uint4*>(fl + boff) = y;
-        acc = add5(mulmod(acc, R), block_limbs(x.x, x.y, x.z, x.w));
+        if (a.ablate & 2) acc.v[j % 5] += x.x ^ x.w;
+        else acc = add5(mulmod(acc, R), block_limbs(x.x, x.y, x.z, x.w));
       } else if (act && blk == nblk_ct) {
         acc = add5(mulmod(acc, R), block_limbs(0u, 0u, len, 0u));  // le64(0) || le64(len)
       }
     }
     __builtin_amdgcn_wave_barrier();
+    CE_PHASE(2)
 
     // 4) cross-lane tree inside the group: position p holds the lane whose last block has
-    //    weight r^(LPF - p); level k multiplies by r^(2^k); finally * r.
+    //    weight r^(LPF - p); level k multiplies by r^(2^k) and adds position p + 2^k (DPP row
+    //    shifts up to 8 lanes); finally * r.  Only position 0 (sub 0) ends with the sum.
     L5 v;
     {
       const int srcl = (int)(grp * LPF + ((sub + nb) & (LPF - 1)));
@@ -185,31 +248,36 @@ void k_open_fold_small(DecodeArgs a) {
       for (int i = 0; i < 5; i++) rk.v[i] = act ? Pp->rpow[k][i] : 0u;
       L5 o;
 #pragma unroll
-      for (int i = 0; i < 5; i++) o.v[i] = __shfl_down(v.v[i], 1u << k);
+      for (int i = 0; i < 5; i++)
+        o.v[i] = k < 4 ? row_down(v.v[i], 1 << k) : (uint32_t)__shfl_down((int)v.v[i], 1u << k);
       v = carry5(add5(mulmod(v, rk), o));
     }
     L5 r1;
 #pragma unroll
     for (int i = 0; i < 5; i++) r1.v[i] = act ? Pp->rpow[0][i] : 0u;
-    L5 tot = mulmod(v, r1);
-#pragma unroll
-    for (int i = 0; i < 5; i++) tot.v[i] = __shfl(tot.v[i], (int)(grp * LPF));
-    bool ok = false;
-    if (act) {
+    const L5 tot = mulmod(v, r1);
+    bool tag_ok = false;
+    if (act && sub == 0) {
       const uint32_t sv[4] = {Pp->s[0], Pp->s[1], Pp->s[2], Pp->s[3]};
       uint32_t tag[4];
       poly_tag(tot, sv, tag);
-      ok = ((tag[0] ^ Pp->tag[0]) | (tag[1] ^ Pp->tag[1]) | (tag[2] ^ Pp->tag[2]) |
-            (tag[3] ^ Pp->tag[3])) == 0;
-      if (!ok && sub == 0) {
+      tag_ok = ((tag[0] ^ Pp->tag[0]) | (tag[1] ^ Pp->tag[1]) | (tag[2] ^ Pp->tag[2]) |
+                (tag[3] ^ Pp->tag[3])) == 0;
+      if (!tag_ok) {
         a.status[f] = CE_ERR_AUTH;
         atomicAdd(&a.counters[2], 1u);
         atomicMin(&a.counters[5], f);
       }
     }
+    bool ok = grp_bits<LPF>(tag_ok, grp) != 0;
+
+    // next iteration's parameters: their latency hides under the decode
+    nx = load_pre(a, (g + stride) * F + grp);
+    CE_PHASE(3)
 
     // 5) decode from LDS
     int32_t st = CE_OK;
+    if (a.ablate) ok = !(a.ablate & 1);
     bool live = act && ok;
     if (live) {
       if (len < 16) st = CE_ERR_PT_LEN;
@@ -233,17 +301,23 @@ void k_open_fold_small(DecodeArgs a) {
       if (!rd_array_hdr(r, &count) || count > blen) st = CE_ERR_DECODE;
       else { remaining = count; pos = (uint32_t)r.i; }
     }
-    const bool do_fold = live && st == CE_OK && (a.apply == nullptr || a.apply[f]);
-    GroupFold gf{0xffffffffu, 0ull};
+    const bool do_fold = live && st == CE_OK && cur.apply;
+    CE_PHASE(4)
+    // pending max per lane: flushed with atomicMax when the lane's actor changes
+    uint32_t pslot = 0xffffffffu;
+    unsigned long long pbest = 0;
     for (;;) {
       const bool busy = live && st == CE_OK && remaining > 0;
       if (!__any(busy)) break;
-      const uint32_t L = busy && pos + 34 <= blen ? dot_len_of_marker(body[pos + 33]) : 0u;
+      // round: lane sub reads the candidate Dot at pos + sub * Ls.  Lane 0 is at a Dot start
+      // whatever Ls is and checks its Dot at its own marker's length; lanes >= 1 are at Dot
+      // starts only when every earlier Dot of the round had length Ls.
       bool valid = false;
+      uint32_t Lme = 0;
       uint32_t k0 = 0, k1 = 0, k2 = 0, k3 = 0;
       unsigned long long ctr = 0;
-      const uint32_t cand = pos + sub * L;
-      if (L && sub < remaining && cand + L <= blen) {
+      const uint32_t cand = pos + sub * Ls;
+      if (busy && sub < remaining && cand + 34 <= blen) {
         // 13 aligned LDS dwords -> the 48-byte window at cand
         const uint32_t* d = reinterpret_cast<const uint32_t*>(body) + (cand >> 2);
         const uint32_t sh = cand & 3;
@@ -253,68 +327,130 @@ void k_open_fold_small(DecodeArgs a) {
         uint32_t w[12];
 #pragma unroll
         for (int i = 0; i < 12; i++) w[i] = __builtin_amdgcn_alignbyte(dd[i + 1], dd[i], sh);
-        valid = canon_dot(w, L, k0, k1, k2, k3, ctr);
+        Lme = dot_len_of_marker((w[8] >> 8) & 0xff);
+        const uint32_t L = sub == 0 ? Lme : Ls;
+        valid = Lme != 0 && Lme == L && cand + L <= blen && canon_dot(w, L, k0, k1, k2, k3, ctr);
       }
       constexpr unsigned long long GM = LPF == 64 ? ~0ull : ((1ull << LPF) - 1);
-      const unsigned long long gb = (__ballot(valid) >> (grp * LPF)) & GM;
-      const uint32_t k = gb == GM ? (uint32_t)LPF : (uint32_t)__builtin_ctzll(~gb);
+      const unsigned long long vb = grp_bits<LPF>(valid, grp);
+      uint32_t k = vb == GM ? (uint32_t)LPF : (uint32_t)__builtin_ctzll(~vb);
+      const bool m0 = grp_bits<LPF>(sub == 0 && Lme == Ls, grp) != 0;
+      if (!m0 && k > 1) k = 1;  // lanes >= 1 read at the wrong offsets
+      // next speculation: the first lane past the round sits exactly on the next Dot
+      const uint32_t inf = m0 ? k : 0u;
+      const uint32_t code = sub == inf ? len_code(Lme) : 0u;
+      const uint32_t nc = (grp_bits<LPF>(code & 1, grp) ? 1u : 0u) |
+                          (grp_bits<LPF>(code & 2, grp) ? 2u : 0u) |
+                          (grp_bits<LPF>(code & 4, grp) ? 4u : 0u);
+      const uint32_t Lold = Ls;
+      if (nc) Ls = code_len(nc);  // when !m0 this is lane 0's own length
       // general grammar for one element (group leader), e.g. reordered keys / array form
       const bool general = busy && k == 0;
-      int gok = 0;
-      uint32_t g0 = 0, g1 = 0, g2 = 0, g3 = 0, npos = pos;
-      unsigned long long gc = 0;
-      if (general && sub == 0) {
-        Rd q{body, blen, pos};
-        uint64_t aoff = 0, c = 0;
-        gok = parse_dot(q, &aoff, &c);
-        if (gok == 1) {
-          g0 = ld_le32(body + aoff); g1 = ld_le32(body + aoff + 4);
-          g2 = ld_le32(body + aoff + 8); g3 = ld_le32(body + aoff + 12);
-          gc = c;
-          npos = (uint32_t)q.i;
+      bool fold_me = do_fold && busy && sub < k;
+      if (__any(general)) {
+        int gok = 0;
+        uint32_t npos = pos;
+        if (general && sub == 0) {
+          Rd q{body, blen, pos};
+          uint64_t aoff = 0, c = 0;
+          gok = parse_dot(q, &aoff, &c);
+          if (gok == 1) {
+            k0 = ld_le32(body + aoff); k1 = ld_le32(body + aoff + 4);
+            k2 = ld_le32(body + aoff + 8); k3 = ld_le32(body + aoff + 12);
+            ctr = c;
+            npos = (uint32_t)q.i;
+            fold_me = do_fold;
+          }
+        }
+        gok = __shfl(gok, (int)(grp * LPF));
+        npos = __shfl(npos, (int)(grp * LPF));
+        if (general) {
+          if (gok != 1) st = CE_ERR_DECODE;
+          else { pos = npos; remaining -= 1; }
         }
       }
-      gok = __shfl(gok, (int)(grp * LPF));
-      npos = __shfl(npos, (int)(grp * LPF));
-      if (general && gok != 1) st = CE_ERR_DECODE;
-      const bool fold_fast = do_fold && busy && k > 0;
-      const bool fold_gen = do_fold && general && gok == 1;
-      if (__any(fold_fast || fold_gen)) {
-        const bool active = (fold_fast && sub < k) || (fold_gen && sub == 0);
-        fold_group<LPF>(a, f, active, fold_fast ? k0 : g0, fold_fast ? k1 : g1,
-                        fold_fast ? k2 : g2, fold_fast ? k3 : g3, fold_fast ? ctr : gc, gf, grp,
-                        sub);
+      if (fold_me) {
+        uint32_t slot;
+        // per-lane cache of the last resolved actor: a file's dots are usually its writer's
+        if (k0 == ck0 && k1 == ck1 && k2 == ck2 && k3 == ck3 && cslot != 0xffffffffu) slot = cslot;
+        else {
+          slot = lookup_slot(a.table, a.mask, k0, k1, k2, k3);
+          if (slot != 0xffffffffu) { ck0 = k0; ck1 = k1; ck2 = k2; ck3 = k3; cslot = slot; }
+        }
+        if (slot == 0xffffffffu) {
+          const uint32_t mi = atomicAdd(&a.counters[4], 1u);
+          if (mi < a.miss_cap) a.miss_list[mi] = make_uint4(k0, k1, k2, k3);
+          a.refold[f] = 1;
+        } else if (slot == pslot) {
+          pbest = ctr > pbest ? ctr : pbest;
+        } else {
+          if (pslot != 0xffffffffu) atomicMax(&a.batch[pslot], pbest);
+          pslot = slot;
+          pbest = ctr;
+        }
       }
       if (busy && k > 0) {
-        pos += k * L;
+        pos += m0 ? k * Lold : Ls;  // !m0: k == 1 and Ls == lane 0's Dot length
         remaining -= k;
-      } else if (general && gok == 1) {
-        pos = npos;
-        remaining -= 1;
       }
     }
-    if (gf.slot != 0xffffffffu && sub == 0) atomicMax(&a.batch[gf.slot], gf.best);
+    // flush: one atomicMax per file when the group's pending actors agree
+    {
+      const uint32_t hi = pslot == 0xffffffffu ? 0u : pslot + 1;
+      const uint32_t lo = pslot == 0xffffffffu ? 0xffffffffu : pslot + 1;
+      const uint32_t mx = grp_reduce<LPF>(hi, [](uint32_t x, uint32_t y) { return x > y ? x : y; });
+      const uint32_t mn = grp_reduce<LPF>(lo, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
+      const unsigned long long b = grp_max64<LPF>(pslot == 0xffffffffu ? 0ull : pbest);
+      if (mx != 0 && mn == mx) {
+        if (sub == 0) atomicMax(&a.batch[mx - 1], b);
+      } else if (pslot != 0xffffffffu) {
+        atomicMax(&a.batch[pslot], pbest);
+      }
+    }
     if (live && st != CE_OK && sub == 0) {
       a.status[f] = st;
       atomicAdd(&a.counters[3], 1u);
       atomicMin(&a.counters[5], f);
     }
     __builtin_amdgcn_wave_barrier();
+    CE_PHASE(5)
+    pc[6]++;
   }
+#undef CE_PHASE
+  if (a.prof && lane == 0) {
+    unsigned long long* o = a.prof + 8ull * (blockIdx.x * C::WPB + wib);
+#pragma unroll
+    for (int i = 0; i < 7; i++) o[i] = pc[i];
+  }
+}
+
+// Resident blocks per CU for a kernel, from the occupancy calculator (LDS and VGPRs both
+// bound it); the grid-stride loop then runs exactly one round of resident blocks.
+template <typename K>
+static uint32_t resident_blocks(K kernel, int threads) {
+  int dev = 0, per_cu = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
+  return (uint32_t)(per_cu * cus);
 }
 
 hipError_t launch_open_fold_small(hipStream_t s, const DecodeArgs& a, int files_per_wave) {
   if (a.n == 0) return hipSuccess;
+  static const uint32_t res16 = resident_blocks(k_open_fold_small<16>, 128);
+  static const uint32_t res32 = resident_blocks(k_open_fold_small<32>, 256);
+  static const uint32_t res64 = resident_blocks(k_open_fold_small<64>, 256);
   const uint32_t groups = (a.n + files_per_wave - 1) / files_per_wave;
-  // resident waves: LDS caps blocks per CU (160 KiB / block LDS)
   if (files_per_wave == 4) {
-    const uint32_t blocks = std::min<uint32_t>((groups + 1) / 2, 256u * 4u);
+    const uint32_t blocks = std::min<uint32_t>((groups + 1) / 2, res16);
     hipLaunchKernelGGL(k_open_fold_small<16>, dim3(blocks), dim3(128), 0, s, a);
   } else if (files_per_wave == 2) {
-    const uint32_t blocks = std::min<uint32_t>((groups + 3) / 4, 256u * 4u);
+    const uint32_t blocks = std::min<uint32_t>((groups + 3) / 4, res32);
     hipLaunchKernelGGL(k_open_fold_small<32>, dim3(blocks), dim3(256), 0, s, a);
   } else {
-    const uint32_t blocks = std::min<uint32_t>((groups + 3) / 4, 256u * 8u);
+    const uint32_t blocks = std::min<uint32_t>((groups + 3) / 4, res64);
     hipLaunchKernelGGL(k_open_fold_small<64>, dim3(blocks), dim3(256), 0, s, a);
   }
   return hipGetLastError();

@@ -77,7 +77,7 @@ struct ce_ctx {
   std::recursive_mutex mu;
   std::string last_error;
   // batch scratch (device)
-  ce::DevBuf params, status, counters, extra, multi, partials, out, apply, refold, miss,
+  ce::DevBuf params, status, counters, extra, multi, partials, large, out, apply, refold, miss,
       supported, blob, offs, nonces, out_offs, outer_ver, batch_counters;
   ce::HostBuf h_counters, h_apply, h_stage, h_stage2;
   // kernel timing (ce_ctx_set_timing)

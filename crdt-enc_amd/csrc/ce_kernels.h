@@ -41,11 +41,13 @@ struct SegScratch {
   uint32_t* counters;     // [0] extra segments, [1] multi-segment files, [2] auth failures,
                           // [3] decode failures, [4] misses, [5] first failing index (min),
                           // [6] partial slots, [7] host-parse envelopes, [8] setup failures,
-                          // [12] gate: batch not in load_ops shape, [13] gate: first gap
+                          // [9] large files, [12] gate: batch not in load_ops shape,
+                          // [13] gate: first gap
   uint2* extra_list;      // (file, seg) for segments j >= 1
   uint32_t extra_cap;
   uint32_t* multi_files;  // files with nseg > 1
   uint32_t* partials;     // 5 limbs per segment: [file-major] base = extra index
+  uint32_t* large_list;   // files with more than one page (counters[9] entries)
 };
 
 // file-level open: outer version check (when outer), envelope parse, key schedule.
@@ -83,7 +85,11 @@ struct DecodeArgs {
   uint32_t miss_cap;
   uint8_t* refold;              // per file: had a miss
   const uint8_t* only;          // null, or per-file: process only files with only[i] != 0
-  int large_only;               // with only == null: skip files the fused kernel handles
+  int large_only;               // skip files the fused kernel handles (iterate large_list)
+  int ablate;                   // diagnostics only (CE_ABLATE): 1 no decode, 2 no Poly1305,
+                                // 4 no ChaCha20, 8 no ciphertext loads -- results invalid
+  unsigned long long* prof;     // diagnostics only (CE_PROF): per-wave phase cycles, 8 per wave
+  const uint32_t* large_list;
   const uint8_t* blob;          // fused kernel: input files (ciphertext at FileParams.in_off)
 };
 hipError_t launch_decode_dots(hipStream_t s, const DecodeArgs& a, uint32_t grid_waves);

@@ -90,6 +90,7 @@ __global__ __launch_bounds__(256) void k_open_setup(const uint8_t* __restrict__ 
     for (int i = 0; i < 4; i++) P.tag[i] = ld_le32(t + 4 * i);
     key_schedule(key, enc + e.nonce_off, P);
     reserve_segments(P, f, sc);
+    if (P.len > kSmallMax) sc.large_list[atomicAdd(&sc.counters[9], 1u)] = f;
   }
   params[f] = P;
   status[f] = st;
@@ -148,13 +149,15 @@ __global__ __launch_bounds__(256) void k_segments(const uint8_t* __restrict__ in
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wib = threadIdx.x >> 6;
   uint8_t* ks = lds + wib * 64 * kKsStride;
-  const uint32_t total = n + *((volatile uint32_t*)&sc.counters[0]);
+  // skip_small: the first-segment work comes from the large-file list built by the setup
+  const uint32_t nfirst = skip_small ? *((volatile uint32_t*)&sc.counters[9]) : n;
+  const uint32_t total = nfirst + *((volatile uint32_t*)&sc.counters[0]);
   const uint32_t stride = gridDim.x * kWavesPerBlock;
 
   for (uint32_t w = bcast(blockIdx.x * kWavesPerBlock + wib); w < total; w += stride) {
     uint32_t f, j;
-    if (w < n) { f = w; j = 0; }
-    else { const uint2 e = sc.extra_list[w - n]; f = bcast(e.x); j = bcast(e.y); }
+    if (w < nfirst) { f = skip_small ? bcast(sc.large_list[w]) : w; j = 0; }
+    else { const uint2 e = sc.extra_list[w - nfirst]; f = bcast(e.x); j = bcast(e.y); }
     const FileParams* Pp = params + f;
     if (Pp->status != CE_OK) continue;  // setup status (never rewritten: read-only here)
     const uint32_t len = Pp->len;
@@ -391,7 +394,10 @@ __device__ __forceinline__ void fold_flush(const DecodeArgs& a, FoldState& fs) {
 __global__ __launch_bounds__(256) void k_decode_dots(DecodeArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t stride = gridDim.x * kWavesPerBlock;
-  for (uint32_t f = bcast(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)); f < a.n; f += stride) {
+  // large_only: iterate the large-file list of the setup kernel (counters[9])
+  const uint32_t nwork = (a.large_only && !a.only) ? *((volatile uint32_t*)&a.counters[9]) : a.n;
+  for (uint32_t w = bcast(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)); w < nwork; w += stride) {
+    const uint32_t f = (a.large_only && !a.only) ? bcast(a.large_list[w]) : w;
     const FileParams* Pp = a.params + f;
     if ((a.only && !a.only[f]) || (a.large_only && Pp->len <= kSmallMax)) continue;
     if (a.status[f] != CE_OK) continue;
