@@ -29,6 +29,7 @@ import torch.distributed as dist
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "crdt-enc_amd"))
 import crdtenc  # noqa: E402
+import shard  # noqa: E402
 
 METRIC = ("op files compacted/sec + AEAD-open GB/s, 1M×4KiB ops/4096 actors, 1–8 GPUs")
 APP = bytes.fromhex("aadfd5a66e194b24a8024fa27c72f20c")      # examples/test/src/main.rs:7
@@ -131,8 +132,9 @@ def main():
     ctx.set_stream(stream.cuda_stream)
 
     actors_all = actors_table()
-    per = N_ACTORS // world
-    actors_local = actors_all[rank * per:(rank + 1) * per]
+    lo, hi = shard.actor_range(N_ACTORS, world, rank)
+    per = hi - lo
+    actors_local = actors_all[lo:hi]
     versions = args.versions * world                    # weak scaling: 1M files per GPU
     key = bytes(np.random.default_rng(7).integers(0, 256, 32, dtype=np.uint8))
 
@@ -163,8 +165,7 @@ def main():
             raise crdtenc.CeError(rc, ctx.last_error())
         if world > 1:
             core.export_dense(st_t.data_ptr(), nov_t.data_ptr())
-            dist.all_reduce(st_t, op=dist.ReduceOp.MAX)
-            dist.all_reduce(nov_t, op=dist.ReduceOp.MAX)
+            shard.merge_dense(st_t, nov_t)     # all_reduce(MAX) over u64
             core.import_dense(st_t.data_ptr(), nov_t.data_ptr())
         if rank == 0:
             f, name = core.compact_to_buffer()

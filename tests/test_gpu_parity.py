@@ -433,3 +433,45 @@ def test_device_metadata_api(ctx, oracle):
     oc = oracle.Core(oracle.STATE_VCLOCK)
     assert oc.read_remote_ops(key, [APP], files, [actors[i] for i in fa], vers)[0] == 0
     assert core.state_bytes() == oc.serialize()
+
+
+def test_dense_exchange_two_shards(ctx, oracle):
+    """The multi-GPU exchange on one GPU: two cores fold disjoint actor shards (stress dots with
+    u64 counters >= 2^63 across shards), export_dense, u64-max combine, import_dense -> the
+    single-fold state (shard.py; bench.py runs the same over RCCL)."""
+    torch = pytest.importorskip("torch")
+    import shard
+    key = os.urandom(32)
+    files, actors, fa, vers = make_ops_batch(ctx, key, 10, 4, 17, seed=21, stress=True)
+    oc = oracle.Core()
+    assert oc.read_remote_ops(key, [APP], files, [actors[i] for i in fa], vers)[0] == 0
+    cores, dense = [], []
+    for r in range(2):
+        lo, hi = shard.actor_range(len(actors), 2, r)
+        sel = [i for i in range(len(files)) if lo <= fa[i] < hi]
+        c = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+        c.set_latest_key(key)
+        c.register_actors(actors)
+        rc, _ = c.ingest_ops([files[i] for i in sel], actors[lo:hi], [fa[i] - lo for i in sel],
+                             [vers[i] for i in sel])
+        assert rc == 0
+        cap = c.dense_capacity()
+        st = torch.zeros(cap, dtype=torch.int64, device="cuda")
+        nv = torch.zeros(cap, dtype=torch.int64, device="cuda")
+        c.export_dense(st.data_ptr(), nv.data_ptr())
+        cores.append(c)
+        dense.append((st, nv))
+    assert cores[0].dense_capacity() == cores[1].dense_capacity()
+    # device merge through import_dense
+    cores[0].import_dense(dense[1][0].data_ptr(), dense[1][1].data_ptr())
+    assert cores[0].state_bytes() == oc.serialize()
+    # the collective's form: u64 max on int64 views, imported into an empty core
+    st, nv = dense[0][0].clone(), dense[0][1].clone()
+    shard.max_u64_(st, dense[1][0])
+    shard.max_u64_(nv, dense[1][1])
+    torch.cuda.synchronize()
+    fresh = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+    fresh.set_latest_key(key)
+    fresh.register_actors(actors)
+    fresh.import_dense(st.data_ptr(), nv.data_ptr())
+    assert fresh.state_bytes() == oc.serialize()

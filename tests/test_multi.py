@@ -1,0 +1,141 @@
+"""N>1 path on CPU: world_size-2 gloo ranks, files sharded by writer actor (shard.actor_range),
+partial StateWrapper<GCounter|VClock> folded per rank, exchanged once with
+shard.merge_dense (all_reduce MAX over u64 with the sign flip), and the merged state must
+serialize to the bytes of a single-process fold over all files (crdt-enc/src/lib.rs:471-547,
+739-743).  The per-rank fold here is the oracle (no GPU in this container); on the GPU box the
+same exchange runs over Core.export_dense / import_dense (test_gpu_parity)."""
+import os
+import random
+import socket
+import sys
+
+import msgpack
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(REPO, "crdt-enc_amd"), REPO):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import shard  # noqa: E402
+
+APP = bytes.fromhex("aadfd5a66e194b24a8024fa27c72f20c")
+CORE = bytes.fromhex("e834d789101b463498239de990a9051f")
+
+
+def _workload(seed=5, n_actors=6, versions=5):
+    import oracle
+    rng = random.Random(seed)
+    key = rng.randbytes(32)
+    actors = sorted(rng.randbytes(16) for _ in range(n_actors))
+    files, fa, fv = [], [], []
+    for a in range(n_actors):
+        for v in range(versions):
+            dots = []
+            for _ in range(rng.randint(1, 12)):
+                big = rng.random() < 0.15
+                ctr = rng.getrandbits(64) | (1 << 63) if big else rng.getrandbits(rng.choice([5, 14, 30]))
+                dots.append({"actor": actors[a] if rng.random() < 0.7 else rng.choice(actors),
+                             "counter": max(ctr, 1)})
+            clear = APP + msgpack.packb(dots, use_bin_type=True)
+            st, enc = oracle.cryptor_encrypt(key, rng.randbytes(24), clear)
+            assert st == 0
+            files.append(CORE + enc)
+            fa.append(a)
+            fv.append(v)
+    return key, actors, files, fa, fv
+
+
+def _fold(kind, key, actors, files, fa, fv):
+    import oracle
+    oc = oracle.Core(kind)
+    rc, _ = oc.read_remote_ops(key, [APP], files, [actors[i] for i in fa], fv)
+    assert rc == 0
+    return oc.serialize()
+
+
+def _dense(kind, ser, actors):
+    import oracle
+    d = msgpack.unpackb(ser, raw=True, strict_map_key=False)
+    nov = d[b"next_op_versions"][b"dots"]
+    st = d[b"state"][b"inner"][b"dots"] if kind == oracle.STATE_GCOUNTER else d[b"state"][b"dots"]
+    idx = {a: i for i, a in enumerate(actors)}
+    s = np.zeros(len(actors), dtype=np.uint64)
+    n = np.zeros(len(actors), dtype=np.uint64)
+    for a, c in st.items():
+        s[idx[a]] = c
+    for a, c in nov.items():
+        n[idx[a]] = c
+    return torch.from_numpy(s.view(np.int64).copy()), torch.from_numpy(n.view(np.int64).copy())
+
+
+def _serialize_dense(kind, actors, s, n):
+    import oracle
+    su, nu = s.numpy().view(np.uint64), n.numpy().view(np.uint64)
+    nov = {a: int(nu[i]) for i, a in enumerate(actors) if nu[i]}
+    st = {a: int(su[i]) for i, a in enumerate(actors) if su[i]}
+    state = {"inner": {"dots": st}} if kind == oracle.STATE_GCOUNTER else {"dots": st}
+    return msgpack.packb({"next_op_versions": {"dots": nov}, "state": state}, use_bin_type=True)
+
+
+def _rank_main(rank, world, port, kind, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        key, actors, files, fa, fv = _workload()
+        lo, hi = shard.actor_range(len(actors), world, rank)
+        sel = [i for i in range(len(files)) if lo <= fa[i] < hi]
+        ser = _fold(kind, key, actors, [files[i] for i in sel], [fa[i] for i in sel], [fv[i] for i in sel])
+        s, n = _dense(kind, ser, actors)
+        shard.merge_dense(s, n)
+        if rank == 0:
+            with open(out_path, "wb") as f:
+                f.write(_serialize_dense(kind, actors, s, n))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_actor_range_partitions():
+    for n in (1, 5, 4096):
+        for w in (1, 2, 3, 8):
+            ranges = [shard.actor_range(n, w, r) for r in range(w)]
+            assert ranges[0][0] == 0 and ranges[-1][1] == n
+            assert all(ranges[i][1] == ranges[i + 1][0] for i in range(w - 1))
+            for a in range(n):
+                r = shard.file_rank(a, n, w)
+                assert ranges[r][0] <= a < ranges[r][1]
+
+
+def test_merge_dense_is_u64_max():
+    # single-rank gloo group: the flip must leave values intact and order u64 correctly
+    port = _free_port()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        v = np.array([0, 1, 2**63 - 1, 2**63, 2**64 - 1], dtype=np.uint64)
+        t = torch.from_numpy(v.view(np.int64).copy())
+        shard.merge_dense(t)
+        assert (t.numpy().view(np.uint64) == v).all()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", [0, 1], ids=["vclock", "gcounter"])
+def test_two_rank_exchange_equals_single_fold(kind, tmp_path):
+    key, actors, files, fa, fv = _workload()
+    want = _fold(kind, key, actors, files, fa, fv)
+    out = str(tmp_path / "merged.bin")
+    mp.spawn(_rank_main, args=(2, _free_port(), kind, out), nprocs=2, join=True)
+    with open(out, "rb") as f:
+        got = f.read()
+    assert got == want
