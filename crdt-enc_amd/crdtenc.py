@@ -12,7 +12,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcrdtenc.so")
+# CRDTENC_LIB selects another in-tree build (e.g. libcrdtenc_prof.so, the diagnostics build)
+LIB_PATH = os.environ.get("CRDTENC_LIB") or os.path.join(HERE, "libcrdtenc.so")
 
 OK = 0
 STATUS_NAMES = {

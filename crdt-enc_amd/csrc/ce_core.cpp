@@ -631,9 +631,13 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
   da.mask = c->cap - 1;
   da.batch = c->d_batch.as<unsigned long long>();
   da.large_list = ctx->large.as<uint32_t>();
+#if CE_FUSED_DIAG  // diagnostics build (make prof -> libcrdtenc_prof.so)
   if (const char* ab = getenv("CE_ABLATE")) da.ablate = atoi(ab);
-  static DevBuf& prof_buf = *new DevBuf;  // CE_PROF diagnostics (never freed): per-wave phase cycles
   const bool prof = getenv("CE_PROF") != nullptr;
+#else
+  const bool prof = false;
+#endif
+  static DevBuf& prof_buf = *new DevBuf;  // CE_PROF diagnostics (never freed): per-wave phase cycles
   if (prof) {
     if ((e = prof_buf.reserve(8ull * 8 * 65536)) || (e = hipMemsetAsync(prof_buf.p, 0, 8ull * 8 * 65536, ctx->stream)))
       return ctx->hip_fail(e, "prof");

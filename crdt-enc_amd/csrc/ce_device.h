@@ -228,26 +228,29 @@ __device__ __forceinline__ uint32_t win_word(const uint32_t (&w)[12], int b) {
 }
 
 // canonical rmp-serde Dot: 82 a5"actor" c4 10 <16> a7"counter" <uint>: length from the marker
+// (positive fixint 34; cc/cd/ce/cf = 34 + 1/2/4/8; anything else 0).  Branch-free.
 __device__ __forceinline__ uint32_t dot_len_of_marker(uint32_t mk) {
-  return mk <= 0x7f ? 34 : mk == 0xcc ? 35 : mk == 0xcd ? 36 : mk == 0xce ? 38 : mk == 0xcf ? 42 : 0;
+  const uint32_t t = mk - 0xccu;
+  return mk < 0x80u ? 34u : (t < 4u ? 34u + (1u << t) : 0u);
 }
 
-// check one canonical Dot of length L in the window w (bytes cand..cand+47); extract fields
+// check one canonical Dot of length L in the window w (bytes cand..cand+47); extract fields.
+// Branch-free: every test is evaluated; the counter is one shift of the big-endian 8 bytes.
 __device__ __forceinline__ bool canon_dot(const uint32_t (&w)[12], uint32_t L, uint32_t& k0,
                                           uint32_t& k1, uint32_t& k2, uint32_t& k3,
                                           unsigned long long& ctr) {
   const uint32_t mk = (w[8] >> 8) & 0xff;
   const uint32_t Lc = dot_len_of_marker(mk);
-  const bool ok = w[0] == 0x6361a582u && w[1] == 0xc4726f74u && (w[2] & 0xffu) == 0x10u &&
-                  win_word(w, 25) == 0x756f63a7u && win_word(w, 29) == 0x7265746eu && Lc == L;
+  const uint32_t ok = (uint32_t)(w[0] == 0x6361a582u) & (uint32_t)(w[1] == 0xc4726f74u) &
+                      (uint32_t)((w[2] & 0xffu) == 0x10u) &
+                      (uint32_t)(win_word(w, 25) == 0x756f63a7u) &
+                      (uint32_t)(win_word(w, 29) == 0x7265746eu) & (uint32_t)(Lc == L);
   k0 = win_word(w, 9); k1 = win_word(w, 13); k2 = win_word(w, 17); k3 = win_word(w, 21);
-  const uint32_t hi = bswap32(win_word(w, 34)), lo = bswap32(win_word(w, 38));
-  ctr = L == 34 ? mk
-      : L == 35 ? (hi >> 24)
-      : L == 36 ? (hi >> 16)
-      : L == 38 ? hi
-      : (((unsigned long long)hi << 32) | lo);
-  return ok;
+  const unsigned long long be =
+      ((unsigned long long)bswap32(win_word(w, 34)) << 32) | bswap32(win_word(w, 38));
+  const uint32_t t = (mk - 0xccu) & 3u;   // cc..cf -> 1, 2, 4, 8 bytes
+  ctr = mk < 0x80u ? (unsigned long long)mk : be >> (64u - (8u << t));
+  return ok != 0;
 }
 
 }  // namespace ce

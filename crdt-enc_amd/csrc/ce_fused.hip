@@ -133,6 +133,7 @@ void k_open_fold_small(DecodeArgs a) {
   const uint32_t stride = gridDim.x * C::WPB;
   // CE_PROF: s_memtime at phase boundaries, summed per wave (params+loads, ChaCha20,
   // XOR+Horner, tree+tag, decode prelude, decode rounds+flush, iterations)
+#if CE_FUSED_DIAG
   unsigned long long pc[7] = {0, 0, 0, 0, 0, 0, 0};
   unsigned long long tp = a.prof ? __builtin_amdgcn_s_memtime() : 0;
 #define CE_PHASE(i)                                            \
@@ -141,6 +142,9 @@ void k_open_fold_small(DecodeArgs a) {
     pc[i] += tn - tp;                                          \
     tp = tn;                                                   \
   }
+#else
+#define CE_PHASE(i)
+#endif
 
   uint32_t g = bcast(blockIdx.x * C::WPB + wib);
   FilePre nx = load_pre(a, g * F + grp);
@@ -155,7 +159,9 @@ void k_open_fold_small(DecodeArgs a) {
     const bool act = cur.ok && cur.len <= kSmallMax;
     const uint32_t nblk_ct = (len + 15) >> 4;
     const uint32_t nb = nblk_ct + 1;
-    const uint8_t* src = a.blob + (act ? (((uint64_t)cur.in_hi << 32) | cur.in_off) : 0);
+    // inactive lanes read 16 B of the (always allocated) params array instead of the blob
+    const uint8_t* src = act ? a.blob + (((uint64_t)cur.in_hi << 32) | cur.in_off)
+                             : reinterpret_cast<const uint8_t*>(a.params);
     const FileParams* Pp = a.params + (act ? f : 0);
 
     // 1) ciphertext pieces -> registers (issued first: latency hides under the ChaCha20)
@@ -164,11 +170,13 @@ void k_open_fold_small(DecodeArgs a) {
     for (int j = 0; j < PPL; j++) {
       const uint32_t blk = sub + LPF * j;
       const uint32_t boff = blk * 16;
-      if (a.ablate & 8) ct[j] = make_uint4(boff, len, sub, 0);
       // the 16-byte tag follows the ciphertext, so a 16-byte load at any boff < len stays
-      // inside the file; bytes past len are zeroed below (Poly1305 pad16, plaintext tail)
-      else if (act && boff < len) ct[j] = *reinterpret_cast<const uint4*>(src + boff);
-      else ct[j] = make_uint4(0, 0, 0, 0);
+      // inside the file; bytes past len are zeroed below (Poly1305 pad16, plaintext tail).
+      // Pieces past the end load the file's first piece (in bounds) and are never used.
+      ct[j] = *reinterpret_cast<const uint4*>(src + (boff < len ? boff : 0u));
+#if CE_FUSED_DIAG
+      if (a.ablate & 8) ct[j] = make_uint4(boff, len, sub, 0);
+#endif
     }
     __builtin_amdgcn_wave_barrier();
     CE_PHASE(0)
@@ -179,10 +187,13 @@ void k_open_fold_small(DecodeArgs a) {
       const uint32_t b = sub + LPF * k;
       if (act && b * 64 < len) {
         uint32_t kb[16];
+#if CE_FUSED_DIAG
         if (a.ablate & 4) {
 #pragma unroll
           for (int i = 0; i < 16; i++) kb[i] = cur.key[i & 7] + b;
-        } else chacha_block(cur.key, 1u + b, 0u, cur.n2a, cur.n2b, kb);
+        } else
+#endif
+          chacha_block(cur.key, 1u + b, 0u, cur.n2a, cur.n2b, kb);
         uint4* kd = reinterpret_cast<uint4*>(fl + b * kKsStride);
         kd[0] = make_uint4(kb[0], kb[1], kb[2], kb[3]);
         kd[1] = make_uint4(kb[4], kb[5], kb[6], kb[7]);
@@ -223,8 +234,11 @@ void k_open_fold_small(DecodeArgs a) {
         uint4 y = make_uint4(x.x ^ (k4.x & kw_mask[0]), x.y ^ (k4.y & kw_mask[1]),
                              x.z ^ (k4.z & kw_mask[2]), x.w ^ (k4.w & kw_mask[3]));
         *reinterpret_cast<uint4*>(fl + boff) = y;
+#if CE_FUSED_DIAG
         if (a.ablate & 2) acc.v[j % 5] += x.x ^ x.w;
-        else acc = add5(mulmod(acc, R), block_limbs(x.x, x.y, x.z, x.w));
+        else
+#endif
+          acc = add5(mulmod(acc, R), block_limbs(x.x, x.y, x.z, x.w));
       } else if (act && blk == nblk_ct) {
         acc = add5(mulmod(acc, R), block_limbs(0u, 0u, len, 0u));  // le64(0) || le64(len)
       }
@@ -277,7 +291,9 @@ void k_open_fold_small(DecodeArgs a) {
 
     // 5) decode from LDS
     int32_t st = CE_OK;
+#if CE_FUSED_DIAG
     if (a.ablate) ok = !(a.ablate & 1);
+#endif
     bool live = act && ok;
     if (live) {
       if (len < 16) st = CE_ERR_PT_LEN;
@@ -329,7 +345,8 @@ void k_open_fold_small(DecodeArgs a) {
         for (int i = 0; i < 12; i++) w[i] = __builtin_amdgcn_alignbyte(dd[i + 1], dd[i], sh);
         Lme = dot_len_of_marker((w[8] >> 8) & 0xff);
         const uint32_t L = sub == 0 ? Lme : Ls;
-        valid = Lme != 0 && Lme == L && cand + L <= blen && canon_dot(w, L, k0, k1, k2, k3, ctr);
+        valid = ((uint32_t)canon_dot(w, L, k0, k1, k2, k3, ctr) & (uint32_t)(Lme != 0) &
+                 (uint32_t)(cand + L <= blen)) != 0;
       }
       constexpr unsigned long long GM = LPF == 64 ? ~0ull : ((1ull << LPF) - 1);
       const unsigned long long vb = grp_bits<LPF>(valid, grp);
@@ -414,14 +431,18 @@ void k_open_fold_small(DecodeArgs a) {
     }
     __builtin_amdgcn_wave_barrier();
     CE_PHASE(5)
+#if CE_FUSED_DIAG
     pc[6]++;
+#endif
   }
 #undef CE_PHASE
+#if CE_FUSED_DIAG
   if (a.prof && lane == 0) {
     unsigned long long* o = a.prof + 8ull * (blockIdx.x * C::WPB + wib);
 #pragma unroll
     for (int i = 0; i < 7; i++) o[i] = pc[i];
   }
+#endif
 }
 
 // Resident blocks per CU for a kernel, from the occupancy calculator (LDS and VGPRs both
