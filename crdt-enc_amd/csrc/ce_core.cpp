@@ -51,6 +51,12 @@ struct ce_core {
   std::vector<uint64_t> nov;  // next_op_versions by slot
   std::unordered_map<Uuid, uint32_t, UuidHash> slot_of;
   bool table_dirty = true;
+  uint64_t table_gen = 0;               // bumped whenever an actor gets a slot or slots move
+  std::vector<uint32_t> sorted_slots;   // used slots in UUID byte order (BTreeMap order)
+  uint64_t sorted_gen = ~0ull;
+  std::vector<uint8_t> last_writers;    // writer list of the previous ingest and its slots
+  std::vector<uint32_t> last_wslot;
+  uint64_t last_writers_gen = ~0ull;
   DevBuf d_table, d_state, d_batch, d_supported, d_refold2, d_tmp, d_gate, d_meta;
   int files_per_wave = 4;  // fused kernel geometry (CE_FILES_PER_WAVE overrides)
   std::set<std::string> read_states;  // lib.rs:205
@@ -294,6 +300,7 @@ uint32_t probe_slot(const std::vector<ActorSlot>& t, uint32_t mask, const Uuid& 
 }
 
 int table_init(ce_core* c, uint32_t cap) {
+  c->table_gen++;
   c->cap = cap;
   c->size = 0;
   c->h_table.assign(cap, ActorSlot{});
@@ -374,6 +381,7 @@ int insert_actor(ce_core* c, const Uuid& u, uint32_t* slot) {
   c->slot_of[u] = s;
   c->size++;
   c->table_dirty = true;
+  c->table_gen++;
   *slot = s;
   return CE_OK;
 }
@@ -414,14 +422,20 @@ int serialize_state(ce_core* c, std::vector<uint8_t>* out) {
   std::vector<uint64_t> st;
   int rc = download_state(c, &st);
   if (rc) return rc;
-  std::vector<uint32_t> slots;
-  for (uint32_t s = 0; s < c->cap; s++)
-    if (c->h_table[s].used) slots.push_back(s);
-  std::sort(slots.begin(), slots.end(),
-            [&](uint32_t a, uint32_t b) { return c->slot_actor[a] < c->slot_actor[b]; });
+  if (c->sorted_gen != c->table_gen) {
+    c->sorted_slots.clear();
+    for (uint32_t s = 0; s < c->cap; s++)
+      if (c->h_table[s].used) c->sorted_slots.push_back(s);
+    std::sort(c->sorted_slots.begin(), c->sorted_slots.end(), [&](uint32_t a, uint32_t b) {
+      return std::memcmp(c->slot_actor[a].data(), c->slot_actor[b].data(), 16) < 0;
+    });
+    c->sorted_gen = c->table_gen;
+  }
+  const std::vector<uint32_t>& slots = c->sorted_slots;
   size_t n_nov = 0, n_st = 0;
   for (uint32_t s : slots) { n_nov += c->nov[s] != 0; n_st += st[s] != 0; }
   Wr w;
+  w.b.reserve(64 + 28 * (n_nov + n_st));
   w.map(2);
   w.str("next_op_versions");
   w.map(1);
@@ -562,12 +576,22 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
   hipError_t e;
   const KeyRef key = key_of(c);
   // writer actors (the op directories) get slots first: the version gate is keyed by them
-  std::vector<uint32_t> wslot(m);
-  for (uint32_t a = 0; a < m; a++) {
-    Uuid u;
-    std::memcpy(u.data(), actors + 16ull * a, 16);
-    int rc = insert_actor(c, u, &wslot[a]);
-    if (rc) return rc;
+  // (a repeated writer list -- the same shard every step -- reuses the previous lookup)
+  std::vector<uint32_t> wslot;
+  if (c->last_writers_gen == c->table_gen && c->last_writers.size() == 16ull * m &&
+      std::memcmp(c->last_writers.data(), actors, 16ull * m) == 0) {
+    wslot = c->last_wslot;
+  } else {
+    wslot.resize(m);
+    for (uint32_t a = 0; a < m; a++) {
+      Uuid u;
+      std::memcpy(u.data(), actors + 16ull * a, 16);
+      int rc = insert_actor(c, u, &wslot[a]);
+      if (rc) return rc;
+    }
+    c->last_writers.assign(actors, actors + 16ull * m);
+    c->last_wslot = wslot;
+    c->last_writers_gen = c->table_gen;
   }
   int rc = table_upload(c);
   if (rc) return rc;

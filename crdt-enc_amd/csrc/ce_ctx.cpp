@@ -191,29 +191,25 @@ int seal_one(ce_ctx* ctx, const KeyRef& key, const uint8_t* outer_version, const
   if (nonce) std::memcpy(nb, nonce, 24);
   else os_random(nb, 24);
   hipError_t e;
-  // staging: [offs(2) | out_offs(1) | outer(16) | nonce(24)] small args, clear text, output
-  if ((e = ctx->offs.reserve(64)) != hipSuccess || (e = ctx->out_offs.reserve(64)) != hipSuccess ||
-      (e = ctx->outer_ver.reserve(64)) != hipSuccess || (e = ctx->nonces.reserve(64)) != hipSuccess ||
-      (e = ctx->blob.reserve(clear_len + 64)) != hipSuccess ||
+  // one pinned upload: clear text, then at A = align256(clear_len) the small arguments
+  // [offs(2) | out_offs(1) | nonce(24 B) | outer version(16 B)]
+  const uint64_t A = (clear_len + 255) & ~255ull;
+  if ((e = ctx->blob.reserve(A + 128)) != hipSuccess ||
       (e = ctx->out.reserve(total + 64)) != hipSuccess ||
-      (e = ctx->h_stage.reserve(std::max<uint64_t>(clear_len, total) + 256)) != hipSuccess)
+      (e = ctx->h_stage.reserve(std::max<uint64_t>(A + 128, total) + 256)) != hipSuccess)
     return ctx->hip_fail(e, "seal_one reserve");
   uint8_t* hs = ctx->h_stage.as<uint8_t>();
-  const uint64_t offs[2] = {0, clear_len};
-  const uint64_t oo[1] = {0};
+  const uint64_t args[3] = {0, clear_len, 0};
   std::memcpy(hs, clear, clear_len);
-  if ((e = hipMemcpyAsync(ctx->blob.p, hs, clear_len, hipMemcpyHostToDevice, ctx->stream)) ||
-      (e = hipMemcpyAsync(ctx->offs.p, offs, 16, hipMemcpyHostToDevice, ctx->stream)) ||
-      (e = hipMemcpyAsync(ctx->out_offs.p, oo, 8, hipMemcpyHostToDevice, ctx->stream)) ||
-      (e = hipMemcpyAsync(ctx->nonces.p, nb, 24, hipMemcpyHostToDevice, ctx->stream)))
+  std::memcpy(hs + A, args, 24);
+  std::memcpy(hs + A + 24, nb, 24);
+  if (outer_version) std::memcpy(hs + A + 48, outer_version, 16);
+  if ((e = hipMemcpyAsync(ctx->blob.p, hs, A + 64, hipMemcpyHostToDevice, ctx->stream)))
     return ctx->hip_fail(e, "seal_one upload");
-  if (outer_version &&
-      (e = hipMemcpyAsync(ctx->outer_ver.p, outer_version, 16, hipMemcpyHostToDevice, ctx->stream)))
-    return ctx->hip_fail(e, "seal_one upload");
-  int rc = device_seal(ctx, ctx->blob.as<uint8_t>(), ctx->offs.as<uint64_t>(), 1, clear_len,
-                       outer_version ? ctx->outer_ver.as<uint8_t>() : nullptr,
-                       ctx->nonces.as<uint8_t>(), ctx->out.as<uint8_t>(),
-                       ctx->out_offs.as<uint64_t>(), key);
+  uint8_t* db = ctx->blob.as<uint8_t>();
+  int rc = device_seal(ctx, db, reinterpret_cast<const uint64_t*>(db + A), 1, clear_len,
+                       outer_version ? db + A + 48 : nullptr, db + A + 24, ctx->out.as<uint8_t>(),
+                       reinterpret_cast<const uint64_t*>(db + A + 16), key);
   if (rc) return rc;
   if ((e = hipMemcpyAsync(hs, ctx->out.p, total, hipMemcpyDeviceToHost, ctx->stream)) ||
       (e = hipStreamSynchronize(ctx->stream)))

@@ -510,8 +510,12 @@ __global__ void k_gate_apply(GateArgs g) {
   if (a < g.m) {
     const uint64_t e0 = g.e0[a];
     const uint64_t vf = g.fv[g.run_first[a]];
-    ap = g.fv[i] >= e0 && vf <= e0 && i < g.flags[1];
-    if (ap) atomicMax(&g.newnov[a], (unsigned long long)(g.fv[i] + 1));
+    const uint32_t gap = g.flags[1];
+    ap = g.fv[i] >= e0 && vf <= e0 && i < gap;
+    // versions are consecutive inside a run: only the run's last applied file bumps
+    // next_op_versions (one atomic per actor instead of one per file)
+    const bool last = i + 1 == g.n || g.fa[i + 1] != a || i + 1 >= gap;
+    if (ap && last) atomicMax(&g.newnov[a], (unsigned long long)(g.fv[i] + 1));
   }
   g.apply[i] = ap ? 1 : 0;
 }

@@ -65,40 +65,41 @@ Uuid uuid_v4() {
   return u;
 }
 
-// ---- SHA3-256 (FIPS 202), lane-unrolled Keccak-f[1600] ----
-static inline uint64_t rotl64(uint64_t x, int n) { return (x << n) | (x >> ((64 - n) & 63)); }
+// ---- SHA3-256 (FIPS 202): Keccak-f[1600] with every index compile-time (fully unrolled) ----
+static inline uint64_t rotl64(uint64_t x, int n) { return n ? (x << n) | (x >> (64 - n)) : x; }
+
+namespace {
+constexpr uint64_t kRC[24] = {
+    0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808aull, 0x8000000080008000ull,
+    0x000000000000808bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
+    0x000000000000008aull, 0x0000000000000088ull, 0x0000000080008009ull, 0x000000008000000aull,
+    0x000000008000808bull, 0x800000000000008bull, 0x8000000000008089ull, 0x8000000000008003ull,
+    0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800aull, 0x800000008000000aull,
+    0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
+// rho offsets r[x][y] (lane x + 5y)
+constexpr int kRho[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43,
+                          25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
+}  // namespace
 
 static void keccakf(uint64_t s[25]) {
-  static const uint64_t RC[24] = {
-      0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808aull, 0x8000000080008000ull,
-      0x000000000000808bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
-      0x000000000000008aull, 0x0000000000000088ull, 0x0000000080008009ull, 0x000000008000000aull,
-      0x000000008000808bull, 0x800000000000008bull, 0x8000000000008089ull, 0x8000000000008003ull,
-      0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800aull, 0x800000008000000aull,
-      0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
-  static const int PI[24] = {10, 7, 11, 17, 18, 3, 5, 16, 8, 21, 24, 4,
-                             15, 23, 19, 13, 12, 2, 20, 14, 22, 9, 6, 1};
-  static const int RHO[24] = {1, 3, 6, 10, 15, 21, 28, 36, 45, 55, 2, 14,
-                              27, 41, 56, 8, 25, 43, 62, 18, 39, 61, 20, 44};
   for (int r = 0; r < 24; r++) {
-    uint64_t bc[5];
-    for (int i = 0; i < 5; i++) bc[i] = s[i] ^ s[i + 5] ^ s[i + 10] ^ s[i + 15] ^ s[i + 20];
-    for (int i = 0; i < 5; i++) {
-      const uint64_t t = bc[(i + 4) % 5] ^ rotl64(bc[(i + 1) % 5], 1);
-      for (int j = 0; j < 25; j += 5) s[j + i] ^= t;
+    uint64_t c[5], b[25];
+#pragma clang loop unroll(full)
+    for (int x = 0; x < 5; x++) c[x] = s[x] ^ s[x + 5] ^ s[x + 10] ^ s[x + 15] ^ s[x + 20];
+    // theta + rho + pi: B[y, 2x+3y] = rot(A[x, y] ^ D[x], r[x, y])
+#pragma clang loop unroll(full)
+    for (int x = 0; x < 5; x++) {
+      const uint64_t d = c[(x + 4) % 5] ^ rotl64(c[(x + 1) % 5], 1);
+#pragma clang loop unroll(full)
+      for (int y = 0; y < 5; y++) b[y + 5 * ((2 * x + 3 * y) % 5)] = rotl64(s[x + 5 * y] ^ d, kRho[x + 5 * y]);
     }
-    uint64_t t = s[1];
-    for (int i = 0; i < 24; i++) {
-      const int j = PI[i];
-      const uint64_t b = s[j];
-      s[j] = rotl64(t, RHO[i]);
-      t = b;
+    // chi + iota
+#pragma clang loop unroll(full)
+    for (int y = 0; y < 25; y += 5) {
+#pragma clang loop unroll(full)
+      for (int x = 0; x < 5; x++) s[y + x] = b[y + x] ^ (~b[y + (x + 1) % 5] & b[y + (x + 2) % 5]);
     }
-    for (int j = 0; j < 25; j += 5) {
-      for (int i = 0; i < 5; i++) bc[i] = s[j + i];
-      for (int i = 0; i < 5; i++) s[j + i] ^= (~bc[(i + 1) % 5]) & bc[(i + 2) % 5];
-    }
-    s[0] ^= RC[r];
+    s[0] ^= kRC[r];
   }
 }
 
