@@ -80,13 +80,14 @@ __device__ __forceinline__ unsigned long long grp_bits(bool p, uint32_t grp) {
   return (__ballot(p) >> (grp * LPF)) & GM;
 }
 
-// canonical Dot lengths <-> 3-bit codes (ballot transport of the next Dot's length)
+// canonical Dot lengths <-> 3-bit codes (ballot transport of the next Dot's length), branch-free:
+// L - 34 in {0, 1, 2, 4, 8} -> code 1..5 through a nibble table; anything else -> 0
 __device__ __forceinline__ uint32_t len_code(uint32_t L) {
-  return L == 34 ? 1u : L == 35 ? 2u : L == 36 ? 3u : L == 38 ? 4u : L == 42 ? 5u : 0u;
+  const uint32_t d = L - 34u;
+  return d < 16u ? (uint32_t)((0x500040321ull >> (4u * d)) & 0xfu) : 0u;
 }
-__device__ __forceinline__ uint32_t code_len(uint32_t c) {
-  return c == 1 ? 34u : c == 2 ? 35u : c == 3 ? 36u : c == 4 ? 38u : 42u;
-}
+// code 1..5 -> 34 + {0, 1, 2, 4, 8}
+__device__ __forceinline__ uint32_t code_len(uint32_t c) { return 34u + ((1u << c) >> 2); }
 
 // per-iteration inputs of one file, prefetched one grid-stride iteration ahead
 struct FilePre {
@@ -322,6 +323,66 @@ void k_open_fold_small(DecodeArgs a) {
     // pending max per lane: flushed with atomicMax when the lane's actor changes
     uint32_t pslot = 0xffffffffu;
     unsigned long long pbest = 0;
+    auto fold_dot = [&](uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3, unsigned long long ctr) {
+      uint32_t slot;
+      // per-lane cache of the last resolved actor: a file's dots are usually its writer's
+      if (k0 == ck0 && k1 == ck1 && k2 == ck2 && k3 == ck3 && cslot != 0xffffffffu) slot = cslot;
+      else {
+        slot = lookup_slot(a.table, a.mask, k0, k1, k2, k3);
+        if (slot != 0xffffffffu) { ck0 = k0; ck1 = k1; ck2 = k2; ck3 = k3; cslot = slot; }
+      }
+      if (slot == 0xffffffffu) {
+        const uint32_t mi = atomicAdd(&a.counters[4], 1u);
+        if (mi < a.miss_cap) a.miss_list[mi] = make_uint4(k0, k1, k2, k3);
+        a.refold[f] = 1;
+      } else if (slot == pslot) {
+        pbest = ctr > pbest ? ctr : pbest;
+      } else {
+        if (pslot != 0xffffffffu) atomicMax(&a.batch[pslot], pbest);
+        pslot = slot;
+        pbest = ctr;
+      }
+    };
+    // fast path: every Dot canonical with the first Dot's length L0, so Dot i sits at
+    // pos + i * L0 and a round needs one validity ballot.  It stops at the first Dot that is
+    // not (nothing past it is folded); the sequential loop below takes over from there.
+    {
+      uint32_t L0 = 0;
+      if (live && st == CE_OK && remaining > 0 && pos + 34 <= blen) L0 = dot_len_of_marker(body[pos + 33]);
+      uint32_t done = 0;
+      bool fast = L0 != 0;
+      for (;;) {
+        const bool fb = fast && done < remaining;
+        if (!__any(fb)) break;
+        const uint32_t i = done + sub;
+        const uint32_t cand = pos + i * L0;
+        const bool need = fb && i < remaining;
+        bool valid = false;
+        uint32_t k0 = 0, k1 = 0, k2 = 0, k3 = 0;
+        unsigned long long ctr = 0;
+        if (need && cand + L0 <= blen) {
+          const uint32_t* d = reinterpret_cast<const uint32_t*>(body) + (cand >> 2);
+          const uint32_t sh = cand & 3;
+          uint32_t dd[13];
+#pragma unroll
+          for (int q = 0; q < 13; q++) dd[q] = d[q];
+          uint32_t w[12];
+#pragma unroll
+          for (int q = 0; q < 12; q++) w[q] = __builtin_amdgcn_alignbyte(dd[q + 1], dd[q], sh);
+          valid = canon_dot(w, L0, k0, k1, k2, k3, ctr);
+        }
+        const unsigned long long bad = grp_bits<LPF>(need && !valid, grp);
+        const uint32_t kk = bad ? (uint32_t)__builtin_ctzll(bad) : (uint32_t)LPF;  // valid prefix
+        if (do_fold && need && sub < kk) fold_dot(k0, k1, k2, k3, ctr);
+        if (fb) {
+          const uint32_t adv = bad ? kk : min((uint32_t)LPF, (uint32_t)(remaining - done));
+          done += adv;
+          if (bad) fast = false;
+        }
+      }
+      pos += done * L0;
+      remaining -= done;
+    }
     for (;;) {
       const bool busy = live && st == CE_OK && remaining > 0;
       if (!__any(busy)) break;
@@ -386,26 +447,7 @@ void k_open_fold_small(DecodeArgs a) {
           else { pos = npos; remaining -= 1; }
         }
       }
-      if (fold_me) {
-        uint32_t slot;
-        // per-lane cache of the last resolved actor: a file's dots are usually its writer's
-        if (k0 == ck0 && k1 == ck1 && k2 == ck2 && k3 == ck3 && cslot != 0xffffffffu) slot = cslot;
-        else {
-          slot = lookup_slot(a.table, a.mask, k0, k1, k2, k3);
-          if (slot != 0xffffffffu) { ck0 = k0; ck1 = k1; ck2 = k2; ck3 = k3; cslot = slot; }
-        }
-        if (slot == 0xffffffffu) {
-          const uint32_t mi = atomicAdd(&a.counters[4], 1u);
-          if (mi < a.miss_cap) a.miss_list[mi] = make_uint4(k0, k1, k2, k3);
-          a.refold[f] = 1;
-        } else if (slot == pslot) {
-          pbest = ctr > pbest ? ctr : pbest;
-        } else {
-          if (pslot != 0xffffffffu) atomicMax(&a.batch[pslot], pbest);
-          pslot = slot;
-          pbest = ctr;
-        }
-      }
+      if (fold_me) fold_dot(k0, k1, k2, k3, ctr);
       if (busy && k > 0) {
         pos += m0 ? k * Lold : Ls;  // !m0: k == 1 and Ls == lane 0's Dot length
         remaining -= k;
