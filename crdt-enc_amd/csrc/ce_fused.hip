@@ -98,8 +98,10 @@ struct FilePre {
   uint32_t in_hi;
   uint32_t key[8];
   uint32_t n2a, n2b;
+  uint32_t R[5];    // r^LPF (Horner step)
 };
 
+template <int LOG>
 __device__ __forceinline__ FilePre load_pre(const DecodeArgs& a, uint32_t f) {
   FilePre p;
   const bool in = f < a.n;
@@ -116,6 +118,8 @@ __device__ __forceinline__ FilePre load_pre(const DecodeArgs& a, uint32_t f) {
   for (int i = 0; i < 8; i++) p.key[i] = Pp->subkey[i];
   p.n2a = Pp->n2[0];
   p.n2b = Pp->n2[1];
+#pragma unroll
+  for (int i = 0; i < 5; i++) p.R[i] = Pp->rpow[LOG][i];
   return p;
 }
 
@@ -148,7 +152,7 @@ void k_open_fold_small(DecodeArgs a) {
 #endif
 
   uint32_t g = bcast(blockIdx.x * C::WPB + wib);
-  FilePre nx = load_pre(a, g * F + grp);
+  FilePre nx = load_pre<C::LOG>(a, g * F + grp);
   // decode state carried across files: speculated Dot length, per-lane actor cache
   uint32_t Ls = 38;
   uint32_t ck0 = 0, ck1 = 0, ck2 = 0, ck3 = 0, cslot = 0xffffffffu;
@@ -205,10 +209,22 @@ void k_open_fold_small(DecodeArgs a) {
     __builtin_amdgcn_wave_barrier();
     CE_PHASE(1)
 
+    // tree powers r^(2^k), k < LOG, and s || expected tag: 16-byte loads issued now, used
+    // after the Horner pass (their latency hides under it).  Inactive lanes read params[0].
+    constexpr int NRW = 5 * C::LOG;
+    uint32_t rp[(NRW + 3) / 4 * 4];
+#pragma unroll
+    for (int q = 0; q < (NRW + 3) / 4; q++) {
+      const uint4 v = *reinterpret_cast<const uint4*>(&Pp->rpow[0][0] + 4 * q);
+      rp[4 * q] = v.x; rp[4 * q + 1] = v.y; rp[4 * q + 2] = v.z; rp[4 * q + 3] = v.w;
+    }
+    const uint4 sv4 = *reinterpret_cast<const uint4*>(Pp->s);
+    const uint4 tg4 = *reinterpret_cast<const uint4*>(Pp->tag);
+
     // 3) XOR, plaintext into LDS (over consumed keystream), strided Horner in r^LPF
     L5 R;
 #pragma unroll
-    for (int i = 0; i < 5; i++) R.v[i] = act ? Pp->rpow[C::LOG][i] : 0u;
+    for (int i = 0; i < 5; i++) R.v[i] = cur.R[i];
     L5 acc = {{0, 0, 0, 0, 0}};
 #pragma unroll
     for (int j = 0; j < C::ROWS; j++) {
@@ -260,7 +276,7 @@ void k_open_fold_small(DecodeArgs a) {
     for (int k = 0; k < C::LOG; k++) {
       L5 rk;
 #pragma unroll
-      for (int i = 0; i < 5; i++) rk.v[i] = act ? Pp->rpow[k][i] : 0u;
+      for (int i = 0; i < 5; i++) rk.v[i] = rp[5 * k + i];
       L5 o;
 #pragma unroll
       for (int i = 0; i < 5; i++)
@@ -269,15 +285,14 @@ void k_open_fold_small(DecodeArgs a) {
     }
     L5 r1;
 #pragma unroll
-    for (int i = 0; i < 5; i++) r1.v[i] = act ? Pp->rpow[0][i] : 0u;
+    for (int i = 0; i < 5; i++) r1.v[i] = rp[i];
     const L5 tot = mulmod(v, r1);
     bool tag_ok = false;
     if (act && sub == 0) {
-      const uint32_t sv[4] = {Pp->s[0], Pp->s[1], Pp->s[2], Pp->s[3]};
+      const uint32_t sv[4] = {sv4.x, sv4.y, sv4.z, sv4.w};
       uint32_t tag[4];
       poly_tag(tot, sv, tag);
-      tag_ok = ((tag[0] ^ Pp->tag[0]) | (tag[1] ^ Pp->tag[1]) | (tag[2] ^ Pp->tag[2]) |
-                (tag[3] ^ Pp->tag[3])) == 0;
+      tag_ok = ((tag[0] ^ tg4.x) | (tag[1] ^ tg4.y) | (tag[2] ^ tg4.z) | (tag[3] ^ tg4.w)) == 0;
       if (!tag_ok) {
         a.status[f] = CE_ERR_AUTH;
         atomicAdd(&a.counters[2], 1u);
@@ -287,7 +302,7 @@ void k_open_fold_small(DecodeArgs a) {
     bool ok = grp_bits<LPF>(tag_ok, grp) != 0;
 
     // next iteration's parameters: their latency hides under the decode
-    nx = load_pre(a, (g + stride) * F + grp);
+    nx = load_pre<C::LOG>(a, (g + stride) * F + grp);
     CE_PHASE(3)
 
     // 5) decode from LDS
