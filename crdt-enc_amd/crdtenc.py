@@ -22,7 +22,7 @@ STATUS_NAMES = {
     10: "PT_LEN", 11: "PT_VERSION", 12: "DECODE", 13: "OP_VERSION", 64: "INVALID_ARG",
     65: "DEVICE", 66: "NO_KEY", 67: "IO", 68: "NO_LOCAL_META",
 }
-STATE_VCLOCK, STATE_GCOUNTER = 0, 1
+STATE_VCLOCK, STATE_GCOUNTER, STATE_ORSWOT, STATE_MVREG = 0, 1, 2, 3
 OPEN_CREATE, COMPACT_INGEST_FORMAT = 1, 2
 
 CORE_VERSION = bytes.fromhex("e834d789101b463498239de990a9051f")   # crdt-enc/src/lib.rs:26
@@ -44,7 +44,7 @@ EXPORTS = [
     "ce_core_register_actors", "ce_core_dense_capacity", "ce_core_export_dense",
     "ce_core_import_dense", "ce_vbuf_init", "ce_vbuf_remaining", "ce_vbuf_chunk",
     "ce_vbuf_advance", "ce_vbuf_chunks_vectored", "ce_ctx_set_timing", "ce_ctx_timing_read",
-    "ce_ctx_timing_reset", "ce_core_reset",
+    "ce_ctx_timing_reset", "ce_core_reset", "ce_core_merge_state",
 ]
 
 
@@ -330,7 +330,8 @@ class Storage:
 
 
 class Core:
-    """Core<S> for S in {VClock<Uuid>, GCounter<Uuid>} (crdt-enc/src/lib.rs)."""
+    """Core<S> for S in {VClock<Uuid>, GCounter<Uuid>, Orswot<u64, Uuid>, MVReg<u64, Uuid>}
+    (crdt-enc/src/lib.rs)."""
 
     def __init__(self, ctx, kind=STATE_GCOUNTER, supported=(), current_data_version=None,
                  local_path=None, remote_path=None, flags=0):
@@ -434,6 +435,11 @@ class Core:
 
     def reset(self):
         self.ctx.check(lib().ce_core_reset(self.p), "reset")
+
+    def merge_state(self, state_wrapper_msgpack):
+        """read_remote_states' merge of one decrypted StateWrapper (lib.rs:447, 458-466)."""
+        return lib().ce_core_merge_state(self.p, _cbuf(state_wrapper_msgpack),
+                                         ctypes.c_size_t(len(state_wrapper_msgpack)))
 
     def register_actors(self, actors):
         self.ctx.check(lib().ce_core_register_actors(self.p, _cbuf(b"".join(actors)),

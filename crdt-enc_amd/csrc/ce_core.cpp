@@ -1,5 +1,6 @@
-// ce_core.cpp -- Core<S, Storage, Cryptor, _> (crdt-enc/src/lib.rs:188-723) for S in
-// {VClock<Uuid>, GCounter<Uuid>}, driving the GPU batch engine.
+// ce_core.cpp -- Core<S, Storage, Cryptor, _> (crdt-enc/src/lib.rs:188-723), driving the GPU
+// batch engine.  S = VClock<Uuid> / GCounter<Uuid> live here; S = Orswot<u64, Uuid> /
+// MVReg<u64, Uuid> (the dot-set kinds) dispatch to ce_dotset_host.cpp.
 //
 // State layout: a host-built open-addressing actor table (UUID -> dense slot) mirrored in HBM;
 // the CRDT state (VClock dots / GCounter.inner) is a dense u64[cap] max-register array in HBM;
@@ -10,100 +11,21 @@
 #include <functional>
 #include <set>
 
-#include "ce_internal.h"
-
-namespace ce {
-int storage_load_ops_vec(ce_storage* s, const std::vector<Uuid>& actors,
-                         const std::vector<uint64_t>& first, std::vector<uint8_t>* blob,
-                         std::vector<uint64_t>* offs, std::vector<uint32_t>* aidx,
-                         std::vector<uint64_t>* vers);
-int storage_list_op_actors_vec(ce_storage* s, std::vector<Uuid>* out);
-int storage_list_states_vec(ce_storage* s, std::vector<std::string>* out);
-int storage_read_state(ce_storage* s, const std::string& name, std::vector<uint8_t>* out);
-int storage_store_content(ce_storage* s, const char* sub, const uint8_t* d, size_t n,
-                          std::string* name);
-int storage_remove_state(ce_storage* s, const std::string& name);
-int storage_store_op(ce_storage* s, const Uuid& actor, uint64_t version, const uint8_t* d,
-                     size_t n);
-int storage_remove_op(ce_storage* s, const Uuid& actor, uint64_t version);
-int storage_load_local_meta(ce_storage* s, std::vector<uint8_t>* out, bool* missing);
-int storage_store_local_meta(ce_storage* s, const uint8_t* d, size_t n);
-ce_storage* storage_new(const std::string& local, const std::string& remote);
-}  // namespace ce
+#include "ce_core.h"
 
 using namespace ce;
 
-struct ce_core {
-  ce_ctx* ctx = nullptr;
-  int kind = CE_STATE_GCOUNTER;
-  std::vector<Uuid> supported;  // sorted (lib.rs:227-228)
-  Uuid current_data_version{};
-  ce_storage* storage = nullptr;
-  uint32_t flags = 0;
-  Uuid local_actor{};
-  bool has_key = false;
-  uint8_t key_version[16] = {0};
-  std::vector<uint8_t> key;
-  // actor table
-  uint32_t cap = 0, size = 0, registered = 0;
-  std::vector<ActorSlot> h_table;
-  std::vector<Uuid> slot_actor;
-  std::vector<uint64_t> nov;  // next_op_versions by slot
-  std::unordered_map<Uuid, uint32_t, UuidHash> slot_of;
-  bool table_dirty = true;
-  uint64_t table_gen = 0;               // bumped whenever an actor gets a slot or slots move
-  std::vector<uint32_t> sorted_slots;   // used slots in UUID byte order (BTreeMap order)
-  uint64_t sorted_gen = ~0ull;
-  std::vector<uint8_t> last_writers;    // writer list of the previous ingest and its slots
-  std::vector<uint32_t> last_wslot;
-  uint64_t last_writers_gen = ~0ull;
-  DevBuf d_table, d_state, d_batch, d_supported, d_refold2, d_tmp, d_gate, d_meta;
-  int files_per_wave = 4;  // fused kernel geometry (CE_FILES_PER_WAVE overrides)
-  std::set<std::string> read_states;  // lib.rs:205
-  ce_ctx* aux = nullptr;              // single-file work during a batch (exotic envelopes)
-};
-
-namespace {
+namespace ce {
 
 // ---------------------------------------------------------------------------------------
 // msgpack writer (rmp-serde to_vec_named)
 // ---------------------------------------------------------------------------------------
-struct Wr {
-  std::vector<uint8_t> b;
-  void u8(uint8_t v) { b.push_back(v); }
-  void be(uint64_t v, int k) {
-    for (int j = k - 1; j >= 0; j--) b.push_back((uint8_t)(v >> (8 * j)));
-  }
-  void uint(uint64_t v) {
-    if (v <= 0x7f) u8((uint8_t)v);
-    else if (v <= 0xff) { u8(0xcc); be(v, 1); }
-    else if (v <= 0xffff) { u8(0xcd); be(v, 2); }
-    else if (v <= 0xffffffffull) { u8(0xce); be(v, 4); }
-    else { u8(0xcf); be(v, 8); }
-  }
-  void str(const char* s) {
-    const size_t l = std::strlen(s);
-    u8((uint8_t)(0xa0 | l));
-    b.insert(b.end(), s, s + l);
-  }
-  void bin(const uint8_t* d, size_t l) {
-    if (l <= 0xff) { u8(0xc4); be(l, 1); }
-    else if (l <= 0xffff) { u8(0xc5); be(l, 2); }
-    else { u8(0xc6); be(l, 4); }
-    b.insert(b.end(), d, d + l);
-  }
-  void map(size_t n) {
-    if (n <= 15) u8((uint8_t)(0x80 | n));
-    else if (n <= 0xffff) { u8(0xde); be(n, 2); }
-    else { u8(0xdf); be(n, 4); }
-  }
-};
 
 // ---------------------------------------------------------------------------------------
 // host-side msgpack reading (states, local ops, local meta, exotic envelopes)
 // ---------------------------------------------------------------------------------------
 // skip one value, recursion depth bounded like rmp-serde's default (1024)
-bool skip_any(Rd& r, int depth = 0) {
+bool skip_any(Rd& r, int depth) {
   if (depth > 1024) return false;
   uint64_t at, cnt = 0;
   if (r.i >= r.n) return false;
@@ -190,8 +112,6 @@ bool read_struct(Rd& r, const std::vector<const char*>& names,
   }
   return seen == (1u << nf) - 1;
 }
-
-using Dots = std::vector<std::pair<Uuid, uint64_t>>;
 
 // VClock { dots: BTreeMap<Uuid, u64> }: later duplicate keys overwrite earlier ones
 bool read_vclock(Rd& r, Dots* out) {
@@ -305,6 +225,7 @@ int table_init(ce_core* c, uint32_t cap) {
   c->size = 0;
   c->h_table.assign(cap, ActorSlot{});
   c->slot_actor.assign(cap, Uuid{});
+  c->id_actor.clear();
   c->nov.assign(cap, 0);
   c->slot_of.clear();
   c->table_dirty = true;
@@ -339,8 +260,15 @@ int table_grow(ce_core* c) {
     return c->ctx->hip_fail(e, "grow");
   std::vector<Uuid> actors;
   std::vector<uint64_t> nov, sv;
+  std::vector<uint32_t> ids;
   for (uint32_t s = 0; s < old_cap; s++)
-    if (c->h_table[s].used) { actors.push_back(c->slot_actor[s]); nov.push_back(c->nov[s]); sv.push_back(st[s]); }
+    if (c->h_table[s].used) {
+      actors.push_back(c->slot_actor[s]);
+      nov.push_back(c->nov[s]);
+      sv.push_back(st[s]);
+      ids.push_back(c->h_table[s].pad[0]);
+    }
+  const std::vector<Uuid> id_actor = c->id_actor;
   // keep insertion order stable: re-insert in the old slot order
   const uint32_t reg = c->registered;
   DevBuf keep_state;
@@ -352,12 +280,14 @@ int table_grow(ce_core* c) {
     const uint32_t s = probe_slot(c->h_table, c->cap - 1, actors[i], &found);
     std::memcpy(c->h_table[s].k, actors[i].data(), 16);
     c->h_table[s].used = 1;
+    c->h_table[s].pad[0] = ids[i];
     c->slot_actor[s] = actors[i];
     c->slot_of[actors[i]] = s;
     c->nov[s] = nov[i];
     nst[s] = sv[i];
     c->size++;
   }
+  c->id_actor = id_actor;
   c->registered = reg;
   if ((e = hipMemcpyAsync(c->d_state.p, nst.data(), c->cap * 8ull, hipMemcpyHostToDevice,
                           c->ctx->stream)) ||
@@ -377,6 +307,8 @@ int insert_actor(ce_core* c, const Uuid& u, uint32_t* slot) {
   const uint32_t s = probe_slot(c->h_table, c->cap - 1, u, &found);
   std::memcpy(c->h_table[s].k, u.data(), 16);
   c->h_table[s].used = 1;
+  c->h_table[s].pad[0] = (uint32_t)c->id_actor.size();
+  c->id_actor.push_back(u);
   c->slot_actor[s] = u;
   c->slot_of[u] = s;
   c->size++;
@@ -419,6 +351,7 @@ int merge_dots_host(ce_core* c, const Dots& dots) {
 }
 
 int serialize_state(ce_core* c, std::vector<uint8_t>* out) {
+  if (is_dotset_kind(c->kind)) return ds_serialize(c, out);
   std::vector<uint64_t> st;
   int rc = download_state(c, &st);
   if (rc) return rc;
@@ -573,6 +506,8 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
   ce_ctx* ctx = c->ctx;
   if (!c->has_key) return ctx->fail(CE_ERR_NO_KEY, "no latest key");
   if (n == 0) return CE_OK;
+  if (is_dotset_kind(c->kind))
+    return ds_ingest_ops(c, d_blob, d_offs, n, blob_len, actors, m, d_fa, d_fv, status_out);
   hipError_t e;
   const KeyRef key = key_of(c);
   // writer actors (the op directories) get slots first: the version gate is keyed by them
@@ -904,6 +839,20 @@ int ingest_states_host(ce_core* c, const uint8_t* blob, const uint64_t* offs, ui
       (e = hipMemcpyAsync(out.data(), ctx->out.p, blen + 16ull * n, hipMemcpyDeviceToHost, ctx->stream)) ||
       (e = hipStreamSynchronize(ctx->stream)))
     return ctx->hip_fail(e, "states download");
+  if (is_dotset_kind(c->kind)) {
+    std::vector<std::pair<const uint8_t*, size_t>> sws(n, {nullptr, 0});
+    for (uint32_t i = 0; i < n; i++) {
+      if (st[i] != CE_OK) continue;
+      const uint8_t* pt = out.data() + P[i].out_off;
+      const uint32_t len = P[i].len;
+      if (len < 16) { st[i] = CE_ERR_PT_LEN; continue; }
+      Uuid v;
+      std::memcpy(v.data(), pt, 16);
+      if (!std::binary_search(c->supported.begin(), c->supported.end(), v)) { st[i] = CE_ERR_PT_VERSION; continue; }
+      sws[i] = {pt + 16, len - 16};
+    }
+    return ds_merge_states(c, sws, st.data(), status_out);
+  }
   // host pass: StateWrapper msgpack -> dots (north star: "host pass that flattens decoded
   // ops/states into columnar arrays")
   std::vector<Dots> novs(n), sts(n);
@@ -1009,14 +958,16 @@ int compact_bytes(ce_core* c, const uint8_t* nonce, std::vector<uint8_t>* file) 
                   clear.size(), file);
 }
 
-}  // namespace
+}  // namespace ce
 
 extern "C" {
 
 int ce_core_open(ce_ctx* ctx, const ce_open_options* o, ce_core** out) {
   if (!ctx || !o || !out || !o->current_data_version || (o->n_supported && !o->supported_data_versions))
     return CE_ERR_INVALID_ARG;
-  if (o->state_kind != CE_STATE_VCLOCK && o->state_kind != CE_STATE_GCOUNTER) return CE_ERR_INVALID_ARG;
+  if (o->state_kind != CE_STATE_VCLOCK && o->state_kind != CE_STATE_GCOUNTER &&
+      !is_dotset_kind(o->state_kind))
+    return CE_ERR_INVALID_ARG;
   std::lock_guard<std::recursive_mutex> g(ctx->mu);
   (void)hipSetDevice(ctx->device);
   ce_core* c = new ce_core();
@@ -1036,6 +987,7 @@ int ce_core_open(ce_ctx* ctx, const ce_open_options* o, ce_core** out) {
   std::sort(c->supported.begin(), c->supported.end());
   int rc = table_init(c, 8192);
   if (rc) { delete c; return rc; }
+  if (is_dotset_kind(c->kind) && (rc = ds_init(c))) { ce_core_close(c); return rc; }
   if (o->local_path || o->remote_path) {
     if (!o->local_path || !o->remote_path || o->local_path[0] != '/' || o->remote_path[0] != '/') {
       delete c;
@@ -1082,6 +1034,7 @@ void ce_core_close(ce_core* c) {
   if (c->ctx) (void)hipStreamSynchronize(c->ctx->stream);
   delete c->storage;
   delete c->aux;
+  ds_free(c->ds);
   delete c;
 }
 
@@ -1209,7 +1162,13 @@ int ce_core_apply_ops(ce_core* c, const uint8_t* ops, size_t len) {
   (void)hipSetDevice(c->ctx->device);
   if (!c->has_key) return c->ctx->fail(CE_ERR_NO_KEY, "no latest key");
   Dots dots;
-  if (!read_dots(ops, len, &dots)) return c->ctx->fail(CE_ERR_DECODE, "ops are not a Vec<Dot<Uuid>>");
+  const bool ds = is_dotset_kind(c->kind);
+  if (ds) {
+    int rc = ds_check_ops(c, ops, len);
+    if (rc) return rc;
+  } else if (!read_dots(ops, len, &dots)) {
+    return c->ctx->fail(CE_ERR_DECODE, "ops are not a Vec<Dot<Uuid>>");
+  }
   // clear_text = VersionBytes(current_data_version, msgpack(ops)).serialize() (lib.rs:670-671)
   std::vector<uint8_t> clear(c->current_data_version.begin(), c->current_data_version.end());
   clear.insert(clear.end(), ops, ops + len);
@@ -1221,7 +1180,8 @@ int ce_core_apply_ops(ce_core* c, const uint8_t* ops, size_t len) {
   const uint64_t version = c->nov[s];  // next_op_versions.get(actor) (lib.rs:703)
   if (c->storage && (rc = storage_store_op(c->storage, c->local_actor, version, file.data(), file.size())))
     return c->ctx->fail(rc, "failed writing ops file");
-  if ((rc = merge_dots_host(c, dots))) return rc;  // state.apply(op) for op in ops (lib.rs:710-712)
+  // state.apply(op) for op in ops (lib.rs:710-712)
+  if ((rc = ds ? ds_apply_local_ops(c, ops, len) : merge_dots_host(c, dots))) return rc;
   c->nov[s] = version + 1;                         // next_op_versions.inc(actor) (lib.rs:714-715)
   return table_upload(c);
 }
@@ -1233,7 +1193,7 @@ int ce_core_reset(ce_core* c) {
   c->read_states.clear();
   hipError_t e = hipMemsetAsync(c->d_state.p, 0, c->cap * 8ull, c->ctx->stream);
   if (e) return c->ctx->hip_fail(e, "reset");
-  return CE_OK;
+  return is_dotset_kind(c->kind) ? ds_reset(c) : CE_OK;
 }
 
 int ce_core_register_actors(ce_core* c, const uint8_t* actors, uint32_t m) {
@@ -1258,7 +1218,7 @@ int ce_core_register_actors(ce_core* c, const uint8_t* actors, uint32_t m) {
 uint32_t ce_core_dense_capacity(ce_core* c) { return c ? c->cap : 0; }
 
 int ce_core_export_dense(ce_core* c, uint64_t* d_state, uint64_t* d_nov) {
-  if (!c || !d_state || !d_nov) return CE_ERR_INVALID_ARG;
+  if (!c || !d_state || !d_nov || is_dotset_kind(c->kind)) return CE_ERR_INVALID_ARG;
   std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
   if (c->registered != c->size) return c->ctx->fail(CE_ERR_INVALID_ARG, "actors outside the registered set");
   hipError_t e;
@@ -1270,7 +1230,7 @@ int ce_core_export_dense(ce_core* c, uint64_t* d_state, uint64_t* d_nov) {
 }
 
 int ce_core_import_dense(ce_core* c, const uint64_t* d_state, const uint64_t* d_nov) {
-  if (!c || !d_state || !d_nov) return CE_ERR_INVALID_ARG;
+  if (!c || !d_state || !d_nov || is_dotset_kind(c->kind)) return CE_ERR_INVALID_ARG;
   std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
   if (c->registered != c->size) return c->ctx->fail(CE_ERR_INVALID_ARG, "actors outside the registered set");
   std::vector<uint64_t> nv(c->cap);
@@ -1282,6 +1242,28 @@ int ce_core_import_dense(ce_core* c, const uint64_t* d_state, const uint64_t* d_
     return c->ctx->hip_fail(e, "import");
   for (uint32_t s = 0; s < c->cap; s++) c->nov[s] = std::max(c->nov[s], nv[s]);
   return CE_OK;
+}
+
+int ce_core_merge_state(ce_core* c, const uint8_t* sw, size_t len) {
+  if (!c || (len && !sw)) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  (void)hipSetDevice(c->ctx->device);
+  if (is_dotset_kind(c->kind)) {
+    std::vector<std::pair<const uint8_t*, size_t>> sws{{sw, len}};
+    int32_t st = CE_OK;
+    return ds_merge_states(c, sws, &st, nullptr);
+  }
+  Dots nov, state;
+  if (!read_state_wrapper(sw, len, c->kind, &nov, &state))
+    return c->ctx->fail(CE_ERR_DECODE, "not a StateWrapper");
+  int rc = merge_dots_host(c, state);  // state.merge(sw.state) (lib.rs:460)
+  if (rc) return rc;
+  for (auto& d : nov) {                // next_op_versions.merge(..) (lib.rs:461-463)
+    uint32_t s;
+    if ((rc = insert_actor(c, d.first, &s))) return rc;
+    c->nov[s] = std::max(c->nov[s], d.second);
+  }
+  return table_upload(c);
 }
 
 }  // extern "C"

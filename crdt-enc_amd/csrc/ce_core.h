@@ -1,0 +1,141 @@
+// ce_core.h -- the Core object (crdt-enc/src/lib.rs:188-207 Core / CoreMutData) and the host
+// helpers shared by ce_core.cpp (VClock / GCounter state) and ce_dotset_host.cpp (Orswot / MVReg).
+#pragma once
+#include <functional>
+#include <set>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "ce_internal.h"
+
+namespace ce {
+int storage_load_ops_vec(ce_storage* s, const std::vector<Uuid>& actors,
+                         const std::vector<uint64_t>& first, std::vector<uint8_t>* blob,
+                         std::vector<uint64_t>* offs, std::vector<uint32_t>* aidx,
+                         std::vector<uint64_t>* vers);
+int storage_list_op_actors_vec(ce_storage* s, std::vector<Uuid>* out);
+int storage_list_states_vec(ce_storage* s, std::vector<std::string>* out);
+int storage_read_state(ce_storage* s, const std::string& name, std::vector<uint8_t>* out);
+int storage_store_content(ce_storage* s, const char* sub, const uint8_t* d, size_t n,
+                          std::string* name);
+int storage_remove_state(ce_storage* s, const std::string& name);
+int storage_store_op(ce_storage* s, const Uuid& actor, uint64_t version, const uint8_t* d,
+                     size_t n);
+int storage_remove_op(ce_storage* s, const Uuid& actor, uint64_t version);
+int storage_load_local_meta(ce_storage* s, std::vector<uint8_t>* out, bool* missing);
+int storage_store_local_meta(ce_storage* s, const uint8_t* d, size_t n);
+ce_storage* storage_new(const std::string& local, const std::string& remote);
+
+struct DsState;  // Orswot / MVReg state (ce_dotset_host.cpp)
+void ds_free(DsState* d);
+
+inline bool is_dotset_kind(int kind) { return kind == CE_STATE_ORSWOT || kind == CE_STATE_MVREG; }
+}  // namespace ce
+
+struct ce_core {
+  ce_ctx* ctx = nullptr;
+  int kind = CE_STATE_GCOUNTER;
+  std::vector<ce::Uuid> supported;  // sorted (lib.rs:227-228)
+  ce::Uuid current_data_version{};
+  ce_storage* storage = nullptr;
+  uint32_t flags = 0;
+  ce::Uuid local_actor{};
+  bool has_key = false;
+  uint8_t key_version[16] = {0};
+  std::vector<uint8_t> key;
+  // actor table: UUID -> hash slot; ActorSlot.pad[0] holds the actor's stable id (insertion
+  // order, survives table growth) used by the dot-set kinds' device arrays.
+  uint32_t cap = 0, size = 0, registered = 0;
+  std::vector<ce::ActorSlot> h_table;
+  std::vector<ce::Uuid> slot_actor;
+  std::vector<ce::Uuid> id_actor;   // stable id -> UUID
+  std::vector<uint64_t> nov;  // next_op_versions by slot
+  std::unordered_map<ce::Uuid, uint32_t, ce::UuidHash> slot_of;
+  bool table_dirty = true;
+  uint64_t table_gen = 0;               // bumped whenever an actor gets a slot or slots move
+  std::vector<uint32_t> sorted_slots;   // used slots in UUID byte order (BTreeMap order)
+  uint64_t sorted_gen = ~0ull;
+  std::vector<uint8_t> last_writers;    // writer list of the previous ingest and its slots
+  std::vector<uint32_t> last_wslot;
+  uint64_t last_writers_gen = ~0ull;
+  ce::DevBuf d_table, d_state, d_batch, d_supported, d_refold2, d_tmp, d_gate, d_meta;
+  int files_per_wave = 4;  // fused kernel geometry (CE_FILES_PER_WAVE overrides)
+  std::set<std::string> read_states;  // lib.rs:205
+  ce_ctx* aux = nullptr;              // single-file work during a batch (exotic envelopes)
+  ce::DsState* ds = nullptr;          // Orswot / MVReg state (dot-set kinds only)
+};
+
+namespace ce {
+
+// msgpack writer (rmp-serde to_vec_named)
+struct Wr {
+  std::vector<uint8_t> b;
+  void u8(uint8_t v) { b.push_back(v); }
+  void be(uint64_t v, int k) {
+    for (int j = k - 1; j >= 0; j--) b.push_back((uint8_t)(v >> (8 * j)));
+  }
+  void uint(uint64_t v) {
+    if (v <= 0x7f) u8((uint8_t)v);
+    else if (v <= 0xff) { u8(0xcc); be(v, 1); }
+    else if (v <= 0xffff) { u8(0xcd); be(v, 2); }
+    else if (v <= 0xffffffffull) { u8(0xce); be(v, 4); }
+    else { u8(0xcf); be(v, 8); }
+  }
+  void str(const char* s) {
+    const size_t l = std::strlen(s);
+    u8((uint8_t)(0xa0 | l));
+    b.insert(b.end(), s, s + l);
+  }
+  void bin(const uint8_t* d, size_t l) {
+    if (l <= 0xff) { u8(0xc4); be(l, 1); }
+    else if (l <= 0xffff) { u8(0xc5); be(l, 2); }
+    else { u8(0xc6); be(l, 4); }
+    b.insert(b.end(), d, d + l);
+  }
+  void map(size_t n) {
+    if (n <= 15) u8((uint8_t)(0x80 | n));
+    else if (n <= 0xffff) { u8(0xde); be(n, 2); }
+    else { u8(0xdf); be(n, 4); }
+  }
+  void arr(size_t n) {
+    if (n <= 15) u8((uint8_t)(0x90 | n));
+    else if (n <= 0xffff) { u8(0xdc); be(n, 2); }
+    else { u8(0xdd); be(n, 4); }
+  }
+};
+
+using Dots = std::vector<std::pair<Uuid, uint64_t>>;
+
+bool skip_any(Rd& r, int depth = 0);
+bool bytes_any(Rd& r, std::vector<uint8_t>* out);
+bool read_struct(Rd& r, const std::vector<const char*>& names,
+                 const std::function<bool(int, Rd&)>& cb);
+bool read_vclock(Rd& r, Dots* out);
+int insert_actor(ce_core* c, const Uuid& u, uint32_t* slot);
+inline uint32_t actor_id_of_slot(const ce_core* c, uint32_t slot) { return c->h_table[slot].pad[0]; }
+int table_upload(ce_core* c);
+KeyRef key_of(ce_core* c);
+int ensure_supported(ce_core* c);
+int resolve_host_parse(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
+                       bool outer);
+uint32_t host_gate(const uint32_t* fa, const uint64_t* fv, uint32_t n, std::vector<uint64_t>* expect,
+                   uint8_t* apply);
+int merge_dots_host(ce_core* c, const Dots& dots);
+
+// dot-set kinds (ce_dotset_host.cpp): same contracts as the VClock/GCounter paths in ce_core.cpp
+int ds_init(ce_core* c);
+int ds_reset(ce_core* c);
+int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
+                  uint64_t blob_len, const uint8_t* actors, uint32_t m, const uint32_t* d_fa,
+                  const uint64_t* d_fv, int32_t* status_out);
+// read_remote_states after load_states; plaintext StateWrappers (after the data version)
+// sws[i] = {nullptr, 0} for files whose status st[i] is already a failure.
+int ds_merge_states(ce_core* c, const std::vector<std::pair<const uint8_t*, size_t>>& sws,
+                    int32_t* st, int32_t* status_out);
+int ds_serialize(ce_core* c, std::vector<uint8_t>* out);
+// Core::apply_ops for a local Vec<S::Op> (already validated by ds_check_ops)
+int ds_check_ops(ce_core* c, const uint8_t* ops, size_t len);
+int ds_apply_local_ops(ce_core* c, const uint8_t* ops, size_t len);
+
+}  // namespace ce

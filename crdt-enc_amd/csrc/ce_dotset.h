@@ -1,0 +1,153 @@
+// ce_dotset.h -- launch interface of the dot-set fold kernels (ce_dotset.hip): decode of
+// Vec<orswot::Op> / Vec<mvreg::Op> op files into columnar arrays, and the data-parallel
+// Orswot / MVReg fold (the formulation is stated, and checked against the sequential oracle, in
+// tests/dotset_model.py).
+//
+// HBM layout (all arrays device-resident, one set per Core):
+//   actors        stable actor id (ActorSlot.pad[0]) indexes every dense per-actor array
+//   clock         u64[n_actors]          Orswot.clock (VClock::dots by id)
+//   member table  u64 mkey[mcap + 1]     open addressing on the u64 member; the bucket index is
+//                                        the member's handle; bucket mcap is reserved for the
+//                                        member ~0 (the empty-key sentinel)
+//   pair table    u64 pkey[pcap]         (member handle << 24 | actor id), EMPTY = ~0
+//                 u64 cur/add/kill/oth[pcap]  entry value (Orswot.entries[m][a]), the batch's
+//                                        applied-add max, removal threshold, merged state's value
+//   ops (CSR)     adds: actor u32, counter u64, mbeg u32 -> add members u64
+//                 removals / puts: cbeg u32 -> clock (actor u32, counter u64), mbeg u32 ->
+//                 members u64 (removals), val u64 (puts)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ce_common.h"
+#include "ce_kernels.h"
+
+namespace ce {
+
+static constexpr unsigned long long kDsEmpty = ~0ull;
+static constexpr uint32_t kDsNoActor = 0xffffffffu;
+static constexpr int32_t kStatusHostDecode = 101;  // op vector the device leaves to the host
+static constexpr int kDsActorBits = 24;            // actor ids < 2^24 in a pair key
+
+enum DsKind { kDsOrswot = 0, kDsMVReg = 1 };
+
+// per-file counts (count pass) / bases (after the exclusive scan), 5 arrays of n
+enum { kCntAdd = 0, kCntAddM = 1, kCntRm = 2, kCntRmC = 3, kCntRmM = 4, kCntN = 5 };
+
+struct DsOps {
+  uint32_t* add_actor;
+  unsigned long long* add_ctr;
+  uint32_t* add_mbeg;          // [n_add + 1]
+  unsigned long long* add_mem;
+  uint32_t* rm_cbeg;           // [n_rm + 1]  (MVReg: puts)
+  uint32_t* rm_mbeg;           // [n_rm + 1]
+  uint32_t* rmc_actor;
+  unsigned long long* rmc_ctr;
+  unsigned long long* rm_mem;
+  unsigned long long* put_val; // MVReg
+};
+
+struct DsDecodeArgs {
+  int kind;                     // DsKind
+  const uint8_t* pt;            // plaintext blob (FileParams.out_off / len)
+  const FileParams* params;
+  int32_t* status;
+  uint32_t n;
+  const uint8_t* supported;     // n_supported * 16 bytes
+  uint32_t n_supported;
+  const uint8_t* apply;         // version gate: 1 = fold this file
+  uint32_t* cnt;                // [kCntN][n] counts (count pass) / bases (emit pass)
+  uint32_t base_off[kCntN];     // emit: added to every base (MVReg: current values first)
+  const ActorSlot* table;
+  uint32_t mask;
+  DsOps ops;
+  uint32_t* counters;           // [0] decode failures, [1] host-decode files, [2] misses
+  uint4* miss_list;
+  uint32_t miss_cap;
+};
+hipError_t launch_ds_count(hipStream_t s, const DsDecodeArgs& a);
+hipError_t launch_ds_emit(hipStream_t s, const DsDecodeArgs& a);
+
+struct DsTables {
+  unsigned long long* mkey;
+  uint32_t mmask;               // mcap - 1 (mcap = power of two)
+  unsigned long long* pkey;
+  unsigned long long* cur;
+  unsigned long long* add;
+  unsigned long long* kill;
+  unsigned long long* oth;
+  uint32_t pmask;
+  uint32_t* live;               // [0] live pairs after finalize, [1] used pairs, [2] probe overflow
+};
+
+// applied flags of the adds: keys = add_actor sorted stably, perm = add index per position
+hipError_t launch_ds_iota(hipStream_t s, uint32_t* v, uint32_t n);
+hipError_t launch_ds_gather_ctr(hipStream_t s, const uint32_t* perm, const unsigned long long* ctr,
+                                unsigned long long* out, uint32_t n);
+hipError_t launch_ds_applied(hipStream_t s, const uint32_t* keys_sorted, const uint32_t* perm,
+                             const unsigned long long* ctr_sorted,
+                             const unsigned long long* excl_max, const unsigned long long* clock,
+                             uint8_t* applied, uint32_t n);
+// clock[a] = max(clock[a], counter) for every add
+hipError_t launch_ds_clock(hipStream_t s, const uint32_t* add_actor, const unsigned long long* add_ctr,
+                           unsigned long long* clock, uint32_t n_add);
+// insert (member, actor) of every applied add, add[pair] = max counter
+hipError_t launch_ds_add_pairs(hipStream_t s, DsTables t, DsOps o, const uint8_t* applied,
+                               uint32_t n_add);
+// removal thresholds: kill[(m, a)] = max R[a] over removals listing m (existing pairs only)
+hipError_t launch_ds_kill(hipStream_t s, DsTables t, const uint32_t* cbeg, const uint32_t* mbeg,
+                          const uint32_t* c_actor, const unsigned long long* c_ctr,
+                          const unsigned long long* mem, uint32_t n_rm);
+// v = max(cur, add); v <= kill -> 0; cur = v; add = kill = 0; live/used counts
+hipError_t launch_ds_finalize(hipStream_t s, DsTables t);
+// deferred[r] = !(R <= clock)
+hipError_t launch_ds_deferred(hipStream_t s, const uint32_t* cbeg, const uint32_t* c_actor,
+                              const unsigned long long* c_ctr, const unsigned long long* clock,
+                              uint8_t* deferred, uint32_t n_rm);
+// state merge: insert the other state's entries with oth = value, then the per-pair merge rule
+hipError_t launch_ds_put_other(hipStream_t s, DsTables t, const unsigned long long* member,
+                               const uint32_t* actor, const unsigned long long* value, uint32_t n);
+hipError_t launch_ds_merge(hipStream_t s, DsTables t, const unsigned long long* clock,
+                           const unsigned long long* oclock);
+// live pairs -> (member, actor, value) in bucket order; count in t.live[0] beforehand
+hipError_t launch_ds_collect(hipStream_t s, DsTables t, unsigned long long* member, uint32_t* actor,
+                             unsigned long long* value, uint32_t* n_out);
+// rebuild: insert (member, actor, value) into fresh (cleared) tables as cur
+hipError_t launch_ds_reinsert(hipStream_t s, DsTables t, const unsigned long long* member,
+                              const uint32_t* actor, const unsigned long long* value, uint32_t n);
+hipError_t launch_ds_gather_entries(hipStream_t s, const uint32_t* perm, const uint32_t* actor_in,
+                                    const unsigned long long* value_in, uint32_t* actor_out,
+                                    unsigned long long* value_out, uint32_t n);
+
+// device-wide primitives (hipCUB): tmp = nullptr queries the temp size into tb
+hipError_t ds_sort_pairs_u32(void* tmp, size_t& tb, const uint32_t* kin, uint32_t* kout,
+                             const uint32_t* vin, uint32_t* vout, uint32_t n, int bits, hipStream_t s);
+hipError_t ds_sort_pairs_u64(void* tmp, size_t& tb, const unsigned long long* kin,
+                             unsigned long long* kout, const uint32_t* vin, uint32_t* vout,
+                             uint32_t n, hipStream_t s);
+// out[i] = max(vals[j] : j < i, keys[j] == keys[i]) (0 for a segment's first element)
+hipError_t ds_excl_max_by_key(void* tmp, size_t& tb, const uint32_t* keys,
+                              const unsigned long long* vals, unsigned long long* out, uint32_t n,
+                              hipStream_t s);
+hipError_t ds_excl_sum_u32(void* tmp, size_t& tb, const uint32_t* in, uint32_t* out, uint32_t n,
+                           hipStream_t s);
+
+// MVReg survivors: candidates = CSR clocks (cbeg, actor, ctr) with priorities (index order)
+struct MvArgs {
+  const uint32_t* cbeg;
+  const uint32_t* c_actor;
+  const unsigned long long* c_ctr;
+  uint32_t n;
+  int later_wins;                 // ties (equal clocks): 1 = highest index wins, 0 = lowest
+  uint8_t* alive;
+  unsigned long long* sum_hi;     // 128-bit counter sums
+  unsigned long long* sum_lo;
+  unsigned long long* blk;        // per-block best: 4 words (hi, lo, prio, idx)
+  uint32_t n_blk;
+  uint32_t* win;                  // [0] winner index or ~0, [1] alive count
+  unsigned long long* wclock;     // dense winner clock by actor id (kept zero between rounds)
+};
+hipError_t launch_mv_prep(hipStream_t s, const MvArgs& a);
+hipError_t launch_mv_round(hipStream_t s, const MvArgs& a);  // argmax + scatter + kill + clear
+
+}  // namespace ce

@@ -1,0 +1,642 @@
+// ce_dotset.hip -- gfx950 kernels of the Orswot / MVReg fold (crdts 7 semantics, see
+// ce_dotset.h for the HBM layout and tests/dotset_model.py for the formulation).
+//
+// Everything here is integer / pointer-chasing work bounded by HBM latency and atomics, so the
+// kernels are grid-stride loops of 256-thread blocks, one lane per file / op / pair bucket;
+// block-level LDS counters keep the global atomics to one per block.  No MFMA: nothing here is a
+// contraction.
+#include <hip/hip_runtime.h>
+
+#include <hipcub/hipcub.hpp>
+
+#include "ce_dotset.h"
+#include "ce_dotset_codec.h"
+
+namespace ce {
+namespace {
+
+constexpr int kBlock = 256;
+
+inline uint32_t blocks_for(uint64_t n, uint32_t cap = 8192) {
+  uint64_t b = (n + kBlock - 1) / kBlock;
+  if (b == 0) b = 1;
+  return (uint32_t)(b < cap ? b : cap);
+}
+
+__device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+__device__ __forceinline__ unsigned long long ld_volatile(const unsigned long long* p) {
+  return __atomic_load_n(p, __ATOMIC_RELAXED);
+}
+
+// member handle (bucket index) or kDsEmpty when absent (insert = false)
+__device__ unsigned long long member_find(const DsTables& t, unsigned long long m, bool insert) {
+  if (m == kDsEmpty) return (unsigned long long)t.mmask + 1;  // reserved bucket
+  uint32_t h = (uint32_t)mix64(m) & t.mmask;
+  for (uint32_t probe = 0; probe <= t.mmask; probe++) {
+    const unsigned long long k = ld_volatile(t.mkey + h);
+    if (k == m) return h;
+    if (k == kDsEmpty) {
+      if (!insert) return kDsEmpty;
+      const unsigned long long prev = atomicCAS(t.mkey + h, kDsEmpty, m);
+      if (prev == kDsEmpty || prev == m) return h;
+    }
+    h = (h + 1) & t.mmask;
+  }
+  atomicAdd(t.live + 2, 1u);  // table full (host sizes it to <= 50% load)
+  return kDsEmpty;
+}
+
+__device__ unsigned long long pair_find(const DsTables& t, unsigned long long key, bool insert) {
+  uint32_t h = (uint32_t)mix64(key) & t.pmask;
+  for (uint32_t probe = 0; probe <= t.pmask; probe++) {
+    const unsigned long long k = ld_volatile(t.pkey + h);
+    if (k == key) return h;
+    if (k == kDsEmpty) {
+      if (!insert) return kDsEmpty;
+      const unsigned long long prev = atomicCAS(t.pkey + h, kDsEmpty, key);
+      if (prev == kDsEmpty || prev == key) return h;
+    }
+    h = (h + 1) & t.pmask;
+  }
+  atomicAdd(t.live + 2, 1u);
+  return kDsEmpty;
+}
+
+__device__ __forceinline__ unsigned long long pair_key(unsigned long long handle, uint32_t aid) {
+  return (handle << kDsActorBits) | aid;
+}
+
+__device__ __forceinline__ unsigned long long member_of(const DsTables& t, unsigned long long h) {
+  return h == (unsigned long long)t.mmask + 1 ? kDsEmpty : t.mkey[h];
+}
+
+// block-aggregated counter increment: returns this lane's index among all incrementing lanes
+__device__ __forceinline__ uint32_t block_count(uint32_t* global, bool pred, uint32_t* lds) {
+  if (threadIdx.x == 0) *lds = 0;
+  __syncthreads();
+  uint32_t mine = 0;
+  if (pred) mine = atomicAdd(lds, 1u);
+  __syncthreads();
+  if (threadIdx.x == 0 && *lds) lds[1] = atomicAdd(global, *lds);
+  __syncthreads();
+  return lds[1] + mine;
+}
+
+// ---------------------------------------------------------------------------------------
+// decode: one lane per file
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lookup_actor(const DsDecodeArgs& a, const uint8_t* u) {
+  uint32_t w[4];
+  for (int j = 0; j < 4; j++)
+    w[j] = (uint32_t)u[4 * j] | ((uint32_t)u[4 * j + 1] << 8) | ((uint32_t)u[4 * j + 2] << 16) |
+           ((uint32_t)u[4 * j + 3] << 24);
+  uint32_t h = actor_hash(w[0], w[1], w[2], w[3]) & a.mask;
+  for (uint32_t probe = 0; probe <= a.mask; probe++) {
+    const ActorSlot& s = a.table[h];
+    if (!s.used) break;
+    if (s.k[0] == w[0] && s.k[1] == w[1] && s.k[2] == w[2] && s.k[3] == w[3]) return s.pad[0];
+    h = (h + 1) & a.mask;
+  }
+  const uint32_t i = atomicAdd(a.counters + 2, 1u);
+  if (i < a.miss_cap) a.miss_list[i] = make_uint4(w[0], w[1], w[2], w[3]);
+  return kDsNoActor;
+}
+
+struct CountSink {
+  uint32_t c[kCntN] = {0, 0, 0, 0, 0};
+  __device__ void add_begin() { c[kCntAdd]++; }
+  __device__ void add_dot(uint64_t, uint64_t) {}
+  __device__ void add_member(uint64_t) { c[kCntAddM]++; }
+  __device__ void add_end() {}
+  __device__ void rm_begin() { c[kCntRm]++; }
+  __device__ void rm_dot(uint64_t, uint64_t) { c[kCntRmC]++; }
+  __device__ void rm_member(uint64_t) { c[kCntRmM]++; }
+  __device__ void rm_end() {}
+  __device__ void put_begin() { c[kCntRm]++; }
+  __device__ void put_dot(uint64_t, uint64_t) { c[kCntRmC]++; }
+  __device__ void put_val(uint64_t) {}
+  __device__ void put_end() {}
+};
+
+struct EmitSink {
+  const DsDecodeArgs* a;
+  const uint8_t* p;
+  uint32_t ia, iam, ir, irc, irm;
+  __device__ void add_begin() { a->ops.add_mbeg[ia] = iam; }
+  __device__ void add_dot(uint64_t off, uint64_t c) {
+    a->ops.add_actor[ia] = lookup_actor(*a, p + off);
+    a->ops.add_ctr[ia] = c;
+  }
+  __device__ void add_member(uint64_t m) { a->ops.add_mem[iam++] = m; }
+  __device__ void add_end() { ia++; }
+  __device__ void rm_begin() {
+    a->ops.rm_cbeg[ir] = irc;
+    a->ops.rm_mbeg[ir] = irm;
+  }
+  __device__ void rm_dot(uint64_t off, uint64_t c) {
+    a->ops.rmc_actor[irc] = lookup_actor(*a, p + off);
+    a->ops.rmc_ctr[irc] = c;
+    irc++;
+  }
+  __device__ void rm_member(uint64_t m) { a->ops.rm_mem[irm++] = m; }
+  __device__ void rm_end() { ir++; }
+  __device__ void put_begin() { a->ops.rm_cbeg[ir] = irc; }
+  __device__ void put_dot(uint64_t off, uint64_t c) { rm_dot(off, c); }
+  __device__ void put_val(uint64_t v) { a->ops.put_val[ir] = v; }
+  __device__ void put_end() { ir++; }
+};
+
+template <typename S>
+__device__ int parse_file(int kind, const uint8_t* p, uint64_t n, S& sink) {
+  return kind == kDsOrswot ? ds_parse_orswot_ops(p, n, sink) : ds_parse_mvreg_ops(p, n, sink);
+}
+
+__global__ void __launch_bounds__(kBlock) k_ds_count(DsDecodeArgs a) {
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < a.n; i += gridDim.x * kBlock) {
+    CountSink cs;
+    int32_t st = a.status[i];
+    if (st == CE_OK) {
+      const uint32_t len = a.params[i].len;
+      const uint8_t* p = a.pt + a.params[i].out_off;
+      if (len < 16) {
+        st = CE_ERR_PT_LEN;  // VersionBytesRef::deserialize (lib.rs:504)
+      } else {
+        bool ok = false;
+        for (uint32_t v = 0; v < a.n_supported && !ok; v++) {
+          bool eq = true;
+          for (int b = 0; b < 16; b++) eq = eq && p[b] == a.supported[16 * v + b];
+          ok = eq;
+        }
+        if (!ok) {
+          st = CE_ERR_PT_VERSION;  // ensure_versions (lib.rs:505)
+        } else {
+          const int r = parse_file(a.kind, p + 16, len - 16, cs);  // from_slice (lib.rs:507)
+          if (r == kDsErr) {
+            st = CE_ERR_DECODE;
+            atomicAdd(a.counters + 0, 1u);
+          } else if (r == kDsHost) {
+            st = kStatusHostDecode;
+            atomicAdd(a.counters + 1, 1u);
+          }
+        }
+      }
+      if (st != CE_OK) a.status[i] = st;
+    }
+    const bool keep = st == CE_OK && a.apply[i];
+    for (int k = 0; k < kCntN; k++) a.cnt[(size_t)k * a.n + i] = keep ? cs.c[k] : 0u;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_ds_emit(DsDecodeArgs a) {
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < a.n; i += gridDim.x * kBlock) {
+    if (a.status[i] != CE_OK || !a.apply[i]) continue;
+    const uint32_t len = a.params[i].len;
+    const uint8_t* p = a.pt + a.params[i].out_off + 16;
+    EmitSink es;
+    es.a = &a;
+    es.p = p;
+    es.ia = a.base_off[kCntAdd] + a.cnt[(size_t)kCntAdd * a.n + i];
+    es.iam = a.base_off[kCntAddM] + a.cnt[(size_t)kCntAddM * a.n + i];
+    es.ir = a.base_off[kCntRm] + a.cnt[(size_t)kCntRm * a.n + i];
+    es.irc = a.base_off[kCntRmC] + a.cnt[(size_t)kCntRmC * a.n + i];
+    es.irm = a.base_off[kCntRmM] + a.cnt[(size_t)kCntRmM * a.n + i];
+    parse_file(a.kind, p, len - 16, es);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Orswot fold
+// ---------------------------------------------------------------------------------------
+__global__ void k_ds_iota(uint32_t* v, uint32_t n) {
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) v[i] = i;
+}
+
+__global__ void k_ds_gather_ctr(const uint32_t* perm, const unsigned long long* ctr,
+                                unsigned long long* out, uint32_t n) {
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) out[i] = ctr[perm[i]];
+}
+
+// applied(add k) = c_k > max(C0[a_k], max{c_j : j < k, a_j = a_k})  (crdts Orswot::apply:
+// "if self.clock.get(&dot.actor) >= dot.counter { return }")
+__global__ void k_ds_applied(const uint32_t* keys, const uint32_t* perm,
+                             const unsigned long long* ctr, const unsigned long long* excl,
+                             const unsigned long long* clock, uint8_t* applied, uint32_t n) {
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+    const unsigned long long c0 = clock[keys[i]];
+    const unsigned long long prev = excl[i] > c0 ? excl[i] : c0;
+    applied[perm[i]] = ctr[i] > prev;
+  }
+}
+
+__global__ void k_ds_clock(const uint32_t* add_actor, const unsigned long long* add_ctr,
+                           unsigned long long* clock, uint32_t n) {
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
+    atomicMax(clock + add_actor[i], add_ctr[i]);
+}
+
+__global__ void __launch_bounds__(kBlock) k_ds_add_pairs(DsTables t, DsOps o, const uint8_t* applied,
+                                                         uint32_t n) {
+  for (uint32_t k = blockIdx.x * kBlock + threadIdx.x; k < n; k += gridDim.x * kBlock) {
+    if (!applied[k]) continue;
+    const uint32_t aid = o.add_actor[k];
+    const unsigned long long c = o.add_ctr[k];
+    for (uint32_t j = o.add_mbeg[k]; j < o.add_mbeg[k + 1]; j++) {
+      const unsigned long long h = member_find(t, o.add_mem[j], true);
+      if (h == kDsEmpty) continue;
+      const unsigned long long b = pair_find(t, pair_key(h, aid), true);
+      if (b != kDsEmpty) atomicMax(t.add + b, c);
+    }
+  }
+}
+
+// crdts Orswot::apply_rm: entry.reset_remove(clock) drops actor a when R[a] >= entry[a]
+__global__ void __launch_bounds__(kBlock) k_ds_kill(DsTables t, const uint32_t* cbeg, const uint32_t* mbeg,
+                                                    const uint32_t* c_actor,
+                                                    const unsigned long long* c_ctr,
+                                                    const unsigned long long* mem, uint32_t n) {
+  for (uint32_t r = blockIdx.x * kBlock + threadIdx.x; r < n; r += gridDim.x * kBlock) {
+    const uint32_t c0 = cbeg[r], c1 = cbeg[r + 1];
+    if (c0 == c1) continue;
+    for (uint32_t j = mbeg[r]; j < mbeg[r + 1]; j++) {
+      const unsigned long long h = member_find(t, mem[j], false);
+      if (h == kDsEmpty) continue;
+      for (uint32_t e = c0; e < c1; e++) {
+        const unsigned long long b = pair_find(t, pair_key(h, c_actor[e]), false);
+        if (b != kDsEmpty) atomicMax(t.kill + b, c_ctr[e]);
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_ds_finalize(DsTables t) {
+  __shared__ uint32_t lds[2];
+  const uint32_t cap = t.pmask + 1;
+  // every block runs the same number of iterations (block_count needs all threads)
+  const uint32_t stride = gridDim.x * kBlock;
+  const uint32_t iters = (cap + stride - 1) / stride;
+  for (uint32_t it = 0; it < iters; it++) {
+    const uint32_t b = it * stride + blockIdx.x * kBlock + threadIdx.x;
+    bool used = false, live = false;
+    if (b < cap && t.pkey[b] != kDsEmpty) {
+      used = true;
+      unsigned long long v = t.cur[b] > t.add[b] ? t.cur[b] : t.add[b];
+      if (v != 0 && v <= t.kill[b]) v = 0;
+      t.cur[b] = v;
+      t.add[b] = 0;
+      t.kill[b] = 0;
+      live = v != 0;
+    }
+    block_count(t.live + 0, live, lds);
+    block_count(t.live + 1, used, lds);
+  }
+}
+
+__global__ void k_ds_deferred(const uint32_t* cbeg, const uint32_t* c_actor,
+                              const unsigned long long* c_ctr, const unsigned long long* clock,
+                              uint8_t* deferred, uint32_t n) {
+  for (uint32_t r = blockIdx.x * kBlock + threadIdx.x; r < n; r += gridDim.x * kBlock) {
+    bool d = false;
+    for (uint32_t e = cbeg[r]; e < cbeg[r + 1] && !d; e++) d = c_ctr[e] > clock[c_actor[e]];
+    deferred[r] = d;  // !(clock <= self.clock)
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_ds_put_other(DsTables t, const unsigned long long* member,
+                                                         const uint32_t* actor,
+                                                         const unsigned long long* value, uint32_t n) {
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+    const unsigned long long h = member_find(t, member[i], true);
+    if (h == kDsEmpty) continue;
+    const unsigned long long b = pair_find(t, pair_key(h, actor[i]), true);
+    if (b != kDsEmpty) t.oth[b] = value[i];
+  }
+}
+
+// Orswot::merge per (member, actor): keep ours if equal to theirs (VClock::intersection) or
+// newer than their clock (clone_without(other.clock)); take theirs if newer than our clock.
+__global__ void k_ds_merge(DsTables t, const unsigned long long* clock, const unsigned long long* oclock) {
+  const uint32_t cap = t.pmask + 1;
+  for (uint32_t b = blockIdx.x * kBlock + threadIdx.x; b < cap; b += gridDim.x * kBlock) {
+    const unsigned long long key = t.pkey[b];
+    if (key == kDsEmpty) continue;
+    const uint32_t a = (uint32_t)(key & ((1u << kDsActorBits) - 1));
+    const unsigned long long s = t.cur[b], o = t.oth[b];
+    unsigned long long r = 0;
+    if (s == o) r = s;
+    if (s > oclock[a] && s > r) r = s;
+    if (o > clock[a] && o > r) r = o;
+    t.cur[b] = r;
+    t.oth[b] = 0;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_ds_collect(DsTables t, unsigned long long* member, uint32_t* actor,
+                                                       unsigned long long* value, uint32_t* n_out) {
+  __shared__ uint32_t lds[2];
+  const uint32_t cap = t.pmask + 1;
+  const uint32_t stride = gridDim.x * kBlock;
+  const uint32_t iters = (cap + stride - 1) / stride;
+  for (uint32_t it = 0; it < iters; it++) {
+    const uint32_t b = it * stride + blockIdx.x * kBlock + threadIdx.x;
+    unsigned long long key = kDsEmpty, v = 0;
+    if (b < cap) {
+      key = t.pkey[b];
+      if (key != kDsEmpty) v = t.cur[b];
+    }
+    const bool live = key != kDsEmpty && v != 0;
+    const uint32_t idx = block_count(n_out, live, lds);
+    if (live) {
+      member[idx] = member_of(t, key >> kDsActorBits);
+      actor[idx] = (uint32_t)(key & ((1u << kDsActorBits) - 1));
+      value[idx] = v;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_ds_reinsert(DsTables t, const unsigned long long* member,
+                                                        const uint32_t* actor,
+                                                        const unsigned long long* value, uint32_t n) {
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+    const unsigned long long h = member_find(t, member[i], true);
+    if (h == kDsEmpty) continue;
+    const unsigned long long b = pair_find(t, pair_key(h, actor[i]), true);
+    if (b != kDsEmpty) t.cur[b] = value[i];
+  }
+}
+
+__global__ void k_ds_gather_entries(const uint32_t* perm, const uint32_t* actor_in,
+                                    const unsigned long long* value_in, uint32_t* actor_out,
+                                    unsigned long long* value_out, uint32_t n) {
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+    actor_out[i] = actor_in[perm[i]];
+    value_out[i] = value_in[perm[i]];
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// MVReg: survivors = maximal clocks, one round per survivor
+// ---------------------------------------------------------------------------------------
+__global__ void k_mv_prep(MvArgs a) {
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < a.n; i += gridDim.x * kBlock) {
+    unsigned long long hi = 0, lo = 0;
+    for (uint32_t e = a.cbeg[i]; e < a.cbeg[i + 1]; e++) {
+      const unsigned long long c = a.c_ctr[e];
+      lo += c;
+      hi += lo < c;
+    }
+    a.sum_hi[i] = hi;
+    a.sum_lo[i] = lo;
+    a.alive[i] = a.cbeg[i + 1] > a.cbeg[i];  // MVReg::apply ignores an empty clock
+  }
+}
+
+struct MvKey {
+  unsigned long long hi, lo, prio;
+  uint32_t idx;
+};
+
+__device__ __forceinline__ bool mv_better(const MvKey& x, const MvKey& y) {
+  if (x.idx == 0xffffffffu) return false;
+  if (y.idx == 0xffffffffu) return true;
+  if (x.hi != y.hi) return x.hi > y.hi;
+  if (x.lo != y.lo) return x.lo > y.lo;
+  return x.prio > y.prio;
+}
+
+__device__ MvKey mv_block_reduce(MvKey k) {
+  __shared__ unsigned long long sh[kBlock], sl[kBlock], sp[kBlock];
+  __shared__ uint32_t si[kBlock];
+  sh[threadIdx.x] = k.hi;
+  sl[threadIdx.x] = k.lo;
+  sp[threadIdx.x] = k.prio;
+  si[threadIdx.x] = k.idx;
+  __syncthreads();
+  for (int w = kBlock / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      MvKey x{sh[threadIdx.x], sl[threadIdx.x], sp[threadIdx.x], si[threadIdx.x]};
+      MvKey y{sh[threadIdx.x + w], sl[threadIdx.x + w], sp[threadIdx.x + w], si[threadIdx.x + w]};
+      if (mv_better(y, x)) {
+        sh[threadIdx.x] = y.hi;
+        sl[threadIdx.x] = y.lo;
+        sp[threadIdx.x] = y.prio;
+        si[threadIdx.x] = y.idx;
+      }
+    }
+    __syncthreads();
+  }
+  return MvKey{sh[0], sl[0], sp[0], si[0]};
+}
+
+__global__ void __launch_bounds__(kBlock) k_mv_argmax(MvArgs a) {
+  MvKey best{0, 0, 0, 0xffffffffu};
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < a.n; i += gridDim.x * kBlock) {
+    if (!a.alive[i]) continue;
+    MvKey k{a.sum_hi[i], a.sum_lo[i], a.later_wins ? i : (unsigned long long)(a.n - 1 - i), i};
+    if (mv_better(k, best)) best = k;
+  }
+  best = mv_block_reduce(best);
+  if (threadIdx.x == 0) {
+    a.blk[4 * blockIdx.x + 0] = best.hi;
+    a.blk[4 * blockIdx.x + 1] = best.lo;
+    a.blk[4 * blockIdx.x + 2] = best.prio;
+    a.blk[4 * blockIdx.x + 3] = best.idx;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_mv_final(MvArgs a) {
+  MvKey best{0, 0, 0, 0xffffffffu};
+  for (uint32_t b = threadIdx.x; b < a.n_blk; b += kBlock) {
+    MvKey k{a.blk[4 * b], a.blk[4 * b + 1], a.blk[4 * b + 2], (uint32_t)a.blk[4 * b + 3]};
+    if (mv_better(k, best)) best = k;
+  }
+  best = mv_block_reduce(best);
+  if (threadIdx.x == 0) a.win[0] = best.idx;
+  if (best.idx == 0xffffffffu) return;
+  // winner clock -> dense
+  for (uint32_t e = a.cbeg[best.idx] + threadIdx.x; e < a.cbeg[best.idx + 1]; e += kBlock)
+    a.wclock[a.c_actor[e]] = a.c_ctr[e];
+}
+
+// candidates whose clock is <= the winner's (equal included) are dominated
+__global__ void k_mv_kill(MvArgs a) {
+  const uint32_t w = a.win[0];
+  if (w == 0xffffffffu) return;
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < a.n; i += gridDim.x * kBlock) {
+    if (!a.alive[i]) continue;
+    bool le = true;
+    for (uint32_t e = a.cbeg[i]; e < a.cbeg[i + 1] && le; e++) le = a.c_ctr[e] <= a.wclock[a.c_actor[e]];
+    if (le) a.alive[i] = 0;
+  }
+}
+
+__global__ void k_mv_clear(MvArgs a) {
+  const uint32_t w = a.win[0];
+  if (w == 0xffffffffu) return;
+  for (uint32_t e = a.cbeg[w] + threadIdx.x; e < a.cbeg[w + 1]; e += kBlock) a.wclock[a.c_actor[e]] = 0;
+}
+
+}  // namespace
+
+namespace {
+struct MaxOp {
+  __host__ __device__ unsigned long long operator()(unsigned long long a, unsigned long long b) const {
+    return a > b ? a : b;
+  }
+};
+}  // namespace
+
+hipError_t ds_sort_pairs_u32(void* tmp, size_t& tb, const uint32_t* kin, uint32_t* kout,
+                             const uint32_t* vin, uint32_t* vout, uint32_t n, int bits, hipStream_t s) {
+  return hipcub::DeviceRadixSort::SortPairs(tmp, tb, kin, kout, vin, vout, (int)n, 0, bits, s);
+}
+
+hipError_t ds_sort_pairs_u64(void* tmp, size_t& tb, const unsigned long long* kin,
+                             unsigned long long* kout, const uint32_t* vin, uint32_t* vout,
+                             uint32_t n, hipStream_t s) {
+  return hipcub::DeviceRadixSort::SortPairs(tmp, tb, kin, kout, vin, vout, (int)n, 0, 64, s);
+}
+
+hipError_t ds_excl_max_by_key(void* tmp, size_t& tb, const uint32_t* keys,
+                              const unsigned long long* vals, unsigned long long* out, uint32_t n,
+                              hipStream_t s) {
+  return hipcub::DeviceScan::ExclusiveScanByKey(tmp, tb, keys, vals, out, MaxOp(), 0ull, (int)n,
+                                                hipcub::Equality(), s);
+}
+
+hipError_t ds_excl_sum_u32(void* tmp, size_t& tb, const uint32_t* in, uint32_t* out, uint32_t n,
+                           hipStream_t s) {
+  return hipcub::DeviceScan::ExclusiveSum(tmp, tb, in, out, (int)n, s);
+}
+
+hipError_t launch_ds_count(hipStream_t s, const DsDecodeArgs& a) {
+  if (a.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ds_count, dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_ds_emit(hipStream_t s, const DsDecodeArgs& a) {
+  if (a.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ds_emit, dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_ds_iota(hipStream_t s, uint32_t* v, uint32_t n) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ds_iota, dim3(blocks_for(n)), dim3(kBlock), 0, s, v, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_ds_gather_ctr(hipStream_t s, const uint32_t* perm, const unsigned long long* ctr,
+                                unsigned long long* out, uint32_t n) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ds_gather_ctr, dim3(blocks_for(n)), dim3(kBlock), 0, s, perm, ctr, out, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_ds_applied(hipStream_t s, const uint32_t* keys_sorted, const uint32_t* perm,
+                             const unsigned long long* ctr_sorted,
+                             const unsigned long long* excl_max, const unsigned long long* clock,
+                             uint8_t* applied, uint32_t n) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ds_applied, dim3(blocks_for(n)), dim3(kBlock), 0, s, keys_sorted, perm,
+                     ctr_sorted, excl_max, clock, applied, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_ds_clock(hipStream_t s, const uint32_t* add_actor, const unsigned long long* add_ctr,
+                           unsigned long long* clock, uint32_t n_add) {
+  if (n_add == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ds_clock, dim3(blocks_for(n_add)), dim3(kBlock), 0, s, add_actor, add_ctr,
+                     clock, n_add);
+  return hipGetLastError();
+}
+
+hipError_t launch_ds_add_pairs(hipStream_t s, DsTables t, DsOps o, const uint8_t* applied,
+                               uint32_t n_add) {
+  if (n_add == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ds_add_pairs, dim3(blocks_for(n_add)), dim3(kBlock), 0, s, t, o, applied, n_add);
+  return hipGetLastError();
+}
+
+hipError_t launch_ds_kill(hipStream_t s, DsTables t, const uint32_t* cbeg, const uint32_t* mbeg,
+                          const uint32_t* c_actor, const unsigned long long* c_ctr,
+                          const unsigned long long* mem, uint32_t n_rm) {
+  if (n_rm == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ds_kill, dim3(blocks_for(n_rm)), dim3(kBlock), 0, s, t, cbeg, mbeg, c_actor,
+                     c_ctr, mem, n_rm);
+  return hipGetLastError();
+}
+
+hipError_t launch_ds_finalize(hipStream_t s, DsTables t) {
+  hipLaunchKernelGGL(k_ds_finalize, dim3(blocks_for((uint64_t)t.pmask + 1, 2048)), dim3(kBlock), 0, s, t);
+  return hipGetLastError();
+}
+
+hipError_t launch_ds_deferred(hipStream_t s, const uint32_t* cbeg, const uint32_t* c_actor,
+                              const unsigned long long* c_ctr, const unsigned long long* clock,
+                              uint8_t* deferred, uint32_t n_rm) {
+  if (n_rm == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ds_deferred, dim3(blocks_for(n_rm)), dim3(kBlock), 0, s, cbeg, c_actor, c_ctr,
+                     clock, deferred, n_rm);
+  return hipGetLastError();
+}
+
+hipError_t launch_ds_put_other(hipStream_t s, DsTables t, const unsigned long long* member,
+                               const uint32_t* actor, const unsigned long long* value, uint32_t n) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ds_put_other, dim3(blocks_for(n)), dim3(kBlock), 0, s, t, member, actor, value, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_ds_merge(hipStream_t s, DsTables t, const unsigned long long* clock,
+                           const unsigned long long* oclock) {
+  hipLaunchKernelGGL(k_ds_merge, dim3(blocks_for((uint64_t)t.pmask + 1)), dim3(kBlock), 0, s, t, clock, oclock);
+  return hipGetLastError();
+}
+
+hipError_t launch_ds_collect(hipStream_t s, DsTables t, unsigned long long* member, uint32_t* actor,
+                             unsigned long long* value, uint32_t* n_out) {
+  hipLaunchKernelGGL(k_ds_collect, dim3(blocks_for((uint64_t)t.pmask + 1, 2048)), dim3(kBlock), 0, s, t,
+                     member, actor, value, n_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_ds_reinsert(hipStream_t s, DsTables t, const unsigned long long* member,
+                              const uint32_t* actor, const unsigned long long* value, uint32_t n) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ds_reinsert, dim3(blocks_for(n)), dim3(kBlock), 0, s, t, member, actor, value, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_ds_gather_entries(hipStream_t s, const uint32_t* perm, const uint32_t* actor_in,
+                                    const unsigned long long* value_in, uint32_t* actor_out,
+                                    unsigned long long* value_out, uint32_t n) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ds_gather_entries, dim3(blocks_for(n)), dim3(kBlock), 0, s, perm, actor_in,
+                     value_in, actor_out, value_out, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_mv_prep(hipStream_t s, const MvArgs& a) {
+  if (a.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_mv_prep, dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_mv_round(hipStream_t s, const MvArgs& a) {
+  hipLaunchKernelGGL(k_mv_argmax, dim3(a.n_blk), dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL(k_mv_final, dim3(1), dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL(k_mv_kill, dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL(k_mv_clear, dim3(1), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace ce

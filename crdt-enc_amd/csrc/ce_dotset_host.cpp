@@ -1,0 +1,1236 @@
+// ce_dotset_host.cpp -- Core<S> for the dot-set kinds S = Orswot<u64, Uuid> and MVReg<u64, Uuid>
+// (crdts 7), driving the kernels of ce_dotset.hip.
+//
+//   read_remote_ops   (crdt-enc/src/lib.rs:471-547)  GPU open -> version gate -> device decode of
+//                     Vec<S::Op> into columnar arrays -> data-parallel fold (Orswot: applied
+//                     flags by a stable sort + segmented max scan, pair-table max-insert,
+//                     removal thresholds; MVReg: maximal-clock rounds)
+//   read_remote_states (lib.rs:401-469)  GPU open -> host flatten of StateWrapper<S> -> per-pair
+//                     Orswot::merge kernel (MVReg: survivor rounds with earlier-wins ties)
+//   apply_ops         (lib.rs:666-722)   host parse of the local ops -> the same GPU fold
+//
+// The deferred removals of an Orswot and the values of an MVReg are small and live on the host;
+// the entries (member -> VClock) live in HBM in the member / pair tables of ce_dotset.h.
+#include <algorithm>
+#include <cstdio>
+#include <map>
+#include <set>
+
+#include "ce_core.h"
+#include "ce_dotset.h"
+#include "ce_dotset_codec.h"
+
+namespace ce {
+
+using IdDots = std::vector<std::pair<uint32_t, uint64_t>>;  // (actor id, counter), ids ascending
+
+struct DsState {
+  int kind = CE_STATE_ORSWOT;
+  // Orswot
+  DevBuf clock;  // u64[clock_cap] by actor id
+  uint32_t clock_cap = 0;
+  DevBuf mkey, pkey, cur, add, kill, oth, live;
+  uint32_t pcap = 0;  // member table and pair table share the capacity (members <= pairs)
+  uint64_t used_pairs = 0, live_pairs = 0;
+  std::map<IdDots, std::set<uint64_t>> deferred;  // removal clock -> members (HashMap in crdts)
+  // MVReg
+  std::vector<std::pair<IdDots, uint64_t>> vals;
+  // scratch
+  DevBuf cnt, ops[10], applied, sort_keys, sort_perm, sort_keys2, sort_perm2, ctr_sorted, excl,
+      cub_tmp, deferred_flags, d0[5], col[6], mv[6], other[4], oclock;
+  DevBuf misses;
+  HostBuf h_cnt;
+};
+
+void ds_free(DsState* d) { delete d; }
+
+namespace {
+
+constexpr uint32_t kMissCap = 65536;
+
+uint32_t pow2_at_least(uint64_t v) {
+  uint64_t p = 1;
+  while (p < v) p <<= 1;
+  return (uint32_t)p;
+}
+
+int bits_for(uint32_t v) {
+  int b = 1;
+  while (b < 32 && (1ull << b) <= v) b++;
+  return b;
+}
+
+DsTables tables(DsState* d) {
+  DsTables t;
+  t.mkey = d->mkey.as<unsigned long long>();
+  t.mmask = d->pcap - 1;
+  t.pkey = d->pkey.as<unsigned long long>();
+  t.cur = d->cur.as<unsigned long long>();
+  t.add = d->add.as<unsigned long long>();
+  t.kill = d->kill.as<unsigned long long>();
+  t.oth = d->oth.as<unsigned long long>();
+  t.pmask = d->pcap - 1;
+  t.live = d->live.as<uint32_t>();
+  return t;
+}
+
+int tables_alloc(ce_core* c, uint32_t cap) {
+  DsState* d = c->ds;
+  ce_ctx* ctx = c->ctx;
+  hipError_t e;
+  if ((e = d->mkey.reserve((cap + 1ull) * 8)) || (e = d->pkey.reserve(cap * 8ull)) ||
+      (e = d->cur.reserve(cap * 8ull)) || (e = d->add.reserve(cap * 8ull)) ||
+      (e = d->kill.reserve(cap * 8ull)) || (e = d->oth.reserve(cap * 8ull)) ||
+      (e = d->live.reserve(64)))
+    return ctx->hip_fail(e, "dot-set tables");
+  d->pcap = cap;
+  if ((e = hipMemsetAsync(d->mkey.p, 0xff, (cap + 1ull) * 8, ctx->stream)) ||
+      (e = hipMemsetAsync(d->pkey.p, 0xff, cap * 8ull, ctx->stream)) ||
+      (e = hipMemsetAsync(d->cur.p, 0, cap * 8ull, ctx->stream)) ||
+      (e = hipMemsetAsync(d->add.p, 0, cap * 8ull, ctx->stream)) ||
+      (e = hipMemsetAsync(d->kill.p, 0, cap * 8ull, ctx->stream)) ||
+      (e = hipMemsetAsync(d->oth.p, 0, cap * 8ull, ctx->stream)) ||
+      (e = hipMemsetAsync(d->live.p, 0, 64, ctx->stream)))
+    return ctx->hip_fail(e, "dot-set tables");
+  d->used_pairs = 0;
+  d->live_pairs = 0;
+  return CE_OK;
+}
+
+int ensure_clock(ce_core* c) {
+  DsState* d = c->ds;
+  const uint32_t need = std::max<uint32_t>(1024, (uint32_t)c->id_actor.size());
+  if (need <= d->clock_cap) return CE_OK;
+  const uint32_t cap = pow2_at_least(need);
+  DevBuf nb;
+  hipError_t e;
+  if ((e = nb.reserve(cap * 8ull)) || (e = hipMemsetAsync(nb.p, 0, cap * 8ull, c->ctx->stream)) ||
+      (d->clock_cap && (e = hipMemcpyAsync(nb.p, d->clock.p, d->clock_cap * 8ull,
+                                           hipMemcpyDeviceToDevice, c->ctx->stream))) ||
+      (e = hipStreamSynchronize(c->ctx->stream)))
+    return c->ctx->hip_fail(e, "clock");
+  std::swap(d->clock.p, nb.p);
+  std::swap(d->clock.cap, nb.cap);
+  d->clock_cap = cap;
+  if ((e = d->oclock.reserve(cap * 8ull))) return c->ctx->hip_fail(e, "clock");
+  return CE_OK;
+}
+
+// live entries -> (member, actor id, value) columns in d->col[0..2]; returns the count
+int collect(ce_core* c, uint32_t* n_live) {
+  DsState* d = c->ds;
+  ce_ctx* ctx = c->ctx;
+  const uint64_t cap = d->pcap;
+  hipError_t e;
+  if ((e = d->col[0].reserve(cap * 8 + 64)) || (e = d->col[1].reserve(cap * 4 + 64)) ||
+      (e = d->col[2].reserve(cap * 8 + 64)) || (e = d->col[5].reserve(64)))
+    return ctx->hip_fail(e, "collect");
+  uint32_t* cnt = d->col[5].as<uint32_t>();
+  if ((e = hipMemsetAsync(cnt, 0, 4, ctx->stream)) ||
+      (e = launch_ds_collect(ctx->stream, tables(d), d->col[0].as<unsigned long long>(),
+                             d->col[1].as<uint32_t>(), d->col[2].as<unsigned long long>(), cnt)) ||
+      (e = hipMemcpyAsync(n_live, cnt, 4, hipMemcpyDeviceToHost, ctx->stream)) ||
+      (e = hipStreamSynchronize(ctx->stream)))
+    return ctx->hip_fail(e, "collect");
+  return CE_OK;
+}
+
+// make room for `extra` new pairs at <= 50% load: rebuild from the live entries when needed
+int ensure_pairs(ce_core* c, uint64_t extra) {
+  DsState* d = c->ds;
+  if ((d->used_pairs + extra) * 2 <= d->pcap) return CE_OK;
+  uint32_t n_live = 0;
+  int rc = collect(c, &n_live);
+  if (rc) return rc;
+  const uint32_t cap = pow2_at_least(std::max<uint64_t>(4096, 2 * (n_live + extra) + 1));
+  // the collected columns survive the reallocation of the tables
+  if ((rc = tables_alloc(c, cap))) return rc;
+  hipError_t e;
+  if ((e = launch_ds_reinsert(c->ctx->stream, tables(d), d->col[0].as<unsigned long long>(),
+                              d->col[1].as<uint32_t>(), d->col[2].as<unsigned long long>(), n_live)))
+    return c->ctx->hip_fail(e, "rebuild");
+  d->used_pairs = n_live;
+  d->live_pairs = n_live;
+  return CE_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// host-side op decoding (local apply_ops, and op vectors the device defers to the host:
+// unsorted clocks, nesting beyond the device parser's stack)
+// ---------------------------------------------------------------------------------------
+struct HostOp {
+  int type = 0;             // 0 Add / Put, 1 Rm
+  Uuid dot_actor{};
+  uint64_t dot_ctr = 0;
+  Dots clock;               // Rm / Put clock, BTreeMap semantics (sorted, later duplicate wins)
+  std::vector<uint64_t> members;
+  uint64_t val = 0;
+};
+
+// externally tagged enum: map(1) {name | index: body}
+bool read_variant(Rd& r, const std::vector<const char*>& names, int* v) {
+  uint64_t cnt;
+  if (r.i >= r.n || !is_map_marker(r.p[r.i]) || !rd_map_hdr(r, &cnt) || cnt != 1) return false;
+  if (r.i >= r.n) return false;
+  if (is_binstr_marker(r.p[r.i])) {
+    int kind;
+    uint64_t off, l;
+    if (!rd_binstr(r, &kind, &off, &l)) return false;
+    for (size_t j = 0; j < names.size(); j++)
+      if (std::strlen(names[j]) == l && std::memcmp(names[j], r.p + off, l) == 0) { *v = (int)j; return true; }
+    return false;
+  }
+  uint64_t x;
+  if (!rd_u64(r, &x) || x >= names.size()) return false;
+  *v = (int)x;
+  return true;
+}
+
+bool read_members(Rd& r, std::vector<uint64_t>* out) {
+  uint64_t cnt, m;
+  if (r.i >= r.n || !is_array_marker(r.p[r.i]) || !rd_array_hdr(r, &cnt) || cnt > r.n - r.i) return false;
+  for (uint64_t k = 0; k < cnt; k++) {
+    if (!rd_u64(r, &m)) return false;
+    out->push_back(m);
+  }
+  return true;
+}
+
+void sort_dots(Dots* d) {
+  std::sort(d->begin(), d->end(), [](const std::pair<Uuid, uint64_t>& a, const std::pair<Uuid, uint64_t>& b) {
+    return a.first < b.first;
+  });
+}
+
+bool parse_ops_host(int kind, const uint8_t* p, size_t n, std::vector<HostOp>* out) {
+  Rd r{p, n, 0};
+  uint64_t cnt;
+  if (r.n == 0 || !is_array_marker(r.p[0]) || !rd_array_hdr(r, &cnt) || cnt > r.n) return false;
+  for (uint64_t k = 0; k < cnt; k++) {
+    HostOp op;
+    int v;
+    if (kind == CE_STATE_ORSWOT) {
+      if (!read_variant(r, {"Add", "Rm"}, &v)) return false;
+      op.type = v;
+      bool ok;
+      if (v == 0) {
+        ok = read_struct(r, {"dot", "members"}, [&](int f, Rd& q) {
+          if (f == 1) return read_members(q, &op.members);
+          return read_struct(q, {"actor", "counter"}, [&](int g, Rd& s) {
+            if (g == 1) return rd_u64(s, &op.dot_ctr);
+            uint64_t off;
+            if (!rd_uuid(s, &off)) return false;
+            std::memcpy(op.dot_actor.data(), s.p + off, 16);
+            return true;
+          });
+        });
+      } else {
+        ok = read_struct(r, {"clock", "members"}, [&](int f, Rd& q) {
+          if (f == 1) return read_members(q, &op.members);
+          return read_vclock(q, &op.clock);
+        });
+      }
+      if (!ok) return false;
+    } else {
+      if (!read_variant(r, {"Put"}, &v)) return false;
+      if (!read_struct(r, {"clock", "val"}, [&](int f, Rd& q) {
+            if (f == 0) return read_vclock(q, &op.clock);
+            return rd_u64(q, &op.val);
+          }))
+        return false;
+    }
+    sort_dots(&op.clock);
+    out->push_back(std::move(op));
+  }
+  return true;
+}
+
+// compact canonical re-encoding (structs as arrays, variants as indices, minimal integers,
+// sorted clocks): never longer than any accepted input form of the same ops
+void encode_ops_compact(int kind, const std::vector<HostOp>& ops, Wr* w) {
+  w->arr(ops.size());
+  auto vclock = [&](const Dots& d) {
+    w->arr(1);
+    w->map(d.size());
+    for (auto& x : d) { w->bin(x.first.data(), 16); w->uint(x.second); }
+  };
+  auto members = [&](const std::vector<uint64_t>& m) {
+    w->arr(m.size());
+    for (uint64_t x : m) w->uint(x);
+  };
+  for (auto& op : ops) {
+    w->map(1);
+    w->uint(kind == CE_STATE_ORSWOT ? (uint64_t)op.type : 0);
+    w->arr(2);
+    if (kind == CE_STATE_ORSWOT && op.type == 0) {
+      w->arr(2);
+      w->bin(op.dot_actor.data(), 16);
+      w->uint(op.dot_ctr);
+      members(op.members);
+    } else if (kind == CE_STATE_ORSWOT) {
+      vclock(op.clock);
+      members(op.members);
+    } else {
+      vclock(op.clock);
+      w->uint(op.val);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// columnar batches
+// ---------------------------------------------------------------------------------------
+struct Counts {
+  uint64_t v[kCntN] = {0, 0, 0, 0, 0};
+};
+
+int reserve_ops(ce_core* c, const Counts& k) {
+  DsState* d = c->ds;
+  hipError_t e;
+  const uint64_t na = k.v[kCntAdd] + 1, nam = k.v[kCntAddM] + 1, nr = k.v[kCntRm] + 1,
+                 nrc = k.v[kCntRmC] + 1, nrm = k.v[kCntRmM] + 1;
+  if ((e = d->ops[0].reserve(na * 4)) || (e = d->ops[1].reserve(na * 8)) ||
+      (e = d->ops[2].reserve(na * 4)) || (e = d->ops[3].reserve(nam * 8)) ||
+      (e = d->ops[4].reserve(nr * 4)) || (e = d->ops[5].reserve(nr * 4)) ||
+      (e = d->ops[6].reserve(nrc * 4)) || (e = d->ops[7].reserve(nrc * 8)) ||
+      (e = d->ops[8].reserve(nrm * 8)) || (e = d->ops[9].reserve(nr * 8)))
+    return c->ctx->hip_fail(e, "ops reserve");
+  return CE_OK;
+}
+
+DsOps ops_view(DsState* d) {
+  DsOps o;
+  o.add_actor = d->ops[0].as<uint32_t>();
+  o.add_ctr = d->ops[1].as<unsigned long long>();
+  o.add_mbeg = d->ops[2].as<uint32_t>();
+  o.add_mem = d->ops[3].as<unsigned long long>();
+  o.rm_cbeg = d->ops[4].as<uint32_t>();
+  o.rm_mbeg = d->ops[5].as<uint32_t>();
+  o.rmc_actor = d->ops[6].as<uint32_t>();
+  o.rmc_ctr = d->ops[7].as<unsigned long long>();
+  o.rm_mem = d->ops[8].as<unsigned long long>();
+  o.put_val = d->ops[9].as<unsigned long long>();
+  return o;
+}
+
+// write the CSR end sentinels: add_mbeg[n_add], rm_cbeg[n_rm], rm_mbeg[n_rm]
+int write_sentinels(ce_core* c, const Counts& k) {
+  DsState* d = c->ds;
+  DsOps o = ops_view(d);
+  uint32_t* h = d->h_cnt.as<uint32_t>() + 16;
+  h[0] = (uint32_t)k.v[kCntAddM];
+  h[1] = (uint32_t)k.v[kCntRmC];
+  h[2] = (uint32_t)k.v[kCntRmM];
+  hipError_t e;
+  if ((e = hipMemcpyAsync(o.add_mbeg + k.v[kCntAdd], h + 0, 4, hipMemcpyHostToDevice, c->ctx->stream)) ||
+      (e = hipMemcpyAsync(o.rm_cbeg + k.v[kCntRm], h + 1, 4, hipMemcpyHostToDevice, c->ctx->stream)) ||
+      (e = hipMemcpyAsync(o.rm_mbeg + k.v[kCntRm], h + 2, 4, hipMemcpyHostToDevice, c->ctx->stream)) ||
+      (e = hipStreamSynchronize(c->ctx->stream)))
+    return c->ctx->hip_fail(e, "sentinels");
+  return CE_OK;
+}
+
+// host ops -> columnar arrays at the given offsets (ids must exist).  Orswot adds/removals or
+// MVReg puts.
+struct HostCols {
+  std::vector<uint32_t> add_actor, add_mbeg, rm_cbeg, rm_mbeg, rmc_actor;
+  std::vector<unsigned long long> add_ctr, add_mem, rmc_ctr, rm_mem, put_val;
+};
+
+int host_cols(ce_core* c, const std::vector<HostOp>& ops, const Counts& base, HostCols* hc) {
+  for (auto& op : ops) {
+    if (c->kind == CE_STATE_ORSWOT && op.type == 0) {
+      uint32_t s;
+      int rc = insert_actor(c, op.dot_actor, &s);
+      if (rc) return rc;
+      hc->add_mbeg.push_back((uint32_t)(base.v[kCntAddM] + hc->add_mem.size()));
+      hc->add_actor.push_back(actor_id_of_slot(c, s));
+      hc->add_ctr.push_back(op.dot_ctr);
+      for (uint64_t m : op.members) hc->add_mem.push_back(m);
+    } else {
+      hc->rm_cbeg.push_back((uint32_t)(base.v[kCntRmC] + hc->rmc_actor.size()));
+      hc->rm_mbeg.push_back((uint32_t)(base.v[kCntRmM] + hc->rm_mem.size()));
+      for (auto& x : op.clock) {
+        uint32_t s;
+        int rc = insert_actor(c, x.first, &s);
+        if (rc) return rc;
+        hc->rmc_actor.push_back(actor_id_of_slot(c, s));
+        hc->rmc_ctr.push_back(x.second);
+      }
+      for (uint64_t m : op.members) hc->rm_mem.push_back(m);
+      hc->put_val.push_back(op.val);
+    }
+  }
+  return CE_OK;
+}
+
+template <typename T>
+hipError_t up(T* dst, const std::vector<T>& v, hipStream_t s) {
+  if (v.empty()) return hipSuccess;
+  return hipMemcpyAsync(dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s);
+}
+
+int upload_cols(ce_core* c, const HostCols& hc, const Counts& base) {
+  DsOps o = ops_view(c->ds);
+  hipStream_t s = c->ctx->stream;
+  hipError_t e;
+  if ((e = up(o.add_actor + base.v[kCntAdd], hc.add_actor, s)) ||
+      (e = up(o.add_ctr + base.v[kCntAdd], hc.add_ctr, s)) ||
+      (e = up(o.add_mbeg + base.v[kCntAdd], hc.add_mbeg, s)) ||
+      (e = up(o.add_mem + base.v[kCntAddM], hc.add_mem, s)) ||
+      (e = up(o.rm_cbeg + base.v[kCntRm], hc.rm_cbeg, s)) ||
+      (e = up(o.rm_mbeg + base.v[kCntRm], hc.rm_mbeg, s)) ||
+      (e = up(o.rmc_actor + base.v[kCntRmC], hc.rmc_actor, s)) ||
+      (e = up(o.rmc_ctr + base.v[kCntRmC], hc.rmc_ctr, s)) ||
+      (e = up(o.rm_mem + base.v[kCntRmM], hc.rm_mem, s)) ||
+      (e = up(o.put_val + base.v[kCntRm], hc.put_val, s)) || (e = hipStreamSynchronize(s)))
+    return c->ctx->hip_fail(e, "ops upload");
+  return CE_OK;
+}
+
+// deferred removals (host) -> CSR removal arrays in d->d0 (cbeg, mbeg, actor, ctr, members)
+int upload_removals(ce_core* c, const std::vector<std::pair<IdDots, std::vector<uint64_t>>>& rms) {
+  DsState* d = c->ds;
+  std::vector<uint32_t> cbeg{0}, mbeg{0}, act;
+  std::vector<unsigned long long> ctr, mem;
+  for (auto& r : rms) {
+    for (auto& x : r.first) { act.push_back(x.first); ctr.push_back(x.second); }
+    for (uint64_t m : r.second) mem.push_back(m);
+    cbeg.push_back((uint32_t)act.size());
+    mbeg.push_back((uint32_t)mem.size());
+  }
+  hipError_t e;
+  if ((e = d->d0[0].reserve(cbeg.size() * 4)) || (e = d->d0[1].reserve(mbeg.size() * 4)) ||
+      (e = d->d0[2].reserve(act.size() * 4 + 4)) || (e = d->d0[3].reserve(ctr.size() * 8 + 8)) ||
+      (e = d->d0[4].reserve(mem.size() * 8 + 8)))
+    return c->ctx->hip_fail(e, "removals");
+  hipStream_t s = c->ctx->stream;
+  if ((e = up(d->d0[0].as<uint32_t>(), cbeg, s)) || (e = up(d->d0[1].as<uint32_t>(), mbeg, s)) ||
+      (e = up(d->d0[2].as<uint32_t>(), act, s)) || (e = up(d->d0[3].as<unsigned long long>(), ctr, s)) ||
+      (e = up(d->d0[4].as<unsigned long long>(), mem, s)) || (e = hipStreamSynchronize(s)))
+    return c->ctx->hip_fail(e, "removals");
+  return CE_OK;
+}
+
+std::vector<std::pair<IdDots, std::vector<uint64_t>>> deferred_list(DsState* d) {
+  std::vector<std::pair<IdDots, std::vector<uint64_t>>> v;
+  for (auto& x : d->deferred) v.push_back({x.first, std::vector<uint64_t>(x.second.begin(), x.second.end())});
+  return v;
+}
+
+int flags_for(ce_core* c, const uint32_t* cbeg, const uint32_t* act, const unsigned long long* ctr,
+              uint32_t n_rm, std::vector<uint8_t>* flags) {
+  DsState* d = c->ds;
+  flags->assign(n_rm, 0);
+  if (!n_rm) return CE_OK;
+  hipError_t e;
+  if ((e = d->deferred_flags.reserve(n_rm + 64)) ||
+      (e = launch_ds_deferred(c->ctx->stream, cbeg, act, ctr, d->clock.as<unsigned long long>(),
+                              d->deferred_flags.as<uint8_t>(), n_rm)) ||
+      (e = hipMemcpyAsync(flags->data(), d->deferred_flags.p, n_rm, hipMemcpyDeviceToHost, c->ctx->stream)) ||
+      (e = hipStreamSynchronize(c->ctx->stream)))
+    return c->ctx->hip_fail(e, "deferred");
+  return CE_OK;
+}
+
+int finalize(ce_core* c) {
+  DsState* d = c->ds;
+  uint32_t h[4];
+  hipError_t e;
+  if ((e = hipMemsetAsync(d->live.p, 0, 8, c->ctx->stream)) ||
+      (e = launch_ds_finalize(c->ctx->stream, tables(d))) ||
+      (e = hipMemcpyAsync(h, d->live.p, 16, hipMemcpyDeviceToHost, c->ctx->stream)) ||
+      (e = hipStreamSynchronize(c->ctx->stream)))
+    return c->ctx->hip_fail(e, "finalize");
+  if (h[2]) return c->ctx->fail(CE_ERR_DEVICE, "dot-set table overflow");
+  d->live_pairs = h[0];
+  d->used_pairs = h[1];
+  return CE_OK;
+}
+
+// Orswot fold of a columnar batch in application order (k = counts); the removals of the
+// batch plus the current deferred set (re-applied by apply_deferred) set the thresholds.
+int orswot_fold(ce_core* c, const Counts& k) {
+  DsState* d = c->ds;
+  ce_ctx* ctx = c->ctx;
+  hipStream_t s = ctx->stream;
+  DsOps o = ops_view(d);
+  hipError_t e;
+  int rc;
+  if ((rc = ensure_clock(c))) return rc;
+  const uint32_t na = (uint32_t)k.v[kCntAdd], nr = (uint32_t)k.v[kCntRm];
+  // 1) applied flags: stable sort of the adds by actor, segmented exclusive max of counters
+  if ((e = d->applied.reserve(na + 64))) return ctx->hip_fail(e, "applied");
+  if (na) {
+    if ((e = d->sort_keys.reserve(na * 4ull)) || (e = d->sort_perm.reserve(na * 4ull)) ||
+        (e = d->sort_keys2.reserve(na * 4ull)) || (e = d->sort_perm2.reserve(na * 4ull)) ||
+        (e = d->ctr_sorted.reserve(na * 8ull)) || (e = d->excl.reserve(na * 8ull)))
+      return ctx->hip_fail(e, "applied");
+    const int bits = bits_for((uint32_t)c->id_actor.size());
+    size_t t1 = 0, t2 = 0;
+    uint32_t* keys2 = d->sort_keys2.as<uint32_t>();
+    uint32_t* perm = d->sort_perm.as<uint32_t>();
+    uint32_t* perm2 = d->sort_perm2.as<uint32_t>();
+    unsigned long long* cs = d->ctr_sorted.as<unsigned long long>();
+    unsigned long long* ex = d->excl.as<unsigned long long>();
+    if ((e = ds_sort_pairs_u32(nullptr, t1, o.add_actor, keys2, perm, perm2, na, bits, s)) ||
+        (e = ds_excl_max_by_key(nullptr, t2, keys2, cs, ex, na, s)))
+      return ctx->hip_fail(e, "applied");
+    if ((e = d->cub_tmp.reserve(std::max(t1, t2) + 256))) return ctx->hip_fail(e, "applied");
+    t1 = t2 = d->cub_tmp.cap;
+    if ((e = launch_ds_iota(s, perm, na)) ||
+        (e = ds_sort_pairs_u32(d->cub_tmp.p, t1, o.add_actor, keys2, perm, perm2, na, bits, s)) ||
+        (e = launch_ds_gather_ctr(s, perm2, o.add_ctr, cs, na)) ||
+        (e = ds_excl_max_by_key(d->cub_tmp.p, t2, keys2, cs, ex, na, s)) ||
+        (e = launch_ds_applied(s, keys2, perm2, cs, ex, d->clock.as<unsigned long long>(),
+                               d->applied.as<uint8_t>(), na)))
+      return ctx->hip_fail(e, "applied");
+  }
+  // 2) entries: max-insert the applied adds (capacity for every add member)
+  if ((rc = ensure_pairs(c, k.v[kCntAddM]))) return rc;
+  if ((e = launch_ds_add_pairs(s, tables(d), o, d->applied.as<uint8_t>(), na)) ||
+      (e = launch_ds_clock(s, o.add_actor, o.add_ctr, d->clock.as<unsigned long long>(), na)))
+    return ctx->hip_fail(e, "add");
+  // 3) removal thresholds: the batch's removals and the deferred set
+  auto d0 = deferred_list(d);
+  if ((rc = upload_removals(c, d0))) return rc;
+  const uint32_t n0 = (uint32_t)d0.size();
+  if ((e = launch_ds_kill(s, tables(d), o.rm_cbeg, o.rm_mbeg, o.rmc_actor, o.rmc_ctr, o.rm_mem, nr)) ||
+      (e = launch_ds_kill(s, tables(d), d->d0[0].as<uint32_t>(), d->d0[1].as<uint32_t>(),
+                          d->d0[2].as<uint32_t>(), d->d0[3].as<unsigned long long>(),
+                          d->d0[4].as<unsigned long long>(), n0)))
+    return ctx->hip_fail(e, "kill");
+  if ((rc = finalize(c))) return rc;
+  // 4) deferred = removals whose clock is not covered by the new clock
+  std::vector<uint8_t> f_batch, f_d0;
+  if ((rc = flags_for(c, o.rm_cbeg, o.rmc_actor, o.rmc_ctr, nr, &f_batch)) ||
+      (rc = flags_for(c, d->d0[0].as<uint32_t>(), d->d0[2].as<uint32_t>(),
+                      d->d0[3].as<unsigned long long>(), n0, &f_d0)))
+    return rc;
+  std::map<IdDots, std::set<uint64_t>> nd;
+  for (uint32_t i = 0; i < n0; i++)
+    if (f_d0[i]) nd[d0[i].first].insert(d0[i].second.begin(), d0[i].second.end());
+  bool any = false;
+  for (uint8_t f : f_batch) any = any || f;
+  if (any) {
+    std::vector<uint32_t> cb(nr + 1), mb(nr + 1), act(k.v[kCntRmC]);
+    std::vector<unsigned long long> ctr(k.v[kCntRmC]), mem(k.v[kCntRmM]);
+    if ((e = hipMemcpyAsync(cb.data(), o.rm_cbeg, (nr + 1) * 4ull, hipMemcpyDeviceToHost, s)) ||
+        (e = hipMemcpyAsync(mb.data(), o.rm_mbeg, (nr + 1) * 4ull, hipMemcpyDeviceToHost, s)) ||
+        (!act.empty() && (e = hipMemcpyAsync(act.data(), o.rmc_actor, act.size() * 4, hipMemcpyDeviceToHost, s))) ||
+        (!ctr.empty() && (e = hipMemcpyAsync(ctr.data(), o.rmc_ctr, ctr.size() * 8, hipMemcpyDeviceToHost, s))) ||
+        (!mem.empty() && (e = hipMemcpyAsync(mem.data(), o.rm_mem, mem.size() * 8, hipMemcpyDeviceToHost, s))) ||
+        (e = hipStreamSynchronize(s)))
+      return ctx->hip_fail(e, "deferred download");
+    for (uint32_t r = 0; r < nr; r++) {
+      if (!f_batch[r]) continue;
+      IdDots key;
+      for (uint32_t j = cb[r]; j < cb[r + 1]; j++) key.push_back({act[j], ctr[j]});
+      std::sort(key.begin(), key.end());
+      auto& set = nd[key];
+      for (uint32_t j = mb[r]; j < mb[r + 1]; j++) set.insert(mem[j]);
+    }
+  }
+  d->deferred = std::move(nd);
+  return CE_OK;
+}
+
+// MVReg survivors among n candidates already in ops rm_cbeg/rmc_*/put_val; returns indices in
+// ascending (insertion) order
+int mvreg_survivors(ce_core* c, uint32_t n, bool later_wins, std::vector<uint32_t>* out) {
+  DsState* d = c->ds;
+  ce_ctx* ctx = c->ctx;
+  hipStream_t s = ctx->stream;
+  out->clear();
+  if (n == 0) return CE_OK;
+  int rc;
+  if ((rc = ensure_clock(c))) return rc;
+  DsOps o = ops_view(d);
+  MvArgs a{};
+  a.cbeg = o.rm_cbeg;
+  a.c_actor = o.rmc_actor;
+  a.c_ctr = o.rmc_ctr;
+  a.n = n;
+  a.later_wins = later_wins ? 1 : 0;
+  a.n_blk = std::min<uint32_t>(1024, (n + 255) / 256);
+  hipError_t e;
+  if ((e = d->mv[0].reserve(n + 64)) || (e = d->mv[1].reserve(n * 8ull)) || (e = d->mv[2].reserve(n * 8ull)) ||
+      (e = d->mv[3].reserve(a.n_blk * 32ull)) || (e = d->mv[4].reserve(64)) ||
+      (e = d->mv[5].reserve(d->clock_cap * 8ull)))
+    return ctx->hip_fail(e, "mvreg");
+  if (d->mv[5].cap < d->clock_cap * 8ull) return ctx->fail(CE_ERR_DEVICE, "mvreg scratch");
+  a.alive = d->mv[0].as<uint8_t>();
+  a.sum_hi = d->mv[1].as<unsigned long long>();
+  a.sum_lo = d->mv[2].as<unsigned long long>();
+  a.blk = d->mv[3].as<unsigned long long>();
+  a.win = d->mv[4].as<uint32_t>();
+  a.wclock = d->mv[5].as<unsigned long long>();
+  if ((e = hipMemsetAsync(a.wclock, 0, d->clock_cap * 8ull, s)) || (e = launch_mv_prep(s, a)))
+    return ctx->hip_fail(e, "mvreg");
+  for (uint32_t round = 0; round <= n; round++) {
+    uint32_t w;
+    if ((e = launch_mv_round(s, a)) || (e = hipMemcpyAsync(&w, a.win, 4, hipMemcpyDeviceToHost, s)) ||
+        (e = hipStreamSynchronize(s)))
+      return ctx->hip_fail(e, "mvreg round");
+    if (w == 0xffffffffu) break;
+    if (w >= n) return ctx->fail(CE_ERR_DEVICE, "mvreg winner out of range");
+    out->push_back(w);
+  }
+  std::sort(out->begin(), out->end());
+  return CE_OK;
+}
+
+// candidate i's clock and value (device) -> host
+int fetch_candidate(ce_core* c, uint32_t i, std::pair<IdDots, uint64_t>* v) {
+  DsOps o = ops_view(c->ds);
+  hipStream_t s = c->ctx->stream;
+  uint32_t cb[2];
+  hipError_t e;
+  if ((e = hipMemcpyAsync(cb, o.rm_cbeg + i, 8, hipMemcpyDeviceToHost, s)) ||
+      (e = hipMemcpyAsync(&v->second, o.put_val + i, 8, hipMemcpyDeviceToHost, s)) ||
+      (e = hipStreamSynchronize(s)))
+    return c->ctx->hip_fail(e, "candidate");
+  const uint32_t k = cb[1] - cb[0];
+  std::vector<uint32_t> act(k);
+  std::vector<unsigned long long> ctr(k);
+  if (k && ((e = hipMemcpyAsync(act.data(), o.rmc_actor + cb[0], k * 4ull, hipMemcpyDeviceToHost, s)) ||
+            (e = hipMemcpyAsync(ctr.data(), o.rmc_ctr + cb[0], k * 8ull, hipMemcpyDeviceToHost, s)) ||
+            (e = hipStreamSynchronize(s))))
+    return c->ctx->hip_fail(e, "candidate");
+  v->first.clear();
+  for (uint32_t j = 0; j < k; j++) v->first.push_back({act[j], ctr[j]});
+  std::sort(v->first.begin(), v->first.end());
+  return CE_OK;
+}
+
+// current MVReg values -> host columns (prefix of the candidate list)
+void vals_cols(DsState* d, HostCols* hc) {
+  for (auto& v : d->vals) {
+    hc->rm_cbeg.push_back((uint32_t)hc->rmc_actor.size());
+    hc->rm_mbeg.push_back(0);
+    for (auto& x : v.first) { hc->rmc_actor.push_back(x.first); hc->rmc_ctr.push_back(x.second); }
+    hc->put_val.push_back(v.second);
+  }
+}
+
+// MVReg: candidates = the K current values (prefix) then n_new more; survivors -> vals
+int mvreg_commit(ce_core* c, uint32_t K, uint32_t total, bool later_wins) {
+  DsState* d = c->ds;
+  std::vector<uint32_t> surv;
+  int rc = mvreg_survivors(c, total, later_wins, &surv);
+  if (rc) return rc;
+  std::vector<std::pair<IdDots, uint64_t>> nv;
+  for (uint32_t i : surv) {
+    if (i < K) { nv.push_back(d->vals[i]); continue; }
+    std::pair<IdDots, uint64_t> v;
+    if ((rc = fetch_candidate(c, i, &v))) return rc;
+    nv.push_back(std::move(v));
+  }
+  d->vals = std::move(nv);
+  return CE_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// version gate (lib.rs:519-538), device first, host for batches outside load_ops order
+// ---------------------------------------------------------------------------------------
+int gate(ce_core* c, const uint32_t* d_fa, const uint64_t* d_fv, uint32_t n, uint32_t m,
+         const std::vector<uint32_t>& wslot, uint32_t* first_gap, std::vector<uint64_t>* expect) {
+  ce_ctx* ctx = c->ctx;
+  hipError_t e;
+  if ((e = ctx->apply.reserve(n + 64)) || (e = c->d_gate.reserve(m * 24ull + 64)) ||
+      (e = ctx->h_stage2.reserve(m * 16ull + 64)))
+    return ctx->hip_fail(e, "gate reserve");
+  uint64_t* he0 = ctx->h_stage2.as<uint64_t>();
+  for (uint32_t a = 0; a < m; a++) he0[a] = c->nov[wslot[a]];
+  expect->assign(he0, he0 + m);
+  GateArgs ga{};
+  ga.fa = d_fa;
+  ga.fv = d_fv;
+  ga.n = n;
+  ga.m = m;
+  uint8_t* gbase = c->d_gate.as<uint8_t>();
+  ga.e0 = reinterpret_cast<const uint64_t*>(gbase);
+  ga.newnov = reinterpret_cast<unsigned long long*>(gbase + 8ull * m);
+  ga.run_count = reinterpret_cast<uint32_t*>(gbase + 16ull * m);
+  ga.run_first = reinterpret_cast<uint32_t*>(gbase + 20ull * m);
+  ga.flags = ctx->counters.as<uint32_t>() + 12;
+  ga.apply = ctx->apply.as<uint8_t>();
+  uint32_t hf[2];
+  if ((e = hipMemcpyAsync(gbase, he0, m * 8ull, hipMemcpyHostToDevice, ctx->stream)) ||
+      (e = hipMemsetAsync(gbase + 8ull * m, 0, 16ull * m, ctx->stream)) ||
+      (e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ga.flags), 0u, 1, ctx->stream)) ||
+      (e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ga.flags + 1), 0xffffffffu, 1, ctx->stream)))
+    return ctx->hip_fail(e, "gate");
+  const int t = ctx->tbegin("gate");
+  if ((e = launch_gate(ctx->stream, ga))) return ctx->hip_fail(e, "gate");
+  ctx->tend(t);
+  if ((e = hipMemcpyAsync(hf, ga.flags, 8, hipMemcpyDeviceToHost, ctx->stream)) ||
+      (e = hipStreamSynchronize(ctx->stream)))
+    return ctx->hip_fail(e, "gate");
+  if (hf[0]) {
+    std::vector<uint32_t> fa(n);
+    std::vector<uint64_t> fv(n);
+    std::vector<uint8_t> ap(n);
+    if ((e = hipMemcpyAsync(fa.data(), d_fa, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (e = hipMemcpyAsync(fv.data(), d_fv, n * 8ull, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+      return ctx->hip_fail(e, "host gate");
+    for (uint32_t i = 0; i < n; i++)
+      if (fa[i] >= m) return ctx->fail(CE_ERR_INVALID_ARG, "file_actor out of range");
+    *first_gap = host_gate(fa.data(), fv.data(), n, expect, ap.data());
+    if ((e = hipMemcpyAsync(ctx->apply.p, ap.data(), n, hipMemcpyHostToDevice, ctx->stream)) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+      return ctx->hip_fail(e, "host gate");
+    return CE_OK;
+  }
+  *first_gap = hf[1] == 0xffffffffu ? n : hf[1];
+  std::vector<uint64_t> nn(m);
+  if ((e = hipMemcpyAsync(nn.data(), gbase + 8ull * m, m * 8ull, hipMemcpyDeviceToHost, ctx->stream)) ||
+      (e = hipStreamSynchronize(ctx->stream)))
+    return ctx->hip_fail(e, "gate");
+  for (uint32_t a = 0; a < m; a++) (*expect)[a] = std::max((*expect)[a], nn[a]);
+  return CE_OK;
+}
+
+// files the device parser left to the host: re-encode compactly in place, patch the length
+int resolve_host_decode(ce_core* c, uint32_t n, std::vector<int32_t>* st) {
+  ce_ctx* ctx = c->ctx;
+  hipError_t e;
+  for (uint32_t i = 0; i < n; i++) {
+    if ((*st)[i] != kStatusHostDecode) continue;
+    FileParams P;
+    if ((e = hipMemcpy(&P, ctx->params.as<FileParams>() + i, sizeof P, hipMemcpyDeviceToHost)))
+      return ctx->hip_fail(e, "host decode");
+    std::vector<uint8_t> pt(P.len);
+    if ((e = hipMemcpy(pt.data(), ctx->out.as<uint8_t>() + P.out_off, P.len, hipMemcpyDeviceToHost)))
+      return ctx->hip_fail(e, "host decode");
+    std::vector<HostOp> ops;
+    int32_t s = CE_OK;
+    if (!parse_ops_host(c->kind, pt.data() + 16, pt.size() - 16, &ops)) {
+      s = CE_ERR_DECODE;
+    } else {
+      Wr w;
+      w.b.assign(pt.begin(), pt.begin() + 16);
+      encode_ops_compact(c->kind, ops, &w);
+      if (w.b.size() > pt.size()) return ctx->fail(CE_ERR_DEVICE, "compact op encoding grew");
+      FileParams NP = P;
+      NP.len = (uint32_t)w.b.size();
+      if ((e = hipMemcpy(ctx->out.as<uint8_t>() + P.out_off, w.b.data(), w.b.size(), hipMemcpyHostToDevice)) ||
+          (e = hipMemcpy(ctx->params.as<FileParams>() + i, &NP, sizeof NP, hipMemcpyHostToDevice)))
+        return ctx->hip_fail(e, "host decode");
+    }
+    (*st)[i] = s;
+    if ((e = hipMemcpy(ctx->status.as<int32_t>() + i, &s, 4, hipMemcpyHostToDevice)))
+      return ctx->hip_fail(e, "host decode");
+  }
+  return CE_OK;
+}
+
+DsDecodeArgs decode_args(ce_core* c, uint32_t n) {
+  ce_ctx* ctx = c->ctx;
+  DsState* d = c->ds;
+  DsDecodeArgs a{};
+  a.kind = c->kind == CE_STATE_ORSWOT ? kDsOrswot : kDsMVReg;
+  a.pt = ctx->out.as<uint8_t>();
+  a.params = ctx->params.as<FileParams>();
+  a.status = ctx->status.as<int32_t>();
+  a.n = n;
+  a.supported = c->d_supported.as<uint8_t>();
+  a.n_supported = (uint32_t)c->supported.size();
+  a.apply = ctx->apply.as<uint8_t>();
+  a.cnt = d->cnt.as<uint32_t>();
+  a.table = c->d_table.as<ActorSlot>();
+  a.mask = c->cap - 1;
+  a.ops = ops_view(d);
+  a.counters = d->misses.as<uint32_t>();
+  a.miss_list = reinterpret_cast<uint4*>(d->misses.as<uint8_t>() + 64);
+  a.miss_cap = kMissCap;
+  return a;
+}
+
+int fail_first(ce_core* c, const std::vector<int32_t>& st, int32_t* status_out, uint32_t n) {
+  if (status_out) std::memcpy(status_out, st.data(), n * 4ull);
+  for (uint32_t i = 0; i < n; i++)
+    if (st[i] != CE_OK) return st[i];
+  (void)c;
+  return CE_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+// entry points (ce_core.h)
+// ---------------------------------------------------------------------------------------
+int ds_init(ce_core* c) {
+  c->ds = new DsState();
+  c->ds->kind = c->kind;
+  hipError_t e;
+  if ((e = c->ds->misses.reserve(64 + kMissCap * 16ull)) || (e = c->ds->h_cnt.reserve(256)))
+    return c->ctx->hip_fail(e, "dot-set init");
+  int rc = ensure_clock(c);
+  if (rc) return rc;
+  return c->kind == CE_STATE_ORSWOT ? tables_alloc(c, 4096) : CE_OK;
+}
+
+int ds_reset(ce_core* c) {
+  DsState* d = c->ds;
+  d->deferred.clear();
+  d->vals.clear();
+  hipError_t e;
+  if (d->clock_cap && (e = hipMemsetAsync(d->clock.p, 0, d->clock_cap * 8ull, c->ctx->stream)))
+    return c->ctx->hip_fail(e, "reset");
+  if (c->kind == CE_STATE_ORSWOT) return tables_alloc(c, std::max<uint32_t>(4096, d->pcap));
+  return CE_OK;
+}
+
+int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
+                  uint64_t blob_len, const uint8_t* actors, uint32_t m, const uint32_t* d_fa,
+                  const uint64_t* d_fv, int32_t* status_out) {
+  ce_ctx* ctx = c->ctx;
+  DsState* d = c->ds;
+  hipError_t e;
+  int rc;
+  // writers get actor ids first (the gate is keyed by them)
+  std::vector<uint32_t> wslot(m);
+  for (uint32_t a = 0; a < m; a++) {
+    Uuid u;
+    std::memcpy(u.data(), actors + 16ull * a, 16);
+    if ((rc = insert_actor(c, u, &wslot[a]))) return rc;
+  }
+  if ((rc = table_upload(c)) || (rc = ensure_supported(c))) return rc;
+  if ((e = ctx->out.reserve(blob_len + 16ull * n + 128)) || (e = ctx->status.reserve(n * 4ull + 64)) ||
+      (e = d->cnt.reserve(2ull * kCntN * n * 4 + 64)))
+    return ctx->hip_fail(e, "ingest reserve");
+  // 1) open every file (lib.rs:501-502), plaintext -> HBM
+  if ((rc = device_open(ctx, d_blob, d_offs, n, blob_len, true, key_of(c), ctx->out.as<uint8_t>(),
+                        ctx->status.as<int32_t>(), false)))
+    return rc;
+  std::vector<int32_t> st(n);
+  if ((e = hipMemcpyAsync(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
+      (e = hipStreamSynchronize(ctx->stream)))
+    return ctx->hip_fail(e, "status");
+  for (uint32_t i = 0; i < n; i++)
+    if (st[i] == kStatusHostParse) {
+      if ((rc = resolve_host_parse(c, d_blob, d_offs, n, true))) return rc;
+      break;
+    }
+  // 2) version gate -> apply flags (decode errors reject the batch whatever the gate says)
+  uint32_t first_gap = n;
+  std::vector<uint64_t> expect;
+  if ((rc = gate(c, d_fa, d_fv, n, m, wslot, &first_gap, &expect))) return rc;
+  // 3) data version + Vec<S::Op> decode, count pass
+  DsDecodeArgs a = decode_args(c, n);
+  if ((e = hipMemsetAsync(d->misses.p, 0, 64, ctx->stream)) || (e = launch_ds_count(ctx->stream, a)) ||
+      (e = hipMemcpyAsync(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
+      (e = hipStreamSynchronize(ctx->stream)))
+    return ctx->hip_fail(e, "count");
+  bool host_dec = false;
+  for (uint32_t i = 0; i < n; i++) host_dec = host_dec || st[i] == kStatusHostDecode;
+  if (host_dec) {
+    if ((rc = resolve_host_decode(c, n, &st))) return rc;
+    if ((e = launch_ds_count(ctx->stream, a)) ||
+        (e = hipMemcpyAsync(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+      return ctx->hip_fail(e, "count");
+  }
+  if ((rc = fail_first(c, st, status_out, n))) return rc;  // all-or-nothing (lib.rs:497-514)
+  // 4) bases: exclusive scan of each count column
+  Counts k;
+  {
+    uint32_t* cnt = d->cnt.as<uint32_t>();
+    uint32_t last_cnt[kCntN], last_base[kCntN];
+    for (int j = 0; j < kCntN; j++)
+      if ((e = hipMemcpyAsync(&last_cnt[j], cnt + (size_t)j * n + n - 1, 4, hipMemcpyDeviceToHost, ctx->stream)))
+        return ctx->hip_fail(e, "scan");
+    uint32_t* bases = cnt + (size_t)kCntN * n;
+    size_t tb = 0;
+    if ((e = ds_excl_sum_u32(nullptr, tb, cnt, bases, n, ctx->stream)) || (e = d->cub_tmp.reserve(tb + 256)))
+      return ctx->hip_fail(e, "scan");
+    for (int j = 0; j < kCntN; j++) {
+      size_t t = d->cub_tmp.cap;
+      if ((e = ds_excl_sum_u32(d->cub_tmp.p, t, cnt + (size_t)j * n, bases + (size_t)j * n, n, ctx->stream)) ||
+          (e = hipMemcpyAsync(&last_base[j], bases + (size_t)j * n + n - 1, 4, hipMemcpyDeviceToHost, ctx->stream)))
+        return ctx->hip_fail(e, "scan");
+    }
+    if ((e = hipStreamSynchronize(ctx->stream))) return ctx->hip_fail(e, "scan");
+    for (int j = 0; j < kCntN; j++) k.v[j] = (uint64_t)last_cnt[j] + last_base[j];
+  }
+  // MVReg: the current values come first in the candidate list
+  HostCols vc;
+  Counts base;
+  if (c->kind == CE_STATE_MVREG) {
+    vals_cols(d, &vc);
+    base.v[kCntRm] = vc.rm_cbeg.size();
+    base.v[kCntRmC] = vc.rmc_actor.size();
+  }
+  Counts tot;
+  for (int j = 0; j < kCntN; j++) tot.v[j] = k.v[j] + base.v[j];
+  if (tot.v[kCntRmC] >= (1ull << 32) || tot.v[kCntAddM] >= (1ull << 32) || tot.v[kCntRmM] >= (1ull << 32))
+    return ctx->fail(CE_ERR_INVALID_ARG, "batch too large for 32-bit op offsets");
+  if ((rc = reserve_ops(c, tot))) return rc;
+  if (c->kind == CE_STATE_MVREG && (rc = upload_cols(c, vc, Counts{}))) return rc;
+  // 5) emit (actor ids from the device table; unknown actors -> insert and emit again)
+  a = decode_args(c, n);
+  a.cnt = d->cnt.as<uint32_t>() + (size_t)kCntN * n;  // bases
+  for (int j = 0; j < kCntN; j++) a.base_off[j] = (uint32_t)base.v[j];
+  for (int round = 0;; round++) {
+    uint32_t hm[4];
+    if ((e = hipMemsetAsync(d->misses.p, 0, 64, ctx->stream)) || (e = launch_ds_emit(ctx->stream, a)) ||
+        (e = hipMemcpyAsync(hm, d->misses.p, 16, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+      return ctx->hip_fail(e, "emit");
+    if (hm[2] == 0) break;
+    if (round > 64) return ctx->fail(CE_ERR_DEVICE, "actor table did not converge");
+    const uint32_t nm = std::min<uint32_t>(hm[2], kMissCap);
+    std::vector<uint4> ml(nm);
+    if ((e = hipMemcpy(ml.data(), d->misses.as<uint8_t>() + 64, nm * 16ull, hipMemcpyDeviceToHost)))
+      return ctx->hip_fail(e, "misses");
+    for (auto& x : ml) {
+      Uuid u;
+      std::memcpy(u.data(), &x, 16);
+      uint32_t s;
+      if ((rc = insert_actor(c, u, &s))) return rc;
+    }
+    if ((rc = table_upload(c))) return rc;
+    a.table = c->d_table.as<ActorSlot>();
+    a.mask = c->cap - 1;
+  }
+  if ((rc = write_sentinels(c, tot))) return rc;
+  // 6) fold (lib.rs:534-535 `state.apply(op)` for every op of every applied file, in order)
+  if (c->kind == CE_STATE_ORSWOT) {
+    const int t = ctx->tbegin("dotset_fold");
+    rc = orswot_fold(c, tot);
+    ctx->tend(t);
+  } else {
+    rc = mvreg_commit(c, (uint32_t)base.v[kCntRm], (uint32_t)tot.v[kCntRm], true);
+  }
+  if (rc) return rc;
+  // 7) next_op_versions (lib.rs:537-538) and the gap error (lib.rs:527-531)
+  for (uint32_t w = 0; w < m; w++) c->nov[wslot[w]] = std::max(c->nov[wslot[w]], expect[w]);
+  if (first_gap < n) {
+    if (status_out) status_out[first_gap] = CE_ERR_OP_VERSION;
+    return CE_ERR_OP_VERSION;
+  }
+  return CE_OK;
+}
+
+namespace {
+
+// StateWrapper<Orswot<u64, Uuid>> / StateWrapper<MVReg<u64, Uuid>> (host flatten)
+struct HostState {
+  Dots nov;
+  Dots clock;
+  std::vector<std::pair<uint64_t, Dots>> entries;          // HashMap: later duplicate wins
+  std::vector<std::pair<Dots, std::vector<uint64_t>>> deferred;
+  std::vector<std::pair<Dots, uint64_t>> vals;
+};
+
+bool read_state(int kind, const uint8_t* p, size_t n, HostState* hs) {
+  Rd r{p, n, 0};
+  return read_struct(r, {"next_op_versions", "state"}, [&](int f, Rd& q) {
+    if (f == 0) return read_vclock(q, &hs->nov);
+    if (kind == CE_STATE_ORSWOT)
+      return read_struct(q, {"clock", "entries", "deferred"}, [&](int g, Rd& s) {
+        uint64_t cnt;
+        if (g == 0) return read_vclock(s, &hs->clock);
+        if (!rd_map_hdr(s, &cnt) || cnt > s.n) return false;
+        std::map<uint64_t, size_t> seen;
+        for (uint64_t k = 0; k < cnt; k++) {
+          if (g == 1) {
+            uint64_t m;
+            Dots dv;
+            if (!rd_u64(s, &m) || !read_vclock(s, &dv)) return false;
+            auto it = seen.find(m);
+            if (it != seen.end()) hs->entries[it->second].second = dv;
+            else { seen[m] = hs->entries.size(); hs->entries.push_back({m, dv}); }
+          } else {
+            Dots key;
+            std::vector<uint64_t> ms;
+            if (!read_vclock(s, &key) || !read_members(s, &ms)) return false;
+            hs->deferred.push_back({key, ms});
+          }
+        }
+        return true;
+      });
+    return read_struct(q, {"vals"}, [&](int, Rd& s) {
+      uint64_t cnt;
+      if (!rd_array_hdr(s, &cnt) || cnt > s.n) return false;
+      for (uint64_t k = 0; k < cnt; k++) {
+        uint64_t two, v;
+        Dots dv;
+        if (!rd_array_hdr(s, &two) || two != 2 || !read_vclock(s, &dv) || !rd_u64(s, &v)) return false;
+        hs->vals.push_back({dv, v});
+      }
+      return true;
+    });
+  });
+}
+
+int id_dots(ce_core* c, Dots d, IdDots* out) {
+  sort_dots(&d);
+  out->clear();
+  for (auto& x : d) {
+    uint32_t s;
+    int rc = insert_actor(c, x.first, &s);
+    if (rc) return rc;
+    out->push_back({actor_id_of_slot(c, s), x.second});
+  }
+  std::sort(out->begin(), out->end());
+  return CE_OK;
+}
+
+// Orswot::merge(other) on the device (entries) and host (deferred)
+int orswot_merge_one(ce_core* c, const HostState& hs) {
+  DsState* d = c->ds;
+  ce_ctx* ctx = c->ctx;
+  hipStream_t s = ctx->stream;
+  int rc;
+  IdDots oclock;
+  if ((rc = id_dots(c, hs.clock, &oclock))) return rc;
+  std::vector<unsigned long long> mem, val;
+  std::vector<uint32_t> act;
+  for (auto& en : hs.entries) {
+    IdDots v;
+    if ((rc = id_dots(c, en.second, &v))) return rc;
+    for (auto& x : v) {
+      if (x.second == 0) continue;  // a zero counter is no dot (absent)
+      mem.push_back(en.first);
+      act.push_back(x.first);
+      val.push_back(x.second);
+    }
+  }
+  std::vector<std::pair<IdDots, std::vector<uint64_t>>> od;
+  for (auto& x : hs.deferred) {
+    IdDots k;
+    if ((rc = id_dots(c, x.first, &k))) return rc;
+    od.push_back({k, x.second});
+  }
+  if ((rc = table_upload(c)) || (rc = ensure_clock(c)) || (rc = ensure_pairs(c, mem.size()))) return rc;
+  hipError_t e;
+  const uint32_t cap = d->clock_cap;
+  std::vector<unsigned long long> oc(cap, 0);
+  for (auto& x : oclock) oc[x.first] = x.second;
+  if ((e = d->other[0].reserve(mem.size() * 8 + 8)) || (e = d->other[1].reserve(act.size() * 4 + 4)) ||
+      (e = d->other[2].reserve(val.size() * 8 + 8)))
+    return ctx->hip_fail(e, "merge");
+  if ((e = up(d->other[0].as<unsigned long long>(), mem, s)) || (e = up(d->other[1].as<uint32_t>(), act, s)) ||
+      (e = up(d->other[2].as<unsigned long long>(), val, s)) ||
+      (e = up(d->oclock.as<unsigned long long>(), oc, s)) ||
+      (e = launch_ds_put_other(s, tables(d), d->other[0].as<unsigned long long>(), d->other[1].as<uint32_t>(),
+                               d->other[2].as<unsigned long long>(), (uint32_t)mem.size())) ||
+      (e = launch_ds_merge(s, tables(d), d->clock.as<unsigned long long>(), d->oclock.as<unsigned long long>())))
+    return ctx->hip_fail(e, "merge");
+  // other.deferred applied, clocks merged, apply_deferred: thresholds from both deferred sets
+  auto rms = deferred_list(d);
+  rms.insert(rms.end(), od.begin(), od.end());
+  if ((rc = upload_removals(c, rms))) return rc;
+  const uint32_t nr = (uint32_t)rms.size();
+  if ((e = launch_ds_kill(s, tables(d), d->d0[0].as<uint32_t>(), d->d0[1].as<uint32_t>(), d->d0[2].as<uint32_t>(),
+                          d->d0[3].as<unsigned long long>(), d->d0[4].as<unsigned long long>(), nr)) ||
+      (e = launch_merge_max(s, d->clock.as<unsigned long long>(), d->oclock.as<unsigned long long>(), cap)))
+    return ctx->hip_fail(e, "merge");
+  if ((rc = finalize(c))) return rc;
+  std::vector<uint8_t> fl;
+  if ((rc = flags_for(c, d->d0[0].as<uint32_t>(), d->d0[2].as<uint32_t>(), d->d0[3].as<unsigned long long>(), nr, &fl)))
+    return rc;
+  std::map<IdDots, std::set<uint64_t>> nd;
+  for (uint32_t i = 0; i < nr; i++)
+    if (fl[i]) nd[rms[i].first].insert(rms[i].second.begin(), rms[i].second.end());
+  d->deferred = std::move(nd);
+  return CE_OK;
+}
+
+int mvreg_merge_one(ce_core* c, const HostState& hs) {
+  DsState* d = c->ds;
+  int rc;
+  HostCols hc;
+  vals_cols(d, &hc);
+  const uint32_t K = (uint32_t)d->vals.size();
+  for (auto& v : hs.vals) {
+    IdDots id;
+    if ((rc = id_dots(c, v.first, &id))) return rc;
+    hc.rm_cbeg.push_back((uint32_t)hc.rmc_actor.size());
+    hc.rm_mbeg.push_back(0);
+    for (auto& x : id) { hc.rmc_actor.push_back(x.first); hc.rmc_ctr.push_back(x.second); }
+    hc.put_val.push_back(v.second);
+  }
+  Counts tot;
+  tot.v[kCntRm] = hc.rm_cbeg.size();
+  tot.v[kCntRmC] = hc.rmc_actor.size();
+  if ((rc = ensure_clock(c)) || (rc = reserve_ops(c, tot)) || (rc = upload_cols(c, hc, Counts{})) ||
+      (rc = write_sentinels(c, tot)))
+    return rc;
+  return mvreg_commit(c, K, (uint32_t)tot.v[kCntRm], false);
+}
+
+}  // namespace
+
+int ds_merge_states(ce_core* c, const std::vector<std::pair<const uint8_t*, size_t>>& sws,
+                    int32_t* st, int32_t* status_out) {
+  const size_t n = sws.size();
+  std::vector<HostState> hs(n);
+  int first = CE_OK;
+  for (size_t i = 0; i < n; i++) {
+    if (st[i] == CE_OK && !read_state(c->kind, sws[i].first, sws[i].second, &hs[i])) st[i] = CE_ERR_DECODE;
+    if (st[i] != CE_OK && first == CE_OK) first = st[i];
+  }
+  if (status_out) std::memcpy(status_out, st, n * 4);
+  if (first != CE_OK) return first;  // nothing merged (lib.rs:431-456)
+  for (size_t i = 0; i < n; i++) {   // lib.rs:458-466
+    int rc = c->kind == CE_STATE_ORSWOT ? orswot_merge_one(c, hs[i]) : mvreg_merge_one(c, hs[i]);
+    if (rc) return rc;
+    for (auto& x : hs[i].nov) {
+      uint32_t s;
+      if ((rc = insert_actor(c, x.first, &s))) return rc;
+      c->nov[s] = std::max(c->nov[s], x.second);
+    }
+  }
+  return table_upload(c);
+}
+
+int ds_check_ops(ce_core* c, const uint8_t* ops, size_t len) {
+  std::vector<HostOp> v;
+  if (!parse_ops_host(c->kind, ops, len, &v))
+    return c->ctx->fail(CE_ERR_DECODE, c->kind == CE_STATE_ORSWOT ? "ops are not a Vec<orswot::Op<u64, Uuid>>"
+                                                                 : "ops are not a Vec<mvreg::Op<u64, Uuid>>");
+  return CE_OK;
+}
+
+int ds_apply_local_ops(ce_core* c, const uint8_t* ops, size_t len) {
+  DsState* d = c->ds;
+  std::vector<HostOp> v;
+  if (!parse_ops_host(c->kind, ops, len, &v)) return c->ctx->fail(CE_ERR_DECODE, "ops");
+  HostCols hc;
+  Counts base;
+  if (c->kind == CE_STATE_MVREG) {
+    vals_cols(d, &hc);
+    base.v[kCntRm] = hc.rm_cbeg.size();
+    base.v[kCntRmC] = hc.rmc_actor.size();
+  }
+  int rc = host_cols(c, v, Counts{}, &hc);  // offsets continue after the current values in hc
+  if (rc) return rc;
+  Counts tot;
+  tot.v[kCntAdd] = hc.add_actor.size();
+  tot.v[kCntAddM] = hc.add_mem.size();
+  tot.v[kCntRm] = hc.rm_cbeg.size();
+  tot.v[kCntRmC] = hc.rmc_actor.size();
+  tot.v[kCntRmM] = hc.rm_mem.size();
+  if ((rc = table_upload(c)) || (rc = ensure_clock(c)) || (rc = reserve_ops(c, tot)) ||
+      (rc = upload_cols(c, hc, Counts{})) || (rc = write_sentinels(c, tot)))
+    return rc;
+  if (c->kind == CE_STATE_ORSWOT) return orswot_fold(c, tot);
+  return mvreg_commit(c, (uint32_t)base.v[kCntRm], (uint32_t)tot.v[kCntRm], true);
+}
+
+// canonical to_vec_named(StateWrapper<S>) (lib.rs:336, 739-743); HashMap / HashSet contents
+// sorted (members ascending, deferred clocks by their msgpack bytes) -- SURVEY.md F9
+int ds_serialize(ce_core* c, std::vector<uint8_t>* out) {
+  DsState* d = c->ds;
+  ce_ctx* ctx = c->ctx;
+  hipStream_t s = ctx->stream;
+  hipError_t e;
+  auto uuid_dots = [&](const IdDots& v) {
+    Dots o;
+    for (auto& x : v) o.push_back({c->id_actor[x.first], x.second});
+    sort_dots(&o);
+    return o;
+  };
+  auto put_vclock = [](Wr& w, const Dots& v) {
+    w.map(1);
+    w.str("dots");
+    w.map(v.size());
+    for (auto& x : v) { w.bin(x.first.data(), 16); w.uint(x.second); }
+  };
+  Dots nov;
+  for (uint32_t sl = 0; sl < c->cap; sl++)
+    if (c->h_table[sl].used && c->nov[sl]) nov.push_back({c->slot_actor[sl], c->nov[sl]});
+  sort_dots(&nov);
+  Wr w;
+  w.map(2);
+  w.str("next_op_versions");
+  put_vclock(w, nov);
+  w.str("state");
+  if (c->kind == CE_STATE_MVREG) {
+    w.map(1);
+    w.str("vals");
+    w.arr(d->vals.size());
+    for (auto& v : d->vals) {
+      w.arr(2);
+      put_vclock(w, uuid_dots(v.first));
+      w.uint(v.second);
+    }
+    *out = std::move(w.b);
+    return CE_OK;
+  }
+  // clock
+  const uint32_t na = (uint32_t)c->id_actor.size();
+  std::vector<unsigned long long> ck(na);
+  if (na && ((e = hipMemcpyAsync(ck.data(), d->clock.p, na * 8ull, hipMemcpyDeviceToHost, s)) ||
+             (e = hipStreamSynchronize(s))))
+    return ctx->hip_fail(e, "clock download");
+  IdDots clock;
+  for (uint32_t i = 0; i < na; i++)
+    if (ck[i]) clock.push_back({i, ck[i]});
+  // entries: collect live pairs, sort by member on the device
+  uint32_t nl = 0;
+  int rc = collect(c, &nl);
+  if (rc) return rc;
+  std::vector<unsigned long long> mem(nl), val(nl);
+  std::vector<uint32_t> act(nl);
+  if (nl) {
+    if ((e = d->col[3].reserve(nl * 8ull)) || (e = d->col[4].reserve(nl * 4ull)) ||
+        (e = d->sort_perm.reserve(nl * 4ull)) || (e = d->sort_perm2.reserve(nl * 4ull)) ||
+        (e = d->ctr_sorted.reserve(nl * 8ull)))
+      return ctx->hip_fail(e, "serialize");
+    size_t tb = 0;
+    unsigned long long* k0 = d->col[0].as<unsigned long long>();
+    unsigned long long* k1 = d->col[3].as<unsigned long long>();
+    uint32_t* p0 = d->sort_perm.as<uint32_t>();
+    uint32_t* p1 = d->sort_perm2.as<uint32_t>();
+    if ((e = ds_sort_pairs_u64(nullptr, tb, k0, k1, p0, p1, nl, s)) || (e = d->cub_tmp.reserve(tb + 256)))
+      return ctx->hip_fail(e, "serialize");
+    tb = d->cub_tmp.cap;
+    if ((e = launch_ds_iota(s, p0, nl)) || (e = ds_sort_pairs_u64(d->cub_tmp.p, tb, k0, k1, p0, p1, nl, s)) ||
+        (e = launch_ds_gather_entries(s, d->sort_perm2.as<uint32_t>(), d->col[1].as<uint32_t>(),
+                                      d->col[2].as<unsigned long long>(), d->col[4].as<uint32_t>(),
+                                      d->ctr_sorted.as<unsigned long long>(), nl)) ||
+        (e = hipMemcpyAsync(mem.data(), d->col[3].p, nl * 8ull, hipMemcpyDeviceToHost, s)) ||
+        (e = hipMemcpyAsync(act.data(), d->col[4].p, nl * 4ull, hipMemcpyDeviceToHost, s)) ||
+        (e = hipMemcpyAsync(val.data(), d->ctr_sorted.p, nl * 8ull, hipMemcpyDeviceToHost, s)) ||
+        (e = hipStreamSynchronize(s)))
+      return ctx->hip_fail(e, "serialize");
+  }
+  size_t n_members = 0;
+  for (uint32_t i = 0; i < nl; i++) n_members += i == 0 || mem[i] != mem[i - 1];
+  w.map(3);
+  w.str("clock");
+  put_vclock(w, uuid_dots(clock));
+  w.str("entries");
+  w.map(n_members);
+  for (uint32_t i = 0; i < nl;) {
+    uint32_t j = i;
+    IdDots g;
+    while (j < nl && mem[j] == mem[i]) { g.push_back({act[j], val[j]}); j++; }
+    w.uint(mem[i]);
+    put_vclock(w, uuid_dots(g));
+    i = j;
+  }
+  w.str("deferred");
+  std::vector<std::pair<std::vector<uint8_t>, const std::set<uint64_t>*>> df;
+  for (auto& x : d->deferred) {
+    Wr kw;
+    put_vclock(kw, uuid_dots(x.first));
+    df.push_back({kw.b, &x.second});
+  }
+  std::sort(df.begin(), df.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  w.map(df.size());
+  for (auto& x : df) {
+    w.b.insert(w.b.end(), x.first.begin(), x.first.end());
+    w.arr(x.second->size());
+    for (uint64_t m : *x.second) w.uint(m);
+  }
+  *out = std::move(w.b);
+  return CE_OK;
+}
+
+}  // namespace ce

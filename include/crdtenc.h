@@ -173,8 +173,16 @@ int ce_content_name(const uint8_t *data, size_t len, char name_out[64]);
 /* ---------------------------------------------------------------------------------------- */
 typedef struct ce_core ce_core;
 
-/* StateWrapper<S> state type S */
-enum ce_state_kind { CE_STATE_VCLOCK = 0, CE_STATE_GCOUNTER = 1 };
+/* StateWrapper<S> state type S (crdts 7 types; Orswot and MVReg over u64 members / values) */
+enum ce_state_kind {
+  CE_STATE_VCLOCK = 0,   /* VClock<Uuid>                                                      */
+  CE_STATE_GCOUNTER = 1, /* GCounter<Uuid>                                                    */
+  CE_STATE_ORSWOT = 2,   /* Orswot<u64, Uuid>: op = orswot::Op {Add{dot, members}, Rm{clock,
+                            members}}; entries/deferred serialized in canonical order (members
+                            ascending, deferred clocks by their msgpack bytes): the reference's
+                            HashMap order is random                           */
+  CE_STATE_MVREG = 3     /* MVReg<u64, Uuid>: op = mvreg::Op::Put{clock, val}                 */
+};
 
 enum ce_open_flags {
   CE_OPEN_CREATE = 1,            /* OpenOptions.create (lib.rs:729)                          */
@@ -237,11 +245,17 @@ int ce_core_ingest_states(ce_core *c, const uint8_t *blob, const uint64_t *offs,
  * return the state file bytes and its content name.  nonce: 24 bytes or NULL (OS RNG). */
 int ce_core_compact_to_buffer(ce_core *c, const uint8_t *nonce, ce_buf *file, char name_out[64]);
 
+/* What read_remote_states does with one decrypted state (lib.rs:447, 458-466):
+ * rmp_serde::from_slice::<StateWrapper<S>>(sw) then state.merge + next_op_versions.merge.
+ * Also the exchange step of the dot-set kinds across GPUs (all-gather of partial states). */
+int ce_core_merge_state(ce_core *c, const uint8_t *sw, size_t len);
+
 /* Dense state exchange for multi-GPU merges (one process per GPU): actors registered in the
  * same order on every rank get the same dense index.  export copies the dense state counters
  * (u64[cap]) and next_op_versions (u64[cap]) into device buffers; import max-merges them back.
  * cap = ce_core_dense_capacity(). */
 int ce_core_register_actors(ce_core *c, const uint8_t *actors, uint32_t m);
+/* export/import_dense: VClock / GCounter only (CE_ERR_INVALID_ARG for the dot-set kinds). */
 uint32_t ce_core_dense_capacity(ce_core *c);
 int ce_core_export_dense(ce_core *c, uint64_t *d_state, uint64_t *d_nov);
 int ce_core_import_dense(ce_core *c, const uint64_t *d_state, const uint64_t *d_nov);

@@ -196,9 +196,12 @@ class _Map(list):
 
 
 def _unpack(b):
+    """first value of b; bytes after it are ignored (rmp_serde::from_slice reads one value)"""
     try:
-        return msgpack.unpackb(b, raw=False, strict_map_key=False, use_list=True,
-                               object_pairs_hook=_Map)
+        u = msgpack.Unpacker(raw=False, strict_map_key=False, use_list=True,
+                             object_pairs_hook=_Map, max_buffer_size=max(len(b), 1 << 20))
+        u.feed(b)
+        return u.unpack()
     except Exception as e:  # noqa: BLE001 -- any msgpack error is a decode error
         raise DecodeError(str(e))
 
@@ -272,6 +275,8 @@ def _enum(obj, variants):
     if len(p) != 1:
         raise DecodeError("enum")
     k, body = p[0]
+    if isinstance(k, bytes):
+        k = k.decode("latin-1")
     if isinstance(k, int) and not isinstance(k, bool) and 0 <= k < len(variants):
         k = variants[k]
     if k not in variants:

@@ -1,0 +1,261 @@
+"""GPU parity of the dot-set kinds (Orswot<u64, Uuid>, MVReg<u64, Uuid>) through the C ABI,
+against the sequential crdts restatement (oracle/crdts.py).
+
+Compared bit-exactly: per-file statuses, return codes and the canonical serialized StateWrapper
+(the reference's HashMap order is random; both sides sort).  Parity with crdts 7
+itself is unpinned: the oracle restates its published source.
+"""
+import random
+
+import msgpack
+import pytest
+
+import crdtenc
+import dotset_gen as G
+from oracle import crdts as C
+
+pytestmark = pytest.mark.gpu
+APP = bytes.fromhex("aadfd5a66e194b24a8024fa27c72f20c")
+CORE = crdtenc.CORE_VERSION
+KIND = {"orswot": crdtenc.STATE_ORSWOT, "mvreg": crdtenc.STATE_MVREG}
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = crdtenc.Context(0)
+    yield c
+    c.close()
+
+
+def seal_files(ctx, key, clears):
+    return [CORE + e for e in ctx.encrypt_batch(key, clears)]
+
+
+def new_core(ctx, kind, key):
+    core = crdtenc.Core(ctx, kind=KIND[kind], supported=[APP], current_data_version=APP)
+    core.set_latest_key(key)
+    return core
+
+
+def check_ops(ctx, kind, key, core, oc, actors, clears, fa, fv):
+    files = seal_files(ctx, key, clears)
+    rc, st = core.ingest_ops(files, actors, fa, fv)
+    orc, ost = oc.read_remote_ops(key, [APP], files, [actors[i] for i in fa], fv)
+    assert (rc, st) == (orc, ost)
+    assert core.state_bytes() == oc.serialize()
+    return rc
+
+
+def gen(kind, rng, actors, versions, ops, members, adversarial):
+    if kind == "orswot":
+        if adversarial:
+            return G.adversarial_orswot(rng, actors, versions, ops, members)
+        return G.well_formed_orswot(rng, actors, versions, ops, members)[0]
+    if adversarial:
+        return G.adversarial_mvreg(rng, actors, versions, ops)
+    return G.well_formed_mvreg(rng, actors, versions, ops)
+
+
+@pytest.mark.parametrize("kind", ["orswot", "mvreg"])
+@pytest.mark.parametrize("seed", range(6))
+def test_ops_parity(ctx, kind, seed):
+    rng = random.Random(1000 + seed)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, rng.randint(2, 9))
+    core, oc = new_core(ctx, kind, key), C.Core(kind)
+    adversarial = seed % 2 == 1
+    files = gen(kind, rng, actors, 6, rng.randint(1, 8), 40, adversarial)
+    # two batches: versions 0..2 then 3..5 (state and deferred removals carried over)
+    first = {a: [ops for ops in files[a][:3]] for a in files}
+    acts, clears, fa, fv = G.batch(first, kind, APP)
+    assert check_ops(ctx, kind, key, core, oc, acts, clears, fa, fv) == 0
+    acts, clears, fa, fv = G.batch(files, kind, APP, start={a: 3 for a in files})
+    assert check_ops(ctx, kind, key, core, oc, acts, clears, fa, fv) == 0
+    core.close()
+
+
+@pytest.mark.parametrize("kind", ["orswot", "mvreg"])
+def test_ops_parity_larger(ctx, kind):
+    """table growth / rebuild, many actors, thousands of ops"""
+    rng = random.Random(77)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 64)
+    core, oc = new_core(ctx, kind, key), C.Core(kind)
+    files = gen(kind, rng, actors, 8, 12, 3000, False)
+    for lo in range(0, 8, 2):
+        part = {a: files[a][: lo + 2] for a in files}
+        acts, clears, fa, fv = G.batch(part, kind, APP, start={a: lo for a in files})
+        assert check_ops(ctx, kind, key, core, oc, acts, clears, fa, fv) == 0
+    core.close()
+
+
+@pytest.mark.parametrize("kind", ["orswot", "mvreg"])
+def test_reject_and_gap(ctx, kind):
+    rng = random.Random(5)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 3)
+    core, oc = new_core(ctx, kind, key), C.Core(kind)
+    files = gen(kind, rng, actors, 4, 3, 10, False)
+    acts, clears, fa, fv = G.batch(files, kind, APP)
+    sealed = seal_files(ctx, key, clears)
+    # a tampered tag anywhere: nothing folded (lib.rs:497-514)
+    bad = list(sealed)
+    b = bytearray(bad[5])
+    b[-1] ^= 1
+    bad[5] = bytes(b)
+    rc, st = core.ingest_ops(bad, acts, fa, fv)
+    orc, ost = oc.read_remote_ops(key, [APP], bad, [acts[i] for i in fa], fv)
+    assert rc == orc == 9 and st == ost
+    # a decode error (not a Vec<Op>) rejects too
+    bad = list(clears)
+    bad[2] = APP + msgpack.packb({"x": 1})
+    rc2 = check_ops(ctx, kind, key, core, oc, acts, bad, fa, fv)
+    assert rc2 == 12
+    assert core.state_bytes() == oc.serialize() == C.Core(kind).serialize()
+    # a version gap for actor 1: earlier files stay folded, error at the gap (lib.rs:527-531)
+    keep = [i for i in range(len(fa)) if not (fa[i] == 1 and fv[i] == 1)]
+    rc3 = check_ops(ctx, kind, key, core, oc, acts, [clears[i] for i in keep], [fa[i] for i in keep],
+                    [fv[i] for i in keep])
+    assert rc3 == 13
+    core.close()
+
+
+def _noncanonical_orswot(ops, rng):
+    """same ops, other accepted encodings: struct arrays, variant indices, field maps in a
+    different order with unknown keys, unsorted removal clocks"""
+    out = []
+    for op in ops:
+        if op[0] == "Add":
+            _, (a, c), ms = op
+            form = rng.randrange(3)
+            if form == 0:
+                out.append({0: [[a, c], ms]})
+            elif form == 1:
+                out.append({"Add": {"zz": [1, {"q": None}], "members": ms, "dot": {"counter": c, "actor": a}}})
+            else:
+                out.append({"Add": [{"actor": a, "counter": c}, ms]})
+        else:
+            _, clock, ms = op
+            dots = list(clock.dots.items())
+            rng.shuffle(dots)
+            out.append({1: {"members": ms, "clock": [dict(dots)]}})
+    return msgpack.packb(out, use_bin_type=True)
+
+
+def test_orswot_accepts_rmp_forms(ctx):
+    rng = random.Random(9)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 4)
+    files = G.adversarial_orswot(rng, actors, 3, 6, 12)
+    acts = sorted(files)
+    clears, fa, fv = [], [], []
+    for i, a in enumerate(acts):
+        for v, ops in enumerate(files[a]):
+            clears.append(APP + _noncanonical_orswot(ops, rng))
+            fa.append(i)
+            fv.append(v)
+    core, oc = new_core(ctx, "orswot", key), C.Core("orswot")
+    assert check_ops(ctx, "orswot", key, core, oc, acts, clears, fa, fv) == 0
+    core.close()
+
+
+def seal_states(ctx, key, sws):
+    """state files in the format read_remote_states reads (lib.rs:435-447)"""
+    return seal_files(ctx, key, [APP + sw for sw in sws])
+
+
+@pytest.mark.parametrize("kind", ["orswot", "mvreg"])
+@pytest.mark.parametrize("seed", range(4))
+def test_states_then_ops(ctx, kind, seed):
+    rng = random.Random(300 + seed)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 5)
+    adversarial = seed % 2 == 1
+    # partial replicas -> state files
+    sws = []
+    for _ in range(3):
+        part = C.Core(kind)
+        files = gen(kind, rng, actors, 2, 5, 20, adversarial)
+        acts, clears, fa, fv = G.batch(files, kind, APP)
+        f = [CORE + C._oc.cryptor_encrypt(key, bytes(24), c)[1] for c in clears]
+        assert part.read_remote_ops(key, [APP], f, [acts[i] for i in fa], fv)[0] == 0
+        sws.append(part.serialize())
+    core, oc = new_core(ctx, kind, key), C.Core(kind)
+    sf = seal_states(ctx, key, sws)
+    rc, st = core.ingest_states(sf)
+    orc, ost = oc.read_remote_states(key, [APP], sf)
+    assert (rc, st) == (orc, ost) == (0, [0, 0, 0])
+    assert core.state_bytes() == oc.serialize()
+    # then ops on top (read_remote: states, then ops), from writers the states have not seen
+    files = gen(kind, rng, actors[:2] + G.actors_for(rng, 3), 3, 4, 20, adversarial)
+    acts, clears, fa, fv = G.batch(files, kind, APP)
+    check_ops(ctx, kind, key, core, oc, acts, clears, fa, fv)
+    # and another state merged into a non-empty state
+    sf = seal_states(ctx, key, [sws[0]])
+    assert core.ingest_states(sf)[0] == oc.read_remote_states(key, [APP], sf)[0] == 0
+    assert core.state_bytes() == oc.serialize()
+    core.close()
+
+
+@pytest.mark.parametrize("kind", ["orswot", "mvreg"])
+def test_local_apply_ops(ctx, kind):
+    rng = random.Random(44)
+    key = rng.randbytes(32)
+    core = new_core(ctx, kind, key)
+    me = core.info_actor()
+    actors = G.actors_for(rng, 3)
+    files = gen(kind, rng, actors, 2, 4, 10, True)
+    oc = C.Core(kind)
+    enc = C.enc_orswot_ops if kind == "orswot" else C.enc_mvreg_ops
+    for a in sorted(files):
+        for ops in files[a]:
+            assert core.apply_ops(enc(ops)) == 0
+            for op in ops:
+                oc.state.apply(op)
+            oc.nov.apply(me, oc.nov.get(me) + 1)
+    assert core.state_bytes() == oc.serialize()
+    assert core.apply_ops(msgpack.packb([{"Nope": 1}])) == 12
+    core.close()
+
+
+def test_orswot_sharded_merge_equals_single(ctx):
+    """multi-GPU exchange step: actor shards fold independently, then each merges the other's
+    partial StateWrapper (all-gather + local merge) == one core over everything"""
+    rng = random.Random(8)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 8)
+    files = G.well_formed_orswot(rng, actors, 4, 6, 30)[0]
+    acts, clears, fa, fv = G.batch(files, "orswot", APP)
+    sealed = seal_files(ctx, key, clears)
+    whole = new_core(ctx, "orswot", key)
+    assert whole.ingest_ops(sealed, acts, fa, fv)[0] == 0
+    parts = []
+    for r in range(2):
+        idx = [i for i in range(len(fa)) if fa[i] % 2 == r]
+        core = new_core(ctx, "orswot", key)
+        assert core.ingest_ops([sealed[i] for i in idx], acts, [fa[i] for i in idx],
+                               [fv[i] for i in idx])[0] == 0
+        parts.append(core)
+    sw = [p.state_bytes() for p in parts]
+    assert parts[0].merge_state(sw[1]) == 0 and parts[1].merge_state(sw[0]) == 0
+    assert parts[0].state_bytes() == parts[1].state_bytes() == whole.state_bytes()
+    for p in parts + [whole]:
+        p.close()
+
+
+def test_compact_roundtrip(ctx):
+    rng = random.Random(12)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 3)
+    files = G.well_formed_orswot(rng, actors, 3, 5, 15)[0]
+    acts, clears, fa, fv = G.batch(files, "orswot", APP)
+    core = crdtenc.Core(ctx, kind=crdtenc.STATE_ORSWOT, supported=[APP], current_data_version=APP,
+                        flags=crdtenc.COMPACT_INGEST_FORMAT)
+    core.set_latest_key(key)
+    assert core.ingest_ops(seal_files(ctx, key, clears), acts, fa, fv)[0] == 0
+    f, name = core.compact_to_buffer(nonce=bytes(24))
+    other = new_core(ctx, "orswot", key)
+    assert other.ingest_states([f])[0] == 0
+    assert other.state_bytes() == core.state_bytes()
+    core.close()
+    other.close()
