@@ -10,6 +10,13 @@ latency-bound message per array on xGMI; with gloo it runs the same code on CPU 
 
 Counters are u64 but the collective's MAX is signed int64: the sign bit is flipped before and
 after the reduce, which maps u64 order onto i64 order (values >= 2^63 stay correctly ordered).
+
+Orswot / MVReg (dot sets) do not reduce pointwise: each rank serializes its partial
+StateWrapper, the byte strings are all-gathered (one length exchange + one padded all_gather),
+and every rank merges the others' partial states with Core.merge_state -- the CvRDT merge
+read_remote_states applies to state files (crdt-enc/src/lib.rs:458-466), run by the GPU merge
+kernel.  Sharding by writer keeps every actor's ops on one rank, so each partial state is an
+op-based replica of that shard and the merge equals one fold over all files.
 """
 import torch
 import torch.distributed as dist
@@ -53,3 +60,32 @@ def max_u64_(dst, src):
     torch.maximum(a, b, out=a)
     dst.copy_(a.bitwise_xor_(_FLIP))
     return dst
+
+
+def all_gather_bytes(data, group=None, device="cpu"):
+    """Every rank's byte string, in rank order (variable lengths: padded to the longest)."""
+    world = dist.get_world_size(group)
+    n = torch.tensor([len(data)], dtype=torch.int64, device=device)
+    lens = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(world)]
+    dist.all_gather(lens, n, group=group)
+    lens = [int(x.item()) for x in lens]
+    width = max(max(lens), 1)
+    buf = torch.zeros(width, dtype=torch.uint8, device=device)
+    if data:
+        buf[: len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(device)
+    parts = [torch.empty(width, dtype=torch.uint8, device=device) for _ in range(world)]
+    dist.all_gather(parts, buf, group=group)
+    return [bytes(p[:k].cpu().numpy().tobytes()) for p, k in zip(parts, lens)]
+
+
+def exchange_dotset(core, group=None, device="cpu"):
+    """Merge the partial Orswot / MVReg states of all ranks into `core` (a crdtenc.Core or any
+    object with state_bytes() / merge_state(bytes) -> status)."""
+    rank = dist.get_rank(group)
+    states = all_gather_bytes(core.state_bytes(), group=group, device=device)
+    for r, sw in enumerate(states):
+        if r != rank:
+            rc = core.merge_state(sw)
+            if rc:
+                raise RuntimeError("merge_state of rank %d failed: %d" % (r, rc))
+    return core

@@ -139,3 +139,68 @@ def test_two_rank_exchange_equals_single_fold(kind, tmp_path):
     with open(out, "rb") as f:
         got = f.read()
     assert got == want
+
+
+class _OracleDotCore:
+    """state_bytes / merge_state over the sequential oracle (oracle/crdts.py)"""
+
+    def __init__(self, kind):
+        from oracle import crdts as C
+        self.C = C
+        self.core = C.Core(kind)
+
+    def state_bytes(self):
+        return self.core.serialize()
+
+    def merge_state(self, sw):
+        nov, st = self.C.dec_state(self.core.kind, sw)
+        self.core.state.merge(st)
+        self.core.nov.merge(nov)
+        return 0
+
+
+def _dot_workload(kind):
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import dotset_gen as G
+    rng = random.Random(21)
+    actors = G.actors_for(rng, 6)
+    if kind == "orswot":
+        files = G.well_formed_orswot(rng, actors, 4, 5, 25)[0]
+    else:
+        files = G.well_formed_mvreg(rng, actors, 4, 3)
+    return G.batch(files, kind, APP)
+
+
+def _dot_fold(kind, actors, clears, fa, fv, sel):
+    import oracle
+    key = bytes(range(32))
+    core = _OracleDotCore(kind)
+    files = [CORE + oracle.cryptor_encrypt(key, bytes(24), clears[i])[1] for i in sel]
+    rc, _ = core.core.read_remote_ops(key, [APP], files, [actors[fa[i]] for i in sel], [fv[i] for i in sel])
+    assert rc == 0
+    return core
+
+
+def _dot_rank_main(rank, world, port, kind, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        actors, clears, fa, fv = _dot_workload(kind)
+        lo, hi = shard.actor_range(len(actors), world, rank)
+        core = _dot_fold(kind, actors, clears, fa, fv, [i for i in range(len(fa)) if lo <= fa[i] < hi])
+        shard.exchange_dotset(core)
+        with open("%s.%d" % (out_path, rank), "wb") as f:
+            f.write(core.state_bytes())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["orswot", "mvreg"])
+def test_two_rank_dotset_exchange_equals_single_fold(kind, tmp_path):
+    actors, clears, fa, fv = _dot_workload(kind)
+    want = _dot_fold(kind, actors, clears, fa, fv, range(len(fa))).state_bytes()
+    out = str(tmp_path / "merged")
+    mp.spawn(_dot_rank_main, args=(2, _free_port(), kind, out), nprocs=2, join=True)
+    for r in range(2):
+        with open("%s.%d" % (out, r), "rb") as f:
+            assert f.read() == want
