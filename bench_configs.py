@@ -1,0 +1,271 @@
+#!/usr/bin/env python3
+"""bench_configs.py -- the other BASELINE.json configs on one MI355X (bench.py measures C2).
+
+  --config c3   Orswot<u64, Uuid>, 100k members, 4096 actors, mixed state + op files:
+                8 state files (each the compaction of 512 actors' first V0 versions) then
+                4096 x V op files of 32 ops (26 Add + 6 Rm, 1961 B plaintext); one step =
+                reset + read_remote_states + read_remote_ops + compact (crdt-enc/src/lib.rs:
+                332-547) with the op files resident in HBM and the state files on the host.
+
+Prints one JSON line per run.  Checks (size-independent): the merged clock equals its closed
+form (actor a's adds count 26 per version), and an actor-sharded fold of the same files merged
+with merge_state (the multi-GPU exchange) serializes to the same bytes.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "crdt-enc_amd"))
+import crdtenc  # noqa: E402
+
+APP = bytes.fromhex("aadfd5a66e194b24a8024fa27c72f20c")
+CORE = crdtenc.CORE_VERSION
+N_ACTORS = 4096
+N_MEMBERS = 100_000
+N_ADD, N_RM = 26, 6
+# one Add / Rm op in rmp-serde's to_vec_named form with fixed-width (uint32) integers
+ADD_T = (b"\x81\xa3Add\x82\xa3dot\x82\xa5actor\xc4\x10" + bytes(16) + b"\xa7counter\xce" + bytes(4) +
+         b"\xa7members\x91\xce" + bytes(4))
+RM_T = (b"\x81\xa2Rm\x82\xa5clock\x81\xa4dots\x81\xc4\x10" + bytes(16) + b"\xce" + bytes(4) +
+        b"\xa7members\x91\xce" + bytes(4))
+ADD_UUID, ADD_CTR, ADD_MEM = 19, 44, 58
+RM_UUID, RM_CTR, RM_MEM = 20, 37, 51
+HDR = APP + b"\xdc" + (N_ADD + N_RM).to_bytes(2, "big")
+PT_LEN = len(HDR) + N_ADD * len(ADD_T) + N_RM * len(RM_T)
+assert (len(ADD_T), len(RM_T), PT_LEN) == (62, 55, 1961)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def actors_table(seed=0xC0FFEE):
+    rng = np.random.default_rng(seed)
+    a = rng.integers(0, 256, size=(N_ACTORS, 16), dtype=np.uint8)
+    a[:, 6] = (a[:, 6] & 0x0F) | 0x40
+    a[:, 8] = (a[:, 8] & 0x3F) | 0x80
+    order = sorted(range(N_ACTORS), key=lambda i: a[i].tobytes())
+    return a[order]
+
+
+def member_of(a, v, j):
+    """deterministic member of actor a's add j in version v (int64 tensors)"""
+    h = (a * 1000003 + v * 7919 + j * 104729) * 2654435761
+    return (h ^ (h >> 13)) % N_MEMBERS
+
+
+def _be32(x, out):
+    for b in range(4):
+        out[..., b] = ((x >> (8 * (3 - b))) & 255).to(torch.uint8)
+
+
+def orswot_clears(actors, a_idx, v, dev):
+    """plaintexts [m, PT_LEN] of op files (actor a_idx[i], version v[i]): adds with dots
+    (a, 26 v + j + 1); removals of the actor's own earlier adds (previous version, or this one)"""
+    m = a_idx.shape[0]
+    out = torch.empty((m, PT_LEN), dtype=torch.uint8, device=dev)
+    out[:, :len(HDR)] = torch.tensor(list(HDR), dtype=torch.uint8, device=dev)
+    act = torch.from_numpy(actors).to(dev)[a_idx]
+    adds = out[:, len(HDR):len(HDR) + N_ADD * 62].view(m, N_ADD, 62)
+    adds[:] = torch.tensor(list(ADD_T), dtype=torch.uint8, device=dev)
+    adds[:, :, ADD_UUID:ADD_UUID + 16] = act[:, None, :]
+    j = torch.arange(N_ADD, dtype=torch.int64, device=dev)[None, :]
+    _be32(v[:, None] * N_ADD + j + 1, adds[:, :, ADD_CTR:ADD_CTR + 4])
+    _be32(member_of(a_idx[:, None], v[:, None], j), adds[:, :, ADD_MEM:ADD_MEM + 4])
+    rms = out[:, len(HDR) + N_ADD * 62:].view(m, N_RM, 55)
+    rms[:] = torch.tensor(list(RM_T), dtype=torch.uint8, device=dev)
+    rms[:, :, RM_UUID:RM_UUID + 16] = act[:, None, :]
+    k = torch.arange(N_RM, dtype=torch.int64, device=dev)[None, :]
+    jv = (k * 5 + 3) % N_ADD
+    vv = torch.where(v[:, None] > 0, v[:, None] - 1, v[:, None])
+    _be32(vv * N_ADD + jv + 1, rms[:, :, RM_CTR:RM_CTR + 4])
+    _be32(member_of(a_idx[:, None], vv, jv), rms[:, :, RM_MEM:RM_MEM + 4])
+    return out
+
+
+def seal_op_files(ctx, key, actors, a_lo, a_hi, v_lo, v_hi, dev, seed):
+    """op files of actors [a_lo, a_hi) x versions [v_lo, v_hi), actor-major (load_ops order)"""
+    na, nv = a_hi - a_lo, v_hi - v_lo
+    n = na * nv
+    flen = 16 + crdtenc.sealed_len(PT_LEN)
+    files = torch.empty(n * flen + 64, dtype=torch.uint8, device=dev)
+    offs = torch.arange(n + 1, dtype=torch.int64, device=dev) * flen
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed)
+    chunk = 1 << 15
+    for c0 in range(0, n, chunk):
+        m = min(chunk, n - c0)
+        idx = torch.arange(c0, c0 + m, dtype=torch.int64, device=dev)
+        a_idx, v = a_lo + idx // nv, v_lo + idx % nv
+        clear = orswot_clears(actors, a_idx, v, dev)
+        coffs = torch.arange(m + 1, dtype=torch.int64, device=dev) * PT_LEN
+        nonces = torch.randint(0, 256, (m, 24), dtype=torch.uint8, device=dev, generator=gen)
+        ooffs = (idx * flen).contiguous()
+        torch.cuda.current_stream().synchronize()
+        ctx.encrypt_batch_device(key, clear.data_ptr(), coffs.data_ptr(), m, nonces.data_ptr(),
+                                 files.data_ptr(), ooffs.data_ptr(), outer_version=CORE)
+        ctx.synchronize()
+    fa = torch.arange(na, dtype=torch.int32, device=dev).repeat_interleave(nv)
+    fv = torch.arange(v_lo, v_hi, dtype=torch.int64, device=dev).repeat(na)
+    return files, offs, n, n * flen, fa, fv
+
+
+def new_core(ctx, key, flags=0):
+    core = crdtenc.Core(ctx, kind=crdtenc.STATE_ORSWOT, supported=[APP], current_data_version=APP,
+                        flags=flags)
+    core.set_latest_key(key)
+    return core
+
+
+def run_c3(args, ctx, dev):
+    actors = actors_table()
+    key = bytes(np.random.default_rng(7).integers(0, 256, 32, dtype=np.uint8))
+    V0, V = args.state_versions, args.versions
+    t0 = time.time()
+    # state files: compaction (ingest-readable format) of 512 actors' versions [0, V0) each
+    states = []
+    per = N_ACTORS // 8
+    for j in range(8):
+        f, o, n, bl, fa, fv = seal_op_files(ctx, key, actors, j * per, (j + 1) * per, 0, V0, dev, 99 + j)
+        sc = new_core(ctx, key, flags=crdtenc.COMPACT_INGEST_FORMAT)
+        rc = sc.ingest_ops_device(f.data_ptr(), o.data_ptr(), n, bl,
+                                  b"".join(bytes(a) for a in actors[j * per:(j + 1) * per]),
+                                  fa.data_ptr(), fv.data_ptr())
+        if rc:
+            raise crdtenc.CeError(rc, ctx.last_error())
+        states.append(sc.compact_to_buffer(nonce=bytes(24))[0])
+        sc.close()
+        del f, o
+    files, offs, n, blob_len, fa, fv = seal_op_files(ctx, key, actors, 0, N_ACTORS, V0, V0 + V, dev, 1234)
+    all_actors = b"".join(bytes(a) for a in actors)
+    log("c3: %d state files (%.1f MB), %d op files (%.2f GB) in %.1f s" % (
+        len(states), sum(map(len, states)) / 1e6, n, blob_len / 1e9, time.time() - t0))
+
+    core = new_core(ctx, key)
+    core.register_actors([bytes(a) for a in actors])
+    out = {}
+
+    phase = {"reset": 0.0, "states": 0.0, "ops": 0.0, "compact": 0.0}
+
+    def step():
+        t = time.perf_counter()
+        core.reset()
+        t1 = time.perf_counter()
+        rc, st = core.ingest_states(states)
+        if rc:
+            raise crdtenc.CeError(rc, ctx.last_error())
+        t2 = time.perf_counter()
+        rc = core.ingest_ops_device(files.data_ptr(), offs.data_ptr(), n, blob_len, all_actors,
+                                    fa.data_ptr(), fv.data_ptr())
+        if rc:
+            raise crdtenc.CeError(rc, ctx.last_error())
+        t3 = time.perf_counter()
+        out["file"], out["name"] = core.compact_to_buffer()
+        t4 = time.perf_counter()
+        for k, a, b in (("reset", t, t1), ("states", t1, t2), ("ops", t2, t3), ("compact", t3, t4)):
+            phase[k] += (b - a) * 1e3
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    for k in phase:
+        phase[k] = 0.0
+    ctx.timing_reset()
+    ctx.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / args.steps
+    ctx.set_timing(False)
+    names = ("open_setup", "segments_open", "finalize_open", "gate", "ds_count", "ds_emit",
+             "ds_applied", "ds_add_pairs", "ds_kill", "ds_finalize", "ds_merge", "seal_setup",
+             "segments_seal")
+    kern = {k: ctx.timing(k) for k in names}
+    sb = core.state_bytes()
+
+    # checks: closed-form clock; sharded fold + merge_state == whole fold
+    import msgpack
+    d = msgpack.unpackb(sb, raw=True, strict_map_key=False)
+    clock = d[b"state"][b"clock"][b"dots"]
+    want = N_ADD * (V0 + V)
+    clock_ok = len(clock) == N_ACTORS and all(c == want for c in clock.values())
+    entries = len(d[b"state"][b"entries"])
+    parts = []
+    for r in range(2):
+        p = new_core(ctx, key)
+        lo, hi = r * N_ACTORS // 2, (r + 1) * N_ACTORS // 2
+        for sw_i in range(8 * r // 2, 8 * (r + 1) // 2):
+            assert p.ingest_states([states[sw_i]])[0] == 0
+        flen = blob_len // n
+        f0, f1 = lo * V, hi * V
+        sub = files[f0 * flen: f1 * flen]
+        so = offs[: f1 - f0 + 1]
+        rc = p.ingest_ops_device(sub.data_ptr(), so.data_ptr(), f1 - f0, (f1 - f0) * flen,
+                                 b"".join(bytes(a) for a in actors[lo:hi]),
+                                 (fa[f0:f1] - lo).contiguous().data_ptr(), fv[f0:f1].contiguous().data_ptr())
+        assert rc == 0, rc
+        parts.append(p)
+    parts[0].merge_state(parts[1].state_bytes())
+    shard_ok = parts[0].state_bytes() == sb
+    for p in parts:
+        p.close()
+
+    k_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in kern.items() if v[1]}
+    n_state = len(states)
+    ct = n * PT_LEN + sum(len(s) for s in states)
+    open_ms = sum(k_ms.get(x, 0) for x in ("open_setup", "segments_open", "finalize_open"))
+    # fold roofline: algorithmic bytes of the columnar fold per step -- adds: actor 4 + counter 8
+    # + mbeg 4 + member 8 + pair key/value RMW 32; removals: cbeg/mbeg 8 + clock entry 12 +
+    # member 8 + pair key/kill 24
+    n_add, n_rm = n * N_ADD, n * N_RM
+    fold_bytes = n_add * (4 + 8 + 4 + 8 + 32) + n_rm * (8 + 12 + 8 + 24)
+    fold_ms = sum(k_ms.get(x, 0) for x in ("ds_applied", "ds_add_pairs", "ds_kill"))
+    line = {
+        "metric": "C3 op+state files compacted/sec (Orswot<u64,Uuid>)",
+        "value": round((n + n_state) / (ms / 1e3), 1), "unit": "files/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+        "higher_is_better": True, "dtype": "u32/u64", "data": "synthetic (GPU-sealed, seeded)",
+        "config": {"workload": "C3: Orswot, %d members, %d actors; %d state files (512 actors x %d "
+                               "versions each) + %d op files (4096 x %d versions, 26 Add + 6 Rm, %d B)"
+                               % (N_MEMBERS, N_ACTORS, n_state, V0, n, V, PT_LEN),
+                   "ops": n * (N_ADD + N_RM), "entries": entries},
+        "aead_open_GBps": round(ct / (open_ms / 1e3) / 1e9, 1) if open_ms else None,
+        "fold": {"kernels": "ds_applied + ds_add_pairs + ds_kill", "ms": round(fold_ms, 4),
+                 "algorithmic_bytes": fold_bytes,
+                 "achieved_GBps": round(fold_bytes / (fold_ms / 1e3) / 1e9, 1) if fold_ms else None,
+                 "peak_GBps": 8000.0},
+        "kernels_ms_per_step": k_ms,
+        "phases_ms_per_step": {k: round(v / args.steps, 3) for k, v in phase.items()},
+        "checks": {"closed_form_clock": clock_ok, "sharded_merge_equals_whole": shard_ok},
+    }
+    print(json.dumps(line), flush=True)
+    core.close()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3", choices=["c3"])
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--versions", type=int, default=16, help="op-file versions per actor")
+    ap.add_argument("--state-versions", type=int, default=4, help="versions folded into states")
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
+    ctx = crdtenc.Context(0)
+    ctx.set_stream(stream.cuda_stream)
+    run_c3(args, ctx, dev)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -115,21 +115,39 @@ bool read_struct(Rd& r, const std::vector<const char*>& names,
 
 // VClock { dots: BTreeMap<Uuid, u64> }: later duplicate keys overwrite earlier ones
 bool read_vclock(Rd& r, Dots* out) {
-  return read_struct(r, {"dots"}, [&](int, Rd& q) {
+  // dots map: a later duplicate key overwrites the earlier value (BTreeMap::insert).  Keys in
+  // strictly ascending order (what to_vec_named writes) cannot repeat: no lookup structure.
+  auto dots = [&](Rd& q) {
     uint64_t cnt;
-    if (!rd_map_hdr(q, &cnt)) return false;
-    std::unordered_map<Uuid, size_t, UuidHash> idx;
+    if (!rd_map_hdr(q, &cnt) || cnt > q.n - q.i) return false;
+    const size_t base = out->size();
+    bool ascending = true;
     for (uint64_t k = 0; k < cnt; k++) {
       uint64_t off, c;
       if (!rd_uuid(q, &off) || !rd_u64(q, &c)) return false;
       Uuid u;
       std::memcpy(u.data(), q.p + off, 16);
-      auto it = idx.find(u);
-      if (it != idx.end()) out->at(it->second).second = c;
-      else { idx[u] = out->size(); out->push_back({u, c}); }
+      if (k && !(out->back().first < u)) ascending = false;
+      out->push_back({u, c});
+    }
+    if (!ascending) {
+      Dots v(out->begin() + base, out->end());
+      out->resize(base);
+      std::unordered_map<Uuid, size_t, UuidHash> idx;
+      for (auto& d : v) {
+        auto it = idx.find(d.first);
+        if (it != idx.end()) (*out)[it->second].second = d.second;
+        else { idx[d.first] = out->size(); out->push_back(d); }
+      }
     }
     return true;
-  });
+  };
+  // canonical struct form: fixmap(1) "dots"
+  if (r.n - r.i >= 6 && r.p[r.i] == 0x81 && r.p[r.i + 1] == 0xa4 && std::memcmp(r.p + r.i + 2, "dots", 4) == 0) {
+    r.i += 6;
+    return dots(r);
+  }
+  return read_struct(r, {"dots"}, [&](int, Rd& q) { return dots(q); });
 }
 
 // StateWrapper<S> { next_op_versions: VClock, state: S } (lib.rs:739-743)
@@ -616,7 +634,7 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
       SegScratch sc = segscratch(ctx, ec);
       int t = ctx->tbegin("segments_open");
       if ((e = launch_segments(ctx->stream, false, d_blob, ctx->out.as<uint8_t>(), da.params, n,
-                               da.status, sc, grid_waves_for(n), true)))
+                               da.status, sc, grid_waves_for(n + ec), true)))
         return ctx->hip_fail(e, "segments");
       ctx->tend(t);
       t = ctx->tbegin("finalize_open");
@@ -817,6 +835,7 @@ int ingest_states_host(ce_core* c, const uint8_t* blob, const uint64_t* offs, ui
   if ((e = hipMemcpyAsync(ctx->blob.p, blob, blen, hipMemcpyHostToDevice, ctx->stream)) ||
       (e = hipMemcpyAsync(ctx->offs.p, offs, (n + 1) * 8ull, hipMemcpyHostToDevice, ctx->stream)))
     return ctx->hip_fail(e, "states upload");
+  HostPhase hp("states: open + download");
   int rc = device_open(ctx, ctx->blob.as<uint8_t>(), ctx->offs.as<uint64_t>(), n, blen, true,
                        key_of(c), ctx->out.as<uint8_t>(), ctx->status.as<int32_t>(), false);
   if (rc) return rc;
@@ -943,6 +962,7 @@ int read_remote(ce_core* c) {
 
 // clear text + file of a compaction (lib.rs:335-360)
 int compact_bytes(ce_core* c, const uint8_t* nonce, std::vector<uint8_t>* file) {
+  HostPhase hp("compact_bytes");
   if (!c->has_key) return c->ctx->fail(CE_ERR_NO_KEY, "no latest key");
   std::vector<uint8_t> clear;
   int rc = serialize_state(c, &clear);
@@ -1120,6 +1140,7 @@ int ce_core_compact_to_buffer(ce_core* c, const uint8_t* nonce, ce_buf* file, ch
   int rc = compact_bytes(c, nonce, &f);
   if (rc) return rc;
   if (name_out) {
+    HostPhase hp("sha3 name");
     uint8_t h[32];
     sha3_256(f.data(), f.size(), h);
     std::snprintf(name_out, 64, "%s", base32_nopad(h, 32).c_str());

@@ -1,6 +1,9 @@
 // ce_core.h -- the Core object (crdt-enc/src/lib.rs:188-207 Core / CoreMutData) and the host
 // helpers shared by ce_core.cpp (VClock / GCounter state) and ce_dotset_host.cpp (Orswot / MVReg).
 #pragma once
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <functional>
 #include <set>
 #include <string>
@@ -106,6 +109,19 @@ struct Wr {
 };
 
 using Dots = std::vector<std::pair<Uuid, uint64_t>>;
+
+// CE_HOST_PROF=1: wall time of host phases to stderr (diagnostics only)
+struct HostPhase {
+  const char* name;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  explicit HostPhase(const char* n) : name(n) {}
+  ~HostPhase() {
+    static const bool on = std::getenv("CE_HOST_PROF") != nullptr;
+    if (!on || !name || !*name) return;
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    std::fprintf(stderr, "CE_HOST_PROF %-24s %9.3f ms\n", name, ms);
+  }
+};
 
 bool skip_any(Rd& r, int depth = 0);
 bool bytes_any(Rd& r, std::vector<uint8_t>* out);

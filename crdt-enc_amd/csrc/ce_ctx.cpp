@@ -137,7 +137,7 @@ int device_open(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint
   ctx->tend(t);
   t = ctx->tbegin("segments_open");
   if ((e = launch_segments(ctx->stream, false, d_blob, d_out, P, n, d_status, sc,
-                           grid_waves_for(n))) != hipSuccess)
+                           grid_waves_for(n + ec))) != hipSuccess)
     return ctx->hip_fail(e, "open segments");
   ctx->tend(t);
   t = ctx->tbegin("finalize_open");
@@ -170,8 +170,9 @@ int device_seal(ce_ctx* ctx, const uint8_t* d_clear, const uint64_t* d_offs, uin
     return ctx->hip_fail(e, "seal setup");
   ctx->tend(t);
   t = ctx->tbegin("segments_seal");
+  // one wave per 16 KiB segment: a single large state file still fills the chip
   if ((e = launch_segments(ctx->stream, true, d_clear, d_out, P, n, ctx->status.as<int32_t>(), sc,
-                           grid_waves_for(n))) != hipSuccess)
+                           grid_waves_for(n + ec))) != hipSuccess)
     return ctx->hip_fail(e, "seal segments");
   ctx->tend(t);
   t = ctx->tbegin("finalize_seal");

@@ -437,8 +437,11 @@ int finalize(ce_core* c) {
   DsState* d = c->ds;
   uint32_t h[4];
   hipError_t e;
-  if ((e = hipMemsetAsync(d->live.p, 0, 8, c->ctx->stream)) ||
-      (e = launch_ds_finalize(c->ctx->stream, tables(d))) ||
+  if ((e = hipMemsetAsync(d->live.p, 0, 8, c->ctx->stream))) return c->ctx->hip_fail(e, "finalize");
+  const int t = c->ctx->tbegin("ds_finalize");
+  if ((e = launch_ds_finalize(c->ctx->stream, tables(d)))) return c->ctx->hip_fail(e, "finalize");
+  c->ctx->tend(t);
+  if (
       (e = hipMemcpyAsync(h, d->live.p, 16, hipMemcpyDeviceToHost, c->ctx->stream)) ||
       (e = hipStreamSynchronize(c->ctx->stream)))
     return c->ctx->hip_fail(e, "finalize");
@@ -478,6 +481,7 @@ int orswot_fold(ce_core* c, const Counts& k) {
       return ctx->hip_fail(e, "applied");
     if ((e = d->cub_tmp.reserve(std::max(t1, t2) + 256))) return ctx->hip_fail(e, "applied");
     t1 = t2 = d->cub_tmp.cap;
+    const int ta = ctx->tbegin("ds_applied");
     if ((e = launch_ds_iota(s, perm, na)) ||
         (e = ds_sort_pairs_u32(d->cub_tmp.p, t1, o.add_actor, keys2, perm, perm2, na, bits, s)) ||
         (e = launch_ds_gather_ctr(s, perm2, o.add_ctr, cs, na)) ||
@@ -485,21 +489,26 @@ int orswot_fold(ce_core* c, const Counts& k) {
         (e = launch_ds_applied(s, keys2, perm2, cs, ex, d->clock.as<unsigned long long>(),
                                d->applied.as<uint8_t>(), na)))
       return ctx->hip_fail(e, "applied");
+    ctx->tend(ta);
   }
   // 2) entries: max-insert the applied adds (capacity for every add member)
   if ((rc = ensure_pairs(c, k.v[kCntAddM]))) return rc;
+  const int tp = ctx->tbegin("ds_add_pairs");
   if ((e = launch_ds_add_pairs(s, tables(d), o, d->applied.as<uint8_t>(), na)) ||
       (e = launch_ds_clock(s, o.add_actor, o.add_ctr, d->clock.as<unsigned long long>(), na)))
     return ctx->hip_fail(e, "add");
+  ctx->tend(tp);
   // 3) removal thresholds: the batch's removals and the deferred set
   auto d0 = deferred_list(d);
   if ((rc = upload_removals(c, d0))) return rc;
   const uint32_t n0 = (uint32_t)d0.size();
+  const int tk = ctx->tbegin("ds_kill");
   if ((e = launch_ds_kill(s, tables(d), o.rm_cbeg, o.rm_mbeg, o.rmc_actor, o.rmc_ctr, o.rm_mem, nr)) ||
       (e = launch_ds_kill(s, tables(d), d->d0[0].as<uint32_t>(), d->d0[1].as<uint32_t>(),
                           d->d0[2].as<uint32_t>(), d->d0[3].as<unsigned long long>(),
                           d->d0[4].as<unsigned long long>(), n0)))
     return ctx->hip_fail(e, "kill");
+  ctx->tend(tk);
   if ((rc = finalize(c))) return rc;
   // 4) deferred = removals whose clock is not covered by the new clock
   std::vector<uint8_t> f_batch, f_d0;
@@ -802,6 +811,7 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
       (e = d->cnt.reserve(2ull * kCntN * n * 4 + 64)))
     return ctx->hip_fail(e, "ingest reserve");
   // 1) open every file (lib.rs:501-502), plaintext -> HBM
+  HostPhase hpo("ops: open+gate+count");
   if ((rc = device_open(ctx, d_blob, d_offs, n, blob_len, true, key_of(c), ctx->out.as<uint8_t>(),
                         ctx->status.as<int32_t>(), false)))
     return rc;
@@ -820,8 +830,11 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
   if ((rc = gate(c, d_fa, d_fv, n, m, wslot, &first_gap, &expect))) return rc;
   // 3) data version + Vec<S::Op> decode, count pass
   DsDecodeArgs a = decode_args(c, n);
-  if ((e = hipMemsetAsync(d->misses.p, 0, 64, ctx->stream)) || (e = launch_ds_count(ctx->stream, a)) ||
-      (e = hipMemcpyAsync(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
+  if ((e = hipMemsetAsync(d->misses.p, 0, 64, ctx->stream))) return ctx->hip_fail(e, "count");
+  const int tc = ctx->tbegin("ds_count");
+  if ((e = launch_ds_count(ctx->stream, a))) return ctx->hip_fail(e, "count");
+  ctx->tend(tc);
+  if ((e = hipMemcpyAsync(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
       (e = hipStreamSynchronize(ctx->stream)))
     return ctx->hip_fail(e, "count");
   bool host_dec = false;
@@ -834,6 +847,9 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
       return ctx->hip_fail(e, "count");
   }
   if ((rc = fail_first(c, st, status_out, n))) return rc;  // all-or-nothing (lib.rs:497-514)
+  hpo.~HostPhase();
+  hpo.name = "";
+  HostPhase hps("ops: scan+emit");
   // 4) bases: exclusive scan of each count column
   Counts k;
   {
@@ -875,8 +891,11 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
   for (int j = 0; j < kCntN; j++) a.base_off[j] = (uint32_t)base.v[j];
   for (int round = 0;; round++) {
     uint32_t hm[4];
-    if ((e = hipMemsetAsync(d->misses.p, 0, 64, ctx->stream)) || (e = launch_ds_emit(ctx->stream, a)) ||
-        (e = hipMemcpyAsync(hm, d->misses.p, 16, hipMemcpyDeviceToHost, ctx->stream)) ||
+    if ((e = hipMemsetAsync(d->misses.p, 0, 64, ctx->stream))) return ctx->hip_fail(e, "emit");
+    const int te = ctx->tbegin("ds_emit");
+    if ((e = launch_ds_emit(ctx->stream, a))) return ctx->hip_fail(e, "emit");
+    ctx->tend(te);
+    if ((e = hipMemcpyAsync(hm, d->misses.p, 16, hipMemcpyDeviceToHost, ctx->stream)) ||
         (e = hipStreamSynchronize(ctx->stream)))
       return ctx->hip_fail(e, "emit");
     if (hm[2] == 0) break;
@@ -896,11 +915,12 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
     a.mask = c->cap - 1;
   }
   if ((rc = write_sentinels(c, tot))) return rc;
+  hps.~HostPhase();
+  hps.name = "";
+  HostPhase hpf("ops: fold");
   // 6) fold (lib.rs:534-535 `state.apply(op)` for every op of every applied file, in order)
   if (c->kind == CE_STATE_ORSWOT) {
-    const int t = ctx->tbegin("dotset_fold");
     rc = orswot_fold(c, tot);
-    ctx->tend(t);
   } else {
     rc = mvreg_commit(c, (uint32_t)base.v[kCntRm], (uint32_t)tot.v[kCntRm], true);
   }
@@ -920,7 +940,10 @@ namespace {
 struct HostState {
   Dots nov;
   Dots clock;
-  std::vector<std::pair<uint64_t, Dots>> entries;          // HashMap: later duplicate wins
+  // entries flattened: member e_member[i] has dots e_dots[e_beg[i] .. e_beg[i + 1])
+  std::vector<uint64_t> e_member;
+  std::vector<uint32_t> e_beg{0};
+  Dots e_dots;
   std::vector<std::pair<Dots, std::vector<uint64_t>>> deferred;
   std::vector<std::pair<Dots, uint64_t>> vals;
 };
@@ -934,21 +957,37 @@ bool read_state(int kind, const uint8_t* p, size_t n, HostState* hs) {
         uint64_t cnt;
         if (g == 0) return read_vclock(s, &hs->clock);
         if (!rd_map_hdr(s, &cnt) || cnt > s.n) return false;
-        std::map<uint64_t, size_t> seen;
+        bool ascending = true;
         for (uint64_t k = 0; k < cnt; k++) {
           if (g == 1) {
             uint64_t m;
-            Dots dv;
-            if (!rd_u64(s, &m) || !read_vclock(s, &dv)) return false;
-            auto it = seen.find(m);
-            if (it != seen.end()) hs->entries[it->second].second = dv;
-            else { seen[m] = hs->entries.size(); hs->entries.push_back({m, dv}); }
+            if (!rd_u64(s, &m) || !read_vclock(s, &hs->e_dots)) return false;
+            if (k && m <= hs->e_member.back()) ascending = false;
+            hs->e_member.push_back(m);
+            hs->e_beg.push_back((uint32_t)hs->e_dots.size());
           } else {
             Dots key;
             std::vector<uint64_t> ms;
             if (!read_vclock(s, &key) || !read_members(s, &ms)) return false;
             hs->deferred.push_back({key, ms});
           }
+        }
+        if (g == 1 && !ascending) {
+          // HashMap<M, VClock>: a repeated member keeps its later clock
+          std::unordered_map<uint64_t, size_t> last;
+          for (size_t i = 0; i < hs->e_member.size(); i++) last[hs->e_member[i]] = i;
+          std::vector<uint64_t> mem;
+          std::vector<uint32_t> beg{0};
+          Dots dd;
+          for (size_t i = 0; i < hs->e_member.size(); i++) {
+            if (last[hs->e_member[i]] != i) continue;
+            mem.push_back(hs->e_member[i]);
+            dd.insert(dd.end(), hs->e_dots.begin() + hs->e_beg[i], hs->e_dots.begin() + hs->e_beg[i + 1]);
+            beg.push_back((uint32_t)dd.size());
+          }
+          hs->e_member.swap(mem);
+          hs->e_beg.swap(beg);
+          hs->e_dots.swap(dd);
         }
         return true;
       });
@@ -989,15 +1028,30 @@ int orswot_merge_one(ce_core* c, const HostState& hs) {
   if ((rc = id_dots(c, hs.clock, &oclock))) return rc;
   std::vector<unsigned long long> mem, val;
   std::vector<uint32_t> act;
-  for (auto& en : hs.entries) {
-    IdDots v;
-    if ((rc = id_dots(c, en.second, &v))) return rc;
-    for (auto& x : v) {
-      if (x.second == 0) continue;  // a zero counter is no dot (absent)
-      mem.push_back(en.first);
-      act.push_back(x.first);
-      val.push_back(x.second);
-    }
+  mem.reserve(hs.e_dots.size());
+  act.reserve(hs.e_dots.size());
+  val.reserve(hs.e_dots.size());
+  {
+    // actor id lookups: the state's clock names (almost) every actor of its entries
+    std::unordered_map<Uuid, uint32_t, UuidHash> ids;
+    ids.reserve(hs.clock.size() * 2 + 16);
+    for (size_t i = 0; i < hs.e_member.size(); i++)
+      for (uint32_t j = hs.e_beg[i]; j < hs.e_beg[i + 1]; j++) {
+        const auto& x = hs.e_dots[j];
+        if (x.second == 0) continue;  // a zero counter is no dot (absent)
+        auto it = ids.find(x.first);
+        uint32_t id;
+        if (it != ids.end()) id = it->second;
+        else {
+          uint32_t sl;
+          if ((rc = insert_actor(c, x.first, &sl))) return rc;
+          id = actor_id_of_slot(c, sl);
+          ids.emplace(x.first, id);
+        }
+        mem.push_back(hs.e_member[i]);
+        act.push_back(id);
+        val.push_back(x.second);
+      }
   }
   std::vector<std::pair<IdDots, std::vector<uint64_t>>> od;
   for (auto& x : hs.deferred) {
@@ -1015,11 +1069,14 @@ int orswot_merge_one(ce_core* c, const HostState& hs) {
     return ctx->hip_fail(e, "merge");
   if ((e = up(d->other[0].as<unsigned long long>(), mem, s)) || (e = up(d->other[1].as<uint32_t>(), act, s)) ||
       (e = up(d->other[2].as<unsigned long long>(), val, s)) ||
-      (e = up(d->oclock.as<unsigned long long>(), oc, s)) ||
-      (e = launch_ds_put_other(s, tables(d), d->other[0].as<unsigned long long>(), d->other[1].as<uint32_t>(),
+      (e = up(d->oclock.as<unsigned long long>(), oc, s)))
+    return ctx->hip_fail(e, "merge");
+  const int tm = ctx->tbegin("ds_merge");
+  if ((e = launch_ds_put_other(s, tables(d), d->other[0].as<unsigned long long>(), d->other[1].as<uint32_t>(),
                                d->other[2].as<unsigned long long>(), (uint32_t)mem.size())) ||
       (e = launch_ds_merge(s, tables(d), d->clock.as<unsigned long long>(), d->oclock.as<unsigned long long>())))
     return ctx->hip_fail(e, "merge");
+  ctx->tend(tm);
   // other.deferred applied, clocks merged, apply_deferred: thresholds from both deferred sets
   auto rms = deferred_list(d);
   rms.insert(rms.end(), od.begin(), od.end());
@@ -1070,12 +1127,16 @@ int ds_merge_states(ce_core* c, const std::vector<std::pair<const uint8_t*, size
   const size_t n = sws.size();
   std::vector<HostState> hs(n);
   int first = CE_OK;
-  for (size_t i = 0; i < n; i++) {
-    if (st[i] == CE_OK && !read_state(c->kind, sws[i].first, sws[i].second, &hs[i])) st[i] = CE_ERR_DECODE;
-    if (st[i] != CE_OK && first == CE_OK) first = st[i];
+  {
+    HostPhase hp("states: host parse");
+    for (size_t i = 0; i < n; i++) {
+      if (st[i] == CE_OK && !read_state(c->kind, sws[i].first, sws[i].second, &hs[i])) st[i] = CE_ERR_DECODE;
+      if (st[i] != CE_OK && first == CE_OK) first = st[i];
+    }
   }
   if (status_out) std::memcpy(status_out, st, n * 4);
   if (first != CE_OK) return first;  // nothing merged (lib.rs:431-456)
+  HostPhase hp("states: merge");
   for (size_t i = 0; i < n; i++) {   // lib.rs:458-466
     int rc = c->kind == CE_STATE_ORSWOT ? orswot_merge_one(c, hs[i]) : mvreg_merge_one(c, hs[i]);
     if (rc) return rc;
@@ -1125,6 +1186,7 @@ int ds_apply_local_ops(ce_core* c, const uint8_t* ops, size_t len) {
 // canonical to_vec_named(StateWrapper<S>) (lib.rs:336, 739-743); HashMap / HashSet contents
 // sorted (members ascending, deferred clocks by their msgpack bytes) -- SURVEY.md F9
 int ds_serialize(ce_core* c, std::vector<uint8_t>* out) {
+  HostPhase hp("serialize");
   DsState* d = c->ds;
   ce_ctx* ctx = c->ctx;
   hipStream_t s = ctx->stream;
@@ -1173,6 +1235,7 @@ int ds_serialize(ce_core* c, std::vector<uint8_t>* out) {
     if (ck[i]) clock.push_back({i, ck[i]});
   // entries: collect live pairs, sort by member on the device
   uint32_t nl = 0;
+  HostPhase hp1("ser: collect/sort/download");
   int rc = collect(c, &nl);
   if (rc) return rc;
   std::vector<unsigned long long> mem(nl), val(nl);
@@ -1200,21 +1263,58 @@ int ds_serialize(ce_core* c, std::vector<uint8_t>* out) {
         (e = hipStreamSynchronize(s)))
       return ctx->hip_fail(e, "serialize");
   }
+  hp1.~HostPhase();
+  hp1.name = "";
+  HostPhase hp2("ser: host write");
   size_t n_members = 0;
   for (uint32_t i = 0; i < nl; i++) n_members += i == 0 || mem[i] != mem[i - 1];
+  // actor id -> rank in UUID byte order (BTreeMap order of a VClock)
+  std::vector<uint32_t> order(na), rank(na);
+  for (uint32_t i = 0; i < na; i++) order[i] = i;
+  std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return c->id_actor[a] < c->id_actor[b]; });
+  for (uint32_t i = 0; i < na; i++) rank[order[i]] = i;
+  w.b.reserve(w.b.size() + 64 + (size_t)n_members * 16 + (size_t)nl * 28 + clock.size() * 28);
   w.map(3);
   w.str("clock");
   put_vclock(w, uuid_dots(clock));
   w.str("entries");
   w.map(n_members);
+  std::vector<std::pair<uint32_t, uint64_t>> g;  // (rank, counter) of one member
+  // raw-pointer writes into a buffer sized for the worst case, trimmed afterwards
+  size_t pos = w.b.size();
+  w.b.resize(pos + (size_t)n_members * 20 + (size_t)nl * 27 + 64);
+  uint8_t* o = w.b.data();
+  auto put_uint = [&](uint64_t v) {
+    if (v <= 0x7f) { o[pos++] = (uint8_t)v; return; }
+    int k;
+    if (v <= 0xff) { o[pos++] = 0xcc; k = 1; }
+    else if (v <= 0xffff) { o[pos++] = 0xcd; k = 2; }
+    else if (v <= 0xffffffffull) { o[pos++] = 0xce; k = 4; }
+    else { o[pos++] = 0xcf; k = 8; }
+    for (int b = k - 1; b >= 0; b--) o[pos++] = (uint8_t)(v >> (8 * b));
+  };
   for (uint32_t i = 0; i < nl;) {
     uint32_t j = i;
-    IdDots g;
-    while (j < nl && mem[j] == mem[i]) { g.push_back({act[j], val[j]}); j++; }
-    w.uint(mem[i]);
-    put_vclock(w, uuid_dots(g));
+    g.clear();
+    while (j < nl && mem[j] == mem[i]) { g.push_back({rank[act[j]], val[j]}); j++; }
+    if (g.size() > 1) std::sort(g.begin(), g.end());
+    put_uint(mem[i]);
+    std::memcpy(o + pos, "\x81\xa4" "dots", 6);  // VClock {dots: ..}
+    pos += 6;
+    const size_t k = g.size();
+    if (k <= 15) o[pos++] = (uint8_t)(0x80 | k);
+    else if (k <= 0xffff) { o[pos++] = 0xde; o[pos++] = (uint8_t)(k >> 8); o[pos++] = (uint8_t)k; }
+    else { o[pos++] = 0xdf; for (int b = 3; b >= 0; b--) o[pos++] = (uint8_t)(k >> (8 * b)); }
+    for (auto& x : g) {
+      o[pos++] = 0xc4;
+      o[pos++] = 16;
+      std::memcpy(o + pos, c->id_actor[order[x.first]].data(), 16);
+      pos += 16;
+      put_uint(x.second);
+    }
     i = j;
   }
+  w.b.resize(pos);
   w.str("deferred");
   std::vector<std::pair<std::vector<uint8_t>, const std::set<uint64_t>*>> df;
   for (auto& x : d->deferred) {
