@@ -38,6 +38,59 @@ __device__ __forceinline__ void chacha_block(const uint32_t (&k)[8], uint32_t ct
   out[12] = x[12] + ctr; out[13] = x[13] + n0; out[14] = x[14] + n1; out[15] = x[15] + n2;
 }
 
+// Counter-independent part of a ChaCha20 block (key, 96-bit nonce n0 n1 n2 fixed, counter
+// varying): the first column round's quarter rounds on columns 1..3 and the first add of
+// column 0.  Computed once per file and reused for every block of it (13 words).
+struct ChachaPre {
+  uint32_t c[12];  // x1 x5 x9 x13 | x2 x6 x10 x14 | x3 x7 x11 x15 after the first column round
+  uint32_t a0;     // x0 + x4
+};
+
+__device__ __forceinline__ ChachaPre chacha_pre(const uint32_t (&k)[8], uint32_t n0, uint32_t n1,
+                                                uint32_t n2) {
+  uint32_t x1 = 0x3320646eu, x5 = k[1], x9 = k[5], x13 = n0;
+  uint32_t x2 = 0x79622d32u, x6 = k[2], x10 = k[6], x14 = n1;
+  uint32_t x3 = 0x6b206574u, x7 = k[3], x11 = k[7], x15 = n2;
+  CE_QR(x1, x5, x9, x13);
+  CE_QR(x2, x6, x10, x14);
+  CE_QR(x3, x7, x11, x15);
+  ChachaPre p;
+  p.c[0] = x1; p.c[1] = x5; p.c[2] = x9; p.c[3] = x13;
+  p.c[4] = x2; p.c[5] = x6; p.c[6] = x10; p.c[7] = x14;
+  p.c[8] = x3; p.c[9] = x7; p.c[10] = x11; p.c[11] = x15;
+  p.a0 = 0x61707865u + k[0];
+  return p;
+}
+
+// chacha_block with the counter-independent first-round work taken from `pre`
+__device__ __forceinline__ void chacha_block_pre(const ChachaPre& pre, const uint32_t (&k)[8],
+                                                 uint32_t ctr, uint32_t n0, uint32_t n1,
+                                                 uint32_t n2, uint32_t (&out)[16]) {
+  uint32_t x[16];
+  x[1] = pre.c[0]; x[5] = pre.c[1]; x[9] = pre.c[2]; x[13] = pre.c[3];
+  x[2] = pre.c[4]; x[6] = pre.c[5]; x[10] = pre.c[6]; x[14] = pre.c[7];
+  x[3] = pre.c[8]; x[7] = pre.c[9]; x[11] = pre.c[10]; x[15] = pre.c[11];
+  // column 0 of the first round, after its first add
+  x[0] = pre.a0; x[4] = k[0]; x[8] = k[4]; x[12] = ctr;
+  x[12] ^= x[0]; x[12] = rotl32(x[12], 16); x[8] += x[12]; x[4] ^= x[8]; x[4] = rotl32(x[4], 12);
+  x[0] += x[4]; x[12] ^= x[0]; x[12] = rotl32(x[12], 8); x[8] += x[12]; x[4] ^= x[8]; x[4] = rotl32(x[4], 7);
+  // first diagonal round, then 9 double rounds
+  CE_QR(x[0], x[5], x[10], x[15]); CE_QR(x[1], x[6], x[11], x[12]);
+  CE_QR(x[2], x[7], x[8], x[13]); CE_QR(x[3], x[4], x[9], x[14]);
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    CE_QR(x[0], x[4], x[8], x[12]); CE_QR(x[1], x[5], x[9], x[13]);
+    CE_QR(x[2], x[6], x[10], x[14]); CE_QR(x[3], x[7], x[11], x[15]);
+    CE_QR(x[0], x[5], x[10], x[15]); CE_QR(x[1], x[6], x[11], x[12]);
+    CE_QR(x[2], x[7], x[8], x[13]); CE_QR(x[3], x[4], x[9], x[14]);
+  }
+  out[0] = x[0] + 0x61707865u; out[1] = x[1] + 0x3320646eu;
+  out[2] = x[2] + 0x79622d32u; out[3] = x[3] + 0x6b206574u;
+#pragma unroll
+  for (int i = 0; i < 8; i++) out[4 + i] = x[4 + i] + k[i];
+  out[12] = x[12] + ctr; out[13] = x[13] + n0; out[14] = x[14] + n1; out[15] = x[15] + n2;
+}
+
 __device__ __forceinline__ void hchacha20(const uint32_t (&k)[8], const uint32_t (&n)[4],
                                           uint32_t (&sub)[8]) {
   uint32_t x[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, k[0], k[1], k[2], k[3],
@@ -150,15 +203,15 @@ __device__ __forceinline__ uint32_t ld_le32(const uint8_t* p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
-// key schedule shared by open/seal setup: subkey, (r, s), r^(2^k)
-__device__ void key_schedule(const DevKey& key, const uint8_t* nonce, FileParams& P) {
+// key schedule shared by open/seal setup: subkey, (r, s), r^(2^k); nonce as 6 LE words
+__device__ void key_schedule_w(const DevKey& key, const uint32_t (&nw)[6], FileParams& P) {
   uint32_t k[8], n16[4], sub[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) k[i] = key.k[i];
 #pragma unroll
-  for (int i = 0; i < 4; i++) n16[i] = ld_le32(nonce + 4 * i);
+  for (int i = 0; i < 4; i++) n16[i] = nw[i];
   hchacha20(k, n16, sub);
-  const uint32_t n2a = ld_le32(nonce + 16), n2b = ld_le32(nonce + 20);
+  const uint32_t n2a = nw[4], n2b = nw[5];
   uint32_t b0[16];
   chacha_block(sub, 0, 0, n2a, n2b, b0);
 #pragma unroll
@@ -182,6 +235,13 @@ __device__ void key_schedule(const DevKey& key, const uint8_t* nonce, FileParams
 #pragma unroll
     for (int i = 0; i < 5; i++) P.rpow[kk][i] = p.v[i];
   }
+}
+
+__device__ __forceinline__ void key_schedule(const DevKey& key, const uint8_t* nonce, FileParams& P) {
+  uint32_t nw[6];
+#pragma unroll
+  for (int i = 0; i < 6; i++) nw[i] = ld_le32(nonce + 4 * i);
+  key_schedule_w(key, nw, P);
 }
 
 __device__ __forceinline__ void reserve_segments(FileParams& P, uint32_t f, SegScratch sc) {

@@ -25,13 +25,20 @@ namespace ce {
 // beyond this costs resident blocks: 4 x (2 waves x 4 files x 5120 B) is exactly 160 KiB.
 static constexpr uint32_t kRegion = 64 * kKsStride;
 
+#ifndef CE_NCH
+#define CE_NCH 2
+#endif
 template <int LPF>
 struct FusedCfg {
   static constexpr int F = 64 / LPF;                       // files per wave
   static constexpr int WPB = LPF == 16 ? 2 : 4;            // waves per block
   static constexpr int LOG = LPF == 16 ? 4 : LPF == 32 ? 5 : 6;
-  static constexpr int ROWS = (256 + 1 + LPF - 1) / LPF;   // Horner steps for a full page
   static constexpr int WAVES_PER_SIMD = LPF == 16 ? 2 : LPF == 32 ? 3 : 4;  // LDS-limited
+  // independent Horner chains per lane: chain c takes the lane's slots t = c mod NCH and steps
+  // by r^(LPF * NCH) (FileParams.rpow[LOG + LOGCH]) -- NCH-way ILP on the mulmod dependency
+  // chain for one extra mulmod per chain to combine them
+  static constexpr int NCH = LPF * CE_NCH <= 64 ? CE_NCH : 64 / LPF;  // step r^(LPF NCH) <= r^64
+  static constexpr int LOGCH = NCH == 4 ? 2 : NCH == 2 ? 1 : 0;
 };
 
 // ---- lane-group collectives (a group = the LPF lanes of one file) --------------------------
@@ -98,10 +105,10 @@ struct FilePre {
   uint32_t in_hi;
   uint32_t key[8];
   uint32_t n2a, n2b;
-  uint32_t R[5];    // r^LPF (Horner step)
+  uint32_t R[5];    // r^(LPF * NCH): the Horner step of every chain
 };
 
-template <int LOG>
+template <int RIDX>
 __device__ __forceinline__ FilePre load_pre(const DecodeArgs& a, uint32_t f) {
   FilePre p;
   const bool in = f < a.n;
@@ -119,7 +126,7 @@ __device__ __forceinline__ FilePre load_pre(const DecodeArgs& a, uint32_t f) {
   p.n2a = Pp->n2[0];
   p.n2b = Pp->n2[1];
 #pragma unroll
-  for (int i = 0; i < 5; i++) p.R[i] = Pp->rpow[LOG][i];
+  for (int i = 0; i < 5; i++) p.R[i] = Pp->rpow[RIDX][i];
   return p;
 }
 
@@ -152,7 +159,7 @@ void k_open_fold_small(DecodeArgs a) {
 #endif
 
   uint32_t g = bcast(blockIdx.x * C::WPB + wib);
-  FilePre nx = load_pre<C::LOG>(a, g * F + grp);
+  FilePre nx = load_pre<C::LOG + C::LOGCH>(a, g * F + grp);
   // decode state carried across files: speculated Dot length, per-lane actor cache
   uint32_t Ls = 38;
   uint32_t ck0 = 0, ck1 = 0, ck2 = 0, ck3 = 0, cslot = 0xffffffffu;
@@ -163,22 +170,25 @@ void k_open_fold_small(DecodeArgs a) {
     const uint32_t len = cur.ok && cur.len <= kSmallMax ? cur.len : 0u;
     const bool act = cur.ok && cur.len <= kSmallMax;
     const uint32_t nblk_ct = (len + 15) >> 4;
-    const uint32_t nb = nblk_ct + 1;
     // inactive lanes read 16 B of the (always allocated) params array instead of the blob
     const uint8_t* src = act ? a.blob + (((uint64_t)cur.in_hi << 32) | cur.in_off)
                              : reinterpret_cast<const uint8_t*>(a.params);
     const FileParams* Pp = a.params + (act ? f : 0);
 
-    // 1) ciphertext pieces -> registers (issued first: latency hides under the ChaCha20)
-    uint4 ct[PPL];
+    // 1) ciphertext pieces -> registers (issued first: latency hides under the ChaCha20).
+    //    Poly1305 blocks are dealt from the END: lane sub, slot t holds block b = nblk_ct - sub -
+    //    LPF t (b == nblk_ct: the length block; b < 0: none), whose weight is r^(sub + 1) *
+    //    (r^LPF)^t -- every lane's Horner ends at weight 1 whatever the length (shorter files
+    //    only drop leading terms).
+    uint4 ct[PPL + 1];
 #pragma unroll
-    for (int j = 0; j < PPL; j++) {
-      const uint32_t blk = sub + LPF * j;
-      const uint32_t boff = blk * 16;
+    for (int j = 0; j <= PPL; j++) {
+      const int32_t blk = (int32_t)nblk_ct - (int32_t)sub - LPF * j;
+      const uint32_t boff = blk >= 0 && blk < (int32_t)nblk_ct ? (uint32_t)blk * 16u : 0u;
       // the 16-byte tag follows the ciphertext, so a 16-byte load at any boff < len stays
       // inside the file; bytes past len are zeroed below (Poly1305 pad16, plaintext tail).
-      // Pieces past the end load the file's first piece (in bounds) and are never used.
-      ct[j] = *reinterpret_cast<const uint4*>(src + (boff < len ? boff : 0u));
+      // Slots before the first piece load the file's first piece (in bounds), never used.
+      ct[j] = *reinterpret_cast<const uint4*>(src + boff);
 #if CE_FUSED_DIAG
       if (a.ablate & 8) ct[j] = make_uint4(boff, len, sub, 0);
 #endif
@@ -186,7 +196,9 @@ void k_open_fold_small(DecodeArgs a) {
     __builtin_amdgcn_wave_barrier();
     CE_PHASE(0)
 
-    // 2) keystream: lane computes blocks sub + LPF*k (ChaCha20 counter 1 + block)
+    // 2) keystream: lane computes blocks sub + LPF*k (ChaCha20 counter 1 + block); the
+    //    counter-independent first-round work is shared by the lane's F blocks
+    const ChachaPre cpre = chacha_pre(cur.key, 0u, cur.n2a, cur.n2b);
 #pragma unroll
     for (int k = 0; k < F; k++) {
       const uint32_t b = sub + LPF * k;
@@ -198,7 +210,7 @@ void k_open_fold_small(DecodeArgs a) {
           for (int i = 0; i < 16; i++) kb[i] = cur.key[i & 7] + b;
         } else
 #endif
-          chacha_block(cur.key, 1u + b, 0u, cur.n2a, cur.n2b, kb);
+          chacha_block_pre(cpre, cur.key, 1u + b, 0u, cur.n2a, cur.n2b, kb);
         uint4* kd = reinterpret_cast<uint4*>(fl + b * kKsStride);
         kd[0] = make_uint4(kb[0], kb[1], kb[2], kb[3]);
         kd[1] = make_uint4(kb[4], kb[5], kb[6], kb[7]);
@@ -209,9 +221,11 @@ void k_open_fold_small(DecodeArgs a) {
     __builtin_amdgcn_wave_barrier();
     CE_PHASE(1)
 
-    // tree powers r^(2^k), k < LOG, and s || expected tag: 16-byte loads issued now, used
-    // after the Horner pass (their latency hides under it).  Inactive lanes read params[0].
-    constexpr int NRW = 5 * C::LOG;
+    // tree powers r^(2^k), k < LOG + 2 (r^LPF, r^2LPF combine the chains), and s || expected
+    // tag: 16-byte loads issued now, used after the Horner pass (their latency hides under it).
+    // Inactive lanes read params[0].
+    constexpr int NPOW = C::LOG + C::NCH - 1 < 7 ? C::LOG + C::NCH - 1 : 7;
+    constexpr int NRW = 5 * NPOW;
     uint32_t rp[(NRW + 3) / 4 * 4];
 #pragma unroll
     for (int q = 0; q < (NRW + 3) / 4; q++) {
@@ -221,20 +235,26 @@ void k_open_fold_small(DecodeArgs a) {
     const uint4 sv4 = *reinterpret_cast<const uint4*>(Pp->s);
     const uint4 tg4 = *reinterpret_cast<const uint4*>(Pp->tag);
 
-    // 3) XOR, plaintext into LDS (over consumed keystream), strided Horner in r^LPF
-    L5 R;
+    // 3) XOR, plaintext into LDS (over consumed keystream), NCH Horner chains in r^64 over the
+    //    lane's slots, highest slot first (slots before the first piece are leading zeros)
+    L5 RS;
 #pragma unroll
-    for (int i = 0; i < 5; i++) R.v[i] = cur.R[i];
-    L5 acc = {{0, 0, 0, 0, 0}};
+    for (int i = 0; i < 5; i++) RS.v[i] = cur.R[i];
+    L5 acc[C::NCH];
 #pragma unroll
-    for (int j = 0; j < C::ROWS; j++) {
-      const uint32_t blk = sub + LPF * j;
-      if (act && blk < nblk_ct) {
+    for (int c = 0; c < C::NCH; c++) acc[c] = L5{{0, 0, 0, 0, 0}};
+#pragma unroll
+    for (int j = PPL; j >= 0; j--) {
+      const int32_t blk = (int32_t)nblk_ct - (int32_t)sub - LPF * j;
+      const int c = j % C::NCH;
+      if (act && blk == (int32_t)nblk_ct) {
+        acc[c] = add5(mulmod(acc[c], RS), block_limbs(0u, 0u, len, 0u));  // le64(0) || le64(len)
+      } else if (act && blk >= 0) {
         uint32_t kw_mask[4] = {~0u, ~0u, ~0u, ~0u};
-        const uint32_t q = blk;  // piece index within the page
+        const uint32_t q = (uint32_t)blk;  // piece index within the page
         const uint4 k4 = *reinterpret_cast<const uint4*>(fl + (q >> 2) * kKsStride + (q & 3) * 16);
-        uint4 x = j < PPL ? ct[j < PPL ? j : 0] : make_uint4(0, 0, 0, 0);
-        const uint32_t boff = blk * 16;
+        uint4 x = ct[j];
+        const uint32_t boff = q * 16;
         if (boff + 16 > len) {  // tail piece: zero the bytes past the ciphertext
           const uint32_t rem = len - boff;
           uint32_t xw[4] = {x.x, x.y, x.z, x.w};
@@ -252,26 +272,33 @@ void k_open_fold_small(DecodeArgs a) {
                              x.z ^ (k4.z & kw_mask[2]), x.w ^ (k4.w & kw_mask[3]));
         *reinterpret_cast<uint4*>(fl + boff) = y;
 #if CE_FUSED_DIAG
-        if (a.ablate & 2) acc.v[j % 5] += x.x ^ x.w;
+        if (a.ablate & 2) acc[c].v[j % 5] += x.x ^ x.w;
         else
 #endif
-          acc = add5(mulmod(acc, R), block_limbs(x.x, x.y, x.z, x.w));
-      } else if (act && blk == nblk_ct) {
-        acc = add5(mulmod(acc, R), block_limbs(0u, 0u, len, 0u));  // le64(0) || le64(len)
+          acc[c] = add5(mulmod(acc[c], RS), block_limbs(x.x, x.y, x.z, x.w));
       }
+    }
+    // lane value = sum_c acc_c * (r^LPF)^c
+    L5 lv = acc[0];
+    {
+      L5 p1, p2;
+#pragma unroll
+      for (int i = 0; i < 5; i++) {
+        p1.v[i] = rp[5 * C::LOG + i];
+        p2.v[i] = C::NCH > 2 ? rp[5 * (C::LOG + 1) + i] : 0u;
+      }
+      if (C::NCH > 1) lv = add5(lv, mulmod(acc[C::NCH > 1 ? 1 : 0], p1));
+      if (C::NCH > 2) lv = add5(lv, mulmod(acc[C::NCH > 2 ? 2 : 0], p2));
+      if (C::NCH > 3) lv = add5(lv, mulmod(acc[C::NCH > 3 ? 3 : 0], mulmod(p1, p2)));
+      lv = carry5(lv);
     }
     __builtin_amdgcn_wave_barrier();
     CE_PHASE(2)
 
-    // 4) cross-lane tree inside the group: position p holds the lane whose last block has
-    //    weight r^(LPF - p); level k multiplies by r^(2^k) and adds position p + 2^k (DPP row
-    //    shifts up to 8 lanes); finally * r.  Only position 0 (sub 0) ends with the sum.
-    L5 v;
-    {
-      const int srcl = (int)(grp * LPF + ((sub + nb) & (LPF - 1)));
-#pragma unroll
-      for (int i = 0; i < 5; i++) v.v[i] = __shfl(acc.v[i], srcl);
-    }
+    // 4) cross-lane tree inside the group: U = sum_s lane_s * r^s (level k adds lane s + 2^k
+    //    times r^(2^k): DPP row shifts up to 8 lanes), then T = U * r.  Only position 0 (sub 0)
+    //    ends with the sum.
+    L5 v = lv;
 #pragma unroll
     for (int k = 0; k < C::LOG; k++) {
       L5 rk;
@@ -281,7 +308,7 @@ void k_open_fold_small(DecodeArgs a) {
 #pragma unroll
       for (int i = 0; i < 5; i++)
         o.v[i] = k < 4 ? row_down(v.v[i], 1 << k) : (uint32_t)__shfl_down((int)v.v[i], 1u << k);
-      v = carry5(add5(mulmod(v, rk), o));
+      v = carry5(add5(v, mulmod(o, rk)));
     }
     L5 r1;
 #pragma unroll
@@ -302,7 +329,7 @@ void k_open_fold_small(DecodeArgs a) {
     bool ok = grp_bits<LPF>(tag_ok, grp) != 0;
 
     // next iteration's parameters: their latency hides under the decode
-    nx = load_pre<C::LOG>(a, (g + stride) * F + grp);
+    nx = load_pre<C::LOG + C::LOGCH>(a, (g + stride) * F + grp);
     CE_PHASE(3)
 
     // 5) decode from LDS

@@ -38,8 +38,13 @@ __global__ __launch_bounds__(256) void k_open_setup(const uint8_t* __restrict__ 
     // ensure_versions_phf(SUPPORTED_VERSIONS) (crdt-enc/src/lib.rs:501)
     if (flen < 16) st = CE_ERR_OUTER_LEN;
     else {
-      for (int i = 0; i < 16; i++)
-        if (enc[i] != kCoreVersion[i]) { st = CE_ERR_OUTER_VERSION; break; }
+      // one (unaligned) 16-byte load against the version's little-endian words
+      const uint4 v = *reinterpret_cast<const uint4*>(enc);
+      auto le = [](int i) {
+        return (uint32_t)kCoreVersion[4 * i] | ((uint32_t)kCoreVersion[4 * i + 1] << 8) |
+               ((uint32_t)kCoreVersion[4 * i + 2] << 16) | ((uint32_t)kCoreVersion[4 * i + 3] << 24);
+      };
+      if (v.x != le(0) || v.y != le(1) || v.z != le(2) || v.w != le(3)) st = CE_ERR_OUTER_VERSION;
       enc += 16;
       enc_len -= 16;
     }
@@ -47,6 +52,7 @@ __global__ __launch_bounds__(256) void k_open_setup(const uint8_t* __restrict__ 
   if (st == CE_OK) st = key_status;  // key version / length (xchacha lib.rs:74-78)
   Envelope e{};
   bool fast = false;
+  uint32_t nw[6];  // nonce words (fast path: from the header registers)
   if (st == CE_OK && enc_len >= 67 + 16) {
     // canonical EncHandler::encrypt box with a bin16 EncBox (clear text ~190 B .. 64 KiB),
     // checked from registers: 92 c4 10 <box16> c5 EE EE 82 a5"nonce" c4 18 <24> a8"enc_data"
@@ -72,6 +78,8 @@ __global__ __launch_bounds__(256) void k_open_setup(const uint8_t* __restrict__ 
     if (ok && eb == 45 + l2 && 22ull + eb <= enc_len && l2 >= 16) {
       e.nonce_off = 31; e.nonce_len = 24; e.enc_off = 67; e.enc_len = l2;
       fast = true;
+#pragma unroll
+      for (int k = 0; k < 6; k++) nw[k] = __builtin_amdgcn_alignbyte(w[8 + k], w[7 + k], 3);  // bytes 31..54
     }
   }
   if (st == CE_OK && !fast) st = parse_envelope(enc, enc_len, &e);
@@ -86,9 +94,13 @@ __global__ __launch_bounds__(256) void k_open_setup(const uint8_t* __restrict__ 
     const uint64_t ct_off = (uint64_t)(enc - blob) + e.enc_off;
     P.in_off = ct_off;
     P.len = (uint32_t)(e.enc_len - 16);
-    const uint8_t* t = blob + ct_off + P.len;
-    for (int i = 0; i < 4; i++) P.tag[i] = ld_le32(t + 4 * i);
-    key_schedule(key, enc + e.nonce_off, P);
+    const uint4 t = *reinterpret_cast<const uint4*>(blob + ct_off + P.len);  // unaligned 16 B
+    P.tag[0] = t.x; P.tag[1] = t.y; P.tag[2] = t.z; P.tag[3] = t.w;
+    if (!fast) {
+#pragma unroll
+      for (int k = 0; k < 6; k++) nw[k] = ld_le32(enc + e.nonce_off + 4 * k);
+    }
+    key_schedule_w(key, nw, P);
     reserve_segments(P, f, sc);
     if (P.len > kSmallMax) sc.large_list[atomicAdd(&sc.counters[9], 1u)] = f;
   }
