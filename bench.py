@@ -39,6 +39,12 @@ K_DOTS = 107                       # 16 + 3 + 107 * 38 = 4085 B of plaintext
 PT_LEN = 16 + 3 + 38 * K_DOTS
 HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md chip table (spec)
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # 256 CU x 4 SIMD32 x 2.4 GHz = 78.6 T int32 lane-ops/s
+# measured ceiling of the int32 ARX stream itself: tools/ubench_chacha (pure ChaCha20 blocks,
+# 8 waves/SIMD) reaches 2.55 TB/s of keystream = 39.8 G blocks/s x 976 ops = 38.9 T lane-ops/s,
+# i.e. wave64 int32 VALU instructions issue once per ~4 cycles per SIMD, not every 2
+# (profiles/r01_ubench_chacha.txt)
+VALU_INT32_MEASURED_TOPS = 38.9
+DEFAULT_FUSED = 1                  # ce_core.h `fused` default (CE_FUSED overrides it in both)
 
 
 def log(*a):
@@ -251,6 +257,11 @@ def main():
         if os.path.exists(tf):
             with open(tf) as f:
                 traffic = json.load(f).get("bytes_per_launch")
+        fused = os.environ.get("CE_FUSED", str(DEFAULT_FUSED))
+        lpf = 64 // int(os.environ.get("CE_FILES_PER_WAVE", "4"))
+        kname = ("k_open_fold_v2<%d> (XChaCha20-Poly1305 open + Vec<Dot> decode + fold, "
+                 "lane-owned ChaCha20 blocks)" % lpf if fused == "2" and lpf != 64 else
+                 "k_open_fold_small<%d> (XChaCha20-Poly1305 open + Vec<Dot> decode + fold)" % lpf)
         line = {
             "metric": METRIC,
             "value": round(n * world / (ms_max / 1e3), 1),
@@ -275,12 +286,14 @@ def main():
             },
             "aead_open_GBps": round(ct_bytes / avg_s / 1e9, 1) if avg_s > 0 else None,
             "roofline": {
-                "kernel": "k_open_fold_small (XChaCha20-Poly1305 open + Vec<Dot> decode + fold)",
+                "kernel": kname,
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "bytes_per_launch": bytes_per_launch, "avg_launch_ms": round(avg_s * 1e3, 4),
                 "valu": {"achieved_tops": round(valu, 2), "peak_tops": round(VALU_PEAK_TOPS, 1),
                          "frac": round(valu / VALU_PEAK_TOPS, 4),
+                         "int32_measured_peak_tops": VALU_INT32_MEASURED_TOPS,
+                         "frac_of_measured": round(valu / VALU_INT32_MEASURED_TOPS, 4),
                          "ops_per_file": ops_per_file},
             },
             "kernels_ms_per_step": {k: round(v[0] / max(v[1], 1), 4) for k, v in kern.items() if v[1]},

@@ -627,7 +627,9 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
     da.large_only = 1;
     {
       const int t = ctx->tbegin("open_fold_small");
-      if ((e = launch_open_fold_small(ctx->stream, da, c->files_per_wave))) return ctx->hip_fail(e, "fused");
+      e = c->fused == 2 && c->files_per_wave != 1 ? launch_open_fold_v2(ctx->stream, da, c->files_per_wave)
+                                                  : launch_open_fold_small(ctx->stream, da, c->files_per_wave);
+      if (e) return ctx->hip_fail(e, "fused");
       ctx->tend(t);
     }
     if (!only) {
@@ -996,6 +998,10 @@ int ce_core_open(ce_ctx* ctx, const ce_open_options* o, ce_core** out) {
   if (const char* fw = getenv("CE_FILES_PER_WAVE")) {
     const int v = atoi(fw);
     if (v == 1 || v == 2 || v == 4) c->files_per_wave = v;
+  }
+  if (const char* fu = getenv("CE_FUSED")) {
+    const int v = atoi(fu);
+    if (v == 1 || v == 2) c->fused = v;
   }
   c->flags = o->flags;
   std::memcpy(c->current_data_version.data(), o->current_data_version, 16);

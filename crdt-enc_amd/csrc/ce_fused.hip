@@ -23,7 +23,11 @@ namespace ce {
 
 // LDS per file in flight: 64 keystream blocks at an 80-byte stride (5120 B).  Any padding
 // beyond this costs resident blocks: 4 x (2 waves x 4 files x 5120 B) is exactly 160 KiB.
-static constexpr uint32_t kRegion = 64 * kKsStride;
+// Regions are packed at a 5104-byte stride: the last keystream block's 16 pad bytes are never
+// touched, so neighbouring regions may overlap them.  5104 B = 1276 dwords = -4 (mod 64 banks):
+// the four files of a wave sit on different banks at equal offsets (their decode reads would
+// otherwise collide 4-way), and 8 regions still fit 40 KiB per 2-wave block (4 blocks/CU).
+static constexpr uint32_t kRegion = 64 * kKsStride - 16;
 
 #ifndef CE_NCH
 #define CE_NCH 2
@@ -130,6 +134,208 @@ __device__ __forceinline__ FilePre load_pre(const DecodeArgs& a, uint32_t f) {
   return p;
 }
 
+// decode state a lane group carries from file to file: speculated Dot length, actor cache
+struct DecState {
+  uint32_t Ls;
+  uint32_t ck0, ck1, ck2, ck3, cslot;
+};
+
+// Steps 5-6 of the fused kernels for the file of this lane group whose plaintext sits in LDS at
+// fl: VersionBytes data-version check (crdt-enc/src/lib.rs:504-505), rmp-serde Vec<Dot<Uuid>>
+// decode (lib.rs:507) and the max-fold of the dots of applied files (VClock::apply).  `live` =
+// the file is active and its tag verified.  Called from wave-uniform control flow (ballots).
+template <int LPF>
+__device__ __forceinline__ void decode_fold(const DecodeArgs& a, const uint8_t* fl, uint32_t len,
+                                            bool live, bool apply, uint32_t f, uint32_t grp,
+                                            uint32_t sub, DecState& S) {
+  int32_t st = CE_OK;
+  if (live) {
+    if (len < 16) st = CE_ERR_PT_LEN;
+    else {
+      const uint4 dv = *reinterpret_cast<const uint4*>(fl);
+      bool found = false;
+      for (uint32_t s = 0; s < a.n_supported; s++) {
+        const uint4 sv = *reinterpret_cast<const uint4*>(a.supported + 16 * s);
+        found |= dv.x == sv.x && dv.y == sv.y && dv.z == sv.z && dv.w == sv.w;
+      }
+      if (!found) st = CE_ERR_PT_VERSION;
+    }
+  }
+  const uint8_t* body = fl + 16;
+  const uint32_t blen = len >= 16 ? len - 16 : 0;
+  uint64_t remaining = 0;
+  uint32_t pos = 0;
+  if (live && st == CE_OK) {
+    Rd r{body, blen, 0};
+    uint64_t count = 0;
+    if (!rd_array_hdr(r, &count) || count > blen) st = CE_ERR_DECODE;
+    else { remaining = count; pos = (uint32_t)r.i; }
+  }
+  const bool do_fold = live && st == CE_OK && apply;
+  // pending max per lane: flushed with atomicMax when the lane's actor changes
+  uint32_t pslot = 0xffffffffu;
+  unsigned long long pbest = 0;
+  auto fold_dot = [&](uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3, unsigned long long ctr) {
+    uint32_t slot;
+    // per-lane cache of the last resolved actor: a file's dots are usually its writer's
+    if (k0 == S.ck0 && k1 == S.ck1 && k2 == S.ck2 && k3 == S.ck3 && S.cslot != 0xffffffffu) slot = S.cslot;
+    else {
+      slot = lookup_slot(a.table, a.mask, k0, k1, k2, k3);
+      if (slot != 0xffffffffu) { S.ck0 = k0; S.ck1 = k1; S.ck2 = k2; S.ck3 = k3; S.cslot = slot; }
+    }
+    if (slot == 0xffffffffu) {
+      const uint32_t mi = atomicAdd(&a.counters[4], 1u);
+      if (mi < a.miss_cap) a.miss_list[mi] = make_uint4(k0, k1, k2, k3);
+      a.refold[f] = 1;
+    } else if (slot == pslot) {
+      pbest = ctr > pbest ? ctr : pbest;
+    } else {
+      if (pslot != 0xffffffffu) atomicMax(&a.batch[pslot], pbest);
+      pslot = slot;
+      pbest = ctr;
+    }
+  };
+  // fast path: every Dot canonical with the first Dot's length L0, so Dot i sits at pos + i L0.
+  // A round takes two Dots per lane (done + sub and done + LPF + sub): their 26 LDS reads are in
+  // flight together.  It stops at the first Dot that is not canonical with length L0 (nothing
+  // past it is folded); the sequential loop below takes over from there.
+  {
+    uint32_t L0 = 0;
+    if (live && st == CE_OK && remaining > 0 && pos + 34 <= blen) L0 = dot_len_of_marker(body[pos + 33]);
+    uint32_t done = 0;
+    bool fast = L0 != 0;
+    for (;;) {
+      const bool fb = fast && done < remaining;
+      if (!__any(fb)) break;
+      bool need[2], rd[2], valid[2];
+      uint32_t k0[2], k1[2], k2[2], k3[2], cand[2];
+      unsigned long long ctr[2];
+      uint32_t dd[2][13];
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const uint32_t i = done + sub + LPF * h;
+        cand[h] = pos + i * L0;
+        need[h] = fb && i < remaining;
+        rd[h] = need[h] && cand[h] + L0 <= blen;
+        const uint32_t* d = reinterpret_cast<const uint32_t*>(body) + ((rd[h] ? cand[h] : 0u) >> 2);
+#pragma unroll
+        for (int q = 0; q < 13; q++) dd[h][q] = d[q];
+      }
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const uint32_t sh = cand[h] & 3;
+        uint32_t w[12];
+#pragma unroll
+        for (int q = 0; q < 12; q++) w[q] = __builtin_amdgcn_alignbyte(dd[h][q + 1], dd[h][q], sh);
+        valid[h] = canon_dot(w, L0, k0[h], k1[h], k2[h], k3[h], ctr[h]) && rd[h];
+      }
+      const unsigned long long bad0 = grp_bits<LPF>(need[0] && !valid[0], grp);
+      const unsigned long long bad1 = grp_bits<LPF>(need[1] && !valid[1], grp);
+      // valid prefix of the round's 2 LPF Dots (lane order within h, h = 0 first)
+      const uint32_t kk = bad0 ? (uint32_t)__builtin_ctzll(bad0)
+                               : bad1 ? (uint32_t)LPF + (uint32_t)__builtin_ctzll(bad1) : 2u * LPF;
+      if (do_fold && need[0] && sub < kk) fold_dot(k0[0], k1[0], k2[0], k3[0], ctr[0]);
+      if (do_fold && need[1] && LPF + sub < kk) fold_dot(k0[1], k1[1], k2[1], k3[1], ctr[1]);
+      if (fb) {
+        const bool bad = (bad0 | bad1) != 0;
+        const uint64_t left = remaining - done;
+        done += bad ? kk : (uint32_t)(left < 2u * LPF ? left : 2u * LPF);
+        if (bad) fast = false;
+      }
+    }
+    pos += done * L0;
+    remaining -= done;
+  }
+  for (;;) {
+    const bool busy = live && st == CE_OK && remaining > 0;
+    if (!__any(busy)) break;
+    // round: lane sub reads the candidate Dot at pos + sub * Ls.  Lane 0 is at a Dot start
+    // whatever Ls is and checks its Dot at its own marker's length; lanes >= 1 are at Dot
+    // starts only when every earlier Dot of the round had length Ls.
+    bool valid = false;
+    uint32_t Lme = 0;
+    uint32_t k0 = 0, k1 = 0, k2 = 0, k3 = 0;
+    unsigned long long ctr = 0;
+    const uint32_t cand = pos + sub * S.Ls;
+    if (busy && sub < remaining && cand + 34 <= blen) {
+      // 13 aligned LDS dwords -> the 48-byte window at cand
+      const uint32_t* d = reinterpret_cast<const uint32_t*>(body) + (cand >> 2);
+      const uint32_t sh = cand & 3;
+      uint32_t dd[13];
+#pragma unroll
+      for (int i = 0; i < 13; i++) dd[i] = d[i];
+      uint32_t w[12];
+#pragma unroll
+      for (int i = 0; i < 12; i++) w[i] = __builtin_amdgcn_alignbyte(dd[i + 1], dd[i], sh);
+      Lme = dot_len_of_marker((w[8] >> 8) & 0xff);
+      const uint32_t L = sub == 0 ? Lme : S.Ls;
+      valid = ((uint32_t)canon_dot(w, L, k0, k1, k2, k3, ctr) & (uint32_t)(Lme != 0) &
+               (uint32_t)(cand + L <= blen)) != 0;
+    }
+    constexpr unsigned long long GM = LPF == 64 ? ~0ull : ((1ull << LPF) - 1);
+    const unsigned long long vb = grp_bits<LPF>(valid, grp);
+    uint32_t k = vb == GM ? (uint32_t)LPF : (uint32_t)__builtin_ctzll(~vb);
+    const bool m0 = grp_bits<LPF>(sub == 0 && Lme == S.Ls, grp) != 0;
+    if (!m0 && k > 1) k = 1;  // lanes >= 1 read at the wrong offsets
+    // next speculation: the first lane past the round sits exactly on the next Dot
+    const uint32_t inf = m0 ? k : 0u;
+    const uint32_t code = sub == inf ? len_code(Lme) : 0u;
+    const uint32_t nc = (grp_bits<LPF>(code & 1, grp) ? 1u : 0u) |
+                        (grp_bits<LPF>(code & 2, grp) ? 2u : 0u) |
+                        (grp_bits<LPF>(code & 4, grp) ? 4u : 0u);
+    const uint32_t Lold = S.Ls;
+    if (nc) S.Ls = code_len(nc);  // when !m0 this is lane 0's own length
+    // general grammar for one element (group leader), e.g. reordered keys / array form
+    const bool general = busy && k == 0;
+    bool fold_me = do_fold && busy && sub < k;
+    if (__any(general)) {
+      int gok = 0;
+      uint32_t npos = pos;
+      if (general && sub == 0) {
+        Rd q{body, blen, pos};
+        uint64_t aoff = 0, c = 0;
+        gok = parse_dot(q, &aoff, &c);
+        if (gok == 1) {
+          k0 = ld_le32(body + aoff); k1 = ld_le32(body + aoff + 4);
+          k2 = ld_le32(body + aoff + 8); k3 = ld_le32(body + aoff + 12);
+          ctr = c;
+          npos = (uint32_t)q.i;
+          fold_me = do_fold;
+        }
+      }
+      gok = __shfl(gok, (int)(grp * LPF));
+      npos = __shfl(npos, (int)(grp * LPF));
+      if (general) {
+        if (gok != 1) st = CE_ERR_DECODE;
+        else { pos = npos; remaining -= 1; }
+      }
+    }
+    if (fold_me) fold_dot(k0, k1, k2, k3, ctr);
+    if (busy && k > 0) {
+      pos += m0 ? k * Lold : S.Ls;  // !m0: k == 1 and Ls == lane 0's Dot length
+      remaining -= k;
+    }
+  }
+  // flush: one atomicMax per file when the group's pending actors agree
+  {
+    const uint32_t hi = pslot == 0xffffffffu ? 0u : pslot + 1;
+    const uint32_t lo = pslot == 0xffffffffu ? 0xffffffffu : pslot + 1;
+    const uint32_t mx = grp_reduce<LPF>(hi, [](uint32_t x, uint32_t y) { return x > y ? x : y; });
+    const uint32_t mn = grp_reduce<LPF>(lo, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
+    const unsigned long long b = grp_max64<LPF>(pslot == 0xffffffffu ? 0ull : pbest);
+    if (mx != 0 && mn == mx) {
+      if (sub == 0) atomicMax(&a.batch[mx - 1], b);
+    } else if (pslot != 0xffffffffu) {
+      atomicMax(&a.batch[pslot], pbest);
+    }
+  }
+  if (live && st != CE_OK && sub == 0) {
+    a.status[f] = st;
+    atomicAdd(&a.counters[3], 1u);
+    atomicMin(&a.counters[5], f);
+  }
+}
+
 template <int LPF>
 __global__ __launch_bounds__(FusedCfg<LPF>::WPB * 64, FusedCfg<LPF>::WAVES_PER_SIMD)
 void k_open_fold_small(DecodeArgs a) {
@@ -161,8 +367,7 @@ void k_open_fold_small(DecodeArgs a) {
   uint32_t g = bcast(blockIdx.x * C::WPB + wib);
   FilePre nx = load_pre<C::LOG + C::LOGCH>(a, g * F + grp);
   // decode state carried across files: speculated Dot length, per-lane actor cache
-  uint32_t Ls = 38;
-  uint32_t ck0 = 0, ck1 = 0, ck2 = 0, ck3 = 0, cslot = 0xffffffffu;
+  DecState S{38, 0, 0, 0, 0, 0xffffffffu};
 
   for (; g < ngroups; g += stride) {
     const uint32_t f = g * F + grp;
@@ -332,187 +537,12 @@ void k_open_fold_small(DecodeArgs a) {
     nx = load_pre<C::LOG + C::LOGCH>(a, (g + stride) * F + grp);
     CE_PHASE(3)
 
-    // 5) decode from LDS
-    int32_t st = CE_OK;
+    // 5)+6) data-version check, decode from LDS, fold
 #if CE_FUSED_DIAG
     if (a.ablate) ok = !(a.ablate & 1);
 #endif
-    bool live = act && ok;
-    if (live) {
-      if (len < 16) st = CE_ERR_PT_LEN;
-      else {
-        const uint4 dv = *reinterpret_cast<const uint4*>(fl);
-        bool found = false;
-        for (uint32_t s = 0; s < a.n_supported; s++) {
-          const uint4 sv = *reinterpret_cast<const uint4*>(a.supported + 16 * s);
-          found |= dv.x == sv.x && dv.y == sv.y && dv.z == sv.z && dv.w == sv.w;
-        }
-        if (!found) st = CE_ERR_PT_VERSION;
-      }
-    }
-    const uint8_t* body = fl + 16;
-    const uint32_t blen = len >= 16 ? len - 16 : 0;
-    uint64_t remaining = 0;
-    uint32_t pos = 0;
-    if (live && st == CE_OK) {
-      Rd r{body, blen, 0};
-      uint64_t count = 0;
-      if (!rd_array_hdr(r, &count) || count > blen) st = CE_ERR_DECODE;
-      else { remaining = count; pos = (uint32_t)r.i; }
-    }
-    const bool do_fold = live && st == CE_OK && cur.apply;
     CE_PHASE(4)
-    // pending max per lane: flushed with atomicMax when the lane's actor changes
-    uint32_t pslot = 0xffffffffu;
-    unsigned long long pbest = 0;
-    auto fold_dot = [&](uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3, unsigned long long ctr) {
-      uint32_t slot;
-      // per-lane cache of the last resolved actor: a file's dots are usually its writer's
-      if (k0 == ck0 && k1 == ck1 && k2 == ck2 && k3 == ck3 && cslot != 0xffffffffu) slot = cslot;
-      else {
-        slot = lookup_slot(a.table, a.mask, k0, k1, k2, k3);
-        if (slot != 0xffffffffu) { ck0 = k0; ck1 = k1; ck2 = k2; ck3 = k3; cslot = slot; }
-      }
-      if (slot == 0xffffffffu) {
-        const uint32_t mi = atomicAdd(&a.counters[4], 1u);
-        if (mi < a.miss_cap) a.miss_list[mi] = make_uint4(k0, k1, k2, k3);
-        a.refold[f] = 1;
-      } else if (slot == pslot) {
-        pbest = ctr > pbest ? ctr : pbest;
-      } else {
-        if (pslot != 0xffffffffu) atomicMax(&a.batch[pslot], pbest);
-        pslot = slot;
-        pbest = ctr;
-      }
-    };
-    // fast path: every Dot canonical with the first Dot's length L0, so Dot i sits at
-    // pos + i * L0 and a round needs one validity ballot.  It stops at the first Dot that is
-    // not (nothing past it is folded); the sequential loop below takes over from there.
-    {
-      uint32_t L0 = 0;
-      if (live && st == CE_OK && remaining > 0 && pos + 34 <= blen) L0 = dot_len_of_marker(body[pos + 33]);
-      uint32_t done = 0;
-      bool fast = L0 != 0;
-      for (;;) {
-        const bool fb = fast && done < remaining;
-        if (!__any(fb)) break;
-        const uint32_t i = done + sub;
-        const uint32_t cand = pos + i * L0;
-        const bool need = fb && i < remaining;
-        bool valid = false;
-        uint32_t k0 = 0, k1 = 0, k2 = 0, k3 = 0;
-        unsigned long long ctr = 0;
-        if (need && cand + L0 <= blen) {
-          const uint32_t* d = reinterpret_cast<const uint32_t*>(body) + (cand >> 2);
-          const uint32_t sh = cand & 3;
-          uint32_t dd[13];
-#pragma unroll
-          for (int q = 0; q < 13; q++) dd[q] = d[q];
-          uint32_t w[12];
-#pragma unroll
-          for (int q = 0; q < 12; q++) w[q] = __builtin_amdgcn_alignbyte(dd[q + 1], dd[q], sh);
-          valid = canon_dot(w, L0, k0, k1, k2, k3, ctr);
-        }
-        const unsigned long long bad = grp_bits<LPF>(need && !valid, grp);
-        const uint32_t kk = bad ? (uint32_t)__builtin_ctzll(bad) : (uint32_t)LPF;  // valid prefix
-        if (do_fold && need && sub < kk) fold_dot(k0, k1, k2, k3, ctr);
-        if (fb) {
-          const uint32_t adv = bad ? kk : min((uint32_t)LPF, (uint32_t)(remaining - done));
-          done += adv;
-          if (bad) fast = false;
-        }
-      }
-      pos += done * L0;
-      remaining -= done;
-    }
-    for (;;) {
-      const bool busy = live && st == CE_OK && remaining > 0;
-      if (!__any(busy)) break;
-      // round: lane sub reads the candidate Dot at pos + sub * Ls.  Lane 0 is at a Dot start
-      // whatever Ls is and checks its Dot at its own marker's length; lanes >= 1 are at Dot
-      // starts only when every earlier Dot of the round had length Ls.
-      bool valid = false;
-      uint32_t Lme = 0;
-      uint32_t k0 = 0, k1 = 0, k2 = 0, k3 = 0;
-      unsigned long long ctr = 0;
-      const uint32_t cand = pos + sub * Ls;
-      if (busy && sub < remaining && cand + 34 <= blen) {
-        // 13 aligned LDS dwords -> the 48-byte window at cand
-        const uint32_t* d = reinterpret_cast<const uint32_t*>(body) + (cand >> 2);
-        const uint32_t sh = cand & 3;
-        uint32_t dd[13];
-#pragma unroll
-        for (int i = 0; i < 13; i++) dd[i] = d[i];
-        uint32_t w[12];
-#pragma unroll
-        for (int i = 0; i < 12; i++) w[i] = __builtin_amdgcn_alignbyte(dd[i + 1], dd[i], sh);
-        Lme = dot_len_of_marker((w[8] >> 8) & 0xff);
-        const uint32_t L = sub == 0 ? Lme : Ls;
-        valid = ((uint32_t)canon_dot(w, L, k0, k1, k2, k3, ctr) & (uint32_t)(Lme != 0) &
-                 (uint32_t)(cand + L <= blen)) != 0;
-      }
-      constexpr unsigned long long GM = LPF == 64 ? ~0ull : ((1ull << LPF) - 1);
-      const unsigned long long vb = grp_bits<LPF>(valid, grp);
-      uint32_t k = vb == GM ? (uint32_t)LPF : (uint32_t)__builtin_ctzll(~vb);
-      const bool m0 = grp_bits<LPF>(sub == 0 && Lme == Ls, grp) != 0;
-      if (!m0 && k > 1) k = 1;  // lanes >= 1 read at the wrong offsets
-      // next speculation: the first lane past the round sits exactly on the next Dot
-      const uint32_t inf = m0 ? k : 0u;
-      const uint32_t code = sub == inf ? len_code(Lme) : 0u;
-      const uint32_t nc = (grp_bits<LPF>(code & 1, grp) ? 1u : 0u) |
-                          (grp_bits<LPF>(code & 2, grp) ? 2u : 0u) |
-                          (grp_bits<LPF>(code & 4, grp) ? 4u : 0u);
-      const uint32_t Lold = Ls;
-      if (nc) Ls = code_len(nc);  // when !m0 this is lane 0's own length
-      // general grammar for one element (group leader), e.g. reordered keys / array form
-      const bool general = busy && k == 0;
-      bool fold_me = do_fold && busy && sub < k;
-      if (__any(general)) {
-        int gok = 0;
-        uint32_t npos = pos;
-        if (general && sub == 0) {
-          Rd q{body, blen, pos};
-          uint64_t aoff = 0, c = 0;
-          gok = parse_dot(q, &aoff, &c);
-          if (gok == 1) {
-            k0 = ld_le32(body + aoff); k1 = ld_le32(body + aoff + 4);
-            k2 = ld_le32(body + aoff + 8); k3 = ld_le32(body + aoff + 12);
-            ctr = c;
-            npos = (uint32_t)q.i;
-            fold_me = do_fold;
-          }
-        }
-        gok = __shfl(gok, (int)(grp * LPF));
-        npos = __shfl(npos, (int)(grp * LPF));
-        if (general) {
-          if (gok != 1) st = CE_ERR_DECODE;
-          else { pos = npos; remaining -= 1; }
-        }
-      }
-      if (fold_me) fold_dot(k0, k1, k2, k3, ctr);
-      if (busy && k > 0) {
-        pos += m0 ? k * Lold : Ls;  // !m0: k == 1 and Ls == lane 0's Dot length
-        remaining -= k;
-      }
-    }
-    // flush: one atomicMax per file when the group's pending actors agree
-    {
-      const uint32_t hi = pslot == 0xffffffffu ? 0u : pslot + 1;
-      const uint32_t lo = pslot == 0xffffffffu ? 0xffffffffu : pslot + 1;
-      const uint32_t mx = grp_reduce<LPF>(hi, [](uint32_t x, uint32_t y) { return x > y ? x : y; });
-      const uint32_t mn = grp_reduce<LPF>(lo, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
-      const unsigned long long b = grp_max64<LPF>(pslot == 0xffffffffu ? 0ull : pbest);
-      if (mx != 0 && mn == mx) {
-        if (sub == 0) atomicMax(&a.batch[mx - 1], b);
-      } else if (pslot != 0xffffffffu) {
-        atomicMax(&a.batch[pslot], pbest);
-      }
-    }
-    if (live && st != CE_OK && sub == 0) {
-      a.status[f] = st;
-      atomicAdd(&a.counters[3], 1u);
-      atomicMin(&a.counters[5], f);
-    }
+    decode_fold<LPF>(a, fl, len, act && ok, cur.apply != 0, f, grp, sub, S);
     __builtin_amdgcn_wave_barrier();
     CE_PHASE(5)
 #if CE_FUSED_DIAG
@@ -557,6 +587,249 @@ hipError_t launch_open_fold_small(hipStream_t s, const DecodeArgs& a, int files_
   } else {
     const uint32_t blocks = std::min<uint32_t>((groups + 3) / 4, res64);
     hipLaunchKernelGGL(k_open_fold_small<64>, dim3(blocks), dim3(256), 0, s, a);
+  }
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------------------
+// k_open_fold_v2<LPF>: the same open + decode + fold, with whole ChaCha20 blocks per lane.
+//   Lane sub of a file's LPF-lane group owns blocks b = nblk - 1 - sub - LPF k (k < 64 / LPF,
+//   only b >= 0), dealt from the END: lane 0 slot 0 always holds the last, possibly partial,
+//   block.  The lane loads its blocks' 64-byte ciphertext runs, computes their keystream in
+//   registers and writes only plaintext to LDS: 4 KiB per file and one LDS store per piece
+//   (k_open_fold_small stores the keystream, reads it back transposed and stores plaintext:
+//   5 KiB per file, three LDS operations per piece).  One wave per workgroup: 16 KiB of LDS
+//   (LPF 16, 10 waves per CU) or 8 KiB (LPF 32, 20 waves per CU).
+//   Poly1305 over the lane's blocks, earliest first: G = Horner in r over the block's pieces,
+//   acc = acc r^(4 LPF) + G.  Lane s >= 1 ends at piece 4 nblk - 1 - 4 s.  Lane 0 keeps its last
+//   block apart (G'), so its chain ends at piece 4 nblk - 1 - 4 LPF, where a lane LPF would.
+//   Moving every chain one lane down puts them at tree positions q = 0..LPF-1 four pieces apart
+//   (q = 0 latest): U = sum_q v_q r^(4q) through the DPP tree in r^4 .. r^(2 LPF).  With
+//   delta = 4 nblk - npc (pieces missing from the last block), T = (U r^(5-delta) + G' r + lenblock) r.
+// ----------------------------------------------------------------------------------------
+static constexpr uint32_t kRegion2 = 4096;
+
+template <int LPF>
+struct V2Cfg {
+  static constexpr int F = 64 / LPF;               // files per wave
+  static constexpr int BPL = 64 / LPF;             // ChaCha20 blocks per lane (one page)
+  static constexpr int LOG = LPF == 16 ? 4 : 5;    // tree levels
+  static constexpr int WAVES = LPF == 16 ? 3 : 4;  // VGPR budget (LDS: 2.5 / 5 waves per SIMD)
+  static constexpr int NRP = LPF == 16 ? 8 : 9;    // 16-byte loads of r^(2^k), k <= LOG + 1
+};
+
+struct FilePre2 {
+  uint32_t ok, apply, len, in_off, in_hi;
+  uint32_t key[8];
+  uint32_t n2a, n2b;
+  uint32_t R1[5];   // r
+  uint32_t R64[5];  // r^64
+};
+
+__device__ __forceinline__ FilePre2 load_pre2(const DecodeArgs& a, uint32_t f) {
+  FilePre2 p;
+  const bool in = f < a.n;
+  const uint32_t fi = in ? f : 0u;
+  const FileParams* Pp = a.params + fi;
+  bool ok = in && a.status[fi] == CE_OK;
+  if (a.only) ok = ok && a.only[fi] != 0;
+  p.ok = ok;
+  p.apply = a.apply == nullptr || a.apply[fi] != 0;
+  p.len = Pp->len;
+  p.in_off = (uint32_t)Pp->in_off;
+  p.in_hi = (uint32_t)(Pp->in_off >> 32);
+#pragma unroll
+  for (int i = 0; i < 8; i++) p.key[i] = Pp->subkey[i];
+  p.n2a = Pp->n2[0];
+  p.n2b = Pp->n2[1];
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    p.R1[i] = Pp->rpow[0][i];
+    p.R64[i] = Pp->rpow[6][i];
+  }
+  return p;
+}
+
+template <int LPF>
+__global__ __launch_bounds__(64, V2Cfg<LPF>::WAVES)
+void k_open_fold_v2(DecodeArgs a) {
+  using C = V2Cfg<LPF>;
+  constexpr int F = C::F;
+  constexpr int BPL = C::BPL;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[F * kRegion2];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t grp = lane / LPF, sub = lane % LPF;
+  uint8_t* fl = lds + grp * kRegion2;
+  const uint32_t ngroups = (a.n + F - 1) / F;
+  const uint32_t stride = gridDim.x;
+  uint32_t g = bcast(blockIdx.x);
+  FilePre2 nx = load_pre2(a, g * F + grp);
+  DecState S{38, 0, 0, 0, 0, 0xffffffffu};
+
+  for (; g < ngroups; g += stride) {
+    const uint32_t f = g * F + grp;
+    const FilePre2 cur = nx;
+    const bool act = cur.ok && cur.len <= kSmallMax;
+    const uint32_t len = act ? cur.len : 0u;
+    const uint32_t npc = (len + 15) >> 4;             // ciphertext Poly1305 blocks
+    const int32_t nblk = (int32_t)((len + 63) >> 6);  // ChaCha20 blocks
+    // inactive lanes read the (always allocated) params array instead of the blob
+    const uint8_t* src = act ? a.blob + (((uint64_t)cur.in_hi << 32) | cur.in_off)
+                             : reinterpret_cast<const uint8_t*>(a.params);
+    const FileParams* Pp = a.params + (act ? f : 0);
+
+    // 1) the lane's ciphertext runs -> registers.  The 16-byte tag follows the ciphertext, so a
+    //    16-byte load at any piece < npc stays inside the file; absent pieces load piece 0.
+    uint4 ct[BPL][4];
+#pragma unroll
+    for (int k = BPL - 1; k >= 0; k--) {
+      const int32_t b = nblk - 1 - (int32_t)sub - LPF * k;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t q = (uint32_t)(4 * b + j);
+        const uint32_t off = b >= 0 && q < npc ? q * 16u : 0u;
+        ct[k][j] = *reinterpret_cast<const uint4*>(src + off);
+      }
+    }
+
+    // 2) per block, earliest first: keystream (counter 1 + b) in registers, XOR, plaintext ->
+    //    LDS, Poly1305.  Branch-free: lanes without a block (short files) compute garbage that
+    //    is neither stored where it matters nor accumulated.
+    const ChachaPre cpre = chacha_pre(cur.key, 0u, cur.n2a, cur.n2b);
+    L5 R1, RC;
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      R1.v[i] = cur.R1[i];
+      RC.v[i] = cur.R64[i];
+    }
+    if (LPF == 32) RC = mulmod(RC, RC);  // chain step r^(4 LPF) = r^128
+    L5 acc{{0, 0, 0, 0, 0}}, glast{{0, 0, 0, 0, 0}};
+#pragma unroll
+    for (int k = BPL - 1; k >= 0; k--) {
+      const int32_t b = nblk - 1 - (int32_t)sub - LPF * k;
+      const bool has = b >= 0;
+      uint32_t kb[16];
+      chacha_block_pre(cpre, cur.key, 1u + (uint32_t)b, 0u, cur.n2a, cur.n2b, kb);
+      L5 G;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t q = (uint32_t)(4 * b + j);
+        uint32_t xw[4] = {ct[k][j].x, ct[k][j].y, ct[k][j].z, ct[k][j].w};
+        uint32_t kw[4] = {kb[4 * j], kb[4 * j + 1], kb[4 * j + 2], kb[4 * j + 3]};
+        if (k == 0) {  // only lane 0's slot 0 (the file's last block) can be partial
+          const uint32_t boff = q * 16u;
+          const uint32_t rem = len > boff ? len - boff : 0u;
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const uint32_t lo = 4 * i;
+            const uint32_t keep = rem >= lo + 4 ? 0xffffffffu
+                                  : (rem <= lo ? 0u : ((1u << (8 * (rem - lo))) - 1));
+            xw[i] &= keep;
+            kw[i] &= keep;
+          }
+        }
+        // a lane without a block stores to bytes 4080..4095: past the end of any file that
+        // has absent blocks (nblk < 64)
+        const uint32_t st_off = has ? q * 16u : kRegion2 - 16u;
+        *reinterpret_cast<uint4*>(fl + st_off) =
+            make_uint4(xw[0] ^ kw[0], xw[1] ^ kw[1], xw[2] ^ kw[2], xw[3] ^ kw[3]);
+        const L5 m = block_limbs(xw[0], xw[1], xw[2], xw[3]);
+        if (j == 0) {
+          G = m;  // piece 4 b exists whenever the block does
+        } else {
+          const L5 gn = add5(mulmod(G, R1), m);
+          if (k == 0) {
+            const bool ex = q < npc;
+#pragma unroll
+            for (int i = 0; i < 5; i++) G.v[i] = ex ? gn.v[i] : G.v[i];
+          } else {
+            G = gn;
+          }
+        }
+      }
+      const L5 an = add5(mulmod(acc, RC), G);
+      const bool to_acc = has && !(k == 0 && sub == 0);
+#pragma unroll
+      for (int i = 0; i < 5; i++) acc.v[i] = to_acc ? an.v[i] : acc.v[i];
+      if (k == 0) {
+#pragma unroll
+        for (int i = 0; i < 5; i++) glast.v[i] = has && sub == 0 ? G.v[i] : 0u;
+      }
+    }
+
+    // r^(2^k), k <= LOG + 1; s || expected tag
+    uint32_t rp[4 * C::NRP];
+#pragma unroll
+    for (int q = 0; q < C::NRP; q++) {
+      const uint4 v = *reinterpret_cast<const uint4*>(&Pp->rpow[0][0] + 4 * q);
+      rp[4 * q] = v.x; rp[4 * q + 1] = v.y; rp[4 * q + 2] = v.z; rp[4 * q + 3] = v.w;
+    }
+    const uint4 sv4 = *reinterpret_cast<const uint4*>(Pp->s);
+    const uint4 tg4 = *reinterpret_cast<const uint4*>(Pp->tag);
+
+    // 3) chains -> tree positions (q takes lane q + 1's chain, q = LPF - 1 lane 0's), then
+    //    U = sum_q v_q r^(4q) at q = 0
+    const int srcl = (int)(grp * LPF + ((sub + 1) & (LPF - 1)));
+    L5 v;
+#pragma unroll
+    for (int i = 0; i < 5; i++) v.v[i] = (uint32_t)__shfl((int)acc.v[i], srcl);
+#pragma unroll
+    for (int k = 0; k < C::LOG; k++) {
+      L5 rk, o;
+#pragma unroll
+      for (int i = 0; i < 5; i++) {
+        rk.v[i] = rp[5 * (k + 2) + i];
+        o.v[i] = k < 4 ? row_down(v.v[i], 1 << k) : (uint32_t)__shfl_down((int)v.v[i], 16);
+      }
+      v = carry5(add5(v, mulmod(o, rk)));
+    }
+    // T = (U r^(5 - delta) + G' r + lenblock) r; r^(5 - delta) = r^4 r, r^4, r^2 r, r^2
+    const uint32_t delta = (uint32_t)(4 * nblk) - npc;
+    L5 r1, base;
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      r1.v[i] = rp[i];
+      base.v[i] = delta < 2 ? rp[10 + i] : rp[5 + i];
+    }
+    const L5 br = mulmod(base, r1);
+    L5 e;
+#pragma unroll
+    for (int i = 0; i < 5; i++) e.v[i] = (delta & 1) ? base.v[i] : br.v[i];
+    const L5 y = add5(mulmod(glast, r1), block_limbs(0u, 0u, len, 0u));  // le64(0) || le64(len)
+    const L5 tot = mulmod(carry5(add5(mulmod(v, e), y)), r1);
+    bool tag_ok = false;
+    if (act && sub == 0) {
+      const uint32_t sv[4] = {sv4.x, sv4.y, sv4.z, sv4.w};
+      uint32_t tag[4];
+      poly_tag(tot, sv, tag);
+      tag_ok = ((tag[0] ^ tg4.x) | (tag[1] ^ tg4.y) | (tag[2] ^ tg4.z) | (tag[3] ^ tg4.w)) == 0;
+      if (!tag_ok) {
+        a.status[f] = CE_ERR_AUTH;
+        atomicAdd(&a.counters[2], 1u);
+        atomicMin(&a.counters[5], f);
+      }
+    }
+    const bool ok = grp_bits<LPF>(tag_ok, grp) != 0;
+
+    // next iteration's parameters: their latency hides under the decode
+    nx = load_pre2(a, (g + stride) * F + grp);
+
+    // 4) data-version check, decode from LDS, fold
+    decode_fold<LPF>(a, fl, len, act && ok, cur.apply != 0, f, grp, sub, S);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+hipError_t launch_open_fold_v2(hipStream_t s, const DecodeArgs& a, int files_per_wave) {
+  if (a.n == 0) return hipSuccess;
+  static const uint32_t res16 = resident_blocks(k_open_fold_v2<16>, 64);
+  static const uint32_t res32 = resident_blocks(k_open_fold_v2<32>, 64);
+  if (files_per_wave == 2) {
+    const uint32_t groups = (a.n + 1) / 2;
+    hipLaunchKernelGGL(k_open_fold_v2<32>, dim3(std::min<uint32_t>(groups, res32)), dim3(64), 0, s, a);
+  } else {
+    const uint32_t groups = (a.n + 3) / 4;
+    hipLaunchKernelGGL(k_open_fold_v2<16>, dim3(std::min<uint32_t>(groups, res16)), dim3(64), 0, s, a);
   }
   return hipGetLastError();
 }

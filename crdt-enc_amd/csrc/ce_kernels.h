@@ -96,6 +96,9 @@ hipError_t launch_decode_dots(hipStream_t s, const DecodeArgs& a, uint32_t grid_
 
 // fused open + decode + fold of single-page files (ce_fused.hip); files_per_wave in {1, 2, 4}
 hipError_t launch_open_fold_small(hipStream_t s, const DecodeArgs& a, int files_per_wave);
+// the same with whole ChaCha20 blocks per lane (keystream XOR in registers; ce_fused.hip
+// k_open_fold_v2); files_per_wave in {2, 4}
+hipError_t launch_open_fold_v2(hipStream_t s, const DecodeArgs& a, int files_per_wave);
 
 // version gate on the device (ce_fused.hip): files grouped by actor with consecutive versions
 // (Storage::load_ops order, storage.rs:36-40) -> apply flags, first gap, next versions.

@@ -347,12 +347,14 @@ def test_reference_compact_format_is_unreadable_by_read_remote(ctx, tmp_path):
     assert c2.read_remote() == 2     # "version check failed" (lib.rs:435)
 
 
-@pytest.mark.parametrize("fpw", ["1", "2", "4"])
-def test_fused_geometries_match_oracle(ctx, oracle, fpw, monkeypatch):
-    """k_open_fold_small with 1, 2 and 4 files per wavefront; mixed single-page sizes."""
+@pytest.mark.parametrize("fused,fpw", [("1", "1"), ("1", "2"), ("1", "4"), ("2", "2"), ("2", "4")])
+def test_fused_geometries_match_oracle(ctx, oracle, fused, fpw, monkeypatch):
+    """k_open_fold_small (CE_FUSED=1) with 1, 2 and 4 files per wavefront and k_open_fold_v2
+    (CE_FUSED=2) with 2 and 4; mixed single-page sizes."""
     monkeypatch.setenv("CE_FILES_PER_WAVE", fpw)
+    monkeypatch.setenv("CE_FUSED", fused)
     key = os.urandom(32)
-    rng = random.Random(int(fpw))
+    rng = random.Random(int(fpw) + 10 * int(fused))
     actors = sorted(rng.randbytes(16) for _ in range(13))
     clears, fa, vers = [], [], []
     for a in range(13):
@@ -381,6 +383,78 @@ def test_fused_geometries_match_oracle(ctx, oracle, fpw, monkeypatch):
     empty = core2.state_bytes()
     rc, st = core2.ingest_ops(files2, actors, fa, vers)
     assert rc == 9 and st[50] == 9 and core2.state_bytes() == empty
+
+
+def _tail_length_batch(rng, actors, lens):
+    """Plaintexts of exactly the given lengths: APP || msgpack(Vec<Dot>) || trailing bytes
+    (rmp_serde::from_slice reads one value; the oracle ignores the tail the same way)."""
+    clears, fa, vers = [], [], []
+    per = -(-len(lens) // len(actors))
+    for i, L in enumerate(lens):
+        a, v = i // per, i % per
+        dots, body = [], msgpack.packb([])
+        while True:
+            d = {"actor": actors[a] if rng.random() < 0.8 else rng.choice(actors),
+                 "counter": rng.getrandbits(rng.choice([6, 16, 31, 40]))}
+            nb = msgpack.packb(dots + [d], use_bin_type=True)
+            if 16 + len(nb) > L:
+                break
+            dots.append(d)
+            body = nb
+        clears.append(APP + body + rng.randbytes(L - 16 - len(body)))
+        fa.append(a)
+        vers.append(v)
+    return clears, fa, vers
+
+
+@pytest.mark.parametrize("fused,fpw", [("1", "4"), ("2", "4"), ("2", "2")])
+def test_fused_every_tail_length(ctx, oracle, fused, fpw, monkeypatch):
+    """Single-page files of every length class: each ciphertext length mod 64 (0..3 Poly1305
+    pieces missing from the last ChaCha20 block, partial last pieces), the shortest envelopes and
+    the last 128 lengths up to one page, through both fused kernels; then tampered tags and
+    ciphertext bytes at several tail classes (per-file statuses == oracle, batch rejected)."""
+    monkeypatch.setenv("CE_FILES_PER_WAVE", fpw)
+    monkeypatch.setenv("CE_FUSED", fused)
+    key = os.urandom(32)
+    rng = random.Random(1000 + 10 * int(fused) + int(fpw))
+    actors = sorted(rng.randbytes(16) for _ in range(6))
+    lens = list(range(17, 17 + 192)) + list(range(4096 - 127, 4097)) + \
+        [rng.randrange(17, 4097) for _ in range(160)]
+    rng.shuffle(lens)
+    clears, fa, vers = _tail_length_batch(rng, actors, lens)
+    assert sorted(len(c) for c in clears) == sorted(lens)
+    files = [CORE + e for e in ctx.encrypt_batch(key, clears)]
+    core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+    core.set_latest_key(key)
+    rc, st = core.ingest_ops(files, actors, fa, vers)
+    oc = oracle.Core()
+    orc, ost = oc.read_remote_ops(key, [APP], files, [actors[i] for i in fa], vers)
+    assert rc == orc == 0 and st == ost
+    assert core.state_bytes() == oc.serialize()
+    # tamper: the tag of one file per (length mod 64) class in 1..4 pieces-missing shapes, and a
+    # ciphertext byte in the partial last piece of another
+    bad = list(files)
+    picked = {}
+    for i, L in enumerate(lens):
+        cls = (L % 64 + 15) // 16
+        if cls not in picked and L % 16:
+            picked[cls] = i
+    for cls, i in picked.items():
+        b = bytearray(bad[i])
+        if cls % 2:
+            b[-1] ^= 0x80                 # tag
+        else:
+            b[-17] ^= 0x01                # last ciphertext byte
+        bad[i] = bytes(b)
+    core2 = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+    core2.set_latest_key(key)
+    empty = core2.state_bytes()
+    rc2, st2 = core2.ingest_ops(bad, actors, fa, vers)
+    oc2 = oracle.Core()
+    orc2, ost2 = oc2.read_remote_ops(key, [APP], bad, [actors[i] for i in fa], vers)
+    assert rc2 == orc2 == 9 and st2 == ost2
+    assert all(st2[i] == 9 for i in picked.values())
+    assert core2.state_bytes() == empty
 
 
 def test_unordered_batch_uses_host_gate(ctx, oracle):
