@@ -44,7 +44,7 @@ VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # 256 CU x 4 SIMD32 x 2.4 GHz = 7
 # i.e. wave64 int32 VALU instructions issue once per ~4 cycles per SIMD, not every 2
 # (profiles/r01_ubench_chacha.txt)
 VALU_INT32_MEASURED_TOPS = 38.9
-DEFAULT_FUSED = 1                  # ce_core.h `fused` default (CE_FUSED overrides it in both)
+DEFAULT_FUSED = 2                  # ce_core.h `fused` default (CE_FUSED overrides it in both)
 
 
 def log(*a):
@@ -162,6 +162,11 @@ def main():
     fv_d = torch.from_numpy(fv.astype(np.int64)).to(dev)
 
     out = {}
+    # The SHA3-256 content name of step i's state file (host, ~0.2 MB) is computed on a host
+    # thread while step i+1's kernels run; every name is done before the timed region ends.
+    from concurrent.futures import ThreadPoolExecutor
+    namer = ThreadPoolExecutor(1)
+    names = []
 
     def step():
         core.reset()
@@ -174,11 +179,15 @@ def main():
             shard.merge_dense(st_t, nov_t)     # all_reduce(MAX) over u64
             core.import_dense(st_t.data_ptr(), nov_t.data_ptr())
         if rank == 0:
-            f, name = core.compact_to_buffer()
-            out["file"], out["name"] = f, name
+            f, _ = core.compact_to_buffer(name=False)
+            out["file"] = f
+            names.append(namer.submit(crdtenc.content_name, f))
 
     for _ in range(args.warmup):
         step()
+    for fu in names:
+        fu.result()
+    names.clear()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -187,6 +196,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    for fu in names:
+        out["name"] = fu.result()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -422,13 +422,15 @@ class Core:
         rc = lib().ce_core_compact(self.p, name)
         return rc, name.value.decode()
 
-    def compact_to_buffer(self, nonce=None):
+    def compact_to_buffer(self, nonce=None, name=True):
+        """(file, content name); name=False skips the SHA3-256 name (None): content_name(file)
+        gives it later, e.g. on another thread."""
         b = Buf()
-        name = ctypes.create_string_buffer(64)
+        nm = ctypes.create_string_buffer(64) if name else None
         rc = lib().ce_core_compact_to_buffer(self.p, _cbuf(nonce) if nonce is not None else None,
-                                             ctypes.byref(b), name)
+                                             ctypes.byref(b), nm)
         self.ctx.check(rc, "compact_to_buffer")
-        return _take(b), name.value.decode()
+        return _take(b), (nm.value.decode() if name else None)
 
     def apply_ops(self, ops_msgpack):
         return lib().ce_core_apply_ops(self.p, _cbuf(ops_msgpack), ctypes.c_size_t(len(ops_msgpack)))

@@ -64,7 +64,7 @@ struct ce_core {
   uint64_t last_writers_gen = ~0ull;
   ce::DevBuf d_table, d_state, d_batch, d_supported, d_refold2, d_tmp, d_gate, d_meta;
   int files_per_wave = 4;  // fused kernel geometry (CE_FILES_PER_WAVE overrides)
-  int fused = 1;           // fused kernel: 1 keystream staged in LDS, 2 block-owning lanes (CE_FUSED)
+  int fused = 2;           // fused kernel: 1 keystream staged in LDS, 2 block-owning lanes (CE_FUSED)
   std::set<std::string> read_states;  // lib.rs:205
   ce_ctx* aux = nullptr;              // single-file work during a batch (exotic envelopes)
   ce::DsState* ds = nullptr;          // Orswot / MVReg state (dot-set kinds only)

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <map>
 #include <set>
+#include <thread>
 
 #include "ce_core.h"
 #include "ce_dotset.h"
@@ -1129,10 +1130,25 @@ int ds_merge_states(ce_core* c, const std::vector<std::pair<const uint8_t*, size
   int first = CE_OK;
   {
     HostPhase hp("states: host parse");
-    for (size_t i = 0; i < n; i++) {
+    // one host thread per state file (files are independent; the merge below stays in order)
+    auto parse = [&](size_t i) {
       if (st[i] == CE_OK && !read_state(c->kind, sws[i].first, sws[i].second, &hs[i])) st[i] = CE_ERR_DECODE;
-      if (st[i] != CE_OK && first == CE_OK) first = st[i];
+    };
+    size_t big = 0;
+    for (size_t i = 0; i < n; i++) big += sws[i].second >= (1u << 16);
+    if (n > 1 && big > 1) {
+      std::vector<std::thread> th;
+      const size_t T = std::min<size_t>(16, n);
+      for (size_t t = 0; t < T; t++)
+        th.emplace_back([&, t] {
+          for (size_t i = t; i < n; i += T) parse(i);
+        });
+      for (auto& x : th) x.join();
+    } else {
+      for (size_t i = 0; i < n; i++) parse(i);
     }
+    for (size_t i = 0; i < n; i++)
+      if (st[i] != CE_OK && first == CE_OK) first = st[i];
   }
   if (status_out) std::memcpy(status_out, st, n * 4);
   if (first != CE_OK) return first;  // nothing merged (lib.rs:431-456)
@@ -1279,42 +1295,63 @@ int ds_serialize(ce_core* c, std::vector<uint8_t>* out) {
   put_vclock(w, uuid_dots(clock));
   w.str("entries");
   w.map(n_members);
-  std::vector<std::pair<uint32_t, uint64_t>> g;  // (rank, counter) of one member
-  // raw-pointer writes into a buffer sized for the worst case, trimmed afterwards
-  size_t pos = w.b.size();
-  w.b.resize(pos + (size_t)n_members * 20 + (size_t)nl * 27 + 64);
-  uint8_t* o = w.b.data();
-  auto put_uint = [&](uint64_t v) {
-    if (v <= 0x7f) { o[pos++] = (uint8_t)v; return; }
-    int k;
-    if (v <= 0xff) { o[pos++] = 0xcc; k = 1; }
-    else if (v <= 0xffff) { o[pos++] = 0xcd; k = 2; }
-    else if (v <= 0xffffffffull) { o[pos++] = 0xce; k = 4; }
-    else { o[pos++] = 0xcf; k = 8; }
-    for (int b = k - 1; b >= 0; b--) o[pos++] = (uint8_t)(v >> (8 * b));
-  };
-  for (uint32_t i = 0; i < nl;) {
-    uint32_t j = i;
-    g.clear();
-    while (j < nl && mem[j] == mem[i]) { g.push_back({rank[act[j]], val[j]}); j++; }
-    if (g.size() > 1) std::sort(g.begin(), g.end());
-    put_uint(mem[i]);
-    std::memcpy(o + pos, "\x81\xa4" "dots", 6);  // VClock {dots: ..}
-    pos += 6;
-    const size_t k = g.size();
-    if (k <= 15) o[pos++] = (uint8_t)(0x80 | k);
-    else if (k <= 0xffff) { o[pos++] = 0xde; o[pos++] = (uint8_t)(k >> 8); o[pos++] = (uint8_t)k; }
-    else { o[pos++] = 0xdf; for (int b = 3; b >= 0; b--) o[pos++] = (uint8_t)(k >> (8 * b)); }
-    for (auto& x : g) {
-      o[pos++] = 0xc4;
-      o[pos++] = 16;
-      std::memcpy(o + pos, c->id_actor[order[x.first]].data(), 16);
-      pos += 16;
-      put_uint(x.second);
+  // members are written in parallel: the sorted pairs are cut at member boundaries into one
+  // chunk per host thread, each chunk written with raw-pointer stores into its own buffer
+  // (sized for the worst case, trimmed), and the chunks appended in order
+  auto write_members = [&](uint32_t i0, uint32_t i1, std::vector<uint8_t>* ob) {
+    std::vector<std::pair<uint32_t, uint64_t>> g;  // (rank, counter) of one member
+    ob->resize((size_t)(i1 - i0) * 47 + 64);
+    uint8_t* o = ob->data();
+    size_t pos = 0;
+    auto put_uint = [&](uint64_t v) {
+      if (v <= 0x7f) { o[pos++] = (uint8_t)v; return; }
+      int k;
+      if (v <= 0xff) { o[pos++] = 0xcc; k = 1; }
+      else if (v <= 0xffff) { o[pos++] = 0xcd; k = 2; }
+      else if (v <= 0xffffffffull) { o[pos++] = 0xce; k = 4; }
+      else { o[pos++] = 0xcf; k = 8; }
+      for (int b = k - 1; b >= 0; b--) o[pos++] = (uint8_t)(v >> (8 * b));
+    };
+    for (uint32_t i = i0; i < i1;) {
+      uint32_t j = i;
+      g.clear();
+      while (j < i1 && mem[j] == mem[i]) { g.push_back({rank[act[j]], val[j]}); j++; }
+      if (g.size() > 1) std::sort(g.begin(), g.end());
+      put_uint(mem[i]);
+      std::memcpy(o + pos, "\x81\xa4" "dots", 6);  // VClock {dots: ..}
+      pos += 6;
+      const size_t k = g.size();
+      if (k <= 15) o[pos++] = (uint8_t)(0x80 | k);
+      else if (k <= 0xffff) { o[pos++] = 0xde; o[pos++] = (uint8_t)(k >> 8); o[pos++] = (uint8_t)k; }
+      else { o[pos++] = 0xdf; for (int b = 3; b >= 0; b--) o[pos++] = (uint8_t)(k >> (8 * b)); }
+      for (auto& x : g) {
+        o[pos++] = 0xc4;
+        o[pos++] = 16;
+        std::memcpy(o + pos, c->id_actor[order[x.first]].data(), 16);
+        pos += 16;
+        put_uint(x.second);
+      }
+      i = j;
     }
-    i = j;
+    ob->resize(pos);
+  };
+  const uint32_t T = nl < (1u << 16) ? 1u : std::min<uint32_t>(16, std::max(1u, std::thread::hardware_concurrency()));
+  std::vector<uint32_t> cut(T + 1, nl);
+  cut[0] = 0;
+  for (uint32_t t = 1; t < T; t++) {
+    uint32_t x = std::max<uint32_t>(cut[t - 1], (uint32_t)((uint64_t)nl * t / T));
+    while (x < nl && x > 0 && mem[x] == mem[x - 1]) x++;
+    cut[t] = x;
   }
-  w.b.resize(pos);
+  std::vector<std::vector<uint8_t>> parts(T);
+  if (T == 1) {
+    write_members(0, nl, &parts[0]);
+  } else {
+    std::vector<std::thread> th;
+    for (uint32_t t = 0; t < T; t++) th.emplace_back(write_members, cut[t], cut[t + 1], &parts[t]);
+    for (auto& x : th) x.join();
+  }
+  for (auto& p : parts) w.b.insert(w.b.end(), p.begin(), p.end());
   w.str("deferred");
   std::vector<std::pair<std::vector<uint8_t>, const std::set<uint64_t>*>> df;
   for (auto& x : d->deferred) {

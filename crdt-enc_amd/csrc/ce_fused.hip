@@ -118,10 +118,13 @@ __device__ __forceinline__ FilePre load_pre(const DecodeArgs& a, uint32_t f) {
   const bool in = f < a.n;
   const uint32_t fi = in ? f : 0u;
   const FileParams* Pp = a.params + fi;
-  bool ok = in && a.status[fi] == CE_OK;
-  if (a.only) ok = ok && a.only[fi] != 0;
-  p.ok = ok;
-  p.apply = a.apply == nullptr || a.apply[fi] != 0;
+  // status, only and apply are independent loads: no per-lane short circuit (that would wait
+  // for each before issuing the next)
+  const int32_t stv = a.status[fi];
+  const uint32_t ov = a.only ? (uint32_t)a.only[fi] : 1u;
+  const uint32_t av = a.apply ? (uint32_t)a.apply[fi] : 1u;
+  p.ok = (uint32_t)in & (uint32_t)(stv == CE_OK) & (uint32_t)(ov != 0);
+  p.apply = av != 0;
   p.len = Pp->len;
   p.in_off = (uint32_t)Pp->in_off;
   p.in_hi = (uint32_t)(Pp->in_off >> 32);
@@ -144,23 +147,35 @@ struct DecState {
 // fl: VersionBytes data-version check (crdt-enc/src/lib.rs:504-505), rmp-serde Vec<Dot<Uuid>>
 // decode (lib.rs:507) and the max-fold of the dots of applied files (VClock::apply).  `live` =
 // the file is active and its tag verified.  Called from wave-uniform control flow (ballots).
-template <int LPF>
-__device__ __forceinline__ void decode_fold(const DecodeArgs& a, const uint8_t* fl, uint32_t len,
-                                            bool live, bool apply, uint32_t f, uint32_t grp,
-                                            uint32_t sub, DecState& S) {
+// the supported data versions (Core's supported_data_versions), the first two held in registers
+// for the whole kernel so the per-file check issues no global load
+struct SupVers {
+  uint4 v0, v1;
+  __device__ __forceinline__ explicit SupVers(const DecodeArgs& a) {
+    v0 = a.n_supported > 0 ? *reinterpret_cast<const uint4*>(a.supported) : make_uint4(0, 0, 0, 0);
+    v1 = a.n_supported > 1 ? *reinterpret_cast<const uint4*>(a.supported + 16) : make_uint4(0, 0, 0, 0);
+  }
+  __device__ __forceinline__ bool has(const DecodeArgs& a, const uint4& dv) const {
+    auto eq = [&](const uint4& x) { return dv.x == x.x && dv.y == x.y && dv.z == x.z && dv.w == x.w; };
+    bool found = (a.n_supported > 0 && eq(v0)) || (a.n_supported > 1 && eq(v1));
+    for (uint32_t s = 2; s < a.n_supported; s++) found |= eq(*reinterpret_cast<const uint4*>(a.supported + 16 * s));
+    return found;
+  }
+};
+
+// `prefetch` (the next file's parameters) is called once, after the decode's first round: a
+// global load issued before the round's actor-table lookups would be waited for with them
+// (vmcnt counts in order), exposing its latency.
+template <int LPF, typename Pf>
+__device__ __forceinline__ void decode_fold(const DecodeArgs& a, const SupVers& sup, const uint8_t* fl,
+                                            uint32_t len, bool live, bool apply, uint32_t f,
+                                            uint32_t grp, uint32_t sub, DecState& S, Pf&& prefetch) {
   int32_t st = CE_OK;
   if (live) {
     if (len < 16) st = CE_ERR_PT_LEN;
-    else {
-      const uint4 dv = *reinterpret_cast<const uint4*>(fl);
-      bool found = false;
-      for (uint32_t s = 0; s < a.n_supported; s++) {
-        const uint4 sv = *reinterpret_cast<const uint4*>(a.supported + 16 * s);
-        found |= dv.x == sv.x && dv.y == sv.y && dv.z == sv.z && dv.w == sv.w;
-      }
-      if (!found) st = CE_ERR_PT_VERSION;
-    }
+    else if (!sup.has(a, *reinterpret_cast<const uint4*>(fl))) st = CE_ERR_PT_VERSION;
   }
+  bool pf_done = false;
   const uint8_t* body = fl + 16;
   const uint32_t blen = len >= 16 ? len - 16 : 0;
   uint64_t remaining = 0;
@@ -236,6 +251,10 @@ __device__ __forceinline__ void decode_fold(const DecodeArgs& a, const uint8_t* 
                                : bad1 ? (uint32_t)LPF + (uint32_t)__builtin_ctzll(bad1) : 2u * LPF;
       if (do_fold && need[0] && sub < kk) fold_dot(k0[0], k1[0], k2[0], k3[0], ctr[0]);
       if (do_fold && need[1] && LPF + sub < kk) fold_dot(k0[1], k1[1], k2[1], k3[1], ctr[1]);
+      if (!pf_done) {
+        prefetch();
+        pf_done = true;
+      }
       if (fb) {
         const bool bad = (bad0 | bad1) != 0;
         const uint64_t left = remaining - done;
@@ -245,6 +264,10 @@ __device__ __forceinline__ void decode_fold(const DecodeArgs& a, const uint8_t* 
     }
     pos += done * L0;
     remaining -= done;
+  }
+  if (!pf_done) {
+    prefetch();
+    pf_done = true;
   }
   for (;;) {
     const bool busy = live && st == CE_OK && remaining > 0;
@@ -366,6 +389,7 @@ void k_open_fold_small(DecodeArgs a) {
 
   uint32_t g = bcast(blockIdx.x * C::WPB + wib);
   FilePre nx = load_pre<C::LOG + C::LOGCH>(a, g * F + grp);
+  const SupVers sup(a);
   // decode state carried across files: speculated Dot length, per-lane actor cache
   DecState S{38, 0, 0, 0, 0, 0xffffffffu};
 
@@ -533,8 +557,6 @@ void k_open_fold_small(DecodeArgs a) {
     }
     bool ok = grp_bits<LPF>(tag_ok, grp) != 0;
 
-    // next iteration's parameters: their latency hides under the decode
-    nx = load_pre<C::LOG + C::LOGCH>(a, (g + stride) * F + grp);
     CE_PHASE(3)
 
     // 5)+6) data-version check, decode from LDS, fold
@@ -542,7 +564,9 @@ void k_open_fold_small(DecodeArgs a) {
     if (a.ablate) ok = !(a.ablate & 1);
 #endif
     CE_PHASE(4)
-    decode_fold<LPF>(a, fl, len, act && ok, cur.apply != 0, f, grp, sub, S);
+    // the next iteration's parameters are loaded inside (their latency hides under the decode)
+    decode_fold<LPF>(a, sup, fl, len, act && ok, cur.apply != 0, f, grp, sub, S,
+                     [&] { nx = load_pre<C::LOG + C::LOGCH>(a, (g + stride) * F + grp); });
     __builtin_amdgcn_wave_barrier();
     CE_PHASE(5)
 #if CE_FUSED_DIAG
@@ -614,7 +638,6 @@ struct V2Cfg {
   static constexpr int F = 64 / LPF;               // files per wave
   static constexpr int BPL = 64 / LPF;             // ChaCha20 blocks per lane (one page)
   static constexpr int LOG = LPF == 16 ? 4 : 5;    // tree levels
-  static constexpr int WAVES = LPF == 16 ? 3 : 4;  // VGPR budget (LDS: 2.5 / 5 waves per SIMD)
   static constexpr int NRP = LPF == 16 ? 8 : 9;    // 16-byte loads of r^(2^k), k <= LOG + 1
 };
 
@@ -631,10 +654,13 @@ __device__ __forceinline__ FilePre2 load_pre2(const DecodeArgs& a, uint32_t f) {
   const bool in = f < a.n;
   const uint32_t fi = in ? f : 0u;
   const FileParams* Pp = a.params + fi;
-  bool ok = in && a.status[fi] == CE_OK;
-  if (a.only) ok = ok && a.only[fi] != 0;
-  p.ok = ok;
-  p.apply = a.apply == nullptr || a.apply[fi] != 0;
+  // status, only and apply are independent loads: no per-lane short circuit (that would wait
+  // for each before issuing the next)
+  const int32_t stv = a.status[fi];
+  const uint32_t ov = a.only ? (uint32_t)a.only[fi] : 1u;
+  const uint32_t av = a.apply ? (uint32_t)a.apply[fi] : 1u;
+  p.ok = (uint32_t)in & (uint32_t)(stv == CE_OK) & (uint32_t)(ov != 0);
+  p.apply = av != 0;
   p.len = Pp->len;
   p.in_off = (uint32_t)Pp->in_off;
   p.in_hi = (uint32_t)(Pp->in_off >> 32);
@@ -650,8 +676,9 @@ __device__ __forceinline__ FilePre2 load_pre2(const DecodeArgs& a, uint32_t f) {
   return p;
 }
 
-template <int LPF>
-__global__ __launch_bounds__(64, V2Cfg<LPF>::WAVES)
+// W = waves per SIMD the VGPR budget is sized for (LDS allows 2.5 at LPF 16, 5 at LPF 32)
+template <int LPF, int W>
+__global__ __launch_bounds__(64, W)
 void k_open_fold_v2(DecodeArgs a) {
   using C = V2Cfg<LPF>;
   constexpr int F = C::F;
@@ -664,6 +691,7 @@ void k_open_fold_v2(DecodeArgs a) {
   const uint32_t stride = gridDim.x;
   uint32_t g = bcast(blockIdx.x);
   FilePre2 nx = load_pre2(a, g * F + grp);
+  const SupVers sup(a);
   DecState S{38, 0, 0, 0, 0, 0xffffffffu};
 
   for (; g < ngroups; g += stride) {
@@ -704,10 +732,23 @@ void k_open_fold_v2(DecodeArgs a) {
     }
     if (LPF == 32) RC = mulmod(RC, RC);  // chain step r^(4 LPF) = r^128
     L5 acc{{0, 0, 0, 0, 0}}, glast{{0, 0, 0, 0, 0}};
+    uint32_t rp[4 * C::NRP];  // r^(2^k), k <= LOG + 1
+    uint4 sv4, tg4;           // s || expected tag
 #pragma unroll
     for (int k = BPL - 1; k >= 0; k--) {
       const int32_t b = nblk - 1 - (int32_t)sub - LPF * k;
       const bool has = b >= 0;
+      if (k == 0) {
+        // the tree's powers, s and the tag: issued before the last block's ChaCha20 so their
+        // latency hides under it (the other blocks' ciphertext registers are free by now)
+#pragma unroll
+        for (int q = 0; q < C::NRP; q++) {
+          const uint4 v = *reinterpret_cast<const uint4*>(&Pp->rpow[0][0] + 4 * q);
+          rp[4 * q] = v.x; rp[4 * q + 1] = v.y; rp[4 * q + 2] = v.z; rp[4 * q + 3] = v.w;
+        }
+        sv4 = *reinterpret_cast<const uint4*>(Pp->s);
+        tg4 = *reinterpret_cast<const uint4*>(Pp->tag);
+      }
       uint32_t kb[16];
       chacha_block_pre(cpre, cur.key, 1u + (uint32_t)b, 0u, cur.n2a, cur.n2b, kb);
       L5 G;
@@ -757,16 +798,6 @@ void k_open_fold_v2(DecodeArgs a) {
       }
     }
 
-    // r^(2^k), k <= LOG + 1; s || expected tag
-    uint32_t rp[4 * C::NRP];
-#pragma unroll
-    for (int q = 0; q < C::NRP; q++) {
-      const uint4 v = *reinterpret_cast<const uint4*>(&Pp->rpow[0][0] + 4 * q);
-      rp[4 * q] = v.x; rp[4 * q + 1] = v.y; rp[4 * q + 2] = v.z; rp[4 * q + 3] = v.w;
-    }
-    const uint4 sv4 = *reinterpret_cast<const uint4*>(Pp->s);
-    const uint4 tg4 = *reinterpret_cast<const uint4*>(Pp->tag);
-
     // 3) chains -> tree positions (q takes lane q + 1's chain, q = LPF - 1 lane 0's), then
     //    U = sum_q v_q r^(4q) at q = 0
     const int srcl = (int)(grp * LPF + ((sub + 1) & (LPF - 1)));
@@ -811,25 +842,34 @@ void k_open_fold_v2(DecodeArgs a) {
     }
     const bool ok = grp_bits<LPF>(tag_ok, grp) != 0;
 
-    // next iteration's parameters: their latency hides under the decode
-    nx = load_pre2(a, (g + stride) * F + grp);
-
-    // 4) data-version check, decode from LDS, fold
-    decode_fold<LPF>(a, fl, len, act && ok, cur.apply != 0, f, grp, sub, S);
+    // 4) data-version check, decode from LDS, fold; the next iteration's parameters are loaded
+    //    inside (their latency hides under the decode)
+    decode_fold<LPF>(a, sup, fl, len, act && ok, cur.apply != 0, f, grp, sub, S,
+                     [&] { nx = load_pre2(a, (g + stride) * F + grp); });
     __builtin_amdgcn_wave_barrier();
   }
 }
 
+template <int LPF, int W>
+static void launch_v2(hipStream_t s, const DecodeArgs& a) {
+  static const uint32_t res = resident_blocks(k_open_fold_v2<LPF, W>, 64);
+  const uint32_t groups = (a.n + 64 / LPF - 1) / (64 / LPF);
+  hipLaunchKernelGGL((k_open_fold_v2<LPF, W>), dim3(std::min<uint32_t>(groups, res)), dim3(64), 0, s, a);
+}
+
 hipError_t launch_open_fold_v2(hipStream_t s, const DecodeArgs& a, int files_per_wave) {
   if (a.n == 0) return hipSuccess;
-  static const uint32_t res16 = resident_blocks(k_open_fold_v2<16>, 64);
-  static const uint32_t res32 = resident_blocks(k_open_fold_v2<32>, 64);
+  // VGPR budget (CE_V2_WAVES, diagnostics): 2 or 3 waves per SIMD at LPF 16, 3 or 4 at LPF 32
+  static const int w = [] {
+    const char* e = getenv("CE_V2_WAVES");
+    return e ? atoi(e) : 0;
+  }();
   if (files_per_wave == 2) {
-    const uint32_t groups = (a.n + 1) / 2;
-    hipLaunchKernelGGL(k_open_fold_v2<32>, dim3(std::min<uint32_t>(groups, res32)), dim3(64), 0, s, a);
+    if (w == 4) launch_v2<32, 4>(s, a);
+    else launch_v2<32, 3>(s, a);
   } else {
-    const uint32_t groups = (a.n + 3) / 4;
-    hipLaunchKernelGGL(k_open_fold_v2<16>, dim3(std::min<uint32_t>(groups, res16)), dim3(64), 0, s, a);
+    if (w == 3) launch_v2<16, 3>(s, a);
+    else launch_v2<16, 2>(s, a);
   }
   return hipGetLastError();
 }
