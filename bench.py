@@ -267,7 +267,11 @@ def main():
         tf = os.path.join(REPO, "profiles", "traffic_open_fold_small.json")
         if os.path.exists(tf):
             with open(tf) as f:
-                traffic = json.load(f).get("bytes_per_launch")
+                rec = json.load(f)
+            # only a measurement of the kernel this run used (and of the same 1M-file launch)
+            if kname.split(" (")[0].rstrip(">") in rec.get("kernel", "") and \
+                    rec.get("files_per_launch") == n:
+                traffic = rec.get("bytes_per_launch")
         fused = os.environ.get("CE_FUSED", str(DEFAULT_FUSED))
         lpf = 64 // int(os.environ.get("CE_FILES_PER_WAVE", "4"))
         kname = ("k_open_fold_v2<%d> (XChaCha20-Poly1305 open + Vec<Dot> decode + fold, "

@@ -134,6 +134,49 @@ __device__ __forceinline__ L5 mulmod(const L5& h, const L5& r) {
   return o;
 }
 
+// A multiplier with its 5x limbs (2^130 = 5 mod p), for sums of products reduced once:
+// mac5 adds h * r into five 64-bit column sums without carrying, reduce5 carries them.  Each
+// product adds < 5 * 2^27 * 2^28.4 < 2^57.7 per column (h limbs < 2^27), so up to 64 products
+// fit a column; reduce5 keeps every carry in 64 bits.
+struct MulR {
+  uint32_t v[5], s[4];  // s[i] = 5 * v[i + 1]
+};
+
+__device__ __forceinline__ MulR mul_r(const L5& r) {
+  MulR o;
+#pragma unroll
+  for (int i = 0; i < 5; i++) o.v[i] = r.v[i];
+#pragma unroll
+  for (int i = 0; i < 4; i++) o.s[i] = r.v[i + 1] * 5;
+  return o;
+}
+
+__device__ __forceinline__ void mac5(uint64_t (&d)[5], const L5& h, const MulR& r) {
+  d[0] += (uint64_t)h.v[0] * r.v[0] + (uint64_t)h.v[1] * r.s[3] + (uint64_t)h.v[2] * r.s[2] +
+          (uint64_t)h.v[3] * r.s[1] + (uint64_t)h.v[4] * r.s[0];
+  d[1] += (uint64_t)h.v[0] * r.v[1] + (uint64_t)h.v[1] * r.v[0] + (uint64_t)h.v[2] * r.s[3] +
+          (uint64_t)h.v[3] * r.s[2] + (uint64_t)h.v[4] * r.s[1];
+  d[2] += (uint64_t)h.v[0] * r.v[2] + (uint64_t)h.v[1] * r.v[1] + (uint64_t)h.v[2] * r.v[0] +
+          (uint64_t)h.v[3] * r.s[3] + (uint64_t)h.v[4] * r.s[2];
+  d[3] += (uint64_t)h.v[0] * r.v[3] + (uint64_t)h.v[1] * r.v[2] + (uint64_t)h.v[2] * r.v[1] +
+          (uint64_t)h.v[3] * r.v[0] + (uint64_t)h.v[4] * r.s[3];
+  d[4] += (uint64_t)h.v[0] * r.v[4] + (uint64_t)h.v[1] * r.v[3] + (uint64_t)h.v[2] * r.v[2] +
+          (uint64_t)h.v[3] * r.v[1] + (uint64_t)h.v[4] * r.v[0];
+}
+
+__device__ __forceinline__ L5 reduce5(uint64_t (&d)[5]) {
+  L5 o;
+  d[1] += d[0] >> 26; o.v[0] = (uint32_t)d[0] & M26;
+  d[2] += d[1] >> 26; o.v[1] = (uint32_t)d[1] & M26;
+  d[3] += d[2] >> 26; o.v[2] = (uint32_t)d[2] & M26;
+  d[4] += d[3] >> 26; o.v[3] = (uint32_t)d[3] & M26;
+  o.v[4] = (uint32_t)d[4] & M26;
+  const uint64_t t = (d[4] >> 26) * 5 + o.v[0];
+  o.v[0] = (uint32_t)t & M26;
+  o.v[1] += (uint32_t)(t >> 26);
+  return o;
+}
+
 __device__ __forceinline__ L5 add5(const L5& a, const L5& b) {
   L5 o;
 #pragma unroll

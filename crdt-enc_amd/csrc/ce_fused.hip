@@ -677,7 +677,7 @@ __device__ __forceinline__ FilePre2 load_pre2(const DecodeArgs& a, uint32_t f) {
 }
 
 // W = waves per SIMD the VGPR budget is sized for (LDS allows 2.5 at LPF 16, 5 at LPF 32)
-template <int LPF, int W>
+template <int LPF, int W, bool JIT>
 __global__ __launch_bounds__(64, W)
 void k_open_fold_v2(DecodeArgs a) {
   using C = V2Cfg<LPF>;
@@ -709,16 +709,22 @@ void k_open_fold_v2(DecodeArgs a) {
     // 1) the lane's ciphertext runs -> registers.  The 16-byte tag follows the ciphertext, so a
     //    16-byte load at any piece < npc stays inside the file; absent pieces load piece 0.
     uint4 ct[BPL][4];
-#pragma unroll
-    for (int k = BPL - 1; k >= 0; k--) {
+    auto load_block = [&](int k) {
       const int32_t b = nblk - 1 - (int32_t)sub - LPF * k;
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         const uint32_t q = (uint32_t)(4 * b + j);
         const uint32_t off = b >= 0 && q < npc ? q * 16u : 0u;
         ct[k][j] = *reinterpret_cast<const uint4*>(src + off);
+#if CE_FUSED_DIAG
+        if (a.ablate & 8) ct[k][j] = make_uint4(off, len, sub, (uint32_t)k);
+#endif
       }
-    }
+    };
+    // JIT: block k - 1's loads are issued when block k starts (half the ciphertext registers);
+    // otherwise every block's loads are issued up front
+#pragma unroll
+    for (int k = BPL - 1; k >= (JIT ? BPL - 1 : 0); k--) load_block(k);
 
     // 2) per block, earliest first: keystream (counter 1 + b) in registers, XOR, plaintext ->
     //    LDS, Poly1305.  Branch-free: lanes without a block (short files) compute garbage that
@@ -731,6 +737,10 @@ void k_open_fold_v2(DecodeArgs a) {
       RC.v[i] = cur.R64[i];
     }
     if (LPF == 32) RC = mulmod(RC, RC);  // chain step r^(4 LPF) = r^128
+    L5 R2;
+#pragma unroll
+    for (int i = 0; i < 5; i++) R2.v[i] = Pp->rpow[1][i];
+    const MulR M1 = mul_r(R1), M2 = mul_r(R2), M3 = mul_r(mulmod(R2, R1)), MC = mul_r(RC);
     L5 acc{{0, 0, 0, 0, 0}}, glast{{0, 0, 0, 0, 0}};
     uint32_t rp[4 * C::NRP];  // r^(2^k), k <= LOG + 1
     uint4 sv4, tg4;           // s || expected tag
@@ -738,6 +748,10 @@ void k_open_fold_v2(DecodeArgs a) {
     for (int k = BPL - 1; k >= 0; k--) {
       const int32_t b = nblk - 1 - (int32_t)sub - LPF * k;
       const bool has = b >= 0;
+      if (JIT && k > 0) {
+        load_block(k - 1);
+        __builtin_amdgcn_sched_barrier(0);  // keep the loads here, ahead of this block's ChaCha20
+      }
       if (k == 0) {
         // the tree's powers, s and the tag: issued before the last block's ChaCha20 so their
         // latency hides under it (the other blocks' ciphertext registers are free by now)
@@ -750,8 +764,14 @@ void k_open_fold_v2(DecodeArgs a) {
         tg4 = *reinterpret_cast<const uint4*>(Pp->tag);
       }
       uint32_t kb[16];
-      chacha_block_pre(cpre, cur.key, 1u + (uint32_t)b, 0u, cur.n2a, cur.n2b, kb);
-      L5 G;
+#if CE_FUSED_DIAG
+      if (a.ablate & 4) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) kb[i] = cur.key[i & 7] + (uint32_t)b;
+      } else
+#endif
+        chacha_block_pre(cpre, cur.key, 1u + (uint32_t)b, 0u, cur.n2a, cur.n2b, kb);
+      L5 G, mj[4];
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         const uint32_t q = (uint32_t)(4 * b + j);
@@ -775,10 +795,16 @@ void k_open_fold_v2(DecodeArgs a) {
         *reinterpret_cast<uint4*>(fl + st_off) =
             make_uint4(xw[0] ^ kw[0], xw[1] ^ kw[1], xw[2] ^ kw[2], xw[3] ^ kw[3]);
         const L5 m = block_limbs(xw[0], xw[1], xw[2], xw[3]);
-        if (j == 0) {
+        if (k > 0) {
+          mj[j] = m;   // a full block: Poly1305 below, one reduction for the whole block
+        } else if (j == 0) {
           G = m;  // piece 4 b exists whenever the block does
         } else {
+#if CE_FUSED_DIAG
+          const L5 gn = (a.ablate & 2) ? add5(G, m) : add5(mulmod(G, R1), m);
+#else
           const L5 gn = add5(mulmod(G, R1), m);
+#endif
           if (k == 0) {
             const bool ex = q < npc;
 #pragma unroll
@@ -788,7 +814,19 @@ void k_open_fold_v2(DecodeArgs a) {
           }
         }
       }
-      const L5 an = add5(mulmod(acc, RC), G);
+      L5 an;
+      if (k > 0) {
+        // every block but slot 0 is full: acc r^(4 LPF) + m0 r^3 + m1 r^2 + m2 r + m3 as four
+        // products into one set of column sums, carried once (vs four Horner mulmods)
+        uint64_t d[5] = {mj[3].v[0], mj[3].v[1], mj[3].v[2], mj[3].v[3], mj[3].v[4]};
+        mac5(d, acc, MC);
+        mac5(d, mj[0], M3);
+        mac5(d, mj[1], M2);
+        mac5(d, mj[2], M1);
+        an = reduce5(d);
+      } else {
+        an = add5(mulmod(acc, RC), G);
+      }
       const bool to_acc = has && !(k == 0 && sub == 0);
 #pragma unroll
       for (int i = 0; i < 5; i++) acc.v[i] = to_acc ? an.v[i] : acc.v[i];
@@ -812,7 +850,7 @@ void k_open_fold_v2(DecodeArgs a) {
         rk.v[i] = rp[5 * (k + 2) + i];
         o.v[i] = k < 4 ? row_down(v.v[i], 1 << k) : (uint32_t)__shfl_down((int)v.v[i], 16);
       }
-      v = carry5(add5(v, mulmod(o, rk)));
+      v = add5(v, mulmod(o, rk));  // limbs < 2^28 after 4 levels: mulmod carries in 64 bits
     }
     // T = (U r^(5 - delta) + G' r + lenblock) r; r^(5 - delta) = r^4 r, r^4, r^2 r, r^2
     const uint32_t delta = (uint32_t)(4 * nblk) - npc;
@@ -840,7 +878,10 @@ void k_open_fold_v2(DecodeArgs a) {
         atomicMin(&a.counters[5], f);
       }
     }
-    const bool ok = grp_bits<LPF>(tag_ok, grp) != 0;
+    bool ok = grp_bits<LPF>(tag_ok, grp) != 0;
+#if CE_FUSED_DIAG
+    if (a.ablate) ok = !(a.ablate & 1);
+#endif
 
     // 4) data-version check, decode from LDS, fold; the next iteration's parameters are loaded
     //    inside (their latency hides under the decode)
@@ -850,11 +891,11 @@ void k_open_fold_v2(DecodeArgs a) {
   }
 }
 
-template <int LPF, int W>
+template <int LPF, int W, bool JIT>
 static void launch_v2(hipStream_t s, const DecodeArgs& a) {
-  static const uint32_t res = resident_blocks(k_open_fold_v2<LPF, W>, 64);
+  static const uint32_t res = resident_blocks(k_open_fold_v2<LPF, W, JIT>, 64);
   const uint32_t groups = (a.n + 64 / LPF - 1) / (64 / LPF);
-  hipLaunchKernelGGL((k_open_fold_v2<LPF, W>), dim3(std::min<uint32_t>(groups, res)), dim3(64), 0, s, a);
+  hipLaunchKernelGGL((k_open_fold_v2<LPF, W, JIT>), dim3(std::min<uint32_t>(groups, res)), dim3(64), 0, s, a);
 }
 
 hipError_t launch_open_fold_v2(hipStream_t s, const DecodeArgs& a, int files_per_wave) {
@@ -864,12 +905,15 @@ hipError_t launch_open_fold_v2(hipStream_t s, const DecodeArgs& a, int files_per
     const char* e = getenv("CE_V2_WAVES");
     return e ? atoi(e) : 0;
   }();
+  // CE_V2_WAVES (diagnostics): 13 = 3 waves/SIMD with JIT ciphertext loads, 12 = 2 with them
   if (files_per_wave == 2) {
-    if (w == 4) launch_v2<32, 4>(s, a);
-    else launch_v2<32, 3>(s, a);
+    if (w == 4) launch_v2<32, 4, false>(s, a);
+    else launch_v2<32, 3, false>(s, a);
   } else {
-    if (w == 3) launch_v2<16, 3>(s, a);
-    else launch_v2<16, 2>(s, a);
+    if (w == 3) launch_v2<16, 3, false>(s, a);
+    else if (w == 13) launch_v2<16, 3, true>(s, a);
+    else if (w == 12) launch_v2<16, 2, true>(s, a);
+    else launch_v2<16, 2, false>(s, a);
   }
   return hipGetLastError();
 }

@@ -24,16 +24,19 @@ def per_launch(counter):
     vals = {}
     for fn in glob.glob(os.path.join(out, counter, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(fn)):
-            if "k_open_fold_small" in row["Kernel_Name"] and row["Counter_Name"] == counter:
+            if "k_open_fold" in row["Kernel_Name"] and row["Counter_Name"] == counter:
                 vals.setdefault(row["Dispatch_Id"], []).append((float(row["Counter_Value"]), row["Grid_Size"]))
+                kernel[0] = row["Kernel_Name"]
     return [sum(v for v, _ in x) for x in vals.values()]
+
+kernel = [""]
 
 fs, ws = per_launch("FETCH_SIZE"), per_launch("WRITE_SIZE")
 if fs and ws:
     fetch = sum(fs) / len(fs) * 1024 * 2
     write = sum(ws) / len(ws) * 1024
     files = 1 << 20
-    rec = {"kernel": "k_open_fold_small<16>", "launches_measured": [len(fs), len(ws)],
+    rec = {"kernel": kernel[0], "launches_measured": [len(fs), len(ws)],
            "files_per_launch": files,
            "fetch_bytes_per_launch": round(fetch), "write_bytes_per_launch": round(write),
            "bytes_per_launch": round(fetch + write),
