@@ -263,6 +263,11 @@ def main():
         ops_per_file = 992 * -(-PT_LEN // 64) + 48 * (-(-PT_LEN // 16) + 1)
         achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
         valu = n * ops_per_file / avg_s / 1e12 if avg_s > 0 else 0.0
+        fused = os.environ.get("CE_FUSED", str(DEFAULT_FUSED))
+        lpf = 64 // int(os.environ.get("CE_FILES_PER_WAVE", "4"))
+        kname = ("k_open_fold_v2<%d> (XChaCha20-Poly1305 open + Vec<Dot> decode + fold, "
+                 "lane-owned ChaCha20 blocks)" % lpf if fused == "2" and lpf != 64 else
+                 "k_open_fold_small<%d> (XChaCha20-Poly1305 open + Vec<Dot> decode + fold)" % lpf)
         traffic = None
         tf = os.path.join(REPO, "profiles", "traffic_open_fold_small.json")
         if os.path.exists(tf):
@@ -272,11 +277,6 @@ def main():
             if kname.split(" (")[0].rstrip(">") in rec.get("kernel", "") and \
                     rec.get("files_per_launch") == n:
                 traffic = rec.get("bytes_per_launch")
-        fused = os.environ.get("CE_FUSED", str(DEFAULT_FUSED))
-        lpf = 64 // int(os.environ.get("CE_FILES_PER_WAVE", "4"))
-        kname = ("k_open_fold_v2<%d> (XChaCha20-Poly1305 open + Vec<Dot> decode + fold, "
-                 "lane-owned ChaCha20 blocks)" % lpf if fused == "2" and lpf != 64 else
-                 "k_open_fold_small<%d> (XChaCha20-Poly1305 open + Vec<Dot> decode + fold)" % lpf)
         line = {
             "metric": METRIC,
             "value": round(n * world / (ms_max / 1e3), 1),

@@ -41,6 +41,9 @@ PT_LEN = len(HDR) + N_ADD * len(ADD_T) + N_RM * len(RM_T)
 assert (len(ADD_T), len(RM_T), PT_LEN) == (62, 55, 1961)
 
 
+HOST_PROF = bool(os.environ.get("CE_HOST_PROF"))
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -155,8 +158,12 @@ def run_c3(args, ctx, dev):
     # the SHA3-256 content name of step i's state file is computed on a host thread while step
     # i+1 runs (as in bench.py); every name is done before the timed region ends
     from concurrent.futures import ThreadPoolExecutor
-    namer = ThreadPoolExecutor(1)
+    # SHA3-256 is a sequential sponge (~200 MB/s per core): one 8 MB name takes about as long
+    # as the rest of a step, so two host threads hash consecutive steps' files side by side
+    NB = 3
+    namer = ThreadPoolExecutor(NB - 1)
     names = []
+    obuf = [np.empty(1 << 20, np.uint8) for _ in range(NB)]
 
     def step():
         t = time.perf_counter()
@@ -171,9 +178,18 @@ def run_c3(args, ctx, dev):
         if rc:
             raise crdtenc.CeError(rc, ctx.last_error())
         t3 = time.perf_counter()
-        out["file"], _ = core.compact_to_buffer(name=False)
+        # NB reused output buffers: NB - 1 namer threads hash the previous steps' files while
+        # this step fills the next buffer (its last hash is awaited before it is written again)
+        k = len(names) % NB
+        if len(names) >= NB:
+            names[-NB].result()
+        obuf[k], ln, _ = core.compact_into(obuf[k], name=False)
+        out["file"] = obuf[k][:ln]
+        t35 = time.perf_counter()
         names.append(namer.submit(crdtenc.content_name, out["file"]))
         t4 = time.perf_counter()
+        if HOST_PROF:
+            log("py: compact_to_buffer %.3f ms, submit %.3f ms" % ((t35 - t3) * 1e3, (t4 - t35) * 1e3))
         for k, a, b in (("reset", t, t1), ("states", t1, t2), ("ops", t2, t3), ("compact", t3, t4)):
             phase[k] += (b - a) * 1e3
 

@@ -41,6 +41,7 @@ EXPORTS = [
     "ce_core_close", "ce_core_set_latest_key", "ce_core_info_actor", "ce_core_read_remote",
     "ce_core_compact", "ce_core_apply_ops", "ce_core_state_bytes", "ce_core_ingest_ops",
     "ce_core_ingest_ops_device", "ce_core_ingest_states", "ce_core_compact_to_buffer",
+    "ce_core_compact_into",
     "ce_core_register_actors", "ce_core_dense_capacity", "ce_core_export_dense",
     "ce_core_import_dense", "ce_vbuf_init", "ce_vbuf_remaining", "ce_vbuf_chunk",
     "ce_vbuf_advance", "ce_vbuf_chunks_vectored", "ce_ctx_set_timing", "ce_ctx_timing_read",
@@ -115,9 +116,21 @@ def sealed_len(n):
     return lib().ce_cryptor_sealed_len(n)
 
 
+def _ptr(data):
+    """(pointer, length) of bytes / bytearray / a contiguous uint8 numpy array, without a copy
+    (the object must outlive the call)."""
+    if isinstance(data, bytes):
+        return ctypes.c_char_p(data), len(data)
+    mv = memoryview(data).cast("B")
+    if mv.readonly:
+        return _cbuf(data), mv.nbytes
+    return (ctypes.c_char * mv.nbytes).from_buffer(mv), mv.nbytes
+
+
 def content_name(data):
     out = ctypes.create_string_buffer(64)
-    rc = lib().ce_content_name(_cbuf(data), ctypes.c_size_t(len(data)), out)
+    p, n = _ptr(data)
+    rc = lib().ce_content_name(p, ctypes.c_size_t(n), out)
     if rc:
         raise CeError(rc)
     return out.value.decode()
@@ -431,6 +444,23 @@ class Core:
                                              ctypes.byref(b), nm)
         self.ctx.check(rc, "compact_to_buffer")
         return _take(b), (nm.value.decode() if name else None)
+
+    def compact_into(self, buf, nonce=None, name=True):
+        """compact_to_buffer into a caller-owned uint8 numpy array `buf` (grown when too small,
+        so pass the returned array back next time): (array, length, content name or None)."""
+        import numpy as np
+        n = ctypes.c_size_t(0)
+        nm = ctypes.create_string_buffer(64) if name else None
+        nc = _cbuf(nonce) if nonce is not None else None
+        for _ in range(2):
+            rc = lib().ce_core_compact_into(self.p, nc, ctypes.c_void_p(buf.ctypes.data),
+                                            ctypes.c_size_t(buf.nbytes), ctypes.byref(n), nm)
+            if rc == 64 and n.value > buf.nbytes:
+                buf = np.empty(n.value + (n.value >> 3), np.uint8)
+                continue
+            break
+        self.ctx.check(rc, "compact_into")
+        return buf, n.value, (nm.value.decode() if name else None)
 
     def apply_ops(self, ops_msgpack):
         return lib().ce_core_apply_ops(self.p, _cbuf(ops_msgpack), ctypes.c_size_t(len(ops_msgpack)))

@@ -386,6 +386,8 @@ int serialize_state(ce_core* c, std::vector<uint8_t>* out) {
   size_t n_nov = 0, n_st = 0;
   for (uint32_t s : slots) { n_nov += c->nov[s] != 0; n_st += st[s] != 0; }
   Wr w;
+  w.b.swap(*out);  // reuse the caller's capacity
+  w.b.clear();
   w.b.reserve(64 + 28 * (n_nov + n_st));
   w.map(2);
   w.str("next_op_versions");
@@ -401,7 +403,7 @@ int serialize_state(ce_core* c, std::vector<uint8_t>* out) {
   w.map(n_st);
   for (uint32_t s : slots)
     if (st[s]) { w.bin(c->slot_actor[s].data(), 16); w.uint(st[s]); }
-  *out = std::move(w.b);
+  out->swap(w.b);
   return CE_OK;
 }
 
@@ -966,15 +968,13 @@ int read_remote(ce_core* c) {
 int compact_bytes(ce_core* c, const uint8_t* nonce, std::vector<uint8_t>* file) {
   HostPhase hp("compact_bytes");
   if (!c->has_key) return c->ctx->fail(CE_ERR_NO_KEY, "no latest key");
-  std::vector<uint8_t> clear;
+  std::vector<uint8_t>& clear = c->ser_buf;
   int rc = serialize_state(c, &clear);
   if (rc) return rc;
-  if (c->flags & CE_COMPACT_INGEST_FORMAT) {
-    // readable by read_remote_states: CURRENT_VERSION || encrypt(data_version || state)
-    std::vector<uint8_t> vb(c->current_data_version.begin(), c->current_data_version.end());
-    vb.insert(vb.end(), clear.begin(), clear.end());
-    return seal_one(c->ctx, key_of(c), kCoreVersion, nonce, vb.data(), vb.size(), file);
-  }
+  HostPhase hs("compact: seal");
+  if (c->flags & CE_COMPACT_INGEST_FORMAT)  // readable by read_remote_states: CURRENT_VERSION ||
+    return seal_one(c->ctx, key_of(c), kCoreVersion, nonce, clear.data(), clear.size(), file,
+                    c->current_data_version.data());  // encrypt(data_version || state)
   // exactly what Core::compact writes: VersionBytes(current_data_version, encrypt(state))
   return seal_one(c->ctx, key_of(c), c->current_data_version.data(), nonce, clear.data(),
                   clear.size(), file);
@@ -1117,6 +1117,7 @@ int ce_core_ingest_ops_device(ce_core* c, const uint8_t* d_blob, const uint64_t*
                               int32_t* status) {
   if (!c || (n && (!d_blob || !d_offs || !actors || !d_file_actor || !d_file_version)))
     return CE_ERR_INVALID_ARG;
+  HostPhase hp("ingest_ops_device (all)");
   std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
   (void)hipSetDevice(c->ctx->device);
   return ingest_ops_dev(c, d_blob, d_offs, n, blob_len, actors, m, d_file_actor, d_file_version,
@@ -1126,6 +1127,7 @@ int ce_core_ingest_ops_device(ce_core* c, const uint8_t* d_blob, const uint64_t*
 int ce_core_ingest_states(ce_core* c, const uint8_t* blob, const uint64_t* offs, uint32_t n,
                           int32_t* status) {
   if (!c || (n && (!blob || !offs))) return CE_ERR_INVALID_ARG;
+  HostPhase hp("ingest_states (all)");
   std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
   (void)hipSetDevice(c->ctx->device);
   return ingest_states_host(c, blob, offs, n, status);
@@ -1142,7 +1144,7 @@ int ce_core_compact_to_buffer(ce_core* c, const uint8_t* nonce, ce_buf* file, ch
   if (!c || !file) return CE_ERR_INVALID_ARG;
   std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
   (void)hipSetDevice(c->ctx->device);
-  std::vector<uint8_t> f;
+  std::vector<uint8_t>& f = c->file_buf;
   int rc = compact_bytes(c, nonce, &f);
   if (rc) return rc;
   if (name_out) {
@@ -1154,6 +1156,27 @@ int ce_core_compact_to_buffer(ce_core* c, const uint8_t* nonce, ce_buf* file, ch
   file->data = (uint8_t*)malloc(f.size() ? f.size() : 1);
   std::memcpy(file->data, f.data(), f.size());
   file->len = f.size();
+  return CE_OK;
+}
+
+int ce_core_compact_into(ce_core* c, const uint8_t* nonce, uint8_t* dst, size_t cap, size_t* len,
+                         char name_out[64]) {
+  if (!c || !len || (cap && !dst)) return CE_ERR_INVALID_ARG;
+  HostPhase hw("compact_into");
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  (void)hipSetDevice(c->ctx->device);
+  std::vector<uint8_t>& f = c->file_buf;
+  int rc = compact_bytes(c, nonce, &f);
+  if (rc) return rc;
+  *len = f.size();
+  if (cap < f.size()) return c->ctx->fail(CE_ERR_INVALID_ARG, "compact_into: buffer too small");
+  std::memcpy(dst, f.data(), f.size());
+  if (name_out) {
+    HostPhase hp("sha3 name");
+    uint8_t h[32];
+    sha3_256(dst, f.size(), h);
+    std::snprintf(name_out, 64, "%s", base32_nopad(h, 32).c_str());
+  }
   return CE_OK;
 }
 

@@ -57,6 +57,7 @@ struct ce_core {
   std::unordered_map<ce::Uuid, uint32_t, ce::UuidHash> slot_of;
   bool table_dirty = true;
   uint64_t table_gen = 0;               // bumped whenever an actor gets a slot or slots move
+  std::vector<uint8_t> ser_buf, file_buf;  // compaction: serialized state, sealed file (reused)
   std::vector<uint32_t> sorted_slots;   // used slots in UUID byte order (BTreeMap order)
   uint64_t sorted_gen = ~0ull;
   std::vector<uint8_t> last_writers;    // writer list of the previous ingest and its slots

@@ -184,8 +184,11 @@ int device_seal(ce_ctx* ctx, const uint8_t* d_clear, const uint64_t* d_offs, uin
 }
 
 int seal_one(ce_ctx* ctx, const KeyRef& key, const uint8_t* outer_version, const uint8_t* nonce,
-             const uint8_t* clear, size_t clear_len, std::vector<uint8_t>* file) {
+             const uint8_t* clear_in, size_t clear_in_len, std::vector<uint8_t>* file,
+             const uint8_t* prefix16) {
   if (int32_t ks = key_status(key)) return ctx->fail(ks, "key rejected");
+  const size_t pl = prefix16 ? 16 : 0;
+  const size_t clear_len = pl + clear_in_len;
   const uint64_t pre = outer_version ? 16 : 0;
   const uint64_t total = pre + sealed_len(clear_len);
   uint8_t nb[24];
@@ -201,7 +204,8 @@ int seal_one(ce_ctx* ctx, const KeyRef& key, const uint8_t* outer_version, const
     return ctx->hip_fail(e, "seal_one reserve");
   uint8_t* hs = ctx->h_stage.as<uint8_t>();
   const uint64_t args[3] = {0, clear_len, 0};
-  std::memcpy(hs, clear, clear_len);
+  if (pl) std::memcpy(hs, prefix16, 16);
+  std::memcpy(hs + pl, clear_in, clear_in_len);
   std::memcpy(hs + A, args, 24);
   std::memcpy(hs + A + 24, nb, 24);
   if (outer_version) std::memcpy(hs + A + 48, outer_version, 16);
@@ -215,7 +219,8 @@ int seal_one(ce_ctx* ctx, const KeyRef& key, const uint8_t* outer_version, const
   if ((e = hipMemcpyAsync(hs, ctx->out.p, total, hipMemcpyDeviceToHost, ctx->stream)) ||
       (e = hipStreamSynchronize(ctx->stream)))
     return ctx->hip_fail(e, "seal_one download");
-  file->assign(hs, hs + total);
+  file->resize(total);
+  std::memcpy(file->data(), hs, total);
   return CE_OK;
 }
 
@@ -277,6 +282,13 @@ int ce_ctx_create(int device, ce_ctx** out) {
     return CE_ERR_DEVICE;
   }
   c->own_stream = true;
+  // the counter block is addressed by every batch path (gate flags live in it): allocate it
+  // with the context, not on first use
+  if (c->counters.reserve(256) != hipSuccess || c->h_counters.reserve(256) != hipSuccess ||
+      hipMemset(c->counters.p, 0, 256) != hipSuccess) {
+    ce_ctx_destroy(c);
+    return CE_ERR_DEVICE;
+  }
   *out = c;
   return CE_OK;
 }

@@ -36,6 +36,7 @@ struct DsState {
   std::map<IdDots, std::set<uint64_t>> deferred;  // removal clock -> members (HashMap in crdts)
   // MVReg
   std::vector<std::pair<IdDots, uint64_t>> vals;
+  std::vector<std::vector<uint8_t>> ser_parts;  // per-thread entry writer output (reused)
   // scratch
   DevBuf cnt, ops[10], applied, sort_keys, sort_perm, sort_keys2, sort_perm2, ctr_sorted, excl,
       cub_tmp, deferred_flags, d0[5], col[6], mv[6], other[4], oclock;
@@ -1224,6 +1225,8 @@ int ds_serialize(ce_core* c, std::vector<uint8_t>* out) {
     if (c->h_table[sl].used && c->nov[sl]) nov.push_back({c->slot_actor[sl], c->nov[sl]});
   sort_dots(&nov);
   Wr w;
+  w.b.swap(*out);  // reuse the caller's capacity
+  w.b.clear();
   w.map(2);
   w.str("next_op_versions");
   put_vclock(w, nov);
@@ -1237,7 +1240,7 @@ int ds_serialize(ce_core* c, std::vector<uint8_t>* out) {
       put_vclock(w, uuid_dots(v.first));
       w.uint(v.second);
     }
-    *out = std::move(w.b);
+    out->swap(w.b);
     return CE_OK;
   }
   // clock
@@ -1343,7 +1346,8 @@ int ds_serialize(ce_core* c, std::vector<uint8_t>* out) {
     while (x < nl && x > 0 && mem[x] == mem[x - 1]) x++;
     cut[t] = x;
   }
-  std::vector<std::vector<uint8_t>> parts(T);
+  std::vector<std::vector<uint8_t>>& parts = d->ser_parts;  // reused across compactions
+  if (parts.size() < T) parts.resize(T);
   if (T == 1) {
     write_members(0, nl, &parts[0]);
   } else {
@@ -1351,7 +1355,7 @@ int ds_serialize(ce_core* c, std::vector<uint8_t>* out) {
     for (uint32_t t = 0; t < T; t++) th.emplace_back(write_members, cut[t], cut[t + 1], &parts[t]);
     for (auto& x : th) x.join();
   }
-  for (auto& p : parts) w.b.insert(w.b.end(), p.begin(), p.end());
+  for (uint32_t t = 0; t < T; t++) w.b.insert(w.b.end(), parts[t].begin(), parts[t].end());
   w.str("deferred");
   std::vector<std::pair<std::vector<uint8_t>, const std::set<uint64_t>*>> df;
   for (auto& x : d->deferred) {
@@ -1366,7 +1370,7 @@ int ds_serialize(ce_core* c, std::vector<uint8_t>* out) {
     w.arr(x.second->size());
     for (uint64_t m : *x.second) w.uint(m);
   }
-  *out = std::move(w.b);
+  out->swap(w.b);
   return CE_OK;
 }
 

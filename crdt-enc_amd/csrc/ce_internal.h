@@ -141,9 +141,12 @@ int device_seal(ce_ctx* ctx, const uint8_t* d_clear, const uint64_t* d_offs, uin
                 uint64_t clear_len_total, const uint8_t* d_outer_version, const uint8_t* d_nonces,
                 uint8_t* d_out, const uint64_t* d_out_offs, const KeyRef& key);
 
-// Seal one host clear text into a host file: [outer(16)] || Cryptor::encrypt(clear).
+// Seal one host clear text into a host file: [outer(16)] || Cryptor::encrypt([prefix16] ||
+// clear).  `file` keeps its capacity across calls (the pinned staging buffer is the only copy
+// of the clear text the seal makes).
 int seal_one(ce_ctx* ctx, const KeyRef& key, const uint8_t* outer_version, const uint8_t* nonce,
-             const uint8_t* clear, size_t clear_len, std::vector<uint8_t>* file);
+             const uint8_t* clear, size_t clear_len, std::vector<uint8_t>* file,
+             const uint8_t* prefix16 = nullptr);
 
 uint32_t grid_waves_for(uint32_t work);
 

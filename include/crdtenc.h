@@ -244,6 +244,11 @@ int ce_core_ingest_states(ce_core *c, const uint8_t *blob, const uint64_t *offs,
 /* compact() without storage: serialize the state, seal it on the GPU with the latest key and
  * return the state file bytes and its content name.  nonce: 24 bytes or NULL (OS RNG). */
 int ce_core_compact_to_buffer(ce_core *c, const uint8_t *nonce, ce_buf *file, char name_out[64]);
+/* The same into a caller-owned buffer (no per-call allocation): *len = the file size.  When
+ * cap < *len nothing is written and CE_ERR_INVALID_ARG is returned with *len set, so the caller
+ * can grow its buffer and call again (the state is unchanged; the nonce is drawn again). */
+int ce_core_compact_into(ce_core *c, const uint8_t *nonce, uint8_t *dst, size_t cap, size_t *len,
+                         char name_out[64]);
 
 /* What read_remote_states does with one decrypted state (lib.rs:447, 458-466):
  * rmp_serde::from_slice::<StateWrapper<S>>(sw) then state.merge + next_op_versions.merge.

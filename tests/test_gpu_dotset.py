@@ -8,6 +8,7 @@ itself is unpinned: the oracle restates its published source.
 import random
 
 import msgpack
+import numpy as np
 import pytest
 
 import crdtenc
@@ -254,6 +255,8 @@ def test_compact_roundtrip(ctx):
     core.set_latest_key(key)
     assert core.ingest_ops(seal_files(ctx, key, clears), acts, fa, fv)[0] == 0
     f, name = core.compact_to_buffer(nonce=bytes(24))
+    buf, n, name2 = core.compact_into(np.zeros(1, np.uint8), nonce=bytes(24))
+    assert bytes(buf[:n]) == f and name2 == name
     other = new_core(ctx, "orswot", key)
     assert other.ingest_states([f])[0] == 0
     assert other.state_bytes() == core.state_bytes()

@@ -8,6 +8,7 @@ import random
 import struct
 
 import msgpack
+import numpy as np
 import pytest
 
 import crdtenc
@@ -178,10 +179,17 @@ def test_compact_to_buffer_matches_fixture(ctx, repo_fx):
     for kind, k in (("gcounter", crdtenc.STATE_GCOUNTER), ("vclock", crdtenc.STATE_VCLOCK)):
         core = new_core(ctx, repo_fx, k)
         files, actors, fa, vers = files_of(repo_fx)
-        assert core.ingest_ops(files, actors, fa, vers)[0] == 0
+        rc = core.ingest_ops(files, actors, fa, vers)[0]
+        assert rc == 0, (kind, rc, ctx.last_error())
         c = repo_fx["compact"][kind]
         f, name = core.compact_to_buffer(nonce=H(c["nonce"]))
         assert f.hex() == c["file"] and name == c["name"]
+        # caller-owned buffer: grown from 16 bytes, then reused; the name is over its bytes
+        buf = np.zeros(16, np.uint8)
+        for _ in range(2):
+            buf, n, name2 = core.compact_into(buf, nonce=H(c["nonce"]))
+            assert bytes(buf[:n]) == f and name2 == name and buf.nbytes >= n
+        assert crdtenc.content_name(buf[:n]) == name == crdtenc.content_name(f)
 
 
 # ------------------------------------------------------------------ larger random batches
