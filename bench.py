@@ -117,7 +117,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--versions", type=int, default=256, help="versions per actor per GPU")
-    ap.add_argument("--cpu-sample", type=int, default=32768, help="files in the CPU baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=0,
+                    help="files in the CPU baseline sample (0 = the whole per-GPU workload, "
+                         "~5-10 s of CPU work at 16 threads)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -227,7 +229,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         sys.path.insert(0, REPO)
         import oracle
-        s = min(args.cpu_sample, n)
+        s = min(args.cpu_sample, n) if args.cpu_sample > 0 else n
         s -= s % versions
         file_len = blob_len // n
         host = files[: s * file_len].cpu().numpy()
