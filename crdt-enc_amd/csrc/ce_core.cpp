@@ -368,20 +368,24 @@ int merge_dots_host(ce_core* c, const Dots& dots) {
   return CE_OK;
 }
 
+// used slots in UUID byte order (BTreeMap iteration order), cached per table generation
+void ensure_sorted(ce_core* c) {
+  if (c->sorted_gen == c->table_gen) return;
+  c->sorted_slots.clear();
+  for (uint32_t s = 0; s < c->cap; s++)
+    if (c->h_table[s].used) c->sorted_slots.push_back(s);
+  std::sort(c->sorted_slots.begin(), c->sorted_slots.end(), [&](uint32_t a, uint32_t b) {
+    return std::memcmp(c->slot_actor[a].data(), c->slot_actor[b].data(), 16) < 0;
+  });
+  c->sorted_gen = c->table_gen;
+}
+
 int serialize_state(ce_core* c, std::vector<uint8_t>* out) {
   if (is_dotset_kind(c->kind)) return ds_serialize(c, out);
   std::vector<uint64_t> st;
   int rc = download_state(c, &st);
   if (rc) return rc;
-  if (c->sorted_gen != c->table_gen) {
-    c->sorted_slots.clear();
-    for (uint32_t s = 0; s < c->cap; s++)
-      if (c->h_table[s].used) c->sorted_slots.push_back(s);
-    std::sort(c->sorted_slots.begin(), c->sorted_slots.end(), [&](uint32_t a, uint32_t b) {
-      return std::memcmp(c->slot_actor[a].data(), c->slot_actor[b].data(), 16) < 0;
-    });
-    c->sorted_gen = c->table_gen;
-  }
+  ensure_sorted(c);
   const std::vector<uint32_t>& slots = c->sorted_slots;
   size_t n_nov = 0, n_st = 0;
   for (uint32_t s : slots) { n_nov += c->nov[s] != 0; n_st += st[s] != 0; }
@@ -492,12 +496,15 @@ int resolve_host_parse(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs
 }
 
 int ensure_supported(ce_core* c) {
+  if (c->supported_on_device) return CE_OK;  // fixed at open (lib.rs:227-228): upload once
   const size_t bytes = c->supported.size() * 16;
   hipError_t e;
   if ((e = c->d_supported.reserve(bytes + 16))) return c->ctx->hip_fail(e, "supported");
   if (bytes && (e = hipMemcpyAsync(c->d_supported.p, c->supported.data(), bytes,
                                    hipMemcpyHostToDevice, c->ctx->stream)))
     return c->ctx->hip_fail(e, "supported");
+  if ((e = hipStreamSynchronize(c->ctx->stream))) return c->ctx->hip_fail(e, "supported");
+  c->supported_on_device = true;
   return CE_OK;
 }
 
@@ -580,6 +587,16 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
     int rr = device_open_setup(ctx, d_blob, d_offs, n, blob_len, true, key, ctx->status.as<int32_t>(), &ec);
     if (rr) return rr;
   }
+  // the setup's counters (large-file count [9]) -> host behind an event: read while the fused
+  // kernel runs, they decide whether the multi-page kernels are launched at all
+  uint32_t* hsetup = ctx->h_counters.as<uint32_t>() + 32;
+  if (!ctx->setup_ev && (e = hipEventCreateWithFlags(&ctx->setup_ev, hipEventDisableTiming)))
+    return ctx->hip_fail(e, "event");
+  if ((e = hipMemcpyAsync(hsetup, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->stream)) ||
+      (e = hipEventRecord(ctx->setup_ev, ctx->stream)))
+    return ctx->hip_fail(e, "setup counters");
+  bool setup_known = false;
+  uint32_t n_large = 0;
   if ((e = hipMemcpyAsync(gbase, he0, m * 8ull, hipMemcpyHostToDevice, ctx->stream)) ||
       (e = hipMemsetAsync(gbase + 8ull * m, 0, 16ull * m, ctx->stream)) ||
       (e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ga.flags + 1), 0xffffffffu, 1, ctx->stream)))
@@ -634,6 +651,12 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
       if (e) return ctx->hip_fail(e, "fused");
       ctx->tend(t);
     }
+    if (!setup_known) {  // landed long ago: the gate and the fused kernel follow it
+      if ((e = hipEventSynchronize(ctx->setup_ev))) return ctx->hip_fail(e, "setup counters");
+      n_large = hsetup[9];
+      setup_known = true;
+    }
+    if (n_large == 0) return CE_OK;  // every file was single-page: nothing for the kernels below
     if (!only) {
       SegScratch sc = segscratch(ctx, ec);
       int t = ctx->tbegin("segments_open");
@@ -652,6 +675,19 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
     return CE_OK;
   };
   if ((rc = run_fold(nullptr))) return rc;
+  // commit on the device unless the counters flag a slow path (k_merge_max_if), then one read
+  // of the counters and of the gate's next_op_versions
+  {
+    const int t = ctx->tbegin("merge");
+    if ((e = launch_merge_max_if(ctx->stream, c->d_state.as<unsigned long long>(),
+                                 c->d_batch.as<unsigned long long>(), c->cap,
+                                 ctx->counters.as<uint32_t>())))
+      return ctx->hip_fail(e, "merge");
+    ctx->tend(t);
+  }
+  uint64_t* hnov = he0 + m;
+  if ((e = hipMemcpyAsync(hnov, gbase + 8ull * m, m * 8ull, hipMemcpyDeviceToHost, ctx->stream)))
+    return ctx->hip_fail(e, "nov");
   if (prof) {
     std::vector<unsigned long long> hp(8ull * 65536);
     if ((e = hipMemcpyAsync(hp.data(), prof_buf.p, hp.size() * 8, hipMemcpyDeviceToHost, ctx->stream)) ||
@@ -673,6 +709,7 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
   if ((e = hipMemcpyAsync(hc, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->stream)) ||
       (e = hipStreamSynchronize(ctx->stream)))
     return ctx->hip_fail(e, "fold sync");
+  const bool merged_on_device = (hc[2] | hc[3] | hc[4] | hc[7] | hc[8] | hc[12]) == 0;
 
   // 3) batches outside the device gate's shape: host gate, fold again with its flags
   std::vector<uint64_t> expect(he0, he0 + m);
@@ -781,21 +818,23 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
   if (first != CE_OK) return first;  // all-or-nothing: batch state discarded (lib.rs:497-514)
 
   // 5) commit: state = max(state, batch); next_op_versions from the gate
-  {
+  if (merged_on_device) {
+    for (uint32_t a = 0; a < m; a++) expect[a] = std::max(expect[a], hnov[a]);
+  } else {
     const int t = ctx->tbegin("merge");
     if ((e = launch_merge_max(ctx->stream, c->d_state.as<unsigned long long>(),
                               c->d_batch.as<unsigned long long>(), c->cap)))
       return ctx->hip_fail(e, "merge");
     ctx->tend(t);
-  }
-  if (!host_gated) {
-    std::vector<uint64_t> nn(m);
-    if ((e = hipMemcpyAsync(nn.data(), gbase + 8ull * m, m * 8ull, hipMemcpyDeviceToHost, ctx->stream)) ||
-        (e = hipStreamSynchronize(ctx->stream)))
-      return ctx->hip_fail(e, "nov");
-    for (uint32_t a = 0; a < m; a++) expect[a] = std::max(expect[a], nn[a]);
-  } else if ((e = hipStreamSynchronize(ctx->stream))) {
-    return ctx->hip_fail(e, "merge");
+    if (!host_gated) {
+      std::vector<uint64_t> nn(m);
+      if ((e = hipMemcpyAsync(nn.data(), gbase + 8ull * m, m * 8ull, hipMemcpyDeviceToHost, ctx->stream)) ||
+          (e = hipStreamSynchronize(ctx->stream)))
+        return ctx->hip_fail(e, "nov");
+      for (uint32_t a = 0; a < m; a++) expect[a] = std::max(expect[a], nn[a]);
+    } else if ((e = hipStreamSynchronize(ctx->stream))) {
+      return ctx->hip_fail(e, "merge");
+    }
   }
   for (uint32_t a = 0; a < m; a++) c->nov[wslot[a]] = std::max(c->nov[wslot[a]], expect[a]);
   if (first_gap < n) {
@@ -964,10 +1003,79 @@ int read_remote(ce_core* c) {
                              ab.data(), (uint32_t)actors.size(), aidx.data(), vers.data(), nullptr);
 }
 
+// compaction of a VClock / GCounter state without leaving the device: the StateWrapper is
+// serialized from the dense arrays (k_serialize_vclock) into the seal's input, sealed, and only
+// the sealed file comes back (one synchronisation).  Same bytes as serialize_state + seal_one.
+int compact_device(ce_core* c, const uint8_t* nonce, std::vector<uint8_t>* file) {
+  ce_ctx* ctx = c->ctx;
+  const KeyRef key = key_of(c);
+  if (int32_t ks = key_status(key)) return ctx->fail(ks, "key rejected");
+  const bool ingest_fmt = (c->flags & CE_COMPACT_INGEST_FORMAT) != 0;
+  // readable by read_remote_states: CURRENT_VERSION || encrypt(data_version || state); else
+  // exactly what Core::compact writes: VersionBytes(current_data_version, encrypt(state))
+  const uint8_t* outer = ingest_fmt ? kCoreVersion : c->current_data_version.data();
+  ensure_sorted(c);
+  const uint32_t k = (uint32_t)c->sorted_slots.size();
+  int rc = table_upload(c);  // the serializer reads the UUIDs from the device table
+  if (rc) return rc;
+  hipError_t e;
+  if (c->d_sorted_gen != c->sorted_gen) {
+    if ((e = c->d_sorted.reserve(4ull * k + 64)) ||
+        (k && (e = hipMemcpyAsync(c->d_sorted.p, c->sorted_slots.data(), 4ull * k, hipMemcpyHostToDevice,
+                                  ctx->stream))) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+      return ctx->hip_fail(e, "sorted slots");
+    c->d_sorted_gen = c->sorted_gen;
+  }
+  const uint64_t U = vclock_ser_bound(k);             // clear length bound (prefix included)
+  const uint64_t A = (U + 255) & ~255ull;              // small arguments after the clear text
+  const uint64_t total_max = 16 + sealed_len(U);
+  const uint64_t nov_bytes = 8ull * c->cap;
+  if ((e = ctx->blob.reserve(A + 128)) || (e = ctx->out.reserve(total_max + 64)) ||
+      (e = ctx->h_stage.reserve(std::max<uint64_t>(total_max + 64, 128 + nov_bytes))) ||
+      (e = c->d_tmp.reserve(nov_bytes)))
+    return ctx->hip_fail(e, "compact reserve");
+  // staging: [offs(2) | out_offs(1) | nonce(24) | outer(16) | prefix16(16)] at 0, nov at 128
+  uint8_t* hs = ctx->h_stage.as<uint8_t>();
+  const uint64_t args[3] = {0, 0, 0};
+  std::memcpy(hs, args, 24);
+  if (nonce) std::memcpy(hs + 24, nonce, 24);
+  else os_random(hs + 24, 24);
+  std::memcpy(hs + 48, outer, 16);
+  std::memcpy(hs + 64, c->current_data_version.data(), 16);
+  std::memcpy(hs + 128, c->nov.data(), nov_bytes);
+  uint8_t* db = ctx->blob.as<uint8_t>();
+  if ((e = hipMemcpyAsync(db + A, hs, 80, hipMemcpyHostToDevice, ctx->stream)) ||
+      (e = hipMemcpyAsync(c->d_tmp.p, hs + 128, nov_bytes, hipMemcpyHostToDevice, ctx->stream)))
+    return ctx->hip_fail(e, "compact upload");
+  auto* d_offs = reinterpret_cast<unsigned long long*>(db + A);
+  if ((e = launch_serialize_vclock(ctx->stream, c->d_tmp.as<unsigned long long>(),
+                                   c->d_state.as<unsigned long long>(), c->d_sorted.as<uint32_t>(), k,
+                                   c->d_table.as<ActorSlot>(), c->kind == CE_STATE_GCOUNTER,
+                                   ingest_fmt ? db + A + 64 : nullptr, db, d_offs)))
+    return ctx->hip_fail(e, "serialize");
+  rc = device_seal(ctx, db, reinterpret_cast<const uint64_t*>(d_offs), 1, U, db + A + 48, db + A + 24,
+                       ctx->out.as<uint8_t>(), reinterpret_cast<const uint64_t*>(db + A + 16), key);
+  if (rc) return rc;
+  // the sealed file (its bound) and the clear length, one synchronisation
+  if ((e = hipMemcpyAsync(hs, ctx->out.p, total_max, hipMemcpyDeviceToHost, ctx->stream)) ||
+      (e = hipMemcpyAsync(hs + total_max, db + A + 8, 8, hipMemcpyDeviceToHost, ctx->stream)) ||
+      (e = hipStreamSynchronize(ctx->stream)))
+    return ctx->hip_fail(e, "compact download");
+  uint64_t clear_len;
+  std::memcpy(&clear_len, hs + total_max, 8);
+  if (clear_len > U) return ctx->fail(CE_ERR_DEVICE, "serializer overran its bound");
+  const uint64_t total = 16 + sealed_len(clear_len);
+  file->resize(total);
+  std::memcpy(file->data(), hs, total);
+  return CE_OK;
+}
+
 // clear text + file of a compaction (lib.rs:335-360)
 int compact_bytes(ce_core* c, const uint8_t* nonce, std::vector<uint8_t>* file) {
   HostPhase hp("compact_bytes");
   if (!c->has_key) return c->ctx->fail(CE_ERR_NO_KEY, "no latest key");
+  if (!is_dotset_kind(c->kind) && !c->host_compact) return compact_device(c, nonce, file);
   std::vector<uint8_t>& clear = c->ser_buf;
   int rc = serialize_state(c, &clear);
   if (rc) return rc;
@@ -1003,6 +1111,7 @@ int ce_core_open(ce_ctx* ctx, const ce_open_options* o, ce_core** out) {
     const int v = atoi(fu);
     if (v == 1 || v == 2) c->fused = v;
   }
+  if (const char* hc = getenv("CE_HOST_COMPACT")) c->host_compact = atoi(hc) != 0;
   c->flags = o->flags;
   std::memcpy(c->current_data_version.data(), o->current_data_version, 16);
   for (size_t i = 0; i < o->n_supported; i++) {

@@ -64,7 +64,11 @@ struct ce_core {
   std::vector<uint32_t> last_wslot;
   uint64_t last_writers_gen = ~0ull;
   ce::DevBuf d_table, d_state, d_batch, d_supported, d_refold2, d_tmp, d_gate, d_meta;
+  ce::DevBuf d_sorted;                  // sorted_slots on the device (compaction serializer)
+  uint64_t d_sorted_gen = ~0ull;
   int files_per_wave = 4;  // fused kernel geometry (CE_FILES_PER_WAVE overrides)
+  bool supported_on_device = false;
+  bool host_compact = false;  // CE_HOST_COMPACT=1: serialize on the host (reference check)
   int fused = 2;           // fused kernel: 1 keystream staged in LDS, 2 block-owning lanes (CE_FUSED)
   std::set<std::string> read_states;  // lib.rs:205
   ce_ctx* aux = nullptr;              // single-file work during a batch (exotic envelopes)

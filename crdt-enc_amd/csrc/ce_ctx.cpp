@@ -299,6 +299,7 @@ void ce_ctx_destroy(ce_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& t : c->timed) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
+  if (c->setup_ev) (void)hipEventDestroy(c->setup_ev);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }

@@ -80,6 +80,8 @@ struct ce_ctx {
   ce::DevBuf params, status, counters, extra, multi, partials, large, out, apply, refold, miss,
       supported, blob, offs, nonces, out_offs, outer_ver, batch_counters;
   ce::HostBuf h_counters, h_apply, h_stage, h_stage2;
+  // marks the setup kernel's counter snapshot (h_counters + 128) as landed on the host
+  hipEvent_t setup_ev = nullptr;
   // kernel timing (ce_ctx_set_timing)
   bool timing = false;
   struct TimedLaunch {

@@ -118,5 +118,15 @@ hipError_t launch_gate(hipStream_t s, const GateArgs& g);
 // dst[i] = max(dst[i], src[i])
 hipError_t launch_merge_max(hipStream_t s, unsigned long long* dst,
                             const unsigned long long* src, uint32_t n);
+// launch_merge_max unless the counter block flags a batch that cannot commit as folded
+hipError_t launch_merge_max_if(hipStream_t s, unsigned long long* dst, const unsigned long long* src,
+                               uint32_t n, const uint32_t* counters);
+// to_vec_named(StateWrapper<VClock|GCounter>) from the dense nov / state arrays (k sorted slots);
+// clear length -> offs[1] (offs[0] = 0).  Upper bound of the output: vclock_ser_bound(k)
+hipError_t launch_serialize_vclock(hipStream_t s, const unsigned long long* nov,
+                                  const unsigned long long* st, const uint32_t* sorted, uint32_t k,
+                                  const ActorSlot* table, bool gcounter, const uint8_t* prefix16,
+                                  uint8_t* out, unsigned long long* offs);
+inline uint64_t vclock_ser_bound(uint64_t k) { return 16 + 24 + 5 + 27 * k + 19 + 5 + 27 * k; }
 
 }  // namespace ce

@@ -507,6 +507,200 @@ __global__ void k_merge_max(unsigned long long* __restrict__ dst,
   }
 }
 
+// the same merge, skipped on the device when the batch cannot commit as folded: any auth /
+// decode / setup failure ([2] [3] [8]), unregistered actors ([4]), host-parse envelopes ([7]) or
+// a batch the device gate could not take ([12]).  The host reads the same counters afterwards and
+// takes its slow path exactly when this kernel skipped (no round trip between fold and commit).
+__global__ void k_merge_max_if(unsigned long long* __restrict__ dst,
+                               const unsigned long long* __restrict__ src, uint32_t n,
+                               const uint32_t* __restrict__ counters) {
+  if (counters[2] | counters[3] | counters[4] | counters[7] | counters[8] | counters[12]) return;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const unsigned long long s = src[i];
+    if (s > dst[i]) dst[i] = s;
+  }
+}
+
+
+// ----------------------------------------------------------------------------------------
+// k_serialize_vclock: to_vec_named(StateWrapper) for S = VClock<Uuid> / GCounter<Uuid>
+// (crdt-enc/src/lib.rs:336,739-743) straight from the dense device arrays, so a compaction
+// needs no state download and no host serializer.  Byte-identical to serialize_state (ce_core.cpp):
+//   [prefix16] 82 b0 "next_op_versions" 81 a4 "dots" <map n_nov> {c4 10 <uuid> <uint>}..
+//              a5 "state" [81 a5 "inner"] 81 a4 "dots" <map n_st> {..}
+// entries in UUID byte order (BTreeMap), zero counters absent.  Workgroup r (1024 lanes) writes
+// sorted entries r*1024 + lane (adjacent lanes write adjacent entries), placed by a block scan of
+// their lengths; the bytes of the entries before its round it sums itself from all entries (a
+// few KB of loads, no inter-workgroup step).  Workgroup 0 writes the headers and the clear length
+// to offs[1] (offs[0] = 0) for the seal that follows on the same stream.
+// ----------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t mp_uint_len(unsigned long long v) {
+  return v <= 0x7full ? 1u : v <= 0xffull ? 2u : v <= 0xffffull ? 3u : v <= 0xffffffffull ? 5u : 9u;
+}
+__device__ __forceinline__ uint32_t mp_map_hdr_len(uint32_t n) { return n <= 15 ? 1u : n <= 0xffff ? 3u : 5u; }
+__device__ __forceinline__ uint32_t mp_put_map_hdr(uint8_t* o, uint32_t n) {
+  if (n <= 15) { o[0] = (uint8_t)(0x80 | n); return 1; }
+  if (n <= 0xffff) { o[0] = 0xde; o[1] = (uint8_t)(n >> 8); o[2] = (uint8_t)n; return 3; }
+  o[0] = 0xdf; o[1] = (uint8_t)(n >> 24); o[2] = (uint8_t)(n >> 16); o[3] = (uint8_t)(n >> 8); o[4] = (uint8_t)n;
+  return 5;
+}
+__device__ __forceinline__ uint32_t mp_put_str(uint8_t* o, const char* s, uint32_t l) {
+  o[0] = (uint8_t)(0xa0 | l);
+  for (uint32_t i = 0; i < l; i++) o[1 + i] = (uint8_t)s[i];
+  return l + 1;
+}
+// exclusive block scan over the 1024 lanes (16 waves); *total = the sum
+__device__ __forceinline__ uint32_t block_scan_1024(uint32_t v, uint32_t* ws, uint32_t* total) {
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, d);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  if (lane == 63) ws[w] = x;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 16; i++) {
+    const uint32_t s = ws[i];
+    pre += i < w ? s : 0u;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + x - v;
+}
+
+template <int R>
+__global__ __launch_bounds__(1024) void k_serialize_vclock(
+    const unsigned long long* __restrict__ nov, const unsigned long long* __restrict__ st,
+    const uint32_t* __restrict__ sorted, uint32_t k, const ActorSlot* __restrict__ table,
+    int gcounter, const uint8_t* __restrict__ prefix16, uint8_t* __restrict__ out,
+    unsigned long long* __restrict__ offs) {
+  __shared__ uint32_t ws[16];
+  const uint32_t t = threadIdx.x;
+  // R rounds per chunk held in registers: every load of a chunk is issued before any is used
+  // (one latency per chunk, not three dependent ones per round).  k <= 1024 R: one chunk, the
+  // registers also serve the write pass.
+  const uint32_t rounds = (k + 1023) / 1024;
+  uint32_t sl[R];
+  unsigned long long nv[R], sv[R];
+  auto load_chunk = [&](uint32_t r0) {
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const uint32_t i = (r0 + r) * 1024 + t;
+      sl[r] = i < k ? sorted[i] : 0xffffffffu;
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      nv[r] = sl[r] != 0xffffffffu ? nov[sl[r]] : 0ull;
+      sv[r] = sl[r] != 0xffffffffu ? st[sl[r]] : 0ull;
+    }
+  };
+  // pass 1 (every workgroup, over all entries): entry counts and bytes of both maps, and the
+  // bytes of the entries before this workgroup's round (counts packed in 16-bit halves when
+  // they fit: <= 1024 R each)
+  const uint32_t me = blockIdx.x;  // the round this workgroup writes
+  uint32_t cnt = 0, bn = 0, bs = 0, pn = 0, ps = 0;
+  for (uint32_t r0 = 0; r0 < rounds; r0 += R) {
+    load_chunk(r0);
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      cnt += (nv[r] != 0 ? 1u : 0u) + (sv[r] != 0 ? 0x10000u : 0u);
+      const uint32_t ln = nv[r] != 0 ? 18u + mp_uint_len(nv[r]) : 0u;
+      const uint32_t ls = sv[r] != 0 ? 18u + mp_uint_len(sv[r]) : 0u;
+      bn += ln;
+      bs += ls;
+      if (r0 + r < me) { pn += ln; ps += ls; }
+    }
+  }
+  uint32_t tc, tbn, tbs, tpn, tps;
+  (void)block_scan_1024(cnt, ws, &tc);
+  (void)block_scan_1024(bn, ws, &tbn);
+  (void)block_scan_1024(bs, ws, &tbs);
+  (void)block_scan_1024(pn, ws, &tpn);
+  (void)block_scan_1024(ps, ws, &tps);
+  uint32_t cn = tc & 0xffff, cs = tc >> 16;
+  if (rounds > R) {  // counts can pass 16 bits: recount exactly
+    uint32_t a = 0, b = 0;
+    for (uint32_t r0 = 0; r0 < rounds; r0 += R) {
+      load_chunk(r0);
+#pragma unroll
+      for (int r = 0; r < R; r++) { a += nv[r] != 0; b += sv[r] != 0; }
+    }
+    (void)block_scan_1024(a, ws, &cn);
+    (void)block_scan_1024(b, ws, &cs);
+  }
+  const uint32_t pl = prefix16 ? 16u : 0u;
+  const uint32_t nov_at = pl + 24 + mp_map_hdr_len(cn);                 // first nov entry
+  const uint32_t st_hdr = nov_at + tbn;                                  // "state" ...
+  const uint32_t st_at = st_hdr + 6 + (gcounter ? 7u : 0u) + 6 + mp_map_hdr_len(cs);
+  if (me == 0 && t == 0) {
+    uint8_t* o = out;
+    for (uint32_t i = 0; i < pl; i++) *o++ = prefix16[i];
+    *o++ = 0x82;
+    o += mp_put_str(o, "next_op_versions", 16);
+    *o++ = 0x81;
+    o += mp_put_str(o, "dots", 4);
+    o += mp_put_map_hdr(o, cn);
+    o = out + st_hdr;
+    o += mp_put_str(o, "state", 5);
+    if (gcounter) {
+      *o++ = 0x81;
+      o += mp_put_str(o, "inner", 5);
+    }
+    *o++ = 0x81;
+    o += mp_put_str(o, "dots", 4);
+    o += mp_put_map_hdr(o, cs);
+    offs[0] = 0;
+    offs[1] = st_at + tbs;
+  }
+  // one entry c4 10 <uuid16> <uint>: 19..27 bytes assembled as 7 little-endian dwords, stored
+  // as unaligned dwords + the 1..3 trailing bytes (a third of the byte stores; adjacent entries
+  // never share a dword store)
+  auto put = [&](uint32_t at, const ActorSlot& a, unsigned long long v) {
+    const uint32_t ul = mp_uint_len(v);
+    const uint32_t nb = ul - 1;  // big-endian payload bytes after the marker
+    const unsigned long long be = nb ? __builtin_bswap64(v) >> (8 * (8 - nb)) : 0ull;
+    const uint32_t mk = ul == 2 ? 0xccu : ul == 3 ? 0xcdu : ul == 5 ? 0xceu : 0xcfu;
+    const unsigned long long lo = ul == 1 ? v : (mk | (be << 8));
+    const uint32_t hi = ul == 9 ? (uint32_t)(be >> 56) : 0u;
+    const uint32_t t0 = (uint32_t)lo, t1 = (uint32_t)(lo >> 32);
+    uint32_t w[7];
+    w[0] = 0x10c4u | (a.k[0] << 16);
+    w[1] = (a.k[0] >> 16) | (a.k[1] << 16);
+    w[2] = (a.k[1] >> 16) | (a.k[2] << 16);
+    w[3] = (a.k[2] >> 16) | (a.k[3] << 16);
+    w[4] = (a.k[3] >> 16) | (t0 << 16);
+    w[5] = (t0 >> 16) | (t1 << 16);
+    w[6] = (t1 >> 16) | (hi << 16);
+    const uint32_t len = 18 + ul, nd = len >> 2;
+    uint8_t* o = out + at;
+#pragma unroll
+    for (uint32_t q = 0; q < 7; q++)
+      if (q < nd) *reinterpret_cast<uint32_t*>(o + 4 * q) = w[q];
+    const uint32_t tail = w[nd < 7 ? nd : 6];
+    for (uint32_t b = 4 * nd; b < len; b++) o[b] = (uint8_t)(tail >> (8 * (b & 3)));
+  };
+  // pass 2: this workgroup's round; both maps' entry lengths scanned at once (16-bit halves:
+  // <= 27 x 1024)
+  {
+    const uint32_t i = me * 1024 + t;
+    const uint32_t slot = i < k ? sorted[i] : 0xffffffffu;
+    const unsigned long long vn = slot != 0xffffffffu ? nov[slot] : 0ull;
+    const unsigned long long vs = slot != 0xffffffffu ? st[slot] : 0ull;
+    const uint32_t ln = vn != 0 ? 18u + mp_uint_len(vn) : 0u;
+    const uint32_t ls = vs != 0 ? 18u + mp_uint_len(vs) : 0u;
+    ActorSlot a;
+    if (ln | ls) a = table[slot];
+    uint32_t tot;
+    const uint32_t at = block_scan_1024(ln | (ls << 16), ws, &tot);
+    if (ln) put(nov_at + tpn + (at & 0xffff), a, vn);
+    if (ls) put(st_at + tps + (at >> 16), a, vs);
+  }
+}
+
 // ----------------------------------------------------------------------------------------
 // launchers
 // ----------------------------------------------------------------------------------------
@@ -564,6 +758,25 @@ hipError_t launch_merge_max(hipStream_t s, unsigned long long* dst, const unsign
   if (n == 0) return hipSuccess;
   const uint32_t blocks = min((n + 255) / 256, 1024u);
   hipLaunchKernelGGL(k_merge_max, dim3(blocks), dim3(256), 0, s, dst, src, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_merge_max_if(hipStream_t s, unsigned long long* dst, const unsigned long long* src,
+                               uint32_t n, const uint32_t* counters) {
+  if (n == 0) return hipSuccess;
+  const uint32_t blocks = min((n + 255) / 256, 1024u);
+  hipLaunchKernelGGL(k_merge_max_if, dim3(blocks), dim3(256), 0, s, dst, src, n, counters);
+  return hipGetLastError();
+}
+
+hipError_t launch_serialize_vclock(hipStream_t s, const unsigned long long* nov,
+                                  const unsigned long long* st, const uint32_t* sorted, uint32_t k,
+                                  const ActorSlot* table, bool gcounter, const uint8_t* prefix16,
+                                  uint8_t* out, unsigned long long* offs) {
+  // one workgroup per 1024 sorted entries (at least one: the headers)
+  const uint32_t rounds = k ? (k + 1023) / 1024 : 1;
+  hipLaunchKernelGGL(k_serialize_vclock<4>, dim3(rounds), dim3(1024), 0, s, nov, st, sorted, k, table,
+                     gcounter ? 1 : 0, prefix16, out, offs);
   return hipGetLastError();
 }
 

@@ -192,6 +192,43 @@ def test_compact_to_buffer_matches_fixture(ctx, repo_fx):
         assert crdtenc.content_name(buf[:n]) == name == crdtenc.content_name(f)
 
 
+@pytest.mark.parametrize("n_act", [0, 1, 15, 16, 300, 2500, 5000])
+@pytest.mark.parametrize("kind", [crdtenc.STATE_GCOUNTER, crdtenc.STATE_VCLOCK])
+@pytest.mark.parametrize("flags", [0, crdtenc.COMPACT_INGEST_FORMAT])
+def test_device_compaction_serializer(ctx, oracle, n_act, kind, flags):
+    """compact_to_buffer serializes the StateWrapper on the device (k_serialize_vclock): its
+    sealed clear text must equal the host serializer's state_bytes(), at every uint width and
+    map-header size (fixmap <= 15 < map16), with actors present in only one of the two maps."""
+    rng = random.Random(n_act * 7 + kind + 3 * flags)
+    key = rng.randbytes(32)
+    actors = sorted(rng.randbytes(16) for _ in range(n_act))
+    widths = [7, 8, 16, 32, 64]
+
+    def val():
+        w = rng.choice(widths)
+        return rng.randrange(1, 1 << w)
+
+    nov = {a: val() for a in actors if rng.random() < 0.8}
+    st = {a: val() for a in actors if rng.random() < 0.8}
+    inner = {"dots": dict(sorted(st.items()))}
+    sw = {"next_op_versions": {"dots": dict(sorted(nov.items()))},
+          "state": {"inner": inner} if kind == crdtenc.STATE_GCOUNTER else inner}
+    want = msgpack.packb(sw, use_bin_type=True)
+    core = crdtenc.Core(ctx, kind=kind, supported=[APP], current_data_version=APP, flags=flags)
+    core.set_latest_key(key)
+    core.merge_state(want)
+    assert core.state_bytes() == want
+    nonce = rng.randbytes(24)
+    f, name = core.compact_to_buffer(nonce=nonce)
+    ingest = flags == crdtenc.COMPACT_INGEST_FORMAT
+    assert f[:16] == (CORE if ingest else APP)
+    stt, pt = oracle.cryptor_decrypt(key, f[16:])
+    assert stt == 0 and pt == (APP + want if ingest else want)
+    assert f[16:] == oracle.cryptor_encrypt(key, nonce, pt)[1]
+    assert name == crdtenc.content_name(f)
+    core.close()
+
+
 # ------------------------------------------------------------------ larger random batches
 def make_ops_batch(ctx, key, n_actors, n_versions, dots_per_file, seed, stress=False):
     rng = random.Random(seed)
