@@ -172,6 +172,16 @@ def main():
 
     def step():
         core.reset()
+        if world == 1:
+            # Core::compact (lib.rs:332-380): read_remote_ops + the compaction output in one call
+            rc, f, _ = core.compact_ops_device(files.data_ptr(), offs.data_ptr(), n, blob_len,
+                                               local_actor_bytes, fa_d.data_ptr(), fv_d.data_ptr(),
+                                               name=False)
+            if rc:
+                raise crdtenc.CeError(rc, ctx.last_error())
+            out["file"] = f
+            names.append(namer.submit(crdtenc.content_name, f))
+            return
         rc = core.ingest_ops_device(files.data_ptr(), offs.data_ptr(), n, blob_len,
                                     local_actor_bytes, fa_d.data_ptr(), fv_d.data_ptr())
         if rc:

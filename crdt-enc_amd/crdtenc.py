@@ -41,7 +41,7 @@ EXPORTS = [
     "ce_core_close", "ce_core_set_latest_key", "ce_core_info_actor", "ce_core_read_remote",
     "ce_core_compact", "ce_core_apply_ops", "ce_core_state_bytes", "ce_core_ingest_ops",
     "ce_core_ingest_ops_device", "ce_core_ingest_states", "ce_core_compact_to_buffer",
-    "ce_core_compact_into",
+    "ce_core_compact_into", "ce_core_compact_ops_device",
     "ce_core_register_actors", "ce_core_dense_capacity", "ce_core_export_dense",
     "ce_core_import_dense", "ce_vbuf_init", "ce_vbuf_remaining", "ce_vbuf_chunk",
     "ce_vbuf_advance", "ce_vbuf_chunks_vectored", "ce_ctx_set_timing", "ce_ctx_timing_read",
@@ -413,6 +413,21 @@ class Core:
             ctypes.c_uint64(blob_len), _cbuf(actors), ctypes.c_uint32(len(actors) // 16),
             ctypes.c_void_p(d_file_actor), ctypes.c_void_p(d_file_version), st)
         return (rc, list(st)[:n]) if want_status else rc
+
+    def compact_ops_device(self, d_blob, d_offs, n, blob_len, actors, d_file_actor,
+                           d_file_version, nonce=None, name=True):
+        """Core::compact over a batch resident in HBM (read_remote_ops + compaction output in
+        one call): returns (rc, file, name); file/name are None when rc != 0."""
+        b = Buf()
+        nm = ctypes.create_string_buffer(64) if name else None
+        rc = lib().ce_core_compact_ops_device(
+            self.p, ctypes.c_void_p(d_blob), ctypes.c_void_p(d_offs), ctypes.c_uint32(n),
+            ctypes.c_uint64(blob_len), _cbuf(actors), ctypes.c_uint32(len(actors) // 16),
+            ctypes.c_void_p(d_file_actor), ctypes.c_void_p(d_file_version),
+            _cbuf(nonce) if nonce is not None else None, ctypes.byref(b), nm)
+        if rc:
+            return rc, None, None
+        return rc, _take(b), (nm.value.decode() if name else None)
 
     def ingest_states(self, files):
         n = len(files)

@@ -527,9 +527,15 @@ uint32_t host_gate(const uint32_t* fa, const uint64_t* fv, uint32_t n, std::vect
 
 // Core::read_remote_ops after Storage::load_ops (lib.rs:495-546), files and per-file metadata
 // resident in HBM (d_fa = local actor index per file, d_fv = version per file).
+// after_commit (optional): called once the device commit (k_merge_max_if) is enqueued, before
+// the host waits -- work it enqueues on the stream overlaps the fused kernel's run on the host
+// side.  merged_out: whether the commit happened on the device (the fast path).
+using AfterCommit = std::function<int(const NovApply&)>;
 int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
                    uint64_t blob_len, const uint8_t* actors, uint32_t m, const uint32_t* d_fa,
-                   const uint64_t* d_fv, int32_t* status_out) {
+                   const uint64_t* d_fv, int32_t* status_out, const AfterCommit* after_commit = nullptr,
+                   bool* merged_out = nullptr) {
+  if (merged_out) *merged_out = false;
   ce_ctx* ctx = c->ctx;
   if (!c->has_key) return ctx->fail(CE_ERR_NO_KEY, "no latest key");
   if (n == 0) return CE_OK;
@@ -561,7 +567,8 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
   if ((e = ctx->out.reserve(blob_len + 16ull * n + 128)) || (e = ctx->status.reserve(n * 4ull + 64)) ||
       (e = ctx->apply.reserve(n + 64)) || (e = ctx->refold.reserve(n + 64)) ||
       (e = c->d_refold2.reserve(n + 64)) || (e = ctx->miss.reserve(65536 * 16)) ||
-      (e = c->d_gate.reserve(m * 24ull + 64)) || (e = ctx->h_stage2.reserve(m * 16ull + 64)))
+      (e = c->d_gate.reserve(m * 24ull + 64)) || (e = ctx->h_stage2.reserve(m * 20ull + 64)) ||
+      (after_commit && (e = c->d_wslot.reserve(m * 4ull + 64))))
     return ctx->hip_fail(e, "ingest reserve");
 
   // expected versions per writer (next_op_versions.get, lib.rs:481) -> device
@@ -688,6 +695,15 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
   uint64_t* hnov = he0 + m;
   if ((e = hipMemcpyAsync(hnov, gbase + 8ull * m, m * 8ull, hipMemcpyDeviceToHost, ctx->stream)))
     return ctx->hip_fail(e, "nov");
+  if (after_commit) {
+    uint32_t* hw = reinterpret_cast<uint32_t*>(he0 + 2ull * m);
+    std::memcpy(hw, wslot.data(), m * 4ull);
+    if ((e = hipMemcpyAsync(c->d_wslot.p, hw, m * 4ull, hipMemcpyHostToDevice, ctx->stream)))
+      return ctx->hip_fail(e, "writer slots");
+    const NovApply na{c->d_wslot.as<uint32_t>(), reinterpret_cast<const unsigned long long*>(gbase + 8ull * m),
+                      m, ctx->counters.as<uint32_t>()};
+    if ((rc = (*after_commit)(na))) return rc;
+  }
   if (prof) {
     std::vector<unsigned long long> hp(8ull * 65536);
     if ((e = hipMemcpyAsync(hp.data(), prof_buf.p, hp.size() * 8, hipMemcpyDeviceToHost, ctx->stream)) ||
@@ -710,6 +726,7 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
       (e = hipStreamSynchronize(ctx->stream)))
     return ctx->hip_fail(e, "fold sync");
   const bool merged_on_device = (hc[2] | hc[3] | hc[4] | hc[7] | hc[8] | hc[12]) == 0;
+  if (merged_out) *merged_out = merged_on_device;
 
   // 3) batches outside the device gate's shape: host gate, fold again with its flags
   std::vector<uint64_t> expect(he0, he0 + m);
@@ -1005,11 +1022,19 @@ int read_remote(ce_core* c) {
 
 // compaction of a VClock / GCounter state without leaving the device: the StateWrapper is
 // serialized from the dense arrays (k_serialize_vclock) into the seal's input, sealed, and only
-// the sealed file comes back (one synchronisation).  Same bytes as serialize_state + seal_one.
-int compact_device(ce_core* c, const uint8_t* nonce, std::vector<uint8_t>* file) {
-  ce_ctx* ctx = c->ctx;
+// the sealed file comes back.  Same bytes as serialize_state + seal_one.
+//   compact_enqueue: everything up to the download into x->h_stage, on x's stream (no sync).
+//     With `na`, next_op_versions of the ingest still in flight is folded in on the device
+//     (k_nov_apply, skipped exactly when that ingest's merge is) -- the host nov is then the
+//     pre-ingest one.
+//   compact_finish: after the stream has been synchronised, the file from the staging buffer.
+struct CompactPending {
+  uint64_t U = 0, total_max = 0;
+};
+
+int compact_enqueue(ce_core* c, ce_ctx* x, const uint8_t* nonce, const NovApply* na, CompactPending* pend) {
   const KeyRef key = key_of(c);
-  if (int32_t ks = key_status(key)) return ctx->fail(ks, "key rejected");
+  if (int32_t ks = key_status(key)) return x->fail(ks, "key rejected");
   const bool ingest_fmt = (c->flags & CE_COMPACT_INGEST_FORMAT) != 0;
   // readable by read_remote_states: CURRENT_VERSION || encrypt(data_version || state); else
   // exactly what Core::compact writes: VersionBytes(current_data_version, encrypt(state))
@@ -1022,21 +1047,21 @@ int compact_device(ce_core* c, const uint8_t* nonce, std::vector<uint8_t>* file)
   if (c->d_sorted_gen != c->sorted_gen) {
     if ((e = c->d_sorted.reserve(4ull * k + 64)) ||
         (k && (e = hipMemcpyAsync(c->d_sorted.p, c->sorted_slots.data(), 4ull * k, hipMemcpyHostToDevice,
-                                  ctx->stream))) ||
-        (e = hipStreamSynchronize(ctx->stream)))
-      return ctx->hip_fail(e, "sorted slots");
+                                  x->stream))) ||
+        (e = hipStreamSynchronize(x->stream)))
+      return x->hip_fail(e, "sorted slots");
     c->d_sorted_gen = c->sorted_gen;
   }
   const uint64_t U = vclock_ser_bound(k);             // clear length bound (prefix included)
   const uint64_t A = (U + 255) & ~255ull;              // small arguments after the clear text
   const uint64_t total_max = 16 + sealed_len(U);
   const uint64_t nov_bytes = 8ull * c->cap;
-  if ((e = ctx->blob.reserve(A + 128)) || (e = ctx->out.reserve(total_max + 64)) ||
-      (e = ctx->h_stage.reserve(std::max<uint64_t>(total_max + 64, 128 + nov_bytes))) ||
+  if ((e = x->blob.reserve(A + 128)) || (e = x->out.reserve(total_max + 64)) ||
+      (e = x->h_stage.reserve(std::max<uint64_t>(total_max + 64, 128 + nov_bytes))) ||
       (e = c->d_tmp.reserve(nov_bytes)))
-    return ctx->hip_fail(e, "compact reserve");
+    return x->hip_fail(e, "compact reserve");
   // staging: [offs(2) | out_offs(1) | nonce(24) | outer(16) | prefix16(16)] at 0, nov at 128
-  uint8_t* hs = ctx->h_stage.as<uint8_t>();
+  uint8_t* hs = x->h_stage.as<uint8_t>();
   const uint64_t args[3] = {0, 0, 0};
   std::memcpy(hs, args, 24);
   if (nonce) std::memcpy(hs + 24, nonce, 24);
@@ -1044,31 +1069,49 @@ int compact_device(ce_core* c, const uint8_t* nonce, std::vector<uint8_t>* file)
   std::memcpy(hs + 48, outer, 16);
   std::memcpy(hs + 64, c->current_data_version.data(), 16);
   std::memcpy(hs + 128, c->nov.data(), nov_bytes);
-  uint8_t* db = ctx->blob.as<uint8_t>();
-  if ((e = hipMemcpyAsync(db + A, hs, 80, hipMemcpyHostToDevice, ctx->stream)) ||
-      (e = hipMemcpyAsync(c->d_tmp.p, hs + 128, nov_bytes, hipMemcpyHostToDevice, ctx->stream)))
-    return ctx->hip_fail(e, "compact upload");
+  uint8_t* db = x->blob.as<uint8_t>();
+  if ((e = hipMemcpyAsync(db + A, hs, 80, hipMemcpyHostToDevice, x->stream)) ||
+      (e = hipMemcpyAsync(c->d_tmp.p, hs + 128, nov_bytes, hipMemcpyHostToDevice, x->stream)))
+    return x->hip_fail(e, "compact upload");
+  if (na && (e = launch_nov_apply(x->stream, c->d_tmp.as<unsigned long long>(), na->wslot, na->newnov,
+                                  na->m, na->counters)))
+    return x->hip_fail(e, "nov apply");
   auto* d_offs = reinterpret_cast<unsigned long long*>(db + A);
-  if ((e = launch_serialize_vclock(ctx->stream, c->d_tmp.as<unsigned long long>(),
+  if ((e = launch_serialize_vclock(x->stream, c->d_tmp.as<unsigned long long>(),
                                    c->d_state.as<unsigned long long>(), c->d_sorted.as<uint32_t>(), k,
                                    c->d_table.as<ActorSlot>(), c->kind == CE_STATE_GCOUNTER,
                                    ingest_fmt ? db + A + 64 : nullptr, db, d_offs)))
-    return ctx->hip_fail(e, "serialize");
-  rc = device_seal(ctx, db, reinterpret_cast<const uint64_t*>(d_offs), 1, U, db + A + 48, db + A + 24,
-                       ctx->out.as<uint8_t>(), reinterpret_cast<const uint64_t*>(db + A + 16), key);
+    return x->hip_fail(e, "serialize");
+  rc = device_seal(x, db, reinterpret_cast<const uint64_t*>(d_offs), 1, U, db + A + 48, db + A + 24,
+                   x->out.as<uint8_t>(), reinterpret_cast<const uint64_t*>(db + A + 16), key);
   if (rc) return rc;
-  // the sealed file (its bound) and the clear length, one synchronisation
-  if ((e = hipMemcpyAsync(hs, ctx->out.p, total_max, hipMemcpyDeviceToHost, ctx->stream)) ||
-      (e = hipMemcpyAsync(hs + total_max, db + A + 8, 8, hipMemcpyDeviceToHost, ctx->stream)) ||
-      (e = hipStreamSynchronize(ctx->stream)))
-    return ctx->hip_fail(e, "compact download");
+  // the sealed file (its bound) and the clear length
+  if ((e = hipMemcpyAsync(hs, x->out.p, total_max, hipMemcpyDeviceToHost, x->stream)) ||
+      (e = hipMemcpyAsync(hs + total_max, db + A + 8, 8, hipMemcpyDeviceToHost, x->stream)))
+    return x->hip_fail(e, "compact download");
+  pend->U = U;
+  pend->total_max = total_max;
+  return CE_OK;
+}
+
+int compact_finish(ce_ctx* x, const CompactPending& pend, std::vector<uint8_t>* file) {
+  const uint8_t* hs = x->h_stage.as<uint8_t>();
   uint64_t clear_len;
-  std::memcpy(&clear_len, hs + total_max, 8);
-  if (clear_len > U) return ctx->fail(CE_ERR_DEVICE, "serializer overran its bound");
+  std::memcpy(&clear_len, hs + pend.total_max, 8);
+  if (clear_len > pend.U) return x->fail(CE_ERR_DEVICE, "serializer overran its bound");
   const uint64_t total = 16 + sealed_len(clear_len);
   file->resize(total);
   std::memcpy(file->data(), hs, total);
   return CE_OK;
+}
+
+int compact_device(ce_core* c, const uint8_t* nonce, std::vector<uint8_t>* file) {
+  CompactPending pend;
+  int rc = compact_enqueue(c, c->ctx, nonce, nullptr, &pend);
+  if (rc) return rc;
+  hipError_t e;
+  if ((e = hipStreamSynchronize(c->ctx->stream))) return c->ctx->hip_fail(e, "compact sync");
+  return compact_finish(c->ctx, pend, file);
 }
 
 // clear text + file of a compaction (lib.rs:335-360)
@@ -1231,6 +1274,51 @@ int ce_core_ingest_ops_device(ce_core* c, const uint8_t* d_blob, const uint64_t*
   (void)hipSetDevice(c->ctx->device);
   return ingest_ops_dev(c, d_blob, d_offs, n, blob_len, actors, m, d_file_actor, d_file_version,
                         status);
+}
+
+// Core::compact (lib.rs:332-380) over op files resident in HBM: read_remote_ops, then the
+// compaction output.  The compaction (nov fold, serialize, seal, download) is enqueued behind
+// the ingest's device commit on the aux context's buffers, so one host synchronisation covers
+// both; when the ingest leaves its fast path the speculative file is dropped and the compaction
+// runs again from the committed host state.
+int ce_core_compact_ops_device(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
+                               uint64_t blob_len, const uint8_t* actors, uint32_t m,
+                               const uint32_t* d_file_actor, const uint64_t* d_file_version,
+                               const uint8_t* nonce, ce_buf* file, char name_out[64]) {
+  if (!c || !file || (n && (!d_blob || !d_offs || !actors || !d_file_actor || !d_file_version)))
+    return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  (void)hipSetDevice(c->ctx->device);
+  if (!c->has_key) return c->ctx->fail(CE_ERR_NO_KEY, "no latest key");
+  std::vector<uint8_t>& f = c->file_buf;
+  int rc;
+  bool merged = false;
+  const bool spec = !is_dotset_kind(c->kind) && !c->host_compact && n > 0;
+  ce_ctx* x = aux_ctx(c);
+  x->stream = c->ctx->stream;  // the compaction is ordered behind the ingest on one stream
+  CompactPending pend;
+  uint8_t nb[24];  // one nonce for the speculative and (if needed) the repeated compaction
+  if (nonce) std::memcpy(nb, nonce, 24);
+  else os_random(nb, 24);
+  const AfterCommit hook = [&](const NovApply& na) { return compact_enqueue(c, x, nb, &na, &pend); };
+  rc = ingest_ops_dev(c, d_blob, d_offs, n, blob_len, actors, m, d_file_actor, d_file_version, nullptr,
+                      spec ? &hook : nullptr, &merged);
+  if (rc) {
+    if (spec) (void)hipStreamSynchronize(c->ctx->stream);  // nothing left in flight on x's buffers
+    return rc;  // read_remote's error: compact writes nothing (lib.rs:333)
+  }
+  if (spec && merged) rc = compact_finish(x, pend, &f);
+  else rc = compact_bytes(c, nb, &f);
+  if (rc) return rc;
+  if (name_out) {
+    uint8_t h[32];
+    sha3_256(f.data(), f.size(), h);
+    std::snprintf(name_out, 64, "%s", base32_nopad(h, 32).c_str());
+  }
+  file->data = (uint8_t*)malloc(f.size() ? f.size() : 1);
+  std::memcpy(file->data, f.data(), f.size());
+  file->len = f.size();
+  return CE_OK;
 }
 
 int ce_core_ingest_states(ce_core* c, const uint8_t* blob, const uint64_t* offs, uint32_t n,

@@ -64,7 +64,7 @@ struct ce_core {
   std::vector<uint32_t> last_wslot;
   uint64_t last_writers_gen = ~0ull;
   ce::DevBuf d_table, d_state, d_batch, d_supported, d_refold2, d_tmp, d_gate, d_meta;
-  ce::DevBuf d_sorted;                  // sorted_slots on the device (compaction serializer)
+  ce::DevBuf d_sorted, d_wslot;                  // sorted_slots on the device (compaction serializer)
   uint64_t d_sorted_gen = ~0ull;
   int files_per_wave = 4;  // fused kernel geometry (CE_FILES_PER_WAVE overrides)
   bool supported_on_device = false;
@@ -127,6 +127,14 @@ struct HostPhase {
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     std::fprintf(stderr, "CE_HOST_PROF %-24s %9.3f ms\n", name, ms);
   }
+};
+
+// next_op_versions of an ingest whose device commit is still in flight (compact_enqueue)
+struct NovApply {
+  const uint32_t* wslot;                 // device: slot of each writer
+  const unsigned long long* newnov;      // device: the gate's next_op_versions per writer
+  uint32_t m;
+  const uint32_t* counters;              // device: the ingest's counter block
 };
 
 bool skip_any(Rd& r, int depth = 0);

@@ -275,6 +275,11 @@ int ce_ctx_create(int device, ce_ctx** out) {
   if (hipGetDeviceCount(&count) != hipSuccess || count <= device || device < 0)
     return CE_ERR_DEVICE;  // no GPU: the product has no CPU path
   if (hipSetDevice(device) != hipSuccess) return CE_ERR_DEVICE;
+  // CE_SPIN=1 (diagnostics): host waits spin instead of yielding (wake-up latency of the
+  // per-step synchronisations)
+  if (const char* sp = getenv("CE_SPIN")) {
+    if (atoi(sp)) (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
+  }
   ce_ctx* c = new ce_ctx();
   c->device = device;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {

@@ -247,7 +247,7 @@ __device__ __forceinline__ uint32_t ld_le32(const uint8_t* p) {
 }
 
 // key schedule shared by open/seal setup: subkey, (r, s), r^(2^k); nonce as 6 LE words
-__device__ void key_schedule_w(const DevKey& key, const uint32_t (&nw)[6], FileParams& P) {
+__device__ __forceinline__ void key_schedule_w(const DevKey& key, const uint32_t (&nw)[6], FileParams& P) {
   uint32_t k[8], n16[4], sub[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) k[i] = key.k[i];
@@ -273,6 +273,7 @@ __device__ void key_schedule_w(const DevKey& key, const uint32_t (&nw)[6], FileP
 #pragma unroll
   for (int i = 0; i < 5; i++) P.rpow[0][i] = r.v[i];
   L5 p = r;
+#pragma unroll  // constant rpow indices: P stays in registers (no scratch in the setup kernels)
   for (int kk = 1; kk < 7; kk++) {
     p = mulmod(p, p);
 #pragma unroll

@@ -121,6 +121,9 @@ hipError_t launch_merge_max(hipStream_t s, unsigned long long* dst,
 // launch_merge_max unless the counter block flags a batch that cannot commit as folded
 hipError_t launch_merge_max_if(hipStream_t s, unsigned long long* dst, const unsigned long long* src,
                                uint32_t n, const uint32_t* counters);
+// nov[wslot[a]] = max(nov[wslot[a]], newnov[a]) unless the counters flag (as launch_merge_max_if)
+hipError_t launch_nov_apply(hipStream_t s, unsigned long long* nov, const uint32_t* wslot,
+                            const unsigned long long* newnov, uint32_t m, const uint32_t* counters);
 // to_vec_named(StateWrapper<VClock|GCounter>) from the dense nov / state arrays (k sorted slots);
 // clear length -> offs[1] (offs[0] = 0).  Upper bound of the output: vclock_ser_bound(k)
 hipError_t launch_serialize_vclock(hipStream_t s, const unsigned long long* nov,

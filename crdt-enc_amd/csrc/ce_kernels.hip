@@ -522,6 +522,16 @@ __global__ void k_merge_max_if(unsigned long long* __restrict__ dst,
 }
 
 
+// next_op_versions of a gated batch on the device: nov[wslot[a]] = max(nov, newnov[a]) (lib.rs:
+// 537-538), under the same skip condition as k_merge_max_if
+__global__ void k_nov_apply(unsigned long long* __restrict__ nov, const uint32_t* __restrict__ wslot,
+                            const unsigned long long* __restrict__ newnov, uint32_t m,
+                            const uint32_t* __restrict__ counters) {
+  if (counters[2] | counters[3] | counters[4] | counters[7] | counters[8] | counters[12]) return;
+  for (uint32_t a = blockIdx.x * blockDim.x + threadIdx.x; a < m; a += gridDim.x * blockDim.x)
+    atomicMax(&nov[wslot[a]], newnov[a]);
+}
+
 // ----------------------------------------------------------------------------------------
 // k_serialize_vclock: to_vec_named(StateWrapper) for S = VClock<Uuid> / GCounter<Uuid>
 // (crdt-enc/src/lib.rs:336,739-743) straight from the dense device arrays, so a compaction
@@ -766,6 +776,14 @@ hipError_t launch_merge_max_if(hipStream_t s, unsigned long long* dst, const uns
   if (n == 0) return hipSuccess;
   const uint32_t blocks = min((n + 255) / 256, 1024u);
   hipLaunchKernelGGL(k_merge_max_if, dim3(blocks), dim3(256), 0, s, dst, src, n, counters);
+  return hipGetLastError();
+}
+
+hipError_t launch_nov_apply(hipStream_t s, unsigned long long* nov, const uint32_t* wslot,
+                            const unsigned long long* newnov, uint32_t m, const uint32_t* counters) {
+  if (m == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_nov_apply, dim3(min((m + 255) / 256, 256u)), dim3(256), 0, s, nov,
+                     wslot, newnov, m, counters);
   return hipGetLastError();
 }
 

@@ -241,6 +241,15 @@ int ce_core_ingest_ops_device(ce_core *c, const uint8_t *d_blob, const uint64_t 
 /* What read_remote_states does after Storage::load_states (lib.rs:425-466). */
 int ce_core_ingest_states(ce_core *c, const uint8_t *blob, const uint64_t *offs, uint32_t n,
                           int32_t *status);
+/* Core::compact (crdt-enc/src/lib.rs:332-380) over a batch resident in HBM: read_remote_ops over
+ * the op files exactly as ce_core_ingest_ops_device, then the compaction output as
+ * ce_core_compact_to_buffer.  For VClock/GCounter the compaction is queued on the device behind
+ * the ingest's commit (one host synchronisation for both).  A read_remote error is returned
+ * before anything is written (file untouched).  nonce: 24 bytes or NULL; name_out may be NULL. */
+int ce_core_compact_ops_device(ce_core *c, const uint8_t *d_blob, const uint64_t *d_offs, uint32_t n,
+                               uint64_t blob_len, const uint8_t *actors, uint32_t m,
+                               const uint32_t *d_file_actor, const uint64_t *d_file_version,
+                               const uint8_t *nonce, ce_buf *file, char name_out[64]);
 /* compact() without storage: serialize the state, seal it on the GPU with the latest key and
  * return the state file bytes and its content name.  nonce: 24 bytes or NULL (OS RNG). */
 int ce_core_compact_to_buffer(ce_core *c, const uint8_t *nonce, ce_buf *file, char name_out[64]);

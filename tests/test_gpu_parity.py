@@ -594,3 +594,76 @@ def test_dense_exchange_two_shards(ctx, oracle):
     fresh.register_actors(actors)
     fresh.import_dense(st.data_ptr(), nv.data_ptr())
     assert fresh.state_bytes() == oc.serialize()
+
+
+def _to_device(files, fa, vers):
+    torch = pytest.importorskip("torch")
+    blob = b"".join(files)
+    offs = np.zeros(len(files) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum([len(f) for f in files])
+    d = (torch.tensor(list(blob) + [0] * 64, dtype=torch.uint8, device="cuda"),
+         torch.tensor(offs, device="cuda"),
+         torch.tensor(np.array(fa, dtype=np.int32), device="cuda"),
+         torch.tensor(np.array(vers, dtype=np.int64), device="cuda"))
+    torch.cuda.synchronize()
+    return d, len(blob)
+
+
+@pytest.mark.parametrize("case", ["clean", "stress", "foreign_actors", "tampered", "gap"])
+@pytest.mark.parametrize("kind", [crdtenc.STATE_GCOUNTER, crdtenc.STATE_VCLOCK])
+def test_compact_ops_device(ctx, oracle, case, kind):
+    """ce_core_compact_ops_device (Core::compact, lib.rs:332-380, over a batch in HBM) == the
+    two-call path ingest_ops_device + compact_to_buffer with the same nonce, on the fast path
+    (compaction queued behind the device commit) and on every slow path: actors outside the
+    table (refold), a failing tag (read_remote error, nothing written, state unchanged) and a
+    version gap (error)."""
+    key = os.urandom(32)
+    files, actors, fa, vers = make_ops_batch(ctx, key, 6, 5, 20, seed=11, stress=(case != "clean"))
+    if case == "foreign_actors":  # dots of actors no writer list names: device misses + refold
+        rng = random.Random(3)
+        foreign = sorted(rng.randbytes(16) for _ in range(5))
+        clears = [APP + msgpack.packb([{"actor": rng.choice(foreign), "counter": rng.getrandbits(40)}
+                                       for _ in range(7)], use_bin_type=True) for _ in files]
+        files = [CORE + e for e in ctx.encrypt_batch(key, clears)]
+    if case == "tampered":
+        b = bytearray(files[9]); b[-3] ^= 1; files[9] = bytes(b)
+    if case == "gap":  # drop one version of actor 0: versions after it are not contiguous
+        keep = [i for i in range(len(files)) if not (fa[i] == 0 and vers[i] == 2)]
+        files, fa, vers = [files[i] for i in keep], [fa[i] for i in keep], [vers[i] for i in keep]
+    (d_blob, d_offs, d_fa, d_fv), blen = _to_device(files, fa, vers)
+    nonce = bytes(range(24))
+
+    def new():
+        c = crdtenc.Core(ctx, kind=kind, supported=[APP], current_data_version=APP)
+        c.set_latest_key(key)
+        return c
+    ref = new()
+    rc_ref = ref.ingest_ops_device(d_blob.data_ptr(), d_offs.data_ptr(), len(files), blen,
+                                   b"".join(actors), d_fa.data_ptr(), d_fv.data_ptr())
+    core = new()
+    before = core.state_bytes()
+    rc, f, name = core.compact_ops_device(d_blob.data_ptr(), d_offs.data_ptr(), len(files), blen,
+                                          b"".join(actors), d_fa.data_ptr(), d_fv.data_ptr(),
+                                          nonce=nonce)
+    assert rc == rc_ref, (rc, rc_ref, ctx.last_error())
+    if case == "tampered":
+        assert rc == 9 and f is None and core.state_bytes() == before
+    elif case == "gap":
+        assert rc == 13 and f is None
+        assert core.state_bytes() == ref.state_bytes()   # files before the gap stay folded
+    else:
+        assert rc == 0
+        want, want_name = ref.compact_to_buffer(nonce=nonce)
+        assert f == want and name == want_name
+        assert core.state_bytes() == ref.state_bytes()
+        oc = oracle.Core(oracle.STATE_GCOUNTER if kind == crdtenc.STATE_GCOUNTER else oracle.STATE_VCLOCK)
+        assert oc.read_remote_ops(key, [APP], files, [actors[i] for i in fa], vers)[0] == 0
+        st, pt = oracle.cryptor_decrypt(key, f[16:])
+        assert st == 0 and pt == oc.serialize()
+        # a second compaction over the same batch: every file is below next_op_versions now
+        rc2, f2, _ = core.compact_ops_device(d_blob.data_ptr(), d_offs.data_ptr(), len(files), blen,
+                                             b"".join(actors), d_fa.data_ptr(), d_fv.data_ptr(),
+                                             nonce=nonce)
+        assert rc2 == 0 and f2 == f
+    core.close()
+    ref.close()
