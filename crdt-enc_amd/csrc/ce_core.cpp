@@ -417,9 +417,9 @@ ce_ctx* aux_ctx(ce_core* c) {
   if (!c->aux) {
     c->aux = new ce_ctx();
     c->aux->device = c->ctx->device;
-    c->aux->stream = c->ctx->stream;
     c->aux->own_stream = false;
   }
+  c->aux->stream = c->ctx->stream;  // follows ce_ctx_set_stream
   return c->aux;
 }
 
@@ -1294,8 +1294,7 @@ int ce_core_compact_ops_device(ce_core* c, const uint8_t* d_blob, const uint64_t
   int rc;
   bool merged = false;
   const bool spec = !is_dotset_kind(c->kind) && !c->host_compact && n > 0;
-  ce_ctx* x = aux_ctx(c);
-  x->stream = c->ctx->stream;  // the compaction is ordered behind the ingest on one stream
+  ce_ctx* x = aux_ctx(c);  // same stream: the compaction is ordered behind the ingest
   CompactPending pend;
   uint8_t nb[24];  // one nonce for the speculative and (if needed) the repeated compaction
   if (nonce) std::memcpy(nb, nonce, 24);
