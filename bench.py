@@ -289,6 +289,21 @@ def main():
             if kname.split(" (")[0].rstrip(">") in rec.get("kernel", "") and \
                     rec.get("files_per_launch") == n:
                 traffic = rec.get("bytes_per_launch")
+        # VALU issue from the PMC record of this kernel (SQ_INSTS_VALU x 64 lanes per file,
+        # tools/pmc_valu.sh) at this run's launch time: the kernel's binding roofline
+        valu_pmc = None
+        vf = os.path.join(REPO, "profiles", "r01_valu_pmc.json")
+        if os.path.exists(vf) and avg_s > 0 and fused == "2" and lpf == 16:
+            with open(vf) as f:
+                rec = json.load(f).get("fused", {})
+            ipf = rec.get("valu_instr_per_file_per_lane")
+            if ipf:
+                t = n * ipf / avg_s / 1e12
+                valu_pmc = {"instr_per_file": ipf, "achieved_tops": round(t, 2),
+                            "frac_of_measured": round(t / VALU_INT32_MEASURED_TOPS, 4),
+                            "frac_of_peak": round(t / VALU_PEAK_TOPS, 4),
+                            "source": "profiles/r01_valu_pmc.json (rocprofv3 SQ_INSTS_VALU x 64 "
+                                      "per file, same kernel and workload)"}
         line = {
             "metric": METRIC,
             "value": round(n * world / (ms_max / 1e3), 1),
@@ -321,7 +336,7 @@ def main():
                          "frac": round(valu / VALU_PEAK_TOPS, 4),
                          "int32_measured_peak_tops": VALU_INT32_MEASURED_TOPS,
                          "frac_of_measured": round(valu / VALU_INT32_MEASURED_TOPS, 4),
-                         "ops_per_file": ops_per_file},
+                         "ops_per_file": ops_per_file, "pmc_instructions": valu_pmc},
             },
             "kernels_ms_per_step": {k: round(v[0] / max(v[1], 1), 4) for k, v in kern.items() if v[1]},
             "state_check": "closed-form StateWrapper bytes: %s" % ("ok" if ok else "MISMATCH"),
