@@ -154,8 +154,9 @@ def main():
     core.set_latest_key(key)
     core.register_actors([bytes(a) for a in actors_all])   # same dense slots on every rank
     cap = core.dense_capacity()
-    st_t = torch.zeros(cap, dtype=torch.int64, device=dev)
-    nov_t = torch.zeros(cap, dtype=torch.int64, device=dev)
+    # state and next_op_versions side by side: one all_reduce(MAX) per step (latency-bound)
+    dense = torch.zeros(2 * cap, dtype=torch.int64, device=dev)
+    st_t, nov_t = dense[:cap], dense[cap:]
     local_actor_bytes = b"".join(bytes(a) for a in actors_local)
     fa = np.repeat(np.arange(per, dtype=np.uint32), versions)
     fv = np.tile(np.arange(versions, dtype=np.uint64), per)
@@ -188,7 +189,7 @@ def main():
             raise crdtenc.CeError(rc, ctx.last_error())
         if world > 1:
             core.export_dense(st_t.data_ptr(), nov_t.data_ptr())
-            shard.merge_dense(st_t, nov_t)     # all_reduce(MAX) over u64
+            shard.merge_dense(dense)           # all_reduce(MAX) over u64
             core.import_dense(st_t.data_ptr(), nov_t.data_ptr())
         if rank == 0:
             f, _ = core.compact_to_buffer(name=False)

@@ -7,6 +7,17 @@
                 reset + read_remote_states + read_remote_ops + compact (crdt-enc/src/lib.rs:
                 332-547) with the op files resident in HBM and the state files on the host.
 
+  --config c4   skewed sizes: 1024 actors x 32 versions of GCounter op files whose plaintexts are
+                log-uniform on [256 B, 1 MiB] (~4 GB, the C2 byte volume): single-page files take
+                the fused kernel, larger ones the 16 KiB-segment open + the wave-per-file decode.
+                One step = reset + Core::compact over the batch in HBM (compact_ops_device).
+                Check: the StateWrapper equals its closed form.
+  --config c5   key-rotation mix: the C2 batch (1M x 4 KiB, 4096 actors) with the odd actors'
+                files sealed under a second data key and 0.1% of all files with one flipped tag
+                bit.  One step = reset + read_remote_ops with per-file statuses under the latest
+                key (key_cryptor.rs:59-70): every second-key and tampered file must be rejected
+                (CE_ERR_AUTH), every other file accepted, and nothing folded (lib.rs:497-516).
+
 Prints one JSON line per run.  Checks (size-independent): the merged clock equals its closed
 form (actor a's adds count 26 per version), and an actor-sharded fold of the same files merged
 with merge_state (the multi-GPU exchange) serializes to the same bytes.
@@ -42,6 +53,7 @@ assert (len(ADD_T), len(RM_T), PT_LEN) == (62, 55, 1961)
 
 
 HOST_PROF = bool(os.environ.get("CE_HOST_PROF"))
+KEY = bytes(np.random.default_rng(7).integers(0, 256, 32, dtype=np.uint8))  # latest data key
 
 
 def log(*a):
@@ -276,9 +288,195 @@ def run_c3(args, ctx, dev):
     core.close()
 
 
+
+def dots_plaintext(uuid, k, ctr0):
+    """APP || msgpack([Dot{actor, counter}] * k), counters ctr0+1 .. ctr0+k as uint32 (38 B per
+    Dot, rmp-serde's smallest array header)."""
+    hdr = bytes([0x90 | k]) if k <= 15 else (b"\xdc" + k.to_bytes(2, "big") if k <= 0xffff
+                                             else b"\xdd" + k.to_bytes(4, "big"))
+    d = np.empty((k, 38), np.uint8)
+    d[:, 0:9] = np.frombuffer(b"\x82\xa5actor\xc4\x10", np.uint8)
+    d[:, 9:25] = uuid
+    d[:, 25:33] = np.frombuffer(b"\xa7counter", np.uint8)
+    d[:, 33] = 0xce
+    c = np.arange(ctr0 + 1, ctr0 + k + 1, dtype=np.uint64)
+    for b in range(4):
+        d[:, 34 + b] = (c >> np.uint64(8 * (3 - b))) & np.uint64(255)
+    return APP + hdr + d.tobytes()
+
+
+def run_c4(args, ctx, dev):
+    import msgpack
+    actors = actors_table()[::4]                      # 1024 actors, UUID order
+    m, V = actors.shape[0], args.c4_versions
+    rng = np.random.default_rng(404)
+    size = np.exp(rng.uniform(np.log(256), np.log(1 << 20), size=(m, V))).astype(np.int64)
+    kd = np.maximum(1, (size - 19) // 38)             # dots per file
+    n = m * V
+    pt_len = [16 + (1 if k <= 15 else 3 if k <= 0xffff else 5) + 38 * int(k) for k in kd.ravel()]
+    f_len = [16 + crdtenc.sealed_len(x) for x in pt_len]
+    offs_h = np.zeros(n + 1, np.int64)
+    offs_h[1:] = np.cumsum(f_len)
+    blob_len = int(offs_h[-1])
+    files = torch.empty(blob_len + 64, dtype=torch.uint8, device=dev)
+    t0 = time.time()
+    # seal in chunks of ~256 MB of plaintext on the GPU (seeded nonces)
+    gen = np.random.default_rng(405)
+    i = 0
+    cum = np.zeros(m, np.int64)
+    while i < n:
+        j, tot = i, 0
+        while j < n and (j == i or tot + pt_len[j] <= 1 << 28):
+            tot += pt_len[j]
+            j += 1
+        parts, coffs = [], [0]
+        for f in range(i, j):
+            a, v = divmod(f, V)
+            parts.append(dots_plaintext(actors[a], int(kd[a, v]), 65536 + int(cum[a])))
+            cum[a] += kd[a, v]
+            coffs.append(coffs[-1] + len(parts[-1]))
+        clear = torch.from_numpy(np.frombuffer(b"".join(parts), np.uint8).copy()).to(dev)
+        co = torch.tensor(coffs, dtype=torch.int64, device=dev)
+        nonces = torch.from_numpy(gen.integers(0, 256, (j - i, 24), dtype=np.uint8)).to(dev)
+        oo = torch.from_numpy(offs_h[i:j].copy()).to(dev)
+        torch.cuda.current_stream().synchronize()
+        ctx.encrypt_batch_device(KEY, clear.data_ptr(), co.data_ptr(), j - i, nonces.data_ptr(),
+                                 files.data_ptr(), oo.data_ptr(), outer_version=CORE)
+        ctx.synchronize()
+        i = j
+    offs = torch.from_numpy(offs_h).to(dev)
+    fa = torch.from_numpy(np.repeat(np.arange(m, dtype=np.int32), V)).to(dev)
+    fv = torch.from_numpy(np.tile(np.arange(V, dtype=np.int64), m)).to(dev)
+    log("c4: sealed %d files (%.2f GB, %d > 4 KiB) in %.1f s" % (n, blob_len / 1e9,
+                                                                int((np.array(pt_len) > 4096).sum()), time.time() - t0))
+    core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+    core.set_latest_key(KEY)
+    wr = b"".join(bytes(a) for a in actors)
+
+    def step():
+        core.reset()
+        rc, f, _ = core.compact_ops_device(files.data_ptr(), offs.data_ptr(), n, blob_len, wr,
+                                           fa.data_ptr(), fv.data_ptr(), name=False)
+        if rc:
+            raise crdtenc.CeError(rc, ctx.last_error())
+        return f
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ctx.timing_reset()
+    ctx.set_timing(True)
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        f = step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t) * 1e3 / args.steps
+    ctx.set_timing(False)
+    k_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in
+            ((k, ctx.timing(k)) for k in ("open_setup", "gate", "open_fold_small", "segments_open",
+                                         "finalize_open", "decode", "merge")) if v[1]}
+    want = msgpack.packb({"next_op_versions": {"dots": {bytes(a): V for a in actors}},
+                          "state": {"inner": {"dots": {bytes(actors[a]): 65536 + int(kd[a].sum())
+                                                       for a in range(m)}}}}, use_bin_type=True)
+    ok = core.state_bytes() == want
+    ct = sum(pt_len)
+    line = {
+        "metric": "C4 skewed-size op files compacted/sec + AEAD GB/s (GCounter, 256 B-1 MiB)",
+        "value": round(n / (ms / 1e3), 1), "unit": "files/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+        "higher_is_better": True, "dtype": "u32", "data": "synthetic (GPU-sealed, seeded)",
+        "config": {"workload": "C4: %d GCounter op files (%d actors x %d versions), plaintext "
+                               "log-uniform on [256 B, 1 MiB], %.2f GB" % (n, m, V, ct / 1e9),
+                   "files_single_page": int((np.array(pt_len) <= 4096).sum()),
+                   "dots": int(kd.sum())},
+        "aead_GBps_end_to_end": round(ct / (ms / 1e3) / 1e9, 1),
+        "kernels_ms_per_step": k_ms,
+        "checks": {"closed_form_state": ok},
+    }
+    print(json.dumps(line), flush=True)
+    core.close()
+
+
+def run_c5(args, ctx, dev):
+    sys.path.insert(0, REPO)
+    import bench
+    actors = bench.actors_table()
+    key1 = bytes(np.random.default_rng(8).integers(0, 256, 32, dtype=np.uint8))
+    V = args.c5_versions
+    ev, od = np.ascontiguousarray(actors[0::2]), np.ascontiguousarray(actors[1::2])
+    t0 = time.time()
+    f0, o0, n0, l0 = bench.build_files(ctx, KEY, ev, V, dev, seed=1234)
+    f1, o1, n1, l1 = bench.build_files(ctx, KEY if args.c5_clean else key1, od, V, dev, seed=1235)
+    n = n0 + n1
+    files = torch.cat([f0[:l0], f1[:l1], torch.zeros(64, dtype=torch.uint8, device=dev)])
+    del f0, f1
+    offs = torch.cat([o0[:n0], o1 + l0])
+    blob_len = l0 + l1
+    flen = l0 // n0
+    # 0.1% of all files (either key) get one flipped tag bit
+    rng = np.random.default_rng(506)
+    tam = np.sort(rng.choice(n, size=0 if args.c5_clean else n // 1000, replace=False))
+    pos = torch.from_numpy((tam + 1) * flen - 1).to(dev)
+    files[pos] ^= 1
+    writers = np.concatenate([ev, od])
+    m = writers.shape[0]
+    fa = torch.from_numpy(np.repeat(np.arange(m, dtype=np.int32), V)).to(dev)
+    fv = torch.from_numpy(np.tile(np.arange(V, dtype=np.int64), m)).to(dev)
+    want = np.zeros(n, np.int32)
+    want[n0:] = 0 if args.c5_clean else 9
+    want[tam] = 9
+    log("c5: %d files (%d under the second key, %d tampered) in %.1f s" % (n, n1, len(tam), time.time() - t0))
+    core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+    core.set_latest_key(KEY)
+    wr = b"".join(bytes(a) for a in writers)
+    empty = core.state_bytes()
+
+    def step(status=False):
+        core.reset()
+        return core.ingest_ops_device(files.data_ptr(), offs.data_ptr(), n, blob_len, wr,
+                                      fa.data_ptr(), fv.data_ptr(), want_status=status)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ctx.timing_reset()
+    ctx.set_timing(True)
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        rc = step()   # the batch verdict; the per-file statuses are fetched either way
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t) * 1e3 / args.steps
+    ctx.set_timing(False)
+    k_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in
+            ((k, ctx.timing(k)) for k in ("open_setup", "gate", "open_fold_small")) if v[1]}
+    rc2, st = step(status=True)  # untimed: the statuses as a Python list for the check
+    st = np.array(st, np.int32)
+    checks = {"batch_rejected": (rc == 9 and rc2 == 9) != args.c5_clean, "statuses_match": bool((st == want).all()),
+              "state_unchanged": (core.state_bytes() == empty) != args.c5_clean}
+    line = {
+        "metric": "C5 key-rotation mix: op files verified/sec on the reject path",
+        "value": round(n / (ms / 1e3), 1), "unit": "files/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+        "higher_is_better": True, "dtype": "u32", "data": "synthetic (GPU-sealed, seeded)",
+        "config": {"workload": "C5: %d x 4 KiB GCounter op files, 4096 actors; odd actors' files under "
+                               "a second data key, %d files with a flipped tag bit; latest key only"
+                               % (n, len(tam)),
+                   "rejected": int((want != 0).sum())},
+        "aead_open_GBps": round(n * bench.PT_LEN / (k_ms["open_fold_small"] / 1e3) / 1e9, 1)
+        if k_ms.get("open_fold_small") else None,
+        "kernels_ms_per_step": k_ms,
+        "checks": checks,
+    }
+    print(json.dumps(line), flush=True)
+    core.close()
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="c3", choices=["c3"])
+    ap.add_argument("--config", default="c3", choices=["c3", "c4", "c5"])
+    ap.add_argument("--c4-versions", type=int, default=32, help="C4 versions per actor (1024 actors)")
+    ap.add_argument("--c5-versions", type=int, default=256, help="C5 versions per actor (4096 actors)")
+    ap.add_argument("--c5-clean", action="store_true",
+                    help="C5 control: every file under the latest key, none tampered (accept path)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--versions", type=int, default=16, help="op-file versions per actor")
@@ -290,7 +488,7 @@ def main():
     torch.cuda.set_stream(stream)
     ctx = crdtenc.Context(0)
     ctx.set_stream(stream.cuda_stream)
-    run_c3(args, ctx, dev)
+    {"c3": run_c3, "c4": run_c4, "c5": run_c5}[args.config](args, ctx, dev)
     ctx.close()
 
 

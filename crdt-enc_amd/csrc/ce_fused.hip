@@ -84,6 +84,29 @@ __device__ __forceinline__ unsigned long long grp_max64(unsigned long long v) {
   if (LPF >= 64) step((uint32_t)__shfl_xor((int)(uint32_t)v, 32), (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), 32));
   return v;
 }
+// failure counters of the wave's rejected files (counters[2] += count, counters[5] = min file
+// index), accumulated wave-uniformly over the grid-stride loop and added once per wave at the
+// end (AuthFails::flush).  Same-address atomics serialise in one L2 channel: per file or even
+// per wave-iteration they cost ~1 ms when half of 1M files are rejected (C5).  The lowest set
+// lane of a ballot holds the iteration's lowest failing index (file = g * F + lane group).
+struct AuthFails {
+  uint32_t n = 0, fmin = 0xffffffffu;
+  __device__ __forceinline__ void add(bool failed, uint32_t f) {
+    const unsigned long long bm = __ballot(failed);
+    if (bm) {
+      n += (uint32_t)__builtin_popcountll(bm);
+      const uint32_t f0 = (uint32_t)__shfl((int)f, (int)__builtin_ctzll(bm));
+      fmin = f0 < fmin ? f0 : fmin;
+    }
+  }
+  __device__ __forceinline__ void flush(const DecodeArgs& a) const {
+    if (n && (threadIdx.x & 63) == 0) {
+      atomicAdd(&a.counters[2], n);
+      atomicMin(&a.counters[5], fmin);
+    }
+  }
+};
+
 // this lane's group bit of a wave ballot
 template <int LPF>
 __device__ __forceinline__ unsigned long long grp_bits(bool p, uint32_t grp) {
@@ -392,6 +415,7 @@ void k_open_fold_small(DecodeArgs a) {
   const SupVers sup(a);
   // decode state carried across files: speculated Dot length, per-lane actor cache
   DecState S{38, 0, 0, 0, 0, 0xffffffffu};
+  AuthFails fails;
 
   for (; g < ngroups; g += stride) {
     const uint32_t f = g * F + grp;
@@ -549,12 +573,9 @@ void k_open_fold_small(DecodeArgs a) {
       uint32_t tag[4];
       poly_tag(tot, sv, tag);
       tag_ok = ((tag[0] ^ tg4.x) | (tag[1] ^ tg4.y) | (tag[2] ^ tg4.z) | (tag[3] ^ tg4.w)) == 0;
-      if (!tag_ok) {
-        a.status[f] = CE_ERR_AUTH;
-        atomicAdd(&a.counters[2], 1u);
-        atomicMin(&a.counters[5], f);
-      }
+      if (!tag_ok) a.status[f] = CE_ERR_AUTH;
     }
+    fails.add(act && sub == 0 && !tag_ok, f);
     bool ok = grp_bits<LPF>(tag_ok, grp) != 0;
 
     CE_PHASE(3)
@@ -573,6 +594,7 @@ void k_open_fold_small(DecodeArgs a) {
     pc[6]++;
 #endif
   }
+  fails.flush(a);
 #undef CE_PHASE
 #if CE_FUSED_DIAG
   if (a.prof && lane == 0) {
@@ -693,6 +715,7 @@ void k_open_fold_v2(DecodeArgs a) {
   FilePre2 nx = load_pre2(a, g * F + grp);
   const SupVers sup(a);
   DecState S{38, 0, 0, 0, 0, 0xffffffffu};
+  AuthFails fails;
 
   for (; g < ngroups; g += stride) {
     const uint32_t f = g * F + grp;
@@ -872,12 +895,9 @@ void k_open_fold_v2(DecodeArgs a) {
       uint32_t tag[4];
       poly_tag(tot, sv, tag);
       tag_ok = ((tag[0] ^ tg4.x) | (tag[1] ^ tg4.y) | (tag[2] ^ tg4.z) | (tag[3] ^ tg4.w)) == 0;
-      if (!tag_ok) {
-        a.status[f] = CE_ERR_AUTH;
-        atomicAdd(&a.counters[2], 1u);
-        atomicMin(&a.counters[5], f);
-      }
+      if (!tag_ok) a.status[f] = CE_ERR_AUTH;
     }
+    fails.add(act && sub == 0 && !tag_ok, f);
     bool ok = grp_bits<LPF>(tag_ok, grp) != 0;
 #if CE_FUSED_DIAG
     if (a.ablate) ok = !(a.ablate & 1);
@@ -889,6 +909,7 @@ void k_open_fold_v2(DecodeArgs a) {
                      [&] { nx = load_pre2(a, (g + stride) * F + grp); });
     __builtin_amdgcn_wave_barrier();
   }
+  fails.flush(a);
 }
 
 template <int LPF, int W, bool JIT>

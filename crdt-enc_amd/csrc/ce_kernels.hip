@@ -106,9 +106,14 @@ __global__ __launch_bounds__(256) void k_open_setup(const uint8_t* __restrict__ 
   }
   params[f] = P;
   status[f] = st;
-  if (st == kStatusHostParse) atomicAdd(&sc.counters[7], 1u);
-  else if (st != CE_OK) {
-    atomicAdd(&sc.counters[8], 1u);
+  // counters once per wave (a batch under a wrong key fails every file: per-file atomics on
+  // these words would serialise in L2); the lowest set lane holds the wave's lowest index
+  const uint32_t lane = threadIdx.x & 63;
+  const unsigned long long hp = __ballot(st == kStatusHostParse);
+  const unsigned long long bad = __ballot(st != CE_OK && st != kStatusHostParse);
+  if (hp && lane == (uint32_t)__builtin_ctzll(hp)) atomicAdd(&sc.counters[7], (uint32_t)__builtin_popcountll(hp));
+  if (bad && lane == (uint32_t)__builtin_ctzll(bad)) {
+    atomicAdd(&sc.counters[8], (uint32_t)__builtin_popcountll(bad));
     atomicMin(&sc.counters[5], f);
   }
 }
@@ -356,53 +361,6 @@ __global__ __launch_bounds__(256) void k_finalize_multi(uint8_t* __restrict__ ou
 // ----------------------------------------------------------------------------------------
 // decode + fold: one wavefront per file
 // ----------------------------------------------------------------------------------------
-struct FoldState {
-  uint32_t slot;             // wave-uniform pending slot (0xffffffff = none)
-  unsigned long long best;   // pending max
-};
-
-__device__ __forceinline__ void fold_lane(const DecodeArgs& a, uint32_t f, bool active,
-                                          uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3,
-                                          unsigned long long ctr, FoldState& fs) {
-  uint32_t slot = 0xffffffffu;
-  if (active) {
-    slot = lookup_slot(a.table, a.mask, k0, k1, k2, k3);
-    if (slot == 0xffffffffu) {
-      const uint32_t mi = atomicAdd(&a.counters[4], 1u);
-      if (mi < a.miss_cap) a.miss_list[mi] = make_uint4(k0, k1, k2, k3);
-      a.refold[f] = 1;
-    }
-  }
-  const bool live = active && slot != 0xffffffffu;
-  // common case: every live lane folds into one slot -> one wave max, one pending update
-  const uint32_t first_live = __builtin_ctzll(__ballot(live) | (1ull << 63));
-  const uint32_t s0 = __shfl(slot, first_live);
-  const bool same = __ballot(live && slot != s0) == 0;
-  if (same && __ballot(live) != 0) {
-    unsigned long long v = live ? ctr : 0ull;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-      const unsigned long long o = __shfl_xor(v, d);
-      v = o > v ? o : v;
-    }
-    if (fs.slot != s0) {
-      if (fs.slot != 0xffffffffu && __lane_id() == 0) atomicMax(&a.batch[fs.slot], fs.best);
-      fs.slot = s0;
-      fs.best = v;
-    } else if (v > fs.best) {
-      fs.best = v;
-    }
-  } else if (live) {
-    atomicMax(&a.batch[slot], ctr);
-  }
-}
-
-__device__ __forceinline__ void fold_flush(const DecodeArgs& a, FoldState& fs) {
-  if (fs.slot != 0xffffffffu && __lane_id() == 0) atomicMax(&a.batch[fs.slot], fs.best);
-  fs.slot = 0xffffffffu;
-  fs.best = 0;
-}
-
 __global__ __launch_bounds__(256) void k_decode_dots(DecodeArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t stride = gridDim.x * kWavesPerBlock;
@@ -428,7 +386,30 @@ __global__ __launch_bounds__(256) void k_decode_dots(DecodeArgs a) {
       if (!found) st = CE_ERR_PT_VERSION;
     }
     const bool do_fold = st == CE_OK && (a.apply == nullptr || a.apply[f]);
-    FoldState fs{0xffffffffu, 0ull};
+    // per-lane fold: the last resolved actor is cached (a file's dots are mostly one actor's),
+    // the running max for the current slot stays in the lane and is flushed on a slot change;
+    // at the end of the file one wave max when every lane holds the same slot
+    uint32_t pslot = 0xffffffffu, cslot = 0xffffffffu, c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    unsigned long long pbest = 0;
+    auto fold_dot = [&](uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3, unsigned long long ctr) {
+      uint32_t slot;
+      if (cslot != 0xffffffffu && k0 == c0 && k1 == c1 && k2 == c2 && k3 == c3) slot = cslot;
+      else {
+        slot = lookup_slot(a.table, a.mask, k0, k1, k2, k3);
+        if (slot != 0xffffffffu) { c0 = k0; c1 = k1; c2 = k2; c3 = k3; cslot = slot; }
+      }
+      if (slot == 0xffffffffu) {
+        const uint32_t mi = atomicAdd(&a.counters[4], 1u);
+        if (mi < a.miss_cap) a.miss_list[mi] = make_uint4(k0, k1, k2, k3);
+        a.refold[f] = 1;
+      } else if (slot == pslot) {
+        pbest = ctr > pbest ? ctr : pbest;
+      } else {
+        if (pslot != 0xffffffffu) atomicMax(&a.batch[pslot], pbest);
+        pslot = slot;
+        pbest = ctr;
+      }
+    };
     if (st == CE_OK) {
       const uint8_t* body = pt + 16;
       const uint32_t blen = len - 16;
@@ -438,58 +419,91 @@ __global__ __launch_bounds__(256) void k_decode_dots(DecodeArgs a) {
       uint32_t pos = (uint32_t)r.i;
       uint64_t remaining = st == CE_OK ? count : 0;
       if (remaining > blen) st = CE_ERR_DECODE, remaining = 0;  // each Dot takes >= 1 byte
+      // canonical rmp-serde Dot: 82 a5"actor" c4 10 <16> a7"counter" <uint>  (33 + 1..9 bytes).
+      // A round reads 64 candidate Dots at pos + lane L.  L is speculated from the previous round
+      // (the first round's from the marker), so the next round's loads are issued before this
+      // round's fold; a round whose first Dot does not have length L re-reads the marker.
+      uint32_t L = remaining > 0 && pos + 34 <= blen ? dot_len_of_marker(body[pos + 33]) : 0;
+      uint4 A = make_uint4(0, 0, 0, 0), B = A, C = A;
+      auto load = [&](uint32_t p0, uint64_t rem) {
+        const uint32_t cand = p0 + lane * L;
+        const bool in = L != 0 && lane < rem && cand + L <= blen;
+        const uint8_t* q = body + (in ? cand : 0u);
+        A = *reinterpret_cast<const uint4*>(q);
+        B = *reinterpret_cast<const uint4*>(q + 16);
+        C = *reinterpret_cast<const uint4*>(q + 32);
+        return in;
+      };
+      bool in = load(pos, remaining);
       while (remaining > 0 && st == CE_OK) {
-        // canonical rmp-serde Dot: 82 a5"actor" c4 10 <16> a7"counter" <uint>  (33 + 1..9 bytes)
-        const uint32_t L = pos + 34 <= blen ? dot_len_of_marker(body[pos + 33]) : 0;
         bool valid = false;
         uint32_t k0 = 0, k1 = 0, k2 = 0, k3 = 0;
         unsigned long long ctr = 0;
-        if (L) {
-          const uint32_t cand = pos + lane * L;
-          if (lane < remaining && cand + L <= blen) {
-            uint32_t w[12];
-            const uint4 A = *reinterpret_cast<const uint4*>(body + cand);
-            const uint4 B = *reinterpret_cast<const uint4*>(body + cand + 16);
-            const uint4 C = *reinterpret_cast<const uint4*>(body + cand + 32);
-            w[0] = A.x; w[1] = A.y; w[2] = A.z; w[3] = A.w;
-            w[4] = B.x; w[5] = B.y; w[6] = B.z; w[7] = B.w;
-            w[8] = C.x; w[9] = C.y; w[10] = C.z; w[11] = C.w;
-            valid = canon_dot(w, L, k0, k1, k2, k3, ctr);
-          }
+        if (in) {
+          const uint32_t w[12] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w, C.x, C.y, C.z, C.w};
+          valid = canon_dot(w, L, k0, k1, k2, k3, ctr);
         }
         const unsigned long long vm = __ballot(valid);
         // leading run of valid lanes (ctz of 0 is undefined: all 64 valid -> 64)
         const uint32_t k = vm == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~vm);
         if (k > 0) {
-          if (do_fold) fold_lane(a, f, lane < k, k0, k1, k2, k3, ctr, fs);
           pos += k * L;
           remaining -= k;
-        } else {
-          // general grammar for one element (lane 0), e.g. reordered keys / array form
-          int ok = 0;
-          uint32_t g0 = 0, g1 = 0, g2 = 0, g3 = 0;
-          unsigned long long gc = 0;
-          uint32_t npos = pos;
-          if (lane == 0) {
-            Rd q{body, blen, pos};
-            uint64_t aoff = 0, c = 0;
-            ok = parse_dot(q, &aoff, &c);
-            if (ok == 1) {
-              g0 = ld_le32(body + aoff); g1 = ld_le32(body + aoff + 4);
-              g2 = ld_le32(body + aoff + 8); g3 = ld_le32(body + aoff + 12);
-              gc = c;
-              npos = (uint32_t)q.i;
-            }
+          const bool me = lane < k;
+          in = load(pos, remaining);  // next round in flight while this one folds
+          if (do_fold && me) fold_dot(k0, k1, k2, k3, ctr);
+          continue;
+        }
+        const uint32_t L2 = pos + 34 <= blen ? dot_len_of_marker(body[pos + 33]) : 0;
+        if (L2 != 0 && L2 != L) {  // the Dot length changed: the same position, the new length
+          L = L2;
+          in = load(pos, remaining);
+          continue;
+        }
+        // general grammar for one element (lane 0), e.g. reordered keys / array form
+        int ok = 0;
+        uint32_t g0 = 0, g1 = 0, g2 = 0, g3 = 0;
+        unsigned long long gc = 0;
+        uint32_t npos = pos;
+        if (lane == 0) {
+          Rd q{body, blen, pos};
+          uint64_t aoff = 0, c = 0;
+          ok = parse_dot(q, &aoff, &c);
+          if (ok == 1) {
+            g0 = ld_le32(body + aoff); g1 = ld_le32(body + aoff + 4);
+            g2 = ld_le32(body + aoff + 8); g3 = ld_le32(body + aoff + 12);
+            gc = c;
+            npos = (uint32_t)q.i;
           }
-          ok = __shfl(ok, 0);
-          if (ok != 1) { st = CE_ERR_DECODE; break; }
-          npos = bcast(npos);
-          if (do_fold) fold_lane(a, f, lane == 0, g0, g1, g2, g3, gc, fs);
-          pos = npos;
-          remaining -= 1;
+        }
+        ok = __shfl(ok, 0);
+        if (ok != 1) { st = CE_ERR_DECODE; break; }
+        npos = bcast(npos);
+        if (do_fold && lane == 0) fold_dot(g0, g1, g2, g3, gc);
+        pos = npos;
+        remaining -= 1;
+        L = remaining > 0 && pos + 34 <= blen ? dot_len_of_marker(body[pos + 33]) : 0;
+        in = load(pos, remaining);
+      }
+      if (do_fold) {  // flush: one atomicMax per file when the lanes' pending slots agree
+        const uint32_t hi = pslot == 0xffffffffu ? 0u : pslot + 1;
+        const uint32_t lo = pslot == 0xffffffffu ? 0xffffffffu : pslot + 1;
+        uint32_t mx = hi, mn = lo;
+        unsigned long long b = pslot == 0xffffffffu ? 0ull : pbest;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+          const uint32_t omx = (uint32_t)__shfl_xor((int)mx, d), omn = (uint32_t)__shfl_xor((int)mn, d);
+          const unsigned long long ob = __shfl_xor(b, d);
+          mx = omx > mx ? omx : mx;
+          mn = omn < mn ? omn : mn;
+          b = ob > b ? ob : b;
+        }
+        if (mx != 0 && mn == mx) {
+          if (lane == 0) atomicMax(&a.batch[mx - 1], b);
+        } else if (pslot != 0xffffffffu) {
+          atomicMax(&a.batch[pslot], pbest);
         }
       }
-      if (do_fold) fold_flush(a, fs);
     }
     if (st != CE_OK && lane == 0) {
       a.status[f] = st;

@@ -33,3 +33,16 @@ def test_c3_plaintexts_decode():
             vv = vi - 1 if vi else vi
             assert kind == "Rm" and clock.dots == {bytes(actors[ai]): vv * B.N_ADD + jv + 1}
             assert ms == [int(B.member_of(torch.tensor(ai), torch.tensor(vv), torch.tensor(jv)))]
+
+
+def test_c4_plaintexts_decode():
+    """C4's Vec<Dot> plaintexts: rmp-serde's smallest array header at every size class, the
+    actor's UUID and consecutive counters (checked with msgpack, CPU only)."""
+    import msgpack
+    import numpy as np
+    u = np.arange(16, dtype=np.uint8)
+    for k in (1, 15, 16, 300, 65535, 65536):
+        pt = B.dots_plaintext(u, k, 65536 + 7)
+        assert pt[:16] == B.APP
+        want = [{"actor": bytes(range(16)), "counter": 65536 + 7 + i + 1} for i in range(k)]
+        assert msgpack.packb(want, use_bin_type=True) == pt[16:]
