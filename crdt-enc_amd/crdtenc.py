@@ -410,7 +410,7 @@ class Core:
         st = (ctypes.c_int32 * max(n, 1))() if want_status else None
         rc = lib().ce_core_ingest_ops_device(
             self.p, ctypes.c_void_p(d_blob), ctypes.c_void_p(d_offs), ctypes.c_uint32(n),
-            ctypes.c_uint64(blob_len), _cbuf(actors), ctypes.c_uint32(len(actors) // 16),
+            ctypes.c_uint64(blob_len), _ptr(actors)[0], ctypes.c_uint32(len(actors) // 16),
             ctypes.c_void_p(d_file_actor), ctypes.c_void_p(d_file_version), st)
         return (rc, list(st)[:n]) if want_status else rc
 
@@ -422,7 +422,7 @@ class Core:
         nm = ctypes.create_string_buffer(64) if name else None
         rc = lib().ce_core_compact_ops_device(
             self.p, ctypes.c_void_p(d_blob), ctypes.c_void_p(d_offs), ctypes.c_uint32(n),
-            ctypes.c_uint64(blob_len), _cbuf(actors), ctypes.c_uint32(len(actors) // 16),
+            ctypes.c_uint64(blob_len), _ptr(actors)[0], ctypes.c_uint32(len(actors) // 16),
             ctypes.c_void_p(d_file_actor), ctypes.c_void_p(d_file_version),
             _cbuf(nonce) if nonce is not None else None, ctypes.byref(b), nm)
         if rc:
