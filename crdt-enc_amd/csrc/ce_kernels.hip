@@ -26,14 +26,18 @@ __global__ __launch_bounds__(256) void k_open_setup(const uint8_t* __restrict__ 
                                                     int outer, DevKey key, int32_t key_status,
                                                     FileParams* __restrict__ params,
                                                     int32_t* __restrict__ status, SegScratch sc) {
+  // parameters are staged in LDS, 128 B per lane per half (16-B columns XOR-swizzled by the
+  // lane), and stored as the block's contiguous rows: a per-lane 256-B struct store touches 64
+  // lines per instruction.  32 KiB keeps 5 workgroups per CU.
+  __shared__ uint4 stage[256 * 8];
   const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= n) return;
-  const uint64_t off = offs[f];
-  const uint64_t flen = offs[f + 1] - off;
+  const bool active = f < n;
+  const uint64_t off = active ? offs[f] : 0;
+  const uint64_t flen = active ? offs[f + 1] - off : 0;
   const uint8_t* enc = blob + off;
   uint64_t enc_len = flen;
-  int32_t st = CE_OK;
-  if (outer) {
+  int32_t st = active ? CE_OK : CE_ERR_OUTER_LEN;
+  if (active && outer) {
     // Storage: VersionBytes::deserialize (tokio lib.rs:241), then the core's
     // ensure_versions_phf(SUPPORTED_VERSIONS) (crdt-enc/src/lib.rs:501)
     if (flen < 16) st = CE_ERR_OUTER_LEN;
@@ -104,13 +108,32 @@ __global__ __launch_bounds__(256) void k_open_setup(const uint8_t* __restrict__ 
     reserve_segments(P, f, sc);
     if (P.len > kSmallMax) sc.large_list[atomicAdd(&sc.counters[9], 1u)] = f;
   }
-  params[f] = P;
+  {
+    const uint4* pv = reinterpret_cast<const uint4*>(&P);
+    const uint32_t f0 = blockIdx.x * blockDim.x;
+    const uint32_t nrow = min(n - f0, (uint32_t)blockDim.x);
+    uint4* dstp = reinterpret_cast<uint4*>(params + f0);
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      if (h) __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 8; i++) stage[threadIdx.x * 8 + (i ^ (threadIdx.x & 7))] = pv[8 * h + i];
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint32_t j = threadIdx.x + 256u * k;
+        const uint32_t row = j >> 3, col = j & 7;
+        if (row < nrow) dstp[row * 16 + 8 * h + col] = stage[row * 8 + (col ^ (row & 7))];
+      }
+    }
+  }
+  if (!active) return;
   status[f] = st;
   // counters once per wave (a batch under a wrong key fails every file: per-file atomics on
   // these words would serialise in L2); the lowest set lane holds the wave's lowest index
   const uint32_t lane = threadIdx.x & 63;
-  const unsigned long long hp = __ballot(st == kStatusHostParse);
-  const unsigned long long bad = __ballot(st != CE_OK && st != kStatusHostParse);
+  const unsigned long long hp = __ballot(active && st == kStatusHostParse);
+  const unsigned long long bad = __ballot(active && st != CE_OK && st != kStatusHostParse);
   if (hp && lane == (uint32_t)__builtin_ctzll(hp)) atomicAdd(&sc.counters[7], (uint32_t)__builtin_popcountll(hp));
   if (bad && lane == (uint32_t)__builtin_ctzll(bad)) {
     atomicAdd(&sc.counters[8], (uint32_t)__builtin_popcountll(bad));
