@@ -331,13 +331,13 @@ __global__ __launch_bounds__(256) void k_segments(const uint8_t* __restrict__ in
 }
 
 // ----------------------------------------------------------------------------------------
-// multi-segment finalize: one lane per multi-segment file (grid-stride)
+// multi-segment finalize: one wavefront per multi-segment file (grid-stride)
 // ----------------------------------------------------------------------------------------
+// r^e for any 32-bit e, from r^(2^k) (k <= 6) and further squarings
 __device__ L5 rpow_any(const FileParams& P, uint32_t e) {
-  // r^e, 1 <= e <= 1024, from r^(2^k) (k <= 6) and further squarings
   L5 acc = {{1, 0, 0, 0, 0}};
   L5 p = load_l5(P.rpow[0]);
-  for (int k = 0; k < 11; k++) {
+  for (int k = 0; k < 32 && (e >> k) != 0; k++) {
     if (k <= 6) p = load_l5(P.rpow[k]);
     else p = mulmod(p, p);
     if (e & (1u << k)) acc = mulmod(acc, p);
@@ -345,37 +345,58 @@ __device__ L5 rpow_any(const FileParams& P, uint32_t e) {
   return acc;
 }
 
+// The segment partials combine as Horner, acc = acc * r^(blocks of segment j) + p_j, which is
+// the sum of p_j * r^(blocks after segment j): lane j takes segment j's term (64 segments a
+// round), and a butterfly sums the wave, so a 1 MiB file is not a 65-step dependent chain.
 template <bool SEAL>
 __global__ __launch_bounds__(256) void k_finalize_multi(uint8_t* __restrict__ out,
                                                         const FileParams* __restrict__ params,
                                                         int32_t* __restrict__ status,
                                                         SegScratch sc) {
   const uint32_t nm = sc.counters[1];
-  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nm; t += gridDim.x * blockDim.x) {
-    const uint32_t f = sc.multi_files[t];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t stride = gridDim.x * kWavesPerBlock;
+  for (uint32_t t = bcast(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)); t < nm; t += stride) {
+    const uint32_t f = bcast(sc.multi_files[t]);
     const FileParams& P = params[f];
-    const uint32_t nblk = ((P.len + 15) >> 4) + 1;
-    const L5 rseg = rpow_any(P, kSegBlocks);
-    L5 acc = load_l5(sc.partials + 5ull * P.extra_base);
-    for (uint32_t j = 1; j < P.nseg; j++) {
-      const uint32_t nb = min(nblk - j * kSegBlocks, kSegBlocks);
-      const L5 rj = nb == kSegBlocks ? rseg : rpow_any(P, nb);
-      acc = carry5(add5(mulmod(acc, rj), load_l5(sc.partials + 5ull * (P.extra_base + j))));
+    const uint32_t len = P.len, nseg = P.nseg, base = P.extra_base;
+    const uint32_t nblk = ((len + 15) >> 4) + 1;
+    L5 sum = {{0, 0, 0, 0, 0}};
+    for (uint32_t j0 = 0; j0 < nseg; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      if (j < nseg) {
+        const uint32_t through = min((j + 1) * kSegBlocks, nblk);
+        const L5 pj = load_l5(sc.partials + 5ull * (base + j));
+        sum = carry5(add5(sum, mulmod(pj, rpow_any(P, nblk - through))));
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      L5 o;
+#pragma unroll
+      for (int i = 0; i < 5; i++) o.v[i] = __shfl_xor(sum.v[i], 1 << k);
+      sum = carry5(add5(sum, o));
     }
     uint32_t tag[4];
     const uint32_t sv[4] = {P.s[0], P.s[1], P.s[2], P.s[3]};
-    poly_tag(acc, sv, tag);
+    poly_tag(sum, sv, tag);
     uint8_t* dst = out + P.out_off;
     if (SEAL) {
-      for (int i = 0; i < 16; i++) dst[P.len + i] = (uint8_t)(tag[i >> 2] >> (8 * (i & 3)));
+      if (lane < 16) dst[len + lane] = (uint8_t)(tag[lane >> 2] >> (8 * (lane & 3)));
     } else {
       const bool ok = ((tag[0] ^ P.tag[0]) | (tag[1] ^ P.tag[1]) | (tag[2] ^ P.tag[2]) |
                        (tag[3] ^ P.tag[3])) == 0;
       if (!ok) {
-        for (uint32_t b = 0; b < P.len; b++) dst[b] = 0;
-        status[f] = CE_ERR_AUTH;
-        atomicAdd(&sc.counters[2], 1u);
-        atomicMin(&sc.counters[5], f);
+        // verify-before-release: scrub the plaintext (out_off is 16-byte aligned for open)
+        for (uint32_t o = lane * 16; o < len; o += 64 * 16) {
+          if (o + 16 <= len) *reinterpret_cast<uint4*>(dst + o) = make_uint4(0, 0, 0, 0);
+          else for (uint32_t q = o; q < len; q++) dst[q] = 0;
+        }
+        if (lane == 0) {
+          status[f] = CE_ERR_AUTH;
+          atomicAdd(&sc.counters[2], 1u);
+          atomicMin(&sc.counters[5], f);
+        }
       }
     }
   }
@@ -787,9 +808,9 @@ hipError_t launch_segments(hipStream_t s, bool seal, const uint8_t* in, uint8_t*
 hipError_t launch_finalize_multi(hipStream_t s, bool seal, uint8_t* out, const FileParams* params,
                                  int32_t* status, SegScratch sc) {
   if (seal)
-    hipLaunchKernelGGL(k_finalize_multi<true>, dim3(64), dim3(256), 0, s, out, params, status, sc);
+    hipLaunchKernelGGL(k_finalize_multi<true>, dim3(1024), dim3(256), 0, s, out, params, status, sc);
   else
-    hipLaunchKernelGGL(k_finalize_multi<false>, dim3(64), dim3(256), 0, s, out, params, status, sc);
+    hipLaunchKernelGGL(k_finalize_multi<false>, dim3(1024), dim3(256), 0, s, out, params, status, sc);
   return hipGetLastError();
 }
 
