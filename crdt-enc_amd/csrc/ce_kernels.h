@@ -94,6 +94,16 @@ struct DecodeArgs {
 };
 hipError_t launch_decode_dots(hipStream_t s, const DecodeArgs& a, uint32_t grid_waves);
 
+// multi-page Vec<Dot> decode split over kSplitParts waves per file (large_list order); files
+// with fewer than kSplitMinDots Dots, or whose parts do not all verify, take the one-wave path
+static constexpr uint32_t kSplitParts = 16;
+static constexpr uint32_t kSplitMinDots = 2048;
+static constexpr uint32_t kSplitDone = 0xfffffffeu;  // record 0: file decoded in one wave
+struct SplitScratch {
+  uint4* part;     // [n_large * kSplitParts] (slot + 1 | 0 none | ~0 failed, 0, max lo, max hi)
+};
+hipError_t launch_decode_split(hipStream_t s, const DecodeArgs& a, SplitScratch sp, uint32_t n_large);
+
 // fused open + decode + fold of single-page files (ce_fused.hip); files_per_wave in {1, 2, 4}
 hipError_t launch_open_fold_small(hipStream_t s, const DecodeArgs& a, int files_per_wave);
 // the same with whole ChaCha20 blocks per lane (keystream XOR in registers; ce_fused.hip

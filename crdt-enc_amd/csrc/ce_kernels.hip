@@ -405,16 +405,10 @@ __global__ __launch_bounds__(256) void k_finalize_multi(uint8_t* __restrict__ ou
 // ----------------------------------------------------------------------------------------
 // decode + fold: one wavefront per file
 // ----------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_decode_dots(DecodeArgs a) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t stride = gridDim.x * kWavesPerBlock;
-  // large_only: iterate the large-file list of the setup kernel (counters[9])
-  const uint32_t nwork = (a.large_only && !a.only) ? *((volatile uint32_t*)&a.counters[9]) : a.n;
-  for (uint32_t w = bcast(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)); w < nwork; w += stride) {
-    const uint32_t f = (a.large_only && !a.only) ? bcast(a.large_list[w]) : w;
+// one wave decodes and folds file f front to back (the general path; k_decode_split's fallback)
+__device__ void decode_file(const DecodeArgs& a, uint32_t f, uint32_t lane) {
+  {
     const FileParams* Pp = a.params + f;
-    if ((a.only && !a.only[f]) || (a.large_only && Pp->len <= kSmallMax)) continue;
-    if (a.status[f] != CE_OK) continue;
     const uint8_t* pt = a.pt + Pp->out_off;
     const uint32_t len = Pp->len;
     int32_t st = CE_OK;
@@ -553,6 +547,145 @@ __global__ __launch_bounds__(256) void k_decode_dots(DecodeArgs a) {
       a.status[f] = st;
       atomicAdd(&a.counters[3], 1u);
       atomicMin(&a.counters[5], f);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_decode_dots(DecodeArgs a) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t stride = gridDim.x * kWavesPerBlock;
+  // large_only: iterate the large-file list of the setup kernel (counters[9])
+  const uint32_t nwork = (a.large_only && !a.only) ? *((volatile uint32_t*)&a.counters[9]) : a.n;
+  for (uint32_t w = bcast(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)); w < nwork; w += stride) {
+    const uint32_t f = (a.large_only && !a.only) ? bcast(a.large_list[w]) : w;
+    const FileParams* Pp = a.params + f;
+    if ((a.only && !a.only[f]) || (a.large_only && Pp->len <= kSmallMax)) continue;
+    if (a.status[f] != CE_OK) continue;
+    decode_file(a, f, lane);
+  }
+}
+
+// Multi-page files split over kSplitParts waves (C4's 1 MiB files were one wave each: ~380
+// dependent 64-Dot rounds set the kernel's tail).  Part p takes Dots [p*D, (p+1)*D) at byte
+// pos0 + p*D*L, assuming every Dot before it is canonical with the first Dot's length L.  That
+// only holds once every part has checked its own Dots, so no part folds: each leaves one
+// (slot, max) record (its lanes must agree on one actor, no misses), and k_decode_split_apply,
+// the next launch on the stream, applies a file's records, or runs decode_file over the whole
+// file when any part failed (another Dot length, a non-canonical Dot, a second actor, a miss).
+// (A last-finisher counter in one kernel needed two device-scope fences per part: 13x slower.)
+__global__ __launch_bounds__(256) void k_decode_split(DecodeArgs a, SplitScratch sp) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t stride = gridDim.x * kWavesPerBlock;
+  const uint32_t nl = *((volatile uint32_t*)&a.counters[9]);
+  for (uint32_t item = bcast(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)); item < nl * kSplitParts;
+       item += stride) {
+    const uint32_t w = item / kSplitParts, part = item % kSplitParts;
+    const uint32_t f = bcast(a.large_list[w]);
+    const FileParams* Pp = a.params + f;
+    if (Pp->len <= kSmallMax || a.status[f] != CE_OK) continue;
+    const uint8_t* pt = a.pt + Pp->out_off;
+    const uint32_t len = Pp->len;
+    // eligibility: supported data version, array header, canonical first Dot length, enough
+    // Dots, folded (not gated off); everything else is decode_file's, on part 0
+    bool split = len >= 16 && (a.apply == nullptr || a.apply[f]);
+    uint32_t count = 0, pos0 = 0, L = 0;
+    const uint8_t* body = pt + 16;
+    const uint32_t blen = split ? len - 16 : 0;
+    if (split) {
+      const uint4 dv = *reinterpret_cast<const uint4*>(pt);
+      bool found = false;
+      for (uint32_t s = 0; s < a.n_supported; s++) {
+        const uint4 sv = *reinterpret_cast<const uint4*>(a.supported + 16 * s);
+        found |= dv.x == sv.x && dv.y == sv.y && dv.z == sv.z && dv.w == sv.w;
+      }
+      Rd r{body, blen, 0};
+      uint64_t c64 = 0;
+      split = found && rd_array_hdr(r, &c64) && c64 <= blen && c64 >= kSplitMinDots;
+      if (split) {
+        count = (uint32_t)c64;
+        pos0 = (uint32_t)r.i;
+        L = pos0 + 34 <= blen ? dot_len_of_marker(body[pos0 + 33]) : 0;
+        split = L != 0;
+      }
+    }
+    if (!split) {
+      if (part == 0) {
+        decode_file(a, f, lane);
+        if (lane == 0) sp.part[item] = make_uint4(kSplitDone, 0u, 0u, 0u);
+      }
+      continue;
+    }
+    const uint32_t D = ((count + kSplitParts - 1) / kSplitParts + 63) & ~63u;
+    const uint32_t d0 = min(part * D, count), d1 = min(d0 + D, count);
+    bool fail = false;
+    uint32_t myslot = 0xffffffffu, cslot = 0xffffffffu, c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    unsigned long long best = 0;
+    for (uint32_t i = d0; i < d1; i += 64) {
+      const uint32_t k = i + lane;
+      const uint64_t cand = pos0 + (uint64_t)k * L;
+      const bool in = k < d1 && cand + L <= blen;
+      const uint8_t* q = body + (in ? cand : 0u);
+      const uint4 A = *reinterpret_cast<const uint4*>(q);
+      const uint4 B = *reinterpret_cast<const uint4*>(q + 16);
+      const uint4 C = *reinterpret_cast<const uint4*>(q + 32);
+      uint32_t k0 = 0, k1 = 0, k2 = 0, k3 = 0;
+      unsigned long long ctr = 0;
+      bool valid = false;
+      if (in) {
+        const uint32_t wv[12] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w, C.x, C.y, C.z, C.w};
+        valid = canon_dot(wv, L, k0, k1, k2, k3, ctr);
+      }
+      if (k < d1 && !valid) fail = true;
+      if (valid) {
+        uint32_t slot;
+        if (cslot != 0xffffffffu && k0 == c0 && k1 == c1 && k2 == c2 && k3 == c3) slot = cslot;
+        else {
+          slot = lookup_slot(a.table, a.mask, k0, k1, k2, k3);
+          c0 = k0; c1 = k1; c2 = k2; c3 = k3; cslot = slot;
+        }
+        if (slot == 0xffffffffu || (myslot != 0xffffffffu && slot != myslot)) fail = true;
+        else {
+          best = (myslot == 0xffffffffu || ctr > best) ? ctr : best;
+          myslot = slot;
+        }
+      }
+    }
+    // the wave's record: one slot for all lanes (+1, 0 = no Dots) and the max counter
+    uint32_t mx = myslot == 0xffffffffu ? 0u : myslot + 1;
+    uint32_t mn = myslot == 0xffffffffu ? 0xffffffffu : myslot + 1;
+    unsigned long long bm = best;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      const uint32_t omx = (uint32_t)__shfl_xor((int)mx, d), omn = (uint32_t)__shfl_xor((int)mn, d);
+      const unsigned long long ob = __shfl_xor(bm, d);
+      mx = omx > mx ? omx : mx;
+      mn = omn < mn ? omn : mn;
+      bm = ob > bm ? ob : bm;
+    }
+    const bool wfail = __ballot(fail) != 0 || (mx != 0 && mn != mx);
+    if (lane == 0)
+      sp.part[item] = make_uint4(wfail ? 0xffffffffu : mx, 0u, (uint32_t)bm, (uint32_t)(bm >> 32));
+  }
+}
+
+// wave per large file: apply the split parts' records, or decode the file in one wave
+__global__ __launch_bounds__(256) void k_decode_split_apply(DecodeArgs a, SplitScratch sp) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t stride = gridDim.x * kWavesPerBlock;
+  const uint32_t nl = *((volatile uint32_t*)&a.counters[9]);
+  for (uint32_t w = bcast(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)); w < nl; w += stride) {
+    const uint32_t f = bcast(a.large_list[w]);
+    const FileParams* Pp = a.params + f;
+    if (Pp->len <= kSmallMax || a.status[f] != CE_OK) continue;
+    uint4 rec = make_uint4(0, 0, 0, 0);
+    if (lane < kSplitParts) rec = sp.part[(uint64_t)w * kSplitParts + lane];
+    if (bcast(rec.x) == kSplitDone) continue;  // decoded in one wave by part 0
+    const bool anyfail = __ballot(lane < kSplitParts && rec.x == 0xffffffffu) != 0;
+    if (!anyfail) {
+      if (lane < kSplitParts && rec.x != 0)
+        atomicMax(&a.batch[rec.x - 1], (unsigned long long)rec.z | ((unsigned long long)rec.w << 32));
+    } else {
+      decode_file(a, f, lane);
     }
   }
 }
@@ -818,6 +951,15 @@ hipError_t launch_decode_dots(hipStream_t s, const DecodeArgs& a, uint32_t grid_
   if (a.n == 0) return hipSuccess;
   const uint32_t blocks = (grid_waves + kWavesPerBlock - 1) / kWavesPerBlock;
   hipLaunchKernelGGL(k_decode_dots, dim3(blocks), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_decode_split(hipStream_t s, const DecodeArgs& a, SplitScratch sp, uint32_t n_large) {
+  if (n_large == 0) return hipSuccess;
+  const uint32_t waves = min(n_large * kSplitParts, 256u * 32u);
+  hipLaunchKernelGGL(k_decode_split, dim3((waves + kWavesPerBlock - 1) / kWavesPerBlock), dim3(256), 0, s, a, sp);
+  const uint32_t w2 = min(n_large, 256u * 32u);
+  hipLaunchKernelGGL(k_decode_split_apply, dim3((w2 + kWavesPerBlock - 1) / kWavesPerBlock), dim3(256), 0, s, a, sp);
   return hipGetLastError();
 }
 

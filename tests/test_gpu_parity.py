@@ -329,6 +329,48 @@ def test_skewed_sizes_multi_segment(ctx, oracle):
     assert rc == 9 and st[-1] == 9
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("split", [False, True])
+def test_split_decode_paths(ctx, oracle, monkeypatch, split):
+    """With CE_SPLIT=1, multi-page files of >= 2048 Dots go to k_decode_split (16 waves per file): uniform Dot
+    length with one actor folds from the part records; a second registered actor, an
+    unregistered actor (miss), a Dot length change in the last part and a non-canonical Dot
+    each fall back to the one-wave decode of the whole file.  State == oracle for every file."""
+    key = os.urandom(32)
+    rng = random.Random(21)
+    writer, other, stranger = rng.randbytes(16), rng.randbytes(16), rng.randbytes(16)
+    base = 1 << 20                      # uint32 counters: 38-byte Dots throughout
+
+    def dots(n, actor_of=lambda i: writer, ctr_of=lambda i: base + i):
+        return [{"actor": actor_of(i), "counter": ctr_of(i)} for i in range(n)]
+
+    bodies = [
+        dots(5000),                                                    # fast path
+        dots(3000, ctr_of=lambda i: base + 7 * i),                     # fast path, max not last
+        dots(4000, actor_of=lambda i: other if i == 3999 else writer),  # second actor, last part
+        dots(4000, actor_of=lambda i: stranger if i == 2500 else writer),  # miss
+        dots(4000, ctr_of=lambda i: 5 if i == 3998 else base + i),     # shorter Dot near the end
+        dots(2047),                                                    # below the split size
+    ]
+    clears = [APP + msgpack.packb(b, use_bin_type=True) for b in bodies]
+    # a non-canonical Dot (keys in the other order) in the middle of a uniform file
+    od = msgpack.packb({"counter": base + 1, "actor": writer}, use_bin_type=True)
+    canon = [msgpack.packb(d, use_bin_type=True) for d in dots(4000)]
+    canon[1700] = od
+    clears.append(APP + b"\xdd" + (4000).to_bytes(4, "big") + b"".join(canon))
+    n = len(clears)
+    files = [CORE + e for e in ctx.encrypt_batch(key, clears)]
+    if split:  # opt-in multi-wave decode (read per ingest call by the library)
+        monkeypatch.setenv("CE_SPLIT", "1")
+    core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+    core.set_latest_key(key)
+    rc, st = core.ingest_ops(files, [writer, other], [0] * n, list(range(n)))
+    oc = oracle.Core()
+    orc = oc.read_remote_ops(key, [APP], files, [writer] * n, list(range(n)))[0]
+    assert rc == orc == 0, (rc, orc, st)
+    assert core.state_bytes() == oc.serialize()
+
+
 # ------------------------------------------------------------------ storage end to end
 def test_storage_apply_read_compact(ctx, tmp_path, oracle):
     """Two replicas share a remote dir (syncthing-style, README.md:3-4)."""
