@@ -679,7 +679,10 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
     const int t = ctx->tbegin("decode");
     // CE_SPLIT=1: k_decode_split (measured slower on C4: 1.67 vs 1.36 ms)
     if (only || !getenv("CE_SPLIT")) {
-      if ((e = launch_decode_dots(ctx->stream, da, grid_waves_for(n)))) return ctx->hip_fail(e, "decode");
+      // counters[15]: the large-file list's pull index (k_decode_dots, large_only && !only)
+      if ((!only && (e = hipMemsetAsync(ctx->counters.as<uint32_t>() + 15, 0, 4, ctx->stream))) ||
+          (e = launch_decode_dots(ctx->stream, da, grid_waves_for(n))))
+        return ctx->hip_fail(e, "decode");
     } else {
       // every record a file's apply step reads is written by this batch's parts (no memset)
       if ((e = ctx->split.reserve((size_t)n_large * kSplitParts * 16))) return ctx->hip_fail(e, "split scratch");

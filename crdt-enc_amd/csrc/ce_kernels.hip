@@ -556,8 +556,23 @@ __global__ __launch_bounds__(256) void k_decode_dots(DecodeArgs a) {
   const uint32_t stride = gridDim.x * kWavesPerBlock;
   // large_only: iterate the large-file list of the setup kernel (counters[9])
   const uint32_t nwork = (a.large_only && !a.only) ? *((volatile uint32_t*)&a.counters[9]) : a.n;
+  if (a.large_only && !a.only) {
+    // the large-file list is pulled one file per wave (counters[15], zeroed before the launch):
+    // files run from 4 KiB to MiBs, so a static stride leaves some waves with several big ones
+    for (;;) {
+      uint32_t w = 0;
+      if (lane == 0) w = atomicAdd(&a.counters[15], 1u);
+      w = __shfl(w, 0);
+      if (w >= nwork) break;
+      const uint32_t f = bcast(a.large_list[w]);
+      const FileParams* Pp = a.params + f;
+      if (Pp->len <= kSmallMax || a.status[f] != CE_OK) continue;
+      decode_file(a, f, lane);
+    }
+    return;
+  }
   for (uint32_t w = bcast(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)); w < nwork; w += stride) {
-    const uint32_t f = (a.large_only && !a.only) ? bcast(a.large_list[w]) : w;
+    const uint32_t f = w;
     const FileParams* Pp = a.params + f;
     if ((a.only && !a.only[f]) || (a.large_only && Pp->len <= kSmallMax)) continue;
     if (a.status[f] != CE_OK) continue;
