@@ -672,7 +672,7 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
         return ctx->hip_fail(e, "segments");
       ctx->tend(t);
       t = ctx->tbegin("finalize_open");
-      if ((e = launch_finalize_multi(ctx->stream, false, ctx->out.as<uint8_t>(), da.params, da.status, sc)))
+      if ((e = launch_finalize_multi(ctx->stream, false, ctx->out.as<uint8_t>(), da.params, da.status, sc, n)))
         return ctx->hip_fail(e, "finalize");
       ctx->tend(t);
     }

@@ -141,7 +141,7 @@ int device_open(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint
     return ctx->hip_fail(e, "open segments");
   ctx->tend(t);
   t = ctx->tbegin("finalize_open");
-  if ((e = launch_finalize_multi(ctx->stream, false, d_out, P, d_status, sc)) != hipSuccess)
+  if ((e = launch_finalize_multi(ctx->stream, false, d_out, P, d_status, sc, n)) != hipSuccess)
     return ctx->hip_fail(e, "open finalize");
   ctx->tend(t);
   if (sync_counters) {
@@ -176,7 +176,7 @@ int device_seal(ce_ctx* ctx, const uint8_t* d_clear, const uint64_t* d_offs, uin
     return ctx->hip_fail(e, "seal segments");
   ctx->tend(t);
   t = ctx->tbegin("finalize_seal");
-  if ((e = launch_finalize_multi(ctx->stream, true, d_out, P, ctx->status.as<int32_t>(), sc)) !=
+  if ((e = launch_finalize_multi(ctx->stream, true, d_out, P, ctx->status.as<int32_t>(), sc, n)) !=
       hipSuccess)
     return ctx->hip_fail(e, "seal finalize");
   ctx->tend(t);

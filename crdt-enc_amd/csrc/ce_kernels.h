@@ -63,9 +63,10 @@ hipError_t launch_seal_setup(hipStream_t s, const uint8_t* clear, const uint64_t
 hipError_t launch_segments(hipStream_t s, bool seal, const uint8_t* in, uint8_t* out,
                            const FileParams* params, uint32_t n, int32_t* status, SegScratch sc,
                            uint32_t grid_waves, bool skip_small = false);
-// multi-segment files: combine partial Poly1305 sums, emit/compare tag (one lane per file).
+// multi-segment files: combine partial Poly1305 sums, emit/compare tag (one wave per file);
+// n = files in the batch (bounds the multi-segment count, sizes the grid)
 hipError_t launch_finalize_multi(hipStream_t s, bool seal, uint8_t* out, const FileParams* params,
-                                 int32_t* status, SegScratch sc);
+                                 int32_t* status, SegScratch sc, uint32_t n);
 
 // decode Vec<Dot<Uuid>> of every opened file and max-fold the dots of applied files into
 // batch_counters (dense by actor slot).  One wavefront per file.

@@ -954,11 +954,13 @@ hipError_t launch_segments(hipStream_t s, bool seal, const uint8_t* in, uint8_t*
 }
 
 hipError_t launch_finalize_multi(hipStream_t s, bool seal, uint8_t* out, const FileParams* params,
-                                 int32_t* status, SegScratch sc) {
+                                 int32_t* status, SegScratch sc, uint32_t n) {
+  if (n == 0) return hipSuccess;
+  const uint32_t blocks = min((n + kWavesPerBlock - 1) / kWavesPerBlock, 1024u);
   if (seal)
-    hipLaunchKernelGGL(k_finalize_multi<true>, dim3(1024), dim3(256), 0, s, out, params, status, sc);
+    hipLaunchKernelGGL(k_finalize_multi<true>, dim3(blocks), dim3(256), 0, s, out, params, status, sc);
   else
-    hipLaunchKernelGGL(k_finalize_multi<false>, dim3(1024), dim3(256), 0, s, out, params, status, sc);
+    hipLaunchKernelGGL(k_finalize_multi<false>, dim3(blocks), dim3(256), 0, s, out, params, status, sc);
   return hipGetLastError();
 }
 
