@@ -330,6 +330,38 @@ def test_skewed_sizes_multi_segment(ctx, oracle):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [255, 256, 257, 769])
+def test_setup_block_tails(ctx, oracle, n):
+    """k_open_setup stages each 256-file block's FileParams through LDS and stores the rows
+    that exist: batches around the block size, a tampered file and a wrong-version file in the
+    last (partial) block, state and every status == oracle."""
+    key = os.urandom(32)
+    rng = random.Random(n)
+    actors = [rng.randbytes(16) for _ in range(7)]
+    fa = sorted(i % 7 for i in range(n))          # Storage::load_ops order: actor, then version
+    ver = [fa[:i].count(fa[i]) for i in range(n)]
+    clears = []
+    for i in range(n):
+        a = actors[fa[i]]
+        clears.append(APP + msgpack.packb([{"actor": a, "counter": 1 + i * 3 + k} for k in range(1 + i % 5)],
+                                          use_bin_type=True))
+    files = [CORE + e for e in ctx.encrypt_batch(key, clears)]
+    bad = bytearray(files[n - 1])
+    bad[-5] ^= 1                                   # tag of the very last file
+    files[n - 1] = bytes(bad)
+    files[n - 2] = b"\x00" * 16 + files[n - 2][16:]  # outer version of the one before
+    core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+    core.set_latest_key(key)
+    rc, st = core.ingest_ops(files, actors, fa, ver)
+    oc = oracle.Core()
+    orc = oc.read_remote_ops(key, [APP], files, [actors[i] for i in fa], ver)
+    assert rc == orc[0] and rc != 0
+    assert st[n - 1] != 0 and st[n - 2] != 0 and all(x == 0 for x in st[:n - 2])
+    assert st == orc[1]
+    assert core.state_bytes() == oc.serialize()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("split", [False, True])
 def test_split_decode_paths(ctx, oracle, monkeypatch, split):
     """With CE_SPLIT=1, multi-page files of >= 2048 Dots go to k_decode_split (16 waves per file): uniform Dot
