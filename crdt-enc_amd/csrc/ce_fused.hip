@@ -842,11 +842,18 @@ void k_open_fold_v2(DecodeArgs a) {
         // every block but slot 0 is full: acc r^(4 LPF) + m0 r^3 + m1 r^2 + m2 r + m3 as four
         // products into one set of column sums, carried once (vs four Horner mulmods)
         uint64_t d[5] = {mj[3].v[0], mj[3].v[1], mj[3].v[2], mj[3].v[3], mj[3].v[4]};
-        mac5(d, acc, MC);
-        mac5(d, mj[0], M3);
-        mac5(d, mj[1], M2);
-        mac5(d, mj[2], M1);
-        an = reduce5(d);
+#if CE_FUSED_DIAG
+        if (a.ablate & 2) {
+          an = add5(add5(acc, mj[0]), add5(add5(mj[1], mj[2]), mj[3]));
+        } else
+#endif
+        {
+          mac5(d, acc, MC);
+          mac5(d, mj[0], M3);
+          mac5(d, mj[1], M2);
+          mac5(d, mj[2], M1);
+          an = reduce5(d);
+        }
       } else {
         an = add5(mulmod(acc, RC), G);
       }

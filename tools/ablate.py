@@ -10,5 +10,10 @@ def patched(self, *a, **k):
     orig(self, *a, **k)
     return 0
 crdtenc.Core.ingest_ops_device = patched
+orig_c = crdtenc.Core.compact_ops_device
+def patched_c(self, *a, **k):
+    orig_c(self, *a, **k)
+    return 0, b"", None
+crdtenc.Core.compact_ops_device = patched_c
 crdtenc.Core.state_bytes = lambda self: b""
 bench.main()
