@@ -20,7 +20,7 @@ PROF_LIB   := $(PKG)/libcrdtenc_prof.so
 PROF_OBJS  := $(patsubst $(CSRC)/%.hip,$(PKG)/build_prof/%.o,$(HIP_SRCS)) \
               $(patsubst $(CSRC)/%.cpp,$(PKG)/build_prof/%.o,$(CPP_SRCS))
 
-HIPFLAGS   := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -I$(CSRC) -Wall -Wno-unused-function
+HIPFLAGS   := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -mllvm -pragma-unroll-threshold=1000000 -Iinclude -I$(CSRC) -Wall -Wno-unused-function
 CXXFLAGS   := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Xarch_host -march=x86-64-v3 -Iinclude -I$(CSRC) -Wall -Wno-unused-function
 
 all: product oracle

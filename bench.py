@@ -7,18 +7,26 @@ max-fold (read_remote_ops, lib.rs:471-547), StateWrapper serialization, GPU seal
 state and its SHA3-256/BASE32 content name.  The core is reset to the empty state before each
 step so every step folds all files.
 
-Workload per GPU (weak scaling): 1,048,576 op files from this rank's actor shard; plaintext =
-APP_VERSION(16) || msgpack(Vec<Dot>) with 107 Dots (4085 B, "4 KiB"); actor a's file v holds
-its own increments (variant A).  The global job at N GPUs has 4096 actors x 256*N versions,
-sharded by actor (all versions of an actor on one rank, as the version gate needs); the per-rank
-partial GCounters meet in one RCCL all_reduce(MAX) over the dense actor-indexed state.
+Workload per GPU (weak scaling): 1,048,576 op files from this rank's actor shard.
+  Variant A (the headline, SURVEY.md ยง8d "semantic"): plaintext = APP_VERSION(16) ||
+    msgpack(Vec<Dot>) with 107 Dots (4085 B, "4 KiB"); actor a's file v holds its own increments.
+  Variant B (ยง8d "stress", reported as the line's `variant_b` key): 97 Dots per file whose
+    actors are uniform over all 4096 actors and whose counters are uniform u64 (4093 B), so
+    every Dot takes the actor-table probe and most take an atomicMax.
+The global job at N GPUs has 4096 actors x 256*N versions, sharded by actor (all versions of an
+actor on one rank, as the version gate needs); the per-rank partial GCounters meet in one RCCL
+all_reduce(MAX) over the dense actor-indexed state (shard.exchange_vclock).
 
-Prints ONE JSON line (rank 0).
+`--gpus N` without a launcher starts N rank processes itself (the parent never touches the GPU);
+under torch.distributed.run WORLD_SIZE must equal --gpus.  Prints ONE JSON line (rank 0) and
+exits non-zero if any size-independent result check fails.
 """
 import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,15 +43,20 @@ METRIC = ("op files compacted/sec + AEAD-open GB/s, 1Mร4KiB ops/4096 actors, 1โ
 APP = bytes.fromhex("aadfd5a66e194b24a8024fa27c72f20c")      # examples/test/src/main.rs:7
 CORE = crdtenc.CORE_VERSION
 N_ACTORS = 4096
-K_DOTS = 107                       # 16 + 3 + 107 * 38 = 4085 B of plaintext
-PT_LEN = 16 + 3 + 38 * K_DOTS
+K_DOTS = {"a": 107, "b": 97}       # 16 + 3 + 107 * 38 = 4085 B;  16 + 3 + 97 * 42 = 4093 B
+DOT_LEN = {"a": 38, "b": 42}       # counter as uint32 (ce) / uint64 (cf)
 HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md chip table (spec)
-VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # 256 CU x 4 SIMD32 x 2.4 GHz = 78.6 T int32 lane-ops/s
-# measured ceiling of the int32 ARX stream itself: tools/ubench_chacha (pure ChaCha20 blocks,
-# 8 waves/SIMD) reaches 2.55 TB/s of keystream = 39.8 G blocks/s x 976 ops = 38.9 T lane-ops/s,
-# i.e. wave64 int32 VALU instructions issue once per ~4 cycles per SIMD, not every 2
-# (profiles/r01_ubench_chacha.txt)
-VALU_INT32_MEASURED_TOPS = 38.9
+# int32 VALU lane-op peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (a wave64 full-rate VALU
+# instruction every 2 cycles per SIMD, MI355X_MICROARCH.md:54,473)
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+# Measured issue ceilings on one MI355X (tools/ubench_valu.hip, tools/ubench_chacha.hip;
+# profiles/r02_ubench_valu.txt, profiles/r02_ubench_chacha.txt, in-kernel clock 2.38-2.40 GHz):
+#   v_add/v_xor/v_and/v_bitop3/v_fma_f32: 2 cycles per wave64 instruction (63-69 T lane-ops/s);
+#   v_alignbit/v_perm/v_add3/v_xad/v_mul_lo and the SDWA forms: 4 cycles (~37 T);
+#   v_mad_u64_u32: 4 cycles (34 T at 8 waves/SIMD);
+#   ChaCha20 (add/xor/rotate) keystream: 2.50-2.58 TB/s = ~40 T lane-ops/s of the 992-op blocks.
+CHACHA_KS_TBPS = 2.58              # best measured ChaCha20 keystream rate (sdwa rot16, 8 waves/SIMD)
+VALU_CHACHA_TOPS = CHACHA_KS_TBPS * 1e12 / 64 * 992 / 1e12   # = 40.0 T: the ARX-mix ceiling
 DEFAULT_FUSED = 2                  # ce_core.h `fused` default (CE_FUSED overrides it in both)
 
 
@@ -60,55 +73,289 @@ def actors_table(seed=0xC0FFEE):
     return a[order]
 
 
-def build_files(ctx, key, actors_local, versions, dev, seed):
-    """Seal n = len(actors_local) * versions op files on the GPU; returns (files, offs, n, len)."""
+def pt_len(variant):
+    return 16 + 3 + DOT_LEN[variant] * K_DOTS[variant]
+
+
+def build_files(ctx, key, actors_local, actors_all, versions, dev, seed, variant="a"):
+    """Seal n = len(actors_local) * versions op files on the GPU.  Returns (files, offs, n,
+    blob_len, smax): smax = the u64 max counter per global actor (variant B; int64 views with
+    the sign flipped, shard._FLIP), None for variant A (closed form)."""
     m_act = actors_local.shape[0]
     n = m_act * versions
-    file_len = 16 + crdtenc.sealed_len(PT_LEN)
+    K, L = K_DOTS[variant], DOT_LEN[variant]
+    PT = pt_len(variant)
+    file_len = 16 + crdtenc.sealed_len(PT)
     files = torch.empty(n * file_len + 64, dtype=torch.uint8, device=dev)
     offs = torch.arange(n + 1, dtype=torch.int64, device=dev) * file_len
     act = torch.from_numpy(actors_local).to(dev)
+    act_all = torch.from_numpy(actors_all).to(dev)
     pre1 = torch.tensor(list(b"\x82\xa5actor\xc4\x10"), dtype=torch.uint8, device=dev)
     pre2 = torch.tensor(list(b"\xa7counter"), dtype=torch.uint8, device=dev)
     app = torch.tensor(list(APP), dtype=torch.uint8, device=dev)
-    hdr = torch.tensor([0xdc, K_DOTS >> 8, K_DOTS & 255], dtype=torch.uint8, device=dev)
+    hdr = torch.tensor([0xdc, K >> 8, K & 255], dtype=torch.uint8, device=dev)
     gen = torch.Generator(device=dev)
     gen.manual_seed(seed)
-    kk = torch.arange(K_DOTS, dtype=torch.int64, device=dev)
+    kk = torch.arange(K, dtype=torch.int64, device=dev)
+    smax = torch.full((N_ACTORS,), shard._FLIP, dtype=torch.int64, device=dev) if variant == "b" else None
     chunk = 1 << 16
     for c0 in range(0, n, chunk):
         m = min(chunk, n - c0)
         idx = torch.arange(c0, c0 + m, dtype=torch.int64, device=dev)
         a_loc, v = idx // versions, idx % versions
-        clear = torch.empty((m, PT_LEN), dtype=torch.uint8, device=dev)
+        clear = torch.empty((m, PT), dtype=torch.uint8, device=dev)
         clear[:, :16] = app
         clear[:, 16:19] = hdr
-        dots = clear[:, 19:].view(m, K_DOTS, 38)
+        dots = clear[:, 19:].view(m, K, L)
         dots[:, :, 0:9] = pre1
-        dots[:, :, 9:25] = act[a_loc][:, None, :]
         dots[:, :, 25:33] = pre2
-        dots[:, :, 33] = 0xce                                  # uint32, big endian
-        cval = 65536 + v[:, None] * K_DOTS + kk[None, :] + 1   # actor's own increments
-        for b in range(4):
-            dots[:, :, 34 + b] = ((cval >> (8 * (3 - b))) & 255).to(torch.uint8)
-        coffs = torch.arange(m + 1, dtype=torch.int64, device=dev) * PT_LEN
+        if variant == "a":
+            dots[:, :, 9:25] = act[a_loc][:, None, :]
+            dots[:, :, 33] = 0xce                                  # uint32, big endian
+            cval = 65536 + v[:, None] * K + kk[None, :] + 1        # actor's own increments
+            for b in range(4):
+                dots[:, :, 34 + b] = ((cval >> (8 * (3 - b))) & 255).to(torch.uint8)
+        else:
+            da = torch.randint(0, N_ACTORS, (m, K), dtype=torch.int64, device=dev, generator=gen)
+            dots[:, :, 9:25] = act_all[da]
+            dots[:, :, 33] = 0xcf                                  # uint64, big endian
+            cb = torch.randint(0, 256, (m, K, 8), dtype=torch.uint8, device=dev, generator=gen)
+            cb[:, :, 0] |= 0x01                                    # >= 2^56: canonical cf form
+            dots[:, :, 34:42] = cb
+            cw = cb.to(torch.int64)
+            ctr = torch.zeros((m, K), dtype=torch.int64, device=dev)
+            for b in range(8):
+                ctr = (ctr << 8) | cw[:, :, b]
+            smax.scatter_reduce_(0, da.reshape(-1), ctr.reshape(-1) ^ shard._FLIP, reduce="amax")
+        coffs = torch.arange(m + 1, dtype=torch.int64, device=dev) * PT
         nonces = torch.randint(0, 256, (m, 24), dtype=torch.uint8, device=dev, generator=gen)
         ooffs = (idx * file_len).contiguous()
         torch.cuda.current_stream().synchronize()
         ctx.encrypt_batch_device(key, clear.data_ptr(), coffs.data_ptr(), m, nonces.data_ptr(),
                                  files.data_ptr(), ooffs.data_ptr(), outer_version=CORE)
         ctx.synchronize()
-    return files, offs, n, n * file_len
+    return files, offs, n, n * file_len, smax
 
 
-def expected_state(actors_all, versions_global):
-    """Closed form of the merged StateWrapper<GCounter> (size-independent check)."""
+def expected_state(actors_all, versions_global, variant="a", smax=None):
+    """Size-independent check: the merged StateWrapper<GCounter> in closed form (variant A) or
+    from the generator's per-actor max (variant B)."""
     import msgpack
-    top = 65536 + versions_global * K_DOTS
     nov = {bytes(a): versions_global for a in actors_all}
-    st = {bytes(a): top for a in actors_all}
+    if variant == "a":
+        top = 65536 + versions_global * K_DOTS["a"]
+        st = {bytes(a): top for a in actors_all}
+    else:
+        mx = (smax ^ shard._FLIP).cpu().numpy().view(np.uint64)
+        st = {bytes(actors_all[i]): int(mx[i]) for i in range(N_ACTORS) if mx[i]}
     return msgpack.packb({"next_op_versions": {"dots": nov}, "state": {"inner": {"dots": st}}},
                          use_bin_type=True)
+
+
+def host_cpu():
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    share = int(os.environ.get("OMP_NUM_THREADS") or avail)   # the job's CPU share (16 on the box)
+    return model, avail, max(1, min(avail, share, 256))
+
+
+def launch_ranks(args):
+    """--gpus N without torch.distributed.run: start N rank processes (this parent never
+    initialises HIP), forward rank 0's stdout, exit with the worst rank status."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env, stdout=subprocess.PIPE if r == 0 else sys.stderr))
+    out = procs[0].stdout.read()
+    rcs = [p.wait() for p in procs]
+    sys.stdout.write(out.decode())
+    sys.stdout.flush()
+    return max(rcs, key=abs)
+
+
+class Workload:
+    """One variant's sealed batch on this rank, its core and its step function."""
+
+    def __init__(self, ctx, variant, args, world, rank, dev, actors_all):
+        self.variant = variant
+        self.world, self.rank = world, rank
+        lo, hi = shard.actor_range(N_ACTORS, world, rank)
+        self.per = hi - lo
+        self.actors_local = actors_all[lo:hi]
+        self.actors_all = actors_all
+        self.versions = args.versions * world                  # weak scaling: 1M files per GPU
+        self.key = bytes(np.random.default_rng(7).integers(0, 256, 32, dtype=np.uint8))
+        t0 = time.time()
+        self.files, self.offs, self.n, self.blob_len, smax = build_files(
+            ctx, self.key, self.actors_local, actors_all, self.versions, dev,
+            seed=1234 + rank + (7919 if variant == "b" else 0), variant=variant)
+        if smax is not None and world > 1:
+            shard.all_reduce_(smax, dist.ReduceOp.MAX)   # flipped u64 -> signed max
+        self.smax = smax
+        log("rank %d: variant %s: sealed %d op files (%.2f GB) in %.1f s" % (
+            rank, variant, self.n, self.blob_len / 1e9, time.time() - t0))
+        self.core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP],
+                                 current_data_version=APP)
+        self.core.set_latest_key(self.key)
+        self.core.register_actors([bytes(a) for a in actors_all])   # same dense slots on every rank
+        cap = self.core.dense_capacity()
+        # state and next_op_versions side by side: one all_reduce(MAX) per step (latency-bound)
+        self.dense = torch.zeros(2 * cap, dtype=torch.int64, device=dev)
+        self.local_actor_bytes = b"".join(bytes(a) for a in self.actors_local)
+        self.fa = np.repeat(np.arange(self.per, dtype=np.uint32), self.versions)
+        self.fv = np.tile(np.arange(self.versions, dtype=np.uint64), self.per)
+        # per-file metadata lives in HBM with the files (what Storage::load_ops hands over)
+        self.fa_d = torch.from_numpy(self.fa.astype(np.int32)).to(dev)
+        self.fv_d = torch.from_numpy(self.fv.astype(np.int64)).to(dev)
+        self.out = {}
+        self.paths = set()
+        # The SHA3-256 content name of step i's state file (host, ~0.2 MB) is computed on a host
+        # thread while step i+1's kernels run; every name is done before the timed region ends.
+        from concurrent.futures import ThreadPoolExecutor
+        self.namer = ThreadPoolExecutor(1)
+        self.names = []
+
+    def step(self):
+        core = self.core
+        core.reset()
+        if self.world == 1:
+            # Core::compact (lib.rs:332-380): read_remote_ops + the compaction output in one call
+            rc, f, _ = core.compact_ops_device(self.files.data_ptr(), self.offs.data_ptr(), self.n,
+                                               self.blob_len, self.local_actor_bytes,
+                                               self.fa_d.data_ptr(), self.fv_d.data_ptr(), name=False)
+            if rc:
+                raise crdtenc.CeError(rc, core.ctx.last_error())
+            self.out["file"] = f
+            self.names.append(self.namer.submit(crdtenc.content_name, f))
+            return
+        rc = core.ingest_ops_device(self.files.data_ptr(), self.offs.data_ptr(), self.n,
+                                    self.blob_len, self.local_actor_bytes, self.fa_d.data_ptr(),
+                                    self.fv_d.data_ptr())
+        if rc:
+            raise crdtenc.CeError(rc, core.ctx.last_error())
+        self.paths.add(shard.exchange_vclock(core, self.dense))   # all_reduce(MAX) over RCCL
+        if self.rank == 0:
+            f, _ = core.compact_to_buffer(name=False)
+            self.out["file"] = f
+            self.names.append(self.namer.submit(crdtenc.content_name, f))
+
+    def close(self):
+        self.namer.shutdown()
+        self.core.close()
+
+    def drain_names(self):
+        for fu in self.names:
+            self.out["name"] = fu.result()
+        self.names.clear()
+
+    def run(self, ctx, steps, warmup):
+        for _ in range(warmup):
+            self.step()
+        self.drain_names()
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ctx.timing_reset()
+        ctx.set_timing(True)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            self.step()
+        self.drain_names()
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        ctx.set_timing(False)
+        ms = (t1 - t0) * 1e3 / steps
+        ms_t = torch.tensor([ms], dtype=torch.float64, device=self.dense.device)
+        if self.world > 1:
+            shard.all_reduce_(ms_t, dist.ReduceOp.MAX)
+        kern = {k: ctx.timing(k) for k in ("open_setup", "gate", "open_fold_small", "segments_open",
+                                           "finalize_open", "decode", "merge", "seal_setup",
+                                           "segments_seal", "finalize_seal")}
+        ok = True
+        if self.rank == 0:
+            sb = self.core.state_bytes()
+            ok = sb == expected_state(self.actors_all if self.world > 1 else self.actors_local,
+                                      self.versions, self.variant, self.smax)
+            if not ok:
+                log("STATE MISMATCH (variant %s)" % self.variant)
+        return float(ms_t.item()), kern, ok
+
+    def cpu_baseline(self, args):
+        """The oracle (C restatement of the reference path) on this host, both modes, over the
+        same files; each mode's serialized state must equal the GPU path's on the sample."""
+        sys.path.insert(0, REPO)
+        import oracle
+        model, avail, threads = host_cpu()
+        n, versions = self.n, self.versions
+        s = min(args.cpu_sample, n) if args.cpu_sample > 0 else n
+        s -= s % versions
+        file_len = self.blob_len // n
+        host = self.files[: s * file_len].cpu().numpy()
+        h_offs = (np.arange(s + 1, dtype=np.uint64) * file_len)
+        h_act = np.ascontiguousarray(self.actors_local[self.fa[:s]])
+        h_ver = np.ascontiguousarray(self.fv[:s])
+        # the same sample through the GPU path
+        self.core.reset()
+        rc = self.core.ingest_ops_device(self.files.data_ptr(), self.offs.data_ptr(), s,
+                                         s * file_len, b"".join(bytes(a) for a in self.actors_local[: s // versions]),
+                                         self.fa_d.data_ptr(), self.fv_d.data_ptr())
+        gpu_state = self.core.state_bytes() if rc == 0 else None
+        res = {}
+        for mode, best, th in (("best", True, threads), ("reference_shaped", False, min(16, threads))):
+            t = time.perf_counter()
+            err, ser = oracle.compact_ops_baseline(
+                oracle.STATE_GCOUNTER, self.key, APP, host.ctypes.data_as(ctypes.c_void_p),
+                h_offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                h_act.ctypes.data_as(ctypes.c_void_p),
+                h_ver.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), s, th, best=best)
+            dt = time.perf_counter() - t
+            res[mode] = {"value": round(s / dt, 1), "cores": th, "seconds": round(dt, 3),
+                         "same_state_as_gpu": err == 0 and ser == gpu_state}
+        b, r = res["best"], res["reference_shaped"]
+        return {
+            "value": b["value"], "unit": "op files/s", "cores": b["cores"], "kind": "port",
+            "sample": "%d files (%d actors x %d versions) of this workload; oracle/ce_oracle.c "
+                      "best-CPU mode: AEAD open + decode parallel over files, version gate + "
+                      "fold parallel over actors, private states merged, on %d threads; "
+                      "serialized state == GPU path: %s" % (s, s // versions, versions, b["cores"],
+                                                            b["same_state_as_gpu"]),
+            "seconds": b["seconds"], "host_cpu": model, "nproc": avail,
+            "reference_shaped": dict(r, unit="op files/s", mode="%d AEAD threads (buffered(16), "
+                                     "lib.rs:497-514), decode + fold on one thread "
+                                     "(lib.rs:516-544)" % r["cores"]),
+        }, b["same_state_as_gpu"] and r["same_state_as_gpu"]
+
+
+def kernel_summary(w, ms, kern):
+    seg_ms, seg_n = kern["open_fold_small"]
+    avg_s = seg_ms / max(seg_n, 1) / 1e3
+    PT = pt_len(w.variant)
+    n = w.n
+    ops_per_file = 992 * -(-PT // 64) + 48 * (-(-PT // 16) + 1)     # SURVEY.md ยง8d
+    valu = n * ops_per_file / avg_s / 1e12 if avg_s > 0 else 0.0
+    bytes_per_launch = n * (PT + 16)              # read ct + tag; plaintext stays in LDS
+    return {"value": round(n * w.world / (ms / 1e3), 1), "ms_per_step": round(ms, 4),
+            "avg_launch_ms": round(avg_s * 1e3, 4), "ops_per_file": ops_per_file,
+            "valu_tops": round(valu, 2), "valu_frac": round(valu / VALU_PEAK_TOPS, 4),
+            "hbm_GBps": round(bytes_per_launch / avg_s / 1e9, 1) if avg_s > 0 else None,
+            "aead_open_GBps": round(n * PT / avg_s / 1e9, 1) if avg_s > 0 else None,
+            "bytes_per_launch": bytes_per_launch,
+            "kernels_ms_per_step": {k: round(v[0] / max(v[1], 1), 4) for k, v in kern.items() if v[1]}}
 
 
 def main():
@@ -118,164 +365,63 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--versions", type=int, default=256, help="versions per actor per GPU")
     ap.add_argument("--cpu-sample", type=int, default=0,
-                    help="files in the CPU baseline sample (0 = the whole per-GPU workload, "
-                         "~5-10 s of CPU work at 16 threads)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+                    help="files in the CPU baseline sample (0 = the whole per-GPU workload)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-variant-b", action="store_true", help="skip the stress-dot variant")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # CE_BENCH_SHARE_GPU=1: every rank on device 0 (multi-rank rehearsal on a one-GPU box, with
+    # CE_DIST_BACKEND=gloo since RCCL refuses two ranks on one device)
+    dev_idx = 0 if os.environ.get("CE_BENCH_SHARE_GPU") == "1" else local
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("CE_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     if N_ACTORS % world:
         raise SystemExit("world size must divide 4096")
 
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
-    ctx = crdtenc.Context(local)
+    ctx = crdtenc.Context(dev_idx)
     ctx.set_stream(stream.cuda_stream)
-
     actors_all = actors_table()
-    lo, hi = shard.actor_range(N_ACTORS, world, rank)
-    per = hi - lo
-    actors_local = actors_all[lo:hi]
-    versions = args.versions * world                    # weak scaling: 1M files per GPU
-    key = bytes(np.random.default_rng(7).integers(0, 256, 32, dtype=np.uint8))
 
-    t0 = time.time()
-    files, offs, n, blob_len = build_files(ctx, key, actors_local, versions, dev, seed=1234 + rank)
-    log("rank %d: sealed %d op files (%.2f GB) in %.1f s" % (rank, n, blob_len / 1e9, time.time() - t0))
-
-    core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
-    core.set_latest_key(key)
-    core.register_actors([bytes(a) for a in actors_all])   # same dense slots on every rank
-    cap = core.dense_capacity()
-    # state and next_op_versions side by side: one all_reduce(MAX) per step (latency-bound)
-    dense = torch.zeros(2 * cap, dtype=torch.int64, device=dev)
-    st_t, nov_t = dense[:cap], dense[cap:]
-    local_actor_bytes = b"".join(bytes(a) for a in actors_local)
-    fa = np.repeat(np.arange(per, dtype=np.uint32), versions)
-    fv = np.tile(np.arange(versions, dtype=np.uint64), per)
-    # per-file metadata lives in HBM with the files (what Storage::load_ops hands over)
-    fa_d = torch.from_numpy(fa.astype(np.int32)).to(dev)
-    fv_d = torch.from_numpy(fv.astype(np.int64)).to(dev)
-
-    out = {}
-    # The SHA3-256 content name of step i's state file (host, ~0.2 MB) is computed on a host
-    # thread while step i+1's kernels run; every name is done before the timed region ends.
-    from concurrent.futures import ThreadPoolExecutor
-    namer = ThreadPoolExecutor(1)
-    names = []
-
-    def step():
-        core.reset()
-        if world == 1:
-            # Core::compact (lib.rs:332-380): read_remote_ops + the compaction output in one call
-            rc, f, _ = core.compact_ops_device(files.data_ptr(), offs.data_ptr(), n, blob_len,
-                                               local_actor_bytes, fa_d.data_ptr(), fv_d.data_ptr(),
-                                               name=False)
-            if rc:
-                raise crdtenc.CeError(rc, ctx.last_error())
-            out["file"] = f
-            names.append(namer.submit(crdtenc.content_name, f))
-            return
-        rc = core.ingest_ops_device(files.data_ptr(), offs.data_ptr(), n, blob_len,
-                                    local_actor_bytes, fa_d.data_ptr(), fv_d.data_ptr())
-        if rc:
-            raise crdtenc.CeError(rc, ctx.last_error())
-        if world > 1:
-            core.export_dense(st_t.data_ptr(), nov_t.data_ptr())
-            shard.merge_dense(dense)           # all_reduce(MAX) over u64
-            core.import_dense(st_t.data_ptr(), nov_t.data_ptr())
-        if rank == 0:
-            f, _ = core.compact_to_buffer(name=False)
-            out["file"] = f
-            names.append(namer.submit(crdtenc.content_name, f))
-
-    for _ in range(args.warmup):
-        step()
-    for fu in names:
-        fu.result()
-    names.clear()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ctx.timing_reset()
-    ctx.set_timing(True)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    for fu in names:
-        out["name"] = fu.result()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    ctx.set_timing(False)
-    ms = (t1 - t0) * 1e3 / args.steps
-    ms_t = torch.tensor([ms], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(ms_t, op=dist.ReduceOp.MAX)
-    ms_max = float(ms_t.item())
-
-    kern = {k: ctx.timing(k) for k in ("open_setup", "gate", "open_fold_small", "segments_open",
-                                       "finalize_open", "decode", "merge", "seal_setup",
-                                       "segments_seal", "finalize_seal")}
-
-    # size-independent correctness check of the last step's result
-    ok = True
-    if rank == 0:
-        sb = core.state_bytes()
-        ok = sb == expected_state(actors_all if world > 1 else actors_local, versions)
-        if not ok:
-            log("STATE MISMATCH vs closed form")
-
-    # CPU baseline: the oracle (C restatement of the reference path), reference-shaped:
-    # cpu_threads AEAD workers, decode + ordered fold on one thread (lib.rs:497-544)
-    cpu = None
+    wa = Workload(ctx, "a", args, world, rank, dev, actors_all)
+    ms, kern, ok = wa.run(ctx, args.steps, args.warmup)
+    sa = kernel_summary(wa, ms, kern)
+    cpu, cpu_ok = None, True
     if rank == 0 and world == 1 and not args.no_cpu:
-        sys.path.insert(0, REPO)
-        import oracle
-        s = min(args.cpu_sample, n) if args.cpu_sample > 0 else n
-        s -= s % versions
-        file_len = blob_len // n
-        host = files[: s * file_len].cpu().numpy()
-        h_offs = (np.arange(s + 1, dtype=np.uint64) * file_len)
-        h_act = np.ascontiguousarray(actors_local[fa[:s]])
-        h_ver = np.ascontiguousarray(fv[:s])
-        threads = min(args.cpu_threads, os.cpu_count() or 1)
-        t = time.perf_counter()
-        err, ser = oracle.compact_ops_baseline(
-            oracle.STATE_GCOUNTER, key, APP, host.ctypes.data_as(ctypes.c_void_p),
-            h_offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
-            h_act.ctypes.data_as(ctypes.c_void_p),
-            h_ver.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), s, threads)
-        dt = time.perf_counter() - t
-        # the same sample through the GPU path must serialize to the same bytes
-        core.reset()
-        rc = core.ingest_ops_device(files.data_ptr(), offs.data_ptr(), s, s * file_len,
-                                    b"".join(bytes(a) for a in actors_local[: s // versions]),
-                                    fa_d.data_ptr(), fv_d.data_ptr())
-        same = rc == 0 and err == 0 and core.state_bytes() == ser
-        cpu = {"value": round(s / dt, 1), "unit": "op files/s", "cores": threads, "kind": "port",
-               "sample": "%d files (%d actors x %d versions) of this workload, oracle/ce_oracle.c "
-                         "reference-shaped: %d AEAD threads, decode+fold on one thread; "
-                         "serialized state == GPU path: %s" % (s, s // versions, versions, threads, same),
-               "seconds": round(dt, 3)}
+        cpu, cpu_ok = wa.cpu_baseline(args)
+    paths_a = sorted(wa.paths)
+    wa.close()
+    del wa
+
+    vb = None
+    if not args.no_variant_b:
+        wb = Workload(ctx, "b", args, world, rank, dev, actors_all)
+        ms_b, kern_b, ok_b = wb.run(ctx, args.steps, args.warmup)
+        ok = ok and ok_b
+        sb = kernel_summary(wb, ms_b, kern_b)
+        vb = dict(sb, workload="C2 variant B (SURVEY.md ยง8d stress): 1,048,576 x 4093 B op files "
+                               "per GPU, 97 Dots each with actors uniform over 4096 and uniform "
+                               "u64 counters", dots_per_file=K_DOTS["b"],
+                  state_check="StateWrapper bytes == generator's per-actor max: %s" % ("ok" if ok_b else "MISMATCH"))
+        wb.close()
+        del wb
 
     if rank == 0:
-        # dominant kernel: the fused open+decode+fold of the 4 KiB op files
-        seg_ms, seg_n = kern["open_fold_small"]
-        avg_s = seg_ms / max(seg_n, 1) / 1e3
-        ct_bytes = n * PT_LEN
-        bytes_per_launch = n * (PT_LEN + 16)              # read ct + tag; plaintext stays in LDS
-        ops_per_file = 992 * -(-PT_LEN // 64) + 48 * (-(-PT_LEN // 16) + 1)
-        achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
-        valu = n * ops_per_file / avg_s / 1e12 if avg_s > 0 else 0.0
         fused = os.environ.get("CE_FUSED", str(DEFAULT_FUSED))
         lpf = 64 // int(os.environ.get("CE_FILES_PER_WAVE", "4"))
         kname = ("k_open_fold_v2<%d> (XChaCha20-Poly1305 open + Vec<Dot> decode + fold, "
@@ -288,31 +434,28 @@ def main():
                 rec = json.load(f)
             # only a measurement of the kernel this run used (and of the same 1M-file launch)
             if kname.split(" (")[0].rstrip(">") in rec.get("kernel", "") and \
-                    rec.get("files_per_launch") == n:
+                    rec.get("files_per_launch") == wa_n(args, world):
                 traffic = rec.get("bytes_per_launch")
-        # VALU issue from the PMC record of this kernel (SQ_INSTS_VALU x 64 lanes per file,
-        # tools/pmc_valu.sh) at this run's launch time: the kernel's binding roofline
         valu_pmc = None
-        vf = os.path.join(REPO, "profiles", "r01_valu_pmc.json")
-        if os.path.exists(vf) and avg_s > 0 and fused == "2" and lpf == 16:
+        vf = os.path.join(REPO, "profiles", "valu_pmc.json")
+        if os.path.exists(vf) and sa["avg_launch_ms"] > 0:
             with open(vf) as f:
                 rec = json.load(f).get("fused", {})
             ipf = rec.get("valu_instr_per_file_per_lane")
-            if ipf:
-                t = n * ipf / avg_s / 1e12
+            if ipf and rec.get("kernel", "") in kname:
+                t = wa_n(args, world) * ipf / (sa["avg_launch_ms"] / 1e3) / 1e12
                 valu_pmc = {"instr_per_file": ipf, "achieved_tops": round(t, 2),
-                            "frac_of_measured": round(t / VALU_INT32_MEASURED_TOPS, 4),
                             "frac_of_peak": round(t / VALU_PEAK_TOPS, 4),
-                            "source": "profiles/r01_valu_pmc.json (rocprofv3 SQ_INSTS_VALU x 64 "
-                                      "per file, same kernel and workload)"}
+                            "source": "profiles/valu_pmc.json (rocprofv3 SQ_INSTS_VALU x 64 per "
+                                      "file, same kernel and workload)"}
         line = {
             "metric": METRIC,
-            "value": round(n * world / (ms_max / 1e3), 1),
+            "value": sa["value"],
             "unit": "op files/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms_max, 4),
+            "ms_per_step": sa["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -321,34 +464,54 @@ def main():
             "config": {
                 "workload": "C2: 1,048,576 x 4 KiB encrypted GCounter op files per GPU "
                             "(4096 actors x %d versions at N=%d, actor-sharded), decrypt + "
-                            "max-join + compact" % (versions, world),
-                "files_per_gpu": n, "plaintext_bytes": PT_LEN, "file_bytes": blob_len // n,
-                "dots_per_file": K_DOTS, "actors": N_ACTORS,
-                "parallelism": "actor-sharded files, RCCL all_reduce(MAX) of dense state"
+                            "max-join + compact" % (args.versions * world, world),
+                "files_per_gpu": wa_n(args, world), "plaintext_bytes": pt_len("a"),
+                "dots_per_file": K_DOTS["a"], "actors": N_ACTORS,
+                "parallelism": ("actor-sharded files, all_reduce(MAX) of dense state (%s), "
+                                "exchange path %s" % (os.environ.get("CE_DIST_BACKEND", "nccl"),
+                                                       "/".join(paths_a)))
                                if world > 1 else "single GPU",
             },
-            "aead_open_GBps": round(ct_bytes / avg_s / 1e9, 1) if avg_s > 0 else None,
+            "aead_open_GBps": sa["aead_open_GBps"],
             "roofline": {
                 "kernel": kname,
-                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "bytes_per_launch": bytes_per_launch, "avg_launch_ms": round(avg_s * 1e3, 4),
-                "valu": {"achieved_tops": round(valu, 2), "peak_tops": round(VALU_PEAK_TOPS, 1),
-                         "frac": round(valu / VALU_PEAK_TOPS, 4),
-                         "int32_measured_peak_tops": VALU_INT32_MEASURED_TOPS,
-                         "frac_of_measured": round(valu / VALU_INT32_MEASURED_TOPS, 4),
-                         "ops_per_file": ops_per_file, "pmc_instructions": valu_pmc},
+                "bound": "valu",
+                "achieved": sa["valu_tops"], "peak": round(VALU_PEAK_TOPS, 1),
+                "unit": "T int32 lane-ops/s", "frac": sa["valu_frac"],
+                "ops_per_file": sa["ops_per_file"], "avg_launch_ms": sa["avg_launch_ms"],
+                "traffic": traffic,
+                "ops_formula": "992*ceil(ct/64) + 48*(ceil(ct/16)+1) per file (SURVEY.md ยง8d), "
+                               "x files per launch / avg launch (HIP events on the kernel's stream)",
+                "measured_chacha20_ceiling": {
+                    "tops": round(VALU_CHACHA_TOPS, 1), "keystream_TBps": CHACHA_KS_TBPS,
+                    "frac": round(sa["valu_tops"] / VALU_CHACHA_TOPS, 4),
+                    "source": "profiles/r02_ubench_chacha.txt, profiles/r02_ubench_valu.txt"},
+                "hbm": {"achieved": sa["hbm_GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round((sa["hbm_GBps"] or 0) / HBM_PEAK_GBS, 4),
+                        "bytes_per_launch": sa["bytes_per_launch"]},
+                "pmc_valu": valu_pmc,
             },
-            "kernels_ms_per_step": {k: round(v[0] / max(v[1], 1), 4) for k, v in kern.items() if v[1]},
+            "kernels_ms_per_step": sa["kernels_ms_per_step"],
             "state_check": "closed-form StateWrapper bytes: %s" % ("ok" if ok else "MISMATCH"),
+            "variant_b": vb,
             "cpu_baseline": cpu,
         }
+        if not (ok and cpu_ok):
+            line.pop("value")
+            line["error"] = "result check failed: see state_check / cpu_baseline"
         print(json.dumps(line), flush=True)
+    all_ok = torch.tensor([1 if (ok and cpu_ok) else 0], dtype=torch.int64, device=dev)
     if world > 1:
+        shard.all_reduce_(all_ok, dist.ReduceOp.MIN)
         dist.barrier()
         dist.destroy_process_group()
-    core.close()
     ctx.close()
+    if int(all_ok.item()) != 1:
+        sys.exit(3)
+
+
+def wa_n(args, world):
+    return N_ACTORS // world * args.versions * world
 
 
 if __name__ == "__main__":

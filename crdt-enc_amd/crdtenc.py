@@ -495,6 +495,10 @@ class Core:
     def dense_capacity(self):
         return lib().ce_core_dense_capacity(self.p)
 
+    def dense_ready(self):
+        """True when export/import_dense can carry the whole state (no unregistered actor)."""
+        return lib().ce_core_dense_ready(self.p) == 1
+
     def export_dense(self, d_state, d_nov):
         self.ctx.check(lib().ce_core_export_dense(self.p, ctypes.c_void_p(d_state),
                                                   ctypes.c_void_p(d_nov)), "export_dense")

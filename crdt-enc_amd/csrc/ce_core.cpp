@@ -1474,6 +1474,12 @@ int ce_core_register_actors(ce_core* c, const uint8_t* actors, uint32_t m) {
 
 uint32_t ce_core_dense_capacity(ce_core* c) { return c ? c->cap : 0; }
 
+int ce_core_dense_ready(ce_core* c) {
+  if (!c || is_dotset_kind(c->kind)) return 0;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  return c->registered == c->size ? 1 : 0;
+}
+
 int ce_core_export_dense(ce_core* c, uint64_t* d_state, uint64_t* d_nov) {
   if (!c || !d_state || !d_nov || is_dotset_kind(c->kind)) return CE_ERR_INVALID_ARG;
   std::lock_guard<std::recursive_mutex> g(c->ctx->mu);

@@ -6,7 +6,9 @@ folded its shard, the partial states meet in ONE exchange: VClock/GCounter merge
 max (crdts VClock::merge; GCounter::merge delegates to it), so the dense actor-indexed arrays
 (batch state and next_op_versions, exported with Core.export_dense over slots registered
 identically on every rank) are combined with all_reduce(MAX).  Over RCCL that is one 64 KiB
-latency-bound message per array on xGMI; with gloo it runs the same code on CPU tensors.
+latency-bound message per array on xGMI; with gloo it runs the same code on CPU tensors.  A
+Dot naming an actor outside the registered slots sends every rank to the all-gather of
+serialized partial states instead (exchange_vclock).
 
 Counters are u64 but the collective's MAX is signed int64: the sign bit is flipped before and
 after the reduce, which maps u64 order onto i64 order (values >= 2^63 stay correctly ordered).
@@ -41,6 +43,22 @@ def file_rank(actor_index, n_actors, world):
     return r
 
 
+def _host_staged(t, group=None):
+    """gloo reduces host tensors: device tensors are staged through host memory for it (the
+    CPU tests and the one-GPU multi-rank rehearsal); RCCL ("nccl") reduces them in place."""
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def all_reduce_(t, op, group=None):
+    if _host_staged(t, group):
+        h = t.cpu()
+        dist.all_reduce(h, op=op, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op, group=group)
+    return t
+
+
 def merge_dense(*tensors, group=None):
     """In place: every tensor (int64 views of u64 arrays) becomes the elementwise u64 max over
     all ranks."""
@@ -48,9 +66,33 @@ def merge_dense(*tensors, group=None):
         if t.dtype != torch.int64:
             raise TypeError("dense arrays are int64 views of u64")
         t.bitwise_xor_(_FLIP)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        all_reduce_(t, dist.ReduceOp.MAX, group=group)
         t.bitwise_xor_(_FLIP)
     return tensors
+
+
+def exchange_vclock(core, dense, group=None):
+    """Merge the partial VClock / GCounter states of all ranks into every rank's `core`.
+
+    Fast path: the dense actor-indexed arrays (state ‖ next_op_versions, `dense` = int64[2 cap]
+    on the rank's device) are exported, all_reduce(MAX)ed once and imported.  A Dot may name an
+    actor outside the registered set (VClock::apply takes any actor, crdt-enc/src/lib.rs:
+    533-535); when any rank holds one, every rank falls back to the all-gather of serialized
+    StateWrappers + merge_state (the exchange the dot-set kinds use).  The decision is itself
+    one all_reduce(MAX) of a flag, so all ranks take the same path.  Returns "dense" or "bytes".
+    """
+    flag = torch.tensor([0 if core.dense_ready() else 1], dtype=torch.int64, device=dense.device)
+    all_reduce_(flag, dist.ReduceOp.MAX, group=group)
+    if int(flag.item()) == 0:
+        cap = dense.numel() // 2
+        st, nov = dense[:cap], dense[cap:]
+        core.export_dense(st.data_ptr(), nov.data_ptr())
+        merge_dense(dense, group=group)
+        core.import_dense(st.data_ptr(), nov.data_ptr())
+        return "dense"
+    exchange_dotset(core, group=group,
+                    device="cpu" if dist.get_backend(group) == "gloo" else dense.device)
+    return "bytes"
 
 
 def max_u64_(dst, src):

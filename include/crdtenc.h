@@ -273,6 +273,11 @@ int ce_core_register_actors(ce_core *c, const uint8_t *actors, uint32_t m);
 uint32_t ce_core_dense_capacity(ce_core *c);
 int ce_core_export_dense(ce_core *c, uint64_t *d_state, uint64_t *d_nov);
 int ce_core_import_dense(ce_core *c, const uint64_t *d_state, const uint64_t *d_nov);
+/* 1 when every actor the state (or next_op_versions) holds has a registered dense slot, so
+ * export/import_dense can carry it; 0 otherwise (a Dot named an actor outside
+ * register_actors -- VClock::apply takes any actor, lib.rs:533-535).  Ranks then exchange
+ * ce_core_state_bytes + ce_core_merge_state instead (crdtenc shard.exchange_vclock). */
+int ce_core_dense_ready(ce_core *c);
 
 /* Framing helpers (crdt-enc/src/utils/version_bytes.rs): VersionBytesBuf chunk/advance. */
 typedef struct ce_vbuf {

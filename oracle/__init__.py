@@ -34,6 +34,7 @@ def lib():
         L.oc_base32_nopad.restype = S
         L.oc_open_batch_mt.restype = S
         L.oc_compact_ops_baseline.restype = S
+        L.oc_compact_ops_best.restype = S
         L.oc_vclock_get.restype = ctypes.c_uint64
         _lib = L
     return _lib
@@ -176,15 +177,17 @@ _out_buf = None
 
 
 def compact_ops_baseline(kind, key, data_version, blob, offs, file_actor, file_version,
-                         n_files, n_threads):
-    """CPU baseline over numpy/ctypes buffers (blob: bytes-like, offs: uint64[n+1])."""
+                         n_files, n_threads, best=False):
+    """CPU baseline over numpy/ctypes buffers (blob: bytes-like, offs: uint64[n+1]).
+    best=False: reference-shaped (n_threads AEAD workers, decode + fold on one thread);
+    best=True: every stage on n_threads threads (fold sharded by actor)."""
     global _out_buf
     cap = 8 << 20
     if _out_buf is None:
         _out_buf = ctypes.create_string_buffer(cap)
     out = _out_buf
     err = ctypes.c_int(0)
-    n = lib().oc_compact_ops_baseline(kind, _buf(key), _buf(data_version), blob, offs, file_actor,
-                                      file_version, ctypes.c_size_t(n_files), n_threads, out,
-                                      ctypes.c_size_t(cap), ctypes.byref(err))
+    fn = lib().oc_compact_ops_best if best else lib().oc_compact_ops_baseline
+    n = fn(kind, _buf(key), _buf(data_version), blob, offs, file_actor, file_version,
+           ctypes.c_size_t(n_files), n_threads, out, ctypes.c_size_t(cap), ctypes.byref(err))
     return err.value, out.raw[:n]

@@ -1004,3 +1004,101 @@ size_t oc_compact_ops_baseline(int kind, const uint8_t key[32], const uint8_t da
   *err = e;
   return n_out;
 }
+
+/* ---- best-CPU baseline: open/decode parallel over files, gate + fold parallel over actors -- */
+typedef struct {
+  mt_job *j;
+  const uint8_t (*file_actor)[16];
+  const uint64_t *file_version;
+  int kind, t, n_threads;
+  oc_core core;
+  int err;
+} best_fold;
+
+static uint32_t actor_owner(const uint8_t a[16], int n) {
+  uint32_t h = 2166136261u;
+  for (int i = 0; i < 16; i++) h = (h ^ a[i]) * 16777619u;
+  return h % (uint32_t)n;
+}
+
+static void *best_check_worker(void *arg) {  /* decode check (rmp_serde::from_slice, lib.rs:507) */
+  best_fold *b = (best_fold *)arg;
+  for (size_t i = (size_t)b->t; i < b->j->n; i += (size_t)b->n_threads)
+    if (b->j->status[i] == OC_OK && oc_decode_apply_dots(&b->core, b->j->pts[i], b->j->pt_lens[i], 1))
+      b->j->status[i] = OC_ERR_DECODE;
+  return NULL;
+}
+
+static void *best_fold_worker(void *arg) {   /* lib.rs:516-544 for the actors this thread owns */
+  best_fold *b = (best_fold *)arg;
+  for (size_t i = 0; i < b->j->n && !b->err; i++) {
+    if ((int)actor_owner(b->file_actor[i], b->n_threads) != b->t) continue;
+    uint64_t expected = oc_vclock_get(&b->core.next_op_versions, b->file_actor[i]);
+    if (b->file_version[i] < expected) continue;
+    if (expected < b->file_version[i]) { b->err = OC_ERR_OP_VERSION; break; }
+    oc_decode_apply_dots(&b->core, b->j->pts[i], b->j->pt_lens[i], 0);
+    oc_vclock_apply(&b->core.next_op_versions, b->file_actor[i], expected + 1);
+  }
+  return NULL;
+}
+
+size_t oc_compact_ops_best(int kind, const uint8_t key[32], const uint8_t data_version[16],
+                           const uint8_t *blob, const uint64_t *offs,
+                           const uint8_t (*file_actor)[16], const uint64_t *file_version,
+                           size_t n_files, int n_threads, uint8_t *out, size_t cap, int *err) {
+  if (n_threads < 1) n_threads = 1;
+  if (n_threads > 256) n_threads = 256;
+  mt_job j;
+  memset(&j, 0, sizeof j);
+  j.key = key; j.blob = blob; j.offs = offs; j.n = n_files; j.data_version = data_version;
+  j.status = (int32_t *)calloc(n_files ? n_files : 1, sizeof(int32_t));
+  j.pts = (uint8_t **)calloc(n_files ? n_files : 1, sizeof(uint8_t *));
+  j.pt_lens = (size_t *)calloc(n_files ? n_files : 1, sizeof(size_t));
+  mt_run(&j, n_threads);
+  best_fold *bf = (best_fold *)calloc((size_t)n_threads, sizeof(best_fold));
+  pthread_t th[256];
+  for (int t = 0; t < n_threads; t++) {
+    bf[t].j = &j; bf[t].file_actor = file_actor; bf[t].file_version = file_version;
+    bf[t].kind = kind; bf[t].t = t; bf[t].n_threads = n_threads;
+    oc_core_init(&bf[t].core, kind);
+  }
+  for (int t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, best_check_worker, &bf[t]);
+  for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+  int e = OC_OK;
+  for (size_t i = 0; i < n_files && !e; i++)
+    if (j.status[i]) e = j.status[i];
+  size_t n_out = 0;
+  oc_core c;
+  oc_core_init(&c, kind);
+  if (!e) {
+    for (int t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, best_fold_worker, &bf[t]);
+    for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+    int gap = 0;
+    for (int t = 0; t < n_threads; t++) gap |= bf[t].err;
+    if (gap) {  /* sequential fold: stop at the gap in batch order */
+      for (size_t i = 0; i < n_files; i++) {
+        uint64_t expected = oc_vclock_get(&c.next_op_versions, file_actor[i]);
+        if (file_version[i] < expected) continue;
+        if (expected < file_version[i]) { e = OC_ERR_OP_VERSION; break; }
+        oc_decode_apply_dots(&c, j.pts[i], j.pt_lens[i], 0);
+        oc_vclock_apply(&c.next_op_versions, file_actor[i], expected + 1);
+      }
+    } else {
+      for (int t = 0; t < n_threads; t++) {  /* VClock::merge of the private states */
+        for (size_t i = 0; i < bf[t].core.state.n; i++)
+          oc_vclock_apply(&c.state, bf[t].core.state.actor[i], bf[t].core.state.counter[i]);
+        for (size_t i = 0; i < bf[t].core.next_op_versions.n; i++)
+          oc_vclock_apply(&c.next_op_versions, bf[t].core.next_op_versions.actor[i],
+                          bf[t].core.next_op_versions.counter[i]);
+      }
+    }
+    if (!e) n_out = oc_core_serialize(&c, out, cap);
+  }
+  for (int t = 0; t < n_threads; t++) oc_core_free(&bf[t].core);
+  free(bf);
+  oc_core_free(&c);
+  for (size_t i = 0; i < n_files; i++) free(j.pts[i]);
+  free(j.pts); free(j.pt_lens); free(j.status);
+  *err = e;
+  return n_out;
+}

@@ -144,6 +144,17 @@ size_t oc_compact_ops_baseline(int kind, const uint8_t key[32], const uint8_t da
                                size_t n_files, int n_threads, uint8_t *out, size_t cap,
                                int *err);
 
+/* Best-CPU baseline (SURVEY.md §8d mode ii): the same result with every stage on n_threads
+ * threads -- open + decode check parallel over files, then the version gate and the fold
+ * parallel over actors (thread t folds the files of the actors it owns, in batch order, into a
+ * private StateWrapper), then the private states merged (VClock::merge, pointwise max).  A
+ * batch with a version gap is folded sequentially instead (the reference stops at the gap in
+ * batch order, lib.rs:527-531).  Returns serialized length. */
+size_t oc_compact_ops_best(int kind, const uint8_t key[32], const uint8_t data_version[16],
+                           const uint8_t *blob, const uint64_t *offs,
+                           const uint8_t (*file_actor)[16], const uint64_t *file_version,
+                           size_t n_files, int n_threads, uint8_t *out, size_t cap, int *err);
+
 #ifdef __cplusplus
 }
 #endif

@@ -156,3 +156,36 @@ def test_version_gate(oracle, repo_fx):
     ref = oracle.Core()
     rc, _ = ref.read_remote_ops(key, [H(repo_fx["data_version"])], files[:3], actors[:3], versions[:3])
     assert rc == 0 and ref.serialize() == core.serialize()
+
+
+@pytest.mark.parametrize("best", [False, True], ids=["reference_shaped", "best_cpu"])
+@pytest.mark.parametrize("kind", ["gcounter", "vclock"])
+def test_cpu_baselines_match_sequential_fold(oracle, repo_fx, kind, best):
+    """Both CPU baseline modes (bench.py cpu_baseline) serialize what the sequential
+    read_remote_ops oracle serializes: fixture files, then a version gap (fold stops there)."""
+    import ctypes
+    import numpy as np
+    key = H(repo_fx["key"])
+    dv = H(repo_fx["data_version"])
+    k = oracle.STATE_GCOUNTER if kind == "gcounter" else oracle.STATE_VCLOCK
+    fx = repo_fx["files"]
+    for drop in (None, 5):
+        sel = [i for i in range(len(fx)) if i != drop]
+        files = [H(fx[i]["file"]) for i in sel]
+        actors = [H(fx[i]["actor"]) for i in sel]
+        versions = [fx[i]["version"] for i in sel]
+        ref = oracle.Core(k)
+        rc_ref, _ = ref.read_remote_ops(key, [dv], files, actors, versions)
+        blob = np.frombuffer(b"".join(files), dtype=np.uint8).copy()
+        offs = np.cumsum([0] + [len(f) for f in files]).astype(np.uint64)
+        act = np.frombuffer(b"".join(actors), dtype=np.uint8).copy()
+        ver = np.array(versions, dtype=np.uint64)
+        for threads in (1, 3, 8):
+            err, ser = oracle.compact_ops_baseline(
+                k, key, dv, blob.ctypes.data_as(ctypes.c_void_p),
+                offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                act.ctypes.data_as(ctypes.c_void_p),
+                ver.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), len(files), threads, best=best)
+            assert err == rc_ref, (drop, threads)
+            if err == 0:
+                assert ser == ref.serialize(), (drop, threads)
