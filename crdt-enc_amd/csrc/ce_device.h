@@ -19,21 +19,23 @@ __device__ __forceinline__ uint32_t rotl32(uint32_t x, int c) {
 // rotl32(d ^ a, 16) as two SDWA xors, one per 16-bit half of the result.  Measured on
 // MI355X (tools/ubench_chacha, profiles/r02_ubench_chacha.txt): ChaCha20 at 2 waves/SIMD runs
 // 2.50 TB/s of keystream this way against 2.26 TB/s with xor + v_alignbit_b32.
-__device__ __forceinline__ uint32_t xor_rotl16(uint32_t d, uint32_t a) {
-#if CE_ROT16_SDWA
+template <bool SD>
+__device__ __forceinline__ uint32_t xor_rotl16_t(uint32_t d, uint32_t a) {
+  if (!SD) return rotl32(d ^ a, 16);
   uint32_t r;
   asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1\n\t"
       "v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0"
       : "=&v"(r) : "v"(d), "v"(a));
   return r;
-#else
-  return rotl32(d ^ a, 16);
-#endif
+}
+__device__ __forceinline__ uint32_t xor_rotl16(uint32_t d, uint32_t a) {
+  return xor_rotl16_t<CE_ROT16_SDWA != 0>(d, a);
 }
 
-#define CE_QR(a, b, c, d)                                                                   \
-  a += b; d = xor_rotl16(d, a); c += d; b ^= c; b = rotl32(b, 12);                         \
+#define CE_QR_T(SD, a, b, c, d)                                                             \
+  a += b; d = xor_rotl16_t<SD>(d, a); c += d; b ^= c; b = rotl32(b, 12);                   \
   a += b; d ^= a; d = rotl32(d, 8);  c += d; b ^= c; b = rotl32(b, 7);
+#define CE_QR(a, b, c, d) CE_QR_T(CE_ROT16_SDWA != 0, a, b, c, d)
 
 __device__ __forceinline__ void chacha_rounds(uint32_t (&x)[16]) {
 #pragma unroll
@@ -82,6 +84,7 @@ __device__ __forceinline__ ChachaPre chacha_pre(const uint32_t (&k)[8], uint32_t
 }
 
 // chacha_block with the counter-independent first-round work taken from `pre`
+template <bool SD = (CE_ROT16_SDWA != 0)>
 __device__ __forceinline__ void chacha_block_pre(const ChachaPre& pre, const uint32_t (&k)[8],
                                                  uint32_t ctr, uint32_t n0, uint32_t n1,
                                                  uint32_t n2, uint32_t (&out)[16]) {
@@ -91,17 +94,17 @@ __device__ __forceinline__ void chacha_block_pre(const ChachaPre& pre, const uin
   x[3] = pre.c[8]; x[7] = pre.c[9]; x[11] = pre.c[10]; x[15] = pre.c[11];
   // column 0 of the first round, after its first add
   x[0] = pre.a0; x[4] = k[0]; x[8] = k[4]; x[12] = ctr;
-  x[12] = xor_rotl16(x[12], x[0]); x[8] += x[12]; x[4] ^= x[8]; x[4] = rotl32(x[4], 12);
+  x[12] = xor_rotl16_t<SD>(x[12], x[0]); x[8] += x[12]; x[4] ^= x[8]; x[4] = rotl32(x[4], 12);
   x[0] += x[4]; x[12] ^= x[0]; x[12] = rotl32(x[12], 8); x[8] += x[12]; x[4] ^= x[8]; x[4] = rotl32(x[4], 7);
   // first diagonal round, then 9 double rounds
-  CE_QR(x[0], x[5], x[10], x[15]); CE_QR(x[1], x[6], x[11], x[12]);
-  CE_QR(x[2], x[7], x[8], x[13]); CE_QR(x[3], x[4], x[9], x[14]);
+  CE_QR_T(SD, x[0], x[5], x[10], x[15]); CE_QR_T(SD, x[1], x[6], x[11], x[12]);
+  CE_QR_T(SD, x[2], x[7], x[8], x[13]); CE_QR_T(SD, x[3], x[4], x[9], x[14]);
 #pragma unroll
   for (int i = 0; i < 9; i++) {
-    CE_QR(x[0], x[4], x[8], x[12]); CE_QR(x[1], x[5], x[9], x[13]);
-    CE_QR(x[2], x[6], x[10], x[14]); CE_QR(x[3], x[7], x[11], x[15]);
-    CE_QR(x[0], x[5], x[10], x[15]); CE_QR(x[1], x[6], x[11], x[12]);
-    CE_QR(x[2], x[7], x[8], x[13]); CE_QR(x[3], x[4], x[9], x[14]);
+    CE_QR_T(SD, x[0], x[4], x[8], x[12]); CE_QR_T(SD, x[1], x[5], x[9], x[13]);
+    CE_QR_T(SD, x[2], x[6], x[10], x[14]); CE_QR_T(SD, x[3], x[7], x[11], x[15]);
+    CE_QR_T(SD, x[0], x[5], x[10], x[15]); CE_QR_T(SD, x[1], x[6], x[11], x[12]);
+    CE_QR_T(SD, x[2], x[7], x[8], x[13]); CE_QR_T(SD, x[3], x[4], x[9], x[14]);
   }
   out[0] = x[0] + 0x61707865u; out[1] = x[1] + 0x3320646eu;
   out[2] = x[2] + 0x79622d32u; out[3] = x[3] + 0x6b206574u;

@@ -698,10 +698,16 @@ __device__ __forceinline__ FilePre2 load_pre2(const DecodeArgs& a, uint32_t f) {
   return p;
 }
 
-// W = waves per SIMD the VGPR budget is sized for (LDS allows 2.5 at LPF 16, 5 at LPF 32)
-template <int LPF, int W, bool JIT>
+// W = waves per SIMD the VGPR budget is sized for (LDS allows 2.5 at LPF 16, 5 at LPF 32).
+// OPT bits: 1 = rot16 as two SDWA xors (ce_device.h xor_rotl16_t), 2 = the next iteration's
+// ciphertext loads issued inside this iteration's decode (after its first round, with the
+// parameters loaded one iteration earlier), so they land while the decode and the next
+// iteration's first ChaCha20 block run instead of being waited for at the first XOR.
+template <int LPF, int W, bool JIT, int OPT = 3>
 __global__ __launch_bounds__(64, W)
 void k_open_fold_v2(DecodeArgs a) {
+  constexpr bool SD = (OPT & 1) != 0;
+  constexpr bool PF = (OPT & 2) != 0 && !JIT;
   using C = V2Cfg<LPF>;
   constexpr int F = C::F;
   constexpr int BPL = C::BPL;
@@ -717,37 +723,54 @@ void k_open_fold_v2(DecodeArgs a) {
   DecState S{38, 0, 0, 0, 0, 0xffffffffu};
   AuthFails fails;
 
+  // 1) a file's ciphertext runs -> registers.  The 16-byte tag follows the ciphertext, so a
+  //    16-byte load at any piece < npc stays inside the file; absent pieces load piece 0.
+  //    Inactive lanes read the (always allocated) params array instead of the blob.
+  uint4 ct[BPL][4];
+  auto load_block_of = [&](const FilePre2& p, int k) {
+    const bool act_ = p.ok && p.len <= kSmallMax;
+    const uint32_t len_ = act_ ? p.len : 0u;
+    const uint32_t npc_ = (len_ + 15) >> 4;
+    const int32_t nblk_ = (int32_t)((len_ + 63) >> 6);
+    const uint8_t* src_ = act_ ? a.blob + (((uint64_t)p.in_hi << 32) | p.in_off)
+                               : reinterpret_cast<const uint8_t*>(a.params);
+    const int32_t b = nblk_ - 1 - (int32_t)sub - LPF * k;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t q = (uint32_t)(4 * b + j);
+      const uint32_t off = b >= 0 && q < npc_ ? q * 16u : 0u;
+      ct[k][j] = *reinterpret_cast<const uint4*>(src_ + off);
+#if CE_FUSED_DIAG
+      if (a.ablate & 8) ct[k][j] = make_uint4(off, len_, sub, (uint32_t)k);
+#endif
+    }
+  };
+  FilePre2 nn;  // PF: the parameters of the iteration after next
+  if (PF) {
+    // prologue: this wave's first ciphertext, and the next iteration's parameters
+#pragma unroll
+    for (int k = BPL - 1; k >= 0; k--) load_block_of(nx, k);
+    nn = load_pre2(a, (g + stride) * F + grp);
+  }
+
   for (; g < ngroups; g += stride) {
     const uint32_t f = g * F + grp;
     const FilePre2 cur = nx;
+    if (PF) nx = nn;
     const bool act = cur.ok && cur.len <= kSmallMax;
     const uint32_t len = act ? cur.len : 0u;
     const uint32_t npc = (len + 15) >> 4;             // ciphertext Poly1305 blocks
     const int32_t nblk = (int32_t)((len + 63) >> 6);  // ChaCha20 blocks
-    // inactive lanes read the (always allocated) params array instead of the blob
-    const uint8_t* src = act ? a.blob + (((uint64_t)cur.in_hi << 32) | cur.in_off)
-                             : reinterpret_cast<const uint8_t*>(a.params);
     const FileParams* Pp = a.params + (act ? f : 0);
 
-    // 1) the lane's ciphertext runs -> registers.  The 16-byte tag follows the ciphertext, so a
-    //    16-byte load at any piece < npc stays inside the file; absent pieces load piece 0.
-    uint4 ct[BPL][4];
-    auto load_block = [&](int k) {
-      const int32_t b = nblk - 1 - (int32_t)sub - LPF * k;
+    auto load_block = [&](int k) { load_block_of(cur, k); };
+    // PF: this iteration's loads were issued during the previous one.  JIT: block k - 1's loads
+    // are issued when block k starts (half the ciphertext registers); otherwise every block's
+    // loads are issued up front.
+    if (!PF) {
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const uint32_t q = (uint32_t)(4 * b + j);
-        const uint32_t off = b >= 0 && q < npc ? q * 16u : 0u;
-        ct[k][j] = *reinterpret_cast<const uint4*>(src + off);
-#if CE_FUSED_DIAG
-        if (a.ablate & 8) ct[k][j] = make_uint4(off, len, sub, (uint32_t)k);
-#endif
-      }
-    };
-    // JIT: block k - 1's loads are issued when block k starts (half the ciphertext registers);
-    // otherwise every block's loads are issued up front
-#pragma unroll
-    for (int k = BPL - 1; k >= (JIT ? BPL - 1 : 0); k--) load_block(k);
+      for (int k = BPL - 1; k >= (JIT ? BPL - 1 : 0); k--) load_block(k);
+    }
 
     // 2) per block, earliest first: keystream (counter 1 + b) in registers, XOR, plaintext ->
     //    LDS, Poly1305.  Branch-free: lanes without a block (short files) compute garbage that
@@ -793,7 +816,7 @@ void k_open_fold_v2(DecodeArgs a) {
         for (int i = 0; i < 16; i++) kb[i] = cur.key[i & 7] + (uint32_t)b;
       } else
 #endif
-        chacha_block_pre(cpre, cur.key, 1u + (uint32_t)b, 0u, cur.n2a, cur.n2b, kb);
+        chacha_block_pre<SD>(cpre, cur.key, 1u + (uint32_t)b, 0u, cur.n2a, cur.n2b, kb);
       L5 G, mj[4];
 #pragma unroll
       for (int j = 0; j < 4; j++) {
@@ -912,18 +935,27 @@ void k_open_fold_v2(DecodeArgs a) {
 
     // 4) data-version check, decode from LDS, fold; the next iteration's parameters are loaded
     //    inside (their latency hides under the decode)
-    decode_fold<LPF>(a, sup, fl, len, act && ok, cur.apply != 0, f, grp, sub, S,
-                     [&] { nx = load_pre2(a, (g + stride) * F + grp); });
+    decode_fold<LPF>(a, sup, fl, len, act && ok, cur.apply != 0, f, grp, sub, S, [&] {
+      if (PF) {
+        // next iteration's ciphertext (its parameters arrived one iteration ago) into the
+        // registers this iteration no longer needs, then the parameters one further ahead
+#pragma unroll
+        for (int k = BPL - 1; k >= 0; k--) load_block_of(nx, k);
+        nn = load_pre2(a, (g + 2 * stride) * F + grp);
+      } else {
+        nx = load_pre2(a, (g + stride) * F + grp);
+      }
+    });
     __builtin_amdgcn_wave_barrier();
   }
   fails.flush(a);
 }
 
-template <int LPF, int W, bool JIT>
+template <int LPF, int W, bool JIT, int OPT = 3>
 static void launch_v2(hipStream_t s, const DecodeArgs& a) {
-  static const uint32_t res = resident_blocks(k_open_fold_v2<LPF, W, JIT>, 64);
+  static const uint32_t res = resident_blocks(k_open_fold_v2<LPF, W, JIT, OPT>, 64);
   const uint32_t groups = (a.n + 64 / LPF - 1) / (64 / LPF);
-  hipLaunchKernelGGL((k_open_fold_v2<LPF, W, JIT>), dim3(std::min<uint32_t>(groups, res)), dim3(64), 0, s, a);
+  hipLaunchKernelGGL((k_open_fold_v2<LPF, W, JIT, OPT>), dim3(std::min<uint32_t>(groups, res)), dim3(64), 0, s, a);
 }
 
 hipError_t launch_open_fold_v2(hipStream_t s, const DecodeArgs& a, int files_per_wave) {
@@ -934,6 +966,11 @@ hipError_t launch_open_fold_v2(hipStream_t s, const DecodeArgs& a, int files_per
     return e ? atoi(e) : 0;
   }();
   // CE_V2_WAVES (diagnostics): 13 = 3 waves/SIMD with JIT ciphertext loads, 12 = 2 with them
+  // CE_V2_OPT (diagnostics, same-box A/B): the OPT bits of the default LPF 16 kernel
+  static const int opt = [] {
+    const char* e = getenv("CE_V2_OPT");
+    return e ? atoi(e) : 3;
+  }();
   if (files_per_wave == 2) {
     if (w == 4) launch_v2<32, 4, false>(s, a);
     else launch_v2<32, 3, false>(s, a);
@@ -941,7 +978,10 @@ hipError_t launch_open_fold_v2(hipStream_t s, const DecodeArgs& a, int files_per
     if (w == 3) launch_v2<16, 3, false>(s, a);
     else if (w == 13) launch_v2<16, 3, true>(s, a);
     else if (w == 12) launch_v2<16, 2, true>(s, a);
-    else launch_v2<16, 2, false>(s, a);
+    else if (opt == 0) launch_v2<16, 2, false, 0>(s, a);
+    else if (opt == 1) launch_v2<16, 2, false, 1>(s, a);
+    else if (opt == 2) launch_v2<16, 2, false, 2>(s, a);
+    else launch_v2<16, 2, false, 3>(s, a);
   }
   return hipGetLastError();
 }

@@ -1,0 +1,81 @@
+"""One rank of the multi-process product exchange tests (tests/test_gpu_multi.py): a real
+torch.distributed group (gloo, every rank on GPU 0 of the box), the HIP ingest through the C ABI
+on this rank's actor shard, then shard.exchange_vclock -- the dense all_reduce(MAX) when every
+Dot names a registered actor, else the all-gather of serialized StateWrappers + merge_state.
+Writes the merged StateWrapper bytes and the path taken to <out>.<rank>.
+
+  python tests/multi_rank_worker.py RANK WORLD PORT MODE OUT     (MODE: registered|unregistered)
+"""
+import os
+import random
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(REPO, "crdt-enc_amd"), REPO):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+APP = bytes.fromhex("aadfd5a66e194b24a8024fa27c72f20c")
+
+
+def workload(mode, seed=77, n_actors=6, versions=5):
+    """Seeded op files (sealed with the oracle): writer actors `actors`; with mode
+    'unregistered' some Dots name `strangers`, actors no rank registers."""
+    import msgpack
+    import oracle
+    import crdtenc
+    rng = random.Random(seed)
+    key = rng.randbytes(32)
+    actors = sorted(rng.randbytes(16) for _ in range(n_actors))
+    strangers = sorted(rng.randbytes(16) for _ in range(3))
+    files, fa, fv = [], [], []
+    for a in range(n_actors):
+        for v in range(versions):
+            dots = []
+            for _ in range(rng.randint(1, 9)):
+                r = rng.random()
+                who = actors[a] if r < 0.6 else rng.choice(actors)
+                if mode == "unregistered" and a % 3 == 2 and r > 0.85:
+                    who = rng.choice(strangers)
+                ctr = rng.getrandbits(64) | (1 << 63) if rng.random() < 0.2 else rng.getrandbits(20)
+                dots.append({"actor": who, "counter": max(ctr, 1)})
+            clear = APP + msgpack.packb(dots, use_bin_type=True)
+            st, enc = oracle.cryptor_encrypt(key, rng.randbytes(24), clear)
+            assert st == 0
+            files.append(crdtenc.CORE_VERSION + enc)
+            fa.append(a)
+            fv.append(v)
+    return key, actors, files, fa, fv
+
+
+def main():
+    rank, world, port, mode, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+    import torch
+    import torch.distributed as dist
+    import crdtenc
+    import shard
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        key, actors, files, fa, fv = workload(mode)
+        ctx = crdtenc.Context(0)
+        core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+        core.set_latest_key(key)
+        core.register_actors(actors)
+        lo, hi = shard.actor_range(len(actors), world, rank)
+        sel = [i for i in range(len(files)) if lo <= fa[i] < hi]
+        rc, _ = core.ingest_ops([files[i] for i in sel], actors[lo:hi], [fa[i] - lo for i in sel],
+                                [fv[i] for i in sel])
+        assert rc == 0, rc
+        dense = torch.zeros(2 * core.dense_capacity(), dtype=torch.int64, device="cuda")
+        path = shard.exchange_vclock(core, dense)
+        with open("%s.%d" % (out, rank), "wb") as f:
+            f.write(path.encode() + b"\n" + core.state_bytes())
+        core.close()
+        ctx.close()
+    finally:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,58 @@
+"""Multi-rank runs of the product on the one GPU of the box (gloo group, every rank on
+device 0; RCCL refuses two ranks on one device, and the driver's 8-GPU node runs the same code
+over RCCL).  Covers the N>1 path end to end through the C ABI:
+  * bench.py --gpus 2 launching its own ranks (CE_BENCH_SHARE_GPU=1, CE_DIST_BACKEND=gloo);
+  * shard.exchange_vclock with every Dot on a registered actor (dense all_reduce(MAX) path) and
+    with Dots on actors no rank registered (state all-gather + merge_state path), each merged
+    state == the oracle's single fold over all files (crdt-enc/src/lib.rs:471-547)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+APP = bytes.fromhex("aadfd5a66e194b24a8024fa27c72f20c")
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_bench_two_ranks_share_gpu():
+    env = dict(os.environ, CE_BENCH_SHARE_GPU="1", CE_DIST_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--versions",
+                        "2", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-variant-b"],
+                       env=env, capture_output=True, timeout=240)
+    assert p.returncode == 0, p.stderr.decode()[-2000:]
+    line = json.loads(p.stdout.decode().strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["state_check"].endswith("ok")
+    assert line["config"]["files_per_gpu"] == 4096 * 2
+    assert "dense" in line["config"]["parallelism"]
+
+
+@pytest.mark.parametrize("mode,path", [("registered", "dense"), ("unregistered", "bytes")])
+def test_exchange_vclock_two_processes(tmp_path, oracle, mode, path):
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import multi_rank_worker as W
+    key, actors, files, fa, fv = W.workload(mode)
+    oc = oracle.Core(oracle.STATE_GCOUNTER)
+    assert oc.read_remote_ops(key, [APP], files, [actors[i] for i in fa], fv)[0] == 0
+    want = oc.serialize()
+    out = str(tmp_path / "m")
+    port = str(_port())
+    procs = [subprocess.Popen([sys.executable, os.path.join(REPO, "tests", "multi_rank_worker.py"),
+                               str(r), "2", port, mode, out]) for r in range(2)]
+    rcs = [p.wait(timeout=180) for p in procs]
+    assert rcs == [0, 0]
+    for r in range(2):
+        with open("%s.%d" % (out, r), "rb") as f:
+            got_path, state = f.read().split(b"\n", 1)
+        assert got_path.decode() == path
+        assert state == want

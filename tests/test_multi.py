@@ -204,3 +204,90 @@ def test_two_rank_dotset_exchange_equals_single_fold(kind, tmp_path):
     for r in range(2):
         with open("%s.%d" % (out, r), "rb") as f:
             assert f.read() == want
+
+
+class _DenseCore:
+    """Host stand-in for crdtenc.Core's exchange surface (dense_ready, export/import_dense,
+    state_bytes, merge_state) over the product's StateWrapper<GCounter> bytes: registered actors
+    own dense slots in registration order; a Dot on any other actor makes dense_ready() False."""
+
+    def __init__(self, kind, registered):
+        self.kind, self.reg = kind, list(registered)
+        self.slot = {a: i for i, a in enumerate(self.reg)}
+        self.state, self.nov = {}, {}
+
+    def fold(self, ser):
+        import msgpack
+        d = msgpack.unpackb(ser, raw=True, strict_map_key=False)
+        nov = d[b"next_op_versions"][b"dots"]
+        st = d[b"state"][b"inner"][b"dots"] if self.kind == 1 else d[b"state"][b"dots"]
+        for a, c in st.items():
+            self.state[a] = max(self.state.get(a, 0), c)
+        for a, c in nov.items():
+            self.nov[a] = max(self.nov.get(a, 0), c)
+
+    def dense_ready(self):
+        return all(a in self.slot for a in list(self.state) + list(self.nov))
+
+    def export_dense(self, p_state, p_nov):
+        self._dense[: len(self.reg)] = torch.from_numpy(np.array(
+            [self.state.get(a, 0) for a in self.reg], dtype=np.uint64).view(np.int64))
+        cap = self._dense.numel() // 2
+        self._dense[cap: cap + len(self.reg)] = torch.from_numpy(np.array(
+            [self.nov.get(a, 0) for a in self.reg], dtype=np.uint64).view(np.int64))
+
+    def import_dense(self, p_state, p_nov):
+        cap = self._dense.numel() // 2
+        s = self._dense[: len(self.reg)].numpy().view(np.uint64)
+        n = self._dense[cap: cap + len(self.reg)].numpy().view(np.uint64)
+        for i, a in enumerate(self.reg):
+            if s[i]:
+                self.state[a] = max(self.state.get(a, 0), int(s[i]))
+            if n[i]:
+                self.nov[a] = max(self.nov.get(a, 0), int(n[i]))
+
+    def state_bytes(self):
+        import msgpack
+        st = dict(sorted(self.state.items()))
+        body = {"inner": {"dots": st}} if self.kind == 1 else {"dots": st}
+        return msgpack.packb({"next_op_versions": {"dots": dict(sorted(self.nov.items()))},
+                              "state": body}, use_bin_type=True)
+
+    def merge_state(self, sw):
+        self.fold(sw)
+        return 0
+
+
+def _vclock_rank_main(rank, world, port, kind, n_reg, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        key, actors, files, fa, fv = _workload()
+        lo, hi = shard.actor_range(len(actors), world, rank)
+        sel = [i for i in range(len(files)) if lo <= fa[i] < hi]
+        core = _DenseCore(kind, actors[:n_reg])
+        core.fold(_fold(kind, key, actors, [files[i] for i in sel], [fa[i] for i in sel],
+                        [fv[i] for i in sel]))
+        core._dense = dense = torch.zeros(2 * 16, dtype=torch.int64)
+        path = shard.exchange_vclock(core, dense)
+        with open("%s.%d" % (out_path, rank), "wb") as f:
+            f.write(path.encode() + b"\n" + core.state_bytes())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_reg,path", [(6, "dense"), (4, "bytes")], ids=["all_registered", "unregistered_actor"])
+def test_exchange_vclock_paths(tmp_path, n_reg, path):
+    """shard.exchange_vclock under a real world-2 gloo group: every actor registered -> one
+    dense all_reduce(MAX); an actor outside the registered slots on either rank -> both ranks
+    take the state all-gather + merge_state path.  Either way == the single fold."""
+    kind = 1
+    key, actors, files, fa, fv = _workload()
+    want = _fold(kind, key, actors, files, fa, fv)
+    out = str(tmp_path / "v")
+    mp.spawn(_vclock_rank_main, args=(2, _free_port(), kind, n_reg, out), nprocs=2, join=True)
+    for r in range(2):
+        with open("%s.%d" % (out, r), "rb") as f:
+            got_path, state = f.read().split(b"\n", 1)
+        assert got_path.decode() == path
+        assert state == want
