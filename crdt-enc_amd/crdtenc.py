@@ -23,7 +23,7 @@ STATUS_NAMES = {
     65: "DEVICE", 66: "NO_KEY", 67: "IO", 68: "NO_LOCAL_META",
 }
 STATE_VCLOCK, STATE_GCOUNTER, STATE_ORSWOT, STATE_MVREG = 0, 1, 2, 3
-OPEN_CREATE, COMPACT_INGEST_FORMAT = 1, 2
+OPEN_CREATE, COMPACT_INGEST_FORMAT, OPEN_MULTI_KEY = 1, 2, 4
 
 CORE_VERSION = bytes.fromhex("e834d789101b463498239de990a9051f")   # crdt-enc/src/lib.rs:26
 KEY_VERSION = bytes.fromhex("5df28591439a4cef8ca68433276cc9ed")    # xchacha lib.rs:13
@@ -45,7 +45,9 @@ EXPORTS = [
     "ce_core_register_actors", "ce_core_dense_capacity", "ce_core_export_dense",
     "ce_core_import_dense", "ce_vbuf_init", "ce_vbuf_remaining", "ce_vbuf_chunk",
     "ce_vbuf_advance", "ce_vbuf_chunks_vectored", "ce_ctx_set_timing", "ce_ctx_timing_read",
-    "ce_ctx_timing_reset", "ce_core_reset", "ce_core_merge_state",
+    "ce_ctx_timing_reset", "ce_core_reset", "ce_core_merge_state", "ce_core_dense_ready",
+    "ce_keys_decode", "ce_keys_from_remote_metas", "ce_keys_merge", "ce_keys_free",
+    "ce_keys_count", "ce_keys_latest", "ce_keys_get", "ce_keys_at", "ce_core_set_keys",
 ]
 
 
@@ -95,6 +97,7 @@ def lib():
         L.ce_cryptor_sealed_len.restype = ctypes.c_size_t
         L.ce_cryptor_sealed_len.argtypes = [ctypes.c_size_t]
         L.ce_core_dense_capacity.restype = ctypes.c_uint32
+        L.ce_keys_count.restype = ctypes.c_uint32
         L.ce_vbuf_remaining.restype = ctypes.c_size_t
         L.ce_vbuf_chunk.restype = ctypes.c_size_t
         L.ce_vbuf_chunks_vectored.restype = ctypes.c_size_t
@@ -342,6 +345,87 @@ class Storage:
         return _take(b)
 
 
+class Keys:
+    """Keys { latest_key_id: MVReg<Uuid, Uuid>, keys: Orswot<Key, Uuid> }
+    (crdt-enc/src/key_cryptor.rs:35-82), decoded and merged on the host by the product."""
+
+    def __init__(self, p):
+        self.p = p
+
+    @classmethod
+    def decode(cls, msgpack_bytes):
+        p = ctypes.c_void_p()
+        rc = lib().ce_keys_decode(_cbuf(msgpack_bytes), ctypes.c_size_t(len(msgpack_bytes)),
+                                  ctypes.byref(p))
+        if rc:
+            raise CeError(rc, "ce_keys_decode")
+        return cls(p)
+
+    @classmethod
+    def from_remote_metas(cls, files):
+        """Core::read_remote_meta_ + the gpgme KeyHandler's decode of the key register."""
+        n = len(files)
+        offs = (ctypes.c_uint64 * (n + 1))()
+        o = 0
+        for i, f in enumerate(files):
+            offs[i] = o
+            o += len(f)
+        offs[n] = o
+        p = ctypes.c_void_p()
+        rc = lib().ce_keys_from_remote_metas(_cbuf(b"".join(files)), offs, ctypes.c_uint32(n),
+                                             ctypes.byref(p))
+        if rc:
+            raise CeError(rc, "ce_keys_from_remote_metas")
+        return cls(p)
+
+    def close(self):
+        if self.p:
+            lib().ce_keys_free(self.p)
+            self.p = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def merge(self, other):
+        rc = lib().ce_keys_merge(self.p, other.p)
+        if rc:
+            raise CeError(rc, "ce_keys_merge")
+
+    def __len__(self):
+        return lib().ce_keys_count(self.p)
+
+    def _get(self, fn, *args):
+        n = ctypes.c_size_t(0)
+        ver = ctypes.create_string_buffer(16)
+        ident = ctypes.create_string_buffer(16)
+        rc = fn(self.p, *args, ident, ver, None, ctypes.c_size_t(0), ctypes.byref(n)) if fn is not \
+            lib().ce_keys_get else fn(self.p, *args, ver, None, ctypes.c_size_t(0), ctypes.byref(n))
+        if rc:
+            raise CeError(rc)
+        key = ctypes.create_string_buffer(max(n.value, 1))
+        if fn is lib().ce_keys_get:
+            rc = fn(self.p, *args, ver, key, ctypes.c_size_t(n.value), ctypes.byref(n))
+        else:
+            rc = fn(self.p, *args, ident, ver, key, ctypes.c_size_t(n.value), ctypes.byref(n))
+        if rc:
+            raise CeError(rc)
+        return ident.raw, ver.raw, key.raw[:n.value]
+
+    def latest(self):
+        """Keys::latest_key -> (id, key version, key); CeError NO_KEY / DECODE otherwise."""
+        return self._get(lib().ce_keys_latest)
+
+    def get(self, key_id):
+        _, ver, key = self._get(lib().ce_keys_get, _cbuf(key_id))
+        return ver, key
+
+    def items(self):
+        return [self._get(lib().ce_keys_at, ctypes.c_uint32(i)) for i in range(len(self))]
+
+
 class Core:
     """Core<S> for S in {VClock<Uuid>, GCounter<Uuid>, Orswot<u64, Uuid>, MVReg<u64, Uuid>}
     (crdt-enc/src/lib.rs)."""
@@ -375,6 +459,11 @@ class Core:
     def set_latest_key(self, key, key_version=KEY_VERSION):
         self.ctx.check(lib().ce_core_set_latest_key(self.p, _cbuf(key_version), _cbuf(key),
                                                     ctypes.c_size_t(len(key))), "set_latest_key")
+
+    def set_keys(self, keys):
+        """CoreSubHandle::set_keys (lib.rs:382-388): Keys::latest_key for reads and writes; the
+        other keys are tried on AUTH failures only with OPEN_MULTI_KEY."""
+        self.ctx.check(lib().ce_core_set_keys(self.p, keys.p), "set_keys")
 
     def info_actor(self):
         out = ctypes.create_string_buffer(16)

@@ -531,10 +531,97 @@ uint32_t host_gate(const uint32_t* fa, const uint64_t* fv, uint32_t n, std::vect
 // the host waits -- work it enqueues on the stream overlaps the fused kernel's run on the host
 // side.  merged_out: whether the commit happened on the device (the fast path).
 using AfterCommit = std::function<int(const NovApply&)>;
-int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
-                   uint64_t blob_len, const uint8_t* actors, uint32_t m, const uint32_t* d_fa,
-                   const uint64_t* d_fv, int32_t* status_out, const AfterCommit* after_commit = nullptr,
-                   bool* merged_out = nullptr) {
+
+// ingest_ops_dev_once asks for a fresh pass: actors found while decoding plaintext that is not
+// re-opened by the fused kernel (host-parse envelopes, CE_OPEN_MULTI_KEY retries) grew the actor
+// table, so every slot moved and the partial batch state is stale.  The new actors stay in the
+// table, so the next pass finds them.
+static constexpr int kRestartIngest = -1000;
+
+// Decode + fold the files flagged in d_mask (n bytes) whose plaintext sits in ctx->out
+// (k_decode_dots), with actor-table misses resolved as the fused path does (insert, upload,
+// fold the missed files again).  Returns kRestartIngest when the table had to grow.
+int decode_only_resolving(ce_core* c, DecodeArgs& da, uint32_t n, uint8_t* d_mask) {
+  ce_ctx* ctx = c->ctx;
+  uint32_t* hc = ctx->h_counters.as<uint32_t>();
+  hipError_t e;
+  for (int round = 0;; round++) {
+    da.only = d_mask;
+    da.large_only = 0;
+    da.table = c->d_table.as<ActorSlot>();
+    da.mask = c->cap - 1;
+    da.batch = c->d_batch.as<unsigned long long>();
+    if ((e = hipMemsetAsync(ctx->counters.as<uint32_t>() + 4, 0, 4, ctx->stream)) ||
+        (e = hipMemsetAsync(ctx->refold.p, 0, n, ctx->stream)) ||
+        (e = launch_decode_dots(ctx->stream, da, grid_waves_for(n))) ||
+        (e = hipMemcpyAsync(hc, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+      return ctx->hip_fail(e, "decode plaintext");
+    if (hc[4] == 0) return CE_OK;
+    if (round > 64) return ctx->fail(CE_ERR_DEVICE, "actor table did not converge");
+    const uint32_t nm = std::min<uint32_t>(hc[4], 65536);
+    std::vector<uint4> ml(nm);
+    if ((e = hipMemcpyAsync(ml.data(), ctx->miss.p, nm * 16ull, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (e = hipMemcpyAsync(d_mask, ctx->refold.p, n, hipMemcpyDeviceToDevice, ctx->stream)) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+      return ctx->hip_fail(e, "miss");
+    const uint32_t old_cap = c->cap;
+    for (auto& x : ml) {
+      Uuid u;
+      std::memcpy(u.data(), &x, 16);
+      uint32_t s;
+      int rc = insert_actor(c, u, &s);
+      if (rc) return rc;
+    }
+    int rc = table_upload(c);
+    if (rc) return rc;
+    if (c->cap != old_cap) return kRestartIngest;
+  }
+}
+
+// CE_OPEN_MULTI_KEY (beyond the reference): the files that failed authentication
+// under the latest key are opened again under each other key of the set, in id order (whole
+// batch opened per key with device_open, plaintext into ctx->out; only the files still failing
+// and now opening are decoded and folded).  st: per-file statuses, updated in place.
+int retry_alt_keys(ce_core* c, DecodeArgs& da, const uint8_t* d_blob, const uint64_t* d_offs,
+                   uint32_t n, uint64_t blob_len, std::vector<int32_t>& st) {
+  ce_ctx* ctx = c->ctx;
+  hipError_t e;
+  std::vector<int32_t> sk(n);
+  std::vector<uint8_t> sel(n);
+  for (const AltKey& ak : c->alt_keys) {
+    bool any = false;
+    for (uint32_t i = 0; i < n; i++) any |= st[i] == CE_ERR_AUTH;
+    if (!any) break;
+    const KeyRef kr{ak.version, ak.key.data(), ak.key.size()};
+    int rc = device_open(ctx, d_blob, d_offs, n, blob_len, true, kr, ctx->out.as<uint8_t>(),
+                         ctx->status.as<int32_t>(), false);
+    if (rc) return rc;
+    if ((e = hipMemcpyAsync(sk.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+      return ctx->hip_fail(e, "multi-key status");
+    bool opened = false;
+    for (uint32_t i = 0; i < n; i++) {
+      sel[i] = st[i] == CE_ERR_AUTH && sk[i] == CE_OK;
+      opened |= sel[i] != 0;
+    }
+    if (!opened) continue;
+    if ((e = hipMemcpyAsync(c->d_refold2.p, sel.data(), n, hipMemcpyHostToDevice, ctx->stream)))
+      return ctx->hip_fail(e, "multi-key mask");
+    if ((rc = decode_only_resolving(c, da, n, c->d_refold2.as<uint8_t>()))) return rc;
+    if ((e = hipMemcpyAsync(sk.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+      return ctx->hip_fail(e, "multi-key status");
+    for (uint32_t i = 0; i < n; i++)
+      if (sel[i]) st[i] = sk[i];  // CE_OK, or the decode's CE_ERR_DECODE / PT_* status
+  }
+  return CE_OK;
+}
+
+int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
+                        uint64_t blob_len, const uint8_t* actors, uint32_t m, const uint32_t* d_fa,
+                        const uint64_t* d_fv, int32_t* status_out, const AfterCommit* after_commit,
+                        bool* merged_out) {
   if (merged_out) *merged_out = false;
   ce_ctx* ctx = c->ctx;
   if (!c->has_key) return ctx->fail(CE_ERR_NO_KEY, "no latest key");
@@ -768,7 +855,10 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
   }
 
   // 4) misses: actors not in the table -> insert, upload, fold again the files that missed
-  for (int round = 0; hc[4] != 0 && hc[2] == 0 && hc[3] == 0 && hc[8] == 0; round++) {
+  // (with CE_OPEN_MULTI_KEY an authentication failure may still be retried under another key,
+  // so the files that did open must have their misses folded too)
+  const bool may_retry = (c->flags & CE_OPEN_MULTI_KEY) && !c->alt_keys.empty();
+  for (int round = 0; hc[4] != 0 && (hc[2] == 0 || may_retry) && hc[3] == 0 && hc[8] == 0; round++) {
     const uint32_t nm = std::min<uint32_t>(hc[4], 65536);
     std::vector<uint4> ml(nm);
     if ((e = hipMemcpyAsync(ml.data(), ctx->miss.p, nm * 16ull, hipMemcpyDeviceToHost, ctx->stream)) ||
@@ -825,17 +915,17 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
     std::vector<uint8_t> only(n, 0);
     for (uint32_t i = 0; i < n; i++) only[i] = st[i] == kStatusHostParse;
     if ((e = hipMemcpy(c->d_refold2.p, only.data(), n, hipMemcpyHostToDevice))) return ctx->hip_fail(e, "x");
-    da.only = c->d_refold2.as<uint8_t>();
-    da.large_only = 0;
-    da.table = c->d_table.as<ActorSlot>();
-    da.mask = c->cap - 1;
-    da.batch = c->d_batch.as<unsigned long long>();
-    if ((e = launch_decode_dots(ctx->stream, da, grid_waves_for(n))) ||
-        (e = hipMemcpyAsync(hc, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->stream)) ||
-        (e = hipStreamSynchronize(ctx->stream)))
-      return ctx->hip_fail(e, "exotic decode");
-    if (hc[4]) return ctx->fail(CE_ERR_DEVICE, "unregistered actor in an exotic file");
+    // misses go through the same insert / upload / fold-again loop as the fused path's
+    if ((rc = decode_only_resolving(c, da, n, c->d_refold2.as<uint8_t>()))) return rc;
     if ((rc = fetch_status())) return rc;
+  }
+  if ((c->flags & CE_OPEN_MULTI_KEY) && !c->alt_keys.empty() && st.size() == n) {
+    bool only_auth = true, any_auth = false;
+    for (uint32_t i = 0; i < n; i++) {
+      only_auth &= st[i] == CE_OK || st[i] == CE_ERR_AUTH;
+      any_auth |= st[i] == CE_ERR_AUTH;
+    }
+    if (any_auth && only_auth && (rc = retry_alt_keys(c, da, d_blob, d_offs, n, blob_len, st))) return rc;
   }
   int first = CE_OK;
   if (st.size() == n) {
@@ -870,6 +960,18 @@ int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, ui
     return CE_ERR_OP_VERSION;
   }
   return CE_OK;
+}
+
+int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
+                   uint64_t blob_len, const uint8_t* actors, uint32_t m, const uint32_t* d_fa,
+                   const uint64_t* d_fv, int32_t* status_out, const AfterCommit* after_commit = nullptr,
+                   bool* merged_out = nullptr) {
+  for (int pass = 0;; pass++) {
+    int rc = ingest_ops_dev_once(c, d_blob, d_offs, n, blob_len, actors, m, d_fa, d_fv, status_out,
+                                 after_commit, merged_out);
+    if (rc != kRestartIngest) return rc;
+    if (pass > 8) return c->ctx->fail(CE_ERR_DEVICE, "actor table did not converge");
+  }
 }
 
 // host metadata -> device, then ingest_ops_dev
@@ -1230,9 +1332,11 @@ void ce_core_close(ce_core* c) {
 int ce_core_set_latest_key(ce_core* c, const uint8_t key_version[16], const uint8_t* key,
                            size_t key_len) {
   if (!c || !key_version || (key_len && !key)) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
   std::memcpy(c->key_version, key_version, 16);
   c->key.assign(key, key + key_len);
   c->has_key = true;
+  c->alt_keys.clear();
   return CE_OK;
 }
 

@@ -36,6 +36,13 @@ void ds_free(DsState* d);
 inline bool is_dotset_kind(int kind) { return kind == CE_STATE_ORSWOT || kind == CE_STATE_MVREG; }
 }  // namespace ce
 
+namespace ce {
+struct AltKey {  // a key of the set besides the latest (ce_core_set_keys, CE_OPEN_MULTI_KEY)
+  uint8_t version[16];
+  std::vector<uint8_t> key;
+};
+}  // namespace ce
+
 struct ce_core {
   ce_ctx* ctx = nullptr;
   int kind = CE_STATE_GCOUNTER;
@@ -47,6 +54,7 @@ struct ce_core {
   bool has_key = false;
   uint8_t key_version[16] = {0};
   std::vector<uint8_t> key;
+  std::vector<ce::AltKey> alt_keys;  // tried in id order on AUTH failures (CE_OPEN_MULTI_KEY)
   // actor table: UUID -> hash slot; ActorSlot.pad[0] holds the actor's stable id (insertion
   // order, survives table growth) used by the dot-set kinds' device arrays.
   uint32_t cap = 0, size = 0, registered = 0;

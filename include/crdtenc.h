@@ -186,9 +186,15 @@ enum ce_state_kind {
 
 enum ce_open_flags {
   CE_OPEN_CREATE = 1,            /* OpenOptions.create (lib.rs:729)                          */
-  CE_COMPACT_INGEST_FORMAT = 2   /* write compacted states in the format read_remote_states
+  CE_COMPACT_INGEST_FORMAT = 2,  /* write compacted states in the format read_remote_states
                                     reads (outer CURRENT_VERSION + inner data-version prefix)
                                     instead of the reference's compact() bytes   */
+  CE_OPEN_MULTI_KEY = 4          /* beyond the reference (opt-in): files that fail
+                                    authentication under the latest key are opened again under
+                                    the other keys of the set given to ce_core_set_keys, in id
+                                    order; the batch is rejected only if some file opens under
+                                    none.  Off, every file must open under Keys::latest_key, as
+                                    the reference requires (lib.rs:414-420,484-490) */
 };
 
 typedef struct ce_open_options {
@@ -278,6 +284,40 @@ int ce_core_import_dense(ce_core *c, const uint64_t *d_state, const uint64_t *d_
  * register_actors -- VClock::apply takes any actor, lib.rs:533-535).  Ranks then exchange
  * ce_core_state_bytes + ce_core_merge_state instead (crdtenc shard.exchange_vclock). */
 int ce_core_dense_ready(ce_core *c);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Keys (crdt-enc/src/key_cryptor.rs:35-82): the data keys the core reads and writes with     */
+/* ---------------------------------------------------------------------------------------- */
+typedef struct ce_keys ce_keys;
+/* rmp_serde::from_slice::<Keys>: Keys { latest_key_id: MVReg<Uuid, Uuid>,
+ * keys: Orswot<Key, Uuid> }, Key { id: Uuid, key: VersionBytes } (key_cryptor.rs:35-40,85-89). */
+int ce_keys_decode(const uint8_t *msgpack, size_t len, ce_keys **out);
+/* The remote meta files (each VersionBytes(CURRENT_VERSION, msgpack(RemoteMeta)), lib.rs:
+ * 647-664) merged as Core::read_remote_meta_ does (lib.rs:553-612), then the key cryptor's
+ * register decoded as the gpgme KeyHandler does (crdt-enc-gpgme/src/lib.rs:79-105;
+ * utils/mod.rs:94-126): every value VersionBytes(gpgme version, msgpack(Keys)), merged.
+ * blob[offs[i], offs[i+1]) = file i as Storage::load_remote_metas returns it. */
+int ce_keys_from_remote_metas(const uint8_t *blob, const uint64_t *offs, uint32_t n, ce_keys **out);
+/* Keys::merge (key_cryptor.rs:42-50): MVReg::merge + Orswot::merge */
+int ce_keys_merge(ce_keys *k, const ce_keys *other);
+void ce_keys_free(ce_keys *k);
+/* keys.read().val.len() */
+uint32_t ce_keys_count(const ce_keys *k);
+/* Keys::latest_key (key_cryptor.rs:59-70): the min-id key among the register's latest ids.
+ * CE_ERR_NO_KEY when the register is empty; CE_ERR_DECODE when a latest id names no key (the
+ * reference panics, :67).  Outputs may be NULL; key_out needs *key_len bytes (cap). */
+int ce_keys_latest(const ce_keys *k, uint8_t id_out[16], uint8_t key_version_out[16],
+                   uint8_t *key_out, size_t cap, size_t *key_len);
+/* Keys::get_key (key_cryptor.rs:55-57): CE_ERR_NO_KEY when absent */
+int ce_keys_get(const ce_keys *k, const uint8_t id[16], uint8_t key_version_out[16],
+                uint8_t *key_out, size_t cap, size_t *key_len);
+/* the i-th key of keys.read().val in id order (enumeration) */
+int ce_keys_at(const ce_keys *k, uint32_t i, uint8_t id_out[16], uint8_t key_version_out[16],
+               uint8_t *key_out, size_t cap, size_t *key_len);
+/* CoreSubHandle::set_keys (lib.rs:382-388): the core reads and writes with Keys::latest_key
+ * from now on; the other keys are kept for CE_OPEN_MULTI_KEY.  (ce_core_set_latest_key sets
+ * one key and drops any others.) */
+int ce_core_set_keys(ce_core *c, const ce_keys *k);
 
 /* Framing helpers (crdt-enc/src/utils/version_bytes.rs): VersionBytesBuf chunk/advance. */
 typedef struct ce_vbuf {

@@ -129,3 +129,70 @@ def test_c5_key_rotation_mix(ctx, oracle, tamper):
     assert (rc, st) == (orc, ost) and rc == 0
     assert core.state_bytes() == oc.serialize()
     core.close()
+
+
+@pytest.mark.parametrize("tamper", [0, 2])
+def test_multi_key_opt_in(ctx, oracle, tamper):
+    """Keys with a rotated data key (ce_keys from the wire form, latest = Keys::latest_key).
+    Default (reference): files under the older key fail like tampered ones, the batch
+    is rejected and nothing folds.  CE_OPEN_MULTI_KEY: those files open under the older key (in
+    id order), so the batch folds to the state of all plaintexts; a tampered file still fails
+    under every key and rejects the batch.  Files of the older key also carry Dots on actors the
+    table has never seen (the retry path's miss resolution)."""
+    from oracle import keys as K
+    rng = random.Random(911 + tamper)
+    writer = rng.randbytes(16)
+    ks = K.Keys()
+    old_id, new_id = rng.randbytes(16), rng.randbytes(16)
+    k_old, k_new = rng.randbytes(32), rng.randbytes(32)
+    ks.insert_latest_key(writer, old_id, k_old)
+    ks.insert_latest_key(writer, new_id, k_new)
+    keys = crdtenc.Keys.decode(ks.to_bytes())
+    assert keys.latest()[2] == k_new and len(keys) == 2
+    actors = sorted(rng.randbytes(16) for _ in range(12))
+    strangers = [rng.randbytes(16) for _ in range(5)]
+    clears, fa, fv, old = [], [], [], []
+    for a in range(12):
+        for v in range(24):
+            o = rng.random() < 0.5
+            c = _dots_clear(rng, actors, a, rng.choice([600, 4000, 9000]))
+            if o and rng.random() < 0.3:
+                dots = msgpack.unpackb(c[16:])
+                dots.append({"actor": rng.choice(strangers), "counter": rng.getrandbits(30)})
+                c = APP + msgpack.packb(dots, use_bin_type=True)
+            clears.append(c)
+            fa.append(a)
+            fv.append(v)
+            old.append(o)
+    s_old, s_new = ctx.encrypt_batch(k_old, clears), ctx.encrypt_batch(k_new, clears)
+    files = [CORE + (so if o else sn) for so, sn, o in zip(s_old, s_new, old)]
+    tampered = set(rng.sample(range(len(files)), tamper))
+    for i in tampered:
+        b = bytearray(files[i])
+        b[-1 - rng.randrange(16)] ^= 1 << rng.randrange(8)
+        files[i] = bytes(b)
+    # reference behaviour (flag off): latest key only
+    oc = oracle.Core()
+    empty = oc.serialize()
+    orc, ost = oc.read_remote_ops(k_new, [APP], files, [actors[i] for i in fa], fv)
+    core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+    core.set_keys(keys)
+    rc, st = core.ingest_ops(files, actors, fa, fv)
+    assert rc == orc == 9 and st == ost
+    assert core.state_bytes() == empty
+    core.close()
+    # opt-in
+    core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP,
+                        flags=crdtenc.OPEN_MULTI_KEY)
+    core.set_keys(keys)
+    rc, st = core.ingest_ops(files, actors, fa, fv)
+    if tamper:
+        assert rc == 9 and sorted(i for i, s in enumerate(st) if s) == sorted(tampered)
+        assert core.state_bytes() == empty
+    else:
+        assert rc == 0 and all(s == 0 for s in st)
+        ref = oracle.Core()
+        assert ref.read_remote_ops(k_new, [APP], [CORE + s for s in s_new],
+                                   [actors[i] for i in fa], fv)[0] == 0
+        assert core.state_bytes() == ref.serialize()
+    core.close()

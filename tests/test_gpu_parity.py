@@ -741,3 +741,46 @@ def test_compact_ops_device(ctx, oracle, case, kind):
         assert rc2 == 0 and f2 == f
     core.close()
     ref.close()
+
+
+@pytest.mark.parametrize("n_new", [3, 200])
+def test_exotic_envelope_new_actors(ctx, oracle, n_new):
+    """Cryptor boxes whose nonce / enc_data are serde_bytes sequences of u8 (not bin): the
+    device leaves them to the host parser (kStatusHostParse), which opens the canonical form and
+    decodes the plaintext on the GPU.  Their Dots name actors no writer has: those misses go
+    through the insert / upload / fold-again loop (200 new actors grow the table, so the ingest
+    restarts with the new slots) -- VClock::apply takes any actor (lib.rs:533-535)."""
+    rng = random.Random(4242 + n_new)
+    key = rng.randbytes(32)
+    actors = sorted(rng.randbytes(16) for _ in range(8))
+    strangers = [rng.randbytes(16) for _ in range(n_new)]
+    files, fa, fv, exotic = [], [], [], 0
+    for a in range(8):
+        for v in range(6):
+            dots = [{"actor": actors[a], "counter": 10 * v + d + 1} for d in range(5)]
+            ex = (a + v) % 3 == 0
+            if ex:
+                dots += [{"actor": rng.choice(strangers), "counter": rng.getrandbits(33)}
+                         for _ in range(max(1, n_new // 10))]
+            clear = APP + msgpack.packb(dots, use_bin_type=True)
+            enc = ctx.encrypt(key, clear, nonce=rng.randbytes(24))
+            if ex:
+                ver, inner = msgpack.unpackb(enc)
+                eb = msgpack.unpackb(inner)
+                inner = msgpack.packb({"nonce": list(eb["nonce"]), "enc_data": list(eb["enc_data"])},
+                                      use_bin_type=True)
+                enc = msgpack.packb([ver, inner], use_bin_type=True)
+                exotic += 1
+            files.append(CORE + enc)
+            fa.append(a)
+            fv.append(v)
+    assert exotic > 0
+    oc = oracle.Core()
+    orc, ost = oc.read_remote_ops(key, [APP], files, [actors[i] for i in fa], fv)
+    assert orc == 0
+    core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+    core.set_latest_key(key)
+    rc, st = core.ingest_ops(files, actors, fa, fv)
+    assert (rc, st) == (orc, ost)
+    assert core.state_bytes() == oc.serialize()
+    core.close()
