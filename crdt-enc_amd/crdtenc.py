@@ -48,6 +48,7 @@ EXPORTS = [
     "ce_ctx_timing_reset", "ce_core_reset", "ce_core_merge_state", "ce_core_dense_ready",
     "ce_keys_decode", "ce_keys_from_remote_metas", "ce_keys_merge", "ce_keys_free",
     "ce_keys_count", "ce_keys_latest", "ce_keys_get", "ce_keys_at", "ce_core_set_keys",
+    "ce_core_apply_ops_batch", "ce_core_ingest_ops_iov", "ce_core_compact_ops_iov",
 ]
 
 
@@ -518,6 +519,35 @@ class Core:
             return rc, None, None
         return rc, _take(b), (nm.value.decode() if name else None)
 
+    def ingest_ops_iov(self, files, actors, file_actor, versions, want_status=True):
+        """Per-file host buffers (Storage::load_ops's Vec<u8>s): no concatenation."""
+        n = len(files)
+        bufs = [_cbuf(f) for f in files]
+        ptrs = (ctypes.c_void_p * max(n, 1))(*[ctypes.cast(b, ctypes.c_void_p) for b in bufs])
+        lens = (ctypes.c_size_t * max(n, 1))(*[len(f) for f in files])
+        st = (ctypes.c_int32 * max(n, 1))() if want_status else None
+        fa = (ctypes.c_uint32 * max(n, 1))(*file_actor)
+        fv = (ctypes.c_uint64 * max(n, 1))(*versions)
+        rc = lib().ce_core_ingest_ops_iov(self.p, ptrs, lens, ctypes.c_uint32(n),
+                                          _cbuf(b"".join(actors)), ctypes.c_uint32(len(actors)), fa,
+                                          fv, st)
+        return rc, (list(st)[:n] if want_status else None)
+
+    def compact_ops_iov(self, ptrs, lens, n, actors, file_actor, file_version, nonce=None,
+                        name=True):
+        """Core::compact over per-file host buffers: ptrs / lens = ctypes arrays (n entries) of
+        file addresses and sizes, file_actor (u32) / file_version (u64) host arrays (ctypes or
+        numpy .ctypes pointers).  Returns (rc, file, name)."""
+        b = Buf()
+        nm = ctypes.create_string_buffer(64) if name else None
+        rc = lib().ce_core_compact_ops_iov(
+            self.p, ptrs, lens, ctypes.c_uint32(n), _ptr(actors)[0],
+            ctypes.c_uint32(len(actors) // 16), file_actor, file_version,
+            _cbuf(nonce) if nonce is not None else None, ctypes.byref(b), nm)
+        if rc:
+            return rc, None, None
+        return rc, _take(b), (nm.value.decode() if name else None)
+
     def ingest_states(self, files):
         n = len(files)
         blob = b"".join(files)
@@ -568,6 +598,26 @@ class Core:
 
     def apply_ops(self, ops_msgpack):
         return lib().ce_core_apply_ops(self.p, _cbuf(ops_msgpack), ctypes.c_size_t(len(ops_msgpack)))
+
+    def apply_ops_batch(self, ops_list, nonces=None):
+        """n Core::apply_ops calls in one GPU seal: returns (rc, [op file bytes])."""
+        n = len(ops_list)
+        offs = (ctypes.c_uint64 * (n + 1))()
+        o = 0
+        for i, x in enumerate(ops_list):
+            offs[i] = o
+            o += len(x)
+        offs[n] = o
+        fb, fo = Buf(), Buf()
+        rc = lib().ce_core_apply_ops_batch(self.p, _cbuf(b"".join(ops_list)), offs, ctypes.c_uint32(n),
+                                           _cbuf(b"".join(nonces)) if nonces is not None else None,
+                                           ctypes.byref(fb), ctypes.byref(fo))
+        if rc:
+            return rc, None
+        blob, fofs = _take(fb), _take(fo)
+        import struct
+        o = struct.unpack("<%dQ" % (n + 1), fofs)
+        return 0, [blob[o[i]:o[i + 1]] for i in range(n)]
 
     def reset(self):
         self.ctx.check(lib().ce_core_reset(self.p), "reset")

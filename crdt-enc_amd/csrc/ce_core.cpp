@@ -1366,16 +1366,37 @@ int ce_core_ingest_ops(ce_core* c, const uint8_t* blob, const uint64_t* offs, ui
   (void)hipSetDevice(c->ctx->device);
   if (n == 0) return CE_OK;
   ce_ctx* ctx = c->ctx;
-  hipError_t e;
-  const uint64_t blen = offs[n];
-  if ((e = ctx->blob.reserve(blen + 64)) || (e = ctx->offs.reserve((n + 1) * 8ull)))
-    return ctx->hip_fail(e, "ingest reserve");
-  if ((e = hipMemcpyAsync(ctx->blob.p, blob, blen, hipMemcpyHostToDevice, ctx->stream)) ||
-      (e = hipMemcpyAsync(ctx->offs.p, offs, (n + 1) * 8ull, hipMemcpyHostToDevice, ctx->stream)) ||
-      (e = hipStreamSynchronize(ctx->stream)))
-    return ctx->hip_fail(e, "ingest upload");
-  return ingest_ops_hostmeta(c, ctx->blob.as<uint8_t>(), ctx->offs.as<uint64_t>(), n, blen, actors,
+  // the blob goes up in chunks through pinned staging (ce_upload.cpp), ordered on the stream
+  std::vector<const uint8_t*> fp(n);
+  for (uint32_t i = 0; i < n; i++) fp[i] = blob + offs[i];
+  std::vector<uint64_t> rel(offs, offs + n + 1);
+  for (auto& x : rel) x -= offs[0];
+  int rc = stage_host_batch(ctx, fp.data(), rel.data(), n);
+  if (rc) return rc;
+  return ingest_ops_hostmeta(c, ctx->blob.as<uint8_t>(), ctx->offs.as<uint64_t>(), n, rel[n], actors,
                              m, file_actor, file_version, status);
+}
+
+static int iov_offsets(const size_t* lens, uint32_t n, std::vector<uint64_t>* offs) {
+  offs->resize(n + 1);
+  (*offs)[0] = 0;
+  for (uint32_t i = 0; i < n; i++) (*offs)[i + 1] = (*offs)[i] + lens[i];
+  return CE_OK;
+}
+
+int ce_core_ingest_ops_iov(ce_core* c, const uint8_t* const* files, const size_t* lens, uint32_t n,
+                           const uint8_t* actors, uint32_t m, const uint32_t* file_actor,
+                           const uint64_t* file_version, int32_t* status) {
+  if (!c || (n && (!files || !lens || !actors || !file_actor || !file_version))) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  (void)hipSetDevice(c->ctx->device);
+  if (n == 0) return CE_OK;
+  std::vector<uint64_t> offs;
+  iov_offsets(lens, n, &offs);
+  int rc = stage_host_batch(c->ctx, files, offs.data(), n);
+  if (rc) return rc;
+  return ingest_ops_hostmeta(c, c->ctx->blob.as<uint8_t>(), c->ctx->offs.as<uint64_t>(), n, offs[n],
+                             actors, m, file_actor, file_version, status);
 }
 
 int ce_core_ingest_ops_device(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs,
@@ -1433,6 +1454,33 @@ int ce_core_compact_ops_device(ce_core* c, const uint8_t* d_blob, const uint64_t
   std::memcpy(file->data, f.data(), f.size());
   file->len = f.size();
   return CE_OK;
+}
+
+int ce_core_compact_ops_iov(ce_core* c, const uint8_t* const* files, const size_t* lens, uint32_t n,
+                            const uint8_t* actors, uint32_t m, const uint32_t* file_actor,
+                            const uint64_t* file_version, const uint8_t* nonce, ce_buf* file,
+                            char name_out[64]) {
+  if (!c || !file || (n && (!files || !lens || !actors || !file_actor || !file_version)))
+    return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  (void)hipSetDevice(c->ctx->device);
+  ce_ctx* ctx = c->ctx;
+  std::vector<uint64_t> offs;
+  iov_offsets(lens, n, &offs);
+  hipError_t e;
+  if ((e = c->d_meta.reserve(n * 12ull + 64))) return ctx->hip_fail(e, "meta");
+  if (n) {
+    int rc = stage_host_batch(ctx, files, offs.data(), n);
+    if (rc) return rc;
+    uint8_t* mb = c->d_meta.as<uint8_t>();
+    if ((e = hipMemcpyAsync(mb, file_version, n * 8ull, hipMemcpyHostToDevice, ctx->stream)) ||
+        (e = hipMemcpyAsync(mb + 8ull * n, file_actor, n * 4ull, hipMemcpyHostToDevice, ctx->stream)))
+      return ctx->hip_fail(e, "meta upload");
+  }
+  const uint8_t* mb = c->d_meta.as<uint8_t>();
+  return ce_core_compact_ops_device(c, ctx->blob.as<uint8_t>(), ctx->offs.as<uint64_t>(), n, offs[n],
+                                    actors, m, reinterpret_cast<const uint32_t*>(mb + 8ull * n),
+                                    reinterpret_cast<const uint64_t*>(mb), nonce, file, name_out);
 }
 
 int ce_core_ingest_states(ce_core* c, const uint8_t* blob, const uint64_t* offs, uint32_t n,
@@ -1544,6 +1592,95 @@ int ce_core_apply_ops(ce_core* c, const uint8_t* ops, size_t len) {
   // state.apply(op) for op in ops (lib.rs:710-712)
   if ((rc = ds ? ds_apply_local_ops(c, ops, len) : merge_dots_host(c, dots))) return rc;
   c->nov[s] = version + 1;                         // next_op_versions.inc(actor) (lib.rs:714-715)
+  return table_upload(c);
+}
+
+// n successive Core::apply_ops calls (lib.rs:666-722) as one batch: every clear text
+// VersionBytes(current_data_version, ops_i) sealed by one GPU launch under the latest key, file i
+// stored as ops/<local actor>/<next_op_versions.get(actor) + i>, the ops applied in order and
+// next_op_versions bumped by n.  Every ops blob is decoded before anything is sealed or written.
+int ce_core_apply_ops_batch(ce_core* c, const uint8_t* ops, const uint64_t* offs, uint32_t n,
+                            const uint8_t* nonces, ce_buf* files, ce_buf* file_offs) {
+  if (!c || (n && (!ops || !offs))) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  (void)hipSetDevice(c->ctx->device);
+  ce_ctx* ctx = c->ctx;
+  if (!c->has_key) return ctx->fail(CE_ERR_NO_KEY, "no latest key");
+  const bool ds = is_dotset_kind(c->kind);
+  std::vector<Dots> dots(ds ? 0 : n);
+  for (uint32_t i = 0; i < n; i++) {
+    const uint8_t* p = ops + offs[i];
+    const size_t l = offs[i + 1] - offs[i];
+    if (ds) {
+      int rc = ds_check_ops(c, p, l);
+      if (rc) return rc;
+    } else if (!read_dots(p, l, &dots[i])) {
+      return ctx->fail(CE_ERR_DECODE, "ops are not a Vec<Dot<Uuid>>");
+    }
+  }
+  // clear text i = current_data_version || ops_i (lib.rs:670-671); file i = CURRENT_VERSION ||
+  // Cryptor::encrypt(clear_i) (lib.rs:682-695)
+  std::vector<uint64_t> coffs(n + 1), foffs(n + 1);
+  coffs[0] = foffs[0] = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    coffs[i + 1] = coffs[i] + 16 + (offs[i + 1] - offs[i]);
+    foffs[i + 1] = foffs[i] + 16 + sealed_len(16 + (offs[i + 1] - offs[i]));
+  }
+  std::vector<uint8_t> clear(coffs[n]);
+  for (uint32_t i = 0; i < n; i++) {
+    std::memcpy(clear.data() + coffs[i], c->current_data_version.data(), 16);
+    std::memcpy(clear.data() + coffs[i] + 16, ops + offs[i], offs[i + 1] - offs[i]);
+  }
+  std::vector<uint8_t> nb;
+  if (!nonces) {
+    nb.resize(24ull * n + 1);
+    os_random(nb.data(), 24ull * n);
+    nonces = nb.data();
+  }
+  std::vector<uint8_t> out(foffs[n]);
+  if (n) {
+    hipError_t e;
+    if ((e = ctx->blob.reserve(coffs[n] + 64)) || (e = ctx->offs.reserve((n + 1) * 8ull)) ||
+        (e = ctx->out_offs.reserve((n + 1) * 8ull)) || (e = ctx->nonces.reserve(24ull * n)) ||
+        (e = ctx->out.reserve(foffs[n] + 64)) || (e = ctx->outer_ver.reserve(64)))
+      return ctx->hip_fail(e, "apply_ops_batch reserve");
+    if ((e = hipMemcpyAsync(ctx->blob.p, clear.data(), coffs[n], hipMemcpyHostToDevice, ctx->stream)) ||
+        (e = hipMemcpyAsync(ctx->offs.p, coffs.data(), (n + 1) * 8ull, hipMemcpyHostToDevice, ctx->stream)) ||
+        (e = hipMemcpyAsync(ctx->out_offs.p, foffs.data(), (n + 1) * 8ull, hipMemcpyHostToDevice, ctx->stream)) ||
+        (e = hipMemcpyAsync(ctx->nonces.p, nonces, 24ull * n, hipMemcpyHostToDevice, ctx->stream)) ||
+        (e = hipMemcpyAsync(ctx->outer_ver.p, kCoreVersion, 16, hipMemcpyHostToDevice, ctx->stream)))
+      return ctx->hip_fail(e, "apply_ops_batch upload");
+    int rc = device_seal(ctx, ctx->blob.as<uint8_t>(), ctx->offs.as<uint64_t>(), n, coffs[n],
+                         ctx->outer_ver.as<uint8_t>(), ctx->nonces.as<uint8_t>(), ctx->out.as<uint8_t>(),
+                         ctx->out_offs.as<uint64_t>(), key_of(c));
+    if (rc) return rc;
+    if ((e = hipMemcpyAsync(out.data(), ctx->out.p, foffs[n], hipMemcpyDeviceToHost, ctx->stream)) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+      return ctx->hip_fail(e, "apply_ops_batch download");
+  }
+  uint32_t s;
+  int rc = insert_actor(c, c->local_actor, &s);
+  if (rc) return rc;
+  const uint64_t v0 = c->nov[s];  // next_op_versions.get(actor) (lib.rs:703)
+  for (uint32_t i = 0; i < n; i++) {
+    if (c->storage && (rc = storage_store_op(c->storage, c->local_actor, v0 + i, out.data() + foffs[i],
+                                             foffs[i + 1] - foffs[i])))
+      return ctx->fail(rc, "failed writing ops file");
+    // state.apply(op) for op in ops (lib.rs:710-712), then next_op_versions.inc (lib.rs:714-715)
+    if ((rc = ds ? ds_apply_local_ops(c, ops + offs[i], offs[i + 1] - offs[i]) : merge_dots_host(c, dots[i])))
+      return rc;
+    c->nov[s] = v0 + i + 1;
+  }
+  if (files) {
+    files->data = (uint8_t*)malloc(out.size() ? out.size() : 1);
+    std::memcpy(files->data, out.data(), out.size());
+    files->len = out.size();
+  }
+  if (file_offs) {
+    file_offs->data = (uint8_t*)malloc((n + 1) * 8ull);
+    std::memcpy(file_offs->data, foffs.data(), (n + 1) * 8ull);
+    file_offs->len = (n + 1) * 8ull;
+  }
   return table_upload(c);
 }
 

@@ -305,6 +305,7 @@ void ce_ctx_destroy(ce_ctx* c) {
   for (auto& t : c->timed) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   if (c->setup_ev) (void)hipEventDestroy(c->setup_ev);
+  destroy_uploader(c);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }

@@ -66,6 +66,10 @@ struct OpenResult {
 
 }  // namespace ce
 
+namespace ce {
+struct Uploader;  // ce_upload.cpp: pinned staging ring + copy stream + host thread pool
+}
+
 struct ce_storage {
   std::string local, remote;  // crdt-enc-tokio Storage{local_path, remote_path} (lib.rs:22-26)
 };
@@ -82,6 +86,7 @@ struct ce_ctx {
   ce::HostBuf h_counters, h_apply, h_stage, h_stage2;
   // marks the setup kernel's counter snapshot (h_counters + 128) as landed on the host
   hipEvent_t setup_ev = nullptr;
+  ce::Uploader* up = nullptr;  // host-buffer entry points (created on first use)
   // kernel timing (ce_ctx_set_timing)
   bool timing = false;
   struct TimedLaunch {
@@ -151,5 +156,10 @@ int seal_one(ce_ctx* ctx, const KeyRef& key, const uint8_t* outer_version, const
              const uint8_t* prefix16 = nullptr);
 
 uint32_t grid_waves_for(uint32_t work);
+
+// ce_upload.cpp: host files -> ctx->blob / ctx->offs through the pinned staging ring (ordered
+// before later work on ctx->stream, no host synchronise)
+int stage_host_batch(ce_ctx* ctx, const uint8_t* const* files, const uint64_t* offs, uint32_t n);
+void destroy_uploader(ce_ctx* ctx);
 
 }  // namespace ce

@@ -221,6 +221,14 @@ int ce_core_read_remote(ce_core *c);
 int ce_core_compact(ce_core *c, char name_out[64]);
 /* Core::apply_ops (lib.rs:666-722): ops = rmp-serde msgpack of Vec<S::Op> (Vec<Dot<Uuid>>). */
 int ce_core_apply_ops(ce_core *c, const uint8_t *ops, size_t len);
+/* n successive Core::apply_ops calls (lib.rs:666-722) as one batch: ops i =
+ * ops[offs[i], offs[i+1]) (offs: n+1 entries); every clear text sealed by one GPU launch; file i
+ * stored (with storage) as ops/<local actor>/<next_op_versions.get(actor) + i>; the ops applied
+ * in order; next_op_versions bumped by n.  All n ops blobs are decoded before anything is sealed
+ * or written.  nonces: n*24 bytes or NULL (OS RNG).  files / file_offs (may be NULL) receive
+ * the op files back to back and their n+1 u64 offsets (what Storage::store_ops got). */
+int ce_core_apply_ops_batch(ce_core *c, const uint8_t *ops, const uint64_t *offs, uint32_t n,
+                            const uint8_t *nonces, ce_buf *files, ce_buf *file_offs);
 /* rmp_serde::to_vec_named(&StateWrapper) (lib.rs:336, 739-743) */
 int ce_core_state_bytes(ce_core *c, ce_buf *out);
 /* Back to the empty StateWrapper (Default, lib.rs:240-243), keeping registered actors and the
@@ -244,6 +252,13 @@ int ce_core_ingest_ops_device(ce_core *c, const uint8_t *d_blob, const uint64_t 
                               uint32_t n, uint64_t blob_len, const uint8_t *actors, uint32_t m,
                               const uint32_t *d_file_actor, const uint64_t *d_file_version,
                               int32_t *status);
+/* The same from the per-file host buffers Storage::load_ops returns (one Vec<u8> per file,
+ * crdt-enc-tokio/src/lib.rs:222-278): files[i] holds lens[i] bytes.  The files are gathered
+ * into pinned staging chunks by host threads and DMA'd while the next chunk fills; no
+ * concatenated copy is needed on the caller's side. */
+int ce_core_ingest_ops_iov(ce_core *c, const uint8_t *const *files, const size_t *lens, uint32_t n,
+                           const uint8_t *actors, uint32_t m, const uint32_t *file_actor,
+                           const uint64_t *file_version, int32_t *status);
 /* What read_remote_states does after Storage::load_states (lib.rs:425-466). */
 int ce_core_ingest_states(ce_core *c, const uint8_t *blob, const uint64_t *offs, uint32_t n,
                           int32_t *status);
@@ -256,6 +271,12 @@ int ce_core_compact_ops_device(ce_core *c, const uint8_t *d_blob, const uint64_t
                                uint64_t blob_len, const uint8_t *actors, uint32_t m,
                                const uint32_t *d_file_actor, const uint64_t *d_file_version,
                                const uint8_t *nonce, ce_buf *file, char name_out[64]);
+/* ce_core_compact_ops_device over per-file host buffers (upload as ce_core_ingest_ops_iov,
+ * then the device path; file_actor / file_version are host arrays). */
+int ce_core_compact_ops_iov(ce_core *c, const uint8_t *const *files, const size_t *lens, uint32_t n,
+                            const uint8_t *actors, uint32_t m, const uint32_t *file_actor,
+                            const uint64_t *file_version, const uint8_t *nonce, ce_buf *file,
+                            char name_out[64]);
 /* compact() without storage: serialize the state, seal it on the GPU with the latest key and
  * return the state file bytes and its content name.  nonce: 24 bytes or NULL (OS RNG). */
 int ce_core_compact_to_buffer(ce_core *c, const uint8_t *nonce, ce_buf *file, char name_out[64]);

@@ -784,3 +784,131 @@ def test_exotic_envelope_new_actors(ctx, oracle, n_new):
     assert (rc, st) == (orc, ost)
     assert core.state_bytes() == oc.serialize()
     core.close()
+
+
+def test_concurrent_decrypts_one_context(ctx, oracle):
+    """include/crdtenc.h: entry points are thread-safe per context.  The reference issues up to
+    16 decrypts at once (buffered(16), crdt-enc/src/lib.rs:452,512): 16 threads x 8 calls of
+    ce_cryptor_decrypt (ctypes drops the GIL) plus a batch ingest on the same context, every
+    result == the oracle's."""
+    from concurrent.futures import ThreadPoolExecutor
+    rng = random.Random(1616)
+    key = rng.randbytes(32)
+    items = []
+    for i in range(128):
+        pt = rng.randbytes(rng.choice([0, 1, 63, 64, 65, 1000, 4096, 20000]))
+        enc = ctx.encrypt(key, pt, nonce=rng.randbytes(24))
+        if i % 11 == 5:
+            b = bytearray(enc)
+            b[-1] ^= 0x40
+            enc = bytes(b)
+        items.append(enc)
+    want = [oracle.cryptor_decrypt(key, e) for e in items]
+    files, actors, fa, vers = make_ops_batch(ctx, key, 9, 5, 17, seed=16)
+    oc = oracle.Core()
+    assert oc.read_remote_ops(key, [APP], files, [actors[i] for i in fa], vers)[0] == 0
+
+    def one(i):
+        return ctx.decrypt(key, items[i])
+
+    def ingest():
+        core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+        core.set_latest_key(key)
+        rc, _ = core.ingest_ops(files, actors, fa, vers)
+        out = (rc, core.state_bytes())
+        core.close()
+        return out
+
+    with ThreadPoolExecutor(16) as pool:
+        futs = [pool.submit(one, i) for i in range(len(items))]
+        ing = [pool.submit(ingest) for _ in range(3)]
+        got = [f.result() for f in futs]
+        ingested = [f.result() for f in ing]
+    for (st, pt), (wst, wpt) in zip(got, want):
+        assert st == wst
+        if st == 0:
+            assert pt == wpt
+    for rc, sb in ingested:
+        assert rc == 0 and sb == oc.serialize()
+
+
+def test_c1_three_replicas_1k_ops(ctx, tmp_path, oracle):
+    """BASELINE C1 at its stated size: 3 replicas (actors) share a remote dir and write ~1k ops
+    (Core::apply_ops, lib.rs:666-722: batched with ce_core_apply_ops_batch and single calls
+    mixed), whose Dots name 800 distinct actors (table growth; a ~25 KB state file sealed and
+    opened in several 16 KiB segments).  Every replica's read_remote folds to the oracle's
+    state; compact (ingest format) + a fresh replica reproduce it (lib.rs:332-380, 390-547)."""
+    rng = random.Random(1000)
+    key = rng.randbytes(32)
+    remote = str(tmp_path / "remote")
+    pool = [rng.randbytes(16) for _ in range(800)]
+    cores = []
+    for r in range(3):
+        cores.append(crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP],
+                                  current_data_version=APP, local_path=str(tmp_path / ("l%d" % r)),
+                                  remote_path=remote,
+                                  flags=crdtenc.OPEN_CREATE | crdtenc.COMPACT_INGEST_FORMAT))
+        cores[-1].set_latest_key(key)
+    acts = [c.info_actor() for c in cores]
+    written = {a: [] for a in acts}
+    for r, c in enumerate(cores):
+        total = 0
+        while total < 333:
+            k = rng.choice([1, 7, 40])
+            ops = [msgpack.packb([{"actor": rng.choice(pool + [acts[r]] * 50), "counter": rng.getrandbits(40) + 1}
+                                  for _ in range(rng.randint(1, 4))], use_bin_type=True) for _ in range(k)]
+            if k == 1:
+                assert c.apply_ops(ops[0]) == 0
+                written[acts[r]].append(None)
+            else:
+                rc, files = c.apply_ops_batch(ops, nonces=[rng.randbytes(24) for _ in ops])
+                assert rc == 0 and len(files) == k
+                written[acts[r]].extend(files)
+            total += k
+    st = crdtenc.Storage(str(tmp_path / "l0"), remote)
+    loaded = st.load_ops([(a, 0) for a in acts])
+    assert sum(len(v) for v in written.values()) == len(loaded)
+    # what apply_ops_batch returned is what Storage::store_ops wrote
+    for a, files in written.items():
+        on_disk = [x[2] for x in loaded if x[0] == a]
+        assert all(f is None or f == d for f, d in zip(files, on_disk))
+    oc = oracle.Core()
+    assert oc.read_remote_ops(key, [APP], [x[2] for x in loaded], [x[0] for x in loaded],
+                              [x[1] for x in loaded])[0] == 0
+    for c in cores:
+        assert c.read_remote() == 0
+        assert c.state_bytes() == oc.serialize()
+    assert len(oc.serialize()) > 20000
+    rc, name = cores[1].compact()
+    assert rc == 0 and st.list_state_names() == [name]
+    fresh = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP,
+                         local_path=str(tmp_path / "l9"), remote_path=remote, flags=crdtenc.OPEN_CREATE)
+    fresh.set_latest_key(key)
+    assert fresh.read_remote() == 0
+    assert fresh.state_bytes() == oc.serialize()
+    for c in cores + [fresh]:
+        c.close()
+
+
+def test_host_iov_ingest_matches_device(ctx, oracle):
+    """ce_core_ingest_ops_iov (per-file host buffers, pinned staging ring + copy stream) and
+    the contiguous ce_core_ingest_ops == the oracle, here with 8 KiB chunks so files straddle
+    chunk boundaries and the two staging buffers are reused many times (a fresh context picks
+    CE_UPLOAD_CHUNK up when its uploader is created)."""
+    os.environ["CE_UPLOAD_CHUNK"] = "8192"
+    try:
+        c2 = crdtenc.Context(0)
+        key = os.urandom(32)
+        files, actors, fa, vers = make_ops_batch(c2, key, 13, 7, 31, seed=77, stress=True)
+        oc = oracle.Core()
+        orc, ost = oc.read_remote_ops(key, [APP], files, [actors[i] for i in fa], vers)
+        for fn in ("ingest_ops_iov", "ingest_ops"):
+            core = crdtenc.Core(c2, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+            core.set_latest_key(key)
+            rc, st = getattr(core, fn)(files, actors, fa, vers)
+            assert (rc, st) == (orc, ost) and rc == 0
+            assert core.state_bytes() == oc.serialize()
+            core.close()
+        c2.close()
+    finally:
+        del os.environ["CE_UPLOAD_CHUNK"]
