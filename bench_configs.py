@@ -172,7 +172,7 @@ def run_c3(args, ctx, dev):
     from concurrent.futures import ThreadPoolExecutor
     # SHA3-256 is a sequential sponge (~200 MB/s per core): one 8 MB name takes about as long
     # as the rest of a step, so two host threads hash consecutive steps' files side by side
-    NB = 3
+    NB = 6
     namer = ThreadPoolExecutor(NB - 1)
     names = []
     obuf = [np.empty(1 << 20, np.uint8) for _ in range(NB)]
@@ -477,7 +477,7 @@ def main():
     ap.add_argument("--c5-versions", type=int, default=256, help="C5 versions per actor (4096 actors)")
     ap.add_argument("--c5-clean", action="store_true",
                     help="C5 control: every file under the latest key, none tampered (accept path)")
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--versions", type=int, default=16, help="op-file versions per actor")
     ap.add_argument("--state-versions", type=int, default=4, help="versions folded into states")

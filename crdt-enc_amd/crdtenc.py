@@ -49,6 +49,7 @@ EXPORTS = [
     "ce_keys_decode", "ce_keys_from_remote_metas", "ce_keys_merge", "ce_keys_free",
     "ce_keys_count", "ce_keys_latest", "ce_keys_get", "ce_keys_at", "ce_core_set_keys",
     "ce_core_apply_ops_batch", "ce_core_ingest_ops_iov", "ce_core_compact_ops_iov",
+    "ce_core_path_count",
 ]
 
 
@@ -99,6 +100,7 @@ def lib():
         L.ce_cryptor_sealed_len.argtypes = [ctypes.c_size_t]
         L.ce_core_dense_capacity.restype = ctypes.c_uint32
         L.ce_keys_count.restype = ctypes.c_uint32
+        L.ce_core_path_count.restype = ctypes.c_uint64
         L.ce_vbuf_remaining.restype = ctypes.c_size_t
         L.ce_vbuf_chunk.restype = ctypes.c_size_t
         L.ce_vbuf_chunks_vectored.restype = ctypes.c_size_t
@@ -633,6 +635,9 @@ class Core:
 
     def dense_capacity(self):
         return lib().ce_core_dense_capacity(self.p)
+
+    def path_count(self, path):
+        return lib().ce_core_path_count(self.p, path.encode())
 
     def dense_ready(self):
         """True when export/import_dense can carry the whole state (no unregistered actor)."""

@@ -1025,6 +1025,31 @@ int ingest_states_host(ce_core* c, const uint8_t* blob, const uint64_t* offs, ui
       break;
     }
   std::vector<FileParams> P(n);
+  if (c->kind == CE_STATE_ORSWOT && !getenv("CE_HOST_STATES")) {
+    // plaintexts stay in HBM: the device reader decodes canonical states (ce_dotset_io.hip)
+    if ((e = hipMemcpyAsync(P.data(), ctx->params.p, n * sizeof(FileParams), hipMemcpyDeviceToHost, ctx->stream)) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+      return ctx->hip_fail(e, "states params");
+    std::vector<uint64_t> off(n, 0), len(n, 0);
+    std::vector<uint8_t> ver(16ull * n);
+    for (uint32_t i = 0; i < n; i++) {
+      if (st[i] != CE_OK) continue;
+      if (P[i].len < 16) { st[i] = CE_ERR_PT_LEN; continue; }
+      if ((e = hipMemcpyAsync(ver.data() + 16ull * i, ctx->out.as<uint8_t>() + P[i].out_off, 16,
+                              hipMemcpyDeviceToHost, ctx->stream)))
+        return ctx->hip_fail(e, "states version");
+      off[i] = P[i].out_off + 16;
+      len[i] = P[i].len - 16;
+    }
+    if ((e = hipStreamSynchronize(ctx->stream))) return ctx->hip_fail(e, "states version");
+    for (uint32_t i = 0; i < n; i++) {
+      if (st[i] != CE_OK) continue;
+      Uuid v;
+      std::memcpy(v.data(), ver.data() + 16ull * i, 16);
+      if (!std::binary_search(c->supported.begin(), c->supported.end(), v)) st[i] = CE_ERR_PT_VERSION;
+    }
+    return ds_merge_states_device(c, ctx->out.as<uint8_t>(), off, len, st.data(), status_out);
+  }
   std::vector<uint8_t> out(blen + 16ull * n + 64);
   if ((e = hipMemcpyAsync(P.data(), ctx->params.p, n * sizeof(FileParams), hipMemcpyDeviceToHost,
                           ctx->stream)) ||
@@ -1232,6 +1257,12 @@ int compact_bytes(ce_core* c, const uint8_t* nonce, std::vector<uint8_t>* file) 
   HostPhase hp("compact_bytes");
   if (!c->has_key) return c->ctx->fail(CE_ERR_NO_KEY, "no latest key");
   if (!is_dotset_kind(c->kind) && !c->host_compact) return compact_device(c, nonce, file);
+  if (c->kind == CE_STATE_ORSWOT && !c->host_compact) {
+    // entries serialized, sealed and downloaded once on the device (ce_dotset_io.hip)
+    const bool ingest_fmt = (c->flags & CE_COMPACT_INGEST_FORMAT) != 0;
+    return ds_compact_device(c, c->ctx, ingest_fmt ? kCoreVersion : c->current_data_version.data(),
+                             ingest_fmt ? c->current_data_version.data() : nullptr, nonce, key_of(c), file);
+  }
   std::vector<uint8_t>& clear = c->ser_buf;
   int rc = serialize_state(c, &clear);
   if (rc) return rc;
@@ -1714,6 +1745,13 @@ int ce_core_register_actors(ce_core* c, const uint8_t* actors, uint32_t m) {
 }
 
 uint32_t ce_core_dense_capacity(ce_core* c) { return c ? c->cap : 0; }
+
+uint64_t ce_core_path_count(ce_core* c, const char* path) {
+  if (!c || !path) return 0;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  auto it = c->path_counts.find(path);
+  return it == c->path_counts.end() ? 0 : it->second;
+}
 
 int ce_core_dense_ready(ce_core* c) {
   if (!c || is_dotset_kind(c->kind)) return 0;

@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <functional>
+#include <map>
 #include <set>
 #include <string>
 #include <utility>
@@ -55,6 +56,7 @@ struct ce_core {
   uint8_t key_version[16] = {0};
   std::vector<uint8_t> key;
   std::vector<ce::AltKey> alt_keys;  // tried in id order on AUTH failures (CE_OPEN_MULTI_KEY)
+  std::map<std::string, uint64_t> path_counts;  // which code path ran (ce_core_path_count)
   // actor table: UUID -> hash slot; ActorSlot.pad[0] holds the actor's stable id (insertion
   // order, survives table growth) used by the dot-set kinds' device arrays.
   uint32_t cap = 0, size = 0, registered = 0;
@@ -169,6 +171,10 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
                   const uint64_t* d_fv, int32_t* status_out);
 // read_remote_states after load_states; plaintext StateWrappers (after the data version)
 // sws[i] = {nullptr, 0} for files whose status st[i] is already a failure.
+int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t* prefix16,
+                      const uint8_t* nonce, const KeyRef& key, std::vector<uint8_t>* file);
+int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uint64_t>& off,
+                           const std::vector<uint64_t>& len, int32_t* st, int32_t* status_out);
 int ds_merge_states(ce_core* c, const std::vector<std::pair<const uint8_t*, size_t>>& sws,
                     int32_t* st, int32_t* status_out);
 int ds_serialize(ce_core* c, std::vector<uint8_t>* out);

@@ -20,6 +20,7 @@
 #include "ce_core.h"
 #include "ce_dotset.h"
 #include "ce_dotset_codec.h"
+#include "ce_dotset_io.h"
 
 namespace ce {
 
@@ -42,6 +43,11 @@ struct DsState {
       cub_tmp, deferred_flags, d0[5], col[6], mv[6], other[4], oclock;
   DevBuf misses;
   HostBuf h_cnt;
+  // device state reader (per state file: candidates, sorted heads, entry ends, Dot counts and
+  // bases, members, sorted members) and device writer scratch
+  std::vector<std::array<DevBuf, 7>> rd;
+  DevBuf rd_tmp, rd_misc, ser[16], uuid_of_id, rank_of_id;
+  uint64_t uuid_ids = ~0ull;  // id count uuid_of_id / rank_of_id were built for
 };
 
 void ds_free(DsState* d) { delete d; }
@@ -1020,6 +1026,9 @@ int id_dots(ce_core* c, Dots d, IdDots* out) {
   return CE_OK;
 }
 
+int orswot_merge_cols(ce_core* c, const IdDots& oclock,
+                      const std::vector<std::pair<IdDots, std::vector<uint64_t>>>& od, uint32_t n);
+
 // Orswot::merge(other) on the device (entries) and host (deferred)
 int orswot_merge_one(ce_core* c, const HostState& hs) {
   DsState* d = c->ds;
@@ -1063,19 +1072,32 @@ int orswot_merge_one(ce_core* c, const HostState& hs) {
   }
   if ((rc = table_upload(c)) || (rc = ensure_clock(c)) || (rc = ensure_pairs(c, mem.size()))) return rc;
   hipError_t e;
-  const uint32_t cap = d->clock_cap;
-  std::vector<unsigned long long> oc(cap, 0);
-  for (auto& x : oclock) oc[x.first] = x.second;
   if ((e = d->other[0].reserve(mem.size() * 8 + 8)) || (e = d->other[1].reserve(act.size() * 4 + 4)) ||
       (e = d->other[2].reserve(val.size() * 8 + 8)))
     return ctx->hip_fail(e, "merge");
   if ((e = up(d->other[0].as<unsigned long long>(), mem, s)) || (e = up(d->other[1].as<uint32_t>(), act, s)) ||
-      (e = up(d->other[2].as<unsigned long long>(), val, s)) ||
-      (e = up(d->oclock.as<unsigned long long>(), oc, s)))
+      (e = up(d->other[2].as<unsigned long long>(), val, s)))
     return ctx->hip_fail(e, "merge");
+  return orswot_merge_cols(c, oclock, od, (uint32_t)mem.size());
+}
+
+// Orswot::merge(other) with other's entries already in d->other[0..2] as (member, actor id,
+// counter) columns of n pairs, its clock and deferred removals by actor id
+int orswot_merge_cols(ce_core* c, const IdDots& oclock,
+                      const std::vector<std::pair<IdDots, std::vector<uint64_t>>>& od, uint32_t n) {
+  DsState* d = c->ds;
+  ce_ctx* ctx = c->ctx;
+  hipStream_t s = ctx->stream;
+  int rc;
+  if ((rc = ensure_clock(c))) return rc;
+  hipError_t e;
+  const uint32_t cap = d->clock_cap;
+  std::vector<unsigned long long> oc(cap, 0);
+  for (auto& x : oclock) oc[x.first] = x.second;
+  if ((e = up(d->oclock.as<unsigned long long>(), oc, s))) return ctx->hip_fail(e, "merge");
   const int tm = ctx->tbegin("ds_merge");
   if ((e = launch_ds_put_other(s, tables(d), d->other[0].as<unsigned long long>(), d->other[1].as<uint32_t>(),
-                               d->other[2].as<unsigned long long>(), (uint32_t)mem.size())) ||
+                               d->other[2].as<unsigned long long>(), n)) ||
       (e = launch_ds_merge(s, tables(d), d->clock.as<unsigned long long>(), d->oclock.as<unsigned long long>())))
     return ctx->hip_fail(e, "merge");
   ctx->tend(tm);
@@ -1123,6 +1145,245 @@ int mvreg_merge_one(ce_core* c, const HostState& hs) {
 }
 
 }  // namespace
+
+// ---------------------------------------------------------------------------------------
+// read_remote_states for Orswot with the plaintexts left in HBM (ce_dotset_io.hip reader)
+// ---------------------------------------------------------------------------------------
+namespace {
+
+bool key_is(Rd& r, const char* name) {
+  int kind;
+  uint64_t off, len;
+  if (r.i >= r.n || !is_binstr_marker(r.p[r.i]) || !rd_binstr(r, &kind, &off, &len)) return false;
+  return len == std::strlen(name) && std::memcmp(r.p + off, name, len) == 0;
+}
+
+// canonical StateWrapper<Orswot> head: map(2) "next_op_versions" VClock "state" map(3) "clock"
+// VClock "entries" map(N) -> body offset.  0 = parsed, 1 = not the canonical layout (host
+// parser), 2 = ran out of bytes (fetch a longer prefix)
+int parse_state_prefix(const uint8_t* p, size_t n, bool whole, HostState* hs, uint64_t* body,
+                       uint64_t* n_entries) {
+  Rd r{p, n, 0};
+  uint64_t cnt;
+  auto fail = [&]() { return whole ? 1 : 2; };
+  hs->nov.clear();
+  hs->clock.clear();
+  if (!rd_map_hdr(r, &cnt)) return fail();
+  if (cnt != 2) return 1;
+  if (!key_is(r, "next_op_versions")) return r.i >= r.n ? fail() : 1;
+  if (!read_vclock(r, &hs->nov)) return fail();
+  if (!key_is(r, "state")) return r.i >= r.n ? fail() : 1;
+  if (!rd_map_hdr(r, &cnt)) return fail();
+  if (cnt != 3) return 1;
+  if (!key_is(r, "clock")) return r.i >= r.n ? fail() : 1;
+  if (!read_vclock(r, &hs->clock)) return fail();
+  if (!key_is(r, "entries")) return r.i >= r.n ? fail() : 1;
+  if (r.i >= r.n) return fail();
+  if (!rd_map_hdr(r, n_entries)) return fail();
+  *body = r.i;
+  return 0;
+}
+
+// "deferred" map(k) { VClock: [members] } after the entries
+bool parse_state_tail(const uint8_t* p, size_t n, HostState* hs) {
+  Rd r{p, n, 0};
+  uint64_t cnt;
+  if (!key_is(r, "deferred") || !rd_map_hdr(r, &cnt) || cnt > r.n) return false;
+  hs->deferred.clear();
+  for (uint64_t k = 0; k < cnt; k++) {
+    Dots key;
+    std::vector<uint64_t> ms;
+    if (!read_vclock(r, &key) || !read_members(r, &ms)) return false;
+    hs->deferred.push_back({key, ms});
+  }
+  return true;
+}
+
+struct DevState {
+  bool device = false;
+  uint64_t pt = 0;      // plaintext offset (past the 16-byte data version) in ctx->out
+  uint64_t len = 0;
+  uint64_t body = 0;
+  uint32_t n_entries = 0, n_dots = 0;
+  HostState hs;
+};
+
+hipError_t dl(void* dst, const void* src, size_t n, hipStream_t s) {
+  hipError_t e = hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, s);
+  return e ? e : hipStreamSynchronize(s);
+}
+
+OrswotReadArgs read_args(ce_core* c, DsState* d, size_t f, const DevState& ds, const uint8_t* out,
+                         uint32_t cap) {
+  OrswotReadArgs a{};
+  a.s = out + ds.pt;
+  a.lo = ds.body;
+  a.hi = ds.len;
+  auto& b = d->rd[f];
+  a.cand_raw = b[0].as<uint32_t>();
+  a.n_cand_dev = d->rd_misc.as<uint32_t>() + 2 * f;
+  a.flags = d->rd_misc.as<uint32_t>() + 2 * f + 1;
+  a.cap = cap;
+  a.n_cand = ds.n_entries;
+  a.cand = b[1].as<uint32_t>();
+  a.end = b[2].as<uint32_t>();
+  a.ndots = b[3].as<uint32_t>();
+  a.dbase = b[4].as<uint32_t>();
+  a.member = b[5].as<unsigned long long>();
+  a.msort = b[6].as<unsigned long long>();
+  a.table = c->d_table.as<ActorSlot>();
+  a.mask = c->cap - 1;
+  return a;
+}
+
+}  // namespace
+
+// files i = plaintexts at out + off[i] (after the 16-byte data version), len[i] bytes, st[i] =
+// status so far.  Canonical Orswot states are decoded on the device; others go to read_state.
+int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uint64_t>& off,
+                           const std::vector<uint64_t>& len, int32_t* st, int32_t* status_out) {
+  DsState* d = c->ds;
+  ce_ctx* ctx = c->ctx;
+  hipStream_t s = ctx->stream;
+  const size_t n = off.size();
+  std::vector<DevState> ds(n);
+  std::vector<std::vector<uint8_t>> host_pt(n);
+  hipError_t e;
+  if (d->rd.size() < n) d->rd.resize(n);
+  if ((e = d->rd_misc.reserve(8ull * n + 64)) || (e = hipMemsetAsync(d->rd_misc.p, 0, 8ull * n, s)))
+    return ctx->hip_fail(e, "state reader");
+  auto host_parse = [&](size_t i) -> int {  // the whole plaintext through read_state
+    ds[i].device = false;
+    c->path_counts["states_host_parse"]++;
+    host_pt[i].resize(len[i]);
+    if (len[i] && (e = dl(host_pt[i].data(), out + off[i], len[i], s))) return ctx->hip_fail(e, "state download");
+    ds[i].hs = HostState();
+    if (!read_state(c->kind, host_pt[i].data(), len[i], &ds[i].hs)) st[i] = CE_ERR_DECODE;
+    return CE_OK;
+  };
+  int first = CE_OK;
+  {
+    HostPhase hp("states: device read");
+    std::vector<uint8_t> pre;
+    for (size_t i = 0; i < n; i++) {
+      if (st[i] != CE_OK) continue;
+      DevState& x = ds[i];
+      x.pt = off[i];
+      x.len = len[i];
+      // 1) the head on the host: a prefix long enough for next_op_versions and the clock
+      uint64_t want = std::min<uint64_t>(len[i], 1u << 18), body = 0, ne = 0;
+      int pr;
+      for (;;) {
+        pre.resize(want);
+        if (want && (e = dl(pre.data(), out + off[i], want, s))) return ctx->hip_fail(e, "state head");
+        pr = parse_state_prefix(pre.data(), want, want == len[i], &x.hs, &body, &ne);
+        if (pr != 2) break;
+        want = std::min<uint64_t>(len[i], want * 4);
+      }
+      if (pr != 0 || ne == 0 || ne > 0xffffffffull || len[i] > 0xffffffffull) {
+        int rc = host_parse(i);
+        if (rc) return rc;
+        continue;
+      }
+      x.body = body;
+      x.n_entries = (uint32_t)ne;
+      // 2) entry heads (search covers the deferred map too: its VClock keys look alike)
+      const uint32_t cap = (uint32_t)std::min<uint64_t>(ne + 65536, len[i] / 7 + 1);
+      auto& b = d->rd[i];
+      if ((e = b[0].reserve(4ull * cap + 64)) || (e = b[1].reserve(4ull * cap + 64)) ||
+          (e = b[2].reserve(4ull * ne + 64)) || (e = b[3].reserve(4ull * ne + 64)) ||
+          (e = b[4].reserve(4ull * ne + 64)) || (e = b[5].reserve(8ull * ne + 64)) ||
+          (e = b[6].reserve(8ull * ne + 64)) || (e = d->rd_tmp.reserve(orswot_read_tmp_bytes(cap))))
+        return ctx->hip_fail(e, "state reader");
+      OrswotReadArgs a = read_args(c, d, i, x, out, cap);
+      uint32_t found[2];
+      if ((e = launch_orswot_read(s, a, d->rd_tmp.p, d->rd_tmp.cap, 0)) ||
+          (e = dl(found, d->rd_misc.as<uint32_t>() + 2 * i, 8, s)))
+        return ctx->hip_fail(e, "state reader");
+      if (found[0] < ne || found[0] > cap) {  // fewer heads than entries, or the list overflowed
+        int rc = host_parse(i);
+        if (rc) return rc;
+        continue;
+      }
+      // 3) the first N heads in position order are the entries: parse, chain, repeats, scan
+      a.n_cand = found[0];
+      {
+        size_t tb = d->rd_tmp.cap;
+        if ((e = hipcub_sort_u32(d->rd_tmp.p, tb, a.cand_raw, a.cand, found[0], s)))
+          return ctx->hip_fail(e, "state reader");
+      }
+      a.n_cand = x.n_entries;
+      uint32_t tail[4];
+      if ((e = launch_orswot_read(s, a, d->rd_tmp.p, d->rd_tmp.cap, 1)) ||
+          (e = hipMemcpyAsync(tail, a.end + ne - 1, 4, hipMemcpyDeviceToHost, s)) ||
+          (e = hipMemcpyAsync(tail + 1, a.dbase + ne - 1, 4, hipMemcpyDeviceToHost, s)) ||
+          (e = hipMemcpyAsync(tail + 2, a.ndots + ne - 1, 4, hipMemcpyDeviceToHost, s)) ||
+          (e = dl(tail + 3, a.flags, 4, s)))
+        return ctx->hip_fail(e, "state reader");
+      const uint64_t eend = x.body + (uint64_t)tail[0];
+      std::vector<uint8_t> tl;
+      bool ok = tail[3] == 0 && tail[0] != 0xffffffffu && eend <= len[i];
+      if (ok) {
+        tl.resize(len[i] - eend);
+        if (!tl.empty() && (e = dl(tl.data(), out + off[i] + eend, tl.size(), s))) return ctx->hip_fail(e, "state tail");
+        ok = parse_state_tail(tl.data(), tl.size(), &x.hs);
+      }
+      if (!ok) {
+        int rc = host_parse(i);
+        if (rc) return rc;
+        continue;
+      }
+      x.device = true;
+      x.n_dots = tail[1] + tail[2];
+      c->path_counts["states_device_read"]++;
+    }
+    for (size_t i = 0; i < n; i++)
+      if (st[i] != CE_OK && first == CE_OK) first = st[i];
+  }
+  if (status_out) std::memcpy(status_out, st, n * 4);
+  if (first != CE_OK) return first;  // nothing merged (lib.rs:431-456)
+  HostPhase hp("states: merge");
+  for (size_t i = 0; i < n; i++) {  // lib.rs:458-466, in order
+    int rc;
+    DevState& x = ds[i];
+    if (x.device) {
+      IdDots oclock;
+      std::vector<std::pair<IdDots, std::vector<uint64_t>>> od;
+      if ((rc = id_dots(c, x.hs.clock, &oclock))) return rc;
+      for (auto& y : x.hs.deferred) {
+        IdDots k;
+        if ((rc = id_dots(c, y.first, &k))) return rc;
+        od.push_back({k, y.second});
+      }
+      if ((rc = table_upload(c)) || (rc = ensure_pairs(c, x.n_dots))) return rc;
+      if ((e = d->other[0].reserve(8ull * x.n_dots + 8)) || (e = d->other[1].reserve(4ull * x.n_dots + 4)) ||
+          (e = d->other[2].reserve(8ull * x.n_dots + 8)))
+        return ctx->hip_fail(e, "merge");
+      OrswotReadArgs a = read_args(c, d, i, x, out, 0);
+      a.col_member = d->other[0].as<unsigned long long>();
+      a.col_actor = d->other[1].as<uint32_t>();
+      a.col_value = d->other[2].as<unsigned long long>();
+      uint32_t fl;
+      if ((e = launch_orswot_read(s, a, d->rd_tmp.p, d->rd_tmp.cap, 2)) || (e = dl(&fl, a.flags, 4, s)))
+        return ctx->hip_fail(e, "state reader");
+      if (fl == 0) {
+        if ((rc = orswot_merge_cols(c, oclock, od, x.n_dots))) return rc;
+      } else {  // an entry names an actor outside the table (not in the state's clock)
+        if ((rc = host_parse(i))) return rc;
+        if (st[i] != CE_OK) return c->ctx->fail(CE_ERR_DEVICE, "state reader and host parser disagree");
+        if ((rc = orswot_merge_one(c, x.hs))) return rc;
+      }
+    } else {
+      if ((rc = orswot_merge_one(c, x.hs))) return rc;
+    }
+    for (auto& y : x.hs.nov) {
+      uint32_t sl;
+      if ((rc = insert_actor(c, y.first, &sl))) return rc;
+      c->nov[sl] = std::max(c->nov[sl], y.second);
+    }
+  }
+  return table_upload(c);
+}
 
 int ds_merge_states(ce_core* c, const std::vector<std::pair<const uint8_t*, size_t>>& sws,
                     int32_t* st, int32_t* status_out) {
@@ -1198,6 +1459,162 @@ int ds_apply_local_ops(ce_core* c, const uint8_t* ops, size_t len) {
     return rc;
   if (c->kind == CE_STATE_ORSWOT) return orswot_fold(c, tot);
   return mvreg_commit(c, (uint32_t)base.v[kCntRm], (uint32_t)tot.v[kCntRm], true);
+}
+
+// Compaction of an Orswot state without bringing the entries to the host: the clear text
+// (prefix16 || to_vec_named(StateWrapper), the same bytes as ds_serialize) is written into
+// x->blob by the device writer (ce_dotset_io.hip) around a host-built head (next_op_versions,
+// clock) and tail (deferred), sealed on the device and downloaded once.
+int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t* prefix16,
+                      const uint8_t* nonce, const KeyRef& key, std::vector<uint8_t>* file) {
+  HostPhase hp("ds compact (device writer)");
+  c->path_counts["compact_device_writer"]++;
+  DsState* d = c->ds;
+  hipStream_t s = x->stream;
+  hipError_t e;
+  int rc;
+  auto uuid_dots = [&](const IdDots& v) {
+    Dots o;
+    for (auto& y : v) o.push_back({c->id_actor[y.first], y.second});
+    sort_dots(&o);
+    return o;
+  };
+  auto put_vclock = [](Wr& w, const Dots& v) {
+    w.map(1);
+    w.str("dots");
+    w.map(v.size());
+    for (auto& y : v) { w.bin(y.first.data(), 16); w.uint(y.second); }
+  };
+  // head: [prefix16] map(2) "next_op_versions" nov "state" map(3) "clock" clock "entries"
+  Dots nov;
+  for (uint32_t sl = 0; sl < c->cap; sl++)
+    if (c->h_table[sl].used && c->nov[sl]) nov.push_back({c->slot_actor[sl], c->nov[sl]});
+  sort_dots(&nov);
+  const uint32_t na = (uint32_t)c->id_actor.size();
+  std::vector<unsigned long long> ck(na);
+  if ((rc = ensure_clock(c))) return rc;
+  if (na && ((e = hipMemcpyAsync(ck.data(), d->clock.p, na * 8ull, hipMemcpyDeviceToHost, c->ctx->stream)) ||
+             (e = hipStreamSynchronize(c->ctx->stream))))
+    return x->hip_fail(e, "clock download");
+  IdDots clock;
+  for (uint32_t i = 0; i < na; i++)
+    if (ck[i]) clock.push_back({i, ck[i]});
+  Wr hw;
+  if (prefix16) hw.b.insert(hw.b.end(), prefix16, prefix16 + 16);
+  hw.map(2);
+  hw.str("next_op_versions");
+  put_vclock(hw, nov);
+  hw.str("state");
+  hw.map(3);
+  hw.str("clock");
+  put_vclock(hw, uuid_dots(clock));
+  hw.str("entries");
+  // tail: "deferred" map {VClock bytes: [members]} sorted by the clock's bytes
+  Wr tw;
+  tw.str("deferred");
+  std::vector<std::pair<std::vector<uint8_t>, const std::set<uint64_t>*>> df;
+  for (auto& y : d->deferred) {
+    Wr kw;
+    put_vclock(kw, uuid_dots(y.first));
+    df.push_back({kw.b, &y.second});
+  }
+  std::sort(df.begin(), df.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  tw.map(df.size());
+  for (auto& y : df) {
+    tw.b.insert(tw.b.end(), y.first.begin(), y.first.end());
+    tw.arr(y.second->size());
+    for (uint64_t m : *y.second) tw.uint(m);
+  }
+  // live pairs, actor UUIDs and UUID-order ranks by stable id
+  uint32_t nl = 0;
+  if ((rc = collect(c, &nl))) return rc;
+  if (d->uuid_ids != na) {
+    std::vector<uint8_t> u(16ull * na + 16);
+    std::vector<uint32_t> order(na), rank(na + 1);
+    for (uint32_t i = 0; i < na; i++) {
+      std::memcpy(u.data() + 16ull * i, c->id_actor[i].data(), 16);
+      order[i] = i;
+    }
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return c->id_actor[a] < c->id_actor[b]; });
+    for (uint32_t i = 0; i < na; i++) rank[order[i]] = i;
+    if ((e = d->uuid_of_id.reserve(u.size())) || (e = d->rank_of_id.reserve(4ull * rank.size())) ||
+        (e = hipMemcpyAsync(d->uuid_of_id.p, u.data(), u.size(), hipMemcpyHostToDevice, s)) ||
+        (e = hipMemcpyAsync(d->rank_of_id.p, rank.data(), 4ull * rank.size(), hipMemcpyHostToDevice, s)) ||
+        (e = hipStreamSynchronize(s)))
+      return x->hip_fail(e, "actor ranks");
+    d->uuid_ids = na;
+  }
+  // clear text bound: head + map header + entries (member <= 9 + 6 + 5, Dot <= 18 + 9) + tail
+  const uint64_t U = hw.b.size() + 5 + 20ull * nl + 27ull * nl + tw.b.size();
+  const uint64_t A = (U + 255) & ~255ull;  // [offs(2) | out_offs(1) | stats | nonce | outer] after it
+  const uint64_t total_max = 16 + sealed_len(U);
+  if ((e = x->blob.reserve(A + 256 + hw.b.size() + tw.b.size())) || (e = x->out.reserve(total_max + 64)) ||
+      (e = x->h_stage.reserve(std::max<uint64_t>(total_max + 64, 256 + hw.b.size() + tw.b.size()))))
+    return x->hip_fail(e, "ds compact reserve");
+  for (int k = 0; k < 15; k++) {
+    // 0-3 u32 sort keys / perms, 4-6 u64 keys / sorted members / values, 7-10 actors, heads,
+    // ranks, lengths, 11 entry CSR (n + 1), 12 byte offsets
+    const size_t sz = k >= 4 && k <= 6 ? 8ull * nl + 64 : k <= 12 ? 4ull * nl + 68 : 64;
+    if ((e = d->ser[k].reserve(sz))) return x->hip_fail(e, "ds compact reserve");
+  }
+  if ((e = d->ser[15].reserve(orswot_ser_tmp_bytes(std::max<uint32_t>(nl, 1))))) return x->hip_fail(e, "ds compact reserve");
+  uint8_t* db = x->blob.as<uint8_t>();
+  uint8_t* hs = x->h_stage.as<uint8_t>();
+  std::memset(hs, 0, 128);
+  if (nonce) std::memcpy(hs + 32, nonce, 24);
+  else os_random(hs + 32, 24);
+  std::memcpy(hs + 56, outer, 16);
+  std::memcpy(hs + 128, hw.b.data(), hw.b.size());
+  std::memcpy(hs + 128 + hw.b.size(), tw.b.data(), tw.b.size());
+  if ((e = hipMemcpyAsync(db + A, hs, 128 + hw.b.size() + tw.b.size(), hipMemcpyHostToDevice, s)))
+    return x->hip_fail(e, "ds compact upload");
+  OrswotSerScratch sc{};
+  sc.member_in = d->col[0].as<unsigned long long>();
+  sc.actor_in = d->col[1].as<uint32_t>();
+  sc.value_in = d->col[2].as<unsigned long long>();
+  sc.rank_of_id = d->rank_of_id.as<uint32_t>();
+  sc.rank_bits = bits_for(na);
+  sc.k32a = d->ser[0].as<uint32_t>();
+  sc.k32b = d->ser[1].as<uint32_t>();
+  sc.p32a = d->ser[2].as<uint32_t>();
+  sc.p32b = d->ser[3].as<uint32_t>();
+  sc.k64a = d->ser[4].as<unsigned long long>();
+  sc.member_sorted = d->ser[5].as<unsigned long long>();
+  sc.value_sorted = d->ser[6].as<unsigned long long>();
+  sc.actor_sorted = d->ser[7].as<uint32_t>();
+  sc.head = d->ser[8].as<uint32_t>();
+  sc.hrank = d->ser[9].as<uint32_t>();
+  sc.len = d->ser[10].as<uint32_t>();
+  sc.seg = d->ser[11].as<uint32_t>();
+  sc.pos = d->ser[12].as<uint32_t>();
+  sc.tmp = d->ser[15].p;
+  sc.tmp_bytes = d->ser[15].cap;
+  OrswotSerArgs a{};
+  a.out = db;
+  a.prefix = db + A + 128;
+  a.prefix_len = hw.b.size();
+  a.suffix = db + A + 128 + hw.b.size();
+  a.suffix_len = tw.b.size();
+  a.uuid_of_id = d->uuid_of_id.as<uint8_t>();
+  a.n = nl;
+  auto* offs = reinterpret_cast<unsigned long long*>(db + A);  // [0] 0, [1] clear len, [2] out_offs
+  a.seal_offs = offs;
+  a.stats = reinterpret_cast<uint32_t*>(db + A + 24);
+  const int t = x->tbegin("ds_serialize");
+  if ((e = launch_orswot_ser(s, sc, a))) return x->hip_fail(e, "ds serialize");
+  x->tend(t);
+  rc = device_seal(x, db, reinterpret_cast<const uint64_t*>(offs), 1, U, db + A + 56, db + A + 32,
+                   x->out.as<uint8_t>(), reinterpret_cast<const uint64_t*>(db + A + 16), key);
+  if (rc) return rc;
+  uint64_t clear_len = 0;
+  if ((e = hipMemcpyAsync(&clear_len, db + A + 8, 8, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s)))
+    return x->hip_fail(e, "ds compact");
+  if (clear_len > U) return x->fail(CE_ERR_DEVICE, "serializer overran its bound");
+  const uint64_t total = 16 + sealed_len(clear_len);
+  file->resize(total);
+  if ((e = hipMemcpyAsync(file->data(), x->out.p, total, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s)))
+    return x->hip_fail(e, "ds compact download");
+  return CE_OK;
 }
 
 // canonical to_vec_named(StateWrapper<S>) (lib.rs:336, 739-743); HashMap / HashSet contents

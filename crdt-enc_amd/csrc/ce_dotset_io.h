@@ -1,0 +1,78 @@
+// ce_dotset_io.h -- launch interface of ce_dotset_io.hip: StateWrapper<Orswot<u64, Uuid>> bytes
+// written from / read into the device entry columns.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ce_common.h"
+#include "ce_kernels.h"
+
+namespace ce {
+
+// writer: out = prefix || map header(n_members) || entries || suffix (prefix = the host-built
+// bytes up to and including the "entries" key; suffix = "deferred" and its map)
+struct OrswotSerArgs {
+  uint8_t* out;
+  const uint8_t* prefix;
+  uint64_t prefix_len;
+  const uint8_t* suffix;
+  uint64_t suffix_len;
+  const uint8_t* uuid_of_id;       // 16 bytes per stable actor id
+  uint32_t n;                      // live pairs
+  unsigned long long* seal_offs;   // [0] = 0, [1] = clear length, [2] = 0 (the seal's out_offs)
+  uint32_t* stats;                 // [0] = members written
+  // filled by launch_orswot_ser (sorted columns and scans)
+  const unsigned long long* member;
+  const uint32_t* actor;
+  const unsigned long long* value;
+  const uint32_t* head;
+  const uint32_t* hrank;
+  const uint32_t* seg;
+  const uint32_t* pos;
+  const uint32_t* len;
+};
+
+struct OrswotSerScratch {
+  const unsigned long long* member_in;   // collect order
+  const uint32_t* actor_in;
+  const unsigned long long* value_in;
+  const uint32_t* rank_of_id;            // UUID byte order rank of each stable actor id
+  int rank_bits;
+  uint32_t *k32a, *k32b, *p32a, *p32b;   // n each
+  unsigned long long *k64a, *member_sorted, *value_sorted;
+  uint32_t* actor_sorted;
+  uint32_t *head, *hrank, *len, *pos;    // n each
+  uint32_t* seg;                         // n + 1
+  void* tmp;
+  size_t tmp_bytes;
+};
+hipError_t launch_orswot_ser(hipStream_t s, OrswotSerScratch& sc, const OrswotSerArgs& a);
+size_t orswot_ser_tmp_bytes(uint32_t n);
+
+// reader over the bytes [lo, hi) of state plaintext s that follow the entries map header
+struct OrswotReadArgs {
+  const uint8_t* s;
+  uint64_t lo, hi;
+  uint32_t* cand_raw;   // cap
+  uint32_t* n_cand_dev;
+  uint32_t cap;
+  uint32_t n_cand;      // stage >= 1: candidates found (host-checked against the map count)
+  uint32_t* cand;       // sorted, n_cand
+  uint32_t* end;        // entry end (relative to lo), n_cand
+  uint32_t* ndots;      // non-zero Dots per entry
+  uint32_t* dbase;      // exclusive scan of ndots
+  unsigned long long* member;  // per entry
+  unsigned long long* msort;   // members sorted (repeat check)
+  uint32_t* flags;      // 1 non-canonical entry, 2 broken chain, 4 unknown actor, 8 repeated member
+  const ActorSlot* table;
+  uint32_t mask;
+  unsigned long long* col_member;
+  uint32_t* col_actor;
+  unsigned long long* col_value;
+};
+// stage 0: candidate search; 1: sort + per-entry parse + chain check + scan; 2: emit columns
+hipError_t launch_orswot_read(hipStream_t s, OrswotReadArgs a, void* tmp, size_t tmp_bytes, int stage);
+size_t orswot_read_tmp_bytes(uint32_t n);
+hipError_t hipcub_sort_u32(void* tmp, size_t& tb, const uint32_t* kin, uint32_t* kout, uint32_t n, hipStream_t s);
+
+}  // namespace ce

@@ -306,6 +306,10 @@ int ce_core_import_dense(ce_core *c, const uint64_t *d_state, const uint64_t *d_
  * ce_core_state_bytes + ce_core_merge_state instead (crdtenc shard.exchange_vclock). */
 int ce_core_dense_ready(ce_core *c);
 
+/* Diagnostics: how many times a code path ran on this core ("states_device_read",
+ * "states_host_parse", "compact_device_writer"); lets tests show which path did the work. */
+uint64_t ce_core_path_count(ce_core *c, const char *path);
+
 /* ---------------------------------------------------------------------------------------- */
 /* Keys (crdt-enc/src/key_cryptor.rs:35-82): the data keys the core reads and writes with     */
 /* ---------------------------------------------------------------------------------------- */

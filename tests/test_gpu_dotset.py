@@ -262,3 +262,124 @@ def test_compact_roundtrip(ctx):
     assert other.state_bytes() == core.state_bytes()
     core.close()
     other.close()
+
+
+def _orswot_state_forms(sw, rng):
+    """Re-encodings of one canonical StateWrapper<Orswot> (oracle bytes) that
+    read_remote_states accepts: (name, bytes, device-reader eligible)."""
+    d = msgpack.unpackb(sw, raw=True, strict_map_key=False, object_pairs_hook=list)
+    dd = dict(d)
+    nov, st = dd[b"next_op_versions"], dict(dd[b"state"])
+    entries = st[b"entries"]
+
+    def enc(entries_pairs, member_enc=None, vclock_enc=None):
+        w = C.Wr()
+        w.map(2)
+        w.str("next_op_versions")
+        w.b += msgpack.packb(dict(nov), use_bin_type=True) if False else _vclock_bytes(nov)
+        w.str("state")
+        w.map(3)
+        w.str("clock")
+        w.b += _vclock_bytes(st[b"clock"])
+        w.str("entries")
+        w.map(len(entries_pairs))
+        for m, vc in entries_pairs:
+            w.b += member_enc(m) if member_enc else msgpack.packb(m)
+            w.b += vclock_enc(vc) if vclock_enc else _vclock_bytes(vc)
+        w.str("deferred")
+        w.b += msgpack.packb(st[b"deferred"], use_bin_type=True) if False else _raw_deferred(sw)
+        return bytes(w.b)
+
+    out = [("canonical", sw, True)]
+    shuffled = list(entries)
+    rng.shuffle(shuffled)
+    out.append(("hashmap_order", enc(shuffled), True))
+    if len(entries) >= 2:
+        dup = list(entries) + [(entries[0][0], entries[1][1])]   # repeated member: later clock wins
+        out.append(("repeated_member", enc(dup), False))
+        out.append(("long_uint_member", enc(list(entries), member_enc=lambda m: b"\xcf" + m.to_bytes(8, "big")), False))
+        out.append(("descending_dots", enc(list(entries), vclock_enc=lambda vc: _vclock_bytes(vc, reverse=True)), False))
+    return out
+
+
+def _vclock_bytes(vc, reverse=False):
+    pairs = dict(vc)[b"dots"] if isinstance(vc, list) else vc[b"dots"]
+    w = C.Wr()
+    w.map(1)
+    w.str("dots")
+    items = sorted(pairs, key=lambda p: p[0], reverse=reverse)
+    w.map(len(items))
+    for a, c in items:
+        w.bin(a)
+        w.uint(c)
+    return bytes(w.b)
+
+
+def _raw_deferred(sw):
+    """the canonical deferred map's bytes (everything after the "deferred" key)"""
+    i = sw.rindex(b"\xa8deferred")
+    return sw[i + 9:]
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_orswot_state_reader_forms(ctx, seed):
+    """read_remote_states for Orswot decodes canonical state files on the device
+    (ce_dotset_io.hip: parallel entry-head search + chained per-entry parse) and declines every
+    other accepted form to the host parser; both give the oracle's state.  CE_HOST_STATES=1
+    (the host parser for everything) is compared too."""
+    import os
+    rng = random.Random(900 + seed)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 6)
+    part = C.Core("orswot")
+    files = gen("orswot", rng, actors, 3, 6, 40, seed == 2)
+    acts, clears, fa, fv = G.batch(files, "orswot", APP)
+    f = [CORE + C._oc.cryptor_encrypt(key, bytes(24), c)[1] for c in clears]
+    assert part.read_remote_ops(key, [APP], f, [acts[i] for i in fa], fv)[0] == 0
+    sw = part.serialize()
+    for name, body, eligible in _orswot_state_forms(sw, rng):
+        sf = seal_files(ctx, key, [APP + body])
+        oc = C.Core("orswot")
+        orc, ost = oc.read_remote_states(key, [APP], sf)
+        assert orc == 0, name
+        for host in (False, True):
+            if host:
+                os.environ["CE_HOST_STATES"] = "1"
+            try:
+                core = new_core(ctx, "orswot", key)
+                rc, st = core.ingest_states(sf)
+                assert (rc, st) == (orc, ost), (name, host)
+                assert core.state_bytes() == oc.serialize(), (name, host)
+                dev = core.path_count("states_device_read")
+                assert dev == (1 if (eligible and not host) else 0), (name, host, dev)
+                if not host:
+                    assert core.path_count("states_host_parse") == 1 - dev
+                core.close()
+            finally:
+                os.environ.pop("CE_HOST_STATES", None)
+
+
+def test_orswot_device_compaction_bytes(ctx):
+    """Core::compact for Orswot writes the clear text on the device (ce_dotset_io.hip writer):
+    the sealed file opens to exactly data_version || the canonical StateWrapper (host writer ==
+    oracle bytes), in both output formats."""
+    rng = random.Random(77)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 7)
+    files = G.well_formed_orswot(rng, actors, 5, 8, 300)[0]
+    acts, clears, fa, fv = G.batch(files, "orswot", APP)
+    oc = C.Core("orswot")
+    sealed = seal_files(ctx, key, clears)
+    assert oc.read_remote_ops(key, [APP], sealed, [acts[i] for i in fa], fv)[0] == 0
+    for flags, outer, pre in ((crdtenc.COMPACT_INGEST_FORMAT, CORE, APP), (0, APP, b"")):
+        core = crdtenc.Core(ctx, kind=crdtenc.STATE_ORSWOT, supported=[APP], current_data_version=APP,
+                            flags=flags)
+        core.set_latest_key(key)
+        assert core.ingest_ops(sealed, acts, fa, fv)[0] == 0
+        assert core.state_bytes() == oc.serialize()
+        f, _ = core.compact_to_buffer(nonce=bytes(24))
+        assert f[:16] == outer
+        st, pt = ctx.decrypt(key, f[16:])
+        assert st == 0 and pt == pre + oc.serialize()
+        assert core.path_count("compact_device_writer") == 1
+        core.close()
