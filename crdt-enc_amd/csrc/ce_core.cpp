@@ -751,17 +751,31 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
       setup_known = true;
     }
     if (n_large == 0) return CE_OK;  // every file was single-page: nothing for the kernels below
+    // decode inside the segment pass (CE_SEGDEC=0 or CE_SPLIT=1: the separate decode kernels
+    // below; read per call, as CE_SPLIT)
+    const char* sdv = getenv("CE_SEGDEC");
+    const bool segdec = !(sdv && sdv[0] == '0') && !getenv("CE_SPLIT");
     if (!only) {
       SegScratch sc = segscratch(ctx, ec);
+      if (segdec && (e = ctx->segrec.reserve((size_t)ec * 2 * 32))) return ctx->hip_fail(e, "segment records");
       int t = ctx->tbegin("segments_open");
-      if ((e = launch_segments(ctx->stream, false, d_blob, ctx->out.as<uint8_t>(), da.params, n,
-                               da.status, sc, grid_waves_for(n + ec), true)))
+      if ((e = segdec ? launch_segments_decode(ctx->stream, d_blob, ctx->out.as<uint8_t>(), da, sc,
+                                               grid_waves_for(n + ec), ctx->segrec.as<uint4>())
+                      : launch_segments(ctx->stream, false, d_blob, ctx->out.as<uint8_t>(), da.params, n,
+                                        da.status, sc, grid_waves_for(n + ec), true)))
         return ctx->hip_fail(e, "segments");
       ctx->tend(t);
       t = ctx->tbegin("finalize_open");
       if ((e = launch_finalize_multi(ctx->stream, false, ctx->out.as<uint8_t>(), da.params, da.status, sc, n)))
         return ctx->hip_fail(e, "finalize");
       ctx->tend(t);
+      if (segdec) {
+        t = ctx->tbegin("decode");
+        if ((e = launch_segdec_apply(ctx->stream, da, sc, ctx->segrec.as<uint4>(), n_large)))
+          return ctx->hip_fail(e, "decode");
+        ctx->tend(t);
+        return CE_OK;
+      }
     }
     const int t = ctx->tbegin("decode");
     // CE_SPLIT=1: k_decode_split (measured slower on C4: 1.67 vs 1.36 ms)
@@ -825,6 +839,8 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
     return ctx->hip_fail(e, "fold sync");
   const bool merged_on_device = (hc[2] | hc[3] | hc[4] | hc[7] | hc[8] | hc[12]) == 0;
   if (merged_out) *merged_out = merged_on_device;
+  if (hc[11]) c->path_counts["segdec_records"] += hc[11];
+  if (hc[14]) c->path_counts["segdec_fallback"] += hc[14];
 
   // 3) batches outside the device gate's shape: host gate, fold again with its flags
   std::vector<uint64_t> expect(he0, he0 + m);

@@ -277,25 +277,29 @@ __global__ void __launch_bounds__(kBlock) k_ds_kill(DsTables t, const uint32_t* 
 }
 
 __global__ void __launch_bounds__(kBlock) k_ds_finalize(DsTables t) {
-  __shared__ uint32_t lds[2];
+  // per-lane counts over the grid-stride loop, summed per wave at the end (two atomics per
+  // wave instead of a block-wide barrier + atomic per counter per iteration)
   const uint32_t cap = t.pmask + 1;
-  // every block runs the same number of iterations (block_count needs all threads)
-  const uint32_t stride = gridDim.x * kBlock;
-  const uint32_t iters = (cap + stride - 1) / stride;
-  for (uint32_t it = 0; it < iters; it++) {
-    const uint32_t b = it * stride + blockIdx.x * kBlock + threadIdx.x;
-    bool used = false, live = false;
-    if (b < cap && t.pkey[b] != kDsEmpty) {
-      used = true;
-      unsigned long long v = t.cur[b] > t.add[b] ? t.cur[b] : t.add[b];
-      if (v != 0 && v <= t.kill[b]) v = 0;
-      t.cur[b] = v;
-      t.add[b] = 0;
-      t.kill[b] = 0;
-      live = v != 0;
-    }
-    block_count(t.live + 0, live, lds);
-    block_count(t.live + 1, used, lds);
+  uint32_t n_used = 0, n_live = 0;
+  for (uint32_t b = blockIdx.x * kBlock + threadIdx.x; b < cap; b += gridDim.x * kBlock) {
+    if (t.pkey[b] == kDsEmpty) continue;
+    n_used++;
+    const unsigned long long c = t.cur[b], ad = t.add[b], kl = t.kill[b];
+    unsigned long long v = c > ad ? c : ad;
+    if (v != 0 && v <= kl) v = 0;
+    if (v != c) t.cur[b] = v;
+    if (ad) t.add[b] = 0;
+    if (kl) t.kill[b] = 0;
+    n_live += v != 0;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    n_used += __shfl_xor(n_used, o);
+    n_live += __shfl_xor(n_live, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (n_live) atomicAdd(t.live + 0, n_live);
+    if (n_used) atomicAdd(t.live + 1, n_used);
   }
 }
 

@@ -44,9 +44,11 @@ struct DsState {
   DevBuf misses;
   HostBuf h_cnt;
   // device state reader (per state file: candidates, sorted heads, entry ends, Dot counts and
-  // bases, members, sorted members) and device writer scratch
-  std::vector<std::array<DevBuf, 7>> rd;
+  // bases, members, sorted members [0..6]
+  // and emitted (member, actor id, value) columns [7..9]), pinned staging for its downloads
+  std::vector<std::array<DevBuf, 10>> rd;
   DevBuf rd_tmp, rd_misc, ser[16], uuid_of_id, rank_of_id;
+  HostBuf rd_host, rd_small, rd_clock;
   uint64_t uuid_ids = ~0ull;  // id count uuid_of_id / rank_of_id were built for
 };
 
@@ -1026,8 +1028,16 @@ int id_dots(ce_core* c, Dots d, IdDots* out) {
   return CE_OK;
 }
 
+struct OtherCols {  // the other state's (member, actor id, value) columns in HBM
+  const unsigned long long* member;
+  const uint32_t* actor;
+  const unsigned long long* value;
+  const unsigned long long* clock_host = nullptr;  // pinned dense clock by actor id, or null
+  uint32_t clock_cap = 0;
+};
 int orswot_merge_cols(ce_core* c, const IdDots& oclock,
-                      const std::vector<std::pair<IdDots, std::vector<uint64_t>>>& od, uint32_t n);
+                      const std::vector<std::pair<IdDots, std::vector<uint64_t>>>& od,
+                      const OtherCols& oc, uint32_t n, uint32_t* live_async, bool* queued = nullptr);
 
 // Orswot::merge(other) on the device (entries) and host (deferred)
 int orswot_merge_one(ce_core* c, const HostState& hs) {
@@ -1078,13 +1088,21 @@ int orswot_merge_one(ce_core* c, const HostState& hs) {
   if ((e = up(d->other[0].as<unsigned long long>(), mem, s)) || (e = up(d->other[1].as<uint32_t>(), act, s)) ||
       (e = up(d->other[2].as<unsigned long long>(), val, s)))
     return ctx->hip_fail(e, "merge");
-  return orswot_merge_cols(c, oclock, od, (uint32_t)mem.size());
+  return orswot_merge_cols(c, oclock, od,
+                           {d->other[0].as<unsigned long long>(), d->other[1].as<uint32_t>(),
+                            d->other[2].as<unsigned long long>()},
+                           (uint32_t)mem.size(), nullptr);
 }
 
 // Orswot::merge(other) with other's entries already in d->other[0..2] as (member, actor id,
 // counter) columns of n pairs, its clock and deferred removals by actor id
+// Orswot::merge(other) for other's columns in HBM.  With live_async set and no deferred
+// removals on either side the merge is queued without a host round trip: finalize's counts are
+// copied to live_async (pinned, 4 words) for the caller to read after its own synchronise, and
+// used_pairs grows by the upper bound n meanwhile.
 int orswot_merge_cols(ce_core* c, const IdDots& oclock,
-                      const std::vector<std::pair<IdDots, std::vector<uint64_t>>>& od, uint32_t n) {
+                      const std::vector<std::pair<IdDots, std::vector<uint64_t>>>& od,
+                      const OtherCols& ocols, uint32_t n, uint32_t* live_async, bool* queued) {
   DsState* d = c->ds;
   ce_ctx* ctx = c->ctx;
   hipStream_t s = ctx->stream;
@@ -1092,18 +1110,34 @@ int orswot_merge_cols(ce_core* c, const IdDots& oclock,
   if ((rc = ensure_clock(c))) return rc;
   hipError_t e;
   const uint32_t cap = d->clock_cap;
-  std::vector<unsigned long long> oc(cap, 0);
-  for (auto& x : oclock) oc[x.first] = x.second;
-  if ((e = up(d->oclock.as<unsigned long long>(), oc, s))) return ctx->hip_fail(e, "merge");
+  if (live_async && ocols.clock_host && ocols.clock_cap == cap) {  // pinned: no host wait
+    if ((e = hipMemcpyAsync(d->oclock.p, ocols.clock_host, cap * 8ull, hipMemcpyHostToDevice, s)))
+      return ctx->hip_fail(e, "merge");
+  } else {
+    std::vector<unsigned long long> oc(cap, 0);
+    for (auto& x : oclock) oc[x.first] = x.second;
+    if ((e = up(d->oclock.as<unsigned long long>(), oc, s))) return ctx->hip_fail(e, "merge");
+  }
   const int tm = ctx->tbegin("ds_merge");
-  if ((e = launch_ds_put_other(s, tables(d), d->other[0].as<unsigned long long>(), d->other[1].as<uint32_t>(),
-                               d->other[2].as<unsigned long long>(), n)) ||
+  if ((e = launch_ds_put_other(s, tables(d), ocols.member, ocols.actor, ocols.value, n)) ||
       (e = launch_ds_merge(s, tables(d), d->clock.as<unsigned long long>(), d->oclock.as<unsigned long long>())))
     return ctx->hip_fail(e, "merge");
   ctx->tend(tm);
   // other.deferred applied, clocks merged, apply_deferred: thresholds from both deferred sets
   auto rms = deferred_list(d);
   rms.insert(rms.end(), od.begin(), od.end());
+  if (live_async && rms.empty()) {
+    if ((e = launch_merge_max(s, d->clock.as<unsigned long long>(), d->oclock.as<unsigned long long>(), cap)) ||
+        (e = hipMemsetAsync(d->live.p, 0, 8, s)))
+      return ctx->hip_fail(e, "merge");
+    const int t = ctx->tbegin("ds_finalize");
+    if ((e = launch_ds_finalize(s, tables(d)))) return ctx->hip_fail(e, "finalize");
+    ctx->tend(t);
+    if ((e = hipMemcpyAsync(live_async, d->live.p, 16, hipMemcpyDeviceToHost, s))) return ctx->hip_fail(e, "finalize");
+    d->used_pairs += n;
+    if (queued) *queued = true;
+    return CE_OK;
+  }
   if ((rc = upload_removals(c, rms))) return rc;
   const uint32_t nr = (uint32_t)rms.size();
   if ((e = launch_ds_kill(s, tables(d), d->d0[0].as<uint32_t>(), d->d0[1].as<uint32_t>(), d->d0[2].as<uint32_t>(),
@@ -1204,8 +1238,10 @@ struct DevState {
   uint64_t pt = 0;      // plaintext offset (past the 16-byte data version) in ctx->out
   uint64_t len = 0;
   uint64_t body = 0;
-  uint32_t n_entries = 0, n_dots = 0;
+  uint32_t n_entries = 0, n_dots = 0, cap = 0;
   HostState hs;
+  IdDots oclock;
+  std::vector<std::pair<IdDots, std::vector<uint64_t>>> od;
 };
 
 hipError_t dl(void* dst, const void* src, size_t n, hipStream_t s) {
@@ -1240,18 +1276,25 @@ OrswotReadArgs read_args(ce_core* c, DsState* d, size_t f, const DevState& ds, c
 
 // files i = plaintexts at out + off[i] (after the 16-byte data version), len[i] bytes, st[i] =
 // status so far.  Canonical Orswot states are decoded on the device; others go to read_state.
+// Every stage runs over all files before its one host round trip (heads, entry counts, entry
+// ends, tails, emitted columns); the merges are then queued back to back and synchronised once.
 int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uint64_t>& off,
                            const std::vector<uint64_t>& len, int32_t* st, int32_t* status_out) {
   DsState* d = c->ds;
   ce_ctx* ctx = c->ctx;
   hipStream_t s = ctx->stream;
   const size_t n = off.size();
+  constexpr uint64_t kPrefix = 1u << 18;
   std::vector<DevState> ds(n);
   std::vector<std::vector<uint8_t>> host_pt(n);
   hipError_t e;
+  int rc;
   if (d->rd.size() < n) d->rd.resize(n);
-  if ((e = d->rd_misc.reserve(8ull * n + 64)) || (e = hipMemsetAsync(d->rd_misc.p, 0, 8ull * n, s)))
+  // pinned words: [0, 2n) candidate counts / flags, [2n, 6n) entry tails, [6n, 10n) live counts
+  if ((e = d->rd_misc.reserve(8ull * n + 64)) || (e = d->rd_small.reserve(40ull * n + 64)) ||
+      (e = hipMemsetAsync(d->rd_misc.p, 0, 8ull * n, s)))
     return ctx->hip_fail(e, "state reader");
+  uint32_t* small = d->rd_small.as<uint32_t>();
   auto host_parse = [&](size_t i) -> int {  // the whole plaintext through read_state
     ds[i].device = false;
     c->path_counts["states_host_parse"]++;
@@ -1261,81 +1304,160 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     if (!read_state(c->kind, host_pt[i].data(), len[i], &ds[i].hs)) st[i] = CE_ERR_DECODE;
     return CE_OK;
   };
+  auto sync = [&](const char* what) { return (e = hipStreamSynchronize(s)) ? ctx->hip_fail(e, what) : CE_OK; };
   int first = CE_OK;
   {
     HostPhase hp("states: device read");
-    std::vector<uint8_t> pre;
+    // 1) the heads on the host: a prefix of every file long enough for next_op_versions and
+    //    the clock (a longer one, file by file, when it is not)
+    std::vector<uint64_t> poff(n + 1, 0);
+    for (size_t i = 0; i < n; i++)
+      poff[i + 1] = poff[i] + (st[i] == CE_OK ? std::min<uint64_t>(len[i], kPrefix) : 0);
+    if ((e = d->rd_host.reserve(poff[n] + 64))) return ctx->hip_fail(e, "state head");
+    uint8_t* hb = d->rd_host.as<uint8_t>();
+    for (size_t i = 0; i < n; i++)
+      if (poff[i + 1] > poff[i] &&
+          (e = hipMemcpyAsync(hb + poff[i], out + off[i], poff[i + 1] - poff[i], hipMemcpyDeviceToHost, s)))
+        return ctx->hip_fail(e, "state head");
+    if ((rc = sync("state head"))) return rc;
+    std::vector<size_t> dev;
     for (size_t i = 0; i < n; i++) {
       if (st[i] != CE_OK) continue;
       DevState& x = ds[i];
       x.pt = off[i];
       x.len = len[i];
-      // 1) the head on the host: a prefix long enough for next_op_versions and the clock
-      uint64_t want = std::min<uint64_t>(len[i], 1u << 18), body = 0, ne = 0;
-      int pr;
-      for (;;) {
-        pre.resize(want);
-        if (want && (e = dl(pre.data(), out + off[i], want, s))) return ctx->hip_fail(e, "state head");
-        pr = parse_state_prefix(pre.data(), want, want == len[i], &x.hs, &body, &ne);
-        if (pr != 2) break;
+      uint64_t want = poff[i + 1] - poff[i], body = 0, ne = 0;
+      int pr = parse_state_prefix(hb + poff[i], want, want == len[i], &x.hs, &body, &ne);
+      std::vector<uint8_t> pre;
+      while (pr == 2) {
         want = std::min<uint64_t>(len[i], want * 4);
+        pre.resize(want);
+        if ((e = dl(pre.data(), out + off[i], want, s))) return ctx->hip_fail(e, "state head");
+        pr = parse_state_prefix(pre.data(), want, want == len[i], &x.hs, &body, &ne);
       }
       if (pr != 0 || ne == 0 || ne > 0xffffffffull || len[i] > 0xffffffffull) {
-        int rc = host_parse(i);
-        if (rc) return rc;
+        if ((rc = host_parse(i))) return rc;
         continue;
       }
       x.body = body;
       x.n_entries = (uint32_t)ne;
-      // 2) entry heads (search covers the deferred map too: its VClock keys look alike)
-      const uint32_t cap = (uint32_t)std::min<uint64_t>(ne + 65536, len[i] / 7 + 1);
+      x.cap = (uint32_t)std::min<uint64_t>(ne + 65536, len[i] / 7 + 1);
+      dev.push_back(i);
+    }
+    // 2) the states' actors into the table (the emitted columns carry their ids), then the
+    //    entry-head search over every file (it covers the deferred map too: its VClock keys
+    //    look alike)
+    size_t tmp_need = 0;
+    for (size_t i : dev) {
+      DevState& x = ds[i];
+      if ((rc = id_dots(c, x.hs.clock, &x.oclock))) return rc;
+      for (auto& y : x.hs.deferred) {
+        IdDots k;
+        if ((rc = id_dots(c, y.first, &k))) return rc;
+        x.od.push_back({k, y.second});
+      }
+      const uint64_t ne = x.n_entries;
       auto& b = d->rd[i];
-      if ((e = b[0].reserve(4ull * cap + 64)) || (e = b[1].reserve(4ull * cap + 64)) ||
+      if ((e = b[0].reserve(4ull * x.cap + 64)) || (e = b[1].reserve(4ull * x.cap + 64)) ||
           (e = b[2].reserve(4ull * ne + 64)) || (e = b[3].reserve(4ull * ne + 64)) ||
           (e = b[4].reserve(4ull * ne + 64)) || (e = b[5].reserve(8ull * ne + 64)) ||
-          (e = b[6].reserve(8ull * ne + 64)) || (e = d->rd_tmp.reserve(orswot_read_tmp_bytes(cap))))
+          (e = b[6].reserve(8ull * ne + 64)))
         return ctx->hip_fail(e, "state reader");
-      OrswotReadArgs a = read_args(c, d, i, x, out, cap);
-      uint32_t found[2];
-      if ((e = launch_orswot_read(s, a, d->rd_tmp.p, d->rd_tmp.cap, 0)) ||
-          (e = dl(found, d->rd_misc.as<uint32_t>() + 2 * i, 8, s)))
+      tmp_need = std::max(tmp_need, orswot_read_tmp_bytes(x.cap));
+    }
+    if ((rc = table_upload(c)) || (rc = ensure_clock(c))) return rc;
+    if ((e = d->rd_tmp.reserve(tmp_need))) return ctx->hip_fail(e, "state reader");
+    for (size_t i : dev)
+      if ((e = launch_orswot_read(s, read_args(c, d, i, ds[i], out, ds[i].cap), d->rd_tmp.p, d->rd_tmp.cap, 0)))
         return ctx->hip_fail(e, "state reader");
-      if (found[0] < ne || found[0] > cap) {  // fewer heads than entries, or the list overflowed
-        int rc = host_parse(i);
-        if (rc) return rc;
+    if (!dev.empty() && ((e = hipMemcpyAsync(small, d->rd_misc.p, 8ull * n, hipMemcpyDeviceToHost, s)) ||
+                         (rc = sync("state reader")))) return rc ? rc : ctx->hip_fail(e, "state reader");
+    // 3) the first N heads in position order are the entries: parse, chain, repeats, scan
+    std::vector<size_t> dev2;
+    std::vector<uint32_t> found(n, 0);
+    for (size_t i : dev) found[i] = small[2 * i];
+    for (size_t i : dev) {
+      DevState& x = ds[i];
+      if (found[i] < x.n_entries || found[i] > x.cap) {  // fewer heads than entries, or overflow
+        if ((rc = host_parse(i))) return rc;
         continue;
       }
-      // 3) the first N heads in position order are the entries: parse, chain, repeats, scan
-      a.n_cand = found[0];
-      {
-        size_t tb = d->rd_tmp.cap;
-        if ((e = hipcub_sort_u32(d->rd_tmp.p, tb, a.cand_raw, a.cand, found[0], s)))
-          return ctx->hip_fail(e, "state reader");
-      }
-      a.n_cand = x.n_entries;
-      uint32_t tail[4];
+      OrswotReadArgs a = read_args(c, d, i, x, out, x.cap);
+      size_t tb = d->rd_tmp.cap;
+      if ((e = hipcub_sort_u32(d->rd_tmp.p, tb, a.cand_raw, a.cand, found[i], s)))
+        return ctx->hip_fail(e, "state reader");
+      uint32_t* tail = small + 2 * n + 4 * i;
+      const uint32_t ne = x.n_entries;
       if ((e = launch_orswot_read(s, a, d->rd_tmp.p, d->rd_tmp.cap, 1)) ||
           (e = hipMemcpyAsync(tail, a.end + ne - 1, 4, hipMemcpyDeviceToHost, s)) ||
           (e = hipMemcpyAsync(tail + 1, a.dbase + ne - 1, 4, hipMemcpyDeviceToHost, s)) ||
           (e = hipMemcpyAsync(tail + 2, a.ndots + ne - 1, 4, hipMemcpyDeviceToHost, s)) ||
-          (e = dl(tail + 3, a.flags, 4, s)))
+          (e = hipMemcpyAsync(tail + 3, a.flags, 4, hipMemcpyDeviceToHost, s)))
         return ctx->hip_fail(e, "state reader");
-      const uint64_t eend = x.body + (uint64_t)tail[0];
-      std::vector<uint8_t> tl;
-      bool ok = tail[3] == 0 && tail[0] != 0xffffffffu && eend <= len[i];
-      if (ok) {
-        tl.resize(len[i] - eend);
-        if (!tl.empty() && (e = dl(tl.data(), out + off[i] + eend, tl.size(), s))) return ctx->hip_fail(e, "state tail");
-        ok = parse_state_tail(tl.data(), tl.size(), &x.hs);
+      dev2.push_back(i);
+    }
+    if (!dev2.empty() && (rc = sync("state reader"))) return rc;
+    // 4) the deferred maps after the entries, on the host
+    std::vector<uint64_t> toff(n + 1, 0), eend(n, 0);
+    std::vector<size_t> dev3;
+    for (size_t i : dev2) {
+      const uint32_t* tail = small + 2 * n + 4 * i;
+      eend[i] = ds[i].body + (uint64_t)tail[0];
+      if (tail[3] == 0 && tail[0] != 0xffffffffu && eend[i] <= len[i]) {
+        ds[i].n_dots = tail[1] + tail[2];
+        dev3.push_back(i);
+      } else if ((rc = host_parse(i))) {
+        return rc;
       }
-      if (!ok) {
-        int rc = host_parse(i);
-        if (rc) return rc;
-        continue;
+    }
+    uint64_t ttot = 0;
+    for (size_t i : dev3) { toff[i] = ttot; ttot += len[i] - eend[i]; }
+    if ((e = d->rd_host.reserve(ttot + 64))) return ctx->hip_fail(e, "state tail");
+    hb = d->rd_host.as<uint8_t>();
+    for (size_t i : dev3)
+      if (len[i] > eend[i] &&
+          (e = hipMemcpyAsync(hb + toff[i], out + off[i] + eend[i], len[i] - eend[i], hipMemcpyDeviceToHost, s)))
+        return ctx->hip_fail(e, "state tail");
+    if (ttot && (rc = sync("state tail"))) return rc;
+    std::vector<size_t> dev4;
+    for (size_t i : dev3) {
+      if (parse_state_tail(hb + toff[i], len[i] - eend[i], &ds[i].hs)) {
+        DevState& x = ds[i];
+        x.od.clear();
+        for (auto& y : x.hs.deferred) {
+          IdDots k;
+          if ((rc = id_dots(c, y.first, &k))) return rc;
+          x.od.push_back({k, y.second});
+        }
+        dev4.push_back(i);
+      } else if ((rc = host_parse(i))) {
+        return rc;
       }
-      x.device = true;
-      x.n_dots = tail[1] + tail[2];
-      c->path_counts["states_device_read"]++;
+    }
+    // 5) (member, actor id, value) columns of every entry Dot; an actor outside the table (not
+    //    in the state's clock) flags the file for the host parser
+    if ((rc = table_upload(c))) return rc;
+    for (size_t i : dev4) {
+      DevState& x = ds[i];
+      auto& b = d->rd[i];
+      if ((e = b[7].reserve(8ull * x.n_dots + 8)) || (e = b[8].reserve(4ull * x.n_dots + 4)) ||
+          (e = b[9].reserve(8ull * x.n_dots + 8)))
+        return ctx->hip_fail(e, "state reader");
+      OrswotReadArgs a = read_args(c, d, i, x, out, 0);
+      a.col_member = b[7].as<unsigned long long>();
+      a.col_actor = b[8].as<uint32_t>();
+      a.col_value = b[9].as<unsigned long long>();
+      if ((e = launch_orswot_read(s, a, d->rd_tmp.p, d->rd_tmp.cap, 2))) return ctx->hip_fail(e, "state reader");
+    }
+    if (!dev4.empty() && ((e = hipMemcpyAsync(small, d->rd_misc.p, 8ull * n, hipMemcpyDeviceToHost, s)) ||
+                          (rc = sync("state reader")))) return rc ? rc : ctx->hip_fail(e, "state reader");
+    for (size_t i : dev4) {
+      if (small[2 * i + 1] == 0) {
+        ds[i].device = true;
+        c->path_counts["states_device_read"]++;
+      } else if ((rc = host_parse(i))) {
+        return rc;
+      }
     }
     for (size_t i = 0; i < n; i++)
       if (st[i] != CE_OK && first == CE_OK) first = st[i];
@@ -1343,38 +1465,38 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
   if (status_out) std::memcpy(status_out, st, n * 4);
   if (first != CE_OK) return first;  // nothing merged (lib.rs:431-456)
   HostPhase hp("states: merge");
+  uint64_t dev_dots = 0;
+  for (size_t i = 0; i < n; i++)
+    if (ds[i].device) dev_dots += ds[i].n_dots;
+  if ((rc = ensure_pairs(c, dev_dots))) return rc;
+  uint32_t* live = small + 6 * n;
+  // dense other-clocks in pinned memory, so the queued merges never wait on a pageable copy
+  const uint32_t ccap = d->clock_cap;
+  if ((e = d->rd_clock.reserve(8ull * ccap * n + 64))) return ctx->hip_fail(e, "merge");
+  auto* hclk = d->rd_clock.as<unsigned long long>();
+  for (size_t i = 0; i < n; i++)
+    if (ds[i].device) {
+      std::memset(hclk + (size_t)ccap * i, 0, 8ull * ccap);
+      for (auto& y : ds[i].oclock) hclk[(size_t)ccap * i + y.first] = y.second;
+    }
+  std::vector<uint8_t> queued(n, 0);
+  bool last_queued = false;
   for (size_t i = 0; i < n; i++) {  // lib.rs:458-466, in order
-    int rc;
     DevState& x = ds[i];
     if (x.device) {
-      IdDots oclock;
-      std::vector<std::pair<IdDots, std::vector<uint64_t>>> od;
-      if ((rc = id_dots(c, x.hs.clock, &oclock))) return rc;
-      for (auto& y : x.hs.deferred) {
-        IdDots k;
-        if ((rc = id_dots(c, y.first, &k))) return rc;
-        od.push_back({k, y.second});
-      }
-      if ((rc = table_upload(c)) || (rc = ensure_pairs(c, x.n_dots))) return rc;
-      if ((e = d->other[0].reserve(8ull * x.n_dots + 8)) || (e = d->other[1].reserve(4ull * x.n_dots + 4)) ||
-          (e = d->other[2].reserve(8ull * x.n_dots + 8)))
-        return ctx->hip_fail(e, "merge");
-      OrswotReadArgs a = read_args(c, d, i, x, out, 0);
-      a.col_member = d->other[0].as<unsigned long long>();
-      a.col_actor = d->other[1].as<uint32_t>();
-      a.col_value = d->other[2].as<unsigned long long>();
-      uint32_t fl;
-      if ((e = launch_orswot_read(s, a, d->rd_tmp.p, d->rd_tmp.cap, 2)) || (e = dl(&fl, a.flags, 4, s)))
-        return ctx->hip_fail(e, "state reader");
-      if (fl == 0) {
-        if ((rc = orswot_merge_cols(c, oclock, od, x.n_dots))) return rc;
-      } else {  // an entry names an actor outside the table (not in the state's clock)
-        if ((rc = host_parse(i))) return rc;
-        if (st[i] != CE_OK) return c->ctx->fail(CE_ERR_DEVICE, "state reader and host parser disagree");
-        if ((rc = orswot_merge_one(c, x.hs))) return rc;
-      }
+      auto& b = d->rd[i];
+      bool q = false;
+      if ((rc = ensure_pairs(c, x.n_dots)) ||
+          (rc = orswot_merge_cols(c, x.oclock, x.od,
+                                  {b[7].as<unsigned long long>(), b[8].as<uint32_t>(), b[9].as<unsigned long long>(),
+                                   hclk + (size_t)ccap * i, ccap},
+                                  x.n_dots, live + 4 * i, &q)))
+        return rc;
+      queued[i] = q;
+      last_queued = q;
     } else {
       if ((rc = orswot_merge_one(c, x.hs))) return rc;
+      last_queued = false;
     }
     for (auto& y : x.hs.nov) {
       uint32_t sl;
@@ -1382,6 +1504,17 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
       c->nov[sl] = std::max(c->nov[sl], y.second);
     }
   }
+  if ((rc = sync("merge"))) return rc;
+  for (size_t i = 0; i < n; i++)
+    if (queued[i] && live[4 * i + 2]) return ctx->fail(CE_ERR_DEVICE, "dot-set table overflow");
+  for (size_t i = n; i-- > 0;)
+    if (queued[i]) {
+      if (last_queued) {
+        d->live_pairs = live[4 * i];
+        d->used_pairs = live[4 * i + 1];
+      }
+      break;
+    }
   return table_upload(c);
 }
 

@@ -969,7 +969,7 @@ hipError_t launch_open_fold_v2(hipStream_t s, const DecodeArgs& a, int files_per
   // CE_V2_OPT (diagnostics, same-box A/B): the OPT bits of the default LPF 16 kernel
   static const int opt = [] {
     const char* e = getenv("CE_V2_OPT");
-    return e ? atoi(e) : 3;
+    return e ? atoi(e) : 1;  // SDWA rot16 on, next-ciphertext prefetch off (same-box A/B r02)
   }();
   if (files_per_wave == 2) {
     if (w == 4) launch_v2<32, 4, false>(s, a);

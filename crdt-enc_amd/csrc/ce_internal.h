@@ -82,7 +82,7 @@ struct ce_ctx {
   std::string last_error;
   // batch scratch (device)
   ce::DevBuf params, status, counters, extra, multi, partials, large, out, apply, refold, miss,
-      supported, blob, offs, nonces, out_offs, outer_ver, batch_counters, split;
+      supported, blob, offs, nonces, out_offs, outer_ver, batch_counters, split, segrec;
   ce::HostBuf h_counters, h_apply, h_stage, h_stage2;
   // marks the setup kernel's counter snapshot (h_counters + 128) as landed on the host
   hipEvent_t setup_ev = nullptr;

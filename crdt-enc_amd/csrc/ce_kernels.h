@@ -41,7 +41,9 @@ struct SegScratch {
   uint32_t* counters;     // [0] extra segments, [1] multi-segment files, [2] auth failures,
                           // [3] decode failures, [4] misses, [5] first failing index (min),
                           // [6] partial slots, [7] host-parse envelopes, [8] setup failures,
-                          // [9] large files, [12] gate: batch not in load_ops shape,
+                          // [9] large files, [11] / [14] multi-segment files folded from
+                          // segment records / decoded whole (k_segdec_apply),
+                          // [12] gate: batch not in load_ops shape,
                           // [13] gate: first gap
   uint2* extra_list;      // (file, seg) for segments j >= 1
   uint32_t extra_cap;
@@ -104,6 +106,13 @@ struct SplitScratch {
   uint4* part;     // [n_large * kSplitParts] (slot + 1 | 0 none | ~0 failed, 0, max lo, max hi)
 };
 hipError_t launch_decode_split(hipStream_t s, const DecodeArgs& a, SplitScratch sp, uint32_t n_large);
+// C4 fused decode: open segments of large files with the decode in the same pass (one-segment
+// files folded there; longer files leave per-segment records, 2 uint4 per Poly1305 partial
+// slot), then k_segdec_apply after launch_finalize_multi checks the records and folds
+hipError_t launch_segments_decode(hipStream_t s, const uint8_t* in, uint8_t* out, const DecodeArgs& da,
+                                  SegScratch sc, uint32_t grid_waves, uint4* rec);
+hipError_t launch_segdec_apply(hipStream_t s, const DecodeArgs& a, SegScratch sc, const uint4* rec,
+                               uint32_t n_large);
 
 // fused open + decode + fold of single-page files (ce_fused.hip); files_per_wave in {1, 2, 4}
 hipError_t launch_open_fold_small(hipStream_t s, const DecodeArgs& a, int files_per_wave);

@@ -179,12 +179,127 @@ __global__ __launch_bounds__(256) void k_seal_setup(const uint8_t* __restrict__ 
 // segment kernel: one wavefront per (file, 16 KiB segment)
 // ----------------------------------------------------------------------------------------
 static constexpr int kWavesPerBlock = 4;
-template <bool SEAL>
+static constexpr uint32_t kSegBytes = kSegBlocks * 16;
+
+__device__ void decode_file(const DecodeArgs& a, uint32_t f, uint32_t lane);
+
+// the 48-byte window at pt + p (unaligned global loads)
+__device__ __forceinline__ void dot_window(const uint8_t* pt, uint32_t p, uint32_t (&w)[12]) {
+  const uint4 A = *reinterpret_cast<const uint4*>(pt + p);
+  const uint4 B = *reinterpret_cast<const uint4*>(pt + p + 16);
+  const uint4 C = *reinterpret_cast<const uint4*>(pt + p + 32);
+  w[0] = A.x; w[1] = A.y; w[2] = A.z; w[3] = A.w;
+  w[4] = B.x; w[5] = B.y; w[6] = B.z; w[7] = B.w;
+  w[8] = C.x; w[9] = C.y; w[10] = C.z; w[11] = C.w;
+}
+
+// slot of an actor through a one-entry per-lane cache (a file's Dots are mostly its writer's)
+struct SlotCache {
+  uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, slot = 0xffffffffu;
+  __device__ __forceinline__ uint32_t get(const DecodeArgs& a, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
+    if (slot != 0xffffffffu && k0 == c0 && k1 == c1 && k2 == c2 && k3 == c3) return slot;
+    const uint32_t s = lookup_slot(a.table, a.mask, k0, k1, k2, k3);
+    if (s != 0xffffffffu) { c0 = k0; c1 = k1; c2 = k2; c3 = k3; slot = s; }
+    return s;
+  }
+};
+
+// C4's fused decode, part 1 (k_segments<false, true>, files of more than one segment): the
+// canonical Dots lying wholly inside this segment's plaintext [S, E), decoded speculatively
+// before the file's tag is known: segment 0 takes the Dot grid from the array header, a later
+// segment from the first canonical Dot in its first 64 bytes.  Nothing is folded here; the
+// record {first Dot offset | ~0, Dots, slot + 1 | 0 none | ~0 failed, Dot length},
+// {max lo, max hi} is checked against the file's true grid by k_segdec_apply after the tag.
+__device__ void seg_record(const DecodeArgs& a, const uint8_t* pt, uint32_t len, uint32_t S,
+                           uint32_t E, uint32_t lane, uint4* rec) {
+  uint32_t m = 0xffffffffu, L = 0;
+  if (S == 0) {
+    uint32_t hm = 0xffffffffu, hl = 0;
+    if (lane == 0 && len >= 16) {
+      Rd r{pt + 16, len - 16, 0};
+      uint64_t cnt = 0;
+      if (rd_array_hdr(r, &cnt) && 16 + r.i + 34 <= E) {
+        hm = 16 + (uint32_t)r.i;
+        hl = dot_len_of_marker(pt[hm + 33]);
+        if (hl == 0) hm = 0xffffffffu;
+      }
+    }
+    m = bcast(hm);
+    L = bcast(hl);
+  } else {
+    const uint32_t p = S + lane;
+    uint32_t Ll = 0;
+    bool v = false;
+    if (p + 34 <= E) {
+      Ll = dot_len_of_marker(pt[p + 33]);
+      if (Ll != 0 && p + Ll <= E) {
+        uint32_t w[12], k0, k1, k2, k3;
+        unsigned long long ctr;
+        dot_window(pt, p, w);
+        v = canon_dot(w, Ll, k0, k1, k2, k3, ctr);
+      }
+    }
+    const unsigned long long vm = __ballot(v);
+    if (vm) {
+      const uint32_t fl = (uint32_t)__builtin_ctzll(vm);
+      m = S + fl;
+      L = (uint32_t)__shfl((int)Ll, (int)fl);
+    }
+  }
+  uint32_t nd = 0, myslot = 0xffffffffu;
+  unsigned long long best = 0;
+  bool fail = false;
+  if (m != 0xffffffffu) {
+    SlotCache cache;
+    for (uint32_t base = m;;) {
+      const uint32_t p = base + lane * L;
+      const bool in = p + L <= E;
+      uint32_t w[12], k0 = 0, k1 = 0, k2 = 0, k3 = 0;
+      unsigned long long ctr = 0;
+      dot_window(pt, in ? p : m, w);
+      const bool valid = in && canon_dot(w, L, k0, k1, k2, k3, ctr);
+      const unsigned long long vm = __ballot(valid);
+      const uint32_t k = vm == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~vm);
+      if (lane < k) {
+        const uint32_t sl = cache.get(a, k0, k1, k2, k3);
+        if (sl == 0xffffffffu || (myslot != 0xffffffffu && sl != myslot)) fail = true;
+        else {
+          best = (myslot == 0xffffffffu || ctr > best) ? ctr : best;
+          myslot = sl;
+        }
+      }
+      nd += k;
+      base += k * L;
+      if (k < 64) break;
+    }
+  }
+  uint32_t mx = myslot == 0xffffffffu ? 0u : myslot + 1;
+  uint32_t mn = myslot == 0xffffffffu ? 0xffffffffu : myslot + 1;
+  unsigned long long bm = best;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint32_t omx = (uint32_t)__shfl_xor((int)mx, d), omn = (uint32_t)__shfl_xor((int)mn, d);
+    const unsigned long long ob = __shfl_xor(bm, d);
+    mx = omx > mx ? omx : mx;
+    mn = omn < mn ? omn : mn;
+    bm = ob > bm ? ob : bm;
+  }
+  const bool wfail = __ballot(fail) != 0 || (mx != 0 && mn != mx);
+  if (lane == 0) {
+    rec[0] = make_uint4(m, nd, wfail ? 0xffffffffu : mx, L);
+    rec[1] = make_uint4((uint32_t)bm, (uint32_t)(bm >> 32), 0u, 0u);
+  }
+}
+
+// DEC (open only): decode during the segment pass -- a one-segment file is decoded and folded
+// by its own wave once its tag verifies (decode_file, the plaintext just written is L2-hot); a
+// longer file's segments leave seg_record records (rec, indexed like the Poly1305 partials)
+template <bool SEAL, bool DEC>
 __global__ __launch_bounds__(256) void k_segments(const uint8_t* __restrict__ in,
                                                   uint8_t* __restrict__ out,
                                                   const FileParams* __restrict__ params, uint32_t n,
                                                   int32_t* __restrict__ status, SegScratch sc,
-                                                  int skip_small) {
+                                                  int skip_small, DecodeArgs da, uint4* rec) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWavesPerBlock * 64 * kKsStride];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wib = threadIdx.x >> 6;
@@ -295,6 +410,7 @@ __global__ __launch_bounds__(256) void k_segments(const uint8_t* __restrict__ in
 #pragma unroll
     for (int i = 0; i < 5; i++) tot.v[i] = bcast(tot.v[i]);
 
+    bool auth_ok = true;
     if (nseg == 1) {
       const uint32_t sv[4] = {Pp->s[0], Pp->s[1], Pp->s[2], Pp->s[3]};
       uint32_t tag[4];
@@ -309,6 +425,7 @@ __global__ __launch_bounds__(256) void k_segments(const uint8_t* __restrict__ in
       } else {
         const bool ok = ((tag[0] ^ Pp->tag[0]) | (tag[1] ^ Pp->tag[1]) | (tag[2] ^ Pp->tag[2]) |
                          (tag[3] ^ Pp->tag[3])) == 0;
+        auth_ok = ok;
         if (!ok) {
           // verify-before-release: scrub the speculative plaintext
           for (uint32_t b = lane * 16; b < len; b += 64 * 16) {
@@ -326,6 +443,17 @@ __global__ __launch_bounds__(256) void k_segments(const uint8_t* __restrict__ in
       uint32_t* pp = sc.partials + 5ull * (Pp->extra_base + j);
 #pragma unroll
       for (int i = 0; i < 5; i++) pp[i] = tot.v[i];
+    }
+    if (DEC) {
+      // this wave's plaintext stores complete before its lanes read each other's bytes
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      if (nseg == 1) {
+        if (auth_ok) decode_file(da, f, lane);
+      } else {
+        const uint32_t S = j * kSegBytes;
+        seg_record(da, dst, len, S, min(len, S + kSegBytes), lane, rec + 2ull * (Pp->extra_base + j));
+      }
     }
   }
 }
@@ -705,6 +833,110 @@ __global__ __launch_bounds__(256) void k_decode_split_apply(DecodeArgs a, SplitS
   }
 }
 
+// C4's fused decode, part 2: one wave per multi-segment file after k_finalize_multi (tags
+// known).  The file's true Dot grid (header, first Dot length) says which Dots lie wholly inside
+// each segment; every segment's record must match it exactly (first offset, count, length, one
+// resolved actor), lane j decodes the Dot crossing segment j's end from the plaintext in HBM,
+// and the maxima are folded.  Any mismatch -- another Dot length, a non-canonical Dot, a second
+// actor, a miss, a grid from a look-alike -- runs decode_file over the whole file instead.
+__global__ __launch_bounds__(256) void k_segdec_apply(DecodeArgs a, SegScratch sc, const uint4* __restrict__ rec) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t nm = *((volatile uint32_t*)&sc.counters[1]);
+  const uint32_t stride = gridDim.x * kWavesPerBlock;
+  for (uint32_t t = bcast(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)); t < nm; t += stride) {
+    const uint32_t f = bcast(sc.multi_files[t]);
+    const FileParams* Pp = a.params + f;
+    if (a.status[f] != CE_OK) continue;
+    const uint8_t* pt = a.pt + Pp->out_off;
+    const uint32_t len = Pp->len, nseg = Pp->nseg, eb = Pp->extra_base;
+    uint32_t hb = 0, hl = 0, hc = 0, hok = 0;
+    if (lane == 0 && len >= 16) {
+      const uint4 dv = *reinterpret_cast<const uint4*>(pt);
+      bool found = false;
+      for (uint32_t q = 0; q < a.n_supported; q++) {
+        const uint4 sv = *reinterpret_cast<const uint4*>(a.supported + 16 * q);
+        found |= dv.x == sv.x && dv.y == sv.y && dv.z == sv.z && dv.w == sv.w;
+      }
+      Rd r{pt + 16, len - 16, 0};
+      uint64_t c64 = 0;
+      if (found && rd_array_hdr(r, &c64) && c64 <= len) {
+        hb = 16 + (uint32_t)r.i;
+        hc = (uint32_t)c64;
+        hl = hb + 34 <= len ? dot_len_of_marker(pt[hb + 33]) : 0u;
+        hok = hl != 0 && (uint64_t)hb + (uint64_t)hc * hl <= len;
+      }
+    }
+    hok = bcast(hok);
+    const bool fold_ok = a.apply == nullptr || a.apply[f];
+    if (!hok || !fold_ok) {
+      if (lane == 0) atomicAdd(&a.counters[14], 1u);
+      decode_file(a, f, lane);
+      continue;
+    }
+    hb = bcast(hb);
+    hl = bcast(hl);
+    hc = bcast(hc);
+    bool bad = false;
+    uint32_t myslot = 0xffffffffu;
+    unsigned long long best = 0;
+    SlotCache cache;
+    auto take = [&](uint32_t sl, unsigned long long v) {
+      if (myslot != 0xffffffffu && sl != myslot) bad = true;
+      else {
+        best = (myslot == 0xffffffffu || v > best) ? v : best;
+        myslot = sl;
+      }
+    };
+    for (uint32_t j0 = 0; j0 < nseg; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      if (j >= nseg) continue;
+      const uint32_t S = j * kSegBytes, E = min(len, S + kSegBytes);
+      const uint32_t kf = S <= hb ? 0u : (S - hb + hl - 1) / hl;  // first grid Dot starting >= S
+      const uint32_t kw = E <= hb ? 0u : (E - hb) / hl;           // grid Dots ending <= E
+      const uint32_t ke = min(hc, kw);
+      const uint32_t en = ke > kf ? ke - kf : 0u;
+      const uint4 r0 = rec[2ull * (eb + j)], r1 = rec[2ull * (eb + j) + 1];
+      if (r0.y != en || (en != 0 && (r0.x != hb + kf * hl || r0.z == 0xffffffffu || r0.w != hl))) bad = true;
+      else if (en != 0 && r0.z != 0) take(r0.z - 1, (unsigned long long)r1.x | ((unsigned long long)r1.y << 32));
+      // the grid Dot that starts inside the segment and ends past E
+      const uint32_t ps = hb + kw * hl;
+      if (E > hb && kw < hc && ps < E && ps >= S) {
+        uint32_t w[12], k0, k1, k2, k3;
+        unsigned long long ctr;
+        dot_window(pt, ps, w);
+        if (!canon_dot(w, hl, k0, k1, k2, k3, ctr)) bad = true;
+        else {
+          const uint32_t sl = cache.get(a, k0, k1, k2, k3);
+          if (sl == 0xffffffffu) bad = true;
+          else take(sl, ctr);
+        }
+      }
+    }
+    if (__ballot(bad) != 0) {
+      if (lane == 0) atomicAdd(&a.counters[14], 1u);
+      decode_file(a, f, lane);
+      continue;
+    }
+    if (lane == 0) atomicAdd(&a.counters[11], 1u);
+    uint32_t mx = myslot == 0xffffffffu ? 0u : myslot + 1;
+    uint32_t mn = myslot == 0xffffffffu ? 0xffffffffu : myslot + 1;
+    unsigned long long bm = myslot == 0xffffffffu ? 0ull : best;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      const uint32_t omx = (uint32_t)__shfl_xor((int)mx, d), omn = (uint32_t)__shfl_xor((int)mn, d);
+      const unsigned long long ob = __shfl_xor(bm, d);
+      mx = omx > mx ? omx : mx;
+      mn = omn < mn ? omn : mn;
+      bm = ob > bm ? ob : bm;
+    }
+    if (mx != 0 && mn == mx) {
+      if (lane == 0) atomicMax(&a.batch[mx - 1], bm);
+    } else if (myslot != 0xffffffffu) {
+      atomicMax(&a.batch[myslot], best);
+    }
+  }
+}
+
 __global__ void k_merge_max(unsigned long long* __restrict__ dst,
                             const unsigned long long* __restrict__ src, uint32_t n) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -945,11 +1177,27 @@ hipError_t launch_segments(hipStream_t s, bool seal, const uint8_t* in, uint8_t*
   if (n == 0) return hipSuccess;
   const uint32_t blocks = (grid_waves + kWavesPerBlock - 1) / kWavesPerBlock;
   if (seal)
-    hipLaunchKernelGGL(k_segments<true>, dim3(blocks), dim3(256), 0, s, in, out, params, n,
-                       status, sc, 0);
+    hipLaunchKernelGGL((k_segments<true, false>), dim3(blocks), dim3(256), 0, s, in, out, params, n,
+                       status, sc, 0, DecodeArgs{}, (uint4*)nullptr);
   else
-    hipLaunchKernelGGL(k_segments<false>, dim3(blocks), dim3(256), 0, s, in, out, params, n,
-                       status, sc, skip_small ? 1 : 0);
+    hipLaunchKernelGGL((k_segments<false, false>), dim3(blocks), dim3(256), 0, s, in, out, params, n,
+                       status, sc, skip_small ? 1 : 0, DecodeArgs{}, (uint4*)nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_segments_decode(hipStream_t s, const uint8_t* in, uint8_t* out, const DecodeArgs& da,
+                                  SegScratch sc, uint32_t grid_waves, uint4* rec) {
+  if (da.n == 0) return hipSuccess;
+  const uint32_t blocks = (grid_waves + kWavesPerBlock - 1) / kWavesPerBlock;
+  hipLaunchKernelGGL((k_segments<false, true>), dim3(blocks), dim3(256), 0, s, in, out, da.params, da.n,
+                     da.status, sc, 1, da, rec);
+  return hipGetLastError();
+}
+
+hipError_t launch_segdec_apply(hipStream_t s, const DecodeArgs& a, SegScratch sc, const uint4* rec, uint32_t n_large) {
+  if (n_large == 0) return hipSuccess;
+  const uint32_t w = min(n_large, 256u * 32u);
+  hipLaunchKernelGGL(k_segdec_apply, dim3((w + kWavesPerBlock - 1) / kWavesPerBlock), dim3(256), 0, s, a, sc, rec);
   return hipGetLastError();
 }
 

@@ -18,6 +18,14 @@ __device__ __forceinline__ uint32_t rot(uint32_t x, int c) {
   }
   if (IMPL == 2) return (x << c) | (x >> (32 - c));                           // shl, shr, or
   if (IMPL == 4) return __builtin_amdgcn_alignbit(x, x, 32 - c);
+  if (IMPL >= 5) {  // full-rate VOP2 only: shl, shr, or (asm so the compiler cannot fold it back)
+    if (IMPL == 7 && c == 8) return __builtin_amdgcn_perm(x, x, 0x02010003u);
+    uint32_t h, l, r;
+    asm("v_lshlrev_b32 %0, %1, %2" : "=v"(h) : "i"(c), "v"(x));
+    asm("v_lshrrev_b32 %0, %1, %2" : "=v"(l) : "i"(32 - c), "v"(x));
+    asm("v_or_b32 %0, %1, %2" : "=v"(r) : "v"(h), "v"(l));
+    return r;
+  }
   // IMPL 3: v_lshl_or_b32(x, c, x >> (32 - c))
   uint32_t r;
   asm volatile("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "i"(c), "v"(x >> (32 - c)));
@@ -28,9 +36,9 @@ __device__ __forceinline__ uint32_t rot(uint32_t x, int c) {
 // a xor plus a (half-rate) v_alignbit_b32
 template <int IMPL>
 __device__ __forceinline__ uint32_t xr16(uint32_t d, uint32_t a) {
-  if (IMPL != 4) return rot<IMPL>(d ^ a, 16);
+  if (IMPL != 4 && IMPL != 6 && IMPL != 7) return rot<IMPL>(d ^ a, 16);
   uint32_t r;
-  asm volatile(
+  asm(
       "v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1\n"
       "v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0"
       : "=&v"(r) : "v"(d), "v"(a));
@@ -86,17 +94,20 @@ int main() {
   const int block = 256, iters = 64;
   uint32_t* o;
   CHECK(hipMalloc(&o, (size_t)256 * 16 * block * 4));
-  const char* names[5] = {"alignbit", "perm16/8+alignbit", "shl|shr", "lshl_or+shr", "sdwa-xor rot16"};
+  const char* names[8] = {"alignbit", "perm16/8+alignbit", "shl|shr", "lshl_or+shr", "sdwa-xor rot16", "shl/shr/or asm", "sdwa16+shl/shr/or", "sdwa16+perm8+shl/shr/or"};
   for (int occ : {2, 8}) {  // waves per SIMD
     const int grid = 256 * occ;  // 4 waves per block -> occ waves per SIMD
     const double blocks = (double)grid * block * iters;
-    float t[5][2];
+    float t[8][2];
     t[0][0] = run(k_chacha<0, 1>, o, grid, block, iters); t[0][1] = run(k_chacha<0, 2>, o, grid, block, iters);
     t[1][0] = run(k_chacha<1, 1>, o, grid, block, iters); t[1][1] = run(k_chacha<1, 2>, o, grid, block, iters);
     t[2][0] = run(k_chacha<2, 1>, o, grid, block, iters); t[2][1] = run(k_chacha<2, 2>, o, grid, block, iters);
     t[3][0] = run(k_chacha<3, 1>, o, grid, block, iters); t[3][1] = run(k_chacha<3, 2>, o, grid, block, iters);
     t[4][0] = run(k_chacha<4, 1>, o, grid, block, iters); t[4][1] = run(k_chacha<4, 2>, o, grid, block, iters);
-    for (int i = 0; i < 5; i++)
+    t[5][0] = run(k_chacha<5, 1>, o, grid, block, iters); t[5][1] = run(k_chacha<5, 2>, o, grid, block, iters);
+    t[6][0] = run(k_chacha<6, 1>, o, grid, block, iters); t[6][1] = run(k_chacha<6, 2>, o, grid, block, iters);
+    t[7][0] = run(k_chacha<7, 1>, o, grid, block, iters); t[7][1] = run(k_chacha<7, 2>, o, grid, block, iters);
+    for (int i = 0; i < 8; i++)
       printf("%d waves/SIMD %-20s 1 blk/lane %7.1f GB/s keystream   2 blk/lane %7.1f GB/s\n", occ, names[i],
              blocks * 64 / (t[i][0] * 1e-3) / 1e9, blocks * 2 * 64 / (t[i][1] * 1e-3) / 1e9);
   }
