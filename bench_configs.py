@@ -175,7 +175,7 @@ def run_c3(args, ctx, dev):
     NB = 6
     namer = ThreadPoolExecutor(NB - 1)
     names = []
-    obuf = [np.empty(1 << 20, np.uint8) for _ in range(NB)]
+    obuf = [np.zeros(1 << 25, np.uint8) for _ in range(NB)]  # committed pages, room for the file
 
     def step():
         t = time.perf_counter()
@@ -391,6 +391,11 @@ def run_c4(args, ctx, dev):
                    "dots": int(kd.sum())},
         "aead_GBps_end_to_end": round(ct / (ms / 1e3) / 1e9, 1),
         "kernels_ms_per_step": k_ms,
+        # multi-segment files folded from the segment pass's records vs decoded whole, over
+        # every ingest of the run (warmup + steps)
+        "decode_paths": {"ingests": args.warmup + args.steps,
+                         "segdec_records": core.path_count("segdec_records"),
+                         "segdec_fallback": core.path_count("segdec_fallback")},
         "checks": {"closed_form_state": ok},
     }
     print(json.dumps(line), flush=True)

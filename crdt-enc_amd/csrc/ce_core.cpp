@@ -757,7 +757,9 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
     const bool segdec = !(sdv && sdv[0] == '0') && !getenv("CE_SPLIT");
     if (!only) {
       SegScratch sc = segscratch(ctx, ec);
-      if (segdec && (e = ctx->segrec.reserve((size_t)ec * 2 * 32))) return ctx->hip_fail(e, "segment records");
+      if (segdec && ((e = ctx->segrec.reserve((size_t)ec * 2 * 32)) || (e = ctx->redo.reserve(n + 64)) ||
+                     (e = hipMemsetAsync(ctx->redo.p, 0, n, ctx->stream))))
+        return ctx->hip_fail(e, "segment records");
       int t = ctx->tbegin("segments_open");
       if ((e = segdec ? launch_segments_decode(ctx->stream, d_blob, ctx->out.as<uint8_t>(), da, sc,
                                                grid_waves_for(n + ec), ctx->segrec.as<uint4>())
@@ -771,8 +773,13 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
       ctx->tend(t);
       if (segdec) {
         t = ctx->tbegin("decode");
-        if ((e = launch_segdec_apply(ctx->stream, da, sc, ctx->segrec.as<uint4>(), n_large)))
+        DecodeArgs rd = da;
+        rd.redo = ctx->redo.as<uint8_t>();
+        if ((e = launch_segdec_apply(ctx->stream, rd, sc, ctx->segrec.as<uint4>(), n_large)))
           return ctx->hip_fail(e, "decode");
+        // files whose records did not prove out: the whole-file decode over the marked ones
+        rd.only = rd.redo;
+        if ((e = launch_decode_dots(ctx->stream, rd, grid_waves_for(n)))) return ctx->hip_fail(e, "decode");
         ctx->tend(t);
         return CE_OK;
       }
@@ -1572,15 +1579,24 @@ int ce_core_compact_into(ce_core* c, const uint8_t* nonce, uint8_t* dst, size_t 
   std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
   (void)hipSetDevice(c->ctx->device);
   std::vector<uint8_t>& f = c->file_buf;
+  c->sink = dst;
+  c->sink_cap = cap;
+  c->sink_len = 0;
   int rc = compact_bytes(c, nonce, &f);
+  c->sink = nullptr;
+  c->sink_cap = 0;
   if (rc) return rc;
-  *len = f.size();
-  if (cap < f.size()) return c->ctx->fail(CE_ERR_INVALID_ARG, "compact_into: buffer too small");
-  std::memcpy(dst, f.data(), f.size());
+  if (c->sink_len) {
+    *len = c->sink_len;
+  } else {
+    *len = f.size();
+    if (cap < f.size()) return c->ctx->fail(CE_ERR_INVALID_ARG, "compact_into: buffer too small");
+    std::memcpy(dst, f.data(), f.size());
+  }
   if (name_out) {
     HostPhase hp("sha3 name");
     uint8_t h[32];
-    sha3_256(dst, f.size(), h);
+    sha3_256(dst, *len, h);
     std::snprintf(name_out, 64, "%s", base32_nopad(h, 32).c_str());
   }
   return CE_OK;

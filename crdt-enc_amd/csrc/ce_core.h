@@ -68,6 +68,10 @@ struct ce_core {
   bool table_dirty = true;
   uint64_t table_gen = 0;               // bumped whenever an actor gets a slot or slots move
   std::vector<uint8_t> ser_buf, file_buf;  // compaction: serialized state, sealed file (reused)
+  // compact_into: the caller's buffer; a compaction that fits writes the file there directly
+  // (sink_len = its length) instead of into file_buf
+  uint8_t* sink = nullptr;
+  size_t sink_cap = 0, sink_len = 0;
   std::vector<uint32_t> sorted_slots;   // used slots in UUID byte order (BTreeMap order)
   uint64_t sorted_gen = ~0ull;
   std::vector<uint8_t> last_writers;    // writer list of the previous ingest and its slots

@@ -17,6 +17,8 @@
 #include <set>
 #include <thread>
 
+#include <memory>
+
 #include "ce_core.h"
 #include "ce_dotset.h"
 #include "ce_dotset_codec.h"
@@ -1015,6 +1017,19 @@ bool read_state(int kind, const uint8_t* p, size_t n, HostState* hs) {
   });
 }
 
+// id_dots without inserting: false when an actor is not in the table (safe on several threads)
+bool id_dots_lookup(const ce_core* c, const Dots& d, IdDots* out) {
+  out->clear();
+  out->reserve(d.size());
+  for (auto& x : d) {
+    auto it = c->slot_of.find(x.first);
+    if (it == c->slot_of.end()) return false;
+    out->push_back({actor_id_of_slot(c, it->second), x.second});
+  }
+  std::sort(out->begin(), out->end());
+  return true;
+}
+
 int id_dots(ce_core* c, Dots d, IdDots* out) {
   sort_dots(&d);
   out->clear();
@@ -1313,6 +1328,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     std::vector<uint64_t> poff(n + 1, 0);
     for (size_t i = 0; i < n; i++)
       poff[i + 1] = poff[i] + (st[i] == CE_OK ? std::min<uint64_t>(len[i], kPrefix) : 0);
+    auto ph = std::make_unique<HostPhase>("  rd: heads download");
     if ((e = d->rd_host.reserve(poff[n] + 64))) return ctx->hip_fail(e, "state head");
     uint8_t* hb = d->rd_host.as<uint8_t>();
     for (size_t i = 0; i < n; i++)
@@ -1320,6 +1336,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
           (e = hipMemcpyAsync(hb + poff[i], out + off[i], poff[i + 1] - poff[i], hipMemcpyDeviceToHost, s)))
         return ctx->hip_fail(e, "state head");
     if ((rc = sync("state head"))) return rc;
+    ph = std::make_unique<HostPhase>("  rd: heads parse");
     std::vector<size_t> dev;
     for (size_t i = 0; i < n; i++) {
       if (st[i] != CE_OK) continue;
@@ -1347,15 +1364,18 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     // 2) the states' actors into the table (the emitted columns carry their ids), then the
     //    entry-head search over every file (it covers the deferred map too: its VClock keys
     //    look alike)
+    ph = std::make_unique<HostPhase>("  rd: actors + search");
+    // clocks -> actor ids: read-only lookups on the host threads; a file naming an actor
+    // outside the table inserts it below, in file order (the order the ids are handed out in)
+    std::vector<uint8_t> need_insert(n, 0);
+    host_parallel_for(ctx, (uint32_t)dev.size(), [&](uint32_t k) {
+      if (!id_dots_lookup(c, ds[dev[k]].hs.clock, &ds[dev[k]].oclock)) need_insert[dev[k]] = 1;
+    });
+    for (size_t i : dev)
+      if (need_insert[i] && (rc = id_dots(c, ds[i].hs.clock, &ds[i].oclock))) return rc;
     size_t tmp_need = 0;
     for (size_t i : dev) {
       DevState& x = ds[i];
-      if ((rc = id_dots(c, x.hs.clock, &x.oclock))) return rc;
-      for (auto& y : x.hs.deferred) {
-        IdDots k;
-        if ((rc = id_dots(c, y.first, &k))) return rc;
-        x.od.push_back({k, y.second});
-      }
       const uint64_t ne = x.n_entries;
       auto& b = d->rd[i];
       if ((e = b[0].reserve(4ull * x.cap + 64)) || (e = b[1].reserve(4ull * x.cap + 64)) ||
@@ -1373,6 +1393,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     if (!dev.empty() && ((e = hipMemcpyAsync(small, d->rd_misc.p, 8ull * n, hipMemcpyDeviceToHost, s)) ||
                          (rc = sync("state reader")))) return rc ? rc : ctx->hip_fail(e, "state reader");
     // 3) the first N heads in position order are the entries: parse, chain, repeats, scan
+    ph = std::make_unique<HostPhase>("  rd: entries");
     std::vector<size_t> dev2;
     std::vector<uint32_t> found(n, 0);
     for (size_t i : dev) found[i] = small[2 * i];
@@ -1398,6 +1419,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     }
     if (!dev2.empty() && (rc = sync("state reader"))) return rc;
     // 4) the deferred maps after the entries, on the host
+    ph = std::make_unique<HostPhase>("  rd: tails");
     std::vector<uint64_t> toff(n + 1, 0), eend(n, 0);
     std::vector<size_t> dev3;
     for (size_t i : dev2) {
@@ -1436,6 +1458,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     }
     // 5) (member, actor id, value) columns of every entry Dot; an actor outside the table (not
     //    in the state's clock) flags the file for the host parser
+    ph = std::make_unique<HostPhase>("  rd: emit");
     if ((rc = table_upload(c))) return rc;
     for (size_t i : dev4) {
       DevState& x = ds[i];
@@ -1504,7 +1527,10 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
       c->nov[sl] = std::max(c->nov[sl], y.second);
     }
   }
-  if ((rc = sync("merge"))) return rc;
+  {
+    HostPhase hs("  merge: wait");
+    if ((rc = sync("merge"))) return rc;
+  }
   for (size_t i = 0; i < n; i++)
     if (queued[i] && live[4 * i + 2]) return ctx->fail(CE_ERR_DEVICE, "dot-set table overflow");
   for (size_t i = n; i-- > 0;)
@@ -1744,8 +1770,16 @@ int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t
     return x->hip_fail(e, "ds compact");
   if (clear_len > U) return x->fail(CE_ERR_DEVICE, "serializer overran its bound");
   const uint64_t total = 16 + sealed_len(clear_len);
-  file->resize(total);
-  if ((e = hipMemcpyAsync(file->data(), x->out.p, total, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s)))
+  uint8_t* to = nullptr;
+  if (c->sink && total <= c->sink_cap) {  // compact_into: straight into the caller's buffer
+    file->clear();
+    c->sink_len = total;
+    to = c->sink;
+  } else {
+    file->resize(total);
+    to = file->data();
+  }
+  if ((e = hipMemcpyAsync(to, x->out.p, total, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s)))
     return x->hip_fail(e, "ds compact download");
   return CE_OK;
 }

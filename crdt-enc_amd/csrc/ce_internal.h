@@ -7,6 +7,7 @@
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <functional>
 #include <vector>
 
 #include "ce_common.h"
@@ -67,7 +68,8 @@ struct OpenResult {
 }  // namespace ce
 
 namespace ce {
-struct Uploader;  // ce_upload.cpp: pinned staging ring + copy stream + host thread pool
+struct Uploader;  // ce_upload.cpp: pinned staging ring + copy stream
+struct HostPool;  // ce_upload.cpp: host worker threads (gather copies, per-file host parsing)
 }
 
 struct ce_storage {
@@ -82,11 +84,12 @@ struct ce_ctx {
   std::string last_error;
   // batch scratch (device)
   ce::DevBuf params, status, counters, extra, multi, partials, large, out, apply, refold, miss,
-      supported, blob, offs, nonces, out_offs, outer_ver, batch_counters, split, segrec;
+      supported, blob, offs, nonces, out_offs, outer_ver, batch_counters, split, segrec, redo;
   ce::HostBuf h_counters, h_apply, h_stage, h_stage2;
   // marks the setup kernel's counter snapshot (h_counters + 128) as landed on the host
   hipEvent_t setup_ev = nullptr;
   ce::Uploader* up = nullptr;  // host-buffer entry points (created on first use)
+  ce::HostPool* pool = nullptr;  // created on first use
   // kernel timing (ce_ctx_set_timing)
   bool timing = false;
   struct TimedLaunch {
@@ -161,5 +164,8 @@ uint32_t grid_waves_for(uint32_t work);
 // before later work on ctx->stream, no host synchronise)
 int stage_host_batch(ce_ctx* ctx, const uint8_t* const* files, const uint64_t* offs, uint32_t n);
 void destroy_uploader(ce_ctx* ctx);
+// fn(i) for i in [0, n) on the context's host threads (inline when n < 2); fn must not touch
+// HIP streams or shared mutable state
+void host_parallel_for(ce_ctx* ctx, uint32_t n, const std::function<void(uint32_t)>& fn);
 
 }  // namespace ce

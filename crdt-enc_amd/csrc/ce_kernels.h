@@ -94,6 +94,7 @@ struct DecodeArgs {
   unsigned long long* prof;     // diagnostics only (CE_PROF): per-wave phase cycles, 8 per wave
   const uint32_t* large_list;
   const uint8_t* blob;          // fused kernel: input files (ciphertext at FileParams.in_off)
+  uint8_t* redo;                // k_segdec_apply: files left to the whole-file decode
 };
 hipError_t launch_decode_dots(hipStream_t s, const DecodeArgs& a, uint32_t grid_waves);
 

@@ -212,16 +212,26 @@ struct SlotCache {
 // {max lo, max hi} is checked against the file's true grid by k_segdec_apply after the tag.
 __device__ void seg_record(const DecodeArgs& a, const uint8_t* pt, uint32_t len, uint32_t S,
                            uint32_t E, uint32_t lane, uint4* rec) {
-  uint32_t m = 0xffffffffu, L = 0;
+  uint32_t m = 0xffffffffu, L = 0, hcount = 0, hok = 0;
   if (S == 0) {
+    // the file's header for k_segdec_apply too: supported data version, Dot count, and
+    // whether the whole array fits the grid (crdt-enc/src/lib.rs:504-507)
     uint32_t hm = 0xffffffffu, hl = 0;
     if (lane == 0 && len >= 16) {
+      const uint4 dv = *reinterpret_cast<const uint4*>(pt);
+      bool found = false;
+      for (uint32_t q = 0; q < a.n_supported; q++) {
+        const uint4 sv = *reinterpret_cast<const uint4*>(a.supported + 16 * q);
+        found |= dv.x == sv.x && dv.y == sv.y && dv.z == sv.z && dv.w == sv.w;
+      }
       Rd r{pt + 16, len - 16, 0};
       uint64_t cnt = 0;
       if (rd_array_hdr(r, &cnt) && 16 + r.i + 34 <= E) {
         hm = 16 + (uint32_t)r.i;
         hl = dot_len_of_marker(pt[hm + 33]);
         if (hl == 0) hm = 0xffffffffu;
+        hcount = cnt <= len ? (uint32_t)cnt : 0u;
+        hok = found && hl != 0 && cnt <= len && (uint64_t)hm + cnt * hl <= len;
       }
     }
     m = bcast(hm);
@@ -287,7 +297,7 @@ __device__ void seg_record(const DecodeArgs& a, const uint8_t* pt, uint32_t len,
   const bool wfail = __ballot(fail) != 0 || (mx != 0 && mn != mx);
   if (lane == 0) {
     rec[0] = make_uint4(m, nd, wfail ? 0xffffffffu : mx, L);
-    rec[1] = make_uint4((uint32_t)bm, (uint32_t)(bm >> 32), 0u, 0u);
+    rec[1] = make_uint4((uint32_t)bm, (uint32_t)(bm >> 32), hcount, hok);
   }
 }
 
@@ -334,31 +344,42 @@ __global__ __launch_bounds__(256) void k_segments(const uint8_t* __restrict__ in
     const uint32_t rows = (nb + 63) >> 6;
 
     L5 acc = {{0, 0, 0, 0, 0}};
-    for (uint32_t row = 0; row < rows; row++) {
-      const uint32_t rb = b_lo + row * 64;  // first block of this row
-      if ((row & 3) == 0) {
-        const uint32_t page_byte = rb * 16;
-        __builtin_amdgcn_wave_barrier();
-        if (page_byte < len) {
-          uint32_t kb[16];
-          chacha_block(key, 1u + (page_byte >> 6) + lane, 0u, n2a, n2b, kb);
-          uint4* kd = reinterpret_cast<uint4*>(ks + lane * kKsStride);
-          kd[0] = make_uint4(kb[0], kb[1], kb[2], kb[3]);
-          kd[1] = make_uint4(kb[4], kb[5], kb[6], kb[7]);
-          kd[2] = make_uint4(kb[8], kb[9], kb[10], kb[11]);
-          kd[3] = make_uint4(kb[12], kb[13], kb[14], kb[15]);
-        }
-        __builtin_amdgcn_wave_barrier();
+    // a page = 4 rows of 64 pieces = the 64 ChaCha20 blocks the lanes compute together
+    for (uint32_t row0 = 0; row0 < rows; row0 += 4) {
+      // the page's ciphertext is loaded first: its latency hides under the page's keystream
+      uint4 xin[4];
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const uint32_t boff = (b_lo + (row0 + r) * 64 + lane) * 16;
+        xin[r] = make_uint4(0, 0, 0, 0);
+        if (row0 + r < rows && boff + 16 <= len) xin[r] = *reinterpret_cast<const uint4*>(src + boff);
       }
+      const uint32_t page_byte = (b_lo + row0 * 64) * 16;
+      __builtin_amdgcn_wave_barrier();
+      if (page_byte < len) {
+        uint32_t kb[16];
+        chacha_block(key, 1u + (page_byte >> 6) + lane, 0u, n2a, n2b, kb);
+        uint4* kd = reinterpret_cast<uint4*>(ks + lane * kKsStride);
+        kd[0] = make_uint4(kb[0], kb[1], kb[2], kb[3]);
+        kd[1] = make_uint4(kb[4], kb[5], kb[6], kb[7]);
+        kd[2] = make_uint4(kb[8], kb[9], kb[10], kb[11]);
+        kd[3] = make_uint4(kb[12], kb[13], kb[14], kb[15]);
+      }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const uint32_t row = row0 + r;
+      if (row >= rows) break;
+      const uint32_t rb = b_lo + row * 64;  // first block of this row
       const uint32_t blk = rb + lane;
       if (blk < nblk_ct) {
         const uint32_t boff = blk * 16;
-        const uint32_t q = (row & 3) * 64 + lane;  // piece within the page
+        const uint32_t q = (uint32_t)r * 64 + lane;  // piece within the page
         const uint4 k4 = *reinterpret_cast<const uint4*>(ks + (q >> 2) * kKsStride + (q & 3) * 16);
         uint4 x;
         const bool full = boff + 16 <= len;
         if (full) {
-          x = *reinterpret_cast<const uint4*>(src + boff);
+          x = xin[r];
         } else {
           uint32_t wv[4] = {0, 0, 0, 0};
           for (uint32_t b = 0; b < len - boff; b++) wv[b >> 2] |= (uint32_t)src[boff + b] << (8 * (b & 3));
@@ -390,6 +411,7 @@ __global__ __launch_bounds__(256) void k_segments(const uint8_t* __restrict__ in
         // length block: le64(aad_len = 0) || le64(ct_len)
         acc = add5(mulmod(acc, R), block_limbs(0u, 0u, len, 0u));
       }
+    }
     }
     // rotate so position p = lane holds the lane whose last block has weight r^(64 - p)
     L5 v;
@@ -838,7 +860,9 @@ __global__ __launch_bounds__(256) void k_decode_split_apply(DecodeArgs a, SplitS
 // each segment; every segment's record must match it exactly (first offset, count, length, one
 // resolved actor), lane j decodes the Dot crossing segment j's end from the plaintext in HBM,
 // and the maxima are folded.  Any mismatch -- another Dot length, a non-canonical Dot, a second
-// actor, a miss, a grid from a look-alike -- runs decode_file over the whole file instead.
+// actor, a miss, a grid from a look-alike -- marks the file in redo instead, for k_decode_dots
+// (the whole-file decode, launched next over the marked files; decode_file inline here cost
+// the common path its registers and a scratch frame).
 __global__ __launch_bounds__(256) void k_segdec_apply(DecodeArgs a, SegScratch sc, const uint4* __restrict__ rec) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t nm = *((volatile uint32_t*)&sc.counters[1]);
@@ -849,33 +873,23 @@ __global__ __launch_bounds__(256) void k_segdec_apply(DecodeArgs a, SegScratch s
     if (a.status[f] != CE_OK) continue;
     const uint8_t* pt = a.pt + Pp->out_off;
     const uint32_t len = Pp->len, nseg = Pp->nseg, eb = Pp->extra_base;
-    uint32_t hb = 0, hl = 0, hc = 0, hok = 0;
-    if (lane == 0 && len >= 16) {
-      const uint4 dv = *reinterpret_cast<const uint4*>(pt);
-      bool found = false;
-      for (uint32_t q = 0; q < a.n_supported; q++) {
-        const uint4 sv = *reinterpret_cast<const uint4*>(a.supported + 16 * q);
-        found |= dv.x == sv.x && dv.y == sv.y && dv.z == sv.z && dv.w == sv.w;
-      }
-      Rd r{pt + 16, len - 16, 0};
-      uint64_t c64 = 0;
-      if (found && rd_array_hdr(r, &c64) && c64 <= len) {
-        hb = 16 + (uint32_t)r.i;
-        hc = (uint32_t)c64;
-        hl = hb + 34 <= len ? dot_len_of_marker(pt[hb + 33]) : 0u;
-        hok = hl != 0 && (uint64_t)hb + (uint64_t)hc * hl <= len;
-      }
+    // the first 64 segments' records in one round trip; segment 0's carries the header
+    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
+    if (lane < nseg) {
+      q0 = rec[2ull * (eb + lane)];
+      q1 = rec[2ull * (eb + lane) + 1];
     }
-    hok = bcast(hok);
+    const uint32_t hok = (uint32_t)__shfl((int)q1.w, 0);
     const bool fold_ok = a.apply == nullptr || a.apply[f];
-    if (!hok || !fold_ok) {
-      if (lane == 0) atomicAdd(&a.counters[14], 1u);
-      decode_file(a, f, lane);
+    if (!hok || !fold_ok) {  // the whole-file decode (k_decode_dots over redo) takes it
+      if (lane == 0) {
+        a.redo[f] = 1;
+        atomicAdd(&a.counters[14], 1u);
+      }
       continue;
     }
-    hb = bcast(hb);
-    hl = bcast(hl);
-    hc = bcast(hc);
+    const uint32_t hb = (uint32_t)__shfl((int)q0.x, 0), hl = (uint32_t)__shfl((int)q0.w, 0),
+                   hc = (uint32_t)__shfl((int)q1.z, 0);
     bool bad = false;
     uint32_t myslot = 0xffffffffu;
     unsigned long long best = 0;
@@ -895,7 +909,7 @@ __global__ __launch_bounds__(256) void k_segdec_apply(DecodeArgs a, SegScratch s
       const uint32_t kw = E <= hb ? 0u : (E - hb) / hl;           // grid Dots ending <= E
       const uint32_t ke = min(hc, kw);
       const uint32_t en = ke > kf ? ke - kf : 0u;
-      const uint4 r0 = rec[2ull * (eb + j)], r1 = rec[2ull * (eb + j) + 1];
+      const uint4 r0 = j0 == 0 ? q0 : rec[2ull * (eb + j)], r1 = j0 == 0 ? q1 : rec[2ull * (eb + j) + 1];
       if (r0.y != en || (en != 0 && (r0.x != hb + kf * hl || r0.z == 0xffffffffu || r0.w != hl))) bad = true;
       else if (en != 0 && r0.z != 0) take(r0.z - 1, (unsigned long long)r1.x | ((unsigned long long)r1.y << 32));
       // the grid Dot that starts inside the segment and ends past E
@@ -913,8 +927,10 @@ __global__ __launch_bounds__(256) void k_segdec_apply(DecodeArgs a, SegScratch s
       }
     }
     if (__ballot(bad) != 0) {
-      if (lane == 0) atomicAdd(&a.counters[14], 1u);
-      decode_file(a, f, lane);
+      if (lane == 0) {
+        a.redo[f] = 1;
+        atomicAdd(&a.counters[14], 1u);
+      }
       continue;
     }
     if (lane == 0) atomicAdd(&a.counters[11], 1u);

@@ -9,6 +9,7 @@
 // PCIe rate.  The compute stream waits for the last chunk with an event (no host synchronise);
 // the kernels then run on the whole batch.
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <functional>
 #include <thread>
@@ -71,13 +72,11 @@ struct Uploader {
   HostBuf stage[2];
   hipEvent_t ev[2] = {nullptr, nullptr}, t0 = nullptr, t1 = nullptr, order = nullptr;
   bool used[2] = {false, false};
-  HostPool* pool = nullptr;
   ~Uploader() {
     if (copy) (void)hipStreamSynchronize(copy);
     for (auto e : {ev[0], ev[1], t0, t1, order})
       if (e) (void)hipEventDestroy(e);
     if (copy) (void)hipStreamDestroy(copy);
-    delete pool;
   }
 };
 
@@ -103,16 +102,33 @@ static int get_uploader(ce_ctx* ctx, Uploader** out) {
       delete u;
       return ctx->hip_fail(e, "uploader");
     }
-    u->pool = new HostPool(pool_threads());
     ctx->up = u;
   }
   *out = ctx->up;
   return CE_OK;
 }
 
+static HostPool* get_pool(ce_ctx* ctx) {
+  if (!ctx->pool) ctx->pool = new HostPool(pool_threads());
+  return ctx->pool;
+}
+
 void destroy_uploader(ce_ctx* ctx) {
   delete ctx->up;
   ctx->up = nullptr;
+  delete ctx->pool;
+  ctx->pool = nullptr;
+}
+
+void host_parallel_for(ce_ctx* ctx, uint32_t n, const std::function<void(uint32_t)>& fn) {
+  if (n < 2) {
+    for (uint32_t i = 0; i < n; i++) fn(i);
+    return;
+  }
+  std::atomic<uint32_t> next{0};
+  get_pool(ctx)->run([&](int) {
+    for (uint32_t i; (i = next.fetch_add(1)) < n;) fn(i);
+  });
 }
 
 // Logical blob = files[0] || files[1] || ... (offs: n+1 prefix sums).  Upload it into d_dst on
@@ -135,12 +151,13 @@ int upload_iov(ce_ctx* ctx, const uint8_t* const* files, const uint64_t* offs, u
     ctx->timed.push_back(t);
     tl = (int)ctx->timed.size() - 1;
   }
-  const int T = u->pool->size();
+  HostPool* pool = get_pool(ctx);
+  const int T = pool->size();
   for (uint64_t c0 = 0, k = 0; c0 < total; c0 += u->chunk, k ^= 1) {
     const uint64_t len = std::min<uint64_t>(u->chunk, total - c0);
     if (u->used[k] && (e = hipEventSynchronize(u->ev[k]))) return ctx->hip_fail(e, "upload ring");
     uint8_t* st = u->stage[k].as<uint8_t>();
-    u->pool->run([&](int t) {
+    pool->run([&](int t) {
       uint64_t lo = c0 + len * t / T, hi = c0 + len * (t + 1) / T;
       if (lo >= hi) return;
       // first file overlapping lo
