@@ -138,6 +138,59 @@ def new_core(ctx, key, flags=0):
     return core
 
 
+def gcounter_cpu_baseline(key, host_blob, h_offs, h_act, h_ver, check, what):
+    """oracle/ce_oracle.c on this host over a bounded sample of the workload, both modes
+    (bench.py's cpu_baseline legs); check(err, serialized) compares with the GPU path."""
+    import ctypes
+    sys.path.insert(0, REPO)
+    import bench
+    import oracle
+    model, avail, threads = bench.host_cpu()
+    s = len(h_offs) - 1
+    res = {}
+    for mode, best, th in (("best", True, threads), ("reference_shaped", False, min(16, threads))):
+        t = time.perf_counter()
+        err, ser = oracle.compact_ops_baseline(
+            oracle.STATE_GCOUNTER, key, APP, host_blob.ctypes.data_as(ctypes.c_void_p),
+            h_offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), h_act.ctypes.data_as(ctypes.c_void_p),
+            h_ver.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), s, th, best=best)
+        dt = time.perf_counter() - t
+        res[mode] = {"value": round(s / dt, 1), "cores": th, "seconds": round(dt, 3),
+                     "same_result_as_gpu": bool(check(err, ser))}
+    res["best"]["mode"] = "open + decode parallel over files, fold parallel over actors"
+    res["reference_shaped"]["mode"] = ("%d AEAD threads (buffered(16), lib.rs:497-514), decode + "
+                                       "fold on one thread" % res["reference_shaped"]["cores"])
+    # the headline is the faster mode (on a reject-path batch the reference-shaped one stops
+    # after the opens, while the best mode also runs its parallel decode check)
+    top = max(res, key=lambda k: res[k]["value"])
+    t = res[top]
+    return {"value": t["value"], "unit": "files/s", "cores": t["cores"], "kind": "port",
+            "sample": "%s; oracle/ce_oracle.c, %s mode (%s) on %d threads" % (what, top, t["mode"], t["cores"]),
+            "seconds": t["seconds"], "same_result_as_gpu": all(v["same_result_as_gpu"] for v in res.values()),
+            "host_cpu": model, "nproc": avail,
+            "modes": {k: dict(v, unit="files/s") for k, v in res.items()}}
+
+
+def orswot_cpu_baseline(key, state_files, op_files, actors, versions, gpu_state, what):
+    """The Python restatement (oracle/crdts.py Core) over a small sample: 1 core, a 'port'
+    figure for scale only (the restatement is pure Python: no best-CPU Orswot exists here)."""
+    sys.path.insert(0, REPO)
+    import bench
+    from oracle import crdts as C
+    model, avail, _ = bench.host_cpu()
+    t = time.perf_counter()
+    oc = C.Core("orswot")
+    rs = oc.read_remote_states(key, [APP, CORE], state_files)[0]
+    ro = oc.read_remote_ops(key, [APP, CORE], op_files, actors, versions)[0]
+    ser = oc.serialize()
+    dt = time.perf_counter() - t
+    nf = len(state_files) + len(op_files)
+    return {"value": round(nf / dt, 1), "unit": "files/s", "cores": 1, "kind": "port",
+            "sample": "%s; oracle/crdts.py (pure-Python restatement, one thread)" % what,
+            "seconds": round(dt, 3), "same_result_as_gpu": rs == 0 and ro == 0 and ser == gpu_state,
+            "host_cpu": model, "nproc": avail}
+
+
 def run_c3(args, ctx, dev):
     actors = actors_table()
     key = bytes(np.random.default_rng(7).integers(0, 256, 32, dtype=np.uint8))
@@ -256,6 +309,26 @@ def run_c3(args, ctx, dev):
     for p in parts:
         p.close()
 
+    # CPU baseline sample: state file 0 + the op files of the first A actors, GPU vs oracle
+    cpu = None
+    if not args.no_cpu:
+        A = args.c3_cpu_actors
+        flen = blob_len // n
+        p = new_core(ctx, key)
+        assert p.ingest_states([states[0]])[0] == 0
+        rc = p.ingest_ops_device(files.data_ptr(), offs.data_ptr(), A * V, A * V * flen,
+                                 b"".join(bytes(a) for a in actors[:A]),
+                                 fa[: A * V].contiguous().data_ptr(), fv[: A * V].contiguous().data_ptr())
+        gpu_sample = p.state_bytes() if rc == 0 else None
+        p.close()
+        hb = files[: A * V * flen].cpu().numpy().tobytes()
+        op_files = [hb[i * flen:(i + 1) * flen] for i in range(A * V)]
+        cpu = orswot_cpu_baseline(key, [states[0]], op_files,
+                                  [bytes(actors[i // V]) for i in range(A * V)],
+                                  [V0 + i % V for i in range(A * V)], gpu_sample,
+                                  "1 state file + %d op files (%d actors x %d versions) of this workload"
+                                  % (A * V, A, V))
+
     k_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in kern.items() if v[1]}
     n_state = len(states)
     ct = n * PT_LEN + sum(len(s) for s in states)
@@ -282,6 +355,7 @@ def run_c3(args, ctx, dev):
                  "peak_GBps": 8000.0},
         "kernels_ms_per_step": k_ms,
         "phases_ms_per_step": {k: round(v / args.steps, 3) for k, v in phase.items()},
+        "cpu_baseline": cpu,
         "checks": {"closed_form_clock": clock_ok, "sharded_merge_equals_whole": shard_ok},
     }
     print(json.dumps(line), flush=True)
@@ -380,6 +454,20 @@ def run_c4(args, ctx, dev):
                                                        for a in range(m)}}}}, use_bin_type=True)
     ok = core.state_bytes() == want
     ct = sum(pt_len)
+    cpu = None
+    if not args.no_cpu:  # the first A actors' files through the GPU path and the oracle
+        A = min(args.c4_cpu_actors, m)
+        sn = A * V
+        core.reset()
+        rc = core.ingest_ops_device(files.data_ptr(), offs.data_ptr(), sn, int(offs_h[sn]), wr[: 16 * A],
+                                    fa.data_ptr(), fv.data_ptr())
+        gpu_sample = core.state_bytes() if rc == 0 else None
+        hb = files[: int(offs_h[sn])].cpu().numpy()
+        h_act = np.ascontiguousarray(actors[np.repeat(np.arange(A), V)])
+        cpu = gcounter_cpu_baseline(KEY, hb, np.ascontiguousarray(offs_h[: sn + 1].astype(np.uint64)), h_act,
+                                    np.tile(np.arange(V, dtype=np.uint64), A), lambda e, ser: e == 0 and ser == gpu_sample,
+                                    "%d files (%d actors x %d versions, %.2f GB) of this workload"
+                                    % (sn, A, V, offs_h[sn] / 1e9))
     line = {
         "metric": "C4 skewed-size op files compacted/sec + AEAD GB/s (GCounter, 256 B-1 MiB)",
         "value": round(n / (ms / 1e3), 1), "unit": "files/s", "n_gpus": 1,
@@ -393,6 +481,7 @@ def run_c4(args, ctx, dev):
         "kernels_ms_per_step": k_ms,
         # multi-segment files folded from the segment pass's records vs decoded whole, over
         # every ingest of the run (warmup + steps)
+        "cpu_baseline": cpu,
         "decode_paths": {"ingests": args.warmup + args.steps,
                          "segdec_records": core.path_count("segdec_records"),
                          "segdec_fallback": core.path_count("segdec_fallback")},
@@ -410,8 +499,8 @@ def run_c5(args, ctx, dev):
     V = args.c5_versions
     ev, od = np.ascontiguousarray(actors[0::2]), np.ascontiguousarray(actors[1::2])
     t0 = time.time()
-    f0, o0, n0, l0 = bench.build_files(ctx, KEY, ev, V, dev, seed=1234)
-    f1, o1, n1, l1 = bench.build_files(ctx, KEY if args.c5_clean else key1, od, V, dev, seed=1235)
+    f0, o0, n0, l0, _ = bench.build_files(ctx, KEY, ev, actors, V, dev, seed=1234)
+    f1, o1, n1, l1, _ = bench.build_files(ctx, KEY if args.c5_clean else key1, od, actors, V, dev, seed=1235)
     n = n0 + n1
     files = torch.cat([f0[:l0], f1[:l1], torch.zeros(64, dtype=torch.uint8, device=dev)])
     del f0, f1
@@ -456,6 +545,25 @@ def run_c5(args, ctx, dev):
             ((k, ctx.timing(k)) for k in ("open_setup", "gate", "open_fold_small")) if v[1]}
     rc2, st = step(status=True)  # untimed: the statuses as a Python list for the check
     st = np.array(st, np.int32)
+    cpu = None
+    if not args.no_cpu:  # the first A actors under each key, GPU verdict vs the oracle's
+        A = min(args.c5_cpu_actors, ev.shape[0])
+        sn = A * V
+        sub = torch.cat([files[: sn * flen], files[l0: l0 + sn * flen], torch.zeros(64, dtype=torch.uint8, device=dev)])
+        so = torch.arange(2 * sn + 1, dtype=torch.int64, device=dev) * flen
+        sw = np.concatenate([ev[:A], od[:A]])
+        sfa = torch.from_numpy(np.repeat(np.arange(2 * A, dtype=np.int32), V)).to(dev)
+        sfv = torch.from_numpy(np.tile(np.arange(V, dtype=np.int64), 2 * A)).to(dev)
+        core.reset()
+        g_rc = core.ingest_ops_device(sub.data_ptr(), so.data_ptr(), 2 * sn, 2 * sn * flen,
+                                      b"".join(bytes(a) for a in sw), sfa.data_ptr(), sfv.data_ptr())
+        hb = sub[: 2 * sn * flen].cpu().numpy()
+        cpu = gcounter_cpu_baseline(KEY, hb, (np.arange(2 * sn + 1, dtype=np.uint64) * flen),
+                                    np.ascontiguousarray(sw[np.repeat(np.arange(2 * A), V)]),
+                                    np.tile(np.arange(V, dtype=np.uint64), 2 * A),
+                                    lambda e, ser: e == g_rc,
+                                    "%d files (%d actors under each key x %d versions; all opened, the batch rejected) "
+                                    "of this workload" % (2 * sn, A, V))
     checks = {"batch_rejected": (rc == 9 and rc2 == 9) != args.c5_clean, "statuses_match": bool((st == want).all()),
               "state_unchanged": (core.state_bytes() == empty) != args.c5_clean}
     line = {
@@ -467,9 +575,10 @@ def run_c5(args, ctx, dev):
                                "a second data key, %d files with a flipped tag bit; latest key only"
                                % (n, len(tam)),
                    "rejected": int((want != 0).sum())},
-        "aead_open_GBps": round(n * bench.PT_LEN / (k_ms["open_fold_small"] / 1e3) / 1e9, 1)
+        "aead_open_GBps": round(n * bench.pt_len("a") / (k_ms["open_fold_small"] / 1e3) / 1e9, 1)
         if k_ms.get("open_fold_small") else None,
         "kernels_ms_per_step": k_ms,
+        "cpu_baseline": cpu,
         "checks": checks,
     }
     print(json.dumps(line), flush=True)
@@ -483,6 +592,10 @@ def main():
     ap.add_argument("--c5-clean", action="store_true",
                     help="C5 control: every file under the latest key, none tampered (accept path)")
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--c3-cpu-actors", type=int, default=16, help="C3 CPU sample: op files of this many actors")
+    ap.add_argument("--c4-cpu-actors", type=int, default=256, help="C4 CPU sample: files of this many actors")
+    ap.add_argument("--c5-cpu-actors", type=int, default=128, help="C5 CPU sample: actors per key")
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--versions", type=int, default=16, help="op-file versions per actor")
     ap.add_argument("--state-versions", type=int, default=4, help="versions folded into states")

@@ -42,7 +42,7 @@ if fs and ws:
            "bytes_per_launch": round(fetch + write),
            "algorithmic_bytes_per_launch": files * 4101,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of "
-                     "bench.py --steps 2 --warmup 1 --no-cpu (1M files, past the 256 MiB L3); "
+                     "bench.py --steps 2 --warmup 1 --no-cpu --no-variant-b --no-host-buffers (1M files, past the 256 MiB L3); "
                      "FETCH_SIZE (KB) x 1024 x 2 (gfx950: FETCH_SIZE reports half of 16-B/lane "
                      "streaming reads) + WRITE_SIZE (KB) x 1024"}
     with open(os.path.join(prof, "traffic_open_fold_small.json"), "w") as f:
