@@ -307,7 +307,9 @@ int ce_core_import_dense(ce_core *c, const uint64_t *d_state, const uint64_t *d_
 int ce_core_dense_ready(ce_core *c);
 
 /* Diagnostics: how many times a code path ran on this core ("states_device_read",
- * "states_host_parse", "compact_device_writer"); lets tests show which path did the work. */
+ * "states_host_parse", "compact_device_writer"; per multi-segment op file "segdec_records"
+ * (folded from the segment pass's records) and "segdec_fallback" (decoded whole)); lets tests
+ * show which path did the work. */
 uint64_t ce_core_path_count(ce_core *c, const char *path);
 
 /* ---------------------------------------------------------------------------------------- */
