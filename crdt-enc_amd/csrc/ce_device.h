@@ -330,6 +330,13 @@ static constexpr int kKsStride = 80;  // LDS bytes per keystream block (64 + 16 
 
 __device__ __forceinline__ uint32_t bcast(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// atomicMax into the batch state, skipped when a plain read already shows a value >= v: the
+// state only grows during a launch, so a stale (smaller) read costs at most a redundant atomic.
+// Dots of many actors with random counters (C2 variant B) otherwise issue one L2 atomic each.
+__device__ __forceinline__ void batch_max(unsigned long long* p, unsigned long long v) {
+  if (v > *p) atomicMax(p, v);
+}
+
 __device__ __forceinline__ uint32_t lookup_slot(const ActorSlot* __restrict__ tab, uint32_t mask,
                                                 uint32_t k0, uint32_t k1, uint32_t k2,
                                                 uint32_t k3) {

@@ -213,14 +213,8 @@ __device__ __forceinline__ void decode_fold(const DecodeArgs& a, const SupVers& 
   // pending max per lane: flushed with atomicMax when the lane's actor changes
   uint32_t pslot = 0xffffffffu;
   unsigned long long pbest = 0;
-  auto fold_dot = [&](uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3, unsigned long long ctr) {
-    uint32_t slot;
-    // per-lane cache of the last resolved actor: a file's dots are usually its writer's
-    if (k0 == S.ck0 && k1 == S.ck1 && k2 == S.ck2 && k3 == S.ck3 && S.cslot != 0xffffffffu) slot = S.cslot;
-    else {
-      slot = lookup_slot(a.table, a.mask, k0, k1, k2, k3);
-      if (slot != 0xffffffffu) { S.ck0 = k0; S.ck1 = k1; S.ck2 = k2; S.ck3 = k3; S.cslot = slot; }
-    }
+  auto fold_slot = [&](uint32_t slot, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3,
+                       unsigned long long ctr) {
     if (slot == 0xffffffffu) {
       const uint32_t mi = atomicAdd(&a.counters[4], 1u);
       if (mi < a.miss_cap) a.miss_list[mi] = make_uint4(k0, k1, k2, k3);
@@ -228,10 +222,26 @@ __device__ __forceinline__ void decode_fold(const DecodeArgs& a, const SupVers& 
     } else if (slot == pslot) {
       pbest = ctr > pbest ? ctr : pbest;
     } else {
-      if (pslot != 0xffffffffu) atomicMax(&a.batch[pslot], pbest);
+      if (pslot != 0xffffffffu) batch_max(&a.batch[pslot], pbest);
       pslot = slot;
       pbest = ctr;
     }
+  };
+  // per-lane cache of the last resolved actor: a file's dots are usually its writer's
+  auto cached = [&](uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
+    return k0 == S.ck0 && k1 == S.ck1 && k2 == S.ck2 && k3 == S.ck3 && S.cslot != 0xffffffffu;
+  };
+  auto remember = [&](uint32_t slot, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
+    if (slot != 0xffffffffu) { S.ck0 = k0; S.ck1 = k1; S.ck2 = k2; S.ck3 = k3; S.cslot = slot; }
+  };
+  auto fold_dot = [&](uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3, unsigned long long ctr) {
+    uint32_t slot;
+    if (cached(k0, k1, k2, k3)) slot = S.cslot;
+    else {
+      slot = lookup_slot(a.table, a.mask, k0, k1, k2, k3);
+      remember(slot, k0, k1, k2, k3);
+    }
+    fold_slot(slot, k0, k1, k2, k3, ctr);
   };
   // fast path: every Dot canonical with the first Dot's length L0, so Dot i sits at pos + i L0.
   // A round takes two Dots per lane (done + sub and done + LPF + sub): their 26 LDS reads are in
@@ -370,9 +380,9 @@ __device__ __forceinline__ void decode_fold(const DecodeArgs& a, const SupVers& 
     const uint32_t mn = grp_reduce<LPF>(lo, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
     const unsigned long long b = grp_max64<LPF>(pslot == 0xffffffffu ? 0ull : pbest);
     if (mx != 0 && mn == mx) {
-      if (sub == 0) atomicMax(&a.batch[mx - 1], b);
+      if (sub == 0) batch_max(&a.batch[mx - 1], b);
     } else if (pslot != 0xffffffffu) {
-      atomicMax(&a.batch[pslot], pbest);
+      batch_max(&a.batch[pslot], pbest);
     }
   }
   if (live && st != CE_OK && sub == 0) {

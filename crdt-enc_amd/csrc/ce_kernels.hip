@@ -593,7 +593,7 @@ __device__ void decode_file(const DecodeArgs& a, uint32_t f, uint32_t lane) {
       } else if (slot == pslot) {
         pbest = ctr > pbest ? ctr : pbest;
       } else {
-        if (pslot != 0xffffffffu) atomicMax(&a.batch[pslot], pbest);
+        if (pslot != 0xffffffffu) batch_max(&a.batch[pslot], pbest);
         pslot = slot;
         pbest = ctr;
       }
@@ -687,9 +687,9 @@ __device__ void decode_file(const DecodeArgs& a, uint32_t f, uint32_t lane) {
           b = ob > b ? ob : b;
         }
         if (mx != 0 && mn == mx) {
-          if (lane == 0) atomicMax(&a.batch[mx - 1], b);
+          if (lane == 0) batch_max(&a.batch[mx - 1], b);
         } else if (pslot != 0xffffffffu) {
-          atomicMax(&a.batch[pslot], pbest);
+          batch_max(&a.batch[pslot], pbest);
         }
       }
     }
@@ -848,7 +848,7 @@ __global__ __launch_bounds__(256) void k_decode_split_apply(DecodeArgs a, SplitS
     const bool anyfail = __ballot(lane < kSplitParts && rec.x == 0xffffffffu) != 0;
     if (!anyfail) {
       if (lane < kSplitParts && rec.x != 0)
-        atomicMax(&a.batch[rec.x - 1], (unsigned long long)rec.z | ((unsigned long long)rec.w << 32));
+        batch_max(&a.batch[rec.x - 1], (unsigned long long)rec.z | ((unsigned long long)rec.w << 32));
     } else {
       decode_file(a, f, lane);
     }
@@ -946,9 +946,9 @@ __global__ __launch_bounds__(256) void k_segdec_apply(DecodeArgs a, SegScratch s
       bm = ob > bm ? ob : bm;
     }
     if (mx != 0 && mn == mx) {
-      if (lane == 0) atomicMax(&a.batch[mx - 1], bm);
+      if (lane == 0) batch_max(&a.batch[mx - 1], bm);
     } else if (myslot != 0xffffffffu) {
-      atomicMax(&a.batch[myslot], best);
+      batch_max(&a.batch[myslot], best);
     }
   }
 }
