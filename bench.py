@@ -268,7 +268,13 @@ class Workload:
         if self.world > 1:
             dist.barrier()
         torch.cuda.synchronize()
+        names = ("open_setup", "gate", "open_fold_small", "segments_open", "finalize_open", "decode",
+                 "merge", "seal_setup", "segments_seal", "finalize_seal")
+        # the timed steps carry HIP events around the fused kernel only (every timed launch adds
+        # two stream markers); the other kernels are timed on two extra steps afterwards
+        time_all = bool(os.environ.get("CE_BENCH_TIME_ALL"))
         ctx.timing_reset()
+        ctx.set_timing_only(None if time_all else "open_fold_small")
         ctx.set_timing(True)
         t0 = time.perf_counter()
         for _ in range(steps):
@@ -283,9 +289,16 @@ class Workload:
         ms_t = torch.tensor([ms], dtype=torch.float64, device=self.dense.device)
         if self.world > 1:
             shard.all_reduce_(ms_t, dist.ReduceOp.MAX)
-        kern = {k: ctx.timing(k) for k in ("open_setup", "gate", "open_fold_small", "segments_open",
-                                           "finalize_open", "decode", "merge", "seal_setup",
-                                           "segments_seal", "finalize_seal")}
+        kern = {k: ctx.timing(k) for k in names}
+        if not time_all:
+            ctx.timing_reset()
+            ctx.set_timing_only(None)
+            ctx.set_timing(True)
+            for _ in range(2):
+                self.step()
+            self.drain_names()
+            ctx.set_timing(False)
+            kern.update({k: ctx.timing(k) for k in names if k != "open_fold_small"})
         ok = True
         if self.rank == 0:
             sb = self.core.state_bytes()

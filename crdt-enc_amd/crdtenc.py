@@ -45,7 +45,7 @@ EXPORTS = [
     "ce_core_register_actors", "ce_core_dense_capacity", "ce_core_export_dense",
     "ce_core_import_dense", "ce_vbuf_init", "ce_vbuf_remaining", "ce_vbuf_chunk",
     "ce_vbuf_advance", "ce_vbuf_chunks_vectored", "ce_ctx_set_timing", "ce_ctx_timing_read",
-    "ce_ctx_timing_reset", "ce_core_reset", "ce_core_merge_state", "ce_core_dense_ready",
+    "ce_ctx_timing_reset", "ce_ctx_set_timing_only", "ce_core_reset", "ce_core_merge_state", "ce_core_dense_ready",
     "ce_keys_decode", "ce_keys_from_remote_metas", "ce_keys_merge", "ce_keys_free",
     "ce_keys_count", "ce_keys_latest", "ce_keys_get", "ce_keys_at", "ce_core_set_keys",
     "ce_core_apply_ops_batch", "ce_core_ingest_ops_iov", "ce_core_compact_ops_iov",
@@ -181,6 +181,11 @@ class Context:
 
     def set_timing(self, enable=True):
         self.check(lib().ce_ctx_set_timing(self.p, 1 if enable else 0), "set_timing")
+
+    def set_timing_only(self, kernel=None):
+        """Time only launches named `kernel` (None: every launch)."""
+        self.check(lib().ce_ctx_set_timing_only(self.p, kernel.encode() if kernel else None),
+                   "set_timing_only")
 
     def timing(self, kernel):
         """(total_ms, launches) of one kernel since the last reset (HIP events on our stream)."""

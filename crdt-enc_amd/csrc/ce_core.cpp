@@ -654,13 +654,16 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
   if ((e = ctx->out.reserve(blob_len + 16ull * n + 128)) || (e = ctx->status.reserve(n * 4ull + 64)) ||
       (e = ctx->apply.reserve(n + 64)) || (e = ctx->refold.reserve(n + 64)) ||
       (e = c->d_refold2.reserve(n + 64)) || (e = ctx->miss.reserve(65536 * 16)) ||
-      (e = c->d_gate.reserve(m * 24ull + 64)) || (e = ctx->h_stage2.reserve(m * 20ull + 64)) ||
-      (after_commit && (e = c->d_wslot.reserve(m * 4ull + 64))))
+      (e = c->d_gate.reserve(m * 32ull + 64)) || (e = ctx->h_stage2.reserve(m * 24ull + 64)) ||
+      (e = ctx->redo.reserve(n + 64)))
     return ctx->hip_fail(e, "ingest reserve");
 
-  // expected versions per writer (next_op_versions.get, lib.rs:481) -> device
+  // expected versions per writer (next_op_versions.get, lib.rs:481) and the writers' slots ->
+  // device in one copy.  Device gate block: e0 u64[m] | wslot u32[m] (8m bytes) | newnov u64[m]
+  // | run_count u32[m] | run_first u32[m]; host stage: e0 | wslot | nov read back
   uint64_t* he0 = ctx->h_stage2.as<uint64_t>();
   for (uint32_t a = 0; a < m; a++) he0[a] = c->nov[wslot[a]];
+  std::memcpy(he0 + m, wslot.data(), m * 4ull);
   GateArgs ga{};
   ga.fa = d_fa;
   ga.fv = d_fv;
@@ -668,17 +671,25 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
   ga.m = m;
   uint8_t* gbase = c->d_gate.as<uint8_t>();
   ga.e0 = reinterpret_cast<const uint64_t*>(gbase);
-  ga.newnov = reinterpret_cast<unsigned long long*>(gbase + 8ull * m);
-  ga.run_count = reinterpret_cast<uint32_t*>(gbase + 16ull * m);
-  ga.run_first = reinterpret_cast<uint32_t*>(gbase + 20ull * m);
+  ga.newnov = reinterpret_cast<unsigned long long*>(gbase + 16ull * m);
+  ga.run_count = reinterpret_cast<uint32_t*>(gbase + 24ull * m);
+  ga.run_first = reinterpret_cast<uint32_t*>(gbase + 28ull * m);
   ga.flags = ctx->counters.as<uint32_t>() + 12;  // [12] not grouped, [13] first gap
   ga.apply = ctx->apply.as<uint8_t>();
 
-  // 1) GPU: setup (outer version, envelope, key schedule) + device gate
+  // 1) GPU: scratch initialisation (one launch: counters, gate, batch state, miss / redo
+  //    marks), setup (outer version, envelope, key schedule), device gate
   uint32_t ec;
   {
+    FillArgs fl{};
+    fl.r[0] = {reinterpret_cast<uint32_t*>(gbase + 16ull * m), 4ull * m, 0u};  // newnov, runs
+    fl.r[1] = {c->d_batch.as<uint32_t>(), 2ull * c->cap, 0u};
+    fl.r[2] = {ctx->refold.as<uint32_t>(), (n + 3ull) / 4, 0u};
+    fl.r[3] = {ctx->redo.as<uint32_t>(), (n + 3ull) / 4, 0u};
+    fl.n = 4;
     // device_open's setup only; the fused kernel replaces its segment pass for small files
-    int rr = device_open_setup(ctx, d_blob, d_offs, n, blob_len, true, key, ctx->status.as<int32_t>(), &ec);
+    int rr = device_open_setup(ctx, d_blob, d_offs, n, blob_len, true, key, ctx->status.as<int32_t>(),
+                               &ec, &fl);
     if (rr) return rr;
   }
   // the setup's counters (large-file count [9]) -> host behind an event: read while the fused
@@ -691,19 +702,13 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
     return ctx->hip_fail(e, "setup counters");
   bool setup_known = false;
   uint32_t n_large = 0;
-  if ((e = hipMemcpyAsync(gbase, he0, m * 8ull, hipMemcpyHostToDevice, ctx->stream)) ||
-      (e = hipMemsetAsync(gbase + 8ull * m, 0, 16ull * m, ctx->stream)) ||
-      (e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ga.flags + 1), 0xffffffffu, 1, ctx->stream)))
+  if ((e = hipMemcpyAsync(gbase, he0, m * 16ull, hipMemcpyHostToDevice, ctx->stream)))
     return ctx->hip_fail(e, "gate upload");
   {
     const int t = ctx->tbegin("gate");
     if ((e = launch_gate(ctx->stream, ga))) return ctx->hip_fail(e, "gate");
     ctx->tend(t);
   }
-  if ((e = hipMemsetAsync(c->d_batch.p, 0, c->cap * 8ull, ctx->stream)) ||
-      (e = hipMemsetAsync(ctx->refold.p, 0, n, ctx->stream)))
-    return ctx->hip_fail(e, "ingest memset");
-
   DecodeArgs da{};
   da.pt = ctx->out.as<uint8_t>();
   da.blob = d_blob;
@@ -757,9 +762,7 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
     const bool segdec = !(sdv && sdv[0] == '0') && !getenv("CE_SPLIT");
     if (!only) {
       SegScratch sc = segscratch(ctx, ec);
-      if (segdec && ((e = ctx->segrec.reserve((size_t)ec * 2 * 32)) || (e = ctx->redo.reserve(n + 64)) ||
-                     (e = hipMemsetAsync(ctx->redo.p, 0, n, ctx->stream))))
-        return ctx->hip_fail(e, "segment records");
+      if (segdec && (e = ctx->segrec.reserve((size_t)ec * 2 * 32))) return ctx->hip_fail(e, "segment records");
       int t = ctx->tbegin("segments_open");
       if ((e = segdec ? launch_segments_decode(ctx->stream, d_blob, ctx->out.as<uint8_t>(), da, sc,
                                                grid_waves_for(n + ec), ctx->segrec.as<uint4>())
@@ -787,9 +790,9 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
     const int t = ctx->tbegin("decode");
     // CE_SPLIT=1: k_decode_split (measured slower on C4: 1.67 vs 1.36 ms)
     if (only || !getenv("CE_SPLIT")) {
-      // counters[15]: the large-file list's pull index (k_decode_dots, large_only && !only)
-      if ((!only && (e = hipMemsetAsync(ctx->counters.as<uint32_t>() + 15, 0, 4, ctx->stream))) ||
-          (e = launch_decode_dots(ctx->stream, da, grid_waves_for(n))))
+      // counters[15]: the large-file list's pull index (k_decode_dots, large_only && !only),
+      // zeroed with the counter block
+      if ((e = launch_decode_dots(ctx->stream, da, grid_waves_for(n))))
         return ctx->hip_fail(e, "decode");
     } else {
       // every record a file's apply step reads is written by this batch's parts (no memset)
@@ -811,18 +814,16 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
       return ctx->hip_fail(e, "merge");
     ctx->tend(t);
   }
-  uint64_t* hnov = he0 + m;
-  if ((e = hipMemcpyAsync(hnov, gbase + 8ull * m, m * 8ull, hipMemcpyDeviceToHost, ctx->stream)))
-    return ctx->hip_fail(e, "nov");
-  if (after_commit) {
-    uint32_t* hw = reinterpret_cast<uint32_t*>(he0 + 2ull * m);
-    std::memcpy(hw, wslot.data(), m * 4ull);
-    if ((e = hipMemcpyAsync(c->d_wslot.p, hw, m * 4ull, hipMemcpyHostToDevice, ctx->stream)))
-      return ctx->hip_fail(e, "writer slots");
-    const NovApply na{c->d_wslot.as<uint32_t>(), reinterpret_cast<const unsigned long long*>(gbase + 8ull * m),
-                      m, ctx->counters.as<uint32_t>()};
+  if (after_commit) {  // the compaction, queued behind the commit (the writers' slots came with e0)
+    const NovApply na{reinterpret_cast<const uint32_t*>(gbase + 8ull * m),
+                      reinterpret_cast<const unsigned long long*>(gbase + 16ull * m), m,
+                      ctx->counters.as<uint32_t>()};
     if ((rc = (*after_commit)(na))) return rc;
   }
+  // the gate's next_op_versions and the counter block, read back together at the end
+  uint64_t* hnov = he0 + 2ull * m;
+  if ((e = hipMemcpyAsync(hnov, gbase + 16ull * m, m * 8ull, hipMemcpyDeviceToHost, ctx->stream)))
+    return ctx->hip_fail(e, "nov");
   if (prof) {
     std::vector<unsigned long long> hp(8ull * 65536);
     if ((e = hipMemcpyAsync(hp.data(), prof_buf.p, hp.size() * 8, hipMemcpyDeviceToHost, ctx->stream)) ||
@@ -842,7 +843,7 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
   }
   uint32_t* hc = ctx->h_counters.as<uint32_t>();
   if ((e = hipMemcpyAsync(hc, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->stream)) ||
-      (e = hipStreamSynchronize(ctx->stream)))
+      (e = ctx->sync_spin()))
     return ctx->hip_fail(e, "fold sync");
   const bool merged_on_device = (hc[2] | hc[3] | hc[4] | hc[7] | hc[8] | hc[12]) == 0;
   if (merged_out) *merged_out = merged_on_device;
@@ -969,7 +970,7 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
     ctx->tend(t);
     if (!host_gated) {
       std::vector<uint64_t> nn(m);
-      if ((e = hipMemcpyAsync(nn.data(), gbase + 8ull * m, m * 8ull, hipMemcpyDeviceToHost, ctx->stream)) ||
+      if ((e = hipMemcpyAsync(nn.data(), gbase + 16ull * m, m * 8ull, hipMemcpyDeviceToHost, ctx->stream)) ||
           (e = hipStreamSynchronize(ctx->stream)))
         return ctx->hip_fail(e, "nov");
       for (uint32_t a = 0; a < m; a++) expect[a] = std::max(expect[a], nn[a]);

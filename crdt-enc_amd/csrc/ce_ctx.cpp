@@ -106,11 +106,16 @@ static hipError_t reset_counters(ce_ctx* ctx) {
 
 int device_open_setup(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
                       uint64_t blob_len, bool outer, const KeyRef& key, int32_t* d_status,
-                      uint32_t* extra_cap) {
+                      uint32_t* extra_cap, FillArgs* fills) {
   int rc = reserve_batch(ctx, n, blob_len, extra_cap);
   if (rc) return rc;
   hipError_t e;
-  if ((e = reset_counters(ctx)) != hipSuccess) return ctx->hip_fail(e, "memset counters");
+  if (fills) {  // the caller's scratch and the counter block in one launch
+    fills->counters = ctx->counters.as<uint32_t>();
+    if ((e = launch_fill(ctx->stream, *fills)) != hipSuccess) return ctx->hip_fail(e, "fill");
+  } else if ((e = reset_counters(ctx)) != hipSuccess) {
+    return ctx->hip_fail(e, "memset counters");
+  }
   SegScratch sc = segscratch(ctx, *extra_cap);
   const int t = ctx->tbegin("open_setup");
   if ((e = launch_open_setup(ctx->stream, d_blob, d_offs, n, outer, dev_key(key), key_status(key),
@@ -305,6 +310,7 @@ void ce_ctx_destroy(ce_ctx* c) {
   for (auto& t : c->timed) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   if (c->setup_ev) (void)hipEventDestroy(c->setup_ev);
+  if (c->spin_ev) (void)hipEventDestroy(c->spin_ev);
   destroy_uploader(c);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -335,6 +341,13 @@ int ce_ctx_set_timing(ce_ctx* c, int enable) {
   if (!c) return CE_ERR_INVALID_ARG;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   c->timing = enable != 0;
+  return CE_OK;
+}
+
+int ce_ctx_set_timing_only(ce_ctx* c, const char* kernel) {
+  if (!c) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  c->timing_only = kernel ? kernel : "";
   return CE_OK;
 }
 

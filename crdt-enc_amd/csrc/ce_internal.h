@@ -109,8 +109,9 @@ struct ce_ctx {
     return e;
   }
   // brackets one launch: t0 = begin(name) ... end(t0)
+  std::string timing_only;  // ce_ctx_set_timing_only: time one kernel name ("" = all)
   int tbegin(const char* name) {
-    if (!timing) return -1;
+    if (!timing || (!timing_only.empty() && timing_only != name)) return -1;
     TimedLaunch t{name, take_event(), take_event()};
     (void)hipEventRecord(t.a, stream);
     timed.push_back(t);
@@ -118,6 +119,20 @@ struct ce_ctx {
   }
   void tend(int idx) {
     if (idx >= 0) (void)hipEventRecord(timed[idx].b, stream);
+  }
+
+  // stream synchronise by polling an event (CE_SYNC_YIELD=1: hipStreamSynchronize).  The
+  // blocking wait's wake-up costs tens of microseconds per step on the box; a step waits once.
+  hipEvent_t spin_ev = nullptr;
+  hipError_t sync_spin() {
+    static const bool yield = getenv("CE_SYNC_YIELD") != nullptr;
+    if (yield) return hipStreamSynchronize(stream);
+    hipError_t e;
+    if (!spin_ev && (e = hipEventCreateWithFlags(&spin_ev, hipEventDisableTiming))) return e;
+    if ((e = hipEventRecord(spin_ev, stream))) return e;
+    while ((e = hipEventQuery(spin_ev)) == hipErrorNotReady) {
+    }
+    return e;
   }
 
   int fail(int code, const std::string& msg) {
@@ -140,7 +155,7 @@ DevKey dev_key(const KeyRef& k);
 // per-file statuses and ctx->params the FileParams; counters are copied to h_counters.
 int device_open_setup(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
                       uint64_t blob_len, bool outer, const KeyRef& key, int32_t* d_status,
-                      uint32_t* extra_cap);
+                      uint32_t* extra_cap, FillArgs* fills = nullptr);
 SegScratch segscratch(ce_ctx* ctx, uint32_t extra_cap);
 int device_open(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
                 uint64_t blob_len, bool outer, const KeyRef& key, uint8_t* d_out,

@@ -52,6 +52,22 @@ struct SegScratch {
   uint32_t* large_list;   // files with more than one page (counters[9] entries)
 };
 
+// One launch for an ingest's scratch initialisation (each hipMemsetAsync is its own blit
+// dispatch with its own gap): ranges of u32 words set to a value, and the 16-word counter block
+// zeroed with [5] (first failing index) and [13] (the gate's first gap) = UINT32_MAX.
+static constexpr int kMaxFill = 8;
+struct FillRange {
+  uint32_t* p;
+  uint64_t words;
+  uint32_t value;
+};
+struct FillArgs {
+  FillRange r[kMaxFill];
+  int n;
+  uint32_t* counters;  // or null
+};
+hipError_t launch_fill(hipStream_t s, const FillArgs& a);
+
 // file-level open: outer version check (when outer), envelope parse, key schedule.
 hipError_t launch_open_setup(hipStream_t s, const uint8_t* blob, const uint64_t* offs,
                              uint32_t n, bool outer, DevKey key, int32_t key_status,

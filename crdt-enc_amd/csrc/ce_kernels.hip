@@ -1177,6 +1177,26 @@ hipError_t launch_open_setup(hipStream_t s, const uint8_t* blob, const uint64_t*
   return hipGetLastError();
 }
 
+__global__ void k_fill(FillArgs a) {
+  const uint32_t r = blockIdx.y;
+  if ((int)r == a.n) {  // the counter block
+    if (blockIdx.x == 0 && threadIdx.x < 16)
+      a.counters[threadIdx.x] = (threadIdx.x == 5 || threadIdx.x == 13) ? 0xffffffffu : 0u;
+    return;
+  }
+  const FillRange f = a.r[r];
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < f.words; i += (uint64_t)gridDim.x * blockDim.x)
+    f.p[i] = f.value;
+}
+
+hipError_t launch_fill(hipStream_t s, const FillArgs& a) {
+  uint64_t mx = 16;
+  for (int i = 0; i < a.n; i++) mx = a.r[i].words > mx ? a.r[i].words : mx;
+  const uint32_t gx = (uint32_t)std::min<uint64_t>((mx + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_fill, dim3(gx, a.n + (a.counters ? 1 : 0)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_seal_setup(hipStream_t s, const uint8_t* clear, const uint64_t* offs, uint32_t n,
                              const uint8_t* outer_version, const uint8_t* nonces, uint8_t* out,
                              const uint64_t* out_offs, DevKey key, FileParams* params,

@@ -73,6 +73,9 @@ const char *ce_ctx_last_error(ce_ctx *ctx);
  * count of one kernel ("open_setup", "segments_open", "finalize_open", "decode", "merge",
  * "seal_setup", "segments_seal", "finalize_seal"). */
 int ce_ctx_set_timing(ce_ctx *ctx, int enable);
+/* Restrict the timing to one kernel name (NULL = every launch): each timed launch adds two
+ * event markers to the stream, so a timed step measures only the kernel it reports. */
+int ce_ctx_set_timing_only(ce_ctx *ctx, const char *kernel);
 int ce_ctx_timing_read(ce_ctx *ctx, const char *kernel, double *total_ms, uint64_t *launches);
 void ce_ctx_timing_reset(ce_ctx *ctx);
 

@@ -383,3 +383,38 @@ def test_orswot_device_compaction_bytes(ctx):
         assert st == 0 and pt == pre + oc.serialize()
         assert core.path_count("compact_device_writer") == 1
         core.close()
+
+
+def test_c3_shaped_medium(ctx):
+    """C3's shape at a size the Python oracle folds in a few seconds: 256 actors, 10k members,
+    four state files (each a quarter of the actors' first two versions) decoded on the device,
+    then two more versions of op files from every actor (12 ops each, single-member Adds and
+    Rms whose clocks span the actors), then the compaction through the device writer.  State
+    bytes == oracle at every stage."""
+    rng = random.Random(3)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 256)
+    files = G.well_formed_orswot(rng, actors, 4, 12, 10000, max_members=1)[0]
+    sws = []
+    for q in range(4):
+        part = C.Core("orswot")
+        sub = {a: files[a][:2] for a in actors[q * 64:(q + 1) * 64]}
+        acts, clears, fa, fv = G.batch(sub, "orswot", APP)
+        f = seal_files(ctx, key, clears)
+        assert part.read_remote_ops(key, [APP], f, [acts[i] for i in fa], fv)[0] == 0
+        sws.append(part.serialize())
+    core = crdtenc.Core(ctx, kind=crdtenc.STATE_ORSWOT, supported=[APP], current_data_version=APP)
+    core.set_latest_key(key)
+    oc = C.Core("orswot")
+    sf = seal_states(ctx, key, sws)
+    rc, st = core.ingest_states(sf)
+    assert (rc, st) == oc.read_remote_states(key, [APP], sf) == (0, [0] * 4)
+    assert core.state_bytes() == oc.serialize()
+    assert core.path_count("states_device_read") == 4
+    acts, clears, fa, fv = G.batch(files, "orswot", APP, start={a: 2 for a in actors})
+    assert check_ops(ctx, "orswot", key, core, oc, acts, clears, fa, fv) == 0
+    f, _ = core.compact_to_buffer(nonce=bytes(24))
+    st, pt = ctx.decrypt(key, f[16:])
+    assert st == 0 and pt == oc.serialize()
+    assert core.path_count("compact_device_writer") == 1
+    core.close()
