@@ -48,7 +48,7 @@ EXPORTS = [
     "ce_ctx_timing_reset", "ce_ctx_set_timing_only", "ce_core_reset", "ce_core_merge_state", "ce_core_dense_ready",
     "ce_keys_decode", "ce_keys_from_remote_metas", "ce_keys_merge", "ce_keys_free",
     "ce_keys_count", "ce_keys_latest", "ce_keys_get", "ce_keys_at", "ce_core_set_keys",
-    "ce_core_apply_ops_batch", "ce_core_ingest_ops_iov", "ce_core_compact_ops_iov",
+    "ce_core_apply_ops_batch", "ce_core_ingest_ops_iov", "ce_core_ingest_states_iov", "ce_core_compact_ops_iov",
     "ce_core_path_count",
 ]
 
@@ -566,6 +566,16 @@ class Core:
         offs[n] = o
         st = (ctypes.c_int32 * max(n, 1))()
         rc = lib().ce_core_ingest_states(self.p, _cbuf(blob), offs, ctypes.c_uint32(n), st)
+        return rc, list(st)[:n]
+
+    def ingest_states_iov(self, files):
+        """ingest_states over per-file host buffers (no concatenation, no copy)."""
+        n = len(files)
+        bufs = [_ptr(f)[0] for f in files]
+        ptrs = (ctypes.c_void_p * max(n, 1))(*[ctypes.cast(b, ctypes.c_void_p) for b in bufs])
+        lens = (ctypes.c_size_t * max(n, 1))(*[len(f) for f in files])
+        st = (ctypes.c_int32 * max(n, 1))()
+        rc = lib().ce_core_ingest_states_iov(self.p, ptrs, lens, ctypes.c_uint32(n), st)
         return rc, list(st)[:n]
 
     def read_remote(self):

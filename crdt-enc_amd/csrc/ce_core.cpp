@@ -1019,8 +1019,10 @@ int ingest_ops_hostmeta(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
 }
 
 // Core::read_remote_states after Storage::load_states (lib.rs:425-466)
+// files (optional): per-file host buffers instead of one blob (ce_core_ingest_states_iov),
+// uploaded through the pinned staging ring
 int ingest_states_host(ce_core* c, const uint8_t* blob, const uint64_t* offs, uint32_t n,
-                       int32_t* status_out) {
+                       int32_t* status_out, const uint8_t* const* files = nullptr) {
   ce_ctx* ctx = c->ctx;
   if (!c->has_key) return ctx->fail(CE_ERR_NO_KEY, "no latest key");
   if (n == 0) return CE_OK;
@@ -1029,9 +1031,13 @@ int ingest_states_host(ce_core* c, const uint8_t* blob, const uint64_t* offs, ui
   if ((e = ctx->blob.reserve(blen + 64)) || (e = ctx->offs.reserve((n + 1) * 8ull)) ||
       (e = ctx->out.reserve(blen + 16ull * n + 128)) || (e = ctx->status.reserve(n * 4ull + 64)))
     return ctx->hip_fail(e, "states reserve");
-  if ((e = hipMemcpyAsync(ctx->blob.p, blob, blen, hipMemcpyHostToDevice, ctx->stream)) ||
-      (e = hipMemcpyAsync(ctx->offs.p, offs, (n + 1) * 8ull, hipMemcpyHostToDevice, ctx->stream)))
+  if (files) {
+    int rc = stage_host_batch(ctx, files, offs, n);
+    if (rc) return rc;
+  } else if ((e = hipMemcpyAsync(ctx->blob.p, blob, blen, hipMemcpyHostToDevice, ctx->stream)) ||
+             (e = hipMemcpyAsync(ctx->offs.p, offs, (n + 1) * 8ull, hipMemcpyHostToDevice, ctx->stream))) {
     return ctx->hip_fail(e, "states upload");
+  }
   HostPhase hp("states: open + download");
   int rc = device_open(ctx, ctx->blob.as<uint8_t>(), ctx->offs.as<uint64_t>(), n, blen, true,
                        key_of(c), ctx->out.as<uint8_t>(), ctx->status.as<int32_t>(), false);
@@ -1545,6 +1551,17 @@ int ce_core_ingest_states(ce_core* c, const uint8_t* blob, const uint64_t* offs,
   std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
   (void)hipSetDevice(c->ctx->device);
   return ingest_states_host(c, blob, offs, n, status);
+}
+
+int ce_core_ingest_states_iov(ce_core* c, const uint8_t* const* files, const size_t* lens, uint32_t n,
+                              int32_t* status) {
+  if (!c || (n && (!files || !lens))) return CE_ERR_INVALID_ARG;
+  HostPhase hp("ingest_states (all)");
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  (void)hipSetDevice(c->ctx->device);
+  std::vector<uint64_t> offs(n + 1, 0);
+  for (uint32_t i = 0; i < n; i++) offs[i + 1] = offs[i] + lens[i];
+  return ingest_states_host(c, nullptr, offs.data(), n, status, files);
 }
 
 int ce_core_read_remote(ce_core* c) {

@@ -89,8 +89,8 @@ hipError_t launch_ds_applied(hipStream_t s, const uint32_t* keys_sorted, const u
                              const unsigned long long* excl_max, const unsigned long long* clock,
                              uint8_t* applied, uint32_t n);
 // clock[a] = max(clock[a], counter) for every add
-hipError_t launch_ds_clock(hipStream_t s, const uint32_t* add_actor, const unsigned long long* add_ctr,
-                           unsigned long long* clock, uint32_t n_add);
+hipError_t launch_ds_clock(hipStream_t s, const uint32_t* keys_sorted, const unsigned long long* ctr_sorted,
+                           const unsigned long long* excl_max, unsigned long long* clock, uint32_t n_add);
 // insert (member, actor) of every applied add, add[pair] = max counter
 hipError_t launch_ds_add_pairs(hipStream_t s, DsTables t, DsOps o, const uint8_t* applied,
                                uint32_t n_add);

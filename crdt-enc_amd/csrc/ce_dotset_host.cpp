@@ -507,7 +507,8 @@ int orswot_fold(ce_core* c, const Counts& k) {
   if ((rc = ensure_pairs(c, k.v[kCntAddM]))) return rc;
   const int tp = ctx->tbegin("ds_add_pairs");
   if ((e = launch_ds_add_pairs(s, tables(d), o, d->applied.as<uint8_t>(), na)) ||
-      (e = launch_ds_clock(s, o.add_actor, o.add_ctr, d->clock.as<unsigned long long>(), na)))
+      (e = launch_ds_clock(s, d->sort_keys2.as<uint32_t>(), d->ctr_sorted.as<unsigned long long>(),
+                           d->excl.as<unsigned long long>(), d->clock.as<unsigned long long>(), na)))
     return ctx->hip_fail(e, "add");
   ctx->tend(tp);
   // 3) removal thresholds: the batch's removals and the deferred set
@@ -1368,11 +1369,15 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     // clocks -> actor ids: read-only lookups on the host threads; a file naming an actor
     // outside the table inserts it below, in file order (the order the ids are handed out in)
     std::vector<uint8_t> need_insert(n, 0);
-    host_parallel_for(ctx, (uint32_t)dev.size(), [&](uint32_t k) {
-      if (!id_dots_lookup(c, ds[dev[k]].hs.clock, &ds[dev[k]].oclock)) need_insert[dev[k]] = 1;
-    });
-    for (size_t i : dev)
-      if (need_insert[i] && (rc = id_dots(c, ds[i].hs.clock, &ds[i].oclock))) return rc;
+    {
+      HostPhase h1("   rd.a lookups");
+      host_parallel_for(ctx, (uint32_t)dev.size(), [&](uint32_t k) {
+        if (!id_dots_lookup(c, ds[dev[k]].hs.clock, &ds[dev[k]].oclock)) need_insert[dev[k]] = 1;
+      });
+      for (size_t i : dev)
+        if (need_insert[i] && (rc = id_dots(c, ds[i].hs.clock, &ds[i].oclock))) return rc;
+    }
+    auto h2 = std::make_unique<HostPhase>("   rd.b reserve");
     size_t tmp_need = 0;
     for (size_t i : dev) {
       DevState& x = ds[i];
@@ -1387,11 +1392,14 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     }
     if ((rc = table_upload(c)) || (rc = ensure_clock(c))) return rc;
     if ((e = d->rd_tmp.reserve(tmp_need))) return ctx->hip_fail(e, "state reader");
+    h2 = std::make_unique<HostPhase>("   rd.c launch");
     for (size_t i : dev)
       if ((e = launch_orswot_read(s, read_args(c, d, i, ds[i], out, ds[i].cap), d->rd_tmp.p, d->rd_tmp.cap, 0)))
         return ctx->hip_fail(e, "state reader");
+    h2 = std::make_unique<HostPhase>("   rd.d sync");
     if (!dev.empty() && ((e = hipMemcpyAsync(small, d->rd_misc.p, 8ull * n, hipMemcpyDeviceToHost, s)) ||
                          (rc = sync("state reader")))) return rc ? rc : ctx->hip_fail(e, "state reader");
+    h2.reset();
     // 3) the first N heads in position order are the entries: parse, chain, repeats, scan
     ph = std::make_unique<HostPhase>("  rd: entries");
     std::vector<size_t> dev2;

@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 
 #include <hipcub/hipcub.hpp>
+#include <map>
+#include <mutex>
 
 #include "ce_device.h"
 #include "ce_dotset.h"
@@ -132,17 +134,27 @@ __global__ void k_ser_write(OrswotSerArgs a) {
   }
 }
 
-// one block: the prefix and the entries map header, the suffix after the entries, the clear
-// length into the seal's offsets (offs[0] = 0, offs[1] = clear length, out_offs[0] = 0)
+// the prefix and the entries map header, the suffix after the entries, the clear length into
+// the seal's offsets (offs[0] = 0, offs[1] = clear length, out_offs[0] = 0)
 __global__ void k_ser_tail(OrswotSerArgs a) {
   const uint32_t nm = a.n ? a.hrank[a.n - 1] + a.head[a.n - 1] : 0u;
   const uint64_t body = a.n ? (uint64_t)a.pos[a.n - 1] + a.len[a.n - 1] : 0ull;
   const uint64_t hl = maplen(nm);
-  for (uint64_t j = threadIdx.x; j < a.prefix_len; j += blockDim.x) a.out[j] = a.prefix[j];
-  if (threadIdx.x == 0) put_map(a.out + a.prefix_len, nm);
+  const uint64_t gt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, gs = (uint64_t)gridDim.x * blockDim.x;
+  // the prefix (next_op_versions and the clock: ~200 KB at 4096 actors) in 16-byte pieces when
+  // both ends allow it -- one block copying bytes took ~0.2 ms
+  if (((reinterpret_cast<uintptr_t>(a.out) | reinterpret_cast<uintptr_t>(a.prefix)) & 15) == 0) {
+    const uint64_t n16 = a.prefix_len / 16;
+    for (uint64_t j = gt; j < n16; j += gs)
+      reinterpret_cast<uint4*>(a.out)[j] = reinterpret_cast<const uint4*>(a.prefix)[j];
+    for (uint64_t j = 16 * n16 + gt; j < a.prefix_len; j += gs) a.out[j] = a.prefix[j];
+  } else {
+    for (uint64_t j = gt; j < a.prefix_len; j += gs) a.out[j] = a.prefix[j];
+  }
   const uint64_t s0 = a.prefix_len + hl + body;
-  for (uint64_t j = threadIdx.x; j < a.suffix_len; j += blockDim.x) a.out[s0 + j] = a.suffix[j];
-  if (threadIdx.x == 0) {
+  for (uint64_t j = gt; j < a.suffix_len; j += gs) a.out[s0 + j] = a.suffix[j];
+  if (gt == 0) put_map(a.out + a.prefix_len, nm);
+  if (gt == 0) {
     a.seal_offs[0] = 0;
     a.seal_offs[1] = s0 + a.suffix_len;
     a.seal_offs[2] = 0;  // out_offs[0]
@@ -173,17 +185,48 @@ __device__ __forceinline__ uint32_t rd_uint(const uint8_t* p, const uint8_t* end
   return 1 + k;
 }
 
-// candidate entry heads: 81 a4 'd' 'o' 't' 's' at p, followed by a map header
-__global__ void k_rd_find(const uint8_t* s, uint64_t lo, uint64_t hi, uint32_t* cand, uint32_t* n_cand,
-                          uint32_t cap) {
-  for (uint64_t p = lo + (uint64_t)blockIdx.x * kB + threadIdx.x; p + 7 <= hi; p += (uint64_t)gridDim.x * kB) {
-    if (s[p] != 0x81 || s[p + 1] != 0xa4 || s[p + 2] != 'd' || s[p + 3] != 'o' || s[p + 4] != 't' ||
-        s[p + 5] != 's')
-      continue;
-    const uint8_t m = s[p + 6];
-    if ((m & 0xf0) != 0x80 && m != 0xde && m != 0xdf) continue;
-    const uint32_t k = atomicAdd(n_cand, 1u);
-    if (k < cap) cand[k] = (uint32_t)(p - lo);
+// candidate entry heads: 81 a4 'd' 'o' 't' 's' at p, followed by a map header.  A block takes
+// kFindChunk consecutive positions and collects its heads in LDS; one global atomicAdd per block
+// reserves their slice of the list (one head every ~50 bytes: per-wave or per-lane atomics on
+// the one counter serialised in L2 at ~10 ns each, 217 us per C3 state file)
+static constexpr uint32_t kFindPer = 16, kFindChunk = kFindPer * kB, kFindLds = 1024;
+__device__ __forceinline__ bool entry_head_at(const uint8_t* s, uint64_t p) {
+  if (s[p] != 0x81 || s[p + 1] != 0xa4 || s[p + 2] != 'd' || s[p + 3] != 'o' || s[p + 4] != 't' ||
+      s[p + 5] != 's')
+    return false;
+  const uint8_t m = s[p + 6];
+  return (m & 0xf0) == 0x80 || m == 0xde || m == 0xdf;
+}
+
+__global__ void __launch_bounds__(kB) k_rd_find(const uint8_t* s, uint64_t lo, uint64_t hi, uint32_t* cand,
+                                                uint32_t* n_cand, uint32_t cap) {
+  __shared__ uint32_t lcount, lbase;
+  __shared__ uint32_t lst[kFindLds];
+  for (uint64_t c0 = lo + (uint64_t)blockIdx.x * kFindChunk; c0 < hi; c0 += (uint64_t)gridDim.x * kFindChunk) {
+    if (threadIdx.x == 0) lcount = 0;
+    __syncthreads();
+#pragma unroll 4
+    for (uint32_t k = 0; k < kFindPer; k++) {
+      const uint64_t p = c0 + k * kB + threadIdx.x;
+      if (p + 7 <= hi && entry_head_at(s, p)) {
+        const uint32_t i = atomicAdd(&lcount, 1u);
+        if (i < kFindLds) {
+          lst[i] = (uint32_t)(p - lo);
+        } else {  // more heads than the LDS list holds (adversarial bytes): one by one
+          const uint32_t g = atomicAdd(n_cand, 1u);
+          if (g < cap) cand[g] = (uint32_t)(p - lo);
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t m = lcount < kFindLds ? lcount : kFindLds;
+    if (threadIdx.x == 0 && m) lbase = atomicAdd(n_cand, m);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < m; i += kB) {
+      const uint32_t g = lbase + i;
+      if (g < cap) cand[g] = lst[i];
+    }
+    __syncthreads();
   }
 }
 
@@ -315,11 +358,23 @@ hipError_t launch_orswot_ser(hipStream_t s, OrswotSerScratch& sc, const OrswotSe
     a.len = sc.len;
     hipLaunchKernelGGL(k_ser_write, dim3(nblk(n)), dim3(kB), 0, s, a);
   }
-  hipLaunchKernelGGL(k_ser_tail, dim3(1), dim3(kB), 0, s, a);
+  hipLaunchKernelGGL(k_ser_tail, dim3(64), dim3(kB), 0, s, a);
   return hipGetLastError();
 }
 
-size_t orswot_ser_tmp_bytes(uint32_t n) {
+static size_t cached_tmp_bytes(uint32_t n, size_t (*raw)(uint32_t), std::map<uint32_t, size_t>& cache) {
+  static std::mutex mu;
+  uint32_t p = 1;
+  while (p < n && p < 0x80000000u) p <<= 1;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(p);
+  if (it != cache.end()) return it->second;
+  const size_t v = raw(p);
+  cache[p] = v;
+  return v;
+}
+
+static size_t ser_tmp_bytes_raw(uint32_t n) {
   size_t a = 0, b = 0, c = 0;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                            (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 32);
@@ -330,10 +385,16 @@ size_t orswot_ser_tmp_bytes(uint32_t n) {
   return std::max(a, std::max(b, c)) + 256;
 }
 
+size_t orswot_ser_tmp_bytes(uint32_t n) {
+  static std::map<uint32_t, size_t> cache;
+  return cached_tmp_bytes(n, ser_tmp_bytes_raw, cache);
+}
+
 hipError_t launch_orswot_read(hipStream_t s, OrswotReadArgs a, void* tmp, size_t tmp_bytes, int stage) {
   hipError_t e;
   if (stage == 0) {  // candidates, then sorted by position
-    hipLaunchKernelGGL(k_rd_find, dim3(nblk(a.hi - a.lo)), dim3(kB), 0, s, a.s, a.lo, a.hi, a.cand_raw,
+    hipLaunchKernelGGL(k_rd_find, dim3(nblk((a.hi - a.lo + kFindPer - 1) / kFindPer)), dim3(kB), 0, s, a.s, a.lo,
+                       a.hi, a.cand_raw,
                        a.n_cand_dev, a.cap);
     return hipGetLastError();
   }
@@ -358,13 +419,21 @@ hipError_t hipcub_sort_u32(void* tmp, size_t& tb, const uint32_t* kin, uint32_t*
   return hipcub::DeviceRadixSort::SortKeys(tmp, tb, kin, kout, (int)n, 0, 32, s);
 }
 
-size_t orswot_read_tmp_bytes(uint32_t n) {
+// hipCUB's temp-storage queries cost tens of microseconds each on the host; the sizes only
+// grow with n, so they are taken once per power of two and cached
+static size_t read_tmp_bytes_raw(uint32_t n) {
   size_t a = 0, b = 0, c = 0;
   (void)hipcub::DeviceRadixSort::SortKeys(nullptr, a, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 32);
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
   (void)hipcub::DeviceRadixSort::SortKeys(nullptr, c, (unsigned long long*)nullptr,
                                           (unsigned long long*)nullptr, (int)n, 0, 64);
   return std::max(a, std::max(b, c)) + 256;
+}
+
+
+size_t orswot_read_tmp_bytes(uint32_t n) {
+  static std::map<uint32_t, size_t> cache;
+  return cached_tmp_bytes(n, read_tmp_bytes_raw, cache);
 }
 
 }  // namespace ce

@@ -265,6 +265,11 @@ int ce_core_ingest_ops_iov(ce_core *c, const uint8_t *const *files, const size_t
 /* What read_remote_states does after Storage::load_states (lib.rs:425-466). */
 int ce_core_ingest_states(ce_core *c, const uint8_t *blob, const uint64_t *offs, uint32_t n,
                           int32_t *status);
+/* ce_core_ingest_states over per-file host buffers (what Storage::load_states returns as
+ * Vec<u8>s, crdt-enc/src/lib.rs:425-431): files[i] holds lens[i] bytes, uploaded through the
+ * pinned staging ring (no concatenated copy). */
+int ce_core_ingest_states_iov(ce_core *c, const uint8_t *const *files, const size_t *lens, uint32_t n,
+                              int32_t *status);
 /* Core::compact (crdt-enc/src/lib.rs:332-380) over a batch resident in HBM: read_remote_ops over
  * the op files exactly as ce_core_ingest_ops_device, then the compaction output as
  * ce_core_compact_to_buffer.  For VClock/GCounter the compaction is queued on the device behind

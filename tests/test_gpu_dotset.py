@@ -418,3 +418,32 @@ def test_c3_shaped_medium(ctx):
     assert st == 0 and pt == oc.serialize()
     assert core.path_count("compact_device_writer") == 1
     core.close()
+
+
+def test_ingest_states_iov_matches_blob(ctx):
+    """ce_core_ingest_states_iov (per-file host buffers through the pinned staging ring) ==
+    ce_core_ingest_states (one blob): statuses and state bytes, a tampered file included."""
+    rng = random.Random(11)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 6)
+    sws = []
+    for _ in range(3):
+        part = C.Core("orswot")
+        files = gen("orswot", rng, actors, 2, 6, 50, False)
+        acts, clears, fa, fv = G.batch(files, "orswot", APP)
+        f = seal_files(ctx, key, clears)
+        assert part.read_remote_ops(key, [APP], f, [acts[i] for i in fa], fv)[0] == 0
+        sws.append(part.serialize())
+    sf = seal_states(ctx, key, sws)
+    a, b = new_core(ctx, "orswot", key), new_core(ctx, "orswot", key)
+    assert a.ingest_states(sf) == b.ingest_states_iov(sf) == (0, [0, 0, 0])
+    assert a.state_bytes() == b.state_bytes()
+    bad = list(sf)
+    t = bytearray(bad[1])
+    t[-3] ^= 1
+    bad[1] = bytes(t)
+    ra, rb = a.ingest_states(bad), b.ingest_states_iov(bad)
+    assert ra == rb and ra[0] == 9
+    assert a.state_bytes() == b.state_bytes()
+    a.close()
+    b.close()
