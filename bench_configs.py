@@ -223,12 +223,12 @@ def run_c3(args, ctx, dev):
     # the SHA3-256 content name of step i's state file is computed on a host thread while step
     # i+1 runs (as in bench.py); every name is done before the timed region ends
     from concurrent.futures import ThreadPoolExecutor
-    # SHA3-256 is a sequential sponge (~200 MB/s per core): one 8 MB name takes about as long
-    # as the rest of a step, so two host threads hash consecutive steps' files side by side
-    NB = 6
+    # SHA3-256 is a sequential sponge (~0.7 GB/s per core): one 35 MB name takes ~48 ms, about
+    # four steps, so NB - 1 = 12 host threads hash consecutive steps' files side by side
+    NB = 13
     namer = ThreadPoolExecutor(NB - 1)
     names = []
-    obuf = [np.zeros(1 << 25, np.uint8) for _ in range(NB)]  # committed pages, room for the file
+    obuf = [torch.zeros(1 << 26, dtype=torch.uint8, pin_memory=True).numpy() for _ in range(NB)]  # pinned (the 35 MB download is a DMA, not a staged copy), room for the file
 
     def step():
         t = time.perf_counter()
@@ -595,7 +595,8 @@ def main():
     ap.add_argument("--c5-versions", type=int, default=256, help="C5 versions per actor (4096 actors)")
     ap.add_argument("--c5-clean", action="store_true",
                     help="C5 control: every file under the latest key, none tampered (accept path)")
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default 20; 40 for c3, whose last names are hashed after its last step)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--c3-cpu-actors", type=int, default=16, help="C3 CPU sample: op files of this many actors")
     ap.add_argument("--c4-cpu-actors", type=int, default=256, help="C4 CPU sample: files of this many actors")
@@ -604,6 +605,8 @@ def main():
     ap.add_argument("--versions", type=int, default=16, help="op-file versions per actor")
     ap.add_argument("--state-versions", type=int, default=4, help="versions folded into states")
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = 40 if args.config == "c3" else 20
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     stream = torch.cuda.Stream(device=dev)
