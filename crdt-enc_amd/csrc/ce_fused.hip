@@ -379,6 +379,10 @@ __device__ __forceinline__ void decode_fold(const DecodeArgs& a, const SupVers& 
     const uint32_t mx = grp_reduce<LPF>(hi, [](uint32_t x, uint32_t y) { return x > y ? x : y; });
     const uint32_t mn = grp_reduce<LPF>(lo, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
     const unsigned long long b = grp_max64<LPF>(pslot == 0xffffffffu ? 0ull : pbest);
+#if CE_FUSED_DIAG
+    if (a.ablate & 16) {  // diagnostics: no fold atomics (results invalid)
+    } else
+#endif
     if (mx != 0 && mn == mx) {
       if (sub == 0) batch_max(&a.batch[mx - 1], b);
     } else if (pslot != 0xffffffffu) {

@@ -867,6 +867,10 @@ __global__ __launch_bounds__(256) void k_segdec_apply(DecodeArgs a, SegScratch s
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t nm = *((volatile uint32_t*)&sc.counters[1]);
   const uint32_t stride = gridDim.x * kWavesPerBlock;
+  // files folded from records, counted per wave and added once per block (one global atomic
+  // per file on one word serialised in L2: ~0.18 ms at C4's 16K files)
+  __shared__ uint32_t folded[kWavesPerBlock];
+  uint32_t n_folded = 0;
   for (uint32_t t = bcast(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)); t < nm; t += stride) {
     const uint32_t f = bcast(sc.multi_files[t]);
     const FileParams* Pp = a.params + f;
@@ -933,7 +937,7 @@ __global__ __launch_bounds__(256) void k_segdec_apply(DecodeArgs a, SegScratch s
       }
       continue;
     }
-    if (lane == 0) atomicAdd(&a.counters[11], 1u);
+    n_folded++;
     uint32_t mx = myslot == 0xffffffffu ? 0u : myslot + 1;
     uint32_t mn = myslot == 0xffffffffu ? 0xffffffffu : myslot + 1;
     unsigned long long bm = myslot == 0xffffffffu ? 0ull : best;
@@ -950,6 +954,13 @@ __global__ __launch_bounds__(256) void k_segdec_apply(DecodeArgs a, SegScratch s
     } else if (myslot != 0xffffffffu) {
       batch_max(&a.batch[myslot], best);
     }
+  }
+  if (lane == 0) folded[threadIdx.x >> 6] = n_folded;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0;
+    for (int w = 0; w < kWavesPerBlock; w++) tot += folded[w];
+    if (tot) atomicAdd(&a.counters[11], tot);
   }
 }
 
