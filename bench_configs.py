@@ -171,24 +171,33 @@ def gcounter_cpu_baseline(key, host_blob, h_offs, h_act, h_ver, check, what):
             "modes": {k: dict(v, unit="files/s") for k, v in res.items()}}
 
 
-def orswot_cpu_baseline(key, state_files, op_files, actors, versions, gpu_state, what):
-    """The Python restatement (oracle/crdts.py Core) over a small sample: 1 core, a 'port'
-    figure for scale only (the restatement is pure Python: no best-CPU Orswot exists here)."""
+def orswot_cpu_baseline(key, state_files, blob, offs, file_actor, file_version, gpu_state, what):
+    """oracle/ce_oracle.c oc_compact_orswot_best (the C restatement of oracle/crdts.py) on this
+    host: every file opened + decoded on T threads, the state merges and the op fold in file
+    order on one thread (order-dependent: removals defer), then the canonical StateWrapper
+    serialized, sealed and named as Core::compact does.  Two thread counts: the host's CPU
+    share ('best') and 16 ('reference_shaped': load_ops' buffered(16), lib.rs:497-514)."""
     sys.path.insert(0, REPO)
     import bench
-    from oracle import crdts as C
-    model, avail, _ = bench.host_cpu()
-    t = time.perf_counter()
-    oc = C.Core("orswot")
-    rs = oc.read_remote_states(key, [APP, CORE], state_files)[0]
-    ro = oc.read_remote_ops(key, [APP, CORE], op_files, actors, versions)[0]
-    ser = oc.serialize()
-    dt = time.perf_counter() - t
-    nf = len(state_files) + len(op_files)
-    return {"value": round(nf / dt, 1), "unit": "files/s", "cores": 1, "kind": "port",
-            "sample": "%s; oracle/crdts.py (pure-Python restatement, one thread)" % what,
-            "seconds": round(dt, 3), "same_result_as_gpu": rs == 0 and ro == 0 and ser == gpu_state,
-            "host_cpu": model, "nproc": avail}
+    import oracle
+    model, avail, threads = bench.host_cpu()
+    nf = len(state_files) + len(offs) - 1
+    res = {}
+    for mode, th in (("best", threads), ("reference_shaped", min(16, threads))):
+        err, ser, dt, ph = oracle.compact_orswot_best(key, APP, state_files, blob, offs, file_actor,
+                                                      file_version, th, seal=True)
+        res[mode] = {"value": round(nf / dt, 1), "cores": th, "seconds": round(dt, 3),
+                     "phases_s": {k: round(v, 4) for k, v in
+                                  zip(("open_decode", "state_merges", "op_fold", "serialize_seal"), ph)},
+                     "same_result_as_gpu": err == 0 and ser == gpu_state}
+    top = max(res, key=lambda k: res[k]["value"])
+    t = res[top]
+    return {"value": t["value"], "unit": "files/s", "cores": t["cores"], "kind": "port",
+            "sample": "%s; oracle/ce_oracle.c oc_compact_orswot_best, %s mode (open + decode on %d "
+                      "threads, merges + fold on one)" % (what, top, t["cores"]),
+            "seconds": t["seconds"], "same_result_as_gpu": all(v["same_result_as_gpu"] for v in res.values()),
+            "host_cpu": model, "nproc": avail,
+            "modes": {k: dict(v, unit="files/s") for k, v in res.items()}}
 
 
 def run_c3(args, ctx, dev):
@@ -312,25 +321,17 @@ def run_c3(args, ctx, dev):
     for p in parts:
         p.close()
 
-    # CPU baseline sample: state file 0 + the op files of the first A actors, GPU vs oracle
+    # CPU baseline: the whole step's workload (every state and op file), state bytes vs the GPU's
     cpu = None
     if not args.no_cpu:
-        A = args.c3_cpu_actors
-        flen = blob_len // n
-        p = new_core(ctx, key)
-        assert p.ingest_states([states[0]])[0] == 0
-        rc = p.ingest_ops_device(files.data_ptr(), offs.data_ptr(), A * V, A * V * flen,
-                                 b"".join(bytes(a) for a in actors[:A]),
-                                 fa[: A * V].contiguous().data_ptr(), fv[: A * V].contiguous().data_ptr())
-        gpu_sample = p.state_bytes() if rc == 0 else None
-        p.close()
-        hb = files[: A * V * flen].cpu().numpy().tobytes()
-        op_files = [hb[i * flen:(i + 1) * flen] for i in range(A * V)]
-        cpu = orswot_cpu_baseline(key, [states[0]], op_files,
-                                  [bytes(actors[i // V]) for i in range(A * V)],
-                                  [V0 + i % V for i in range(A * V)], gpu_sample,
-                                  "1 state file + %d op files (%d actors x %d versions) of this workload"
-                                  % (A * V, A, V))
+        hb = files[:blob_len].cpu().numpy()
+        ho = offs.cpu().numpy().astype(np.uint64)
+        ha = actors[fa.cpu().numpy()]
+        hv = fv.cpu().numpy().astype(np.uint64)
+        cpu = orswot_cpu_baseline(key, states, hb, ho, ha, hv, sb,
+                                  "the whole step: %d state files + %d op files, sealed + named"
+                                  % (len(states), n))
+        del hb
 
     k_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in kern.items() if v[1]}
     n_state = len(states)
@@ -598,7 +599,6 @@ def main():
     ap.add_argument("--steps", type=int, default=None,
                     help="timed steps (default 20; 40 for c3, whose last names are hashed after its last step)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--c3-cpu-actors", type=int, default=16, help="C3 CPU sample: op files of this many actors")
     ap.add_argument("--c4-cpu-actors", type=int, default=256, help="C4 CPU sample: files of this many actors")
     ap.add_argument("--c5-cpu-actors", type=int, default=128, help="C5 CPU sample: actors per key")
     ap.add_argument("--warmup", type=int, default=1)

@@ -35,6 +35,10 @@ def lib():
         L.oc_open_batch_mt.restype = S
         L.oc_compact_ops_baseline.restype = S
         L.oc_compact_ops_best.restype = S
+        L.oc_compact_orswot_best.restype = S
+        L.oc_compact_orswot_best.argtypes = [P, P, P, P, S, P, P, P, P, S, ctypes.c_int,
+                                             ctypes.c_int, P, S, ctypes.POINTER(ctypes.c_int),
+                                             ctypes.POINTER(ctypes.c_double)]
         L.oc_vclock_get.restype = ctypes.c_uint64
         _lib = L
     return _lib
@@ -191,3 +195,43 @@ def compact_ops_baseline(kind, key, data_version, blob, offs, file_actor, file_v
     n = fn(kind, _buf(key), _buf(data_version), blob, offs, file_actor, file_version,
            ctypes.c_size_t(n_files), n_threads, out, ctypes.c_size_t(cap), ctypes.byref(err))
     return err.value, out.raw[:n]
+
+
+def _addr(x):
+    """address of a bytes-like / numpy buffer (kept alive by the caller)"""
+    if hasattr(x, "ctypes"):
+        return x.ctypes.data
+    return ctypes.cast(ctypes.c_char_p(x), ctypes.c_void_p).value
+
+
+def compact_orswot_best(key, data_version, state_files, blob, offs, file_actor, file_version,
+                        n_threads, seal=True, cap=1 << 27):
+    """Orswot CPU baseline (oc_compact_orswot_best).  state_files: list of bytes; blob: op files
+    back to back (bytes or uint8 numpy), offs: uint64 numpy [n+1], file_actor: uint8 numpy
+    [n, 16], file_version: uint64 numpy [n].  Returns (err, StateWrapper bytes, seconds of the
+    C call, phase seconds [open+decode, state merges, op fold, serialize+seal])."""
+    import time
+    import numpy as np
+    sblob = b"".join(state_files) or b"\0"
+    soffs = np.zeros(len(state_files) + 1, dtype=np.uint64)
+    for i, f in enumerate(state_files):
+        soffs[i + 1] = soffs[i] + len(f)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    fa = np.ascontiguousarray(file_actor, dtype=np.uint8).reshape(-1, 16)
+    fv = np.ascontiguousarray(file_version, dtype=np.uint64)
+    n = len(offs) - 1
+    assert fa.shape[0] >= n and fv.shape[0] >= n
+    kb, dv = _buf(key), _buf(data_version)
+    while True:
+        out = ctypes.create_string_buffer(cap)
+        err = ctypes.c_int(0)
+        ph = (ctypes.c_double * 4)()
+        t = time.perf_counter()
+        ln = lib().oc_compact_orswot_best(
+            ctypes.addressof(kb), ctypes.addressof(dv), _addr(sblob), soffs.ctypes.data,
+            len(state_files), _addr(blob), offs.ctypes.data, fa.ctypes.data, fv.ctypes.data, n,
+            n_threads, 1 if seal else 0, ctypes.addressof(out), cap, ctypes.byref(err), ph)
+        dt = time.perf_counter() - t
+        if ln <= cap:
+            return err.value, out.raw[:ln], dt, list(ph)
+        cap = ln

@@ -1102,3 +1102,819 @@ size_t oc_compact_ops_best(int kind, const uint8_t key[32], const uint8_t data_v
   *err = e;
   return n_out;
 }
+
+/* ------------------------------------------------------------------------------------ */
+/* Orswot<u64, Uuid> CPU baseline (C3): a C restatement of oracle/crdts.py's Orswot and  */
+/* Core (crdts 7 orswot.rs; crdt-enc/src/lib.rs:401-547)           */
+/* ------------------------------------------------------------------------------------ */
+/* Data layout: actors interned to dense ids (first-seen order); the Orswot's own clock and
+ * next_op_versions are dense arrays indexed by id (they never hold zero counters: every
+ * insertion goes through VClock::apply); an entry's or a removal's VClock is a small array
+ * sorted by id (it may hold explicit zero counters, as a decoded BTreeMap may); entries are an
+ * open-addressed member -> VClock table; deferred removals a list of (clock, members). */
+#include <time.h>
+
+static double oc_now(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+typedef struct { uint64_t *p; size_t n, cap; } u64v;
+static void u64v_push(u64v *v, uint64_t x) {
+  if (v->n == v->cap) {
+    v->cap = v->cap ? 2 * v->cap : 64;
+    v->p = (uint64_t *)realloc(v->p, v->cap * 8);
+  }
+  v->p[v->n++] = x;
+}
+static void u64v_free(u64v *v) { free(v->p); memset(v, 0, sizeof *v); }
+
+static int rd_map_hdr(rd_t *r, uint64_t *len) {
+  const uint8_t *q;
+  if (rd_take(r, 1, &q)) return -1;
+  uint8_t m = q[0];
+  if ((m & 0xf0) == 0x80) { *len = m & 0x0f; return 0; }
+  if (m == 0xde) return rd_be(r, 2, len);
+  if (m == 0xdf) return rd_be(r, 4, len);
+  return -1;
+}
+
+/* --- raw (uuid-keyed) decode, run on the worker threads ---------------------------------- */
+/* VClock {dots: BTreeMap<Uuid, u64>} (crdts.py dec_vclock): a later duplicate key overwrites an
+ * earlier one, zero counters kept.  Appends [n, (uuid lo, uuid hi, counter) x n]. */
+typedef struct { uint8_t a[16]; uint64_t c; uint32_t ord; } rawdot;
+static int rawdot_cmp(const void *x, const void *y) {
+  const rawdot *p = (const rawdot *)x, *q = (const rawdot *)y;
+  int c = memcmp(p->a, q->a, 16);
+  if (c) return c;
+  return p->ord < q->ord ? -1 : p->ord > q->ord;
+}
+typedef struct { u64v *out; rawdot *tmp; size_t tcap; } vcraw_ctx;
+static int vcraw_dots_cb(int f, rd_t *r, void *ctx) {
+  (void)f;
+  vcraw_ctx *x = (vcraw_ctx *)ctx;
+  uint64_t cnt;
+  if (rd_map_hdr(r, &cnt) || cnt > r->n - r->i) return -1;
+  if (cnt > x->tcap) {
+    x->tcap = cnt;
+    x->tmp = (rawdot *)realloc(x->tmp, cnt * sizeof(rawdot));
+  }
+  for (uint64_t k = 0; k < cnt; k++) {
+    if (rd_uuid(r, x->tmp[k].a) || rd_u64(r, &x->tmp[k].c)) return -1;
+    x->tmp[k].ord = (uint32_t)k;
+  }
+  size_t n = (size_t)cnt;
+  if (n > 1) {
+    qsort(x->tmp, n, sizeof(rawdot), rawdot_cmp);
+    size_t w = 0;
+    for (size_t k = 0; k < n; k++) {
+      if (k + 1 < n && memcmp(x->tmp[k].a, x->tmp[k + 1].a, 16) == 0) continue;  /* last wins */
+      x->tmp[w++] = x->tmp[k];
+    }
+    n = w;
+  }
+  u64v_push(x->out, n);
+  for (size_t k = 0; k < n; k++) {
+    uint64_t lo, hi;
+    memcpy(&lo, x->tmp[k].a, 8);
+    memcpy(&hi, x->tmp[k].a + 8, 8);
+    u64v_push(x->out, lo);
+    u64v_push(x->out, hi);
+    u64v_push(x->out, x->tmp[k].c);
+  }
+  return 0;
+}
+static int rd_vcraw(rd_t *r, vcraw_ctx *x, u64v *out) {
+  static const char *const F[1] = {"dots"};
+  x->out = out;
+  return rd_struct(r, F, 1, vcraw_dots_cb, x);
+}
+
+static int rd_members(rd_t *r, u64v *out) {  /* Vec<u64> (crdts.py _seq + _u64) */
+  uint64_t cnt, m;
+  if (rd_array_hdr(r, &cnt) || cnt > r->n - r->i) return -1;
+  u64v_push(out, cnt);
+  for (uint64_t k = 0; k < cnt; k++) {
+    if (rd_u64(r, &m)) return -1;
+    u64v_push(out, m);
+  }
+  return 0;
+}
+
+/* StateWrapper<Orswot> (crdts.py dec_state): four raw sections, each in wire order */
+typedef struct { u64v nov, clk, ent, def; } ow_raw;
+typedef struct { vcraw_ctx vc; ow_raw *s; } ow_rawctx;
+static int ow_set_cb(int f, rd_t *r, void *ctx) {
+  ow_rawctx *x = (ow_rawctx *)ctx;
+  uint64_t cnt, m;
+  if (f == 0) return rd_vcraw(r, &x->vc, &x->s->clk);
+  if (rd_map_hdr(r, &cnt) || cnt > r->n - r->i) return -1;
+  u64v *o = f == 1 ? &x->s->ent : &x->s->def;
+  u64v_push(o, cnt);
+  for (uint64_t k = 0; k < cnt; k++) {
+    if (f == 1) {          /* entries: member -> VClock */
+      if (rd_u64(r, &m)) return -1;
+      u64v_push(o, m);
+      if (rd_vcraw(r, &x->vc, o)) return -1;
+    } else {               /* deferred: VClock -> Vec<member> */
+      if (rd_vcraw(r, &x->vc, o) || rd_members(r, o)) return -1;
+    }
+  }
+  return 0;
+}
+static int ow_sw_cb(int f, rd_t *r, void *ctx) {
+  static const char *const F[3] = {"clock", "entries", "deferred"};
+  ow_rawctx *x = (ow_rawctx *)ctx;
+  if (f == 0) return rd_vcraw(r, &x->vc, &x->s->nov);
+  return rd_struct(r, F, 3, ow_set_cb, x);
+}
+static int ow_decode_state(const uint8_t *pt, size_t len, ow_rawctx *x) {
+  static const char *const F[2] = {"next_op_versions", "state"};
+  rd_t r = {pt, len, 0};
+  return rd_struct(&r, F, 2, ow_sw_cb, x);
+}
+
+/* Vec<orswot::Op<u64, Uuid>> (crdts.py dec_orswot_op): externally tagged {"Add": {dot, members}}
+ * | {"Rm": {clock, members}} -> [0, uuid lo, uuid hi, counter, nm, m..] | [1, <vc>, nm, m..] */
+typedef struct { vcraw_ctx vc; dot_t dot; u64v clk, mem; } ow_opctx;
+static int ow_add_cb(int f, rd_t *r, void *ctx) {
+  static const char *const DF[2] = {"actor", "counter"};
+  ow_opctx *x = (ow_opctx *)ctx;
+  if (f == 0) return rd_struct(r, DF, 2, dot_cb, &x->dot);
+  x->mem.n = 0;
+  return rd_members(r, &x->mem);
+}
+static int ow_rm_cb(int f, rd_t *r, void *ctx) {
+  ow_opctx *x = (ow_opctx *)ctx;
+  if (f == 0) { x->clk.n = 0; return rd_vcraw(r, &x->vc, &x->clk); }
+  x->mem.n = 0;
+  return rd_members(r, &x->mem);
+}
+static int ow_decode_ops(const uint8_t *pt, size_t len, ow_opctx *x, u64v *out) {
+  static const char *const V[2] = {"Add", "Rm"};
+  static const char *const AF[2] = {"dot", "members"};
+  static const char *const RF[2] = {"clock", "members"};
+  rd_t r = {pt, len, 0};
+  uint64_t cnt, one;
+  if (rd_array_hdr(&r, &cnt) || cnt > len) return -1;
+  for (uint64_t k = 0; k < cnt; k++) {
+    if (rd_map_hdr(&r, &one) || one != 1) return -1;
+    int v = rd_field(&r, V, 2);
+    if (v < 0 || v >= 2) return -1;
+    if (v == 0) {
+      if (rd_struct(&r, AF, 2, ow_add_cb, x)) return -1;
+      uint64_t lo, hi;
+      memcpy(&lo, x->dot.actor, 8);
+      memcpy(&hi, x->dot.actor + 8, 8);
+      u64v_push(out, 0); u64v_push(out, lo); u64v_push(out, hi); u64v_push(out, x->dot.counter);
+    } else {
+      if (rd_struct(&r, RF, 2, ow_rm_cb, x)) return -1;
+      u64v_push(out, 1);
+      for (size_t i = 0; i < x->clk.n; i++) u64v_push(out, x->clk.p[i]);
+    }
+    for (size_t i = 0; i < x->mem.n; i++) u64v_push(out, x->mem.p[i]);
+  }
+  return 0;
+}
+
+/* --- fold structures --------------------------------------------------------------------- */
+typedef struct {
+  uint8_t (*uuid)[16];
+  uint32_t n, cap;
+  uint32_t *tab;  /* id + 1, 0 = empty */
+  uint32_t mask;
+} ow_actors;
+static uint32_t uuid_hash(const uint8_t *u) {
+  uint64_t a, b;
+  memcpy(&a, u, 8);
+  memcpy(&b, u + 8, 8);
+  uint64_t h = (a ^ (b * 0x9E3779B97F4A7C15ULL)) * 0xBF58476D1CE4E5B9ULL;
+  return (uint32_t)(h >> 32);
+}
+static uint32_t ow_intern(ow_actors *t, uint64_t lo, uint64_t hi) {
+  uint8_t u[16];
+  memcpy(u, &lo, 8);
+  memcpy(u + 8, &hi, 8);
+  if (2 * (t->n + 1) > t->mask + 1 || !t->tab) {
+    uint32_t ncap = t->tab ? 2 * (t->mask + 1) : 1024;
+    free(t->tab);
+    t->tab = (uint32_t *)calloc(ncap, 4);
+    t->mask = ncap - 1;
+    for (uint32_t i = 0; i < t->n; i++) {
+      uint32_t h = uuid_hash(t->uuid[i]) & t->mask;
+      while (t->tab[h]) h = (h + 1) & t->mask;
+      t->tab[h] = i + 1;
+    }
+  }
+  uint32_t h = uuid_hash(u) & t->mask;
+  while (t->tab[h]) {
+    if (memcmp(t->uuid[t->tab[h] - 1], u, 16) == 0) return t->tab[h] - 1;
+    h = (h + 1) & t->mask;
+  }
+  if (t->n == t->cap) {
+    t->cap = t->cap ? 2 * t->cap : 1024;
+    t->uuid = (uint8_t (*)[16])realloc(t->uuid, (size_t)t->cap * 16);
+  }
+  memcpy(t->uuid[t->n], u, 16);
+  t->tab[h] = t->n + 1;
+  return t->n++;
+}
+
+typedef struct { uint32_t aid; uint64_t ctr; } ow_dot;
+typedef struct { uint32_t n, cap; union { ow_dot one; ow_dot *heap; } u; } ow_vc;  /* sorted by aid */
+static ow_dot *vc_d(ow_vc *v) { return v->cap > 1 ? v->u.heap : &v->u.one; }
+static const ow_dot *vc_cd(const ow_vc *v) { return v->cap > 1 ? v->u.heap : &v->u.one; }
+static void vc_free(ow_vc *v) {
+  if (v->cap > 1) free(v->u.heap);
+  memset(v, 0, sizeof *v);
+}
+static size_t vc_find(const ow_vc *v, uint32_t aid, int *found) {
+  const ow_dot *d = vc_cd(v);
+  size_t lo = 0, hi = v->n;
+  while (lo < hi) {
+    size_t mid = (lo + hi) / 2;
+    if (d[mid].aid < aid) lo = mid + 1; else hi = mid;
+  }
+  *found = lo < v->n && d[lo].aid == aid;
+  return lo;
+}
+static uint64_t vc_get(const ow_vc *v, uint32_t aid) {
+  int f;
+  size_t i = vc_find(v, aid, &f);
+  return f ? vc_cd(v)[i].ctr : 0;
+}
+static void vc_insert_at(ow_vc *v, size_t i, uint32_t aid, uint64_t c) {
+  uint32_t capn = v->cap > 1 ? v->cap : 1;
+  if (v->n == capn) {
+    uint32_t nc = v->cap > 1 ? 2 * v->cap : 4;
+    ow_dot *h = (ow_dot *)malloc((size_t)nc * sizeof(ow_dot));
+    memcpy(h, vc_d(v), v->n * sizeof(ow_dot));
+    if (v->cap > 1) free(v->u.heap);
+    v->u.heap = h;
+    v->cap = nc;
+  }
+  ow_dot *d = vc_d(v);
+  memmove(d + i + 1, d + i, (v->n - i) * sizeof(ow_dot));
+  d[i].aid = aid;
+  d[i].ctr = c;
+  v->n++;
+}
+static void vc_remove_at(ow_vc *v, size_t i) {
+  ow_dot *d = vc_d(v);
+  memmove(d + i, d + i + 1, (v->n - i - 1) * sizeof(ow_dot));
+  v->n--;
+}
+static void vc_apply_dot(ow_vc *v, uint32_t aid, uint64_t c) {  /* VClock::apply */
+  int f;
+  size_t i = vc_find(v, aid, &f);
+  if (f) { if (vc_d(v)[i].ctr < c) vc_d(v)[i].ctr = c; }
+  else if (c > 0) vc_insert_at(v, i, aid, c);
+}
+static void vc_put(ow_vc *v, uint32_t aid, uint64_t c) {
+  int f;
+  size_t i = vc_find(v, aid, &f);
+  if (f) vc_d(v)[i].ctr = c; else vc_insert_at(v, i, aid, c);
+}
+static void vc_clone(ow_vc *dst, const ow_vc *src) {
+  memset(dst, 0, sizeof *dst);
+  if (src->n <= 1) { *dst = *src; dst->cap = src->n ? 1 : 0; if (src->n) dst->u.one = vc_cd(src)[0]; return; }
+  dst->u.heap = (ow_dot *)malloc(src->n * sizeof(ow_dot));
+  memcpy(dst->u.heap, vc_cd(src), src->n * sizeof(ow_dot));
+  dst->n = dst->cap = src->n;
+  if (dst->cap == 1) dst->cap = 2;
+}
+static int vc_eq(const ow_vc *a, const ow_vc *b) {
+  if (a->n != b->n) return 0;
+  const ow_dot *x = vc_cd(a), *y = vc_cd(b);
+  for (uint32_t i = 0; i < a->n; i++)
+    if (x[i].aid != y[i].aid || x[i].ctr != y[i].ctr) return 0;
+  return 1;
+}
+/* v.reset_remove(other): drop a when other holds a with counter >= v[a] */
+static void vc_reset_remove(ow_vc *v, const ow_vc *other) {
+  for (size_t i = v->n; i-- > 0;) {
+    int f;
+    size_t j = vc_find(other, vc_d(v)[i].aid, &f);
+    if (f && vc_cd(other)[j].ctr >= vc_d(v)[i].ctr) vc_remove_at(v, i);
+  }
+}
+static int dot_cmp_aid(const void *x, const void *y) {
+  uint32_t a = ((const ow_dot *)x)->aid, b = ((const ow_dot *)y)->aid;
+  return a < b ? -1 : a > b;
+}
+/* raw [n, (lo, hi, c) x n] (distinct uuids) -> v; returns the words consumed */
+static size_t vc_from_raw(ow_vc *v, const uint64_t *p, ow_actors *A) {
+  size_t n = (size_t)p[0];
+  memset(v, 0, sizeof *v);
+  if (n == 1) { vc_insert_at(v, 0, ow_intern(A, p[1], p[2]), p[3]); return 4; }
+  if (n > 1) {
+    v->u.heap = (ow_dot *)malloc(n * sizeof(ow_dot));
+    v->cap = (uint32_t)n;
+    for (size_t k = 0; k < n; k++) {
+      v->u.heap[k].aid = ow_intern(A, p[1 + 3 * k], p[2 + 3 * k]);
+      v->u.heap[k].ctr = p[3 + 3 * k];
+    }
+    qsort(v->u.heap, n, sizeof(ow_dot), dot_cmp_aid);
+    v->n = (uint32_t)n;
+  }
+  return 1 + 3 * n;
+}
+
+typedef struct { uint64_t *c; size_t cap; } ow_dense;  /* clock by actor id; 0 = absent */
+static uint64_t dn_get(const ow_dense *d, uint32_t a) { return a < d->cap ? d->c[a] : 0; }
+static void dn_apply(ow_dense *d, uint32_t a, uint64_t v) {
+  if (a >= d->cap) {
+    size_t nc = d->cap ? d->cap : 1024;
+    while (nc <= a) nc *= 2;
+    d->c = (uint64_t *)realloc(d->c, nc * 8);
+    memset(d->c + d->cap, 0, (nc - d->cap) * 8);
+    d->cap = nc;
+  }
+  if (d->c[a] < v) d->c[a] = v;
+}
+static int vc_le_dense(const ow_vc *v, const ow_dense *d) {
+  const ow_dot *x = vc_cd(v);
+  for (uint32_t i = 0; i < v->n; i++)
+    if (dn_get(d, x[i].aid) < x[i].ctr) return 0;
+  return 1;
+}
+static int vc_le(const ow_vc *v, const ow_vc *o) {
+  const ow_dot *x = vc_cd(v);
+  for (uint32_t i = 0; i < v->n; i++)
+    if (vc_get(o, x[i].aid) < x[i].ctr) return 0;
+  return 1;
+}
+/* v.reset_remove(dense clock): the dense clock holds a iff its counter is nonzero */
+static void vc_reset_remove_dense(ow_vc *v, const ow_dense *d) {
+  for (size_t i = v->n; i-- > 0;) {
+    uint64_t c = dn_get(d, vc_d(v)[i].aid);
+    if (c && c >= vc_d(v)[i].ctr) vc_remove_at(v, i);
+  }
+}
+
+typedef struct { uint64_t key; ow_vc vc; uint32_t used; } ow_slot;
+typedef struct { ow_slot *s; size_t mask, n; } ow_map;
+static uint64_t mix64(uint64_t x) {
+  x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ULL;
+  x ^= x >> 27; x *= 0x94D049BB133111EBULL;
+  return x ^ (x >> 31);
+}
+static ow_slot *map_find(const ow_map *m, uint64_t k) {
+  if (!m->s) return NULL;
+  size_t h = mix64(k) & m->mask;
+  while (m->s[h].used) {
+    if (m->s[h].key == k) return &m->s[h];
+    h = (h + 1) & m->mask;
+  }
+  return NULL;
+}
+static ow_slot *map_add(ow_map *m, uint64_t k, int *fresh) {  /* get or insert (empty clock) */
+  if (!m->s || 2 * (m->n + 1) > m->mask + 1) {
+    size_t nc = m->s ? 2 * (m->mask + 1) : 1024;
+    ow_slot *old = m->s;
+    size_t ocap = m->s ? m->mask + 1 : 0;
+    m->s = (ow_slot *)calloc(nc, sizeof(ow_slot));
+    m->mask = nc - 1;
+    for (size_t i = 0; i < ocap; i++) {
+      if (!old[i].used) continue;
+      size_t h = mix64(old[i].key) & m->mask;
+      while (m->s[h].used) h = (h + 1) & m->mask;
+      m->s[h] = old[i];
+    }
+    free(old);
+  }
+  size_t h = mix64(k) & m->mask;
+  while (m->s[h].used) {
+    if (m->s[h].key == k) { *fresh = 0; return &m->s[h]; }
+    h = (h + 1) & m->mask;
+  }
+  m->s[h].used = 1;
+  m->s[h].key = k;
+  memset(&m->s[h].vc, 0, sizeof(ow_vc));
+  m->n++;
+  *fresh = 1;
+  return &m->s[h];
+}
+static void map_del(ow_map *m, ow_slot *s) {  /* backward-shift deletion */
+  size_t i = (size_t)(s - m->s);
+  vc_free(&m->s[i].vc);
+  size_t j = i;
+  for (;;) {
+    j = (j + 1) & m->mask;
+    if (!m->s[j].used) break;
+    size_t k = mix64(m->s[j].key) & m->mask;
+    if (i <= j ? (i < k && k <= j) : (i < k || k <= j)) continue;
+    m->s[i] = m->s[j];
+    i = j;
+  }
+  memset(&m->s[i], 0, sizeof(ow_slot));
+  m->n--;
+}
+static void map_free(ow_map *m) {
+  if (m->s)
+    for (size_t i = 0; i <= m->mask; i++)
+      if (m->s[i].used) vc_free(&m->s[i].vc);
+  free(m->s);
+  memset(m, 0, sizeof *m);
+}
+
+typedef struct { ow_vc clock; u64v mem; } ow_def;
+typedef struct { ow_def *d; size_t n, cap; } ow_defs;
+static void defs_free(ow_defs *D) {
+  for (size_t i = 0; i < D->n; i++) { vc_free(&D->d[i].clock); u64v_free(&D->d[i].mem); }
+  free(D->d);
+  memset(D, 0, sizeof *D);
+}
+/* deferred.setdefault(clock.key(), set()).update(members) */
+static void defs_add(ow_defs *D, const ow_vc *clock, const uint64_t *m, size_t nm) {
+  size_t i = 0;
+  while (i < D->n && !vc_eq(&D->d[i].clock, clock)) i++;
+  if (i == D->n) {
+    if (D->n == D->cap) {
+      D->cap = D->cap ? 2 * D->cap : 8;
+      D->d = (ow_def *)realloc(D->d, D->cap * sizeof(ow_def));
+    }
+    vc_clone(&D->d[i].clock, clock);
+    memset(&D->d[i].mem, 0, sizeof(u64v));
+    D->n++;
+  }
+  for (size_t k = 0; k < nm; k++) u64v_push(&D->d[i].mem, m[k]);
+}
+
+typedef struct { ow_dense clk; ow_map ent; ow_defs def; } ow_self;   /* the Core's Orswot */
+typedef struct { ow_vc clk; ow_map ent; ow_defs def; } ow_other;    /* a decoded state's */
+
+/* Orswot::apply_rm (crdts.py:113-121) */
+static void ow_apply_rm(ow_self *o, const uint64_t *m, size_t nm, const ow_vc *clock) {
+  for (size_t k = 0; k < nm; k++) {
+    ow_slot *s = map_find(&o->ent, m[k]);
+    if (!s) continue;
+    vc_reset_remove(&s->vc, clock);
+    if (s->vc.n == 0) map_del(&o->ent, s);
+  }
+  if (!vc_le_dense(clock, &o->clk)) defs_add(&o->def, clock, m, nm);
+}
+/* Orswot::apply_deferred (crdts.py:123-126) */
+static void ow_apply_deferred(ow_self *o) {
+  if (!o->def.n) return;
+  ow_defs old = o->def;
+  memset(&o->def, 0, sizeof o->def);
+  for (size_t i = 0; i < old.n; i++) ow_apply_rm(o, old.d[i].mem.p, old.d[i].mem.n, &old.d[i].clock);
+  defs_free(&old);
+}
+/* Orswot::merge (crdts.py:129-160) */
+static void ow_merge(ow_self *o, ow_other *x) {
+  u64v drop = {0};
+  if (o->ent.s)
+    for (size_t i = 0; i <= o->ent.mask; i++) {
+      ow_slot *s = &o->ent.s[i];
+      if (!s->used || map_find(&x->ent, s->key)) continue;
+      if (vc_le(&s->vc, &x->clk)) u64v_push(&drop, s->key);  /* other has seen it and dropped it */
+      else vc_reset_remove(&s->vc, &x->clk);
+    }
+  for (size_t k = 0; k < drop.n; k++) map_del(&o->ent, map_find(&o->ent, drop.p[k]));
+  u64v_free(&drop);
+  if (x->ent.s)
+    for (size_t i = 0; i <= x->ent.mask; i++) {
+      ow_slot *t = &x->ent.s[i];
+      if (!t->used) continue;
+      const ow_vc *clock = &t->vc;
+      const ow_dot *cd = vc_cd(clock);
+      ow_slot *ours = map_find(&o->ent, t->key);
+      if (ours) {
+        ow_vc cm;
+        memset(&cm, 0, sizeof cm);
+        for (uint32_t k = 0; k < clock->n; k++)      /* VClock::intersection(clock, ours) */
+          if (vc_get(&ours->vc, cd[k].aid) == cd[k].ctr) vc_put(&cm, cd[k].aid, cd[k].ctr);
+        for (uint32_t k = 0; k < clock->n; k++) {    /* .merge(clock.clone_without(self.clock)) */
+          uint64_t c = dn_get(&o->clk, cd[k].aid);
+          if (!(c && c >= cd[k].ctr)) vc_apply_dot(&cm, cd[k].aid, cd[k].ctr);
+        }
+        const ow_dot *od = vc_cd(&ours->vc);         /* .merge(ours.clone_without(other.clock)) */
+        for (uint32_t k = 0; k < ours->vc.n; k++) {
+          int f;
+          size_t j = vc_find(&x->clk, od[k].aid, &f);
+          if (!(f && vc_cd(&x->clk)[j].ctr >= od[k].ctr)) vc_apply_dot(&cm, od[k].aid, od[k].ctr);
+        }
+        if (cm.n == 0) { vc_free(&cm); map_del(&o->ent, ours); }
+        else { vc_free(&ours->vc); ours->vc = cm; }
+      } else {
+        if (vc_le_dense(clock, &o->clk)) continue;  /* seen and dropped */
+        ow_vc c;
+        vc_clone(&c, clock);
+        vc_reset_remove_dense(&c, &o->clk);
+        int fresh;
+        ow_slot *s = map_add(&o->ent, t->key, &fresh);
+        s->vc = c;
+      }
+    }
+  for (size_t i = 0; i < x->def.n; i++) ow_apply_rm(o, x->def.d[i].mem.p, x->def.d[i].mem.n, &x->def.d[i].clock);
+  const ow_dot *xd = vc_cd(&x->clk);
+  for (uint32_t k = 0; k < x->clk.n; k++) dn_apply(&o->clk, xd[k].aid, xd[k].ctr);
+  ow_apply_deferred(o);
+}
+
+/* Orswot::apply over one op file's raw stream (crdts.py:99-111) */
+static void ow_apply_ops(ow_self *o, ow_actors *A, const u64v *ops) {
+  const uint64_t *p = ops->p, *e = ops->p + ops->n;
+  ow_vc clock;
+  memset(&clock, 0, sizeof clock);
+  while (p < e) {
+    if (p[0] == 0) {
+      uint32_t a = ow_intern(A, p[1], p[2]);
+      uint64_t c = p[3];
+      size_t nm = (size_t)p[4];
+      const uint64_t *m = p + 5;
+      p = m + nm;
+      if (dn_get(&o->clk, a) >= c) continue;  /* already seen */
+      for (size_t k = 0; k < nm; k++) {
+        int fresh;
+        vc_apply_dot(&map_add(&o->ent, m[k], &fresh)->vc, a, c);
+      }
+      dn_apply(&o->clk, a, c);
+      ow_apply_deferred(o);
+    } else {
+      p += 1 + vc_from_raw(&clock, p + 1, A);
+      size_t nm = (size_t)p[0];
+      ow_apply_rm(o, p + 1, nm, &clock);
+      p += 1 + nm;
+      vc_free(&clock);
+    }
+  }
+}
+
+static void ow_other_build(ow_other *x, const ow_raw *r, ow_actors *A) {
+  memset(x, 0, sizeof *x);
+  vc_from_raw(&x->clk, r->clk.p, A);
+  const uint64_t *p = r->ent.p;
+  size_t ne = (size_t)*p++;
+  for (size_t k = 0; k < ne; k++) {
+    uint64_t m = *p++;
+    int fresh;
+    ow_slot *s = map_add(&x->ent, m, &fresh);
+    if (!fresh) vc_free(&s->vc);  /* a later duplicate member overwrites */
+    p += vc_from_raw(&s->vc, p, A);
+  }
+  p = r->def.p;
+  size_t nd = (size_t)*p++;
+  for (size_t k = 0; k < nd; k++) {
+    ow_vc c;
+    p += vc_from_raw(&c, p, A);
+    size_t nm = (size_t)*p++;
+    defs_add(&x->def, &c, p, nm);
+    p += nm;
+    vc_free(&c);
+  }
+}
+static void ow_other_free(ow_other *x) { vc_free(&x->clk); map_free(&x->ent); defs_free(&x->def); }
+
+/* --- canonical serialization (crdts.py serialize: members ascending, deferred by clock bytes) */
+typedef struct { const uint32_t *rank; const ow_actors *A; } ow_ser;
+static void wr_arr_hdr(wr_t *w, size_t n) {
+  if (n <= 15) wr_u8(w, (uint8_t)(0x90 | n));
+  else if (n <= 0xffff) { wr_u8(w, 0xdc); wr_be(w, n, 2); }
+  else { wr_u8(w, 0xdd); wr_be(w, n, 4); }
+}
+static void wr_dense(wr_t *w, const ow_dense *d, const ow_actors *A, const uint32_t *order) {
+  size_t n = 0;
+  for (uint32_t i = 0; i < A->n; i++) n += dn_get(d, i) != 0;
+  wr_map_hdr(w, 1);
+  wr_str(w, "dots");
+  wr_map_hdr(w, n);
+  for (uint32_t r = 0; r < A->n; r++) {
+    uint64_t c = dn_get(d, order[r]);
+    if (c) { wr_bin(w, A->uuid[order[r]], 16); wr_uint(w, c); }
+  }
+}
+static void wr_sparse(wr_t *w, const ow_vc *v, const ow_ser *S) {
+  ow_dot tmp[16], *t = v->n <= 16 ? tmp : (ow_dot *)malloc(v->n * sizeof(ow_dot));
+  memcpy(t, vc_cd(v), v->n * sizeof(ow_dot));
+  for (uint32_t i = 1; i < v->n; i++) {  /* insertion sort by uuid rank */
+    ow_dot x = t[i];
+    uint32_t j = i;
+    while (j > 0 && S->rank[t[j - 1].aid] > S->rank[x.aid]) { t[j] = t[j - 1]; j--; }
+    t[j] = x;
+  }
+  wr_map_hdr(w, 1);
+  wr_str(w, "dots");
+  wr_map_hdr(w, v->n);
+  for (uint32_t i = 0; i < v->n; i++) { wr_bin(w, S->A->uuid[t[i].aid], 16); wr_uint(w, t[i].ctr); }
+  if (t != tmp) free(t);
+}
+static const ow_actors *g_sort_actors;
+static int aid_uuid_cmp(const void *x, const void *y) {
+  return memcmp(g_sort_actors->uuid[*(const uint32_t *)x], g_sort_actors->uuid[*(const uint32_t *)y], 16);
+}
+static int u64_cmp(const void *x, const void *y) {
+  uint64_t a = *(const uint64_t *)x, b = *(const uint64_t *)y;
+  return a < b ? -1 : a > b;
+}
+typedef struct { uint64_t key; ow_vc *vc; } ow_ent_ref;
+static int ent_cmp(const void *x, const void *y) { return u64_cmp(x, y); }
+typedef struct { uint8_t *b; size_t n; ow_def *d; } ow_def_ref;
+static int def_cmp(const void *x, const void *y) {
+  const ow_def_ref *p = (const ow_def_ref *)x, *q = (const ow_def_ref *)y;
+  size_t l = p->n < q->n ? p->n : q->n;
+  int c = memcmp(p->b, q->b, l);
+  if (c) return c;
+  return p->n < q->n ? -1 : p->n > q->n;
+}
+static size_t ow_serialize(ow_self *o, const ow_dense *nov, const ow_actors *A, uint8_t *out, size_t cap) {
+  uint32_t *order = (uint32_t *)malloc((A->n + 1) * 4), *rank = (uint32_t *)malloc((A->n + 1) * 4);
+  for (uint32_t i = 0; i < A->n; i++) order[i] = i;
+  g_sort_actors = A;
+  qsort(order, A->n, 4, aid_uuid_cmp);
+  for (uint32_t r = 0; r < A->n; r++) rank[order[r]] = r;
+  ow_ser S = {rank, A};
+  wr_t w = {out, cap, 0};
+  wr_map_hdr(&w, 2);
+  wr_str(&w, "next_op_versions");
+  wr_dense(&w, nov, A, order);
+  wr_str(&w, "state");
+  wr_map_hdr(&w, 3);
+  wr_str(&w, "clock");
+  wr_dense(&w, &o->clk, A, order);
+  wr_str(&w, "entries");
+  ow_ent_ref *er = (ow_ent_ref *)malloc((o->ent.n + 1) * sizeof(ow_ent_ref));
+  size_t ne = 0;
+  if (o->ent.s)
+    for (size_t i = 0; i <= o->ent.mask; i++)
+      if (o->ent.s[i].used) { er[ne].key = o->ent.s[i].key; er[ne].vc = &o->ent.s[i].vc; ne++; }
+  qsort(er, ne, sizeof(ow_ent_ref), ent_cmp);
+  wr_map_hdr(&w, ne);
+  for (size_t i = 0; i < ne; i++) { wr_uint(&w, er[i].key); wr_sparse(&w, er[i].vc, &S); }
+  free(er);
+  wr_str(&w, "deferred");
+  ow_def_ref *dr = (ow_def_ref *)malloc((o->def.n + 1) * sizeof(ow_def_ref));
+  for (size_t i = 0; i < o->def.n; i++) {
+    wr_t k = {NULL, 0, 0};
+    wr_sparse(&k, &o->def.d[i].clock, &S);
+    dr[i].b = (uint8_t *)malloc(k.n);
+    dr[i].n = k.n;
+    wr_t k2 = {dr[i].b, k.n, 0};
+    wr_sparse(&k2, &o->def.d[i].clock, &S);
+    dr[i].d = &o->def.d[i];
+  }
+  qsort(dr, o->def.n, sizeof(ow_def_ref), def_cmp);
+  wr_map_hdr(&w, o->def.n);
+  for (size_t i = 0; i < o->def.n; i++) {
+    u64v *m = &dr[i].d->mem;
+    qsort(m->p, m->n, 8, u64_cmp);
+    size_t u = 0;
+    for (size_t k = 0; k < m->n; k++)
+      if (k == 0 || m->p[k] != m->p[k - 1]) m->p[u++] = m->p[k];
+    m->n = u;
+    wr_put(&w, dr[i].b, dr[i].n);
+    wr_arr_hdr(&w, u);
+    for (size_t k = 0; k < u; k++) wr_uint(&w, m->p[k]);
+    free(dr[i].b);
+  }
+  free(dr);
+  free(order);
+  free(rank);
+  return w.n;
+}
+
+/* --- the baseline: open + decode parallel over files, merge + fold on one thread --------- */
+typedef struct {
+  const uint8_t *key, *dv;
+  const uint8_t *sblob, *blob;
+  const uint64_t *soffs, *offs;
+  size_t ns, n, next;
+  pthread_mutex_t mu;
+  int32_t *status;  /* [ns + n] */
+  ow_raw *states;   /* [ns] */
+  u64v *ops;        /* [n] */
+} ow_job;
+
+static void *ow_worker(void *arg) {
+  ow_job *j = (ow_job *)arg;
+  ow_opctx ox;
+  memset(&ox, 0, sizeof ox);
+  uint8_t *buf = NULL;
+  size_t bcap = 0;
+  for (;;) {
+    pthread_mutex_lock(&j->mu);
+    size_t lo = j->next;
+    j->next += lo < j->ns ? 1 : 64;  /* a state file per claim, op files 64 at a time */
+    pthread_mutex_unlock(&j->mu);
+    if (lo >= j->ns + j->n) break;
+    size_t hi = lo < j->ns ? lo + 1 : (lo + 64 < j->ns + j->n ? lo + 64 : j->ns + j->n);
+    for (size_t i = lo; i < hi; i++) {
+      int is_state = i < j->ns;
+      size_t k = is_state ? i : i - j->ns;
+      const uint8_t *b = is_state ? j->sblob : j->blob;
+      const uint64_t *of = is_state ? j->soffs : j->offs;
+      size_t flen = of[k + 1] - of[k];
+      if (flen + 1 > bcap) { bcap = flen + 1; buf = (uint8_t *)realloc(buf, bcap); }
+      const uint8_t *pt;
+      size_t pl;
+      int st = open_file(KEY_VERSION, j->key, 32, (const uint8_t(*)[16])j->dv, 1, b + of[k], flen,
+                         buf, &pt, &pl);
+      if (st == OC_OK) {
+        if (is_state) {
+          ow_rawctx rx = {ox.vc, &j->states[k]};
+          if (ow_decode_state(pt, pl, &rx)) st = OC_ERR_DECODE;
+          ox.vc = rx.vc;
+        } else if (ow_decode_ops(pt, pl, &ox, &j->ops[k])) st = OC_ERR_DECODE;
+      }
+      j->status[i] = st;
+    }
+  }
+  free(buf);
+  free(ox.vc.tmp);
+  u64v_free(&ox.clk);
+  u64v_free(&ox.mem);
+  return NULL;
+}
+
+size_t oc_compact_orswot_best(const uint8_t key[32], const uint8_t data_version[16],
+                              const uint8_t *state_blob, const uint64_t *state_offs,
+                              size_t n_states, const uint8_t *blob, const uint64_t *offs,
+                              const uint8_t (*file_actor)[16], const uint64_t *file_version,
+                              size_t n_files, int n_threads, int seal, uint8_t *out, size_t cap,
+                              int *err, double phase_s[4]) {
+  if (n_threads < 1) n_threads = 1;
+  if (n_threads > 256) n_threads = 256;
+  double t0 = oc_now();
+  ow_job j;
+  memset(&j, 0, sizeof j);
+  j.key = key; j.dv = data_version;
+  j.sblob = state_blob; j.soffs = state_offs; j.ns = n_states;
+  j.blob = blob; j.offs = offs; j.n = n_files;
+  j.status = (int32_t *)calloc(n_states + n_files + 1, sizeof(int32_t));
+  j.states = (ow_raw *)calloc(n_states + 1, sizeof(ow_raw));
+  j.ops = (u64v *)calloc(n_files + 1, sizeof(u64v));
+  pthread_mutex_init(&j.mu, NULL);
+  pthread_t th[256];
+  for (int t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, ow_worker, &j);
+  for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+  pthread_mutex_destroy(&j.mu);
+  double t1 = oc_now();
+
+  int e = OC_OK;
+  size_t n_out = 0;
+  ow_actors A;
+  memset(&A, 0, sizeof A);
+  ow_self o;
+  memset(&o, 0, sizeof o);
+  ow_dense nov;
+  memset(&nov, 0, sizeof nov);
+  /* read_remote_states (lib.rs:401-469): any failing file rejects the batch */
+  for (size_t i = 0; i < n_states && !e; i++) e = j.status[i];
+  for (size_t i = 0; i < n_states && !e; i++) {
+    ow_other x;
+    ow_other_build(&x, &j.states[i], &A);
+    ow_merge(&o, &x);
+    ow_other_free(&x);
+    const uint64_t *p = j.states[i].nov.p;
+    for (size_t k = 0; k < (size_t)p[0]; k++)
+      dn_apply(&nov, ow_intern(&A, p[1 + 3 * k], p[2 + 3 * k]), p[3 + 3 * k]);
+  }
+  double t2 = oc_now();
+  /* read_remote_ops (lib.rs:471-547): every file opened and decoded first, then the gate */
+  for (size_t i = 0; i < n_files && !e; i++) e = j.status[n_states + i];
+  if (!e)
+    for (size_t i = 0; i < n_files; i++) {
+      uint64_t lo, hi;
+      memcpy(&lo, file_actor[i], 8);
+      memcpy(&hi, file_actor[i] + 8, 8);
+      uint32_t a = ow_intern(&A, lo, hi);
+      uint64_t expected = dn_get(&nov, a);
+      if (file_version[i] < expected) continue;
+      if (expected < file_version[i]) { e = OC_ERR_OP_VERSION; break; }
+      ow_apply_ops(&o, &A, &j.ops[i]);
+      dn_apply(&nov, a, expected + 1);
+    }
+  double t3 = oc_now();
+  if (!e) {
+    n_out = ow_serialize(&o, &nov, &A, out, cap);
+    if (seal && n_out <= cap) {  /* Core::compact's file: outer version || Cryptor::encrypt(..) */
+      uint8_t *clear = (uint8_t *)malloc(n_out + 16);
+      memcpy(clear, data_version, 16);
+      memcpy(clear + 16, out, n_out);
+      uint8_t *file = (uint8_t *)malloc(16 + oc_cryptor_sealed_len(n_out + 16));
+      memcpy(file, CORE_VERSION, 16);
+      size_t fl = 0;
+      static const uint8_t nonce[24] = {0};
+      oc_cryptor_encrypt(KEY_VERSION, key, 32, nonce, clear, n_out + 16, file + 16, &fl);
+      uint8_t name[32];
+      oc_sha3_256(file, fl + 16, name);  /* content name (crdt-enc-tokio lib.rs:403-432) */
+      free(clear);
+      free(file);
+    }
+  }
+  double t4 = oc_now();
+  if (phase_s) { phase_s[0] = t1 - t0; phase_s[1] = t2 - t1; phase_s[2] = t3 - t2; phase_s[3] = t4 - t3; }
+  for (size_t i = 0; i < n_states; i++) {
+    u64v_free(&j.states[i].nov); u64v_free(&j.states[i].clk);
+    u64v_free(&j.states[i].ent); u64v_free(&j.states[i].def);
+  }
+  for (size_t i = 0; i < n_files; i++) u64v_free(&j.ops[i]);
+  free(j.states); free(j.ops); free(j.status);
+  map_free(&o.ent); defs_free(&o.def); free(o.clk.c); free(nov.c);
+  free(A.uuid); free(A.tab);
+  *err = e;
+  return n_out;
+}

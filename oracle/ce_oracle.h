@@ -155,6 +155,21 @@ size_t oc_compact_ops_best(int kind, const uint8_t key[32], const uint8_t data_v
                            const uint8_t (*file_actor)[16], const uint64_t *file_version,
                            size_t n_files, int n_threads, uint8_t *out, size_t cap, int *err);
 
+/* Orswot<u64, Uuid> CPU baseline (C3): a C restatement of oracle/crdts.py (crdts 7 Orswot
+ * apply / apply_rm / apply_deferred / merge, Core.read_remote_states then read_remote_ops).
+ * Every state and op file is opened and decoded on n_threads threads; the state merges, the
+ * version gate and the op fold then run in file order on the calling thread (the fold is
+ * order-dependent: removals defer on the clock).  Returns the length of the canonical
+ * StateWrapper (crdts.py serialize; writes it when out != NULL and it fits in cap); seal != 0
+ * also seals it as Core::compact does (version prefix, Cryptor::encrypt, SHA3-256 name).
+ * phase_s (nullable) receives [open+decode, state merges, op fold, serialize(+seal)] seconds. */
+size_t oc_compact_orswot_best(const uint8_t key[32], const uint8_t data_version[16],
+                              const uint8_t *state_blob, const uint64_t *state_offs,
+                              size_t n_states, const uint8_t *blob, const uint64_t *offs,
+                              const uint8_t (*file_actor)[16], const uint64_t *file_version,
+                              size_t n_files, int n_threads, int seal, uint8_t *out, size_t cap,
+                              int *err, double phase_s[4]);
+
 #ifdef __cplusplus
 }
 #endif
