@@ -837,8 +837,11 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
         for (int i = 0; i < 7; i++) sum[i] += (double)hp[8 * w + i];
       }
     if (waves)
-      fprintf(stderr, "CE_PROF waves %u iters/wave %.1f cycles/iter: params %.0f chacha %.0f xor_horner %.0f "
-              "tree_tag %.0f decode_prelude %.0f decode_rounds %.0f\n", waves, sum[6] / waves,
+      // phase order: k_open_fold_small = params, chacha, xor_horner, tree_tag, decode prelude,
+      // decode rounds; k_open_fold_v2 = setup, first block, middle blocks, last block,
+      // tree_tag, decode
+      fprintf(stderr, "CE_PROF waves %u iters/wave %.1f cycles/iter: p0 %.0f p1 %.0f p2 %.0f "
+              "p3 %.0f p4 %.0f p5 %.0f\n", waves, sum[6] / waves,
               sum[0] / sum[6], sum[1] / sum[6], sum[2] / sum[6], sum[3] / sum[6], sum[4] / sum[6], sum[5] / sum[6]);
   }
   uint32_t* hc = ctx->h_counters.as<uint32_t>();

@@ -83,8 +83,10 @@ __device__ __forceinline__ ChachaPre chacha_pre(const uint32_t (&k)[8], uint32_t
   return p;
 }
 
-// chacha_block with the counter-independent first-round work taken from `pre`
-template <bool SD = (CE_ROT16_SDWA != 0)>
+// chacha_block with the counter-independent first-round work taken from `pre`.  UNR = double
+// rounds per trip of the 9-trip loop (9: straight-line code; 1 or 3: a rolled loop, a fraction
+// of the instruction bytes for kernels whose loop body would otherwise crowd the I-cache).
+template <bool SD = (CE_ROT16_SDWA != 0), int UNR = 9>
 __device__ __forceinline__ void chacha_block_pre(const ChachaPre& pre, const uint32_t (&k)[8],
                                                  uint32_t ctr, uint32_t n0, uint32_t n1,
                                                  uint32_t n2, uint32_t (&out)[16]) {
@@ -99,12 +101,21 @@ __device__ __forceinline__ void chacha_block_pre(const ChachaPre& pre, const uin
   // first diagonal round, then 9 double rounds
   CE_QR_T(SD, x[0], x[5], x[10], x[15]); CE_QR_T(SD, x[1], x[6], x[11], x[12]);
   CE_QR_T(SD, x[2], x[7], x[8], x[13]); CE_QR_T(SD, x[3], x[4], x[9], x[14]);
-#pragma unroll
-  for (int i = 0; i < 9; i++) {
+  auto dround = [&] {
     CE_QR_T(SD, x[0], x[4], x[8], x[12]); CE_QR_T(SD, x[1], x[5], x[9], x[13]);
     CE_QR_T(SD, x[2], x[6], x[10], x[14]); CE_QR_T(SD, x[3], x[7], x[11], x[15]);
     CE_QR_T(SD, x[0], x[5], x[10], x[15]); CE_QR_T(SD, x[1], x[6], x[11], x[12]);
     CE_QR_T(SD, x[2], x[7], x[8], x[13]); CE_QR_T(SD, x[3], x[4], x[9], x[14]);
+  };
+  if constexpr (UNR == 1) {
+#pragma unroll 1
+    for (int i = 0; i < 9; i++) dround();
+  } else if constexpr (UNR == 3) {
+#pragma unroll 1
+    for (int i = 0; i < 3; i++) { dround(); dround(); dround(); }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 9; i++) dround();
   }
   out[0] = x[0] + 0x61707865u; out[1] = x[1] + 0x3320646eu;
   out[2] = x[2] + 0x79622d32u; out[3] = x[3] + 0x6b206574u;

@@ -189,7 +189,9 @@ struct SupVers {
 // `prefetch` (the next file's parameters) is called once, after the decode's first round: a
 // global load issued before the round's actor-table lookups would be waited for with them
 // (vmcnt counts in order), exposing its latency.
-template <int LPF, typename Pf>
+// DOPT (diagnostics of k_open_fold_v2's OPT 128 / 256, results invalid for 128): 1 = actor
+// lookups replaced by the hash slot (no table load), 2 = the flush's atomicMax without its read
+template <int LPF, int DOPT = 0, typename Pf>
 __device__ __forceinline__ void decode_fold(const DecodeArgs& a, const SupVers& sup, const uint8_t* fl,
                                             uint32_t len, bool live, bool apply, uint32_t f,
                                             uint32_t grp, uint32_t sub, DecState& S, Pf&& prefetch) {
@@ -237,7 +239,10 @@ __device__ __forceinline__ void decode_fold(const DecodeArgs& a, const SupVers& 
   auto fold_dot = [&](uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3, unsigned long long ctr) {
     uint32_t slot;
     if (cached(k0, k1, k2, k3)) slot = S.cslot;
-    else {
+    else if (DOPT & 1) {
+      slot = actor_hash(k0, k1, k2, k3) & a.mask;
+      remember(slot, k0, k1, k2, k3);
+    } else {
       slot = lookup_slot(a.table, a.mask, k0, k1, k2, k3);
       remember(slot, k0, k1, k2, k3);
     }
@@ -384,7 +389,9 @@ __device__ __forceinline__ void decode_fold(const DecodeArgs& a, const SupVers& 
     } else
 #endif
     if (mx != 0 && mn == mx) {
-      if (sub == 0) batch_max(&a.batch[mx - 1], b);
+      if (DOPT & 2) {
+        if (sub == 0) atomicMax(&a.batch[mx - 1], b);
+      } else if (sub == 0) batch_max(&a.batch[mx - 1], b);
     } else if (pslot != 0xffffffffu) {
       batch_max(&a.batch[pslot], pbest);
     }
@@ -683,6 +690,7 @@ struct FilePre2 {
   uint32_t n2a, n2b;
   uint32_t R1[5];   // r
   uint32_t R64[5];  // r^64
+  uint32_t R2[5];   // r^2 (used by OPT 64 only; dead loads otherwise)
 };
 
 __device__ __forceinline__ FilePre2 load_pre2(const DecodeArgs& a, uint32_t f) {
@@ -708,6 +716,7 @@ __device__ __forceinline__ FilePre2 load_pre2(const DecodeArgs& a, uint32_t f) {
   for (int i = 0; i < 5; i++) {
     p.R1[i] = Pp->rpow[0][i];
     p.R64[i] = Pp->rpow[6][i];
+    p.R2[i] = Pp->rpow[1][i];
   }
   return p;
 }
@@ -716,12 +725,22 @@ __device__ __forceinline__ FilePre2 load_pre2(const DecodeArgs& a, uint32_t f) {
 // OPT bits: 1 = rot16 as two SDWA xors (ce_device.h xor_rotl16_t), 2 = the next iteration's
 // ciphertext loads issued inside this iteration's decode (after its first round, with the
 // parameters loaded one iteration earlier), so they land while the decode and the next
-// iteration's first ChaCha20 block run instead of being waited for at the first XOR.
+// iteration's first ChaCha20 block run instead of being waited for at the first XOR;
+// 4 / 8 = ChaCha20's 9 trailing double rounds as a rolled loop of 1 / 3 (instruction bytes);
+// 16 = one block of the next iteration's ciphertext in flight across the iteration boundary.
 template <int LPF, int W, bool JIT, int OPT = 3>
 __global__ __launch_bounds__(64, W)
 void k_open_fold_v2(DecodeArgs a) {
   constexpr bool SD = (OPT & 1) != 0;
   constexpr bool PF = (OPT & 2) != 0 && !JIT;
+  constexpr int UNR = (OPT & 4) ? 1 : (OPT & 8) ? 3 : 9;  // ChaCha20 double rounds per loop trip
+  // OPT 16: the first-processed block (k = BPL - 1) of the NEXT iteration is loaded as soon as
+  // this iteration has consumed its own (its parameters are loaded at this iteration's start)
+  constexpr bool PF1 = (OPT & 16) != 0 && !PF && !JIT;
+  // OPT 64: parameters two iterations ahead, loaded after the decode's last global read (its
+  // flush), with r^2 among them -- no wait inside an iteration covers a load issued in it
+  // before its own ciphertext
+  constexpr bool DP = (OPT & 64) != 0 && !PF;
   using C = V2Cfg<LPF>;
   constexpr int F = C::F;
   constexpr int BPL = C::BPL;
@@ -760,6 +779,30 @@ void k_open_fold_v2(DecodeArgs a) {
     }
   };
   FilePre2 nn;  // PF: the parameters of the iteration after next
+  // CE_PROF (diagnostics build): s_memtime at phase boundaries, summed per wave: setup, first
+  // block (waits for its ciphertext), middle blocks, last block, tree+tag, decode, iterations
+#if CE_FUSED_DIAG
+  unsigned long long pc[7] = {0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tp = a.prof ? __builtin_amdgcn_s_memtime() : 0;
+#define CE_PHASE2(i)                                           \
+  if (a.prof) {                                                \
+    const unsigned long long tn = __builtin_amdgcn_s_memtime(); \
+    pc[i] += tn - tp;                                          \
+    tp = tn;                                                   \
+  }
+#else
+#define CE_PHASE2(i)
+#endif
+  if (OPT & 32) {
+    // diagnostics: waves in odd SIMD slots start ~half an iteration late (phase-locked waves?)
+    const uint32_t hw = __builtin_amdgcn_s_getreg((3 << 11) | 4);  // HW_ID.WAVE_ID
+    if (hw & 1) {
+      __builtin_amdgcn_s_sleep(127);
+      __builtin_amdgcn_s_sleep(127);
+    }
+  }
+  if (PF1) load_block_of(nx, BPL - 1);
+  if (DP) nn = load_pre2(a, (g + stride) * F + grp);
   if (PF) {
     // prologue: this wave's first ciphertext, and the next iteration's parameters
 #pragma unroll
@@ -770,7 +813,8 @@ void k_open_fold_v2(DecodeArgs a) {
   for (; g < ngroups; g += stride) {
     const uint32_t f = g * F + grp;
     const FilePre2 cur = nx;
-    if (PF) nx = nn;
+    if (PF || DP) nx = nn;
+    if (PF1 && !DP) nx = load_pre2(a, (g + stride) * F + grp);  // issued before this iteration's loads
     const bool act = cur.ok && cur.len <= kSmallMax;
     const uint32_t len = act ? cur.len : 0u;
     const uint32_t npc = (len + 15) >> 4;             // ciphertext Poly1305 blocks
@@ -783,7 +827,8 @@ void k_open_fold_v2(DecodeArgs a) {
     // loads are issued up front.
     if (!PF) {
 #pragma unroll
-      for (int k = BPL - 1; k >= (JIT ? BPL - 1 : 0); k--) load_block(k);
+      for (int k = BPL - 1; k >= (JIT ? BPL - 1 : 0); k--)
+        if (!PF1 || k != BPL - 1) load_block(k);
     }
 
     // 2) per block, earliest first: keystream (counter 1 + b) in registers, XOR, plaintext ->
@@ -799,11 +844,12 @@ void k_open_fold_v2(DecodeArgs a) {
     if (LPF == 32) RC = mulmod(RC, RC);  // chain step r^(4 LPF) = r^128
     L5 R2;
 #pragma unroll
-    for (int i = 0; i < 5; i++) R2.v[i] = Pp->rpow[1][i];
+    for (int i = 0; i < 5; i++) R2.v[i] = DP ? cur.R2[i] : Pp->rpow[1][i];
     const MulR M1 = mul_r(R1), M2 = mul_r(R2), M3 = mul_r(mulmod(R2, R1)), MC = mul_r(RC);
     L5 acc{{0, 0, 0, 0, 0}}, glast{{0, 0, 0, 0, 0}};
     uint32_t rp[4 * C::NRP];  // r^(2^k), k <= LOG + 1
     uint4 sv4, tg4;           // s || expected tag
+    CE_PHASE2(0)
 #pragma unroll
     for (int k = BPL - 1; k >= 0; k--) {
       const int32_t b = nblk - 1 - (int32_t)sub - LPF * k;
@@ -830,7 +876,7 @@ void k_open_fold_v2(DecodeArgs a) {
         for (int i = 0; i < 16; i++) kb[i] = cur.key[i & 7] + (uint32_t)b;
       } else
 #endif
-        chacha_block_pre<SD>(cpre, cur.key, 1u + (uint32_t)b, 0u, cur.n2a, cur.n2b, kb);
+        chacha_block_pre<SD, UNR>(cpre, cur.key, 1u + (uint32_t)b, 0u, cur.n2a, cur.n2b, kb);
       L5 G, mj[4];
 #pragma unroll
       for (int j = 0; j < 4; j++) {
@@ -897,10 +943,14 @@ void k_open_fold_v2(DecodeArgs a) {
       const bool to_acc = has && !(k == 0 && sub == 0);
 #pragma unroll
       for (int i = 0; i < 5; i++) acc.v[i] = to_acc ? an.v[i] : acc.v[i];
+      if (PF1 && k == BPL - 1) load_block_of(nx, BPL - 1);  // next iteration's first block
       if (k == 0) {
 #pragma unroll
         for (int i = 0; i < 5; i++) glast.v[i] = has && sub == 0 ? G.v[i] : 0u;
       }
+      if (k == BPL - 1) { CE_PHASE2(1) }
+      else if (k == 1) { CE_PHASE2(2) }
+      else if (k == 0) { CE_PHASE2(3) }
     }
 
     // 3) chains -> tree positions (q takes lane q + 1's chain, q = LPF - 1 lane 0's), then
@@ -946,23 +996,37 @@ void k_open_fold_v2(DecodeArgs a) {
 #if CE_FUSED_DIAG
     if (a.ablate) ok = !(a.ablate & 1);
 #endif
+    CE_PHASE2(4)
 
     // 4) data-version check, decode from LDS, fold; the next iteration's parameters are loaded
     //    inside (their latency hides under the decode)
-    decode_fold<LPF>(a, sup, fl, len, act && ok, cur.apply != 0, f, grp, sub, S, [&] {
+    decode_fold<LPF, (OPT >> 7) & 3>(a, sup, fl, len, act && ok, cur.apply != 0, f, grp, sub, S, [&] {
       if (PF) {
         // next iteration's ciphertext (its parameters arrived one iteration ago) into the
         // registers this iteration no longer needs, then the parameters one further ahead
 #pragma unroll
         for (int k = BPL - 1; k >= 0; k--) load_block_of(nx, k);
         nn = load_pre2(a, (g + 2 * stride) * F + grp);
-      } else {
+      } else if (!PF1 && !DP) {
         nx = load_pre2(a, (g + stride) * F + grp);
       }
     });
+    if (DP) nn = load_pre2(a, (g + 2 * stride) * F + grp);
     __builtin_amdgcn_wave_barrier();
+    CE_PHASE2(5)
+#if CE_FUSED_DIAG
+    pc[6]++;
+#endif
   }
   fails.flush(a);
+#undef CE_PHASE2
+#if CE_FUSED_DIAG
+  if (a.prof && lane == 0) {
+    unsigned long long* o = a.prof + 8ull * blockIdx.x;
+#pragma unroll
+    for (int i = 0; i < 7; i++) o[i] = pc[i];
+  }
+#endif
 }
 
 template <int LPF, int W, bool JIT, int OPT = 3>
@@ -995,6 +1059,16 @@ hipError_t launch_open_fold_v2(hipStream_t s, const DecodeArgs& a, int files_per
     else if (opt == 0) launch_v2<16, 2, false, 0>(s, a);
     else if (opt == 1) launch_v2<16, 2, false, 1>(s, a);
     else if (opt == 2) launch_v2<16, 2, false, 2>(s, a);
+    else if (opt == 5) launch_v2<16, 2, false, 5>(s, a);
+    else if (opt == 9) launch_v2<16, 2, false, 9>(s, a);
+    else if (opt == 17) launch_v2<16, 2, false, 17>(s, a);
+    else if (opt == 21) launch_v2<16, 2, false, 21>(s, a);
+    else if (opt == 33) launch_v2<16, 2, false, 33>(s, a);
+    else if (opt == 65) launch_v2<16, 2, false, 65>(s, a);
+    else if (opt == 129) launch_v2<16, 2, false, 129>(s, a);
+    else if (opt == 257) launch_v2<16, 2, false, 257>(s, a);
+    else if (opt == 385) launch_v2<16, 2, false, 385>(s, a);
+    else if (opt == 81) launch_v2<16, 2, false, 81>(s, a);
     else launch_v2<16, 2, false, 3>(s, a);
   }
   return hipGetLastError();
