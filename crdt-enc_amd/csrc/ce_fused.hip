@@ -189,13 +189,28 @@ struct SupVers {
 // `prefetch` (the next file's parameters) is called once, after the decode's first round: a
 // global load issued before the round's actor-table lookups would be waited for with them
 // (vmcnt counts in order), exposing its latency.
-// DOPT (diagnostics of k_open_fold_v2's OPT 128 / 256, results invalid for 128): 1 = actor
-// lookups replaced by the hash slot (no table load), 2 = the flush's atomicMax without its read
+// DOPT (diagnostics of k_open_fold_v2's OPT 128 / 256 / 512 / 1024, results invalid for 128):
+// 1 = actor lookups replaced by the hash slot (no table load), 2 = the flush's atomicMax without
+// its read, 4 = one extra ChaCha20 block's double rounds spread over the fast rounds (one per
+// round, the rest after the loop), 8 = the same extra block after the decode loops (4 vs 8:
+// how much independent VALU work the decode's stalls could absorb)
 template <int LPF, int DOPT = 0, typename Pf>
 __device__ __forceinline__ void decode_fold(const DecodeArgs& a, const SupVers& sup, const uint8_t* fl,
                                             uint32_t len, bool live, bool apply, uint32_t f,
                                             uint32_t grp, uint32_t sub, DecState& S, Pf&& prefetch) {
   int32_t st = CE_OK;
+  uint32_t xs[16];
+  int drn = 0;
+  auto dround = [&] {
+    CE_QR_T(true, xs[0], xs[4], xs[8], xs[12]); CE_QR_T(true, xs[1], xs[5], xs[9], xs[13]);
+    CE_QR_T(true, xs[2], xs[6], xs[10], xs[14]); CE_QR_T(true, xs[3], xs[7], xs[11], xs[15]);
+    CE_QR_T(true, xs[0], xs[5], xs[10], xs[15]); CE_QR_T(true, xs[1], xs[6], xs[11], xs[12]);
+    CE_QR_T(true, xs[2], xs[7], xs[8], xs[13]); CE_QR_T(true, xs[3], xs[4], xs[9], xs[14]);
+  };
+  if (DOPT & 12) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) xs[i] = f * 16u + (uint32_t)i + sub;
+  }
   if (live) {
     if (len < 16) st = CE_ERR_PT_LEN;
     else if (!sup.has(a, *reinterpret_cast<const uint4*>(fl))) st = CE_ERR_PT_VERSION;
@@ -274,6 +289,10 @@ __device__ __forceinline__ void decode_fold(const DecodeArgs& a, const SupVers& 
 #pragma unroll
         for (int q = 0; q < 13; q++) dd[h][q] = d[q];
       }
+      if ((DOPT & 4) && drn < 10) {
+        dround();
+        drn++;
+      }
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         const uint32_t sh = cand[h] & 3;
@@ -302,6 +321,10 @@ __device__ __forceinline__ void decode_fold(const DecodeArgs& a, const SupVers& 
     }
     pos += done * L0;
     remaining -= done;
+  }
+  if (DOPT & 12) {
+#pragma unroll 1
+    for (; drn < 10; drn++) dround();
   }
   if (!pf_done) {
     prefetch();
@@ -396,6 +419,7 @@ __device__ __forceinline__ void decode_fold(const DecodeArgs& a, const SupVers& 
       batch_max(&a.batch[pslot], pbest);
     }
   }
+  if ((DOPT & 12) && (xs[0] ^ xs[5] ^ xs[10] ^ xs[15]) == 0x9e3779b9u) a.status[f] = 77;
   if (live && st != CE_OK && sub == 0) {
     a.status[f] = st;
     atomicAdd(&a.counters[3], 1u);
@@ -1000,7 +1024,7 @@ void k_open_fold_v2(DecodeArgs a) {
 
     // 4) data-version check, decode from LDS, fold; the next iteration's parameters are loaded
     //    inside (their latency hides under the decode)
-    decode_fold<LPF, (OPT >> 7) & 3>(a, sup, fl, len, act && ok, cur.apply != 0, f, grp, sub, S, [&] {
+    decode_fold<LPF, (OPT >> 7) & 15>(a, sup, fl, len, act && ok, cur.apply != 0, f, grp, sub, S, [&] {
       if (PF) {
         // next iteration's ciphertext (its parameters arrived one iteration ago) into the
         // registers this iteration no longer needs, then the parameters one further ahead
@@ -1068,6 +1092,8 @@ hipError_t launch_open_fold_v2(hipStream_t s, const DecodeArgs& a, int files_per
     else if (opt == 129) launch_v2<16, 2, false, 129>(s, a);
     else if (opt == 257) launch_v2<16, 2, false, 257>(s, a);
     else if (opt == 385) launch_v2<16, 2, false, 385>(s, a);
+    else if (opt == 513) launch_v2<16, 2, false, 513>(s, a);
+    else if (opt == 1025) launch_v2<16, 2, false, 1025>(s, a);
     else if (opt == 81) launch_v2<16, 2, false, 81>(s, a);
     else launch_v2<16, 2, false, 3>(s, a);
   }
