@@ -22,20 +22,20 @@ namespace ce {
 enum { kDsErr = 0, kDsOk = 1, kDsHost = -1 };
 
 // read an enum header: map(1) then the variant identifier; returns variant index, -2 error
-template <int NV>
-CE_HD int ds_variant(Rd& r, const char* const (&names)[NV]) {
+template <int NV, typename R>
+CE_HD int ds_variant(R& r, const char* const (&names)[NV]) {
   uint64_t cnt;
-  if (r.i >= r.n || !is_map_marker(r.p[r.i])) return -2;
+  if (r.i >= r.n || !is_map_marker(rb(r, r.i))) return -2;
   if (!rd_map_hdr(r, &cnt) || cnt != 1) return -2;
   const int v = rd_field<NV>(r, names);
   return (v < 0 || v >= NV) ? -2 : v;
 }
 
 // Vec<u64>: calls sink.member(m) for each element
-template <typename F>
-CE_HD int ds_members(Rd& r, F&& member) {
+template <typename R, typename F>
+CE_HD int ds_members(R& r, F&& member) {
   uint64_t cnt, m;
-  if (r.i >= r.n || !is_array_marker(r.p[r.i])) return kDsErr;
+  if (r.i >= r.n || !is_array_marker(rb(r, r.i))) return kDsErr;
   if (!rd_array_hdr(r, &cnt) || cnt > r.n - r.i) return kDsErr;
   for (uint64_t k = 0; k < cnt; k++) {
     if (!rd_u64(r, &m)) return kDsErr;
@@ -45,14 +45,14 @@ CE_HD int ds_members(Rd& r, F&& member) {
 }
 
 // VClock {dots: map<Uuid, u64>}: calls dot(actor_off, counter) per entry.
-template <typename F>
-CE_HD int ds_vclock(Rd& r, F&& dot) {
+template <typename R, typename F>
+CE_HD int ds_vclock(R& r, F&& dot) {
   static constexpr const char* kF[1] = {"dots"};
   if (r.i >= r.n) return kDsErr;
   uint64_t cnt;
-  const uint8_t m0 = r.p[r.i];
+  const uint8_t m0 = rb(r, r.i);
   bool have = false;
-  auto dots = [&](Rd& q) -> int {
+  auto dots = [&](R& q) -> int {
     uint64_t n, off, c, prev = 0;
     if (!rd_map_hdr(q, &n) || n > q.n - q.i) return kDsErr;
     for (uint64_t k = 0; k < n; k++) {
@@ -62,7 +62,7 @@ CE_HD int ds_vclock(Rd& r, F&& dot) {
       if (k) {
         int cmp = 0;
         for (int b = 0; b < 16 && cmp == 0; b++)
-          cmp = (int)q.p[off + b] - (int)q.p[prev + b];
+          cmp = (int)q.p[off + b] - (int)q.p[prev + b];  // direct: two keys apart
         if (cmp <= 0) return kDsHost;
       }
       prev = off;
@@ -92,11 +92,11 @@ CE_HD int ds_vclock(Rd& r, F&& dot) {
 }
 
 // Struct body with two fields, each parsed by fn(field_index, rd) -> kDs*.
-template <typename F>
-CE_HD int ds_struct2(Rd& r, const char* const (&names)[2], F&& fn) {
+template <typename R, typename F>
+CE_HD int ds_struct2(R& r, const char* const (&names)[2], F&& fn) {
   if (r.i >= r.n) return kDsErr;
   uint64_t cnt;
-  if (is_array_marker(r.p[r.i])) {
+  if (is_array_marker(rb(r, r.i))) {
     if (!rd_array_hdr(r, &cnt) || cnt != 2) return kDsErr;
     for (int f = 0; f < 2; f++) {
       const int s = fn(f, r);
@@ -126,21 +126,21 @@ CE_HD int ds_struct2(Rd& r, const char* const (&names)[2], F&& fn) {
 //   add_begin(); add_dot(actor_off, counter); add_member(m); add_end();
 //   rm_begin();  rm_dot(actor_off, counter);  rm_member(m);  rm_end();
 // Fields may come in any order (struct maps), so a sink must not assume dot-before-members.
-template <typename S>
+template <typename S, typename R = Rd>
 CE_HD int ds_parse_orswot_ops(const uint8_t* p, uint64_t n, S& sink) {
   static constexpr const char* kV[2] = {"Add", "Rm"};
   static constexpr const char* kAdd[2] = {"dot", "members"};
   static constexpr const char* kRm[2] = {"clock", "members"};
-  Rd r{p, n, 0};
+  R r{p, n, 0};
   uint64_t cnt;
-  if (r.n == 0 || !is_array_marker(r.p[0]) || !rd_array_hdr(r, &cnt) || cnt > r.n) return kDsErr;
+  if (r.n == 0 || !is_array_marker(rb(r, 0)) || !rd_array_hdr(r, &cnt) || cnt > r.n) return kDsErr;
   for (uint64_t k = 0; k < cnt; k++) {
     const int v = ds_variant<2>(r, kV);
     if (v < 0) return kDsErr;
     int s;
     if (v == 0) {
       sink.add_begin();
-      s = ds_struct2(r, kAdd, [&](int f, Rd& q) -> int {
+      s = ds_struct2(r, kAdd, [&](int f, R& q) -> int {
         if (f == 1) return ds_members(q, [&](uint64_t m) { sink.add_member(m); });
         uint64_t aoff, c;
         const int d = parse_dot(q, &aoff, &c);
@@ -151,7 +151,7 @@ CE_HD int ds_parse_orswot_ops(const uint8_t* p, uint64_t n, S& sink) {
       if (s == kDsOk) sink.add_end();
     } else {
       sink.rm_begin();
-      s = ds_struct2(r, kRm, [&](int f, Rd& q) -> int {
+      s = ds_struct2(r, kRm, [&](int f, R& q) -> int {
         if (f == 1) return ds_members(q, [&](uint64_t m) { sink.rm_member(m); });
         return ds_vclock(q, [&](uint64_t off, uint64_t c) { sink.rm_dot(off, c); });
       });
@@ -163,18 +163,18 @@ CE_HD int ds_parse_orswot_ops(const uint8_t* p, uint64_t n, S& sink) {
 }
 
 // Sink for MVReg ops: put_begin(); put_dot(actor_off, counter); put_val(v); put_end();
-template <typename S>
+template <typename S, typename R = Rd>
 CE_HD int ds_parse_mvreg_ops(const uint8_t* p, uint64_t n, S& sink) {
   static constexpr const char* kV[1] = {"Put"};
   static constexpr const char* kPut[2] = {"clock", "val"};
-  Rd r{p, n, 0};
+  R r{p, n, 0};
   uint64_t cnt;
-  if (r.n == 0 || !is_array_marker(r.p[0]) || !rd_array_hdr(r, &cnt) || cnt > r.n) return kDsErr;
+  if (r.n == 0 || !is_array_marker(rb(r, 0)) || !rd_array_hdr(r, &cnt) || cnt > r.n) return kDsErr;
   for (uint64_t k = 0; k < cnt; k++) {
     const int v = ds_variant<1>(r, kV);
     if (v < 0) return kDsErr;
     sink.put_begin();
-    const int s = ds_struct2(r, kPut, [&](int f, Rd& q) -> int {
+    const int s = ds_struct2(r, kPut, [&](int f, R& q) -> int {
       if (f == 0) return ds_vclock(q, [&](uint64_t off, uint64_t c) { sink.put_dot(off, c); });
       uint64_t val;
       if (!rd_u64(q, &val)) return kDsErr;
