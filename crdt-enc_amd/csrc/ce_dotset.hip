@@ -93,16 +93,27 @@ __device__ __forceinline__ uint32_t block_count(uint32_t* global, bool pred, uin
 // ---------------------------------------------------------------------------------------
 // decode: one lane per file
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t lookup_actor(const DsDecodeArgs& a, const uint8_t* u) {
-  uint32_t w[4];
-  for (int j = 0; j < 4; j++)
-    w[j] = (uint32_t)u[4 * j] | ((uint32_t)u[4 * j + 1] << 8) | ((uint32_t)u[4 * j + 2] << 16) |
-           ((uint32_t)u[4 * j + 3] << 24);
+// the last actor a lane resolved (a file's ops are mostly its writer's)
+struct ActorCache {
+  uint4 k = make_uint4(0, 0, 0, 0);
+  uint32_t id = kDsNoActor;
+};
+
+__device__ __forceinline__ uint32_t lookup_actor(const DsDecodeArgs& a, const uint8_t* u,
+                                                 ActorCache* cache = nullptr) {
+  const uint4 k = *reinterpret_cast<const uint4*>(u);  // unaligned 16 B inside the plaintext
+  if (cache && cache->id != kDsNoActor && k.x == cache->k.x && k.y == cache->k.y &&
+      k.z == cache->k.z && k.w == cache->k.w)
+    return cache->id;
+  const uint32_t w[4] = {k.x, k.y, k.z, k.w};
   uint32_t h = actor_hash(w[0], w[1], w[2], w[3]) & a.mask;
   for (uint32_t probe = 0; probe <= a.mask; probe++) {
     const ActorSlot& s = a.table[h];
     if (!s.used) break;
-    if (s.k[0] == w[0] && s.k[1] == w[1] && s.k[2] == w[2] && s.k[3] == w[3]) return s.pad[0];
+    if (s.k[0] == w[0] && s.k[1] == w[1] && s.k[2] == w[2] && s.k[3] == w[3]) {
+      if (cache) { cache->k = k; cache->id = s.pad[0]; }
+      return s.pad[0];
+    }
     h = (h + 1) & a.mask;
   }
   const uint32_t i = atomicAdd(a.counters + 2, 1u);
@@ -130,9 +141,10 @@ struct EmitSink {
   const DsDecodeArgs* a;
   const uint8_t* p;
   uint32_t ia, iam, ir, irc, irm;
+  ActorCache cache;
   __device__ void add_begin() { a->ops.add_mbeg[ia] = iam; }
   __device__ void add_dot(uint64_t off, uint64_t c) {
-    a->ops.add_actor[ia] = lookup_actor(*a, p + off);
+    a->ops.add_actor[ia] = lookup_actor(*a, p + off, &cache);
     a->ops.add_ctr[ia] = c;
   }
   __device__ void add_member(uint64_t m) { a->ops.add_mem[iam++] = m; }
@@ -142,7 +154,7 @@ struct EmitSink {
     a->ops.rm_mbeg[ir] = irm;
   }
   __device__ void rm_dot(uint64_t off, uint64_t c) {
-    a->ops.rmc_actor[irc] = lookup_actor(*a, p + off);
+    a->ops.rmc_actor[irc] = lookup_actor(*a, p + off, &cache);
     a->ops.rmc_ctr[irc] = c;
     irc++;
   }
@@ -154,9 +166,107 @@ struct EmitSink {
   __device__ void put_end() { ir++; }
 };
 
+// ---- canonical-op fast path of the lane-per-file Orswot op decode --------------------------
+// The grammar (ce_dotset_codec.h) walks a file byte by byte, one dependent global load per byte.
+// The forms rmp-serde's to_vec_named writes for the common ops are checked instead from 64-byte
+// register windows (unaligned 16-byte loads; every plaintext buffer has >= 64 bytes of slack
+// past its last file):
+//   Add: 81 a3"Add" 82 a3"dot" 82 a5"actor" c4 10 <uuid> a7"counter" <uint> a7"members" 91 <uint>
+//   Rm:  81 a2"Rm" 82 a5"clock" 81 a4"dots" 81 c4 10 <uuid> <uint> a7"members" 91 <uint>
+// (one member; a one-entry clock), <uint> = positive fixint / cc / cd / ce / cf.  Anything else
+// -- other widths, more members or clock entries, reordered or extra fields -- is parsed by the
+// grammar from the same op on (no sink call is made before an op is fully proven), so the sink
+// sees exactly the calls ds_parse_orswot_ops would make.
+struct Win64 {
+  uint32_t w[16];
+  __device__ __forceinline__ explicit Win64(const uint8_t* q) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint4 v = *reinterpret_cast<const uint4*>(q + 16 * k);  // unaligned
+      w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+    }
+  }
+  // LE word at byte b (b compile-time, b + 4 <= 64)
+  __device__ __forceinline__ uint32_t word(int b) const {
+    return (b & 3) ? __builtin_amdgcn_alignbyte(w[(b >> 2) + 1], w[b >> 2], b & 3) : w[b >> 2];
+  }
+  __device__ __forceinline__ uint32_t byte(int b) const { return (w[b >> 2] >> (8 * (b & 3))) & 0xffu; }
+  // msgpack uint at byte b (positive fixint, cc, cd, ce, cf); *len = its size, 0 if another form
+  __device__ __forceinline__ uint64_t uint_at(int b, uint32_t* len) const {
+    const uint32_t m = byte(b);
+    const uint32_t x0 = __builtin_bswap32(word(b + 1)), x1 = __builtin_bswap32(word(b + 5));
+    if (m < 0x80u) { *len = 1; return m; }
+    if (m == 0xccu) { *len = 2; return x0 >> 24; }
+    if (m == 0xcdu) { *len = 3; return x0 >> 16; }
+    if (m == 0xceu) { *len = 5; return x0; }
+    if (m == 0xcfu) { *len = 9; return ((uint64_t)x0 << 32) | x1; }
+    *len = 0;
+    return 0;
+  }
+};
+
+// "a7 members 91 <uint>" at q: the one-member array; returns bytes consumed, 0 if not that form
+__device__ __forceinline__ uint32_t fast_members1(const uint8_t* q, uint64_t* m) {
+  const Win64 v(q);
+  if (v.word(0) != 0x6d656da7u || v.word(4) != 0x73726562u || v.byte(8) != 0x91u) return 0;
+  uint32_t l;
+  *m = v.uint_at(9, &l);
+  return l ? 9 + l : 0;
+}
+
+template <typename S>
+__device__ __forceinline__ bool fast_orswot_op(const uint8_t* p, uint64_t n, uint64_t& i, S& sink) {
+  if (n - i < 32) return false;
+  const uint8_t* q = p + i;
+  const Win64 v(q);
+  uint32_t l, lm;
+  uint64_t ctr, mem;
+  if (v.w[0] == 0x6441a381u && v.w[1] == 0x64a38264u && v.w[2] == 0xa582746fu &&
+      v.w[3] == 0x6f746361u && (v.w[4] & 0xffffffu) == 0x10c472u && v.word(35) == 0x756f63a7u &&
+      v.word(39) == 0x7265746eu) {  // Add
+    ctr = v.uint_at(43, &l);
+    if (!l) return false;
+    lm = fast_members1(q + 43 + l, &mem);
+    if (!lm || 43ull + l + lm > n - i) return false;
+    sink.add_begin();
+    sink.add_dot(i + 19, ctr);
+    sink.add_member(mem);
+    sink.add_end();
+    i += 43 + l + lm;
+    return true;
+  }
+  if (v.w[0] == 0x6d52a281u && v.w[1] == 0x6c63a582u && v.w[2] == 0x816b636fu &&
+      v.w[3] == 0x746f64a4u && v.w[4] == 0x10c48173u) {  // Rm with a one-entry clock
+    ctr = v.uint_at(36, &l);
+    if (!l) return false;
+    lm = fast_members1(q + 36 + l, &mem);
+    if (!lm || 36ull + l + lm > n - i) return false;
+    sink.rm_begin();
+    sink.rm_dot(i + 20, ctr);
+    sink.rm_member(mem);
+    sink.rm_end();
+    i += 36 + l + lm;
+    return true;
+  }
+  return false;
+}
+
+template <typename S>
+__device__ int parse_orswot_fast(const uint8_t* p, uint64_t n, S& sink) {
+  Rd r{p, n, 0};
+  uint64_t cnt;
+  if (r.n == 0 || !is_array_marker(p[0]) || !rd_array_hdr(r, &cnt) || cnt > r.n) return kDsErr;
+  for (uint64_t k = 0; k < cnt; k++) {
+    if (fast_orswot_op(p, n, r.i, sink)) continue;
+    const int s = ds_orswot_op(r, sink);
+    if (s != kDsOk) return s;
+  }
+  return kDsOk;
+}
+
 template <typename S>
 __device__ int parse_file(int kind, const uint8_t* p, uint64_t n, S& sink) {
-  return kind == kDsOrswot ? ds_parse_orswot_ops(p, n, sink) : ds_parse_mvreg_ops(p, n, sink);
+  return kind == kDsOrswot ? parse_orswot_fast(p, n, sink) : ds_parse_mvreg_ops(p, n, sink);
 }
 
 __global__ void __launch_bounds__(kBlock) k_ds_count(DsDecodeArgs a) {

@@ -126,37 +126,44 @@ CE_HD int ds_struct2(R& r, const char* const (&names)[2], F&& fn) {
 //   add_begin(); add_dot(actor_off, counter); add_member(m); add_end();
 //   rm_begin();  rm_dot(actor_off, counter);  rm_member(m);  rm_end();
 // Fields may come in any order (struct maps), so a sink must not assume dot-before-members.
-template <typename S, typename R = Rd>
-CE_HD int ds_parse_orswot_ops(const uint8_t* p, uint64_t n, S& sink) {
+// One orswot::Op at r.i (the element grammar of the Vec below).
+template <typename R, typename S>
+CE_HD int ds_orswot_op(R& r, S& sink) {
   static constexpr const char* kV[2] = {"Add", "Rm"};
   static constexpr const char* kAdd[2] = {"dot", "members"};
   static constexpr const char* kRm[2] = {"clock", "members"};
+  const int v = ds_variant<2>(r, kV);
+  if (v < 0) return kDsErr;
+  int s;
+  if (v == 0) {
+    sink.add_begin();
+    s = ds_struct2(r, kAdd, [&](int f, R& q) -> int {
+      if (f == 1) return ds_members(q, [&](uint64_t m) { sink.add_member(m); });
+      uint64_t aoff, c;
+      const int d = parse_dot(q, &aoff, &c);
+      if (d <= 0) return d == 0 ? kDsErr : kDsHost;
+      sink.add_dot(aoff, c);
+      return kDsOk;
+    });
+    if (s == kDsOk) sink.add_end();
+  } else {
+    sink.rm_begin();
+    s = ds_struct2(r, kRm, [&](int f, R& q) -> int {
+      if (f == 1) return ds_members(q, [&](uint64_t m) { sink.rm_member(m); });
+      return ds_vclock(q, [&](uint64_t off, uint64_t c) { sink.rm_dot(off, c); });
+    });
+    if (s == kDsOk) sink.rm_end();
+  }
+  return s;
+}
+
+template <typename S, typename R = Rd>
+CE_HD int ds_parse_orswot_ops(const uint8_t* p, uint64_t n, S& sink) {
   R r{p, n, 0};
   uint64_t cnt;
   if (r.n == 0 || !is_array_marker(rb(r, 0)) || !rd_array_hdr(r, &cnt) || cnt > r.n) return kDsErr;
   for (uint64_t k = 0; k < cnt; k++) {
-    const int v = ds_variant<2>(r, kV);
-    if (v < 0) return kDsErr;
-    int s;
-    if (v == 0) {
-      sink.add_begin();
-      s = ds_struct2(r, kAdd, [&](int f, R& q) -> int {
-        if (f == 1) return ds_members(q, [&](uint64_t m) { sink.add_member(m); });
-        uint64_t aoff, c;
-        const int d = parse_dot(q, &aoff, &c);
-        if (d <= 0) return d == 0 ? kDsErr : kDsHost;
-        sink.add_dot(aoff, c);
-        return kDsOk;
-      });
-      if (s == kDsOk) sink.add_end();
-    } else {
-      sink.rm_begin();
-      s = ds_struct2(r, kRm, [&](int f, R& q) -> int {
-        if (f == 1) return ds_members(q, [&](uint64_t m) { sink.rm_member(m); });
-        return ds_vclock(q, [&](uint64_t off, uint64_t c) { sink.rm_dot(off, c); });
-      });
-      if (s == kDsOk) sink.rm_end();
-    }
+    const int s = ds_orswot_op(r, sink);
     if (s != kDsOk) return s;
   }
   return kDsOk;  // rmp_serde::from_slice does not look past the value (as ce_fused's Vec<Dot>)

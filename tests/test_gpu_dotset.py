@@ -447,3 +447,69 @@ def test_ingest_states_iov_matches_blob(ctx):
     assert a.state_bytes() == b.state_bytes()
     a.close()
     b.close()
+
+
+def _u(x, w):
+    """msgpack uint in a chosen width (rmp-serde's reader accepts every one of them)"""
+    if w == "fix":
+        return bytes([x])
+    if w == "d2":  # signed int32 marker, non-negative value (the serde u64 visitor accepts it)
+        return b"\xd2" + x.to_bytes(4, "big", signed=True)
+    n = {"cc": 1, "cd": 2, "ce": 4, "cf": 8}[w]
+    return bytes([{"cc": 0xcc, "cd": 0xcd, "ce": 0xce, "cf": 0xcf}[w]]) + x.to_bytes(n, "big")
+
+
+def _arr(n):
+    return bytes([0x90 | n]) if n < 16 else b"\xdc" + n.to_bytes(2, "big")
+
+
+def _add(actor, ctr, members, cw, mw):
+    return (b"\x81\xa3Add\x82\xa3dot\x82\xa5actor\xc4\x10" + actor + b"\xa7counter" + _u(ctr, cw) +
+            b"\xa7members" + _arr(len(members)) + b"".join(_u(m, mw) for m in members))
+
+
+def _rm(clock, members, cw, mw):
+    return (b"\x81\xa2Rm\x82\xa5clock\x81\xa4dots" + bytes([0x80 | len(clock)]) +
+            b"".join(b"\xc4\x10" + a + _u(c, cw) for a, c in clock) +
+            b"\xa7members" + _arr(len(members)) + b"".join(_u(m, mw) for m in members))
+
+
+@pytest.mark.parametrize("case", ["widths", "mixed_fallback", "truncated_tail", "near_template"])
+def test_orswot_op_fast_path_boundaries(ctx, case):
+    """The device op decode proves canonical one-member Add / one-entry-clock Rm ops from register
+    windows (ce_dotset.hip fast_orswot_op) and hands every other form to the grammar from the
+    same op on: each uint width, multi-member / multi-entry ops between fast ones, a signed
+    marker, a field-name near miss and a file cut inside its last op -- all == oracle."""
+    rng = random.Random(hash(case) & 0xffff)
+    key = rng.randbytes(32)
+    actors = sorted(rng.randbytes(16) for _ in range(3))
+    widths = ["fix", "cc", "cd", "ce", "cf"]
+    clears, fa, fv = [], [], []
+    for a in range(3):
+        for v in range(4):
+            ops = []
+            base = 64 * v + 1
+            for j in range(10):
+                cw, mw = widths[(j + v) % 5], widths[(j + a) % 5]
+                ctr = base + j if cw != "fix" else min(base + j, 127)
+                lim = {"fix": 128, "cc": 256, "cd": 65536, "ce": 1 << 32, "cf": 1 << 64}
+                mem = rng.randrange(0, lim[mw])
+                if case == "widths" or j % 3:
+                    ops.append(_add(actors[a], ctr, [mem], cw, mw))
+                elif case == "mixed_fallback":
+                    ops.append(_add(actors[a], ctr, [1, 2, 3], cw, "cd") if j % 2 else
+                               _rm([(actors[0], 5), (actors[2], 9)], [4], "cc", "fix"))
+                    ops.append(_add(actors[a], 2000 + ctr, [7], "d2", "cc"))
+                else:
+                    ops.append(_rm([(actors[(a + j) % 3], base)], [mem % 50], "cc" if cw == "fix" else cw, "cd"))
+            if case == "near_template" and v == 2:
+                ops[4] = ops[4].replace(b"members", b"membres", 1)  # unknown field -> members missing
+            body = _arr(len(ops)) + b"".join(ops)
+            if case == "truncated_tail" and a == 1 and v == 3:
+                body = body[:-3]
+            clears.append(APP + body)
+            fa.append(a)
+            fv.append(v)
+    core, oc = new_core(ctx, "orswot", key), C.Core("orswot")
+    check_ops(ctx, "orswot", key, core, oc, actors, clears, fa, fv)
+    core.close()
