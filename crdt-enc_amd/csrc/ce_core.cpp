@@ -226,6 +226,11 @@ int32_t normalize_envelope(const uint8_t* enc, size_t len, std::vector<uint8_t>*
 // ---------------------------------------------------------------------------------------
 // actor table
 // ---------------------------------------------------------------------------------------
+// The actor table is kept at most 1/4 full: linear probing then averages ~1.17 probes per
+// successful lookup (1.5 at 1/2), and every probe of a device lookup is a dependent L2 load --
+// C2 variant B resolves one per Dot.
+static constexpr uint64_t kTableLoadInv = 4;
+
 uint32_t probe_slot(const std::vector<ActorSlot>& t, uint32_t mask, const Uuid& u, bool* found) {
   uint32_t w[4];
   std::memcpy(w, u.data(), 16);
@@ -235,6 +240,14 @@ uint32_t probe_slot(const std::vector<ActorSlot>& t, uint32_t mask, const Uuid& 
     if (std::memcmp(t[h].k, w, 16) == 0) { *found = true; return h; }
     h = (h + 1) & mask;
   }
+}
+
+// DecodeArgs.nil_actor: whether the device lookups must take the two-load probe (the nil UUID
+// is the one used key that reads like an empty slot, ce_device.h lookup_slot1)
+static int table_has_nil(ce_core* c) {
+  bool found = false;
+  (void)probe_slot(c->h_table, c->cap - 1, Uuid{}, &found);
+  return found ? 1 : 0;
 }
 
 int table_init(ce_core* c, uint32_t cap) {
@@ -317,7 +330,7 @@ int table_grow(ce_core* c) {
 int insert_actor(ce_core* c, const Uuid& u, uint32_t* slot) {
   auto it = c->slot_of.find(u);
   if (it != c->slot_of.end()) { *slot = it->second; return CE_OK; }
-  if ((c->size + 1) * 2 > c->cap) {
+  if ((c->size + 1) * kTableLoadInv > c->cap) {
     int rc = table_grow(c);
     if (rc) return rc;
   }
@@ -550,6 +563,7 @@ int decode_only_resolving(ce_core* c, DecodeArgs& da, uint32_t n, uint8_t* d_mas
     da.large_only = 0;
     da.table = c->d_table.as<ActorSlot>();
     da.mask = c->cap - 1;
+    da.nil_actor = table_has_nil(c);
     da.batch = c->d_batch.as<unsigned long long>();
     if ((e = hipMemsetAsync(ctx->counters.as<uint32_t>() + 4, 0, 4, ctx->stream)) ||
         (e = hipMemsetAsync(ctx->refold.p, 0, n, ctx->stream)) ||
@@ -724,6 +738,7 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
   da.refold = ctx->refold.as<uint8_t>();
   da.table = c->d_table.as<ActorSlot>();
   da.mask = c->cap - 1;
+  da.nil_actor = table_has_nil(c);
   da.batch = c->d_batch.as<unsigned long long>();
   da.large_list = ctx->large.as<uint32_t>();
 #if CE_FUSED_DIAG  // diagnostics build (make prof -> libcrdtenc_prof.so)
@@ -915,6 +930,7 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
     }
     da.table = c->d_table.as<ActorSlot>();
     da.mask = c->cap - 1;
+    da.nil_actor = table_has_nil(c);
     da.batch = c->d_batch.as<unsigned long long>();
     if ((rc = run_fold(c->d_refold2.as<uint8_t>()))) return rc;
     if ((e = hipMemcpyAsync(hc, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->stream)) ||
@@ -1782,7 +1798,7 @@ int ce_core_register_actors(ce_core* c, const uint8_t* actors, uint32_t m) {
   if (!c || (m && !actors)) return CE_ERR_INVALID_ARG;
   std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
   if (c->registered != c->size) return CE_ERR_INVALID_ARG;
-  while ((c->size + m) * 2 > c->cap) {
+  while ((c->size + m) * kTableLoadInv > c->cap) {
     int rc = table_grow(c);
     if (rc) return rc;
   }

@@ -362,6 +362,24 @@ __device__ __forceinline__ uint32_t lookup_slot(const ActorSlot* __restrict__ ta
   return 0xffffffffu;
 }
 
+// lookup_slot with one 16-byte load per probe: an empty slot's key is all zero (ActorSlot{}), and
+// a used slot's key is zero only for the nil UUID, so the key alone decides unless the nil UUID
+// is the key looked up or is in the table (nil_in_table: the host's probe at launch time).  C2
+// variant B (a lookup per Dot) spends its time in these L2 requests.
+__device__ __forceinline__ uint32_t lookup_slot1(const ActorSlot* __restrict__ tab, uint32_t mask,
+                                                 int nil_in_table, uint32_t k0, uint32_t k1,
+                                                 uint32_t k2, uint32_t k3) {
+  if (nil_in_table || (k0 | k1 | k2 | k3) == 0) return lookup_slot(tab, mask, k0, k1, k2, k3);
+  uint32_t h = actor_hash(k0, k1, k2, k3) & mask;
+  for (uint32_t probe = 0; probe <= mask; probe++) {
+    const uint4 a = *reinterpret_cast<const uint4*>(tab[h].k);
+    if (a.x == k0 && a.y == k1 && a.z == k2 && a.w == k3) return h;
+    if ((a.x | a.y | a.z | a.w) == 0) return 0xffffffffu;
+    h = (h + 1) & mask;
+  }
+  return 0xffffffffu;
+}
+
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
 // bytes [b, b+4) of a 48-byte window held as 12 LE words (b compile-time)

@@ -258,7 +258,7 @@ __device__ __forceinline__ void decode_fold(const DecodeArgs& a, const SupVers& 
       slot = actor_hash(k0, k1, k2, k3) & a.mask;
       remember(slot, k0, k1, k2, k3);
     } else {
-      slot = lookup_slot(a.table, a.mask, k0, k1, k2, k3);
+      slot = lookup_slot1(a.table, a.mask, a.nil_actor, k0, k1, k2, k3);
       remember(slot, k0, k1, k2, k3);
     }
     fold_slot(slot, k0, k1, k2, k3, ctr);

@@ -111,6 +111,8 @@ struct DecodeArgs {
   const uint32_t* large_list;
   const uint8_t* blob;          // fused kernel: input files (ciphertext at FileParams.in_off)
   uint8_t* redo;                // k_segdec_apply: files left to the whole-file decode
+  int nil_actor;                // the nil UUID is in the actor table: lookups take the two-load
+                                // probe (lookup_slot1)
 };
 hipError_t launch_decode_dots(hipStream_t s, const DecodeArgs& a, uint32_t grid_waves);
 

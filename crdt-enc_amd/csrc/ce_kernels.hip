@@ -198,7 +198,7 @@ struct SlotCache {
   uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, slot = 0xffffffffu;
   __device__ __forceinline__ uint32_t get(const DecodeArgs& a, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
     if (slot != 0xffffffffu && k0 == c0 && k1 == c1 && k2 == c2 && k3 == c3) return slot;
-    const uint32_t s = lookup_slot(a.table, a.mask, k0, k1, k2, k3);
+    const uint32_t s = lookup_slot1(a.table, a.mask, a.nil_actor, k0, k1, k2, k3);
     if (s != 0xffffffffu) { c0 = k0; c1 = k1; c2 = k2; c3 = k3; slot = s; }
     return s;
   }
@@ -583,7 +583,7 @@ __device__ void decode_file(const DecodeArgs& a, uint32_t f, uint32_t lane) {
       uint32_t slot;
       if (cslot != 0xffffffffu && k0 == c0 && k1 == c1 && k2 == c2 && k3 == c3) slot = cslot;
       else {
-        slot = lookup_slot(a.table, a.mask, k0, k1, k2, k3);
+        slot = lookup_slot1(a.table, a.mask, a.nil_actor, k0, k1, k2, k3);
         if (slot != 0xffffffffu) { c0 = k0; c1 = k1; c2 = k2; c3 = k3; cslot = slot; }
       }
       if (slot == 0xffffffffu) {
@@ -805,7 +805,7 @@ __global__ __launch_bounds__(256) void k_decode_split(DecodeArgs a, SplitScratch
         uint32_t slot;
         if (cslot != 0xffffffffu && k0 == c0 && k1 == c1 && k2 == c2 && k3 == c3) slot = cslot;
         else {
-          slot = lookup_slot(a.table, a.mask, k0, k1, k2, k3);
+          slot = lookup_slot1(a.table, a.mask, a.nil_actor, k0, k1, k2, k3);
           c0 = k0; c1 = k1; c2 = k2; c3 = k3; cslot = slot;
         }
         if (slot == 0xffffffffu || (myslot != 0xffffffffu && slot != myslot)) fail = true;

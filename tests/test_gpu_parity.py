@@ -912,3 +912,35 @@ def test_host_iov_ingest_matches_device(ctx, oracle):
         c2.close()
     finally:
         del os.environ["CE_UPLOAD_CHUNK"]
+
+
+@pytest.mark.parametrize("nil_where", ["writer", "dot_only", "absent"])
+def test_nil_uuid_actor_lookups(ctx, oracle, nil_where):
+    """The device actor lookup reads only the 16-byte key per probe (an empty slot is all zero,
+    ce_device.h lookup_slot1); the nil UUID is the one actor whose key looks empty, so with it in
+    the table (or looked up) the two-load probe is used.  Stress Dots over a pool that holds the
+    nil UUID as a writer, as a Dot actor only (a table miss, inserted and refolded), or not at
+    all -- state == oracle in each case."""
+    key = os.urandom(32)
+    rng = random.Random({"writer": 1, "dot_only": 2, "absent": 3}[nil_where])
+    writers = sorted(rng.randbytes(16) for _ in range(12))
+    if nil_where == "writer":
+        writers[0] = bytes(16)
+    pool = writers + ([bytes(16)] if nil_where == "dot_only" else [])
+    clears, fa, vers = [], [], []
+    for a in range(len(writers)):
+        for v in range(6):
+            dots = [{"actor": rng.choice(pool), "counter": rng.getrandbits(rng.choice([7, 16, 32, 64]))}
+                    for _ in range(60)]
+            clears.append(APP + msgpack.packb(dots, use_bin_type=True))
+            fa.append(a)
+            vers.append(v)
+    files = [CORE + e for e in ctx.encrypt_batch(key, clears)]
+    core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+    core.set_latest_key(key)
+    rc, st = core.ingest_ops(files, writers, fa, vers)
+    oc = oracle.Core()
+    orc, ost = oc.read_remote_ops(key, [APP], files, [writers[i] for i in fa], vers)
+    assert (rc, list(st)) == (orc, list(ost)) and rc == 0
+    assert core.state_bytes() == oc.serialize()
+    core.close()
