@@ -360,15 +360,28 @@ int download_state(ce_core* c, std::vector<uint64_t>* st) {
 }
 
 // max-merge host dots into the device state (VClock::merge / apply)
+// slots of m actors (16 bytes each) after a table growth moved the ones handed out before it
+void refresh_slots(ce_core* c, const uint8_t* actors, uint32_t m, std::vector<uint32_t>* slots) {
+  for (uint32_t a = 0; a < m; a++) {
+    Uuid u;
+    std::memcpy(u.data(), actors + 16ull * a, 16);
+    (*slots)[a] = c->slot_of.at(u);
+  }
+}
+
 int merge_dots_host(ce_core* c, const Dots& dots) {
   if (dots.empty()) return CE_OK;
   std::vector<std::pair<uint32_t, uint64_t>> sv;
+  const uint64_t gen0 = c->table_gen;
   for (auto& d : dots) {
     uint32_t s;
     int rc = insert_actor(c, d.first, &s);
     if (rc) return rc;
     sv.push_back({s, d.second});
   }
+  // a growth during the loop moved every slot handed out before it
+  if (c->table_gen != gen0)
+    for (size_t i = 0; i < dots.size(); i++) sv[i].first = c->slot_of.at(dots[i].first);
   std::vector<uint64_t> dense(c->cap, 0);
   for (auto& p : sv) dense[p.first] = std::max(dense[p.first], p.second);
   hipError_t e;
@@ -652,12 +665,14 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
     wslot = c->last_wslot;
   } else {
     wslot.resize(m);
+    const uint64_t gen0 = c->table_gen;
     for (uint32_t a = 0; a < m; a++) {
       Uuid u;
       std::memcpy(u.data(), actors + 16ull * a, 16);
       int rc = insert_actor(c, u, &wslot[a]);
       if (rc) return rc;
     }
+    if (c->table_gen != gen0) refresh_slots(c, actors, m, &wslot);  // a growth moved them
     c->last_writers.assign(actors, actors + 16ull * m);
     c->last_wslot = wslot;
     c->last_writers_gen = c->table_gen;

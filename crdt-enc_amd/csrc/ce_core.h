@@ -157,6 +157,8 @@ bool read_struct(Rd& r, const std::vector<const char*>& names,
                  const std::function<bool(int, Rd&)>& cb);
 bool read_vclock(Rd& r, Dots* out);
 int insert_actor(ce_core* c, const Uuid& u, uint32_t* slot);
+// slots of m actors (16 bytes each) after a table growth moved the ones handed out before it
+void refresh_slots(ce_core* c, const uint8_t* actors, uint32_t m, std::vector<uint32_t>* slots);
 inline uint32_t actor_id_of_slot(const ce_core* c, uint32_t slot) { return c->h_table[slot].pad[0]; }
 int table_upload(ce_core* c);
 KeyRef key_of(ce_core* c);

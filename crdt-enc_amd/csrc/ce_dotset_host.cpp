@@ -814,11 +814,13 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
   int rc;
   // writers get actor ids first (the gate is keyed by them)
   std::vector<uint32_t> wslot(m);
+  const uint64_t gen0 = c->table_gen;
   for (uint32_t a = 0; a < m; a++) {
     Uuid u;
     std::memcpy(u.data(), actors + 16ull * a, 16);
     if ((rc = insert_actor(c, u, &wslot[a]))) return rc;
   }
+  if (c->table_gen != gen0) refresh_slots(c, actors, m, &wslot);  // a growth moved them
   if ((rc = table_upload(c)) || (rc = ensure_supported(c))) return rc;
   if ((e = ctx->out.reserve(blob_len + 16ull * n + 128)) || (e = ctx->status.reserve(n * 4ull + 64)) ||
       (e = d->cnt.reserve(2ull * kCntN * n * 4 + 64)))

@@ -944,3 +944,39 @@ def test_nil_uuid_actor_lookups(ctx, oracle, nil_where):
     assert (rc, list(st)) == (orc, list(ost)) and rc == 0
     assert core.state_bytes() == oc.serialize()
     core.close()
+
+
+@pytest.mark.parametrize("kind", [crdtenc.STATE_GCOUNTER, crdtenc.STATE_ORSWOT])
+def test_table_growth_inside_one_call(ctx, oracle, kind):
+    """More new writers in one ingest (and more actors in one merged state) than the actor table
+    holds before it grows: slots handed out before a growth move with it (refresh_slots), so the
+    version gate and the merged clock still land on the right actors."""
+    key = os.urandom(32)
+    if kind == crdtenc.STATE_GCOUNTER:
+        files, actors, fa, vers = make_ops_batch(ctx, key, 5000, 1, 3, seed=77)
+        core = crdtenc.Core(ctx, kind=kind, supported=[APP], current_data_version=APP)
+        core.set_latest_key(key)
+        rc, st = core.ingest_ops(files, actors, fa, vers)
+        oc = oracle.Core()
+        orc, ost = oc.read_remote_ops(key, [APP], files, [actors[i] for i in fa], vers)
+        assert (rc, list(st)) == (orc, list(ost)) and rc == 0
+        assert core.state_bytes() == oc.serialize()
+        core.close()
+        return
+    # Orswot: a state whose clock names 5000 actors, merged into a fresh core
+    rng = random.Random(5)
+    actors = sorted(rng.randbytes(16) for _ in range(5000))
+    clock = {a: rng.randrange(1, 1 << 20) for a in actors}
+    sw = {"next_op_versions": {"dots": dict(sorted((a, 1) for a in actors[:3000]))},
+          "state": {"clock": {"dots": dict(sorted(clock.items()))}, "entries": {}, "deferred": {}}}
+    want = msgpack.packb(sw, use_bin_type=True)
+    core = crdtenc.Core(ctx, kind=kind, supported=[APP], current_data_version=APP)
+    core.set_latest_key(key)
+    assert core.merge_state(want) == 0
+    from oracle import crdts as C
+    oc = C.Core("orswot")
+    nov, st = C.dec_state("orswot", want)
+    oc.state.merge(st)
+    oc.nov.merge(nov)
+    assert core.state_bytes() == oc.serialize()
+    core.close()
