@@ -1267,6 +1267,13 @@ hipError_t dl(void* dst, const void* src, size_t n, hipStream_t s) {
   return e ? e : hipStreamSynchronize(s);
 }
 
+// the repeat-check set of a file with n entries: a power of two >= 2 n words (mask = size - 1)
+uint32_t dset_mask_for(uint64_t n) {
+  uint64_t p = 64;
+  while (p < 2 * n) p <<= 1;
+  return (uint32_t)(p - 1);
+}
+
 OrswotReadArgs read_args(ce_core* c, DsState* d, size_t f, const DevState& ds, const uint8_t* out,
                          uint32_t cap) {
   OrswotReadArgs a{};
@@ -1285,6 +1292,7 @@ OrswotReadArgs read_args(ce_core* c, DsState* d, size_t f, const DevState& ds, c
   a.dbase = b[4].as<uint32_t>();
   a.member = b[5].as<unsigned long long>();
   a.msort = b[6].as<unsigned long long>();
+  a.dset_mask = dset_mask_for(ds.n_entries);
   a.table = c->d_table.as<ActorSlot>();
   a.mask = c->cap - 1;
   return a;
@@ -1309,7 +1317,8 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
   int rc;
   if (d->rd.size() < n) d->rd.resize(n);
   // pinned words: [0, 2n) candidate counts / flags, [2n, 6n) entry tails, [6n, 10n) live counts
-  if ((e = d->rd_misc.reserve(8ull * n + 64)) || (e = d->rd_small.reserve(40ull * n + 64)) ||
+  // device words: [0, 2n) candidate counts / flags, [2n, 6n) entry tails (k_rd_tail)
+  if ((e = d->rd_misc.reserve(24ull * n + 64)) || (e = d->rd_small.reserve(40ull * n + 64)) ||
       (e = hipMemsetAsync(d->rd_misc.p, 0, 8ull * n, s)))
     return ctx->hip_fail(e, "state reader");
   uint32_t* small = d->rd_small.as<uint32_t>();
@@ -1388,7 +1397,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
       if ((e = b[0].reserve(4ull * x.cap + 64)) || (e = b[1].reserve(4ull * x.cap + 64)) ||
           (e = b[2].reserve(4ull * ne + 64)) || (e = b[3].reserve(4ull * ne + 64)) ||
           (e = b[4].reserve(4ull * ne + 64)) || (e = b[5].reserve(8ull * ne + 64)) ||
-          (e = b[6].reserve(8ull * ne + 64)))
+          (e = b[6].reserve(8ull * (dset_mask_for(ne) + 2) + 64)))
         return ctx->hip_fail(e, "state reader");
       tmp_need = std::max(tmp_need, orswot_read_tmp_bytes(x.cap));
     }
@@ -1417,17 +1426,14 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
       size_t tb = d->rd_tmp.cap;
       if ((e = hipcub_sort_u32(d->rd_tmp.p, tb, a.cand_raw, a.cand, found[i], s)))
         return ctx->hip_fail(e, "state reader");
-      uint32_t* tail = small + 2 * n + 4 * i;
-      const uint32_t ne = x.n_entries;
-      if ((e = launch_orswot_read(s, a, d->rd_tmp.p, d->rd_tmp.cap, 1)) ||
-          (e = hipMemcpyAsync(tail, a.end + ne - 1, 4, hipMemcpyDeviceToHost, s)) ||
-          (e = hipMemcpyAsync(tail + 1, a.dbase + ne - 1, 4, hipMemcpyDeviceToHost, s)) ||
-          (e = hipMemcpyAsync(tail + 2, a.ndots + ne - 1, 4, hipMemcpyDeviceToHost, s)) ||
-          (e = hipMemcpyAsync(tail + 3, a.flags, 4, hipMemcpyDeviceToHost, s)))
-        return ctx->hip_fail(e, "state reader");
+      a.tail_out = d->rd_misc.as<uint32_t>() + 2 * n + 4 * i;
+      if ((e = launch_orswot_read(s, a, d->rd_tmp.p, d->rd_tmp.cap, 1))) return ctx->hip_fail(e, "state reader");
       dev2.push_back(i);
     }
-    if (!dev2.empty() && (rc = sync("state reader"))) return rc;
+    // every file's tail words in one download
+    if (!dev2.empty() && ((e = hipMemcpyAsync(small + 2 * n, d->rd_misc.as<uint32_t>() + 2 * n, 16ull * n,
+                                              hipMemcpyDeviceToHost, s)) ||
+                          (rc = sync("state reader")))) return rc ? rc : ctx->hip_fail(e, "state reader");
     // 4) the deferred maps after the entries, on the host
     ph = std::make_unique<HostPhase>("  rd: tails");
     std::vector<uint64_t> toff(n + 1, 0), eend(n, 0);

@@ -62,7 +62,10 @@ struct OrswotReadArgs {
   uint32_t* ndots;      // non-zero Dots per entry
   uint32_t* dbase;      // exclusive scan of ndots
   unsigned long long* member;  // per entry
-  unsigned long long* msort;   // members sorted (repeat check)
+  unsigned long long* msort;   // repeat check: open-addressing set of the members, dset_mask + 2
+                               // words (all ones = empty; the last word counts all-ones members)
+  uint32_t dset_mask;          // power of two minus one, >= 2 n_cand - 1
+  uint32_t* tail_out;          // stage 1: end, dbase, ndots of the last entry and the flags word
   uint32_t* flags;      // 1 non-canonical entry, 2 broken chain, 4 unknown actor, 8 repeated member
   const ActorSlot* table;
   uint32_t mask;

@@ -280,10 +280,44 @@ __global__ void k_rd_chain(OrswotReadArgs a) {
 }
 
 // HashMap<M, VClock> keeps a repeated member's later clock: a file with repeated members goes to
-// the host parser (flag 8), found on the sorted member keys
-__global__ void k_rd_dups(const unsigned long long* msort, uint32_t* flags, uint32_t n) {
-  for (uint32_t i = 1 + blockIdx.x * kB + threadIdx.x; i < n; i += gridDim.x * kB)
-    if (msort[i] == msort[i - 1]) atomicOr(flags, 8u);
+// the host parser (flag 8).  Found by inserting every member into an open-addressing set
+// (atomicCAS on the all-ones empty word; all-ones members are counted in the word after the
+// set): one launch where a 64-bit radix sort + neighbour compare took a dozen.
+__device__ __forceinline__ uint32_t mix_member(unsigned long long x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+
+__global__ void k_rd_dups_hash(const unsigned long long* member, unsigned long long* set, uint32_t mask,
+                               uint32_t* flags, uint32_t n) {
+  constexpr unsigned long long kEmpty = ~0ull;
+  for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < n; i += gridDim.x * kB) {
+    const unsigned long long m = member[i];
+    if (m == kEmpty) {
+      if (atomicAdd(&set[(size_t)mask + 1], 1ull) != kEmpty) atomicOr(flags, 8u);  // second one
+      continue;
+    }
+    uint32_t h = mix_member(m) & mask;
+    for (uint32_t probe = 0; probe <= mask; probe++) {
+      const unsigned long long old = atomicCAS(&set[h], kEmpty, m);
+      if (old == kEmpty) break;
+      if (old == m) { atomicOr(flags, 8u); break; }
+      h = (h + 1) & mask;
+    }
+  }
+}
+
+// the last entry's end / Dot base / Dot count and the flags word, for one download of all files
+__global__ void k_rd_tail(OrswotReadArgs a) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const uint32_t l = a.n_cand - 1;
+    a.tail_out[0] = a.end[l];
+    a.tail_out[1] = a.dbase[l];
+    a.tail_out[2] = a.ndots[l];
+    a.tail_out[3] = *a.flags;
+  }
 }
 
 // lane per entry: its non-zero Dots -> (member, actor id, counter) at its exclusive-scan base;
@@ -403,11 +437,12 @@ hipError_t launch_orswot_read(hipStream_t s, OrswotReadArgs a, void* tmp, size_t
     if (a.n_cand) {
       hipLaunchKernelGGL(k_rd_entry, dim3(nblk(a.n_cand)), dim3(kB), 0, s, a);
       hipLaunchKernelGGL(k_rd_chain, dim3(nblk(a.n_cand)), dim3(kB), 0, s, a);
-      tb = tmp_bytes;
-      if ((e = hipcub::DeviceRadixSort::SortKeys(tmp, tb, a.member, a.msort, (int)a.n_cand, 0, 64, s))) return e;
-      hipLaunchKernelGGL(k_rd_dups, dim3(nblk(a.n_cand)), dim3(kB), 0, s, a.msort, a.flags, a.n_cand);
+      if ((e = hipMemsetAsync(a.msort, 0xff, 8ull * ((size_t)a.dset_mask + 2), s))) return e;
+      hipLaunchKernelGGL(k_rd_dups_hash, dim3(nblk(a.n_cand)), dim3(kB), 0, s, a.member, a.msort, a.dset_mask,
+                         a.flags, a.n_cand);
       tb = tmp_bytes;
       if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, a.ndots, a.dbase, (int)a.n_cand, s))) return e;
+      if (a.tail_out) hipLaunchKernelGGL(k_rd_tail, dim3(1), dim3(64), 0, s, a);
     }
     return hipGetLastError();
   }

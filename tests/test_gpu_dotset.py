@@ -299,6 +299,10 @@ def _orswot_state_forms(sw, rng):
         out.append(("repeated_member", enc(dup), False))
         out.append(("long_uint_member", enc(list(entries), member_enc=lambda m: b"\xcf" + m.to_bytes(8, "big")), False))
         out.append(("descending_dots", enc(list(entries), vclock_enc=lambda vc: _vclock_bytes(vc, reverse=True)), False))
+        # the all-ones member is the repeat check's empty word: once (device) and repeated (host)
+        top = (1 << 64) - 1
+        out.append(("all_ones_member", enc([(top, entries[0][1])] + list(entries[1:])), True))
+        out.append(("repeated_all_ones_member", enc([(top, entries[0][1]), (top, entries[1][1])] + list(entries[2:])), False))
     return out
 
 
