@@ -980,3 +980,22 @@ def test_table_growth_inside_one_call(ctx, oracle, kind):
     oc.nov.merge(nov)
     assert core.state_bytes() == oc.serialize()
     core.close()
+
+
+@pytest.mark.parametrize("size", [(1 << 20) + 17, (5 << 20) + 1000, 35_000_000])
+def test_many_segment_files_seal_and_open(ctx, oracle, size):
+    """Files of more than 64 Poly1305 segments (16 KiB each): k_finalize_multi runs one Horner
+    chain per lane over segments j = lane, lane + 64, ... in r^(64 S), the last segment apart.
+    Seal == the oracle's (OpenSSL ChaCha20 + a reference Poly1305) byte for byte; open returns the
+    plaintext, and a flipped ciphertext bit is rejected with the plaintext scrubbed."""
+    rng = random.Random(size)
+    key, nonce = rng.randbytes(32), rng.randbytes(24)
+    pt = rng.randbytes(size)
+    enc = ctx.encrypt(key, pt, nonce=nonce)
+    st, want = oracle.cryptor_encrypt(key, nonce, pt)
+    assert st == 0 and enc == want
+    b = bytearray(enc)
+    b[len(b) // 2] ^= 0x10
+    rc, sts, pts, raw, offs = ctx.decrypt_batch(key, [enc, bytes(b)])
+    assert list(sts) == [0, 9] and pts[0] == pt
+    assert raw[offs[1]:offs[1] + size] == bytes(size)
