@@ -321,18 +321,37 @@ __device__ __forceinline__ void key_schedule(const DevKey& key, const uint8_t* n
   key_schedule_w(key, nw, P);
 }
 
-__device__ __forceinline__ void reserve_segments(FileParams& P, uint32_t f, SegScratch sc) {
+// Segment bookkeeping of a file (lane per file).  Every lane of the wave calls it, `mine` =
+// the lane holds a file to set up (the others only help): a file's (file, segment) work items go
+// to extra_list, up to 32 by its own lane, longer runs (a 35 MB compaction has 2,200) by the
+// whole wave, one file at a time.
+__device__ __forceinline__ void reserve_segments(FileParams& P, uint32_t f, SegScratch sc, bool mine = true) {
   const uint64_t nblk = ((uint64_t)P.len + 15) / 16 + 1;
-  const uint32_t nseg = (uint32_t)((nblk + kSegBlocks - 1) / kSegBlocks);
-  P.nseg = nseg;
-  P.extra_base = 0;
+  const uint32_t nseg = mine ? (uint32_t)((nblk + kSegBlocks - 1) / kSegBlocks) : 0u;
+  if (mine) {
+    P.nseg = nseg;
+    P.extra_base = 0;
+  }
+  uint32_t e = 0;
   if (nseg > 1) {
-    const uint32_t e = atomicAdd(&sc.counters[0], nseg - 1);
+    e = atomicAdd(&sc.counters[0], nseg - 1);
     const uint32_t pb = atomicAdd(&sc.counters[6], nseg);
     const uint32_t mf = atomicAdd(&sc.counters[1], 1u);
     P.extra_base = pb;
     sc.multi_files[mf] = f;
-    for (uint32_t j = 1; j < nseg; j++) sc.extra_list[e + j - 1] = make_uint2(f, j);
+    if (nseg <= 33)
+      for (uint32_t j = 1; j < nseg; j++) sc.extra_list[e + j - 1] = make_uint2(f, j);
+  }
+  // the lanes running here (every lane of the wave, for the callers above): rank among them
+  const unsigned long long act = __ballot(true);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t rank = (uint32_t)__builtin_popcountll(act & ((1ull << lane) - 1ull));
+  const uint32_t nact = (uint32_t)__builtin_popcountll(act);
+  for (unsigned long long big = __ballot(nseg > 33); big; big &= big - 1) {
+    const int src = (int)__builtin_ctzll(big);
+    const uint32_t fe = (uint32_t)__shfl((int)e, src), ff = (uint32_t)__shfl((int)f, src);
+    const uint32_t fn = (uint32_t)__shfl((int)nseg, src);
+    for (uint32_t j = 1 + rank; j < fn; j += nact) sc.extra_list[fe + j - 1] = make_uint2(ff, j);
   }
 }
 

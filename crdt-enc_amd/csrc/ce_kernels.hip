@@ -105,9 +105,9 @@ __global__ __launch_bounds__(256) void k_open_setup(const uint8_t* __restrict__ 
       for (int k = 0; k < 6; k++) nw[k] = ld_le32(enc + e.nonce_off + 4 * k);
     }
     key_schedule_w(key, nw, P);
-    reserve_segments(P, f, sc);
     if (P.len > kSmallMax) sc.large_list[atomicAdd(&sc.counters[9], 1u)] = f;
   }
+  reserve_segments(P, f, sc, st == CE_OK);  // the whole wave (long files are filled together)
   {
     const uint4* pv = reinterpret_cast<const uint4*>(&P);
     const uint32_t f0 = blockIdx.x * blockDim.x;
@@ -150,29 +150,32 @@ __global__ __launch_bounds__(256) void k_seal_setup(const uint8_t* __restrict__ 
                                                     DevKey key, FileParams* __restrict__ params,
                                                     SegScratch sc) {
   const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= n) return;
-  const uint64_t off = offs[f];
-  const uint64_t len = offs[f + 1] - off;
-  uint8_t* o = out + out_offs[f];
-  uint64_t k = 0;
-  if (outer_version) {
-    for (int i = 0; i < 16; i++) o[i] = outer_version[i];
-    k = 16;
-  }
-  uint8_t hdr[96];
-  const uint8_t* nonce = nonces + 24ull * f;
-  uint8_t nb[24];
-  for (int i = 0; i < 24; i++) nb[i] = nonce[i];
-  const uint64_t h = put_envelope_header(hdr, len, nb);
-  for (uint64_t i = 0; i < h; i++) o[k + i] = hdr[i];
+  const bool mine = f < n;
   FileParams P;
-  P.status = CE_OK;
-  P.in_off = off;
-  P.out_off = out_offs[f] + k + h;
-  P.len = (uint32_t)len;
-  key_schedule(key, nb, P);
-  reserve_segments(P, f, sc);
-  params[f] = P;
+  P.len = 0;
+  if (mine) {
+    const uint64_t off = offs[f];
+    const uint64_t len = offs[f + 1] - off;
+    uint8_t* o = out + out_offs[f];
+    uint64_t k = 0;
+    if (outer_version) {
+      for (int i = 0; i < 16; i++) o[i] = outer_version[i];
+      k = 16;
+    }
+    uint8_t hdr[96];
+    const uint8_t* nonce = nonces + 24ull * f;
+    uint8_t nb[24];
+    for (int i = 0; i < 24; i++) nb[i] = nonce[i];
+    const uint64_t h = put_envelope_header(hdr, len, nb);
+    for (uint64_t i = 0; i < h; i++) o[k + i] = hdr[i];
+    P.status = CE_OK;
+    P.in_off = off;
+    P.out_off = out_offs[f] + k + h;
+    P.len = (uint32_t)len;
+    key_schedule(key, nb, P);
+  }
+  reserve_segments(P, f, sc, mine);  // the whole wave (a long file's work items filled together)
+  if (mine) params[f] = P;
 }
 
 // ----------------------------------------------------------------------------------------
