@@ -1364,7 +1364,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
         if ((e = dl(pre.data(), out + off[i], want, s))) return ctx->hip_fail(e, "state head");
         pr = parse_state_prefix(pre.data(), want, want == len[i], &x.hs, &body, &ne);
       }
-      if (pr != 0 || ne == 0 || ne > 0xffffffffull || len[i] > 0xffffffffull) {
+      if (pr != 0 || ne == 0 || ne > (1ull << 30) || len[i] > 0xffffffffull) {  // (the repeat-check set needs 2 ne < 2^32)
         if ((rc = host_parse(i))) return rc;
         continue;
       }
