@@ -4,7 +4,9 @@ on this rank's actor shard, then shard.exchange_vclock -- the dense all_reduce(M
 Dot names a registered actor, else the all-gather of serialized StateWrappers + merge_state.
 Writes the merged StateWrapper bytes and the path taken to <out>.<rank>.
 
-  python tests/multi_rank_worker.py RANK WORLD PORT MODE OUT     (MODE: registered|unregistered)
+  python tests/multi_rank_worker.py RANK WORLD PORT MODE OUT
+    MODE: registered | unregistered (GCounter, exchange_vclock) | orswot (Orswot<u64, Uuid>,
+    shard.exchange_dotset: the all-gather of partial StateWrappers + the GPU Orswot::merge)
 """
 import os
 import random
@@ -48,8 +50,49 @@ def workload(mode, seed=77, n_actors=6, versions=5):
     return key, actors, files, fa, fv
 
 
+def workload_orswot(seed=88, n_actors=8, versions=4):
+    """Seeded well-formed Orswot op files (tests/dotset_gen.py), sealed with the oracle, in
+    load_ops order: removals may name other writers' adds, so a rank's partial state carries
+    deferred removals the exchange has to resolve."""
+    import crdtenc
+    import dotset_gen as G
+    import oracle
+    rng = random.Random(seed)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, n_actors)
+    files = G.well_formed_orswot(rng, actors, versions, 6, 30)[0]
+    acts, clears, fa, fv = G.batch(files, "orswot", APP)
+    sealed = []
+    for c in clears:
+        st, enc = oracle.cryptor_encrypt(key, rng.randbytes(24), c)
+        assert st == 0
+        sealed.append(crdtenc.CORE_VERSION + enc)
+    return key, acts, sealed, fa, fv
+
+
+def main_orswot(rank, world, out):
+    import crdtenc
+    import shard
+    key, actors, files, fa, fv = workload_orswot()
+    ctx = crdtenc.Context(0)
+    core = crdtenc.Core(ctx, kind=crdtenc.STATE_ORSWOT, supported=[APP], current_data_version=APP)
+    core.set_latest_key(key)
+    lo, hi = shard.actor_range(len(actors), world, rank)
+    sel = [i for i in range(len(files)) if lo <= fa[i] < hi]
+    rc, _ = core.ingest_ops([files[i] for i in sel], actors[lo:hi], [fa[i] - lo for i in sel],
+                            [fv[i] for i in sel])
+    assert rc == 0, rc
+    shard.exchange_dotset(core, device="cpu")
+    with open("%s.%d" % (out, rank), "wb") as f:
+        f.write(b"dotset\n" + core.state_bytes())
+    core.close()
+    ctx.close()
+
+
 def main():
     rank, world, port, mode, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5]
+    if mode == "orswot":
+        sys.path.insert(0, os.path.join(REPO, "tests"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
     import torch
     import torch.distributed as dist
@@ -57,6 +100,9 @@ def main():
     import shard
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        if mode == "orswot":
+            main_orswot(rank, world, out)
+            return
         key, actors, files, fa, fv = workload(mode)
         ctx = crdtenc.Context(0)
         core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)

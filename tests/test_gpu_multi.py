@@ -56,3 +56,27 @@ def test_exchange_vclock_two_processes(tmp_path, oracle, mode, path):
             got_path, state = f.read().split(b"\n", 1)
         assert got_path.decode() == path
         assert state == want
+
+
+def test_exchange_dotset_two_processes(tmp_path):
+    """§8(e) for the dot sets: two ranks fold their writer shards of Orswot op files on the GPU,
+    then shard.exchange_dotset all-gathers the partial StateWrappers over a real (gloo) group and
+    each rank merges the other's with the GPU Orswot::merge (crdt-enc/src/lib.rs:458-466).  Both
+    end with the oracle's single fold over every file."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import multi_rank_worker as W
+    from oracle import crdts as C
+    key, actors, files, fa, fv = W.workload_orswot()
+    oc = C.Core("orswot")
+    assert oc.read_remote_ops(key, [APP], files, [actors[i] for i in fa], fv)[0] == 0
+    want = oc.serialize()
+    out = str(tmp_path / "d")
+    port = str(_port())
+    procs = [subprocess.Popen([sys.executable, os.path.join(REPO, "tests", "multi_rank_worker.py"),
+                               str(r), "2", port, "orswot", out]) for r in range(2)]
+    rcs = [p.wait(timeout=180) for p in procs]
+    assert rcs == [0, 0]
+    for r in range(2):
+        with open("%s.%d" % (out, r), "rb") as f:
+            tag, state = f.read().split(b"\n", 1)
+        assert tag == b"dotset" and state == want
