@@ -347,6 +347,12 @@ __global__ __launch_bounds__(256) void k_segments(const uint8_t* __restrict__ in
     const uint32_t rows = (nb + 63) >> 6;
 
     L5 acc = {{0, 0, 0, 0, 0}};
+    // A page whose 4 pieces are whole ciphertext pieces in every lane folds them as four products
+    // into one set of column sums, acc R^4 + m0 R^3 + m1 R^2 + m2 R + m3 (R = r^64), reduced
+    // once -- instead of four Horner mulmods.  Only the file's last page takes the Horner steps.
+    const MulR M1 = mul_r(R);
+    const L5 R2 = mulmod(R, R), R3 = mulmod(R2, R);
+    const MulR M2 = mul_r(R2), M3 = mul_r(R3), M4 = mul_r(mulmod(R2, R2));
     // a page = 4 rows of 64 pieces = the 64 ChaCha20 blocks the lanes compute together
     for (uint32_t row0 = 0; row0 < rows; row0 += 4) {
       // the page's ciphertext is loaded first: its latency hides under the page's keystream
@@ -369,6 +375,30 @@ __global__ __launch_bounds__(256) void k_segments(const uint8_t* __restrict__ in
         kd[3] = make_uint4(kb[12], kb[13], kb[14], kb[15]);
       }
       __builtin_amdgcn_wave_barrier();
+      {
+        const uint32_t blk3 = b_lo + (row0 + 3) * 64 + lane;  // the lane's last piece of the page
+        if (__all(row0 + 3 < rows && blk3 < nblk_ct && blk3 * 16 + 16 <= len)) {
+          L5 m[4];
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const uint32_t boff = (b_lo + (row0 + r) * 64 + lane) * 16;
+            const uint32_t q = (uint32_t)r * 64 + lane;
+            const uint4 k4 = *reinterpret_cast<const uint4*>(ks + (q >> 2) * kKsStride + (q & 3) * 16);
+            const uint4 x = xin[r];
+            const uint4 y = make_uint4(x.x ^ k4.x, x.y ^ k4.y, x.z ^ k4.z, x.w ^ k4.w);
+            *reinterpret_cast<uint4*>(dst + boff) = y;
+            const uint4 c = SEAL ? y : x;
+            m[r] = block_limbs(c.x, c.y, c.z, c.w);
+          }
+          uint64_t d[5] = {m[3].v[0], m[3].v[1], m[3].v[2], m[3].v[3], m[3].v[4]};
+          mac5(d, acc, M4);
+          mac5(d, m[0], M3);
+          mac5(d, m[1], M2);
+          mac5(d, m[2], M1);
+          acc = reduce5(d);
+          continue;
+        }
+      }
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const uint32_t row = row0 + r;
