@@ -314,9 +314,14 @@ __global__ __launch_bounds__(256) void k_segments(const uint8_t* __restrict__ in
                                                   int32_t* __restrict__ status, SegScratch sc,
                                                   int skip_small, DecodeArgs da, uint4* rec) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWavesPerBlock * 64 * kKsStride];
+  // the segment's Poly1305 multipliers r^64 .. r^256 (4 x MulR, wave-uniform) live in LDS and are
+  // read back (broadcast) right where each product needs them: held in registers across the
+  // page loop they cost 36 VGPRs, and the wave count per SIMD with them
+  __shared__ __attribute__((aligned(16))) uint32_t mul_lds[kWavesPerBlock][36];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wib = threadIdx.x >> 6;
   uint8_t* ks = lds + wib * 64 * kKsStride;
+  uint32_t* ml = mul_lds[wib];
   // skip_small: the first-segment work comes from the large-file list built by the setup
   const uint32_t nfirst = skip_small ? *((volatile uint32_t*)&sc.counters[9]) : n;
   const uint32_t total = nfirst + *((volatile uint32_t*)&sc.counters[0]);
@@ -350,9 +355,29 @@ __global__ __launch_bounds__(256) void k_segments(const uint8_t* __restrict__ in
     // A page whose 4 pieces are whole ciphertext pieces in every lane folds them as four products
     // into one set of column sums, acc R^4 + m0 R^3 + m1 R^2 + m2 R + m3 (R = r^64), reduced
     // once -- instead of four Horner mulmods.  Only the file's last page takes the Horner steps.
-    const MulR M1 = mul_r(R);
-    const L5 R2 = mulmod(R, R), R3 = mulmod(R2, R);
-    const MulR M2 = mul_r(R2), M3 = mul_r(R3), M4 = mul_r(mulmod(R2, R2));
+    {
+      const L5 R2 = mulmod(R, R), R3 = mulmod(R2, R);
+      const MulR Ms[4] = {mul_r(R), mul_r(R2), mul_r(R3), mul_r(mulmod(R2, R2))};
+      __builtin_amdgcn_wave_barrier();  // the previous segment's reads of ml are done
+      if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+#pragma unroll
+          for (int i = 0; i < 5; i++) ml[9 * k + i] = Ms[k].v[i];
+#pragma unroll
+          for (int i = 0; i < 4; i++) ml[9 * k + 5 + i] = Ms[k].s[i];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    auto mul_at = [&](int k) {
+      MulR M;
+#pragma unroll
+      for (int i = 0; i < 5; i++) M.v[i] = ml[9 * k + i];
+#pragma unroll
+      for (int i = 0; i < 4; i++) M.s[i] = ml[9 * k + 5 + i];
+      return M;
+    };
     // a page = 4 rows of 64 pieces = the 64 ChaCha20 blocks the lanes compute together
     for (uint32_t row0 = 0; row0 < rows; row0 += 4) {
       // the page's ciphertext is loaded first: its latency hides under the page's keystream
@@ -378,7 +403,9 @@ __global__ __launch_bounds__(256) void k_segments(const uint8_t* __restrict__ in
       {
         const uint32_t blk3 = b_lo + (row0 + 3) * 64 + lane;  // the lane's last piece of the page
         if (__all(row0 + 3 < rows && blk3 < nblk_ct && blk3 * 16 + 16 <= len)) {
-          L5 m[4];
+          // piece r of the page weighs R^(3 - r); the products go into the column sums as each
+          // piece is decrypted (no four pieces' limbs held at once)
+          uint64_t d[5] = {0, 0, 0, 0, 0};
 #pragma unroll
           for (int r = 0; r < 4; r++) {
             const uint32_t boff = (b_lo + (row0 + r) * 64 + lane) * 16;
@@ -388,13 +415,15 @@ __global__ __launch_bounds__(256) void k_segments(const uint8_t* __restrict__ in
             const uint4 y = make_uint4(x.x ^ k4.x, x.y ^ k4.y, x.z ^ k4.z, x.w ^ k4.w);
             *reinterpret_cast<uint4*>(dst + boff) = y;
             const uint4 c = SEAL ? y : x;
-            m[r] = block_limbs(c.x, c.y, c.z, c.w);
+            const L5 m = block_limbs(c.x, c.y, c.z, c.w);
+            if (r < 3) {
+              mac5(d, m, mul_at(2 - r));
+            } else {
+#pragma unroll
+              for (int i = 0; i < 5; i++) d[i] += m.v[i];
+            }
           }
-          uint64_t d[5] = {m[3].v[0], m[3].v[1], m[3].v[2], m[3].v[3], m[3].v[4]};
-          mac5(d, acc, M4);
-          mac5(d, m[0], M3);
-          mac5(d, m[1], M2);
-          mac5(d, m[2], M1);
+          mac5(d, acc, mul_at(3));
           acc = reduce5(d);
           continue;
         }
