@@ -424,6 +424,54 @@ def test_c3_shaped_medium(ctx):
     core.close()
 
 
+def _c_fold(key, states, files, acts, fa, fv):
+    """oracle/ce_oracle.c oc_compact_orswot_best (the C restatement, pinned to oracle/crdts.py by
+    tests/test_oracle_orswot_c.py): states merged, then the op files folded in load_ops order"""
+    import oracle
+    offs = np.zeros(len(files) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(f) for f in files])
+    actor = np.frombuffer(b"".join(acts[i] for i in fa) or bytes(16), np.uint8).reshape(-1, 16)
+    err, sw, _, _ = oracle.compact_orswot_best(key, APP, states, b"".join(files) or b"\0", offs,
+                                               actor, np.array(list(fv) or [0], np.uint64), 16)
+    return err, sw
+
+
+def test_c3_full_size_adversarial(ctx):
+    """C3 at full size: 4096 actors, members drawn from 100k, four state files (a quarter of the
+    writers' version 0 each) read on the device, then versions 1-2 of every writer: Adds naming
+    other writers' dots, multi-actor removal clocks that defer -- ~98k ops in 12k op files --
+    then the compaction through the device writer.  The Python oracle is too slow at this size;
+    the checker is its C restatement."""
+    rng = random.Random(4096)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 4096)
+    hist = G.adversarial_orswot(rng, actors, 3, 8, 100_000)
+    sws = []
+    for q in range(4):
+        sub = {a: hist[a][:1] for a in actors[q * 1024:(q + 1) * 1024]}
+        acts, clears, fa, fv = G.batch(sub, "orswot", APP)
+        err, sw = _c_fold(key, [], seal_files(ctx, key, clears), acts, fa, fv)
+        assert err == 0
+        sws.append(sw)
+    sf = seal_states(ctx, key, sws)
+    acts, clears, fa, fv = G.batch(hist, "orswot", APP, start={a: 1 for a in actors})
+    files = seal_files(ctx, key, clears)
+    err, want = _c_fold(key, sf, files, acts, fa, fv)
+    assert err == 0 and b"deferred" in want
+    core = new_core(ctx, "orswot", key)
+    assert core.ingest_states(sf) == (0, [0] * 4)
+    assert core.path_count("states_device_read") == 4
+    rc, st = core.ingest_ops(files, acts, fa, fv)
+    assert rc == 0 and st == [0] * len(files)
+    got = core.state_bytes()
+    assert len(got) == len(want) and got == want
+    f, _ = core.compact_to_buffer(nonce=bytes(24))
+    st, pt = ctx.decrypt(key, f[16:])
+    assert st == 0 and pt == want
+    assert core.path_count("compact_device_writer") == 1
+    core.close()
+
+
 def test_ingest_states_iov_matches_blob(ctx):
     """ce_core_ingest_states_iov (per-file host buffers through the pinned staging ring) ==
     ce_core_ingest_states (one blob): statuses and state bytes, a tampered file included."""
