@@ -308,6 +308,32 @@ class Workload:
                 log("STATE MISMATCH (variant %s)" % self.variant)
         return float(ms_t.item()), kern, ok
 
+    def clock_probe(self, ctx):
+        """Shader clock (untimed, after the timed steps): ce_ctx_clock_probe's one-wave blocks,
+        one per XCD, on a side stream, sampling every 100 us for 4 ms -- once with the GPU
+        otherwise idle, once beside a step (the fused kernel runs ~0.2-3.5 ms into it; the
+        probe's waves hold 8 of its wave slots, so that step is slower and is not reported).
+        GHz = shader cycles / reference ticks x 0.1 (100 MHz reference clock)."""
+        blocks, samples, ticks = 8, 40, 10000
+        side = torch.cuda.Stream(device=self.dense.device)
+        res = {}
+        for what in ("idle", "under_step"):
+            out = torch.zeros(blocks * samples * 2, dtype=torch.int64, device=self.dense.device)
+            torch.cuda.synchronize()
+            ctx.clock_probe(out.data_ptr(), blocks, samples, ticks, stream_ptr=side.cuda_stream)
+            if what == "under_step":
+                self.step()
+                self.drain_names()
+            torch.cuda.synchronize()
+            v = out.view(blocks, samples, 2).cpu().numpy().astype(np.float64)
+            ghz = v[:, :, 0] / np.maximum(v[:, :, 1], 1) * 0.1
+            mid = ghz[:, 5:30]   # 0.5-3.0 ms after the probe starts: inside the fused kernel
+            res[what] = {"median_ghz": round(float(np.median(mid)), 3),
+                         "min_ghz": round(float(mid.min()), 3), "max_ghz": round(float(mid.max()), 3)}
+        res["method"] = ("ce_ctx_clock_probe: s_memtime over s_memrealtime per 100-us interval, "
+                         "8 one-wave blocks, intervals 0.5-3.0 ms after launch")
+        return res
+
     def host_buffer_run(self, ctx, steps=3, warmup=1):
         """Core::compact from per-file host buffers (what Storage::load_ops hands a Rust
         caller, lib.rs:495): ce_core_compact_ops_iov gathers the files into pinned staging chunks
@@ -429,6 +455,7 @@ def main():
                     help="files in the CPU baseline sample (0 = the whole per-GPU workload)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-variant-b", action="store_true", help="skip the stress-dot variant")
+    ap.add_argument("--no-clock", action="store_true", help="skip the shader-clock probe")
     ap.add_argument("--no-host-buffers", action="store_true",
                     help="skip the end-to-end run from host buffers (H2D over PCIe)")
     args = ap.parse_args()
@@ -464,6 +491,7 @@ def main():
     wa = Workload(ctx, "a", args, world, rank, dev, actors_all)
     ms, kern, ok = wa.run(ctx, args.steps, args.warmup)
     sa = kernel_summary(wa, ms, kern)
+    clock = wa.clock_probe(ctx) if world == 1 and not args.no_clock else None
     cpu, cpu_ok = None, True
     hostbuf = None
     if world == 1 and not args.no_host_buffers:
@@ -557,6 +585,10 @@ def main():
                         "frac": round((sa["hbm_GBps"] or 0) / HBM_PEAK_GBS, 4),
                         "bytes_per_launch": sa["bytes_per_launch"]},
                 "pmc_valu": valu_pmc,
+                # the peak scales with the shader clock: frac against the peak at the clock the
+                # probe saw beside the fused kernel (VALU_PEAK_TOPS is quoted at 2.4 GHz)
+                "clock": dict(clock, frac_at_measured_clock=round(
+                    sa["valu_frac"] * 2.4 / clock["under_step"]["median_ghz"], 4)) if clock else None,
             },
             "kernels_ms_per_step": sa["kernels_ms_per_step"],
             "state_check": "closed-form StateWrapper bytes: %s" % ("ok" if ok else "MISMATCH"),

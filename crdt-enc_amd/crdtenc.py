@@ -49,7 +49,7 @@ EXPORTS = [
     "ce_keys_decode", "ce_keys_from_remote_metas", "ce_keys_merge", "ce_keys_free",
     "ce_keys_count", "ce_keys_latest", "ce_keys_get", "ce_keys_at", "ce_core_set_keys",
     "ce_core_apply_ops_batch", "ce_core_ingest_ops_iov", "ce_core_ingest_states_iov", "ce_core_compact_ops_iov",
-    "ce_core_path_count",
+    "ce_core_path_count", "ce_ctx_clock_probe",
 ]
 
 
@@ -197,6 +197,13 @@ class Context:
 
     def timing_reset(self):
         lib().ce_ctx_timing_reset(self.p)
+
+    def clock_probe(self, out_ptr, blocks, samples, ticks, stream_ptr=None):
+        """Diagnostics: launch the shader-clock probe (ce_ctx_clock_probe) on stream_ptr (None:
+        the context stream); out_ptr = device uint64[blocks * samples * 2] (cycles, ticks)."""
+        self.check(lib().ce_ctx_clock_probe(self.p, ctypes.c_void_p(stream_ptr), ctypes.c_void_p(out_ptr),
+                                            ctypes.c_uint32(blocks), ctypes.c_uint32(samples),
+                                            ctypes.c_uint32(ticks)), "clock_probe")
 
     # ---- Cryptor ----
     def gen_key(self):

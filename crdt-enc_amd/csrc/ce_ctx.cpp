@@ -351,6 +351,17 @@ int ce_ctx_set_timing_only(ce_ctx* c, const char* kernel) {
   return CE_OK;
 }
 
+int ce_ctx_clock_probe(ce_ctx* c, void* hip_stream, uint64_t* d_out, uint32_t blocks,
+                       uint32_t samples, uint32_t ticks) {
+  if (!c || !d_out || blocks == 0 || blocks > 4096 || samples == 0 || ticks == 0 ||
+      (uint64_t)samples * ticks > 100000000ull)
+    return CE_ERR_INVALID_ARG;
+  const hipError_t e = launch_clock_probe(hip_stream ? (hipStream_t)hip_stream : c->stream,
+                                          reinterpret_cast<unsigned long long*>(d_out), blocks,
+                                          samples, ticks);
+  return e == hipSuccess ? CE_OK : c->hip_fail(e, "clock probe");
+}
+
 int ce_ctx_timing_read(ce_ctx* c, const char* kernel, double* total_ms, uint64_t* launches) {
   if (!c || !kernel || !total_ms || !launches) return CE_ERR_INVALID_ARG;
   std::lock_guard<std::recursive_mutex> g(c->mu);

@@ -115,6 +115,9 @@ struct DecodeArgs {
                                 // probe (lookup_slot1)
 };
 hipError_t launch_decode_dots(hipStream_t s, const DecodeArgs& a, uint32_t grid_waves);
+// diagnostics: shader clock vs the reference clock (ce_ctx_clock_probe)
+hipError_t launch_clock_probe(hipStream_t s, unsigned long long* out, uint32_t blocks,
+                              uint32_t samples, uint32_t ticks);
 
 // multi-page Vec<Dot> decode split over kSplitParts waves per file (large_list order); files
 // with fewer than kSplitMinDots Dots, or whose parts do not all verify, take the one-wave path

@@ -1365,6 +1365,34 @@ hipError_t launch_merge_max_if(hipStream_t s, unsigned long long* dst, const uns
   return hipGetLastError();
 }
 
+// diagnostics (ce_ctx_clock_probe): one wave per block reads the shader cycle counter against
+// the 100 MHz reference clock every `ticks` reference ticks and stores each interval's
+// (cycles, ticks) through lanes 0 and 1.  Launched beside other work, it measures the clock that
+// work runs at (the blocks land on the XCDs round-robin).
+__global__ __launch_bounds__(64) void k_clock_probe(unsigned long long* out, uint32_t samples,
+                                                    uint32_t ticks) {
+  const uint32_t lane = threadIdx.x;
+  unsigned long long c0 = __builtin_amdgcn_s_memtime();
+  unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+  for (uint32_t k = 0; k < samples; k++) {
+    unsigned long long r = r0;
+    while (r - r0 < ticks) {
+      __builtin_amdgcn_s_sleep(2);
+      r = __builtin_amdgcn_s_memrealtime();
+    }
+    const unsigned long long c = __builtin_amdgcn_s_memtime();
+    if (lane < 2) out[2ull * ((unsigned long long)blockIdx.x * samples + k) + lane] = lane ? r - r0 : c - c0;
+    c0 = c;
+    r0 = r;
+  }
+}
+
+hipError_t launch_clock_probe(hipStream_t s, unsigned long long* out, uint32_t blocks,
+                              uint32_t samples, uint32_t ticks) {
+  hipLaunchKernelGGL(k_clock_probe, dim3(blocks), dim3(64), 0, s, out, samples, ticks);
+  return hipGetLastError();
+}
+
 hipError_t launch_nov_apply(hipStream_t s, unsigned long long* nov, const uint32_t* wslot,
                             const unsigned long long* newnov, uint32_t m, const uint32_t* counters) {
   if (m == 0) return hipSuccess;

@@ -78,6 +78,13 @@ int ce_ctx_set_timing(ce_ctx *ctx, int enable);
 int ce_ctx_set_timing_only(ce_ctx *ctx, const char *kernel);
 int ce_ctx_timing_read(ce_ctx *ctx, const char *kernel, double *total_ms, uint64_t *launches);
 void ce_ctx_timing_reset(ce_ctx *ctx);
+/* Diagnostics (no reference counterpart): the shader clock while other work runs.  Launches
+ * `blocks` one-wave blocks on hip_stream (NULL = the context stream); each reads the shader
+ * cycle counter against the 100 MHz reference clock every `ticks` reference ticks, `samples`
+ * times, and writes (cycles, ticks) of every interval to d_out (device memory, blocks * samples
+ * * 2 uint64).  Asynchronous; at most 4096 blocks, samples * ticks <= 10^8 (1 s). */
+int ce_ctx_clock_probe(ce_ctx *ctx, void *hip_stream, uint64_t *d_out, uint32_t blocks,
+                       uint32_t samples, uint32_t ticks);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Cryptor: XChaCha20-Poly1305 EncHandler on the GPU                                          */

@@ -999,3 +999,22 @@ def test_many_segment_files_seal_and_open(ctx, oracle, size):
     rc, sts, pts, raw, offs = ctx.decrypt_batch(key, [enc, bytes(b)])
     assert list(sts) == [0, 9] and pts[0] == pt
     assert raw[offs[1]:offs[1] + size] == bytes(size)
+
+
+def test_clock_probe(ctx):
+    """ce_ctx_clock_probe (diagnostics behind bench.py's roofline.clock): every interval spans
+    at least the requested reference ticks and reports a plausible shader clock; bad arguments
+    are refused before any launch."""
+    import torch
+    blocks, samples, ticks = 8, 4, 5000
+    out = torch.zeros(blocks * samples * 2, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    ctx.clock_probe(out.data_ptr(), blocks, samples, ticks)
+    ctx.synchronize()
+    v = out.view(blocks, samples, 2).cpu().numpy()
+    assert (v[:, :, 1] >= ticks).all()
+    ghz = v[:, :, 0] / v[:, :, 1] * 0.1
+    assert ((ghz > 0.3) & (ghz < 4.0)).all(), ghz
+    for bad in ((0, 4, 5000), (4097, 4, 5000), (8, 0, 5000), (8, 4, 0), (8, 1000, 10 ** 6)):
+        with pytest.raises(crdtenc.CeError):
+            ctx.clock_probe(out.data_ptr(), *bad)
