@@ -167,6 +167,32 @@ def host_cpu():
     return model, avail, max(1, min(avail, share, 256))
 
 
+def probe_clock(ctx, step, dev):
+    """Shader clock (untimed, after the timed steps): ce_ctx_clock_probe's one-wave blocks,
+    one per XCD, on a side stream, sampling every 100 us for 4 ms -- once with the GPU
+    otherwise idle, once beside `step` (its main kernel runs ~0.2-3.5 ms into it; the probe's
+    waves hold 8 of its wave slots, so that step is slower and is not reported).
+    GHz = shader cycles / reference ticks x 0.1 (100 MHz reference clock)."""
+    blocks, samples, ticks = 8, 40, 10000
+    side = torch.cuda.Stream(device=dev)
+    res = {}
+    for what in ("idle", "under_step"):
+        out = torch.zeros(blocks * samples * 2, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()
+        ctx.clock_probe(out.data_ptr(), blocks, samples, ticks, stream_ptr=side.cuda_stream)
+        if what == "under_step":
+            step()
+        torch.cuda.synchronize()
+        v = out.view(blocks, samples, 2).cpu().numpy().astype(np.float64)
+        ghz = v[:, :, 0] / np.maximum(v[:, :, 1], 1) * 0.1
+        mid = ghz[:, 5:30]   # 0.5-3.0 ms after the probe starts: inside the main kernel
+        res[what] = {"median_ghz": round(float(np.median(mid)), 3),
+                     "min_ghz": round(float(mid.min()), 3), "max_ghz": round(float(mid.max()), 3)}
+    res["method"] = ("ce_ctx_clock_probe: s_memtime over s_memrealtime per 100-us interval, "
+                     "8 one-wave blocks, intervals 0.5-3.0 ms after launch")
+    return res
+
+
 def launch_ranks(args):
     """--gpus N without torch.distributed.run: start N rank processes (this parent never
     initialises HIP), forward rank 0's stdout, exit with the worst rank status."""
@@ -309,30 +335,11 @@ class Workload:
         return float(ms_t.item()), kern, ok
 
     def clock_probe(self, ctx):
-        """Shader clock (untimed, after the timed steps): ce_ctx_clock_probe's one-wave blocks,
-        one per XCD, on a side stream, sampling every 100 us for 4 ms -- once with the GPU
-        otherwise idle, once beside a step (the fused kernel runs ~0.2-3.5 ms into it; the
-        probe's waves hold 8 of its wave slots, so that step is slower and is not reported).
-        GHz = shader cycles / reference ticks x 0.1 (100 MHz reference clock)."""
-        blocks, samples, ticks = 8, 40, 10000
-        side = torch.cuda.Stream(device=self.dense.device)
-        res = {}
-        for what in ("idle", "under_step"):
-            out = torch.zeros(blocks * samples * 2, dtype=torch.int64, device=self.dense.device)
-            torch.cuda.synchronize()
-            ctx.clock_probe(out.data_ptr(), blocks, samples, ticks, stream_ptr=side.cuda_stream)
-            if what == "under_step":
-                self.step()
-                self.drain_names()
-            torch.cuda.synchronize()
-            v = out.view(blocks, samples, 2).cpu().numpy().astype(np.float64)
-            ghz = v[:, :, 0] / np.maximum(v[:, :, 1], 1) * 0.1
-            mid = ghz[:, 5:30]   # 0.5-3.0 ms after the probe starts: inside the fused kernel
-            res[what] = {"median_ghz": round(float(np.median(mid)), 3),
-                         "min_ghz": round(float(mid.min()), 3), "max_ghz": round(float(mid.max()), 3)}
-        res["method"] = ("ce_ctx_clock_probe: s_memtime over s_memrealtime per 100-us interval, "
-                         "8 one-wave blocks, intervals 0.5-3.0 ms after launch")
-        return res
+        """Shader clock beside one untimed step (probe_clock)."""
+        def one():
+            self.step()
+            self.drain_names()
+        return probe_clock(ctx, one, self.dense.device)
 
     def host_buffer_run(self, ctx, steps=3, warmup=1):
         """Core::compact from per-file host buffers (what Storage::load_ops hands a Rust

@@ -458,6 +458,9 @@ def run_c4(args, ctx, dev):
                           "state": {"inner": {"dots": {bytes(actors[a]): 65536 + int(kd[a].sum())
                                                        for a in range(m)}}}}, use_bin_type=True)
     ok = core.state_bytes() == want
+    sys.path.insert(0, REPO)
+    import bench
+    clock = None if args.no_clock else bench.probe_clock(ctx, step, dev)
     ct = sum(pt_len)
     cpu = None
     if not args.no_cpu:  # the first A actors' files through the GPU path and the oracle
@@ -484,6 +487,7 @@ def run_c4(args, ctx, dev):
                    "dots": int(kd.sum())},
         "aead_GBps_end_to_end": round(ct / (ms / 1e3) / 1e9, 1),
         "kernels_ms_per_step": k_ms,
+        "clock": clock,
         # multi-segment files folded from the segment pass's records vs decoded whole, over
         # every ingest of the run (warmup + steps)
         "cpu_baseline": cpu,
@@ -599,6 +603,7 @@ def main():
     ap.add_argument("--steps", type=int, default=None,
                     help="timed steps (default 20; 40 for c3, whose last names are hashed after its last step)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-clock", action="store_true", help="skip the shader-clock probe (C4)")
     ap.add_argument("--c4-cpu-actors", type=int, default=256, help="C4 CPU sample: files of this many actors")
     ap.add_argument("--c5-cpu-actors", type=int, default=128, help="C5 CPU sample: actors per key")
     ap.add_argument("--warmup", type=int, default=1)
