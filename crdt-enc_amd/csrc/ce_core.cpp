@@ -1706,6 +1706,8 @@ int ce_core_apply_ops(ce_core* c, const uint8_t* ops, size_t len) {
     return c->ctx->fail(rc, "failed writing ops file");
   // state.apply(op) for op in ops (lib.rs:710-712)
   if ((rc = ds ? ds_apply_local_ops(c, ops, len) : merge_dots_host(c, dots))) return rc;
+  // the apply may have grown the table (new Dot actors), which moves every slot: look it up again
+  s = c->slot_of.at(c->local_actor);
   c->nov[s] = version + 1;                         // next_op_versions.inc(actor) (lib.rs:714-715)
   return table_upload(c);
 }
@@ -1784,6 +1786,7 @@ int ce_core_apply_ops_batch(ce_core* c, const uint8_t* ops, const uint64_t* offs
     // state.apply(op) for op in ops (lib.rs:710-712), then next_op_versions.inc (lib.rs:714-715)
     if ((rc = ds ? ds_apply_local_ops(c, ops + offs[i], offs[i + 1] - offs[i]) : merge_dots_host(c, dots[i])))
       return rc;
+    s = c->slot_of.at(c->local_actor);  // a growth inside the apply moved the local actor's slot
     c->nov[s] = v0 + i + 1;
   }
   if (files) {

@@ -356,6 +356,8 @@ int ce_ctx_clock_probe(ce_ctx* c, void* hip_stream, uint64_t* d_out, uint32_t bl
   if (!c || !d_out || blocks == 0 || blocks > 4096 || samples == 0 || ticks == 0 ||
       (uint64_t)samples * ticks > 100000000ull)
     return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
   const hipError_t e = launch_clock_probe(hip_stream ? (hipStream_t)hip_stream : c->stream,
                                           reinterpret_cast<unsigned long long*>(d_out), blocks,
                                           samples, ticks);

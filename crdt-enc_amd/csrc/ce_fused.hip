@@ -198,6 +198,9 @@ template <int LPF, int DOPT = 0, typename Pf>
 __device__ __forceinline__ void decode_fold(const DecodeArgs& a, const SupVers& sup, const uint8_t* fl,
                                             uint32_t len, bool live, bool apply, uint32_t f,
                                             uint32_t grp, uint32_t sub, DecState& S, Pf&& prefetch) {
+#if !CE_FUSED_DIAG
+  static_assert(DOPT == 0, "decode_fold diagnostics variants exist only in the diagnostics build");
+#endif
   int32_t st = CE_OK;
   uint32_t xs[16];
   int drn = 0;
@@ -755,6 +758,9 @@ __device__ __forceinline__ FilePre2 load_pre2(const DecodeArgs& a, uint32_t f) {
 template <int LPF, int W, bool JIT, int OPT = 3>
 __global__ __launch_bounds__(64, W)
 void k_open_fold_v2(DecodeArgs a) {
+#if !CE_FUSED_DIAG
+  static_assert((OPT & ~3) == 0, "k_open_fold_v2 diagnostics variants exist only in the diagnostics build");
+#endif
   constexpr bool SD = (OPT & 1) != 0;
   constexpr bool PF = (OPT & 2) != 0 && !JIT;
   constexpr int UNR = (OPT & 4) ? 1 : (OPT & 8) ? 3 : 9;  // ChaCha20 double rounds per loop trip
@@ -1062,16 +1068,19 @@ static void launch_v2(hipStream_t s, const DecodeArgs& a) {
 
 hipError_t launch_open_fold_v2(hipStream_t s, const DecodeArgs& a, int files_per_wave) {
   if (a.n == 0) return hipSuccess;
-  // VGPR budget (CE_V2_WAVES, diagnostics): 2 or 3 waves per SIMD at LPF 16, 3 or 4 at LPF 32
+#if CE_FUSED_DIAG
+  // diagnostics build only (libcrdtenc_prof.so): same-box A/B variants.  Several of them are
+  // NOT correct (OPT 129/385 skip the actor lookups, 513/1025 may write status 77), so none is
+  // compiled into the product library, which ignores both variables.
+  // CE_V2_WAVES: 3 = 3 waves/SIMD VGPR budget, 13 = 3 with JIT ciphertext loads, 12 = 2 with
+  // them; 4 = 4 waves at 2 files per wave.  CE_V2_OPT: the OPT bits of the LPF 16 kernel.
   static const int w = [] {
     const char* e = getenv("CE_V2_WAVES");
     return e ? atoi(e) : 0;
   }();
-  // CE_V2_WAVES (diagnostics): 13 = 3 waves/SIMD with JIT ciphertext loads, 12 = 2 with them
-  // CE_V2_OPT (diagnostics, same-box A/B): the OPT bits of the default LPF 16 kernel
   static const int opt = [] {
     const char* e = getenv("CE_V2_OPT");
-    return e ? atoi(e) : 1;  // SDWA rot16 on, next-ciphertext prefetch off (same-box A/B r02)
+    return e ? atoi(e) : 1;
   }();
   if (files_per_wave == 2) {
     if (w == 4) launch_v2<32, 4, false>(s, a);
@@ -1097,6 +1106,12 @@ hipError_t launch_open_fold_v2(hipStream_t s, const DecodeArgs& a, int files_per
     else if (opt == 81) launch_v2<16, 2, false, 81>(s, a);
     else launch_v2<16, 2, false, 3>(s, a);
   }
+#else
+  // product: the measured default only -- SDWA rot16 on, next-ciphertext prefetch off (same-box
+  // A/B r02); 2 files per wave at a 3-wave budget (SDWA rot16 + prefetch) for the fpw = 2 geometry
+  if (files_per_wave == 2) launch_v2<32, 3, false, 3>(s, a);
+  else launch_v2<16, 2, false, 1>(s, a);
+#endif
   return hipGetLastError();
 }
 

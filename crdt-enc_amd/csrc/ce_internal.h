@@ -1,6 +1,7 @@
 // ce_internal.h -- host-side internals shared by ce_ctx.cpp, ce_storage.cpp, ce_core.cpp.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <array>
 #include <cstring>
@@ -123,6 +124,8 @@ struct ce_ctx {
 
   // stream synchronise by polling an event (CE_SYNC_YIELD=1: hipStreamSynchronize).  The
   // blocking wait's wake-up costs tens of microseconds per step on the box; a step waits once.
+  // The poll yields the core between queries after the first few, so the library does not hold a
+  // host core against the upload pool or other ranks' threads for a whole kernel.
   hipEvent_t spin_ev = nullptr;
   hipError_t sync_spin() {
     static const bool yield = getenv("CE_SYNC_YIELD") != nullptr;
@@ -130,8 +133,8 @@ struct ce_ctx {
     hipError_t e;
     if (!spin_ev && (e = hipEventCreateWithFlags(&spin_ev, hipEventDisableTiming))) return e;
     if ((e = hipEventRecord(spin_ev, stream))) return e;
-    while ((e = hipEventQuery(spin_ev)) == hipErrorNotReady) {
-    }
+    for (unsigned i = 0; (e = hipEventQuery(spin_ev)) == hipErrorNotReady; i++)
+      if (i >= 32) sched_yield();
     return e;
   }
 

@@ -346,8 +346,14 @@ int ce_keys_latest(const ce_keys* k, uint8_t id_out[16], uint8_t key_version_out
   if (!k) return CE_ERR_INVALID_ARG;
   // latest_key_id.read().val mapped to keys.read().val, min by id (key_cryptor.rs:59-70)
   const Uuid* best = nullptr;
+  std::vector<const Uuid*> taken;
   for (auto& v : k->latest.vals) {
-    if (!k->keys.entries.count(v.second)) return CE_ERR_DECODE;  // the reference panics (:67)
+    // keys.take(&id) removes the key it returns, so a repeated id finds none: the reference
+    // panics (:67) on a missing key and on a repeat alike
+    if (!k->keys.entries.count(v.second)) return CE_ERR_DECODE;
+    for (const Uuid* t : taken)
+      if (*t == v.second) return CE_ERR_DECODE;
+    taken.push_back(&v.second);
     if (!best || v.second < *best) best = &v.second;
   }
   if (!best) return CE_ERR_NO_KEY;

@@ -54,9 +54,12 @@ class Keys:
 
     def latest_key(self):                # key_cryptor.rs:59-70
         ids = [v for _, v in self.latest.vals]
+        taken = set()
         for i in ids:
-            if i not in self.keys.entries:
+            # keys.take(&id) removes the key, so a second value naming the same id finds nothing
+            if i not in self.keys.entries or i in taken:
                 raise KeyError("Could not find key for latest key id")   # the reference panics
+            taken.add(i)
         if not ids:
             return None
         i = min(ids)

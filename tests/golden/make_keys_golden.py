@@ -63,6 +63,11 @@ def main():
     add("latest_without_key", miss, "a latest id no key carries: the reference panics "
                                    "(key_cryptor.rs:67)")
     add("empty", K.Keys(), "no key at all: latest_key() is None (lib.rs:420 'no latest key')")
+    rep = K.decode_keys(base.to_bytes())
+    rep.latest.vals.append((C.VClock({B: 5}), rep.latest.vals[0][1]))
+    add("repeated_latest_id", rep, "two concurrent register values name the same key id: "
+                                   "keys.take(&id) removed it on the first, so the reference "
+                                   "panics on the second (key_cryptor.rs:60-67)")
 
     # remote metas: two files whose key_cryptor registers hold concurrent Keys values
     reg_a = [(C.VClock({A: 1}), (K.GPGME_VERSION, ka.to_bytes()))]

@@ -57,6 +57,43 @@ def test_content_name_matches_fixture(repo_fx):
         assert crdtenc.content_name(d) == want
 
 
+@pytest.mark.parametrize("no_openssl", [False, True])
+def test_content_name_large_inputs(no_openssl):
+    """BASE32_NOPAD(SHA3-256(bytes)) (crdt-enc-tokio/src/lib.rs:407-417) at and past the 4 KiB
+    cut-over to dlopen'd OpenSSL and up to 3 MiB, against hashlib: in-process (OpenSSL present),
+    and in a child process with CE_NO_OPENSSL=1 (read once, when the first name is taken), which
+    pins the portable Keccak-f[1600] sponge on large inputs."""
+    import subprocess
+    import sys
+    sizes = [4095, 4096, 4097, (1 << 20) + 7, 3 << 20]
+    code = ("import os, sys, hashlib, base64; sys.path.insert(0, %r); import crdtenc\n"
+            "for n in %r:\n"
+            "    d = bytes((i * 2654435761 >> 13) & 255 for i in range(n))\n"
+            "    want = base64.b32encode(hashlib.sha3_256(d).digest()).decode().rstrip('=')\n"
+            "    assert crdtenc.content_name(d) == want, n\n"
+            "print('ok')\n") % (os.path.join(REPO, "crdt-enc_amd"), sizes)
+    env = dict(os.environ)
+    env.pop("CE_NO_OPENSSL", None)
+    if no_openssl:
+        env["CE_NO_OPENSSL"] = "1"
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr[-2000:]
+
+
+def test_product_library_has_no_diagnostic_kernel_variants():
+    """The product libcrdtenc.so carries only the measured default instantiations of
+    k_open_fold_v2 (OPT 1 at 4 files per wave, OPT 3 at 2): the diagnostics variants -- some
+    give wrong results on purpose (OPT 129/385 skip the actor lookups, 513/1025 may write
+    status 77) -- live only in libcrdtenc_prof.so (CE_FUSED_DIAG), so no environment variable
+    can select them from the product."""
+    raw = open(os.path.join(REPO, "crdt-enc_amd", "libcrdtenc.so"), "rb").read()
+    found = set(re.findall(rb"k_open_fold_v2ILi(\d+)ELi(\d+)ELb([01])ELi(\d+)E", raw))
+    assert found, "no k_open_fold_v2 instantiation found in the product library"
+    opts = {(int(l), int(w), int(j), int(o)) for l, w, j, o in found}
+    assert opts <= {(16, 2, 0, 1), (32, 3, 0, 3)}, sorted(opts)
+    assert not re.search(rb"decode_foldILi\d+ELi[1-9]", raw)
+
+
 # ---- VersionBytesBuf: port of crdt-enc/tests/version_box_buf.rs ----
 UUID = H("d8d2cf50a5c6433b98e68c268fd84fa0")
 

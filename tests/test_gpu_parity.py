@@ -835,13 +835,14 @@ def test_concurrent_decrypts_one_context(ctx, oracle):
 def test_c1_three_replicas_1k_ops(ctx, tmp_path, oracle):
     """BASELINE C1 at its stated size: 3 replicas (actors) share a remote dir and write ~1k ops
     (Core::apply_ops, lib.rs:666-722: batched with ce_core_apply_ops_batch and single calls
-    mixed), whose Dots name 800 distinct actors (table growth; a ~25 KB state file sealed and
-    opened in several 16 KiB segments).  Every replica's read_remote folds to the oracle's
+    mixed), whose Dots name ~2,600 distinct actors -- past the 2,048 the initial 8192-slot table
+    holds at 1/4 load, so it grows mid-run (asserted) -- and a state file sealed and opened in
+    several 16 KiB segments.  Every replica's read_remote folds to the oracle's
     state; compact (ingest format) + a fresh replica reproduce it (lib.rs:332-380, 390-547)."""
     rng = random.Random(1000)
     key = rng.randbytes(32)
     remote = str(tmp_path / "remote")
-    pool = [rng.randbytes(16) for _ in range(800)]
+    pool = [rng.randbytes(16) for _ in range(2600)]
     cores = []
     for r in range(3):
         cores.append(crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP],
@@ -850,13 +851,14 @@ def test_c1_three_replicas_1k_ops(ctx, tmp_path, oracle):
                                   flags=crdtenc.OPEN_CREATE | crdtenc.COMPACT_INGEST_FORMAT))
         cores[-1].set_latest_key(key)
     acts = [c.info_actor() for c in cores]
+    cap0 = cores[0].dense_capacity()
     written = {a: [] for a in acts}
     for r, c in enumerate(cores):
         total = 0
         while total < 333:
             k = rng.choice([1, 7, 40])
             ops = [msgpack.packb([{"actor": rng.choice(pool + [acts[r]] * 50), "counter": rng.getrandbits(40) + 1}
-                                  for _ in range(rng.randint(1, 4))], use_bin_type=True) for _ in range(k)]
+                                  for _ in range(rng.randint(1, 16))], use_bin_type=True) for _ in range(k)]
             if k == 1:
                 assert c.apply_ops(ops[0]) == 0
                 written[acts[r]].append(None)
@@ -879,6 +881,7 @@ def test_c1_three_replicas_1k_ops(ctx, tmp_path, oracle):
         assert c.read_remote() == 0
         assert c.state_bytes() == oc.serialize()
     assert len(oc.serialize()) > 20000
+    assert cores[0].dense_capacity() > cap0, "the actor table never grew"
     rc, name = cores[1].compact()
     assert rc == 0 and st.list_state_names() == [name]
     fresh = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP,
@@ -982,6 +985,50 @@ def test_table_growth_inside_one_call(ctx, oracle, kind):
     core.close()
 
 
+@pytest.mark.parametrize("batch", [False, True])
+def test_local_writer_survives_table_growth(ctx, tmp_path, oracle, batch):
+    """Core::apply_ops (lib.rs:666-722) whose Dots name more new actors than the table holds
+    before it grows (2,048 at 1/4 load of 8,192 slots): the apply rehashes the table, so the local
+    actor's next_op_versions slot must be looked up again after it.  Every op file survives at
+    its own version (none overwritten), the next call writes the next version, and a fresh replica
+    reading the remote dir folds to the oracle's state (next_op_versions included)."""
+    rng = random.Random(2049 + batch)
+    key = rng.randbytes(32)
+    remote = str(tmp_path / "remote")
+    core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP,
+                        local_path=str(tmp_path / "l0"), remote_path=remote, flags=crdtenc.OPEN_CREATE)
+    core.set_latest_key(key)
+    me = core.info_actor()
+    cap0 = core.dense_capacity()
+    n_calls = 0
+    for round_ in range(3):
+        ops = [msgpack.packb([{"actor": rng.randbytes(16), "counter": rng.getrandbits(30) + 1}
+                              for _ in range(1500)] + [{"actor": me, "counter": round_ + 1}], use_bin_type=True)
+               for _ in range(2)]
+        if batch:
+            rc, files = core.apply_ops_batch(ops, nonces=[rng.randbytes(24) for _ in ops])
+            assert rc == 0 and len(files) == 2
+        else:
+            for o in ops:
+                assert core.apply_ops(o) == 0
+        n_calls += 2
+    assert core.dense_capacity() > cap0, "the actor table never grew"
+    st = crdtenc.Storage(str(tmp_path / "l1"), remote)
+    loaded = st.load_ops([(me, 0)])
+    assert [x[1] for x in loaded] == list(range(n_calls))
+    oc = oracle.Core()
+    assert oc.read_remote_ops(key, [APP], [x[2] for x in loaded], [x[0] for x in loaded],
+                              [x[1] for x in loaded])[0] == 0
+    assert core.state_bytes() == oc.serialize()
+    fresh = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP,
+                         local_path=str(tmp_path / "l2"), remote_path=remote, flags=crdtenc.OPEN_CREATE)
+    fresh.set_latest_key(key)
+    assert fresh.read_remote() == 0
+    assert fresh.state_bytes() == oc.serialize()
+    for c in (core, fresh):
+        c.close()
+
+
 @pytest.mark.parametrize("size", [(1 << 20) + 17, (5 << 20) + 1000, 35_000_000])
 def test_many_segment_files_seal_and_open(ctx, oracle, size):
     """Files of more than 64 Poly1305 segments (16 KiB each): k_finalize_multi runs one Horner
@@ -1018,3 +1065,18 @@ def test_clock_probe(ctx):
     for bad in ((0, 4, 5000), (4097, 4, 5000), (8, 0, 5000), (8, 4, 0), (8, 1000, 10 ** 6)):
         with pytest.raises(crdtenc.CeError):
             ctx.clock_probe(out.data_ptr(), *bad)
+
+
+@pytest.mark.gpu
+def test_diag_env_cannot_select_wrong_variants():
+    """CE_V2_OPT=129 (actor lookups skipped, wrong results on purpose) and CE_V2_WAVES=13 select
+    diagnostics variants only in libcrdtenc_prof.so; the product library ignores them, so
+    __graft_entry__.smoke() run with them set still folds to the oracle's state."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, CE_V2_OPT="129", CE_V2_WAVES="13")
+    env.pop("CRDTENC_LIB", None)
+    r = subprocess.run([sys.executable, "-c", "import __graft_entry__ as g; g.smoke()"], cwd=repo,
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "smoke ok" in r.stdout, (r.stdout[-1000:], r.stderr[-2000:])

@@ -39,7 +39,7 @@ def test_oracle_reproduces_fixture(keys_fx):
     assert k.latest_key()[0].hex() == m["latest"]["id"] and len(k.keys.entries) == m["count"]
 
 
-@pytest.mark.parametrize("i", range(6))
+@pytest.mark.parametrize("i", range(7))
 def test_product_latest_key(keys_fx, i):
     c = keys_fx["cases"][i]
     k = crdtenc.Keys.decode(H(c["keys"]))
