@@ -77,12 +77,16 @@ def pt_len(variant):
     return 16 + 3 + DOT_LEN[variant] * K_DOTS[variant]
 
 
-def build_files(ctx, key, actors_local, actors_all, versions, dev, seed, variant="a"):
-    """Seal n = len(actors_local) * versions op files on the GPU.  Returns (files, offs, n,
-    blob_len, smax): smax = the u64 max counter per global actor (variant B; int64 views with
-    the sign flipped, shard._FLIP), None for variant A (closed form)."""
+def build_files(ctx, key, actors_local, actors_all, versions, dev, seed, variant="a", fa=None, fv=None):
+    """Seal n = len(actors_local) * versions op files on the GPU (writer i // versions of
+    actors_local, version i % versions), or, with fa / fv (int64 numpy, writer index into
+    actors_local and version per file), exactly those files.  Returns (files, offs, n, blob_len,
+    smax): smax = the u64 max counter per global actor (variant B; int64 views with the sign
+    flipped, shard._FLIP), None for variant A (closed form)."""
     m_act = actors_local.shape[0]
-    n = m_act * versions
+    n = m_act * versions if fa is None else len(fa)
+    fa_t = torch.from_numpy(np.ascontiguousarray(fa, np.int64)).to(dev) if fa is not None else None
+    fv_t = torch.from_numpy(np.ascontiguousarray(fv, np.int64)).to(dev) if fv is not None else None
     K, L = K_DOTS[variant], DOT_LEN[variant]
     PT = pt_len(variant)
     file_len = 16 + crdtenc.sealed_len(PT)
@@ -102,7 +106,10 @@ def build_files(ctx, key, actors_local, actors_all, versions, dev, seed, variant
     for c0 in range(0, n, chunk):
         m = min(chunk, n - c0)
         idx = torch.arange(c0, c0 + m, dtype=torch.int64, device=dev)
-        a_loc, v = idx // versions, idx % versions
+        if fa_t is None:
+            a_loc, v = idx // versions, idx % versions
+        else:
+            a_loc, v = fa_t[c0:c0 + m], fv_t[c0:c0 + m]
         clear = torch.empty((m, PT), dtype=torch.uint8, device=dev)
         clear[:, :16] = app
         clear[:, 16:19] = hdr
@@ -218,16 +225,30 @@ class Workload:
     def __init__(self, ctx, variant, args, world, rank, dev, actors_all):
         self.variant = variant
         self.world, self.rank = world, rank
-        lo, hi = shard.actor_range(N_ACTORS, world, rank)
-        self.per = hi - lo
-        self.actors_local = actors_all[lo:hi]
         self.actors_all = actors_all
         self.versions = args.versions * world                  # weak scaling: 1M files per GPU
         self.key = bytes(np.random.default_rng(7).integers(0, 256, 32, dtype=np.uint8))
+        # N > 1: files partitioned by address (shard.ingest_sharded), every writer on every rank;
+        # --partition actor: the previous writer-sharded layout (shard.exchange_vclock)
+        self.partition = args.partition if world > 1 else "single"
+        fa_sel = fv_sel = None
+        if self.partition == "address":
+            fa_all = np.repeat(np.arange(N_ACTORS, dtype=np.uint32), self.versions)
+            fv_all = np.tile(np.arange(self.versions, dtype=np.uint64), N_ACTORS)
+            own = crdtenc.shard_owners([bytes(a) for a in actors_all], fa_all, fv_all, world)
+            keep = own == rank
+            fa_sel, fv_sel = fa_all[keep].astype(np.int64), fv_all[keep].astype(np.int64)
+            self.actors_local = actors_all
+            self.per = N_ACTORS
+            del fa_all, fv_all, own, keep
+        else:
+            lo, hi = shard.actor_range(N_ACTORS, world, rank)
+            self.per = hi - lo
+            self.actors_local = actors_all[lo:hi]
         t0 = time.time()
         self.files, self.offs, self.n, self.blob_len, smax = build_files(
             ctx, self.key, self.actors_local, actors_all, self.versions, dev,
-            seed=1234 + rank + (7919 if variant == "b" else 0), variant=variant)
+            seed=1234 + rank + (7919 if variant == "b" else 0), variant=variant, fa=fa_sel, fv=fv_sel)
         if smax is not None and world > 1:
             shard.all_reduce_(smax, dist.ReduceOp.MAX)   # flipped u64 -> signed max
         self.smax = smax
@@ -241,13 +262,25 @@ class Workload:
         # state and next_op_versions side by side: one all_reduce(MAX) per step (latency-bound)
         self.dense = torch.zeros(2 * cap, dtype=torch.int64, device=dev)
         self.local_actor_bytes = b"".join(bytes(a) for a in self.actors_local)
-        self.fa = np.repeat(np.arange(self.per, dtype=np.uint32), self.versions)
-        self.fv = np.tile(np.arange(self.versions, dtype=np.uint64), self.per)
+        if fa_sel is not None:
+            self.fa, self.fv = fa_sel.astype(np.uint32), fv_sel.astype(np.uint64)
+        else:
+            self.fa = np.repeat(np.arange(self.per, dtype=np.uint32), self.versions)
+            self.fv = np.tile(np.arange(self.versions, dtype=np.uint64), self.per)
         # per-file metadata lives in HBM with the files (what Storage::load_ops hands over)
         self.fa_d = torch.from_numpy(self.fa.astype(np.int32)).to(dev)
         self.fv_d = torch.from_numpy(self.fv.astype(np.int64)).to(dev)
         self.out = {}
         self.paths = set()
+        self.sharded = None
+        if self.partition == "address":
+            self.sharded = shard.DeviceShardOps(self.core, self.local_actor_bytes, self.files, self.offs,
+                                                self.n, self.blob_len, self.fa_d, self.fv_d)
+        # files of the whole job (the ranks' counts differ slightly under the address partition)
+        tot = torch.tensor([self.n], dtype=torch.int64, device=dev)
+        if world > 1:
+            shard.all_reduce_(tot, dist.ReduceOp.SUM)
+        self.total_files = int(tot.item())
         # The SHA3-256 content name of step i's state file (host, ~0.2 MB) is computed on a host
         # thread while step i+1's kernels run; every name is done before the timed region ends.
         from concurrent.futures import ThreadPoolExecutor
@@ -267,12 +300,20 @@ class Workload:
             self.out["file"] = f
             self.names.append(self.namer.submit(crdtenc.content_name, f))
             return
-        rc = core.ingest_ops_device(self.files.data_ptr(), self.offs.data_ptr(), self.n,
-                                    self.blob_len, self.local_actor_bytes, self.fa_d.data_ptr(),
-                                    self.fv_d.data_ptr())
-        if rc:
-            raise crdtenc.CeError(rc, core.ctx.last_error())
-        self.paths.add(shard.exchange_vclock(core, self.dense))   # all_reduce(MAX) over RCCL
+        if self.sharded is not None:
+            # address partition: cross-rank version gate, pending fold, one all_reduce(MAX) of
+            # the dense batch with the failure flags (shard.ingest_sharded)
+            rc, path = shard.ingest_sharded(self.sharded)
+            if rc:
+                raise crdtenc.CeError(rc, core.ctx.last_error())
+            self.paths.add(path)
+        else:
+            rc = core.ingest_ops_device(self.files.data_ptr(), self.offs.data_ptr(), self.n,
+                                        self.blob_len, self.local_actor_bytes, self.fa_d.data_ptr(),
+                                        self.fv_d.data_ptr())
+            if rc:
+                raise crdtenc.CeError(rc, core.ctx.last_error())
+            self.paths.add(shard.exchange_vclock(core, self.dense))   # all_reduce(MAX) over RCCL
         if self.rank == 0:
             f, _ = core.compact_to_buffer(name=False)
             self.out["file"] = f
@@ -443,7 +484,7 @@ def kernel_summary(w, ms, kern):
     ops_per_file = 992 * -(-PT // 64) + 48 * (-(-PT // 16) + 1)
     valu = n * ops_per_file / avg_s / 1e12 if avg_s > 0 else 0.0
     bytes_per_launch = n * (PT + 16)              # read ct + tag; plaintext stays in LDS
-    return {"value": round(n * w.world / (ms / 1e3), 1), "ms_per_step": round(ms, 4),
+    return {"value": round(w.total_files / (ms / 1e3), 1), "ms_per_step": round(ms, 4),
             "avg_launch_ms": round(avg_s * 1e3, 4), "ops_per_file": ops_per_file,
             "valu_tops": round(valu, 2), "valu_frac": round(valu / VALU_PEAK_TOPS, 4),
             "hbm_GBps": round(bytes_per_launch / avg_s / 1e9, 1) if avg_s > 0 else None,
@@ -465,6 +506,9 @@ def main():
     ap.add_argument("--no-clock", action="store_true", help="skip the shader-clock probe")
     ap.add_argument("--no-host-buffers", action="store_true",
                     help="skip the end-to-end run from host buffers (H2D over PCIe)")
+    ap.add_argument("--partition", choices=("address", "actor"), default="address",
+                    help="N > 1: op files by address hash with the cross-rank gate (default), or "
+                         "whole writers per rank")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ:
@@ -507,6 +551,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu, cpu_ok = wa.cpu_baseline(args)
     paths_a = sorted(wa.paths)
+    wa_total = wa.total_files
     wa.close()
     del wa
 
@@ -565,13 +610,19 @@ def main():
             "data": "synthetic (GPU-sealed op files, seeded)",
             "config": {
                 "workload": "C2: 1,048,576 x 4 KiB encrypted GCounter op files per GPU "
-                            "(4096 actors x %d versions at N=%d, actor-sharded), decrypt + "
-                            "max-join + compact" % (args.versions * world, world),
-                "files_per_gpu": wa_n(args, world), "plaintext_bytes": pt_len("a"),
+                            "(4096 actors x %d versions at N=%d%s), decrypt + max-join + compact"
+                            % (args.versions * world, world,
+                               "" if world == 1 else ", %s-partitioned" % args.partition),
+                "files_per_gpu": wa_n(args, world), "files_total": wa_total,
+                "plaintext_bytes": pt_len("a"),
                 "dots_per_file": K_DOTS["a"], "actors": N_ACTORS,
-                "parallelism": ("actor-sharded files, all_reduce(MAX) of dense state (%s), "
-                                "exchange path %s" % (os.environ.get("CE_DIST_BACKEND", "nccl"),
-                                                       "/".join(paths_a)))
+                "parallelism": (("op files partitioned by address hash (ops/<actor>/<version>), "
+                                 "cross-rank version gate (per-writer stats all_reduce MAX), "
+                                 "pending batch + failure flags all_reduce(MAX) (%s), exchange "
+                                 "path %s" if args.partition == "address" else
+                                 "actor-sharded files, all_reduce(MAX) of dense state (%s), "
+                                 "exchange path %s") % (os.environ.get("CE_DIST_BACKEND", "nccl"),
+                                                        "/".join(paths_a)))
                                if world > 1 else "single GPU",
             },
             "aead_open_GBps": sa["aead_open_GBps"],

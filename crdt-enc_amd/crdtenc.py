@@ -20,8 +20,11 @@ STATUS_NAMES = {
     0: "OK", 1: "OUTER_LEN", 2: "OUTER_VERSION", 3: "KEY_VERSION", 4: "KEY_LEN",
     5: "PARSE_VBOX", 6: "DATA_VERSION", 7: "PARSE_ENCBOX", 8: "NONCE_LEN", 9: "AUTH",
     10: "PT_LEN", 11: "PT_VERSION", 12: "DECODE", 13: "OP_VERSION", 64: "INVALID_ARG",
-    65: "DEVICE", 66: "NO_KEY", 67: "IO", 68: "NO_LOCAL_META",
+    65: "DEVICE", 66: "NO_KEY", 67: "IO", 68: "NO_LOCAL_META", 69: "SHARD",
 }
+ERR_OP_VERSION, ERR_SHARD = 13, 69
+# window flags word (hi[m], include/crdtenc.h ce_core_shard_window)
+SHARD_BAD, SHARD_GAP, SHARD_E0_MISMATCH = 1, 2, 4
 STATE_VCLOCK, STATE_GCOUNTER, STATE_ORSWOT, STATE_MVREG = 0, 1, 2, 3
 OPEN_CREATE, COMPACT_INGEST_FORMAT, OPEN_MULTI_KEY = 1, 2, 4
 
@@ -50,7 +53,76 @@ EXPORTS = [
     "ce_keys_count", "ce_keys_latest", "ce_keys_get", "ce_keys_at", "ce_core_set_keys",
     "ce_core_apply_ops_batch", "ce_core_ingest_ops_iov", "ce_core_ingest_states_iov", "ce_core_compact_ops_iov",
     "ce_core_path_count", "ce_ctx_clock_probe",
+    "ce_shard_owner", "ce_shard_owners", "ce_shard_stats_len", "ce_core_shard_stats",
+    "ce_core_shard_window", "ce_core_ingest_ops_device_sharded", "ce_core_pending_export",
+    "ce_core_pending_commit", "ce_core_writer_versions", "ce_shard_stats_host",
+    "ce_shard_window_host", "ce_shard_window_exact",
 ]
+
+
+def _np_ptr(a, dtype):
+    import numpy as np
+    a = np.ascontiguousarray(a, dtype=dtype)
+    return a, ctypes.c_void_p(a.ctypes.data)
+
+
+def shard_owners(actors, file_actor, file_version, world):
+    """Owner rank of every op file ops/<actors[file_actor[i]]>/<file_version[i]> (numpy u32)."""
+    import numpy as np
+    n = len(file_actor)
+    acts = b"".join(bytes(a) for a in actors)
+    fa, fap = _np_ptr(file_actor, np.uint32)
+    fv, fvp = _np_ptr(file_version, np.uint64)
+    out = np.empty(max(n, 1), np.uint32)
+    rc = lib().ce_shard_owners(_cbuf(acts), ctypes.c_uint32(len(actors)), fap, fvp, ctypes.c_uint64(n),
+                               ctypes.c_uint32(world), ctypes.c_void_p(out.ctypes.data))
+    if rc:
+        raise CeError(rc, "ce_shard_owners")
+    return out[:n]
+
+
+def shard_stats_host(actors, e0, file_actor, file_version, rank, world):
+    """ShardStats (int64[2m + 3]) of one rank's host metadata (the CPU twin of the device pass)."""
+    import numpy as np
+    m = len(actors)
+    st = np.empty(lib().ce_shard_stats_len(m), np.int64)
+    e, ep = _np_ptr(e0, np.uint64)
+    fa, fap = _np_ptr(file_actor, np.uint32)
+    fv, fvp = _np_ptr(file_version, np.uint64)
+    rc = lib().ce_shard_stats_host(_cbuf(b"".join(bytes(a) for a in actors)), ctypes.c_uint32(m), ep, fap, fvp,
+                                   ctypes.c_uint64(len(fa)), ctypes.c_uint32(rank), ctypes.c_uint32(world),
+                                   ctypes.c_void_p(st.ctypes.data))
+    if rc:
+        raise CeError(rc, "ce_shard_stats_host")
+    return st
+
+
+def shard_window_host(e0, stats):
+    """(hi u64[m], flags) from reduced stats."""
+    import numpy as np
+    m = len(e0)
+    hi = np.empty(m + 1, np.uint64)
+    e, ep = _np_ptr(e0, np.uint64)
+    s, sp = _np_ptr(stats, np.int64)
+    rc = lib().ce_shard_window_host(ctypes.c_uint32(m), ep, sp, ctypes.c_void_p(hi.ctypes.data))
+    if rc:
+        raise CeError(rc, "ce_shard_window_host")
+    return hi[:m], int(hi[m])
+
+
+def shard_window_exact(e0, file_actor, file_version):
+    """(hi u64[m], flags) from every rank's gathered (writer, version) metadata."""
+    import numpy as np
+    m = len(e0)
+    hi = np.empty(m + 1, np.uint64)
+    e, ep = _np_ptr(e0, np.uint64)
+    fa, fap = _np_ptr(file_actor, np.uint32)
+    fv, fvp = _np_ptr(file_version, np.uint64)
+    rc = lib().ce_shard_window_exact(ctypes.c_uint32(m), ep, fap, fvp, ctypes.c_uint64(len(fa)),
+                                     ctypes.c_void_p(hi.ctypes.data))
+    if rc:
+        raise CeError(rc, "ce_shard_window_exact")
+    return hi[:m], int(hi[m])
 
 
 class CeError(RuntimeError):
@@ -101,6 +173,9 @@ def lib():
         L.ce_core_dense_capacity.restype = ctypes.c_uint32
         L.ce_keys_count.restype = ctypes.c_uint32
         L.ce_core_path_count.restype = ctypes.c_uint64
+        L.ce_shard_owner.restype = ctypes.c_uint32
+        L.ce_shard_owner.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32]
+        L.ce_shard_stats_len.restype = ctypes.c_uint32
         L.ce_vbuf_remaining.restype = ctypes.c_size_t
         L.ce_vbuf_chunk.restype = ctypes.c_size_t
         L.ce_vbuf_chunks_vectored.restype = ctypes.c_size_t
@@ -668,6 +743,47 @@ class Core:
     def export_dense(self, d_state, d_nov):
         self.ctx.check(lib().ce_core_export_dense(self.p, ctypes.c_void_p(d_state),
                                                   ctypes.c_void_p(d_nov)), "export_dense")
+
+    # ---- multi-GPU partition by op-file address (include/crdtenc.h, shard.ingest_sharded) ----
+    def shard_stats(self, actors, d_fa, d_fv, n, rank, world, d_stats):
+        self.ctx.check(lib().ce_core_shard_stats(self.p, _ptr(actors)[0], ctypes.c_uint32(len(actors) // 16),
+                                                 ctypes.c_void_p(d_fa), ctypes.c_void_p(d_fv),
+                                                 ctypes.c_uint32(n), ctypes.c_uint32(rank),
+                                                 ctypes.c_uint32(world), ctypes.c_void_p(d_stats)),
+                       "shard_stats")
+
+    def shard_window(self, actors, d_stats, d_hi):
+        self.ctx.check(lib().ce_core_shard_window(self.p, _ptr(actors)[0], ctypes.c_uint32(len(actors) // 16),
+                                                  ctypes.c_void_p(d_stats), ctypes.c_void_p(d_hi)),
+                       "shard_window")
+
+    def ingest_ops_device_sharded(self, d_blob, d_offs, n, blob_len, actors, d_fa, d_fv, d_hi,
+                                  want_status=False):
+        st = (ctypes.c_int32 * max(n, 1))() if want_status else None
+        rc = lib().ce_core_ingest_ops_device_sharded(
+            self.p, ctypes.c_void_p(d_blob), ctypes.c_void_p(d_offs), ctypes.c_uint32(n),
+            ctypes.c_uint64(blob_len), _ptr(actors)[0], ctypes.c_uint32(len(actors) // 16),
+            ctypes.c_void_p(d_fa), ctypes.c_void_p(d_fv), ctypes.c_void_p(d_hi), st)
+        return (rc, list(st)[:n]) if want_status else rc
+
+    def pending_export(self, d_batch):
+        ready = ctypes.c_int(0)
+        self.ctx.check(lib().ce_core_pending_export(self.p, ctypes.c_void_p(d_batch), ctypes.byref(ready)),
+                       "pending_export")
+        return ready.value == 1
+
+    def pending_commit(self, accept, d_import=None):
+        self.ctx.check(lib().ce_core_pending_commit(self.p, 1 if accept else 0,
+                                                    ctypes.c_void_p(d_import) if d_import else None),
+                       "pending_commit")
+
+    def writer_versions(self, actors):
+        import numpy as np
+        m = len(actors) // 16
+        out = np.zeros(max(m, 1), np.uint64)
+        self.ctx.check(lib().ce_core_writer_versions(self.p, _ptr(actors)[0], ctypes.c_uint32(m),
+                                                     ctypes.c_void_p(out.ctypes.data)), "writer_versions")
+        return out[:m]
 
     def import_dense(self, d_state, d_nov):
         self.ctx.check(lib().ce_core_import_dense(self.p, ctypes.c_void_p(d_state),

@@ -401,6 +401,71 @@ CE_HD uint32_t actor_hash(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
   return h;
 }
 
+// ---------------------------------------------------------------------------------------
+// Multi-GPU partition of op files (VClock / GCounter): an op file is addressed by its path
+// ops/<actor>/<version> (crdt-enc-tokio/src/lib.rs:280-293; op files are not content-named,
+// SURVEY F8), and its owner rank is a hash of that address, so every rank -- and the storage
+// listing -- agrees on the partition without reading a file.  Each rank folds only its files;
+// the version gate (crdt-enc/src/lib.rs:519-531) becomes per-writer windows [e0, hi) agreed
+// through one all_reduce(MAX) of ShardStats (ce_shard.hip / ce_shard.cpp).
+// ---------------------------------------------------------------------------------------
+CE_HD uint64_t shard_mix64(uint64_t x) {
+  x ^= x >> 31;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 29;
+  x *= 0x94D049BB133111EBull;
+  x ^= x >> 32;
+  return x;
+}
+// owner rank of ops/<actor>/<version> among `world` ranks (multiply-shift range reduction)
+CE_HD uint32_t shard_owner(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3, uint64_t v,
+                           uint32_t world) {
+  const uint64_t a = ((uint64_t)k1 << 32 | k0) * 0x9E3779B97F4A7C15ull ^ ((uint64_t)k3 << 32 | k2);
+  const uint64_t x = shard_mix64(a ^ shard_mix64(v + 0xD1B54A32D192ED03ull));
+  return (uint32_t)(((x & 0xffffffffull) * world) >> 32);
+}
+// ShardStats: int64[2m + 3] per rank, reduced with all_reduce(MAX).  Every word is a u64 with
+// its top bit flipped (u64 order == int64 order):
+//   [a]       ~cand[a]: cand = the smallest version >= e0[a] that this rank owns and does not
+//             hold (MAX of ~cand = the global MIN: the first missing version of writer a)
+//   [m + a]   vmax[a] + 1 over held versions >= e0[a] (0: none)
+//   [2m]      1 when a rank's batch breaks the contract (a writer split into several runs,
+//             versions descending inside a run, a file the partition gives to another rank, a
+//             walk past kShardWalkLimit): the windows are then computed exactly from the
+//             gathered metadata instead (ce_shard_window_exact)
+//   [2m + 1]  h(e0), [2m + 2] ~h(e0): MAX(h) == ~MAX(~h) iff every rank started from the same
+//             next_op_versions (the partition needs the replicated starting state)
+static constexpr uint64_t kShardFlip = 0x8000000000000000ull;
+static constexpr uint64_t kShardWalkLimit = 1u << 16;
+// window flags word (hi[m]): bit 0 = contract broken (exact fallback), bit 1 = a gap (the fold
+// stops there, CE_ERR_OP_VERSION), bit 2 = the ranks' next_op_versions differ
+static constexpr uint64_t kShardBad = 1, kShardGap = 2, kShardE0Mismatch = 4;
+CE_HD uint64_t shard_e0_hash(const uint64_t* e0, uint32_t m) {
+  uint64_t h = 0x243F6A8885A308D3ull ^ m;
+  for (uint32_t a = 0; a < m; a++) h = shard_mix64(h ^ e0[a]) + a;
+  return h;
+}
+// windows from the reduced stats (plain u64, flips removed): hi[a] = the end of writer a's
+// applied versions, hi[m] = flags.  The reference's loop over the batch in (writer, version)
+// order applies every version from e0 while they are consecutive; the first writer (in the
+// shared writer order) whose run has a missing version below its largest held one stops the
+// fold there: its versions up to the hole are applied, later writers get nothing (lib.rs:
+// 519-531, the error returned after the files before it are folded).
+template <typename Get>
+CE_HD uint32_t shard_first_gap(uint32_t m, Get&& cand_vmaxp1) {
+  for (uint32_t a = 0; a < m; a++) {
+    uint64_t cand, vmaxp1;
+    cand_vmaxp1(a, &cand, &vmaxp1);
+    if (vmaxp1 != 0 && cand < vmaxp1) return a;
+  }
+  return m;
+}
+CE_HD uint64_t shard_hi(uint32_t a, uint32_t astar, uint64_t e0, uint64_t cand, uint64_t vmaxp1) {
+  if (a > astar) return e0;
+  if (a == astar) return cand;          // cand >= e0: versions e0..cand-1 are all held somewhere
+  return vmaxp1 > e0 ? vmaxp1 : e0;     // no hole below vmax: e0..vmax all applied
+}
+
 // one actor-table entry: 16-byte UUID key + occupancy (32 bytes, two dwordx4 loads)
 struct alignas(16) ActorSlot {
   uint32_t k[4];

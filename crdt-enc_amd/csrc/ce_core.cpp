@@ -12,6 +12,7 @@
 #include <set>
 
 #include "ce_core.h"
+#include "ce_shard.h"
 
 using namespace ce;
 
@@ -648,9 +649,13 @@ int retry_alt_keys(ce_core* c, DecodeArgs& da, const uint8_t* d_blob, const uint
 int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
                         uint64_t blob_len, const uint8_t* actors, uint32_t m, const uint32_t* d_fa,
                         const uint64_t* d_fv, int32_t* status_out, const AfterCommit* after_commit,
-                        bool* merged_out) {
+                        bool* merged_out, const uint64_t* shard_hi = nullptr) {
   if (merged_out) *merged_out = false;
   ce_ctx* ctx = c->ctx;
+  // sharded (shard_hi): the gate is the agreed windows, and nothing is committed -- the batch
+  // stays in d_batch for ce_core_pending_commit (cross-rank all-or-nothing)
+  const bool sharded = shard_hi != nullptr;
+  c->pending = false;
   if (!c->has_key) return ctx->fail(CE_ERR_NO_KEY, "no latest key");
   if (n == 0) return CE_OK;
   if (is_dotset_kind(c->kind))
@@ -735,7 +740,9 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
     return ctx->hip_fail(e, "gate upload");
   {
     const int t = ctx->tbegin("gate");
-    if ((e = launch_gate(ctx->stream, ga))) return ctx->hip_fail(e, "gate");
+    if ((e = sharded ? launch_gate_window(ctx->stream, ga, shard_hi, ctx->counters.as<uint32_t>())
+                     : launch_gate(ctx->stream, ga)))
+      return ctx->hip_fail(e, "gate");
     ctx->tend(t);
   }
   DecodeArgs da{};
@@ -836,7 +843,7 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
   if ((rc = run_fold(nullptr))) return rc;
   // commit on the device unless the counters flag a slow path (k_merge_max_if), then one read
   // of the counters and of the gate's next_op_versions
-  {
+  if (!sharded) {
     const int t = ctx->tbegin("merge");
     if ((e = launch_merge_max_if(ctx->stream, c->d_state.as<unsigned long long>(),
                                  c->d_batch.as<unsigned long long>(), c->cap,
@@ -878,7 +885,11 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
   if ((e = hipMemcpyAsync(hc, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->stream)) ||
       (e = ctx->sync_spin()))
     return ctx->hip_fail(e, "fold sync");
-  const bool merged_on_device = (hc[2] | hc[3] | hc[4] | hc[7] | hc[8] | hc[12]) == 0;
+  const bool merged_on_device = !sharded && (hc[2] | hc[3] | hc[4] | hc[7] | hc[8] | hc[12]) == 0;
+  if (sharded && (hc[10] & (kShardBad | kShardE0Mismatch)))
+    return ctx->fail(CE_ERR_SHARD, hc[10] & kShardE0Mismatch
+                                       ? "ranks started from different next_op_versions"
+                                       : "a rank's batch breaks the partition contract: exact windows needed");
   if (merged_out) *merged_out = merged_on_device;
   if (hc[11]) c->path_counts["segdec_records"] += hc[11];
   if (hc[14]) c->path_counts["segdec_fallback"] += hc[14];
@@ -994,6 +1005,21 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
   if (first != CE_OK) return first;  // all-or-nothing: batch state discarded (lib.rs:497-514)
 
   // 5) commit: state = max(state, batch); next_op_versions from the gate
+  if (sharded) {  // pending until ce_core_pending_commit: the windows' next_op_versions
+    std::vector<uint64_t> nn(m);
+    if ((e = hipMemcpyAsync(nn.data(), gbase + 16ull * m, m * 8ull, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+      return ctx->hip_fail(e, "nov");
+    c->pending_nov.clear();
+    for (uint32_t a = 0; a < m; a++) {
+      Uuid u;
+      std::memcpy(u.data(), actors + 16ull * a, 16);
+      c->pending_nov.push_back({u, std::max(expect[a], nn[a])});
+    }
+    c->pending = true;
+    c->pending_gen = c->table_gen;
+    return (hc[10] & kShardGap) ? CE_ERR_OP_VERSION : CE_OK;
+  }
   if (merged_on_device) {
     for (uint32_t a = 0; a < m; a++) expect[a] = std::max(expect[a], hnov[a]);
   } else {
@@ -1023,13 +1049,20 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
 int ingest_ops_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
                    uint64_t blob_len, const uint8_t* actors, uint32_t m, const uint32_t* d_fa,
                    const uint64_t* d_fv, int32_t* status_out, const AfterCommit* after_commit = nullptr,
-                   bool* merged_out = nullptr) {
+                   bool* merged_out = nullptr, const uint64_t* shard_hi = nullptr) {
   for (int pass = 0;; pass++) {
     int rc = ingest_ops_dev_once(c, d_blob, d_offs, n, blob_len, actors, m, d_fa, d_fv, status_out,
-                                 after_commit, merged_out);
+                                 after_commit, merged_out, shard_hi);
     if (rc != kRestartIngest) return rc;
     if (pass > 8) return c->ctx->fail(CE_ERR_DEVICE, "actor table did not converge");
   }
+}
+
+int ingest_ops_dev_sharded(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
+                           uint64_t blob_len, const uint8_t* actors, uint32_t m, const uint32_t* d_fa,
+                           const uint64_t* d_fv, const uint64_t* shard_hi, int32_t* status_out) {
+  return ingest_ops_dev(c, d_blob, d_offs, n, blob_len, actors, m, d_fa, d_fv, status_out, nullptr,
+                        nullptr, shard_hi);
 }
 
 // host metadata -> device, then ingest_ops_dev

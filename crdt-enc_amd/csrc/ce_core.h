@@ -87,6 +87,13 @@ struct ce_core {
   std::set<std::string> read_states;  // lib.rs:205
   ce_ctx* aux = nullptr;              // single-file work during a batch (exotic envelopes)
   ce::DsState* ds = nullptr;          // Orswot / MVReg state (dot-set kinds only)
+  // sharded ingest (ce_core_ingest_ops_device_sharded): the batch is folded into d_batch and
+  // held there with its next_op_versions until ce_core_pending_commit
+  bool pending = false;
+  uint64_t pending_gen = 0;                                  // table_gen of the pending batch
+  std::vector<std::pair<ce::Uuid, uint64_t>> pending_nov;    // (writer, next_op_version)
+  ce::DevBuf d_shard;                  // writer UUIDs | e0 | stats scratch (ce_core_shard_*)
+  std::vector<uint8_t> shard_writers;  // the writer list d_shard holds
 };
 
 namespace ce {
@@ -168,6 +175,12 @@ int resolve_host_parse(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs
 uint32_t host_gate(const uint32_t* fa, const uint64_t* fv, uint32_t n, std::vector<uint64_t>* expect,
                    uint8_t* apply);
 int merge_dots_host(ce_core* c, const Dots& dots);
+// read_remote_ops over a batch resident in HBM (ce_core.cpp).  shard_hi (device, m + 1 words):
+// the sharded gate's windows and flags (ce_shard.hip) instead of the local gate; the batch is
+// then left pending (not committed) for ce_core_pending_commit.
+int ingest_ops_dev_sharded(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
+                           uint64_t blob_len, const uint8_t* actors, uint32_t m, const uint32_t* d_fa,
+                           const uint64_t* d_fv, const uint64_t* shard_hi, int32_t* status_out);
 
 // dot-set kinds (ce_dotset_host.cpp): same contracts as the VClock/GCounter paths in ce_core.cpp
 int ds_init(ce_core* c);

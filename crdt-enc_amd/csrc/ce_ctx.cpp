@@ -256,6 +256,7 @@ const char* ce_status_str(int s) {
     case CE_ERR_NO_KEY: return "no latest key";
     case CE_ERR_IO: return "io error";
     case CE_ERR_NO_LOCAL_META: return "local meta does not exist, and `create` option is not set";
+    case CE_ERR_SHARD: return "sharded ingest: partition contract broken or next_op_versions differ";
     default: return "unknown";
   }
 }

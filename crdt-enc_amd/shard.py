@@ -1,14 +1,21 @@
 """Multi-GPU layout of the ingest path (one process per GPU, torch.distributed).
 
-Files are sharded by writer actor: every version of an actor goes to one rank, in order.  The
-version gate (crdt-enc/src/lib.rs:519-531) then only needs rank-local state.  After each rank has
-folded its shard, the partial states meet in ONE exchange: VClock/GCounter merge is a pointwise
-max (crdts VClock::merge; GCounter::merge delegates to it), so the dense actor-indexed arrays
-(batch state and next_op_versions, exported with Core.export_dense over slots registered
-identically on every rank) are combined with all_reduce(MAX).  Over RCCL that is one 64 KiB
-latency-bound message per array on xGMI; with gloo it runs the same code on CPU tensors.  A
-Dot naming an actor outside the registered slots sends every rank to the all-gather of
-serialized partial states instead (exchange_vclock).
+VClock / GCounter: files are partitioned by ADDRESS (north star: "sharded by content hash").  An
+op file is addressed by its path ops/<actor>/<version> (crdt-enc-tokio/src/lib.rs:280-293; op
+files are not content-named), and its owner rank is a hash of that address
+(crdtenc.shard_owners / ce_shard_owner), so one writer's run is spread over every rank and the
+bytes balance however skewed the writers are.  The version gate (crdt-enc/src/lib.rs:519-531)
+is then agreed across ranks before the fold (ingest_sharded): each rank's per-writer statistics
+-- the first version >= e0 it owns but does not hold, the largest version it holds -- meet in
+one all_reduce(MAX), every rank derives the same windows [e0, hi) from them, and folds exactly
+the files the reference's single loop would.  The folded batch stays pending until a second
+all_reduce(MAX) of the dense batch carries every rank's failure status too: any failure leaves
+every rank's state unchanged (lib.rs:497-514), otherwise each rank commits the reduced batch.
+A Dot naming an actor outside the registered slots sends every rank to the all-gather of
+serialized states instead.
+
+Writer sharding (actor_range / file_rank) is kept for the dot-set kinds (below) and as the
+previous layout of the VClock path (exchange_vclock after a local ingest).
 
 Counters are u64 but the collective's MAX is signed int64: the sign bit is flipped before and
 after the reduce, which maps u64 order onto i64 order (values >= 2^63 stay correctly ordered).
@@ -131,3 +138,127 @@ def exchange_dotset(core, group=None, device="cpu"):
             if rc:
                 raise RuntimeError("merge_state of rank %d failed: %d" % (r, rc))
     return core
+
+
+# ---------------------------------------------------------------------------------------------
+# VClock / GCounter partitioned by op-file address: the cross-rank version gate
+# ---------------------------------------------------------------------------------------------
+ERR_OP_VERSION, ERR_SHARD = 13, 69
+SHARD_BAD, SHARD_GAP, SHARD_E0_MISMATCH = 1, 2, 4
+
+
+class DeviceShardOps:
+    """The sharded-ingest steps of a crdtenc.Core over this rank's batch resident in HBM
+    (torch tensors: files u8, offs i64[n+1], fa i32[n] into the shared writer list, fv i64[n])."""
+
+    def __init__(self, core, actors, files, offs, n, blob_len, fa, fv):
+        self.core, self.actors = core, actors
+        self.files, self.offs, self.n, self.blob_len, self.fa, self.fv = files, offs, n, blob_len, fa, fv
+        self.m = len(actors) // 16
+        self.device = fa.device
+        self.stats = torch.empty(2 * self.m + 3, dtype=torch.int64, device=self.device)
+        self.hi = torch.empty(self.m + 1, dtype=torch.int64, device=self.device)
+        self.dense = torch.empty(core.dense_capacity() + 2, dtype=torch.int64, device=self.device)
+
+    def compute_stats(self, rank, world):
+        self.core.shard_stats(self.actors, self.fa.data_ptr(), self.fv.data_ptr(), self.n, rank, world,
+                              self.stats.data_ptr())
+        return self.stats
+
+    def window(self):
+        self.core.shard_window(self.actors, self.stats.data_ptr(), self.hi.data_ptr())
+        return self.hi
+
+    def set_window(self, hi, flags):
+        import numpy as np
+        h = np.append(np.asarray(hi, np.uint64), np.uint64(flags)).view(np.int64)
+        self.hi.copy_(torch.from_numpy(h))
+
+    def metadata(self):
+        return self.fa[: self.n].cpu().numpy().astype("uint32"), self.fv[: self.n].cpu().numpy().astype("uint64")
+
+    def writer_versions(self):
+        return self.core.writer_versions(self.actors)
+
+    def ingest(self):
+        return self.core.ingest_ops_device_sharded(self.files.data_ptr(), self.offs.data_ptr(), self.n,
+                                                   self.blob_len, self.actors, self.fa.data_ptr(),
+                                                   self.fv.data_ptr(), self.hi.data_ptr())
+
+    def dense_buffer(self):
+        self.dense.zero_()
+        return self.dense
+
+    def export_pending(self, dense):
+        if dense.dtype != torch.int64:
+            raise TypeError("dense is an int64 view of u64")
+        return self.core.pending_export(dense.data_ptr())
+
+    def commit(self, accept, reduced=None):
+        self.core.pending_commit(accept, reduced.data_ptr() if reduced is not None else None)
+
+
+def _gather_metadata(fa, fv, group=None):
+    """Every rank's (writer, version) metadata, concatenated (the exact fallback's input)."""
+    import numpy as np
+    blob = np.concatenate([np.asarray(fa, np.uint32).view(np.uint8),
+                           np.asarray(fv, np.uint64).view(np.uint8)]).tobytes()
+    parts = all_gather_bytes(blob, group=group)
+    fas, fvs = [], []
+    for p in parts:
+        k = len(p) // 12
+        fas.append(np.frombuffer(p[: 4 * k], np.uint32))
+        fvs.append(np.frombuffer(p[4 * k:], np.uint64))
+    return np.concatenate(fas), np.concatenate(fvs)
+
+
+def ingest_sharded(ops, group=None, exchange_bytes=None):
+    """read_remote_ops (crdt-enc/src/lib.rs:471-547) over a batch partitioned across the ranks by
+    op-file address.  `ops`: a DeviceShardOps (or the CPU test's twin).  Every rank ends with the
+    state the reference reaches folding the whole batch in (shared writer order, version) order.
+    Returns (rc, path): rc 0, CE_ERR_OP_VERSION (the fold stopped at a gap; the files before it
+    are folded on every rank) or the failing status (every rank's state unchanged); path
+    "dense" | "bytes" (state all-gather) | "rejected", plus "+exact" when the windows came from
+    the gathered metadata."""
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    # 1) the gate: per-writer stats, one all_reduce(MAX), identical windows on every rank
+    stats = ops.compute_stats(rank, world)
+    all_reduce_(stats, dist.ReduceOp.MAX, group=group)
+    ops.window()
+    rc = ops.ingest()
+    exact = ""
+    if rc == ERR_SHARD:
+        # a rank's batch breaks the partition contract (same flags on every rank, from the
+        # reduced stats): the windows from everyone's metadata, the reference loop on the host
+        import crdtenc
+        e0 = ops.writer_versions()
+        fa, fv = ops.metadata()
+        fa_all, fv_all = _gather_metadata(fa, fv, group=group)
+        hi, flags = crdtenc.shard_window_exact(e0, fa_all, fv_all)
+        ops.set_window(hi, flags)
+        rc = ops.ingest()
+        exact = "+exact"
+        if rc == ERR_SHARD:
+            raise RuntimeError("sharded ingest refused its exact windows (next_op_versions differ "
+                               "across ranks?)")
+    # 2) all-or-nothing + exchange: the pending batch and the failure flags in one all_reduce
+    failed = rc not in (0, ERR_OP_VERSION)
+    dense = ops.dense_buffer()
+    cap = dense.numel() - 2
+    ready = ops.export_pending(dense[:cap]) if not failed else True
+    flags = torch.tensor([rc if failed else 0, 0 if ready else 1], dtype=torch.int64)
+    dense[cap:].copy_(flags.to(dense.device))
+    merge_dense(dense, group=group)
+    code, not_ready = (int(x) for x in dense[cap:].cpu().tolist())
+    if code:
+        if not failed:
+            ops.commit(False)
+        return code, "rejected" + exact
+    if not_ready:
+        ops.commit(True)
+        (exchange_bytes or exchange_dotset)(ops.core, group=group,
+                                            device="cpu" if dist.get_backend(group) == "gloo" else dense.device)
+        return rc, "bytes" + exact
+    ops.commit(True, dense[:cap])
+    return rc, "dense" + exact
+

@@ -45,7 +45,10 @@ enum ce_status {
   CE_ERR_DEVICE = 65,       /* HIP runtime failure / no GPU: the product has no CPU path       */
   CE_ERR_NO_KEY = 66,       /* "no latest key" (lib.rs:420,490)                                */
   CE_ERR_IO = 67,
-  CE_ERR_NO_LOCAL_META = 68 /* "local meta does not exist, and `create` option is not set"     */
+  CE_ERR_NO_LOCAL_META = 68, /* "local meta does not exist, and `create` option is not set"    */
+  CE_ERR_SHARD = 69          /* sharded ingest: a rank's batch breaks the partition contract (the
+                                windows must come from ce_shard_window_exact) or the ranks'
+                                next_op_versions differ                                        */
 };
 
 typedef struct ce_buf {
@@ -320,6 +323,61 @@ int ce_core_import_dense(ce_core *c, const uint64_t *d_state, const uint64_t *d_
  * register_actors -- VClock::apply takes any actor, lib.rs:533-535).  Ranks then exchange
  * ce_core_state_bytes + ce_core_merge_state instead (crdtenc shard.exchange_vclock). */
 int ce_core_dense_ready(ce_core *c);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Multi-GPU partition of VClock / GCounter op files (one process per GPU).  North star: files */
+/* sharded by address across the GPUs.  An op file's address is its path ops/<actor>/<version> */
+/* (crdt-enc-tokio/src/lib.rs:280-293; op files are not content-named): its owner   */
+/* rank is a hash of it, so every rank (and a directory listing) agrees on the partition.     */
+/* Replaces, across ranks, the version gate of read_remote_ops (crdt-enc/src/lib.rs:516-544).  */
+/* ---------------------------------------------------------------------------------------- */
+/* owner rank of ops/<actor>/<version> among `world` ranks */
+uint32_t ce_shard_owner(const uint8_t actor[16], uint64_t version, uint32_t world);
+/* owner_out[i] = ce_shard_owner(actors[file_actor[i]], file_version[i], world) */
+int ce_shard_owners(const uint8_t *actors, uint32_t m, const uint32_t *file_actor,
+                    const uint64_t *file_version, uint64_t n, uint32_t world, uint32_t *owner_out);
+/* ShardStats words for m writers (2m + 3 int64; layout in csrc/ce_common.h) */
+uint32_t ce_shard_stats_len(uint32_t m);
+/* This rank's ShardStats over its batch, resident in HBM (d_fa indexes the writer list shared by
+ * every rank, in that shared order; each writer's files one run of ascending versions, as
+ * Storage::load_ops returns them, storage.rs:36-40).  The stats are complete on return; the
+ * ranks then all_reduce(MAX) them (int64). */
+int ce_core_shard_stats(ce_core *c, const uint8_t *actors, uint32_t m, const uint32_t *d_fa,
+                        const uint64_t *d_fv, uint32_t n, uint32_t rank, uint32_t world,
+                        int64_t *d_stats);
+/* The windows from the reduced stats: d_hi[a] = end of writer a's applied versions (from its
+ * next_op_versions), d_hi[m] = flags (1 contract broken, 2 gap, 4 ranks' next_op_versions
+ * differ).  Queued on the context's stream. */
+int ce_core_shard_window(ce_core *c, const uint8_t *actors, uint32_t m, const int64_t *d_stats,
+                         uint64_t *d_hi);
+/* read_remote_ops over this rank's files with the windows as the gate: every file with
+ * e0 <= version < hi is folded, into a PENDING batch -- nothing is committed until
+ * ce_core_pending_commit, so a failure on any rank can leave every rank's state unchanged
+ * (lib.rs:497-514).  Returns CE_OK, the lowest failing file's status, CE_ERR_OP_VERSION when the
+ * windows stop at a gap (the files before it are folded, lib.rs:527-531), or CE_ERR_SHARD (flags
+ * 1 or 4: nothing folded; compute the windows with ce_shard_window_exact and call again). */
+int ce_core_ingest_ops_device_sharded(ce_core *c, const uint8_t *d_blob, const uint64_t *d_offs,
+                                      uint32_t n, uint64_t blob_len, const uint8_t *actors,
+                                      uint32_t m, const uint32_t *d_fa, const uint64_t *d_fv,
+                                      const uint64_t *d_hi, int32_t *status);
+/* The pending batch as a dense u64[ce_core_dense_capacity] over the registered slots (for the
+ * all_reduce(MAX)); *ready = 0 when it names an actor outside register_actors (then commit it
+ * locally and exchange serialized states instead). */
+int ce_core_pending_export(ce_core *c, uint64_t *d_batch, int *ready);
+/* accept: state = max(state, d_import ? d_import (the reduced batch) : the local pending batch),
+ * next_op_versions from the windows; !accept: drop the pending batch. */
+int ce_core_pending_commit(ce_core *c, int accept, const uint64_t *d_import);
+/* next_op_versions.get(writer) for each of m writers (host) */
+int ce_core_writer_versions(ce_core *c, const uint8_t *actors, uint32_t m, uint64_t *e0_out);
+/* Host twins (CPU ranks, tests): ShardStats over host metadata; the windows from reduced stats;
+ * the exact windows from every rank's gathered (writer, version) metadata -- the reference's
+ * loop over the batch in (writer, version) order (lib.rs:516-544). */
+int ce_shard_stats_host(const uint8_t *actors, uint32_t m, const uint64_t *e0, const uint32_t *fa,
+                        const uint64_t *fv, uint64_t n, uint32_t rank, uint32_t world,
+                        int64_t *stats);
+int ce_shard_window_host(uint32_t m, const uint64_t *e0, const int64_t *stats, uint64_t *hi);
+int ce_shard_window_exact(uint32_t m, const uint64_t *e0, const uint32_t *fa, const uint64_t *fv,
+                          uint64_t n, uint64_t *hi);
 
 /* Diagnostics: how many times a code path ran on this core ("states_device_read",
  * "states_host_parse", "compact_device_writer"; per multi-segment op file "segdec_records"

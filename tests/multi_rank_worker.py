@@ -6,7 +6,9 @@ Writes the merged StateWrapper bytes and the path taken to <out>.<rank>.
 
   python tests/multi_rank_worker.py RANK WORLD PORT MODE OUT
     MODE: registered | unregistered (GCounter, exchange_vclock) | orswot (Orswot<u64, Uuid>,
-    shard.exchange_dotset: the all-gather of partial StateWrappers + the GPU Orswot::merge)
+    shard.exchange_dotset: the all-gather of partial StateWrappers + the GPU Orswot::merge) |
+    sharded:<scenario> (GCounter partitioned by address, shard.ingest_sharded; scenarios of
+    tests/test_shard.py)
 """
 import os
 import random
@@ -89,9 +91,47 @@ def main_orswot(rank, world, out):
     ctx.close()
 
 
+def main_sharded(rank, world, name, out):
+    """shard.ingest_sharded through the C ABI: this rank's share (by address) of the scenario's
+    op files resident in HBM, the device gate kernels, the pending fold, the dense exchange."""
+    import msgpack
+    import numpy as np
+    import torch
+    import crdtenc
+    import shard
+    from test_shard import _scenario
+    key, writers, registered, files, fa, fv, pre = _scenario(name)
+    own = crdtenc.shard_owners(writers, fa, fv, world)
+    if name == "contract":
+        own[11] = (own[11] + 1) % world
+    ctx = crdtenc.Context(0)
+    core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+    core.set_latest_key(key)
+    core.register_actors(registered)
+    first = [i for i in range(len(files)) if fv[i] < pre[fa[i]]]
+    if first:  # the replicated starting state
+        rc, _ = core.ingest_ops([files[i] for i in first], writers, [fa[i] for i in first], [fv[i] for i in first])
+        assert rc == 0, rc
+    sel = [i for i in range(len(files)) if own[i] == rank]
+    blob = b"".join(files[i] for i in sel)
+    offs = np.zeros(len(sel) + 1, np.int64)
+    offs[1:] = np.cumsum([len(files[i]) for i in sel])
+    dev = torch.device("cuda", 0)
+    d_files = torch.frombuffer(bytearray(blob + bytes(64)), dtype=torch.uint8).to(dev)
+    d_offs = torch.from_numpy(offs).to(dev)
+    d_fa = torch.tensor([fa[i] for i in sel], dtype=torch.int32, device=dev)
+    d_fv = torch.tensor([fv[i] for i in sel], dtype=torch.int64, device=dev)
+    ops = shard.DeviceShardOps(core, b"".join(writers), d_files, d_offs, len(sel), len(blob), d_fa, d_fv)
+    rc, path = shard.ingest_sharded(ops)
+    with open("%s.%d" % (out, rank), "wb") as f:
+        f.write(msgpack.packb([rc, path, len(sel), core.state_bytes()], use_bin_type=True))
+    core.close()
+    ctx.close()
+
+
 def main():
     rank, world, port, mode, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5]
-    if mode == "orswot":
+    if mode == "orswot" or mode.startswith("sharded:"):
         sys.path.insert(0, os.path.join(REPO, "tests"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
     import torch
@@ -102,6 +142,9 @@ def main():
     try:
         if mode == "orswot":
             main_orswot(rank, world, out)
+            return
+        if mode.startswith("sharded:"):
+            main_sharded(rank, world, mode.split(":", 1)[1], out)
             return
         key, actors, files, fa, fv = workload(mode)
         ctx = crdtenc.Context(0)
