@@ -21,11 +21,13 @@ Counters are u64 but the collective's MAX is signed int64: the sign bit is flipp
 after the reduce, which maps u64 order onto i64 order (values >= 2^63 stay correctly ordered).
 
 Orswot / MVReg (dot sets) do not reduce pointwise: each rank serializes its partial
-StateWrapper, the byte strings are all-gathered (one length exchange + one padded all_gather),
-and every rank merges the others' partial states with Core.merge_state -- the CvRDT merge
+StateWrapper and the partial states are merged with Core.merge_state -- the CvRDT merge
 read_remote_states applies to state files (crdt-enc/src/lib.rs:458-466), run by the GPU merge
-kernel.  Sharding by writer keeps every actor's ops on one rank, so each partial state is an
-op-based replica of that shard and the merge equals one fold over all files.
+kernel -- along a binomial tree to the compacting rank (reduce_dotset: at most ceil(log2 N)
+merges per rank; exchange_dotset, the all-gather to every rank, is kept for callers that need
+the merged state everywhere).  Sharding by writer keeps every actor's ops on one rank, so each
+partial state is an op-based replica of that shard and the merge equals one fold over all files
+(SURVEY.md §8e).
 """
 import torch
 import torch.distributed as dist
@@ -125,6 +127,77 @@ def all_gather_bytes(data, group=None, device="cpu"):
     parts = [torch.empty(width, dtype=torch.uint8, device=device) for _ in range(world)]
     dist.all_gather(parts, buf, group=group)
     return [bytes(p[:k].cpu().numpy().tobytes()) for p, k in zip(parts, lens)]
+
+
+def _send_bytes(data, dst, group=None, device="cpu"):
+    n = torch.tensor([len(data)], dtype=torch.int64, device=device)
+    dist.send(n, dst, group=group)
+    if data:
+        dist.send(torch.frombuffer(bytearray(data), dtype=torch.uint8).to(device), dst, group=group)
+
+
+def _recv_bytes(src, group=None, device="cpu"):
+    n = torch.zeros(1, dtype=torch.int64, device=device)
+    dist.recv(n, src, group=group)
+    k = int(n.item())
+    if not k:
+        return b""
+    buf = torch.empty(k, dtype=torch.uint8, device=device)
+    dist.recv(buf, src, group=group)
+    return bytes(buf.cpu().numpy().tobytes())
+
+
+def _global(group, r):
+    """dist.send / recv take global ranks"""
+    return r if group is None else dist.get_global_rank(group, r)
+
+
+def reduce_dotset(core, group=None, device="cpu", dst=0):
+    """Merge the partial Orswot / MVReg states of all ranks into rank `dst`'s `core` along a
+    binomial tree: in round k (k = 0, 1, ...) the rank at distance 2^k above a multiple of
+    2^(k+1) sends its (already merged) StateWrapper to that multiple, which merge_states it (the
+    CvRDT merge of read_remote_states, crdt-enc/src/lib.rs:458-466, on the GPU).  Only the
+    compacting rank ends with the whole state; every rank does at most ceil(log2 N) merges and
+    each state crosses the fabric once (exchange_dotset: N - 1 merges on every rank).  Returns
+    the number of merges this rank ran."""
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    rel = (rank - dst) % world
+    merges, step = 0, 1
+    while step < world:
+        if rel % (2 * step) == step:          # send to the partner below, then done
+            _send_bytes(core.state_bytes(), _global(group, (rank - step) % world), group=group, device=device)
+            break
+        if rel % (2 * step) == 0 and rel + step < world:
+            sw = _recv_bytes(_global(group, (rank + step) % world), group=group, device=device)
+            rc = core.merge_state(sw)
+            if rc:
+                raise RuntimeError("merge_state from rank %d failed: %d" % ((rank + step) % world, rc))
+            merges += 1
+        step *= 2
+    return merges
+
+
+def ingest_dotset_sharded(core, ingest, group=None, device="cpu", snapshot=True):
+    """read_remote_ops of the dot-set kinds over writer shards (actor_range), then the tree
+    reduce to rank 0.  `ingest()` folds this rank's files into `core` and returns its status.
+    All-or-nothing across ranks (lib.rs:497-514): the statuses meet in one all_reduce(MAX) before
+    any state moves; on a failure anywhere, every rank that folded its shard goes back to the
+    StateWrapper it held before (reset + merge_state of the snapshot) and the failing status is
+    returned on every rank.  Returns (rc, merges)."""
+    s0 = core.state_bytes() if snapshot else None
+    rc = ingest()
+    code = torch.tensor([rc], dtype=torch.int64, device=device)
+    all_reduce_(code, dist.ReduceOp.MAX, group=group)
+    code = int(code.item())
+    if code:
+        if rc == 0:
+            if s0 is None:
+                raise RuntimeError("a rank failed and no snapshot was kept")
+            core.reset()
+            if core.merge_state(s0):
+                raise RuntimeError("restoring the snapshot failed")
+        return code, 0
+    return 0, reduce_dotset(core, group=group, device=device)
 
 
 def exchange_dotset(core, group=None, device="cpu"):

@@ -72,7 +72,7 @@ def workload_orswot(seed=88, n_actors=8, versions=4):
     return key, acts, sealed, fa, fv
 
 
-def main_orswot(rank, world, out):
+def main_orswot(rank, world, out, tree=False):
     import crdtenc
     import shard
     key, actors, files, fa, fv = workload_orswot()
@@ -81,12 +81,22 @@ def main_orswot(rank, world, out):
     core.set_latest_key(key)
     lo, hi = shard.actor_range(len(actors), world, rank)
     sel = [i for i in range(len(files)) if lo <= fa[i] < hi]
-    rc, _ = core.ingest_ops([files[i] for i in sel], actors[lo:hi], [fa[i] - lo for i in sel],
-                            [fv[i] for i in sel])
-    assert rc == 0, rc
-    shard.exchange_dotset(core, device="cpu")
+
+    def ingest():
+        return core.ingest_ops([files[i] for i in sel], actors[lo:hi], [fa[i] - lo for i in sel],
+                               [fv[i] for i in sel])[0]
+
+    if tree:   # the binomial-tree reduce to rank 0 (shard.ingest_dotset_sharded)
+        rc, merges = shard.ingest_dotset_sharded(core, ingest)
+        assert rc == 0, rc
+        tag = b"tree %d" % merges
+    else:
+        rc = ingest()
+        assert rc == 0, rc
+        shard.exchange_dotset(core, device="cpu")
+        tag = b"dotset"
     with open("%s.%d" % (out, rank), "wb") as f:
-        f.write(b"dotset\n" + core.state_bytes())
+        f.write(tag + b"\n" + core.state_bytes())
     core.close()
     ctx.close()
 
@@ -131,7 +141,7 @@ def main_sharded(rank, world, name, out):
 
 def main():
     rank, world, port, mode, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5]
-    if mode == "orswot" or mode.startswith("sharded:"):
+    if mode.startswith("orswot") or mode.startswith("sharded:"):
         sys.path.insert(0, os.path.join(REPO, "tests"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
     import torch
@@ -140,8 +150,8 @@ def main():
     import shard
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        if mode == "orswot":
-            main_orswot(rank, world, out)
+        if mode in ("orswot", "orswot_tree"):
+            main_orswot(rank, world, out, tree=mode == "orswot_tree")
             return
         if mode.startswith("sharded:"):
             main_sharded(rank, world, mode.split(":", 1)[1], out)

@@ -80,3 +80,26 @@ def test_exchange_dotset_two_processes(tmp_path):
         with open("%s.%d" % (out, r), "rb") as f:
             tag, state = f.read().split(b"\n", 1)
         assert tag == b"dotset" and state == want
+
+
+def test_reduce_dotset_two_processes(tmp_path):
+    """shard.ingest_dotset_sharded on the GPU: writer shards folded per rank, then the tree
+    reduce -- rank 1 sends its StateWrapper, rank 0 merges it once (GPU Orswot::merge) and holds
+    the oracle's single fold."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import multi_rank_worker as W
+    from oracle import crdts as C
+    key, actors, files, fa, fv = W.workload_orswot()
+    oc = C.Core("orswot")
+    assert oc.read_remote_ops(key, [APP], files, [actors[i] for i in fa], fv)[0] == 0
+    out = str(tmp_path / "t")
+    port = str(_port())
+    procs = [subprocess.Popen([sys.executable, os.path.join(REPO, "tests", "multi_rank_worker.py"),
+                               str(r), "2", port, "orswot_tree", out]) for r in range(2)]
+    assert [p.wait(timeout=180) for p in procs] == [0, 0]
+    with open(out + ".0", "rb") as f:
+        tag, state = f.read().split(b"\n", 1)
+    assert tag == b"tree 1" and state == oc.serialize()
+    with open(out + ".1", "rb") as f:
+        assert f.read().split(b"\n", 1)[0] == b"tree 0"
+

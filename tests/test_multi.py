@@ -158,6 +158,9 @@ class _OracleDotCore:
         self.core.nov.merge(nov)
         return 0
 
+    def reset(self):
+        self.core = self.C.Core(self.core.kind)
+
 
 def _dot_workload(kind):
     sys.path.insert(0, os.path.join(REPO, "tests"))
@@ -291,3 +294,74 @@ def test_exchange_vclock_paths(tmp_path, n_reg, path):
             got_path, state = f.read().split(b"\n", 1)
         assert got_path.decode() == path
         assert state == want
+
+
+def _c3_medium(tamper_rank=None, world=2):
+    """test_c3_shaped_medium's generator (tests/test_gpu_dotset.py): 256 writers, members from
+    10k, 4 versions x 12 ops per writer, sealed with the oracle; tamper_rank: one file of that
+    rank's writer shard gets a flipped tag bit."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import dotset_gen as G
+    import oracle
+    rng = random.Random(3)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 256)
+    files = G.well_formed_orswot(rng, actors, 4, 12, 10000, max_members=1)[0]
+    acts, clears, fa, fv = G.batch(files, "orswot", APP)
+    sealed = [CORE + oracle.cryptor_encrypt(key, bytes(24), c)[1] for c in clears]
+    if tamper_rank is not None:
+        lo, hi = shard.actor_range(len(acts), world, tamper_rank)
+        i = next(i for i in range(len(fa)) if lo <= fa[i] < hi)
+        sealed[i] = sealed[i][:-1] + bytes([sealed[i][-1] ^ 1])
+    return key, acts, sealed, fa, fv
+
+
+def _tree_rank_main(rank, world, port, tamper_rank, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        key, acts, files, fa, fv = _c3_medium(tamper_rank, world)
+        lo, hi = shard.actor_range(len(acts), world, rank)
+        sel = [i for i in range(len(fa)) if lo <= fa[i] < hi]
+        core = _OracleDotCore("orswot")
+
+        def ingest():
+            return core.core.read_remote_ops(key, [APP], [files[i] for i in sel], [acts[fa[i]] for i in sel],
+                                             [fv[i] for i in sel])[0]
+
+        rc, merges = shard.ingest_dotset_sharded(core, ingest)
+        with open("%s.%d" % (out_path, rank), "wb") as f:
+            f.write(msgpack.packb([rc, merges, core.state_bytes()], use_bin_type=True))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,tamper", [(2, None), (4, None), (3, None), (4, 2)])
+def test_dotset_tree_reduce_c3_medium(tmp_path, world, tamper):
+    """shard.ingest_dotset_sharded at C3's shape (256 writers, 10k members, 1024 op files):
+    writer shards folded per rank, then the binomial-tree reduce -- rank 0 ends with the oracle's
+    single fold and runs ceil(log2 N) merges, no rank more; with a tampered file on one rank every
+    rank returns AUTH with its state unchanged (lib.rs:497-514)."""
+    from oracle import crdts as C
+    key, acts, files, fa, fv = _c3_medium(tamper, world)
+    oc = C.Core("orswot")
+    orc = oc.read_remote_ops(key, [APP], files, [acts[i] for i in fa], fv)[0]
+    out = str(tmp_path / "t")
+    mp.spawn(_tree_rank_main, args=(world, _free_port(), tamper, out), nprocs=world, join=True)
+    empty = C.Core("orswot").serialize()
+    log = []
+    for r in range(world):
+        with open("%s.%d" % (out, r), "rb") as f:
+            rc, merges, state = msgpack.unpackb(f.read(), raw=False)
+        log.append(merges)
+        if tamper is None:
+            assert rc == 0 and orc == 0
+            if r == 0:
+                assert state == oc.serialize()
+        else:
+            assert rc == orc == 9 and state == empty and merges == 0
+    if tamper is None:
+        depth = (world - 1).bit_length()
+        assert log[0] == depth and max(log) <= depth and sum(log) == world - 1, log
+    print("merges per rank:", log)
+
