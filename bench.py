@@ -159,7 +159,29 @@ def expected_state(actors_all, versions_global, variant="a", smax=None):
                          use_bin_type=True)
 
 
+def cgroup_cpus():
+    """CPUs the cgroup quota allows (cpu.max 'quota period'), None when unlimited / unknown."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as f:
+                q, p = f.read().split()[:2]
+            return None if q == "max" else max(1, int(int(q) // int(p)))
+        except (OSError, ValueError):
+            pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            p = int(f.read())
+        return None if q <= 0 else max(1, q // p)
+    except (OSError, ValueError):
+        return None
+
+
 def host_cpu():
+    """(model, usable CPUs, threads for the best-CPU leg, how the count was chosen).  usable =
+    min(affinity, cgroup quota); threads = min(usable, OMP_NUM_THREADS): the job's CPU share --
+    on the GPU box the harness sets OMP_NUM_THREADS=16 per one-GPU job, the share we may use."""
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -169,9 +191,17 @@ def host_cpu():
                     break
     except OSError:
         pass
-    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    share = int(os.environ.get("OMP_NUM_THREADS") or avail)   # the job's CPU share (16 on the box)
-    return model, avail, max(1, min(avail, share, 256))
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = cgroup_cpus()
+    usable = min(aff, quota) if quota else aff
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = max(1, min(usable, int(omp) if omp else usable, 256))
+    why = {"nproc": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota,
+           "OMP_NUM_THREADS": int(omp) if omp else None, "threads": threads,
+           "per_gpu_share_of_8_gpu_node": max(1, (os.cpu_count() or 8) // 8),
+           "rule": "threads = min(affinity, cgroup quota, OMP_NUM_THREADS): the CPU share this "
+                   "one-GPU job is given (the box sets OMP_NUM_THREADS=16)"}
+    return model, usable, threads, why
 
 
 def probe_clock(ctx, step, dev):
@@ -435,7 +465,7 @@ class Workload:
         same files; each mode's serialized state must equal the GPU path's on the sample."""
         sys.path.insert(0, REPO)
         import oracle
-        model, avail, threads = host_cpu()
+        model, avail, threads, why = host_cpu()
         n, versions = self.n, self.versions
         s = min(args.cpu_sample, n) if args.cpu_sample > 0 else n
         s -= s % versions
@@ -469,7 +499,8 @@ class Workload:
                       "fold parallel over actors, private states merged, on %d threads; "
                       "serialized state == GPU path: %s" % (s, s // versions, versions, b["cores"],
                                                             b["same_state_as_gpu"]),
-            "seconds": b["seconds"], "host_cpu": model, "nproc": avail,
+            "seconds": b["seconds"], "host_cpu": model, "nproc": os.cpu_count(), "usable_cpus": avail,
+            "cores_rule": why,
             "reference_shaped": dict(r, unit="op files/s", mode="%d AEAD threads (buffered(16), "
                                      "lib.rs:497-514), decode + fold on one thread "
                                      "(lib.rs:516-544)" % r["cores"]),
@@ -506,6 +537,9 @@ def main():
     ap.add_argument("--no-clock", action="store_true", help="skip the shader-clock probe")
     ap.add_argument("--no-host-buffers", action="store_true",
                     help="skip the end-to-end run from host buffers (H2D over PCIe)")
+    ap.add_argument("--configs", default="c3,c4,c5",
+                    help="N=1: also run these BASELINE configs (bench_configs.py runners) and report "
+                         "them under the line's `configs` key ('' = none)")
     ap.add_argument("--partition", choices=("address", "actor"), default="address",
                     help="N > 1: op files by address hash with the cross-rank gate (default), or "
                          "whole writers per rank")
@@ -567,6 +601,29 @@ def main():
                   state_check="StateWrapper bytes == generator's per-actor max: %s" % ("ok" if ok_b else "MISMATCH"))
         wb.close()
         del wb
+
+    # the other BASELINE configs (C3 Orswot, C4 skewed sizes, C5 key-rotation mix) on this GPU,
+    # each timed and checked by bench_configs.py's runner -- reported beside the C2 line, never
+    # its value
+    configs = None
+    if world == 1 and args.configs:
+        import bench_configs
+        configs = {}
+        for c in [x for x in args.configs.split(",") if x]:
+            steps_c = {"c3": 20, "c4": 10, "c5": 10}[c]
+            ns = bench_configs.make_parser().parse_args(
+                ["--config", c, "--steps", str(steps_c), "--warmup", "1", "--no-clock"] +
+                (["--no-cpu"] if args.no_cpu else []))
+            t_c = time.time()
+            line_c = bench_configs.RUNNERS[c](ns, ctx, dev)
+            line_c["wall_s"] = round(time.time() - t_c, 1)
+            good = all(bool(v) for v in line_c.get("checks", {}).values()) and (
+                line_c.get("cpu_baseline") is None or line_c["cpu_baseline"].get("same_result_as_gpu", True))
+            if not good:
+                log("CONFIG %s CHECK FAILED: %s" % (c, line_c.get("checks")))
+                ok = False
+            configs[c] = line_c
+            torch.cuda.empty_cache()
 
     if rank == 0:
         fused = os.environ.get("CE_FUSED", str(DEFAULT_FUSED))
@@ -653,6 +710,7 @@ def main():
             "variant_b": vb,
             "host_buffers": hostbuf,
             "cpu_baseline": cpu,
+            "configs": configs,
         }
         if not (ok and cpu_ok):
             line.pop("value")

@@ -145,7 +145,7 @@ def gcounter_cpu_baseline(key, host_blob, h_offs, h_act, h_ver, check, what):
     sys.path.insert(0, REPO)
     import bench
     import oracle
-    model, avail, threads = bench.host_cpu()
+    model, avail, threads, why = bench.host_cpu()
     s = len(h_offs) - 1
     res = {}
     for mode, best, th in (("best", True, threads), ("reference_shaped", False, min(16, threads))):
@@ -167,7 +167,7 @@ def gcounter_cpu_baseline(key, host_blob, h_offs, h_act, h_ver, check, what):
     return {"value": t["value"], "unit": "files/s", "cores": t["cores"], "kind": "port",
             "sample": "%s; oracle/ce_oracle.c, %s mode (%s) on %d threads" % (what, top, t["mode"], t["cores"]),
             "seconds": t["seconds"], "same_result_as_gpu": all(v["same_result_as_gpu"] for v in res.values()),
-            "host_cpu": model, "nproc": avail,
+            "host_cpu": model, "nproc": os.cpu_count(), "usable_cpus": avail, "cores_rule": why,
             "modes": {k: dict(v, unit="files/s") for k, v in res.items()}}
 
 
@@ -180,7 +180,7 @@ def orswot_cpu_baseline(key, state_files, blob, offs, file_actor, file_version, 
     sys.path.insert(0, REPO)
     import bench
     import oracle
-    model, avail, threads = bench.host_cpu()
+    model, avail, threads, why = bench.host_cpu()
     nf = len(state_files) + len(offs) - 1
     res = {}
     for mode, th in (("best", threads), ("reference_shaped", min(16, threads))):
@@ -196,7 +196,7 @@ def orswot_cpu_baseline(key, state_files, blob, offs, file_actor, file_version, 
             "sample": "%s; oracle/ce_oracle.c oc_compact_orswot_best, %s mode (open + decode on %d "
                       "threads, merges + fold on one)" % (what, top, t["cores"]),
             "seconds": t["seconds"], "same_result_as_gpu": all(v["same_result_as_gpu"] for v in res.values()),
-            "host_cpu": model, "nproc": avail,
+            "host_cpu": model, "nproc": os.cpu_count(), "usable_cpus": avail, "cores_rule": why,
             "modes": {k: dict(v, unit="files/s") for k, v in res.items()}}
 
 
@@ -293,6 +293,29 @@ def run_c3(args, ctx, dev):
     t_n = time.perf_counter()
     crdtenc.content_name(out["file"])     # one SHA3-256 name, timed alone (untimed region)
     name_ms = round((time.perf_counter() - t_n) * 1e3, 3)
+    # one Core::compact as a caller sees it (crdt-enc/src/lib.rs:332-363): nothing pipelined --
+    # reset, read_remote_states, read_remote_ops, serialize + seal + download, then the content
+    # name store_state needs before compact returns (crdt-enc-tokio/src/lib.rs:403-432)
+    single = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t_s = time.perf_counter()
+        core.reset()
+        assert core.ingest_states_iov(states)[0] == 0
+        assert core.ingest_ops_device(files.data_ptr(), offs.data_ptr(), n, blob_len, all_actors,
+                                      fa.data_ptr(), fv.data_ptr()) == 0
+        t_c = time.perf_counter()
+        obuf[0], ln, _ = core.compact_into(obuf[0], name=False)
+        t_h = time.perf_counter()
+        crdtenc.content_name(obuf[0][:ln])
+        t_e = time.perf_counter()
+        single.append(((t_e - t_s) * 1e3, (t_c - t_s) * 1e3, (t_h - t_c) * 1e3, (t_e - t_h) * 1e3))
+    best = min(single)
+    single_call = {"ms": round(best[0], 3), "read_remote_ms": round(best[1], 3),
+                   "serialize_seal_download_ms": round(best[2], 3), "content_name_ms": round(best[3], 3),
+                   "what": "one Core::compact, nothing pipelined (best of 3): read_remote (states + "
+                           "ops) -> serialize + seal + download -> SHA3-256/BASE32 name of the "
+                           "state file on one host thread (a sequential sponge)"}
 
     # checks: closed-form clock; sharded fold + merge_state == whole fold
     import msgpack
@@ -353,6 +376,7 @@ def run_c3(args, ctx, dev):
                                % (N_MEMBERS, N_ACTORS, n_state, V0, n, V, PT_LEN),
                    "ops": n * (N_ADD + N_RM), "entries": entries,
                    "state_file_bytes": int(len(out["file"])), "name_ms": name_ms},
+        "single_compact_latency": single_call,
         "aead_open_GBps": round(ct / (open_ms / 1e3) / 1e9, 1) if open_ms else None,
         "fold": {"kernels": "ds_applied + ds_add_pairs + ds_kill", "ms": round(fold_ms, 4),
                  "algorithmic_bytes": fold_bytes,
@@ -496,8 +520,8 @@ def run_c4(args, ctx, dev):
                          "segdec_fallback": core.path_count("segdec_fallback")},
         "checks": {"closed_form_state": ok},
     }
-    print(json.dumps(line), flush=True)
     core.close()
+    return line
 
 
 def run_c5(args, ctx, dev):
@@ -590,10 +614,11 @@ def run_c5(args, ctx, dev):
         "cpu_baseline": cpu,
         "checks": checks,
     }
-    print(json.dumps(line), flush=True)
     core.close()
+    return line
 
-def main():
+
+def make_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3", choices=["c3", "c4", "c5"])
     ap.add_argument("--c4-versions", type=int, default=32, help="C4 versions per actor (1024 actors)")
@@ -609,7 +634,14 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--versions", type=int, default=16, help="op-file versions per actor")
     ap.add_argument("--state-versions", type=int, default=4, help="versions folded into states")
-    args = ap.parse_args()
+    return ap
+
+
+RUNNERS = {"c3": run_c3, "c4": run_c4, "c5": run_c5}
+
+
+def main():
+    args = make_parser().parse_args()
     if args.steps is None:
         args.steps = 40 if args.config == "c3" else 20
     torch.cuda.set_device(0)
@@ -618,7 +650,8 @@ def main():
     torch.cuda.set_stream(stream)
     ctx = crdtenc.Context(0)
     ctx.set_stream(stream.cuda_stream)
-    {"c3": run_c3, "c4": run_c4, "c5": run_c5}[args.config](args, ctx, dev)
+    line = RUNNERS[args.config](args, ctx, dev)
+    print(json.dumps(line), flush=True)
     ctx.close()
 
 

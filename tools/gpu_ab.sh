@@ -6,7 +6,7 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 run() {
   echo -n "$1 "
-  env ${1//,/ } timeout -k 10 200 python bench.py --no-cpu ${BENCH_ARGS:-} > gpurun_out/ab.json 2> gpurun_out/ab.err
+  env ${1//,/ } timeout -k 10 200 python bench.py --configs '' --no-cpu ${BENCH_ARGS:-} > gpurun_out/ab.json 2> gpurun_out/ab.err
   local rc=$?
   [ $rc -eq 124 ] || [ $rc -eq 137 ] || [ $rc -ge 128 ] && { echo "bench died rc=$rc"; tail -3 gpurun_out/ab.err; return 1; }
   python3 -c "

@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 for r in 1 2; do
   for L in ${LIBS}; do
     echo -n "$L "
-    CRDTENC_LIB=$PWD/$L timeout -k 10 200 python bench.py --no-cpu --no-host-buffers ${BENCH_ARGS:-} 2> gpurun_out/libab.err | python3 -c "
+    CRDTENC_LIB=$PWD/$L timeout -k 10 200 python bench.py --configs '' --no-cpu --no-host-buffers ${BENCH_ARGS:-} 2> gpurun_out/libab.err | python3 -c "
 import json,sys;d=json.loads(sys.stdin.read().strip().splitlines()[-1]);b=d.get('variant_b') or {}
 print(d['ms_per_step'],d['roofline']['avg_launch_ms'],'B',b.get('ms_per_step'),b.get('avg_launch_ms'))" || { tail -3 gpurun_out/libab.err; exit 1; }
   done

@@ -11,6 +11,6 @@ for P in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ
          "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
          "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $OUT/pass$i -o p -- python3 $R/bench.py --versions 64 --steps 2 --warmup 1 --no-cpu --no-clock > $OUT/pass$i.out 2> $OUT/pass$i.err
+  timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $OUT/pass$i -o p -- python3 $R/bench.py --configs '' --versions 64 --steps 2 --warmup 1 --no-cpu --no-clock > $OUT/pass$i.out 2> $OUT/pass$i.err
   echo "pass $i rc=$?"
 done

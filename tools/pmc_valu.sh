@@ -11,7 +11,7 @@ for P in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_
          "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_INSTS_SMEM GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
   timeout -s KILL 180 rocprofv3 --pmc $P --kernel-trace --output-format csv -d $OUT/pass$i -o p -- \
-    python3 $R/bench.py --steps 2 --warmup 1 --no-cpu --no-variant-b --no-host-buffers --no-clock > $OUT/pass$i.out 2> $OUT/pass$i.err || { echo "pass $i failed rc=$?"; tail -5 $OUT/pass$i.err; exit 1; }
+    python3 $R/bench.py --configs '' --steps 2 --warmup 1 --no-cpu --no-variant-b --no-host-buffers --no-clock > $OUT/pass$i.out 2> $OUT/pass$i.err || { echo "pass $i failed rc=$?"; tail -5 $OUT/pass$i.err; exit 1; }
   echo "pass $i ok"
 done
 python3 $R/tools/summarize_valu.py $OUT
