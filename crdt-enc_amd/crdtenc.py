@@ -250,6 +250,7 @@ class Context:
 
     def set_stream(self, stream_ptr):
         self.check(lib().ce_ctx_set_stream(self.p, ctypes.c_void_p(stream_ptr)), "set_stream")
+        self.stream_ptr = stream_ptr
 
     def synchronize(self):
         lib().ce_ctx_synchronize(self.p)

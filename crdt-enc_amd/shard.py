@@ -233,12 +233,20 @@ class DeviceShardOps:
         self.hi = torch.empty(self.m + 1, dtype=torch.int64, device=self.device)
         self.dense = torch.empty(core.dense_capacity() + 2, dtype=torch.int64, device=self.device)
 
+    def _ordered(self):
+        """The core runs on its context's stream: when that is not torch's current stream, what
+        torch (or a collective) wrote must be complete before the core reads it."""
+        cur = torch.cuda.current_stream(self.device)
+        if getattr(self.core.ctx, "stream_ptr", None) != cur.cuda_stream:
+            cur.synchronize()
+
     def compute_stats(self, rank, world):
         self.core.shard_stats(self.actors, self.fa.data_ptr(), self.fv.data_ptr(), self.n, rank, world,
                               self.stats.data_ptr())
         return self.stats
 
     def window(self):
+        self._ordered()
         self.core.shard_window(self.actors, self.stats.data_ptr(), self.hi.data_ptr())
         return self.hi
 
@@ -246,6 +254,7 @@ class DeviceShardOps:
         import numpy as np
         h = np.append(np.asarray(hi, np.uint64), np.uint64(flags)).view(np.int64)
         self.hi.copy_(torch.from_numpy(h))
+        self._ordered()
 
     def metadata(self):
         return self.fa[: self.n].cpu().numpy().astype("uint32"), self.fv[: self.n].cpu().numpy().astype("uint64")
@@ -265,9 +274,11 @@ class DeviceShardOps:
     def export_pending(self, dense):
         if dense.dtype != torch.int64:
             raise TypeError("dense is an int64 view of u64")
+        self._ordered()
         return self.core.pending_export(dense.data_ptr())
 
     def commit(self, accept, reduced=None):
+        self._ordered()
         self.core.pending_commit(accept, reduced.data_ptr() if reduced is not None else None)
 
 

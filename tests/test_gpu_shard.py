@@ -73,8 +73,10 @@ def test_device_stats_and_window_equal_host(ctx, world):
             assert (got == want).all(), (trial, r)
             dstats.append(got)
         red = torch.from_numpy(np.maximum.reduce(dstats)).to(dev)
+        torch.cuda.synchronize()
         hi = torch.empty(m + 1, dtype=torch.int64, device=dev)
         core.shard_window(b"".join(writers), red.data_ptr(), hi.data_ptr())
+        ctx.synchronize()
         h, flags = crdtenc.shard_window_host(e0, red.cpu().numpy())
         got = hi.cpu().numpy().view(np.uint64)
         assert (got[:m] == h).all() and int(got[m]) == flags
@@ -117,6 +119,7 @@ def test_three_shares_one_process(ctx, oracle, name, want_rc):
         core.shard_stats(W, d["fa"].data_ptr(), d["fv"].data_ptr(), d["n"], r, world, st.data_ptr())
         stats.append(st.cpu().numpy())
     red = torch.from_numpy(np.maximum.reduce(stats)).to(dev)
+    torch.cuda.synchronize()
     rcs, batches, ready = [], [], []
     for core, d in zip(cores, shares):
         hi = torch.empty(m + 1, dtype=torch.int64, device=dev)
@@ -125,6 +128,7 @@ def test_three_shares_one_process(ctx, oracle, name, want_rc):
                                             W, d["fa"].data_ptr(), d["fv"].data_ptr(), hi.data_ptr())
         rcs.append(rc)
         b = torch.zeros(core.dense_capacity(), dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()   # the core's own stream reads / writes it next
         if rc in (0, 13):
             ready.append(core.pending_export(b.data_ptr()))
         batches.append(b.cpu().numpy().view(np.uint64))
@@ -142,6 +146,7 @@ def test_three_shares_one_process(ctx, oracle, name, want_rc):
         assert orc == want_rc
         if all(ready):
             red_b = torch.from_numpy(np.maximum.reduce(batches).view(np.int64).copy()).to(dev)
+            torch.cuda.synchronize()
             for core in cores:
                 core.pending_commit(True, red_b.data_ptr())
         else:   # a Dot on an unregistered actor: commit locally, then merge serialized states

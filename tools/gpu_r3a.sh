@@ -12,3 +12,5 @@ CE_BENCH_SHARE_GPU=1 CE_DIST_BACKEND=gloo timeout -k 10 400 python bench.py --co
 cat gpurun_out/bench2.json
 timeout -k 10 550 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json
+./tools/step_trace.sh > gpurun_out/steptrace.txt 2>&1 || { echo "step trace failed"; tail gpurun_out/steptrace.txt; exit 1; }
+tail -60 gpurun_out/steptrace.txt
