@@ -387,8 +387,9 @@ def run_c3(args, ctx, dev):
         "cpu_baseline": cpu,
         "checks": {"closed_form_clock": clock_ok, "sharded_merge_equals_whole": shard_ok},
     }
-    print(json.dumps(line), flush=True)
+    namer.shutdown()
     core.close()
+    return line
 
 
 
