@@ -276,7 +276,7 @@ int table_upload(ce_core* c) {
                                 hipMemcpyHostToDevice, c->ctx->stream);
   if (e) return c->ctx->hip_fail(e, "table upload");
   // the host vector may be rewritten before the copy runs: wait (table changes are rare)
-  if ((e = hipStreamSynchronize(c->ctx->stream))) return c->ctx->hip_fail(e, "table upload");
+  if ((e = stream_wait(c->ctx->stream))) return c->ctx->hip_fail(e, "table upload");
   c->table_dirty = false;
   return CE_OK;
 }
@@ -288,7 +288,7 @@ int table_grow(ce_core* c) {
   hipError_t e;
   if ((e = hipMemcpyAsync(st.data(), c->d_state.p, old_cap * 8ull, hipMemcpyDeviceToHost,
                           c->ctx->stream)) ||
-      (e = hipStreamSynchronize(c->ctx->stream)))
+      (e = stream_wait(c->ctx->stream)))
     return c->ctx->hip_fail(e, "grow");
   std::vector<Uuid> actors;
   std::vector<uint64_t> nov, sv;
@@ -323,7 +323,7 @@ int table_grow(ce_core* c) {
   c->registered = reg;
   if ((e = hipMemcpyAsync(c->d_state.p, nst.data(), c->cap * 8ull, hipMemcpyHostToDevice,
                           c->ctx->stream)) ||
-      (e = hipStreamSynchronize(c->ctx->stream)))
+      (e = stream_wait(c->ctx->stream)))
     return c->ctx->hip_fail(e, "grow");
   return CE_OK;
 }
@@ -355,7 +355,7 @@ int download_state(ce_core* c, std::vector<uint64_t>* st) {
   hipError_t e;
   if ((e = hipMemcpyAsync(st->data(), c->d_state.p, c->cap * 8ull, hipMemcpyDeviceToHost,
                           c->ctx->stream)) ||
-      (e = hipStreamSynchronize(c->ctx->stream)))
+      (e = stream_wait(c->ctx->stream)))
     return c->ctx->hip_fail(e, "state download");
   return CE_OK;
 }
@@ -390,7 +390,7 @@ int merge_dots_host(ce_core* c, const Dots& dots) {
                           c->ctx->stream)) ||
       (e = launch_merge_max(c->ctx->stream, c->d_state.as<unsigned long long>(),
                             c->d_tmp.as<unsigned long long>(), c->cap)) ||
-      (e = hipStreamSynchronize(c->ctx->stream)))
+      (e = stream_wait(c->ctx->stream)))
     return c->ctx->hip_fail(e, "merge dots");
   return CE_OK;
 }
@@ -468,13 +468,13 @@ int open_one(ce_core* c, const uint8_t* file, size_t flen, bool outer, int32_t* 
   FileParams P;
   if ((e = hipMemcpyAsync(&P, a->params.p, sizeof P, hipMemcpyDeviceToHost, a->stream)) ||
       (e = hipMemcpyAsync(st, a->status.p, 4, hipMemcpyDeviceToHost, a->stream)) ||
-      (e = hipStreamSynchronize(a->stream)))
+      (e = stream_wait(a->stream)))
     return a->hip_fail(e, "open_one");
   if (*st == CE_OK) {
     pt->resize(P.len);
     if (P.len && ((e = hipMemcpyAsync(pt->data(), a->out.as<uint8_t>() + P.out_off, P.len,
                                       hipMemcpyDeviceToHost, a->stream)) ||
-                  (e = hipStreamSynchronize(a->stream))))
+                  (e = stream_wait(a->stream))))
       return a->hip_fail(e, "open_one");
   }
   return CE_OK;
@@ -488,7 +488,7 @@ int resolve_host_parse(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs
   std::vector<int32_t> st(n);
   hipError_t e;
   if ((e = hipMemcpyAsync(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
-      (e = hipStreamSynchronize(ctx->stream)))
+      (e = stream_wait(ctx->stream)))
     return ctx->hip_fail(e, "host parse");
   for (uint32_t i = 0; i < n; i++) {
     if (st[i] != kStatusHostParse) continue;
@@ -530,7 +530,7 @@ int ensure_supported(ce_core* c) {
   if (bytes && (e = hipMemcpyAsync(c->d_supported.p, c->supported.data(), bytes,
                                    hipMemcpyHostToDevice, c->ctx->stream)))
     return c->ctx->hip_fail(e, "supported");
-  if ((e = hipStreamSynchronize(c->ctx->stream))) return c->ctx->hip_fail(e, "supported");
+  if ((e = stream_wait(c->ctx->stream))) return c->ctx->hip_fail(e, "supported");
   c->supported_on_device = true;
   return CE_OK;
 }
@@ -583,7 +583,7 @@ int decode_only_resolving(ce_core* c, DecodeArgs& da, uint32_t n, uint8_t* d_mas
         (e = hipMemsetAsync(ctx->refold.p, 0, n, ctx->stream)) ||
         (e = launch_decode_dots(ctx->stream, da, grid_waves_for(n))) ||
         (e = hipMemcpyAsync(hc, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->stream)) ||
-        (e = hipStreamSynchronize(ctx->stream)))
+        (e = stream_wait(ctx->stream)))
       return ctx->hip_fail(e, "decode plaintext");
     if (hc[4] == 0) return CE_OK;
     if (round > 64) return ctx->fail(CE_ERR_DEVICE, "actor table did not converge");
@@ -591,7 +591,7 @@ int decode_only_resolving(ce_core* c, DecodeArgs& da, uint32_t n, uint8_t* d_mas
     std::vector<uint4> ml(nm);
     if ((e = hipMemcpyAsync(ml.data(), ctx->miss.p, nm * 16ull, hipMemcpyDeviceToHost, ctx->stream)) ||
         (e = hipMemcpyAsync(d_mask, ctx->refold.p, n, hipMemcpyDeviceToDevice, ctx->stream)) ||
-        (e = hipStreamSynchronize(ctx->stream)))
+        (e = stream_wait(ctx->stream)))
       return ctx->hip_fail(e, "miss");
     const uint32_t old_cap = c->cap;
     for (auto& x : ml) {
@@ -626,7 +626,7 @@ int retry_alt_keys(ce_core* c, DecodeArgs& da, const uint8_t* d_blob, const uint
                          ctx->status.as<int32_t>(), false);
     if (rc) return rc;
     if ((e = hipMemcpyAsync(sk.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
-        (e = hipStreamSynchronize(ctx->stream)))
+        (e = stream_wait(ctx->stream)))
       return ctx->hip_fail(e, "multi-key status");
     bool opened = false;
     for (uint32_t i = 0; i < n; i++) {
@@ -638,7 +638,7 @@ int retry_alt_keys(ce_core* c, DecodeArgs& da, const uint8_t* d_blob, const uint
       return ctx->hip_fail(e, "multi-key mask");
     if ((rc = decode_only_resolving(c, da, n, c->d_refold2.as<uint8_t>()))) return rc;
     if ((e = hipMemcpyAsync(sk.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
-        (e = hipStreamSynchronize(ctx->stream)))
+        (e = stream_wait(ctx->stream)))
       return ctx->hip_fail(e, "multi-key status");
     for (uint32_t i = 0; i < n; i++)
       if (sel[i]) st[i] = sk[i];  // CE_OK, or the decode's CE_ERR_DECODE / PT_* status
@@ -864,7 +864,7 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
   if (prof) {
     std::vector<unsigned long long> hp(8ull * 65536);
     if ((e = hipMemcpyAsync(hp.data(), prof_buf.p, hp.size() * 8, hipMemcpyDeviceToHost, ctx->stream)) ||
-        (e = hipStreamSynchronize(ctx->stream)))
+        (e = stream_wait(ctx->stream)))
       return ctx->hip_fail(e, "prof");
     double sum[7] = {0, 0, 0, 0, 0, 0, 0};
     uint32_t waves = 0;
@@ -904,7 +904,7 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
     std::vector<uint8_t> ap(n);
     if ((e = hipMemcpyAsync(fa.data(), d_fa, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
         (e = hipMemcpyAsync(fv.data(), d_fv, n * 8ull, hipMemcpyDeviceToHost, ctx->stream)) ||
-        (e = hipStreamSynchronize(ctx->stream)))
+        (e = stream_wait(ctx->stream)))
       return ctx->hip_fail(e, "host gate");
     for (uint32_t i = 0; i < n; i++)
       if (fa[i] >= m) return ctx->fail(CE_ERR_INVALID_ARG, "file_actor out of range");
@@ -918,7 +918,7 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
       return ctx->hip_fail(e, "host gate");
     if ((rc = run_fold(c->d_refold2.as<uint8_t>()))) return rc;
     if ((e = hipMemcpyAsync(hc, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->stream)) ||
-        (e = hipStreamSynchronize(ctx->stream)))
+        (e = stream_wait(ctx->stream)))
       return ctx->hip_fail(e, "fold sync");
   }
 
@@ -933,7 +933,7 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
         (e = hipMemcpyAsync(c->d_refold2.p, ctx->refold.p, n, hipMemcpyDeviceToDevice, ctx->stream)) ||
         (e = hipMemsetAsync(ctx->refold.p, 0, n, ctx->stream)) ||
         (e = hipMemsetAsync(ctx->counters.as<uint32_t>() + 4, 0, 4, ctx->stream)) ||
-        (e = hipStreamSynchronize(ctx->stream)))
+        (e = stream_wait(ctx->stream)))
       return ctx->hip_fail(e, "miss");
     const uint32_t old_cap = c->cap;
     for (auto& x : ml) {
@@ -960,7 +960,7 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
     da.batch = c->d_batch.as<unsigned long long>();
     if ((rc = run_fold(c->d_refold2.as<uint8_t>()))) return rc;
     if ((e = hipMemcpyAsync(hc, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->stream)) ||
-        (e = hipStreamSynchronize(ctx->stream)))
+        (e = stream_wait(ctx->stream)))
       return ctx->hip_fail(e, "refold");
     if (round > 64) return ctx->fail(CE_ERR_DEVICE, "actor table did not converge");
   }
@@ -971,7 +971,7 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
   auto fetch_status = [&]() -> int {
     st.resize(n);
     if ((e = hipMemcpyAsync(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
-        (e = hipStreamSynchronize(ctx->stream)))
+        (e = stream_wait(ctx->stream)))
       return ctx->hip_fail(e, "status");
     return CE_OK;
   };
@@ -1008,7 +1008,7 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
   if (sharded) {  // pending until ce_core_pending_commit: the windows' next_op_versions
     std::vector<uint64_t> nn(m);
     if ((e = hipMemcpyAsync(nn.data(), gbase + 16ull * m, m * 8ull, hipMemcpyDeviceToHost, ctx->stream)) ||
-        (e = hipStreamSynchronize(ctx->stream)))
+        (e = stream_wait(ctx->stream)))
       return ctx->hip_fail(e, "nov");
     c->pending_nov.clear();
     for (uint32_t a = 0; a < m; a++) {
@@ -1031,10 +1031,10 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
     if (!host_gated) {
       std::vector<uint64_t> nn(m);
       if ((e = hipMemcpyAsync(nn.data(), gbase + 16ull * m, m * 8ull, hipMemcpyDeviceToHost, ctx->stream)) ||
-          (e = hipStreamSynchronize(ctx->stream)))
+          (e = stream_wait(ctx->stream)))
         return ctx->hip_fail(e, "nov");
       for (uint32_t a = 0; a < m; a++) expect[a] = std::max(expect[a], nn[a]);
-    } else if ((e = hipStreamSynchronize(ctx->stream))) {
+    } else if ((e = stream_wait(ctx->stream))) {
       return ctx->hip_fail(e, "merge");
     }
   }
@@ -1078,7 +1078,7 @@ int ingest_ops_hostmeta(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
   uint8_t* mb = c->d_meta.as<uint8_t>();
   if ((e = hipMemcpyAsync(mb, file_version, n * 8ull, hipMemcpyHostToDevice, ctx->stream)) ||
       (e = hipMemcpyAsync(mb + 8ull * n, file_actor, n * 4ull, hipMemcpyHostToDevice, ctx->stream)) ||
-      (e = hipStreamSynchronize(ctx->stream)))
+      (e = stream_wait(ctx->stream)))
     return ctx->hip_fail(e, "meta upload");
   return ingest_ops_dev(c, d_blob, d_offs, n, blob_len, actors, m,
                         reinterpret_cast<const uint32_t*>(mb + 8ull * n),
@@ -1111,7 +1111,7 @@ int ingest_states_host(ce_core* c, const uint8_t* blob, const uint64_t* offs, ui
   if (rc) return rc;
   std::vector<int32_t> st(n);
   if ((e = hipMemcpyAsync(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
-      (e = hipStreamSynchronize(ctx->stream)))
+      (e = stream_wait(ctx->stream)))
     return ctx->hip_fail(e, "states status");
   for (uint32_t i = 0; i < n; i++)
     if (st[i] == kStatusHostParse) {
@@ -1125,7 +1125,7 @@ int ingest_states_host(ce_core* c, const uint8_t* blob, const uint64_t* offs, ui
   if (c->kind == CE_STATE_ORSWOT && !getenv("CE_HOST_STATES")) {
     // plaintexts stay in HBM: the device reader decodes canonical states (ce_dotset_io.hip)
     if ((e = hipMemcpyAsync(P.data(), ctx->params.p, n * sizeof(FileParams), hipMemcpyDeviceToHost, ctx->stream)) ||
-        (e = hipStreamSynchronize(ctx->stream)))
+        (e = stream_wait(ctx->stream)))
       return ctx->hip_fail(e, "states params");
     std::vector<uint64_t> off(n, 0), len(n, 0);
     std::vector<uint8_t> ver(16ull * n);
@@ -1138,7 +1138,7 @@ int ingest_states_host(ce_core* c, const uint8_t* blob, const uint64_t* offs, ui
       off[i] = P[i].out_off + 16;
       len[i] = P[i].len - 16;
     }
-    if ((e = hipStreamSynchronize(ctx->stream))) return ctx->hip_fail(e, "states version");
+    if ((e = stream_wait(ctx->stream))) return ctx->hip_fail(e, "states version");
     for (uint32_t i = 0; i < n; i++) {
       if (st[i] != CE_OK) continue;
       Uuid v;
@@ -1151,7 +1151,7 @@ int ingest_states_host(ce_core* c, const uint8_t* blob, const uint64_t* offs, ui
   if ((e = hipMemcpyAsync(P.data(), ctx->params.p, n * sizeof(FileParams), hipMemcpyDeviceToHost,
                           ctx->stream)) ||
       (e = hipMemcpyAsync(out.data(), ctx->out.p, blen + 16ull * n, hipMemcpyDeviceToHost, ctx->stream)) ||
-      (e = hipStreamSynchronize(ctx->stream)))
+      (e = stream_wait(ctx->stream)))
     return ctx->hip_fail(e, "states download");
   if (is_dotset_kind(c->kind)) {
     std::vector<std::pair<const uint8_t*, size_t>> sws(n, {nullptr, 0});
@@ -1247,7 +1247,7 @@ int read_remote(ce_core* c) {
     return ctx->hip_fail(e, "ops reserve");
   if ((e = hipMemcpyAsync(ctx->blob.p, blob.data(), blob.size(), hipMemcpyHostToDevice, ctx->stream)) ||
       (e = hipMemcpyAsync(ctx->offs.p, offs.data(), (n + 1) * 8ull, hipMemcpyHostToDevice, ctx->stream)) ||
-      (e = hipStreamSynchronize(ctx->stream)))
+      (e = stream_wait(ctx->stream)))
     return ctx->hip_fail(e, "ops upload");
   std::vector<uint8_t> ab(actors.size() * 16);
   for (size_t a = 0; a < actors.size(); a++) std::memcpy(ab.data() + 16 * a, actors[a].data(), 16);
@@ -1283,7 +1283,7 @@ int compact_enqueue(ce_core* c, ce_ctx* x, const uint8_t* nonce, const NovApply*
     if ((e = c->d_sorted.reserve(4ull * k + 64)) ||
         (k && (e = hipMemcpyAsync(c->d_sorted.p, c->sorted_slots.data(), 4ull * k, hipMemcpyHostToDevice,
                                   x->stream))) ||
-        (e = hipStreamSynchronize(x->stream)))
+        (e = stream_wait(x->stream)))
       return x->hip_fail(e, "sorted slots");
     c->d_sorted_gen = c->sorted_gen;
   }
@@ -1345,7 +1345,7 @@ int compact_device(ce_core* c, const uint8_t* nonce, std::vector<uint8_t>* file)
   int rc = compact_enqueue(c, c->ctx, nonce, nullptr, &pend);
   if (rc) return rc;
   hipError_t e;
-  if ((e = hipStreamSynchronize(c->ctx->stream))) return c->ctx->hip_fail(e, "compact sync");
+  if ((e = stream_wait(c->ctx->stream))) return c->ctx->hip_fail(e, "compact sync");
   return compact_finish(c->ctx, pend, file);
 }
 
@@ -1805,7 +1805,7 @@ int ce_core_apply_ops_batch(ce_core* c, const uint8_t* ops, const uint64_t* offs
                          ctx->out_offs.as<uint64_t>(), key_of(c));
     if (rc) return rc;
     if ((e = hipMemcpyAsync(out.data(), ctx->out.p, foffs[n], hipMemcpyDeviceToHost, ctx->stream)) ||
-        (e = hipStreamSynchronize(ctx->stream)))
+        (e = stream_wait(ctx->stream)))
       return ctx->hip_fail(e, "apply_ops_batch download");
   }
   uint32_t s;
@@ -1886,7 +1886,7 @@ int ce_core_export_dense(ce_core* c, uint64_t* d_state, uint64_t* d_nov) {
   hipError_t e;
   if ((e = hipMemcpyAsync(d_state, c->d_state.p, c->cap * 8ull, hipMemcpyDeviceToDevice, c->ctx->stream)) ||
       (e = hipMemcpyAsync(d_nov, c->nov.data(), c->cap * 8ull, hipMemcpyHostToDevice, c->ctx->stream)) ||
-      (e = hipStreamSynchronize(c->ctx->stream)))
+      (e = stream_wait(c->ctx->stream)))
     return c->ctx->hip_fail(e, "export");
   return CE_OK;
 }
@@ -1900,7 +1900,7 @@ int ce_core_import_dense(ce_core* c, const uint64_t* d_state, const uint64_t* d_
   if ((e = launch_merge_max(c->ctx->stream, c->d_state.as<unsigned long long>(),
                             reinterpret_cast<const unsigned long long*>(d_state), c->cap)) ||
       (e = hipMemcpyAsync(nv.data(), d_nov, c->cap * 8ull, hipMemcpyDeviceToHost, c->ctx->stream)) ||
-      (e = hipStreamSynchronize(c->ctx->stream)))
+      (e = stream_wait(c->ctx->stream)))
     return c->ctx->hip_fail(e, "import");
   for (uint32_t s = 0; s < c->cap; s++) c->nov[s] = std::max(c->nov[s], nv[s]);
   return CE_OK;

@@ -152,7 +152,7 @@ int device_open(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint
   if (sync_counters) {
     if ((e = hipMemcpyAsync(ctx->h_counters.p, ctx->counters.p, 64, hipMemcpyDeviceToHost,
                             ctx->stream)) != hipSuccess ||
-        (e = hipStreamSynchronize(ctx->stream)) != hipSuccess)
+        (e = stream_wait(ctx->stream)) != hipSuccess)
       return ctx->hip_fail(e, "open sync");
   }
   return CE_OK;
@@ -222,7 +222,7 @@ int seal_one(ce_ctx* ctx, const KeyRef& key, const uint8_t* outer_version, const
                        reinterpret_cast<const uint64_t*>(db + A + 16), key);
   if (rc) return rc;
   if ((e = hipMemcpyAsync(hs, ctx->out.p, total, hipMemcpyDeviceToHost, ctx->stream)) ||
-      (e = hipStreamSynchronize(ctx->stream)))
+      (e = stream_wait(ctx->stream)))
     return ctx->hip_fail(e, "seal_one download");
   file->resize(total);
   std::memcpy(file->data(), hs, total);
@@ -444,7 +444,7 @@ int ce_cryptor_decrypt_batch(ce_ctx* c, const uint8_t key_version[16], const uin
       (e = hipMemcpyAsync(P.data(), c->params.p, n * sizeof(FileParams), hipMemcpyDeviceToHost,
                           c->stream)) ||
       (e = hipMemcpyAsync(out_blob, c->out.p, blen + 16ull * n, hipMemcpyDeviceToHost, c->stream)) ||
-      (e = hipStreamSynchronize(c->stream)))
+      (e = stream_wait(c->stream)))
     return c->hip_fail(e, "decrypt_batch download");
   int first = CE_OK;
   for (uint32_t i = 0; i < n; i++) {
@@ -506,7 +506,7 @@ int ce_cryptor_encrypt_batch(ce_ctx* c, const uint8_t key_version[16], const uin
                        c->nonces.as<uint8_t>(), c->out.as<uint8_t>(), c->out_offs.as<uint64_t>(), k);
   if (rc) return rc;
   if ((e = hipMemcpyAsync(out_blob, c->out.p, out_offs[n], hipMemcpyDeviceToHost, c->stream)) ||
-      (e = hipStreamSynchronize(c->stream)))
+      (e = stream_wait(c->stream)))
     return c->hip_fail(e, "encrypt_batch download");
   return CE_OK;
 }
@@ -522,7 +522,7 @@ int ce_cryptor_decrypt_batch_device(ce_ctx* c, const uint8_t key_version[16], co
   uint64_t blen = 0;
   hipError_t e;
   if (n && ((e = hipMemcpyAsync(&blen, d_offs + n, 8, hipMemcpyDeviceToHost, c->stream)) ||
-            (e = hipStreamSynchronize(c->stream))))
+            (e = stream_wait(c->stream))))
     return c->hip_fail(e, "decrypt_batch_device offs");
   int32_t* st = d_status;
   if (!st) {
@@ -551,7 +551,7 @@ int ce_cryptor_encrypt_batch_device(ce_ctx* c, const uint8_t key_version[16], co
   uint64_t blen = 0;
   hipError_t e;
   if (n && ((e = hipMemcpyAsync(&blen, d_offs + n, 8, hipMemcpyDeviceToHost, c->stream)) ||
-            (e = hipStreamSynchronize(c->stream))))
+            (e = stream_wait(c->stream))))
     return c->hip_fail(e, "encrypt_batch_device offs");
   const uint8_t* dov = nullptr;
   if (outer_version) {

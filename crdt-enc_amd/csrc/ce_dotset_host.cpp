@@ -119,7 +119,7 @@ int ensure_clock(ce_core* c) {
   if ((e = nb.reserve(cap * 8ull)) || (e = hipMemsetAsync(nb.p, 0, cap * 8ull, c->ctx->stream)) ||
       (d->clock_cap && (e = hipMemcpyAsync(nb.p, d->clock.p, d->clock_cap * 8ull,
                                            hipMemcpyDeviceToDevice, c->ctx->stream))) ||
-      (e = hipStreamSynchronize(c->ctx->stream)))
+      (e = stream_wait(c->ctx->stream)))
     return c->ctx->hip_fail(e, "clock");
   std::swap(d->clock.p, nb.p);
   std::swap(d->clock.cap, nb.cap);
@@ -142,7 +142,7 @@ int collect(ce_core* c, uint32_t* n_live) {
       (e = launch_ds_collect(ctx->stream, tables(d), d->col[0].as<unsigned long long>(),
                              d->col[1].as<uint32_t>(), d->col[2].as<unsigned long long>(), cnt)) ||
       (e = hipMemcpyAsync(n_live, cnt, 4, hipMemcpyDeviceToHost, ctx->stream)) ||
-      (e = hipStreamSynchronize(ctx->stream)))
+      (e = stream_wait(ctx->stream)))
     return ctx->hip_fail(e, "collect");
   return CE_OK;
 }
@@ -337,7 +337,7 @@ int write_sentinels(ce_core* c, const Counts& k) {
   if ((e = hipMemcpyAsync(o.add_mbeg + k.v[kCntAdd], h + 0, 4, hipMemcpyHostToDevice, c->ctx->stream)) ||
       (e = hipMemcpyAsync(o.rm_cbeg + k.v[kCntRm], h + 1, 4, hipMemcpyHostToDevice, c->ctx->stream)) ||
       (e = hipMemcpyAsync(o.rm_mbeg + k.v[kCntRm], h + 2, 4, hipMemcpyHostToDevice, c->ctx->stream)) ||
-      (e = hipStreamSynchronize(c->ctx->stream)))
+      (e = stream_wait(c->ctx->stream)))
     return c->ctx->hip_fail(e, "sentinels");
   return CE_OK;
 }
@@ -395,7 +395,7 @@ int upload_cols(ce_core* c, const HostCols& hc, const Counts& base) {
       (e = up(o.rmc_actor + base.v[kCntRmC], hc.rmc_actor, s)) ||
       (e = up(o.rmc_ctr + base.v[kCntRmC], hc.rmc_ctr, s)) ||
       (e = up(o.rm_mem + base.v[kCntRmM], hc.rm_mem, s)) ||
-      (e = up(o.put_val + base.v[kCntRm], hc.put_val, s)) || (e = hipStreamSynchronize(s)))
+      (e = up(o.put_val + base.v[kCntRm], hc.put_val, s)) || (e = stream_wait(s)))
     return c->ctx->hip_fail(e, "ops upload");
   return CE_OK;
 }
@@ -419,7 +419,7 @@ int upload_removals(ce_core* c, const std::vector<std::pair<IdDots, std::vector<
   hipStream_t s = c->ctx->stream;
   if ((e = up(d->d0[0].as<uint32_t>(), cbeg, s)) || (e = up(d->d0[1].as<uint32_t>(), mbeg, s)) ||
       (e = up(d->d0[2].as<uint32_t>(), act, s)) || (e = up(d->d0[3].as<unsigned long long>(), ctr, s)) ||
-      (e = up(d->d0[4].as<unsigned long long>(), mem, s)) || (e = hipStreamSynchronize(s)))
+      (e = up(d->d0[4].as<unsigned long long>(), mem, s)) || (e = stream_wait(s)))
     return c->ctx->hip_fail(e, "removals");
   return CE_OK;
 }
@@ -440,7 +440,7 @@ int flags_for(ce_core* c, const uint32_t* cbeg, const uint32_t* act, const unsig
       (e = launch_ds_deferred(c->ctx->stream, cbeg, act, ctr, d->clock.as<unsigned long long>(),
                               d->deferred_flags.as<uint8_t>(), n_rm)) ||
       (e = hipMemcpyAsync(flags->data(), d->deferred_flags.p, n_rm, hipMemcpyDeviceToHost, c->ctx->stream)) ||
-      (e = hipStreamSynchronize(c->ctx->stream)))
+      (e = stream_wait(c->ctx->stream)))
     return c->ctx->hip_fail(e, "deferred");
   return CE_OK;
 }
@@ -455,7 +455,7 @@ int finalize(ce_core* c) {
   c->ctx->tend(t);
   if (
       (e = hipMemcpyAsync(h, d->live.p, 16, hipMemcpyDeviceToHost, c->ctx->stream)) ||
-      (e = hipStreamSynchronize(c->ctx->stream)))
+      (e = stream_wait(c->ctx->stream)))
     return c->ctx->hip_fail(e, "finalize");
   if (h[2]) return c->ctx->fail(CE_ERR_DEVICE, "dot-set table overflow");
   d->live_pairs = h[0];
@@ -542,7 +542,7 @@ int orswot_fold(ce_core* c, const Counts& k) {
         (!act.empty() && (e = hipMemcpyAsync(act.data(), o.rmc_actor, act.size() * 4, hipMemcpyDeviceToHost, s))) ||
         (!ctr.empty() && (e = hipMemcpyAsync(ctr.data(), o.rmc_ctr, ctr.size() * 8, hipMemcpyDeviceToHost, s))) ||
         (!mem.empty() && (e = hipMemcpyAsync(mem.data(), o.rm_mem, mem.size() * 8, hipMemcpyDeviceToHost, s))) ||
-        (e = hipStreamSynchronize(s)))
+        (e = stream_wait(s)))
       return ctx->hip_fail(e, "deferred download");
     for (uint32_t r = 0; r < nr; r++) {
       if (!f_batch[r]) continue;
@@ -592,7 +592,7 @@ int mvreg_survivors(ce_core* c, uint32_t n, bool later_wins, std::vector<uint32_
   for (uint32_t round = 0; round <= n; round++) {
     uint32_t w;
     if ((e = launch_mv_round(s, a)) || (e = hipMemcpyAsync(&w, a.win, 4, hipMemcpyDeviceToHost, s)) ||
-        (e = hipStreamSynchronize(s)))
+        (e = stream_wait(s)))
       return ctx->hip_fail(e, "mvreg round");
     if (w == 0xffffffffu) break;
     if (w >= n) return ctx->fail(CE_ERR_DEVICE, "mvreg winner out of range");
@@ -610,14 +610,14 @@ int fetch_candidate(ce_core* c, uint32_t i, std::pair<IdDots, uint64_t>* v) {
   hipError_t e;
   if ((e = hipMemcpyAsync(cb, o.rm_cbeg + i, 8, hipMemcpyDeviceToHost, s)) ||
       (e = hipMemcpyAsync(&v->second, o.put_val + i, 8, hipMemcpyDeviceToHost, s)) ||
-      (e = hipStreamSynchronize(s)))
+      (e = stream_wait(s)))
     return c->ctx->hip_fail(e, "candidate");
   const uint32_t k = cb[1] - cb[0];
   std::vector<uint32_t> act(k);
   std::vector<unsigned long long> ctr(k);
   if (k && ((e = hipMemcpyAsync(act.data(), o.rmc_actor + cb[0], k * 4ull, hipMemcpyDeviceToHost, s)) ||
             (e = hipMemcpyAsync(ctr.data(), o.rmc_ctr + cb[0], k * 8ull, hipMemcpyDeviceToHost, s)) ||
-            (e = hipStreamSynchronize(s))))
+            (e = stream_wait(s))))
     return c->ctx->hip_fail(e, "candidate");
   v->first.clear();
   for (uint32_t j = 0; j < k; j++) v->first.push_back({act[j], ctr[j]});
@@ -687,7 +687,7 @@ int gate(ce_core* c, const uint32_t* d_fa, const uint64_t* d_fv, uint32_t n, uin
   if ((e = launch_gate(ctx->stream, ga))) return ctx->hip_fail(e, "gate");
   ctx->tend(t);
   if ((e = hipMemcpyAsync(hf, ga.flags, 8, hipMemcpyDeviceToHost, ctx->stream)) ||
-      (e = hipStreamSynchronize(ctx->stream)))
+      (e = stream_wait(ctx->stream)))
     return ctx->hip_fail(e, "gate");
   if (hf[0]) {
     std::vector<uint32_t> fa(n);
@@ -695,20 +695,20 @@ int gate(ce_core* c, const uint32_t* d_fa, const uint64_t* d_fv, uint32_t n, uin
     std::vector<uint8_t> ap(n);
     if ((e = hipMemcpyAsync(fa.data(), d_fa, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
         (e = hipMemcpyAsync(fv.data(), d_fv, n * 8ull, hipMemcpyDeviceToHost, ctx->stream)) ||
-        (e = hipStreamSynchronize(ctx->stream)))
+        (e = stream_wait(ctx->stream)))
       return ctx->hip_fail(e, "host gate");
     for (uint32_t i = 0; i < n; i++)
       if (fa[i] >= m) return ctx->fail(CE_ERR_INVALID_ARG, "file_actor out of range");
     *first_gap = host_gate(fa.data(), fv.data(), n, expect, ap.data());
     if ((e = hipMemcpyAsync(ctx->apply.p, ap.data(), n, hipMemcpyHostToDevice, ctx->stream)) ||
-        (e = hipStreamSynchronize(ctx->stream)))
+        (e = stream_wait(ctx->stream)))
       return ctx->hip_fail(e, "host gate");
     return CE_OK;
   }
   *first_gap = hf[1] == 0xffffffffu ? n : hf[1];
   std::vector<uint64_t> nn(m);
   if ((e = hipMemcpyAsync(nn.data(), gbase + 8ull * m, m * 8ull, hipMemcpyDeviceToHost, ctx->stream)) ||
-      (e = hipStreamSynchronize(ctx->stream)))
+      (e = stream_wait(ctx->stream)))
     return ctx->hip_fail(e, "gate");
   for (uint32_t a = 0; a < m; a++) (*expect)[a] = std::max((*expect)[a], nn[a]);
   return CE_OK;
@@ -832,7 +832,7 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
     return rc;
   std::vector<int32_t> st(n);
   if ((e = hipMemcpyAsync(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
-      (e = hipStreamSynchronize(ctx->stream)))
+      (e = stream_wait(ctx->stream)))
     return ctx->hip_fail(e, "status");
   for (uint32_t i = 0; i < n; i++)
     if (st[i] == kStatusHostParse) {
@@ -850,7 +850,7 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
   if ((e = launch_ds_count(ctx->stream, a))) return ctx->hip_fail(e, "count");
   ctx->tend(tc);
   if ((e = hipMemcpyAsync(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
-      (e = hipStreamSynchronize(ctx->stream)))
+      (e = stream_wait(ctx->stream)))
     return ctx->hip_fail(e, "count");
   bool host_dec = false;
   for (uint32_t i = 0; i < n; i++) host_dec = host_dec || st[i] == kStatusHostDecode;
@@ -858,7 +858,7 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
     if ((rc = resolve_host_decode(c, n, &st))) return rc;
     if ((e = launch_ds_count(ctx->stream, a)) ||
         (e = hipMemcpyAsync(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
-        (e = hipStreamSynchronize(ctx->stream)))
+        (e = stream_wait(ctx->stream)))
       return ctx->hip_fail(e, "count");
   }
   if ((rc = fail_first(c, st, status_out, n))) return rc;  // all-or-nothing (lib.rs:497-514)
@@ -883,7 +883,7 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
           (e = hipMemcpyAsync(&last_base[j], bases + (size_t)j * n + n - 1, 4, hipMemcpyDeviceToHost, ctx->stream)))
         return ctx->hip_fail(e, "scan");
     }
-    if ((e = hipStreamSynchronize(ctx->stream))) return ctx->hip_fail(e, "scan");
+    if ((e = stream_wait(ctx->stream))) return ctx->hip_fail(e, "scan");
     for (int j = 0; j < kCntN; j++) k.v[j] = (uint64_t)last_cnt[j] + last_base[j];
   }
   // MVReg: the current values come first in the candidate list
@@ -911,7 +911,7 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
     if ((e = launch_ds_emit(ctx->stream, a))) return ctx->hip_fail(e, "emit");
     ctx->tend(te);
     if ((e = hipMemcpyAsync(hm, d->misses.p, 16, hipMemcpyDeviceToHost, ctx->stream)) ||
-        (e = hipStreamSynchronize(ctx->stream)))
+        (e = stream_wait(ctx->stream)))
       return ctx->hip_fail(e, "emit");
     if (hm[2] == 0) break;
     if (round > 64) return ctx->fail(CE_ERR_DEVICE, "actor table did not converge");
@@ -1264,7 +1264,7 @@ struct DevState {
 
 hipError_t dl(void* dst, const void* src, size_t n, hipStream_t s) {
   hipError_t e = hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, s);
-  return e ? e : hipStreamSynchronize(s);
+  return e ? e : stream_wait(s);
 }
 
 // the repeat-check set of a file with n entries: a power of two >= 2 n words (mask = size - 1)
@@ -1331,7 +1331,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     if (!read_state(c->kind, host_pt[i].data(), len[i], &ds[i].hs)) st[i] = CE_ERR_DECODE;
     return CE_OK;
   };
-  auto sync = [&](const char* what) { return (e = hipStreamSynchronize(s)) ? ctx->hip_fail(e, what) : CE_OK; };
+  auto sync = [&](const char* what) { return (e = stream_wait(s)) ? ctx->hip_fail(e, what) : CE_OK; };
   int first = CE_OK;
   {
     HostPhase hp("states: device read");
@@ -1669,7 +1669,7 @@ int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t
   std::vector<unsigned long long> ck(na);
   if ((rc = ensure_clock(c))) return rc;
   if (na && ((e = hipMemcpyAsync(ck.data(), d->clock.p, na * 8ull, hipMemcpyDeviceToHost, c->ctx->stream)) ||
-             (e = hipStreamSynchronize(c->ctx->stream))))
+             (e = stream_wait(c->ctx->stream))))
     return x->hip_fail(e, "clock download");
   IdDots clock;
   for (uint32_t i = 0; i < na; i++)
@@ -1715,7 +1715,7 @@ int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t
     if ((e = d->uuid_of_id.reserve(u.size())) || (e = d->rank_of_id.reserve(4ull * rank.size())) ||
         (e = hipMemcpyAsync(d->uuid_of_id.p, u.data(), u.size(), hipMemcpyHostToDevice, s)) ||
         (e = hipMemcpyAsync(d->rank_of_id.p, rank.data(), 4ull * rank.size(), hipMemcpyHostToDevice, s)) ||
-        (e = hipStreamSynchronize(s)))
+        (e = stream_wait(s)))
       return x->hip_fail(e, "actor ranks");
     d->uuid_ids = na;
   }
@@ -1782,7 +1782,7 @@ int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t
                    x->out.as<uint8_t>(), reinterpret_cast<const uint64_t*>(db + A + 16), key);
   if (rc) return rc;
   uint64_t clear_len = 0;
-  if ((e = hipMemcpyAsync(&clear_len, db + A + 8, 8, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s)))
+  if ((e = hipMemcpyAsync(&clear_len, db + A + 8, 8, hipMemcpyDeviceToHost, s)) || (e = stream_wait(s)))
     return x->hip_fail(e, "ds compact");
   if (clear_len > U) return x->fail(CE_ERR_DEVICE, "serializer overran its bound");
   const uint64_t total = 16 + sealed_len(clear_len);
@@ -1795,7 +1795,7 @@ int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t
     file->resize(total);
     to = file->data();
   }
-  if ((e = hipMemcpyAsync(to, x->out.p, total, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s)))
+  if ((e = hipMemcpyAsync(to, x->out.p, total, hipMemcpyDeviceToHost, s)) || (e = stream_wait(s)))
     return x->hip_fail(e, "ds compact download");
   return CE_OK;
 }
@@ -1847,7 +1847,7 @@ int ds_serialize(ce_core* c, std::vector<uint8_t>* out) {
   const uint32_t na = (uint32_t)c->id_actor.size();
   std::vector<unsigned long long> ck(na);
   if (na && ((e = hipMemcpyAsync(ck.data(), d->clock.p, na * 8ull, hipMemcpyDeviceToHost, s)) ||
-             (e = hipStreamSynchronize(s))))
+             (e = stream_wait(s))))
     return ctx->hip_fail(e, "clock download");
   IdDots clock;
   for (uint32_t i = 0; i < na; i++)
@@ -1879,7 +1879,7 @@ int ds_serialize(ce_core* c, std::vector<uint8_t>* out) {
         (e = hipMemcpyAsync(mem.data(), d->col[3].p, nl * 8ull, hipMemcpyDeviceToHost, s)) ||
         (e = hipMemcpyAsync(act.data(), d->col[4].p, nl * 4ull, hipMemcpyDeviceToHost, s)) ||
         (e = hipMemcpyAsync(val.data(), d->ctr_sorted.p, nl * 8ull, hipMemcpyDeviceToHost, s)) ||
-        (e = hipStreamSynchronize(s)))
+        (e = stream_wait(s)))
       return ctx->hip_fail(e, "serialize");
   }
   hp1.~HostPhase();

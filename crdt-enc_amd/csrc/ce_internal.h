@@ -54,6 +54,25 @@ struct HostBuf {
   T* as() const { return reinterpret_cast<T*>(p); }
 };
 
+// Wait for everything queued on `s` by polling an event (the blocking wait's wake-up costs tens
+// of microseconds on the box; the dot-set paths wait many times per step), yielding the core
+// between polls after the first few.  CE_SYNC_YIELD=1: hipStreamSynchronize.
+inline hipError_t stream_wait(hipStream_t s) {
+  static const bool yield = getenv("CE_SYNC_YIELD") != nullptr;
+  if (yield) return hipStreamSynchronize(s);
+  thread_local hipEvent_t evs[64] = {};  // per device: an event belongs to the device it was made on
+  int dev = 0;
+  hipError_t e;
+  if ((e = hipGetDevice(&dev))) return e;
+  if (dev < 0 || dev >= 64) return hipStreamSynchronize(s);
+  hipEvent_t& ev = evs[dev];
+  if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming))) return e;
+  if ((e = hipEventRecord(ev, s))) return e;
+  for (unsigned i = 0; (e = hipEventQuery(ev)) == hipErrorNotReady; i++)
+    if (i >= 32) sched_yield();
+  return e;
+}
+
 struct KeyRef {
   const uint8_t* version;  // 16
   const uint8_t* key;
