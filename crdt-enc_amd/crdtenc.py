@@ -56,7 +56,7 @@ EXPORTS = [
     "ce_shard_owner", "ce_shard_owners", "ce_shard_stats_len", "ce_core_shard_stats",
     "ce_core_shard_window", "ce_core_ingest_ops_device_sharded", "ce_core_pending_export",
     "ce_core_pending_commit", "ce_core_writer_versions", "ce_shard_stats_host",
-    "ce_shard_window_host", "ce_shard_window_exact",
+    "ce_shard_window_host", "ce_shard_window_exact", "ce_core_compact_ops_device_into",
 ]
 
 
@@ -608,6 +608,21 @@ class Core:
         if rc:
             return rc, None, None
         return rc, _take(b), (nm.value.decode() if name else None)
+
+    def compact_ops_device_into(self, buf, d_blob, d_offs, n, blob_len, actors, d_file_actor,
+                                d_file_version, nonce=None, name=False):
+        """compact_ops_device with the sealed file downloaded straight into the uint8 numpy
+        array `buf` (pinned, e.g. torch.empty(..., pin_memory=True).numpy()): (rc, length,
+        name or None)."""
+        ln = ctypes.c_size_t(0)
+        nm = ctypes.create_string_buffer(64) if name else None
+        rc = lib().ce_core_compact_ops_device_into(
+            self.p, ctypes.c_void_p(d_blob), ctypes.c_void_p(d_offs), ctypes.c_uint32(n),
+            ctypes.c_uint64(blob_len), _ptr(actors)[0], ctypes.c_uint32(len(actors) // 16),
+            ctypes.c_void_p(d_file_actor), ctypes.c_void_p(d_file_version),
+            _cbuf(nonce) if nonce is not None else None, ctypes.c_void_p(buf.ctypes.data),
+            ctypes.c_size_t(buf.nbytes), ctypes.byref(ln), nm)
+        return rc, ln.value, (nm.value.decode() if (name and rc == 0) else None)
 
     def ingest_ops_iov(self, files, actors, file_actor, versions, want_status=True):
         """Per-file host buffers (Storage::load_ops's Vec<u8>s): no concatenation."""

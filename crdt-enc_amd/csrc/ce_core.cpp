@@ -557,7 +557,7 @@ uint32_t host_gate(const uint32_t* fa, const uint64_t* fv, uint32_t n, std::vect
 // after_commit (optional): called once the device commit (k_merge_max_if) is enqueued, before
 // the host waits -- work it enqueues on the stream overlaps the fused kernel's run on the host
 // side.  merged_out: whether the commit happened on the device (the fast path).
-using AfterCommit = std::function<int(const NovApply&)>;
+using AfterCommit = std::function<int(NovApply&)>;
 
 // ingest_ops_dev_once asks for a fresh pass: actors found while decoding plaintext that is not
 // re-opened by the fused kernel (host-parse envelopes, CE_OPEN_MULTI_KEY retries) grew the actor
@@ -688,16 +688,23 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
   if ((e = ctx->out.reserve(blob_len + 16ull * n + 128)) || (e = ctx->status.reserve(n * 4ull + 64)) ||
       (e = ctx->apply.reserve(n + 64)) || (e = ctx->refold.reserve(n + 64)) ||
       (e = c->d_refold2.reserve(n + 64)) || (e = ctx->miss.reserve(65536 * 16)) ||
-      (e = c->d_gate.reserve(m * 32ull + 64)) || (e = ctx->h_stage2.reserve(m * 24ull + 64)) ||
+      (e = c->d_gate.reserve(m * 32ull + 8ull * c->cap + 64)) ||
+      (e = ctx->h_stage2.reserve(m * 32ull + 8ull * c->cap + 64)) ||
       (e = ctx->redo.reserve(n + 64)))
     return ctx->hip_fail(e, "ingest reserve");
 
   // expected versions per writer (next_op_versions.get, lib.rs:481) and the writers' slots ->
   // device in one copy.  Device gate block: e0 u64[m] | wslot u32[m] (8m bytes) | newnov u64[m]
-  // | run_count u32[m] | run_first u32[m]; host stage: e0 | wslot | nov read back
+  // | run_count u32[m] | run_first u32[m] | (with a compaction behind the ingest) the whole
+  // pre-ingest next_op_versions u64[cap]; host stage: e0 | wslot | nov read back | zeros | nov
   uint64_t* he0 = ctx->h_stage2.as<uint64_t>();
   for (uint32_t a = 0; a < m; a++) he0[a] = c->nov[wslot[a]];
   std::memcpy(he0 + m, wslot.data(), m * 4ull);
+  const uint64_t gate_up = after_commit ? 32ull * m + 8ull * c->cap : 16ull * m;
+  if (after_commit) {  // newnov / runs stay zero (the fill cleared them first); nov behind them
+    std::memset(reinterpret_cast<uint8_t*>(he0) + 16ull * m, 0, 16ull * m);
+    std::memcpy(reinterpret_cast<uint8_t*>(he0) + 32ull * m, c->nov.data(), 8ull * c->cap);
+  }
   GateArgs ga{};
   ga.fa = d_fa;
   ga.fv = d_fv;
@@ -729,14 +736,19 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
   // the setup's counters (large-file count [9]) -> host behind an event: read while the fused
   // kernel runs, they decide whether the multi-page kernels are launched at all
   uint32_t* hsetup = ctx->h_counters.as<uint32_t>() + 32;
-  if (!ctx->setup_ev && (e = hipEventCreateWithFlags(&ctx->setup_ev, hipEventDisableTiming)))
+  if ((!ctx->setup_ev && (e = hipEventCreateWithFlags(&ctx->setup_ev, hipEventDisableTiming))) ||
+      (!ctx->side_ev && (e = hipEventCreateWithFlags(&ctx->side_ev, hipEventDisableTiming))) ||
+      (!ctx->side && (e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking))))
     return ctx->hip_fail(e, "event");
-  if ((e = hipMemcpyAsync(hsetup, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->stream)) ||
-      (e = hipEventRecord(ctx->setup_ev, ctx->stream)))
+  // on the side stream, behind the setup kernel: the main stream goes on to the gate and the
+  // fused kernel without a copy between them
+  if ((e = hipEventRecord(ctx->side_ev, ctx->stream)) || (e = hipStreamWaitEvent(ctx->side, ctx->side_ev, 0)) ||
+      (e = hipMemcpyAsync(hsetup, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->side)) ||
+      (e = hipEventRecord(ctx->setup_ev, ctx->side)))
     return ctx->hip_fail(e, "setup counters");
   bool setup_known = false;
   uint32_t n_large = 0;
-  if ((e = hipMemcpyAsync(gbase, he0, m * 16ull, hipMemcpyHostToDevice, ctx->stream)))
+  if ((e = hipMemcpyAsync(gbase, he0, gate_up, hipMemcpyHostToDevice, ctx->stream)))
     return ctx->hip_fail(e, "gate upload");
   {
     const int t = ctx->tbegin("gate");
@@ -851,15 +863,19 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
       return ctx->hip_fail(e, "merge");
     ctx->tend(t);
   }
+  const uint8_t* host_tail = nullptr;
   if (after_commit) {  // the compaction, queued behind the commit (the writers' slots came with e0)
-    const NovApply na{reinterpret_cast<const uint32_t*>(gbase + 8ull * m),
-                      reinterpret_cast<const unsigned long long*>(gbase + 16ull * m), m,
-                      ctx->counters.as<uint32_t>()};
+    NovApply na{reinterpret_cast<const uint32_t*>(gbase + 8ull * m),
+                reinterpret_cast<const unsigned long long*>(gbase + 16ull * m), m,
+                ctx->counters.as<uint32_t>()};
+    na.nov_dev = reinterpret_cast<unsigned long long*>(gbase + 32ull * m);
     if ((rc = (*after_commit)(na))) return rc;
+    host_tail = na.host_tail;  // it downloads the counters and newnov with its own tail
   }
   // the gate's next_op_versions and the counter block, read back together at the end
   uint64_t* hnov = he0 + 2ull * m;
-  if ((e = hipMemcpyAsync(hnov, gbase + 16ull * m, m * 8ull, hipMemcpyDeviceToHost, ctx->stream)))
+  if (!host_tail &&
+      (e = hipMemcpyAsync(hnov, gbase + 16ull * m, m * 8ull, hipMemcpyDeviceToHost, ctx->stream)))
     return ctx->hip_fail(e, "nov");
   if (prof) {
     std::vector<unsigned long long> hp(8ull * 65536);
@@ -882,9 +898,13 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
               sum[0] / sum[6], sum[1] / sum[6], sum[2] / sum[6], sum[3] / sum[6], sum[4] / sum[6], sum[5] / sum[6]);
   }
   uint32_t* hc = ctx->h_counters.as<uint32_t>();
-  if ((e = hipMemcpyAsync(hc, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->stream)) ||
+  if ((!host_tail && (e = hipMemcpyAsync(hc, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->stream))) ||
       (e = ctx->sync_spin()))
     return ctx->hip_fail(e, "fold sync");
+  if (host_tail) {
+    std::memcpy(hc, host_tail + 8, 64);
+    std::memcpy(hnov, host_tail + 72, 8ull * m);
+  }
   const bool merged_on_device = !sharded && (hc[2] | hc[3] | hc[4] | hc[7] | hc[8] | hc[12]) == 0;
   if (sharded && (hc[10] & (kShardBad | kShardE0Mismatch)))
     return ctx->fail(CE_ERR_SHARD, hc[10] & kShardE0Mismatch
@@ -1265,9 +1285,11 @@ int read_remote(ce_core* c) {
 //   compact_finish: after the stream has been synchronised, the file from the staging buffer.
 struct CompactPending {
   uint64_t U = 0, total_max = 0;
+  const uint8_t* tail = nullptr;  // pinned host: [clear length | counters | newnov] after sync
+  bool to_sink = false;           // the file went straight into the caller's buffer (c->sink)
 };
 
-int compact_enqueue(ce_core* c, ce_ctx* x, const uint8_t* nonce, const NovApply* na, CompactPending* pend) {
+int compact_enqueue(ce_core* c, ce_ctx* x, const uint8_t* nonce, NovApply* na, CompactPending* pend) {
   const KeyRef key = key_of(c);
   if (int32_t ks = key_status(key)) return x->fail(ks, "key rejected");
   const bool ingest_fmt = (c->flags & CE_COMPACT_INGEST_FORMAT) != 0;
@@ -1290,53 +1312,80 @@ int compact_enqueue(ce_core* c, ce_ctx* x, const uint8_t* nonce, const NovApply*
   const uint64_t U = vclock_ser_bound(k);             // clear length bound (prefix included)
   const uint64_t A = (U + 255) & ~255ull;              // small arguments after the clear text
   const uint64_t total_max = 16 + sealed_len(U);
+  const uint64_t T = (total_max + 255) & ~255ull;      // the packed tail after the file bound
+  const uint32_t m = na ? na->m : 0;
+  const uint64_t tail_bytes = 72 + 8ull * m;
   const uint64_t nov_bytes = 8ull * c->cap;
-  if ((e = x->blob.reserve(A + 128)) || (e = x->out.reserve(total_max + 64)) ||
-      (e = x->h_stage.reserve(std::max<uint64_t>(total_max + 64, 128 + nov_bytes))) ||
+  uint32_t* seal_counters = ctx_counters(x);
+  if (!seal_counters || (e = x->blob.reserve(A + 128)) || (e = x->out.reserve(T + tail_bytes + 64)) ||
+      (e = x->h_stage.reserve(std::max<uint64_t>(T + tail_bytes + 64, 128 + nov_bytes))) ||
       (e = c->d_tmp.reserve(nov_bytes)))
-    return x->hip_fail(e, "compact reserve");
-  // staging: [offs(2) | out_offs(1) | nonce(24) | outer(16) | prefix16(16)] at 0, nov at 128
+    return x->hip_fail(e ? e : hipErrorOutOfMemory, "compact reserve");
   uint8_t* hs = x->h_stage.as<uint8_t>();
-  const uint64_t args[3] = {0, 0, 0};
-  std::memcpy(hs, args, 24);
-  if (nonce) std::memcpy(hs + 24, nonce, 24);
-  else os_random(hs + 24, 24);
-  std::memcpy(hs + 48, outer, 16);
-  std::memcpy(hs + 64, c->current_data_version.data(), 16);
-  std::memcpy(hs + 128, c->nov.data(), nov_bytes);
   uint8_t* db = x->blob.as<uint8_t>();
-  if ((e = hipMemcpyAsync(db + A, hs, 80, hipMemcpyHostToDevice, x->stream)) ||
-      (e = hipMemcpyAsync(c->d_tmp.p, hs + 128, nov_bytes, hipMemcpyHostToDevice, x->stream)))
-    return x->hip_fail(e, "compact upload");
-  if (na && (e = launch_nov_apply(x->stream, c->d_tmp.as<unsigned long long>(), na->wslot, na->newnov,
-                                  na->m, na->counters)))
-    return x->hip_fail(e, "nov apply");
+  // next_op_versions on the device: with `na` the pre-ingest copy the ingest uploaded with its
+  // gate block (newnov applied below, in place), else uploaded here
+  unsigned long long* nov = c->d_tmp.as<unsigned long long>();
+  if (na && na->nov_dev) {
+    nov = na->nov_dev;
+  } else {
+    std::memcpy(hs + 128, c->nov.data(), nov_bytes);
+    if ((e = hipMemcpyAsync(nov, hs + 128, nov_bytes, hipMemcpyHostToDevice, x->stream)))
+      return x->hip_fail(e, "compact upload");
+  }
+  CompactArgs ca;
+  if (nonce) std::memcpy(ca.nonce, nonce, 24);
+  else os_random(ca.nonce, 24);
+  std::memcpy(ca.outer, outer, 16);
+  std::memcpy(ca.prefix, c->current_data_version.data(), 16);
+  // args at db + A: [offs(2) | out_offs(1) | nonce(24) | outer(16) | prefix16(16)]
+  if ((e = launch_compact_prologue(x->stream, db + A, ca, seal_counters, nov, na ? na->wslot : nullptr,
+                                   na ? na->newnov : nullptr, m, na ? na->counters : nullptr)))
+    return x->hip_fail(e, "compact prologue");
   auto* d_offs = reinterpret_cast<unsigned long long*>(db + A);
-  if ((e = launch_serialize_vclock(x->stream, c->d_tmp.as<unsigned long long>(),
-                                   c->d_state.as<unsigned long long>(), c->d_sorted.as<uint32_t>(), k,
-                                   c->d_table.as<ActorSlot>(), c->kind == CE_STATE_GCOUNTER,
+  if ((e = launch_serialize_vclock(x->stream, nov, c->d_state.as<unsigned long long>(), c->d_sorted.as<uint32_t>(),
+                                   k, c->d_table.as<ActorSlot>(), c->kind == CE_STATE_GCOUNTER,
                                    ingest_fmt ? db + A + 64 : nullptr, db, d_offs)))
     return x->hip_fail(e, "serialize");
   rc = device_seal(x, db, reinterpret_cast<const uint64_t*>(d_offs), 1, U, db + A + 48, db + A + 24,
-                   x->out.as<uint8_t>(), reinterpret_cast<const uint64_t*>(db + A + 16), key);
+                   x->out.as<uint8_t>(), reinterpret_cast<const uint64_t*>(db + A + 16), key, true);
   if (rc) return rc;
-  // the sealed file (its bound) and the clear length
-  if ((e = hipMemcpyAsync(hs, x->out.p, total_max, hipMemcpyDeviceToHost, x->stream)) ||
-      (e = hipMemcpyAsync(hs + total_max, db + A + 8, 8, hipMemcpyDeviceToHost, x->stream)))
-    return x->hip_fail(e, "compact download");
+  // the tail (clear length, and with `na` the ingest's counters and newnov) packed behind the file
+  uint8_t* dtail = x->out.as<uint8_t>() + T;
+  if ((e = launch_tail_pack(x->stream, dtail, reinterpret_cast<const unsigned long long*>(db + A + 8),
+                            na ? na->counters : seal_counters, na ? na->newnov : nullptr, m)))
+    return x->hip_fail(e, "tail pack");
+  // downloads: the file straight into the caller's buffer when it has room (compact_into), the
+  // tail beside it; else file and tail in one copy
+  pend->to_sink = c->sink && c->sink_cap >= total_max;
+  if (pend->to_sink) {
+    if ((e = hipMemcpyAsync(c->sink, x->out.p, total_max, hipMemcpyDeviceToHost, x->stream)) ||
+        (e = hipMemcpyAsync(hs, dtail, tail_bytes, hipMemcpyDeviceToHost, x->stream)))
+      return x->hip_fail(e, "compact download");
+    pend->tail = hs;
+  } else {
+    if ((e = hipMemcpyAsync(hs, x->out.p, T + tail_bytes, hipMemcpyDeviceToHost, x->stream)))
+      return x->hip_fail(e, "compact download");
+    pend->tail = hs + T;
+  }
+  if (na) na->host_tail = pend->tail;
   pend->U = U;
   pend->total_max = total_max;
   return CE_OK;
 }
 
-int compact_finish(ce_ctx* x, const CompactPending& pend, std::vector<uint8_t>* file) {
-  const uint8_t* hs = x->h_stage.as<uint8_t>();
+int compact_finish(ce_core* c, ce_ctx* x, const CompactPending& pend, std::vector<uint8_t>* file) {
   uint64_t clear_len;
-  std::memcpy(&clear_len, hs + pend.total_max, 8);
+  std::memcpy(&clear_len, pend.tail, 8);
   if (clear_len > pend.U) return x->fail(CE_ERR_DEVICE, "serializer overran its bound");
   const uint64_t total = 16 + sealed_len(clear_len);
+  if (pend.to_sink) {
+    c->sink_len = total;
+    file->clear();
+    return CE_OK;
+  }
   file->resize(total);
-  std::memcpy(file->data(), hs, total);
+  std::memcpy(file->data(), x->h_stage.as<uint8_t>(), total);
   return CE_OK;
 }
 
@@ -1346,7 +1395,7 @@ int compact_device(ce_core* c, const uint8_t* nonce, std::vector<uint8_t>* file)
   if (rc) return rc;
   hipError_t e;
   if ((e = stream_wait(c->ctx->stream))) return c->ctx->hip_fail(e, "compact sync");
-  return compact_finish(c->ctx, pend, file);
+  return compact_finish(c, c->ctx, pend, file);
 }
 
 // clear text + file of a compaction (lib.rs:335-360)
@@ -1545,14 +1594,17 @@ int ce_core_ingest_ops_device(ce_core* c, const uint8_t* d_blob, const uint64_t*
 // the ingest's device commit on the aux context's buffers, so one host synchronisation covers
 // both; when the ingest leaves its fast path the speculative file is dropped and the compaction
 // runs again from the committed host state.
-int ce_core_compact_ops_device(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
-                               uint64_t blob_len, const uint8_t* actors, uint32_t m,
-                               const uint32_t* d_file_actor, const uint64_t* d_file_version,
-                               const uint8_t* nonce, ce_buf* file, char name_out[64]) {
-  if (!c || !file || (n && (!d_blob || !d_offs || !actors || !d_file_actor || !d_file_version)))
-    return CE_ERR_INVALID_ARG;
-  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
-  (void)hipSetDevice(c->ctx->device);
+}  // extern "C"
+
+namespace ce {
+// Core::compact over a batch in HBM (shared by ce_core_compact_ops_device[_into]): the file ends
+// up in c->sink when the caller gave one with room (*out = sink, c->sink_len), else in
+// c->file_buf.  The caller holds the context lock.
+static int compact_ops_device_impl(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
+                                   uint64_t blob_len, const uint8_t* actors, uint32_t m,
+                                   const uint32_t* d_file_actor, const uint64_t* d_file_version,
+                                   const uint8_t* nonce, const uint8_t** out, size_t* out_len,
+                                   char name_out[64]) {
   if (!c->has_key) return c->ctx->fail(CE_ERR_NO_KEY, "no latest key");
   std::vector<uint8_t>& f = c->file_buf;
   int rc;
@@ -1563,24 +1615,77 @@ int ce_core_compact_ops_device(ce_core* c, const uint8_t* d_blob, const uint64_t
   uint8_t nb[24];  // one nonce for the speculative and (if needed) the repeated compaction
   if (nonce) std::memcpy(nb, nonce, 24);
   else os_random(nb, 24);
-  const AfterCommit hook = [&](const NovApply& na) { return compact_enqueue(c, x, nb, &na, &pend); };
+  c->sink_len = 0;
+  const AfterCommit hook = [&](NovApply& na) { return compact_enqueue(c, x, nb, &na, &pend); };
   rc = ingest_ops_dev(c, d_blob, d_offs, n, blob_len, actors, m, d_file_actor, d_file_version, nullptr,
                       spec ? &hook : nullptr, &merged);
   if (rc) {
     if (spec) (void)hipStreamSynchronize(c->ctx->stream);  // nothing left in flight on x's buffers
     return rc;  // read_remote's error: compact writes nothing (lib.rs:333)
   }
-  if (spec && merged) rc = compact_finish(x, pend, &f);
+  if (spec && merged) rc = compact_finish(c, x, pend, &f);
   else rc = compact_bytes(c, nb, &f);
   if (rc) return rc;
+  if (c->sink_len) {
+    *out = c->sink;
+    *out_len = c->sink_len;
+  } else {
+    *out = f.data();
+    *out_len = f.size();
+  }
   if (name_out) {
     uint8_t h[32];
-    sha3_256(f.data(), f.size(), h);
+    sha3_256(*out, *out_len, h);
     std::snprintf(name_out, 64, "%s", base32_nopad(h, 32).c_str());
   }
-  file->data = (uint8_t*)malloc(f.size() ? f.size() : 1);
-  std::memcpy(file->data, f.data(), f.size());
-  file->len = f.size();
+  return CE_OK;
+}
+}  // namespace ce
+
+extern "C" {
+
+int ce_core_compact_ops_device(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
+                               uint64_t blob_len, const uint8_t* actors, uint32_t m,
+                               const uint32_t* d_file_actor, const uint64_t* d_file_version,
+                               const uint8_t* nonce, ce_buf* file, char name_out[64]) {
+  if (!c || !file || (n && (!d_blob || !d_offs || !actors || !d_file_actor || !d_file_version)))
+    return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  (void)hipSetDevice(c->ctx->device);
+  const uint8_t* p = nullptr;
+  size_t len = 0;
+  int rc = compact_ops_device_impl(c, d_blob, d_offs, n, blob_len, actors, m, d_file_actor, d_file_version,
+                                   nonce, &p, &len, name_out);
+  if (rc) return rc;
+  file->data = (uint8_t*)malloc(len ? len : 1);
+  std::memcpy(file->data, p, len);
+  file->len = len;
+  return CE_OK;
+}
+
+int ce_core_compact_ops_device_into(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
+                                    uint64_t blob_len, const uint8_t* actors, uint32_t m,
+                                    const uint32_t* d_file_actor, const uint64_t* d_file_version,
+                                    const uint8_t* nonce, uint8_t* dst, size_t cap, size_t* len,
+                                    char name_out[64]) {
+  if (!c || !len || (cap && !dst) || (n && (!d_blob || !d_offs || !actors || !d_file_actor || !d_file_version)))
+    return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  (void)hipSetDevice(c->ctx->device);
+  c->sink = dst;
+  c->sink_cap = cap;
+  const uint8_t* p = nullptr;
+  size_t l = 0;
+  int rc = compact_ops_device_impl(c, d_blob, d_offs, n, blob_len, actors, m, d_file_actor, d_file_version,
+                                   nonce, &p, &l, name_out);
+  c->sink = nullptr;
+  c->sink_cap = 0;
+  if (rc) return rc;
+  *len = l;
+  if (p != dst) {
+    if (cap < l) return c->ctx->fail(CE_ERR_INVALID_ARG, "compact_ops_device_into: buffer too small");
+    std::memcpy(dst, p, l);
+  }
   return CE_OK;
 }
 

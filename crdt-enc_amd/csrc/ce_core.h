@@ -93,6 +93,8 @@ struct ce_core {
   uint64_t pending_gen = 0;                                  // table_gen of the pending batch
   std::vector<std::pair<ce::Uuid, uint64_t>> pending_nov;    // (writer, next_op_version)
   ce::DevBuf d_shard;                  // writer UUIDs | e0 | stats scratch (ce_core_shard_*)
+  ce::HostBuf h_shard;                 // pinned staging of the e0 upload (its own: the copy is async)
+  std::vector<uint64_t> shard_e0;      // the e0 d_shard holds
   std::vector<uint8_t> shard_writers;  // the writer list d_shard holds
 };
 
@@ -156,6 +158,11 @@ struct NovApply {
   const unsigned long long* newnov;      // device: the gate's next_op_versions per writer
   uint32_t m;
   const uint32_t* counters;              // device: the ingest's counter block
+  unsigned long long* nov_dev = nullptr; // device: the pre-ingest next_op_versions (cap words),
+                                         // uploaded with the gate block; the compaction applies
+                                         // newnov to it in place
+  const uint8_t* host_tail = nullptr;    // out (set by the compaction): pinned host copy of
+                                         // [clear length | the counters | newnov[m]] after sync
 };
 
 bool skip_any(Rd& r, int depth = 0);

@@ -158,15 +158,19 @@ int device_open(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint
   return CE_OK;
 }
 
+uint32_t* ctx_counters(ce_ctx* ctx) {
+  return ctx->counters.reserve(256) == hipSuccess ? ctx->counters.as<uint32_t>() : nullptr;
+}
+
 int device_seal(ce_ctx* ctx, const uint8_t* d_clear, const uint64_t* d_offs, uint32_t n,
                 uint64_t clear_len_total, const uint8_t* d_outer_version, const uint8_t* d_nonces,
-                uint8_t* d_out, const uint64_t* d_out_offs, const KeyRef& key) {
+                uint8_t* d_out, const uint64_t* d_out_offs, const KeyRef& key, bool counters_ready) {
   if (int32_t ks = key_status(key)) return ctx->fail(ks, "key rejected");
   uint32_t ec;
   int rc = reserve_batch(ctx, n, clear_len_total + 16ull * n, &ec);
   if (rc) return rc;
   hipError_t e;
-  if ((e = reset_counters(ctx)) != hipSuccess) return ctx->hip_fail(e, "memset counters");
+  if (!counters_ready && (e = reset_counters(ctx)) != hipSuccess) return ctx->hip_fail(e, "memset counters");
   SegScratch sc = segscratch(ctx, ec);
   FileParams* P = ctx->params.as<FileParams>();
   int t = ctx->tbegin("seal_setup");
@@ -311,6 +315,11 @@ void ce_ctx_destroy(ce_ctx* c) {
   for (auto& t : c->timed) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   if (c->setup_ev) (void)hipEventDestroy(c->setup_ev);
+  if (c->side) {
+    (void)hipStreamSynchronize(c->side);
+    (void)hipStreamDestroy(c->side);
+  }
+  if (c->side_ev) (void)hipEventDestroy(c->side_ev);
   if (c->spin_ev) (void)hipEventDestroy(c->spin_ev);
   destroy_uploader(c);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);

@@ -108,6 +108,10 @@ struct ce_ctx {
   ce::HostBuf h_counters, h_apply, h_stage, h_stage2;
   // marks the setup kernel's counter snapshot (h_counters + 128) as landed on the host
   hipEvent_t setup_ev = nullptr;
+  // a side stream for readbacks that must not sit between the main stream's kernels (the setup
+  // counters), and the event it waits on
+  hipStream_t side = nullptr;
+  hipEvent_t side_ev = nullptr;
   ce::Uploader* up = nullptr;  // host-buffer entry points (created on first use)
   ce::HostPool* pool = nullptr;  // created on first use
   // kernel timing (ce_ctx_set_timing)
@@ -184,9 +188,12 @@ int device_open(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint
                 int32_t* d_status, bool sync_counters);
 
 // Seal n clear texts resident in HBM.  d_out_offs[i] = output start of file i.
+// counters_ready: the caller's kernel already reset ctx's counter block (k_compact_prologue)
 int device_seal(ce_ctx* ctx, const uint8_t* d_clear, const uint64_t* d_offs, uint32_t n,
                 uint64_t clear_len_total, const uint8_t* d_outer_version, const uint8_t* d_nonces,
-                uint8_t* d_out, const uint64_t* d_out_offs, const KeyRef& key);
+                uint8_t* d_out, const uint64_t* d_out_offs, const KeyRef& key, bool counters_ready = false);
+// ctx's counter block (device), allocated on first use
+uint32_t* ctx_counters(ce_ctx* ctx);
 
 // Seal one host clear text into a host file: [outer(16)] || Cryptor::encrypt([prefix16] ||
 // clear).  `file` keeps its capacity across calls (the pinned staging buffer is the only copy

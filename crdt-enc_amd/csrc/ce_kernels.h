@@ -174,4 +174,23 @@ hipError_t launch_serialize_vclock(hipStream_t s, const unsigned long long* nov,
                                   uint8_t* out, unsigned long long* offs);
 inline uint64_t vclock_ser_bound(uint64_t k) { return 16 + 24 + 5 + 27 * k + 19 + 5 + 27 * k; }
 
+// The compaction's prologue as one launch (instead of an 80-byte upload, two counter fills and
+// k_nov_apply): the seal's small arguments at `args` -- offs[2] = {0, (serializer)}, out_offs[1]
+// = {0}, nonce (24 B), outer version (16 B), data-version prefix (16 B) --, the seal context's
+// counter block reset (as reset_counters: zero, [5] = [13] = UINT32_MAX), and, with m > 0,
+// nov[wslot[a]] = max(nov[wslot[a]], newnov[a]) unless the ingest's counters flag (k_nov_apply).
+struct CompactArgs {
+  uint8_t nonce[24];
+  uint8_t outer[16];
+  uint8_t prefix[16];
+};
+hipError_t launch_compact_prologue(hipStream_t s, uint8_t* args, const CompactArgs& ca, uint32_t* seal_counters,
+                                   unsigned long long* nov, const uint32_t* wslot,
+                                   const unsigned long long* newnov, uint32_t m, const uint32_t* counters);
+// The compaction's epilogue readback in one place: dst = [clear length u64 (from src_len) |
+// the ingest's counter block (16 u32) | newnov u64[m]], so one download carries what the host
+// reads after the step.
+hipError_t launch_tail_pack(hipStream_t s, uint8_t* dst, const unsigned long long* src_len,
+                            const uint32_t* counters, const unsigned long long* newnov, uint32_t m);
+
 }  // namespace ce

@@ -1401,6 +1401,51 @@ hipError_t launch_nov_apply(hipStream_t s, unsigned long long* nov, const uint32
   return hipGetLastError();
 }
 
+__global__ void k_compact_prologue(uint8_t* args, CompactArgs ca, uint32_t* seal_counters,
+                                   unsigned long long* nov, const uint32_t* wslot,
+                                   const unsigned long long* newnov, uint32_t m, const uint32_t* counters) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < 24) {  // offs[0] = 0, offs[1] = 0 (the serializer writes the clear length), out_offs[0] = 0
+    args[t] = 0;
+  } else if (t < 48) {
+    args[t] = ca.nonce[t - 24];
+  } else if (t < 64) {
+    args[t] = ca.outer[t - 48];
+  } else if (t < 80) {
+    args[t] = ca.prefix[t - 64];
+  } else if (t < 96) {
+    const uint32_t w = t - 80;
+    seal_counters[w] = (w == 5 || w == 13) ? 0xffffffffu : 0u;
+  }
+  if (m == 0 || (counters[2] | counters[3] | counters[4] | counters[7] | counters[8] | counters[12])) return;
+  for (uint32_t a = t; a < m; a += gridDim.x * blockDim.x) atomicMax(&nov[wslot[a]], newnov[a]);
+}
+
+hipError_t launch_compact_prologue(hipStream_t s, uint8_t* args, const CompactArgs& ca, uint32_t* seal_counters,
+                                   unsigned long long* nov, const uint32_t* wslot,
+                                   const unsigned long long* newnov, uint32_t m, const uint32_t* counters) {
+  const uint32_t blocks = m > 96 ? min((m + 255) / 256, 256u) : 1u;
+  hipLaunchKernelGGL(k_compact_prologue, dim3(blocks), dim3(256), 0, s, args, ca, seal_counters, nov, wslot,
+                     newnov, m, counters);
+  return hipGetLastError();
+}
+
+__global__ void k_tail_pack(uint8_t* dst, const unsigned long long* src_len, const uint32_t* counters,
+                            const unsigned long long* newnov, uint32_t m) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t == 0) *reinterpret_cast<unsigned long long*>(dst) = *src_len;
+  if (t < 16) reinterpret_cast<uint32_t*>(dst + 8)[t] = counters[t];
+  auto* nn = reinterpret_cast<unsigned long long*>(dst + 72);
+  for (uint32_t a = t; a < m; a += gridDim.x * blockDim.x) nn[a] = newnov[a];
+}
+
+hipError_t launch_tail_pack(hipStream_t s, uint8_t* dst, const unsigned long long* src_len,
+                            const uint32_t* counters, const unsigned long long* newnov, uint32_t m) {
+  const uint32_t blocks = m > 256 ? min((m + 255) / 256, 64u) : 1u;
+  hipLaunchKernelGGL(k_tail_pack, dim3(blocks), dim3(256), 0, s, dst, src_len, counters, newnov, m);
+  return hipGetLastError();
+}
+
 hipError_t launch_serialize_vclock(hipStream_t s, const unsigned long long* nov,
                                   const unsigned long long* st, const uint32_t* sorted, uint32_t k,
                                   const ActorSlot* table, bool gcounter, const uint8_t* prefix16,

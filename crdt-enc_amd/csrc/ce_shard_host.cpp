@@ -59,15 +59,22 @@ int stage_writers(ce_core* c, const uint8_t* actors, uint32_t m, std::vector<uin
   hipError_t e;
   if ((e = c->d_shard.reserve(48ull * m + 64))) return ctx->hip_fail(e, "shard scratch");
   uint8_t* b = c->d_shard.as<uint8_t>();
-  if (c->shard_writers.size() != 16ull * m || std::memcmp(c->shard_writers.data(), actors, 16ull * m) != 0) {
+  const bool new_writers =
+      c->shard_writers.size() != 16ull * m || std::memcmp(c->shard_writers.data(), actors, 16ull * m) != 0;
+  if (new_writers) {
     c->shard_writers.assign(actors, actors + 16ull * m);
     if ((e = hipMemcpyAsync(b, c->shard_writers.data(), 16ull * m, hipMemcpyHostToDevice, ctx->stream)))
       return ctx->hip_fail(e, "shard writers");
   }
+  if (!new_writers && c->shard_e0 == *e0) return CE_OK;  // d_shard already holds them
+  c->shard_e0 = *e0;
   // staged through the pinned buffer so the copy is asynchronous
-  if ((e = ctx->h_stage2.reserve(8ull * m + 64))) return ctx->hip_fail(e, "shard e0");
-  std::memcpy(ctx->h_stage2.p, e0->data(), 8ull * m);
-  if ((e = hipMemcpyAsync(b + 16ull * m, ctx->h_stage2.p, 8ull * m, hipMemcpyHostToDevice, ctx->stream)))
+  if ((e = c->h_shard.reserve(8ull * m + 64))) return ctx->hip_fail(e, "shard e0");
+  // the previous upload from this buffer has been consumed (ce_core_shard_stats waits at its end;
+  // a window call's copy is ordered before anything later on the stream that could rewrite it)
+  if ((e = stream_wait(ctx->stream))) return ctx->hip_fail(e, "shard e0");
+  std::memcpy(c->h_shard.p, e0->data(), 8ull * m);
+  if ((e = hipMemcpyAsync(b + 16ull * m, c->h_shard.p, 8ull * m, hipMemcpyHostToDevice, ctx->stream)))
     return ctx->hip_fail(e, "shard e0");
   return CE_OK;
 }

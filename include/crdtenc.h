@@ -289,6 +289,16 @@ int ce_core_compact_ops_device(ce_core *c, const uint8_t *d_blob, const uint64_t
                                uint64_t blob_len, const uint8_t *actors, uint32_t m,
                                const uint32_t *d_file_actor, const uint64_t *d_file_version,
                                const uint8_t *nonce, ce_buf *file, char name_out[64]);
+/* ce_core_compact_ops_device into a caller-owned buffer (pinned host memory: the sealed file is
+ * downloaded straight into it, no intermediate copy): *len = the file size.  cap should be at
+ * least 16 + ce_cryptor_sealed_len(bound of the serialized state); when the file does not fit
+ * CE_ERR_INVALID_ARG is returned with *len set (the state is then already folded: call
+ * ce_core_compact_into for the file).  On an error dst's contents are unspecified. */
+int ce_core_compact_ops_device_into(ce_core *c, const uint8_t *d_blob, const uint64_t *d_offs,
+                                    uint32_t n, uint64_t blob_len, const uint8_t *actors, uint32_t m,
+                                    const uint32_t *d_file_actor, const uint64_t *d_file_version,
+                                    const uint8_t *nonce, uint8_t *dst, size_t cap, size_t *len,
+                                    char name_out[64]);
 /* ce_core_compact_ops_device over per-file host buffers (upload as ce_core_ingest_ops_iov,
  * then the device path; file_actor / file_version are host arrays). */
 int ce_core_compact_ops_iov(ce_core *c, const uint8_t *const *files, const size_t *lens, uint32_t n,

@@ -739,6 +739,24 @@ def test_compact_ops_device(ctx, oracle, case, kind):
                                              b"".join(actors), d_fa.data_ptr(), d_fv.data_ptr(),
                                              nonce=nonce)
         assert rc2 == 0 and f2 == f
+        # the same compaction downloaded straight into a caller's pinned buffer (and into a
+        # pageable one, and one too small for the bound)
+        import torch
+        for pinned in (True, False):
+            c3 = new()
+            buf = torch.empty(1 << 20, dtype=torch.uint8, pin_memory=pinned).numpy()
+            rc3, ln, nm3 = c3.compact_ops_device_into(buf, d_blob.data_ptr(), d_offs.data_ptr(), len(files), blen,
+                                                      b"".join(actors), d_fa.data_ptr(), d_fv.data_ptr(),
+                                                      nonce=nonce, name=True)
+            assert rc3 == 0 and bytes(buf[:ln]) == f and nm3 == name
+            assert c3.state_bytes() == ref.state_bytes()
+            c3.close()
+        c4 = new()
+        small = np.zeros(len(f) - 1, np.uint8)
+        rc4, ln4, _ = c4.compact_ops_device_into(small, d_blob.data_ptr(), d_offs.data_ptr(), len(files), blen,
+                                                 b"".join(actors), d_fa.data_ptr(), d_fv.data_ptr(), nonce=nonce)
+        assert rc4 == 64 and ln4 == len(f)   # CE_ERR_INVALID_ARG with the size it needs
+        c4.close()
     core.close()
     ref.close()
 
