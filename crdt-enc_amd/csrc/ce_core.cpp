@@ -700,11 +700,7 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
   uint64_t* he0 = ctx->h_stage2.as<uint64_t>();
   for (uint32_t a = 0; a < m; a++) he0[a] = c->nov[wslot[a]];
   std::memcpy(he0 + m, wslot.data(), m * 4ull);
-  const uint64_t gate_up = after_commit ? 32ull * m + 8ull * c->cap : 16ull * m;
-  if (after_commit) {  // newnov / runs stay zero (the fill cleared them first); nov behind them
-    std::memset(reinterpret_cast<uint8_t*>(he0) + 16ull * m, 0, 16ull * m);
-    std::memcpy(reinterpret_cast<uint8_t*>(he0) + 32ull * m, c->nov.data(), 8ull * c->cap);
-  }
+  if (after_commit) std::memcpy(reinterpret_cast<uint8_t*>(he0) + 32ull * m, c->nov.data(), 8ull * c->cap);
   GateArgs ga{};
   ga.fa = d_fa;
   ga.fv = d_fv;
@@ -717,6 +713,17 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
   ga.run_first = reinterpret_cast<uint32_t*>(gbase + 28ull * m);
   ga.flags = ctx->counters.as<uint32_t>() + 12;  // [12] not grouped, [13] first gap
   ga.apply = ctx->apply.as<uint8_t>();
+
+  // the gate block upload on a side stream, overlapping the fill and setup kernels (the main
+  // stream waits for it before the gate; the regions it writes are not the fill's): e0 | wslot,
+  // and with a compaction behind the ingest the pre-ingest next_op_versions
+  if ((!ctx->side && (e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking))) ||
+      (!ctx->up_ev && (e = hipEventCreateWithFlags(&ctx->up_ev, hipEventDisableTiming))) ||
+      (e = hipMemcpyAsync(gbase, he0, 12ull * m, hipMemcpyHostToDevice, ctx->side)) ||
+      (after_commit && (e = hipMemcpyAsync(gbase + 32ull * m, reinterpret_cast<uint8_t*>(he0) + 32ull * m,
+                                           8ull * c->cap, hipMemcpyHostToDevice, ctx->side))) ||
+      (e = hipEventRecord(ctx->up_ev, ctx->side)))
+    return ctx->hip_fail(e, "gate upload");
 
   // 1) GPU: scratch initialisation (one launch: counters, gate, batch state, miss / redo
   //    marks), setup (outer version, envelope, key schedule), device gate
@@ -748,8 +755,7 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
     return ctx->hip_fail(e, "setup counters");
   bool setup_known = false;
   uint32_t n_large = 0;
-  if ((e = hipMemcpyAsync(gbase, he0, gate_up, hipMemcpyHostToDevice, ctx->stream)))
-    return ctx->hip_fail(e, "gate upload");
+  if ((e = hipStreamWaitEvent(ctx->stream, ctx->up_ev, 0))) return ctx->hip_fail(e, "gate upload");
   {
     const int t = ctx->tbegin("gate");
     if ((e = sharded ? launch_gate_window(ctx->stream, ga, shard_hi, ctx->counters.as<uint32_t>())
@@ -1358,7 +1364,11 @@ int compact_enqueue(ce_core* c, ce_ctx* x, const uint8_t* nonce, NovApply* na, C
   // downloads: the file straight into the caller's buffer when it has room (compact_into), the
   // tail beside it; else file and tail in one copy
   pend->to_sink = c->sink && c->sink_cap >= total_max;
-  if (pend->to_sink) {
+  if (pend->to_sink && c->sink_cap >= T + tail_bytes) {  // room for the tail too: one copy
+    if ((e = hipMemcpyAsync(c->sink, x->out.p, T + tail_bytes, hipMemcpyDeviceToHost, x->stream)))
+      return x->hip_fail(e, "compact download");
+    pend->tail = c->sink + T;
+  } else if (pend->to_sink) {
     if ((e = hipMemcpyAsync(c->sink, x->out.p, total_max, hipMemcpyDeviceToHost, x->stream)) ||
         (e = hipMemcpyAsync(hs, dtail, tail_bytes, hipMemcpyDeviceToHost, x->stream)))
       return x->hip_fail(e, "compact download");

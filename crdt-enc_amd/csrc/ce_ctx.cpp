@@ -320,6 +320,7 @@ void ce_ctx_destroy(ce_ctx* c) {
     (void)hipStreamDestroy(c->side);
   }
   if (c->side_ev) (void)hipEventDestroy(c->side_ev);
+  if (c->up_ev) (void)hipEventDestroy(c->up_ev);
   if (c->spin_ev) (void)hipEventDestroy(c->spin_ev);
   destroy_uploader(c);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);

@@ -106,9 +106,14 @@ hipError_t launch_ds_deferred(hipStream_t s, const uint32_t* cbeg, const uint32_
                               uint8_t* deferred, uint32_t n_rm);
 // state merge: insert the other state's entries with oth = value, then the per-pair merge rule
 hipError_t launch_ds_put_other(hipStream_t s, DsTables t, const unsigned long long* member,
-                               const uint32_t* actor, const unsigned long long* value, uint32_t n);
+                               const uint32_t* actor, const unsigned long long* value, uint32_t n,
+                               bool zero_counts = false);
 hipError_t launch_ds_merge(hipStream_t s, DsTables t, const unsigned long long* clock,
                            const unsigned long long* oclock);
+// k_ds_merge + k_ds_finalize in one pass (counts into live[0..1], zeroed by put_other with
+// zero_counts)
+hipError_t launch_ds_merge_finalize(hipStream_t s, DsTables t, const unsigned long long* clock,
+                                   const unsigned long long* oclock);
 // live pairs -> (member, actor, value) in bucket order; count in t.live[0] beforehand
 hipError_t launch_ds_collect(hipStream_t s, DsTables t, unsigned long long* member, uint32_t* actor,
                              unsigned long long* value, uint32_t* n_out);

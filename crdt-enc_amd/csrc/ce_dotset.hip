@@ -443,7 +443,10 @@ __global__ void k_ds_deferred(const uint32_t* cbeg, const uint32_t* c_actor,
 
 __global__ void __launch_bounds__(kBlock) k_ds_put_other(DsTables t, const unsigned long long* member,
                                                          const uint32_t* actor,
-                                                         const unsigned long long* value, uint32_t n) {
+                                                         const unsigned long long* value, uint32_t n,
+                                                         int zero_counts) {
+  // k_ds_merge_finalize (next on the stream) counts into live[0..1]
+  if (zero_counts && blockIdx.x == 0 && threadIdx.x < 2) t.live[threadIdx.x] = 0;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
     const unsigned long long h = member_find(t, member[i], true);
     if (h == kDsEmpty) continue;
@@ -467,6 +470,53 @@ __global__ void k_ds_merge(DsTables t, const unsigned long long* clock, const un
     if (o > clock[a] && o > r) r = o;
     t.cur[b] = r;
     t.oth[b] = 0;
+  }
+}
+
+// k_ds_merge then k_ds_finalize in one pass over the pair table (a state merge queued without a
+// host round trip): the merged value goes through finalize's add / kill thresholds, the pair
+// scratch is cleared, and live / used pairs are counted (live[0..1], zeroed by k_ds_put_other).
+__global__ void __launch_bounds__(kBlock) k_ds_merge_finalize(DsTables t, const unsigned long long* clock,
+                                                              const unsigned long long* oclock) {
+  const uint32_t cap = t.pmask + 1;
+  uint32_t n_used = 0, n_live = 0;
+  for (uint32_t b = blockIdx.x * kBlock + threadIdx.x; b < cap; b += gridDim.x * kBlock) {
+    const unsigned long long key = t.pkey[b];
+    if (key == kDsEmpty) continue;
+    n_used++;
+    const uint32_t a = (uint32_t)(key & ((1u << kDsActorBits) - 1));
+    const unsigned long long s = t.cur[b], o = t.oth[b], ad = t.add[b], kl = t.kill[b];
+    unsigned long long r = 0;
+    if (s == o) r = s;
+    if (s > oclock[a] && s > r) r = s;
+    if (o > clock[a] && o > r) r = o;
+    unsigned long long v = r > ad ? r : ad;
+    if (v != 0 && v <= kl) v = 0;
+    if (v != s) t.cur[b] = v;
+    if (o) t.oth[b] = 0;
+    if (ad) t.add[b] = 0;
+    if (kl) t.kill[b] = 0;
+    n_live += v != 0;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    n_used += __shfl_xor(n_used, o);
+    n_live += __shfl_xor(n_live, o);
+  }
+  __shared__ uint32_t part[2][kBlock / 64];
+  if ((threadIdx.x & 63) == 0) {
+    part[0][threadIdx.x >> 6] = n_live;
+    part[1][threadIdx.x >> 6] = n_used;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t l = 0, u = 0;
+    for (int w = 0; w < kBlock / 64; w++) {
+      l += part[0][w];
+      u += part[1][w];
+    }
+    if (l) atomicAdd(t.live + 0, l);
+    if (u) atomicAdd(t.live + 1, u);
   }
 }
 
@@ -722,9 +772,18 @@ hipError_t launch_ds_deferred(hipStream_t s, const uint32_t* cbeg, const uint32_
 }
 
 hipError_t launch_ds_put_other(hipStream_t s, DsTables t, const unsigned long long* member,
-                               const uint32_t* actor, const unsigned long long* value, uint32_t n) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ds_put_other, dim3(blocks_for(n)), dim3(kBlock), 0, s, t, member, actor, value, n);
+                               const uint32_t* actor, const unsigned long long* value, uint32_t n,
+                               bool zero_counts) {
+  if (n == 0 && !zero_counts) return hipSuccess;
+  hipLaunchKernelGGL(k_ds_put_other, dim3(n ? blocks_for(n) : 1), dim3(kBlock), 0, s, t, member, actor, value, n,
+                     zero_counts ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t launch_ds_merge_finalize(hipStream_t s, DsTables t, const unsigned long long* clock,
+                                   const unsigned long long* oclock) {
+  hipLaunchKernelGGL(k_ds_merge_finalize, dim3(blocks_for((uint64_t)t.pmask + 1, 1024)), dim3(kBlock), 0, s, t,
+                     clock, oclock);
   return hipGetLastError();
 }
 

@@ -49,7 +49,7 @@ struct DsState {
   // bases, members, sorted members [0..6]
   // and emitted (member, actor id, value) columns [7..9]), pinned staging for its downloads
   std::vector<std::array<DevBuf, 10>> rd;
-  DevBuf rd_tmp, rd_misc, ser[16], uuid_of_id, rank_of_id;
+  DevBuf rd_tmp, rd_misc, ser[16], uuid_of_id, rank_of_id, rd_oclocks;
   HostBuf rd_host, rd_small, rd_clock;
   uint64_t uuid_ids = ~0ull;  // id count uuid_of_id / rank_of_id were built for
 };
@@ -1052,10 +1052,12 @@ struct OtherCols {  // the other state's (member, actor id, value) columns in HB
   const unsigned long long* value;
   const unsigned long long* clock_host = nullptr;  // pinned dense clock by actor id, or null
   uint32_t clock_cap = 0;
+  const unsigned long long* clock_dev = nullptr;   // the same dense clock already in HBM, or null
 };
 int orswot_merge_cols(ce_core* c, const IdDots& oclock,
                       const std::vector<std::pair<IdDots, std::vector<uint64_t>>>& od,
-                      const OtherCols& oc, uint32_t n, uint32_t* live_async, bool* queued = nullptr);
+                      const OtherCols& oc, uint32_t n, uint32_t* live_async, bool* queued = nullptr,
+                      bool want_live = true);
 
 // Orswot::merge(other) on the device (entries) and host (deferred)
 int orswot_merge_one(ce_core* c, const HostState& hs) {
@@ -1120,7 +1122,8 @@ int orswot_merge_one(ce_core* c, const HostState& hs) {
 // used_pairs grows by the upper bound n meanwhile.
 int orswot_merge_cols(ce_core* c, const IdDots& oclock,
                       const std::vector<std::pair<IdDots, std::vector<uint64_t>>>& od,
-                      const OtherCols& ocols, uint32_t n, uint32_t* live_async, bool* queued) {
+                      const OtherCols& ocols, uint32_t n, uint32_t* live_async, bool* queued,
+                      bool want_live) {
   DsState* d = c->ds;
   ce_ctx* ctx = c->ctx;
   hipStream_t s = ctx->stream;
@@ -1128,7 +1131,14 @@ int orswot_merge_cols(ce_core* c, const IdDots& oclock,
   if ((rc = ensure_clock(c))) return rc;
   hipError_t e;
   const uint32_t cap = d->clock_cap;
-  if (live_async && ocols.clock_host && ocols.clock_cap == cap) {  // pinned: no host wait
+  // other.deferred applied, clocks merged, apply_deferred: thresholds from both deferred sets
+  auto rms = deferred_list(d);
+  rms.insert(rms.end(), od.begin(), od.end());
+  const bool queue = live_async && rms.empty();
+  const unsigned long long* oclk = d->oclock.as<unsigned long long>();
+  if (queue && ocols.clock_dev && ocols.clock_cap == cap) {  // already in HBM
+    oclk = ocols.clock_dev;
+  } else if (queue && ocols.clock_host && ocols.clock_cap == cap) {  // pinned: no host wait
     if ((e = hipMemcpyAsync(d->oclock.p, ocols.clock_host, cap * 8ull, hipMemcpyHostToDevice, s)))
       return ctx->hip_fail(e, "merge");
   } else {
@@ -1136,25 +1146,27 @@ int orswot_merge_cols(ce_core* c, const IdDots& oclock,
     for (auto& x : oclock) oc[x.first] = x.second;
     if ((e = up(d->oclock.as<unsigned long long>(), oc, s))) return ctx->hip_fail(e, "merge");
   }
+  if (queue) {
+    // no deferred removals on either side: merge + finalize in one pass over the pairs, then
+    // the clock; the counts come back only for the merge the caller reads them after
+    const int tm = ctx->tbegin("ds_merge");
+    if ((e = launch_ds_put_other(s, tables(d), ocols.member, ocols.actor, ocols.value, n, true)) ||
+        (e = launch_ds_merge_finalize(s, tables(d), d->clock.as<unsigned long long>(), oclk)) ||
+        (e = launch_merge_max(s, d->clock.as<unsigned long long>(), oclk, cap)))
+      return ctx->hip_fail(e, "merge");
+    ctx->tend(tm);
+    if (want_live && (e = hipMemcpyAsync(live_async, d->live.p, 16, hipMemcpyDeviceToHost, s)))
+      return ctx->hip_fail(e, "finalize");
+    d->used_pairs += n;
+    if (queued) *queued = true;
+    return CE_OK;
+  }
   const int tm = ctx->tbegin("ds_merge");
   if ((e = launch_ds_put_other(s, tables(d), ocols.member, ocols.actor, ocols.value, n)) ||
       (e = launch_ds_merge(s, tables(d), d->clock.as<unsigned long long>(), d->oclock.as<unsigned long long>())))
     return ctx->hip_fail(e, "merge");
   ctx->tend(tm);
-  // other.deferred applied, clocks merged, apply_deferred: thresholds from both deferred sets
-  auto rms = deferred_list(d);
-  rms.insert(rms.end(), od.begin(), od.end());
-  if (live_async && rms.empty()) {
-    if ((e = launch_merge_max(s, d->clock.as<unsigned long long>(), d->oclock.as<unsigned long long>(), cap)) ||
-        (e = hipMemsetAsync(d->live.p, 0, 8, s)))
-      return ctx->hip_fail(e, "merge");
-    const int t = ctx->tbegin("ds_finalize");
-    if ((e = launch_ds_finalize(s, tables(d)))) return ctx->hip_fail(e, "finalize");
-    ctx->tend(t);
-    if ((e = hipMemcpyAsync(live_async, d->live.p, 16, hipMemcpyDeviceToHost, s))) return ctx->hip_fail(e, "finalize");
-    d->used_pairs += n;
-    if (queued) *queued = true;
-    return CE_OK;
+  {
   }
   if ((rc = upload_removals(c, rms))) return rc;
   const uint32_t nr = (uint32_t)rms.size();
@@ -1518,6 +1530,13 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
       std::memset(hclk + (size_t)ccap * i, 0, 8ull * ccap);
       for (auto& y : ds[i].oclock) hclk[(size_t)ccap * i + y.first] = y.second;
     }
+  // every file's dense other-clock in HBM with one copy
+  if ((e = d->rd_oclocks.reserve(8ull * ccap * n + 64)) ||
+      (e = hipMemcpyAsync(d->rd_oclocks.p, hclk, 8ull * ccap * n, hipMemcpyHostToDevice, s)))
+    return ctx->hip_fail(e, "merge");
+  size_t last_dev = n;
+  for (size_t i = 0; i < n; i++)
+    if (ds[i].device) last_dev = i;
   std::vector<uint8_t> queued(n, 0);
   bool last_queued = false;
   for (size_t i = 0; i < n; i++) {  // lib.rs:458-466, in order
@@ -1525,11 +1544,10 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     if (x.device) {
       auto& b = d->rd[i];
       bool q = false;
+      OtherCols oc{b[7].as<unsigned long long>(), b[8].as<uint32_t>(), b[9].as<unsigned long long>(),
+                   hclk + (size_t)ccap * i, ccap, d->rd_oclocks.as<unsigned long long>() + (size_t)ccap * i};
       if ((rc = ensure_pairs(c, x.n_dots)) ||
-          (rc = orswot_merge_cols(c, x.oclock, x.od,
-                                  {b[7].as<unsigned long long>(), b[8].as<uint32_t>(), b[9].as<unsigned long long>(),
-                                   hclk + (size_t)ccap * i, ccap},
-                                  x.n_dots, live + 4 * i, &q)))
+          (rc = orswot_merge_cols(c, x.oclock, x.od, oc, x.n_dots, live + 4 * i, &q, i == last_dev)))
         return rc;
       queued[i] = q;
       last_queued = q;
@@ -1547,8 +1565,9 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     HostPhase hs("  merge: wait");
     if ((rc = sync("merge"))) return rc;
   }
-  for (size_t i = 0; i < n; i++)
-    if (queued[i] && live[4 * i + 2]) return ctx->fail(CE_ERR_DEVICE, "dot-set table overflow");
+  // the overflow flag (live[2]) is sticky on the device: the last merge's download carries it
+  if (last_dev < n && queued[last_dev] && live[4 * last_dev + 2])
+    return ctx->fail(CE_ERR_DEVICE, "dot-set table overflow");
   for (size_t i = n; i-- > 0;)
     if (queued[i]) {
       if (last_queued) {

@@ -112,6 +112,7 @@ struct ce_ctx {
   // counters), and the event it waits on
   hipStream_t side = nullptr;
   hipEvent_t side_ev = nullptr;
+  hipEvent_t up_ev = nullptr;  // the side stream's uploads (the main stream waits on it)
   ce::Uploader* up = nullptr;  // host-buffer entry points (created on first use)
   ce::HostPool* pool = nullptr;  // created on first use
   // kernel timing (ce_ctx_set_timing)
