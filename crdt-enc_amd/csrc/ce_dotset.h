@@ -136,6 +136,11 @@ hipError_t ds_excl_max_by_key(void* tmp, size_t& tb, const uint32_t* keys,
                               hipStream_t s);
 hipError_t ds_excl_sum_u32(void* tmp, size_t& tb, const uint32_t* in, uint32_t* out, uint32_t n,
                            hipStream_t s);
+// totals of the kCntN columns of one back-to-back exclusive scan (out[kCntN], device)
+hipError_t launch_ds_col_totals(hipStream_t s, const uint32_t* cnt, const uint32_t* bases, uint32_t n,
+                                uint32_t* out);
+hipError_t launch_ds_set3(hipStream_t s, uint32_t* p0, uint32_t v0, uint32_t* p1, uint32_t v1, uint32_t* p2,
+                          uint32_t v2);
 
 // MVReg survivors: candidates = CSR clocks (cbeg, actor, ctr) with priorities (index order)
 struct MvArgs {

@@ -313,11 +313,14 @@ __global__ void __launch_bounds__(kBlock) k_ds_emit(DsDecodeArgs a) {
     EmitSink es;
     es.a = &a;
     es.p = p;
-    es.ia = a.base_off[kCntAdd] + a.cnt[(size_t)kCntAdd * a.n + i];
-    es.iam = a.base_off[kCntAddM] + a.cnt[(size_t)kCntAddM * a.n + i];
-    es.ir = a.base_off[kCntRm] + a.cnt[(size_t)kCntRm * a.n + i];
-    es.irc = a.base_off[kCntRmC] + a.cnt[(size_t)kCntRmC * a.n + i];
-    es.irm = a.base_off[kCntRmM] + a.cnt[(size_t)kCntRmM * a.n + i];
+    // the bases are one exclusive scan over all kCntN columns back to back: column k's base is
+    // its entry minus the column's first (u32 arithmetic: exact while a column's total < 2^32)
+    auto base = [&](int k) { return a.cnt[(size_t)k * a.n + i] - a.cnt[(size_t)k * a.n]; };
+    es.ia = a.base_off[kCntAdd] + base(kCntAdd);
+    es.iam = a.base_off[kCntAddM] + base(kCntAddM);
+    es.ir = a.base_off[kCntRm] + base(kCntRm);
+    es.irc = a.base_off[kCntRmC] + base(kCntRmC);
+    es.irm = a.base_off[kCntRmM] + base(kCntRmM);
     parse_file(a.kind, p, len - 16, es);
   }
 }
@@ -696,6 +699,35 @@ hipError_t ds_excl_max_by_key(void* tmp, size_t& tb, const uint32_t* keys,
 hipError_t ds_excl_sum_u32(void* tmp, size_t& tb, const uint32_t* in, uint32_t* out, uint32_t n,
                            hipStream_t s) {
   return hipcub::DeviceScan::ExclusiveSum(tmp, tb, in, out, (int)n, s);
+}
+
+// per column of the back-to-back scan: total = last base + last count - first base
+__global__ void k_ds_col_totals(const uint32_t* cnt, const uint32_t* bases, uint32_t n, uint32_t* out) {
+  const uint32_t k = threadIdx.x;
+  if (k < kCntN) {
+    const size_t c0 = (size_t)k * n, cl = c0 + n - 1;
+    out[k] = bases[cl] + cnt[cl] - bases[c0];
+  }
+}
+
+hipError_t launch_ds_col_totals(hipStream_t s, const uint32_t* cnt, const uint32_t* bases, uint32_t n,
+                                uint32_t* out) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ds_col_totals, dim3(1), dim3(64), 0, s, cnt, bases, n, out);
+  return hipGetLastError();
+}
+
+// up to three u32 stores with by-value data (small patches without a host staging buffer)
+__global__ void k_ds_set3(uint32_t* p0, uint32_t v0, uint32_t* p1, uint32_t v1, uint32_t* p2, uint32_t v2) {
+  if (threadIdx.x == 0 && p0) *p0 = v0;
+  if (threadIdx.x == 1 && p1) *p1 = v1;
+  if (threadIdx.x == 2 && p2) *p2 = v2;
+}
+
+hipError_t launch_ds_set3(hipStream_t s, uint32_t* p0, uint32_t v0, uint32_t* p1, uint32_t v1, uint32_t* p2,
+                          uint32_t v2) {
+  hipLaunchKernelGGL(k_ds_set3, dim3(1), dim3(64), 0, s, p0, v0, p1, v1, p2, v2);
+  return hipGetLastError();
 }
 
 hipError_t launch_ds_count(hipStream_t s, const DsDecodeArgs& a) {

@@ -49,7 +49,7 @@ struct DsState {
   // bases, members, sorted members [0..6]
   // and emitted (member, actor id, value) columns [7..9]), pinned staging for its downloads
   std::vector<std::array<DevBuf, 10>> rd;
-  DevBuf rd_tmp, rd_misc, ser[16], uuid_of_id, rank_of_id, rd_oclocks;
+  DevBuf rd_tmp, rd_misc, ser[16], uuid_of_id, rank_of_id, rd_oclocks, cnt_tot;
   HostBuf rd_host, rd_small, rd_clock;
   uint64_t uuid_ids = ~0ull;  // id count uuid_of_id / rank_of_id were built for
 };
@@ -329,15 +329,10 @@ DsOps ops_view(DsState* d) {
 int write_sentinels(ce_core* c, const Counts& k) {
   DsState* d = c->ds;
   DsOps o = ops_view(d);
-  uint32_t* h = d->h_cnt.as<uint32_t>() + 16;
-  h[0] = (uint32_t)k.v[kCntAddM];
-  h[1] = (uint32_t)k.v[kCntRmC];
-  h[2] = (uint32_t)k.v[kCntRmM];
   hipError_t e;
-  if ((e = hipMemcpyAsync(o.add_mbeg + k.v[kCntAdd], h + 0, 4, hipMemcpyHostToDevice, c->ctx->stream)) ||
-      (e = hipMemcpyAsync(o.rm_cbeg + k.v[kCntRm], h + 1, 4, hipMemcpyHostToDevice, c->ctx->stream)) ||
-      (e = hipMemcpyAsync(o.rm_mbeg + k.v[kCntRm], h + 2, 4, hipMemcpyHostToDevice, c->ctx->stream)) ||
-      (e = stream_wait(c->ctx->stream)))
+  if ((e = launch_ds_set3(c->ctx->stream, o.add_mbeg + k.v[kCntAdd], (uint32_t)k.v[kCntAddM],
+                          o.rm_cbeg + k.v[kCntRm], (uint32_t)k.v[kCntRmC], o.rm_mbeg + k.v[kCntRm],
+                          (uint32_t)k.v[kCntRmM])))
     return c->ctx->hip_fail(e, "sentinels");
   return CE_OK;
 }
@@ -868,23 +863,25 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
   // 4) bases: exclusive scan of each count column
   Counts k;
   {
+    // one exclusive scan over the kCntN count columns back to back (the emit subtracts each
+    // column's first base), the column totals by a one-block kernel, one small download
     uint32_t* cnt = d->cnt.as<uint32_t>();
-    uint32_t last_cnt[kCntN], last_base[kCntN];
-    for (int j = 0; j < kCntN; j++)
-      if ((e = hipMemcpyAsync(&last_cnt[j], cnt + (size_t)j * n + n - 1, 4, hipMemcpyDeviceToHost, ctx->stream)))
-        return ctx->hip_fail(e, "scan");
     uint32_t* bases = cnt + (size_t)kCntN * n;
+    uint32_t* dtot = d->cnt_tot.as<uint32_t>();
+    uint32_t* htot = d->h_cnt.as<uint32_t>() + 32;
+    if ((uint64_t)kCntN * n > 0x7fffffffull) return ctx->fail(CE_ERR_INVALID_ARG, "batch too large for one scan");
     size_t tb = 0;
-    if ((e = ds_excl_sum_u32(nullptr, tb, cnt, bases, n, ctx->stream)) || (e = d->cub_tmp.reserve(tb + 256)))
+    if ((e = d->cnt_tot.reserve(64)) || (e = ds_excl_sum_u32(nullptr, tb, cnt, bases, kCntN * n, ctx->stream)) ||
+        (e = d->cub_tmp.reserve(tb + 256)))
       return ctx->hip_fail(e, "scan");
-    for (int j = 0; j < kCntN; j++) {
-      size_t t = d->cub_tmp.cap;
-      if ((e = ds_excl_sum_u32(d->cub_tmp.p, t, cnt + (size_t)j * n, bases + (size_t)j * n, n, ctx->stream)) ||
-          (e = hipMemcpyAsync(&last_base[j], bases + (size_t)j * n + n - 1, 4, hipMemcpyDeviceToHost, ctx->stream)))
-        return ctx->hip_fail(e, "scan");
-    }
-    if ((e = stream_wait(ctx->stream))) return ctx->hip_fail(e, "scan");
-    for (int j = 0; j < kCntN; j++) k.v[j] = (uint64_t)last_cnt[j] + last_base[j];
+    dtot = d->cnt_tot.as<uint32_t>();
+    size_t t = d->cub_tmp.cap;
+    if ((e = ds_excl_sum_u32(d->cub_tmp.p, t, cnt, bases, kCntN * n, ctx->stream)) ||
+        (e = launch_ds_col_totals(ctx->stream, cnt, bases, n, dtot)) ||
+        (e = hipMemcpyAsync(htot, dtot, 4 * kCntN, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (e = stream_wait(ctx->stream)))
+      return ctx->hip_fail(e, "scan");
+    for (int j = 0; j < kCntN; j++) k.v[j] = htot[j];
   }
   // MVReg: the current values come first in the candidate list
   HostCols vc;
