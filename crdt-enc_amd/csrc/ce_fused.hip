@@ -266,6 +266,101 @@ __device__ __forceinline__ void decode_fold(const DecodeArgs& a, const SupVers& 
     }
     fold_slot(slot, k0, k1, k2, k3, ctr);
   };
+  // Template path (a writer's own increments, the common GCounter op file): Dot 0 canonical and
+  // every Dot carrying Dot 0's 34-byte prefix -- the same actor and marker, hence the same
+  // length L0 > 34 and a canonical Dot -- checked as whole-word compares against Dot 0; each
+  // lane keeps the max counter of its Dots.  Nothing is folded unless every Dot of the file
+  // verifies: any other file (a Dot of another actor, a non-canonical Dot, fixint counters)
+  // goes on to the paths below from Dot 0, exactly as if this block were absent.  Mixed-actor
+  // files stop after their first LPF Dots.  Folding the max counter of Dots that all name one
+  // actor is what folding them one by one does (VClock::apply, crdt-enc/src/lib.rs:533-535).
+  {
+    uint32_t L0 = 0;
+    if (live && st == CE_OK && remaining > 1 && pos + 34 <= blen) L0 = dot_len_of_marker(body[pos + 33]);
+    bool tp = L0 > 34u && (uint64_t)pos + remaining * L0 <= blen;
+    if (__any(tp)) {
+      prefetch();  // lands under the checks below (its wait comes with the fold's table lookup)
+      pf_done = true;
+      const uint32_t* b32 = reinterpret_cast<const uint32_t*>(body);
+      uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+      if (tp) {  // Dot 0 in full (every lane of the group; its actor is the file's)
+        const uint32_t* d = b32 + (pos >> 2);
+        uint32_t dd[13], w[12];
+#pragma unroll
+        for (int q = 0; q < 13; q++) dd[q] = d[q];
+#pragma unroll
+        for (int q = 0; q < 12; q++) w[q] = __builtin_amdgcn_alignbyte(dd[q + 1], dd[q], pos);
+        unsigned long long c0;
+        tp = canon_dot(w, L0, a0, a1, a2, a3, c0);
+        // Dot 1's actor first: files whose Dots name many actors (C2 variant B) leave here
+        const uint32_t p1 = pos + L0 + 9u;
+        const uint32_t* d1 = b32 + (p1 >> 2);
+        uint32_t e[5];
+#pragma unroll
+        for (int q = 0; q < 5; q++) e[q] = d1[q];
+        tp = tp && __builtin_amdgcn_alignbyte(e[1], e[0], p1) == a0 &&
+             __builtin_amdgcn_alignbyte(e[2], e[1], p1) == a1 &&
+             __builtin_amdgcn_alignbyte(e[3], e[2], p1) == a2 &&
+             __builtin_amdgcn_alignbyte(e[4], e[3], p1) == a3;
+      }
+      if (__any(tp)) {
+        // this lane's Dots k = sub + LPF j all start at byte shift s (LPF L0 = 0 mod 4): Dot 0's
+        // prefix laid out at that shift, E[q] = bytes 4q - s .. 4q - s + 3 of Dot 0, with the bytes
+        // outside the prefix masked in the first and last words (M0, M8, M9)
+        const uint32_t s = (pos + sub * L0) & 3u;
+        const int32_t ws = (int32_t)pos - (int32_t)s;  // >= -3: inside the file's LDS region
+        const uint32_t* A = reinterpret_cast<const uint32_t*>(body + (ws & ~3));
+        const uint32_t t = (uint32_t)ws & 3u;
+        uint32_t E[10];
+        {
+          uint32_t Aw[11];
+#pragma unroll
+          for (int q = 0; q < 11; q++) Aw[q] = tp ? A[q] : 0u;
+#pragma unroll
+          for (int q = 0; q < 10; q++) E[q] = __builtin_amdgcn_alignbyte(Aw[q + 1], Aw[q], t);
+        }
+        const uint32_t M0 = ~0u << (8u * s);
+        const uint32_t M8 = s >= 2 ? ~0u : (s == 1 ? 0xffffffu : 0xffffu);
+        const uint32_t M9 = s == 3 ? 0xffu : 0u;
+        const uint32_t cw = L0 - 34u;                       // counter bytes: 1, 2, 4 or 8
+        const uint32_t csh = cw < 4 ? 32u - 8u * cw : 0u;
+        const uint32_t cnt = tp ? (uint32_t)remaining : 0u;
+        uint32_t bad = 0, mx = 0;
+        unsigned long long mx64 = 0;
+        for (uint32_t j = 0;; j++) {
+          const uint32_t k = sub + LPF * j;
+          const bool in = tp && k < cnt;
+          if (!__any(in)) break;
+          if (in) {
+            const uint32_t c = pos + k * L0;
+            const uint32_t* D = b32 + (c >> 2);
+            const uint32_t* Cc = b32 + ((c + 34u) >> 2);
+            uint32_t x = __builtin_amdgcn_bitop3_b32(D[0], E[0], M0, 0x28);  // (D ^ E) & M
+            x |= (D[1] ^ E[1]) | (D[2] ^ E[2]) | (D[3] ^ E[3]) | (D[4] ^ E[4]);
+            x |= (D[5] ^ E[5]) | (D[6] ^ E[6]) | (D[7] ^ E[7]);
+            x |= __builtin_amdgcn_bitop3_b32(D[8], E[8], M8, 0x28) | __builtin_amdgcn_bitop3_b32(D[9], E[9], M9, 0x28);
+            bad |= x;
+            const uint32_t u = c + 34u;  // counter bytes at shift (c + 34) mod 4
+            const uint32_t hi = bswap32(__builtin_amdgcn_alignbyte(Cc[1], Cc[0], u));
+            if (cw == 8) {
+              const uint32_t lo = bswap32(__builtin_amdgcn_alignbyte(Cc[2], Cc[1], u));
+              const unsigned long long v = ((unsigned long long)hi << 32) | lo;
+              mx64 = v > mx64 ? v : mx64;
+            } else {
+              const uint32_t v = hi >> csh;
+              mx = v > mx ? v : mx;
+            }
+          }
+          if (j == 0 && grp_bits<LPF>(bad != 0, grp)) tp = false;  // another actor: stop early
+        }
+        if (grp_bits<LPF>(bad != 0, grp)) tp = false;
+        if (tp) {
+          if (do_fold && sub < cnt) fold_dot(a0, a1, a2, a3, cw == 8 ? mx64 : (unsigned long long)mx);
+          remaining = 0;
+        }
+      }
+    }
+  }
   // fast path: every Dot canonical with the first Dot's length L0, so Dot i sits at pos + i L0.
   // A round takes two Dots per lane (done + sub and done + LPF + sub): their 26 LDS reads are in
   // flight together.  It stops at the first Dot that is not canonical with length L0 (nothing
@@ -702,6 +797,11 @@ hipError_t launch_open_fold_small(hipStream_t s, const DecodeArgs& a, int files_
 //   delta = 4 nblk - npc (pieces missing from the last block), T = (U r^(5-delta) + G' r + lenblock) r.
 // ----------------------------------------------------------------------------------------
 static constexpr uint32_t kRegion2 = 4096;
+// Regions of a wave's files start 4128 B apart (not 4096): the decode's LDS reads of two files
+// in one 32-lane bank group then fall on different banks at equal offsets (4096 = 0 mod 32
+// banks made every such pair collide; tools/lds_banks.py: 1.29 -> 1.0 extra cycles per read
+// at the C2 Dot layout).  64 B of slack past the last region take the decode's over-reads.
+static constexpr uint32_t kRegionStride2 = 4128;
 
 template <int LPF>
 struct V2Cfg {
@@ -774,10 +874,10 @@ void k_open_fold_v2(DecodeArgs a) {
   using C = V2Cfg<LPF>;
   constexpr int F = C::F;
   constexpr int BPL = C::BPL;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[F * kRegion2];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[(F - 1) * kRegionStride2 + kRegion2 + 64];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t grp = lane / LPF, sub = lane % LPF;
-  uint8_t* fl = lds + grp * kRegion2;
+  uint8_t* fl = lds + grp * kRegionStride2;
   const uint32_t ngroups = (a.n + F - 1) / F;
   const uint32_t stride = gridDim.x;
   uint32_t g = bcast(blockIdx.x);

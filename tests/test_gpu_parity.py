@@ -269,6 +269,60 @@ def test_random_batch_matches_oracle(ctx, oracle, stress):
     assert core.state_bytes() == oc.serialize()
 
 
+def test_template_path_cases(ctx, oracle):
+    """The fused kernel's template path (every Dot of a file carries Dot 0's 34-byte prefix) and
+    its fallbacks, file by file against the oracle: counters of every width (cc/cd/ce/cf, fixint
+    first Dots), array16 / fixarray headers, one Dot of another actor, of another width or with
+    reordered keys at any position, a lone Dot, a tampered file."""
+    key = os.urandom(32)
+    rng = random.Random(77)
+    actors = sorted(rng.randbytes(16) for _ in range(6))
+    ranges = {"cc": (128, 255), "cd": (256, 65535), "ce": (65536, (1 << 32) - 1),
+              "cf": (1 << 32, (1 << 64) - 1), "fix": (0, 127)}
+    clears, fa = [], []
+    for i in range(240):
+        w = rng.choice(["cc", "cd", "ce", "cf", "ce", "ce"])
+        n = rng.choice([1, 2, 3, 15, 16, 17, 31, 32, 33, 47, 64, 80, 90])
+        a = rng.randrange(len(actors))
+        dots = [{"actor": actors[a], "counter": rng.randint(*ranges[w])} for _ in range(n)]
+        case = rng.choice(["clean", "clean", "other_actor", "other_width", "reordered", "fix_first", "fix_all"])
+        k = rng.randrange(n)
+        if case == "other_actor":
+            dots[k]["actor"] = actors[(a + 1) % len(actors)]
+        elif case == "other_width":
+            dots[k]["counter"] = rng.randint(*ranges[rng.choice([x for x in ranges if x != w])])
+        elif case == "reordered":
+            dots[k] = {"counter": dots[k]["counter"], "actor": dots[k]["actor"]}
+        elif case == "fix_first":
+            dots[0]["counter"] = rng.randint(*ranges["fix"])
+        elif case == "fix_all":
+            for d in dots:
+                d["counter"] = rng.randint(*ranges["fix"])
+        clears.append(APP + msgpack.packb(dots, use_bin_type=True))
+        fa.append(a)
+    order = sorted(range(len(clears)), key=lambda i: (fa[i], i))
+    clears = [clears[i] for i in order]
+    fa = [fa[i] for i in order]
+    vers, cnt = [], {}
+    for x in fa:
+        vers.append(cnt.get(x, 0))
+        cnt[x] = cnt.get(x, 0) + 1
+    files = [CORE + e for e in ctx.encrypt_batch(key, clears)]
+    for tamper in (False, True):
+        fs = list(files)
+        if tamper:
+            j = rng.randrange(len(fs))
+            fs[j] = fs[j][:-1] + bytes([fs[j][-1] ^ 1])
+        core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+        core.set_latest_key(key)
+        rc, st = core.ingest_ops(fs, actors, fa, vers)
+        oc = oracle.Core()
+        orc, ost = oc.read_remote_ops(key, [APP], fs, [actors[i] for i in fa], vers)
+        assert rc == orc and (tamper or set(st) == {0})
+        assert core.state_bytes() == oc.serialize()
+        core.close()
+
+
 def test_unknown_dot_actors_grow_table(ctx, oracle):
     """Dots naming actors that are not op writers (table misses -> refold)."""
     key = os.urandom(32)
