@@ -285,7 +285,7 @@ def run_c3(args, ctx, dev):
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / args.steps
     ctx.set_timing(False)
-    names = ("open_setup", "segments_open", "finalize_open", "gate", "ds_count", "ds_emit",
+    names = ("open_setup", "open_small", "segments_open", "finalize_open", "gate", "ds_count", "ds_emit",
              "ds_applied", "ds_add_pairs", "ds_kill", "ds_finalize", "ds_merge", "seal_setup",
              "segments_seal")
     kern = {k: ctx.timing(k) for k in names}
@@ -359,7 +359,7 @@ def run_c3(args, ctx, dev):
     k_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in kern.items() if v[1]}
     n_state = len(states)
     ct = n * PT_LEN + sum(len(s) for s in states)
-    open_ms = sum(k_ms.get(x, 0) for x in ("open_setup", "segments_open", "finalize_open"))
+    open_ms = sum(k_ms.get(x, 0) for x in ("open_setup", "open_small", "segments_open", "finalize_open"))
     # fold roofline: algorithmic bytes of the columnar fold per step -- adds: actor 4 + counter 8
     # + mbeg 4 + member 8 + pair key/value RMW 32; removals: cbeg/mbeg 8 + clock entry 12 +
     # member 8 + pair key/kill 24

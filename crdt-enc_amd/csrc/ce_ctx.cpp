@@ -125,9 +125,12 @@ int device_open_setup(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs
   return CE_OK;
 }
 
+// small_lanes: single-page files opened by k_open_fold_v2's open-only form (16 lanes per file,
+// lane-owned ChaCha20 blocks) and the segment pass left with the larger ones -- a wave per
+// single-page file idles half its lanes on a 2 KiB file (C3's op files)
 int device_open(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
                 uint64_t blob_len, bool outer, const KeyRef& key, uint8_t* d_out,
-                int32_t* d_status, bool sync_counters) {
+                int32_t* d_status, bool sync_counters, bool small_lanes) {
   uint32_t ec;
   int rc = reserve_batch(ctx, n, blob_len, &ec);
   if (rc) return rc;
@@ -140,9 +143,21 @@ int device_open(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint
                              P, d_status, sc)) != hipSuccess)
     return ctx->hip_fail(e, "open setup");
   ctx->tend(t);
+  if (small_lanes) {
+    DecodeArgs da{};
+    da.pt = d_out;
+    da.blob = d_blob;
+    da.params = P;
+    da.status = d_status;
+    da.n = n;
+    da.counters = ctx->counters.as<uint32_t>();
+    t = ctx->tbegin("open_small");
+    if ((e = launch_open_small_v2(ctx->stream, da)) != hipSuccess) return ctx->hip_fail(e, "open small");
+    ctx->tend(t);
+  }
   t = ctx->tbegin("segments_open");
   if ((e = launch_segments(ctx->stream, false, d_blob, d_out, P, n, d_status, sc,
-                           grid_waves_for(n + ec))) != hipSuccess)
+                           grid_waves_for(n + ec), small_lanes)) != hipSuccess)
     return ctx->hip_fail(e, "open segments");
   ctx->tend(t);
   t = ctx->tbegin("finalize_open");

@@ -823,7 +823,7 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
   // 1) open every file (lib.rs:501-502), plaintext -> HBM
   HostPhase hpo("ops: open+gate+count");
   if ((rc = device_open(ctx, d_blob, d_offs, n, blob_len, true, key_of(c), ctx->out.as<uint8_t>(),
-                        ctx->status.as<int32_t>(), false)))
+                        ctx->status.as<int32_t>(), false, true)))
     return rc;
   std::vector<int32_t> st(n);
   if ((e = hipMemcpyAsync(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||

@@ -855,7 +855,10 @@ __device__ __forceinline__ FilePre2 load_pre2(const DecodeArgs& a, uint32_t f) {
 // iteration's first ChaCha20 block run instead of being waited for at the first XOR;
 // 4 / 8 = ChaCha20's 9 trailing double rounds as a rolled loop of 1 / 3 (instruction bytes);
 // 16 = one block of the next iteration's ciphertext in flight across the iteration boundary.
-template <int LPF, int W, bool JIT, int OPT = 3>
+// DEC = false: open only (EncHandler::decrypt, xchacha lib.rs:73-101) -- plaintext pieces go to
+// HBM at the file's out_off instead of LDS, the tag check sets the status, nothing is decoded
+// (the dot-set ingest decodes the plaintext afterwards).
+template <int LPF, int W, bool JIT, int OPT = 3, bool DEC = true>
 __global__ __launch_bounds__(64, W)
 void k_open_fold_v2(DecodeArgs a) {
 #if !CE_FUSED_DIAG
@@ -874,7 +877,7 @@ void k_open_fold_v2(DecodeArgs a) {
   using C = V2Cfg<LPF>;
   constexpr int F = C::F;
   constexpr int BPL = C::BPL;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[(F - 1) * kRegionStride2 + kRegion2 + 64];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[DEC ? (F - 1) * kRegionStride2 + kRegion2 + 64 : 16];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t grp = lane / LPF, sub = lane % LPF;
   uint8_t* fl = lds + grp * kRegionStride2;
@@ -950,6 +953,7 @@ void k_open_fold_v2(DecodeArgs a) {
     const uint32_t npc = (len + 15) >> 4;             // ciphertext Poly1305 blocks
     const int32_t nblk = (int32_t)((len + 63) >> 6);  // ChaCha20 blocks
     const FileParams* Pp = a.params + (act ? f : 0);
+    uint8_t* gout = DEC ? nullptr : const_cast<uint8_t*>(a.pt) + Pp->out_off;  // !DEC: plaintext in HBM
 
     auto load_block = [&](int k) { load_block_of(cur, k); };
     // PF: this iteration's loads were issued during the previous one.  JIT: block k - 1's loads
@@ -988,6 +992,9 @@ void k_open_fold_v2(DecodeArgs a) {
         load_block(k - 1);
         __builtin_amdgcn_sched_barrier(0);  // keep the loads here, ahead of this block's ChaCha20
       }
+      // slots no file of the wave has (files under 16 x 64 B per lane slot: C3's 2 KiB op files
+      // use two of the four) are skipped whole; slot 0 always has the file's last block
+      if (k > 0 && !__any(has)) continue;
       if (k == 0) {
         // the tree's powers, s and the tag: issued before the last block's ChaCha20 so their
         // latency hides under it (the other blocks' ciphertext registers are free by now)
@@ -1027,9 +1034,15 @@ void k_open_fold_v2(DecodeArgs a) {
         }
         // a lane without a block stores to bytes 4080..4095: past the end of any file that
         // has absent blocks (nblk < 64)
-        const uint32_t st_off = has ? q * 16u : kRegion2 - 16u;
-        *reinterpret_cast<uint4*>(fl + st_off) =
-            make_uint4(xw[0] ^ kw[0], xw[1] ^ kw[1], xw[2] ^ kw[2], xw[3] ^ kw[3]);
+        const uint4 pv = make_uint4(xw[0] ^ kw[0], xw[1] ^ kw[1], xw[2] ^ kw[2], xw[3] ^ kw[3]);
+        if (DEC) {
+          const uint32_t st_off = has ? q * 16u : kRegion2 - 16u;
+          *reinterpret_cast<uint4*>(fl + st_off) = pv;
+        } else if (act && has && q * 16u < len) {
+          // out_off is 16-aligned and the next file's plaintext starts >= 99 B past this one's
+          // end (its header, envelope and tag), so the zero-padded tail piece is a whole store
+          *reinterpret_cast<uint4*>(gout + q * 16u) = pv;
+        }
         const L5 m = block_limbs(xw[0], xw[1], xw[2], xw[3]);
         if (k > 0) {
           mj[j] = m;   // a full block: Poly1305 below, one reduction for the whole block
@@ -1130,6 +1143,10 @@ void k_open_fold_v2(DecodeArgs a) {
 
     // 4) data-version check, decode from LDS, fold; the next iteration's parameters are loaded
     //    inside (their latency hides under the decode)
+    if (!DEC) {
+      (void)ok;
+      nx = load_pre2(a, (g + stride) * F + grp);
+    } else
     decode_fold<LPF, (OPT >> 7) & 15>(a, sup, fl, len, act && ok, cur.apply != 0, f, grp, sub, S, [&] {
       if (PF) {
         // next iteration's ciphertext (its parameters arrived one iteration ago) into the
@@ -1159,11 +1176,19 @@ void k_open_fold_v2(DecodeArgs a) {
 #endif
 }
 
-template <int LPF, int W, bool JIT, int OPT = 3>
+template <int LPF, int W, bool JIT, int OPT = 3, bool DEC = true>
 static void launch_v2(hipStream_t s, const DecodeArgs& a) {
-  static const uint32_t res = resident_blocks(k_open_fold_v2<LPF, W, JIT, OPT>, 64);
+  static const uint32_t res = resident_blocks(k_open_fold_v2<LPF, W, JIT, OPT, DEC>, 64);
   const uint32_t groups = (a.n + 64 / LPF - 1) / (64 / LPF);
-  hipLaunchKernelGGL((k_open_fold_v2<LPF, W, JIT, OPT>), dim3(std::min<uint32_t>(groups, res)), dim3(64), 0, s, a);
+  hipLaunchKernelGGL((k_open_fold_v2<LPF, W, JIT, OPT, DEC>), dim3(std::min<uint32_t>(groups, res)), dim3(64), 0, s, a);
+}
+
+// single-page files opened into HBM (a.pt at each file's out_off), lane-owned ChaCha20 blocks;
+// a.only / a.apply unused.  Larger files: k_segments with skip_small (their setup's list).
+hipError_t launch_open_small_v2(hipStream_t s, const DecodeArgs& a) {
+  if (a.n == 0) return hipSuccess;
+  launch_v2<16, 3, false, 1, false>(s, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_open_fold_v2(hipStream_t s, const DecodeArgs& a, int files_per_wave) {

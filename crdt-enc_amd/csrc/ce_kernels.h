@@ -141,6 +141,9 @@ hipError_t launch_open_fold_small(hipStream_t s, const DecodeArgs& a, int files_
 // the same with whole ChaCha20 blocks per lane (keystream XOR in registers; ce_fused.hip
 // k_open_fold_v2); files_per_wave in {2, 4}
 hipError_t launch_open_fold_v2(hipStream_t s, const DecodeArgs& a, int files_per_wave);
+// open only: single-page files (<= kSmallMax) into a.pt at their out_off, 16 lanes per file
+// (k_open_fold_v2<..., DEC = false>); statuses and the failure counters as the segment pass sets them
+hipError_t launch_open_small_v2(hipStream_t s, const DecodeArgs& a);
 
 // version gate on the device (ce_fused.hip): files grouped by actor with consecutive versions
 // (Storage::load_ops order, storage.rs:36-40) -> apply flags, first gap, next versions.
