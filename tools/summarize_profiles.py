@@ -5,7 +5,7 @@ import csv, glob, json, os, shutil, sys
 
 out = sys.argv[1]
 repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-prof = os.path.join(repo, "profiles")
+prof = os.environ.get("PROFILE_DIR") or os.path.join(repo, "profiles")  # on a gpurun box: under gpurun_out/
 os.makedirs(prof, exist_ok=True)
 tag = os.environ.get("PROFILE_TAG", "r01")
 

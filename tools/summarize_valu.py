@@ -53,5 +53,7 @@ with open(os.path.join(out, "summary.json"), "w") as f:
 # profiles/valu_pmc.json is what bench.py reads (roofline.pmc_valu); the tagged copy is the record
 tag = os.environ.get("PROFILE_TAG", "r02")
 for name in ("valu_pmc.json", "%s_valu_pmc.json" % tag):
-    with open(os.path.join(repo, "profiles", name), "w") as f:
+    pdir = os.environ.get("PROFILE_DIR") or os.path.join(repo, "profiles")  # gpurun box: under gpurun_out/
+    os.makedirs(pdir, exist_ok=True)
+    with open(os.path.join(pdir, name), "w") as f:
         json.dump(res, f, indent=1)
