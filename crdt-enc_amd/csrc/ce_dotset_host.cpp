@@ -49,8 +49,8 @@ struct DsState {
   // bases, members, sorted members [0..6]
   // and emitted (member, actor id, value) columns [7..9]), pinned staging for its downloads
   std::vector<std::array<DevBuf, 10>> rd;
-  DevBuf rd_tmp, rd_misc, ser[16], uuid_of_id, rank_of_id, rd_oclocks, cnt_tot;
-  HostBuf rd_host, rd_small, rd_clock;
+  DevBuf rd_tmp, rd_misc, ser[16], uuid_of_id, rank_of_id, rd_oclocks, cnt_tot, rd_args_d, rd_chunks;
+  HostBuf rd_host, rd_small, rd_clock, rd_args_h;
   uint64_t uuid_ids = ~0ull;  // id count uuid_of_id / rank_of_id were built for
 };
 
@@ -1290,7 +1290,6 @@ OrswotReadArgs read_args(ce_core* c, DsState* d, size_t f, const DevState& ds, c
   a.lo = ds.body;
   a.hi = ds.len;
   auto& b = d->rd[f];
-  a.cand_raw = b[0].as<uint32_t>();
   a.n_cand_dev = d->rd_misc.as<uint32_t>() + 2 * f;
   a.flags = d->rd_misc.as<uint32_t>() + 2 * f + 1;
   a.cap = cap;
@@ -1398,24 +1397,44 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
         if (need_insert[i] && (rc = id_dots(c, ds[i].hs.clock, &ds[i].oclock))) return rc;
     }
     auto h2 = std::make_unique<HostPhase>("   rd.b reserve");
-    size_t tmp_need = 0;
-    for (size_t i : dev) {
+    // every stage below is one launch per kind for all device files (launch_orswot_read_multi:
+    // descriptors in HBM, gridDim.y = file); the descriptors of the three stages sit in separate
+    // thirds of one pinned buffer (each upload is ordered before the host rewrites its third)
+    const size_t na = std::max<size_t>(dev.size(), 1);
+    if ((e = d->rd_args_h.reserve(3 * na * sizeof(OrswotReadArgs))) ||
+        (e = d->rd_args_d.reserve(3 * na * sizeof(OrswotReadArgs))))
+      return ctx->hip_fail(e, "state reader");
+    OrswotReadArgs* hA = d->rd_args_h.as<OrswotReadArgs>();
+    OrswotReadArgs* dA = d->rd_args_d.as<OrswotReadArgs>();
+    uint32_t nch = 0;
+    for (size_t k = 0; k < dev.size(); k++) {
+      const size_t i = dev[k];
       DevState& x = ds[i];
       const uint64_t ne = x.n_entries;
       auto& b = d->rd[i];
-      if ((e = b[0].reserve(4ull * x.cap + 64)) || (e = b[1].reserve(4ull * x.cap + 64)) ||
-          (e = b[2].reserve(4ull * ne + 64)) || (e = b[3].reserve(4ull * ne + 64)) ||
-          (e = b[4].reserve(4ull * ne + 64)) || (e = b[5].reserve(8ull * ne + 64)) ||
-          (e = b[6].reserve(8ull * (dset_mask_for(ne) + 2) + 64)))
+      if ((e = b[1].reserve(4ull * x.cap + 64)) || (e = b[2].reserve(4ull * ne + 64)) ||
+          (e = b[3].reserve(4ull * ne + 64)) || (e = b[4].reserve(4ull * ne + 64)) ||
+          (e = b[5].reserve(8ull * ne + 64)) || (e = b[6].reserve(8ull * (dset_mask_for(ne) + 2) + 64)))
         return ctx->hip_fail(e, "state reader");
-      tmp_need = std::max(tmp_need, orswot_read_tmp_bytes(x.cap));
+      OrswotReadArgs a = read_args(c, d, i, x, out, x.cap);
+      a.chunk0 = nch;
+      a.nchunks = orswot_read_chunks(a.lo, a.hi);
+      nch += a.nchunks;
+      hA[k] = a;
     }
     if ((rc = table_upload(c)) || (rc = ensure_clock(c))) return rc;
-    if ((e = d->rd_tmp.reserve(tmp_need))) return ctx->hip_fail(e, "state reader");
+    if ((e = d->rd_chunks.reserve(8ull * (nch + 1) + 64)) ||
+        (e = d->rd_tmp.reserve(orswot_read_multi_tmp_bytes(nch))))
+      return ctx->hip_fail(e, "state reader");
+    uint32_t* chunk_cnt = d->rd_chunks.as<uint32_t>();
+    uint32_t* chunk_scan = chunk_cnt + nch + 1;
     h2 = std::make_unique<HostPhase>("   rd.c launch");
-    for (size_t i : dev)
-      if ((e = launch_orswot_read(s, read_args(c, d, i, ds[i], out, ds[i].cap), d->rd_tmp.p, d->rd_tmp.cap, 0)))
-        return ctx->hip_fail(e, "state reader");
+    if (!dev.empty() &&
+        ((e = hipMemsetAsync(chunk_cnt + nch, 0, 4, s)) ||
+         (e = hipMemcpyAsync(dA, hA, dev.size() * sizeof(OrswotReadArgs), hipMemcpyHostToDevice, s)) ||
+         (e = launch_orswot_read_multi(s, dA, hA, (uint32_t)dev.size(), 0, chunk_cnt, chunk_scan, d->rd_tmp.p,
+                                       d->rd_tmp.cap))))
+      return ctx->hip_fail(e, "state reader");
     h2 = std::make_unique<HostPhase>("   rd.d sync");
     if (!dev.empty() && ((e = hipMemcpyAsync(small, d->rd_misc.p, 8ull * n, hipMemcpyDeviceToHost, s)) ||
                          (rc = sync("state reader")))) return rc ? rc : ctx->hip_fail(e, "state reader");
@@ -1423,22 +1442,25 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     // 3) the first N heads in position order are the entries: parse, chain, repeats, scan
     ph = std::make_unique<HostPhase>("  rd: entries");
     std::vector<size_t> dev2;
-    std::vector<uint32_t> found(n, 0);
-    for (size_t i : dev) found[i] = small[2 * i];
-    for (size_t i : dev) {
+    OrswotReadArgs* hA2 = hA + na;
+    for (size_t k = 0; k < dev.size(); k++) {
+      const size_t i = dev[k];
+      const uint32_t found = small[2 * i];
       DevState& x = ds[i];
-      if (found[i] < x.n_entries || found[i] > x.cap) {  // fewer heads than entries, or overflow
+      if (found < x.n_entries || found > x.cap) {  // fewer heads than entries, or overflow
         if ((rc = host_parse(i))) return rc;
         continue;
       }
-      OrswotReadArgs a = read_args(c, d, i, x, out, x.cap);
-      size_t tb = d->rd_tmp.cap;
-      if ((e = hipcub_sort_u32(d->rd_tmp.p, tb, a.cand_raw, a.cand, found[i], s)))
-        return ctx->hip_fail(e, "state reader");
+      OrswotReadArgs a = hA[k];
+      a.n_cand = x.n_entries;
       a.tail_out = d->rd_misc.as<uint32_t>() + 2 * n + 4 * i;
-      if ((e = launch_orswot_read(s, a, d->rd_tmp.p, d->rd_tmp.cap, 1))) return ctx->hip_fail(e, "state reader");
+      hA2[dev2.size()] = a;
       dev2.push_back(i);
     }
+    if (!dev2.empty() &&
+        ((e = hipMemcpyAsync(dA + na, hA2, dev2.size() * sizeof(OrswotReadArgs), hipMemcpyHostToDevice, s)) ||
+         (e = launch_orswot_read_multi(s, dA + na, hA2, (uint32_t)dev2.size(), 1, nullptr, nullptr, nullptr, 0))))
+      return ctx->hip_fail(e, "state reader");
     // every file's tail words in one download
     if (!dev2.empty() && ((e = hipMemcpyAsync(small + 2 * n, d->rd_misc.as<uint32_t>() + 2 * n, 16ull * n,
                                               hipMemcpyDeviceToHost, s)) ||
@@ -1447,6 +1469,8 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     ph = std::make_unique<HostPhase>("  rd: tails");
     std::vector<uint64_t> toff(n + 1, 0), eend(n, 0);
     std::vector<size_t> dev3;
+    std::vector<const OrswotReadArgs*> args_of(n, nullptr);
+    for (size_t k = 0; k < dev2.size(); k++) args_of[dev2[k]] = &hA2[k];
     for (size_t i : dev2) {
       const uint32_t* tail = small + 2 * n + 4 * i;
       eend[i] = ds[i].body + (uint64_t)tail[0];
@@ -1485,20 +1509,28 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     //    in the state's clock) flags the file for the host parser
     ph = std::make_unique<HostPhase>("  rd: emit");
     if ((rc = table_upload(c))) return rc;
-    for (size_t i : dev4) {
+    OrswotReadArgs* hA4 = hA + 2 * na;
+    for (size_t k = 0; k < dev4.size(); k++) {
+      const size_t i = dev4[k];
       DevState& x = ds[i];
       auto& b = d->rd[i];
       if ((e = b[7].reserve(8ull * x.n_dots + 8)) || (e = b[8].reserve(4ull * x.n_dots + 4)) ||
           (e = b[9].reserve(8ull * x.n_dots + 8)))
         return ctx->hip_fail(e, "state reader");
-      OrswotReadArgs a = read_args(c, d, i, x, out, 0);
+      OrswotReadArgs a = *args_of[i];
+      a.table = c->d_table.as<ActorSlot>();  // the table may have grown above
+      a.mask = c->cap - 1;
       a.col_member = b[7].as<unsigned long long>();
       a.col_actor = b[8].as<uint32_t>();
       a.col_value = b[9].as<unsigned long long>();
-      if ((e = launch_orswot_read(s, a, d->rd_tmp.p, d->rd_tmp.cap, 2))) return ctx->hip_fail(e, "state reader");
+      hA4[k] = a;
     }
-    if (!dev4.empty() && ((e = hipMemcpyAsync(small, d->rd_misc.p, 8ull * n, hipMemcpyDeviceToHost, s)) ||
-                          (rc = sync("state reader")))) return rc ? rc : ctx->hip_fail(e, "state reader");
+    if (!dev4.empty() &&
+        ((e = hipMemcpyAsync(dA + 2 * na, hA4, dev4.size() * sizeof(OrswotReadArgs), hipMemcpyHostToDevice, s)) ||
+         (e = launch_orswot_read_multi(s, dA + 2 * na, hA4, (uint32_t)dev4.size(), 2, nullptr, nullptr, nullptr, 0)) ||
+         (e = hipMemcpyAsync(small, d->rd_misc.p, 8ull * n, hipMemcpyDeviceToHost, s))))
+      return ctx->hip_fail(e, "state reader");
+    if (!dev4.empty() && (rc = sync("state reader"))) return rc;
     for (size_t i : dev4) {
       if (small[2 * i + 1] == 0) {
         ds[i].device = true;

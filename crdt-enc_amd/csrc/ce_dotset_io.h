@@ -53,11 +53,10 @@ size_t orswot_ser_tmp_bytes(uint32_t n);
 struct OrswotReadArgs {
   const uint8_t* s;
   uint64_t lo, hi;
-  uint32_t* cand_raw;   // cap
-  uint32_t* n_cand_dev;
-  uint32_t cap;
-  uint32_t n_cand;      // stage >= 1: candidates found (host-checked against the map count)
-  uint32_t* cand;       // sorted, n_cand
+  uint32_t* n_cand_dev;  // stage 0: entry heads found
+  uint32_t cap;          // room in cand
+  uint32_t n_cand;       // stage >= 1: the entries (the first n_cand heads; host-checked)
+  uint32_t* cand;        // entry heads in position order
   uint32_t* end;        // entry end (relative to lo), n_cand
   uint32_t* ndots;      // non-zero Dots per entry
   uint32_t* dbase;      // exclusive scan of ndots
@@ -72,10 +71,16 @@ struct OrswotReadArgs {
   unsigned long long* col_member;
   uint32_t* col_actor;
   unsigned long long* col_value;
+  uint32_t chunk0, nchunks;    // multi-file reader: this file's 4 KiB chunks in the count array
 };
-// stage 0: candidate search; 1: sort + per-entry parse + chain check + scan; 2: emit columns
-hipError_t launch_orswot_read(hipStream_t s, OrswotReadArgs a, void* tmp, size_t tmp_bytes, int stage);
-size_t orswot_read_tmp_bytes(uint32_t n);
-hipError_t hipcub_sort_u32(void* tmp, size_t& tb, const uint32_t* kin, uint32_t* kout, uint32_t n, hipStream_t s);
+// the reader over nf files at once (d_args / h_args: the same descriptors in HBM and on the
+// host): stage 0 = entry heads in position order into `cand` and their count into *n_cand_dev
+// (chunk_cnt / chunk_scan: sum of nchunks + 1 words); 1 = entry parse, chain check, repeated
+// members, Dot scan and tail words; 2 = emit columns
+hipError_t launch_orswot_read_multi(hipStream_t s, const OrswotReadArgs* d_args, const OrswotReadArgs* h_args,
+                                    uint32_t nf, int stage, uint32_t* chunk_cnt, uint32_t* chunk_scan,
+                                    void* tmp, size_t tmp_bytes);
+size_t orswot_read_multi_tmp_bytes(uint32_t nchunks);
+uint32_t orswot_read_chunks(uint64_t lo, uint64_t hi);
 
 }  // namespace ce

@@ -16,6 +16,7 @@
 // Integer / byte work bounded by HBM latency; no MFMA.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <hipcub/hipcub.hpp>
 #include <map>
 #include <mutex>
@@ -186,10 +187,8 @@ __device__ __forceinline__ uint32_t rd_uint(const uint8_t* p, const uint8_t* end
 }
 
 // candidate entry heads: 81 a4 'd' 'o' 't' 's' at p, followed by a map header.  A block takes
-// kFindChunk consecutive positions and collects its heads in LDS; one global atomicAdd per block
-// reserves their slice of the list (one head every ~50 bytes: per-wave or per-lane atomics on
-// the one counter serialised in L2 at ~10 ns each, 217 us per C3 state file)
-static constexpr uint32_t kFindPer = 16, kFindChunk = kFindPer * kB, kFindLds = 1024;
+// kFindChunk consecutive positions (k_rdm_count / k_rdm_write)
+static constexpr uint32_t kFindPer = 16, kFindChunk = kFindPer * kB;
 __device__ __forceinline__ bool entry_head_at(const uint8_t* s, uint64_t p) {
   if (s[p] != 0x81 || s[p + 1] != 0xa4 || s[p + 2] != 'd' || s[p + 3] != 'o' || s[p + 4] != 't' ||
       s[p + 5] != 's')
@@ -198,41 +197,87 @@ __device__ __forceinline__ bool entry_head_at(const uint8_t* s, uint64_t p) {
   return (m & 0xf0) == 0x80 || m == 0xde || m == 0xdf;
 }
 
-__global__ void __launch_bounds__(kB) k_rd_find(const uint8_t* s, uint64_t lo, uint64_t hi, uint32_t* cand,
-                                                uint32_t* n_cand, uint32_t cap) {
-  __shared__ uint32_t lcount, lbase;
-  __shared__ uint32_t lst[kFindLds];
-  for (uint64_t c0 = lo + (uint64_t)blockIdx.x * kFindChunk; c0 < hi; c0 += (uint64_t)gridDim.x * kFindChunk) {
-    if (threadIdx.x == 0) lcount = 0;
-    __syncthreads();
+// HashMap<M, VClock> keeps a repeated member's later clock: a file with repeated members goes to
+// the host parser (flag 8).  Found by inserting every member into an open-addressing set
+// (atomicCAS on the all-ones empty word; all-ones members are counted in the word after the
+// set, k_rdm_dups): one launch where a 64-bit radix sort + neighbour compare took a dozen.
+__device__ __forceinline__ uint32_t mix_member(unsigned long long x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+
+// ---------------------------------------------------------------------------------------
+// reader over many state files at once (gridDim.y = file): every stage is one launch for all
+// files instead of one (or, with the candidate sort, eight) per file -- at C3's 8 state files the
+// per-file launches were host-bound (~110 launches, 0.5 ms).  The entry heads come out in
+// position order without a sort: a count pass per 4 KiB chunk, one exclusive scan over all
+// files' chunks, a write pass that ranks each chunk's heads in order.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* part) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t t = 0;
+#pragma unroll
+  for (int w = 0; w < kB / 64; w++) t += part[w];
+  return t;
+}
+
+__global__ void __launch_bounds__(kB) k_rdm_count(const OrswotReadArgs* fa, uint32_t* cnt) {
+  __shared__ uint32_t part[kB / 64];
+  const OrswotReadArgs& a = fa[blockIdx.y];
+  if (blockIdx.x >= a.nchunks) return;
+  const uint64_t c0 = a.lo + (uint64_t)blockIdx.x * kFindChunk;
+  uint32_t n = 0;
 #pragma unroll 4
-    for (uint32_t k = 0; k < kFindPer; k++) {
-      const uint64_t p = c0 + k * kB + threadIdx.x;
-      if (p + 7 <= hi && entry_head_at(s, p)) {
-        const uint32_t i = atomicAdd(&lcount, 1u);
-        if (i < kFindLds) {
-          lst[i] = (uint32_t)(p - lo);
-        } else {  // more heads than the LDS list holds (adversarial bytes): one by one
-          const uint32_t g = atomicAdd(n_cand, 1u);
-          if (g < cap) cand[g] = (uint32_t)(p - lo);
-        }
-      }
+  for (uint32_t k = 0; k < kFindPer; k++) {
+    const uint64_t p = c0 + k * kB + threadIdx.x;
+    n += (p + 7 <= a.hi && entry_head_at(a.s, p)) ? 1u : 0u;
+  }
+  const uint32_t t = block_sum(n, part);
+  if (threadIdx.x == 0) cnt[a.chunk0 + blockIdx.x] = t;
+}
+
+// chunk heads in position order: cand[scan(chunk) - scan(file's first chunk) + rank]
+__global__ void __launch_bounds__(kB) k_rdm_write(const OrswotReadArgs* fa, const uint32_t* scan) {
+  __shared__ uint32_t part[kB / 64];
+  const OrswotReadArgs& a = fa[blockIdx.y];
+  if (blockIdx.x >= a.nchunks) return;
+  const uint64_t c0 = a.lo + (uint64_t)blockIdx.x * kFindChunk;
+  uint32_t at = scan[a.chunk0 + blockIdx.x] - scan[a.chunk0];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (uint32_t k = 0; k < kFindPer; k++) {
+    const uint64_t p = c0 + k * kB + threadIdx.x;
+    const bool hit = p + 7 <= a.hi && entry_head_at(a.s, p);
+    const unsigned long long bm = __ballot(hit);
+    __syncthreads();
+    if (lane == 0) part[w] = (uint32_t)__builtin_popcountll(bm);
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int j = 0; j < kB / 64; j++) {
+      before += (uint32_t)j < w ? part[j] : 0u;
+      tot += part[j];
     }
-    __syncthreads();
-    const uint32_t m = lcount < kFindLds ? lcount : kFindLds;
-    if (threadIdx.x == 0 && m) lbase = atomicAdd(n_cand, m);
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < m; i += kB) {
-      const uint32_t g = lbase + i;
-      if (g < cap) cand[g] = lst[i];
+    if (hit) {
+      const uint32_t r = at + before + (uint32_t)__builtin_popcountll(bm & ((1ull << lane) - 1ull));
+      if (r < a.cap) a.cand[r] = (uint32_t)(p - a.lo);
     }
-    __syncthreads();
+    at += tot;
   }
 }
 
-// lane per candidate (sorted): parse the entry's VClock from its head; end[i] = byte after it,
-// ndots[i] = its non-zero Dots, ok[i] = canonical (UUIDs strictly ascending, uints canonical)
-__global__ void k_rd_entry(OrswotReadArgs a) {
+__global__ void k_rdm_found(const OrswotReadArgs* fa, const uint32_t* scan, uint32_t nf) {
+  const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f < nf) *fa[f].n_cand_dev = scan[fa[f].chunk0 + fa[f].nchunks] - scan[fa[f].chunk0];
+}
+
+__global__ void k_rdm_entry(const OrswotReadArgs* fa) {
+  const OrswotReadArgs a = fa[blockIdx.y];
   const uint8_t* base = a.s + a.lo;
   const uint8_t* end = a.s + a.hi;
   for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < a.n_cand; i += gridDim.x * kB) {
@@ -246,7 +291,6 @@ __global__ void k_rd_entry(OrswotReadArgs a) {
     uint32_t prev[4] = {0, 0, 0, 0};
     for (uint32_t d = 0; d < k && ok; d++) {
       if (p + 18 > end || p[0] != 0xc4 || p[1] != 16) { ok = false; break; }
-      // big-endian words: byte order = numeric order for the ascending check
       const uint32_t w0 = rd_be32(p + 2), w1 = rd_be32(p + 6), w2 = rd_be32(p + 10), w3 = rd_be32(p + 14);
       if (d > 0) {
         const bool gt = w0 != prev[0] ? w0 > prev[0] : w1 != prev[1] ? w1 > prev[1]
@@ -266,8 +310,10 @@ __global__ void k_rd_entry(OrswotReadArgs a) {
   }
 }
 
-// lane per entry: its member key must exactly fill [end of the previous entry, its head)
-__global__ void k_rd_chain(OrswotReadArgs a) {
+// the chain check (k_rd_chain) and the repeat set's clearing in one pass: the set is cleared
+// here and filled by k_rdm_dups, the next launch
+__global__ void k_rdm_chain(const OrswotReadArgs* fa) {
+  const OrswotReadArgs a = fa[blockIdx.y];
   const uint8_t* base = a.s + a.lo;
   for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < a.n_cand; i += gridDim.x * kB) {
     const uint32_t start = i == 0 ? 0u : a.end[i - 1];
@@ -277,52 +323,68 @@ __global__ void k_rd_chain(OrswotReadArgs a) {
     if (!ul || start + ul != head || a.end[i] == 0xffffffffu) atomicOr(a.flags, 2u);
     a.member[i] = m;
   }
+  for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < a.dset_mask + 2u; i += gridDim.x * kB) a.msort[i] = ~0ull;
 }
 
-// HashMap<M, VClock> keeps a repeated member's later clock: a file with repeated members goes to
-// the host parser (flag 8).  Found by inserting every member into an open-addressing set
-// (atomicCAS on the all-ones empty word; all-ones members are counted in the word after the
-// set): one launch where a 64-bit radix sort + neighbour compare took a dozen.
-__device__ __forceinline__ uint32_t mix_member(unsigned long long x) {
-  x ^= x >> 33;
-  x *= 0xff51afd7ed558ccdull;
-  x ^= x >> 33;
-  return (uint32_t)x;
-}
-
-__global__ void k_rd_dups_hash(const unsigned long long* member, unsigned long long* set, uint32_t mask,
-                               uint32_t* flags, uint32_t n) {
+__global__ void k_rdm_dups(const OrswotReadArgs* fa) {
+  const OrswotReadArgs a = fa[blockIdx.y];
   constexpr unsigned long long kEmpty = ~0ull;
-  for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < n; i += gridDim.x * kB) {
-    const unsigned long long m = member[i];
+  for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < a.n_cand; i += gridDim.x * kB) {
+    const unsigned long long m = a.member[i];
     if (m == kEmpty) {
-      if (atomicAdd(&set[(size_t)mask + 1], 1ull) != kEmpty) atomicOr(flags, 8u);  // second one
+      if (atomicAdd(&a.msort[(size_t)a.dset_mask + 1], 1ull) != kEmpty) atomicOr(a.flags, 8u);
       continue;
     }
-    uint32_t h = mix_member(m) & mask;
-    for (uint32_t probe = 0; probe <= mask; probe++) {
-      const unsigned long long old = atomicCAS(&set[h], kEmpty, m);
+    uint32_t h = mix_member(m) & a.dset_mask;
+    for (uint32_t probe = 0; probe <= a.dset_mask; probe++) {
+      const unsigned long long old = atomicCAS(&a.msort[h], kEmpty, m);
       if (old == kEmpty) break;
-      if (old == m) { atomicOr(flags, 8u); break; }
-      h = (h + 1) & mask;
+      if (old == m) { atomicOr(a.flags, 8u); break; }
+      h = (h + 1) & a.dset_mask;
     }
   }
 }
 
-// the last entry's end / Dot base / Dot count and the flags word, for one download of all files
-__global__ void k_rd_tail(OrswotReadArgs a) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
-    const uint32_t l = a.n_cand - 1;
+// exclusive scan of ndots -> dbase, one 1024-thread block per file (a thread per contiguous run),
+// then the tail words (k_rd_tail) for the file's one download
+__global__ void __launch_bounds__(1024) k_rdm_scan_tail(const OrswotReadArgs* fa) {
+  const OrswotReadArgs a = fa[blockIdx.x];
+  __shared__ uint32_t part[16];
+  const uint32_t n = a.n_cand, t = threadIdx.x;
+  const uint32_t per = (n + 1023) / 1024;
+  const uint32_t b0 = min(n, t * per), b1 = min(n, b0 + per);
+  uint32_t s = 0;
+  for (uint32_t i = b0; i < b1; i++) s += a.ndots[i];
+  // block exclusive scan of s
+  uint32_t incl = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+    if ((int)(t & 63) >= o) incl += y;
+  }
+  if ((t & 63) == 63) part[t >> 6] = incl;
+  __syncthreads();
+  uint32_t wbase = 0;
+  for (uint32_t j = 0; j < (t >> 6); j++) wbase += part[j];
+  uint32_t run = wbase + incl - s;
+  for (uint32_t i = b0; i < b1; i++) {
+    a.dbase[i] = run;
+    run += a.ndots[i];
+  }
+  __syncthreads();
+  if (t == 0 && n && a.tail_out) {
+    uint32_t tot = 0;
+    for (int j = 0; j < 16; j++) tot += part[j];
+    const uint32_t l = n - 1;
     a.tail_out[0] = a.end[l];
-    a.tail_out[1] = a.dbase[l];
+    a.tail_out[1] = tot - a.ndots[l];  // dbase of the last entry
     a.tail_out[2] = a.ndots[l];
     a.tail_out[3] = *a.flags;
   }
 }
 
-// lane per entry: its non-zero Dots -> (member, actor id, counter) at its exclusive-scan base;
-// actor ids from the device actor table (a miss declines the file to the host)
-__global__ void k_rd_emit(OrswotReadArgs a) {
+__global__ void k_rdm_emit(const OrswotReadArgs* fa) {
+  const OrswotReadArgs a = fa[blockIdx.y];
   const uint8_t* base = a.s + a.lo;
   for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < a.n_cand; i += gridDim.x * kB) {
     const uint8_t* p = base + a.cand[i] + 6;
@@ -353,6 +415,47 @@ __global__ void k_rd_emit(OrswotReadArgs a) {
 }
 
 }  // namespace
+
+hipError_t launch_orswot_read_multi(hipStream_t s, const OrswotReadArgs* d_args, const OrswotReadArgs* h_args,
+                                    uint32_t nf, int stage, uint32_t* chunk_cnt, uint32_t* chunk_scan,
+                                    void* tmp, size_t tmp_bytes) {
+  if (nf == 0) return hipSuccess;
+  uint32_t gx = 1;
+  if (stage == 0) {
+    uint32_t nchunks = 0;
+    for (uint32_t f = 0; f < nf; f++) {
+      gx = std::max(gx, h_args[f].nchunks);
+      nchunks = std::max(nchunks, h_args[f].chunk0 + h_args[f].nchunks);
+    }
+    hipLaunchKernelGGL(k_rdm_count, dim3(gx, nf), dim3(kB), 0, s, d_args, chunk_cnt);
+    size_t tb = tmp_bytes;
+    hipError_t e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, chunk_cnt, chunk_scan, (int)(nchunks + 1), s);
+    if (e) return e;
+    hipLaunchKernelGGL(k_rdm_write, dim3(gx, nf), dim3(kB), 0, s, d_args, chunk_scan);
+    hipLaunchKernelGGL(k_rdm_found, dim3((nf + 63) / 64), dim3(64), 0, s, d_args, chunk_scan, nf);
+    return hipGetLastError();
+  }
+  for (uint32_t f = 0; f < nf; f++) gx = std::max(gx, nblk(std::max<uint64_t>(h_args[f].n_cand, h_args[f].dset_mask + 2ull)));
+  if (stage == 1) {
+    hipLaunchKernelGGL(k_rdm_entry, dim3(gx, nf), dim3(kB), 0, s, d_args);
+    hipLaunchKernelGGL(k_rdm_chain, dim3(gx, nf), dim3(kB), 0, s, d_args);
+    hipLaunchKernelGGL(k_rdm_dups, dim3(gx, nf), dim3(kB), 0, s, d_args);
+    hipLaunchKernelGGL(k_rdm_scan_tail, dim3(nf), dim3(1024), 0, s, d_args);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(k_rdm_emit, dim3(gx, nf), dim3(kB), 0, s, d_args);
+  return hipGetLastError();
+}
+
+size_t orswot_read_multi_tmp_bytes(uint32_t nchunks) {
+  size_t b = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)(nchunks + 1));
+  return b + 256;
+}
+
+uint32_t orswot_read_chunks(uint64_t lo, uint64_t hi) {
+  return hi > lo ? (uint32_t)((hi - lo + kFindChunk - 1) / kFindChunk) : 0u;
+}
 
 hipError_t launch_orswot_ser(hipStream_t s, OrswotSerScratch& sc, const OrswotSerArgs& in) {
   // pairs (member, actor id, value) in collect order -> sorted by (member, rank): sort by rank,
@@ -422,53 +525,6 @@ static size_t ser_tmp_bytes_raw(uint32_t n) {
 size_t orswot_ser_tmp_bytes(uint32_t n) {
   static std::map<uint32_t, size_t> cache;
   return cached_tmp_bytes(n, ser_tmp_bytes_raw, cache);
-}
-
-hipError_t launch_orswot_read(hipStream_t s, OrswotReadArgs a, void* tmp, size_t tmp_bytes, int stage) {
-  hipError_t e;
-  if (stage == 0) {  // candidates, then sorted by position
-    hipLaunchKernelGGL(k_rd_find, dim3(nblk((a.hi - a.lo + kFindPer - 1) / kFindPer)), dim3(kB), 0, s, a.s, a.lo,
-                       a.hi, a.cand_raw,
-                       a.n_cand_dev, a.cap);
-    return hipGetLastError();
-  }
-  if (stage == 1) {
-    size_t tb = tmp_bytes;
-    if (a.n_cand) {
-      hipLaunchKernelGGL(k_rd_entry, dim3(nblk(a.n_cand)), dim3(kB), 0, s, a);
-      hipLaunchKernelGGL(k_rd_chain, dim3(nblk(a.n_cand)), dim3(kB), 0, s, a);
-      if ((e = hipMemsetAsync(a.msort, 0xff, 8ull * ((size_t)a.dset_mask + 2), s))) return e;
-      hipLaunchKernelGGL(k_rd_dups_hash, dim3(nblk(a.n_cand)), dim3(kB), 0, s, a.member, a.msort, a.dset_mask,
-                         a.flags, a.n_cand);
-      tb = tmp_bytes;
-      if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, a.ndots, a.dbase, (int)a.n_cand, s))) return e;
-      if (a.tail_out) hipLaunchKernelGGL(k_rd_tail, dim3(1), dim3(64), 0, s, a);
-    }
-    return hipGetLastError();
-  }
-  if (a.n_cand) hipLaunchKernelGGL(k_rd_emit, dim3(nblk(a.n_cand)), dim3(kB), 0, s, a);
-  return hipGetLastError();
-}
-
-hipError_t hipcub_sort_u32(void* tmp, size_t& tb, const uint32_t* kin, uint32_t* kout, uint32_t n, hipStream_t s) {
-  return hipcub::DeviceRadixSort::SortKeys(tmp, tb, kin, kout, (int)n, 0, 32, s);
-}
-
-// hipCUB's temp-storage queries cost tens of microseconds each on the host; the sizes only
-// grow with n, so they are taken once per power of two and cached
-static size_t read_tmp_bytes_raw(uint32_t n) {
-  size_t a = 0, b = 0, c = 0;
-  (void)hipcub::DeviceRadixSort::SortKeys(nullptr, a, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 32);
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
-  (void)hipcub::DeviceRadixSort::SortKeys(nullptr, c, (unsigned long long*)nullptr,
-                                          (unsigned long long*)nullptr, (int)n, 0, 64);
-  return std::max(a, std::max(b, c)) + 256;
-}
-
-
-size_t orswot_read_tmp_bytes(uint32_t n) {
-  static std::map<uint32_t, size_t> cache;
-  return cached_tmp_bytes(n, read_tmp_bytes_raw, cache);
 }
 
 }  // namespace ce
