@@ -112,6 +112,19 @@ hipError_t launch_ds_merge(hipStream_t s, DsTables t, const unsigned long long* 
                            const unsigned long long* oclock);
 // k_ds_merge + k_ds_finalize in one pass (counts into live[0..1], zeroed by put_other with
 // zero_counts)
+// one state file's entry columns (member, actor id, value) for the k-way merge
+struct DsMergeSrc {
+  const unsigned long long* member;
+  const uint32_t* actor;
+  const unsigned long long* value;
+  uint32_t n;
+};
+// Orswot::merge of nf state files at once (no deferred removals on any side): d_src / h_src the
+// same descriptors in HBM and on the host, oclocks = the files' dense clocks at stride ccap,
+// hold = a zeroed u64 per pair slot (left zeroed); live[0..1] = live / used pairs after
+hipError_t launch_ds_kmerge(hipStream_t s, DsTables t, const DsMergeSrc* d_src, const DsMergeSrc* h_src, uint32_t nf,
+                            unsigned long long* clock, const unsigned long long* oclocks, uint32_t ccap,
+                            unsigned long long* hold);
 hipError_t launch_ds_merge_finalize(hipStream_t s, DsTables t, const unsigned long long* clock,
                                    const unsigned long long* oclock);
 // live pairs -> (member, actor, value) in bucket order; count in t.live[0] beforehand

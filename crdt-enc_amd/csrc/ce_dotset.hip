@@ -523,6 +523,98 @@ __global__ void __launch_bounds__(kBlock) k_ds_merge_finalize(DsTables t, const 
   }
 }
 
+// k-way Orswot::merge of nf state files (read on the device) into the current state when no
+// deferred removal exists on any side: one pass over the pair table instead of one per file.
+// Per (member, actor) Orswot::merge keeps our value if theirs is equal (VClock::intersection) or
+// their clock is below it (clone_without), and theirs if our clock is below it (crdts Orswot::merge).
+// Every state's entry values are <= its own clock, so of two different values at most the larger
+// can survive a merge (the smaller is covered by the larger's clock); folding the merges in file
+// order therefore keeps M = the largest value among ours and the files' iff every source that does
+// not hold exactly M has a clock below it: M > C_Y[a] -- a condition independent of the order.
+// k_ds_kput: pairs inserted, oth = max over the files; k_ds_khold: bit f of hold = file f holds
+// that max; k_ds_kfinal: the test above, then finalize's add / kill as k_ds_merge_finalize.
+__global__ void __launch_bounds__(kBlock) k_ds_kput(DsTables t, const DsMergeSrc* src) {
+  const DsMergeSrc x = src[blockIdx.y];
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2) t.live[threadIdx.x] = 0;  // k_ds_kfinal counts
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < x.n; i += gridDim.x * kBlock) {
+    const unsigned long long h = member_find(t, x.member[i], true);
+    if (h == kDsEmpty) continue;
+    const unsigned long long b = pair_find(t, pair_key(h, x.actor[i]), true);
+    if (b != kDsEmpty) atomicMax(&t.oth[b], x.value[i]);
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_ds_khold(DsTables t, const DsMergeSrc* src, unsigned long long* hold) {
+  const DsMergeSrc x = src[blockIdx.y];
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < x.n; i += gridDim.x * kBlock) {
+    const unsigned long long h = member_find(t, x.member[i], false);
+    if (h == kDsEmpty) continue;
+    const unsigned long long b = pair_find(t, pair_key(h, x.actor[i]), false);
+    if (b == kDsEmpty) continue;
+    const unsigned long long c = t.cur[b], o = t.oth[b];
+    if (x.value[i] == (c > o ? c : o)) atomicOr(&hold[b], 1ull << blockIdx.y);
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_ds_kfinal(DsTables t, const unsigned long long* clock,
+                                                      const unsigned long long* oclocks, uint32_t ccap,
+                                                      uint32_t nf, unsigned long long* hold) {
+  const uint32_t cap = t.pmask + 1;
+  uint32_t n_used = 0, n_live = 0;
+  for (uint32_t b = blockIdx.x * kBlock + threadIdx.x; b < cap; b += gridDim.x * kBlock) {
+    const unsigned long long key = t.pkey[b];
+    if (key == kDsEmpty) continue;
+    n_used++;
+    const uint32_t a = (uint32_t)(key & ((1u << kDsActorBits) - 1));
+    const unsigned long long s = t.cur[b], o = t.oth[b], ad = t.add[b], kl = t.kill[b], hm = hold[b];
+    const unsigned long long m = s > o ? s : o;
+    bool keep = m != 0 && (s == m || m > clock[a]);
+    for (uint32_t f = 0; f < nf && keep; f++)
+      if (!((hm >> f) & 1ull)) keep = m > oclocks[(size_t)f * ccap + a];
+    const unsigned long long r = keep ? m : 0ull;
+    unsigned long long v = r > ad ? r : ad;
+    if (v != 0 && v <= kl) v = 0;
+    if (v != s) t.cur[b] = v;
+    if (o) t.oth[b] = 0;
+    if (hm) hold[b] = 0;
+    if (ad) t.add[b] = 0;
+    if (kl) t.kill[b] = 0;
+    n_live += v != 0;
+  }
+#pragma unroll
+  for (int q = 32; q > 0; q >>= 1) {
+    n_used += __shfl_xor(n_used, q);
+    n_live += __shfl_xor(n_live, q);
+  }
+  __shared__ uint32_t part[2][kBlock / 64];
+  if ((threadIdx.x & 63) == 0) {
+    part[0][threadIdx.x >> 6] = n_live;
+    part[1][threadIdx.x >> 6] = n_used;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t l = 0, u = 0;
+    for (int w = 0; w < kBlock / 64; w++) {
+      l += part[0][w];
+      u += part[1][w];
+    }
+    if (l) atomicAdd(t.live + 0, l);
+    if (u) atomicAdd(t.live + 1, u);
+  }
+}
+
+// clock = max(clock, every file's clock)
+__global__ void k_ds_kclock(unsigned long long* clock, const unsigned long long* oclocks, uint32_t ccap, uint32_t nf) {
+  for (uint32_t a = blockIdx.x * kBlock + threadIdx.x; a < ccap; a += gridDim.x * kBlock) {
+    unsigned long long v = clock[a];
+    for (uint32_t f = 0; f < nf; f++) {
+      const unsigned long long w = oclocks[(size_t)f * ccap + a];
+      v = w > v ? w : v;
+    }
+    clock[a] = v;
+  }
+}
+
 __global__ void __launch_bounds__(kBlock) k_ds_collect(DsTables t, unsigned long long* member, uint32_t* actor,
                                                        unsigned long long* value, uint32_t* n_out) {
   __shared__ uint32_t lds[2];
@@ -816,6 +908,20 @@ hipError_t launch_ds_merge_finalize(hipStream_t s, DsTables t, const unsigned lo
                                    const unsigned long long* oclock) {
   hipLaunchKernelGGL(k_ds_merge_finalize, dim3(blocks_for((uint64_t)t.pmask + 1, 1024)), dim3(kBlock), 0, s, t,
                      clock, oclock);
+  return hipGetLastError();
+}
+
+hipError_t launch_ds_kmerge(hipStream_t s, DsTables t, const DsMergeSrc* d_src, const DsMergeSrc* h_src, uint32_t nf,
+                            unsigned long long* clock, const unsigned long long* oclocks, uint32_t ccap,
+                            unsigned long long* hold) {
+  uint32_t nmax = 0;
+  for (uint32_t f = 0; f < nf; f++) nmax = h_src[f].n > nmax ? h_src[f].n : nmax;
+  const uint32_t gx = nmax ? blocks_for(nmax) : 1;
+  hipLaunchKernelGGL(k_ds_kput, dim3(gx, nf), dim3(kBlock), 0, s, t, d_src);
+  hipLaunchKernelGGL(k_ds_khold, dim3(gx, nf), dim3(kBlock), 0, s, t, d_src, hold);
+  hipLaunchKernelGGL(k_ds_kfinal, dim3(blocks_for((uint64_t)t.pmask + 1, 1024)), dim3(kBlock), 0, s, t, clock, oclocks,
+                     ccap, nf, hold);
+  hipLaunchKernelGGL(k_ds_kclock, dim3(blocks_for(ccap)), dim3(kBlock), 0, s, clock, oclocks, ccap, nf);
   return hipGetLastError();
 }
 

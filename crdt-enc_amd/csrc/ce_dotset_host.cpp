@@ -33,7 +33,7 @@ struct DsState {
   // Orswot
   DevBuf clock;  // u64[clock_cap] by actor id
   uint32_t clock_cap = 0;
-  DevBuf mkey, pkey, cur, add, kill, oth, live;
+  DevBuf mkey, pkey, cur, add, kill, oth, live, hold;  // hold: k-way merge holder bits (zero between merges)
   uint32_t pcap = 0;  // member table and pair table share the capacity (members <= pairs)
   uint64_t used_pairs = 0, live_pairs = 0;
   std::map<IdDots, std::set<uint64_t>> deferred;  // removal clock -> members (HashMap in crdts)
@@ -93,7 +93,7 @@ int tables_alloc(ce_core* c, uint32_t cap) {
   if ((e = d->mkey.reserve((cap + 1ull) * 8)) || (e = d->pkey.reserve(cap * 8ull)) ||
       (e = d->cur.reserve(cap * 8ull)) || (e = d->add.reserve(cap * 8ull)) ||
       (e = d->kill.reserve(cap * 8ull)) || (e = d->oth.reserve(cap * 8ull)) ||
-      (e = d->live.reserve(64)))
+      (e = d->hold.reserve(cap * 8ull)) || (e = d->live.reserve(64)))
     return ctx->hip_fail(e, "dot-set tables");
   d->pcap = cap;
   if ((e = hipMemsetAsync(d->mkey.p, 0xff, (cap + 1ull) * 8, ctx->stream)) ||
@@ -102,6 +102,7 @@ int tables_alloc(ce_core* c, uint32_t cap) {
       (e = hipMemsetAsync(d->add.p, 0, cap * 8ull, ctx->stream)) ||
       (e = hipMemsetAsync(d->kill.p, 0, cap * 8ull, ctx->stream)) ||
       (e = hipMemsetAsync(d->oth.p, 0, cap * 8ull, ctx->stream)) ||
+      (e = hipMemsetAsync(d->hold.p, 0, cap * 8ull, ctx->stream)) ||
       (e = hipMemsetAsync(d->live.p, 0, 64, ctx->stream)))
     return ctx->hip_fail(e, "dot-set tables");
   d->used_pairs = 0;
@@ -1330,7 +1331,13 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
       (e = hipMemsetAsync(d->rd_misc.p, 0, 8ull * n, s)))
     return ctx->hip_fail(e, "state reader");
   uint32_t* small = d->rd_small.as<uint32_t>();
+  static const bool rd_debug = getenv("CE_RD_DEBUG") != nullptr;  // which stage declined a file
+  int decline_stage = 0;
   auto host_parse = [&](size_t i) -> int {  // the whole plaintext through read_state
+    if (rd_debug)
+      fprintf(stderr, "CE_RD_DEBUG file %zu declined at stage %d (entries %u, found %u, tail %u %u %u %u, flags %u)\n", i,
+              decline_stage, ds[i].n_entries, small[2 * i], small[2 * n + 4 * i], small[2 * n + 4 * i + 1],
+              small[2 * n + 4 * i + 2], small[2 * n + 4 * i + 3], small[2 * i + 1]);
     ds[i].device = false;
     c->path_counts["states_host_parse"]++;
     host_pt[i].resize(len[i]);
@@ -1373,6 +1380,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
         pr = parse_state_prefix(pre.data(), want, want == len[i], &x.hs, &body, &ne);
       }
       if (pr != 0 || ne == 0 || ne > (1ull << 30) || len[i] > 0xffffffffull) {  // (the repeat-check set needs 2 ne < 2^32)
+        decline_stage = 1;
         if ((rc = host_parse(i))) return rc;
         continue;
       }
@@ -1448,6 +1456,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
       const uint32_t found = small[2 * i];
       DevState& x = ds[i];
       if (found < x.n_entries || found > x.cap) {  // fewer heads than entries, or overflow
+        decline_stage = 2;
         if ((rc = host_parse(i))) return rc;
         continue;
       }
@@ -1477,7 +1486,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
       if (tail[3] == 0 && tail[0] != 0xffffffffu && eend[i] <= len[i]) {
         ds[i].n_dots = tail[1] + tail[2];
         dev3.push_back(i);
-      } else if ((rc = host_parse(i))) {
+      } else if ((decline_stage = 3) && (rc = host_parse(i))) {
         return rc;
       }
     }
@@ -1501,7 +1510,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
           x.od.push_back({k, y.second});
         }
         dev4.push_back(i);
-      } else if ((rc = host_parse(i))) {
+      } else if ((decline_stage = 4) && (rc = host_parse(i))) {
         return rc;
       }
     }
@@ -1535,7 +1544,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
       if (small[2 * i + 1] == 0) {
         ds[i].device = true;
         c->path_counts["states_device_read"]++;
-      } else if ((rc = host_parse(i))) {
+      } else if ((decline_stage = 5) && (rc = host_parse(i))) {
         return rc;
       }
     }
@@ -1563,6 +1572,38 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
   if ((e = d->rd_oclocks.reserve(8ull * ccap * n + 64)) ||
       (e = hipMemcpyAsync(d->rd_oclocks.p, hclk, 8ull * ccap * n, hipMemcpyHostToDevice, s)))
     return ctx->hip_fail(e, "merge");
+  // every file read on the device and no deferred removal anywhere: all merges in one pass
+  // (launch_ds_kmerge; the order-free form of the merges below)
+  bool kway = n >= 2 && n <= 64 && d->deferred.empty();
+  for (size_t i = 0; i < n && kway; i++) kway = ds[i].device && ds[i].od.empty();
+  if (kway && !getenv("CE_NO_KMERGE")) {
+    HostPhase hk("  merge: k-way");
+    if ((e = d->rd_args_h.reserve(n * sizeof(DsMergeSrc) + 64)) || (e = d->rd_args_d.reserve(n * sizeof(DsMergeSrc) + 64)))
+      return ctx->hip_fail(e, "merge");
+    auto* hs = d->rd_args_h.as<DsMergeSrc>();
+    for (size_t i = 0; i < n; i++) {
+      auto& b = d->rd[i];
+      hs[i] = DsMergeSrc{b[7].as<unsigned long long>(), b[8].as<uint32_t>(), b[9].as<unsigned long long>(), ds[i].n_dots};
+    }
+    if ((e = hipMemcpyAsync(d->rd_args_d.p, hs, n * sizeof(DsMergeSrc), hipMemcpyHostToDevice, s)) ||
+        (e = launch_ds_kmerge(s, tables(d), d->rd_args_d.as<DsMergeSrc>(), hs, (uint32_t)n,
+                              d->clock.as<unsigned long long>(), d->rd_oclocks.as<unsigned long long>(), ccap,
+                              d->hold.as<unsigned long long>())) ||
+        (e = hipMemcpyAsync(live, d->live.p, 16, hipMemcpyDeviceToHost, s)))
+      return ctx->hip_fail(e, "merge");
+    c->path_counts["states_kway_merge"]++;
+    for (size_t i = 0; i < n; i++)
+      for (auto& y : ds[i].hs.nov) {
+        uint32_t sl;
+        if ((rc = insert_actor(c, y.first, &sl))) return rc;
+        c->nov[sl] = std::max(c->nov[sl], y.second);
+      }
+    if ((rc = sync("merge"))) return rc;
+    if (live[2]) return ctx->fail(CE_ERR_DEVICE, "dot-set table overflow");
+    d->live_pairs = live[0];
+    d->used_pairs = live[1];
+    return table_upload(c);
+  }
   size_t last_dev = n;
   for (size_t i = 0; i < n; i++)
     if (ds[i].device) last_dev = i;

@@ -1,5 +1,6 @@
 // ce_internal.h -- host-side internals shared by ce_ctx.cpp, ce_storage.cpp, ce_core.cpp.
 #pragma once
+#include <utility>
 #include <hip/hip_runtime.h>
 #include <sched.h>
 
@@ -35,9 +36,20 @@ void sha3_256(const uint8_t* msg, size_t len, uint8_t out[32]);
 std::string base32_nopad(const uint8_t* in, size_t len);
 
 // growable device buffer
+// Owning buffers are move-only: a copy would free the same allocation twice (a vector of them
+// that grows moves its elements).
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : p(o.p), cap(o.cap) { o.p = nullptr; o.cap = 0; }
+  DevBuf& operator=(DevBuf&& o) noexcept {
+    std::swap(p, o.p);
+    std::swap(cap, o.cap);
+    return *this;
+  }
   hipError_t reserve(size_t bytes);
   ~DevBuf();
   template <typename T>
@@ -48,6 +60,15 @@ struct DevBuf {
 struct HostBuf {
   void* p = nullptr;
   size_t cap = 0;
+  HostBuf() = default;
+  HostBuf(const HostBuf&) = delete;
+  HostBuf& operator=(const HostBuf&) = delete;
+  HostBuf(HostBuf&& o) noexcept : p(o.p), cap(o.cap) { o.p = nullptr; o.cap = 0; }
+  HostBuf& operator=(HostBuf&& o) noexcept {
+    std::swap(p, o.p);
+    std::swap(cap, o.cap);
+    return *this;
+  }
   hipError_t reserve(size_t bytes);
   ~HostBuf();
   template <typename T>

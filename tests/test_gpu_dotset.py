@@ -5,6 +5,7 @@ Compared bit-exactly: per-file statuses, return codes and the canonical serializ
 (the reference's HashMap order is random; both sides sort).  Parity with crdts 7
 itself is unpinned: the oracle restates its published source.
 """
+import os
 import random
 
 import msgpack
@@ -196,6 +197,53 @@ def test_states_then_ops(ctx, kind, seed):
     assert core.ingest_states(sf)[0] == oc.read_remote_states(key, [APP], sf)[0] == 0
     assert core.state_bytes() == oc.serialize()
     core.close()
+
+
+@pytest.mark.parametrize("p_rm", [0.0, 0.25])
+def test_orswot_kway_state_merge(ctx, p_rm):
+    """Many state files merged at once (launch_ds_kmerge, taken when no state and no current
+    deferred set holds a removal) == the oracle's merges one by one, in two file orders, into an
+    empty and into a non-empty state, and == the sequential device merges (CE_NO_KMERGE=1).
+    States are version prefixes and writer subsets of one history: the same (member, actor) at
+    different counters, values covered by another file's clock, entries only some files hold."""
+    rng = random.Random(91 + int(p_rm * 100))
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 6)
+    files = G.well_formed_orswot(rng, actors, 6, 6, 40, p_rm=p_rm)[0]
+    sws = []
+    for v in range(1, 7):
+        for sub in (actors, actors[::2], actors[1:4]):
+            part = C.Core("orswot")
+            hist = {a: files[a][:v] for a in sub}
+            acts, clears, fa, fv = G.batch(hist, "orswot", APP)
+            f = [CORE + C._oc.cryptor_encrypt(key, bytes(24), c)[1] for c in clears]
+            assert part.read_remote_ops(key, [APP], f, [acts[i] for i in fa], fv)[0] == 0
+            sws.append(part.serialize())
+    rng.shuffle(sws)
+    kway_runs = 0
+    for batch in (sws[:9], sws[9:], list(reversed(sws))):
+        got = []
+        for env in (None, "1"):
+            if env:
+                os.environ["CE_NO_KMERGE"] = env
+            try:
+                core, oc = new_core(ctx, "orswot", key), C.Core("orswot")
+                pre = seal_states(ctx, key, [sws[0]])          # a non-empty state first
+                assert core.ingest_states(pre)[0] == oc.read_remote_states(key, [APP], pre)[0] == 0
+                sf = seal_states(ctx, key, batch)
+                rc, st = core.ingest_states(sf)
+                orc, ost = oc.read_remote_states(key, [APP], sf)
+                assert (rc, st) == (orc, ost) and rc == 0
+                assert core.state_bytes() == oc.serialize()
+                got.append(core.state_bytes())
+                if not env:
+                    kway_runs += core.path_count("states_kway_merge")
+                core.close()
+            finally:
+                os.environ.pop("CE_NO_KMERGE", None)
+        assert got[0] == got[1]
+    if p_rm == 0.0:
+        assert kway_runs >= 2   # adds only: no deferred removal anywhere
 
 
 @pytest.mark.parametrize("kind", ["orswot", "mvreg"])
