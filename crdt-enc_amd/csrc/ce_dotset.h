@@ -127,9 +127,11 @@ hipError_t launch_ds_kmerge(hipStream_t s, DsTables t, const DsMergeSrc* d_src, 
                             unsigned long long* hold);
 hipError_t launch_ds_merge_finalize(hipStream_t s, DsTables t, const unsigned long long* clock,
                                    const unsigned long long* oclock);
-// live pairs -> (member, actor, value) in bucket order; count in t.live[0] beforehand
+// live pairs -> (member, actor, value) columns (any order); n_out[0] (zeroed beforehand) = their
+// count, n_out[2..3] = the largest member; bmax: kCollectBlocks words of scratch
+static constexpr uint32_t kCollectBlocks = 2048;
 hipError_t launch_ds_collect(hipStream_t s, DsTables t, unsigned long long* member, uint32_t* actor,
-                             unsigned long long* value, uint32_t* n_out);
+                             unsigned long long* value, uint32_t* n_out, unsigned long long* bmax);
 // rebuild: insert (member, actor, value) into fresh (cleared) tables as cur
 hipError_t launch_ds_reinsert(hipStream_t s, DsTables t, const unsigned long long* member,
                               const uint32_t* actor, const unsigned long long* value, uint32_t n);

@@ -79,6 +79,16 @@ __device__ __forceinline__ unsigned long long member_of(const DsTables& t, unsig
 }
 
 // block-aggregated counter increment: returns this lane's index among all incrementing lanes
+__device__ __forceinline__ unsigned long long wave_max64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long y = ((unsigned long long)(uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o) << 32) |
+                                 (uint32_t)__shfl_xor((int)(uint32_t)v, o);
+    v = y > v ? y : v;
+  }
+  return v;
+}
+
 __device__ __forceinline__ uint32_t block_count(uint32_t* global, bool pred, uint32_t* lds) {
   if (threadIdx.x == 0) *lds = 0;
   __syncthreads();
@@ -615,26 +625,72 @@ __global__ void k_ds_kclock(unsigned long long* clock, const unsigned long long*
   }
 }
 
+// live pairs -> (member, actor id, value) columns, in no particular order (the writer sorts).
+// A block owns a contiguous run of slots: it counts its live pairs, reserves their slice with one
+// atomicAdd, then writes them -- a reservation per block and loop trip (3 barriers and a global
+// atomic each, 16K same-address atomics over a 4M-slot table) cost ~0.2 ms at C3.  n_out[2..3]:
+// the largest live member (the writer sorts only its significant bits), per-block maxima through
+// bmax and k_ds_collect_max.
 __global__ void __launch_bounds__(kBlock) k_ds_collect(DsTables t, unsigned long long* member, uint32_t* actor,
-                                                       unsigned long long* value, uint32_t* n_out) {
-  __shared__ uint32_t lds[2];
+                                                       unsigned long long* value, uint32_t* n_out,
+                                                       unsigned long long* bmax) {
+  __shared__ uint32_t part[kBlock / 64];
+  __shared__ uint32_t lcount, base;
+  __shared__ unsigned long long lmax[kBlock / 64];
   const uint32_t cap = t.pmask + 1;
-  const uint32_t stride = gridDim.x * kBlock;
-  const uint32_t iters = (cap + stride - 1) / stride;
-  for (uint32_t it = 0; it < iters; it++) {
-    const uint32_t b = it * stride + blockIdx.x * kBlock + threadIdx.x;
-    unsigned long long key = kDsEmpty, v = 0;
-    if (b < cap) {
-      key = t.pkey[b];
-      if (key != kDsEmpty) v = t.cur[b];
-    }
-    const bool live = key != kDsEmpty && v != 0;
-    const uint32_t idx = block_count(n_out, live, lds);
-    if (live) {
-      member[idx] = member_of(t, key >> kDsActorBits);
-      actor[idx] = (uint32_t)(key & ((1u << kDsActorBits) - 1));
-      value[idx] = v;
-    }
+  const uint32_t per = (cap + gridDim.x - 1) / gridDim.x;
+  const uint32_t r0 = min(cap, blockIdx.x * per), r1 = min(cap, r0 + per);
+  uint32_t n = 0;
+  for (uint32_t b = r0 + threadIdx.x; b < r1; b += kBlock) {
+    const unsigned long long key = t.pkey[b];
+    n += key != kDsEmpty && t.cur[b] != 0;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = n;
+  if (threadIdx.x == 0) lcount = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0;
+    for (int w = 0; w < kBlock / 64; w++) tot += part[w];
+    base = tot ? atomicAdd(n_out, tot) : 0u;
+  }
+  __syncthreads();
+  unsigned long long mx = 0;
+  for (uint32_t b = r0 + threadIdx.x; b < r1; b += kBlock) {
+    const unsigned long long key = t.pkey[b];
+    if (key == kDsEmpty) continue;
+    const unsigned long long v = t.cur[b];
+    if (v == 0) continue;
+    const uint32_t idx = base + atomicAdd(&lcount, 1u);
+    const unsigned long long m = member_of(t, key >> kDsActorBits);
+    member[idx] = m;
+    actor[idx] = (uint32_t)(key & ((1u << kDsActorBits) - 1));
+    value[idx] = v;
+    mx = m > mx ? m : mx;
+  }
+  mx = wave_max64(mx);
+  if ((threadIdx.x & 63) == 0) lmax[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long m = 0;
+    for (int w = 0; w < kBlock / 64; w++) m = lmax[w] > m ? lmax[w] : m;
+    bmax[blockIdx.x] = m;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_ds_collect_max(const unsigned long long* bmax, uint32_t nb, uint32_t* n_out) {
+  __shared__ unsigned long long lmax[kBlock / 64];
+  unsigned long long mx = 0;
+  for (uint32_t i = threadIdx.x; i < nb; i += kBlock) mx = bmax[i] > mx ? bmax[i] : mx;
+  mx = wave_max64(mx);
+  if ((threadIdx.x & 63) == 0) lmax[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long m = 0;
+    for (int w = 0; w < kBlock / 64; w++) m = lmax[w] > m ? lmax[w] : m;
+    n_out[2] = (uint32_t)m;
+    n_out[3] = (uint32_t)(m >> 32);
   }
 }
 
@@ -932,9 +988,10 @@ hipError_t launch_ds_merge(hipStream_t s, DsTables t, const unsigned long long* 
 }
 
 hipError_t launch_ds_collect(hipStream_t s, DsTables t, unsigned long long* member, uint32_t* actor,
-                             unsigned long long* value, uint32_t* n_out) {
-  hipLaunchKernelGGL(k_ds_collect, dim3(blocks_for((uint64_t)t.pmask + 1, 2048)), dim3(kBlock), 0, s, t,
-                     member, actor, value, n_out);
+                             unsigned long long* value, uint32_t* n_out, unsigned long long* bmax) {
+  const uint32_t nb = blocks_for((uint64_t)t.pmask + 1, kCollectBlocks);
+  hipLaunchKernelGGL(k_ds_collect, dim3(nb), dim3(kBlock), 0, s, t, member, actor, value, n_out, bmax);
+  hipLaunchKernelGGL(k_ds_collect_max, dim3(1), dim3(kBlock), 0, s, bmax, nb, n_out);
   return hipGetLastError();
 }
 

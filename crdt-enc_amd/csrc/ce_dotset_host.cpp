@@ -50,8 +50,9 @@ struct DsState {
   // and emitted (member, actor id, value) columns [7..9]), pinned staging for its downloads
   std::vector<std::array<DevBuf, 10>> rd;
   DevBuf rd_tmp, rd_misc, ser[16], uuid_of_id, rank_of_id, rd_oclocks, cnt_tot, rd_args_d, rd_chunks;
-  HostBuf rd_host, rd_small, rd_clock, rd_args_h;
-  uint64_t uuid_ids = ~0ull;  // id count uuid_of_id / rank_of_id were built for
+  HostBuf rd_host, rd_small, rd_clock, rd_args_h, h_clock;
+  uint64_t uuid_ids = ~0ull;  // id count uuid_of_id / rank_of_id (and id_rank / rank_id) were built for
+  std::vector<uint32_t> id_rank, rank_id;  // UUID-order rank of each stable id, and its inverse
 };
 
 void ds_free(DsState* d) { delete d; }
@@ -129,22 +130,31 @@ int ensure_clock(ce_core* c) {
   return CE_OK;
 }
 
-// live entries -> (member, actor id, value) columns in d->col[0..2]; returns the count
-int collect(ce_core* c, uint32_t* n_live) {
+// live entries -> (member, actor id, value) columns in d->col[0..2]; returns the count and
+// (max_member) the largest live member.  extra_dl: one more download (dst, src, bytes) queued
+// before the one wait (the compaction's clock)
+int collect(ce_core* c, uint32_t* n_live, unsigned long long* max_member = nullptr,
+            void* extra_dst = nullptr, const void* extra_src = nullptr, size_t extra_bytes = 0) {
   DsState* d = c->ds;
   ce_ctx* ctx = c->ctx;
   const uint64_t cap = d->pcap;
   hipError_t e;
   if ((e = d->col[0].reserve(cap * 8 + 64)) || (e = d->col[1].reserve(cap * 4 + 64)) ||
-      (e = d->col[2].reserve(cap * 8 + 64)) || (e = d->col[5].reserve(64)))
+      (e = d->col[2].reserve(cap * 8 + 64)) || (e = d->col[5].reserve(64 + 8ull * kCollectBlocks)) ||
+      (e = d->h_cnt.reserve(256)))
     return ctx->hip_fail(e, "collect");
   uint32_t* cnt = d->col[5].as<uint32_t>();
-  if ((e = hipMemsetAsync(cnt, 0, 4, ctx->stream)) ||
+  uint32_t* hc = d->h_cnt.as<uint32_t>() + 48;  // pinned: [0] count, [2..3] max member
+  if ((e = hipMemsetAsync(cnt, 0, 16, ctx->stream)) ||
       (e = launch_ds_collect(ctx->stream, tables(d), d->col[0].as<unsigned long long>(),
-                             d->col[1].as<uint32_t>(), d->col[2].as<unsigned long long>(), cnt)) ||
-      (e = hipMemcpyAsync(n_live, cnt, 4, hipMemcpyDeviceToHost, ctx->stream)) ||
+                             d->col[1].as<uint32_t>(), d->col[2].as<unsigned long long>(), cnt,
+                             reinterpret_cast<unsigned long long*>(d->col[5].as<uint8_t>() + 64))) ||
+      (e = hipMemcpyAsync(hc, cnt, 16, hipMemcpyDeviceToHost, ctx->stream)) ||
+      (extra_bytes && (e = hipMemcpyAsync(extra_dst, extra_src, extra_bytes, hipMemcpyDeviceToHost, ctx->stream))) ||
       (e = stream_wait(ctx->stream)))
     return ctx->hip_fail(e, "collect");
+  *n_live = hc[0];
+  if (max_member) *max_member = ((unsigned long long)hc[3] << 32) | hc[2];
   return CE_OK;
 }
 
@@ -1749,20 +1759,49 @@ int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t
     w.map(v.size());
     for (auto& y : v) { w.bin(y.first.data(), 16); w.uint(y.second); }
   };
-  // head: [prefix16] map(2) "next_op_versions" nov "state" map(3) "clock" clock "entries"
-  Dots nov;
-  for (uint32_t sl = 0; sl < c->cap; sl++)
-    if (c->h_table[sl].used && c->nov[sl]) nov.push_back({c->slot_actor[sl], c->nov[sl]});
-  sort_dots(&nov);
+  // actor UUIDs and UUID-order ranks by stable id (host copies kept: nov and the clock are
+  // written in UUID order by walking the ranks -- no per-step sort)
+  auto cph = std::make_unique<HostPhase>("  cd: actor order");
   const uint32_t na = (uint32_t)c->id_actor.size();
-  std::vector<unsigned long long> ck(na);
+  if (d->uuid_ids != na) {
+    std::vector<uint8_t> u(16ull * na + 16);
+    d->rank_id.resize(na);
+    d->id_rank.assign(na + 1, 0);
+    for (uint32_t i = 0; i < na; i++) {
+      std::memcpy(u.data() + 16ull * i, c->id_actor[i].data(), 16);
+      d->rank_id[i] = i;
+    }
+    std::sort(d->rank_id.begin(), d->rank_id.end(), [&](uint32_t a, uint32_t b) { return c->id_actor[a] < c->id_actor[b]; });
+    for (uint32_t i = 0; i < na; i++) d->id_rank[d->rank_id[i]] = i;
+    if ((e = d->uuid_of_id.reserve(u.size())) || (e = d->rank_of_id.reserve(4ull * d->id_rank.size())) ||
+        (e = hipMemcpyAsync(d->uuid_of_id.p, u.data(), u.size(), hipMemcpyHostToDevice, s)) ||
+        (e = hipMemcpyAsync(d->rank_of_id.p, d->id_rank.data(), 4ull * d->id_rank.size(), hipMemcpyHostToDevice, s)) ||
+        (e = stream_wait(s)))
+      return x->hip_fail(e, "actor ranks");
+    d->uuid_ids = na;
+  }
+  // head: [prefix16] map(2) "next_op_versions" nov "state" map(3) "clock" clock "entries"
+  cph = std::make_unique<HostPhase>("  cd: nov");
+  std::vector<uint64_t> by_rank(na, 0);
+  for (uint32_t sl = 0; sl < c->cap; sl++)
+    if (c->h_table[sl].used && c->nov[sl]) by_rank[d->id_rank[actor_id_of_slot(c, sl)]] = c->nov[sl];
+  Dots nov;
+  for (uint32_t r = 0; r < na; r++)
+    if (by_rank[r]) nov.push_back({c->id_actor[d->rank_id[r]], by_rank[r]});
   if ((rc = ensure_clock(c))) return rc;
-  if (na && ((e = hipMemcpyAsync(ck.data(), d->clock.p, na * 8ull, hipMemcpyDeviceToHost, c->ctx->stream)) ||
-             (e = stream_wait(c->ctx->stream))))
-    return x->hip_fail(e, "clock download");
-  IdDots clock;
-  for (uint32_t i = 0; i < na; i++)
-    if (ck[i]) clock.push_back({i, ck[i]});
+  cph = std::make_unique<HostPhase>("  cd: collect + clock");
+  if ((e = d->h_clock.reserve(8ull * na + 64))) return x->hip_fail(e, "clock download");
+  // live pairs -> columns, their count and largest member, and the clock: one wait
+  uint32_t nl = 0;
+  unsigned long long max_member = 0;
+  if ((rc = collect(c, &nl, &max_member, d->h_clock.p, d->clock.p, 8ull * na))) return rc;
+  const unsigned long long* ck = d->h_clock.as<unsigned long long>();
+  cph = std::make_unique<HostPhase>("  cd: head + tail bytes");
+  Dots clock;
+  for (uint32_t r = 0; r < na; r++) {
+    const uint32_t id = d->rank_id[r];
+    if (ck[id]) clock.push_back({c->id_actor[id], ck[id]});
+  }
   Wr hw;
   if (prefix16) hw.b.insert(hw.b.end(), prefix16, prefix16 + 16);
   hw.map(2);
@@ -1771,7 +1810,7 @@ int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t
   hw.str("state");
   hw.map(3);
   hw.str("clock");
-  put_vclock(hw, uuid_dots(clock));
+  put_vclock(hw, clock);
   hw.str("entries");
   // tail: "deferred" map {VClock bytes: [members]} sorted by the clock's bytes
   Wr tw;
@@ -1789,25 +1828,7 @@ int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t
     tw.arr(y.second->size());
     for (uint64_t m : *y.second) tw.uint(m);
   }
-  // live pairs, actor UUIDs and UUID-order ranks by stable id
-  uint32_t nl = 0;
-  if ((rc = collect(c, &nl))) return rc;
-  if (d->uuid_ids != na) {
-    std::vector<uint8_t> u(16ull * na + 16);
-    std::vector<uint32_t> order(na), rank(na + 1);
-    for (uint32_t i = 0; i < na; i++) {
-      std::memcpy(u.data() + 16ull * i, c->id_actor[i].data(), 16);
-      order[i] = i;
-    }
-    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return c->id_actor[a] < c->id_actor[b]; });
-    for (uint32_t i = 0; i < na; i++) rank[order[i]] = i;
-    if ((e = d->uuid_of_id.reserve(u.size())) || (e = d->rank_of_id.reserve(4ull * rank.size())) ||
-        (e = hipMemcpyAsync(d->uuid_of_id.p, u.data(), u.size(), hipMemcpyHostToDevice, s)) ||
-        (e = hipMemcpyAsync(d->rank_of_id.p, rank.data(), 4ull * rank.size(), hipMemcpyHostToDevice, s)) ||
-        (e = stream_wait(s)))
-      return x->hip_fail(e, "actor ranks");
-    d->uuid_ids = na;
-  }
+  cph = std::make_unique<HostPhase>("  cd: serialize + seal enqueue");
   // clear text bound: head + map header + entries (member <= 9 + 6 + 5, Dot <= 18 + 9) + tail
   const uint64_t U = hw.b.size() + 5 + 20ull * nl + 27ull * nl + tw.b.size();
   const uint64_t A = (U + 255) & ~255ull;  // [offs(2) | out_offs(1) | stats | nonce | outer] after it
@@ -1838,6 +1859,7 @@ int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t
   sc.value_in = d->col[2].as<unsigned long long>();
   sc.rank_of_id = d->rank_of_id.as<uint32_t>();
   sc.rank_bits = bits_for(na);
+  sc.member_bits = max_member ? 64 - __builtin_clzll(max_member) : 1;  // radix passes over those bits only
   sc.k32a = d->ser[0].as<uint32_t>();
   sc.k32b = d->ser[1].as<uint32_t>();
   sc.p32a = d->ser[2].as<uint32_t>();
@@ -1870,6 +1892,7 @@ int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t
   rc = device_seal(x, db, reinterpret_cast<const uint64_t*>(offs), 1, U, db + A + 56, db + A + 32,
                    x->out.as<uint8_t>(), reinterpret_cast<const uint64_t*>(db + A + 16), key);
   if (rc) return rc;
+  cph = std::make_unique<HostPhase>("  cd: length wait");
   uint64_t clear_len = 0;
   if ((e = hipMemcpyAsync(&clear_len, db + A + 8, 8, hipMemcpyDeviceToHost, s)) || (e = stream_wait(s)))
     return x->hip_fail(e, "ds compact");
@@ -1884,6 +1907,7 @@ int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t
     file->resize(total);
     to = file->data();
   }
+  cph = std::make_unique<HostPhase>("  cd: download");
   if ((e = hipMemcpyAsync(to, x->out.p, total, hipMemcpyDeviceToHost, s)) || (e = stream_wait(s)))
     return x->hip_fail(e, "ds compact download");
   return CE_OK;

@@ -38,6 +38,7 @@ struct OrswotSerScratch {
   const unsigned long long* value_in;
   const uint32_t* rank_of_id;            // UUID byte order rank of each stable actor id
   int rank_bits;
+  int member_bits;                       // significant bits of the largest member (<= 64)
   uint32_t *k32a, *k32b, *p32a, *p32b;   // n each
   unsigned long long *k64a, *member_sorted, *value_sorted;
   uint32_t* actor_sorted;

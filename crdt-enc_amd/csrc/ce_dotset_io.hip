@@ -473,7 +473,7 @@ hipError_t launch_orswot_ser(hipStream_t s, OrswotSerScratch& sc, const OrswotSe
     hipLaunchKernelGGL(k_ser_gather_member, dim3(nblk(n)), dim3(kB), 0, s, sc.p32b, sc.member_in, sc.k64a, n);
     tb = sc.tmp_bytes;
     if ((e = hipcub::DeviceRadixSort::SortPairs(sc.tmp, tb, sc.k64a, sc.member_sorted, sc.p32b, sc.p32a,
-                                                 (int)n, 0, 64, s)))
+                                                 (int)n, 0, sc.member_bits > 0 && sc.member_bits <= 64 ? sc.member_bits : 64, s)))
       return e;
     hipLaunchKernelGGL(k_ser_gather2, dim3(nblk(n)), dim3(kB), 0, s, sc.p32a, sc.actor_in, sc.value_in,
                        sc.actor_sorted, sc.value_sorted, n);

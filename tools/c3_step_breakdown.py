@@ -20,8 +20,8 @@ rows.sort()
 count = [i for i, r in enumerate(rows) if "k_ds_count" in r[2]]
 k = int(sys.argv[2]) if len(sys.argv) > 2 else 3     # which ingest_ops (a timed step)
 c = count[k]
-start = max(i for i in range(c) if "k_rd_find" in rows[i][2])
-while start > 0 and "k_rd_find" in rows[start - 1][2]:
+start = max(i for i in range(c) if ("k_rd_find" in rows[i][2] or "k_rdm_count" in rows[i][2]))
+while start > 0 and ("k_rd_find" in rows[start - 1][2] or "k_rdm_count" in rows[start - 1][2]):
     start -= 1
 # back to the step's reset (the fills before the states' upload)
 s0 = start
