@@ -279,10 +279,26 @@ __device__ __forceinline__ void decode_fold(const DecodeArgs& a, const SupVers& 
     if (live && st == CE_OK && remaining > 1 && pos + 34 <= blen) L0 = dot_len_of_marker(body[pos + 33]);
     bool tp = L0 > 34u && (uint64_t)pos + remaining * L0 <= blen;
     if (__any(tp)) {
-      prefetch();  // lands under the checks below (its wait comes with the fold's table lookup)
-      pf_done = true;
       const uint32_t* b32 = reinterpret_cast<const uint32_t*>(body);
       uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+      if (tp) {
+        // Dot 1's actor bytes against Dot 0's first: files whose Dots name many actors (C2
+        // variant B) leave before Dot 0's full check
+        const uint32_t p0 = pos + 9u, p1 = pos + L0 + 9u;
+        const uint32_t* d0 = b32 + (p0 >> 2);
+        const uint32_t* d1 = b32 + (p1 >> 2);
+        uint32_t e0[5], e1[5];
+#pragma unroll
+        for (int q = 0; q < 5; q++) {
+          e0[q] = d0[q];
+          e1[q] = d1[q];
+        }
+        uint32_t diff = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+          diff |= __builtin_amdgcn_alignbyte(e0[q + 1], e0[q], p0) ^ __builtin_amdgcn_alignbyte(e1[q + 1], e1[q], p1);
+        tp = diff == 0;
+      }
       if (tp) {  // Dot 0 in full (every lane of the group; its actor is the file's)
         const uint32_t* d = b32 + (pos >> 2);
         uint32_t dd[13], w[12];
@@ -292,18 +308,13 @@ __device__ __forceinline__ void decode_fold(const DecodeArgs& a, const SupVers& 
         for (int q = 0; q < 12; q++) w[q] = __builtin_amdgcn_alignbyte(dd[q + 1], dd[q], pos);
         unsigned long long c0;
         tp = canon_dot(w, L0, a0, a1, a2, a3, c0);
-        // Dot 1's actor first: files whose Dots name many actors (C2 variant B) leave here
-        const uint32_t p1 = pos + L0 + 9u;
-        const uint32_t* d1 = b32 + (p1 >> 2);
-        uint32_t e[5];
-#pragma unroll
-        for (int q = 0; q < 5; q++) e[q] = d1[q];
-        tp = tp && __builtin_amdgcn_alignbyte(e[1], e[0], p1) == a0 &&
-             __builtin_amdgcn_alignbyte(e[2], e[1], p1) == a1 &&
-             __builtin_amdgcn_alignbyte(e[3], e[2], p1) == a2 &&
-             __builtin_amdgcn_alignbyte(e[4], e[3], p1) == a3;
       }
       if (__any(tp)) {
+        // the next file's parameters: issued once the template path is taken (it lands under the
+        // checks below; the per-Dot path issues it after its first round, whose actor-table
+        // loads would otherwise wait for it -- vmcnt counts in order)
+        prefetch();
+        pf_done = true;
         // this lane's Dots k = sub + LPF j all start at byte shift s (LPF L0 = 0 mod 4): Dot 0's
         // prefix laid out at that shift, E[q] = bytes 4q - s .. 4q - s + 3 of Dot 0, with the bytes
         // outside the prefix masked in the first and last words (M0, M8, M9)
