@@ -1003,9 +1003,11 @@ void k_open_fold_v2(DecodeArgs a) {
         load_block(k - 1);
         __builtin_amdgcn_sched_barrier(0);  // keep the loads here, ahead of this block's ChaCha20
       }
-      // slots no file of the wave has (files under 16 x 64 B per lane slot: C3's 2 KiB op files
-      // use two of the four) are skipped whole; slot 0 always has the file's last block
-      if (k > 0 && !__any(has)) continue;
+      // open only: slots no file of the wave has (files under 16 x 64 B per lane slot: C3's 2 KiB
+      // op files use two of the four) are skipped whole; slot 0 always has the file's last block.
+      // Not in the decoding kernel: the branch splits the straight-line block sequence the
+      // compiler interleaves (C2 A/B: +2-3% with it)
+      if (!DEC && k > 0 && !__any(has)) continue;
       if (k == 0) {
         // the tree's powers, s and the tag: issued before the last block's ChaCha20 so their
         // latency hides under it (the other blocks' ciphertext registers are free by now)
