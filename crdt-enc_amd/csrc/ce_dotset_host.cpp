@@ -517,24 +517,37 @@ int orswot_fold(ce_core* c, const Counts& k) {
                            d->excl.as<unsigned long long>(), d->clock.as<unsigned long long>(), na)))
     return ctx->hip_fail(e, "add");
   ctx->tend(tp);
-  // 3) removal thresholds: the batch's removals and the deferred set
+  // 3) removal thresholds: the batch's removals and the deferred set (uploaded only when there
+  //    is one: the upload waits for its pageable sources)
   auto d0 = deferred_list(d);
-  if ((rc = upload_removals(c, d0))) return rc;
   const uint32_t n0 = (uint32_t)d0.size();
+  if (n0 && (rc = upload_removals(c, d0))) return rc;
   const int tk = ctx->tbegin("ds_kill");
   if ((e = launch_ds_kill(s, tables(d), o.rm_cbeg, o.rm_mbeg, o.rmc_actor, o.rmc_ctr, o.rm_mem, nr)) ||
-      (e = launch_ds_kill(s, tables(d), d->d0[0].as<uint32_t>(), d->d0[1].as<uint32_t>(),
-                          d->d0[2].as<uint32_t>(), d->d0[3].as<unsigned long long>(),
-                          d->d0[4].as<unsigned long long>(), n0)))
+      (n0 && (e = launch_ds_kill(s, tables(d), d->d0[0].as<uint32_t>(), d->d0[1].as<uint32_t>(),
+                                 d->d0[2].as<uint32_t>(), d->d0[3].as<unsigned long long>(),
+                                 d->d0[4].as<unsigned long long>(), n0))))
     return ctx->hip_fail(e, "kill");
   ctx->tend(tk);
-  if ((rc = finalize(c))) return rc;
+  // finalize; its counts come back with the deferred flags below (one wait for both)
+  uint32_t* hl = d->h_cnt.as<uint32_t>() + 56;  // pinned
+  {
+    if ((e = hipMemsetAsync(d->live.p, 0, 8, s))) return ctx->hip_fail(e, "finalize");
+    const int t = ctx->tbegin("ds_finalize");
+    if ((e = launch_ds_finalize(s, tables(d)))) return ctx->hip_fail(e, "finalize");
+    ctx->tend(t);
+    if ((e = hipMemcpyAsync(hl, d->live.p, 16, hipMemcpyDeviceToHost, s))) return ctx->hip_fail(e, "finalize");
+  }
   // 4) deferred = removals whose clock is not covered by the new clock
   std::vector<uint8_t> f_batch, f_d0;
   if ((rc = flags_for(c, o.rm_cbeg, o.rmc_actor, o.rmc_ctr, nr, &f_batch)) ||
       (rc = flags_for(c, d->d0[0].as<uint32_t>(), d->d0[2].as<uint32_t>(),
                       d->d0[3].as<unsigned long long>(), n0, &f_d0)))
     return rc;
+  if (nr == 0 && n0 == 0 && (e = stream_wait(s))) return ctx->hip_fail(e, "finalize");
+  if (hl[2]) return ctx->fail(CE_ERR_DEVICE, "dot-set table overflow");
+  d->live_pairs = hl[0];
+  d->used_pairs = hl[1];
   std::map<IdDots, std::set<uint64_t>> nd;
   for (uint32_t i = 0; i < n0; i++)
     if (f_d0[i]) nd[d0[i].first].insert(d0[i].second.begin(), d0[i].second.end());
@@ -661,17 +674,30 @@ int mvreg_commit(ce_core* c, uint32_t K, uint32_t total, bool later_wins) {
 // ---------------------------------------------------------------------------------------
 // version gate (lib.rs:519-538), device first, host for batches outside load_ops order
 // ---------------------------------------------------------------------------------------
-int gate(ce_core* c, const uint32_t* d_fa, const uint64_t* d_fv, uint32_t n, uint32_t m,
-         const std::vector<uint32_t>& wslot, uint32_t* first_gap, std::vector<uint64_t>* expect) {
+// The version gate in two halves, so its host round trip can share another's: gate_enqueue
+// uploads the expected versions and queues the gate kernels and the download of their flags and
+// next versions (pinned); gate_finish reads them after the caller's wait (the host gate when the
+// batch is not in load_ops shape).
+struct GateJob {
+  uint32_t* hf = nullptr;            // pinned: [0] not grouped, [1] first gap
+  unsigned long long* hnn = nullptr; // pinned: next versions per writer
+  GateArgs ga{};
+};
+
+int gate_enqueue(ce_core* c, const uint32_t* d_fa, const uint64_t* d_fv, uint32_t n, uint32_t m,
+                 const std::vector<uint32_t>& wslot, std::vector<uint64_t>* expect, GateJob* job) {
   ce_ctx* ctx = c->ctx;
   hipError_t e;
   if ((e = ctx->apply.reserve(n + 64)) || (e = c->d_gate.reserve(m * 24ull + 64)) ||
-      (e = ctx->h_stage2.reserve(m * 16ull + 64)))
+      (e = ctx->h_stage2.reserve(m * 16ull + 128)))
     return ctx->hip_fail(e, "gate reserve");
   uint64_t* he0 = ctx->h_stage2.as<uint64_t>();
   for (uint32_t a = 0; a < m; a++) he0[a] = c->nov[wslot[a]];
   expect->assign(he0, he0 + m);
-  GateArgs ga{};
+  job->hnn = reinterpret_cast<unsigned long long*>(he0 + m);
+  job->hf = reinterpret_cast<uint32_t*>(he0 + 2ull * m);
+  GateArgs& ga = job->ga;
+  ga = GateArgs{};
   ga.fa = d_fa;
   ga.fv = d_fv;
   ga.n = n;
@@ -683,7 +709,6 @@ int gate(ce_core* c, const uint32_t* d_fa, const uint64_t* d_fv, uint32_t n, uin
   ga.run_first = reinterpret_cast<uint32_t*>(gbase + 20ull * m);
   ga.flags = ctx->counters.as<uint32_t>() + 12;
   ga.apply = ctx->apply.as<uint8_t>();
-  uint32_t hf[2];
   if ((e = hipMemcpyAsync(gbase, he0, m * 8ull, hipMemcpyHostToDevice, ctx->stream)) ||
       (e = hipMemsetAsync(gbase + 8ull * m, 0, 16ull * m, ctx->stream)) ||
       (e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ga.flags), 0u, 1, ctx->stream)) ||
@@ -692,10 +717,17 @@ int gate(ce_core* c, const uint32_t* d_fa, const uint64_t* d_fv, uint32_t n, uin
   const int t = ctx->tbegin("gate");
   if ((e = launch_gate(ctx->stream, ga))) return ctx->hip_fail(e, "gate");
   ctx->tend(t);
-  if ((e = hipMemcpyAsync(hf, ga.flags, 8, hipMemcpyDeviceToHost, ctx->stream)) ||
-      (e = stream_wait(ctx->stream)))
+  if ((e = hipMemcpyAsync(job->hf, ga.flags, 8, hipMemcpyDeviceToHost, ctx->stream)) ||
+      (e = hipMemcpyAsync(job->hnn, ga.newnov, m * 8ull, hipMemcpyDeviceToHost, ctx->stream)))
     return ctx->hip_fail(e, "gate");
-  if (hf[0]) {
+  return CE_OK;
+}
+
+int gate_finish(ce_core* c, const uint32_t* d_fa, const uint64_t* d_fv, uint32_t n, uint32_t m,
+                const GateJob& job, uint32_t* first_gap, std::vector<uint64_t>* expect) {
+  ce_ctx* ctx = c->ctx;
+  hipError_t e;
+  if (job.hf[0]) {
     std::vector<uint32_t> fa(n);
     std::vector<uint64_t> fv(n);
     std::vector<uint8_t> ap(n);
@@ -711,12 +743,8 @@ int gate(ce_core* c, const uint32_t* d_fa, const uint64_t* d_fv, uint32_t n, uin
       return ctx->hip_fail(e, "host gate");
     return CE_OK;
   }
-  *first_gap = hf[1] == 0xffffffffu ? n : hf[1];
-  std::vector<uint64_t> nn(m);
-  if ((e = hipMemcpyAsync(nn.data(), gbase + 8ull * m, m * 8ull, hipMemcpyDeviceToHost, ctx->stream)) ||
-      (e = stream_wait(ctx->stream)))
-    return ctx->hip_fail(e, "gate");
-  for (uint32_t a = 0; a < m; a++) (*expect)[a] = std::max((*expect)[a], nn[a]);
+  *first_gap = job.hf[1] == 0xffffffffu ? n : job.hf[1];
+  for (uint32_t a = 0; a < m; a++) (*expect)[a] = std::max<uint64_t>((*expect)[a], job.hnn[a]);
   return CE_OK;
 }
 
@@ -836,6 +864,12 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
   if ((rc = device_open(ctx, d_blob, d_offs, n, blob_len, true, key_of(c), ctx->out.as<uint8_t>(),
                         ctx->status.as<int32_t>(), false, true)))
     return rc;
+  // 2) version gate -> apply flags (decode errors reject the batch whatever the gate says); its
+  //    flags and next versions come back with the open's statuses (one wait)
+  uint32_t first_gap = n;
+  std::vector<uint64_t> expect;
+  GateJob gj;
+  if ((rc = gate_enqueue(c, d_fa, d_fv, n, m, wslot, &expect, &gj))) return rc;
   std::vector<int32_t> st(n);
   if ((e = hipMemcpyAsync(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
       (e = stream_wait(ctx->stream)))
@@ -845,10 +879,7 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
       if ((rc = resolve_host_parse(c, d_blob, d_offs, n, true))) return rc;
       break;
     }
-  // 2) version gate -> apply flags (decode errors reject the batch whatever the gate says)
-  uint32_t first_gap = n;
-  std::vector<uint64_t> expect;
-  if ((rc = gate(c, d_fa, d_fv, n, m, wslot, &first_gap, &expect))) return rc;
+  if ((rc = gate_finish(c, d_fa, d_fv, n, m, gj, &first_gap, &expect))) return rc;
   // 3) data version + Vec<S::Op> decode, count pass
   DsDecodeArgs a = decode_args(c, n);
   if ((e = hipMemsetAsync(d->misses.p, 0, 64, ctx->stream))) return ctx->hip_fail(e, "count");
