@@ -1264,18 +1264,12 @@ __global__ void k_gate_runs(GateArgs g) {
   if (i == 0 || g.fa[i - 1] != a) {
     if (atomicAdd(&g.run_count[a], 1u) != 0) atomicOr(&g.flags[0], 1u);  // actor split
     g.run_first[a] = i;
+    // consecutive run starting at version vf: a gap iff vf > expected (at the run's first
+    // file).  An actor split across runs flags [0] above, and the host gate then decides alone.
+    if (g.fv[i] > g.e0[a]) atomicMin(&g.flags[1], i);
   } else if (g.fv[i] != g.fv[i - 1] + 1) {
     atomicOr(&g.flags[0], 1u);  // versions not consecutive: host gate
   }
-}
-
-__global__ void k_gate_gap(GateArgs g) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= g.n) return;
-  const uint32_t a = g.fa[i];
-  if (a >= g.m) return;
-  // consecutive run starting at version vf: a gap iff vf > expected (at the run's first file)
-  if (g.run_first[a] == i && g.fv[i] > g.e0[a]) atomicMin(&g.flags[1], i);
 }
 
 __global__ void k_gate_apply(GateArgs g) {
@@ -1300,7 +1294,6 @@ hipError_t launch_gate(hipStream_t s, const GateArgs& g) {
   if (g.n == 0) return hipSuccess;
   const uint32_t blocks = (g.n + 255) / 256;
   hipLaunchKernelGGL(k_gate_runs, dim3(blocks), dim3(256), 0, s, g);
-  hipLaunchKernelGGL(k_gate_gap, dim3(blocks), dim3(256), 0, s, g);
   hipLaunchKernelGGL(k_gate_apply, dim3(blocks), dim3(256), 0, s, g);
   return hipGetLastError();
 }

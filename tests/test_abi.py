@@ -82,15 +82,16 @@ def test_content_name_large_inputs(no_openssl):
 
 def test_product_library_has_no_diagnostic_kernel_variants():
     """The product libcrdtenc.so carries only the measured default instantiations of
-    k_open_fold_v2 (OPT 1 at 4 files per wave, OPT 3 at 2): the diagnostics variants -- some
+    k_open_fold_v2 (OPT 1 at 4 files per wave, OPT 3 at 2, and the open-only form at 16 lanes
+    per file and 3 blocks per lane, which decodes nothing): the diagnostics variants -- some
     give wrong results on purpose (OPT 129/385 skip the actor lookups, 513/1025 may write
     status 77) -- live only in libcrdtenc_prof.so (CE_FUSED_DIAG), so no environment variable
     can select them from the product."""
     raw = open(os.path.join(REPO, "crdt-enc_amd", "libcrdtenc.so"), "rb").read()
-    found = set(re.findall(rb"k_open_fold_v2ILi(\d+)ELi(\d+)ELb([01])ELi(\d+)E", raw))
+    found = set(re.findall(rb"k_open_fold_v2ILi(\d+)ELi(\d+)ELb([01])ELi(\d+)ELb([01])E", raw))
     assert found, "no k_open_fold_v2 instantiation found in the product library"
-    opts = {(int(l), int(w), int(j), int(o)) for l, w, j, o in found}
-    assert opts <= {(16, 2, 0, 1), (32, 3, 0, 3)}, sorted(opts)
+    opts = {(int(l), int(w), int(j), int(o), int(d)) for l, w, j, o, d in found}
+    assert opts <= {(16, 2, 0, 1, 1), (32, 3, 0, 3, 1), (16, 3, 0, 1, 0)}, sorted(opts)
     assert not re.search(rb"decode_foldILi\d+ELi[1-9]", raw)
 
 

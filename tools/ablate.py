@@ -1,7 +1,8 @@
 """Diagnostics: time k_open_fold_small with phases switched off (CE_ABLATE bits).  Results are
 invalid by construction; only the kernel time matters.  Run: python tools/ablate.py BITS"""
 import os, sys, time
-sys.argv = [sys.argv[0]] + ["--versions", "64", "--steps", "3", "--warmup", "1", "--no-cpu"]
+sys.argv = [sys.argv[0]] + ["--versions", "64", "--steps", "3", "--warmup", "1", "--no-cpu", "--no-variant-b",
+                           "--no-host-buffers", "--configs", ""]
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 import bench, crdtenc, torch
