@@ -798,11 +798,13 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
   auto run_fold = [&](const uint8_t* only) -> int {
     da.only = only;
     da.large_only = 1;
-    {
+    if (c->fused == 2 && c->files_per_wave != 1) {
+      hipEvent_t t0, t1;
+      (void)ctx->tlaunch("open_fold_small", &t0, &t1);
+      if ((e = launch_open_fold_v2(ctx->stream, da, c->files_per_wave, t0, t1))) return ctx->hip_fail(e, "fused");
+    } else {
       const int t = ctx->tbegin("open_fold_small");
-      e = c->fused == 2 && c->files_per_wave != 1 ? launch_open_fold_v2(ctx->stream, da, c->files_per_wave)
-                                                  : launch_open_fold_small(ctx->stream, da, c->files_per_wave);
-      if (e) return ctx->hip_fail(e, "fused");
+      if ((e = launch_open_fold_small(ctx->stream, da, c->files_per_wave))) return ctx->hip_fail(e, "fused");
       ctx->tend(t);
     }
     if (!setup_known) {  // landed long ago: the gate and the fused kernel follow it
@@ -1135,40 +1137,47 @@ int ingest_states_host(ce_core* c, const uint8_t* blob, const uint64_t* offs, ui
   int rc = device_open(ctx, ctx->blob.as<uint8_t>(), ctx->offs.as<uint64_t>(), n, blen, true,
                        key_of(c), ctx->out.as<uint8_t>(), ctx->status.as<int32_t>(), false);
   if (rc) return rc;
+  // one download for what the host reads per file (k_state_heads, 32 B each into pinned
+  // memory): status, clear length, plaintext offset and data version -- per-file copies into
+  // pageable memory each cost a blit dispatch and a staging wait on the box
+  if ((e = ctx->heads.reserve(32ull * n + 64)) || (e = ctx->h_heads.reserve(32ull * n + 64)))
+    return ctx->hip_fail(e, "states heads");
+  const uint8_t* hh = ctx->h_heads.as<uint8_t>();
   std::vector<int32_t> st(n);
-  if ((e = hipMemcpyAsync(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
-      (e = stream_wait(ctx->stream)))
-    return ctx->hip_fail(e, "states status");
+  auto read_heads = [&]() -> hipError_t {
+    hipError_t e2;
+    if ((e2 = launch_state_heads(ctx->stream, ctx->params.as<FileParams>(), ctx->status.as<int32_t>(),
+                                 ctx->out.as<uint8_t>(), n, ctx->heads.as<uint8_t>())) ||
+        (e2 = hipMemcpyAsync(ctx->h_heads.p, ctx->heads.p, 32ull * n, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (e2 = stream_wait(ctx->stream)))
+      return e2;
+    for (uint32_t i = 0; i < n; i++) std::memcpy(&st[i], hh + 32ull * i, 4);
+    return hipSuccess;
+  };
+  if ((e = read_heads())) return ctx->hip_fail(e, "states heads");
   for (uint32_t i = 0; i < n; i++)
     if (st[i] == kStatusHostParse) {
       if ((rc = resolve_host_parse(c, ctx->blob.as<uint8_t>(), ctx->offs.as<uint64_t>(), n, true)))
         return rc;
-      if ((e = hipMemcpy(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost)))
-        return ctx->hip_fail(e, "states status");
+      if ((e = read_heads())) return ctx->hip_fail(e, "states heads");
       break;
     }
   std::vector<FileParams> P(n);
   if (c->kind == CE_STATE_ORSWOT && !getenv("CE_HOST_STATES")) {
     // plaintexts stay in HBM: the device reader decodes canonical states (ce_dotset_io.hip)
-    if ((e = hipMemcpyAsync(P.data(), ctx->params.p, n * sizeof(FileParams), hipMemcpyDeviceToHost, ctx->stream)) ||
-        (e = stream_wait(ctx->stream)))
-      return ctx->hip_fail(e, "states params");
     std::vector<uint64_t> off(n, 0), len(n, 0);
-    std::vector<uint8_t> ver(16ull * n);
     for (uint32_t i = 0; i < n; i++) {
       if (st[i] != CE_OK) continue;
-      if (P[i].len < 16) { st[i] = CE_ERR_PT_LEN; continue; }
-      if ((e = hipMemcpyAsync(ver.data() + 16ull * i, ctx->out.as<uint8_t>() + P[i].out_off, 16,
-                              hipMemcpyDeviceToHost, ctx->stream)))
-        return ctx->hip_fail(e, "states version");
-      off[i] = P[i].out_off + 16;
-      len[i] = P[i].len - 16;
-    }
-    if ((e = stream_wait(ctx->stream))) return ctx->hip_fail(e, "states version");
-    for (uint32_t i = 0; i < n; i++) {
-      if (st[i] != CE_OK) continue;
+      const uint8_t* h = hh + 32ull * i;
+      uint32_t plen;
+      uint64_t out_off;
+      std::memcpy(&plen, h + 4, 4);
+      std::memcpy(&out_off, h + 8, 8);
+      if (plen < 16) { st[i] = CE_ERR_PT_LEN; continue; }
+      off[i] = out_off + 16;
+      len[i] = plen - 16;
       Uuid v;
-      std::memcpy(v.data(), ver.data() + 16ull * i, 16);
+      std::memcpy(v.data(), h + 16, 16);
       if (!std::binary_search(c->supported.begin(), c->supported.end(), v)) st[i] = CE_ERR_PT_VERSION;
     }
     return ds_merge_states_device(c, ctx->out.as<uint8_t>(), off, len, st.data(), status_out);

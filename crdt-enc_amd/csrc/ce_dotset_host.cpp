@@ -49,7 +49,7 @@ struct DsState {
   // bases, members, sorted members [0..6]
   // and emitted (member, actor id, value) columns [7..9]), pinned staging for its downloads
   std::vector<std::array<DevBuf, 10>> rd;
-  DevBuf rd_tmp, rd_misc, ser[16], uuid_of_id, rank_of_id, rd_oclocks, cnt_tot, rd_args_d, rd_chunks;
+  DevBuf rd_tmp, rd_misc, ser[16], uuid_of_id, rank_of_id, rd_oclocks, cnt_tot, rd_args_d, rd_chunks, rd_gather;
   HostBuf rd_host, rd_small, rd_clock, rd_args_h, h_clock;
   uint64_t uuid_ids = ~0ull;  // id count uuid_of_id / rank_of_id (and id_rank / rank_id) were built for
   std::vector<uint32_t> id_rank, rank_id;  // UUID-order rank of each stable id, and its inverse
@@ -1318,6 +1318,19 @@ hipError_t dl(void* dst, const void* src, size_t n, hipStream_t s) {
   return e ? e : stream_wait(s);
 }
 
+// per-file byte ranges of device memory -> the pinned host buffer `hb` at hoff[i], in one
+// download: packed on the device first (launch_gather_ranges), since every hipMemcpyAsync is
+// its own blit dispatch with its own gap on the box.  Not synchronised.
+hipError_t gather_download(DsState* d, hipStream_t s, uint8_t* hb, const std::vector<GatherRange>& r,
+                           uint64_t total) {
+  if (total == 0) return hipSuccess;
+  hipError_t e;
+  if ((e = d->rd_gather.reserve(total + 64)) ||
+      (e = launch_gather_ranges(s, d->rd_gather.as<uint8_t>(), r.data(), (uint32_t)r.size())))
+    return e;
+  return hipMemcpyAsync(hb, d->rd_gather.p, total, hipMemcpyDeviceToHost, s);
+}
+
 // the repeat-check set of a file with n entries: a power of two >= 2 n words (mask = size - 1)
 uint32_t dset_mask_for(uint64_t n) {
   uint64_t p = 64;
@@ -1399,10 +1412,12 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     auto ph = std::make_unique<HostPhase>("  rd: heads download");
     if ((e = d->rd_host.reserve(poff[n] + 64))) return ctx->hip_fail(e, "state head");
     uint8_t* hb = d->rd_host.as<uint8_t>();
-    for (size_t i = 0; i < n; i++)
-      if (poff[i + 1] > poff[i] &&
-          (e = hipMemcpyAsync(hb + poff[i], out + off[i], poff[i + 1] - poff[i], hipMemcpyDeviceToHost, s)))
-        return ctx->hip_fail(e, "state head");
+    {
+      std::vector<GatherRange> gr;
+      for (size_t i = 0; i < n; i++)
+        if (poff[i + 1] > poff[i]) gr.push_back({out + off[i], poff[i], poff[i + 1] - poff[i]});
+      if ((e = gather_download(d, s, hb, gr, poff[n]))) return ctx->hip_fail(e, "state head");
+    }
     if ((rc = sync("state head"))) return rc;
     ph = std::make_unique<HostPhase>("  rd: heads parse");
     std::vector<size_t> dev;
@@ -1535,10 +1550,12 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     for (size_t i : dev3) { toff[i] = ttot; ttot += len[i] - eend[i]; }
     if ((e = d->rd_host.reserve(ttot + 64))) return ctx->hip_fail(e, "state tail");
     hb = d->rd_host.as<uint8_t>();
-    for (size_t i : dev3)
-      if (len[i] > eend[i] &&
-          (e = hipMemcpyAsync(hb + toff[i], out + off[i] + eend[i], len[i] - eend[i], hipMemcpyDeviceToHost, s)))
-        return ctx->hip_fail(e, "state tail");
+    {
+      std::vector<GatherRange> gr;
+      for (size_t i : dev3)
+        if (len[i] > eend[i]) gr.push_back({out + off[i] + eend[i], toff[i], len[i] - eend[i]});
+      if ((e = gather_download(d, s, hb, gr, ttot))) return ctx->hip_fail(e, "state tail");
+    }
     if (ttot && (rc = sync("state tail"))) return rc;
     std::vector<size_t> dev4;
     for (size_t i : dev3) {

@@ -17,6 +17,8 @@
 // Poly1305 tree cost per file falls from 7 mulmods (64 lanes/file) to 5/4 (16 lanes/file).
 #include <algorithm>
 
+#include <hip/hip_ext.h>
+
 #include "ce_device.h"
 
 namespace ce {
@@ -1190,10 +1192,15 @@ void k_open_fold_v2(DecodeArgs a) {
 }
 
 template <int LPF, int W, bool JIT, int OPT = 3, bool DEC = true>
-static void launch_v2(hipStream_t s, const DecodeArgs& a) {
+static void launch_v2(hipStream_t s, const DecodeArgs& a, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr) {
   static const uint32_t res = resident_blocks(k_open_fold_v2<LPF, W, JIT, OPT, DEC>, 64);
   const uint32_t groups = (a.n + 64 / LPF - 1) / (64 / LPF);
-  hipLaunchKernelGGL((k_open_fold_v2<LPF, W, JIT, OPT, DEC>), dim3(std::min<uint32_t>(groups, res)), dim3(64), 0, s, a);
+  const dim3 grid(std::min<uint32_t>(groups, res));
+  if (t0) {  // the launch's own start / end timestamps: no marker packets around the kernel
+    hipExtLaunchKernelGGL((k_open_fold_v2<LPF, W, JIT, OPT, DEC>), grid, dim3(64), 0, s, t0, t1, 0u, a);
+  } else {
+    hipLaunchKernelGGL((k_open_fold_v2<LPF, W, JIT, OPT, DEC>), grid, dim3(64), 0, s, a);
+  }
 }
 
 // single-page files opened into HBM (a.pt at each file's out_off), lane-owned ChaCha20 blocks;
@@ -1204,7 +1211,8 @@ hipError_t launch_open_small_v2(hipStream_t s, const DecodeArgs& a) {
   return hipGetLastError();
 }
 
-hipError_t launch_open_fold_v2(hipStream_t s, const DecodeArgs& a, int files_per_wave) {
+hipError_t launch_open_fold_v2(hipStream_t s, const DecodeArgs& a, int files_per_wave, hipEvent_t t0,
+                               hipEvent_t t1) {
   if (a.n == 0) return hipSuccess;
 #if CE_FUSED_DIAG
   // diagnostics build only (libcrdtenc_prof.so): same-box A/B variants.  Several of them are
@@ -1221,34 +1229,34 @@ hipError_t launch_open_fold_v2(hipStream_t s, const DecodeArgs& a, int files_per
     return e ? atoi(e) : 1;
   }();
   if (files_per_wave == 2) {
-    if (w == 4) launch_v2<32, 4, false>(s, a);
-    else launch_v2<32, 3, false>(s, a);
+    if (w == 4) launch_v2<32, 4, false>(s, a, t0, t1);
+    else launch_v2<32, 3, false>(s, a, t0, t1);
   } else {
-    if (w == 3) launch_v2<16, 3, false>(s, a);
-    else if (w == 13) launch_v2<16, 3, true>(s, a);
-    else if (w == 12) launch_v2<16, 2, true>(s, a);
-    else if (opt == 0) launch_v2<16, 2, false, 0>(s, a);
-    else if (opt == 1) launch_v2<16, 2, false, 1>(s, a);
-    else if (opt == 2) launch_v2<16, 2, false, 2>(s, a);
-    else if (opt == 5) launch_v2<16, 2, false, 5>(s, a);
-    else if (opt == 9) launch_v2<16, 2, false, 9>(s, a);
-    else if (opt == 17) launch_v2<16, 2, false, 17>(s, a);
-    else if (opt == 21) launch_v2<16, 2, false, 21>(s, a);
-    else if (opt == 33) launch_v2<16, 2, false, 33>(s, a);
-    else if (opt == 65) launch_v2<16, 2, false, 65>(s, a);
-    else if (opt == 129) launch_v2<16, 2, false, 129>(s, a);
-    else if (opt == 257) launch_v2<16, 2, false, 257>(s, a);
-    else if (opt == 385) launch_v2<16, 2, false, 385>(s, a);
-    else if (opt == 513) launch_v2<16, 2, false, 513>(s, a);
-    else if (opt == 1025) launch_v2<16, 2, false, 1025>(s, a);
-    else if (opt == 81) launch_v2<16, 2, false, 81>(s, a);
-    else launch_v2<16, 2, false, 3>(s, a);
+    if (w == 3) launch_v2<16, 3, false>(s, a, t0, t1);
+    else if (w == 13) launch_v2<16, 3, true>(s, a, t0, t1);
+    else if (w == 12) launch_v2<16, 2, true>(s, a, t0, t1);
+    else if (opt == 0) launch_v2<16, 2, false, 0>(s, a, t0, t1);
+    else if (opt == 1) launch_v2<16, 2, false, 1>(s, a, t0, t1);
+    else if (opt == 2) launch_v2<16, 2, false, 2>(s, a, t0, t1);
+    else if (opt == 5) launch_v2<16, 2, false, 5>(s, a, t0, t1);
+    else if (opt == 9) launch_v2<16, 2, false, 9>(s, a, t0, t1);
+    else if (opt == 17) launch_v2<16, 2, false, 17>(s, a, t0, t1);
+    else if (opt == 21) launch_v2<16, 2, false, 21>(s, a, t0, t1);
+    else if (opt == 33) launch_v2<16, 2, false, 33>(s, a, t0, t1);
+    else if (opt == 65) launch_v2<16, 2, false, 65>(s, a, t0, t1);
+    else if (opt == 129) launch_v2<16, 2, false, 129>(s, a, t0, t1);
+    else if (opt == 257) launch_v2<16, 2, false, 257>(s, a, t0, t1);
+    else if (opt == 385) launch_v2<16, 2, false, 385>(s, a, t0, t1);
+    else if (opt == 513) launch_v2<16, 2, false, 513>(s, a, t0, t1);
+    else if (opt == 1025) launch_v2<16, 2, false, 1025>(s, a, t0, t1);
+    else if (opt == 81) launch_v2<16, 2, false, 81>(s, a, t0, t1);
+    else launch_v2<16, 2, false, 3>(s, a, t0, t1);
   }
 #else
   // product: the measured default only -- SDWA rot16 on, next-ciphertext prefetch off (same-box
   // A/B r02); 2 files per wave at a 3-wave budget (SDWA rot16 + prefetch) for the fpw = 2 geometry
-  if (files_per_wave == 2) launch_v2<32, 3, false, 3>(s, a);
-  else launch_v2<16, 2, false, 1>(s, a);
+  if (files_per_wave == 2) launch_v2<32, 3, false, 3>(s, a, t0, t1);
+  else launch_v2<16, 2, false, 1>(s, a, t0, t1);
 #endif
   return hipGetLastError();
 }

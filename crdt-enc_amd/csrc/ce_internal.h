@@ -125,8 +125,8 @@ struct ce_ctx {
   std::string last_error;
   // batch scratch (device)
   ce::DevBuf params, status, counters, extra, multi, partials, large, out, apply, refold, miss,
-      supported, blob, offs, nonces, out_offs, outer_ver, batch_counters, split, segrec, redo;
-  ce::HostBuf h_counters, h_apply, h_stage, h_stage2;
+      supported, blob, offs, nonces, out_offs, outer_ver, batch_counters, split, segrec, redo, heads;
+  ce::HostBuf h_counters, h_apply, h_stage, h_stage2, h_heads;
   // marks the setup kernel's counter snapshot (h_counters + 128) as landed on the host
   hipEvent_t setup_ev = nullptr;
   // a side stream for readbacks that must not sit between the main stream's kernels (the setup
@@ -165,6 +165,17 @@ struct ce_ctx {
   }
   void tend(int idx) {
     if (idx >= 0) (void)hipEventRecord(timed[idx].b, stream);
+  }
+  // a timed launch whose dispatch records the two events itself (hipExtLaunchKernel): *a / *b
+  // stay null when the name is not timed
+  int tlaunch(const char* name, hipEvent_t* a, hipEvent_t* b) {
+    *a = *b = nullptr;
+    if (!timing || (!timing_only.empty() && timing_only != name)) return -1;
+    TimedLaunch t{name, take_event(), take_event()};
+    *a = t.a;
+    *b = t.b;
+    timed.push_back(t);
+    return (int)timed.size() - 1;
   }
 
   // stream synchronise by polling an event (CE_SYNC_YIELD=1: hipStreamSynchronize).  The

@@ -140,7 +140,9 @@ hipError_t launch_segdec_apply(hipStream_t s, const DecodeArgs& a, SegScratch sc
 hipError_t launch_open_fold_small(hipStream_t s, const DecodeArgs& a, int files_per_wave);
 // the same with whole ChaCha20 blocks per lane (keystream XOR in registers; ce_fused.hip
 // k_open_fold_v2); files_per_wave in {2, 4}
-hipError_t launch_open_fold_v2(hipStream_t s, const DecodeArgs& a, int files_per_wave);
+// t0 / t1: timing events recorded by the dispatch itself (hipExtLaunchKernel), or none
+hipError_t launch_open_fold_v2(hipStream_t s, const DecodeArgs& a, int files_per_wave,
+                               hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 // open only: single-page files (<= kSmallMax) into a.pt at their out_off, 16 lanes per file
 // (k_open_fold_v2<..., DEC = false>); statuses and the failure counters as the segment pass sets them
 hipError_t launch_open_small_v2(hipStream_t s, const DecodeArgs& a);
@@ -195,5 +197,19 @@ hipError_t launch_compact_prologue(hipStream_t s, uint8_t* args, const CompactAr
 // reads after the step.
 hipError_t launch_tail_pack(hipStream_t s, uint8_t* dst, const unsigned long long* src_len,
                             const uint32_t* counters, const unsigned long long* newnov, uint32_t m);
+
+// Byte ranges of device memory packed into one device buffer (dst + dst_off), so that a batch
+// of per-file pieces comes back in ONE download (each hipMemcpyAsync is its own blit dispatch
+// with its own gap on the box).  Any alignment.
+struct GatherRange {
+  const uint8_t* src;
+  uint64_t dst_off, len;
+};
+hipError_t launch_gather_ranges(hipStream_t s, uint8_t* dst, const GatherRange* r, uint32_t n);
+
+// Per opened state file, 32 bytes: status (i32) | clear length (u32) | plaintext offset (u64) |
+// the plaintext's first 16 bytes (the data version) when the status is CE_OK and len >= 16
+hipError_t launch_state_heads(hipStream_t s, const FileParams* params, const int32_t* status,
+                              const uint8_t* out, uint32_t n, uint8_t* dst);
 
 }  // namespace ce

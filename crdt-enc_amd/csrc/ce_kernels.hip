@@ -1446,6 +1446,70 @@ hipError_t launch_tail_pack(hipStream_t s, uint8_t* dst, const unsigned long lon
   return hipGetLastError();
 }
 
+static constexpr uint32_t kGatherBatch = 16;
+struct GatherBatch {
+  GatherRange r[kGatherBatch];
+};
+// blockIdx.y = range; the blocks of a range stride over its bytes, 16 at a time where source and
+// destination share an alignment, byte by byte at the edges otherwise
+__global__ void k_gather_ranges(uint8_t* __restrict__ dst, GatherBatch b) {
+  const GatherRange g = b.r[blockIdx.y];
+  uint8_t* d = dst + g.dst_off;
+  const uint64_t tid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t nt = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t mis = (16 - ((uintptr_t)g.src & 15)) & 15;
+  if ((((uintptr_t)g.src ^ (uintptr_t)d) & 15) == 0 && g.len > mis + 16) {
+    const uint64_t head = mis, body = (g.len - head) & ~15ull;
+    for (uint64_t i = tid; i < head; i += nt) d[i] = g.src[i];
+    const uint4* s4 = reinterpret_cast<const uint4*>(g.src + head);
+    uint4* d4 = reinterpret_cast<uint4*>(d + head);
+    for (uint64_t i = tid; i < body / 16; i += nt) d4[i] = s4[i];
+    for (uint64_t i = head + body + tid; i < g.len; i += nt) d[i] = g.src[i];
+  } else {
+    for (uint64_t i = tid; i < g.len; i += nt) d[i] = g.src[i];
+  }
+}
+
+hipError_t launch_gather_ranges(hipStream_t s, uint8_t* dst, const GatherRange* r, uint32_t n) {
+  for (uint32_t i0 = 0; i0 < n; i0 += kGatherBatch) {
+    GatherBatch b{};
+    const uint32_t k = min(n - i0, kGatherBatch);
+    uint64_t mx = 0;
+    for (uint32_t i = 0; i < k; i++) {
+      b.r[i] = r[i0 + i];
+      mx = b.r[i].len > mx ? b.r[i].len : mx;
+    }
+    if (mx == 0) continue;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((mx + 16ull * 256 - 1) / (16ull * 256), 256ull);
+    hipLaunchKernelGGL(k_gather_ranges, dim3(blocks, k), dim3(256), 0, s, dst, b);
+  }
+  return hipGetLastError();
+}
+
+__global__ void k_state_heads(const FileParams* __restrict__ params, const int32_t* __restrict__ status,
+                              const uint8_t* __restrict__ out, uint32_t n, uint8_t* __restrict__ dst) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t st = status[i];
+  const FileParams& P = params[i];
+  uint32_t w[8] = {(uint32_t)st, P.len, (uint32_t)P.out_off, (uint32_t)(P.out_off >> 32), 0, 0, 0, 0};
+  if (st == CE_OK && P.len >= 16) {
+    const uint8_t* v = out + P.out_off;  // 16-byte aligned (open)
+    const uint4 q = *reinterpret_cast<const uint4*>(v);
+    w[4] = q.x; w[5] = q.y; w[6] = q.z; w[7] = q.w;
+  }
+  uint4* o = reinterpret_cast<uint4*>(dst + 32ull * i);
+  o[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  o[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+hipError_t launch_state_heads(hipStream_t s, const FileParams* params, const int32_t* status,
+                              const uint8_t* out, uint32_t n, uint8_t* dst) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_state_heads, dim3((n + 255) / 256), dim3(256), 0, s, params, status, out, n, dst);
+  return hipGetLastError();
+}
+
 hipError_t launch_serialize_vclock(hipStream_t s, const unsigned long long* nov,
                                   const unsigned long long* st, const uint32_t* sorted, uint32_t k,
                                   const ActorSlot* table, bool gcounter, const uint8_t* prefix16,
