@@ -3,7 +3,8 @@
 + --kernel-trace + --memory-copy-trace): from the step's k_fill launch call to the next one.
 Rows: 'API' = a host call (start, duration), 'GPU' = a kernel / copy (start, duration).
 
-  tools/c2_api_breakdown.py <rocprofv3 output dir> [step index]"""
+  tools/c2_api_breakdown.py <rocprofv3 output dir> [step index] [step marker kernel]
+(the marker defaults to ce::k_fill, C2's first launch; C3: ce::k_open_setup of the states)"""
 import csv
 import glob
 import sys
@@ -23,8 +24,9 @@ for fn in glob.glob(d + "/**/*hip_api_trace.csv", recursive=True):
         api.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "API", r["Function"][:44]))
 ev += api
 ev.sort()
-fills = [e for e in ev if e[2] == "GPU" and "ce::k_fill" in e[3]]
-k = int(sys.argv[2]) if len(sys.argv) > 2 else len(fills) - 2
+marker = sys.argv[3] if len(sys.argv) > 3 else "ce::k_fill"
+fills = [e for e in ev if e[2] == "GPU" and marker in e[3]]
+k = int(sys.argv[2]) if len(sys.argv) > 2 and int(sys.argv[2]) >= 0 else len(fills) - 2
 g0, g1 = fills[k][0], fills[k + 1][0]
 # the host window: from the launch call of this step's fill to that of the next
 launches = [e for e in api if "LaunchKernel" in e[3] or "ModuleLaunch" in e[3]]
