@@ -40,7 +40,8 @@ EXPORTS = [
     "ce_cryptor_encrypt_batch_device", "ce_storage_open", "ce_storage_close",
     "ce_storage_list_op_actors", "ce_storage_load_ops", "ce_storage_store_ops",
     "ce_storage_remove_ops", "ce_storage_list_state_names", "ce_storage_store_state",
-    "ce_storage_load_state", "ce_storage_remove_state", "ce_content_name", "ce_core_open",
+    "ce_storage_load_state", "ce_storage_remove_state", "ce_content_name", "ce_content_name_async",
+    "ce_content_name_wait", "ce_core_open",
     "ce_core_close", "ce_core_set_latest_key", "ce_core_info_actor", "ce_core_read_remote",
     "ce_core_compact", "ce_core_apply_ops", "ce_core_state_bytes", "ce_core_ingest_ops",
     "ce_core_ingest_ops_device", "ce_core_ingest_states", "ce_core_compact_to_buffer",
@@ -215,6 +216,35 @@ def content_name(data):
     if rc:
         raise CeError(rc)
     return out.value.decode()
+
+
+class NameJob:
+    """ce_content_name_async: the name of `data` computed on the library's host thread; the
+    buffer must stay alive (and unchanged) until result() returns."""
+
+    def __init__(self, data):
+        p, n = _ptr(data)
+        self._keep = (data, p)
+        t = ctypes.c_uint64(0)
+        rc = lib().ce_content_name_async(p, ctypes.c_size_t(n), ctypes.byref(t))
+        if rc:
+            raise CeError(rc)
+        self.ticket = t.value
+        self._name = None
+
+    def result(self):
+        if self._name is None:
+            out = ctypes.create_string_buffer(64)
+            rc = lib().ce_content_name_wait(ctypes.c_uint64(self.ticket), out)
+            if rc:
+                raise CeError(rc)
+            self._name = out.value.decode()
+            self._keep = None
+        return self._name
+
+
+def content_name_async(data):
+    return NameJob(data)
 
 
 class Context:

@@ -10,8 +10,14 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdio>
+#include <deque>
+#include <mutex>
 #include <string>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
 
 #include "ce_internal.h"
 
@@ -346,6 +352,46 @@ ce_storage* storage_new(const std::string& local, const std::string& remote) {
 }
 }  // namespace ce
 
+// One native worker for ce_content_name_async: the caller's thread only queues the job (no
+// Python thread, hence no interpreter-lock hand-offs between the caller and the hash).  The
+// worker is detached and lives for the process.
+namespace {
+struct NameWorker {
+  struct Job {
+    uint64_t id;
+    const uint8_t* data;
+    size_t len;
+  };
+  std::mutex mu;
+  std::condition_variable cv_job, cv_done;
+  std::deque<Job> q;
+  std::unordered_map<uint64_t, std::string> done;
+  std::unordered_set<uint64_t> pending;  // queued or hashing
+  uint64_t next = 1;
+  bool started = false;
+  void run() {
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv_job.wait(lk, [&] { return !q.empty(); });
+      const Job j = q.front();
+      q.pop_front();
+      lk.unlock();
+      uint8_t h[32];
+      sha3_256(j.data, j.len, h);
+      std::string nm = base32_nopad(h, 32);
+      lk.lock();
+      pending.erase(j.id);
+      done.emplace(j.id, std::move(nm));
+      cv_done.notify_all();
+    }
+  }
+};
+NameWorker& name_worker() {
+  static NameWorker* w = new NameWorker;  // never destroyed: the detached worker may still run
+  return *w;
+}
+}  // namespace
+
 extern "C" {
 
 int ce_storage_open(const char* local_path, const char* remote_path, ce_storage** out) {
@@ -441,6 +487,35 @@ int ce_content_name(const uint8_t* data, size_t len, char name_out[64]) {
   uint8_t h[32];
   sha3_256(data, len, h);
   std::snprintf(name_out, 64, "%s", base32_nopad(h, 32).c_str());
+  return CE_OK;
+}
+
+int ce_content_name_async(const uint8_t* data, size_t len, uint64_t* ticket) {
+  if ((len && !data) || !ticket) return CE_ERR_INVALID_ARG;
+  NameWorker& w = name_worker();
+  std::lock_guard<std::mutex> g(w.mu);
+  if (!w.started) {
+    std::thread([&w] { w.run(); }).detach();
+    w.started = true;
+  }
+  *ticket = w.next++;
+  w.pending.insert(*ticket);
+  w.q.push_back({*ticket, data, len});
+  w.cv_job.notify_one();
+  return CE_OK;
+}
+
+int ce_content_name_wait(uint64_t ticket, char name_out[64]) {
+  if (!name_out) return CE_ERR_INVALID_ARG;
+  NameWorker& w = name_worker();
+  std::unique_lock<std::mutex> lk(w.mu);
+  auto it = w.done.find(ticket);
+  if (it == w.done.end() && !w.pending.count(ticket)) return CE_ERR_INVALID_ARG;  // unknown or waited
+  // done, or taken meanwhile by another waiter of the same ticket
+  w.cv_done.wait(lk, [&] { return (it = w.done.find(ticket)) != w.done.end() || !w.pending.count(ticket); });
+  if (it == w.done.end()) return CE_ERR_INVALID_ARG;
+  std::snprintf(name_out, 64, "%s", it->second.c_str());
+  w.done.erase(it);
   return CE_OK;
 }
 

@@ -180,6 +180,12 @@ int ce_storage_load_state(ce_storage *s, const char *name, ce_buf *out);
 int ce_storage_remove_state(ce_storage *s, const char *name);
 /* content address of a blob: BASE32_NOPAD(SHA3-256(data)) (tokio lib.rs:403-417) */
 int ce_content_name(const uint8_t *data, size_t len, char name_out[64]);
+/* the same name computed on the library's own host thread (store_state's hash off the caller's
+   thread, e.g. while the next compaction runs): *ticket identifies the job; data must stay valid
+   until ce_content_name_wait(ticket) returns.  Jobs run in submission order; a ticket is waited
+   once. */
+int ce_content_name_async(const uint8_t *data, size_t len, uint64_t *ticket);
+int ce_content_name_wait(uint64_t ticket, char name_out[64]);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Core (crdt-enc/src/lib.rs)                                                                */

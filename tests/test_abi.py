@@ -57,6 +57,21 @@ def test_content_name_matches_fixture(repo_fx):
         assert crdtenc.content_name(d) == want
 
 
+def test_content_name_async_matches_hashlib():
+    """ce_content_name_async / _wait (the library's host-thread name, what bench.py overlaps
+    with the next step) == BASE32_NOPAD(SHA3-256) for jobs queued together and waited out of
+    order; a ticket cannot be waited twice."""
+    import numpy as np
+    data = np.frombuffer(os.urandom(300000), dtype=np.uint8).copy()
+    sizes = [0, 1, 135, 136, 137, 4095, 4096, 221184, 300000]
+    jobs = [crdtenc.content_name_async(data[:n]) for n in sizes]
+    for n, j in reversed(list(zip(sizes, jobs))):
+        want = base64.b32encode(hashlib.sha3_256(data[:n].tobytes()).digest()).decode().rstrip("=")
+        assert j.result() == want, n
+    out = ctypes.create_string_buffer(64)
+    assert crdtenc.lib().ce_content_name_wait(ctypes.c_uint64(jobs[0].ticket), out) != 0
+
+
 @pytest.mark.parametrize("no_openssl", [False, True])
 def test_content_name_large_inputs(no_openssl):
     """BASE32_NOPAD(SHA3-256(bytes)) (crdt-enc-tokio/src/lib.rs:407-417) at and past the 4 KiB
