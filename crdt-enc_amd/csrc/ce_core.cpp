@@ -863,7 +863,8 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
   if ((rc = run_fold(nullptr))) return rc;
   // commit on the device unless the counters flag a slow path (k_merge_max_if), then one read
   // of the counters and of the gate's next_op_versions
-  if (!sharded) {
+  // (with a compaction behind the ingest, its first kernel does this commit)
+  if (!sharded && !after_commit) {
     const int t = ctx->tbegin("merge");
     if ((e = launch_merge_max_if(ctx->stream, c->d_state.as<unsigned long long>(),
                                  c->d_batch.as<unsigned long long>(), c->cap,
@@ -877,6 +878,11 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
                 reinterpret_cast<const unsigned long long*>(gbase + 16ull * m), m,
                 ctx->counters.as<uint32_t>()};
     na.nov_dev = reinterpret_cast<unsigned long long*>(gbase + 32ull * m);
+    if (!sharded) {
+      na.merge_dst = c->d_state.as<unsigned long long>();
+      na.merge_src = c->d_batch.as<unsigned long long>();
+      na.merge_n = c->cap;
+    }
     if ((rc = (*after_commit)(na))) return rc;
     host_tail = na.host_tail;  // it downloads the counters and newnov with its own tail
   }
@@ -1355,7 +1361,9 @@ int compact_enqueue(ce_core* c, ce_ctx* x, const uint8_t* nonce, NovApply* na, C
   std::memcpy(ca.prefix, c->current_data_version.data(), 16);
   // args at db + A: [offs(2) | out_offs(1) | nonce(24) | outer(16) | prefix16(16)]
   if ((e = launch_compact_prologue(x->stream, db + A, ca, seal_counters, nov, na ? na->wslot : nullptr,
-                                   na ? na->newnov : nullptr, m, na ? na->counters : nullptr)))
+                                   na ? na->newnov : nullptr, m, na ? na->counters : nullptr,
+                                   na ? na->merge_dst : nullptr, na ? na->merge_src : nullptr,
+                                   na ? na->merge_n : 0u)))
     return x->hip_fail(e, "compact prologue");
   auto* d_offs = reinterpret_cast<unsigned long long*>(db + A);
   if ((e = launch_serialize_vclock(x->stream, nov, c->d_state.as<unsigned long long>(), c->d_sorted.as<uint32_t>(),

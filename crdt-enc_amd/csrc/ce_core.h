@@ -163,6 +163,11 @@ struct NovApply {
                                          // newnov to it in place
   const uint8_t* host_tail = nullptr;    // out (set by the compaction): pinned host copy of
                                          // [clear length | the counters | newnov[m]] after sync
+  // the ingest's commit (k_merge_max_if: state = max(state, batch) over merge_n words), left to
+  // the compaction's first kernel when set: one launch and one dependency gap fewer
+  unsigned long long* merge_dst = nullptr;
+  const unsigned long long* merge_src = nullptr;
+  uint32_t merge_n = 0;
 };
 
 bool skip_any(Rd& r, int depth = 0);

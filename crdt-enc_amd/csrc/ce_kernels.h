@@ -189,9 +189,12 @@ struct CompactArgs {
   uint8_t outer[16];
   uint8_t prefix[16];
 };
+// with merge_n > 0 also the ingest's commit, as k_merge_max_if (same skip condition)
 hipError_t launch_compact_prologue(hipStream_t s, uint8_t* args, const CompactArgs& ca, uint32_t* seal_counters,
                                    unsigned long long* nov, const uint32_t* wslot,
-                                   const unsigned long long* newnov, uint32_t m, const uint32_t* counters);
+                                   const unsigned long long* newnov, uint32_t m, const uint32_t* counters,
+                                   unsigned long long* merge_dst = nullptr,
+                                   const unsigned long long* merge_src = nullptr, uint32_t merge_n = 0);
 // The compaction's epilogue readback in one place: dst = [clear length u64 (from src_len) |
 // the ingest's counter block (16 u32) | newnov u64[m]], so one download carries what the host
 // reads after the step.

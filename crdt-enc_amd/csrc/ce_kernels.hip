@@ -1403,7 +1403,9 @@ hipError_t launch_nov_apply(hipStream_t s, unsigned long long* nov, const uint32
 
 __global__ void k_compact_prologue(uint8_t* args, CompactArgs ca, uint32_t* seal_counters,
                                    unsigned long long* nov, const uint32_t* wslot,
-                                   const unsigned long long* newnov, uint32_t m, const uint32_t* counters) {
+                                   const unsigned long long* newnov, uint32_t m, const uint32_t* counters,
+                                   unsigned long long* __restrict__ merge_dst,
+                                   const unsigned long long* __restrict__ merge_src, uint32_t merge_n) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t < 24) {  // offs[0] = 0, offs[1] = 0 (the serializer writes the clear length), out_offs[0] = 0
     args[t] = 0;
@@ -1417,16 +1419,26 @@ __global__ void k_compact_prologue(uint8_t* args, CompactArgs ca, uint32_t* seal
     const uint32_t w = t - 80;
     seal_counters[w] = (w == 5 || w == 13) ? 0xffffffffu : 0u;
   }
-  if (m == 0 || (counters[2] | counters[3] | counters[4] | counters[7] | counters[8] | counters[12])) return;
-  for (uint32_t a = t; a < m; a += gridDim.x * blockDim.x) atomicMax(&nov[wslot[a]], newnov[a]);
+  if ((m == 0 && merge_n == 0) ||
+      (counters[2] | counters[3] | counters[4] | counters[7] | counters[8] | counters[12]))
+    return;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t a = t; a < m; a += stride) atomicMax(&nov[wslot[a]], newnov[a]);
+  for (uint32_t i = t; i < merge_n; i += stride) {  // the ingest's commit (k_merge_max_if)
+    const unsigned long long v = merge_src[i];
+    if (v > merge_dst[i]) merge_dst[i] = v;
+  }
 }
 
 hipError_t launch_compact_prologue(hipStream_t s, uint8_t* args, const CompactArgs& ca, uint32_t* seal_counters,
                                    unsigned long long* nov, const uint32_t* wslot,
-                                   const unsigned long long* newnov, uint32_t m, const uint32_t* counters) {
-  const uint32_t blocks = m > 96 ? min((m + 255) / 256, 256u) : 1u;
+                                   const unsigned long long* newnov, uint32_t m, const uint32_t* counters,
+                                   unsigned long long* merge_dst, const unsigned long long* merge_src,
+                                   uint32_t merge_n) {
+  const uint32_t work = m > merge_n ? m : merge_n;
+  const uint32_t blocks = work > 96 ? min((work + 255) / 256, 256u) : 1u;
   hipLaunchKernelGGL(k_compact_prologue, dim3(blocks), dim3(256), 0, s, args, ca, seal_counters, nov, wslot,
-                     newnov, m, counters);
+                     newnov, m, counters, merge_dst, merge_src, merge_n);
   return hipGetLastError();
 }
 
