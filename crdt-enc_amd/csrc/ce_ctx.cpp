@@ -68,8 +68,9 @@ uint32_t grid_waves_for(uint32_t work) {
   return std::max<uint32_t>(1, std::min<uint32_t>(work, full));
 }
 
-static int reserve_batch(ce_ctx* ctx, uint32_t n, uint64_t blob_len, uint32_t* extra_cap) {
-  const uint64_t ec = blob_len / (kSegBlocks * 16) + 16;
+static int reserve_batch(ce_ctx* ctx, uint32_t n, uint64_t blob_len, uint32_t* extra_cap,
+                         uint32_t seg_blocks = kSegBlocks) {
+  const uint64_t ec = blob_len / (seg_blocks * 16) + 16;
   if (ec > 0xffffffffull) return ctx->fail(CE_ERR_INVALID_ARG, "batch too large");
   *extra_cap = (uint32_t)ec;
   hipError_t e;
@@ -93,6 +94,7 @@ SegScratch segscratch(ce_ctx* ctx, uint32_t extra_cap) {
   sc.multi_files = ctx->multi.as<uint32_t>();
   sc.partials = ctx->partials.as<uint32_t>();
   sc.large_list = ctx->large.as<uint32_t>();
+  sc.seg_blocks = kSegBlocks;
   return sc;
 }
 
@@ -181,12 +183,16 @@ int device_seal(ce_ctx* ctx, const uint8_t* d_clear, const uint64_t* d_offs, uin
                 uint64_t clear_len_total, const uint8_t* d_outer_version, const uint8_t* d_nonces,
                 uint8_t* d_out, const uint64_t* d_out_offs, const KeyRef& key, bool counters_ready) {
   if (int32_t ks = key_status(key)) return ctx->fail(ks, "key rejected");
+  // a compaction's single state file of up to 1 MiB: one-page segments, so its keystream is 4x
+  // the waves (the segment kernel's four dependent pages per wave were most of its time)
+  const uint32_t seg_blocks = n <= 4 && clear_len_total <= (1u << 20) ? kPageBytes / 16 : kSegBlocks;
   uint32_t ec;
-  int rc = reserve_batch(ctx, n, clear_len_total + 16ull * n, &ec);
+  int rc = reserve_batch(ctx, n, clear_len_total + 16ull * n, &ec, seg_blocks);
   if (rc) return rc;
   hipError_t e;
   if (!counters_ready && (e = reset_counters(ctx)) != hipSuccess) return ctx->hip_fail(e, "memset counters");
   SegScratch sc = segscratch(ctx, ec);
+  sc.seg_blocks = seg_blocks;
   FileParams* P = ctx->params.as<FileParams>();
   int t = ctx->tbegin("seal_setup");
   if ((e = launch_seal_setup(ctx->stream, d_clear, d_offs, n, d_outer_version, d_nonces, d_out,
@@ -194,7 +200,7 @@ int device_seal(ce_ctx* ctx, const uint8_t* d_clear, const uint64_t* d_offs, uin
     return ctx->hip_fail(e, "seal setup");
   ctx->tend(t);
   t = ctx->tbegin("segments_seal");
-  // one wave per 16 KiB segment: a single large state file still fills the chip
+  // one wave per segment: a single large state file still fills the chip
   if ((e = launch_segments(ctx->stream, true, d_clear, d_out, P, n, ctx->status.as<int32_t>(), sc,
                            grid_waves_for(n + ec))) != hipSuccess)
     return ctx->hip_fail(e, "seal segments");

@@ -327,7 +327,7 @@ __device__ __forceinline__ void key_schedule(const DevKey& key, const uint8_t* n
 // whole wave, one file at a time.
 __device__ __forceinline__ void reserve_segments(FileParams& P, uint32_t f, SegScratch sc, bool mine = true) {
   const uint64_t nblk = ((uint64_t)P.len + 15) / 16 + 1;
-  const uint32_t nseg = mine ? (uint32_t)((nblk + kSegBlocks - 1) / kSegBlocks) : 0u;
+  const uint32_t nseg = mine ? (uint32_t)((nblk + sc.seg_blocks - 1) / sc.seg_blocks) : 0u;
   if (mine) {
     P.nseg = nseg;
     P.extra_base = 0;

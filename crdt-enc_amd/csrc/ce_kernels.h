@@ -50,6 +50,8 @@ struct SegScratch {
   uint32_t* multi_files;  // files with nseg > 1
   uint32_t* partials;     // 5 limbs per segment: [file-major] base = extra index
   uint32_t* large_list;   // files with more than one page (counters[9] entries)
+  uint32_t seg_blocks;    // Poly1305 blocks per segment: kSegBlocks; a seal of a few small files
+                          // (a compaction's state) uses one page, 4x the waves in flight
 };
 
 // One launch for an ingest's scratch initialisation (each hipMemsetAsync is its own blit

@@ -348,8 +348,9 @@ __global__ __launch_bounds__(256) void k_segments(const uint8_t* __restrict__ in
 
     const uint32_t nblk_ct = (len + 15) >> 4;
     const uint32_t nblk = nblk_ct + 1;
-    const uint32_t b_lo = j * kSegBlocks;
-    const uint32_t b_hi = min(nblk, b_lo + kSegBlocks);
+    const uint32_t SB = SEAL ? sc.seg_blocks : kSegBlocks;  // (the open path keeps its constant)
+    const uint32_t b_lo = j * SB;
+    const uint32_t b_hi = min(nblk, b_lo + SB);
     const uint32_t nb = b_hi - b_lo;
     const uint32_t rows = (nb + 63) >> 6;
 
@@ -568,6 +569,7 @@ __global__ __launch_bounds__(256) void k_finalize_multi(uint8_t* __restrict__ ou
                                                         int32_t* __restrict__ status,
                                                         SegScratch sc) {
   const uint32_t nm = sc.counters[1];
+  const uint32_t SB = SEAL ? sc.seg_blocks : kSegBlocks;  // Poly1305 blocks per segment
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t stride = gridDim.x * kWavesPerBlock;
   for (uint32_t t = bcast(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)); t < nm; t += stride) {
@@ -584,7 +586,7 @@ __global__ __launch_bounds__(256) void k_finalize_multi(uint8_t* __restrict__ ou
     L5 T = load_l5(P.rpow[6]);  // r^64 -> r^(64 S), only when a lane has a second segment
     if (nseg > 65) {
 #pragma unroll 1
-      for (uint32_t e = 64; e < 64u * kSegBlocks; e <<= 1) T = mulmod(T, T);
+      for (uint32_t e = 64; e < 64u * SB; e <<= 1) T = mulmod(T, T);
     }
     if (nseg > 1 + lane) {
       L5 acc = load_l5(sc.partials + 5ull * (base + lane));
@@ -593,7 +595,7 @@ __global__ __launch_bounds__(256) void k_finalize_multi(uint8_t* __restrict__ ou
         acc = add5(mulmod(acc, T), load_l5(sc.partials + 5ull * (base + j)));
         jl = j;
       }
-      sum = mulmod(carry5(acc), rpow_any(P, nblk - (jl + 1) * kSegBlocks));
+      sum = mulmod(carry5(acc), rpow_any(P, nblk - (jl + 1) * SB));
     }
     if (lane == 0) sum = carry5(add5(sum, load_l5(sc.partials + 5ull * (base + nseg - 1))));
 #pragma unroll
