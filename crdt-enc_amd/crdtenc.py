@@ -242,6 +242,18 @@ class NameJob:
             self._keep = None
         return self._name
 
+    def __del__(self):
+        # a job dropped unwaited (e.g. an exception between steps): the worker still reads the
+        # buffer through a raw pointer, so wait for it before the buffer can be freed (this also
+        # retires the ticket's entry in the library's done table)
+        try:
+            if self._name is None and getattr(self, "_keep", None) is not None:
+                out = ctypes.create_string_buffer(64)
+                lib().ce_content_name_wait(ctypes.c_uint64(self.ticket), out)
+                self._keep = None
+        except Exception:
+            pass
+
 
 def content_name_async(data):
     return NameJob(data)
@@ -812,15 +824,18 @@ class Core:
             ctypes.c_void_p(d_fa), ctypes.c_void_p(d_fv), ctypes.c_void_p(d_hi), st)
         return (rc, list(st)[:n]) if want_status else rc
 
-    def pending_export(self, d_batch):
+    def pending_export(self, d_batch, cap_words):
+        """The pending batch into d_batch (u64[cap_words]); False (nothing written) when it names
+        an unregistered actor or the table outgrew cap_words."""
         ready = ctypes.c_int(0)
-        self.ctx.check(lib().ce_core_pending_export(self.p, ctypes.c_void_p(d_batch), ctypes.byref(ready)),
-                       "pending_export")
+        self.ctx.check(lib().ce_core_pending_export(self.p, ctypes.c_void_p(d_batch), ctypes.c_uint64(cap_words),
+                                                    ctypes.byref(ready)), "pending_export")
         return ready.value == 1
 
-    def pending_commit(self, accept, d_import=None):
+    def pending_commit(self, accept, d_import=None, import_words=0):
         self.ctx.check(lib().ce_core_pending_commit(self.p, 1 if accept else 0,
-                                                    ctypes.c_void_p(d_import) if d_import else None),
+                                                    ctypes.c_void_p(d_import) if d_import else None,
+                                                    ctypes.c_uint64(import_words)),
                        "pending_commit")
 
     def writer_versions(self, actors):

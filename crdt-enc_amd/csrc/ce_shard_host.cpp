@@ -284,11 +284,14 @@ int ce_core_ingest_ops_device_sharded(ce_core* c, const uint8_t* d_blob, const u
   return (hi[m] & kShardGap) ? CE_ERR_OP_VERSION : CE_OK;
 }
 
-int ce_core_pending_export(ce_core* c, uint64_t* d_batch, int* ready) {
+int ce_core_pending_export(ce_core* c, uint64_t* d_batch, uint64_t cap_words, int* ready) {
   if (!c || !d_batch || !ready || is_dotset_kind(c->kind)) return CE_ERR_INVALID_ARG;
   std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
   if (!c->pending || c->pending_gen != c->table_gen) return c->ctx->fail(CE_ERR_INVALID_ARG, "no pending batch");
-  *ready = c->registered == c->size ? 1 : 0;
+  // an actor outside the registered slots (the ingest inserted it, and may have grown the table
+  // past the caller's buffer): not exportable, and nothing is written
+  *ready = c->registered == c->size && c->cap <= cap_words ? 1 : 0;
+  if (!*ready) return CE_OK;
   hipError_t e;
   if ((e = hipMemcpyAsync(d_batch, c->d_batch.p, c->cap * 8ull, hipMemcpyDeviceToDevice, c->ctx->stream)) ||
       (e = c->ctx->sync_spin()))
@@ -296,7 +299,7 @@ int ce_core_pending_export(ce_core* c, uint64_t* d_batch, int* ready) {
   return CE_OK;
 }
 
-int ce_core_pending_commit(ce_core* c, int accept, const uint64_t* d_import) {
+int ce_core_pending_commit(ce_core* c, int accept, const uint64_t* d_import, uint64_t import_words) {
   if (!c || is_dotset_kind(c->kind)) return CE_ERR_INVALID_ARG;
   std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
   (void)hipSetDevice(c->ctx->device);
@@ -304,6 +307,8 @@ int ce_core_pending_commit(ce_core* c, int accept, const uint64_t* d_import) {
   c->pending = false;
   if (!accept) return CE_OK;  // another rank's batch failed: the state stays unchanged
   if (c->pending_gen != c->table_gen) return c->ctx->fail(CE_ERR_INVALID_ARG, "actor table changed since the ingest");
+  if (d_import && import_words < c->cap)
+    return c->ctx->fail(CE_ERR_INVALID_ARG, "reduced batch shorter than the dense capacity");
   const hipError_t e = launch_merge_max(c->ctx->stream, c->d_state.as<unsigned long long>(),
                                         d_import ? reinterpret_cast<const unsigned long long*>(d_import)
                                                  : c->d_batch.as<unsigned long long>(),

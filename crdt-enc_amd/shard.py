@@ -272,14 +272,29 @@ class DeviceShardOps:
         return self.dense
 
     def export_pending(self, dense):
+        """False (nothing written) when the batch cannot go through the dense reduce: an actor
+        outside the registered slots, or a table grown past `dense` during the ingest."""
         if dense.dtype != torch.int64:
             raise TypeError("dense is an int64 view of u64")
         self._ordered()
-        return self.core.pending_export(dense.data_ptr())
+        return self.core.pending_export(dense.data_ptr(), dense.numel())
 
     def commit(self, accept, reduced=None):
         self._ordered()
-        self.core.pending_commit(accept, reduced.data_ptr() if reduced is not None else None)
+        if reduced is None:
+            self.core.pending_commit(accept)
+        else:
+            self.core.pending_commit(accept, reduced.data_ptr(), reduced.numel())
+
+
+def contract_flags(stats):
+    """SHARD_BAD | SHARD_E0_MISMATCH from reduced ShardStats (int64[2m + 3], the last three words
+    flipped-u64: contract flag, h(e0), ~h(e0); layout ce_common.h) -- the flags word the window
+    kernel derives, read on the host so every rank branches on the same value."""
+    import numpy as np
+    t = stats[-3:].cpu().numpy().view(np.uint64) ^ np.uint64(1 << 63)
+    bad, h, nh = (int(x) for x in t)
+    return (SHARD_BAD if bad else 0) | (SHARD_E0_MISMATCH if h != (~nh & 0xFFFFFFFFFFFFFFFF) else 0)
 
 
 def _gather_metadata(fa, fv, group=None):
@@ -308,23 +323,30 @@ def ingest_sharded(ops, group=None, exchange_bytes=None):
     # 1) the gate: per-writer stats, one all_reduce(MAX), identical windows on every rank
     stats = ops.compute_stats(rank, world)
     all_reduce_(stats, dist.ReduceOp.MAX, group=group)
-    ops.window()
-    rc = ops.ingest()
+    # The path is chosen from the reduced stats' flag words, identical on every rank, never from
+    # one rank's ingest status: a rank failing early (no key, a bad file) must still take the
+    # same collectives as the others.
+    flags = contract_flags(stats)
+    if flags & SHARD_E0_MISMATCH:
+        # the ranks started from different next_op_versions: no window is right for all of them
+        # (the exact fallback would compute each rank's from its own e0); refused, nothing folded
+        return ERR_SHARD, "refused"
     exact = ""
-    if rc == ERR_SHARD:
-        # a rank's batch breaks the partition contract (same flags on every rank, from the
-        # reduced stats): the windows from everyone's metadata, the reference loop on the host
+    if flags & SHARD_BAD:
+        # a rank's batch breaks the partition contract: the windows from everyone's metadata,
+        # the reference loop on the host (one gather, every rank)
         import crdtenc
         e0 = ops.writer_versions()
         fa, fv = ops.metadata()
         fa_all, fv_all = _gather_metadata(fa, fv, group=group)
-        hi, flags = crdtenc.shard_window_exact(e0, fa_all, fv_all)
-        ops.set_window(hi, flags)
-        rc = ops.ingest()
+        hi, wflags = crdtenc.shard_window_exact(e0, fa_all, fv_all)
+        ops.set_window(hi, wflags)
         exact = "+exact"
-        if rc == ERR_SHARD:
-            raise RuntimeError("sharded ingest refused its exact windows (next_op_versions differ "
-                               "across ranks?)")
+    else:
+        ops.window()
+    # any failure here, including a rank-local early return, reaches every rank through the
+    # reduce below, and every rank keeps its state
+    rc = ops.ingest()
     # 2) all-or-nothing + exchange: the pending batch and the failure flags in one all_reduce
     failed = rc not in (0, ERR_OP_VERSION)
     dense = ops.dense_buffer()

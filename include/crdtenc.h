@@ -377,12 +377,14 @@ int ce_core_ingest_ops_device_sharded(ce_core *c, const uint8_t *d_blob, const u
                                       uint32_t m, const uint32_t *d_fa, const uint64_t *d_fv,
                                       const uint64_t *d_hi, int32_t *status);
 /* The pending batch as a dense u64[ce_core_dense_capacity] over the registered slots (for the
- * all_reduce(MAX)); *ready = 0 when it names an actor outside register_actors (then commit it
- * locally and exchange serialized states instead). */
-int ce_core_pending_export(ce_core *c, uint64_t *d_batch, int *ready);
-/* accept: state = max(state, d_import ? d_import (the reduced batch) : the local pending batch),
- * next_op_versions from the windows; !accept: drop the pending batch. */
-int ce_core_pending_commit(ce_core *c, int accept, const uint64_t *d_import);
+ * all_reduce(MAX)); d_batch holds cap_words u64.  *ready = 0, and nothing is written, when the
+ * batch names an actor outside register_actors or the actor table has grown past cap_words since
+ * the caller sized d_batch (then commit it locally and exchange serialized states instead). */
+int ce_core_pending_export(ce_core *c, uint64_t *d_batch, uint64_t cap_words, int *ready);
+/* accept: state = max(state, d_import ? d_import (the reduced batch, import_words u64; at least
+ * ce_core_dense_capacity) : the local pending batch), next_op_versions from the windows;
+ * !accept: drop the pending batch. */
+int ce_core_pending_commit(ce_core *c, int accept, const uint64_t *d_import, uint64_t import_words);
 /* next_op_versions.get(writer) for each of m writers (host) */
 int ce_core_writer_versions(ce_core *c, const uint8_t *actors, uint32_t m, uint64_t *e0_out);
 /* Host twins (CPU ranks, tests): ShardStats over host metadata; the windows from reduced stats;

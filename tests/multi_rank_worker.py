@@ -109,8 +109,9 @@ def main_sharded(rank, world, name, out):
     import torch
     import crdtenc
     import shard
-    from test_shard import _scenario
+    from test_shard import _scenario, _rank_pre
     key, writers, registered, files, fa, fv, pre = _scenario(name)
+    pre = _rank_pre(name, pre, rank)
     own = crdtenc.shard_owners(writers, fa, fv, world)
     if name == "contract":
         own[11] = (own[11] + 1) % world
@@ -119,9 +120,10 @@ def main_sharded(rank, world, name, out):
     core.set_latest_key(key)
     core.register_actors(registered)
     first = [i for i in range(len(files)) if fv[i] < pre[fa[i]]]
-    if first:  # the replicated starting state
+    if first:  # the starting state (replicated, except for e0_mismatch)
         rc, _ = core.ingest_ops([files[i] for i in first], writers, [fa[i] for i in first], [fv[i] for i in first])
         assert rc == 0, rc
+    start = core.state_bytes()
     sel = [i for i in range(len(files)) if own[i] == rank]
     blob = b"".join(files[i] for i in sel)
     offs = np.zeros(len(sel) + 1, np.int64)
@@ -134,7 +136,7 @@ def main_sharded(rank, world, name, out):
     ops = shard.DeviceShardOps(core, b"".join(writers), d_files, d_offs, len(sel), len(blob), d_fa, d_fv)
     rc, path = shard.ingest_sharded(ops)
     with open("%s.%d" % (out, rank), "wb") as f:
-        f.write(msgpack.packb([rc, path, len(sel), core.state_bytes()], use_bin_type=True))
+        f.write(msgpack.packb([rc, path, len(sel), core.state_bytes(), start], use_bin_type=True))
     core.close()
     ctx.close()
 

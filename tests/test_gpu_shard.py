@@ -27,7 +27,7 @@ import shard
 pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "tests"))
-from test_shard import _random_batch, _scenario, _oracle_fold  # noqa: E402
+from test_shard import _random_batch, _scenario, _oracle_fold, _expected  # noqa: E402
 
 APP = bytes.fromhex("aadfd5a66e194b24a8024fa27c72f20c")
 
@@ -130,7 +130,7 @@ def test_three_shares_one_process(ctx, oracle, name, want_rc):
         b = torch.zeros(core.dense_capacity(), dtype=torch.int64, device=dev)
         torch.cuda.synchronize()   # the core's own stream reads / writes it next
         if rc in (0, 13):
-            ready.append(core.pending_export(b.data_ptr()))
+            ready.append(core.pending_export(b.data_ptr(), b.numel()))
         batches.append(b.cpu().numpy().view(np.uint64))
     failed = [rc for rc in rcs if rc not in (0, 13)]
     if failed:
@@ -148,7 +148,7 @@ def test_three_shares_one_process(ctx, oracle, name, want_rc):
             red_b = torch.from_numpy(np.maximum.reduce(batches).view(np.int64).copy()).to(dev)
             torch.cuda.synchronize()
             for core in cores:
-                core.pending_commit(True, red_b.data_ptr())
+                core.pending_commit(True, red_b.data_ptr(), red_b.numel())
         else:   # a Dot on an unregistered actor: commit locally, then merge serialized states
             assert name == "unregistered"
             for core in cores:
@@ -172,15 +172,16 @@ def _port():
 @pytest.mark.parametrize("name,want_rc,want_path", [
     ("clean", 0, "dense"), ("gap", 13, "dense"), ("old_versions", 0, "dense"),
     ("tamper", 9, "rejected"), ("contract", 0, "dense+exact"), ("unregistered", 0, "bytes"),
+    ("grow", 0, "bytes"), ("e0_mismatch", 69, "refused"),
 ])
 def test_two_process_sharded_ingest(tmp_path, name, want_rc, want_path):
+    """'grow': one rank's Dots name 2100 new actors, so its ingest grows the actor table past the
+    dense buffer sized before it -- the export must decline (no write past the buffer) and every
+    rank take the state all-gather; 'e0_mismatch': the ranks start from different
+    next_op_versions -- refused on every rank, each state unchanged."""
     key, writers, _, files, fa, fv, pre = _scenario(name)
-    if name == "tamper":
-        first = [i for i in range(len(files)) if fv[i] < pre[fa[i]]]
-        want = _oracle_fold(key, writers, [files[i] for i in first], [fa[i] for i in first],
-                            [fv[i] for i in first], {a: 0 for a in pre})[1]
-    else:
-        want = _oracle_fold(key, writers, files, fa, fv, pre)[1]
+    want_rc2, want = _expected(name, key, writers, files, fa, fv, pre)
+    assert want_rc2 == want_rc
     out = str(tmp_path / "s")
     port = str(_port())
     procs = [subprocess.Popen([sys.executable, os.path.join(REPO, "tests", "multi_rank_worker.py"),
@@ -189,7 +190,7 @@ def test_two_process_sharded_ingest(tmp_path, name, want_rc, want_path):
     assert rcs == [0, 0]
     for r in range(2):
         with open("%s.%d" % (out, r), "rb") as f:
-            rc, path, n, state = msgpack.unpackb(f.read(), raw=False)
+            rc, path, n, state, start = msgpack.unpackb(f.read(), raw=False)
         assert (rc, path) == (want_rc, want_path), r
         assert 0 < n < len(files)
-        assert state == want, r
+        assert state == (start if want is None else want), r

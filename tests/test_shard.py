@@ -167,6 +167,10 @@ def _scenario(name, seed=9, m=6, versions=9):
                     for _ in range(rng.randint(1, 8))]
             if name == "unregistered" and a == 4 and v == 6:
                 dots.append({"actor": stranger, "counter": 12345})
+            if name == "grow" and a == 4 and v == 6:
+                # more new actors than the initial table holds (1/4 of 8192 slots): the ingest grows
+                # the actor table past the dense buffer the exchange was sized with
+                dots += [{"actor": rng.randbytes(16), "counter": rng.randint(1, 1 << 30)} for _ in range(2100)]
             st, enc = oracle.cryptor_encrypt(key, rng.randbytes(24), APP + msgpack.packb(dots, use_bin_type=True))
             assert st == 0
             if name == "tamper" and a == 3 and v == 5:
@@ -199,20 +203,43 @@ def _rank_main(rank, world, port, name, out_path):
         if name == "contract":         # one file handed to the other rank
             own[11] = (own[11] + 1) % world
         core = TwinCore()
-        if any(pre.values()):          # the replicated starting state (same on every rank)
+        pre = _rank_pre(name, pre, rank)
+        if any(pre.values()):          # the starting state (replicated, except for e0_mismatch)
             _, ser = _oracle_fold(key, writers, [files[i] for i in range(len(files)) if fv[i] < pre[fa[i]]],
                                   [fa[i] for i in range(len(files)) if fv[i] < pre[fa[i]]],
                                   [fv[i] for i in range(len(files)) if fv[i] < pre[fa[i]]], {a: 0 for a in pre})
             core.fold_bytes(ser)
+        start = core.state_bytes()
         sel = [i for i in range(len(files)) if own[i] == rank]
         split = sorted(set(fa[i] for i in sel))
         ops = HostShardOps(core, key, writers, registered, [files[i] for i in sel], [fa[i] for i in sel],
                            [fv[i] for i in sel])
         rc, path = shard.ingest_sharded(ops)
         with open("%s.%d" % (out_path, rank), "wb") as f:
-            f.write(msgpack.packb([rc, path, len(sel), split, core.state_bytes()], use_bin_type=True))
+            f.write(msgpack.packb([rc, path, len(sel), split, core.state_bytes(), start], use_bin_type=True))
     finally:
         dist.destroy_process_group()
+
+
+def _rank_pre(name, pre, rank):
+    """Versions of each writer folded before the sharded ingest on `rank`: the scenario's
+    replicated start, except e0_mismatch, where rank 1 alone has also folded writer 1's version 0
+    (the ranks start from different next_op_versions)."""
+    if name == "e0_mismatch" and rank == 1:
+        return {**pre, 1: 1}
+    return pre
+
+
+def _expected(name, key, writers, files, fa, fv, pre):
+    """(rc, state) every rank must end with; None for the state when it is the rank's own start."""
+    orc, want = _oracle_fold(key, writers, files, fa, fv, pre)
+    if name == "tamper":   # the reference panics (lib.rs:502): nothing folded, the state unchanged
+        first = [i for i in range(len(files)) if fv[i] < pre[fa[i]]]
+        return 9, _oracle_fold(key, writers, [files[i] for i in first], [fa[i] for i in first],
+                               [fv[i] for i in first], {a: 0 for a in pre})[1]
+    if name == "e0_mismatch":  # refused before any fold: each rank keeps its own start
+        return shard.ERR_SHARD, None
+    return orc, want
 
 
 @pytest.mark.parametrize("name,want_rc,want_path", [
@@ -222,21 +249,22 @@ def _rank_main(rank, world, port, name, out_path):
     ("tamper", 9, "rejected"),
     ("contract", 0, "dense+exact"),
     ("unregistered", 0, "bytes"),
+    ("grow", 0, "bytes"),
+    ("e0_mismatch", 69, "refused"),
 ])
 def test_two_rank_sharded_ingest_equals_single_fold(tmp_path, name, want_rc, want_path):
     key, writers, _, files, fa, fv, pre = _scenario(name)
-    orc, want = _oracle_fold(key, writers, files, fa, fv, pre)
-    if name == "tamper":   # the reference panics (lib.rs:502): nothing folded, the state unchanged
-        want = _oracle_fold(key, writers, [files[i] for i in range(len(files)) if fv[i] < pre[fa[i]]],
-                            [fa[i] for i in range(len(files)) if fv[i] < pre[fa[i]]],
-                            [fv[i] for i in range(len(files)) if fv[i] < pre[fa[i]]], {a: 0 for a in pre})[1]
-    else:
-        assert orc == want_rc
+    orc, want = _expected(name, key, writers, files, fa, fv, pre)
+    assert orc == want_rc
     out = str(tmp_path / "r")
     mp.spawn(_rank_main, args=(2, _free_port(), name, out), nprocs=2, join=True)
+    starts = set()
     for r in range(2):
         with open("%s.%d" % (out, r), "rb") as f:
-            rc, path, n, split, state = msgpack.unpackb(f.read(), raw=False)
+            rc, path, n, split, state, start = msgpack.unpackb(f.read(), raw=False)
         assert (rc, path) == (want_rc, want_path), (r, rc, path)
         assert 0 < n < len(files) and len(split) == len(writers)   # every writer split across ranks
-        assert state == want, r
+        assert state == (start if want is None else want), r
+        starts.add(start)
+    if name == "e0_mismatch":
+        assert len(starts) == 2
