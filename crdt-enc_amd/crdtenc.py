@@ -58,6 +58,7 @@ EXPORTS = [
     "ce_core_shard_window", "ce_core_ingest_ops_device_sharded", "ce_core_pending_export",
     "ce_core_pending_commit", "ce_core_writer_versions", "ce_shard_stats_host",
     "ce_shard_window_host", "ce_shard_window_exact", "ce_core_compact_ops_device_into",
+    "ce_core_state_bytes_device", "ce_core_merge_state_device",
 ]
 
 
@@ -265,6 +266,7 @@ class Context:
     def __init__(self, device=0):
         import weakref
         self.p = ctypes.c_void_p()
+        self.device = device
         self._cores = weakref.WeakSet()  # cores hold the context: close them first
         rc = lib().ce_ctx_create(device, ctypes.byref(self.p))
         if rc:
@@ -783,6 +785,17 @@ class Core:
         """read_remote_states' merge of one decrypted StateWrapper (lib.rs:447, 458-466)."""
         return lib().ce_core_merge_state(self.p, _cbuf(state_wrapper_msgpack),
                                          ctypes.c_size_t(len(state_wrapper_msgpack)))
+
+    def state_bytes_device(self, d_dst, cap):
+        """StateWrapper bytes written into device memory d_dst (cap bytes): (rc, length); rc
+        INVALID_ARG with the needed length when cap is too small."""
+        n = ctypes.c_uint64(0)
+        rc = lib().ce_core_state_bytes_device(self.p, ctypes.c_void_p(d_dst), ctypes.c_uint64(cap), ctypes.byref(n))
+        return rc, n.value
+
+    def merge_state_device(self, d_sw, length):
+        """merge_state of a StateWrapper resident in HBM (device pointer, length bytes)."""
+        return lib().ce_core_merge_state_device(self.p, ctypes.c_void_p(d_sw), ctypes.c_uint64(length))
 
     def register_actors(self, actors):
         self.ctx.check(lib().ce_core_register_actors(self.p, _cbuf(b"".join(actors)),

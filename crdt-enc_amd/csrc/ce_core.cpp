@@ -2060,4 +2060,42 @@ int ce_core_merge_state(ce_core* c, const uint8_t* sw, size_t len) {
   return table_upload(c);
 }
 
+// ce_core_state_bytes into device memory: Orswot through the device writer (the 35 MB C3
+// partial never crosses PCIe); the other kinds' states are small and serialized on the host.
+int ce_core_state_bytes_device(ce_core* c, uint8_t* d_dst, uint64_t cap, uint64_t* len) {
+  if (!c || !len || (cap && !d_dst)) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  (void)hipSetDevice(c->ctx->device);
+  if (c->kind == CE_STATE_ORSWOT && !c->host_compact) return ds_state_bytes_device(c, c->ctx, d_dst, cap, len);
+  std::vector<uint8_t>& b = c->ser_buf;
+  int rc = serialize_state(c, &b);
+  if (rc) return rc;
+  *len = b.size();
+  if (b.size() > cap) return c->ctx->fail(CE_ERR_INVALID_ARG, "device buffer too small for the state");
+  hipError_t e;
+  if (!b.empty() && ((e = hipMemcpyAsync(d_dst, b.data(), b.size(), hipMemcpyHostToDevice, c->ctx->stream)) ||
+                     (e = stream_wait(c->ctx->stream))))
+    return c->ctx->hip_fail(e, "state bytes");
+  return CE_OK;
+}
+
+// ce_core_merge_state over a StateWrapper resident in HBM: Orswot through the device state
+// reader (ds_merge_states_device: only the head -- next_op_versions and the clock -- and the
+// deferred tail come to the host); the other kinds download it (small) and merge on the host.
+int ce_core_merge_state_device(ce_core* c, const uint8_t* d_sw, uint64_t len) {
+  if (!c || (len && !d_sw)) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  (void)hipSetDevice(c->ctx->device);
+  if (c->kind == CE_STATE_ORSWOT && !getenv("CE_HOST_STATES")) {
+    int32_t st = CE_OK;
+    return ds_merge_states_device(c, d_sw, std::vector<uint64_t>{0}, std::vector<uint64_t>{len}, &st, nullptr);
+  }
+  std::vector<uint8_t> h(len);
+  hipError_t e;
+  if (len && ((e = hipMemcpyAsync(h.data(), d_sw, len, hipMemcpyDeviceToHost, c->ctx->stream)) ||
+              (e = stream_wait(c->ctx->stream))))
+    return c->ctx->hip_fail(e, "merge state");
+  return ce_core_merge_state(c, h.data(), len);
+}
+
 }  // extern "C"

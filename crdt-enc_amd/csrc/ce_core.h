@@ -209,6 +209,8 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
 int ds_merge_states(ce_core* c, const std::vector<std::pair<const uint8_t*, size_t>>& sws,
                     int32_t* st, int32_t* status_out);
 int ds_serialize(ce_core* c, std::vector<uint8_t>* out);
+// Orswot: the same bytes written on the device into dst (cap bytes); *len = their length
+int ds_state_bytes_device(ce_core* c, ce_ctx* x, uint8_t* dst, uint64_t cap, uint64_t* len);
 // Core::apply_ops for a local Vec<S::Op> (already validated by ds_check_ops)
 int ds_check_ops(ce_core* c, const uint8_t* ops, size_t len);
 int ds_apply_local_ops(ce_core* c, const uint8_t* ops, size_t len);

@@ -1787,10 +1787,13 @@ int ds_apply_local_ops(ce_core* c, const uint8_t* ops, size_t len) {
 // (prefix16 || to_vec_named(StateWrapper), the same bytes as ds_serialize) is written into
 // x->blob by the device writer (ce_dotset_io.hip) around a host-built head (next_op_versions,
 // clock) and tail (deferred), sealed on the device and downloaded once.
-int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t* prefix16,
-                      const uint8_t* nonce, const KeyRef& key, std::vector<uint8_t>* file) {
-  HostPhase hp("ds compact (device writer)");
-  c->path_counts["compact_device_writer"]++;
+// The device writer itself: prefix16 || to_vec_named(StateWrapper) into `dst` when dst_cap covers
+// the bound U, else into x->blob (*clear = where it went), with the seal's staging words
+// (offsets [0, clear len, out offset], stats, nonce, outer version) at x->blob + *A.  Queued on
+// x->stream; the clear length lands in the second offset word.
+static int ds_serialize_dev(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t* prefix16,
+                            const uint8_t* nonce, uint8_t* dst, uint64_t dst_cap, uint64_t* A_out,
+                            uint64_t* U_out, uint8_t** clear) {
   DsState* d = c->ds;
   hipStream_t s = x->stream;
   hipError_t e;
@@ -1895,8 +1898,8 @@ int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t
   uint8_t* hs = x->h_stage.as<uint8_t>();
   std::memset(hs, 0, 128);
   if (nonce) std::memcpy(hs + 32, nonce, 24);
-  else os_random(hs + 32, 24);
-  std::memcpy(hs + 56, outer, 16);
+  else if (outer) os_random(hs + 32, 24);
+  if (outer) std::memcpy(hs + 56, outer, 16);
   std::memcpy(hs + 128, hw.b.data(), hw.b.size());
   std::memcpy(hs + 128 + hw.b.size(), tw.b.data(), tw.b.size());
   if ((e = hipMemcpyAsync(db + A, hs, 128 + hw.b.size() + tw.b.size(), hipMemcpyHostToDevice, s)))
@@ -1924,7 +1927,7 @@ int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t
   sc.tmp = d->ser[15].p;
   sc.tmp_bytes = d->ser[15].cap;
   OrswotSerArgs a{};
-  a.out = db;
+  a.out = dst && dst_cap >= U ? dst : db;
   a.prefix = db + A + 128;
   a.prefix_len = hw.b.size();
   a.suffix = db + A + 128 + hw.b.size();
@@ -1937,6 +1940,25 @@ int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t
   const int t = x->tbegin("ds_serialize");
   if ((e = launch_orswot_ser(s, sc, a))) return x->hip_fail(e, "ds serialize");
   x->tend(t);
+  *A_out = A;
+  *U_out = U;
+  *clear = a.out;
+  return CE_OK;
+}
+
+int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t* prefix16,
+                      const uint8_t* nonce, const KeyRef& key, std::vector<uint8_t>* file) {
+  HostPhase hp("ds compact (device writer)");
+  c->path_counts["compact_device_writer"]++;
+  hipStream_t s = x->stream;
+  hipError_t e;
+  int rc;
+  uint64_t A = 0, U = 0;
+  uint8_t* clear = nullptr;
+  if ((rc = ds_serialize_dev(c, x, outer, prefix16, nonce, nullptr, 0, &A, &U, &clear))) return rc;
+  uint8_t* db = x->blob.as<uint8_t>();
+  auto* offs = reinterpret_cast<unsigned long long*>(db + A);
+  auto cph = std::make_unique<HostPhase>("  cd: seal enqueue");
   rc = device_seal(x, db, reinterpret_cast<const uint64_t*>(offs), 1, U, db + A + 56, db + A + 32,
                    x->out.as<uint8_t>(), reinterpret_cast<const uint64_t*>(db + A + 16), key);
   if (rc) return rc;
@@ -1958,6 +1980,30 @@ int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t
   cph = std::make_unique<HostPhase>("  cd: download");
   if ((e = hipMemcpyAsync(to, x->out.p, total, hipMemcpyDeviceToHost, s)) || (e = stream_wait(s)))
     return x->hip_fail(e, "ds compact download");
+  return CE_OK;
+}
+
+// to_vec_named(StateWrapper<Orswot>) into device memory (the dot-set exchange between GPUs,
+// crdtenc shard.reduce_dotset): the device writer straight into dst when cap covers its bound,
+// else through x->blob.  *len = the length; CE_ERR_INVALID_ARG (nothing written) when cap < *len.
+int ds_state_bytes_device(ce_core* c, ce_ctx* x, uint8_t* dst, uint64_t cap, uint64_t* len) {
+  hipStream_t s = x->stream;
+  hipError_t e;
+  int rc;
+  uint64_t A = 0, U = 0;
+  uint8_t* clear = nullptr;
+  if ((rc = ds_serialize_dev(c, x, nullptr, nullptr, nullptr, dst, cap, &A, &U, &clear))) return rc;
+  const uint8_t* db = x->blob.as<uint8_t>();
+  uint64_t n = 0;
+  if ((e = hipMemcpyAsync(&n, db + A + 8, 8, hipMemcpyDeviceToHost, s)) || (e = stream_wait(s)))
+    return x->hip_fail(e, "state bytes");
+  if (n > U) return x->fail(CE_ERR_DEVICE, "serializer overran its bound");
+  *len = n;
+  if (clear == dst) return CE_OK;
+  if (n > cap) return x->fail(CE_ERR_INVALID_ARG, "device buffer too small for the state");
+  // complete on return, like the direct write: the caller's collective runs on another stream
+  if (n && ((e = hipMemcpyAsync(dst, clear, n, hipMemcpyDeviceToDevice, s)) || (e = stream_wait(s))))
+    return x->hip_fail(e, "state bytes");
   return CE_OK;
 }
 

@@ -152,38 +152,125 @@ def _global(group, r):
     return r if group is None else dist.get_global_rank(group, r)
 
 
-def reduce_dotset(core, group=None, device="cpu", dst=0):
+class StateBuffer:
+    """A growable byte buffer in HBM for partial StateWrappers (one per rank, reused across
+    steps): the dot-set exchange sends and receives it without a host copy."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.t = None
+
+    def ensure(self, n):
+        if self.t is None or self.t.numel() < n:
+            self.t = torch.empty(max(n + (n >> 3), 1 << 20), dtype=torch.uint8, device=self.device)
+        return self.t
+
+
+_ERR_INVALID_ARG = 64
+
+
+def _send_state_device(core, buf, dst, group, comm_device, timing):
+    """core's StateWrapper serialized into HBM (ce_core_state_bytes_device: the device writer,
+    complete on return) -> dist.send.  With RCCL the bytes go GPU to GPU; gloo stages them
+    through the host (the CPU / one-GPU rehearsal)."""
+    import time
+    t0 = time.perf_counter()
+    t = buf.ensure(1 << 20)
+    rc, n = core.state_bytes_device(t.data_ptr(), t.numel())
+    if rc == _ERR_INVALID_ARG and n > t.numel():
+        t = buf.ensure(n)
+        rc, n = core.state_bytes_device(t.data_ptr(), t.numel())
+    if rc:
+        raise RuntimeError("state_bytes_device failed: %d" % rc)
+    t1 = time.perf_counter()
+    dist.send(torch.tensor([n], dtype=torch.int64, device=comm_device), dst, group=group)
+    if n:
+        dist.send(t[:n] if t.device == torch.device(comm_device) else t[:n].to(comm_device), dst, group=group)
+    if timing is not None:
+        timing.append({"send": True, "bytes": n, "serialize_ms": round((t1 - t0) * 1e3, 3),
+                       "send_ms": round((time.perf_counter() - t1) * 1e3, 3)})
+
+
+def _recv_merge_device(core, buf, src, group, comm_device, timing):
+    """dist.recv of a partial StateWrapper into HBM -> ce_core_merge_state_device (the device
+    state reader and merge; only the state's head and deferred tail reach the host)."""
+    import time
+    t0 = time.perf_counter()
+    hdr = torch.zeros(1, dtype=torch.int64, device=comm_device)
+    dist.recv(hdr, src, group=group)
+    n = int(hdr.item())
+    if not n:
+        raise RuntimeError("rank %d sent an empty state" % src)
+    t = buf.ensure(n)
+    if t.device == torch.device(comm_device):
+        dist.recv(t[:n], src, group=group)
+        # the receive completes on torch's stream; the core reads on its own stream
+        torch.cuda.current_stream(t.device).synchronize()
+    else:
+        h = torch.empty(n, dtype=torch.uint8, device=comm_device)
+        dist.recv(h, src, group=group)
+        t[:n].copy_(h)
+        torch.cuda.current_stream(t.device).synchronize()
+    t1 = time.perf_counter()
+    rc = core.merge_state_device(t.data_ptr(), n)
+    if rc:
+        raise RuntimeError("merge_state_device from rank %d failed: %d" % (src, rc))
+    if timing is not None:
+        timing.append({"recv": True, "bytes": n, "recv_ms": round((t1 - t0) * 1e3, 3),
+                       "merge_ms": round((time.perf_counter() - t1) * 1e3, 3)})
+
+
+def reduce_dotset(core, group=None, device="cpu", dst=0, buf=None, timing=None):
     """Merge the partial Orswot / MVReg states of all ranks into rank `dst`'s `core` along a
     binomial tree: in round k (k = 0, 1, ...) the rank at distance 2^k above a multiple of
-    2^(k+1) sends its (already merged) StateWrapper to that multiple, which merge_states it (the
-    CvRDT merge of read_remote_states, crdt-enc/src/lib.rs:458-466, on the GPU).  Only the
+    2^(k+1) sends its (already merged) StateWrapper to that multiple, which merges it (the
+    CvRDT merge of read_remote_states, crdt-enc/src/lib.rs:446-466, on the GPU).  Only the
     compacting rank ends with the whole state; every rank does at most ceil(log2 N) merges and
-    each state crosses the fabric once (exchange_dotset: N - 1 merges on every rank).  Returns
-    the number of merges this rank ran."""
+    each state crosses the fabric once (exchange_dotset: N - 1 merges on every rank).
+
+    With a crdtenc.Core the state stays in HBM end to end: serialized by the device writer into
+    `buf` (a StateBuffer; made here when None), sent / received as a device tensor (RCCL: GPU to
+    GPU over xGMI; gloo stages it through the host), merged by the device state reader.  Other
+    cores (the CPU tests' twins) exchange host bytes.  `device` is the collectives' device
+    ("cpu" for gloo).  `timing` (a list) receives one record per hop.  Returns the number of
+    merges this rank ran."""
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     rel = (rank - dst) % world
+    on_device = hasattr(core, "state_bytes_device")
+    if on_device and buf is None:
+        buf = StateBuffer(torch.device("cuda", core.ctx.device))
     merges, step = 0, 1
     while step < world:
         if rel % (2 * step) == step:          # send to the partner below, then done
-            _send_bytes(core.state_bytes(), _global(group, (rank - step) % world), group=group, device=device)
+            peer = _global(group, (rank - step) % world)
+            if on_device:
+                _send_state_device(core, buf, peer, group, device, timing)
+            else:
+                _send_bytes(core.state_bytes(), peer, group=group, device=device)
             break
         if rel % (2 * step) == 0 and rel + step < world:
-            sw = _recv_bytes(_global(group, (rank + step) % world), group=group, device=device)
-            rc = core.merge_state(sw)
-            if rc:
-                raise RuntimeError("merge_state from rank %d failed: %d" % ((rank + step) % world, rc))
+            peer = _global(group, (rank + step) % world)
+            if on_device:
+                _recv_merge_device(core, buf, peer, group, device, timing)
+            else:
+                sw = _recv_bytes(peer, group=group, device=device)
+                rc = core.merge_state(sw)
+                if rc:
+                    raise RuntimeError("merge_state from rank %d failed: %d" % (peer, rc))
             merges += 1
         step *= 2
     return merges
 
 
-def ingest_dotset_sharded(core, ingest, group=None, device="cpu", snapshot=True):
+def ingest_dotset_sharded(core, ingest, group=None, device="cpu", snapshot=True, buf=None, timing=None):
     """read_remote_ops of the dot-set kinds over writer shards (actor_range), then the tree
-    reduce to rank 0.  `ingest()` folds this rank's files into `core` and returns its status.
+    reduce to rank 0 (reduce_dotset; buf / timing passed through).  `ingest()` folds this rank's
+    files into `core` and returns its status.
     All-or-nothing across ranks (lib.rs:497-514): the statuses meet in one all_reduce(MAX) before
     any state moves; on a failure anywhere, every rank that folded its shard goes back to the
     StateWrapper it held before (reset + merge_state of the snapshot) and the failing status is
-    returned on every rank.  Returns (rc, merges)."""
+    returned on every rank.  snapshot=False: the caller knows the state before the ingest (e.g.
+    empty after a reset) and restores it itself; a failure then raises.  Returns (rc, merges)."""
     s0 = core.state_bytes() if snapshot else None
     rc = ingest()
     code = torch.tensor([rc], dtype=torch.int64, device=device)
@@ -197,7 +284,7 @@ def ingest_dotset_sharded(core, ingest, group=None, device="cpu", snapshot=True)
             if core.merge_state(s0):
                 raise RuntimeError("restoring the snapshot failed")
         return code, 0
-    return 0, reduce_dotset(core, group=group, device=device)
+    return 0, reduce_dotset(core, group=group, device=device, buf=buf, timing=timing)
 
 
 def exchange_dotset(core, group=None, device="cpu"):

@@ -324,6 +324,15 @@ int ce_core_compact_into(ce_core *c, const uint8_t *nonce, uint8_t *dst, size_t 
  * rmp_serde::from_slice::<StateWrapper<S>>(sw) then state.merge + next_op_versions.merge.
  * Also the exchange step of the dot-set kinds across GPUs (all-gather of partial states). */
 int ce_core_merge_state(ce_core *c, const uint8_t *sw, size_t len);
+/* The multi-GPU dot-set exchange without a host hop (read_remote_states' merge, lib.rs:446-466,
+ * with the partial state travelling GPU to GPU over RCCL): ce_core_state_bytes written into
+ * device memory d_dst (cap bytes; *len = its length; CE_ERR_INVALID_ARG, nothing written, when
+ * cap < *len -- grow and call again), and ce_core_merge_state of a StateWrapper resident in HBM
+ * (d_sw, len bytes).  Orswot states are written and read by the device serializer / state
+ * reader (only the head and the deferred tail reach the host); the small VClock, GCounter and
+ * MVReg states are serialized / parsed on the host and copied. */
+int ce_core_state_bytes_device(ce_core *c, uint8_t *d_dst, uint64_t cap, uint64_t *len);
+int ce_core_merge_state_device(ce_core *c, const uint8_t *d_sw, uint64_t len);
 
 /* Dense state exchange for multi-GPU merges (one process per GPU): actors registered in the
  * same order on every rank get the same dense index.  export copies the dense state counters

@@ -613,3 +613,71 @@ def test_orswot_op_fast_path_boundaries(ctx, case):
     core, oc = new_core(ctx, "orswot", key), C.Core("orswot")
     check_ops(ctx, "orswot", key, core, oc, actors, clears, fa, fv)
     core.close()
+
+
+@pytest.mark.parametrize("kind", ["orswot", "mvreg", "gcounter"])
+def test_state_bytes_and_merge_device(ctx, kind):
+    """The dot-set exchange without a host hop (shard.reduce_dotset): ce_core_state_bytes_device
+    writes exactly ce_core_state_bytes into HBM (straight from the device writer, and through the
+    grow-and-retry path when the buffer is short), and ce_core_merge_state_device of those bytes
+    == ce_core_merge_state of the host copy == the oracle's merge, deferred removals included."""
+    import torch
+    rng = random.Random(31 if kind != "mvreg" else 32)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 12)
+    dev = torch.device("cuda", 0)
+    okind = "orswot" if kind == "gcounter" else kind
+    hist = gen(okind, rng, actors, 3, 8, 400, True)
+    halves = [{a: hist[a] for a in actors[:6]}, {a: hist[a] for a in actors[6:]}]
+    parts = []
+    for h in halves:
+        if kind == "gcounter":
+            core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+            core.set_latest_key(key)
+            acts = list(h)
+            clears, fa, fv = [], [], []
+            for i, a in enumerate(acts):
+                for v in range(3):
+                    dots = [{"actor": rng.choice(actors), "counter": rng.getrandbits(40) + 1} for _ in range(9)]
+                    clears.append(APP + msgpack.packb(dots, use_bin_type=True))
+                    fa.append(i)
+                    fv.append(v)
+            assert core.ingest_ops(seal_files(ctx, key, clears), acts, fa, fv)[0] == 0
+        else:
+            core = new_core(ctx, okind, key)
+            acts, clears, fa, fv = G.batch(h, okind, APP)
+            assert core.ingest_ops(seal_files(ctx, key, clears), acts, fa, fv)[0] == 0
+        parts.append(core)
+    a, b = parts
+    want_b = b.state_bytes()
+    buf = torch.zeros(len(want_b) + 4096, dtype=torch.uint8, device=dev)
+    rc, n = b.state_bytes_device(buf.data_ptr(), buf.numel())
+    assert rc == 0 and n == len(want_b)
+    torch.cuda.synchronize()
+    assert bytes(buf[:n].cpu().numpy().tobytes()) == want_b
+    small = torch.zeros(16, dtype=torch.uint8, device=dev)
+    rc, n2 = b.state_bytes_device(small.data_ptr(), small.numel())
+    assert rc == 64 and n2 == len(want_b)
+    # the host merge on a copy of a's state, then the device merge into a
+    ref = crdtenc.Core(ctx, kind=a_kind(kind), supported=[APP], current_data_version=APP)
+    assert ref.merge_state(a.state_bytes()) == 0 and ref.merge_state(want_b) == 0
+    assert a.merge_state_device(buf.data_ptr(), n) == 0
+    assert a.state_bytes() == ref.state_bytes()
+    if kind != "gcounter":
+        oc = C.Core(okind)
+        oc2 = C.Core(okind)
+        for h, o in zip(halves, (oc, oc2)):
+            acts, clears, fa, fv = G.batch(h, okind, APP)
+            assert o.read_remote_ops(key, [APP], seal_files(ctx, key, clears), [acts[i] for i in fa], fv)[0] == 0
+        assert oc2.serialize() == want_b
+        sf = seal_states(ctx, key, [oc2.serialize()])
+        assert oc.read_remote_states(key, [APP], sf)[0] == 0
+        assert a.state_bytes() == oc.serialize()
+    if kind == "orswot":
+        assert a.path_count("states_device_read") == 1
+    for x in (a, b, ref):
+        x.close()
+
+
+def a_kind(kind):
+    return {"orswot": crdtenc.STATE_ORSWOT, "mvreg": crdtenc.STATE_MVREG, "gcounter": crdtenc.STATE_GCOUNTER}[kind]
