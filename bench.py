@@ -252,11 +252,14 @@ def launch_ranks(args):
 class Workload:
     """One variant's sealed batch on this rank, its core and its step function."""
 
-    def __init__(self, ctx, variant, args, world, rank, dev, actors_all):
+    def __init__(self, ctx, variant, args, world, rank, dev, actors_all, scaling="weak"):
         self.variant = variant
         self.world, self.rank = world, rank
         self.actors_all = actors_all
-        self.versions = args.versions * world                  # weak scaling: 1M files per GPU
+        self.scaling = scaling
+        # weak scaling: 1M files per GPU (the job grows with N); strong: the one 1M-file job split
+        # over the N ranks
+        self.versions = args.versions * (world if scaling == "weak" else 1)
         self.key = bytes(np.random.default_rng(7).integers(0, 256, 32, dtype=np.uint8))
         # N > 1: files partitioned by address (shard.ingest_sharded), every writer on every rank;
         # --partition actor: the previous writer-sharded layout (shard.exchange_vclock)
@@ -547,6 +550,9 @@ def main():
     ap.add_argument("--configs", default="c3,c4,c5",
                     help="N=1: also run these BASELINE configs (bench_configs.py runners) and report "
                          "them under the line's `configs` key ('' = none)")
+    ap.add_argument("--no-strong", action="store_true", help="N > 1: skip the strong-scaling C2 leg")
+    ap.add_argument("--quick", action="store_true",
+                    help="tests: the configs at small sizes, 2 timed steps each (never a reported line)")
     ap.add_argument("--partition", choices=("address", "actor"), default="address",
                     help="N > 1: op files by address hash with the cross-rank gate (default), or "
                          "whole writers per rank")
@@ -609,25 +615,44 @@ def main():
         wb.close()
         del wb
 
-    # the other BASELINE configs (C3 Orswot, C4 skewed sizes, C5 key-rotation mix) on this GPU,
-    # each timed and checked by bench_configs.py's runner -- reported beside the C2 line, never
-    # its value
+    # N > 1: the same 1M-file C2 job split over the N ranks (strong scaling), beside the weak line
+    strong = None
+    if world > 1 and not args.no_strong:
+        ws = Workload(ctx, "a", args, world, rank, dev, actors_all, scaling="strong")
+        ms_s, kern_s, ok_s = ws.run(ctx, args.steps, args.warmup)
+        ok = ok and ok_s
+        ss = kernel_summary(ws, ms_s, kern_s)
+        n_max = torch.tensor([ws.n], dtype=torch.int64, device=dev)
+        shard.all_reduce_(n_max, dist.ReduceOp.MAX)
+        strong = dict(ss, scaling="strong", files_total=ws.total_files, files_per_gpu_max=int(n_max.item()),
+                      workload="C2: the one 1,048,576 x 4 KiB GCounter job (4096 actors x %d versions) "
+                               "partitioned by address over %d ranks" % (args.versions, world),
+                      exchange_paths=sorted(ws.paths),
+                      state_check="closed-form StateWrapper bytes: %s" % ("ok" if ok_s else "MISMATCH"))
+        ws.close()
+        del ws
+
+    # the other BASELINE configs (C3 Orswot, C4 skewed sizes, C5 key-rotation mix), each timed
+    # and checked by bench_configs.py's runner -- reported beside the C2 line, never its value.
+    # N = 1: on this GPU; N > 1: strong scaling over the ranks (bench_configs.run_config)
     configs = None
-    if world == 1 and args.configs:
+    if args.configs:
         import bench_configs
         configs = {}
         for c in [x for x in args.configs.split(",") if x]:
             # C3: 40 steps, so the ~48 ms SHA3 of the last step's 35 MB file weighs ~1 ms a step
             steps_c = {"c3": 40, "c4": 10, "c5": 10}[c]
+            extra = {"c3": ["--versions", "2", "--state-versions", "1"], "c4": ["--c4-versions", "2"],
+                     "c5": ["--c5-versions", "4"]}[c] if args.quick else []
             ns = bench_configs.make_parser().parse_args(
-                ["--config", c, "--steps", str(steps_c), "--warmup", "1", "--no-clock"] +
-                (["--no-cpu"] if args.no_cpu else []))
+                ["--config", c, "--steps", str(2 if args.quick else steps_c), "--warmup", "1", "--no-clock"] +
+                (["--no-cpu"] if args.no_cpu else []) + extra)
             t_c = time.time()
-            line_c = bench_configs.RUNNERS[c](ns, ctx, dev)
+            line_c = bench_configs.run_config(c, ns, ctx, dev, world, rank)
             line_c["wall_s"] = round(time.time() - t_c, 1)
             good = all(bool(v) for v in line_c.get("checks", {}).values()) and (
                 line_c.get("cpu_baseline") is None or line_c["cpu_baseline"].get("same_result_as_gpu", True))
-            if not good:
+            if not good and "skipped" not in line_c:
                 log("CONFIG %s CHECK FAILED: %s" % (c, line_c.get("checks")))
                 ok = False
             configs[c] = line_c
@@ -716,6 +741,7 @@ def main():
             "kernels_ms_per_step": sa["kernels_ms_per_step"],
             "state_check": "closed-form StateWrapper bytes: %s" % ("ok" if ok else "MISMATCH"),
             "variant_b": vb,
+            "strong": strong,
             "host_buffers": hostbuf,
             "cpu_baseline": cpu,
             "configs": configs,

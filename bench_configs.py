@@ -629,6 +629,418 @@ def run_c5(args, ctx, dev):
     return line
 
 
+# ---------------------------------------------------------------------------------------------
+# N > 1 ranks (one process per GPU, torch.distributed; bench.py --gpus N runs these under its
+# `configs` key).  Strong scaling: the config's whole workload is split across the ranks, and
+# value = the job's files / the max-over-ranks step time.
+# ---------------------------------------------------------------------------------------------
+
+def _dist():
+    import torch.distributed as dist
+    import shard
+    return dist, shard
+
+
+def _comm_device(dev):
+    dist, _ = _dist()
+    return "cpu" if dist.get_backend() == "gloo" else dev
+
+
+def _max_over_ranks(x, dev):
+    dist, shard = _dist()
+    t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
+    shard.all_reduce_(t, dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def _all_true(ok, dev):
+    dist, shard = _dist()
+    t = torch.tensor([1 if ok else 0], dtype=torch.int64, device=dev)
+    shard.all_reduce_(t, dist.ReduceOp.MIN)
+    return int(t.item()) == 1
+
+
+def _timed_steps(step, steps, warmup, dev, drain=None):
+    """warmup, then `steps` steps bracketed by barrier + synchronize; the max over ranks (ms)"""
+    dist, _ = _dist()
+    for _ in range(warmup):
+        step()
+    if drain:
+        drain()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    if drain:
+        drain()
+    torch.cuda.synchronize()
+    dist.barrier()
+    return _max_over_ranks((time.perf_counter() - t0) * 1e3 / steps, dev)
+
+
+def _state_files_c3(ctx, key, actors, V0, dev, which):
+    """C3's state files j in `which`: the ingest-readable compaction of writers [512 j, 512 (j+1))'s
+    versions [0, V0) (as run_c3 builds them)"""
+    per = N_ACTORS // 8
+    out = {}
+    for j in which:
+        f, o, n, bl, fa, fv = seal_op_files(ctx, key, actors, j * per, (j + 1) * per, 0, V0, dev, 99 + j)
+        sc = new_core(ctx, key, flags=crdtenc.COMPACT_INGEST_FORMAT)
+        rc = sc.ingest_ops_device(f.data_ptr(), o.data_ptr(), n, bl,
+                                  b"".join(bytes(a) for a in actors[j * per:(j + 1) * per]),
+                                  fa.data_ptr(), fv.data_ptr())
+        if rc:
+            raise crdtenc.CeError(rc, ctx.last_error())
+        out[j] = sc.compact_to_buffer(nonce=bytes(24))[0]
+        sc.close()
+    return out
+
+
+def run_c3_multi(args, ctx, dev, world, rank):
+    """C3 over N ranks: rank r holds the writers shard.actor_range(4096, N, r) -- their op files
+    and the state files of their 512-writer groups -- and folds them (read_remote_states, then
+    read_remote_ops; crdt-enc/src/lib.rs:401-547); the partial StateWrappers then meet along the
+    binomial tree of shard.reduce_dotset, in HBM end to end (device writer -> send/recv -> device
+    state reader + merge, lib.rs:446-466), and rank 0 compacts (lib.rs:332-380).  Checks: rank 0's
+    state == the single-core fold of every file (built on rank 0 after the timed steps) and the
+    closed-form clock."""
+    dist, shard = _dist()
+    if 8 % world:
+        return {"skipped": "C3's 8 state files are 512-writer groups: N must divide 8", "n_gpus": world}
+    actors = actors_table()
+    key = KEY
+    V0, V = args.state_versions, args.versions
+    lo, hi = shard.actor_range(N_ACTORS, world, rank)
+    per = N_ACTORS // 8
+    t0 = time.time()
+    mine = [j for j in range(8) if lo <= j * per < hi]
+    states = _state_files_c3(ctx, key, actors, V0, dev, mine)
+    my_states = [states[j] for j in mine]
+    files, offs, n, blob_len, fa, fv = seal_op_files(ctx, key, actors, lo, hi, V0, V0 + V, dev, 1234 + rank)
+    writers = b"".join(bytes(a) for a in actors[lo:hi])
+    log("c3 rank %d: writers [%d, %d), %d state files, %d op files in %.1f s" % (
+        rank, lo, hi, len(my_states), n, time.time() - t0))
+    core = new_core(ctx, key)
+    core.register_actors([bytes(a) for a in actors])
+    comm = _comm_device(dev)
+    buf = shard.StateBuffer(dev)
+    hops, timing_on = [], [False]
+    from concurrent.futures import ThreadPoolExecutor
+    NB = 13
+    namer = ThreadPoolExecutor(NB - 1) if rank == 0 else None
+    names = []
+    obuf = [torch.zeros(1 << 26, dtype=torch.uint8, pin_memory=True).numpy() for _ in range(NB)] if rank == 0 else None
+    out = {}
+    phase = {"states": 0.0, "ops": 0.0, "reduce": 0.0, "compact": 0.0}
+
+    def step():
+        t_a = time.perf_counter()
+        core.reset()
+        if my_states:
+            rc, _ = core.ingest_states_iov(my_states)
+            if rc:
+                raise crdtenc.CeError(rc, ctx.last_error())
+        t_b = time.perf_counter()
+
+        def ingest():
+            return core.ingest_ops_device(files.data_ptr(), offs.data_ptr(), n, blob_len, writers,
+                                          fa.data_ptr(), fv.data_ptr())
+        t_c = [0.0]
+
+        def ingest_timed():
+            r = ingest()
+            t_c[0] = time.perf_counter()
+            return r
+        rc, _ = shard.ingest_dotset_sharded(core, ingest_timed, device=comm, snapshot=False, buf=buf,
+                                            timing=hops if timing_on[0] else None)
+        if rc:
+            raise crdtenc.CeError(rc, "sharded C3 ingest")
+        t_d = time.perf_counter()
+        if rank == 0:
+            k = len(names) % NB
+            if len(names) >= NB:
+                names[-NB].result()
+            obuf[k], ln, _ = core.compact_into(obuf[k], name=False)
+            out["file"] = obuf[k][:ln]
+            names.append(namer.submit(crdtenc.content_name, out["file"]))
+        t_e = time.perf_counter()
+        if timing_on[0]:
+            for key_, a_, b_ in (("states", t_a, t_b), ("ops", t_b, t_c[0]), ("reduce", t_c[0], t_d),
+                                 ("compact", t_d, t_e)):
+                phase[key_] += (b_ - a_) * 1e3
+
+    def drain():
+        for fu in names:
+            out["name"] = fu.result()
+        names.clear()
+
+    for _ in range(args.warmup):
+        step()
+    drain()
+    timing_on[0] = True
+    ctx.timing_reset()
+    ctx.set_timing(True)
+    ms = _timed_steps(step, args.steps, 0, dev, drain=drain)
+    ctx.set_timing(False)
+    timing_on[0] = False
+    k_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in
+            ((k, ctx.timing(k)) for k in ("open_setup", "open_small", "segments_open", "gate", "ds_count",
+                                         "ds_emit", "ds_applied", "ds_add_pairs", "ds_kill", "ds_finalize",
+                                         "ds_merge", "seal_setup", "segments_seal")) if v[1]}
+    # per-hop exchange figures: mean over the timed steps on each rank, max over ranks
+    def mean(key_):
+        v = [h[key_] for h in hops if key_ in h]
+        return sum(v) / len(v) if v else 0.0
+    hop = {k: round(_max_over_ranks(mean(k), dev), 3) for k in ("serialize_ms", "send_ms", "recv_ms", "merge_ms")}
+    hop_bytes = int(_max_over_ranks(max([h["bytes"] for h in hops] or [0]), dev))
+    tot = torch.tensor([n + len(my_states)], dtype=torch.int64, device=dev)
+    shard.all_reduce_(tot, dist.ReduceOp.SUM)
+    n_total = int(tot.item())
+    ok_clock = ok_whole = True
+    entries = None
+    if rank == 0:
+        import msgpack
+        sb = core.state_bytes()
+        d = msgpack.unpackb(sb, raw=True, strict_map_key=False)
+        clock = d[b"state"][b"clock"][b"dots"]
+        ok_clock = len(clock) == N_ACTORS and all(c == N_ADD * (V0 + V) for c in clock.values())
+        entries = len(d[b"state"][b"entries"])
+        # the single-core fold of every file, untimed
+        all_states = _state_files_c3(ctx, key, actors, V0, dev, range(8))
+        fw, ow, nw, bw, faw, fvw = seal_op_files(ctx, key, actors, 0, N_ACTORS, V0, V0 + V, dev, 4321)
+        whole = new_core(ctx, key)
+        assert whole.ingest_states([all_states[j] for j in range(8)])[0] == 0
+        rc = whole.ingest_ops_device(fw.data_ptr(), ow.data_ptr(), nw, bw, b"".join(bytes(a) for a in actors),
+                                     faw.data_ptr(), fvw.data_ptr())
+        ok_whole = rc == 0 and whole.state_bytes() == sb
+        whole.close()
+        del fw
+        namer.shutdown()
+    ok_clock, ok_whole = _all_true(ok_clock, dev), _all_true(ok_whole, dev)
+    line = {
+        "metric": "C3 op+state files compacted/sec (Orswot<u64,Uuid>)",
+        "value": round(n_total / (ms / 1e3), 1), "unit": "files/s", "n_gpus": world, "scaling": "strong",
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+        "higher_is_better": True, "dtype": "u32/u64", "data": "synthetic (GPU-sealed, seeded)",
+        "config": {"workload": "C3: Orswot, %d members, %d actors; 8 state files (512 actors x %d versions "
+                               "each) + %d op files (4096 x %d versions, 26 Add + 6 Rm, %d B), split over %d "
+                               "ranks by writer" % (N_MEMBERS, N_ACTORS, V0, N_ACTORS * V, V, PT_LEN, world),
+                   "files_total": n_total, "entries": entries,
+                   "parallelism": "writer shards (shard.actor_range) with their 512-writer state groups; "
+                                  "statuses all_reduce(MAX); partial StateWrappers reduced along a binomial "
+                                  "tree to rank 0 in HBM (ce_core_state_bytes_device -> %s send/recv -> "
+                                  "ce_core_merge_state_device); compaction + content name on rank 0"
+                                  % ("RCCL" if comm != "cpu" else "gloo (host-staged)")},
+        "exchange": {"hops_per_step": world - 1, "tree_depth": (world - 1).bit_length(),
+                     "max_state_bytes_per_hop": hop_bytes, "per_hop_ms_max_over_ranks": hop},
+        "kernels_ms_per_step_rank0": k_ms,
+        "phases_ms_per_step_rank0": {k: round(v / args.steps, 3) for k, v in phase.items()},
+        "checks": {"closed_form_clock": ok_clock, "equals_single_core_fold": ok_whole},
+    }
+    core.close()
+    return line
+
+
+def _c4_sizes(args):
+    """C4's file table (run_c4): per (actor, version) Dot counts, plaintext and file lengths, and
+    each file's first counter (65536 + the actor's Dots in earlier versions)"""
+    rng = np.random.default_rng(404)
+    m, V = N_ACTORS // 4, args.c4_versions
+    size = np.exp(rng.uniform(np.log(256), np.log(1 << 20), size=(m, V))).astype(np.int64)
+    kd = np.maximum(1, (size - 19) // 38)
+    ctr0 = 65536 + np.cumsum(kd, axis=1) - kd
+    pt = np.array([16 + (1 if k <= 15 else 3 if k <= 0xffff else 5) + 38 * int(k) for k in kd.ravel()], np.int64)
+    fl = np.array([16 + crdtenc.sealed_len(int(x)) for x in pt], np.int64)
+    return kd, ctr0, pt, fl
+
+
+def _seal_selected(ctx, key, sel, make_clear, f_len, dev, seed):
+    """Seal the files `sel` (global indices, ascending) back to back: make_clear(i) -> plaintext,
+    f_len[i] = its sealed size.  Returns (files, offs i64[n+1] on dev, n, blob_len)."""
+    n = len(sel)
+    offs_h = np.zeros(n + 1, np.int64)
+    offs_h[1:] = np.cumsum(f_len[sel]) if n else []
+    blob_len = int(offs_h[-1])
+    files = torch.empty(blob_len + 64, dtype=torch.uint8, device=dev)
+    gen = np.random.default_rng(seed)
+    i = 0
+    while i < n:
+        j, tot, parts, coffs = i, 0, [], [0]
+        while j < n and (j == i or tot <= (1 << 28)):   # ~256 MB of plaintext per launch
+            c = make_clear(int(sel[j]))
+            parts.append(c)
+            coffs.append(coffs[-1] + len(c))
+            tot += len(c)
+            j += 1
+        clear = torch.from_numpy(np.frombuffer(b"".join(parts), np.uint8).copy()).to(dev)
+        co = torch.tensor(coffs, dtype=torch.int64, device=dev)
+        nonces = torch.from_numpy(gen.integers(0, 256, (j - i, 24), dtype=np.uint8)).to(dev)
+        oo = torch.from_numpy(offs_h[i:j].copy()).to(dev)
+        torch.cuda.current_stream().synchronize()
+        ctx.encrypt_batch_device(key, clear.data_ptr(), co.data_ptr(), j - i, nonces.data_ptr(),
+                                 files.data_ptr(), oo.data_ptr(), outer_version=CORE)
+        ctx.synchronize()
+        i = j
+    return files, torch.from_numpy(offs_h).to(dev), n, blob_len
+
+
+def run_c4_multi(args, ctx, dev, world, rank):
+    """C4 over N ranks: the skewed-size op files partitioned by address (shard.ingest_sharded:
+    cross-rank version gate, pending fold, one all_reduce(MAX) of the dense batch; lib.rs:516-544),
+    rank 0 compacts.  Check: every rank's StateWrapper == the closed form."""
+    import msgpack
+    dist, shard = _dist()
+    actors = actors_table()[::4]
+    m, V = actors.shape[0], args.c4_versions
+    kd, ctr0, pt, fl = _c4_sizes(args)
+    fa_all = np.repeat(np.arange(m, dtype=np.uint32), V)
+    fv_all = np.tile(np.arange(V, dtype=np.uint64), m)
+    own = crdtenc.shard_owners([bytes(a) for a in actors], fa_all, fv_all, world)
+    sel = np.nonzero(own == rank)[0]
+    t0 = time.time()
+    files, offs, n, blob_len = _seal_selected(
+        ctx, KEY, sel, lambda f: dots_plaintext(actors[f // V], int(kd.ravel()[f]), int(ctr0.ravel()[f])),
+        fl, dev, 405 + rank)
+    fa = torch.from_numpy(fa_all[sel].astype(np.int32)).to(dev)
+    fv = torch.from_numpy(fv_all[sel].astype(np.int64)).to(dev)
+    log("c4 rank %d: %d of %d files (%.2f GB) in %.1f s" % (rank, n, m * V, blob_len / 1e9, time.time() - t0))
+    core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+    core.set_latest_key(KEY)
+    core.register_actors([bytes(a) for a in actors])
+    ops = shard.DeviceShardOps(core, b"".join(bytes(a) for a in actors), files, offs, n, blob_len, fa, fv)
+    paths = set()
+
+    def step():
+        core.reset()
+        rc, path = shard.ingest_sharded(ops)
+        if rc:
+            raise crdtenc.CeError(rc, "sharded C4 ingest " + ctx.last_error())
+        paths.add(path)
+        if rank == 0:
+            core.compact_to_buffer(name=False)
+
+    ctx.timing_reset()
+    ctx.set_timing(True)
+    ms = _timed_steps(step, args.steps, args.warmup, dev)
+    ctx.set_timing(False)
+    k_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in
+            ((k, ctx.timing(k)) for k in ("open_setup", "gate", "open_fold_small", "segments_open",
+                                         "finalize_open", "decode")) if v[1]}
+    want = msgpack.packb({"next_op_versions": {"dots": {bytes(a): V for a in actors}},
+                          "state": {"inner": {"dots": {bytes(actors[a]): 65536 + int(kd[a].sum())
+                                                       for a in range(m)}}}}, use_bin_type=True)
+    ok = _all_true(core.state_bytes() == want, dev)
+    ct = int(pt.sum())
+    line = {
+        "metric": "C4 skewed-size op files compacted/sec + AEAD GB/s (GCounter, 256 B-1 MiB)",
+        "value": round(m * V / (ms / 1e3), 1), "unit": "files/s", "n_gpus": world, "scaling": "strong",
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+        "higher_is_better": True, "dtype": "u32", "data": "synthetic (GPU-sealed, seeded)",
+        "config": {"workload": "C4: %d GCounter op files (%d actors x %d versions), plaintext log-uniform on "
+                               "[256 B, 1 MiB], %.2f GB, partitioned by address over %d ranks"
+                               % (m * V, m, V, ct / 1e9, world),
+                   "files_this_rank0": n if rank == 0 else None,
+                   "parallelism": "op files by address hash (ce_shard_owner), cross-rank version gate "
+                                  "(stats all_reduce MAX), pending batch + flags all_reduce(MAX), exchange "
+                                  "path %s; compaction on rank 0" % "/".join(sorted(paths))},
+        "aead_GBps_end_to_end": round(ct / (ms / 1e3) / 1e9, 1),
+        "kernels_ms_per_step_rank0": k_ms,
+        "checks": {"closed_form_state_every_rank": ok},
+    }
+    core.close()
+    return line
+
+
+def run_c5_multi(args, ctx, dev, world, rank):
+    """C5 over N ranks: the key-rotation batch partitioned by address; one tampered or second-key
+    file anywhere rejects the whole batch on every rank (lib.rs:497-516) and no state changes.
+    Checks: every rank returns AUTH, every rank's per-file statuses == expected, state unchanged."""
+    dist, shard = _dist()
+    sys.path.insert(0, REPO)
+    import bench
+    actors = bench.actors_table()
+    key1 = bytes(np.random.default_rng(8).integers(0, 256, 32, dtype=np.uint8))
+    V = args.c5_versions
+    ev, od = np.ascontiguousarray(actors[0::2]), np.ascontiguousarray(actors[1::2])
+    writers = np.concatenate([ev, od])
+    mw = writers.shape[0]
+    fa_all = np.repeat(np.arange(mw, dtype=np.int64), V)
+    fv_all = np.tile(np.arange(V, dtype=np.int64), mw)
+    n_all = mw * V
+    own = crdtenc.shard_owners([bytes(a) for a in writers], fa_all.astype(np.uint32), fv_all.astype(np.uint64), world)
+    sel = np.nonzero(own == rank)[0]
+    half = mw // 2
+    se, so = sel[fa_all[sel] < half], sel[fa_all[sel] >= half]
+    t0 = time.time()
+    f0, o0, n0, l0, _ = bench.build_files(ctx, KEY, ev, actors, V, dev, seed=1234 + rank,
+                                          fa=fa_all[se], fv=fv_all[se])
+    f1, o1, n1, l1, _ = bench.build_files(ctx, KEY if args.c5_clean else key1, od, actors, V, dev,
+                                          seed=5678 + rank, fa=fa_all[so] - half, fv=fv_all[so])
+    n = n0 + n1
+    files = torch.cat([f0[:l0], f1[:l1], torch.zeros(64, dtype=torch.uint8, device=dev)])
+    del f0, f1
+    offs = torch.cat([o0[:n0], o1 + l0])
+    blob_len = l0 + l1
+    flen = l0 // max(n0, 1) if n0 else l1 // max(n1, 1)
+    rng = np.random.default_rng(506)
+    tam = np.sort(rng.choice(n_all, size=0 if args.c5_clean else n_all // 1000, replace=False))
+    loc = np.concatenate([se, so])               # global index of each local file
+    hit = np.nonzero(np.isin(loc, tam))[0]
+    if len(hit):
+        files[torch.from_numpy((hit + 1) * flen - 1).to(dev)] ^= 1
+    want = np.zeros(n, np.int32)
+    if not args.c5_clean:
+        want[n0:] = 9
+    want[hit] = 9
+    fa = torch.from_numpy(fa_all[loc].astype(np.int32)).to(dev)
+    fv = torch.from_numpy(fv_all[loc]).to(dev)
+    log("c5 rank %d: %d of %d files (%d second-key, %d tampered) in %.1f s" % (
+        rank, n, n_all, n1, len(hit), time.time() - t0))
+    core = crdtenc.Core(ctx, kind=crdtenc.STATE_GCOUNTER, supported=[APP], current_data_version=APP)
+    core.set_latest_key(KEY)
+    core.register_actors([bytes(a) for a in writers])
+    empty = core.state_bytes()
+    ops = shard.DeviceShardOps(core, b"".join(bytes(a) for a in writers), files, offs, n, blob_len, fa, fv)
+    res = {}
+
+    def step():
+        core.reset()
+        res["rc"], res["path"] = shard.ingest_sharded(ops)
+
+    ctx.timing_reset()
+    ctx.set_timing(True)
+    ms = _timed_steps(step, args.steps, args.warmup, dev)
+    ctx.set_timing(False)
+    k_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in
+            ((k, ctx.timing(k)) for k in ("open_setup", "gate", "open_fold_small")) if v[1]}
+    ops.want_status = True      # untimed: the statuses of this rank's files
+    core.reset()
+    rc2, path2 = shard.ingest_sharded(ops)
+    ops.want_status = False
+    st = np.array(ops.status, np.int32) if ops.status is not None else np.zeros(0, np.int32)
+    exp_rc = 0 if args.c5_clean else 9
+    checks = {"batch_rejected_every_rank": _all_true(res["rc"] == exp_rc and rc2 == exp_rc, dev),
+              "statuses_match_every_rank": _all_true(len(st) == n and bool((st == want).all()), dev),
+              "state_unchanged_every_rank": _all_true((core.state_bytes() == empty) != args.c5_clean, dev)}
+    line = {
+        "metric": "C5 key-rotation mix: op files verified/sec on the reject path",
+        "value": round(n_all / (ms / 1e3), 1), "unit": "files/s", "n_gpus": world, "scaling": "strong",
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+        "higher_is_better": True, "dtype": "u32", "data": "synthetic (GPU-sealed, seeded)",
+        "config": {"workload": "C5: %d x 4 KiB GCounter op files, 4096 actors; odd actors' files under a second "
+                               "data key, %d files with a flipped tag bit; latest key only; partitioned by "
+                               "address over %d ranks" % (n_all, len(tam), world),
+                   "path": res.get("path"),
+                   "parallelism": "op files by address hash; each rank opens its share; the failure status "
+                                  "meets in the dense batch's all_reduce(MAX), so every rank rejects"},
+        "kernels_ms_per_step_rank0": k_ms,
+        "checks": checks,
+    }
+    core.close()
+    return line
+
+
 def make_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3", choices=["c3", "c4", "c5"])
@@ -649,6 +1061,15 @@ def make_parser():
 
 
 RUNNERS = {"c3": run_c3, "c4": run_c4, "c5": run_c5}
+RUNNERS_MULTI = {"c3": run_c3_multi, "c4": run_c4_multi, "c5": run_c5_multi}
+
+
+def run_config(name, args, ctx, dev, world=1, rank=0):
+    """One config on this rank: the single-GPU runner at N = 1, the strong-scaling one at N > 1
+    (every rank calls it; the line is complete on rank 0)."""
+    if world == 1:
+        return RUNNERS[name](args, ctx, dev)
+    return RUNNERS_MULTI[name](args, ctx, dev, world, rank)
 
 
 def main():

@@ -314,6 +314,8 @@ class DeviceShardOps:
     def __init__(self, core, actors, files, offs, n, blob_len, fa, fv):
         self.core, self.actors = core, actors
         self.files, self.offs, self.n, self.blob_len, self.fa, self.fv = files, offs, n, blob_len, fa, fv
+        self.want_status = False   # True: ingest() keeps the per-file statuses in self.status
+        self.status = None
         self.m = len(actors) // 16
         self.device = fa.device
         self.stats = torch.empty(2 * self.m + 3, dtype=torch.int64, device=self.device)
@@ -350,9 +352,13 @@ class DeviceShardOps:
         return self.core.writer_versions(self.actors)
 
     def ingest(self):
-        return self.core.ingest_ops_device_sharded(self.files.data_ptr(), self.offs.data_ptr(), self.n,
-                                                   self.blob_len, self.actors, self.fa.data_ptr(),
-                                                   self.fv.data_ptr(), self.hi.data_ptr())
+        r = self.core.ingest_ops_device_sharded(self.files.data_ptr(), self.offs.data_ptr(), self.n,
+                                                self.blob_len, self.actors, self.fa.data_ptr(),
+                                                self.fv.data_ptr(), self.hi.data_ptr(),
+                                                want_status=self.want_status)
+        if self.want_status:
+            r, self.status = r
+        return r
 
     def dense_buffer(self):
         self.dense.zero_()

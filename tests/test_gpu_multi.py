@@ -25,16 +25,28 @@ def _port():
 
 
 def test_bench_two_ranks_share_gpu():
+    """bench.py --gpus 2 as the driver's scaling run would start it (here: gloo, both ranks on
+    the one GPU): the weak C2 line, the strong C2 leg, and C3 / C4 / C5 at N = 2 under `configs`,
+    each with every check true (small sizes: --quick)."""
     env = dict(os.environ, CE_BENCH_SHARE_GPU="1", CE_DIST_BACKEND="gloo")
     env.pop("WORLD_SIZE", None)
     p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--versions",
-                        "2", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-variant-b"],
-                       env=env, capture_output=True, timeout=240)
-    assert p.returncode == 0, p.stderr.decode()[-2000:]
+                        "2", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-variant-b", "--quick"],
+                       env=env, capture_output=True, timeout=400)
+    assert p.returncode == 0, p.stderr.decode()[-3000:]
     line = json.loads(p.stdout.decode().strip().splitlines()[-1])
     assert line["n_gpus"] == 2 and line["state_check"].endswith("ok")
     assert line["config"]["files_per_gpu"] == 4096 * 2
     assert "dense" in line["config"]["parallelism"]
+    st = line["strong"]
+    assert st["scaling"] == "strong" and st["state_check"].endswith("ok") and st["files_total"] == 4096 * 2
+    for c in ("c3", "c4", "c5"):
+        cl = line["configs"][c]
+        assert cl["n_gpus"] == 2 and cl["scaling"] == "strong", (c, cl)
+        assert cl["checks"] and all(cl["checks"].values()), (c, cl["checks"])
+    assert line["configs"]["c3"]["exchange"]["hops_per_step"] == 1
+    assert line["configs"]["c3"]["exchange"]["max_state_bytes_per_hop"] > 0
+    assert line["configs"]["c5"]["config"]["path"] == "rejected"
 
 
 @pytest.mark.parametrize("mode,path", [("registered", "dense"), ("unregistered", "bytes")])
