@@ -5,7 +5,8 @@
                 8 state files (each the compaction of 512 actors' first V0 versions) then
                 4096 x V op files of 32 ops (26 Add + 6 Rm, 1961 B plaintext); one step =
                 reset + read_remote_states + read_remote_ops + compact (crdt-enc/src/lib.rs:
-                332-547) with the op files resident in HBM and the state files on the host.
+                332-547) with the op and state files resident in HBM (the line's
+                `states_from_host` times the state files staged from host buffers instead).
 
   --config c4   skewed sizes: 1024 actors x 32 versions of GCounter op files whose plaintexts are
                 log-uniform on [256 B, 1 MiB] (~4 GB, the C2 byte volume): single-page files take
@@ -17,6 +18,9 @@
                 bit.  One step = reset + read_remote_ops with per-file statuses under the latest
                 key (key_cryptor.rs:59-70): every second-key and tampered file must be rejected
                 (CE_ERR_AUTH), every other file accepted, and nothing folded (lib.rs:497-516).
+
+With N > 1 ranks (bench.py --gpus N) every config runs strong-scaled over the ranks
+(run_config -> run_c*_multi below).
 
 Prints one JSON line per run.  Checks (size-independent): the merged clock equals its closed
 form (actor a's adds count 26 per version), and an actor-sharded fold of the same files merged
@@ -131,6 +135,72 @@ def seal_op_files(ctx, key, actors, a_lo, a_hi, v_lo, v_hi, dev, seed):
     return files, offs, n, n * flen, fa, fv
 
 
+class CompactPipe:
+    """Pipelined Core::compact outputs (C3): NB pinned buffers; each file's download is left in
+    flight on the copy stream (ce_core_compact_into_async) while the next step runs on the
+    device, then its SHA3-256 name (crdt-enc-tokio/src/lib.rs:403-432, a sequential sponge, ~48 ms
+    for 35 MB) is hashed on NB - 1 host threads.  flush() completes every download, drain() every
+    name; a buffer is reused only after its name is done."""
+
+    def __init__(self, core, nb=13, use_async=True):
+        from concurrent.futures import ThreadPoolExecutor
+        self.core, self.nb, self.use_async = core, nb, use_async
+        self.namer = ThreadPoolExecutor(nb - 1)
+        self.obuf = [torch.zeros(1 << 26, dtype=torch.uint8, pin_memory=True).numpy() for _ in range(nb)]
+        self.fut = [None] * nb
+        self.inflight = []      # (buffer, length, ticket) of downloads not yet waited for
+        self.order = []         # name futures in step order
+        self.i = 0
+        self.last_file = None
+
+    def _name(self, k, ln, tk):
+        self.core.compact_wait(tk)
+        self.last_file = self.obuf[k][:ln]
+        self.fut[k] = self.namer.submit(crdtenc.content_name, self.last_file)
+        self.order.append(self.fut[k])
+
+    def compact(self):
+        k = self.i % self.nb
+        self.i += 1
+        if self.fut[k] is not None:
+            self.fut[k].result()
+            self.fut[k] = None
+        if self.use_async:
+            ln, tk = self.core.compact_into_async(self.obuf[k])
+        else:
+            self.obuf[k], ln, _ = self.core.compact_into(self.obuf[k], name=False)
+            tk = 0
+        self.inflight.append((k, ln, tk))
+        while len(self.inflight) > 1:       # the previous step's download overlapped this step
+            self._name(*self.inflight.pop(0))
+
+    def flush(self):
+        while self.inflight:
+            self._name(*self.inflight.pop(0))
+
+    def drain(self):
+        self.flush()
+        name = None
+        for fu in self.order:
+            name = fu.result()
+        self.order.clear()
+        return name
+
+    def close(self):
+        self.drain()
+        self.namer.shutdown()
+
+
+def device_blob(files, dev):
+    """files (bytes) back to back in HBM: (u8 tensor with 64 bytes of slack, i64 offsets, length)"""
+    offs = np.zeros(len(files) + 1, np.int64)
+    offs[1:] = np.cumsum([len(f) for f in files])
+    blob = torch.zeros(int(offs[-1]) + 64, dtype=torch.uint8, device=dev)
+    if len(files):
+        blob[: int(offs[-1])] = torch.from_numpy(np.frombuffer(b"".join(files), np.uint8).copy()).to(dev)
+    return blob, torch.from_numpy(offs).to(dev), int(offs[-1])
+
+
 def new_core(ctx, key, flags=0):
     core = crdtenc.Core(ctx, kind=crdtenc.STATE_ORSWOT, supported=[APP], current_data_version=APP,
                         flags=flags)
@@ -227,23 +297,28 @@ def run_c3(args, ctx, dev):
     core = new_core(ctx, key)
     core.register_actors([bytes(a) for a in actors])
     out = {}
+    # the state files resident in HBM like the op files (load_states' result; the bench's inputs
+    # are resident when the timed region starts); `states_from_host` below times them staged
+    # from per-file host buffers instead
+    sdev, soffs, sblob = device_blob(states, dev)
+    host_states = [False]
 
     phase = {"reset": 0.0, "states": 0.0, "ops": 0.0, "compact": 0.0}
-    # the SHA3-256 content name of step i's state file is computed on a host thread while step
-    # i+1 runs (as in bench.py); every name is done before the timed region ends
-    from concurrent.futures import ThreadPoolExecutor
-    # SHA3-256 is a sequential sponge (~0.7 GB/s per core): one 35 MB name takes ~48 ms, about
-    # four steps, so NB - 1 = 12 host threads hash consecutive steps' files side by side
+    # step i's sealed file comes down while step i+1 runs on the device, and its SHA3-256 content
+    # name is computed on host threads (CompactPipe); every download and name is done before the
+    # timed region ends
     NB = 13
-    namer = ThreadPoolExecutor(NB - 1)
-    names = []
-    obuf = [torch.zeros(1 << 26, dtype=torch.uint8, pin_memory=True).numpy() for _ in range(NB)]  # pinned (the 35 MB download is a DMA, not a staged copy), room for the file
+    pipe = CompactPipe(core, NB, use_async=not os.environ.get("CE_C3_SYNC_COMPACT"))
+    obuf = pipe.obuf
 
     def step():
         t = time.perf_counter()
         core.reset()
         t1 = time.perf_counter()
-        rc, st = core.ingest_states_iov(states)   # load_states' per-file buffers, no join
+        if host_states[0]:
+            rc, st = core.ingest_states_iov(states)   # load_states' per-file host buffers, no join
+        else:
+            rc = core.ingest_states_device(sdev.data_ptr(), soffs.data_ptr(), len(states), sblob)
         if rc:
             raise crdtenc.CeError(rc, ctx.last_error())
         t2 = time.perf_counter()
@@ -252,26 +327,14 @@ def run_c3(args, ctx, dev):
         if rc:
             raise crdtenc.CeError(rc, ctx.last_error())
         t3 = time.perf_counter()
-        # NB reused output buffers: NB - 1 namer threads hash the previous steps' files while
-        # this step fills the next buffer (its last hash is awaited before it is written again)
-        k = len(names) % NB
-        if len(names) >= NB:
-            names[-NB].result()
-        obuf[k], ln, _ = core.compact_into(obuf[k], name=False)
-        out["file"] = obuf[k][:ln]
-        t35 = time.perf_counter()
-        names.append(namer.submit(crdtenc.content_name, out["file"]))
+        pipe.compact()
         t4 = time.perf_counter()
-        if HOST_PROF:
-            log("py: compact_to_buffer %.3f ms, submit %.3f ms" % ((t35 - t3) * 1e3, (t4 - t35) * 1e3))
         for k, a, b in (("reset", t, t1), ("states", t1, t2), ("ops", t2, t3), ("compact", t3, t4)):
             phase[k] += (b - a) * 1e3
 
     for _ in range(args.warmup):
         step()
-    for fu in names:
-        fu.result()
-    names.clear()
+    pipe.drain()
     torch.cuda.synchronize()
     for k in phase:
         phase[k] = 0.0
@@ -280,9 +343,10 @@ def run_c3(args, ctx, dev):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    pipe.flush()                 # every sealed file downloaded
     t_loop = time.perf_counter()
-    for fu in names:
-        out["name"] = fu.result()
+    out["name"] = pipe.drain()   # and named
+    out["file"] = pipe.last_file
     torch.cuda.synchronize()
     t_end = time.perf_counter()
     ms = (t_end - t0) * 1e3 / args.steps
@@ -291,6 +355,23 @@ def run_c3(args, ctx, dev):
     ms_loop = (t_loop - t0) * 1e3 / args.steps
     drain_ms = (t_end - t_loop) * 1e3
     ctx.set_timing(False)
+    phase_timed = dict(phase)
+    # the same steps with the state files staged from host buffers (PCIe-inclusive; never value)
+    host_states[0] = True
+    step()
+    pipe.drain()
+    torch.cuda.synchronize()
+    th0 = time.perf_counter()
+    nh = max(4, args.steps // 4)
+    for _ in range(nh):
+        step()
+    pipe.flush()
+    th1 = time.perf_counter()
+    pipe.drain()
+    host_states[0] = False
+    states_from_host = {"pipelined_ms_per_step": round((th1 - th0) * 1e3 / nh, 3), "steps": nh,
+                        "what": "the same step with the 8 state files uploaded from per-file host "
+                                "buffers each step (ce_core_ingest_states_iov: pinned staging + DMA)"}
     names = ("open_setup", "open_small", "segments_open", "finalize_open", "gate", "ds_count", "ds_emit",
              "ds_applied", "ds_add_pairs", "ds_kill", "ds_finalize", "ds_merge", "seal_setup",
              "segments_seal")
@@ -307,7 +388,7 @@ def run_c3(args, ctx, dev):
         torch.cuda.synchronize()
         t_s = time.perf_counter()
         core.reset()
-        assert core.ingest_states_iov(states)[0] == 0
+        assert core.ingest_states_device(sdev.data_ptr(), soffs.data_ptr(), len(states), sblob) == 0
         assert core.ingest_ops_device(files.data_ptr(), offs.data_ptr(), n, blob_len, all_actors,
                                       fa.data_ptr(), fv.data_ptr()) == 0
         t_c = time.perf_counter()
@@ -378,26 +459,29 @@ def run_c3(args, ctx, dev):
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
         "higher_is_better": True, "dtype": "u32/u64", "data": "synthetic (GPU-sealed, seeded)",
         "config": {"workload": "C3: Orswot, %d members, %d actors; %d state files (512 actors x %d "
-                               "versions each) + %d op files (4096 x %d versions, 26 Add + 6 Rm, %d B)"
-                               % (N_MEMBERS, N_ACTORS, n_state, V0, n, V, PT_LEN),
+                               "versions each) + %d op files (4096 x %d versions, 26 Add + 6 Rm, %d B), "
+                               "all resident in HBM" % (N_MEMBERS, N_ACTORS, n_state, V0, n, V, PT_LEN),
                    "ops": n * (N_ADD + N_RM), "entries": entries,
                    "state_file_bytes": int(len(out["file"])), "name_ms": name_ms},
         "single_compact_latency": single_call,
+        "states_from_host": states_from_host,
         "pipelined": {"ms_per_step": round(ms_loop, 3), "name_drain_ms": round(drain_ms, 3),
-                      "what": "steps back to back with the content names on %d host threads, timed up "
-                              "to the last step's return; ms_per_step above adds the names still "
-                              "being hashed then (drain / steps)" % (NB - 1)},
+                      "download_overlap": pipe.use_async,
+                      "what": "steps back to back, each sealed file's download overlapping the next "
+                              "step on the device (ce_core_compact_into_async) and its content name "
+                              "hashed on %d host threads; timed up to the last download; ms_per_step "
+                              "above adds the names still being hashed then (drain / steps)" % (NB - 1)},
         "aead_open_GBps": round(ct / (open_ms / 1e3) / 1e9, 1) if open_ms else None,
         "fold": {"kernels": "ds_applied + ds_add_pairs + ds_kill", "ms": round(fold_ms, 4),
                  "algorithmic_bytes": fold_bytes,
                  "achieved_GBps": round(fold_bytes / (fold_ms / 1e3) / 1e9, 1) if fold_ms else None,
                  "peak_GBps": 8000.0},
         "kernels_ms_per_step": k_ms,
-        "phases_ms_per_step": {k: round(v / args.steps, 3) for k, v in phase.items()},
+        "phases_ms_per_step": {k: round(v / args.steps, 3) for k, v in phase_timed.items()},
         "cpu_baseline": cpu,
         "checks": {"closed_form_clock": clock_ok, "sharded_merge_equals_whole": shard_ok},
     }
-    namer.shutdown()
+    pipe.close()
     core.close()
     return line
 
@@ -723,14 +807,11 @@ def run_c3_multi(args, ctx, dev, world, rank):
         rank, lo, hi, len(my_states), n, time.time() - t0))
     core = new_core(ctx, key)
     core.register_actors([bytes(a) for a in actors])
+    sdev, soffs, sblob = device_blob(my_states, dev)
     comm = _comm_device(dev)
     buf = shard.StateBuffer(dev)
     hops, timing_on = [], [False]
-    from concurrent.futures import ThreadPoolExecutor
-    NB = 13
-    namer = ThreadPoolExecutor(NB - 1) if rank == 0 else None
-    names = []
-    obuf = [torch.zeros(1 << 26, dtype=torch.uint8, pin_memory=True).numpy() for _ in range(NB)] if rank == 0 else None
+    pipe = CompactPipe(core, 13, use_async=not os.environ.get("CE_C3_SYNC_COMPACT")) if rank == 0 else None
     out = {}
     phase = {"states": 0.0, "ops": 0.0, "reduce": 0.0, "compact": 0.0}
 
@@ -738,7 +819,7 @@ def run_c3_multi(args, ctx, dev, world, rank):
         t_a = time.perf_counter()
         core.reset()
         if my_states:
-            rc, _ = core.ingest_states_iov(my_states)
+            rc = core.ingest_states_device(sdev.data_ptr(), soffs.data_ptr(), len(my_states), sblob)
             if rc:
                 raise crdtenc.CeError(rc, ctx.last_error())
         t_b = time.perf_counter()
@@ -758,12 +839,7 @@ def run_c3_multi(args, ctx, dev, world, rank):
             raise crdtenc.CeError(rc, "sharded C3 ingest")
         t_d = time.perf_counter()
         if rank == 0:
-            k = len(names) % NB
-            if len(names) >= NB:
-                names[-NB].result()
-            obuf[k], ln, _ = core.compact_into(obuf[k], name=False)
-            out["file"] = obuf[k][:ln]
-            names.append(namer.submit(crdtenc.content_name, out["file"]))
+            pipe.compact()
         t_e = time.perf_counter()
         if timing_on[0]:
             for key_, a_, b_ in (("states", t_a, t_b), ("ops", t_b, t_c[0]), ("reduce", t_c[0], t_d),
@@ -771,9 +847,8 @@ def run_c3_multi(args, ctx, dev, world, rank):
                 phase[key_] += (b_ - a_) * 1e3
 
     def drain():
-        for fu in names:
-            out["name"] = fu.result()
-        names.clear()
+        if pipe is not None:
+            out["name"] = pipe.drain()
 
     for _ in range(args.warmup):
         step()
@@ -816,7 +891,7 @@ def run_c3_multi(args, ctx, dev, world, rank):
         ok_whole = rc == 0 and whole.state_bytes() == sb
         whole.close()
         del fw
-        namer.shutdown()
+        pipe.close()
     ok_clock, ok_whole = _all_true(ok_clock, dev), _all_true(ok_whole, dev)
     line = {
         "metric": "C3 op+state files compacted/sec (Orswot<u64,Uuid>)",

@@ -58,7 +58,8 @@ EXPORTS = [
     "ce_core_shard_window", "ce_core_ingest_ops_device_sharded", "ce_core_pending_export",
     "ce_core_pending_commit", "ce_core_writer_versions", "ce_shard_stats_host",
     "ce_shard_window_host", "ce_shard_window_exact", "ce_core_compact_ops_device_into",
-    "ce_core_state_bytes_device", "ce_core_merge_state_device",
+    "ce_core_state_bytes_device", "ce_core_merge_state_device", "ce_core_ingest_states_device",
+    "ce_core_compact_into_async", "ce_core_compact_wait",
 ]
 
 
@@ -720,6 +721,13 @@ class Core:
         rc = lib().ce_core_ingest_states_iov(self.p, ptrs, lens, ctypes.c_uint32(n), st)
         return rc, list(st)[:n]
 
+    def ingest_states_device(self, d_blob, d_offs, n, blob_len, want_status=False):
+        """ingest_states over state files resident in HBM (device pointers)."""
+        st = (ctypes.c_int32 * max(n, 1))() if want_status else None
+        rc = lib().ce_core_ingest_states_device(self.p, ctypes.c_void_p(d_blob), ctypes.c_void_p(d_offs),
+                                                ctypes.c_uint32(n), ctypes.c_uint64(blob_len), st)
+        return (rc, list(st)[:n]) if want_status else rc
+
     def read_remote(self):
         return lib().ce_core_read_remote(self.p)
 
@@ -754,6 +762,20 @@ class Core:
             break
         self.ctx.check(rc, "compact_into")
         return buf, n.value, (nm.value.decode() if name else None)
+
+    def compact_into_async(self, buf, nonce=None):
+        """compact_into with the download left in flight: (length, ticket); read buf[:length]
+        only after compact_wait(ticket).  Raises when the file does not fit."""
+        n = ctypes.c_size_t(0)
+        t = ctypes.c_uint64(0)
+        rc = lib().ce_core_compact_into_async(self.p, _cbuf(nonce) if nonce is not None else None,
+                                              ctypes.c_void_p(buf.ctypes.data), ctypes.c_size_t(buf.nbytes),
+                                              ctypes.byref(n), ctypes.byref(t))
+        self.ctx.check(rc, "compact_into_async")
+        return n.value, t.value
+
+    def compact_wait(self, ticket):
+        self.ctx.check(lib().ce_core_compact_wait(self.p, ctypes.c_uint64(ticket)), "compact_wait")
 
     def apply_ops(self, ops_msgpack):
         return lib().ce_core_apply_ops(self.p, _cbuf(ops_msgpack), ctypes.c_size_t(len(ops_msgpack)))

@@ -1119,6 +1119,9 @@ int ingest_ops_hostmeta(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
                         reinterpret_cast<const uint64_t*>(mb), status_out);
 }
 
+int ingest_states_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n, uint64_t blen,
+                      int32_t* status_out);
+
 // Core::read_remote_states after Storage::load_states (lib.rs:425-466)
 // files (optional): per-file host buffers instead of one blob (ce_core_ingest_states_iov),
 // uploaded through the pinned staging ring
@@ -1139,9 +1142,21 @@ int ingest_states_host(ce_core* c, const uint8_t* blob, const uint64_t* offs, ui
              (e = hipMemcpyAsync(ctx->offs.p, offs, (n + 1) * 8ull, hipMemcpyHostToDevice, ctx->stream))) {
     return ctx->hip_fail(e, "states upload");
   }
+  return ingest_states_dev(c, ctx->blob.as<uint8_t>(), ctx->offs.as<uint64_t>(), n, blen, status_out);
+}
+
+// read_remote_states over state files resident in HBM (d_blob / d_offs, n + 1 offsets)
+int ingest_states_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n, uint64_t blen,
+                      int32_t* status_out) {
+  ce_ctx* ctx = c->ctx;
+  if (!c->has_key) return ctx->fail(CE_ERR_NO_KEY, "no latest key");
+  if (n == 0) return CE_OK;
+  hipError_t e;
+  if ((e = ctx->out.reserve(blen + 16ull * n + 128)) || (e = ctx->status.reserve(n * 4ull + 64)))
+    return ctx->hip_fail(e, "states reserve");
   HostPhase hp("states: open + download");
-  int rc = device_open(ctx, ctx->blob.as<uint8_t>(), ctx->offs.as<uint64_t>(), n, blen, true,
-                       key_of(c), ctx->out.as<uint8_t>(), ctx->status.as<int32_t>(), false);
+  int rc = device_open(ctx, d_blob, d_offs, n, blen, true, key_of(c), ctx->out.as<uint8_t>(),
+                       ctx->status.as<int32_t>(), false);
   if (rc) return rc;
   // one download for what the host reads per file (k_state_heads, 32 B each into pinned
   // memory): status, clear length, plaintext offset and data version -- per-file copies into
@@ -1163,8 +1178,7 @@ int ingest_states_host(ce_core* c, const uint8_t* blob, const uint64_t* offs, ui
   if ((e = read_heads())) return ctx->hip_fail(e, "states heads");
   for (uint32_t i = 0; i < n; i++)
     if (st[i] == kStatusHostParse) {
-      if ((rc = resolve_host_parse(c, ctx->blob.as<uint8_t>(), ctx->offs.as<uint64_t>(), n, true)))
-        return rc;
+      if ((rc = resolve_host_parse(c, d_blob, d_offs, n, true))) return rc;
       if ((e = read_heads())) return ctx->hip_fail(e, "states heads");
       break;
     }
@@ -1527,6 +1541,12 @@ int ce_core_open(ce_ctx* ctx, const ce_open_options* o, ce_core** out) {
 void ce_core_close(ce_core* c) {
   if (!c) return;
   if (c->ctx) (void)hipStreamSynchronize(c->ctx->stream);
+  if (c->copy_stream) {
+    (void)hipStreamSynchronize(c->copy_stream);
+    (void)hipStreamDestroy(c->copy_stream);
+  }
+  for (hipEvent_t ev : c->copy_ev)
+    if (ev) (void)hipEventDestroy(ev);
   delete c->storage;
   delete c->aux;
   ds_free(c->ds);
@@ -1763,6 +1783,15 @@ int ce_core_ingest_states_iov(ce_core* c, const uint8_t* const* files, const siz
   return ingest_states_host(c, nullptr, offs.data(), n, status, files);
 }
 
+int ce_core_ingest_states_device(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
+                                 uint64_t blob_len, int32_t* status) {
+  if (!c || (n && (!d_blob || !d_offs))) return CE_ERR_INVALID_ARG;
+  HostPhase hp("ingest_states_device (all)");
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  (void)hipSetDevice(c->ctx->device);
+  return ingest_states_dev(c, d_blob, d_offs, n, blob_len, status);
+}
+
 int ce_core_read_remote(ce_core* c) {
   if (!c) return CE_ERR_INVALID_ARG;
   std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
@@ -1817,6 +1846,36 @@ int ce_core_compact_into(ce_core* c, const uint8_t* nonce, uint8_t* dst, size_t 
     std::snprintf(name_out, 64, "%s", base32_nopad(h, 32).c_str());
   }
   return CE_OK;
+}
+
+int ce_core_compact_into_async(ce_core* c, const uint8_t* nonce, uint8_t* dst, size_t cap, size_t* len,
+                               uint64_t* ticket) {
+  if (!c || !len || !ticket || (cap && !dst)) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  c->sink_async = true;
+  c->sink_ticket = 0;
+  const int rc = ce_core_compact_into(c, nonce, dst, cap, len, nullptr);
+  c->sink_async = false;
+  *ticket = rc == CE_OK ? c->sink_ticket : 0;   // 0: already complete (small or host-written file)
+  c->sink_ticket = 0;
+  return rc;
+}
+
+int ce_core_compact_wait(ce_core* c, uint64_t ticket) {
+  if (!c) return CE_ERR_INVALID_ARG;
+  if (ticket == 0) return CE_OK;
+  hipEvent_t ev = nullptr;
+  {
+    std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+    if (ticket > c->copy_next) return CE_ERR_INVALID_ARG;
+    const uint32_t slot = (uint32_t)(ticket % ce_core::kAsyncSlots);
+    if (c->copy_slot_ticket[slot] != ticket) return CE_OK;  // the slot was reused: synchronised then
+    ev = c->copy_ev[slot];
+  }
+  // outside the context lock: other calls on this core may proceed meanwhile (the event stays
+  // alive until the core is closed)
+  const hipError_t e = hipEventSynchronize(ev);
+  return e ? c->ctx->hip_fail(e, "compact wait") : CE_OK;
 }
 
 int ce_core_compact(ce_core* c, char name_out[64]) {

@@ -72,6 +72,17 @@ struct ce_core {
   // (sink_len = its length) instead of into file_buf
   uint8_t* sink = nullptr;
   size_t sink_cap = 0, sink_len = 0;
+  // ce_core_compact_into_async: the sealed file's download into the sink is left in flight on
+  // copy_stream (ticket -> copy_ev[ticket % kAsyncSlots]); the next compaction's seal waits for
+  // the last one on the device before it rewrites the sealed output
+  static constexpr uint32_t kAsyncSlots = 16;
+  bool sink_async = false;
+  uint64_t sink_ticket = 0;               // set by the device writer when it left a copy in flight
+  hipStream_t copy_stream = nullptr;
+  hipEvent_t copy_ev[kAsyncSlots] = {};
+  uint64_t copy_slot_ticket[kAsyncSlots] = {};
+  uint64_t copy_next = 0;                 // last ticket handed out
+  hipEvent_t copy_last = nullptr;         // the newest in-flight copy's event
   std::vector<uint32_t> sorted_slots;   // used slots in UUID byte order (BTreeMap order)
   uint64_t sorted_gen = ~0ull;
   std::vector<uint8_t> last_writers;    // writer list of the previous ingest and its slots

@@ -88,6 +88,10 @@ hipError_t launch_ds_applied(hipStream_t s, const uint32_t* keys_sorted, const u
                              const unsigned long long* ctr_sorted,
                              const unsigned long long* excl_max, const unsigned long long* clock,
                              uint8_t* applied, uint32_t n);
+// flag |= 1 unless every actor's adds are one contiguous run (marks: u32[n_marks] holding older
+// generations only; gen = a fresh nonzero value per check)
+hipError_t launch_ds_contig(hipStream_t s, const uint32_t* actor, uint32_t n, uint32_t* marks, uint32_t n_marks,
+                            uint32_t gen, uint32_t* flag);
 // clock[a] = max(clock[a], counter) for every add
 hipError_t launch_ds_clock(hipStream_t s, const uint32_t* keys_sorted, const unsigned long long* ctr_sorted,
                            const unsigned long long* excl_max, unsigned long long* clock, uint32_t n_add);

@@ -349,14 +349,29 @@ __global__ void k_ds_gather_ctr(const uint32_t* perm, const unsigned long long* 
 
 // applied(add k) = c_k > max(C0[a_k], max{c_j : j < k, a_j = a_k})  (crdts Orswot::apply:
 // "if self.clock.get(&dot.actor) >= dot.counter { return }")
+// perm null: the adds in their own order (run-contiguous actors, no sort)
 __global__ void k_ds_applied(const uint32_t* keys, const uint32_t* perm,
                              const unsigned long long* ctr, const unsigned long long* excl,
                              const unsigned long long* clock, uint8_t* applied, uint32_t n) {
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
     const unsigned long long c0 = clock[keys[i]];
     const unsigned long long prev = excl[i] > c0 ? excl[i] : c0;
-    applied[perm[i]] = ctr[i] > prev;
+    applied[perm ? perm[i] : i] = ctr[i] > prev;
   }
+}
+
+// flag |= 1 unless every actor's adds form one contiguous run: a run head stamps its actor's
+// mark with this check's generation; a second head of the same actor finds the stamp
+__global__ void k_ds_contig(const uint32_t* actor, uint32_t n, uint32_t* marks, uint32_t n_marks, uint32_t gen,
+                            uint32_t* flag) {
+  bool bad = false;
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+    const uint32_t a = actor[i];
+    if (i > 0 && actor[i - 1] == a) continue;
+    if (a >= n_marks) { bad = true; continue; }
+    bad |= atomicExch(marks + a, gen) == gen;
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
 }
 
 // clock[a] = max(clock[a], every counter of actor a in the batch), from the actor-sorted adds:
@@ -910,6 +925,13 @@ hipError_t launch_ds_applied(hipStream_t s, const uint32_t* keys_sorted, const u
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_ds_applied, dim3(blocks_for(n)), dim3(kBlock), 0, s, keys_sorted, perm,
                      ctr_sorted, excl_max, clock, applied, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_ds_contig(hipStream_t s, const uint32_t* actor, uint32_t n, uint32_t* marks, uint32_t n_marks,
+                            uint32_t gen, uint32_t* flag) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ds_contig, dim3(blocks_for(n)), dim3(kBlock), 0, s, actor, n, marks, n_marks, gen, flag);
   return hipGetLastError();
 }
 

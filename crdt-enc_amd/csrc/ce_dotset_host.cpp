@@ -45,6 +45,11 @@ struct DsState {
       cub_tmp, deferred_flags, d0[5], col[6], mv[6], other[4], oclock;
   DevBuf misses;
   HostBuf h_cnt;
+  // run-contiguity marks of the adds' actors (k_ds_contig: a generation per check, no clearing)
+  DevBuf contig_marks;
+  uint32_t contig_cap = 0, contig_gen = 0;
+  bool adds_contig = false;  // this batch's adds: every actor's adds one contiguous run
+  DevBuf seal_out;           // the compaction's sealed file (ds_compact_device)
   // device state reader (per state file: candidates, sorted heads, entry ends, Dot counts and
   // bases, members, sorted members [0..6]
   // and emitted (member, actor id, value) columns [7..9]), pinned staging for its downloads
@@ -482,7 +487,28 @@ int orswot_fold(ce_core* c, const Counts& k) {
   const uint32_t na = (uint32_t)k.v[kCntAdd], nr = (uint32_t)k.v[kCntRm];
   // 1) applied flags: stable sort of the adds by actor, segmented exclusive max of counters
   if ((e = d->applied.reserve(na + 64))) return ctx->hip_fail(e, "applied");
-  if (na) {
+  // the clock update's keys / counters: sorted copies, or the columns themselves when every
+  // actor's adds already form one contiguous run (the scan by key then needs no sort)
+  const uint32_t* clock_keys = d->sort_keys2.as<uint32_t>();
+  const unsigned long long* clock_ctr = d->ctr_sorted.as<unsigned long long>();
+  if (na && d->adds_contig) {
+    if ((e = d->excl.reserve(na * 8ull))) return ctx->hip_fail(e, "applied");
+    unsigned long long* ex = d->excl.as<unsigned long long>();
+    size_t t2 = 0;
+    if ((e = ds_excl_max_by_key(nullptr, t2, o.add_actor, o.add_ctr, ex, na, s)) ||
+        (e = d->cub_tmp.reserve(t2 + 256)))
+      return ctx->hip_fail(e, "applied");
+    t2 = d->cub_tmp.cap;
+    const int ta = ctx->tbegin("ds_applied");
+    if ((e = ds_excl_max_by_key(d->cub_tmp.p, t2, o.add_actor, o.add_ctr, ex, na, s)) ||
+        (e = launch_ds_applied(s, o.add_actor, nullptr, o.add_ctr, ex, d->clock.as<unsigned long long>(),
+                               d->applied.as<uint8_t>(), na)))
+      return ctx->hip_fail(e, "applied");
+    ctx->tend(ta);
+    c->path_counts["ds_adds_contiguous"]++;
+    clock_keys = o.add_actor;
+    clock_ctr = o.add_ctr;
+  } else if (na) {
     if ((e = d->sort_keys.reserve(na * 4ull)) || (e = d->sort_perm.reserve(na * 4ull)) ||
         (e = d->sort_keys2.reserve(na * 4ull)) || (e = d->sort_perm2.reserve(na * 4ull)) ||
         (e = d->ctr_sorted.reserve(na * 8ull)) || (e = d->excl.reserve(na * 8ull)))
@@ -513,8 +539,8 @@ int orswot_fold(ce_core* c, const Counts& k) {
   if ((rc = ensure_pairs(c, k.v[kCntAddM]))) return rc;
   const int tp = ctx->tbegin("ds_add_pairs");
   if ((e = launch_ds_add_pairs(s, tables(d), o, d->applied.as<uint8_t>(), na)) ||
-      (e = launch_ds_clock(s, d->sort_keys2.as<uint32_t>(), d->ctr_sorted.as<unsigned long long>(),
-                           d->excl.as<unsigned long long>(), d->clock.as<unsigned long long>(), na)))
+      (e = launch_ds_clock(s, clock_keys, clock_ctr, d->excl.as<unsigned long long>(),
+                           d->clock.as<unsigned long long>(), na)))
     return ctx->hip_fail(e, "add");
   ctx->tend(tp);
   // 3) removal thresholds: the batch's removals and the deferred set (uploaded only when there
@@ -949,9 +975,32 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
     const int te = ctx->tbegin("ds_emit");
     if ((e = launch_ds_emit(ctx->stream, a))) return ctx->hip_fail(e, "emit");
     ctx->tend(te);
+    // are every actor's adds one contiguous run (load_ops order, each writer adding its own
+    // dots)?  Then the fold's applied flags need no sort (orswot_fold); the flag rides in
+    // misses[3] with the miss count
+    const uint32_t n_add = (uint32_t)tot.v[kCntAdd];
+    const bool check = c->kind == CE_STATE_ORSWOT && n_add > 0;
+    if (check) {
+      const uint32_t need = std::max<uint32_t>(1024, (uint32_t)c->id_actor.size());
+      if (need > d->contig_cap) {
+        const uint32_t cap = pow2_at_least(need);
+        if ((e = d->contig_marks.reserve(4ull * cap)) || (e = hipMemsetAsync(d->contig_marks.p, 0, 4ull * cap, ctx->stream)))
+          return ctx->hip_fail(e, "contig");
+        d->contig_cap = cap;
+        d->contig_gen = 0;
+      }
+      if (++d->contig_gen == 0) {  // wrapped: marks from 2^32 checks ago could collide
+        if ((e = hipMemsetAsync(d->contig_marks.p, 0, 4ull * d->contig_cap, ctx->stream))) return ctx->hip_fail(e, "contig");
+        d->contig_gen = 1;
+      }
+      if ((e = launch_ds_contig(ctx->stream, a.ops.add_actor, n_add, d->contig_marks.as<uint32_t>(), d->contig_cap,
+                                d->contig_gen, a.counters + 3)))
+        return ctx->hip_fail(e, "contig");
+    }
     if ((e = hipMemcpyAsync(hm, d->misses.p, 16, hipMemcpyDeviceToHost, ctx->stream)) ||
         (e = stream_wait(ctx->stream)))
       return ctx->hip_fail(e, "emit");
+    d->adds_contig = check && hm[3] == 0 && !getenv("CE_DS_SORT_ADDS");
     if (hm[2] == 0) break;
     if (round > 64) return ctx->fail(CE_ERR_DEVICE, "actor table did not converge");
     const uint32_t nm = std::min<uint32_t>(hm[2], kMissCap);
@@ -1884,7 +1933,7 @@ static int ds_serialize_dev(ce_core* c, ce_ctx* x, const uint8_t* outer, const u
   const uint64_t U = hw.b.size() + 5 + 20ull * nl + 27ull * nl + tw.b.size();
   const uint64_t A = (U + 255) & ~255ull;  // [offs(2) | out_offs(1) | stats | nonce | outer] after it
   const uint64_t total_max = 16 + sealed_len(U);
-  if ((e = x->blob.reserve(A + 256 + hw.b.size() + tw.b.size())) || (e = x->out.reserve(total_max + 64)) ||
+  if ((e = x->blob.reserve(A + 256 + hw.b.size() + tw.b.size())) ||
       (e = x->h_stage.reserve(std::max<uint64_t>(total_max + 64, 256 + hw.b.size() + tw.b.size()))))
     return x->hip_fail(e, "ds compact reserve");
   for (int k = 0; k < 15; k++) {
@@ -1959,8 +2008,17 @@ int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t
   uint8_t* db = x->blob.as<uint8_t>();
   auto* offs = reinterpret_cast<unsigned long long*>(db + A);
   auto cph = std::make_unique<HostPhase>("  cd: seal enqueue");
+  // the sealed file in its own buffer (the next ingest reuses the context's plaintext buffer
+  // while an async download of this file may still run); a previous compaction's download may
+  // still read it: the seal waits for it on the device, a reallocation on the host
+  DsState* d = c->ds;
+  const uint64_t total_max = 16 + sealed_len(U);
+  if (total_max + 64 > d->seal_out.cap && c->copy_last && (e = hipEventSynchronize(c->copy_last)))
+    return x->hip_fail(e, "ds compact");
+  if ((e = d->seal_out.reserve(total_max + 64))) return x->hip_fail(e, "ds compact reserve");
+  if (c->copy_last && (e = hipStreamWaitEvent(s, c->copy_last, 0))) return x->hip_fail(e, "ds compact");
   rc = device_seal(x, db, reinterpret_cast<const uint64_t*>(offs), 1, U, db + A + 56, db + A + 32,
-                   x->out.as<uint8_t>(), reinterpret_cast<const uint64_t*>(db + A + 16), key);
+                   d->seal_out.as<uint8_t>(), reinterpret_cast<const uint64_t*>(db + A + 16), key);
   if (rc) return rc;
   cph = std::make_unique<HostPhase>("  cd: length wait");
   uint64_t clear_len = 0;
@@ -1978,7 +2036,28 @@ int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t
     to = file->data();
   }
   cph = std::make_unique<HostPhase>("  cd: download");
-  if ((e = hipMemcpyAsync(to, x->out.p, total, hipMemcpyDeviceToHost, s)) || (e = stream_wait(s)))
+  if (c->sink_async && to == c->sink) {
+    // compact_into_async: the download runs on the copy stream behind the seal; the caller
+    // waits for its ticket (ce_core_compact_wait) before reading the file
+    if ((!c->copy_stream && (e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking))) ||
+        (!x->side_ev && (e = hipEventCreateWithFlags(&x->side_ev, hipEventDisableTiming))))
+      return x->hip_fail(e, "ds compact download");
+    const uint64_t t = ++c->copy_next;
+    const uint32_t slot = (uint32_t)(t % ce_core::kAsyncSlots);
+    hipEvent_t& ev = c->copy_ev[slot];
+    if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming))) return x->hip_fail(e, "ds compact download");
+    if (c->copy_slot_ticket[slot] && (e = hipEventSynchronize(ev)))  // the slot's previous copy
+      return x->hip_fail(e, "ds compact download");
+    if ((e = hipEventRecord(x->side_ev, s)) || (e = hipStreamWaitEvent(c->copy_stream, x->side_ev, 0)) ||
+        (e = hipMemcpyAsync(to, d->seal_out.p, total, hipMemcpyDeviceToHost, c->copy_stream)) ||
+        (e = hipEventRecord(ev, c->copy_stream)))
+      return x->hip_fail(e, "ds compact download");
+    c->copy_slot_ticket[slot] = t;
+    c->copy_last = ev;
+    c->sink_ticket = t;
+    return CE_OK;
+  }
+  if ((e = hipMemcpyAsync(to, d->seal_out.p, total, hipMemcpyDeviceToHost, s)) || (e = stream_wait(s)))
     return x->hip_fail(e, "ds compact download");
   return CE_OK;
 }

@@ -286,6 +286,11 @@ int ce_core_ingest_states(ce_core *c, const uint8_t *blob, const uint64_t *offs,
  * pinned staging ring (no concatenated copy). */
 int ce_core_ingest_states_iov(ce_core *c, const uint8_t *const *files, const size_t *lens, uint32_t n,
                               int32_t *status);
+/* The same with the state files resident in HBM: d_blob / d_offs (n + 1 entries, blob_len =
+ * offs[n]) are device pointers (file i = CURRENT_VERSION || cryptor box, as load_states returns
+ * it); status (may be NULL) is host memory. */
+int ce_core_ingest_states_device(ce_core *c, const uint8_t *d_blob, const uint64_t *d_offs, uint32_t n,
+                                 uint64_t blob_len, int32_t *status);
 /* Core::compact (crdt-enc/src/lib.rs:332-380) over a batch resident in HBM: read_remote_ops over
  * the op files exactly as ce_core_ingest_ops_device, then the compaction output as
  * ce_core_compact_to_buffer.  For VClock/GCounter the compaction is queued on the device behind
@@ -319,6 +324,14 @@ int ce_core_compact_to_buffer(ce_core *c, const uint8_t *nonce, ce_buf *file, ch
  * can grow its buffer and call again (the state is unchanged; the nonce is drawn again). */
 int ce_core_compact_into(ce_core *c, const uint8_t *nonce, uint8_t *dst, size_t cap, size_t *len,
                          char name_out[64]);
+
+/* ce_core_compact_into with the sealed file's download left in flight (pipelined
+ * compactions: the download overlaps the caller's next batch on the device).  *ticket = 0 when
+ * the file is already complete in dst, else pass it to ce_core_compact_wait before reading dst
+ * (dst must stay allocated until then).  Returns the same statuses as ce_core_compact_into. */
+int ce_core_compact_into_async(ce_core *c, const uint8_t *nonce, uint8_t *dst, size_t cap, size_t *len,
+                               uint64_t *ticket);
+int ce_core_compact_wait(ce_core *c, uint64_t ticket);
 
 /* What read_remote_states does with one decrypted state (lib.rs:447, 458-466):
  * rmp_serde::from_slice::<StateWrapper<S>>(sw) then state.merge + next_op_versions.merge.

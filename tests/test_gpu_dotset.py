@@ -681,3 +681,104 @@ def test_state_bytes_and_merge_device(ctx, kind):
 
 def a_kind(kind):
     return {"orswot": crdtenc.STATE_ORSWOT, "mvreg": crdtenc.STATE_MVREG, "gcounter": crdtenc.STATE_GCOUNTER}[kind]
+
+
+def test_ingest_states_device_matches_host(ctx):
+    """ce_core_ingest_states_device (state files resident in HBM) == ce_core_ingest_states (host
+    blob): statuses and state bytes, for Orswot (device state reader) and GCounter (host parse of
+    the device-opened plaintexts), a tampered file included."""
+    import torch
+    rng = random.Random(12)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 6)
+    sws = []
+    for _ in range(3):
+        part = C.Core("orswot")
+        files = gen("orswot", rng, actors, 2, 6, 50, False)
+        acts, clears, fa, fv = G.batch(files, "orswot", APP)
+        f = seal_files(ctx, key, clears)
+        assert part.read_remote_ops(key, [APP], f, [acts[i] for i in fa], fv)[0] == 0
+        sws.append(part.serialize())
+    dev = torch.device("cuda", 0)
+
+    def on_device(fs):
+        offs = np.zeros(len(fs) + 1, np.int64)
+        offs[1:] = np.cumsum([len(x) for x in fs])
+        blob = torch.from_numpy(np.frombuffer(b"".join(fs) + bytes(64), np.uint8).copy()).to(dev)
+        return blob, torch.from_numpy(offs).to(dev), int(offs[-1])
+    for fs in (seal_states(ctx, key, sws), None):
+        if fs is None:   # one tampered file: nothing merged, same statuses
+            fs = seal_states(ctx, key, sws)
+            t = bytearray(fs[1])
+            t[-3] ^= 1
+            fs[1] = bytes(t)
+        a, b = new_core(ctx, "orswot", key), new_core(ctx, "orswot", key)
+        blob, offs, ln = on_device(fs)
+        torch.cuda.synchronize()
+        ra = a.ingest_states(fs)
+        rb = b.ingest_states_device(blob.data_ptr(), offs.data_ptr(), len(fs), ln, want_status=True)
+        assert ra == rb and (ra[0] in (0, 9))
+        assert a.state_bytes() == b.state_bytes()
+        a.close()
+        b.close()
+
+
+@pytest.mark.parametrize("adversarial", [False, True])
+def test_orswot_adds_without_sort(ctx, adversarial):
+    """The fold's applied flags skip the stable sort by actor when every actor's adds form one
+    contiguous run (k_ds_contig): the well-formed history (each writer adding its own dots, in
+    load_ops order) takes that path, the adversarial one (adds naming other writers' dots) the
+    sort; both == the oracle, and == the sort path forced with CE_DS_SORT_ADDS=1."""
+    rng = random.Random(515 + adversarial)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 9)
+    files = gen("orswot", rng, actors, 4, 10, 200, adversarial)
+    acts, clears, fa, fv = G.batch(files, "orswot", APP)
+    sealed = seal_files(ctx, key, clears)
+    oc = C.Core("orswot")
+    assert oc.read_remote_ops(key, [APP], sealed, [acts[i] for i in fa], fv)[0] == 0
+    got = {}
+    for forced in (False, True):
+        if forced:
+            os.environ["CE_DS_SORT_ADDS"] = "1"
+        try:
+            core = new_core(ctx, "orswot", key)
+            assert core.ingest_ops(sealed, acts, fa, fv)[0] == 0
+            got[forced] = (core.state_bytes(), core.path_count("ds_adds_contiguous"))
+            core.close()
+        finally:
+            os.environ.pop("CE_DS_SORT_ADDS", None)
+    assert got[False][0] == got[True][0] == oc.serialize()
+    assert got[True][1] == 0
+    assert got[False][1] == (0 if adversarial else 1)
+
+
+def test_compact_into_async_overlaps_next_ingest(ctx):
+    """ce_core_compact_into_async leaves the sealed file's download in flight: the next batch's
+    reset, ingest and compaction are queued before the first download is waited for, and both
+    files still open to exactly the StateWrappers they were compacted from (the seal has its own
+    output buffer; the second seal waits for the first download on the device)."""
+    import torch
+    rng = random.Random(808)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 8)
+    core = new_core(ctx, "orswot", key)
+    bufs = [torch.zeros(1 << 22, dtype=torch.uint8, pin_memory=True).numpy() for _ in range(2)]
+    want, tickets = [], []
+    for r in range(2):
+        files = gen("orswot", rng, actors, 3, 8, 500 + 100 * r, False)
+        acts, clears, fa, fv = G.batch(files, "orswot", APP)
+        core.reset()
+        assert core.ingest_ops(seal_files(ctx, key, clears), acts, fa, fv)[0] == 0
+        want.append(core.state_bytes())
+        tickets.append(core.compact_into_async(bufs[r], nonce=bytes(24)))
+    assert tickets[0][1] != 0 and tickets[1][1] > tickets[0][1]
+    for r in (1, 0):
+        ln, t = tickets[r]
+        core.compact_wait(t)
+        f = bytes(bufs[r][:ln])
+        assert f[:16] == APP
+        st, pt = ctx.decrypt(key, f[16:])
+        assert st == 0 and pt == want[r]
+    core.compact_wait(tickets[0][1])   # waiting twice is fine
+    core.close()
