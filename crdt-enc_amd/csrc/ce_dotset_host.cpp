@@ -102,15 +102,18 @@ int tables_alloc(ce_core* c, uint32_t cap) {
       (e = d->hold.reserve(cap * 8ull)) || (e = d->live.reserve(64)))
     return ctx->hip_fail(e, "dot-set tables");
   d->pcap = cap;
-  if ((e = hipMemsetAsync(d->mkey.p, 0xff, (cap + 1ull) * 8, ctx->stream)) ||
-      (e = hipMemsetAsync(d->pkey.p, 0xff, cap * 8ull, ctx->stream)) ||
-      (e = hipMemsetAsync(d->cur.p, 0, cap * 8ull, ctx->stream)) ||
-      (e = hipMemsetAsync(d->add.p, 0, cap * 8ull, ctx->stream)) ||
-      (e = hipMemsetAsync(d->kill.p, 0, cap * 8ull, ctx->stream)) ||
-      (e = hipMemsetAsync(d->oth.p, 0, cap * 8ull, ctx->stream)) ||
-      (e = hipMemsetAsync(d->hold.p, 0, cap * 8ull, ctx->stream)) ||
-      (e = hipMemsetAsync(d->live.p, 0, 64, ctx->stream)))
-    return ctx->hip_fail(e, "dot-set tables");
+  // every table cleared by one launch (eight blit fills cost a dispatch gap each)
+  FillArgs fl{};
+  fl.r[0] = {d->mkey.as<uint32_t>(), (cap + 1ull) * 2, 0xffffffffu};
+  fl.r[1] = {d->pkey.as<uint32_t>(), cap * 2ull, 0xffffffffu};
+  fl.r[2] = {d->cur.as<uint32_t>(), cap * 2ull, 0u};
+  fl.r[3] = {d->add.as<uint32_t>(), cap * 2ull, 0u};
+  fl.r[4] = {d->kill.as<uint32_t>(), cap * 2ull, 0u};
+  fl.r[5] = {d->oth.as<uint32_t>(), cap * 2ull, 0u};
+  fl.r[6] = {d->hold.as<uint32_t>(), cap * 2ull, 0u};
+  fl.r[7] = {d->live.as<uint32_t>(), 16, 0u};
+  fl.n = 8;
+  if ((e = launch_fill(ctx->stream, fl))) return ctx->hip_fail(e, "dot-set tables");
   d->used_pairs = 0;
   d->live_pairs = 0;
   return CE_OK;
@@ -489,8 +492,9 @@ int orswot_fold(ce_core* c, const Counts& k) {
   if ((e = d->applied.reserve(na + 64))) return ctx->hip_fail(e, "applied");
   // the clock update's keys / counters: sorted copies, or the columns themselves when every
   // actor's adds already form one contiguous run (the scan by key then needs no sort)
-  const uint32_t* clock_keys = d->sort_keys2.as<uint32_t>();
-  const unsigned long long* clock_ctr = d->ctr_sorted.as<unsigned long long>();
+  // (set after the reserves below: a reserve may move the buffer)
+  const uint32_t* clock_keys = nullptr;
+  const unsigned long long* clock_ctr = nullptr;
   if (na && d->adds_contig) {
     if ((e = d->excl.reserve(na * 8ull))) return ctx->hip_fail(e, "applied");
     unsigned long long* ex = d->excl.as<unsigned long long>();
@@ -513,6 +517,8 @@ int orswot_fold(ce_core* c, const Counts& k) {
         (e = d->sort_keys2.reserve(na * 4ull)) || (e = d->sort_perm2.reserve(na * 4ull)) ||
         (e = d->ctr_sorted.reserve(na * 8ull)) || (e = d->excl.reserve(na * 8ull)))
       return ctx->hip_fail(e, "applied");
+    clock_keys = d->sort_keys2.as<uint32_t>();
+    clock_ctr = d->ctr_sorted.as<unsigned long long>();
     const int bits = bits_for((uint32_t)c->id_actor.size());
     size_t t1 = 0, t2 = 0;
     uint32_t* keys2 = d->sort_keys2.as<uint32_t>();

@@ -1,0 +1,37 @@
+#!/bin/bash
+# C3 fold / decode HBM traffic: FETCH_SIZE and WRITE_SIZE passes (separate runs, per the
+# microarch guide) over a short bench_configs.py --config c3 run, summarised per kernel
+# (median dispatch; FETCH_SIZE KB x 1024 x 2 per the gfx950 correction, WRITE_SIZE KB x 1024)
+# into gpurun_out/c3traffic/c3_traffic.json.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/c3traffic
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+for P in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 240 rocprofv3 --pmc $P --output-format csv -d $O/c3_$P -o p -- \
+    python3 $R/bench_configs.py --config c3 --steps 2 --warmup 1 --no-cpu > $O/c3_$P.out 2> $O/c3_$P.err || { echo "pmc $P rc=$?"; tail -5 $O/c3_$P.err; exit 1; }
+done
+python3 - $O <<'PY'
+import csv, glob, json, sys
+o = sys.argv[1]
+names = ("k_ds_applied", "k_ds_add_pairs", "k_ds_kill", "k_ds_emit", "k_ds_count", "k_ds_collect", "k_ds_finalize",
+         "k_ds_contig", "k_ser_write", "k_ds_kfinal", "k_ds_kput")
+res = {}
+for P in ("FETCH_SIZE", "WRITE_SIZE"):
+    per = {}
+    for fn in glob.glob(o + "/c3_%s/**/*counter_collection.csv" % P, recursive=True):
+        for row in csv.DictReader(open(fn)):
+            k = next((x for x in names if x in row["Kernel_Name"]), None)
+            if k and row["Counter_Name"] == P:
+                per.setdefault(k, {}).setdefault(row["Dispatch_Id"], 0.0)
+                per[k][row["Dispatch_Id"]] += float(row["Counter_Value"])
+    for k, d in per.items():
+        v = sorted(d.values())[len(d) // 2]
+        res.setdefault(k, {})[P.lower() + "_bytes"] = round(v * 1024 * (2 if P == "FETCH_SIZE" else 1))
+json.dump({"method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate runs of bench_configs.py --config c3 "
+           "--steps 2 (median dispatch per kernel; FETCH_SIZE KB x 1024 x 2 per the gfx950 correction, "
+           "WRITE_SIZE KB x 1024)", "kernels": res}, open(o + "/c3_traffic.json", "w"), indent=1)
+print(json.dumps(res))
+PY
+rm -rf $O/c3_FETCH_SIZE $O/c3_WRITE_SIZE
