@@ -467,8 +467,9 @@ class Workload:
                 "pcie_GBps": round(self.blob_len / (up_ms / max(up_n, 1) / 1e3) / 1e9, 1) if up_n else None,
                 "bytes": self.blob_len, "state_check": "ok" if ok else "MISMATCH",
                 "path": "ce_core_compact_ops_iov: 1,048,576 per-file host buffers (pageable) -> "
-                        "host-thread gather into 2 x 64 MiB pinned chunks -> DMA on a copy stream "
-                        "-> device compaction (never the line's value: inputs are not resident)"}, ok
+                        "host-thread gather (threads on the GPU's NUMA node) into a ring of 4 x 32 MiB "
+                        "pinned chunks -> DMA on a copy stream -> device compaction (never the line's "
+                        "value: inputs are not resident)"}, ok
 
     def cpu_baseline(self, args):
         """The oracle (C restatement of the reference path) on this host, both modes, over the

@@ -2,21 +2,65 @@
 // after Storage::load_ops: one Vec<u8> per file, crdt-enc/src/lib.rs:495 and
 // crdt-enc-tokio/src/lib.rs:222-278).
 //
-// The files are gathered, chunk by chunk, into two pinned staging buffers by a pool of host
-// threads, and each filled chunk is DMA'd to its place in the device blob on the context's copy
-// stream while the threads fill the other buffer.  Measured on the box (tools/h2d_probe.py):
+// The files are gathered, chunk by chunk, into a ring of four pinned 32 MiB staging buffers by a
+// pool of host threads (pinned to the GPU's NUMA node when it has room for them), and each filled
+// chunk is DMA'd to its place in the device blob on the context's copy stream while the threads
+// fill the next ones.  Measured on the box (tools/h2d_probe.py):
 // host memcpy reaches ~120 GB/s on 8-16 threads, H2D DMA ~57 GB/s, so the pipeline runs at the
 // PCIe rate.  The compute stream waits for the last chunk with an event (no host synchronise);
 // the kernels then run on the whole batch.
+#include <pthread.h>
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <fstream>
 #include <functional>
+#include <sstream>
 #include <thread>
 
 #include "ce_core.h"
 
 namespace ce {
+
+// The CPUs of the GPU's NUMA node that this process may run on (empty: unknown, or none
+// allowed): the gather threads copy into pinned staging the GPU's DMA engine reads, so on a
+// multi-socket host they run next to it.  CE_UPLOAD_NUMA=0 disables the pinning.
+static std::vector<int> gpu_node_cpus(int device) {
+  std::vector<int> out;
+  const char* env = getenv("CE_UPLOAD_NUMA");
+  if (env && env[0] == '0') return out;
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) return out;
+  std::string id(bus);
+  for (auto& ch : id) ch = (char)std::tolower((unsigned char)ch);
+  int node = -1;
+  {
+    std::ifstream f("/sys/bus/pci/devices/" + id + "/numa_node");
+    if (!(f >> node) || node < 0) return out;
+  }
+  std::ifstream f("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");
+  std::string list;
+  if (!std::getline(f, list)) return out;
+  cpu_set_t allowed;
+  CPU_ZERO(&allowed);
+  if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return out;
+  std::stringstream ss(list);
+  std::string part;
+  while (std::getline(ss, part, ',')) {
+    int a = -1, b = -1;
+    if (sscanf(part.c_str(), "%d-%d", &a, &b) == 2) {
+    } else if (sscanf(part.c_str(), "%d", &a) == 1) {
+      b = a;
+    } else {
+      continue;
+    }
+    for (int c = a; c <= b && c < CPU_SETSIZE; c++)
+      if (c >= 0 && CPU_ISSET(c, &allowed)) out.push_back(c);
+  }
+  return out;
+}
 
 // A fixed pool of host threads for parallel_for (gather copies).
 struct HostPool {
@@ -27,10 +71,21 @@ struct HostPool {
   uint64_t gen = 0;
   int pending = 0;
   bool stop = false;
+  int numa_cpus = 0;  // CPUs of the GPU's node the threads were pinned to (0: not pinned)
 
-  explicit HostPool(int n) {
+  explicit HostPool(int n, int device = -1) {
+    const std::vector<int> cpus = device >= 0 ? gpu_node_cpus(device) : std::vector<int>{};
+    // pin only when the node has room for the whole pool (else the threads would share cores)
+    const bool pin = (int)cpus.size() >= n;
+    if (pin) numa_cpus = (int)cpus.size();
     for (int i = 0; i < n; i++)
-      th.emplace_back([this, i] {
+      th.emplace_back([this, i, pin, cpus] {
+        if (pin) {
+          cpu_set_t set;
+          CPU_ZERO(&set);
+          for (int c : cpus) CPU_SET(c, &set);
+          (void)pthread_setaffinity_np(pthread_self(), sizeof set, &set);
+        }
         uint64_t seen = 0;
         for (;;) {
           std::function<void(int)> f;
@@ -66,15 +121,20 @@ struct HostPool {
   }
 };
 
+// A ring of kRing pinned chunks: the threads fill chunk k + 1.. while the DMAs of the earlier
+// ones run back to back on the copy stream; a chunk is refilled once its DMA is done.
+static constexpr int kRing = 4;
 struct Uploader {
-  size_t chunk = 64ull << 20;  // CE_UPLOAD_CHUNK (bytes) overrides: tests force many chunks
+  size_t chunk = 32ull << 20;  // CE_UPLOAD_CHUNK (bytes) overrides: tests force many chunks
   hipStream_t copy = nullptr;
-  HostBuf stage[2];
-  hipEvent_t ev[2] = {nullptr, nullptr}, t0 = nullptr, t1 = nullptr, order = nullptr;
-  bool used[2] = {false, false};
+  HostBuf stage[kRing];
+  hipEvent_t ev[kRing] = {}, t0 = nullptr, t1 = nullptr, order = nullptr;
+  bool used[kRing] = {};
   ~Uploader() {
     if (copy) (void)hipStreamSynchronize(copy);
-    for (auto e : {ev[0], ev[1], t0, t1, order})
+    for (auto e : ev)
+      if (e) (void)hipEventDestroy(e);
+    for (auto e : {t0, t1, order})
       if (e) (void)hipEventDestroy(e);
     if (copy) (void)hipStreamDestroy(copy);
   }
@@ -92,13 +152,11 @@ static int get_uploader(ce_ctx* ctx, Uploader** out) {
   if (!ctx->up) {
     auto* u = new Uploader();
     if (const char* c = getenv("CE_UPLOAD_CHUNK")) u->chunk = std::max<size_t>(4096, strtoull(c, nullptr, 10));
-    hipError_t e;
-    if ((e = hipStreamCreateWithFlags(&u->copy, hipStreamNonBlocking)) ||
-        (e = hipEventCreateWithFlags(&u->ev[0], hipEventDisableTiming)) ||
-        (e = hipEventCreateWithFlags(&u->ev[1], hipEventDisableTiming)) ||
-        (e = hipEventCreate(&u->t0)) || (e = hipEventCreate(&u->t1)) ||
-        (e = hipEventCreateWithFlags(&u->order, hipEventDisableTiming)) ||
-        (e = u->stage[0].reserve(u->chunk)) || (e = u->stage[1].reserve(u->chunk))) {
+    hipError_t e = hipStreamCreateWithFlags(&u->copy, hipStreamNonBlocking);
+    for (int k = 0; k < kRing && e == hipSuccess; k++)
+      if ((e = hipEventCreateWithFlags(&u->ev[k], hipEventDisableTiming)) == hipSuccess) e = u->stage[k].reserve(u->chunk);
+    if (e || (e = hipEventCreate(&u->t0)) || (e = hipEventCreate(&u->t1)) ||
+        (e = hipEventCreateWithFlags(&u->order, hipEventDisableTiming))) {
       delete u;
       return ctx->hip_fail(e, "uploader");
     }
@@ -109,7 +167,7 @@ static int get_uploader(ce_ctx* ctx, Uploader** out) {
 }
 
 static HostPool* get_pool(ce_ctx* ctx) {
-  if (!ctx->pool) ctx->pool = new HostPool(pool_threads());
+  if (!ctx->pool) ctx->pool = new HostPool(pool_threads(), ctx->device);
   return ctx->pool;
 }
 
@@ -153,7 +211,7 @@ int upload_iov(ce_ctx* ctx, const uint8_t* const* files, const uint64_t* offs, u
   }
   HostPool* pool = get_pool(ctx);
   const int T = pool->size();
-  for (uint64_t c0 = 0, k = 0; c0 < total; c0 += u->chunk, k ^= 1) {
+  for (uint64_t c0 = 0, k = 0; c0 < total; c0 += u->chunk, k = (k + 1) % kRing) {
     const uint64_t len = std::min<uint64_t>(u->chunk, total - c0);
     if (u->used[k] && (e = hipEventSynchronize(u->ev[k]))) return ctx->hip_fail(e, "upload ring");
     uint8_t* st = u->stage[k].as<uint8_t>();
