@@ -47,6 +47,17 @@ struct DsOps {
   unsigned long long* put_val; // MVReg
 };
 
+// The tiled emit (Orswot): file-minor scratch rows per op column (column c = add_actor,
+// add_ctr, add_mbeg, add_mem, rm_cbeg, rm_mbeg, rmc_actor, rmc_ctr, rm_mem), entry k of file i at
+// col[c][k * npad + i]; npad = 0 disables it.  total[g] = the count column totals (the last
+// file's end).  Every per-file count must be <= kTileMaxRows.
+static constexpr uint32_t kTileMaxRows = 96;
+struct DsTile {
+  void* col[9];
+  uint64_t npad;
+  uint32_t total[5];
+};
+
 struct DsDecodeArgs {
   int kind;                     // DsKind
   const uint8_t* pt;            // plaintext blob (FileParams.out_off / len)
@@ -61,9 +72,11 @@ struct DsDecodeArgs {
   const ActorSlot* table;
   uint32_t mask;
   DsOps ops;
-  uint32_t* counters;           // [0] decode failures, [1] host-decode files, [2] misses
+  uint32_t* counters;           // [0] decode failures, [1] host-decode files, [2] misses,
+                                // [3] adds not run-contiguous, [8 + k] largest count of column k
   uint4* miss_list;
   uint32_t miss_cap;
+  DsTile tile;                  // emit: the tiled layout (npad 0: direct CSR stores)
 };
 hipError_t launch_ds_count(hipStream_t s, const DsDecodeArgs& a);
 hipError_t launch_ds_emit(hipStream_t s, const DsDecodeArgs& a);

@@ -147,31 +147,46 @@ struct CountSink {
   __device__ void put_end() {}
 };
 
-struct EmitSink {
+// TILE (Orswot, DsDecodeArgs.tile): every column entry goes to its file-minor scratch row
+// instead -- entry k of file i at tile.col[c][k * npad + i] -- so a wave's 64 files write 64
+// consecutive words per store when their files share a layout (k_ds_untile then writes the CSR
+// columns in order); the values (ids, counters, CSR offsets) are the same.
+template <bool TILE>
+struct EmitSinkT {
   const DsDecodeArgs* a;
   const uint8_t* p;
   uint32_t ia, iam, ir, irc, irm;
+  uint32_t ia0, iam0, ir0, irc0, irm0, file;  // TILE: the file's bases and index
   ActorCache cache;
-  __device__ void add_begin() { a->ops.add_mbeg[ia] = iam; }
-  __device__ void add_dot(uint64_t off, uint64_t c) {
-    a->ops.add_actor[ia] = lookup_actor(*a, p + off, &cache);
-    a->ops.add_ctr[ia] = c;
+  template <typename T>
+  __device__ __forceinline__ void put(T* col, int c, uint32_t idx, uint32_t base, T v) {
+    if (TILE) reinterpret_cast<T*>(a->tile.col[c])[(size_t)(idx - base) * a->tile.npad + file] = v;
+    else col[idx] = v;
   }
-  __device__ void add_member(uint64_t m) { a->ops.add_mem[iam++] = m; }
+  __device__ void add_begin() { put(a->ops.add_mbeg, 2, ia, ia0, iam); }
+  __device__ void add_dot(uint64_t off, uint64_t c) {
+    put(a->ops.add_actor, 0, ia, ia0, lookup_actor(*a, p + off, &cache));
+    put(a->ops.add_ctr, 1, ia, ia0, (unsigned long long)c);
+  }
+  __device__ void add_member(uint64_t m) { put(a->ops.add_mem, 3, iam, iam0, (unsigned long long)m); iam++; }
   __device__ void add_end() { ia++; }
   __device__ void rm_begin() {
-    a->ops.rm_cbeg[ir] = irc;
-    a->ops.rm_mbeg[ir] = irm;
+    put(a->ops.rm_cbeg, 4, ir, ir0, irc);
+    put(a->ops.rm_mbeg, 5, ir, ir0, irm);
   }
   __device__ void rm_dot(uint64_t off, uint64_t c) {
+    put(a->ops.rmc_actor, 6, irc, irc0, lookup_actor(*a, p + off, &cache));
+    put(a->ops.rmc_ctr, 7, irc, irc0, (unsigned long long)c);
+    irc++;
+  }
+  __device__ void rm_member(uint64_t m) { put(a->ops.rm_mem, 8, irm, irm0, (unsigned long long)m); irm++; }
+  __device__ void rm_end() { ir++; }
+  __device__ void put_begin() { a->ops.rm_cbeg[ir] = irc; }
+  __device__ void put_dot(uint64_t off, uint64_t c) {
     a->ops.rmc_actor[irc] = lookup_actor(*a, p + off, &cache);
     a->ops.rmc_ctr[irc] = c;
     irc++;
   }
-  __device__ void rm_member(uint64_t m) { a->ops.rm_mem[irm++] = m; }
-  __device__ void rm_end() { ir++; }
-  __device__ void put_begin() { a->ops.rm_cbeg[ir] = irc; }
-  __device__ void put_dot(uint64_t off, uint64_t c) { rm_dot(off, c); }
   __device__ void put_val(uint64_t v) { a->ops.put_val[ir] = v; }
   __device__ void put_end() { ir++; }
 };
@@ -312,26 +327,80 @@ __global__ void __launch_bounds__(kBlock) k_ds_count(DsDecodeArgs a) {
     }
     const bool keep = st == CE_OK && a.apply[i];
     for (int k = 0; k < kCntN; k++) a.cnt[(size_t)k * a.n + i] = keep ? cs.c[k] : 0u;
+    // the largest per-file count of each column (counters[8 + k]): the tiled emit's row count
+#pragma unroll
+    for (int k = 0; k < kCntN; k++) {
+      uint32_t m = keep ? cs.c[k] : 0u;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+      if ((threadIdx.x & 63) == 0 && m) atomicMax(a.counters + 8 + k, m);
+    }
   }
 }
 
+template <bool TILE>
 __global__ void __launch_bounds__(kBlock) k_ds_emit(DsDecodeArgs a) {
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < a.n; i += gridDim.x * kBlock) {
     if (a.status[i] != CE_OK || !a.apply[i]) continue;
     const uint32_t len = a.params[i].len;
     const uint8_t* p = a.pt + a.params[i].out_off + 16;
-    EmitSink es;
+    EmitSinkT<TILE> es;
     es.a = &a;
     es.p = p;
     // the bases are one exclusive scan over all kCntN columns back to back: column k's base is
     // its entry minus the column's first (u32 arithmetic: exact while a column's total < 2^32)
     auto base = [&](int k) { return a.cnt[(size_t)k * a.n + i] - a.cnt[(size_t)k * a.n]; };
-    es.ia = a.base_off[kCntAdd] + base(kCntAdd);
-    es.iam = a.base_off[kCntAddM] + base(kCntAddM);
-    es.ir = a.base_off[kCntRm] + base(kCntRm);
-    es.irc = a.base_off[kCntRmC] + base(kCntRmC);
-    es.irm = a.base_off[kCntRmM] + base(kCntRmM);
+    es.ia = es.ia0 = a.base_off[kCntAdd] + base(kCntAdd);
+    es.iam = es.iam0 = a.base_off[kCntAddM] + base(kCntAddM);
+    es.ir = es.ir0 = a.base_off[kCntRm] + base(kCntRm);
+    es.irc = es.irc0 = a.base_off[kCntRmC] + base(kCntRmC);
+    es.irm = es.irm0 = a.base_off[kCntRmM] + base(kCntRmM);
+    es.file = i;
     parse_file(a.kind, p, len - 16, es);
+  }
+}
+
+// The tiled emit's scratch rows -> the CSR columns, in order: block (x = 64-file tile, y =
+// column) stages the tile's rows (k < the tile's largest count) in LDS with coalesced reads, then
+// writes the tile's contiguous output range with coalesced stores (each output index finds its
+// file among the tile's 65 bases by binary search in LDS).
+__global__ void __launch_bounds__(kBlock) k_ds_untile(DsDecodeArgs a) {
+  __shared__ unsigned long long tile[kTileMaxRows * 64];
+  __shared__ uint32_t sb[65];
+  __shared__ uint32_t tmax;
+  const int c = blockIdx.y;
+  const int g = c == 0 || c == 1 || c == 2 ? kCntAdd : c == 3 ? kCntAddM : c == 4 || c == 5 ? kCntRm
+                : c == 6 || c == 7 ? kCntRmC : kCntRmM;
+  const bool wide = c == 1 || c == 3 || c == 7 || c == 8;
+  void* const dst[9] = {a.ops.add_actor, a.ops.add_ctr, a.ops.add_mbeg, a.ops.add_mem, a.ops.rm_cbeg,
+                        a.ops.rm_mbeg, a.ops.rmc_actor, a.ops.rmc_ctr, a.ops.rm_mem};
+  const uint32_t i0 = blockIdx.x * 64;
+  if (threadIdx.x == 0) tmax = 0;
+  if (threadIdx.x <= 64) {
+    const uint32_t i = i0 + threadIdx.x;
+    sb[threadIdx.x] = i < a.n ? a.cnt[(size_t)g * a.n + i] - a.cnt[(size_t)g * a.n] + a.base_off[g]
+                              : a.tile.total[g] + a.base_off[g];
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) atomicMax(&tmax, sb[threadIdx.x + 1] - sb[threadIdx.x]);
+  __syncthreads();
+  const uint32_t rows = tmax;  // <= kTileMaxRows (the host checked every column's largest count)
+  const size_t npad = a.tile.npad;
+  for (uint32_t x = threadIdx.x; x < rows * 64; x += kBlock) {
+    const size_t idx = (size_t)(x >> 6) * npad + i0 + (x & 63);
+    tile[x] = wide ? reinterpret_cast<const unsigned long long*>(a.tile.col[c])[idx]
+                   : reinterpret_cast<const uint32_t*>(a.tile.col[c])[idx];
+  }
+  __syncthreads();
+  const uint32_t lo = sb[0], hi = sb[64];
+  for (uint32_t j = lo + threadIdx.x; j < hi; j += kBlock) {
+    uint32_t l = 0;  // last file whose base <= j
+#pragma unroll
+    for (uint32_t step = 32; step > 0; step >>= 1)
+      if (sb[l + step] <= j) l += step;
+    const unsigned long long v = tile[(j - sb[l]) * 64 + l];
+    if (wide) reinterpret_cast<unsigned long long*>(dst[c])[j] = v;
+    else reinterpret_cast<uint32_t*>(dst[c])[j] = (uint32_t)v;
   }
 }
 
@@ -901,7 +970,12 @@ hipError_t launch_ds_count(hipStream_t s, const DsDecodeArgs& a) {
 
 hipError_t launch_ds_emit(hipStream_t s, const DsDecodeArgs& a) {
   if (a.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ds_emit, dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
+  if (a.tile.npad) {
+    hipLaunchKernelGGL(k_ds_emit<true>, dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(k_ds_untile, dim3((a.n + 63) / 64, 9), dim3(kBlock), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(k_ds_emit<false>, dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
+  }
   return hipGetLastError();
 }
 

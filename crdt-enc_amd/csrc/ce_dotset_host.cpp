@@ -50,6 +50,7 @@ struct DsState {
   uint32_t contig_cap = 0, contig_gen = 0;
   bool adds_contig = false;  // this batch's adds: every actor's adds one contiguous run
   DevBuf seal_out;           // the compaction's sealed file (ds_compact_device)
+  DevBuf tile_col[9];        // the tiled emit's file-minor scratch rows (k_ds_emit<true>)
   // device state reader (per state file: candidates, sorted heads, entry ends, Dot counts and
   // bases, members, sorted members [0..6]
   // and emitted (member, actor id, value) columns [7..9]), pinned staging for its downloads
@@ -935,7 +936,7 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
   hpo.name = "";
   HostPhase hps("ops: scan+emit");
   // 4) bases: exclusive scan of each count column
-  Counts k;
+  Counts k, kmax;
   {
     // one exclusive scan over the kCntN count columns back to back (the emit subtracts each
     // column's first base), the column totals by a one-block kernel, one small download
@@ -943,6 +944,7 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
     uint32_t* bases = cnt + (size_t)kCntN * n;
     uint32_t* dtot = d->cnt_tot.as<uint32_t>();
     uint32_t* htot = d->h_cnt.as<uint32_t>() + 32;
+    uint32_t* hmx = d->h_cnt.as<uint32_t>() + 16;  // largest per-file count per column (k_ds_count)
     if ((uint64_t)kCntN * n > 0x7fffffffull) return ctx->fail(CE_ERR_INVALID_ARG, "batch too large for one scan");
     size_t tb = 0;
     if ((e = d->cnt_tot.reserve(64)) || (e = ds_excl_sum_u32(nullptr, tb, cnt, bases, kCntN * n, ctx->stream)) ||
@@ -953,9 +955,13 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
     if ((e = ds_excl_sum_u32(d->cub_tmp.p, t, cnt, bases, kCntN * n, ctx->stream)) ||
         (e = launch_ds_col_totals(ctx->stream, cnt, bases, n, dtot)) ||
         (e = hipMemcpyAsync(htot, dtot, 4 * kCntN, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (e = hipMemcpyAsync(hmx, d->misses.as<uint32_t>() + 8, 4 * kCntN, hipMemcpyDeviceToHost, ctx->stream)) ||
         (e = stream_wait(ctx->stream)))
       return ctx->hip_fail(e, "scan");
-    for (int j = 0; j < kCntN; j++) k.v[j] = htot[j];
+    for (int j = 0; j < kCntN; j++) {
+      k.v[j] = htot[j];
+      kmax.v[j] = hmx[j];
+    }
   }
   // MVReg: the current values come first in the candidate list
   HostCols vc;
@@ -975,6 +981,32 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
   a = decode_args(c, n);
   a.cnt = d->cnt.as<uint32_t>() + (size_t)kCntN * n;  // bases
   for (int j = 0; j < kCntN; j++) a.base_off[j] = (uint32_t)base.v[j];
+  // Orswot: the tiled emit (file-minor scratch rows, then k_ds_untile) when every file's counts
+  // fit its LDS tile and the rows cost at most ~2x the columns (files of similar shape, as op
+  // files in load_ops order are); the direct per-lane stores otherwise
+  {
+    static const int kGroup[9] = {kCntAdd, kCntAdd, kCntAdd, kCntAddM, kCntRm, kCntRm, kCntRmC, kCntRmC, kCntRmM};
+    static const uint32_t kElem[9] = {4, 8, 4, 8, 4, 4, 4, 8, 8};
+    const uint64_t npad = (n + 63ull) & ~63ull;
+    bool tile = c->kind == CE_STATE_ORSWOT && !getenv("CE_DS_EMIT_DIRECT");
+    uint64_t rows_bytes = 0, cols_bytes = 0;
+    for (int cc = 0; cc < 9 && tile; cc++) {
+      const uint64_t mx = kmax.v[kGroup[cc]];
+      if (mx > kTileMaxRows || mx * npad >= (1ull << 32)) tile = false;
+      rows_bytes += mx * npad * kElem[cc];
+      cols_bytes += k.v[kGroup[cc]] * kElem[cc];
+    }
+    if (tile && rows_bytes > 2 * cols_bytes + (1ull << 20)) tile = false;
+    if (tile) {
+      for (int cc = 0; cc < 9; cc++) {
+        if ((e = d->tile_col[cc].reserve(kmax.v[kGroup[cc]] * npad * kElem[cc] + 64))) return ctx->hip_fail(e, "emit tile");
+        a.tile.col[cc] = d->tile_col[cc].p;
+      }
+      a.tile.npad = npad;
+      for (int j = 0; j < kCntN; j++) a.tile.total[j] = (uint32_t)k.v[j];
+      c->path_counts["ds_emit_tiled"]++;
+    }
+  }
   for (int round = 0;; round++) {
     uint32_t hm[4];
     if ((e = hipMemsetAsync(d->misses.p, 0, 64, ctx->stream))) return ctx->hip_fail(e, "emit");

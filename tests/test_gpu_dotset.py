@@ -782,3 +782,31 @@ def test_compact_into_async_overlaps_next_ingest(ctx):
         assert st == 0 and pt == want[r]
     core.compact_wait(tickets[0][1])   # waiting twice is fine
     core.close()
+
+
+@pytest.mark.parametrize("adversarial", [False, True])
+def test_orswot_tiled_emit_equals_direct(ctx, adversarial):
+    """The op decode's tiled emit (file-minor scratch rows, then k_ds_untile into the CSR
+    columns) == the direct per-lane stores (CE_DS_EMIT_DIRECT=1) == the oracle, on uniform and on
+    ragged files (op counts 1-10 per file, empty member lists, multi-entry removal clocks)."""
+    rng = random.Random(616 + adversarial)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 11)
+    files = gen("orswot", rng, actors, 5, 10, 300, adversarial)
+    acts, clears, fa, fv = G.batch(files, "orswot", APP)
+    sealed = seal_files(ctx, key, clears)
+    oc = C.Core("orswot")
+    assert oc.read_remote_ops(key, [APP], sealed, [acts[i] for i in fa], fv)[0] == 0
+    got = {}
+    for direct in (False, True):
+        if direct:
+            os.environ["CE_DS_EMIT_DIRECT"] = "1"
+        try:
+            core = new_core(ctx, "orswot", key)
+            assert core.ingest_ops(sealed, acts, fa, fv)[0] == 0
+            got[direct] = (core.state_bytes(), core.path_count("ds_emit_tiled"))
+            core.close()
+        finally:
+            os.environ.pop("CE_DS_EMIT_DIRECT", None)
+    assert got[False][0] == got[True][0] == oc.serialize()
+    assert got[False][1] == 1 and got[True][1] == 0
