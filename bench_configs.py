@@ -57,6 +57,7 @@ assert (len(ADD_T), len(RM_T), PT_LEN) == (62, 55, 1961)
 
 
 HOST_PROF = bool(os.environ.get("CE_HOST_PROF"))
+NO_NAMES = bool(os.environ.get("CE_C3_NO_NAMES"))
 KEY = bytes(np.random.default_rng(7).integers(0, 256, 32, dtype=np.uint8))  # latest data key
 
 
@@ -156,6 +157,8 @@ class CompactPipe:
     def _name(self, k, ln, tk):
         self.core.compact_wait(tk)
         self.last_file = self.obuf[k][:ln]
+        if NO_NAMES:    # diagnostics only: the step without the host's SHA3 load beside it
+            return
         self.fut[k] = self.namer.submit(crdtenc.content_name, self.last_file)
         self.order.append(self.fut[k])
 

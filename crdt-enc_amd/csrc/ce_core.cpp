@@ -726,7 +726,17 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
     return ctx->hip_fail(e, "gate upload");
 
   // 1) GPU: scratch initialisation (one launch: counters, gate, batch state, miss / redo
-  //    marks), setup (outer version, envelope, key schedule), device gate
+  //    marks), device gate, setup (outer version, envelope, key schedule)
+  static const bool gate_after_setup = getenv("CE_GATE_AFTER_SETUP") != nullptr;
+  auto launch_gate_now = [&]() -> int {
+    if ((e = hipStreamWaitEvent(ctx->stream, ctx->up_ev, 0))) return ctx->hip_fail(e, "gate upload");
+    const int t = ctx->tbegin("gate");
+    if ((e = sharded ? launch_gate_window(ctx->stream, ga, shard_hi, ctx->counters.as<uint32_t>())
+                     : launch_gate(ctx->stream, ga)))
+      return ctx->hip_fail(e, "gate");
+    ctx->tend(t);
+    return CE_OK;
+  };
   uint32_t ec;
   {
     FillArgs fl{};
@@ -735,10 +745,20 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
     fl.r[2] = {ctx->refold.as<uint32_t>(), (n + 3ull) / 4, 0u};
     fl.r[3] = {ctx->redo.as<uint32_t>(), (n + 3ull) / 4, 0u};
     fl.n = 4;
-    // device_open's setup only; the fused kernel replaces its segment pass for small files
-    int rr = device_open_setup(ctx, d_blob, d_offs, n, blob_len, true, key, ctx->status.as<int32_t>(),
-                               &ec, &fl);
-    if (rr) return rr;
+    // device_open's setup only; the fused kernel replaces its segment pass for small files.
+    // The gate between the fill and the setup (it needs the filled gate block and the uploaded
+    // e0, not the setup), so the setup runs straight into the fused kernel (CE_GATE_AFTER_SETUP:
+    // the order before, for A/B)
+    if (!gate_after_setup) {
+      const std::function<int()> gate = launch_gate_now;
+      int rr = device_open_setup(ctx, d_blob, d_offs, n, blob_len, true, key, ctx->status.as<int32_t>(),
+                                 &ec, &fl, &gate);
+      if (rr) return rr;
+    } else {
+      int rr = device_open_setup(ctx, d_blob, d_offs, n, blob_len, true, key, ctx->status.as<int32_t>(),
+                                 &ec, &fl);
+      if (rr) return rr;
+    }
   }
   // the setup's counters (large-file count [9]) -> host behind an event: read while the fused
   // kernel runs, they decide whether the multi-page kernels are launched at all
@@ -755,13 +775,9 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
     return ctx->hip_fail(e, "setup counters");
   bool setup_known = false;
   uint32_t n_large = 0;
-  if ((e = hipStreamWaitEvent(ctx->stream, ctx->up_ev, 0))) return ctx->hip_fail(e, "gate upload");
-  {
-    const int t = ctx->tbegin("gate");
-    if ((e = sharded ? launch_gate_window(ctx->stream, ga, shard_hi, ctx->counters.as<uint32_t>())
-                     : launch_gate(ctx->stream, ga)))
-      return ctx->hip_fail(e, "gate");
-    ctx->tend(t);
+  if (gate_after_setup) {
+    const int rg = launch_gate_now();
+    if (rg) return rg;
   }
   DecodeArgs da{};
   da.pt = ctx->out.as<uint8_t>();

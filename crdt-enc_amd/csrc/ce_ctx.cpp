@@ -108,7 +108,7 @@ static hipError_t reset_counters(ce_ctx* ctx) {
 
 int device_open_setup(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
                       uint64_t blob_len, bool outer, const KeyRef& key, int32_t* d_status,
-                      uint32_t* extra_cap, FillArgs* fills) {
+                      uint32_t* extra_cap, FillArgs* fills, const std::function<int()>* after_fill) {
   int rc = reserve_batch(ctx, n, blob_len, extra_cap);
   if (rc) return rc;
   hipError_t e;
@@ -118,6 +118,9 @@ int device_open_setup(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs
   } else if ((e = reset_counters(ctx)) != hipSuccess) {
     return ctx->hip_fail(e, "memset counters");
   }
+  // the caller's launches that need the filled scratch but not the setup (the version gate):
+  // the setup then runs straight into the kernel that consumes it
+  if (after_fill && (rc = (*after_fill)())) return rc;
   SegScratch sc = segscratch(ctx, *extra_cap);
   const int t = ctx->tbegin("open_setup");
   if ((e = launch_open_setup(ctx->stream, d_blob, d_offs, n, outer, dev_key(key), key_status(key),

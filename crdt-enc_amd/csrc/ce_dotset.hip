@@ -295,6 +295,12 @@ __device__ int parse_file(int kind, const uint8_t* p, uint64_t n, S& sink) {
 }
 
 __global__ void __launch_bounds__(kBlock) k_ds_count(DsDecodeArgs a) {
+  __shared__ uint32_t smax[kCntN];
+  if (threadIdx.x < kCntN) smax[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t mx[kCntN];
+#pragma unroll
+  for (int k = 0; k < kCntN; k++) mx[k] = 0;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < a.n; i += gridDim.x * kBlock) {
     CountSink cs;
     int32_t st = a.status[i];
@@ -327,15 +333,20 @@ __global__ void __launch_bounds__(kBlock) k_ds_count(DsDecodeArgs a) {
     }
     const bool keep = st == CE_OK && a.apply[i];
     for (int k = 0; k < kCntN; k++) a.cnt[(size_t)k * a.n + i] = keep ? cs.c[k] : 0u;
-    // the largest per-file count of each column (counters[8 + k]): the tiled emit's row count
 #pragma unroll
-    for (int k = 0; k < kCntN; k++) {
-      uint32_t m = keep ? cs.c[k] : 0u;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
-      if ((threadIdx.x & 63) == 0 && m) atomicMax(a.counters + 8 + k, m);
-    }
+    for (int k = 0; k < kCntN; k++) mx[k] = max(mx[k], keep ? cs.c[k] : 0u);
   }
+  // the largest per-file count of each column (counters[8 + k]): the tiled emit's row count;
+  // reduced per wave, then per block in LDS, so each block adds one global atomic per column
+#pragma unroll
+  for (int k = 0; k < kCntN; k++) {
+    uint32_t m = mx[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+    if ((threadIdx.x & 63) == 0 && m) atomicMax(&smax[k], m);
+  }
+  __syncthreads();
+  if (threadIdx.x < kCntN && smax[threadIdx.x]) atomicMax(a.counters + 8 + threadIdx.x, smax[threadIdx.x]);
 }
 
 template <bool TILE>

@@ -2086,10 +2086,24 @@ int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t
     if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming))) return x->hip_fail(e, "ds compact download");
     if (c->copy_slot_ticket[slot] && (e = hipEventSynchronize(ev)))  // the slot's previous copy
       return x->hip_fail(e, "ds compact download");
+    // the caller's pinned buffer mapped into the device's address space: a copy kernel on a
+    // few CUs writes it, so the next batch's kernels run beside the download (the runtime's
+    // D2H blit would occupy every CU); other memory through the runtime's copy
+    void* mapped = nullptr;
+    {
+      hipPointerAttribute_t pa{};
+      if (hipPointerGetAttributes(&pa, to) == hipSuccess && pa.type == hipMemoryTypeHost && pa.devicePointer &&
+          !((reinterpret_cast<uintptr_t>(pa.devicePointer) | reinterpret_cast<uintptr_t>(d->seal_out.p)) & 15) &&
+          !getenv("CE_ASYNC_BLIT"))
+        mapped = pa.devicePointer;
+      (void)hipGetLastError();  // an unregistered pointer leaves an error behind
+    }
     if ((e = hipEventRecord(x->side_ev, s)) || (e = hipStreamWaitEvent(c->copy_stream, x->side_ev, 0)) ||
-        (e = hipMemcpyAsync(to, d->seal_out.p, total, hipMemcpyDeviceToHost, c->copy_stream)) ||
+        (e = mapped ? launch_copy_bytes(c->copy_stream, static_cast<uint8_t*>(mapped), d->seal_out.as<uint8_t>(), total, 32)
+                    : hipMemcpyAsync(to, d->seal_out.p, total, hipMemcpyDeviceToHost, c->copy_stream)) ||
         (e = hipEventRecord(ev, c->copy_stream)))
       return x->hip_fail(e, "ds compact download");
+    if (mapped) c->path_counts["compact_async_kernel_copy"]++;
     c->copy_slot_ticket[slot] = t;
     c->copy_last = ev;
     c->sink_ticket = t;

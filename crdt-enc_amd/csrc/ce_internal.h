@@ -214,7 +214,8 @@ DevKey dev_key(const KeyRef& k);
 // per-file statuses and ctx->params the FileParams; counters are copied to h_counters.
 int device_open_setup(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
                       uint64_t blob_len, bool outer, const KeyRef& key, int32_t* d_status,
-                      uint32_t* extra_cap, FillArgs* fills = nullptr);
+                      uint32_t* extra_cap, FillArgs* fills = nullptr,
+                      const std::function<int()>* after_fill = nullptr);
 SegScratch segscratch(ce_ctx* ctx, uint32_t extra_cap);
 int device_open(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
                 uint64_t blob_len, bool outer, const KeyRef& key, uint8_t* d_out,

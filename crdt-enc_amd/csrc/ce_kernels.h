@@ -69,6 +69,9 @@ struct FillArgs {
   uint32_t* counters;  // or null
 };
 hipError_t launch_fill(hipStream_t s, const FillArgs& a);
+// dst <- src (n bytes; both 16-byte aligned) by `blocks` workgroups (dst may be mapped pinned host
+// memory: the device-to-host copy that leaves the rest of the GPU to other streams)
+hipError_t launch_copy_bytes(hipStream_t s, uint8_t* dst, const uint8_t* src, uint64_t n, uint32_t blocks);
 
 // file-level open: outer version check (when outer), envelope parse, key schedule.
 hipError_t launch_open_setup(hipStream_t s, const uint8_t* blob, const uint64_t* offs,

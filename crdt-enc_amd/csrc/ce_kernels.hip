@@ -1278,6 +1278,24 @@ __global__ void k_fill(FillArgs a) {
     f.p[i] = f.value;
 }
 
+// dst <- src, n bytes, with a small grid: a device-to-host copy into mapped pinned memory that
+// leaves most of the GPU to the work queued on other streams (the runtime's blit kernel for a
+// large D2H copy covers every CU for its whole duration)
+__global__ void __launch_bounds__(256) k_copy_bytes(uint8_t* dst, const uint8_t* src, uint64_t n) {
+  const uint64_t n16 = n / 16;
+  const uint64_t gt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = gt; i < n16; i += gs)
+    reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+  for (uint64_t i = 16 * n16 + gt; i < n; i += gs) dst[i] = src[i];
+}
+
+hipError_t launch_copy_bytes(hipStream_t s, uint8_t* dst, const uint8_t* src, uint64_t n, uint32_t blocks) {
+  if (n == 0) return hipSuccess;
+  if ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_copy_bytes, dim3(blocks), dim3(256), 0, s, dst, src, n);
+  return hipGetLastError();
+}
+
 hipError_t launch_fill(hipStream_t s, const FillArgs& a) {
   uint64_t mx = 16;
   for (int i = 0; i < a.n; i++) mx = a.r[i].words > mx ? a.r[i].words : mx;
