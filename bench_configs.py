@@ -58,6 +58,34 @@ assert (len(ADD_T), len(RM_T), PT_LEN) == (62, 55, 1961)
 
 HOST_PROF = bool(os.environ.get("CE_HOST_PROF"))
 NO_NAMES = bool(os.environ.get("CE_C3_NO_NAMES"))
+
+
+class _StepMarks:
+    """CE_ROCTX=1: each timed step as a ROCTx range "c3_step" (rocprofv3 --marker-trace), so the
+    trace tools (tools/c3_step_breakdown.py, c3_host_trace.py) cut exactly the timed steps"""
+
+    def __init__(self):
+        self.lib = None
+        if os.environ.get("CE_ROCTX"):
+            import ctypes
+            for name in ("librocprofiler-sdk-roctx.so", "/opt/rocm/lib/librocprofiler-sdk-roctx.so"):
+                try:
+                    self.lib = ctypes.CDLL(name)   # the ROCTx rocprofv3 --marker-trace intercepts
+                    break
+                except OSError:
+                    pass
+            self.lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+
+    def push(self):
+        if self.lib:
+            self.lib.roctxRangePushA(b"c3_step")
+
+    def pop(self):
+        if self.lib:
+            self.lib.roctxRangePop()
+
+
+MARKS = _StepMarks()
 KEY = bytes(np.random.default_rng(7).integers(0, 256, 32, dtype=np.uint8))  # latest data key
 
 
@@ -155,7 +183,7 @@ class CompactPipe:
         self.last_file = None
 
     def _name(self, k, ln, tk):
-        self.core.compact_wait(tk)
+        ln = self.core.compact_wait(tk) if tk else ln
         self.last_file = self.obuf[k][:ln]
         if NO_NAMES:    # diagnostics only: the step without the host's SHA3 load beside it
             return
@@ -345,7 +373,9 @@ def run_c3(args, ctx, dev):
     ctx.set_timing(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        MARKS.push()
         step()
+        MARKS.pop()
     pipe.flush()                 # every sealed file downloaded
     t_loop = time.perf_counter()
     out["name"] = pipe.drain()   # and named

@@ -764,8 +764,9 @@ class Core:
         return buf, n.value, (nm.value.decode() if name else None)
 
     def compact_into_async(self, buf, nonce=None):
-        """compact_into with the download left in flight: (length, ticket); read buf[:length]
-        only after compact_wait(ticket).  Raises when the file does not fit."""
+        """compact_into with the download left in flight: (length, ticket).  ticket 0: the file
+        is already in buf[:length]; else length is 0 and compact_wait(ticket) returns it once the
+        file is in buf (pinned buf; raises then when the file did not fit)."""
         n = ctypes.c_size_t(0)
         t = ctypes.c_uint64(0)
         rc = lib().ce_core_compact_into_async(self.p, _cbuf(nonce) if nonce is not None else None,
@@ -775,7 +776,10 @@ class Core:
         return n.value, t.value
 
     def compact_wait(self, ticket):
-        self.ctx.check(lib().ce_core_compact_wait(self.p, ctypes.c_uint64(ticket)), "compact_wait")
+        """the length of the file compact_into_async(ticket) left in flight, once it is complete"""
+        n = ctypes.c_uint64(0)
+        self.ctx.check(lib().ce_core_compact_wait(self.p, ctypes.c_uint64(ticket), ctypes.byref(n)), "compact_wait")
+        return n.value
 
     def apply_ops(self, ops_msgpack):
         return lib().ce_core_apply_ops(self.p, _cbuf(ops_msgpack), ctypes.c_size_t(len(ops_msgpack)))

@@ -1877,21 +1877,28 @@ int ce_core_compact_into_async(ce_core* c, const uint8_t* nonce, uint8_t* dst, s
   return rc;
 }
 
-int ce_core_compact_wait(ce_core* c, uint64_t ticket) {
+int ce_core_compact_wait(ce_core* c, uint64_t ticket, uint64_t* len) {
   if (!c) return CE_ERR_INVALID_ARG;
   if (ticket == 0) return CE_OK;
   hipEvent_t ev = nullptr;
+  uint32_t slot;
   {
     std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
     if (ticket > c->copy_next) return CE_ERR_INVALID_ARG;
-    const uint32_t slot = (uint32_t)(ticket % ce_core::kAsyncSlots);
-    if (c->copy_slot_ticket[slot] != ticket) return CE_OK;  // the slot was reused: synchronised then
+    slot = (uint32_t)(ticket % ce_core::kAsyncSlots);
+    if (c->copy_slot_ticket[slot] != ticket)  // the slot was reused (synchronised then): its length is gone
+      return len ? c->ctx->fail(CE_ERR_INVALID_ARG, "compact ticket expired") : CE_OK;
     ev = c->copy_ev[slot];
   }
   // outside the context lock: other calls on this core may proceed meanwhile (the event stays
   // alive until the core is closed)
   const hipError_t e = hipEventSynchronize(ev);
-  return e ? c->ctx->hip_fail(e, "compact wait") : CE_OK;
+  if (e) return c->ctx->hip_fail(e, "compact wait");
+  const uint64_t n = c->copy_len.as<volatile uint64_t>()[slot];
+  if (n == ~1ull) return c->ctx->fail(CE_ERR_DEVICE, "serializer overran its bound");
+  if (n == ~0ull) return c->ctx->fail(CE_ERR_INVALID_ARG, "compact_into_async: buffer too small");
+  if (len) *len = n;
+  return CE_OK;
 }
 
 int ce_core_compact(ce_core* c, char name_out[64]) {

@@ -83,6 +83,9 @@ struct ce_core {
   uint64_t copy_slot_ticket[kAsyncSlots] = {};
   uint64_t copy_next = 0;                 // last ticket handed out
   hipEvent_t copy_last = nullptr;         // the newest in-flight copy's event
+  // pinned, mapped: per slot, the file length the device copy wrote (ce_core_compact_wait)
+  ce::HostBuf copy_len;
+  uint64_t* copy_len_dev = nullptr;
   std::vector<uint32_t> sorted_slots;   // used slots in UUID byte order (BTreeMap order)
   uint64_t sorted_gen = ~0ull;
   std::vector<uint8_t> last_writers;    // writer list of the previous ingest and its slots

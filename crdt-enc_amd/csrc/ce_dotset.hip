@@ -944,19 +944,47 @@ hipError_t ds_excl_sum_u32(void* tmp, size_t& tb, const uint32_t* in, uint32_t* 
   return hipcub::DeviceScan::ExclusiveSum(tmp, tb, in, out, (int)n, s);
 }
 
-// per column of the back-to-back scan: total = last base + last count - first base
-__global__ void k_ds_col_totals(const uint32_t* cnt, const uint32_t* bases, uint32_t n, uint32_t* out) {
+// One block after the count pass and its scan, so the host reads everything the emit's sizing
+// needs in one download: out[0..kCntN) column totals (last base + last count - first base),
+// out[8..8+kCntN) the largest per-file count of each column (k_ds_count's counters[8..]),
+// out[13..16) the status summary: files not OK, files left to the host envelope parser, files
+// left to the host op decoder; out[16] the first file not OK (0xffffffff: none)
+__global__ void __launch_bounds__(1024) k_ds_col_totals(const uint32_t* cnt, const uint32_t* bases, uint32_t n,
+                                                        const uint32_t* maxima, const int32_t* status, uint32_t* out) {
+  __shared__ uint32_t acc[4];
   const uint32_t k = threadIdx.x;
+  if (k < 3) acc[k] = 0;
+  if (k == 3) acc[3] = 0xffffffffu;
   if (k < kCntN) {
     const size_t c0 = (size_t)k * n, cl = c0 + n - 1;
     out[k] = bases[cl] + cnt[cl] - bases[c0];
+    out[8 + k] = maxima[k];
   }
+  __syncthreads();
+  uint32_t bad = 0, hp = 0, hd = 0, first = 0xffffffffu;
+  for (uint32_t i = k; i < n; i += blockDim.x) {
+    const int32_t st = status[i];
+    if (st != CE_OK) {
+      bad++;
+      hp += st == kStatusHostParse;
+      hd += st == kStatusHostDecode;
+      first = min(first, i);
+    }
+  }
+  if (bad) {
+    atomicAdd(&acc[0], bad);
+    if (hp) atomicAdd(&acc[1], hp);
+    if (hd) atomicAdd(&acc[2], hd);
+    atomicMin(&acc[3], first);
+  }
+  __syncthreads();
+  if (k < 4) out[13 + k] = acc[k];
 }
 
 hipError_t launch_ds_col_totals(hipStream_t s, const uint32_t* cnt, const uint32_t* bases, uint32_t n,
-                                uint32_t* out) {
+                                const uint32_t* maxima, const int32_t* status, uint32_t* out) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ds_col_totals, dim3(1), dim3(64), 0, s, cnt, bases, n, out);
+  hipLaunchKernelGGL(k_ds_col_totals, dim3(1), dim3(1024), 0, s, cnt, bases, n, maxima, status, out);
   return hipGetLastError();
 }
 

@@ -150,7 +150,7 @@ int collect(ce_core* c, uint32_t* n_live, unsigned long long* max_member = nullp
   hipError_t e;
   if ((e = d->col[0].reserve(cap * 8 + 64)) || (e = d->col[1].reserve(cap * 4 + 64)) ||
       (e = d->col[2].reserve(cap * 8 + 64)) || (e = d->col[5].reserve(64 + 8ull * kCollectBlocks)) ||
-      (e = d->h_cnt.reserve(256)))
+      (e = d->h_cnt.reserve(512)))
     return ctx->hip_fail(e, "collect");
   uint32_t* cnt = d->col[5].as<uint32_t>();
   uint32_t* hc = d->h_cnt.as<uint32_t>() + 48;  // pinned: [0] count, [2..3] max member
@@ -854,7 +854,7 @@ int ds_init(ce_core* c) {
   c->ds = new DsState();
   c->ds->kind = c->kind;
   hipError_t e;
-  if ((e = c->ds->misses.reserve(64 + kMissCap * 16ull)) || (e = c->ds->h_cnt.reserve(256)))
+  if ((e = c->ds->misses.reserve(64 + kMissCap * 16ull)) || (e = c->ds->h_cnt.reserve(512)))
     return c->ctx->hip_fail(e, "dot-set init");
   int rc = ensure_clock(c);
   if (rc) return rc;
@@ -897,71 +897,75 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
   if ((rc = device_open(ctx, d_blob, d_offs, n, blob_len, true, key_of(c), ctx->out.as<uint8_t>(),
                         ctx->status.as<int32_t>(), false, true)))
     return rc;
-  // 2) version gate -> apply flags (decode errors reject the batch whatever the gate says); its
-  //    flags and next versions come back with the open's statuses (one wait)
+  // 2) version gate -> apply flags (decode errors reject the batch whatever the gate says),
+  // 3) data version + Vec<S::Op> decode, count pass, 4) bases: one exclusive scan over the kCntN
+  // count columns back to back (the emit subtracts each column's first base), then one block for
+  // the column totals, maxima and a status summary.  The gate's flags and next versions and that
+  // block come back in ONE wait; the statuses themselves only when a file is not OK.  Files left
+  // to the host (envelope or op decoder) or a batch outside the device gate's shape: resolve on
+  // the host, then the count pass again.
   uint32_t first_gap = n;
   std::vector<uint64_t> expect;
   GateJob gj;
   if ((rc = gate_enqueue(c, d_fa, d_fv, n, m, wslot, &expect, &gj))) return rc;
-  std::vector<int32_t> st(n);
-  if ((e = hipMemcpyAsync(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
-      (e = stream_wait(ctx->stream)))
-    return ctx->hip_fail(e, "status");
-  for (uint32_t i = 0; i < n; i++)
-    if (st[i] == kStatusHostParse) {
-      if ((rc = resolve_host_parse(c, d_blob, d_offs, n, true))) return rc;
-      break;
-    }
-  if ((rc = gate_finish(c, d_fa, d_fv, n, m, gj, &first_gap, &expect))) return rc;
-  // 3) data version + Vec<S::Op> decode, count pass
   DsDecodeArgs a = decode_args(c, n);
-  if ((e = hipMemsetAsync(d->misses.p, 0, 64, ctx->stream))) return ctx->hip_fail(e, "count");
-  const int tc = ctx->tbegin("ds_count");
-  if ((e = launch_ds_count(ctx->stream, a))) return ctx->hip_fail(e, "count");
-  ctx->tend(tc);
-  if ((e = hipMemcpyAsync(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
-      (e = stream_wait(ctx->stream)))
-    return ctx->hip_fail(e, "count");
-  bool host_dec = false;
-  for (uint32_t i = 0; i < n; i++) host_dec = host_dec || st[i] == kStatusHostDecode;
-  if (host_dec) {
-    if ((rc = resolve_host_decode(c, n, &st))) return rc;
-    if ((e = launch_ds_count(ctx->stream, a)) ||
-        (e = hipMemcpyAsync(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
-        (e = stream_wait(ctx->stream)))
-      return ctx->hip_fail(e, "count");
+  if ((uint64_t)kCntN * n > 0x7fffffffull) return ctx->fail(CE_ERR_INVALID_ARG, "batch too large for one scan");
+  uint32_t* cnt = d->cnt.as<uint32_t>();
+  uint32_t* bases = cnt + (size_t)kCntN * n;
+  {
+    size_t tb = 0;
+    if ((e = d->cnt_tot.reserve(128)) || (e = ds_excl_sum_u32(nullptr, tb, cnt, bases, kCntN * n, ctx->stream)) ||
+        (e = d->cub_tmp.reserve(tb + 256)))
+      return ctx->hip_fail(e, "scan");
   }
-  if ((rc = fail_first(c, st, status_out, n))) return rc;  // all-or-nothing (lib.rs:497-514)
+  uint32_t* hsum = d->h_cnt.as<uint32_t>() + 64;  // pinned: the col_totals block (17 words)
+  auto count_pass = [&]() -> int {
+    if (n == 0) {
+      std::memset(hsum, 0, 17 * 4);
+      return CE_OK;
+    }
+    size_t t = d->cub_tmp.cap;
+    if ((e = hipMemsetAsync(d->misses.p, 0, 64, ctx->stream))) return ctx->hip_fail(e, "count");
+    const int tc = ctx->tbegin("ds_count");
+    if ((e = launch_ds_count(ctx->stream, a))) return ctx->hip_fail(e, "count");
+    ctx->tend(tc);
+    if ((e = ds_excl_sum_u32(d->cub_tmp.p, t, cnt, bases, kCntN * n, ctx->stream)) ||
+        (e = launch_ds_col_totals(ctx->stream, cnt, bases, n, d->misses.as<uint32_t>() + 8, ctx->status.as<int32_t>(),
+                                  d->cnt_tot.as<uint32_t>())) ||
+        (e = hipMemcpyAsync(hsum, d->cnt_tot.p, 17 * 4, hipMemcpyDeviceToHost, ctx->stream)))
+      return ctx->hip_fail(e, "count");
+    return CE_OK;
+  };
+  auto wait = [&](const char* what) { return (e = stream_wait(ctx->stream)) ? ctx->hip_fail(e, what) : CE_OK; };
+  if ((rc = count_pass()) || (rc = wait("count"))) return rc;
+  bool recount = false;
+  if (hsum[14]) {  // envelopes left to the host: normalize + open there, patch the batch
+    if ((rc = resolve_host_parse(c, d_blob, d_offs, n, true))) return rc;
+    recount = true;
+  }
+  recount = recount || gj.hf[0];  // not in load_ops shape: the host gate rewrites the apply flags
+  if ((rc = gate_finish(c, d_fa, d_fv, n, m, gj, &first_gap, &expect))) return rc;
+  if (recount && ((rc = count_pass()) || (rc = wait("count")))) return rc;
+  if (hsum[15]) {  // op vectors left to the host decoder: re-encode compactly, count again
+    std::vector<int32_t> st(n);
+    if ((e = hipMemcpyAsync(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (rc = wait("count")) || (rc = resolve_host_decode(c, n, &st)) || (rc = count_pass()) || (rc = wait("count")))
+      return rc ? rc : ctx->hip_fail(e, "count");
+  }
+  if (hsum[13] || status_out) {  // a file not OK (all-or-nothing, lib.rs:497-514), or asked for
+    std::vector<int32_t> st(n);
+    if ((e = hipMemcpyAsync(st.data(), ctx->status.p, n * 4ull, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (rc = wait("status")))
+      return rc ? rc : ctx->hip_fail(e, "status");
+    if ((rc = fail_first(c, st, status_out, n))) return rc;
+  }
   hpo.~HostPhase();
   hpo.name = "";
   HostPhase hps("ops: scan+emit");
-  // 4) bases: exclusive scan of each count column
   Counts k, kmax;
-  {
-    // one exclusive scan over the kCntN count columns back to back (the emit subtracts each
-    // column's first base), the column totals by a one-block kernel, one small download
-    uint32_t* cnt = d->cnt.as<uint32_t>();
-    uint32_t* bases = cnt + (size_t)kCntN * n;
-    uint32_t* dtot = d->cnt_tot.as<uint32_t>();
-    uint32_t* htot = d->h_cnt.as<uint32_t>() + 32;
-    uint32_t* hmx = d->h_cnt.as<uint32_t>() + 16;  // largest per-file count per column (k_ds_count)
-    if ((uint64_t)kCntN * n > 0x7fffffffull) return ctx->fail(CE_ERR_INVALID_ARG, "batch too large for one scan");
-    size_t tb = 0;
-    if ((e = d->cnt_tot.reserve(64)) || (e = ds_excl_sum_u32(nullptr, tb, cnt, bases, kCntN * n, ctx->stream)) ||
-        (e = d->cub_tmp.reserve(tb + 256)))
-      return ctx->hip_fail(e, "scan");
-    dtot = d->cnt_tot.as<uint32_t>();
-    size_t t = d->cub_tmp.cap;
-    if ((e = ds_excl_sum_u32(d->cub_tmp.p, t, cnt, bases, kCntN * n, ctx->stream)) ||
-        (e = launch_ds_col_totals(ctx->stream, cnt, bases, n, dtot)) ||
-        (e = hipMemcpyAsync(htot, dtot, 4 * kCntN, hipMemcpyDeviceToHost, ctx->stream)) ||
-        (e = hipMemcpyAsync(hmx, d->misses.as<uint32_t>() + 8, 4 * kCntN, hipMemcpyDeviceToHost, ctx->stream)) ||
-        (e = stream_wait(ctx->stream)))
-      return ctx->hip_fail(e, "scan");
-    for (int j = 0; j < kCntN; j++) {
-      k.v[j] = htot[j];
-      kmax.v[j] = hmx[j];
-    }
+  for (int j = 0; j < kCntN; j++) {
+    k.v[j] = hsum[j];
+    kmax.v[j] = hsum[8 + j];
   }
   // MVReg: the current values come first in the candidate list
   HostCols vc;
@@ -2058,6 +2062,53 @@ int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t
   rc = device_seal(x, db, reinterpret_cast<const uint64_t*>(offs), 1, U, db + A + 56, db + A + 32,
                    d->seal_out.as<uint8_t>(), reinterpret_cast<const uint64_t*>(db + A + 16), key);
   if (rc) return rc;
+  // compact_into_async into a pinned buffer: no host round trip at all -- a copy kernel on the
+  // copy stream reads the clear length on the device, copies the sealed file into the caller's
+  // mapped buffer on a few CUs (the next batch's kernels run beside it) and writes the file's
+  // length into a pinned slot ce_core_compact_wait reads.  The clear length travels in
+  // seal_out's tail (the context's blob is the next batch's staging area).
+  if (c->sink_async && c->sink && !getenv("CE_ASYNC_BLIT")) {
+    void* mapped = nullptr;
+    hipPointerAttribute_t pa{};
+    if (hipPointerGetAttributes(&pa, c->sink) == hipSuccess && pa.type == hipMemoryTypeHost && pa.devicePointer &&
+        !(reinterpret_cast<uintptr_t>(pa.devicePointer) & 15))
+      mapped = pa.devicePointer;
+    (void)hipGetLastError();  // an unregistered pointer leaves an error behind
+    if (mapped) {
+      cph = std::make_unique<HostPhase>("  cd: async download");
+      if ((!c->copy_stream && (e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking))) ||
+          (!x->side_ev && (e = hipEventCreateWithFlags(&x->side_ev, hipEventDisableTiming))))
+        return x->hip_fail(e, "ds compact download");
+      if (!c->copy_len_dev) {
+        void* dp = nullptr;
+        if ((e = c->copy_len.reserve(8ull * ce_core::kAsyncSlots)) || (e = hipHostGetDevicePointer(&dp, c->copy_len.p, 0)))
+          return x->hip_fail(e, "ds compact download");
+        c->copy_len_dev = static_cast<uint64_t*>(dp);
+      }
+      const uint64_t t = ++c->copy_next;
+      const uint32_t slot = (uint32_t)(t % ce_core::kAsyncSlots);
+      hipEvent_t& ev = c->copy_ev[slot];
+      if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming))) return x->hip_fail(e, "ds compact download");
+      if (c->copy_slot_ticket[slot] && (e = hipEventSynchronize(ev)))  // the slot's previous copy
+        return x->hip_fail(e, "ds compact download");
+      const uint64_t tail = (total_max + 15) & ~15ull;  // seal_out holds total_max + 64
+      uint8_t* so = d->seal_out.as<uint8_t>();
+      if ((e = hipMemcpyAsync(so + tail, db + A + 8, 8, hipMemcpyDeviceToDevice, s)) ||
+          (e = hipEventRecord(x->side_ev, s)) || (e = hipStreamWaitEvent(c->copy_stream, x->side_ev, 0)) ||
+          (e = launch_copy_sealed(c->copy_stream, static_cast<uint8_t*>(mapped), so,
+                                  reinterpret_cast<const uint64_t*>(so + tail), U, c->sink_cap,
+                                  c->copy_len_dev + slot, 32)) ||
+          (e = hipEventRecord(ev, c->copy_stream)))
+        return x->hip_fail(e, "ds compact download");
+      c->path_counts["compact_async_kernel_copy"]++;
+      c->copy_slot_ticket[slot] = t;
+      c->copy_last = ev;
+      c->sink_ticket = t;
+      c->sink_len = 0;  // known when the ticket completes
+      file->clear();
+      return CE_OK;
+    }
+  }
   cph = std::make_unique<HostPhase>("  cd: length wait");
   uint64_t clear_len = 0;
   if ((e = hipMemcpyAsync(&clear_len, db + A + 8, 8, hipMemcpyDeviceToHost, s)) || (e = stream_wait(s)))
@@ -2074,41 +2125,6 @@ int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t
     to = file->data();
   }
   cph = std::make_unique<HostPhase>("  cd: download");
-  if (c->sink_async && to == c->sink) {
-    // compact_into_async: the download runs on the copy stream behind the seal; the caller
-    // waits for its ticket (ce_core_compact_wait) before reading the file
-    if ((!c->copy_stream && (e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking))) ||
-        (!x->side_ev && (e = hipEventCreateWithFlags(&x->side_ev, hipEventDisableTiming))))
-      return x->hip_fail(e, "ds compact download");
-    const uint64_t t = ++c->copy_next;
-    const uint32_t slot = (uint32_t)(t % ce_core::kAsyncSlots);
-    hipEvent_t& ev = c->copy_ev[slot];
-    if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming))) return x->hip_fail(e, "ds compact download");
-    if (c->copy_slot_ticket[slot] && (e = hipEventSynchronize(ev)))  // the slot's previous copy
-      return x->hip_fail(e, "ds compact download");
-    // the caller's pinned buffer mapped into the device's address space: a copy kernel on a
-    // few CUs writes it, so the next batch's kernels run beside the download (the runtime's
-    // D2H blit would occupy every CU); other memory through the runtime's copy
-    void* mapped = nullptr;
-    {
-      hipPointerAttribute_t pa{};
-      if (hipPointerGetAttributes(&pa, to) == hipSuccess && pa.type == hipMemoryTypeHost && pa.devicePointer &&
-          !((reinterpret_cast<uintptr_t>(pa.devicePointer) | reinterpret_cast<uintptr_t>(d->seal_out.p)) & 15) &&
-          !getenv("CE_ASYNC_BLIT"))
-        mapped = pa.devicePointer;
-      (void)hipGetLastError();  // an unregistered pointer leaves an error behind
-    }
-    if ((e = hipEventRecord(x->side_ev, s)) || (e = hipStreamWaitEvent(c->copy_stream, x->side_ev, 0)) ||
-        (e = mapped ? launch_copy_bytes(c->copy_stream, static_cast<uint8_t*>(mapped), d->seal_out.as<uint8_t>(), total, 32)
-                    : hipMemcpyAsync(to, d->seal_out.p, total, hipMemcpyDeviceToHost, c->copy_stream)) ||
-        (e = hipEventRecord(ev, c->copy_stream)))
-      return x->hip_fail(e, "ds compact download");
-    if (mapped) c->path_counts["compact_async_kernel_copy"]++;
-    c->copy_slot_ticket[slot] = t;
-    c->copy_last = ev;
-    c->sink_ticket = t;
-    return CE_OK;
-  }
   if ((e = hipMemcpyAsync(to, d->seal_out.p, total, hipMemcpyDeviceToHost, s)) || (e = stream_wait(s)))
     return x->hip_fail(e, "ds compact download");
   return CE_OK;

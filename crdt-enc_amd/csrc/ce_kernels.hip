@@ -1296,6 +1296,33 @@ hipError_t launch_copy_bytes(hipStream_t s, uint8_t* dst, const uint8_t* src, ui
   return hipGetLastError();
 }
 
+// A compaction's sealed file -> the caller's mapped pinned buffer without a host round trip for
+// its length: the length is read on the device (the serializer's clear length at clear_len_at ->
+// the file's total), the copy sized by it, and the total written to the mapped len_out for the
+// host to read after the copy's event (~0: it would not fit in cap; ~1: the serializer overran
+// its bound).  Every block computes the same total.
+__global__ void __launch_bounds__(256) k_copy_sealed(uint8_t* dst, const uint8_t* src, const uint64_t* clear_len_at,
+                                                    uint64_t bound, uint64_t cap, uint64_t* len_out) {
+  const uint64_t cl = *clear_len_at;
+  const uint64_t total = 16 + sealed_len(cl);
+  const bool bad = cl > bound || total > cap;
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    *reinterpret_cast<volatile uint64_t*>(len_out) = cl > bound ? ~1ull : total > cap ? ~0ull : total;
+  if (bad) return;
+  const uint64_t n16 = total / 16;
+  const uint64_t gt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = gt; i < n16; i += gs)
+    reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+  for (uint64_t i = 16 * n16 + gt; i < total; i += gs) dst[i] = src[i];
+}
+
+hipError_t launch_copy_sealed(hipStream_t s, uint8_t* dst, const uint8_t* src, const uint64_t* clear_len_at,
+                              uint64_t bound, uint64_t cap, uint64_t* len_out, uint32_t blocks) {
+  if ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_copy_sealed, dim3(blocks), dim3(256), 0, s, dst, src, clear_len_at, bound, cap, len_out);
+  return hipGetLastError();
+}
+
 hipError_t launch_fill(hipStream_t s, const FillArgs& a) {
   uint64_t mx = 16;
   for (int i = 0; i < a.n; i++) mx = a.r[i].words > mx ? a.r[i].words : mx;

@@ -326,12 +326,16 @@ int ce_core_compact_into(ce_core *c, const uint8_t *nonce, uint8_t *dst, size_t 
                          char name_out[64]);
 
 /* ce_core_compact_into with the sealed file's download left in flight (pipelined
- * compactions: the download overlaps the caller's next batch on the device).  *ticket = 0 when
- * the file is already complete in dst, else pass it to ce_core_compact_wait before reading dst
- * (dst must stay allocated until then).  Returns the same statuses as ce_core_compact_into. */
+ * compactions: the download overlaps the caller's next batch on the device, and the call returns
+ * without waiting for the device at all).  *ticket = 0 when the file is already complete in dst
+ * (*len = its length), else *len = 0 and ce_core_compact_wait(ticket, &len) gives the length once
+ * the file is in dst (dst must stay allocated until then; a dst the device cannot write -- not
+ * pinned -- takes the synchronous path, ticket 0).  Returns the same statuses as
+ * ce_core_compact_into; a dst too small for the file is reported by ce_core_compact_wait
+ * (CE_ERR_INVALID_ARG).  A ticket stays valid for the next 15 compactions of the core. */
 int ce_core_compact_into_async(ce_core *c, const uint8_t *nonce, uint8_t *dst, size_t cap, size_t *len,
                                uint64_t *ticket);
-int ce_core_compact_wait(ce_core *c, uint64_t ticket);
+int ce_core_compact_wait(ce_core *c, uint64_t ticket, uint64_t *len);
 
 /* What read_remote_states does with one decrypted state (lib.rs:447, 458-466):
  * rmp_serde::from_slice::<StateWrapper<S>>(sw) then state.merge + next_op_versions.merge.

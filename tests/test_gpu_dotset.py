@@ -773,14 +773,26 @@ def test_compact_into_async_overlaps_next_ingest(ctx):
         want.append(core.state_bytes())
         tickets.append(core.compact_into_async(bufs[r], nonce=bytes(24)))
     assert tickets[0][1] != 0 and tickets[1][1] > tickets[0][1]
+    assert tickets[0][0] == tickets[1][0] == 0      # lengths come with the wait
+    lens = {}
     for r in (1, 0):
-        ln, t = tickets[r]
-        core.compact_wait(t)
+        _, t = tickets[r]
+        lens[r] = ln = core.compact_wait(t)
         f = bytes(bufs[r][:ln])
         assert f[:16] == APP
         st, pt = ctx.decrypt(key, f[16:])
         assert st == 0 and pt == want[r]
-    core.compact_wait(tickets[0][1])   # waiting twice is fine
+    assert core.compact_wait(tickets[0][1]) == lens[0]   # waiting twice is fine
+    assert core.path_count("compact_async_kernel_copy") == 2
+    # a pinned buffer too small: the wait reports it; a pageable buffer: the synchronous path
+    small = torch.zeros(64, dtype=torch.uint8, pin_memory=True).numpy()
+    ln, t = core.compact_into_async(small, nonce=bytes(24))
+    with pytest.raises(Exception):
+        core.compact_wait(t)
+    import numpy as np
+    pageable = np.zeros(1 << 22, np.uint8)
+    ln, t = core.compact_into_async(pageable, nonce=bytes(24))
+    assert t == 0 and ln > 0 and bytes(pageable[:16]) == APP
     core.close()
 
 
