@@ -164,6 +164,23 @@ def seal_op_files(ctx, key, actors, a_lo, a_hi, v_lo, v_hi, dev, seed):
     return files, offs, n, n * flen, fa, fv
 
 
+def name_threads():
+    """SHA3 name threads for the pipelined compactions: the job's CPU share less two (the
+    launching thread and the runtime's), at least 4; CE_NAME_THREADS overrides"""
+    if os.environ.get("CE_NAME_THREADS"):
+        return max(1, int(os.environ["CE_NAME_THREADS"]))
+    import bench
+    return max(4, bench.host_cpu()[2] - 2)
+
+
+def _lower_priority():
+    try:
+        import threading
+        os.setpriority(os.PRIO_PROCESS, threading.get_native_id(), 10)
+    except (AttributeError, OSError):
+        pass
+
+
 class CompactPipe:
     """Pipelined Core::compact outputs (C3): NB pinned buffers; each file's download is left in
     flight on the copy stream (ce_core_compact_into_async) while the next step runs on the
@@ -171,11 +188,15 @@ class CompactPipe:
     for 35 MB) is hashed on NB - 1 host threads.  flush() completes every download, drain() every
     name; a buffer is reused only after its name is done."""
 
-    def __init__(self, core, nb=13, use_async=True):
+    def __init__(self, core, nb=None, use_async=True):
         from concurrent.futures import ThreadPoolExecutor
+        if nb is None:
+            nb = name_threads() + 1
         self.core, self.nb, self.use_async = core, nb, use_async
-        self.namer = ThreadPoolExecutor(nb - 1)
-        self.obuf = [torch.zeros(1 << 26, dtype=torch.uint8, pin_memory=True).numpy() for _ in range(nb)]
+        # the hashing threads below the launching thread's priority: the device pipeline's
+        # host waits and launches are never queued behind a name (the names catch up in the gaps)
+        self.namer = ThreadPoolExecutor(nb - 1, initializer=_lower_priority)
+        self.obuf = [crdtenc.host_buffer(1 << 26) for _ in range(nb)]   # pinned: DMA-engine downloads
         self.fut = [None] * nb
         self.inflight = []      # (buffer, length, ticket) of downloads not yet waited for
         self.order = []         # name futures in step order
@@ -338,8 +359,8 @@ def run_c3(args, ctx, dev):
     # step i's sealed file comes down while step i+1 runs on the device, and its SHA3-256 content
     # name is computed on host threads (CompactPipe); every download and name is done before the
     # timed region ends
-    NB = 13
-    pipe = CompactPipe(core, NB, use_async=not os.environ.get("CE_C3_SYNC_COMPACT"))
+    pipe = CompactPipe(core, use_async=not os.environ.get("CE_C3_SYNC_COMPACT"))
+    NB = pipe.nb
     obuf = pipe.obuf
 
     def step():
@@ -844,7 +865,7 @@ def run_c3_multi(args, ctx, dev, world, rank):
     comm = _comm_device(dev)
     buf = shard.StateBuffer(dev)
     hops, timing_on = [], [False]
-    pipe = CompactPipe(core, 13, use_async=not os.environ.get("CE_C3_SYNC_COMPACT")) if rank == 0 else None
+    pipe = CompactPipe(core, use_async=not os.environ.get("CE_C3_SYNC_COMPACT")) if rank == 0 else None
     out = {}
     phase = {"states": 0.0, "ops": 0.0, "reduce": 0.0, "compact": 0.0}
 

@@ -59,8 +59,35 @@ EXPORTS = [
     "ce_core_pending_commit", "ce_core_writer_versions", "ce_shard_stats_host",
     "ce_shard_window_host", "ce_shard_window_exact", "ce_core_compact_ops_device_into",
     "ce_core_state_bytes_device", "ce_core_merge_state_device", "ce_core_ingest_states_device",
-    "ce_core_compact_into_async", "ce_core_compact_wait",
+    "ce_core_compact_into_async", "ce_core_compact_wait", "ce_host_alloc", "ce_host_free",
 ]
+
+
+class _HostMem:
+    """ce_host_alloc'd memory, freed with the last array viewing it"""
+
+    def __init__(self, n):
+        self.p = lib().ce_host_alloc(n)
+        if not self.p:
+            raise MemoryError("ce_host_alloc(%d)" % n)
+
+    def __del__(self):
+        try:
+            if getattr(self, "p", None):
+                lib().ce_host_free(self.p)
+        except Exception:       # interpreter teardown
+            pass
+        self.p = None
+
+
+def host_buffer(nbytes):
+    """A u8 numpy array over pinned host memory (ce_host_alloc): the destination for
+    Core.compact_into_async, whose download then runs on the device's DMA engines."""
+    import numpy as np
+    m = _HostMem(nbytes)
+    c = (ctypes.c_uint8 * nbytes).from_address(m.p)
+    c._ce_mem = m            # the array's base (c) keeps the allocation alive
+    return np.frombuffer(c, dtype=np.uint8)
 
 
 def _np_ptr(a, dtype):
@@ -182,6 +209,9 @@ def lib():
         L.ce_vbuf_remaining.restype = ctypes.c_size_t
         L.ce_vbuf_chunk.restype = ctypes.c_size_t
         L.ce_vbuf_chunks_vectored.restype = ctypes.c_size_t
+        L.ce_host_alloc.restype = ctypes.c_void_p
+        L.ce_host_alloc.argtypes = [ctypes.c_size_t]
+        L.ce_host_free.argtypes = [ctypes.c_void_p]
         _lib = L
     return _lib
 

@@ -1192,6 +1192,8 @@ int ingest_states_dev(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs,
     return hipSuccess;
   };
   if ((e = read_heads())) return ctx->hip_fail(e, "states heads");
+  // the host has waited for the device: a previous compaction's download can go now
+  if (is_dotset_kind(c->kind) && (rc = ds_async_kick(c, false))) return rc;
   for (uint32_t i = 0; i < n; i++)
     if (st[i] == kStatusHostParse) {
       if ((rc = resolve_host_parse(c, d_blob, d_offs, n, true))) return rc;
@@ -1557,12 +1559,14 @@ int ce_core_open(ce_ctx* ctx, const ce_open_options* o, ce_core** out) {
 void ce_core_close(ce_core* c) {
   if (!c) return;
   if (c->ctx) (void)hipStreamSynchronize(c->ctx->stream);
+  c->pend = false;  // a download not enqueued yet is dropped (its buffer may be gone with the core)
   if (c->copy_stream) {
     (void)hipStreamSynchronize(c->copy_stream);
     (void)hipStreamDestroy(c->copy_stream);
   }
   for (hipEvent_t ev : c->copy_ev)
     if (ev) (void)hipEventDestroy(ev);
+  if (c->seal_ev) (void)hipEventDestroy(c->seal_ev);
   delete c->storage;
   delete c->aux;
   ds_free(c->ds);
@@ -1888,6 +1892,10 @@ int ce_core_compact_wait(ce_core* c, uint64_t ticket, uint64_t* len) {
     slot = (uint32_t)(ticket % ce_core::kAsyncSlots);
     if (c->copy_slot_ticket[slot] != ticket)  // the slot was reused (synchronised then): its length is gone
       return len ? c->ctx->fail(CE_ERR_INVALID_ARG, "compact ticket expired") : CE_OK;
+    if (c->pend && c->pend_slot == slot) {  // its download not enqueued yet: wait for the seal, enqueue
+      const int rk = ds_async_kick(c, true);
+      if (rk) return rk;
+    }
     ev = c->copy_ev[slot];
   }
   // outside the context lock: other calls on this core may proceed meanwhile (the event stays
@@ -2178,6 +2186,15 @@ int ce_core_merge_state_device(ce_core* c, const uint8_t* d_sw, uint64_t len) {
               (e = stream_wait(c->ctx->stream))))
     return c->ctx->hip_fail(e, "merge state");
   return ce_core_merge_state(c, h.data(), len);
+}
+
+void* ce_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  return hipHostMalloc(&p, bytes ? bytes : 1, 0) == hipSuccess ? p : nullptr;
+}
+
+void ce_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
 }
 
 }  // extern "C"

@@ -83,9 +83,15 @@ struct ce_core {
   uint64_t copy_slot_ticket[kAsyncSlots] = {};
   uint64_t copy_next = 0;                 // last ticket handed out
   hipEvent_t copy_last = nullptr;         // the newest in-flight copy's event
-  // pinned, mapped: per slot, the file length the device copy wrote (ce_core_compact_wait)
+  // pinned, mapped: per slot, the sealed file's length the device wrote behind the seal
+  // (ce_core_compact_wait); the download itself is enqueued by ds_async_kick once the seal is
+  // done (the runtime's DMA copy needs the exact length on the host), at most one pending
   ce::HostBuf copy_len;
   uint64_t* copy_len_dev = nullptr;
+  hipEvent_t seal_ev = nullptr;
+  bool pend = false;
+  uint32_t pend_slot = 0;
+  uint8_t* pend_dst = nullptr;
   std::vector<uint32_t> sorted_slots;   // used slots in UUID byte order (BTreeMap order)
   uint64_t sorted_gen = ~0ull;
   std::vector<uint8_t> last_writers;    // writer list of the previous ingest and its slots
@@ -224,6 +230,8 @@ int ds_merge_states(ce_core* c, const std::vector<std::pair<const uint8_t*, size
                     int32_t* st, int32_t* status_out);
 int ds_serialize(ce_core* c, std::vector<uint8_t>* out);
 // Orswot: the same bytes written on the device into dst (cap bytes); *len = their length
+// compact_into_async: enqueue the pending download once its seal is done (force: wait for it)
+int ds_async_kick(ce_core* c, bool force);
 int ds_state_bytes_device(ce_core* c, ce_ctx* x, uint8_t* dst, uint64_t cap, uint64_t* len);
 // Core::apply_ops for a local Vec<S::Op> (already validated by ds_check_ops)
 int ds_check_ops(ce_core* c, const uint8_t* ops, size_t len);

@@ -879,6 +879,7 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
   DsState* d = c->ds;
   hipError_t e;
   int rc;
+  if ((rc = ds_async_kick(c, false))) return rc;  // a previous compaction's download, when its seal is done
   // writers get actor ids first (the gate is keyed by them)
   std::vector<uint32_t> wslot(m);
   const uint64_t gen0 = c->table_gen;
@@ -2037,10 +2038,27 @@ static int ds_serialize_dev(ce_core* c, ce_ctx* x, const uint8_t* outer, const u
   return CE_OK;
 }
 
+int ds_async_kick(ce_core* c, bool force) {
+  if (!c->pend) return CE_OK;
+  hipError_t e = force ? hipEventSynchronize(c->seal_ev) : hipEventQuery(c->seal_ev);
+  if (e == hipErrorNotReady) return CE_OK;
+  if (e) return c->ctx->hip_fail(e, "compact download");
+  const uint32_t slot = c->pend_slot;
+  const uint64_t n = c->copy_len.as<volatile uint64_t>()[slot];
+  if (n < ~1ull && (e = hipMemcpyAsync(c->pend_dst, c->ds->seal_out.p, n, hipMemcpyDeviceToHost, c->copy_stream)))
+    return c->ctx->hip_fail(e, "compact download");
+  if ((e = hipEventRecord(c->copy_ev[slot], c->copy_stream))) return c->ctx->hip_fail(e, "compact download");
+  c->copy_last = c->copy_ev[slot];
+  c->pend = false;
+  return CE_OK;
+}
+
 int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t* prefix16,
                       const uint8_t* nonce, const KeyRef& key, std::vector<uint8_t>* file) {
   HostPhase hp("ds compact (device writer)");
   c->path_counts["compact_device_writer"]++;
+  // a previous compact_into_async's download reads seal_out: enqueue it before this seal
+  if (int rk = ds_async_kick(c, true)) return rk;
   hipStream_t s = x->stream;
   hipError_t e;
   int rc;
@@ -2062,52 +2080,46 @@ int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t
   rc = device_seal(x, db, reinterpret_cast<const uint64_t*>(offs), 1, U, db + A + 56, db + A + 32,
                    d->seal_out.as<uint8_t>(), reinterpret_cast<const uint64_t*>(db + A + 16), key);
   if (rc) return rc;
-  // compact_into_async into a pinned buffer: no host round trip at all -- a copy kernel on the
-  // copy stream reads the clear length on the device, copies the sealed file into the caller's
-  // mapped buffer on a few CUs (the next batch's kernels run beside it) and writes the file's
-  // length into a pinned slot ce_core_compact_wait reads.  The clear length travels in
-  // seal_out's tail (the context's blob is the next batch's staging area).
-  if (c->sink_async && c->sink && !getenv("CE_ASYNC_BLIT")) {
-    void* mapped = nullptr;
+  // compact_into_async: no host round trip.  A one-lane kernel behind the seal writes the file's
+  // length into a pinned slot; the download (the runtime's DMA engine copy, which leaves the
+  // CUs and HBM to the next batch) is enqueued on the copy stream by ds_async_kick once the
+  // seal is done -- at the next batch's first host wait, or at ce_core_compact_wait.
+  bool pinned = false;
+  if (c->sink_async && c->sink) {
     hipPointerAttribute_t pa{};
-    if (hipPointerGetAttributes(&pa, c->sink) == hipSuccess && pa.type == hipMemoryTypeHost && pa.devicePointer &&
-        !(reinterpret_cast<uintptr_t>(pa.devicePointer) & 15))
-      mapped = pa.devicePointer;
+    pinned = hipPointerGetAttributes(&pa, c->sink) == hipSuccess && pa.type == hipMemoryTypeHost;
     (void)hipGetLastError();  // an unregistered pointer leaves an error behind
-    if (mapped) {
-      cph = std::make_unique<HostPhase>("  cd: async download");
-      if ((!c->copy_stream && (e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking))) ||
-          (!x->side_ev && (e = hipEventCreateWithFlags(&x->side_ev, hipEventDisableTiming))))
+  }
+  if (pinned && !getenv("CE_ASYNC_OFF")) {
+    cph = std::make_unique<HostPhase>("  cd: async download");
+    if ((!c->copy_stream && (e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking))) ||
+        (!c->seal_ev && (e = hipEventCreateWithFlags(&c->seal_ev, hipEventDisableTiming))))
+      return x->hip_fail(e, "ds compact download");
+    if (!c->copy_len_dev) {
+      void* dp = nullptr;
+      if ((e = c->copy_len.reserve(8ull * ce_core::kAsyncSlots)) || (e = hipHostGetDevicePointer(&dp, c->copy_len.p, 0)))
         return x->hip_fail(e, "ds compact download");
-      if (!c->copy_len_dev) {
-        void* dp = nullptr;
-        if ((e = c->copy_len.reserve(8ull * ce_core::kAsyncSlots)) || (e = hipHostGetDevicePointer(&dp, c->copy_len.p, 0)))
-          return x->hip_fail(e, "ds compact download");
-        c->copy_len_dev = static_cast<uint64_t*>(dp);
-      }
-      const uint64_t t = ++c->copy_next;
-      const uint32_t slot = (uint32_t)(t % ce_core::kAsyncSlots);
-      hipEvent_t& ev = c->copy_ev[slot];
-      if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming))) return x->hip_fail(e, "ds compact download");
-      if (c->copy_slot_ticket[slot] && (e = hipEventSynchronize(ev)))  // the slot's previous copy
-        return x->hip_fail(e, "ds compact download");
-      const uint64_t tail = (total_max + 15) & ~15ull;  // seal_out holds total_max + 64
-      uint8_t* so = d->seal_out.as<uint8_t>();
-      if ((e = hipMemcpyAsync(so + tail, db + A + 8, 8, hipMemcpyDeviceToDevice, s)) ||
-          (e = hipEventRecord(x->side_ev, s)) || (e = hipStreamWaitEvent(c->copy_stream, x->side_ev, 0)) ||
-          (e = launch_copy_sealed(c->copy_stream, static_cast<uint8_t*>(mapped), so,
-                                  reinterpret_cast<const uint64_t*>(so + tail), U, c->sink_cap,
-                                  c->copy_len_dev + slot, 32)) ||
-          (e = hipEventRecord(ev, c->copy_stream)))
-        return x->hip_fail(e, "ds compact download");
-      c->path_counts["compact_async_kernel_copy"]++;
-      c->copy_slot_ticket[slot] = t;
-      c->copy_last = ev;
-      c->sink_ticket = t;
-      c->sink_len = 0;  // known when the ticket completes
-      file->clear();
-      return CE_OK;
+      c->copy_len_dev = static_cast<uint64_t*>(dp);
     }
+    const uint64_t t = ++c->copy_next;
+    const uint32_t slot = (uint32_t)(t % ce_core::kAsyncSlots);
+    hipEvent_t& ev = c->copy_ev[slot];
+    if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming))) return x->hip_fail(e, "ds compact download");
+    if (c->copy_slot_ticket[slot] && (e = hipEventSynchronize(ev)))  // the slot's previous copy
+      return x->hip_fail(e, "ds compact download");
+    if ((e = launch_publish_sealed_len(s, reinterpret_cast<const uint64_t*>(db + A + 8), U, c->sink_cap,
+                                       c->copy_len_dev + slot)) ||
+        (e = hipEventRecord(c->seal_ev, s)))
+      return x->hip_fail(e, "ds compact download");
+    c->pend = true;
+    c->pend_slot = slot;
+    c->pend_dst = c->sink;
+    c->path_counts["compact_async"]++;
+    c->copy_slot_ticket[slot] = t;
+    c->sink_ticket = t;
+    c->sink_len = 0;  // known when the ticket completes
+    file->clear();
+    return CE_OK;
   }
   cph = std::make_unique<HostPhase>("  cd: length wait");
   uint64_t clear_len = 0;

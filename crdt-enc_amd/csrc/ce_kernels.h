@@ -69,13 +69,10 @@ struct FillArgs {
   uint32_t* counters;  // or null
 };
 hipError_t launch_fill(hipStream_t s, const FillArgs& a);
-// dst <- src (n bytes; both 16-byte aligned) by `blocks` workgroups (dst may be mapped pinned host
-// memory: the device-to-host copy that leaves the rest of the GPU to other streams)
-hipError_t launch_copy_bytes(hipStream_t s, uint8_t* dst, const uint8_t* src, uint64_t n, uint32_t blocks);
-// a sealed compaction file (clear length read on the device at clear_len_at, <= bound) -> dst
-// (cap bytes, mapped pinned memory); its total length (or ~0 / ~1, see ce_kernels.hip) -> len_out
-hipError_t launch_copy_sealed(hipStream_t s, uint8_t* dst, const uint8_t* src, const uint64_t* clear_len_at,
-                              uint64_t bound, uint64_t cap, uint64_t* len_out, uint32_t blocks);
+// a compaction's sealed-file length (clear length read on the device at clear_len_at, <= bound;
+// ~0 when over cap, ~1 when over bound) -> len_out (mapped pinned memory)
+hipError_t launch_publish_sealed_len(hipStream_t s, const uint64_t* clear_len_at, uint64_t bound, uint64_t cap,
+                                     uint64_t* len_out);
 
 // file-level open: outer version check (when outer), envelope parse, key schedule.
 hipError_t launch_open_setup(hipStream_t s, const uint8_t* blob, const uint64_t* offs,

@@ -1278,48 +1278,19 @@ __global__ void k_fill(FillArgs a) {
     f.p[i] = f.value;
 }
 
-// dst <- src, n bytes, with a small grid: a device-to-host copy into mapped pinned memory that
-// leaves most of the GPU to the work queued on other streams (the runtime's blit kernel for a
-// large D2H copy covers every CU for its whole duration)
-__global__ void __launch_bounds__(256) k_copy_bytes(uint8_t* dst, const uint8_t* src, uint64_t n) {
-  const uint64_t n16 = n / 16;
-  const uint64_t gt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, gs = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = gt; i < n16; i += gs)
-    reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
-  for (uint64_t i = 16 * n16 + gt; i < n; i += gs) dst[i] = src[i];
-}
-
-hipError_t launch_copy_bytes(hipStream_t s, uint8_t* dst, const uint8_t* src, uint64_t n, uint32_t blocks) {
-  if (n == 0) return hipSuccess;
-  if ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_copy_bytes, dim3(blocks), dim3(256), 0, s, dst, src, n);
-  return hipGetLastError();
-}
-
-// A compaction's sealed file -> the caller's mapped pinned buffer without a host round trip for
-// its length: the length is read on the device (the serializer's clear length at clear_len_at ->
-// the file's total), the copy sized by it, and the total written to the mapped len_out for the
-// host to read after the copy's event (~0: it would not fit in cap; ~1: the serializer overran
-// its bound).  Every block computes the same total.
-__global__ void __launch_bounds__(256) k_copy_sealed(uint8_t* dst, const uint8_t* src, const uint64_t* clear_len_at,
-                                                    uint64_t bound, uint64_t cap, uint64_t* len_out) {
+// A compaction's sealed-file length -> a mapped pinned word, behind the seal on its stream: the
+// serializer's clear length at clear_len_at -> the file's total (~0: it would not fit in cap;
+// ~1: the serializer overran its bound).  One lane; the host reads the word after the seal's
+// event and sizes the download by it.
+__global__ void k_publish_sealed_len(const uint64_t* clear_len_at, uint64_t bound, uint64_t cap, uint64_t* len_out) {
   const uint64_t cl = *clear_len_at;
   const uint64_t total = 16 + sealed_len(cl);
-  const bool bad = cl > bound || total > cap;
-  if (blockIdx.x == 0 && threadIdx.x == 0)
-    *reinterpret_cast<volatile uint64_t*>(len_out) = cl > bound ? ~1ull : total > cap ? ~0ull : total;
-  if (bad) return;
-  const uint64_t n16 = total / 16;
-  const uint64_t gt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, gs = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = gt; i < n16; i += gs)
-    reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
-  for (uint64_t i = 16 * n16 + gt; i < total; i += gs) dst[i] = src[i];
+  *reinterpret_cast<volatile uint64_t*>(len_out) = cl > bound ? ~1ull : total > cap ? ~0ull : total;
 }
 
-hipError_t launch_copy_sealed(hipStream_t s, uint8_t* dst, const uint8_t* src, const uint64_t* clear_len_at,
-                              uint64_t bound, uint64_t cap, uint64_t* len_out, uint32_t blocks) {
-  if ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_copy_sealed, dim3(blocks), dim3(256), 0, s, dst, src, clear_len_at, bound, cap, len_out);
+hipError_t launch_publish_sealed_len(hipStream_t s, const uint64_t* clear_len_at, uint64_t bound, uint64_t cap,
+                                     uint64_t* len_out) {
+  hipLaunchKernelGGL(k_publish_sealed_len, dim3(1), dim3(1), 0, s, clear_len_at, bound, cap, len_out);
   return hipGetLastError();
 }
 

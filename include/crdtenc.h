@@ -337,6 +337,13 @@ int ce_core_compact_into_async(ce_core *c, const uint8_t *nonce, uint8_t *dst, s
                                uint64_t *ticket);
 int ce_core_compact_wait(ce_core *c, uint64_t ticket, uint64_t *len);
 
+/* Pinned host memory for the asynchronous paths (ce_core_compact_into_async's dst, the *_iov
+ * host-buffer ingests): the device's DMA engines copy it without staging and without occupying
+ * the compute units.  NULL when the allocation fails.  (No reference counterpart: the Rust
+ * caller's Vec<u8> buffers, lib.rs:349-363, would be allocated here for the zero-copy form.) */
+void *ce_host_alloc(size_t bytes);
+void ce_host_free(void *p);
+
 /* What read_remote_states does with one decrypted state (lib.rs:447, 458-466):
  * rmp_serde::from_slice::<StateWrapper<S>>(sw) then state.merge + next_op_versions.merge.
  * Also the exchange step of the dot-set kinds across GPUs (all-gather of partial states). */
