@@ -232,6 +232,8 @@ int ds_serialize(ce_core* c, std::vector<uint8_t>* out);
 // Orswot: the same bytes written on the device into dst (cap bytes); *len = their length
 // compact_into_async: enqueue the pending download once its seal is done (force: wait for it)
 int ds_async_kick(ce_core* c, bool force);
+// the last fold's / k-way merge's closing counts and deferred set (waits for the stream)
+int ds_settle(ce_core* c);
 int ds_state_bytes_device(ce_core* c, ce_ctx* x, uint8_t* dst, uint64_t cap, uint64_t* len);
 // Core::apply_ops for a local Vec<S::Op> (already validated by ds_check_ops)
 int ds_check_ops(ce_core* c, const uint8_t* ops, size_t len);

@@ -118,9 +118,11 @@ hipError_t launch_ds_kill(hipStream_t s, DsTables t, const uint32_t* cbeg, const
 // v = max(cur, add); v <= kill -> 0; cur = v; add = kill = 0; live/used counts
 hipError_t launch_ds_finalize(hipStream_t s, DsTables t);
 // deferred[r] = !(R <= clock)
+// deferred[r] = removal r's clock is not covered by `clock`; any (may be null): set to 1 when
+// some removal is deferred
 hipError_t launch_ds_deferred(hipStream_t s, const uint32_t* cbeg, const uint32_t* c_actor,
                               const unsigned long long* c_ctr, const unsigned long long* clock,
-                              uint8_t* deferred, uint32_t n_rm);
+                              uint8_t* deferred, uint32_t n_rm, uint32_t* any = nullptr);
 // state merge: insert the other state's entries with oth = value, then the per-pair merge rule
 hipError_t launch_ds_put_other(hipStream_t s, DsTables t, const unsigned long long* member,
                                const uint32_t* actor, const unsigned long long* value, uint32_t n,

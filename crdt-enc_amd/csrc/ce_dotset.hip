@@ -541,11 +541,18 @@ __global__ void __launch_bounds__(kBlock) k_ds_finalize(DsTables t) {
 
 __global__ void k_ds_deferred(const uint32_t* cbeg, const uint32_t* c_actor,
                               const unsigned long long* c_ctr, const unsigned long long* clock,
-                              uint8_t* deferred, uint32_t n) {
+                              uint8_t* deferred, uint32_t n, uint32_t* any) {
+  bool some = false;
   for (uint32_t r = blockIdx.x * kBlock + threadIdx.x; r < n; r += gridDim.x * kBlock) {
     bool d = false;
     for (uint32_t e = cbeg[r]; e < cbeg[r + 1] && !d; e++) d = c_ctr[e] > clock[c_actor[e]];
     deferred[r] = d;  // !(clock <= self.clock)
+    some = some || d;
+  }
+  // any[0] = 1 when some removal is deferred (one atomic per wave that has one; rare)
+  if (any) {
+    const unsigned long long b = __ballot(some);
+    if (b && (threadIdx.x & 63) == (uint32_t)(__ffsll(b) - 1)) atomicOr(any, 1u);
   }
 }
 
@@ -1079,10 +1086,10 @@ hipError_t launch_ds_finalize(hipStream_t s, DsTables t) {
 
 hipError_t launch_ds_deferred(hipStream_t s, const uint32_t* cbeg, const uint32_t* c_actor,
                               const unsigned long long* c_ctr, const unsigned long long* clock,
-                              uint8_t* deferred, uint32_t n_rm) {
+                              uint8_t* deferred, uint32_t n_rm, uint32_t* any) {
   if (n_rm == 0) return hipSuccess;
   hipLaunchKernelGGL(k_ds_deferred, dim3(blocks_for(n_rm)), dim3(kBlock), 0, s, cbeg, c_actor, c_ctr,
-                     clock, deferred, n_rm);
+                     clock, deferred, n_rm, any);
   return hipGetLastError();
 }
 

@@ -34,6 +34,12 @@ struct DsState {
   DevBuf clock;  // u64[clock_cap] by actor id
   uint32_t clock_cap = 0;
   DevBuf mkey, pkey, cur, add, kill, oth, live, hold;  // hold: k-way merge holder bits (zero between merges)
+  // a fold / k-way merge whose closing counts (live[0..3] -> pinned h_cnt[56..60)) and deferred
+  // flags have not been read yet: ds_settle reads them at the next host wait
+  bool settle_pending = false, settle_fold = false;
+  uint32_t settle_nr = 0;
+  uint64_t settle_rmc = 0, settle_rmm = 0;
+  std::vector<std::pair<IdDots, std::vector<uint64_t>>> settle_d0;
   uint32_t pcap = 0;  // member table and pair table share the capacity (members <= pairs)
   uint64_t used_pairs = 0, live_pairs = 0;
   std::map<IdDots, std::set<uint64_t>> deferred;  // removal clock -> members (HashMap in crdts)
@@ -562,42 +568,72 @@ int orswot_fold(ce_core* c, const Counts& k) {
                                  d->d0[4].as<unsigned long long>(), n0))))
     return ctx->hip_fail(e, "kill");
   ctx->tend(tk);
-  // finalize; its counts come back with the deferred flags below (one wait for both)
-  uint32_t* hl = d->h_cnt.as<uint32_t>() + 56;  // pinned
+  // finalize and the deferred flags without a host wait: live / used pairs, the overflow flag and
+  // whether any removal stays deferred land in pinned memory; ds_settle reads them at the
+  // caller's next host wait (the removal columns stay intact until then)
+  uint32_t* live = d->live.as<uint32_t>();
+  if ((e = d->deferred_flags.reserve(nr + n0 + 64)) || (e = launch_ds_set3(s, live, 0u, live + 1, 0u, live + 3, 0u)))
+    return ctx->hip_fail(e, "finalize");
   {
-    if ((e = hipMemsetAsync(d->live.p, 0, 8, s))) return ctx->hip_fail(e, "finalize");
     const int t = ctx->tbegin("ds_finalize");
     if ((e = launch_ds_finalize(s, tables(d)))) return ctx->hip_fail(e, "finalize");
     ctx->tend(t);
-    if ((e = hipMemcpyAsync(hl, d->live.p, 16, hipMemcpyDeviceToHost, s))) return ctx->hip_fail(e, "finalize");
   }
-  // 4) deferred = removals whose clock is not covered by the new clock
-  std::vector<uint8_t> f_batch, f_d0;
-  if ((rc = flags_for(c, o.rm_cbeg, o.rmc_actor, o.rmc_ctr, nr, &f_batch)) ||
-      (rc = flags_for(c, d->d0[0].as<uint32_t>(), d->d0[2].as<uint32_t>(),
-                      d->d0[3].as<unsigned long long>(), n0, &f_d0)))
-    return rc;
-  if (nr == 0 && n0 == 0 && (e = stream_wait(s))) return ctx->hip_fail(e, "finalize");
+  uint8_t* fl = d->deferred_flags.as<uint8_t>();
+  if ((e = launch_ds_deferred(s, o.rm_cbeg, o.rmc_actor, o.rmc_ctr, d->clock.as<unsigned long long>(), fl, nr, live + 3)) ||
+      (n0 && (e = launch_ds_deferred(s, d->d0[0].as<uint32_t>(), d->d0[2].as<uint32_t>(),
+                                     d->d0[3].as<unsigned long long>(), d->clock.as<unsigned long long>(), fl + nr,
+                                     n0, live + 3))) ||
+      (e = hipMemcpyAsync(d->h_cnt.as<uint32_t>() + 56, live, 16, hipMemcpyDeviceToHost, s)))
+    return ctx->hip_fail(e, "finalize");
+  d->settle_pending = true;
+  d->settle_fold = true;
+  d->settle_nr = nr;
+  d->settle_rmc = k.v[kCntRmC];
+  d->settle_rmm = k.v[kCntRmM];
+  d->settle_d0 = std::move(d0);
+  return CE_OK;
+}
+
+}  // namespace
+
+// A fold's or k-way merge's closing counts and the new deferred set, once the stream has
+// drained (usually it has: callers settle right after a host wait of their own)
+int ds_settle(ce_core* c) {
+  DsState* d = c->ds;
+  if (!d || !d->settle_pending) return CE_OK;
+  ce_ctx* ctx = c->ctx;
+  hipStream_t s = ctx->stream;
+  hipError_t e;
+  if ((e = stream_wait(s))) return ctx->hip_fail(e, "settle");
+  d->settle_pending = false;
+  const uint32_t* hl = d->h_cnt.as<uint32_t>() + 56;
   if (hl[2]) return ctx->fail(CE_ERR_DEVICE, "dot-set table overflow");
   d->live_pairs = hl[0];
   d->used_pairs = hl[1];
+  if (!d->settle_fold) return CE_OK;
+  // 4) deferred = removals whose clock is not covered by the new clock (none: the usual case)
   std::map<IdDots, std::set<uint64_t>> nd;
-  for (uint32_t i = 0; i < n0; i++)
-    if (f_d0[i]) nd[d0[i].first].insert(d0[i].second.begin(), d0[i].second.end());
-  bool any = false;
-  for (uint8_t f : f_batch) any = any || f;
-  if (any) {
-    std::vector<uint32_t> cb(nr + 1), mb(nr + 1), act(k.v[kCntRmC]);
-    std::vector<unsigned long long> ctr(k.v[kCntRmC]), mem(k.v[kCntRmM]);
-    if ((e = hipMemcpyAsync(cb.data(), o.rm_cbeg, (nr + 1) * 4ull, hipMemcpyDeviceToHost, s)) ||
-        (e = hipMemcpyAsync(mb.data(), o.rm_mbeg, (nr + 1) * 4ull, hipMemcpyDeviceToHost, s)) ||
+  auto d0 = std::move(d->settle_d0);
+  d->settle_d0.clear();
+  if (hl[3]) {
+    const uint32_t nr = d->settle_nr, n0 = (uint32_t)d0.size();
+    DsOps o = ops_view(d);
+    std::vector<uint8_t> f(nr + n0);
+    std::vector<uint32_t> cb(nr + 1), mb(nr + 1), act(d->settle_rmc);
+    std::vector<unsigned long long> ctr(d->settle_rmc), mem(d->settle_rmm);
+    if ((!f.empty() && (e = hipMemcpyAsync(f.data(), d->deferred_flags.p, f.size(), hipMemcpyDeviceToHost, s))) ||
+        (nr && (e = hipMemcpyAsync(cb.data(), o.rm_cbeg, (nr + 1) * 4ull, hipMemcpyDeviceToHost, s))) ||
+        (nr && (e = hipMemcpyAsync(mb.data(), o.rm_mbeg, (nr + 1) * 4ull, hipMemcpyDeviceToHost, s))) ||
         (!act.empty() && (e = hipMemcpyAsync(act.data(), o.rmc_actor, act.size() * 4, hipMemcpyDeviceToHost, s))) ||
         (!ctr.empty() && (e = hipMemcpyAsync(ctr.data(), o.rmc_ctr, ctr.size() * 8, hipMemcpyDeviceToHost, s))) ||
         (!mem.empty() && (e = hipMemcpyAsync(mem.data(), o.rm_mem, mem.size() * 8, hipMemcpyDeviceToHost, s))) ||
         (e = stream_wait(s)))
       return ctx->hip_fail(e, "deferred download");
+    for (uint32_t i = 0; i < n0; i++)
+      if (f[nr + i]) nd[d0[i].first].insert(d0[i].second.begin(), d0[i].second.end());
     for (uint32_t r = 0; r < nr; r++) {
-      if (!f_batch[r]) continue;
+      if (!f[r]) continue;
       IdDots key;
       for (uint32_t j = cb[r]; j < cb[r + 1]; j++) key.push_back({act[j], ctr[j]});
       std::sort(key.begin(), key.end());
@@ -608,6 +644,8 @@ int orswot_fold(ce_core* c, const Counts& k) {
   d->deferred = std::move(nd);
   return CE_OK;
 }
+
+namespace {
 
 // MVReg survivors among n candidates already in ops rm_cbeg/rmc_*/put_val; returns indices in
 // ascending (insertion) order
@@ -863,6 +901,7 @@ int ds_init(ce_core* c) {
 
 int ds_reset(ce_core* c) {
   DsState* d = c->ds;
+  if (int rs = ds_settle(c)) return rs;
   d->deferred.clear();
   d->vals.clear();
   hipError_t e;
@@ -939,6 +978,7 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
   };
   auto wait = [&](const char* what) { return (e = stream_wait(ctx->stream)) ? ctx->hip_fail(e, what) : CE_OK; };
   if ((rc = count_pass()) || (rc = wait("count"))) return rc;
+  if ((rc = ds_settle(c))) return rc;  // the previous fold / merge (drained by the wait above)
   bool recount = false;
   if (hsum[14]) {  // envelopes left to the host: normalize + open there, patch the batch
     if ((rc = resolve_host_parse(c, d_blob, d_offs, n, true))) return rc;
@@ -1466,6 +1506,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
   hipStream_t s = ctx->stream;
   const size_t n = off.size();
   constexpr uint64_t kPrefix = 1u << 18;
+  if (int rs = ds_settle(c)) return rs;
   std::vector<DevState> ds(n);
   std::vector<std::vector<uint8_t>> host_pt(n);
   hipError_t e;
@@ -1735,23 +1776,23 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
       auto& b = d->rd[i];
       hs[i] = DsMergeSrc{b[7].as<unsigned long long>(), b[8].as<uint32_t>(), b[9].as<unsigned long long>(), ds[i].n_dots};
     }
+    // no host wait: the merged counts land in pinned memory for ds_settle (the next ingest's
+    // first wait), like a fold's
     if ((e = hipMemcpyAsync(d->rd_args_d.p, hs, n * sizeof(DsMergeSrc), hipMemcpyHostToDevice, s)) ||
         (e = launch_ds_kmerge(s, tables(d), d->rd_args_d.as<DsMergeSrc>(), hs, (uint32_t)n,
                               d->clock.as<unsigned long long>(), d->rd_oclocks.as<unsigned long long>(), ccap,
                               d->hold.as<unsigned long long>())) ||
-        (e = hipMemcpyAsync(live, d->live.p, 16, hipMemcpyDeviceToHost, s)))
+        (e = hipMemcpyAsync(d->h_cnt.as<uint32_t>() + 56, d->live.p, 16, hipMemcpyDeviceToHost, s)))
       return ctx->hip_fail(e, "merge");
     c->path_counts["states_kway_merge"]++;
+    d->settle_pending = true;
+    d->settle_fold = false;
     for (size_t i = 0; i < n; i++)
       for (auto& y : ds[i].hs.nov) {
         uint32_t sl;
         if ((rc = insert_actor(c, y.first, &sl))) return rc;
         c->nov[sl] = std::max(c->nov[sl], y.second);
       }
-    if ((rc = sync("merge"))) return rc;
-    if (live[2]) return ctx->fail(CE_ERR_DEVICE, "dot-set table overflow");
-    d->live_pairs = live[0];
-    d->used_pairs = live[1];
     return table_upload(c);
   }
   size_t last_dev = n;
@@ -1801,6 +1842,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
 
 int ds_merge_states(ce_core* c, const std::vector<std::pair<const uint8_t*, size_t>>& sws,
                     int32_t* st, int32_t* status_out) {
+  if (int rs = ds_settle(c)) return rs;
   const size_t n = sws.size();
   std::vector<HostState> hs(n);
   int first = CE_OK;
@@ -1842,6 +1884,7 @@ int ds_merge_states(ce_core* c, const std::vector<std::pair<const uint8_t*, size
 }
 
 int ds_check_ops(ce_core* c, const uint8_t* ops, size_t len) {
+  if (int rs = ds_settle(c)) return rs;
   std::vector<HostOp> v;
   if (!parse_ops_host(c->kind, ops, len, &v))
     return c->ctx->fail(CE_ERR_DECODE, c->kind == CE_STATE_ORSWOT ? "ops are not a Vec<orswot::Op<u64, Uuid>>"
@@ -1850,6 +1893,7 @@ int ds_check_ops(ce_core* c, const uint8_t* ops, size_t len) {
 }
 
 int ds_apply_local_ops(ce_core* c, const uint8_t* ops, size_t len) {
+  if (int rs = ds_settle(c)) return rs;
   DsState* d = c->ds;
   std::vector<HostOp> v;
   if (!parse_ops_host(c->kind, ops, len, &v)) return c->ctx->fail(CE_ERR_DECODE, "ops");
@@ -1937,7 +1981,7 @@ static int ds_serialize_dev(ce_core* c, ce_ctx* x, const uint8_t* outer, const u
   // live pairs -> columns, their count and largest member, and the clock: one wait
   uint32_t nl = 0;
   unsigned long long max_member = 0;
-  if ((rc = collect(c, &nl, &max_member, d->h_clock.p, d->clock.p, 8ull * na))) return rc;
+  if ((rc = collect(c, &nl, &max_member, d->h_clock.p, d->clock.p, 8ull * na)) || (rc = ds_settle(c))) return rc;
   const unsigned long long* ck = d->h_clock.as<unsigned long long>();
   cph = std::make_unique<HostPhase>("  cd: head + tail bytes");
   Dots clock;
@@ -2169,6 +2213,7 @@ int ds_state_bytes_device(ce_core* c, ce_ctx* x, uint8_t* dst, uint64_t cap, uin
 // canonical to_vec_named(StateWrapper<S>) (lib.rs:336, 739-743); HashMap / HashSet contents
 // sorted (members ascending, deferred clocks by their msgpack bytes) -- SURVEY.md F9
 int ds_serialize(ce_core* c, std::vector<uint8_t>* out) {
+  if (int rs = ds_settle(c)) return rs;
   HostPhase hp("serialize");
   DsState* d = c->ds;
   ce_ctx* ctx = c->ctx;
