@@ -47,10 +47,10 @@ $(PKG)/build_prof/%.o: $(CSRC)/%.cpp $(HDRS)
 prof: $(PROF_LIB)
 
 $(PROF_LIB): $(PROF_OBJS)
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread -lhsa-runtime64
 
 $(PRODUCT): $(HIP_OBJS) $(CPP_OBJS)
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread -lhsa-runtime64
 
 $(ORACLE): oracle/ce_oracle.c oracle/ce_oracle.h
 	gcc -O3 -march=x86-64-v3 -fPIC -shared -Wall -Wextra -o $@ oracle/ce_oracle.c -lpthread

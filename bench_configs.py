@@ -521,6 +521,8 @@ def run_c3(args, ctx, dev):
         "states_from_host": states_from_host,
         "pipelined": {"ms_per_step": round(ms_loop, 3), "name_drain_ms": round(drain_ms, 3),
                       "download_overlap": pipe.use_async,
+                      "download_engine": "sdma" if core.path_count("compact_download_sdma") else "runtime copy",
+                      "name_threads": NB - 1,
                       "what": "steps back to back, each sealed file's download overlapping the next "
                               "step on the device (ce_core_compact_into_async) and its content name "
                               "hashed on %d host threads; timed up to the last download; ms_per_step "

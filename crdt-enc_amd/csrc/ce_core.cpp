@@ -1566,6 +1566,11 @@ void ce_core_close(ce_core* c) {
   }
   for (hipEvent_t ev : c->copy_ev)
     if (ev) (void)hipEventDestroy(ev);
+  for (uint32_t k = 0; k < ce_core::kAsyncSlots; k++)
+    if (c->copy_sig[k].handle) {
+      ce::dma_wait(c->copy_sig[k]);
+      ce::dma_signal_destroy(c->copy_sig[k]);
+    }
   if (c->seal_ev) (void)hipEventDestroy(c->seal_ev);
   delete c->storage;
   delete c->aux;
@@ -1885,6 +1890,8 @@ int ce_core_compact_wait(ce_core* c, uint64_t ticket, uint64_t* len) {
   if (!c) return CE_ERR_INVALID_ARG;
   if (ticket == 0) return CE_OK;
   hipEvent_t ev = nullptr;
+  hsa_signal_t sig{0};
+  bool dma = false;
   uint32_t slot;
   {
     std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
@@ -1897,11 +1904,17 @@ int ce_core_compact_wait(ce_core* c, uint64_t ticket, uint64_t* len) {
       if (rk) return rk;
     }
     ev = c->copy_ev[slot];
+    dma = c->copy_dma[slot];
+    sig = c->copy_sig[slot];
   }
-  // outside the context lock: other calls on this core may proceed meanwhile (the event stays
-  // alive until the core is closed)
-  const hipError_t e = hipEventSynchronize(ev);
-  if (e) return c->ctx->hip_fail(e, "compact wait");
+  // outside the context lock: other calls on this core may proceed meanwhile (the event and the
+  // signal stay alive until the core is closed)
+  if (dma) {
+    ce::dma_wait(sig);
+  } else {
+    const hipError_t e = hipEventSynchronize(ev);
+    if (e) return c->ctx->hip_fail(e, "compact wait");
+  }
   const uint64_t n = c->copy_len.as<volatile uint64_t>()[slot];
   if (n == ~1ull) return c->ctx->fail(CE_ERR_DEVICE, "serializer overran its bound");
   if (n == ~0ull) return c->ctx->fail(CE_ERR_INVALID_ARG, "compact_into_async: buffer too small");

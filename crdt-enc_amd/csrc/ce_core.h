@@ -82,13 +82,19 @@ struct ce_core {
   hipEvent_t copy_ev[kAsyncSlots] = {};
   uint64_t copy_slot_ticket[kAsyncSlots] = {};
   uint64_t copy_next = 0;                 // last ticket handed out
-  hipEvent_t copy_last = nullptr;         // the newest in-flight copy's event
   // pinned, mapped: per slot, the sealed file's length the device wrote behind the seal
   // (ce_core_compact_wait); the download itself is enqueued by ds_async_kick once the seal is
   // done (the runtime's DMA copy needs the exact length on the host), at most one pending
   ce::HostBuf copy_len;
   uint64_t* copy_len_dev = nullptr;
   hipEvent_t seal_ev = nullptr;
+  // the download on an SDMA engine when the HSA runtime offers one (copy_sig per slot), else the
+  // HIP runtime's copy on copy_stream (copy_ev); copy_last_slot: the newest download's slot
+  ce::DmaD2H dma;
+  bool dma_tried = false;
+  hsa_signal_t copy_sig[kAsyncSlots] = {};
+  bool copy_dma[kAsyncSlots] = {};
+  int copy_last_slot = -1;
   bool pend = false;
   uint32_t pend_slot = 0;
   uint8_t* pend_dst = nullptr;
@@ -232,6 +238,8 @@ int ds_serialize(ce_core* c, std::vector<uint8_t>* out);
 // Orswot: the same bytes written on the device into dst (cap bytes); *len = their length
 // compact_into_async: enqueue the pending download once its seal is done (force: wait for it)
 int ds_async_kick(ce_core* c, bool force);
+// the newest compaction download done reading seal_out (host wait, or ordered on s)
+int ds_download_fence(ce_core* c, hipStream_t s, bool device);
 // the last fold's / k-way merge's closing counts and deferred set (waits for the stream)
 int ds_settle(ce_core* c);
 int ds_state_bytes_device(ce_core* c, ce_ctx* x, uint8_t* dst, uint64_t cap, uint64_t* len);

@@ -2089,12 +2089,38 @@ int ds_async_kick(ce_core* c, bool force) {
   if (e) return c->ctx->hip_fail(e, "compact download");
   const uint32_t slot = c->pend_slot;
   const uint64_t n = c->copy_len.as<volatile uint64_t>()[slot];
-  if (n < ~1ull && (e = hipMemcpyAsync(c->pend_dst, c->ds->seal_out.p, n, hipMemcpyDeviceToHost, c->copy_stream)))
-    return c->ctx->hip_fail(e, "compact download");
-  if ((e = hipEventRecord(c->copy_ev[slot], c->copy_stream))) return c->ctx->hip_fail(e, "compact download");
-  c->copy_last = c->copy_ev[slot];
+  if (!c->dma_tried) {
+    c->dma_tried = true;
+    (void)dma_init(c->ctx->device, &c->dma);
+  }
+  // an SDMA engine when the HSA runtime gives one (the compute units and their memory path stay
+  // with the next batch), else the HIP runtime's copy on the copy stream
+  c->copy_dma[slot] = false;
+  if (n < ~1ull && c->dma.ok && (c->copy_sig[slot].handle || dma_signal(&c->copy_sig[slot])) &&
+      dma_d2h(c->dma, c->pend_dst, c->ds->seal_out.p, n, c->copy_sig[slot])) {
+    c->copy_dma[slot] = true;
+    c->path_counts["compact_download_sdma"]++;
+  } else {
+    if (n < ~1ull && (e = hipMemcpyAsync(c->pend_dst, c->ds->seal_out.p, n, hipMemcpyDeviceToHost, c->copy_stream)))
+      return c->ctx->hip_fail(e, "compact download");
+    if ((e = hipEventRecord(c->copy_ev[slot], c->copy_stream))) return c->ctx->hip_fail(e, "compact download");
+  }
+  c->copy_last_slot = (int)slot;
   c->pend = false;
   return CE_OK;
+}
+
+// wait for the newest download (it reads seal_out): on the host (device = false) or, for a
+// runtime copy, ordered before the next work on stream s
+int ds_download_fence(ce_core* c, hipStream_t s, bool device) {
+  if (c->copy_last_slot < 0) return CE_OK;
+  const int k = c->copy_last_slot;
+  if (c->copy_dma[k]) {
+    dma_wait(c->copy_sig[k]);
+    return CE_OK;
+  }
+  hipError_t e = device ? hipStreamWaitEvent(s, c->copy_ev[k], 0) : hipEventSynchronize(c->copy_ev[k]);
+  return e ? c->ctx->hip_fail(e, "compact download") : CE_OK;
 }
 
 int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t* prefix16,
@@ -2117,10 +2143,9 @@ int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t
   // still read it: the seal waits for it on the device, a reallocation on the host
   DsState* d = c->ds;
   const uint64_t total_max = 16 + sealed_len(U);
-  if (total_max + 64 > d->seal_out.cap && c->copy_last && (e = hipEventSynchronize(c->copy_last)))
-    return x->hip_fail(e, "ds compact");
+  if (total_max + 64 > d->seal_out.cap && (rc = ds_download_fence(c, s, false))) return rc;
   if ((e = d->seal_out.reserve(total_max + 64))) return x->hip_fail(e, "ds compact reserve");
-  if (c->copy_last && (e = hipStreamWaitEvent(s, c->copy_last, 0))) return x->hip_fail(e, "ds compact");
+  if ((rc = ds_download_fence(c, s, true))) return rc;
   rc = device_seal(x, db, reinterpret_cast<const uint64_t*>(offs), 1, U, db + A + 56, db + A + 32,
                    d->seal_out.as<uint8_t>(), reinterpret_cast<const uint64_t*>(db + A + 16), key);
   if (rc) return rc;
@@ -2149,8 +2174,10 @@ int ds_compact_device(ce_core* c, ce_ctx* x, const uint8_t* outer, const uint8_t
     const uint32_t slot = (uint32_t)(t % ce_core::kAsyncSlots);
     hipEvent_t& ev = c->copy_ev[slot];
     if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming))) return x->hip_fail(e, "ds compact download");
-    if (c->copy_slot_ticket[slot] && (e = hipEventSynchronize(ev)))  // the slot's previous copy
-      return x->hip_fail(e, "ds compact download");
+    if (c->copy_slot_ticket[slot]) {  // the slot's previous copy
+      if (c->copy_dma[slot]) dma_wait(c->copy_sig[slot]);
+      else if ((e = hipEventSynchronize(ev))) return x->hip_fail(e, "ds compact download");
+    }
     if ((e = launch_publish_sealed_len(s, reinterpret_cast<const uint64_t*>(db + A + 8), U, c->sink_cap,
                                        c->copy_len_dev + slot)) ||
         (e = hipEventRecord(c->seal_ev, s)))

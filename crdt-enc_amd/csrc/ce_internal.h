@@ -2,6 +2,7 @@
 #pragma once
 #include <utility>
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
 #include <sched.h>
 
 #include <array>
@@ -237,6 +238,18 @@ int seal_one(ce_ctx* ctx, const KeyRef& key, const uint8_t* outer_version, const
              const uint8_t* prefix16 = nullptr);
 
 uint32_t grid_waves_for(uint32_t work);
+
+// ce_dma.cpp: device -> host copies on an SDMA engine (HSA), completion on a signal
+struct DmaD2H {
+  bool ok = false;
+  hsa_agent_t gpu{0}, cpu{0};
+  uint32_t engine = 0;  // hsa_amd_sdma_engine_id_t bit, 0: the runtime's choice
+};
+bool dma_init(int device, DmaD2H* out);
+bool dma_d2h(const DmaD2H& d, void* dst, const void* src, size_t n, hsa_signal_t sig);  // false: not issued
+void dma_wait(hsa_signal_t sig);
+bool dma_signal(hsa_signal_t* sig);
+void dma_signal_destroy(hsa_signal_t sig);
 
 // ce_upload.cpp: host files -> ctx->blob / ctx->offs through the pinned staging ring (ordered
 // before later work on ctx->stream, no host synchronise)

@@ -1,7 +1,10 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-c3() { timeout -k 10 300 python -u bench_configs.py --config c3 --no-cpu > gpurun_out/c3_$1.json 2> gpurun_out/c3_$1.err; }
-AB="CE_GATE_AFTER_SETUP=1 X=0 CE_GATE_AFTER_SETUP=1 X=0" BENCH_ARGS="--no-variant-b --no-host-buffers --steps 40 --no-clock" bash tools/gpu_ab.sh > gpurun_out/ab_gate.txt 2>&1 && \
-CE_C3_NO_NAMES=1 c3 nn && CE_C3_NO_NAMES=1 CE_ASYNC_BLIT=1 c3 nnblit && CE_C3_NO_NAMES=1 CE_C3_SYNC_COMPACT=1 c3 nnsync && c3 names && \
-CE_C3_NO_NAMES=1 bash tools/c3_step.sh
+c3() { CE_C3_NO_NAMES=1 timeout -k 10 300 python -u bench_configs.py --config c3 --no-cpu > gpurun_out/c3_$1.json 2> gpurun_out/c3_$1.err; }
+c3 auto && CE_DMA_ENGINE=0 c3 e0 && CE_DMA_ENGINE=1 c3 e1 && CE_DMA_OFF=1 c3 off && python3 - <<'PY'
+import json
+for v in ("auto", "e0", "e1", "off"):
+    d = json.load(open("gpurun_out/c3_%s.json" % v))
+    print(v, d["ms_per_step"], d["pipelined"]["download_engine"], d["phases_ms_per_step"], d["kernels_ms_per_step"].get("ds_add_pairs"))
+PY
