@@ -1982,6 +1982,40 @@ static int ds_serialize_dev(ce_core* c, ce_ctx* x, const uint8_t* outer, const u
   uint32_t nl = 0;
   unsigned long long max_member = 0;
   if ((rc = collect(c, &nl, &max_member, d->h_clock.p, d->clock.p, 8ull * na)) || (rc = ds_settle(c))) return rc;
+  // the sorts and scans over the collected pairs first (they need nothing from the host): the
+  // head and tail bytes below are built while they run
+  cph = std::make_unique<HostPhase>("  cd: sort enqueue");
+  for (int k = 0; k < 15; k++) {
+    // 0-3 u32 sort keys / perms, 4-6 u64 keys / sorted members / values, 7-10 actors, heads,
+    // ranks, lengths, 11 entry CSR (n + 1), 12 byte offsets
+    const size_t sz = k >= 4 && k <= 6 ? 8ull * nl + 64 : k <= 12 ? 4ull * nl + 68 : 64;
+    if ((e = d->ser[k].reserve(sz))) return x->hip_fail(e, "ds compact reserve");
+  }
+  if ((e = d->ser[15].reserve(orswot_ser_tmp_bytes(std::max<uint32_t>(nl, 1))))) return x->hip_fail(e, "ds compact reserve");
+  OrswotSerScratch sc{};
+  sc.member_in = d->col[0].as<unsigned long long>();
+  sc.actor_in = d->col[1].as<uint32_t>();
+  sc.value_in = d->col[2].as<unsigned long long>();
+  sc.rank_of_id = d->rank_of_id.as<uint32_t>();
+  sc.rank_bits = bits_for(na);
+  sc.member_bits = max_member ? 64 - __builtin_clzll(max_member) : 1;  // radix passes over those bits only
+  sc.k32a = d->ser[0].as<uint32_t>();
+  sc.k32b = d->ser[1].as<uint32_t>();
+  sc.p32a = d->ser[2].as<uint32_t>();
+  sc.p32b = d->ser[3].as<uint32_t>();
+  sc.k64a = d->ser[4].as<unsigned long long>();
+  sc.member_sorted = d->ser[5].as<unsigned long long>();
+  sc.value_sorted = d->ser[6].as<unsigned long long>();
+  sc.actor_sorted = d->ser[7].as<uint32_t>();
+  sc.head = d->ser[8].as<uint32_t>();
+  sc.hrank = d->ser[9].as<uint32_t>();
+  sc.len = d->ser[10].as<uint32_t>();
+  sc.seg = d->ser[11].as<uint32_t>();
+  sc.pos = d->ser[12].as<uint32_t>();
+  sc.tmp = d->ser[15].p;
+  sc.tmp_bytes = d->ser[15].cap;
+  const int t = x->tbegin("ds_serialize");
+  if ((e = launch_orswot_ser_sort(s, sc, nl))) return x->hip_fail(e, "ds serialize");
   const unsigned long long* ck = d->h_clock.as<unsigned long long>();
   cph = std::make_unique<HostPhase>("  cd: head + tail bytes");
   Dots clock;
@@ -2023,13 +2057,6 @@ static int ds_serialize_dev(ce_core* c, ce_ctx* x, const uint8_t* outer, const u
   if ((e = x->blob.reserve(A + 256 + hw.b.size() + tw.b.size())) ||
       (e = x->h_stage.reserve(std::max<uint64_t>(total_max + 64, 256 + hw.b.size() + tw.b.size()))))
     return x->hip_fail(e, "ds compact reserve");
-  for (int k = 0; k < 15; k++) {
-    // 0-3 u32 sort keys / perms, 4-6 u64 keys / sorted members / values, 7-10 actors, heads,
-    // ranks, lengths, 11 entry CSR (n + 1), 12 byte offsets
-    const size_t sz = k >= 4 && k <= 6 ? 8ull * nl + 64 : k <= 12 ? 4ull * nl + 68 : 64;
-    if ((e = d->ser[k].reserve(sz))) return x->hip_fail(e, "ds compact reserve");
-  }
-  if ((e = d->ser[15].reserve(orswot_ser_tmp_bytes(std::max<uint32_t>(nl, 1))))) return x->hip_fail(e, "ds compact reserve");
   uint8_t* db = x->blob.as<uint8_t>();
   uint8_t* hs = x->h_stage.as<uint8_t>();
   std::memset(hs, 0, 128);
@@ -2040,28 +2067,6 @@ static int ds_serialize_dev(ce_core* c, ce_ctx* x, const uint8_t* outer, const u
   std::memcpy(hs + 128 + hw.b.size(), tw.b.data(), tw.b.size());
   if ((e = hipMemcpyAsync(db + A, hs, 128 + hw.b.size() + tw.b.size(), hipMemcpyHostToDevice, s)))
     return x->hip_fail(e, "ds compact upload");
-  OrswotSerScratch sc{};
-  sc.member_in = d->col[0].as<unsigned long long>();
-  sc.actor_in = d->col[1].as<uint32_t>();
-  sc.value_in = d->col[2].as<unsigned long long>();
-  sc.rank_of_id = d->rank_of_id.as<uint32_t>();
-  sc.rank_bits = bits_for(na);
-  sc.member_bits = max_member ? 64 - __builtin_clzll(max_member) : 1;  // radix passes over those bits only
-  sc.k32a = d->ser[0].as<uint32_t>();
-  sc.k32b = d->ser[1].as<uint32_t>();
-  sc.p32a = d->ser[2].as<uint32_t>();
-  sc.p32b = d->ser[3].as<uint32_t>();
-  sc.k64a = d->ser[4].as<unsigned long long>();
-  sc.member_sorted = d->ser[5].as<unsigned long long>();
-  sc.value_sorted = d->ser[6].as<unsigned long long>();
-  sc.actor_sorted = d->ser[7].as<uint32_t>();
-  sc.head = d->ser[8].as<uint32_t>();
-  sc.hrank = d->ser[9].as<uint32_t>();
-  sc.len = d->ser[10].as<uint32_t>();
-  sc.seg = d->ser[11].as<uint32_t>();
-  sc.pos = d->ser[12].as<uint32_t>();
-  sc.tmp = d->ser[15].p;
-  sc.tmp_bytes = d->ser[15].cap;
   OrswotSerArgs a{};
   a.out = dst && dst_cap >= U ? dst : db;
   a.prefix = db + A + 128;
@@ -2073,8 +2078,7 @@ static int ds_serialize_dev(ce_core* c, ce_ctx* x, const uint8_t* outer, const u
   auto* offs = reinterpret_cast<unsigned long long*>(db + A);  // [0] 0, [1] clear len, [2] out_offs
   a.seal_offs = offs;
   a.stats = reinterpret_cast<uint32_t*>(db + A + 24);
-  const int t = x->tbegin("ds_serialize");
-  if ((e = launch_orswot_ser(s, sc, a))) return x->hip_fail(e, "ds serialize");
+  if ((e = launch_orswot_ser_write(s, sc, a))) return x->hip_fail(e, "ds serialize");
   x->tend(t);
   *A_out = A;
   *U_out = U;

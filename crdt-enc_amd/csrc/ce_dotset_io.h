@@ -48,6 +48,10 @@ struct OrswotSerScratch {
   size_t tmp_bytes;
 };
 hipError_t launch_orswot_ser(hipStream_t s, OrswotSerScratch& sc, const OrswotSerArgs& a);
+// the same in two halves: the sorts and scans over the n collected pairs (no host input), then the
+// writer (needs the host-built prefix / suffix) -- the host builds them while the sorts run
+hipError_t launch_orswot_ser_sort(hipStream_t s, OrswotSerScratch& sc, uint32_t n);
+hipError_t launch_orswot_ser_write(hipStream_t s, const OrswotSerScratch& sc, const OrswotSerArgs& a);
 size_t orswot_ser_tmp_bytes(uint32_t n);
 
 // reader over the bytes [lo, hi) of state plaintext s that follow the entries map header

@@ -458,10 +458,13 @@ uint32_t orswot_read_chunks(uint64_t lo, uint64_t hi) {
 }
 
 hipError_t launch_orswot_ser(hipStream_t s, OrswotSerScratch& sc, const OrswotSerArgs& in) {
+  hipError_t e = launch_orswot_ser_sort(s, sc, in.n);
+  return e ? e : launch_orswot_ser_write(s, sc, in);
+}
+
+hipError_t launch_orswot_ser_sort(hipStream_t s, OrswotSerScratch& sc, uint32_t n) {
   // pairs (member, actor id, value) in collect order -> sorted by (member, rank): sort by rank,
   // then stably by member (LSD order), gather
-  OrswotSerArgs a = in;
-  const uint32_t n = a.n;
   hipError_t e;
   if (n) {
     size_t tb = sc.tmp_bytes;
@@ -485,6 +488,14 @@ hipError_t launch_orswot_ser(hipStream_t s, OrswotSerScratch& sc, const OrswotSe
                        sc.hrank, sc.seg, sc.len, n);
     tb = sc.tmp_bytes;
     if ((e = hipcub::DeviceScan::ExclusiveSum(sc.tmp, tb, sc.len, sc.pos, (int)n, s))) return e;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_orswot_ser_write(hipStream_t s, const OrswotSerScratch& sc, const OrswotSerArgs& in) {
+  OrswotSerArgs a = in;
+  const uint32_t n = a.n;
+  if (n) {
     a.member = sc.member_sorted;
     a.actor = sc.actor_sorted;
     a.value = sc.value_sorted;
