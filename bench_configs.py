@@ -559,6 +559,27 @@ def dots_plaintext(uuid, k, ctr0):
     return APP + hdr + d.tobytes()
 
 
+def c4_roofline(pt_len, f_len, k_ms):
+    """C4's segment pass (multi-page files: open + Vec<Dot> decode + fold in k_segments) against
+    the VALU slot peak, like C2's line: ops = 992 * ceil(ct / 64) + 48 * (ceil(ct / 16) + 1) per file
+    (ct = plaintext length), summed over the files the pass takes, / its average launch"""
+    def ops(x):
+        return 992 * -(-x // 64) + 48 * (-(-x // 16) + 1)
+    big = [i for i, x in enumerate(pt_len) if x > 4096]
+    seg_ms = k_ms.get("segments_open")
+    if not big or not seg_ms:
+        return None
+    o = sum(ops(pt_len[i]) for i in big)
+    b = sum(f_len[i] + pt_len[i] for i in big)     # ciphertext read + plaintext written
+    achieved = o / (seg_ms / 1e3) / 1e12
+    return {"kernel": "k_segments<false,true> (multi-page open + decode + fold)", "bound": "valu",
+            "files": len(big), "ops_per_launch": o, "avg_launch_ms": seg_ms,
+            "achieved": round(achieved, 2), "peak": 78.6, "unit": "T int32 lane-ops/s",
+            "frac": round(achieved / 78.6, 4),
+            "hbm": {"bytes_per_launch": b, "achieved_GBps": round(b / (seg_ms / 1e3) / 1e9, 1), "peak_GBps": 8000.0},
+            "ops_formula": "992*ceil(ct/64) + 48*(ceil(ct/16)+1) per multi-page file / avg launch of segments_open"}
+
+
 def run_c4(args, ctx, dev):
     import msgpack
     actors = actors_table()[::4]                      # 1024 actors, UUID order
@@ -662,6 +683,7 @@ def run_c4(args, ctx, dev):
                    "dots": int(kd.sum())},
         "aead_GBps_end_to_end": round(ct / (ms / 1e3) / 1e9, 1),
         "kernels_ms_per_step": k_ms,
+        "roofline": c4_roofline(pt_len, f_len, k_ms),
         "clock": clock,
         # multi-segment files folded from the segment pass's records vs decoded whole, over
         # every ingest of the run (warmup + steps)

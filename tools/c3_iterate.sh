@@ -1,4 +1,5 @@
 set -o pipefail
+# C3 iteration on the GPU box: dot-set tests, the C3 line with and without the content names, one traced step
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_dotset.py > gpurun_out/g5.log 2>&1 && \
