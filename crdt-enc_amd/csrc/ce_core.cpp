@@ -714,22 +714,30 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
   ga.flags = ctx->counters.as<uint32_t>() + 12;  // [12] not grouped, [13] first gap
   ga.apply = ctx->apply.as<uint8_t>();
 
-  // the gate block upload on a side stream, overlapping the fill and setup kernels (the main
-  // stream waits for it before the gate; the regions it writes are not the fill's): e0 | wslot,
-  // and with a compaction behind the ingest the pre-ingest next_op_versions
-  if ((!ctx->side && (e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking))) ||
-      (!ctx->up_ev && (e = hipEventCreateWithFlags(&ctx->up_ev, hipEventDisableTiming))) ||
-      (e = hipMemcpyAsync(gbase, he0, 12ull * m, hipMemcpyHostToDevice, ctx->side)) ||
-      (after_commit && (e = hipMemcpyAsync(gbase + 32ull * m, reinterpret_cast<uint8_t*>(he0) + 32ull * m,
-                                           8ull * c->cap, hipMemcpyHostToDevice, ctx->side))) ||
-      (e = hipEventRecord(ctx->up_ev, ctx->side)))
+  // the gate block (e0 | wslot, and with a compaction behind the ingest the pre-ingest
+  // next_op_versions) read by the scratch fill itself from the mapped pinned stage: no DMA and
+  // no cross-stream event before the gate (CE_GATE_DMA=1: the side-stream upload, for A/B)
+  static const bool gate_dma = getenv("CE_GATE_DMA") != nullptr;
+  const uint8_t* he0_dev = nullptr;
+  if (!gate_dma) {
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, he0, 0) == hipSuccess) he0_dev = static_cast<const uint8_t*>(dp);
+    else (void)hipGetLastError();
+  }
+  if (!he0_dev &&
+      ((!ctx->side && (e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking))) ||
+       (!ctx->up_ev && (e = hipEventCreateWithFlags(&ctx->up_ev, hipEventDisableTiming))) ||
+       (e = hipMemcpyAsync(gbase, he0, 12ull * m, hipMemcpyHostToDevice, ctx->side)) ||
+       (after_commit && (e = hipMemcpyAsync(gbase + 32ull * m, reinterpret_cast<uint8_t*>(he0) + 32ull * m,
+                                            8ull * c->cap, hipMemcpyHostToDevice, ctx->side))) ||
+       (e = hipEventRecord(ctx->up_ev, ctx->side))))
     return ctx->hip_fail(e, "gate upload");
 
   // 1) GPU: scratch initialisation (one launch: counters, gate, batch state, miss / redo
   //    marks), device gate, setup (outer version, envelope, key schedule)
   static const bool gate_after_setup = getenv("CE_GATE_AFTER_SETUP") != nullptr;
   auto launch_gate_now = [&]() -> int {
-    if ((e = hipStreamWaitEvent(ctx->stream, ctx->up_ev, 0))) return ctx->hip_fail(e, "gate upload");
+    if (!he0_dev && (e = hipStreamWaitEvent(ctx->stream, ctx->up_ev, 0))) return ctx->hip_fail(e, "gate upload");
     const int t = ctx->tbegin("gate");
     if ((e = sharded ? launch_gate_window(ctx->stream, ga, shard_hi, ctx->counters.as<uint32_t>())
                      : launch_gate(ctx->stream, ga)))
@@ -745,6 +753,12 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
     fl.r[2] = {ctx->refold.as<uint32_t>(), (n + 3ull) / 4, 0u};
     fl.r[3] = {ctx->redo.as<uint32_t>(), (n + 3ull) / 4, 0u};
     fl.n = 4;
+    if (he0_dev) {
+      fl.r[fl.n++] = {reinterpret_cast<uint32_t*>(gbase), 3ull * m, 0u, reinterpret_cast<const uint32_t*>(he0_dev)};
+      if (after_commit)
+        fl.r[fl.n++] = {reinterpret_cast<uint32_t*>(gbase + 32ull * m), 2ull * c->cap, 0u,
+                        reinterpret_cast<const uint32_t*>(he0_dev + 32ull * m)};
+    }
     // device_open's setup only; the fused kernel replaces its segment pass for small files.
     // The gate between the fill and the setup (it needs the filled gate block and the uploaded
     // e0, not the setup), so the setup runs straight into the fused kernel (CE_GATE_AFTER_SETUP:

@@ -62,6 +62,7 @@ struct FillRange {
   uint32_t* p;
   uint64_t words;
   uint32_t value;
+  const uint32_t* src = nullptr;  // non-null: copy `words` words from src (e.g. mapped pinned host memory)
 };
 struct FillArgs {
   FillRange r[kMaxFill];

@@ -1274,6 +1274,11 @@ __global__ void k_fill(FillArgs a) {
     return;
   }
   const FillRange f = a.r[r];
+  if (f.src) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < f.words; i += (uint64_t)gridDim.x * blockDim.x)
+      f.p[i] = f.src[i];
+    return;
+  }
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < f.words; i += (uint64_t)gridDim.x * blockDim.x)
     f.p[i] = f.value;
 }
