@@ -7,6 +7,7 @@
 // next_op_versions (lib.rs:741) is a dense u64[cap] on the host (the version gate runs there
 // while the GPU decrypts).  Serialization sorts slots by UUID bytes = BTreeMap order.
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <functional>
 #include <set>
@@ -777,16 +778,32 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
   // the setup's counters (large-file count [9]) -> host behind an event: read while the fused
   // kernel runs, they decide whether the multi-page kernels are launched at all
   uint32_t* hsetup = ctx->h_counters.as<uint32_t>() + 32;
-  if ((!ctx->setup_ev && (e = hipEventCreateWithFlags(&ctx->setup_ev, hipEventDisableTiming))) ||
-      (!ctx->side_ev && (e = hipEventCreateWithFlags(&ctx->side_ev, hipEventDisableTiming))) ||
-      (!ctx->side && (e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking))))
-    return ctx->hip_fail(e, "event");
-  // on the side stream, behind the setup kernel: the main stream goes on to the gate and the
-  // fused kernel without a copy between them
-  if ((e = hipEventRecord(ctx->side_ev, ctx->stream)) || (e = hipStreamWaitEvent(ctx->side, ctx->side_ev, 0)) ||
-      (e = hipMemcpyAsync(hsetup, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->side)) ||
-      (e = hipEventRecord(ctx->setup_ev, ctx->side)))
-    return ctx->hip_fail(e, "setup counters");
+  // a one-wave kernel behind the setup writes its counters into the mapped pinned words with a
+  // generation after them (no event marker or side-stream copy between the setup and the fused
+  // kernel; CE_SETUP_EVENT=1: that older form, for A/B)
+  static const bool setup_event = getenv("CE_SETUP_EVENT") != nullptr;
+  uint32_t* hsetup_dev = nullptr;
+  if (!setup_event) {
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, hsetup, 0) == hipSuccess) hsetup_dev = static_cast<uint32_t*>(dp);
+    else (void)hipGetLastError();
+  }
+  const uint32_t gen = ++ctx->publish_gen ? ctx->publish_gen : ++ctx->publish_gen;  // never 0
+  if (hsetup_dev) {
+    if ((e = launch_publish_words(ctx->stream, ctx->counters.as<uint32_t>(), 16, hsetup_dev, gen)))
+      return ctx->hip_fail(e, "setup counters");
+  } else {
+    if ((!ctx->setup_ev && (e = hipEventCreateWithFlags(&ctx->setup_ev, hipEventDisableTiming))) ||
+        (!ctx->side_ev && (e = hipEventCreateWithFlags(&ctx->side_ev, hipEventDisableTiming))) ||
+        (!ctx->side && (e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking))))
+      return ctx->hip_fail(e, "event");
+    // on the side stream, behind the setup kernel: the main stream goes on to the gate and the
+    // fused kernel without a copy between them
+    if ((e = hipEventRecord(ctx->side_ev, ctx->stream)) || (e = hipStreamWaitEvent(ctx->side, ctx->side_ev, 0)) ||
+        (e = hipMemcpyAsync(hsetup, ctx->counters.p, 64, hipMemcpyDeviceToHost, ctx->side)) ||
+        (e = hipEventRecord(ctx->setup_ev, ctx->side)))
+      return ctx->hip_fail(e, "setup counters");
+  }
   bool setup_known = false;
   uint32_t n_large = 0;
   if (gate_after_setup) {
@@ -837,8 +854,21 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
       if ((e = launch_open_fold_small(ctx->stream, da, c->files_per_wave))) return ctx->hip_fail(e, "fused");
       ctx->tend(t);
     }
-    if (!setup_known) {  // landed long ago: the gate and the fused kernel follow it
-      if ((e = hipEventSynchronize(ctx->setup_ev))) return ctx->hip_fail(e, "setup counters");
+    if (!setup_known) {  // landed long ago: the fused kernel follows it
+      if (hsetup_dev) {
+        volatile const uint32_t* hp = hsetup;
+        for (uint64_t i = 0; hp[16] != gen; i++) {
+          if (i >= 64) sched_yield();
+          if (i == (1ull << 22)) {  // (never expected) the stream's own wait, then the word must be there
+            if ((e = hipStreamSynchronize(ctx->stream))) return ctx->hip_fail(e, "setup counters");
+          } else if (i > (1ull << 22) && hp[16] != gen) {
+            return ctx->fail(CE_ERR_DEVICE, "setup counters never published");
+          }
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+      } else if ((e = hipEventSynchronize(ctx->setup_ev))) {
+        return ctx->hip_fail(e, "setup counters");
+      }
       n_large = hsetup[9];
       setup_known = true;
     }

@@ -128,6 +128,7 @@ struct ce_ctx {
   ce::DevBuf params, status, counters, extra, multi, partials, large, out, apply, refold, miss,
       supported, blob, offs, nonces, out_offs, outer_ver, batch_counters, split, segrec, redo, heads;
   ce::HostBuf h_counters, h_apply, h_stage, h_stage2, h_heads;
+  uint32_t publish_gen = 0;  // k_publish_words generations (the setup's counters, C2 path)
   // marks the setup kernel's counter snapshot (h_counters + 128) as landed on the host
   hipEvent_t setup_ev = nullptr;
   // a side stream for readbacks that must not sit between the main stream's kernels (the setup

@@ -70,6 +70,8 @@ struct FillArgs {
   uint32_t* counters;  // or null
 };
 hipError_t launch_fill(hipStream_t s, const FillArgs& a);
+// src[0..n) -> dst[0..n) (mapped pinned memory), then dst[n] = gen once they are visible (n <= 64)
+hipError_t launch_publish_words(hipStream_t s, const uint32_t* src, uint32_t n, uint32_t* dst, uint32_t gen);
 // a compaction's sealed-file length (clear length read on the device at clear_len_at, <= bound;
 // ~0 when over cap, ~1 when over bound) -> len_out (mapped pinned memory)
 hipError_t launch_publish_sealed_len(hipStream_t s, const uint64_t* clear_len_at, uint64_t bound, uint64_t cap,

@@ -1293,6 +1293,20 @@ __global__ void k_publish_sealed_len(const uint64_t* clear_len_at, uint64_t boun
   *reinterpret_cast<volatile uint64_t*>(len_out) = cl > bound ? ~1ull : total > cap ? ~0ull : total;
 }
 
+// n counter words -> mapped pinned memory, then the generation word after them (the host polls
+// it): one wave; the fence orders every lane's stores before lane 0's generation store
+__global__ void k_publish_words(const uint32_t* src, uint32_t n, uint32_t* dst, uint32_t gen) {
+  if (threadIdx.x < n) reinterpret_cast<volatile uint32_t*>(dst)[threadIdx.x] = src[threadIdx.x];
+  __threadfence_system();
+  if (threadIdx.x == 0) reinterpret_cast<volatile uint32_t*>(dst)[n] = gen;
+}
+
+hipError_t launch_publish_words(hipStream_t s, const uint32_t* src, uint32_t n, uint32_t* dst, uint32_t gen) {
+  if (n > 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_publish_words, dim3(1), dim3(64), 0, s, src, n, dst, gen);
+  return hipGetLastError();
+}
+
 hipError_t launch_publish_sealed_len(hipStream_t s, const uint64_t* clear_len_at, uint64_t bound, uint64_t cap,
                                      uint64_t* len_out) {
   hipLaunchKernelGGL(k_publish_sealed_len, dim3(1), dim3(1), 0, s, clear_len_at, bound, cap, len_out);
