@@ -2119,9 +2119,10 @@ int ce_core_reset(ce_core* c) {
   std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
   std::fill(c->nov.begin(), c->nov.end(), 0);
   c->read_states.clear();
+  if (is_dotset_kind(c->kind)) return ds_reset(c);  // (the dense state array is the VClock kinds')
   hipError_t e = hipMemsetAsync(c->d_state.p, 0, c->cap * 8ull, c->ctx->stream);
   if (e) return c->ctx->hip_fail(e, "reset");
-  return is_dotset_kind(c->kind) ? ds_reset(c) : CE_OK;
+  return CE_OK;
 }
 
 int ce_core_register_actors(ce_core* c, const uint8_t* actors, uint32_t m) {

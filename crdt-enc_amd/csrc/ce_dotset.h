@@ -171,9 +171,11 @@ hipError_t ds_excl_max_by_key(void* tmp, size_t& tb, const uint32_t* keys,
 hipError_t ds_excl_sum_u32(void* tmp, size_t& tb, const uint32_t* in, uint32_t* out, uint32_t n,
                            hipStream_t s);
 // totals of the kCntN columns of one back-to-back exclusive scan (out[kCntN], device)
-// out (17 words): column totals [0..kCntN), column maxima [8..8+kCntN), status summary [13..17)
+// out (19 words): column totals [0..kCntN), column maxima [8..8+kCntN), status summary [13..17),
+// the gate's two flags [17..19) (gate_flags may be null); then clear8[0..8) = 0 (may be null)
 hipError_t launch_ds_col_totals(hipStream_t s, const uint32_t* cnt, const uint32_t* bases, uint32_t n,
-                                const uint32_t* maxima, const int32_t* status, uint32_t* out);
+                                const uint32_t* maxima, const int32_t* status, const uint32_t* gate_flags,
+                                uint32_t* clear8, uint32_t* out);
 hipError_t launch_ds_set3(hipStream_t s, uint32_t* p0, uint32_t v0, uint32_t* p1, uint32_t v1, uint32_t* p2,
                           uint32_t v2);
 

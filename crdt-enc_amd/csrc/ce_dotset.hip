@@ -955,9 +955,11 @@ hipError_t ds_excl_sum_u32(void* tmp, size_t& tb, const uint32_t* in, uint32_t* 
 // needs in one download: out[0..kCntN) column totals (last base + last count - first base),
 // out[8..8+kCntN) the largest per-file count of each column (k_ds_count's counters[8..]),
 // out[13..16) the status summary: files not OK, files left to the host envelope parser, files
-// left to the host op decoder; out[16] the first file not OK (0xffffffff: none)
+// left to the host op decoder; out[16] the first file not OK (0xffffffff: none); out[17..19) the
+// version gate's flags (gate_flags, when given); then clear8[0..8) = 0 (the emit's counters)
 __global__ void __launch_bounds__(1024) k_ds_col_totals(const uint32_t* cnt, const uint32_t* bases, uint32_t n,
-                                                        const uint32_t* maxima, const int32_t* status, uint32_t* out) {
+                                                        const uint32_t* maxima, const int32_t* status,
+                                                        const uint32_t* gate_flags, uint32_t* clear8, uint32_t* out) {
   __shared__ uint32_t acc[4];
   const uint32_t k = threadIdx.x;
   if (k < 3) acc[k] = 0;
@@ -967,7 +969,9 @@ __global__ void __launch_bounds__(1024) k_ds_col_totals(const uint32_t* cnt, con
     out[k] = bases[cl] + cnt[cl] - bases[c0];
     out[8 + k] = maxima[k];
   }
+  if (gate_flags && k < 2) out[17 + k] = gate_flags[k];
   __syncthreads();
+  if (clear8 && k < 8) clear8[k] = 0;  // the emit's counters (after the maxima above were read)
   uint32_t bad = 0, hp = 0, hd = 0, first = 0xffffffffu;
   for (uint32_t i = k; i < n; i += blockDim.x) {
     const int32_t st = status[i];
@@ -989,9 +993,11 @@ __global__ void __launch_bounds__(1024) k_ds_col_totals(const uint32_t* cnt, con
 }
 
 hipError_t launch_ds_col_totals(hipStream_t s, const uint32_t* cnt, const uint32_t* bases, uint32_t n,
-                                const uint32_t* maxima, const int32_t* status, uint32_t* out) {
+                                const uint32_t* maxima, const int32_t* status, const uint32_t* gate_flags,
+                                uint32_t* clear8, uint32_t* out) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ds_col_totals, dim3(1), dim3(1024), 0, s, cnt, bases, n, maxima, status, out);
+  hipLaunchKernelGGL(k_ds_col_totals, dim3(1), dim3(1024), 0, s, cnt, bases, n, maxima, status, gate_flags,
+                     clear8, out);
   return hipGetLastError();
 }
 

@@ -99,7 +99,7 @@ DsTables tables(DsState* d) {
   return t;
 }
 
-int tables_alloc(ce_core* c, uint32_t cap) {
+int tables_alloc(ce_core* c, uint32_t cap, const FillRange* extra = nullptr) {
   DsState* d = c->ds;
   ce_ctx* ctx = c->ctx;
   hipError_t e;
@@ -120,6 +120,7 @@ int tables_alloc(ce_core* c, uint32_t cap) {
   fl.r[6] = {d->hold.as<uint32_t>(), cap * 2ull, 0u};
   fl.r[7] = {d->live.as<uint32_t>(), 16, 0u};
   fl.n = 8;
+  if (extra) fl.r[fl.n++] = *extra;
   if ((e = launch_fill(ctx->stream, fl))) return ctx->hip_fail(e, "dot-set tables");
   d->used_pairs = 0;
   d->live_pairs = 0;
@@ -756,7 +757,8 @@ struct GateJob {
 };
 
 int gate_enqueue(ce_core* c, const uint32_t* d_fa, const uint64_t* d_fv, uint32_t n, uint32_t m,
-                 const std::vector<uint32_t>& wslot, std::vector<uint64_t>* expect, GateJob* job) {
+                 const std::vector<uint32_t>& wslot, std::vector<uint64_t>* expect, GateJob* job,
+                 const FillRange* extra = nullptr) {
   ce_ctx* ctx = c->ctx;
   hipError_t e;
   if ((e = ctx->apply.reserve(n + 64)) || (e = c->d_gate.reserve(m * 24ull + 64)) ||
@@ -780,15 +782,27 @@ int gate_enqueue(ce_core* c, const uint32_t* d_fa, const uint64_t* d_fv, uint32_
   ga.run_first = reinterpret_cast<uint32_t*>(gbase + 20ull * m);
   ga.flags = ctx->counters.as<uint32_t>() + 12;
   ga.apply = ctx->apply.as<uint8_t>();
-  if ((e = hipMemcpyAsync(gbase, he0, m * 8ull, hipMemcpyHostToDevice, ctx->stream)) ||
-      (e = hipMemsetAsync(gbase + 8ull * m, 0, 16ull * m, ctx->stream)) ||
-      (e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ga.flags), 0u, 1, ctx->stream)) ||
-      (e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ga.flags + 1), 0xffffffffu, 1, ctx->stream)))
-    return ctx->hip_fail(e, "gate");
+  // one launch: e0 copied from the mapped pinned stage, the gate's scratch and flags set, and the
+  // caller's extra range (the count pass's counters)
+  void* he0_dev = nullptr;
+  if (hipHostGetDevicePointer(&he0_dev, he0, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    he0_dev = nullptr;
+  }
+  FillArgs fl{};
+  if (he0_dev) fl.r[fl.n++] = {reinterpret_cast<uint32_t*>(gbase), 2ull * m, 0u, static_cast<const uint32_t*>(he0_dev)};
+  else if ((e = hipMemcpyAsync(gbase, he0, m * 8ull, hipMemcpyHostToDevice, ctx->stream))) return ctx->hip_fail(e, "gate");
+  fl.r[fl.n++] = {reinterpret_cast<uint32_t*>(gbase + 8ull * m), 4ull * m, 0u};
+  fl.r[fl.n++] = {ga.flags, 1, 0u};
+  fl.r[fl.n++] = {ga.flags + 1, 1, 0xffffffffu};
+  if (extra) fl.r[fl.n++] = *extra;
+  if ((e = launch_fill(ctx->stream, fl))) return ctx->hip_fail(e, "gate");
   const int t = ctx->tbegin("gate");
   if ((e = launch_gate(ctx->stream, ga))) return ctx->hip_fail(e, "gate");
   ctx->tend(t);
-  if ((e = hipMemcpyAsync(job->hf, ga.flags, 8, hipMemcpyDeviceToHost, ctx->stream)) ||
+  // the flags come back with the caller's next download when it passes `extra` (k_ds_col_totals
+  // copies them), else here
+  if ((!extra && (e = hipMemcpyAsync(job->hf, ga.flags, 8, hipMemcpyDeviceToHost, ctx->stream))) ||
       (e = hipMemcpyAsync(job->hnn, ga.newnov, m * 8ull, hipMemcpyDeviceToHost, ctx->stream)))
     return ctx->hip_fail(e, "gate");
   return CE_OK;
@@ -905,9 +919,11 @@ int ds_reset(ce_core* c) {
   d->deferred.clear();
   d->vals.clear();
   hipError_t e;
+  const FillRange clock_zero{d->clock.as<uint32_t>(), 2ull * d->clock_cap, 0u};
+  if (c->kind == CE_STATE_ORSWOT)  // the clock cleared by the tables' fill launch
+    return tables_alloc(c, std::max<uint32_t>(4096, d->pcap), d->clock_cap ? &clock_zero : nullptr);
   if (d->clock_cap && (e = hipMemsetAsync(d->clock.p, 0, d->clock_cap * 8ull, c->ctx->stream)))
     return c->ctx->hip_fail(e, "reset");
-  if (c->kind == CE_STATE_ORSWOT) return tables_alloc(c, std::max<uint32_t>(4096, d->pcap));
   return CE_OK;
 }
 
@@ -947,7 +963,8 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
   uint32_t first_gap = n;
   std::vector<uint64_t> expect;
   GateJob gj;
-  if ((rc = gate_enqueue(c, d_fa, d_fv, n, m, wslot, &expect, &gj))) return rc;
+  const FillRange count_counters{d->misses.as<uint32_t>(), 16, 0u};  // the count pass's counters
+  if ((rc = gate_enqueue(c, d_fa, d_fv, n, m, wslot, &expect, &gj, &count_counters))) return rc;
   DsDecodeArgs a = decode_args(c, n);
   if ((uint64_t)kCntN * n > 0x7fffffffull) return ctx->fail(CE_ERR_INVALID_ARG, "batch too large for one scan");
   uint32_t* cnt = d->cnt.as<uint32_t>();
@@ -959,25 +976,30 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
       return ctx->hip_fail(e, "scan");
   }
   uint32_t* hsum = d->h_cnt.as<uint32_t>() + 64;  // pinned: the col_totals block (17 words)
+  bool counters_clear = true;  // the gate's fill cleared them for the first pass
   auto count_pass = [&]() -> int {
     if (n == 0) {
-      std::memset(hsum, 0, 17 * 4);
+      std::memset(hsum, 0, 19 * 4);
+      hsum[18] = 0xffffffffu;
       return CE_OK;
     }
     size_t t = d->cub_tmp.cap;
-    if ((e = hipMemsetAsync(d->misses.p, 0, 64, ctx->stream))) return ctx->hip_fail(e, "count");
+    if (!counters_clear && (e = hipMemsetAsync(d->misses.p, 0, 64, ctx->stream))) return ctx->hip_fail(e, "count");
+    counters_clear = false;
     const int tc = ctx->tbegin("ds_count");
     if ((e = launch_ds_count(ctx->stream, a))) return ctx->hip_fail(e, "count");
     ctx->tend(tc);
     if ((e = ds_excl_sum_u32(d->cub_tmp.p, t, cnt, bases, kCntN * n, ctx->stream)) ||
         (e = launch_ds_col_totals(ctx->stream, cnt, bases, n, d->misses.as<uint32_t>() + 8, ctx->status.as<int32_t>(),
+                                  ctx->counters.as<uint32_t>() + 12, d->misses.as<uint32_t>(),
                                   d->cnt_tot.as<uint32_t>())) ||
-        (e = hipMemcpyAsync(hsum, d->cnt_tot.p, 17 * 4, hipMemcpyDeviceToHost, ctx->stream)))
+        (e = hipMemcpyAsync(hsum, d->cnt_tot.p, 19 * 4, hipMemcpyDeviceToHost, ctx->stream)))
       return ctx->hip_fail(e, "count");
     return CE_OK;
   };
   auto wait = [&](const char* what) { return (e = stream_wait(ctx->stream)) ? ctx->hip_fail(e, what) : CE_OK; };
   if ((rc = count_pass()) || (rc = wait("count"))) return rc;
+  gj.hf = hsum + 17;  // the gate's flags, copied by k_ds_col_totals
   if ((rc = ds_settle(c))) return rc;  // the previous fold / merge (drained by the wait above)
   bool recount = false;
   if (hsum[14]) {  // envelopes left to the host: normalize + open there, patch the batch
@@ -1054,7 +1076,8 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
   }
   for (int round = 0;; round++) {
     uint32_t hm[4];
-    if ((e = hipMemsetAsync(d->misses.p, 0, 64, ctx->stream))) return ctx->hip_fail(e, "emit");
+    // round 0: k_ds_col_totals (the last kernel of the count pass) cleared misses[0..8)
+    if (round > 0 && (e = hipMemsetAsync(d->misses.p, 0, 64, ctx->stream))) return ctx->hip_fail(e, "emit");
     const int te = ctx->tbegin("ds_emit");
     if ((e = launch_ds_emit(ctx->stream, a))) return ctx->hip_fail(e, "emit");
     ctx->tend(te);

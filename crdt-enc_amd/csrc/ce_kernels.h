@@ -57,7 +57,7 @@ struct SegScratch {
 // One launch for an ingest's scratch initialisation (each hipMemsetAsync is its own blit
 // dispatch with its own gap): ranges of u32 words set to a value, and the 16-word counter block
 // zeroed with [5] (first failing index) and [13] (the gate's first gap) = UINT32_MAX.
-static constexpr int kMaxFill = 8;
+static constexpr int kMaxFill = 10;
 struct FillRange {
   uint32_t* p;
   uint64_t words;
