@@ -178,6 +178,24 @@ def cgroup_cpus():
         return None
 
 
+def gpu_node_cpus(dev):
+    """CPUs of the NUMA node the GPU hangs off (sysfs), within this process's affinity; empty
+    when unknown"""
+    try:
+        p = torch.cuda.get_device_properties(dev)
+        bdf = "%04x:%02x:%02x.0" % (getattr(p, "pci_domain_id", 0), p.pci_bus_id, p.pci_device_id)
+        node = int(open("/sys/bus/pci/devices/%s/numa_node" % bdf).read())
+        if node < 0:
+            return set()
+        cpus = set()
+        for part in open("/sys/devices/system/node/node%d/cpulist" % node).read().strip().split(","):
+            a, _, b = part.partition("-")
+            cpus.update(range(int(a), int(b or a) + 1))
+        return cpus & os.sched_getaffinity(0)
+    except (OSError, ValueError, AttributeError, RuntimeError):
+        return set()
+
+
 def host_cpu():
     """(model, usable CPUs, threads for the best-CPU leg, how the count was chosen).  usable =
     min(affinity, cgroup quota); threads = min(usable, OMP_NUM_THREADS): the job's CPU share --
@@ -253,6 +271,7 @@ class Workload:
     """One variant's sealed batch on this rank, its core and its step function."""
 
     def __init__(self, ctx, variant, args, world, rank, dev, actors_all, scaling="weak"):
+        self.dev = dev
         self.variant = variant
         self.world, self.rank = world, rank
         self.actors_all = actors_all
@@ -429,7 +448,21 @@ class Workload:
         Returns the end-to-end files/s and the PCIe rate of the upload (HIP events on the copy
         stream)."""
         n = self.n
-        host = self.files[: self.blob_len].cpu().numpy()            # pageable, like Vec<u8>s
+        # pageable, like Vec<u8>s, first-touched on the GPU's NUMA node (where a deployment reads
+        # its files into; on the other socket the gather reads cross the socket link and the rate
+        # depends on which socket the process happened to start on: 43 vs 55 GB/s on two boxes)
+        staged = self.files[: self.blob_len].cpu().numpy()
+        cpus = gpu_node_cpus(self.dev)
+        old_aff = os.sched_getaffinity(0) if cpus else None
+        try:
+            if cpus:
+                os.sched_setaffinity(0, cpus)
+            host = np.empty_like(staged)
+            host[:] = staged
+        finally:
+            if old_aff:
+                os.sched_setaffinity(0, old_aff)
+        del staged
         base = host.ctypes.data
         offs = self.offs[: n + 1].cpu().numpy().astype(np.uint64)
         ptrs = (ctypes.c_void_p * n).from_buffer(np.ascontiguousarray(base + offs[:-1]).astype(np.uint64))
