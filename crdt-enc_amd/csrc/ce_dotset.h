@@ -158,7 +158,8 @@ hipError_t launch_ds_gather_entries(hipStream_t s, const uint32_t* perm, const u
                                     const unsigned long long* value_in, uint32_t* actor_out,
                                     unsigned long long* value_out, uint32_t n);
 
-// device-wide primitives (hipCUB): tmp = nullptr queries the temp size into tb
+// device-wide primitives (sorts: hipCUB; scans: ce_scan.hip): tmp = nullptr queries the temp
+// size into tb
 hipError_t ds_sort_pairs_u32(void* tmp, size_t& tb, const uint32_t* kin, uint32_t* kout,
                              const uint32_t* vin, uint32_t* vout, uint32_t n, int bits, hipStream_t s);
 hipError_t ds_sort_pairs_u64(void* tmp, size_t& tb, const unsigned long long* kin,

@@ -939,17 +939,8 @@ hipError_t ds_sort_pairs_u64(void* tmp, size_t& tb, const unsigned long long* ki
   return hipcub::DeviceRadixSort::SortPairs(tmp, tb, kin, kout, vin, vout, (int)n, 0, 64, s);
 }
 
-hipError_t ds_excl_max_by_key(void* tmp, size_t& tb, const uint32_t* keys,
-                              const unsigned long long* vals, unsigned long long* out, uint32_t n,
-                              hipStream_t s) {
-  return hipcub::DeviceScan::ExclusiveScanByKey(tmp, tb, keys, vals, out, MaxOp(), 0ull, (int)n,
-                                                hipcub::Equality(), s);
-}
-
-hipError_t ds_excl_sum_u32(void* tmp, size_t& tb, const uint32_t* in, uint32_t* out, uint32_t n,
-                           hipStream_t s) {
-  return hipcub::DeviceScan::ExclusiveSum(tmp, tb, in, out, (int)n, s);
-}
+// ds_excl_max_by_key / ds_excl_sum_u32: ce_scan.hip (no hipCUB: its scans query the device
+// properties on the host at every call)
 
 // One block after the count pass and its scan, so the host reads everything the emit's sizing
 // needs in one download: out[0..kCntN) column totals (last base + last count - first base),

@@ -429,7 +429,7 @@ hipError_t launch_orswot_read_multi(hipStream_t s, const OrswotReadArgs* d_args,
     }
     hipLaunchKernelGGL(k_rdm_count, dim3(gx, nf), dim3(kB), 0, s, d_args, chunk_cnt);
     size_t tb = tmp_bytes;
-    hipError_t e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, chunk_cnt, chunk_scan, (int)(nchunks + 1), s);
+    hipError_t e = ds_excl_sum_u32(tmp, tb, chunk_cnt, chunk_scan, nchunks + 1, s);
     if (e) return e;
     hipLaunchKernelGGL(k_rdm_write, dim3(gx, nf), dim3(kB), 0, s, d_args, chunk_scan);
     hipLaunchKernelGGL(k_rdm_found, dim3((nf + 63) / 64), dim3(64), 0, s, d_args, chunk_scan, nf);
@@ -449,7 +449,7 @@ hipError_t launch_orswot_read_multi(hipStream_t s, const OrswotReadArgs* d_args,
 
 size_t orswot_read_multi_tmp_bytes(uint32_t nchunks) {
   size_t b = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)(nchunks + 1));
+  (void)ds_excl_sum_u32(nullptr, b, nullptr, nullptr, nchunks + 1, nullptr);
   return b + 256;
 }
 
@@ -482,12 +482,12 @@ hipError_t launch_orswot_ser_sort(hipStream_t s, OrswotSerScratch& sc, uint32_t 
                        sc.actor_sorted, sc.value_sorted, n);
     hipLaunchKernelGGL(k_ser_head, dim3(nblk(n)), dim3(kB), 0, s, sc.member_sorted, sc.head, n);
     tb = sc.tmp_bytes;
-    if ((e = hipcub::DeviceScan::ExclusiveSum(sc.tmp, tb, sc.head, sc.hrank, (int)n, s))) return e;
+    if ((e = ds_excl_sum_u32(sc.tmp, tb, sc.head, sc.hrank, n, s))) return e;
     hipLaunchKernelGGL(k_ser_seg, dim3(nblk(n)), dim3(kB), 0, s, sc.member_sorted, sc.head, sc.hrank, sc.seg, n);
     hipLaunchKernelGGL(k_ser_len, dim3(nblk(n)), dim3(kB), 0, s, sc.member_sorted, sc.value_sorted, sc.head,
                        sc.hrank, sc.seg, sc.len, n);
     tb = sc.tmp_bytes;
-    if ((e = hipcub::DeviceScan::ExclusiveSum(sc.tmp, tb, sc.len, sc.pos, (int)n, s))) return e;
+    if ((e = ds_excl_sum_u32(sc.tmp, tb, sc.len, sc.pos, n, s))) return e;
   }
   return hipGetLastError();
 }
@@ -529,7 +529,7 @@ static size_t ser_tmp_bytes_raw(uint32_t n) {
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, (unsigned long long*)nullptr,
                                            (unsigned long long*)nullptr, (uint32_t*)nullptr,
                                            (uint32_t*)nullptr, (int)n, 0, 64);
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, c, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
+  (void)ds_excl_sum_u32(nullptr, c, nullptr, nullptr, n, nullptr);
   return std::max(a, std::max(b, c)) + 256;
 }
 
