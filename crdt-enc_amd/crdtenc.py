@@ -59,7 +59,7 @@ EXPORTS = [
     "ce_core_pending_commit", "ce_core_writer_versions", "ce_shard_stats_host",
     "ce_shard_window_host", "ce_shard_window_exact", "ce_core_compact_ops_device_into",
     "ce_core_state_bytes_device", "ce_core_merge_state_device", "ce_core_ingest_states_device",
-    "ce_core_compact_into_async", "ce_core_compact_wait", "ce_host_alloc", "ce_host_free",
+    "ce_core_compact_into_async", "ce_core_compact_wait", "ce_host_alloc", "ce_host_free", "ce_content_names",
 ]
 
 
@@ -248,6 +248,22 @@ def content_name(data):
     if rc:
         raise CeError(rc)
     return out.value.decode()
+
+
+def content_names(bufs):
+    """content_name of every buffer, eight SHA3-256 sponges per AVX-512 step (ce_content_names)"""
+    n = len(bufs)
+    if n == 0:
+        return []
+    held = [_ptr(b) for b in bufs]
+    ptrs = (ctypes.c_void_p * n)(*[ctypes.cast(p, ctypes.c_void_p) for p, _ in held])
+    lens = (ctypes.c_size_t * n)(*[k for _, k in held])
+    out = (ctypes.c_char * (64 * n))()
+    rc = lib().ce_content_names(ptrs, lens, ctypes.c_uint32(n), out)
+    if rc:
+        raise CeError(rc)
+    raw = bytes(out)
+    return [raw[64 * i: 64 * (i + 1)].split(b"\0", 1)[0].decode() for i in range(n)]
 
 
 class NameJob:

@@ -88,6 +88,9 @@ constexpr int kRho[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43,
                           25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
 }  // namespace
 
+static void keccakf(uint64_t s[25]);
+void keccakf_portable(uint64_t s[25]) { keccakf(s); }  // (ce_sha3x8.cpp: message tails)
+
 static void keccakf(uint64_t s[25]) {
   for (int r = 0; r < 24; r++) {
     uint64_t c[5], b[25];

@@ -185,6 +185,10 @@ int ce_content_name(const uint8_t *data, size_t len, char name_out[64]);
    until ce_content_name_wait(ticket) returns.  Jobs run in submission order; a ticket is waited
    once. */
 int ce_content_name_async(const uint8_t *data, size_t len, uint64_t *ticket);
+/* ce_content_name of n buffers at once: eight SHA3-256 sponges per AVX-512 core step (the
+ * pipelined compactions' names, crdt-enc-tokio/src/lib.rs:403-432); names_out[i] as
+ * ce_content_name's.  Same result as n ce_content_name calls. */
+int ce_content_names(const uint8_t *const *data, const size_t *lens, uint32_t n, char (*names_out)[64]);
 int ce_content_name_wait(uint64_t ticket, char name_out[64]);
 
 /* ---------------------------------------------------------------------------------------- */

@@ -228,3 +228,20 @@ def test_no_gpu_means_no_compute():
     with pytest.raises(crdtenc.CeError) as e:
         crdtenc.Context(0)
     assert e.value.code == 65
+
+
+def test_content_names_multi_buffer_matches_hashlib():
+    """ce_content_names (eight SHA3-256 sponges per AVX-512 step, message tails on their own
+    sponge) == BASE32_NOPAD(SHA3-256) per buffer, for batches of 1-17 with equal and mixed
+    lengths around the 136-byte rate, empty buffers included (and the scalar fallback when the CPU
+    has no AVX-512F: the same answers)."""
+    import random
+    import numpy as np
+    rng = random.Random(11)
+    for n in (1, 2, 3, 7, 8, 9, 16, 17):
+        for mixed in (False, True):
+            lens = ([rng.choice([0, 1, 135, 136, 137, 271, 272, 1000, 5000, 136 * 50]) for _ in range(n)]
+                    if mixed else [rng.randint(0, 20000)] * n)
+            bufs = [np.frombuffer(os.urandom(k), np.uint8) if k else np.zeros(0, np.uint8) for k in lens]
+            want = [base64.b32encode(hashlib.sha3_256(b.tobytes()).digest()).decode().rstrip("=") for b in bufs]
+            assert crdtenc.content_names(bufs) == want, (n, lens)
