@@ -181,12 +181,60 @@ def _lower_priority():
         pass
 
 
+class BatchNamer:
+    """Content names on `threads` host threads, each taking up to `kmax` pending files at once
+    (crdtenc.content_names: eight SHA3-256 sponges per AVX-512 step, ~2.7x one core's rate at
+    eight, ~2x at four) -- submit() returns a Future of the name"""
+
+    def __init__(self, threads, kmax):
+        import collections
+        import threading
+        self.q = collections.deque()
+        self.cv = threading.Condition()
+        self.kmax, self.stop = kmax, False
+        self.th = [threading.Thread(target=self._run, daemon=True) for _ in range(threads)]
+        for t in self.th:
+            t.start()
+
+    def submit(self, buf):
+        from concurrent.futures import Future
+        f = Future()
+        with self.cv:
+            self.q.append((buf, f))
+            self.cv.notify()
+        return f
+
+    def _run(self):
+        _lower_priority()
+        while True:
+            with self.cv:
+                while not self.q and not self.stop:
+                    self.cv.wait()
+                if not self.q:
+                    return
+                batch = [self.q.popleft() for _ in range(min(self.kmax, len(self.q)))]
+            try:
+                for (_, f), nm in zip(batch, crdtenc.content_names([b for b, _ in batch])):
+                    f.set_result(nm)
+            except Exception as e:  # noqa: BLE001 -- every waiter sees the failure
+                for _, f in batch:
+                    f.set_exception(e)
+
+    def shutdown(self):
+        with self.cv:
+            self.stop = True
+            self.cv.notify_all()
+        for t in self.th:
+            t.join()
+
+
 class CompactPipe:
     """Pipelined Core::compact outputs (C3): NB pinned buffers; each file's download is left in
-    flight on the copy stream (ce_core_compact_into_async) while the next step runs on the
+    flight (ce_core_compact_into_async: an SDMA engine copy) while the next step runs on the
     device, then its SHA3-256 name (crdt-enc-tokio/src/lib.rs:403-432, a sequential sponge, ~48 ms
-    for 35 MB) is hashed on NB - 1 host threads.  flush() completes every download, drain() every
-    name; a buffer is reused only after its name is done."""
+    for 35 MB on one core) is hashed on the host threads, up to four pending files per
+    multi-buffer batch.  flush() completes every download, drain() every name; a buffer is reused
+    only after its name is done."""
 
     def __init__(self, core, nb=None, use_async=True):
         from concurrent.futures import ThreadPoolExecutor
@@ -195,7 +243,16 @@ class CompactPipe:
         self.core, self.nb, self.use_async = core, nb, use_async
         # the hashing threads below the launching thread's priority: the device pipeline's
         # host waits and launches are never queued behind a name (the names catch up in the gaps)
-        self.namer = ThreadPoolExecutor(nb - 1, initializer=_lower_priority)
+        # the names in multi-buffer batches of up to four pending files (crdtenc.content_names;
+        # same box, 120 steps: 3.10-3.47 ms/step against 3.76-3.78 one file per thread, 3.35 at
+        # three, 4.0 at eight -- a batch's latency is the drain); CE_NAME_BATCH=1: one per thread
+        kmax = int(os.environ.get("CE_NAME_BATCH", "4"))
+        if kmax > 1:   # more buffers in flight: a batch holds its files for its whole hash
+            nb = max(nb, int(os.environ.get("CE_NAME_BUFFERS", "32")))
+            self.nb = nb
+            self.namer = BatchNamer(name_threads(), kmax)
+        else:
+            self.namer = ThreadPoolExecutor(nb - 1, initializer=_lower_priority)
         self.obuf = [crdtenc.host_buffer(1 << 26) for _ in range(nb)]   # pinned: DMA-engine downloads
         self.fut = [None] * nb
         self.inflight = []      # (buffer, length, ticket) of downloads not yet waited for
@@ -208,7 +265,8 @@ class CompactPipe:
         self.last_file = self.obuf[k][:ln]
         if NO_NAMES:    # diagnostics only: the step without the host's SHA3 load beside it
             return
-        self.fut[k] = self.namer.submit(crdtenc.content_name, self.last_file)
+        self.fut[k] = (self.namer.submit(self.last_file) if isinstance(self.namer, BatchNamer)
+                       else self.namer.submit(crdtenc.content_name, self.last_file))
         self.order.append(self.fut[k])
 
     def compact(self):
@@ -522,11 +580,12 @@ def run_c3(args, ctx, dev):
         "pipelined": {"ms_per_step": round(ms_loop, 3), "name_drain_ms": round(drain_ms, 3),
                       "download_overlap": pipe.use_async,
                       "download_engine": "sdma" if core.path_count("compact_download_sdma") else "runtime copy",
-                      "name_threads": NB - 1,
+                      "name_threads": name_threads(),
+                      "name_batch": int(os.environ.get("CE_NAME_BATCH", "4")),
                       "what": "steps back to back, each sealed file's download overlapping the next "
                               "step on the device (ce_core_compact_into_async) and its content name "
                               "hashed on %d host threads; timed up to the last download; ms_per_step "
-                              "above adds the names still being hashed then (drain / steps)" % (NB - 1)},
+                              "above adds the names still being hashed then (drain / steps)" % name_threads()},
         "aead_open_GBps": round(ct / (open_ms / 1e3) / 1e9, 1) if open_ms else None,
         "fold": {"kernels": "ds_applied + ds_add_pairs + ds_kill", "ms": round(fold_ms, 4),
                  "algorithmic_bytes": fold_bytes,
@@ -1228,7 +1287,7 @@ def run_config(name, args, ctx, dev, world=1, rank=0):
 def main():
     args = make_parser().parse_args()
     if args.steps is None:
-        args.steps = 40 if args.config == "c3" else 20
+        args.steps = 120 if args.config == "c3" else 20
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     stream = torch.cuda.Stream(device=dev)
