@@ -674,8 +674,10 @@ def main():
         import bench_configs
         configs = {}
         for c in [x for x in args.configs.split(",") if x]:
-            # C3: 40 steps, so the ~48 ms SHA3 of the last step's 35 MB file weighs ~1 ms a step
-            steps_c = {"c3": 40, "c4": 10, "c5": 10}[c]
+            # C3: 120 steps (~0.4 s) -- every step's 35 MB file is named by a ~48 ms SHA3 on a host
+            # thread, so the timed region (which ends when the last name is done) approaches the
+            # steady state only over many steps: the last name's latency weighs ~0.4 ms a step here
+            steps_c = {"c3": 120, "c4": 10, "c5": 10}[c]
             extra = {"c3": ["--versions", "2", "--state-versions", "1"], "c4": ["--c4-versions", "2"],
                      "c5": ["--c5-versions", "4"]}[c] if args.quick else []
             ns = bench_configs.make_parser().parse_args(

@@ -1,9 +1,9 @@
 #!/bin/bash
-# C2 one-step timeline under gpurun_out/r03: a kernel + copy trace of a short variant-A bench run
+# C2 one-step timeline under gpurun_out/c2t: a kernel + copy trace of a short variant-A bench run
 # and tools/c2_step_breakdown.py over one timed step (GPU busy, idle gaps, step - fused).
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r03
+O=$R/gpurun_out/c2t
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $O/c2t -o s -- \
