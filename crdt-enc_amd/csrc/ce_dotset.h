@@ -28,6 +28,8 @@ static constexpr unsigned long long kDsEmpty = ~0ull;
 static constexpr uint32_t kDsNoActor = 0xffffffffu;
 static constexpr int32_t kStatusHostDecode = 101;  // op vector the device leaves to the host
 static constexpr int kDsActorBits = 24;            // actor ids < 2^24 in a pair key
+static constexpr int kDsPartBits = 11;             // pair-table partition: 2048 slots (k_ds_part_apply)
+static constexpr uint32_t kDsPartSlots = 1u << kDsPartBits;
 
 enum DsKind { kDsOrswot = 0, kDsMVReg = 1 };
 
@@ -117,6 +119,47 @@ hipError_t launch_ds_kill(hipStream_t s, DsTables t, const uint32_t* cbeg, const
                           const unsigned long long* mem, uint32_t n_rm);
 // v = max(cur, add); v <= kill -> 0; cur = v; add = kill = 0; live/used counts
 hipError_t launch_ds_finalize(hipStream_t s, DsTables t);
+
+// The partitioned fold (adds + removals + finalize of one Orswot batch; the global kernels above
+// remain for batches outside its limits).  Every (pair key, value) item is bucketed by its
+// pair-table partition, then one workgroup per partition loads the partition's keys into LDS,
+// inserts the adds / max-merges their counters and the removal thresholds there, and writes back
+// only the slots that changed:
+//   launch_ds_part_count   K1: adds (member insert, pair key per add member, per-block partition
+//                          histogram), then removals (member lookup, histogram) -- two launches,
+//                          so a removal's lookup sees every member the batch's adds inserted
+//   ds_excl_sum_u32        hist -> off (the bases of every (partition, block) run)
+//   launch_ds_part_apply   K3 scatter of the items by partition, K4 one workgroup per partition
+// live[0] += change of the live-pair count (two's complement), live[1] += pairs inserted; K1
+// zeroes live[0], live[1] and live[3].
+static constexpr uint32_t kDsPartChunk = 8192;      // adds / removals per K1 / K3 block
+static constexpr uint32_t kDsPartMaxParts = 16384;  // LDS histogram bound (64 KB)
+struct DsKillSrc {
+  const uint32_t* cbeg;
+  const uint32_t* mbeg;
+  const uint32_t* c_actor;
+  const unsigned long long* c_ctr;
+  const unsigned long long* mem;
+  unsigned long long* hk;       // K1 -> K3: member handle per removal member (kDsEmpty: absent)
+  uint32_t n;
+};
+struct DsPartArgs {
+  DsTables t;
+  DsOps o;
+  const uint8_t* applied;
+  uint32_t n_add;
+  unsigned long long* akey;     // K1 -> K3: pair key per add member (kDsEmpty: not inserted)
+  DsKillSrc ks[2];              // the batch's removals, the deferred set
+  uint32_t ba, bk0, bk;         // add blocks, blocks of ks[0], all removal blocks
+  uint32_t parts;               // (pmask + 1) >> kDsPartBits
+  uint32_t chunk;               // adds / removals per K1 / K3 block (kDsPartChunk)
+  uint32_t* hist;               // parts * (ba + bk) + 1 counts: [p * ba + b], then [parts * ba + p * bk + b]
+  const uint32_t* off;          // exclusive scan of hist
+  unsigned long long* items;    // (key, value) pairs, partition-major: adds, then removals
+};
+__host__ __device__ inline uint64_t ds_part_hist_len(const DsPartArgs& a) { return (uint64_t)a.parts * (a.ba + a.bk) + 1; }
+hipError_t launch_ds_part_count(hipStream_t s, const DsPartArgs& a);
+hipError_t launch_ds_part_apply(hipStream_t s, const DsPartArgs& a);
 // deferred[r] = !(R <= clock)
 // deferred[r] = removal r's clock is not covered by `clock`; any (may be null): set to 1 when
 // some removal is deferred

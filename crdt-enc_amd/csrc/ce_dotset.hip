@@ -54,9 +54,18 @@ __device__ unsigned long long member_find(const DsTables& t, unsigned long long 
   return kDsEmpty;
 }
 
+// The pair table is cut into partitions of kDsPartSlots consecutive slots: a key's probe sequence
+// starts at mix64(key) & pmask and wraps inside that slot's partition, so one partition holds every
+// pair whose hash lands in it (k_ds_part_apply folds a partition in LDS).  The tables are always
+// at least one partition (tables_alloc: >= 4096 slots).
+__device__ __forceinline__ uint32_t pair_part(const DsTables& t, unsigned long long key) {
+  return ((uint32_t)mix64(key) & t.pmask) >> kDsPartBits;
+}
+
 __device__ unsigned long long pair_find(const DsTables& t, unsigned long long key, bool insert) {
   uint32_t h = (uint32_t)mix64(key) & t.pmask;
-  for (uint32_t probe = 0; probe <= t.pmask; probe++) {
+  const uint32_t lo = h & ~(kDsPartSlots - 1);
+  for (uint32_t probe = 0; probe < kDsPartSlots; probe++) {
     const unsigned long long k = ld_volatile(t.pkey + h);
     if (k == key) return h;
     if (k == kDsEmpty) {
@@ -64,7 +73,7 @@ __device__ unsigned long long pair_find(const DsTables& t, unsigned long long ke
       const unsigned long long prev = atomicCAS(t.pkey + h, kDsEmpty, key);
       if (prev == kDsEmpty || prev == key) return h;
     }
-    h = (h + 1) & t.pmask;
+    h = lo | ((h + 1) & (kDsPartSlots - 1));
   }
   atomicAdd(t.live + 2, 1u);
   return kDsEmpty;
@@ -536,6 +545,269 @@ __global__ void __launch_bounds__(kBlock) k_ds_finalize(DsTables t) {
     }
     if (l) atomicAdd(t.live + 0, l);
     if (u) atomicAdd(t.live + 1, u);
+  }
+}
+
+// ---- partitioned fold (ce_dotset.h: DsPartArgs) ----------------------------------------
+// The global kernels above cost ~3 random line touches per add (member probe, pair probe, the
+// add slot's atomic) plus two full passes over the 4M-slot table (finalize); here the items are
+// bucketed by partition first (two streaming passes), then each partition's 2048 keys and the
+// counters / thresholds of its items meet in LDS, and only changed slots go back to HBM.
+constexpr int kPartThreads = 1024;     // K1 / K3
+constexpr int kApplyThreads = 512;     // K4
+
+// member handle of m when its first probe holds it (g = mkey[that bucket], read ahead of time
+// for several items at once), else member_find
+__device__ __forceinline__ unsigned long long member_handle(const DsTables& t, unsigned long long m,
+                                                            unsigned long long g, bool insert) {
+  if (g == m && m != kDsEmpty) return (uint32_t)mix64(m) & t.mmask;
+  return member_find(t, m, insert);
+}
+
+constexpr int kPartBatch = 8;  // items per lane whose loads are issued before any is used
+
+__global__ void __launch_bounds__(kPartThreads) k_ds_part_adds(DsPartArgs a) {
+  extern __shared__ uint32_t lh[];  // [parts]
+  for (uint32_t p = threadIdx.x; p < a.parts; p += kPartThreads) lh[p] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    a.t.live[0] = 0;
+    a.t.live[1] = 0;
+    a.t.live[3] = 0;
+    a.hist[ds_part_hist_len(a) - 1] = 0;
+  }
+  __syncthreads();
+  const uint32_t k0 = blockIdx.x * a.chunk;
+  const uint32_t k1 = min(a.n_add, k0 + a.chunk);
+  for (uint32_t kb = k0 + threadIdx.x; kb < k1; kb += kPartThreads * kPartBatch) {
+    uint32_t j0[kPartBatch], j1[kPartBatch], aid[kPartBatch];
+    unsigned long long m[kPartBatch], g[kPartBatch];
+#pragma unroll
+    for (int q = 0; q < kPartBatch; q++) {
+      const uint32_t k = kb + q * kPartThreads;
+      j0[q] = j1[q] = 0;
+      m[q] = g[q] = 0;
+      if (k < k1) {
+        j0[q] = a.o.add_mbeg[k];
+        j1[q] = a.o.add_mbeg[k + 1];
+        aid[q] = a.o.add_actor[k];
+        if (!a.applied[k]) {
+          for (uint32_t j = j0[q]; j < j1[q]; j++) a.akey[j] = kDsEmpty;
+          j1[q] = j0[q];
+        } else if (j1[q] == j0[q] + 1) {
+          m[q] = a.o.add_mem[j0[q]];
+          g[q] = a.t.mkey[(uint32_t)mix64(m[q]) & a.t.mmask];
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kPartBatch; q++) {
+      for (uint32_t j = j0[q]; j < j1[q]; j++) {
+        const unsigned long long mm = j1[q] == j0[q] + 1 ? m[q] : a.o.add_mem[j];
+        const unsigned long long h = member_handle(a.t, mm, j1[q] == j0[q] + 1 ? g[q] : ~mm, true);
+        const unsigned long long key = h == kDsEmpty ? kDsEmpty : pair_key(h, aid[q]);
+        a.akey[j] = key;
+        if (key != kDsEmpty) atomicAdd(&lh[pair_part(a.t, key)], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  if (blockIdx.x < a.ba)  // (one block with no adds still runs for the clears above)
+    for (uint32_t p = threadIdx.x; p < a.parts; p += kPartThreads) a.hist[(size_t)p * a.ba + blockIdx.x] = lh[p];
+}
+
+// removal r kills (m, a_e) for every member m and clock entry e (k_ds_kill); a member absent after
+// the adds has no pair to kill
+__global__ void __launch_bounds__(kPartThreads) k_ds_part_kills(DsPartArgs a) {
+  extern __shared__ uint32_t lh[];
+  for (uint32_t p = threadIdx.x; p < a.parts; p += kPartThreads) lh[p] = 0;
+  __syncthreads();
+  const uint32_t b = blockIdx.x;
+  const DsKillSrc& x = a.ks[b < a.bk0 ? 0 : 1];
+  const uint32_t r0 = (b < a.bk0 ? b : b - a.bk0) * a.chunk;
+  const uint32_t r1 = min(x.n, r0 + a.chunk);
+  for (uint32_t rb = r0 + threadIdx.x; rb < r1; rb += kPartThreads * kPartBatch) {
+    uint32_t c0[kPartBatch], c1[kPartBatch], j0[kPartBatch], j1[kPartBatch];
+    unsigned long long m[kPartBatch], g[kPartBatch];
+#pragma unroll
+    for (int q = 0; q < kPartBatch; q++) {
+      const uint32_t r = rb + q * kPartThreads;
+      c0[q] = c1[q] = j0[q] = j1[q] = 0;
+      m[q] = g[q] = 0;
+      if (r < r1) {
+        c0[q] = x.cbeg[r];
+        c1[q] = x.cbeg[r + 1];
+        j0[q] = x.mbeg[r];
+        j1[q] = x.mbeg[r + 1];
+        if (c0[q] == c1[q]) {  // an empty clock kills nothing
+          for (uint32_t j = j0[q]; j < j1[q]; j++) x.hk[j] = kDsEmpty;
+          j1[q] = j0[q];
+        } else if (j1[q] == j0[q] + 1) {
+          m[q] = x.mem[j0[q]];
+          g[q] = a.t.mkey[(uint32_t)mix64(m[q]) & a.t.mmask];
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kPartBatch; q++) {
+      for (uint32_t j = j0[q]; j < j1[q]; j++) {
+        const bool one = j1[q] == j0[q] + 1;
+        const unsigned long long mm = one ? m[q] : x.mem[j];
+        const unsigned long long h = member_handle(a.t, mm, one ? g[q] : ~mm, false);
+        x.hk[j] = h;
+        if (h == kDsEmpty) continue;
+        for (uint32_t e = c0[q]; e < c1[q]; e++) atomicAdd(&lh[pair_part(a.t, pair_key(h, x.c_actor[e]))], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  const size_t col = (size_t)a.parts * a.ba;
+  for (uint32_t p = threadIdx.x; p < a.parts; p += kPartThreads) a.hist[col + (size_t)p * a.bk + b] = lh[p];
+}
+
+// K3: the same items as K1, block by block, each to its (partition, block) run
+__global__ void __launch_bounds__(kPartThreads) k_ds_part_scatter(DsPartArgs a) {
+  extern __shared__ uint32_t lc[];  // [parts] cursors
+  const uint32_t b = blockIdx.x;
+  const bool adds = b < a.ba;
+  const uint32_t kb = adds ? 0 : b - a.ba;
+  for (uint32_t p = threadIdx.x; p < a.parts; p += kPartThreads)
+    lc[p] = adds ? a.off[(size_t)p * a.ba + b] : a.off[(size_t)a.parts * a.ba + (size_t)p * a.bk + kb];
+  __syncthreads();
+  if (adds) {
+    const uint32_t k0 = b * a.chunk;
+    const uint32_t k1 = min(a.n_add, k0 + a.chunk);
+    for (uint32_t kq = k0 + threadIdx.x; kq < k1; kq += kPartThreads * kPartBatch) {
+      uint32_t j0[kPartBatch], j1[kPartBatch];
+      unsigned long long c[kPartBatch], key1[kPartBatch];
+#pragma unroll
+      for (int q = 0; q < kPartBatch; q++) {
+        const uint32_t k = kq + q * kPartThreads;
+        j0[q] = j1[q] = 0;
+        c[q] = key1[q] = 0;
+        if (k < k1) {
+          j0[q] = a.o.add_mbeg[k];
+          j1[q] = a.o.add_mbeg[k + 1];
+          c[q] = a.o.add_ctr[k];
+          if (j1[q] == j0[q] + 1) key1[q] = a.akey[j0[q]];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < kPartBatch; q++) {
+        for (uint32_t j = j0[q]; j < j1[q]; j++) {
+          const unsigned long long key = j1[q] == j0[q] + 1 ? key1[q] : a.akey[j];
+          if (key == kDsEmpty) continue;
+          const uint32_t pos = atomicAdd(&lc[pair_part(a.t, key)], 1u);
+          *reinterpret_cast<ulonglong2*>(a.items + 2ull * pos) = make_ulonglong2(key, c[q]);
+        }
+      }
+    }
+    return;
+  }
+  const DsKillSrc& x = a.ks[kb < a.bk0 ? 0 : 1];
+  const uint32_t r0 = (kb < a.bk0 ? kb : kb - a.bk0) * a.chunk;
+  const uint32_t r1 = min(x.n, r0 + a.chunk);
+  for (uint32_t r = r0 + threadIdx.x; r < r1; r += kPartThreads) {
+    const uint32_t c0 = x.cbeg[r], c1 = x.cbeg[r + 1];
+    if (c0 == c1) continue;
+    for (uint32_t j = x.mbeg[r]; j < x.mbeg[r + 1]; j++) {
+      const unsigned long long h = x.hk[j];
+      if (h == kDsEmpty) continue;
+      for (uint32_t e = c0; e < c1; e++) {
+        const unsigned long long key = pair_key(h, x.c_actor[e]);
+        const uint32_t pos = atomicAdd(&lc[pair_part(a.t, key)], 1u);
+        *reinterpret_cast<ulonglong2*>(a.items + 2ull * pos) = make_ulonglong2(key, x.c_ctr[e]);
+      }
+    }
+  }
+}
+
+// K4: partition p = blockIdx.x.  Keys in LDS follow pair_find's probe order (start at
+// mix64(key) mod the partition, wrap inside it), so a key inserted here sits where the global
+// kernels look for it.  Then finalize (k_ds_finalize) of the touched slots only: an untouched
+// slot's value is unchanged by it.
+__global__ void __launch_bounds__(kApplyThreads) k_ds_part_apply(DsPartArgs a) {
+  __shared__ unsigned long long key[kDsPartSlots], add[kDsPartSlots], kill[kDsPartSlots];
+  __shared__ uint8_t fresh[kDsPartSlots];
+  __shared__ int part[2][kApplyThreads / 64];
+  const uint32_t p = blockIdx.x;
+  const size_t base = (size_t)p << kDsPartBits;
+  for (uint32_t i = threadIdx.x; i < kDsPartSlots; i += kApplyThreads) {
+    key[i] = a.t.pkey[base + i];
+    add[i] = 0;
+    kill[i] = 0;
+    fresh[i] = 0;
+  }
+  __syncthreads();
+  constexpr uint32_t M = kDsPartSlots - 1;
+  const uint32_t ia0 = a.off[(size_t)p * a.ba], ia1 = a.off[(size_t)(p + 1) * a.ba];
+  for (uint32_t i = ia0 + threadIdx.x; i < ia1; i += kApplyThreads) {
+    const ulonglong2 it = *reinterpret_cast<const ulonglong2*>(a.items + 2ull * i);
+    uint32_t h = (uint32_t)mix64(it.x) & M;
+    bool done = false;
+    for (uint32_t probe = 0; probe < kDsPartSlots && !done; probe++) {
+      const unsigned long long k = key[h];
+      if (k == kDsEmpty) {
+        const unsigned long long prev = atomicCAS(&key[h], kDsEmpty, it.x);
+        if (prev == kDsEmpty) fresh[h] = 1;
+        done = prev == kDsEmpty || prev == it.x;
+      } else {
+        done = k == it.x;
+      }
+      if (!done) h = (h + 1) & M;
+    }
+    if (done) atomicMax(&add[h], it.y);
+    else atomicAdd(a.t.live + 2, 1u);  // partition full (tables sized to <= 50% load)
+  }
+  __syncthreads();
+  const size_t kcol = (size_t)a.parts * a.ba;
+  const uint32_t ik0 = a.off[kcol + (size_t)p * a.bk], ik1 = a.off[kcol + (size_t)(p + 1) * a.bk];
+  for (uint32_t i = ik0 + threadIdx.x; i < ik1; i += kApplyThreads) {
+    const ulonglong2 it = *reinterpret_cast<const ulonglong2*>(a.items + 2ull * i);
+    uint32_t h = (uint32_t)mix64(it.x) & M;
+    for (uint32_t probe = 0; probe < kDsPartSlots; probe++) {
+      const unsigned long long k = key[h];
+      if (k == it.x) {
+        atomicMax(&kill[h], it.y);
+        break;
+      }
+      if (k == kDsEmpty) break;
+      h = (h + 1) & M;
+    }
+  }
+  __syncthreads();
+  int dl = 0, du = 0;
+  for (uint32_t i = threadIdx.x; i < kDsPartSlots; i += kApplyThreads) {
+    const unsigned long long ad = add[i], kl = kill[i];
+    const bool f = fresh[i];
+    if (f) {
+      a.t.pkey[base + i] = key[i];
+      du++;
+    }
+    if (!ad && !kl) continue;
+    const unsigned long long c = f ? 0ull : a.t.cur[base + i];
+    unsigned long long v = c > ad ? c : ad;
+    if (v != 0 && v <= kl) v = 0;
+    if (v != c) a.t.cur[base + i] = v;
+    dl += (int)(v != 0) - (int)(c != 0);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    dl += __shfl_xor(dl, o);
+    du += __shfl_xor(du, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    part[0][threadIdx.x >> 6] = dl;
+    part[1][threadIdx.x >> 6] = du;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int l = 0, u = 0;
+    for (int w = 0; w < kApplyThreads / 64; w++) {
+      l += part[0][w];
+      u += part[1][w];
+    }
+    if (l) atomicAdd(a.t.live + 0, (uint32_t)l);
+    if (u) atomicAdd(a.t.live + 1, (uint32_t)u);
   }
 }
 
@@ -1076,6 +1348,19 @@ hipError_t launch_ds_kill(hipStream_t s, DsTables t, const uint32_t* cbeg, const
 
 hipError_t launch_ds_finalize(hipStream_t s, DsTables t) {
   hipLaunchKernelGGL(k_ds_finalize, dim3(blocks_for((uint64_t)t.pmask + 1, 1024)), dim3(kBlock), 0, s, t);
+  return hipGetLastError();
+}
+
+hipError_t launch_ds_part_count(hipStream_t s, const DsPartArgs& a) {
+  const size_t lds = (size_t)a.parts * 4;
+  hipLaunchKernelGGL(k_ds_part_adds, dim3(a.ba ? a.ba : 1), dim3(kPartThreads), lds, s, a);
+  if (a.bk) hipLaunchKernelGGL(k_ds_part_kills, dim3(a.bk), dim3(kPartThreads), lds, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_ds_part_apply(hipStream_t s, const DsPartArgs& a) {
+  if (a.ba + a.bk) hipLaunchKernelGGL(k_ds_part_scatter, dim3(a.ba + a.bk), dim3(kPartThreads), (size_t)a.parts * 4, s, a);
+  hipLaunchKernelGGL(k_ds_part_apply, dim3(a.parts), dim3(kApplyThreads), 0, s, a);
   return hipGetLastError();
 }
 

@@ -37,6 +37,7 @@ struct DsState {
   // a fold / k-way merge whose closing counts (live[0..3] -> pinned h_cnt[56..60)) and deferred
   // flags have not been read yet: ds_settle reads them at the next host wait
   bool settle_pending = false, settle_fold = false;
+  bool settle_delta = false;  // live[0..1] are changes (the partitioned fold), not totals
   uint32_t settle_nr = 0;
   uint64_t settle_rmc = 0, settle_rmm = 0;
   std::vector<std::pair<IdDots, std::vector<uint64_t>>> settle_d0;
@@ -50,6 +51,7 @@ struct DsState {
   DevBuf cnt, ops[10], applied, sort_keys, sort_perm, sort_keys2, sort_perm2, ctr_sorted, excl,
       cub_tmp, deferred_flags, d0[5], col[6], mv[6], other[4], oclock;
   DevBuf misses;
+  DevBuf part_akey, part_hk[2], part_hist, part_items;  // the partitioned fold (DsPartArgs)
   HostBuf h_cnt;
   // run-contiguity marks of the adds' actors (k_ds_contig: a generation per check, no clearing)
   DevBuf contig_marks;
@@ -487,7 +489,9 @@ int finalize(ce_core* c) {
 
 // Orswot fold of a columnar batch in application order (k = counts); the removals of the
 // batch plus the current deferred set (re-applied by apply_deferred) set the thresholds.
-int orswot_fold(ce_core* c, const Counts& k) {
+// kill_bound: an upper bound on the batch's removal items (sum over removals of members x clock
+// entries; ~0 = unknown: the global kernels)
+int orswot_fold(ce_core* c, const Counts& k, uint64_t kill_bound) {
   DsState* d = c->ds;
   ce_ctx* ctx = c->ctx;
   hipStream_t s = ctx->stream;
@@ -549,36 +553,86 @@ int orswot_fold(ce_core* c, const Counts& k) {
       return ctx->hip_fail(e, "applied");
     ctx->tend(ta);
   }
-  // 2) entries: max-insert the applied adds (capacity for every add member)
+  // 2) entries: max-insert the applied adds (capacity for every add member), 3) removal
+  //    thresholds: the batch's removals and the deferred set (uploaded only when there is one:
+  //    the upload waits for its pageable sources), then finalize -- partitioned (DsPartArgs) when
+  //    the batch fits its limits, else the global kernels
   if ((rc = ensure_pairs(c, k.v[kCntAddM]))) return rc;
-  const int tp = ctx->tbegin("ds_add_pairs");
-  if ((e = launch_ds_add_pairs(s, tables(d), o, d->applied.as<uint8_t>(), na)) ||
-      (e = launch_ds_clock(s, clock_keys, clock_ctr, d->excl.as<unsigned long long>(),
-                           d->clock.as<unsigned long long>(), na)))
-    return ctx->hip_fail(e, "add");
-  ctx->tend(tp);
-  // 3) removal thresholds: the batch's removals and the deferred set (uploaded only when there
-  //    is one: the upload waits for its pageable sources)
   auto d0 = deferred_list(d);
   const uint32_t n0 = (uint32_t)d0.size();
   if (n0 && (rc = upload_removals(c, d0))) return rc;
-  const int tk = ctx->tbegin("ds_kill");
-  if ((e = launch_ds_kill(s, tables(d), o.rm_cbeg, o.rm_mbeg, o.rmc_actor, o.rmc_ctr, o.rm_mem, nr)) ||
-      (n0 && (e = launch_ds_kill(s, tables(d), d->d0[0].as<uint32_t>(), d->d0[1].as<uint32_t>(),
-                                 d->d0[2].as<uint32_t>(), d->d0[3].as<unsigned long long>(),
-                                 d->d0[4].as<unsigned long long>(), n0))))
-    return ctx->hip_fail(e, "kill");
-  ctx->tend(tk);
-  // finalize and the deferred flags without a host wait: live / used pairs, the overflow flag and
-  // whether any removal stays deferred land in pinned memory; ds_settle reads them at the
-  // caller's next host wait (the removal columns stay intact until then)
+  uint64_t m0 = 0, kb0 = 0;  // the deferred set's members and items
+  for (auto& x : d0) {
+    m0 += x.second.size();
+    kb0 += (uint64_t)x.second.size() * x.first.size();
+  }
   uint32_t* live = d->live.as<uint32_t>();
-  if ((e = d->deferred_flags.reserve(nr + n0 + 64)) || (e = launch_ds_set3(s, live, 0u, live + 1, 0u, live + 3, 0u)))
-    return ctx->hip_fail(e, "finalize");
-  {
+  DsPartArgs pa{};
+  pa.parts = d->pcap >> kDsPartBits;
+  static const uint32_t chunk = getenv("CE_DS_PART_CHUNK") ? (uint32_t)std::max(1024, atoi(getenv("CE_DS_PART_CHUNK")))
+                                                          : kDsPartChunk;
+  pa.chunk = chunk;
+  pa.ba = (uint32_t)((na + chunk - 1) / chunk);
+  pa.bk0 = (uint32_t)((nr + chunk - 1) / chunk);
+  pa.bk = pa.bk0 + (uint32_t)((n0 + chunk - 1) / chunk);
+  const uint64_t kill_items = kill_bound == ~0ull ? ~0ull : kill_bound + kb0;
+  const bool part = !getenv("CE_DS_FOLD_GLOBAL") && pa.parts >= 1 && pa.parts <= kDsPartMaxParts &&
+                    kill_items <= 4 * (k.v[kCntRmM] + k.v[kCntRmC] + kb0) + (1ull << 20) &&
+                    ds_part_hist_len(pa) < (1ull << 31) && k.v[kCntAddM] + kill_items < (1ull << 31);
+  if (part) {
+    const uint64_t hl = ds_part_hist_len(pa);
+    size_t tb = 0;
+    if ((e = d->part_akey.reserve(8 * k.v[kCntAddM] + 64)) || (e = d->part_hk[0].reserve(8 * k.v[kCntRmM] + 64)) ||
+        (e = d->part_hk[1].reserve(8 * m0 + 64)) || (e = d->part_hist.reserve(8 * hl + 64)) ||
+        (e = d->part_items.reserve(16 * (k.v[kCntAddM] + kill_items) + 64)) ||
+        (e = ds_excl_sum_u32(nullptr, tb, nullptr, nullptr, (uint32_t)hl, s)) || (e = d->cub_tmp.reserve(tb + 256)))
+      return ctx->hip_fail(e, "fold");
+    pa.t = tables(d);
+    pa.o = o;
+    pa.applied = d->applied.as<uint8_t>();
+    pa.n_add = na;
+    pa.akey = d->part_akey.as<unsigned long long>();
+    pa.ks[0] = {o.rm_cbeg, o.rm_mbeg, o.rmc_actor, o.rmc_ctr, o.rm_mem, d->part_hk[0].as<unsigned long long>(), nr};
+    pa.ks[1] = {d->d0[0].as<uint32_t>(), d->d0[1].as<uint32_t>(), d->d0[2].as<uint32_t>(),
+                d->d0[3].as<unsigned long long>(), d->d0[4].as<unsigned long long>(),
+                d->part_hk[1].as<unsigned long long>(), n0};
+    pa.hist = d->part_hist.as<uint32_t>();
+    pa.off = pa.hist + hl;
+    pa.items = d->part_items.as<unsigned long long>();
+    tb = d->cub_tmp.cap;
+    const int tp = ctx->tbegin("ds_part_fold");
+    if ((e = launch_ds_part_count(s, pa)) ||
+        (e = ds_excl_sum_u32(d->cub_tmp.p, tb, pa.hist, pa.hist + hl, (uint32_t)hl, s)) ||
+        (e = launch_ds_part_apply(s, pa)) ||
+        (e = launch_ds_clock(s, clock_keys, clock_ctr, d->excl.as<unsigned long long>(),
+                             d->clock.as<unsigned long long>(), na)))
+      return ctx->hip_fail(e, "fold");
+    ctx->tend(tp);
+    c->path_counts["ds_fold_partitioned"]++;
+    if ((e = d->deferred_flags.reserve(nr + n0 + 64))) return ctx->hip_fail(e, "finalize");
+  } else {
+    const int tp = ctx->tbegin("ds_add_pairs");
+    if ((e = launch_ds_add_pairs(s, tables(d), o, d->applied.as<uint8_t>(), na)) ||
+        (e = launch_ds_clock(s, clock_keys, clock_ctr, d->excl.as<unsigned long long>(),
+                             d->clock.as<unsigned long long>(), na)))
+      return ctx->hip_fail(e, "add");
+    ctx->tend(tp);
+    const int tk = ctx->tbegin("ds_kill");
+    if ((e = launch_ds_kill(s, tables(d), o.rm_cbeg, o.rm_mbeg, o.rmc_actor, o.rmc_ctr, o.rm_mem, nr)) ||
+        (n0 && (e = launch_ds_kill(s, tables(d), d->d0[0].as<uint32_t>(), d->d0[1].as<uint32_t>(),
+                                   d->d0[2].as<uint32_t>(), d->d0[3].as<unsigned long long>(),
+                                   d->d0[4].as<unsigned long long>(), n0))))
+      return ctx->hip_fail(e, "kill");
+    ctx->tend(tk);
+    // finalize and the deferred flags without a host wait: live / used pairs, the overflow flag and
+    // whether any removal stays deferred land in pinned memory; ds_settle reads them at the
+    // caller's next host wait (the removal columns stay intact until then)
+    if ((e = d->deferred_flags.reserve(nr + n0 + 64)) || (e = launch_ds_set3(s, live, 0u, live + 1, 0u, live + 3, 0u)))
+      return ctx->hip_fail(e, "finalize");
     const int t = ctx->tbegin("ds_finalize");
     if ((e = launch_ds_finalize(s, tables(d)))) return ctx->hip_fail(e, "finalize");
     ctx->tend(t);
+    c->path_counts["ds_fold_global"]++;
   }
   uint8_t* fl = d->deferred_flags.as<uint8_t>();
   if ((e = launch_ds_deferred(s, o.rm_cbeg, o.rmc_actor, o.rmc_ctr, d->clock.as<unsigned long long>(), fl, nr, live + 3)) ||
@@ -589,6 +643,7 @@ int orswot_fold(ce_core* c, const Counts& k) {
     return ctx->hip_fail(e, "finalize");
   d->settle_pending = true;
   d->settle_fold = true;
+  d->settle_delta = part;
   d->settle_nr = nr;
   d->settle_rmc = k.v[kCntRmC];
   d->settle_rmm = k.v[kCntRmM];
@@ -610,8 +665,13 @@ int ds_settle(ce_core* c) {
   d->settle_pending = false;
   const uint32_t* hl = d->h_cnt.as<uint32_t>() + 56;
   if (hl[2]) return ctx->fail(CE_ERR_DEVICE, "dot-set table overflow");
-  d->live_pairs = hl[0];
-  d->used_pairs = hl[1];
+  if (d->settle_delta) {
+    d->live_pairs += (int64_t)(int32_t)hl[0];
+    d->used_pairs += hl[1];
+  } else {
+    d->live_pairs = hl[0];
+    d->used_pairs = hl[1];
+  }
   if (!d->settle_fold) return CE_OK;
   // 4) deferred = removals whose clock is not covered by the new clock (none: the usual case)
   std::map<IdDots, std::set<uint64_t>> nd;
@@ -1129,7 +1189,9 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
   HostPhase hpf("ops: fold");
   // 6) fold (lib.rs:534-535 `state.apply(op)` for every op of every applied file, in order)
   if (c->kind == CE_STATE_ORSWOT) {
-    rc = orswot_fold(c, tot);
+    // removal items <= members x the largest per-file clock-entry count (a removal's clock is
+    // part of one file)
+    rc = orswot_fold(c, tot, tot.v[kCntRmM] * std::max<uint64_t>(1, kmax.v[kCntRmC]));
   } else {
     rc = mvreg_commit(c, (uint32_t)base.v[kCntRm], (uint32_t)tot.v[kCntRm], true);
   }
@@ -1810,6 +1872,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     c->path_counts["states_kway_merge"]++;
     d->settle_pending = true;
     d->settle_fold = false;
+    d->settle_delta = false;
     for (size_t i = 0; i < n; i++)
       for (auto& y : ds[i].hs.nov) {
         uint32_t sl;
@@ -1938,7 +2001,16 @@ int ds_apply_local_ops(ce_core* c, const uint8_t* ops, size_t len) {
   if ((rc = table_upload(c)) || (rc = ensure_clock(c)) || (rc = reserve_ops(c, tot)) ||
       (rc = upload_cols(c, hc, Counts{})) || (rc = write_sentinels(c, tot)))
     return rc;
-  if (c->kind == CE_STATE_ORSWOT) return orswot_fold(c, tot);
+  if (c->kind == CE_STATE_ORSWOT) {
+    uint64_t items = 0;  // removal items, exactly
+    const size_t nr = hc.rm_cbeg.size();
+    for (size_t r = 0; r < nr; r++) {
+      const uint64_t ce = r + 1 < nr ? hc.rm_cbeg[r + 1] : hc.rmc_actor.size();
+      const uint64_t me = r + 1 < nr ? hc.rm_mbeg[r + 1] : hc.rm_mem.size();
+      items += (ce - hc.rm_cbeg[r]) * (me - hc.rm_mbeg[r]);
+    }
+    return orswot_fold(c, tot, items);
+  }
   return mvreg_commit(c, (uint32_t)base.v[kCntRm], (uint32_t)tot.v[kCntRm], true);
 }
 

@@ -822,3 +822,43 @@ def test_orswot_tiled_emit_equals_direct(ctx, adversarial):
             os.environ.pop("CE_DS_EMIT_DIRECT", None)
     assert got[False][0] == got[True][0] == oc.serialize()
     assert got[False][1] == 1 and got[True][1] == 0
+
+
+@pytest.mark.parametrize("adversarial", [False, True])
+def test_orswot_partitioned_fold_equals_global(ctx, adversarial):
+    """The partitioned fold (items bucketed by pair-table partition, each partition folded in LDS:
+    k_ds_part_*) == the global kernels (k_ds_add_pairs / k_ds_kill / k_ds_finalize, forced with
+    CE_DS_FOLD_GLOBAL=1) == the oracle, over four batches that grow the tables past one partition
+    and carry deferred removals from batch to batch (adversarial: removals naming other writers'
+    dots, multi-entry clocks and several members per removal)."""
+    rng = random.Random(717 + adversarial)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 24)
+    files = gen("orswot", rng, actors, 8, 14, 2500, adversarial)
+    batches = []
+    for lo in range(0, 8, 2):
+        part = {a: files[a][: lo + 2] for a in files}
+        acts, clears, fa, fv = G.batch(part, "orswot", APP, start={a: lo for a in files})
+        batches.append((acts, seal_files(ctx, key, clears), fa, fv))
+    oc = C.Core("orswot")
+    want = []
+    for acts, sealed, fa, fv in batches:
+        rc = oc.read_remote_ops(key, [APP], sealed, [acts[i] for i in fa], fv)[0]
+        want.append((rc, oc.serialize()))
+    got = {}
+    for forced in (False, True):
+        if forced:
+            os.environ["CE_DS_FOLD_GLOBAL"] = "1"
+        try:
+            core = new_core(ctx, "orswot", key)
+            out = []
+            for acts, sealed, fa, fv in batches:
+                out.append((core.ingest_ops(sealed, acts, fa, fv)[0], core.state_bytes()))
+            got[forced] = (out, core.path_count("ds_fold_partitioned"), core.path_count("ds_fold_global"))
+            core.close()
+        finally:
+            os.environ.pop("CE_DS_FOLD_GLOBAL", None)
+    assert got[False][0] == want
+    assert got[True][0] == want
+    assert got[False][1] == len(batches) and got[False][2] == 0
+    assert got[True][1] == 0 and got[True][2] == len(batches)
