@@ -6,9 +6,11 @@
 // HBM layout (all arrays device-resident, one set per Core):
 //   actors        stable actor id (ActorSlot.pad[0]) indexes every dense per-actor array
 //   clock         u64[n_actors]          Orswot.clock (VClock::dots by id)
-//   member table  u64 mkey[mcap + 1]     open addressing on the u64 member; the bucket index is
-//                                        the member's handle; bucket mcap is reserved for the
-//                                        member ~0 (the empty-key sentinel)
+//   member table  u64 mkey[ms + pcap + 1] open addressing on the u64 member: a primary table of ms
+//                                        slots (L2-sized, grown with the members present), an
+//                                        overflow table of pcap slots for members whose primary
+//                                        window is full, the last slot reserved for the member ~0
+//                                        (the empty-key sentinel); the slot index is the handle
 //   pair table    u64 pkey[pcap]         (member handle << 24 | actor id), EMPTY = ~0
 //                 u64 cur/add/kill/oth[pcap]  entry value (Orswot.entries[m][a]), the batch's
 //                                        applied-add max, removal threshold, merged state's value
@@ -84,15 +86,17 @@ hipError_t launch_ds_count(hipStream_t s, const DsDecodeArgs& a);
 hipError_t launch_ds_emit(hipStream_t s, const DsDecodeArgs& a);
 
 struct DsTables {
-  unsigned long long* mkey;
-  uint32_t mmask;               // mcap - 1 (mcap = power of two)
+  unsigned long long* mkey;      // [smask + 1] primary, [mmask + 1] overflow, 1 reserved (member ~0)
+  uint32_t smask;               // primary slots - 1 (power of two, sized for the members present)
+  uint32_t mmask;               // overflow slots - 1 (= pmask: members <= pairs)
   unsigned long long* pkey;
   unsigned long long* cur;
   unsigned long long* add;
   unsigned long long* kill;
   unsigned long long* oth;
   uint32_t pmask;
-  uint32_t* live;               // [0] live pairs after finalize, [1] used pairs, [2] probe overflow
+  uint32_t* live;               // [0] live pairs after finalize, [1] used pairs, [2] probe overflow,
+                                // [3] a removal deferred, [4] used primary member slots (part fold, k-way merge)
 };
 
 // applied flags of the adds: keys = add_actor sorted stably, perm = add index per position
@@ -159,6 +163,8 @@ struct DsPartArgs {
 };
 __host__ __device__ inline uint64_t ds_part_hist_len(const DsPartArgs& a) { return (uint64_t)a.parts * (a.ba + a.bk) + 1; }
 hipError_t launch_ds_part_count(hipStream_t s, const DsPartArgs& a);
+// out[0] += members held (primary + overflow); out zeroed beforehand
+hipError_t launch_ds_count_members(hipStream_t s, DsTables t, uint32_t* out);
 hipError_t launch_ds_part_apply(hipStream_t s, const DsPartArgs& a);
 // deferred[r] = !(R <= clock)
 // deferred[r] = removal r's clock is not covered by `clock`; any (may be null): set to 1 when

@@ -36,11 +36,23 @@ __device__ __forceinline__ unsigned long long ld_volatile(const unsigned long lo
   return __atomic_load_n(p, __ATOMIC_RELAXED);
 }
 
-// member handle (bucket index) or kDsEmpty when absent (insert = false)
+// member handle (index into mkey) or kDsEmpty when absent (insert = false).  A member lives in
+// the primary table (smask + 1 slots, sized for the members actually present: small enough to stay
+// in L2) unless the kMemberWindow slots of its probe sequence there were all taken by other members
+// when it was inserted; then it lives in the overflow table (as large as the pair table, so it
+// never fills).  Slots never empty again, so a lookup that meets an empty slot in the window knows
+// the member is in neither table, and every thread inserting one member takes the same branch.
+constexpr uint32_t kMemberWindow = 32;
+
+__device__ __forceinline__ unsigned long long member_reserved(const DsTables& t) {
+  return (unsigned long long)t.smask + 1 + t.mmask + 1;
+}
+
 __device__ unsigned long long member_find(const DsTables& t, unsigned long long m, bool insert) {
-  if (m == kDsEmpty) return (unsigned long long)t.mmask + 1;  // reserved bucket
-  uint32_t h = (uint32_t)mix64(m) & t.mmask;
-  for (uint32_t probe = 0; probe <= t.mmask; probe++) {
+  if (m == kDsEmpty) return member_reserved(t);  // reserved bucket
+  const unsigned long long x = mix64(m);
+  uint32_t h = (uint32_t)x & t.smask;
+  for (uint32_t probe = 0; probe < kMemberWindow; probe++) {
     const unsigned long long k = ld_volatile(t.mkey + h);
     if (k == m) return h;
     if (k == kDsEmpty) {
@@ -48,10 +60,33 @@ __device__ unsigned long long member_find(const DsTables& t, unsigned long long 
       const unsigned long long prev = atomicCAS(t.mkey + h, kDsEmpty, m);
       if (prev == kDsEmpty || prev == m) return h;
     }
+    h = (h + 1) & t.smask;
+  }
+  const unsigned long long base = (unsigned long long)t.smask + 1;
+  unsigned long long* ov = t.mkey + base;
+  h = (uint32_t)(x >> 32) & t.mmask;
+  for (uint32_t probe = 0; probe <= t.mmask; probe++) {
+    const unsigned long long k = ld_volatile(ov + h);
+    if (k == m) return base + h;
+    if (k == kDsEmpty) {
+      if (!insert) return kDsEmpty;
+      const unsigned long long prev = atomicCAS(ov + h, kDsEmpty, m);
+      if (prev == kDsEmpty || prev == m) return base + h;
+    }
     h = (h + 1) & t.mmask;
   }
   atomicAdd(t.live + 2, 1u);  // table full (host sizes it to <= 50% load)
   return kDsEmpty;
+}
+
+// used primary member slots among [b * per, (b + 1) * per) for block b of nb (live[4] after a
+// fold / k-way merge: ensure_pairs grows the primary table past half full)
+__device__ __forceinline__ uint32_t primary_used(const DsTables& t, uint32_t b, uint32_t nb) {
+  const uint32_t ms = t.smask + 1, per = (ms + nb - 1) / nb;
+  const uint32_t i0 = min(ms, b * per), i1 = min(ms, i0 + per);
+  uint32_t n = 0;
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) n += t.mkey[i] != kDsEmpty;
+  return n;
 }
 
 // The pair table is cut into partitions of kDsPartSlots consecutive slots: a key's probe sequence
@@ -84,7 +119,7 @@ __device__ __forceinline__ unsigned long long pair_key(unsigned long long handle
 }
 
 __device__ __forceinline__ unsigned long long member_of(const DsTables& t, unsigned long long h) {
-  return h == (unsigned long long)t.mmask + 1 ? kDsEmpty : t.mkey[h];
+  return h == member_reserved(t) ? kDsEmpty : t.mkey[h];
 }
 
 // block-aggregated counter increment: returns this lane's index among all incrementing lanes
@@ -560,7 +595,7 @@ constexpr int kApplyThreads = 512;     // K4
 // for several items at once), else member_find
 __device__ __forceinline__ unsigned long long member_handle(const DsTables& t, unsigned long long m,
                                                             unsigned long long g, bool insert) {
-  if (g == m && m != kDsEmpty) return (uint32_t)mix64(m) & t.mmask;
+  if (g == m && m != kDsEmpty) return (uint32_t)mix64(m) & t.smask;
   return member_find(t, m, insert);
 }
 
@@ -573,6 +608,7 @@ __global__ void __launch_bounds__(kPartThreads) k_ds_part_adds(DsPartArgs a) {
     a.t.live[0] = 0;
     a.t.live[1] = 0;
     a.t.live[3] = 0;
+    a.t.live[4] = 0;
     a.hist[ds_part_hist_len(a) - 1] = 0;
   }
   __syncthreads();
@@ -595,7 +631,7 @@ __global__ void __launch_bounds__(kPartThreads) k_ds_part_adds(DsPartArgs a) {
           j1[q] = j0[q];
         } else if (j1[q] == j0[q] + 1) {
           m[q] = a.o.add_mem[j0[q]];
-          g[q] = a.t.mkey[(uint32_t)mix64(m[q]) & a.t.mmask];
+          g[q] = a.t.mkey[(uint32_t)mix64(m[q]) & a.t.smask];
         }
       }
     }
@@ -643,7 +679,7 @@ __global__ void __launch_bounds__(kPartThreads) k_ds_part_kills(DsPartArgs a) {
           j1[q] = j0[q];
         } else if (j1[q] == j0[q] + 1) {
           m[q] = x.mem[j0[q]];
-          g[q] = a.t.mkey[(uint32_t)mix64(m[q]) & a.t.mmask];
+          g[q] = a.t.mkey[(uint32_t)mix64(m[q]) & a.t.smask];
         }
       }
     }
@@ -728,7 +764,7 @@ __global__ void __launch_bounds__(kPartThreads) k_ds_part_scatter(DsPartArgs a) 
 __global__ void __launch_bounds__(kApplyThreads) k_ds_part_apply(DsPartArgs a) {
   __shared__ unsigned long long key[kDsPartSlots], add[kDsPartSlots], kill[kDsPartSlots];
   __shared__ uint8_t fresh[kDsPartSlots];
-  __shared__ int part[2][kApplyThreads / 64];
+  __shared__ int part[3][kApplyThreads / 64];
   const uint32_t p = blockIdx.x;
   const size_t base = (size_t)p << kDsPartBits;
   for (uint32_t i = threadIdx.x; i < kDsPartSlots; i += kApplyThreads) {
@@ -776,6 +812,7 @@ __global__ void __launch_bounds__(kApplyThreads) k_ds_part_apply(DsPartArgs a) {
   }
   __syncthreads();
   int dl = 0, du = 0;
+  int dm = (int)primary_used(a.t, p, a.parts);
   for (uint32_t i = threadIdx.x; i < kDsPartSlots; i += kApplyThreads) {
     const unsigned long long ad = add[i], kl = kill[i];
     const bool f = fresh[i];
@@ -794,20 +831,24 @@ __global__ void __launch_bounds__(kApplyThreads) k_ds_part_apply(DsPartArgs a) {
   for (int o = 32; o > 0; o >>= 1) {
     dl += __shfl_xor(dl, o);
     du += __shfl_xor(du, o);
+    dm += __shfl_xor(dm, o);
   }
   if ((threadIdx.x & 63) == 0) {
     part[0][threadIdx.x >> 6] = dl;
     part[1][threadIdx.x >> 6] = du;
+    part[2][threadIdx.x >> 6] = dm;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    int l = 0, u = 0;
+    int l = 0, u = 0, mm = 0;
     for (int w = 0; w < kApplyThreads / 64; w++) {
       l += part[0][w];
       u += part[1][w];
+      mm += part[2][w];
     }
     if (l) atomicAdd(a.t.live + 0, (uint32_t)l);
     if (u) atomicAdd(a.t.live + 1, (uint32_t)u);
+    if (mm) atomicAdd(a.t.live + 4, (uint32_t)mm);
   }
 }
 
@@ -920,6 +961,7 @@ __global__ void __launch_bounds__(kBlock) k_ds_merge_finalize(DsTables t, const 
 __global__ void __launch_bounds__(kBlock) k_ds_kput(DsTables t, const DsMergeSrc* src) {
   const DsMergeSrc x = src[blockIdx.y];
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2) t.live[threadIdx.x] = 0;  // k_ds_kfinal counts
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 2) t.live[4] = 0;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < x.n; i += gridDim.x * kBlock) {
     const unsigned long long h = member_find(t, x.member[i], true);
     if (h == kDsEmpty) continue;
@@ -944,7 +986,7 @@ __global__ void __launch_bounds__(kBlock) k_ds_kfinal(DsTables t, const unsigned
                                                       const unsigned long long* oclocks, uint32_t ccap,
                                                       uint32_t nf, unsigned long long* hold) {
   const uint32_t cap = t.pmask + 1;
-  uint32_t n_used = 0, n_live = 0;
+  uint32_t n_used = 0, n_live = 0, n_mem = primary_used(t, blockIdx.x, gridDim.x);
   for (uint32_t b = blockIdx.x * kBlock + threadIdx.x; b < cap; b += gridDim.x * kBlock) {
     const unsigned long long key = t.pkey[b];
     if (key == kDsEmpty) continue;
@@ -967,21 +1009,25 @@ __global__ void __launch_bounds__(kBlock) k_ds_kfinal(DsTables t, const unsigned
   for (int q = 32; q > 0; q >>= 1) {
     n_used += __shfl_xor(n_used, q);
     n_live += __shfl_xor(n_live, q);
+    n_mem += __shfl_xor(n_mem, q);
   }
-  __shared__ uint32_t part[2][kBlock / 64];
+  __shared__ uint32_t part[3][kBlock / 64];
   if ((threadIdx.x & 63) == 0) {
     part[0][threadIdx.x >> 6] = n_live;
     part[1][threadIdx.x >> 6] = n_used;
+    part[2][threadIdx.x >> 6] = n_mem;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t l = 0, u = 0;
+    uint32_t l = 0, u = 0, mm = 0;
     for (int w = 0; w < kBlock / 64; w++) {
       l += part[0][w];
       u += part[1][w];
+      mm += part[2][w];
     }
     if (l) atomicAdd(t.live + 0, l);
     if (u) atomicAdd(t.live + 1, u);
+    if (mm) atomicAdd(t.live + 4, mm);  // (zeroed by k_ds_kput)
   }
 }
 
@@ -1348,6 +1394,20 @@ hipError_t launch_ds_kill(hipStream_t s, DsTables t, const uint32_t* cbeg, const
 
 hipError_t launch_ds_finalize(hipStream_t s, DsTables t) {
   hipLaunchKernelGGL(k_ds_finalize, dim3(blocks_for((uint64_t)t.pmask + 1, 1024)), dim3(kBlock), 0, s, t);
+  return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(kBlock) k_ds_count_members(DsTables t, uint32_t* out) {
+  const uint64_t n = (uint64_t)t.smask + 1 + t.mmask + 1;
+  uint32_t c = 0;
+  for (uint64_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) c += t.mkey[i] != kDsEmpty;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
+}
+
+hipError_t launch_ds_count_members(hipStream_t s, DsTables t, uint32_t* out) {
+  hipLaunchKernelGGL(k_ds_count_members, dim3(blocks_for((uint64_t)t.smask + t.mmask + 2, 1024)), dim3(kBlock), 0, s, t, out);
   return hipGetLastError();
 }
 

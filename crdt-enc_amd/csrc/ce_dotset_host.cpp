@@ -41,7 +41,11 @@ struct DsState {
   uint32_t settle_nr = 0;
   uint64_t settle_rmc = 0, settle_rmm = 0;
   std::vector<std::pair<IdDots, std::vector<uint64_t>>> settle_d0;
-  uint32_t pcap = 0;  // member table and pair table share the capacity (members <= pairs)
+  uint32_t pcap = 0;  // pair table (and member overflow table: members <= pairs) capacity
+  uint32_t mcap_s = 4096;     // primary member table slots (ensure_pairs grows it past half full)
+  uint64_t used_members = 0;  // used primary member slots at the last fold / k-way merge
+  bool settle_members = false;
+  bool primary_fixed = false;  // CE_DS_PRIMARY_SLOTS: never grown (the overflow path under test)
   uint64_t used_pairs = 0, live_pairs = 0;
   std::map<IdDots, std::set<uint64_t>> deferred;  // removal clock -> members (HashMap in crdts)
   // MVReg
@@ -90,6 +94,7 @@ int bits_for(uint32_t v) {
 DsTables tables(DsState* d) {
   DsTables t;
   t.mkey = d->mkey.as<unsigned long long>();
+  t.smask = d->mcap_s - 1;
   t.mmask = d->pcap - 1;
   t.pkey = d->pkey.as<unsigned long long>();
   t.cur = d->cur.as<unsigned long long>();
@@ -105,7 +110,8 @@ int tables_alloc(ce_core* c, uint32_t cap, const FillRange* extra = nullptr) {
   DsState* d = c->ds;
   ce_ctx* ctx = c->ctx;
   hipError_t e;
-  if ((e = d->mkey.reserve((cap + 1ull) * 8)) || (e = d->pkey.reserve(cap * 8ull)) ||
+  const uint64_t mslots = (uint64_t)d->mcap_s + cap + 1;
+  if ((e = d->mkey.reserve(mslots * 8)) || (e = d->pkey.reserve(cap * 8ull)) ||
       (e = d->cur.reserve(cap * 8ull)) || (e = d->add.reserve(cap * 8ull)) ||
       (e = d->kill.reserve(cap * 8ull)) || (e = d->oth.reserve(cap * 8ull)) ||
       (e = d->hold.reserve(cap * 8ull)) || (e = d->live.reserve(64)))
@@ -113,7 +119,7 @@ int tables_alloc(ce_core* c, uint32_t cap, const FillRange* extra = nullptr) {
   d->pcap = cap;
   // every table cleared by one launch (eight blit fills cost a dispatch gap each)
   FillArgs fl{};
-  fl.r[0] = {d->mkey.as<uint32_t>(), (cap + 1ull) * 2, 0xffffffffu};
+  fl.r[0] = {d->mkey.as<uint32_t>(), mslots * 2, 0xffffffffu};
   fl.r[1] = {d->pkey.as<uint32_t>(), cap * 2ull, 0xffffffffu};
   fl.r[2] = {d->cur.as<uint32_t>(), cap * 2ull, 0u};
   fl.r[3] = {d->add.as<uint32_t>(), cap * 2ull, 0u};
@@ -126,6 +132,7 @@ int tables_alloc(ce_core* c, uint32_t cap, const FillRange* extra = nullptr) {
   if ((e = launch_fill(ctx->stream, fl))) return ctx->hip_fail(e, "dot-set tables");
   d->used_pairs = 0;
   d->live_pairs = 0;
+  d->used_members = 0;
   return CE_OK;
 }
 
@@ -177,12 +184,26 @@ int collect(ce_core* c, uint32_t* n_live, unsigned long long* max_member = nullp
 }
 
 // make room for `extra` new pairs at <= 50% load: rebuild from the live entries when needed
+// (or the primary member table past half full: rebuilt with 2.5x the members it holds)
 int ensure_pairs(ce_core* c, uint64_t extra) {
   DsState* d = c->ds;
-  if ((d->used_pairs + extra) * 2 <= d->pcap) return CE_OK;
+  const bool grow_members = d->used_members * 2 > d->mcap_s && d->mcap_s < (1u << 27) && !d->primary_fixed;
+  if ((d->used_pairs + extra) * 2 <= d->pcap && !grow_members) return CE_OK;
+  int rc;
+  if (grow_members) {  // size the primary table for every member held, the overflow's too
+    hipError_t e;
+    if ((e = d->h_cnt.reserve(512))) return c->ctx->hip_fail(e, "members");
+    uint32_t* hm = d->h_cnt.as<uint32_t>() + 40;
+    if ((e = d->col[5].reserve(64 + 8ull * kCollectBlocks)) ||
+        (e = hipMemsetAsync(d->col[5].p, 0, 4, c->ctx->stream)) ||
+        (e = launch_ds_count_members(c->ctx->stream, tables(d), d->col[5].as<uint32_t>())) ||
+        (e = hipMemcpyAsync(hm, d->col[5].p, 4, hipMemcpyDeviceToHost, c->ctx->stream)) ||
+        (e = stream_wait(c->ctx->stream)))
+      return c->ctx->hip_fail(e, "members");
+    d->mcap_s = pow2_at_least(std::max<uint64_t>(4096, std::min<uint64_t>(1u << 27, hm[0] * 5ull / 2)));
+  }
   uint32_t n_live = 0;
-  int rc = collect(c, &n_live);
-  if (rc) return rc;
+  if ((rc = collect(c, &n_live))) return rc;
   const uint32_t cap = pow2_at_least(std::max<uint64_t>(4096, 2 * (n_live + extra) + 1));
   // the collected columns survive the reallocation of the tables
   if ((rc = tables_alloc(c, cap))) return rc;
@@ -639,11 +660,12 @@ int orswot_fold(ce_core* c, const Counts& k, uint64_t kill_bound) {
       (n0 && (e = launch_ds_deferred(s, d->d0[0].as<uint32_t>(), d->d0[2].as<uint32_t>(),
                                      d->d0[3].as<unsigned long long>(), d->clock.as<unsigned long long>(), fl + nr,
                                      n0, live + 3))) ||
-      (e = hipMemcpyAsync(d->h_cnt.as<uint32_t>() + 56, live, 16, hipMemcpyDeviceToHost, s)))
+      (e = hipMemcpyAsync(d->h_cnt.as<uint32_t>() + 56, live, 20, hipMemcpyDeviceToHost, s)))
     return ctx->hip_fail(e, "finalize");
   d->settle_pending = true;
   d->settle_fold = true;
   d->settle_delta = part;
+  d->settle_members = part;
   d->settle_nr = nr;
   d->settle_rmc = k.v[kCntRmC];
   d->settle_rmm = k.v[kCntRmM];
@@ -672,6 +694,7 @@ int ds_settle(ce_core* c) {
     d->live_pairs = hl[0];
     d->used_pairs = hl[1];
   }
+  if (d->settle_members) d->used_members = hl[4];
   if (!d->settle_fold) return CE_OK;
   // 4) deferred = removals whose clock is not covered by the new clock (none: the usual case)
   std::map<IdDots, std::set<uint64_t>> nd;
@@ -964,6 +987,10 @@ int fail_first(ce_core* c, const std::vector<int32_t>& st, int32_t* status_out, 
 // ---------------------------------------------------------------------------------------
 int ds_init(ce_core* c) {
   c->ds = new DsState();
+  if (const char* ps = getenv("CE_DS_PRIMARY_SLOTS")) {  // tests: a fixed (tiny) primary member table
+    c->ds->mcap_s = pow2_at_least(std::max(32, atoi(ps)));
+    c->ds->primary_fixed = true;
+  }
   c->ds->kind = c->kind;
   hipError_t e;
   if ((e = c->ds->misses.reserve(64 + kMissCap * 16ull)) || (e = c->ds->h_cnt.reserve(512)))
@@ -1867,12 +1894,13 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
         (e = launch_ds_kmerge(s, tables(d), d->rd_args_d.as<DsMergeSrc>(), hs, (uint32_t)n,
                               d->clock.as<unsigned long long>(), d->rd_oclocks.as<unsigned long long>(), ccap,
                               d->hold.as<unsigned long long>())) ||
-        (e = hipMemcpyAsync(d->h_cnt.as<uint32_t>() + 56, d->live.p, 16, hipMemcpyDeviceToHost, s)))
+        (e = hipMemcpyAsync(d->h_cnt.as<uint32_t>() + 56, d->live.p, 20, hipMemcpyDeviceToHost, s)))
       return ctx->hip_fail(e, "merge");
     c->path_counts["states_kway_merge"]++;
     d->settle_pending = true;
     d->settle_fold = false;
     d->settle_delta = false;
+    d->settle_members = true;
     for (size_t i = 0; i < n; i++)
       for (auto& y : ds[i].hs.nov) {
         uint32_t sl;

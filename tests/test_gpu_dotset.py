@@ -199,13 +199,25 @@ def test_states_then_ops(ctx, kind, seed):
     core.close()
 
 
+@pytest.mark.parametrize("primary", [None, "32"])
 @pytest.mark.parametrize("p_rm", [0.0, 0.25])
-def test_orswot_kway_state_merge(ctx, p_rm):
+def test_orswot_kway_state_merge(ctx, p_rm, primary):
     """Many state files merged at once (launch_ds_kmerge, taken when no state and no current
     deferred set holds a removal) == the oracle's merges one by one, in two file orders, into an
     empty and into a non-empty state, and == the sequential device merges (CE_NO_KMERGE=1).
     States are version prefixes and writer subsets of one history: the same (member, actor) at
-    different counters, values covered by another file's clock, entries only some files hold."""
+    different counters, values covered by another file's clock, entries only some files hold.
+    primary "32": a 32-slot primary member table that is never grown (CE_DS_PRIMARY_SLOTS), so
+    most members live in the overflow table."""
+    if primary:
+        os.environ["CE_DS_PRIMARY_SLOTS"] = primary
+    try:
+        _kway_state_merge(ctx, p_rm)
+    finally:
+        os.environ.pop("CE_DS_PRIMARY_SLOTS", None)
+
+
+def _kway_state_merge(ctx, p_rm):
     rng = random.Random(91 + int(p_rm * 100))
     key = rng.randbytes(32)
     actors = G.actors_for(rng, 6)
@@ -846,19 +858,22 @@ def test_orswot_partitioned_fold_equals_global(ctx, adversarial):
         rc = oc.read_remote_ops(key, [APP], sealed, [acts[i] for i in fa], fv)[0]
         want.append((rc, oc.serialize()))
     got = {}
-    for forced in (False, True):
-        if forced:
-            os.environ["CE_DS_FOLD_GLOBAL"] = "1"
+    modes = {"partitioned": {}, "global": {"CE_DS_FOLD_GLOBAL": "1"},
+             "member_overflow": {"CE_DS_PRIMARY_SLOTS": "64"}}   # most members in the overflow table
+    for mode, env in modes.items():
+        os.environ.update(env)
         try:
             core = new_core(ctx, "orswot", key)
             out = []
             for acts, sealed, fa, fv in batches:
                 out.append((core.ingest_ops(sealed, acts, fa, fv)[0], core.state_bytes()))
-            got[forced] = (out, core.path_count("ds_fold_partitioned"), core.path_count("ds_fold_global"))
+            got[mode] = (out, core.path_count("ds_fold_partitioned"), core.path_count("ds_fold_global"))
             core.close()
         finally:
-            os.environ.pop("CE_DS_FOLD_GLOBAL", None)
-    assert got[False][0] == want
-    assert got[True][0] == want
-    assert got[False][1] == len(batches) and got[False][2] == 0
-    assert got[True][1] == 0 and got[True][2] == len(batches)
+            for k in env:
+                os.environ.pop(k, None)
+    for mode in modes:
+        assert got[mode][0] == want, mode
+    assert got["partitioned"][1:] == (len(batches), 0)
+    assert got["member_overflow"][1:] == (len(batches), 0)
+    assert got["global"][1:] == (0, len(batches))
