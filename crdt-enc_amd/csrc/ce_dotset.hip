@@ -7,6 +7,8 @@
 // contraction.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <hipcub/hipcub.hpp>
 
 #include "ce_dotset.h"
@@ -765,7 +767,10 @@ __global__ void __launch_bounds__(kApplyThreads) k_ds_part_apply(DsPartArgs a) {
   __shared__ unsigned long long key[kDsPartSlots], add[kDsPartSlots], kill[kDsPartSlots];
   __shared__ uint8_t fresh[kDsPartSlots];
   __shared__ int part[3][kApplyThreads / 64];
-  const uint32_t p = blockIdx.x;
+  int dl = 0, du = 0, dm = 0;
+  // a grid of a few workgroups per CU walks the partitions (one short-lived workgroup per
+  // partition left the CUs mostly empty between launches)
+  for (uint32_t p = blockIdx.x; p < a.parts; p += gridDim.x) {
   const size_t base = (size_t)p << kDsPartBits;
   for (uint32_t i = threadIdx.x; i < kDsPartSlots; i += kApplyThreads) {
     key[i] = a.t.pkey[base + i];
@@ -811,8 +816,7 @@ __global__ void __launch_bounds__(kApplyThreads) k_ds_part_apply(DsPartArgs a) {
     }
   }
   __syncthreads();
-  int dl = 0, du = 0;
-  int dm = (int)primary_used(a.t, p, a.parts);
+  dm += (int)primary_used(a.t, p, a.parts);
   for (uint32_t i = threadIdx.x; i < kDsPartSlots; i += kApplyThreads) {
     const unsigned long long ad = add[i], kl = kill[i];
     const bool f = fresh[i];
@@ -826,6 +830,8 @@ __global__ void __launch_bounds__(kApplyThreads) k_ds_part_apply(DsPartArgs a) {
     if (v != 0 && v <= kl) v = 0;
     if (v != c) a.t.cur[base + i] = v;
     dl += (int)(v != 0) - (int)(c != 0);
+  }
+  __syncthreads();  // the next partition reuses the LDS tables
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -1420,7 +1426,8 @@ hipError_t launch_ds_part_count(hipStream_t s, const DsPartArgs& a) {
 
 hipError_t launch_ds_part_apply(hipStream_t s, const DsPartArgs& a) {
   if (a.ba + a.bk) hipLaunchKernelGGL(k_ds_part_scatter, dim3(a.ba + a.bk), dim3(kPartThreads), (size_t)a.parts * 4, s, a);
-  hipLaunchKernelGGL(k_ds_part_apply, dim3(a.parts), dim3(kApplyThreads), 0, s, a);
+  static const uint32_t grid = getenv("CE_DS_APPLY_GRID") ? (uint32_t)atoi(getenv("CE_DS_APPLY_GRID")) : 768u;
+  hipLaunchKernelGGL(k_ds_part_apply, dim3(grid && grid < a.parts ? grid : a.parts), dim3(kApplyThreads), 0, s, a);
   return hipGetLastError();
 }
 

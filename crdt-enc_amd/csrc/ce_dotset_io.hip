@@ -16,6 +16,8 @@
 // Integer / byte work bounded by HBM latency; no MFMA.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <hipcub/hipcub.hpp>
 #include <map>
@@ -80,6 +82,30 @@ __global__ void k_ser_gather2(const uint32_t* perm, const uint32_t* actor_in, co
 __global__ void k_ser_gather_member(const uint32_t* perm, const unsigned long long* member_in,
                                     unsigned long long* member_out, uint32_t n) {
   for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < n; i += gridDim.x * kB) member_out[i] = member_in[perm[i]];
+}
+
+// one sort when (member, rank) packs into K: key = member << rank_bits | rank, perm = iota
+// ((member, actor) pairs are unique, so no two keys tie)
+template <typename K>
+__global__ void k_ser_key(const uint32_t* actor, const uint32_t* rank_of_id, const unsigned long long* member,
+                          int rank_bits, K* key, uint32_t* perm, uint32_t n) {
+  for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < n; i += gridDim.x * kB) {
+    key[i] = ((K)member[i] << rank_bits) | (K)rank_of_id[actor[i]];
+    perm[i] = i;
+  }
+}
+
+// member from the sorted key (member_out may alias key), actor / value gathered
+template <typename K>
+__global__ void k_ser_gather3(const uint32_t* perm, const K* key, int rank_bits, const uint32_t* actor_in,
+                              const unsigned long long* value_in, unsigned long long* member_out,
+                              uint32_t* actor_out, unsigned long long* value_out, uint32_t n) {
+  for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < n; i += gridDim.x * kB) {
+    const uint32_t j = perm[i];
+    member_out[i] = (unsigned long long)(key[i] >> rank_bits);
+    actor_out[i] = actor_in[j];
+    value_out[i] = value_in[j];
+  }
 }
 
 // head[i] = pair i starts a member's entry
@@ -463,10 +489,31 @@ hipError_t launch_orswot_ser(hipStream_t s, OrswotSerScratch& sc, const OrswotSe
 }
 
 hipError_t launch_orswot_ser_sort(hipStream_t s, OrswotSerScratch& sc, uint32_t n) {
-  // pairs (member, actor id, value) in collect order -> sorted by (member, rank): sort by rank,
-  // then stably by member (LSD order), gather
+  // pairs (member, actor id, value) in collect order -> sorted by (member, rank): one sort of the
+  // packed (member, rank) key when it fits 64 bits (CE_SER_TWO_SORTS=1: the general form -- sort by
+  // rank, then stably by member, LSD order), gather
   hipError_t e;
-  if (n) {
+  const int kb = sc.member_bits + sc.rank_bits;
+  if (n && kb <= 64 && !getenv("CE_SER_TWO_SORTS")) {
+    // (member, rank) in one key: one radix sort over member_bits + rank_bits
+    size_t tb = sc.tmp_bytes;
+    if (kb <= 32) {
+      hipLaunchKernelGGL(k_ser_key<uint32_t>, dim3(nblk(n)), dim3(kB), 0, s, sc.actor_in, sc.rank_of_id, sc.member_in,
+                         sc.rank_bits, sc.k32a, sc.p32a, n);
+      if ((e = hipcub::DeviceRadixSort::SortPairs(sc.tmp, tb, sc.k32a, sc.k32b, sc.p32a, sc.p32b, (int)n, 0, kb, s)))
+        return e;
+      hipLaunchKernelGGL(k_ser_gather3<uint32_t>, dim3(nblk(n)), dim3(kB), 0, s, sc.p32b, sc.k32b, sc.rank_bits,
+                         sc.actor_in, sc.value_in, sc.member_sorted, sc.actor_sorted, sc.value_sorted, n);
+    } else {
+      hipLaunchKernelGGL(k_ser_key<unsigned long long>, dim3(nblk(n)), dim3(kB), 0, s, sc.actor_in, sc.rank_of_id,
+                         sc.member_in, sc.rank_bits, sc.k64a, sc.p32a, n);
+      if ((e = hipcub::DeviceRadixSort::SortPairs(sc.tmp, tb, sc.k64a, sc.member_sorted, sc.p32a, sc.p32b, (int)n, 0,
+                                                   kb, s)))
+        return e;
+      hipLaunchKernelGGL(k_ser_gather3<unsigned long long>, dim3(nblk(n)), dim3(kB), 0, s, sc.p32b, sc.member_sorted,
+                         sc.rank_bits, sc.actor_in, sc.value_in, sc.member_sorted, sc.actor_sorted, sc.value_sorted, n);
+    }
+  } else if (n) {
     size_t tb = sc.tmp_bytes;
     hipLaunchKernelGGL(k_ser_rank, dim3(nblk(n)), dim3(kB), 0, s, sc.actor_in, sc.rank_of_id, sc.k32a, n);
     hipLaunchKernelGGL(k_ser_iota, dim3(nblk(n)), dim3(kB), 0, s, sc.p32a, n);
@@ -480,6 +527,9 @@ hipError_t launch_orswot_ser_sort(hipStream_t s, OrswotSerScratch& sc, uint32_t 
       return e;
     hipLaunchKernelGGL(k_ser_gather2, dim3(nblk(n)), dim3(kB), 0, s, sc.p32a, sc.actor_in, sc.value_in,
                        sc.actor_sorted, sc.value_sorted, n);
+  }
+  if (n) {
+    size_t tb = sc.tmp_bytes;
     hipLaunchKernelGGL(k_ser_head, dim3(nblk(n)), dim3(kB), 0, s, sc.member_sorted, sc.head, n);
     tb = sc.tmp_bytes;
     if ((e = ds_excl_sum_u32(sc.tmp, tb, sc.head, sc.hrank, n, s))) return e;

@@ -877,3 +877,37 @@ def test_orswot_partitioned_fold_equals_global(ctx, adversarial):
     assert got["partitioned"][1:] == (len(batches), 0)
     assert got["member_overflow"][1:] == (len(batches), 0)
     assert got["global"][1:] == (0, len(batches))
+
+
+@pytest.mark.parametrize("n_members", [300, 1 << 40, (1 << 64) - 1])
+def test_orswot_serializer_one_sort_equals_two(ctx, n_members):
+    """The device serializer sorts the live (member, actor) pairs by one packed key when member
+    bits + actor-rank bits fit 32 (u32 keys) or 64 (u64 keys), else by rank then stably by member;
+    the packed sort == the two-sort form (CE_SER_TWO_SORTS=1) == the oracle's bytes, for small,
+    40-bit and full 64-bit members."""
+    rng = random.Random(929 + n_members % 1000)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 7)
+    files = G.well_formed_orswot(rng, actors, 3, 8, n_members)[0]
+    acts, clears, fa, fv = G.batch(files, "orswot", APP)
+    sealed = seal_files(ctx, key, clears)
+    oc = C.Core("orswot")
+    assert oc.read_remote_ops(key, [APP], sealed, [acts[i] for i in fa], fv)[0] == 0
+    import torch
+    want = oc.serialize()
+    got = []
+    for two in (False, True):
+        if two:
+            os.environ["CE_SER_TWO_SORTS"] = "1"
+        try:
+            core = new_core(ctx, "orswot", key)
+            assert core.ingest_ops(sealed, acts, fa, fv)[0] == 0
+            buf = torch.zeros(len(want) + 4096, dtype=torch.uint8, device="cuda:0")
+            rc, n = core.state_bytes_device(buf.data_ptr(), buf.numel())   # the device serializer
+            assert rc == 0
+            torch.cuda.synchronize()
+            got.append(bytes(buf[:n].cpu().numpy().tobytes()))
+            core.close()
+        finally:
+            os.environ.pop("CE_SER_TWO_SORTS", None)
+    assert got[0] == got[1] == want
