@@ -759,79 +759,123 @@ __global__ void __launch_bounds__(kPartThreads) k_ds_part_scatter(DsPartArgs a) 
   }
 }
 
-// K4: partition p = blockIdx.x.  Keys in LDS follow pair_find's probe order (start at
-// mix64(key) mod the partition, wrap inside it), so a key inserted here sits where the global
-// kernels look for it.  Then finalize (k_ds_finalize) of the touched slots only: an untouched
-// slot's value is unchanged by it.
+// K4: partition p = blockIdx.x (+ k * gridDim.x).  Keys in LDS follow pair_find's probe order
+// (start at mix64(key) mod the partition, wrap inside it), so a key inserted here sits where the
+// global kernels look for it.  Then finalize (k_ds_finalize) of the touched slots only: an
+// untouched slot's value is unchanged by it.  Every phase issues all of a lane's global loads
+// before using any (the compiler does not overlap the trips of a loop: one round trip each).
+constexpr int kApplySlotsPerLane = kDsPartSlots / kApplyThreads;
+constexpr int kApplyItemBatch = 4;
+
+__device__ __forceinline__ uint32_t lds_insert(unsigned long long* key, unsigned long long k) {
+  constexpr uint32_t M = kDsPartSlots - 1;
+  uint32_t h = (uint32_t)mix64(k) & M;
+  for (uint32_t probe = 0; probe < kDsPartSlots; probe++) {
+    const unsigned long long c = key[h];
+    if (c == k) return h;
+    if (c == kDsEmpty) {
+      const unsigned long long prev = atomicCAS(&key[h], kDsEmpty, k);
+      if (prev == kDsEmpty || prev == k) return h;
+    }
+    h = (h + 1) & M;
+  }
+  return ~0u;
+}
+
+__device__ __forceinline__ uint32_t lds_lookup(const unsigned long long* key, unsigned long long k) {
+  constexpr uint32_t M = kDsPartSlots - 1;
+  uint32_t h = (uint32_t)mix64(k) & M;
+  for (uint32_t probe = 0; probe < kDsPartSlots; probe++) {
+    const unsigned long long c = key[h];
+    if (c == k) return h;
+    if (c == kDsEmpty) return ~0u;
+    h = (h + 1) & M;
+  }
+  return ~0u;
+}
+
 __global__ void __launch_bounds__(kApplyThreads) k_ds_part_apply(DsPartArgs a) {
   __shared__ unsigned long long key[kDsPartSlots], add[kDsPartSlots], kill[kDsPartSlots];
-  __shared__ uint8_t fresh[kDsPartSlots];
   __shared__ int part[3][kApplyThreads / 64];
   int dl = 0, du = 0, dm = 0;
-  // a grid of a few workgroups per CU walks the partitions (one short-lived workgroup per
-  // partition left the CUs mostly empty between launches)
+  const uint32_t tid = threadIdx.x;
+  // a grid of a few workgroups per CU walks the partitions
   for (uint32_t p = blockIdx.x; p < a.parts; p += gridDim.x) {
-  const size_t base = (size_t)p << kDsPartBits;
-  for (uint32_t i = threadIdx.x; i < kDsPartSlots; i += kApplyThreads) {
-    key[i] = a.t.pkey[base + i];
-    add[i] = 0;
-    kill[i] = 0;
-    fresh[i] = 0;
-  }
-  __syncthreads();
-  constexpr uint32_t M = kDsPartSlots - 1;
-  const uint32_t ia0 = a.off[(size_t)p * a.ba], ia1 = a.off[(size_t)(p + 1) * a.ba];
-  for (uint32_t i = ia0 + threadIdx.x; i < ia1; i += kApplyThreads) {
-    const ulonglong2 it = *reinterpret_cast<const ulonglong2*>(a.items + 2ull * i);
-    uint32_t h = (uint32_t)mix64(it.x) & M;
-    bool done = false;
-    for (uint32_t probe = 0; probe < kDsPartSlots && !done; probe++) {
-      const unsigned long long k = key[h];
-      if (k == kDsEmpty) {
-        const unsigned long long prev = atomicCAS(&key[h], kDsEmpty, it.x);
-        if (prev == kDsEmpty) fresh[h] = 1;
-        done = prev == kDsEmpty || prev == it.x;
-      } else {
-        done = k == it.x;
+    const size_t base = (size_t)p << kDsPartBits;
+    unsigned long long k0[kApplySlotsPerLane];
+#pragma unroll
+    for (int q = 0; q < kApplySlotsPerLane; q++) k0[q] = a.t.pkey[base + tid + q * kApplyThreads];
+#pragma unroll
+    for (int q = 0; q < kApplySlotsPerLane; q++) {
+      const uint32_t i = tid + q * kApplyThreads;
+      key[i] = k0[q];
+      add[i] = 0;
+      kill[i] = 0;
+    }
+    __syncthreads();
+    // adds: insert, max-merge the counter
+    const uint32_t ia0 = a.off[(size_t)p * a.ba], ia1 = a.off[(size_t)(p + 1) * a.ba];
+    for (uint32_t i0 = ia0; i0 < ia1; i0 += kApplyThreads * kApplyItemBatch) {
+      ulonglong2 it[kApplyItemBatch];
+#pragma unroll
+      for (int b = 0; b < kApplyItemBatch; b++) {
+        const uint32_t i = i0 + tid + b * kApplyThreads;
+        it[b] = i < ia1 ? *reinterpret_cast<const ulonglong2*>(a.items + 2ull * i) : make_ulonglong2(kDsEmpty, 0);
       }
-      if (!done) h = (h + 1) & M;
-    }
-    if (done) atomicMax(&add[h], it.y);
-    else atomicAdd(a.t.live + 2, 1u);  // partition full (tables sized to <= 50% load)
-  }
-  __syncthreads();
-  const size_t kcol = (size_t)a.parts * a.ba;
-  const uint32_t ik0 = a.off[kcol + (size_t)p * a.bk], ik1 = a.off[kcol + (size_t)(p + 1) * a.bk];
-  for (uint32_t i = ik0 + threadIdx.x; i < ik1; i += kApplyThreads) {
-    const ulonglong2 it = *reinterpret_cast<const ulonglong2*>(a.items + 2ull * i);
-    uint32_t h = (uint32_t)mix64(it.x) & M;
-    for (uint32_t probe = 0; probe < kDsPartSlots; probe++) {
-      const unsigned long long k = key[h];
-      if (k == it.x) {
-        atomicMax(&kill[h], it.y);
-        break;
+#pragma unroll
+      for (int b = 0; b < kApplyItemBatch; b++) {
+        if (it[b].x == kDsEmpty) continue;
+        const uint32_t h = lds_insert(key, it[b].x);
+        if (h != ~0u) atomicMax(&add[h], it[b].y);
+        else atomicAdd(a.t.live + 2, 1u);  // partition full (tables sized to <= 50% load)
       }
-      if (k == kDsEmpty) break;
-      h = (h + 1) & M;
     }
-  }
-  __syncthreads();
-  dm += (int)primary_used(a.t, p, a.parts);
-  for (uint32_t i = threadIdx.x; i < kDsPartSlots; i += kApplyThreads) {
-    const unsigned long long ad = add[i], kl = kill[i];
-    const bool f = fresh[i];
-    if (f) {
-      a.t.pkey[base + i] = key[i];
-      du++;
+    __syncthreads();
+    // removals: thresholds of existing pairs
+    const size_t kcol = (size_t)a.parts * a.ba;
+    const uint32_t ik0 = a.off[kcol + (size_t)p * a.bk], ik1 = a.off[kcol + (size_t)(p + 1) * a.bk];
+    for (uint32_t i0 = ik0; i0 < ik1; i0 += kApplyThreads * kApplyItemBatch) {
+      ulonglong2 it[kApplyItemBatch];
+#pragma unroll
+      for (int b = 0; b < kApplyItemBatch; b++) {
+        const uint32_t i = i0 + tid + b * kApplyThreads;
+        it[b] = i < ik1 ? *reinterpret_cast<const ulonglong2*>(a.items + 2ull * i) : make_ulonglong2(kDsEmpty, 0);
+      }
+#pragma unroll
+      for (int b = 0; b < kApplyItemBatch; b++) {
+        if (it[b].x == kDsEmpty) continue;
+        const uint32_t h = lds_lookup(key, it[b].x);
+        if (h != ~0u) atomicMax(&kill[h], it[b].y);
+      }
     }
-    if (!ad && !kl) continue;
-    const unsigned long long c = f ? 0ull : a.t.cur[base + i];
-    unsigned long long v = c > ad ? c : ad;
-    if (v != 0 && v <= kl) v = 0;
-    if (v != c) a.t.cur[base + i] = v;
-    dl += (int)(v != 0) - (int)(c != 0);
-  }
-  __syncthreads();  // the next partition reuses the LDS tables
+    dm += (int)primary_used(a.t, p, a.parts);
+    __syncthreads();
+    // finalize the touched slots: the current values they need, all loads first
+    unsigned long long ad[kApplySlotsPerLane], kl[kApplySlotsPerLane], c[kApplySlotsPerLane];
+    bool fresh[kApplySlotsPerLane];
+#pragma unroll
+    for (int q = 0; q < kApplySlotsPerLane; q++) {
+      const uint32_t i = tid + q * kApplyThreads;
+      ad[q] = add[i];
+      kl[q] = kill[i];
+      fresh[q] = k0[q] == kDsEmpty && key[i] != kDsEmpty;
+      c[q] = 0;
+      if (!fresh[q] && (ad[q] | kl[q])) c[q] = a.t.cur[base + i];
+    }
+#pragma unroll
+    for (int q = 0; q < kApplySlotsPerLane; q++) {
+      const uint32_t i = tid + q * kApplyThreads;
+      if (fresh[q]) {
+        a.t.pkey[base + i] = key[i];
+        du++;
+      }
+      if (!(ad[q] | kl[q])) continue;
+      unsigned long long v = c[q] > ad[q] ? c[q] : ad[q];
+      if (v != 0 && v <= kl[q]) v = 0;
+      if (v != c[q]) a.t.cur[base + i] = v;
+      dl += (int)(v != 0) - (int)(c[q] != 0);
+    }
+    __syncthreads();  // the next partition reuses the LDS tables
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -839,13 +883,13 @@ __global__ void __launch_bounds__(kApplyThreads) k_ds_part_apply(DsPartArgs a) {
     du += __shfl_xor(du, o);
     dm += __shfl_xor(dm, o);
   }
-  if ((threadIdx.x & 63) == 0) {
-    part[0][threadIdx.x >> 6] = dl;
-    part[1][threadIdx.x >> 6] = du;
-    part[2][threadIdx.x >> 6] = dm;
+  if ((tid & 63) == 0) {
+    part[0][tid >> 6] = dl;
+    part[1][tid >> 6] = du;
+    part[2][tid >> 6] = dm;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (tid == 0) {
     int l = 0, u = 0, mm = 0;
     for (int w = 0; w < kApplyThreads / 64; w++) {
       l += part[0][w];
@@ -993,23 +1037,52 @@ __global__ void __launch_bounds__(kBlock) k_ds_kfinal(DsTables t, const unsigned
                                                       uint32_t nf, unsigned long long* hold) {
   const uint32_t cap = t.pmask + 1;
   uint32_t n_used = 0, n_live = 0, n_mem = primary_used(t, blockIdx.x, gridDim.x);
-  for (uint32_t b = blockIdx.x * kBlock + threadIdx.x; b < cap; b += gridDim.x * kBlock) {
-    const unsigned long long key = t.pkey[b];
-    if (key == kDsEmpty) continue;
-    n_used++;
-    const uint32_t a = (uint32_t)(key & ((1u << kDsActorBits) - 1));
-    // (add / kill are zero here: every fold's finalize clears what it set, so a state merge never
-    // meets a batch's scratch -- not read, 64 MB less per pass at C3)
-    const unsigned long long s = t.cur[b], o = t.oth[b], hm = hold[b];
-    const unsigned long long m = s > o ? s : o;
-    bool keep = m != 0 && (s == m || m > clock[a]);
-    for (uint32_t f = 0; f < nf && keep; f++)
-      if (!((hm >> f) & 1ull)) keep = m > oclocks[(size_t)f * ccap + a];
-    const unsigned long long v = keep ? m : 0ull;
-    if (v != s) t.cur[b] = v;
-    if (o) t.oth[b] = 0;
-    if (hm) hold[b] = 0;
-    n_live += v != 0;
+  // kKQ slots per lane and trip, every load of a trip issued before any is used
+  constexpr int kKQ = 4;
+  for (uint32_t b0 = blockIdx.x * kBlock * kKQ + threadIdx.x; b0 < cap; b0 += gridDim.x * kBlock * kKQ) {
+    unsigned long long key[kKQ], s[kKQ], o[kKQ], hm[kKQ];
+#pragma unroll
+    for (int q = 0; q < kKQ; q++) key[q] = b0 + q * kBlock < cap ? t.pkey[b0 + q * kBlock] : kDsEmpty;
+#pragma unroll
+    for (int q = 0; q < kKQ; q++) {
+      s[q] = o[q] = hm[q] = 0;
+      if (key[q] == kDsEmpty) continue;
+      // (add / kill are zero here: every fold's finalize clears what it set, so a state merge never
+      // meets a batch's scratch -- not read, 64 MB less per pass at C3)
+      s[q] = t.cur[b0 + q * kBlock];
+      o[q] = t.oth[b0 + q * kBlock];
+      hm[q] = hold[b0 + q * kBlock];
+    }
+    // the clocks the rule reads: ours and those of the first kKF files not holding the max, one
+    // batch of loads for every slot of the trip (a loop over the files waits on each in turn)
+    constexpr int kKF = 8;
+    unsigned long long ck[kKQ], oc[kKQ][kKF];
+#pragma unroll
+    for (int q = 0; q < kKQ; q++) {
+      const uint32_t a = (uint32_t)(key[q] & ((1u << kDsActorBits) - 1));
+      ck[q] = key[q] != kDsEmpty ? clock[a] : 0ull;
+#pragma unroll
+      for (int f = 0; f < kKF; f++)
+        oc[q][f] = key[q] != kDsEmpty && (uint32_t)f < nf && !((hm[q] >> f) & 1ull) ? oclocks[(size_t)f * ccap + a] : 0ull;
+    }
+#pragma unroll
+    for (int q = 0; q < kKQ; q++) {
+      if (key[q] == kDsEmpty) continue;
+      const uint32_t b = b0 + q * kBlock;
+      n_used++;
+      const uint32_t a = (uint32_t)(key[q] & ((1u << kDsActorBits) - 1));
+      const unsigned long long m = s[q] > o[q] ? s[q] : o[q];
+      bool keep = m != 0 && (s[q] == m || m > ck[q]);
+#pragma unroll
+      for (int f = 0; f < kKF; f++) keep = keep && m > oc[q][f];  // (0 for a holder: m > 0)
+      for (uint32_t f = kKF; f < nf && keep; f++)
+        if (!((hm[q] >> f) & 1ull)) keep = m > oclocks[(size_t)f * ccap + a];
+      const unsigned long long v = keep ? m : 0ull;
+      if (v != s[q]) t.cur[b] = v;
+      if (o[q]) t.oth[b] = 0;
+      if (hm[q]) hold[b] = 0;
+      n_live += v != 0;
+    }
   }
 #pragma unroll
   for (int q = 32; q > 0; q >>= 1) {
@@ -1064,10 +1137,17 @@ __global__ void __launch_bounds__(kBlock) k_ds_collect(DsTables t, unsigned long
   const uint32_t cap = t.pmask + 1;
   const uint32_t per = (cap + gridDim.x - 1) / gridDim.x;
   const uint32_t r0 = min(cap, blockIdx.x * per), r1 = min(cap, r0 + per);
+  // kCQ slots per lane and trip, loads first (one round trip per trip, not per slot)
+  constexpr int kCQ = 8;
   uint32_t n = 0;
-  for (uint32_t b = r0 + threadIdx.x; b < r1; b += kBlock) {
-    const unsigned long long key = t.pkey[b];
-    n += key != kDsEmpty && t.cur[b] != 0;
+  for (uint32_t b0 = r0 + threadIdx.x; b0 < r1; b0 += kBlock * kCQ) {
+    unsigned long long key[kCQ], v[kCQ];
+#pragma unroll
+    for (int q = 0; q < kCQ; q++) key[q] = b0 + q * kBlock < r1 ? t.pkey[b0 + q * kBlock] : kDsEmpty;
+#pragma unroll
+    for (int q = 0; q < kCQ; q++) v[q] = key[q] != kDsEmpty ? t.cur[b0 + q * kBlock] : 0ull;
+#pragma unroll
+    for (int q = 0; q < kCQ; q++) n += v[q] != 0;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
@@ -1081,17 +1161,23 @@ __global__ void __launch_bounds__(kBlock) k_ds_collect(DsTables t, unsigned long
   }
   __syncthreads();
   unsigned long long mx = 0;
-  for (uint32_t b = r0 + threadIdx.x; b < r1; b += kBlock) {
-    const unsigned long long key = t.pkey[b];
-    if (key == kDsEmpty) continue;
-    const unsigned long long v = t.cur[b];
-    if (v == 0) continue;
-    const uint32_t idx = base + atomicAdd(&lcount, 1u);
-    const unsigned long long m = member_of(t, key >> kDsActorBits);
-    member[idx] = m;
-    actor[idx] = (uint32_t)(key & ((1u << kDsActorBits) - 1));
-    value[idx] = v;
-    mx = m > mx ? m : mx;
+  for (uint32_t b0 = r0 + threadIdx.x; b0 < r1; b0 += kBlock * kCQ) {
+    unsigned long long key[kCQ], v[kCQ], m[kCQ];
+#pragma unroll
+    for (int q = 0; q < kCQ; q++) key[q] = b0 + q * kBlock < r1 ? t.pkey[b0 + q * kBlock] : kDsEmpty;
+#pragma unroll
+    for (int q = 0; q < kCQ; q++) v[q] = key[q] != kDsEmpty ? t.cur[b0 + q * kBlock] : 0ull;
+#pragma unroll
+    for (int q = 0; q < kCQ; q++) m[q] = v[q] ? member_of(t, key[q] >> kDsActorBits) : 0ull;
+#pragma unroll
+    for (int q = 0; q < kCQ; q++) {
+      if (v[q] == 0) continue;
+      const uint32_t idx = base + atomicAdd(&lcount, 1u);
+      member[idx] = m[q];
+      actor[idx] = (uint32_t)(key[q] & ((1u << kDsActorBits) - 1));
+      value[idx] = v[q];
+      mx = m[q] > mx ? m[q] : mx;
+    }
   }
   mx = wave_max64(mx);
   if ((threadIdx.x & 63) == 0) lmax[threadIdx.x >> 6] = mx;
