@@ -1123,45 +1123,31 @@ __global__ void k_ds_kclock(unsigned long long* clock, const unsigned long long*
 }
 
 // live pairs -> (member, actor id, value) columns, in no particular order (the writer sorts).
-// A block owns a contiguous run of slots: it counts its live pairs, reserves their slice with one
-// atomicAdd, then writes them -- a reservation per block and loop trip (3 barriers and a global
-// atomic each, 16K same-address atomics over a 4M-slot table) cost ~0.2 ms at C3.  n_out[2..3]:
+// A block owns a contiguous run of slots and walks it in 2048-slot sub-ranges, one reservation
+// (a same-address atomic) per sub-range: 2048 over C3's 4M-slot table (16K reservations, one per
+// 256 slots, cost ~0.2 ms: same-address atomics serialise in L2).  n_out[2..3]:
 // the largest live member (the writer sorts only its significant bits), per-block maxima through
 // bmax and k_ds_collect_max.
 __global__ void __launch_bounds__(kBlock) k_ds_collect(DsTables t, unsigned long long* member, uint32_t* actor,
                                                        unsigned long long* value, uint32_t* n_out,
                                                        unsigned long long* bmax) {
-  __shared__ uint32_t part[kBlock / 64];
+  // one pass: a sub-range's live pairs are staged in LDS (kCQ slots per lane, every load of the
+  // trip issued first), the sub-range reserves its output slice with one atomic, then the staged
+  // columns go out with coalesced stores
+  constexpr int kCQ = 8;
+  constexpr uint32_t kSub = kBlock * kCQ;
+  __shared__ unsigned long long sm[kSub], sv[kSub];
+  __shared__ uint32_t sa[kSub];
   __shared__ uint32_t lcount, base;
   __shared__ unsigned long long lmax[kBlock / 64];
   const uint32_t cap = t.pmask + 1;
   const uint32_t per = (cap + gridDim.x - 1) / gridDim.x;
   const uint32_t r0 = min(cap, blockIdx.x * per), r1 = min(cap, r0 + per);
-  // kCQ slots per lane and trip, loads first (one round trip per trip, not per slot)
-  constexpr int kCQ = 8;
-  uint32_t n = 0;
-  for (uint32_t b0 = r0 + threadIdx.x; b0 < r1; b0 += kBlock * kCQ) {
-    unsigned long long key[kCQ], v[kCQ];
-#pragma unroll
-    for (int q = 0; q < kCQ; q++) key[q] = b0 + q * kBlock < r1 ? t.pkey[b0 + q * kBlock] : kDsEmpty;
-#pragma unroll
-    for (int q = 0; q < kCQ; q++) v[q] = key[q] != kDsEmpty ? t.cur[b0 + q * kBlock] : 0ull;
-#pragma unroll
-    for (int q = 0; q < kCQ; q++) n += v[q] != 0;
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = n;
-  if (threadIdx.x == 0) lcount = 0;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t tot = 0;
-    for (int w = 0; w < kBlock / 64; w++) tot += part[w];
-    base = tot ? atomicAdd(n_out, tot) : 0u;
-  }
-  __syncthreads();
   unsigned long long mx = 0;
-  for (uint32_t b0 = r0 + threadIdx.x; b0 < r1; b0 += kBlock * kCQ) {
+  for (uint32_t s0 = r0; s0 < r1; s0 += kSub) {
+    if (threadIdx.x == 0) lcount = 0;
+    __syncthreads();
+    const uint32_t b0 = s0 + threadIdx.x;
     unsigned long long key[kCQ], v[kCQ], m[kCQ];
 #pragma unroll
     for (int q = 0; q < kCQ; q++) key[q] = b0 + q * kBlock < r1 ? t.pkey[b0 + q * kBlock] : kDsEmpty;
@@ -1172,20 +1158,31 @@ __global__ void __launch_bounds__(kBlock) k_ds_collect(DsTables t, unsigned long
 #pragma unroll
     for (int q = 0; q < kCQ; q++) {
       if (v[q] == 0) continue;
-      const uint32_t idx = base + atomicAdd(&lcount, 1u);
-      member[idx] = m[q];
-      actor[idx] = (uint32_t)(key[q] & ((1u << kDsActorBits) - 1));
-      value[idx] = v[q];
+      const uint32_t idx = atomicAdd(&lcount, 1u);
+      sm[idx] = m[q];
+      sa[idx] = (uint32_t)(key[q] & ((1u << kDsActorBits) - 1));
+      sv[idx] = v[q];
       mx = m[q] > mx ? m[q] : mx;
     }
+    __syncthreads();
+    const uint32_t nl = lcount;
+    if (threadIdx.x == 0) base = nl ? atomicAdd(n_out, nl) : 0u;
+    __syncthreads();
+    const uint32_t o = base;
+    for (uint32_t i = threadIdx.x; i < nl; i += kBlock) {
+      member[o + i] = sm[i];
+      actor[o + i] = sa[i];
+      value[o + i] = sv[i];
+    }
+    __syncthreads();  // the staging is reused by the next sub-range
   }
   mx = wave_max64(mx);
   if ((threadIdx.x & 63) == 0) lmax[threadIdx.x >> 6] = mx;
   __syncthreads();
   if (threadIdx.x == 0) {
-    unsigned long long m = 0;
-    for (int w = 0; w < kBlock / 64; w++) m = lmax[w] > m ? lmax[w] : m;
-    bmax[blockIdx.x] = m;
+    unsigned long long mm = 0;
+    for (int w = 0; w < kBlock / 64; w++) mm = lmax[w] > mm ? lmax[w] : mm;
+    bmax[blockIdx.x] = mm;
   }
 }
 
