@@ -1410,16 +1410,23 @@ hipError_t launch_ds_set3(hipStream_t s, uint32_t* p0, uint32_t v0, uint32_t* p1
   return hipGetLastError();
 }
 
+// CE_DS_DECODE_LDS=bytes: unused LDS per decode block, capping the blocks a CU holds (the lanes'
+// plaintext lines then stay in L2 between a lane's window loads)
+static size_t decode_lds() {
+  static const size_t v = getenv("CE_DS_DECODE_LDS") ? (size_t)atol(getenv("CE_DS_DECODE_LDS")) : 0;
+  return v;
+}
+
 hipError_t launch_ds_count(hipStream_t s, const DsDecodeArgs& a) {
   if (a.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ds_count, dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL(k_ds_count, dim3(blocks_for(a.n)), dim3(kBlock), decode_lds(), s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_ds_emit(hipStream_t s, const DsDecodeArgs& a) {
   if (a.n == 0) return hipSuccess;
   if (a.tile.npad) {
-    hipLaunchKernelGGL(k_ds_emit<true>, dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(k_ds_emit<true>, dim3(blocks_for(a.n)), dim3(kBlock), decode_lds(), s, a);
     hipLaunchKernelGGL(k_ds_untile, dim3((a.n + 63) / 64, 9), dim3(kBlock), 0, s, a);
   } else {
     hipLaunchKernelGGL(k_ds_emit<false>, dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
