@@ -156,7 +156,8 @@ struct DsPartArgs {
   DsKillSrc ks[2];              // the batch's removals, the deferred set
   uint32_t ba, bk0, bk;         // add blocks, blocks of ks[0], all removal blocks
   uint32_t parts;               // (pmask + 1) >> kDsPartBits
-  uint32_t chunk;               // adds / removals per K1 / K3 block (kDsPartChunk)
+  uint32_t chunk;               // adds per K1 / K3 block (kDsPartChunk)
+  uint32_t kchunk;              // removals per K1 / K3 block (fewer items: smaller blocks' worth)
   uint32_t* hist;               // parts * (ba + bk) + 1 counts: [p * ba + b], then [parts * ba + p * bk + b]
   const uint32_t* off;          // exclusive scan of hist
   unsigned long long* items;    // (key, value) pairs, partition-major: adds, then removals

@@ -661,8 +661,8 @@ __global__ void __launch_bounds__(kPartThreads) k_ds_part_kills(DsPartArgs a) {
   __syncthreads();
   const uint32_t b = blockIdx.x;
   const DsKillSrc& x = a.ks[b < a.bk0 ? 0 : 1];
-  const uint32_t r0 = (b < a.bk0 ? b : b - a.bk0) * a.chunk;
-  const uint32_t r1 = min(x.n, r0 + a.chunk);
+  const uint32_t r0 = (b < a.bk0 ? b : b - a.bk0) * a.kchunk;
+  const uint32_t r1 = min(x.n, r0 + a.kchunk);
   for (uint32_t rb = r0 + threadIdx.x; rb < r1; rb += kPartThreads * kPartBatch) {
     uint32_t c0[kPartBatch], c1[kPartBatch], j0[kPartBatch], j1[kPartBatch];
     unsigned long long m[kPartBatch], g[kPartBatch];
@@ -742,8 +742,8 @@ __global__ void __launch_bounds__(kPartThreads) k_ds_part_scatter(DsPartArgs a) 
     return;
   }
   const DsKillSrc& x = a.ks[kb < a.bk0 ? 0 : 1];
-  const uint32_t r0 = (kb < a.bk0 ? kb : kb - a.bk0) * a.chunk;
-  const uint32_t r1 = min(x.n, r0 + a.chunk);
+  const uint32_t r0 = (kb < a.bk0 ? kb : kb - a.bk0) * a.kchunk;
+  const uint32_t r1 = min(x.n, r0 + a.kchunk);
   for (uint32_t r = r0 + threadIdx.x; r < r1; r += kPartThreads) {
     const uint32_t c0 = x.cbeg[r], c1 = x.cbeg[r + 1];
     if (c0 == c1) continue;

@@ -593,9 +593,10 @@ int orswot_fold(ce_core* c, const Counts& k, uint64_t kill_bound) {
   static const uint32_t chunk = getenv("CE_DS_PART_CHUNK") ? (uint32_t)std::max(1024, atoi(getenv("CE_DS_PART_CHUNK")))
                                                           : kDsPartChunk;
   pa.chunk = chunk;
+  pa.kchunk = std::max<uint32_t>(1024, chunk / 4);  // removals are ~1/4 of C3's ops: as many blocks
   pa.ba = (uint32_t)((na + chunk - 1) / chunk);
-  pa.bk0 = (uint32_t)((nr + chunk - 1) / chunk);
-  pa.bk = pa.bk0 + (uint32_t)((n0 + chunk - 1) / chunk);
+  pa.bk0 = (uint32_t)((nr + pa.kchunk - 1) / pa.kchunk);
+  pa.bk = pa.bk0 + (uint32_t)((n0 + pa.kchunk - 1) / pa.kchunk);
   const uint64_t kill_items = kill_bound == ~0ull ? ~0ull : kill_bound + kb0;
   const bool part = !getenv("CE_DS_FOLD_GLOBAL") && pa.parts >= 1 && pa.parts <= kDsPartMaxParts &&
                     kill_items <= 4 * (k.v[kCntRmM] + k.v[kCntRmC] + kb0) + (1ull << 20) &&
