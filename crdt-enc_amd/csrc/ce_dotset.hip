@@ -155,9 +155,25 @@ struct ActorCache {
   uint32_t id = kDsNoActor;
 };
 
+// ST (staged): the file's bytes sit in LDS (k_ds_count / k_ds_emit stage a wave's files); every
+// LDS access stays dword-aligned -- aligned dword loads, bytes shifted into place with alignbyte
+template <bool ST>
+__device__ __forceinline__ uint4 load16(const uint8_t* q) {
+  if (!ST) return *reinterpret_cast<const uint4*>(q);  // unaligned 16 B inside the plaintext
+  const uintptr_t x = reinterpret_cast<uintptr_t>(q);
+  const uint32_t* b = reinterpret_cast<const uint32_t*>(x & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(x & 3);
+  uint32_t d[5];
+#pragma unroll
+  for (int k = 0; k < 5; k++) d[k] = b[k];
+  return make_uint4(__builtin_amdgcn_alignbyte(d[1], d[0], sh), __builtin_amdgcn_alignbyte(d[2], d[1], sh),
+                    __builtin_amdgcn_alignbyte(d[3], d[2], sh), __builtin_amdgcn_alignbyte(d[4], d[3], sh));
+}
+
+template <bool ST = false>
 __device__ __forceinline__ uint32_t lookup_actor(const DsDecodeArgs& a, const uint8_t* u,
                                                  ActorCache* cache = nullptr) {
-  const uint4 k = *reinterpret_cast<const uint4*>(u);  // unaligned 16 B inside the plaintext
+  const uint4 k = load16<ST>(u);
   if (cache && cache->id != kDsNoActor && k.x == cache->k.x && k.y == cache->k.y &&
       k.z == cache->k.z && k.w == cache->k.w)
     return cache->id;
@@ -177,7 +193,9 @@ __device__ __forceinline__ uint32_t lookup_actor(const DsDecodeArgs& a, const ui
   return kDsNoActor;
 }
 
-struct CountSink {
+template <bool ST = false>
+struct CountSinkT {
+  static constexpr bool kStaged = ST;
   uint32_t c[kCntN] = {0, 0, 0, 0, 0};
   __device__ void add_begin() { c[kCntAdd]++; }
   __device__ void add_dot(uint64_t, uint64_t) {}
@@ -197,8 +215,9 @@ struct CountSink {
 // instead -- entry k of file i at tile.col[c][k * npad + i] -- so a wave's 64 files write 64
 // consecutive words per store when their files share a layout (k_ds_untile then writes the CSR
 // columns in order); the values (ids, counters, CSR offsets) are the same.
-template <bool TILE>
+template <bool TILE, bool ST = false>
 struct EmitSinkT {
+  static constexpr bool kStaged = ST;
   const DsDecodeArgs* a;
   const uint8_t* p;
   uint32_t ia, iam, ir, irc, irm;
@@ -211,7 +230,7 @@ struct EmitSinkT {
   }
   __device__ void add_begin() { put(a->ops.add_mbeg, 2, ia, ia0, iam); }
   __device__ void add_dot(uint64_t off, uint64_t c) {
-    put(a->ops.add_actor, 0, ia, ia0, lookup_actor(*a, p + off, &cache));
+    put(a->ops.add_actor, 0, ia, ia0, lookup_actor<ST>(*a, p + off, &cache));
     put(a->ops.add_ctr, 1, ia, ia0, (unsigned long long)c);
   }
   __device__ void add_member(uint64_t m) { put(a->ops.add_mem, 3, iam, iam0, (unsigned long long)m); iam++; }
@@ -221,7 +240,7 @@ struct EmitSinkT {
     put(a->ops.rm_mbeg, 5, ir, ir0, irm);
   }
   __device__ void rm_dot(uint64_t off, uint64_t c) {
-    put(a->ops.rmc_actor, 6, irc, irc0, lookup_actor(*a, p + off, &cache));
+    put(a->ops.rmc_actor, 6, irc, irc0, lookup_actor<ST>(*a, p + off, &cache));
     put(a->ops.rmc_ctr, 7, irc, irc0, (unsigned long long)c);
     irc++;
   }
@@ -229,7 +248,7 @@ struct EmitSinkT {
   __device__ void rm_end() { ir++; }
   __device__ void put_begin() { a->ops.rm_cbeg[ir] = irc; }
   __device__ void put_dot(uint64_t off, uint64_t c) {
-    a->ops.rmc_actor[irc] = lookup_actor(*a, p + off, &cache);
+    a->ops.rmc_actor[irc] = lookup_actor<ST>(*a, p + off, &cache);
     a->ops.rmc_ctr[irc] = c;
     irc++;
   }
@@ -248,9 +267,21 @@ struct EmitSinkT {
 // -- other widths, more members or clock entries, reordered or extra fields -- is parsed by the
 // grammar from the same op on (no sink call is made before an op is fully proven), so the sink
 // sees exactly the calls ds_parse_orswot_ops would make.
+template <bool ST = false>
 struct Win64 {
   uint32_t w[16];
   __device__ __forceinline__ explicit Win64(const uint8_t* q) {
+    if (ST) {  // staged in LDS: 17 aligned dwords, shifted (load16)
+      const uintptr_t x = reinterpret_cast<uintptr_t>(q);
+      const uint32_t* b = reinterpret_cast<const uint32_t*>(x & ~(uintptr_t)3);
+      const uint32_t sh = (uint32_t)(x & 3);
+      uint32_t d[17];
+#pragma unroll
+      for (int k = 0; k < 17; k++) d[k] = b[k];
+#pragma unroll
+      for (int k = 0; k < 16; k++) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+      return;
+    }
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const uint4 v = *reinterpret_cast<const uint4*>(q + 16 * k);  // unaligned
@@ -277,8 +308,9 @@ struct Win64 {
 };
 
 // "a7 members 91 <uint>" at q: the one-member array; returns bytes consumed, 0 if not that form
+template <bool ST>
 __device__ __forceinline__ uint32_t fast_members1(const uint8_t* q, uint64_t* m) {
-  const Win64 v(q);
+  const Win64<ST> v(q);
   if (v.word(0) != 0x6d656da7u || v.word(4) != 0x73726562u || v.byte(8) != 0x91u) return 0;
   uint32_t l;
   *m = v.uint_at(9, &l);
@@ -287,9 +319,10 @@ __device__ __forceinline__ uint32_t fast_members1(const uint8_t* q, uint64_t* m)
 
 template <typename S>
 __device__ __forceinline__ bool fast_orswot_op(const uint8_t* p, uint64_t n, uint64_t& i, S& sink) {
+  constexpr bool ST = S::kStaged;
   if (n - i < 32) return false;
   const uint8_t* q = p + i;
-  const Win64 v(q);
+  const Win64<ST> v(q);
   uint32_t l, lm;
   uint64_t ctr, mem;
   if (v.w[0] == 0x6441a381u && v.w[1] == 0x64a38264u && v.w[2] == 0xa582746fu &&
@@ -297,7 +330,7 @@ __device__ __forceinline__ bool fast_orswot_op(const uint8_t* p, uint64_t n, uin
       v.word(39) == 0x7265746eu) {  // Add
     ctr = v.uint_at(43, &l);
     if (!l) return false;
-    lm = fast_members1(q + 43 + l, &mem);
+    lm = fast_members1<ST>(q + 43 + l, &mem);
     if (!lm || 43ull + l + lm > n - i) return false;
     sink.add_begin();
     sink.add_dot(i + 19, ctr);
@@ -310,7 +343,7 @@ __device__ __forceinline__ bool fast_orswot_op(const uint8_t* p, uint64_t n, uin
       v.w[3] == 0x746f64a4u && v.w[4] == 0x10c48173u) {  // Rm with a one-entry clock
     ctr = v.uint_at(36, &l);
     if (!l) return false;
-    lm = fast_members1(q + 36 + l, &mem);
+    lm = fast_members1<ST>(q + 36 + l, &mem);
     if (!lm || 36ull + l + lm > n - i) return false;
     sink.rm_begin();
     sink.rm_dot(i + 20, ctr);
@@ -340,47 +373,115 @@ __device__ int parse_file(int kind, const uint8_t* p, uint64_t n, S& sink) {
   return kind == kDsOrswot ? parse_orswot_fast(p, n, sink) : ds_parse_mvreg_ops(p, n, sink);
 }
 
+// ---- staged decode: a wave's 64 files copied into LDS first ---------------------------------
+// A lane parses its file op by op, each op's window load waiting on the previous op's length: a
+// chain of ~32 dependent loads per file.  From HBM / L2 each link costs a round trip (and the
+// lanes' scattered 64-byte windows re-fetched every line ~5x at C3); staged, a wave copies its
+// files' byte range [lo, hi) with coalesced 16-byte loads (eight per lane in flight) and the chain
+// runs on LDS.  A wave whose range exceeds kStageWave, or a lane whose file lies outside it,
+// reads HBM as before.
+constexpr uint32_t kStageWave = 39 * 1024;               // bytes per wave (4 waves: 156 KB per CU)
+constexpr uint32_t kStageLds = (kBlock / 64) * kStageWave;
+
+__device__ __forceinline__ unsigned long long wave_min64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long y = ((unsigned long long)(uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o) << 32) |
+                                 (uint32_t)__shfl_xor((int)(uint32_t)v, o);
+    v = y < v ? y : v;
+  }
+  return v;
+}
+
+// this lane's file bytes in the wave's LDS region, or nullptr (read from HBM).  Every lane of the
+// block calls it (the copy is followed by a block barrier).
+__device__ const uint8_t* stage_files(const DsDecodeArgs& a, uint32_t i, bool act, uint8_t* lds) {
+  const uint64_t off = act ? a.params[i].out_off : ~0ull;
+  const uint64_t end = act ? off + a.params[i].len : 0ull;
+  const uint64_t lo = wave_min64(off) & ~15ull, hi = wave_max64(end);
+  uint8_t* region = lds + (threadIdx.x >> 6) * kStageWave;
+  // the windows read up to 64 bytes past a file's end (the buffer's slack) plus the aligned
+  // loads' 4: the region holds hi - lo + 64 + 16 bytes; the copy stops inside the slack (whole
+  // 16-byte vectors only: the last few slack bytes' values are never used)
+  const bool ok = hi > lo && hi - lo + 64 + 16 <= kStageWave;
+  if (ok) {
+    const uint4* src = reinterpret_cast<const uint4*>(a.pt + lo);
+    uint4* dst = reinterpret_cast<uint4*>(region);
+    const uint32_t nv = (uint32_t)((hi + 64 - lo) >> 4), lane = threadIdx.x & 63;
+    for (uint32_t v0 = lane; v0 < nv; v0 += 64 * 8) {
+      uint4 t[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) t[q] = v0 + 64 * q < nv ? src[v0 + 64 * q] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 8; q++)
+        if (v0 + 64 * q < nv) dst[v0 + 64 * q] = t[q];
+    }
+  }
+  __syncthreads();
+  return ok && act ? region + (off - lo) : nullptr;
+}
+
+template <bool ST>
+__device__ __forceinline__ int32_t count_file(const DsDecodeArgs& a, const uint8_t* p, uint32_t len,
+                                              CountSinkT<ST>& cs) {
+  if (len < 16) return CE_ERR_PT_LEN;  // VersionBytesRef::deserialize (lib.rs:504)
+  bool ok = false;
+  for (uint32_t v = 0; v < a.n_supported && !ok; v++) {
+    bool eq = true;
+    for (int b = 0; b < 16; b++) eq = eq && p[b] == a.supported[16 * v + b];
+    ok = eq;
+  }
+  if (!ok) return CE_ERR_PT_VERSION;  // ensure_versions (lib.rs:505)
+  const int r = parse_file(a.kind, p + 16, len - 16, cs);  // from_slice (lib.rs:507)
+  if (r == kDsErr) {
+    atomicAdd(a.counters + 0, 1u);
+    return CE_ERR_DECODE;
+  }
+  if (r == kDsHost) {
+    atomicAdd(a.counters + 1, 1u);
+    return kStatusHostDecode;
+  }
+  return CE_OK;
+}
+
+template <bool STAGE>
 __global__ void __launch_bounds__(kBlock) k_ds_count(DsDecodeArgs a) {
+  extern __shared__ uint8_t stage_lds[];
   __shared__ uint32_t smax[kCntN];
   if (threadIdx.x < kCntN) smax[threadIdx.x] = 0;
   __syncthreads();
   uint32_t mx[kCntN];
 #pragma unroll
   for (int k = 0; k < kCntN; k++) mx[k] = 0;
-  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < a.n; i += gridDim.x * kBlock) {
-    CountSink cs;
-    int32_t st = a.status[i];
-    if (st == CE_OK) {
+  // (STAGE: the trip count is uniform over the block -- every lane reaches the barriers)
+  for (uint32_t i0 = blockIdx.x * kBlock; i0 < a.n; i0 += gridDim.x * kBlock) {
+    const uint32_t i = i0 + threadIdx.x;
+    const bool in = i < a.n;
+    int32_t st = in ? a.status[i] : CE_ERR_DECODE;
+    const uint8_t* sp = STAGE ? stage_files(a, i, in && st == CE_OK, stage_lds) : nullptr;
+    uint32_t c[kCntN] = {0, 0, 0, 0, 0};
+    if (in && st == CE_OK) {
       const uint32_t len = a.params[i].len;
-      const uint8_t* p = a.pt + a.params[i].out_off;
-      if (len < 16) {
-        st = CE_ERR_PT_LEN;  // VersionBytesRef::deserialize (lib.rs:504)
+      if (STAGE && sp) {
+        CountSinkT<true> cs;
+        st = count_file(a, sp, len, cs);
+#pragma unroll
+        for (int k = 0; k < kCntN; k++) c[k] = cs.c[k];
       } else {
-        bool ok = false;
-        for (uint32_t v = 0; v < a.n_supported && !ok; v++) {
-          bool eq = true;
-          for (int b = 0; b < 16; b++) eq = eq && p[b] == a.supported[16 * v + b];
-          ok = eq;
-        }
-        if (!ok) {
-          st = CE_ERR_PT_VERSION;  // ensure_versions (lib.rs:505)
-        } else {
-          const int r = parse_file(a.kind, p + 16, len - 16, cs);  // from_slice (lib.rs:507)
-          if (r == kDsErr) {
-            st = CE_ERR_DECODE;
-            atomicAdd(a.counters + 0, 1u);
-          } else if (r == kDsHost) {
-            st = kStatusHostDecode;
-            atomicAdd(a.counters + 1, 1u);
-          }
-        }
+        CountSinkT<false> cs;
+        st = count_file(a, a.pt + a.params[i].out_off, len, cs);
+#pragma unroll
+        for (int k = 0; k < kCntN; k++) c[k] = cs.c[k];
       }
       if (st != CE_OK) a.status[i] = st;
     }
-    const bool keep = st == CE_OK && a.apply[i];
-    for (int k = 0; k < kCntN; k++) a.cnt[(size_t)k * a.n + i] = keep ? cs.c[k] : 0u;
+    if (in) {
+      const bool keep = st == CE_OK && a.apply[i];
+      for (int k = 0; k < kCntN; k++) a.cnt[(size_t)k * a.n + i] = keep ? c[k] : 0u;
 #pragma unroll
-    for (int k = 0; k < kCntN; k++) mx[k] = max(mx[k], keep ? cs.c[k] : 0u);
+      for (int k = 0; k < kCntN; k++) mx[k] = max(mx[k], keep ? c[k] : 0u);
+    }
+    if (STAGE) __syncthreads();  // the next trip's staging overwrites the region
   }
   // the largest per-file count of each column (counters[8 + k]): the tiled emit's row count;
   // reduced per wave, then per block in LDS, so each block adds one global atomic per column
@@ -395,25 +496,36 @@ __global__ void __launch_bounds__(kBlock) k_ds_count(DsDecodeArgs a) {
   if (threadIdx.x < kCntN && smax[threadIdx.x]) atomicMax(a.counters + 8 + threadIdx.x, smax[threadIdx.x]);
 }
 
-template <bool TILE>
+template <bool TILE, bool ST>
+__device__ __forceinline__ void emit_file(const DsDecodeArgs& a, uint32_t i, const uint8_t* p) {
+  const uint32_t len = a.params[i].len;
+  EmitSinkT<TILE, ST> es;
+  es.a = &a;
+  es.p = p;
+  // the bases are one exclusive scan over all kCntN columns back to back: column k's base is
+  // its entry minus the column's first (u32 arithmetic: exact while a column's total < 2^32)
+  auto base = [&](int k) { return a.cnt[(size_t)k * a.n + i] - a.cnt[(size_t)k * a.n]; };
+  es.ia = es.ia0 = a.base_off[kCntAdd] + base(kCntAdd);
+  es.iam = es.iam0 = a.base_off[kCntAddM] + base(kCntAddM);
+  es.ir = es.ir0 = a.base_off[kCntRm] + base(kCntRm);
+  es.irc = es.irc0 = a.base_off[kCntRmC] + base(kCntRmC);
+  es.irm = es.irm0 = a.base_off[kCntRmM] + base(kCntRmM);
+  es.file = i;
+  parse_file(a.kind, p, len - 16, es);
+}
+
+template <bool TILE, bool STAGE>
 __global__ void __launch_bounds__(kBlock) k_ds_emit(DsDecodeArgs a) {
-  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < a.n; i += gridDim.x * kBlock) {
-    if (a.status[i] != CE_OK || !a.apply[i]) continue;
-    const uint32_t len = a.params[i].len;
-    const uint8_t* p = a.pt + a.params[i].out_off + 16;
-    EmitSinkT<TILE> es;
-    es.a = &a;
-    es.p = p;
-    // the bases are one exclusive scan over all kCntN columns back to back: column k's base is
-    // its entry minus the column's first (u32 arithmetic: exact while a column's total < 2^32)
-    auto base = [&](int k) { return a.cnt[(size_t)k * a.n + i] - a.cnt[(size_t)k * a.n]; };
-    es.ia = es.ia0 = a.base_off[kCntAdd] + base(kCntAdd);
-    es.iam = es.iam0 = a.base_off[kCntAddM] + base(kCntAddM);
-    es.ir = es.ir0 = a.base_off[kCntRm] + base(kCntRm);
-    es.irc = es.irc0 = a.base_off[kCntRmC] + base(kCntRmC);
-    es.irm = es.irm0 = a.base_off[kCntRmM] + base(kCntRmM);
-    es.file = i;
-    parse_file(a.kind, p, len - 16, es);
+  extern __shared__ uint8_t stage_lds[];
+  for (uint32_t i0 = blockIdx.x * kBlock; i0 < a.n; i0 += gridDim.x * kBlock) {
+    const uint32_t i = i0 + threadIdx.x;
+    const bool act = i < a.n && a.status[i] == CE_OK && a.apply[i];
+    const uint8_t* sp = STAGE ? stage_files(a, i, act, stage_lds) : nullptr;
+    if (act) {
+      if (STAGE && sp) emit_file<TILE, true>(a, i, sp + 16);
+      else emit_file<TILE, false>(a, i, a.pt + a.params[i].out_off + 16);
+    }
+    if (STAGE) __syncthreads();
   }
 }
 
@@ -1417,19 +1529,28 @@ static size_t decode_lds() {
   return v;
 }
 
+// CE_DS_DECODE_STAGE=1: the staged decode (a wave's files in LDS)
+static bool decode_stage() {
+  const char* v = getenv("CE_DS_DECODE_STAGE");  // (read per launch: the tests flip it)
+  return v && atoi(v) != 0;
+}
+
 hipError_t launch_ds_count(hipStream_t s, const DsDecodeArgs& a) {
   if (a.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ds_count, dim3(blocks_for(a.n)), dim3(kBlock), decode_lds(), s, a);
+  if (decode_stage()) hipLaunchKernelGGL(k_ds_count<true>, dim3(blocks_for(a.n)), dim3(kBlock), kStageLds, s, a);
+  else hipLaunchKernelGGL(k_ds_count<false>, dim3(blocks_for(a.n)), dim3(kBlock), decode_lds(), s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_ds_emit(hipStream_t s, const DsDecodeArgs& a) {
   if (a.n == 0) return hipSuccess;
   if (a.tile.npad) {
-    hipLaunchKernelGGL(k_ds_emit<true>, dim3(blocks_for(a.n)), dim3(kBlock), decode_lds(), s, a);
+    if (decode_stage()) hipLaunchKernelGGL((k_ds_emit<true, true>), dim3(blocks_for(a.n)), dim3(kBlock), kStageLds, s, a);
+    else hipLaunchKernelGGL((k_ds_emit<true, false>), dim3(blocks_for(a.n)), dim3(kBlock), decode_lds(), s, a);
     hipLaunchKernelGGL(k_ds_untile, dim3((a.n + 63) / 64, 9), dim3(kBlock), 0, s, a);
   } else {
-    hipLaunchKernelGGL(k_ds_emit<false>, dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
+    if (decode_stage()) hipLaunchKernelGGL((k_ds_emit<false, true>), dim3(blocks_for(a.n)), dim3(kBlock), kStageLds, s, a);
+    else hipLaunchKernelGGL((k_ds_emit<false, false>), dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
   }
   return hipGetLastError();
 }

@@ -911,3 +911,30 @@ def test_orswot_serializer_one_sort_equals_two(ctx, n_members):
         finally:
             os.environ.pop("CE_SER_TWO_SORTS", None)
     assert got[0] == got[1] == want
+
+
+@pytest.mark.parametrize("kind", ["orswot", "mvreg"])
+@pytest.mark.parametrize("adversarial", [False, True])
+def test_staged_decode_equals_global(ctx, kind, adversarial):
+    """The staged op decode (CE_DS_DECODE_STAGE=1: a wave's files copied into LDS, the parse
+    reading dword-aligned LDS words) == the HBM-reading decode == the oracle: statuses and state,
+    on canonical and adversarial files (ragged sizes, non-canonical forms, multi-entry clocks)."""
+    rng = random.Random(1313 + adversarial + (kind == "mvreg") * 7)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 9)
+    files = gen(kind, rng, actors, 5, 12, 300, adversarial)
+    acts, clears, fa, fv = G.batch(files, kind, APP)
+    sealed = seal_files(ctx, key, clears)
+    oc = C.Core(kind)
+    want = oc.read_remote_ops(key, [APP], sealed, [acts[i] for i in fa], fv)
+    got = {}
+    for staged in (False, True):
+        os.environ["CE_DS_DECODE_STAGE"] = "1" if staged else "0"
+        try:
+            core = new_core(ctx, kind, key)
+            got[staged] = (core.ingest_ops(sealed, acts, fa, fv), core.state_bytes())
+            core.close()
+        finally:
+            os.environ.pop("CE_DS_DECODE_STAGE", None)
+    assert got[False] == got[True]
+    assert got[True][0] == want and got[True][1] == oc.serialize()
