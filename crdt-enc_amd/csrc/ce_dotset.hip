@@ -1522,13 +1522,6 @@ hipError_t launch_ds_set3(hipStream_t s, uint32_t* p0, uint32_t v0, uint32_t* p1
   return hipGetLastError();
 }
 
-// CE_DS_DECODE_LDS=bytes: unused LDS per decode block, capping the blocks a CU holds (the lanes'
-// plaintext lines then stay in L2 between a lane's window loads)
-static size_t decode_lds() {
-  static const size_t v = getenv("CE_DS_DECODE_LDS") ? (size_t)atol(getenv("CE_DS_DECODE_LDS")) : 0;
-  return v;
-}
-
 // CE_DS_DECODE_STAGE=1: the staged decode (a wave's files in LDS)
 static bool decode_stage() {
   const char* v = getenv("CE_DS_DECODE_STAGE");  // (read per launch: the tests flip it)
@@ -1538,7 +1531,7 @@ static bool decode_stage() {
 hipError_t launch_ds_count(hipStream_t s, const DsDecodeArgs& a) {
   if (a.n == 0) return hipSuccess;
   if (decode_stage()) hipLaunchKernelGGL(k_ds_count<true>, dim3(blocks_for(a.n)), dim3(kBlock), kStageLds, s, a);
-  else hipLaunchKernelGGL(k_ds_count<false>, dim3(blocks_for(a.n)), dim3(kBlock), decode_lds(), s, a);
+  else hipLaunchKernelGGL(k_ds_count<false>, dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 
@@ -1546,7 +1539,7 @@ hipError_t launch_ds_emit(hipStream_t s, const DsDecodeArgs& a) {
   if (a.n == 0) return hipSuccess;
   if (a.tile.npad) {
     if (decode_stage()) hipLaunchKernelGGL((k_ds_emit<true, true>), dim3(blocks_for(a.n)), dim3(kBlock), kStageLds, s, a);
-    else hipLaunchKernelGGL((k_ds_emit<true, false>), dim3(blocks_for(a.n)), dim3(kBlock), decode_lds(), s, a);
+    else hipLaunchKernelGGL((k_ds_emit<true, false>), dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(k_ds_untile, dim3((a.n + 63) / 64, 9), dim3(kBlock), 0, s, a);
   } else {
     if (decode_stage()) hipLaunchKernelGGL((k_ds_emit<false, true>), dim3(blocks_for(a.n)), dim3(kBlock), kStageLds, s, a);
