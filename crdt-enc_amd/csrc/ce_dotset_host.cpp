@@ -67,7 +67,7 @@ struct DsState {
   // bases, members, sorted members [0..6]
   // and emitted (member, actor id, value) columns [7..9]), pinned staging for its downloads
   std::vector<std::array<DevBuf, 10>> rd;
-  DevBuf rd_tmp, rd_misc, ser[16], uuid_of_id, rank_of_id, rd_oclocks, cnt_tot, rd_args_d, rd_chunks, rd_gather;
+  DevBuf rd_tmp, rd_misc, ser[16], uuid_of_id, rank_of_id, id_of_rank, rd_oclocks, cnt_tot, rd_args_d, rd_chunks, rd_gather;
   HostBuf rd_host, rd_small, rd_clock, rd_args_h, h_clock;
   uint64_t uuid_ids = ~0ull;  // id count uuid_of_id / rank_of_id (and id_rank / rank_id) were built for
   std::vector<uint32_t> id_rank, rank_id;  // UUID-order rank of each stable id, and its inverse
@@ -2085,8 +2085,10 @@ static int ds_serialize_dev(ce_core* c, ce_ctx* x, const uint8_t* outer, const u
     std::sort(d->rank_id.begin(), d->rank_id.end(), [&](uint32_t a, uint32_t b) { return c->id_actor[a] < c->id_actor[b]; });
     for (uint32_t i = 0; i < na; i++) d->id_rank[d->rank_id[i]] = i;
     if ((e = d->uuid_of_id.reserve(u.size())) || (e = d->rank_of_id.reserve(4ull * d->id_rank.size())) ||
+        (e = d->id_of_rank.reserve(4ull * d->rank_id.size() + 64)) ||
         (e = hipMemcpyAsync(d->uuid_of_id.p, u.data(), u.size(), hipMemcpyHostToDevice, s)) ||
         (e = hipMemcpyAsync(d->rank_of_id.p, d->id_rank.data(), 4ull * d->id_rank.size(), hipMemcpyHostToDevice, s)) ||
+        (na && (e = hipMemcpyAsync(d->id_of_rank.p, d->rank_id.data(), 4ull * na, hipMemcpyHostToDevice, s))) ||
         (e = stream_wait(s)))
       return x->hip_fail(e, "actor ranks");
     d->uuid_ids = na;
@@ -2121,6 +2123,7 @@ static int ds_serialize_dev(ce_core* c, ce_ctx* x, const uint8_t* outer, const u
   sc.actor_in = d->col[1].as<uint32_t>();
   sc.value_in = d->col[2].as<unsigned long long>();
   sc.rank_of_id = d->rank_of_id.as<uint32_t>();
+  sc.id_of_rank = d->id_of_rank.as<uint32_t>();
   sc.rank_bits = bits_for(na);
   sc.member_bits = max_member ? 64 - __builtin_clzll(max_member) : 1;  // radix passes over those bits only
   sc.k32a = d->ser[0].as<uint32_t>();

@@ -37,6 +37,7 @@ struct OrswotSerScratch {
   const uint32_t* actor_in;
   const unsigned long long* value_in;
   const uint32_t* rank_of_id;            // UUID byte order rank of each stable actor id
+  const uint32_t* id_of_rank;            // its inverse
   int rank_bits;
   int member_bits;                       // significant bits of the largest member (<= 64)
   uint32_t *k32a, *k32b, *p32a, *p32b;   // n each

@@ -84,27 +84,24 @@ __global__ void k_ser_gather_member(const uint32_t* perm, const unsigned long lo
   for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < n; i += gridDim.x * kB) member_out[i] = member_in[perm[i]];
 }
 
-// one sort when (member, rank) packs into K: key = member << rank_bits | rank, perm = iota
-// ((member, actor) pairs are unique, so no two keys tie)
+// one sort when (member, rank) packs into K: key = member << rank_bits | rank ((member, actor)
+// pairs are unique, so no two keys tie); the values ride through the sort itself
 template <typename K>
 __global__ void k_ser_key(const uint32_t* actor, const uint32_t* rank_of_id, const unsigned long long* member,
-                          int rank_bits, K* key, uint32_t* perm, uint32_t n) {
-  for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < n; i += gridDim.x * kB) {
+                          int rank_bits, K* key, uint32_t n) {
+  for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < n; i += gridDim.x * kB)
     key[i] = ((K)member[i] << rank_bits) | (K)rank_of_id[actor[i]];
-    perm[i] = i;
-  }
 }
 
-// member from the sorted key (member_out may alias key), actor / value gathered
+// member and actor id back out of the sorted key (member_out may alias key): no gather
 template <typename K>
-__global__ void k_ser_gather3(const uint32_t* perm, const K* key, int rank_bits, const uint32_t* actor_in,
-                              const unsigned long long* value_in, unsigned long long* member_out,
-                              uint32_t* actor_out, unsigned long long* value_out, uint32_t n) {
+__global__ void k_ser_unpack(const K* key, int rank_bits, const uint32_t* id_of_rank, unsigned long long* member_out,
+                             uint32_t* actor_out, uint32_t n) {
+  const K mask = ((K)1 << rank_bits) - 1;
   for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < n; i += gridDim.x * kB) {
-    const uint32_t j = perm[i];
-    member_out[i] = (unsigned long long)(key[i] >> rank_bits);
-    actor_out[i] = actor_in[j];
-    value_out[i] = value_in[j];
+    const K k = key[i];
+    actor_out[i] = id_of_rank[(uint32_t)(k & mask)];
+    member_out[i] = (unsigned long long)(k >> rank_bits);
   }
 }
 
@@ -499,19 +496,20 @@ hipError_t launch_orswot_ser_sort(hipStream_t s, OrswotSerScratch& sc, uint32_t 
     size_t tb = sc.tmp_bytes;
     if (kb <= 32) {
       hipLaunchKernelGGL(k_ser_key<uint32_t>, dim3(nblk(n)), dim3(kB), 0, s, sc.actor_in, sc.rank_of_id, sc.member_in,
-                         sc.rank_bits, sc.k32a, sc.p32a, n);
-      if ((e = hipcub::DeviceRadixSort::SortPairs(sc.tmp, tb, sc.k32a, sc.k32b, sc.p32a, sc.p32b, (int)n, 0, kb, s)))
+                         sc.rank_bits, sc.k32a, n);
+      if ((e = hipcub::DeviceRadixSort::SortPairs(sc.tmp, tb, sc.k32a, sc.k32b, sc.value_in, sc.value_sorted, (int)n,
+                                                   0, kb, s)))
         return e;
-      hipLaunchKernelGGL(k_ser_gather3<uint32_t>, dim3(nblk(n)), dim3(kB), 0, s, sc.p32b, sc.k32b, sc.rank_bits,
-                         sc.actor_in, sc.value_in, sc.member_sorted, sc.actor_sorted, sc.value_sorted, n);
+      hipLaunchKernelGGL(k_ser_unpack<uint32_t>, dim3(nblk(n)), dim3(kB), 0, s, sc.k32b, sc.rank_bits, sc.id_of_rank,
+                         sc.member_sorted, sc.actor_sorted, n);
     } else {
       hipLaunchKernelGGL(k_ser_key<unsigned long long>, dim3(nblk(n)), dim3(kB), 0, s, sc.actor_in, sc.rank_of_id,
-                         sc.member_in, sc.rank_bits, sc.k64a, sc.p32a, n);
-      if ((e = hipcub::DeviceRadixSort::SortPairs(sc.tmp, tb, sc.k64a, sc.member_sorted, sc.p32a, sc.p32b, (int)n, 0,
-                                                   kb, s)))
+                         sc.member_in, sc.rank_bits, sc.k64a, n);
+      if ((e = hipcub::DeviceRadixSort::SortPairs(sc.tmp, tb, sc.k64a, sc.member_sorted, sc.value_in, sc.value_sorted,
+                                                   (int)n, 0, kb, s)))
         return e;
-      hipLaunchKernelGGL(k_ser_gather3<unsigned long long>, dim3(nblk(n)), dim3(kB), 0, s, sc.p32b, sc.member_sorted,
-                         sc.rank_bits, sc.actor_in, sc.value_in, sc.member_sorted, sc.actor_sorted, sc.value_sorted, n);
+      hipLaunchKernelGGL(k_ser_unpack<unsigned long long>, dim3(nblk(n)), dim3(kB), 0, s, sc.member_sorted,
+                         sc.rank_bits, sc.id_of_rank, sc.member_sorted, sc.actor_sorted, n);
     }
   } else if (n) {
     size_t tb = sc.tmp_bytes;
@@ -580,7 +578,12 @@ static size_t ser_tmp_bytes_raw(uint32_t n) {
                                            (unsigned long long*)nullptr, (uint32_t*)nullptr,
                                            (uint32_t*)nullptr, (int)n, 0, 64);
   (void)ds_excl_sum_u32(nullptr, c, nullptr, nullptr, n, nullptr);
-  return std::max(a, std::max(b, c)) + 256;
+  size_t d = 0, e = 0;  // the packed-key sorts: u64 values
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, d, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                           (unsigned long long*)nullptr, (unsigned long long*)nullptr, (int)n, 0, 32);
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, e, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                           (unsigned long long*)nullptr, (unsigned long long*)nullptr, (int)n, 0, 64);
+  return std::max(std::max(a, b), std::max(c, std::max(d, e))) + 256;
 }
 
 size_t orswot_ser_tmp_bytes(uint32_t n) {
