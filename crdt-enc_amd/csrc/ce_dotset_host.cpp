@@ -46,6 +46,7 @@ struct DsState {
   uint64_t used_members = 0;  // used primary member slots at the last fold / k-way merge
   bool settle_members = false;
   bool primary_fixed = false;  // CE_DS_PRIMARY_SLOTS: never grown (the overflow path under test)
+  uint64_t head_hint = 1u << 18;  // state head prefix to download (ds_merge_states_device)
   uint64_t used_pairs = 0, live_pairs = 0;
   std::map<IdDots, std::set<uint64_t>> deferred;  // removal clock -> members (HashMap in crdts)
   // MVReg
@@ -1618,7 +1619,10 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
   ce_ctx* ctx = c->ctx;
   hipStream_t s = ctx->stream;
   const size_t n = off.size();
-  constexpr uint64_t kPrefix = 1u << 18;
+  // the head prefix per file: sized from the heads the last merge met (x 1.25, 16 KiB .. 256 KiB);
+  // a longer head is fetched file by file below, so the hint only saves bytes (C3: 8 x 256 KiB
+  // was a 51 us blit to host memory for ~20 KiB heads)
+  const uint64_t kPrefix = d->head_hint;
   if (int rs = ds_settle(c)) return rs;
   std::vector<DevState> ds(n);
   std::vector<std::vector<uint8_t>> host_pt(n);
@@ -1667,6 +1671,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     if ((rc = sync("state head"))) return rc;
     ph = std::make_unique<HostPhase>("  rd: heads parse");
     std::vector<size_t> dev;
+    uint64_t head_max = 0;
     for (size_t i = 0; i < n; i++) {
       if (st[i] != CE_OK) continue;
       DevState& x = ds[i];
@@ -1687,9 +1692,15 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
         continue;
       }
       x.body = body;
+      head_max = std::max<uint64_t>(head_max, body);
       x.n_entries = (uint32_t)ne;
       x.cap = (uint32_t)std::min<uint64_t>(ne + 65536, len[i] / 7 + 1);
       dev.push_back(i);
+    }
+    if (head_max) {
+      uint64_t h = 16384;
+      while (h < head_max + head_max / 4 + 1024 && h < (1u << 18)) h <<= 1;
+      d->head_hint = h;
     }
     // 2) the states' actors into the table (the emitted columns carry their ids), then the
     //    entry-head search over every file (it covers the deferred map too: its VClock keys
