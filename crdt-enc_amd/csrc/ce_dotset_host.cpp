@@ -47,6 +47,9 @@ struct DsState {
   bool settle_members = false;
   bool primary_fixed = false;  // CE_DS_PRIMARY_SLOTS: never grown (the overflow path under test)
   uint64_t head_hint = 1u << 18;  // state head prefix to download (ds_merge_states_device)
+  // add / kill / oth / hold hold values between a launch that sets them and the one that clears
+  // them (finalize, merge_finalize, kfinal): only then does tables_alloc need to clear them
+  bool scratch_dirty = true;
   uint64_t used_pairs = 0, live_pairs = 0;
   std::map<IdDots, std::set<uint64_t>> deferred;  // removal clock -> members (HashMap in crdts)
   // MVReg
@@ -112,6 +115,7 @@ int tables_alloc(ce_core* c, uint32_t cap, const FillRange* extra = nullptr) {
   ce_ctx* ctx = c->ctx;
   hipError_t e;
   const uint64_t mslots = (uint64_t)d->mcap_s + cap + 1;
+  void* const was[4] = {d->add.p, d->kill.p, d->oth.p, d->hold.p};
   if ((e = d->mkey.reserve(mslots * 8)) || (e = d->pkey.reserve(cap * 8ull)) ||
       (e = d->cur.reserve(cap * 8ull)) || (e = d->add.reserve(cap * 8ull)) ||
       (e = d->kill.reserve(cap * 8ull)) || (e = d->oth.reserve(cap * 8ull)) ||
@@ -123,14 +127,21 @@ int tables_alloc(ce_core* c, uint32_t cap, const FillRange* extra = nullptr) {
   fl.r[0] = {d->mkey.as<uint32_t>(), mslots * 2, 0xffffffffu};
   fl.r[1] = {d->pkey.as<uint32_t>(), cap * 2ull, 0xffffffffu};
   fl.r[2] = {d->cur.as<uint32_t>(), cap * 2ull, 0u};
-  fl.r[3] = {d->add.as<uint32_t>(), cap * 2ull, 0u};
-  fl.r[4] = {d->kill.as<uint32_t>(), cap * 2ull, 0u};
-  fl.r[5] = {d->oth.as<uint32_t>(), cap * 2ull, 0u};
-  fl.r[6] = {d->hold.as<uint32_t>(), cap * 2ull, 0u};
-  fl.r[7] = {d->live.as<uint32_t>(), 16, 0u};
-  fl.n = 8;
+  fl.r[3] = {d->live.as<uint32_t>(), 16, 0u};
+  fl.n = 4;
+  // the scratch columns are zero after every completed fold / merge: cleared only when new or
+  // when an operation stopped between setting and clearing them (~128 MB of fill at C3)
+  const bool moved = was[0] != d->add.p || was[1] != d->kill.p || was[2] != d->oth.p || was[3] != d->hold.p;
+  if (moved || d->scratch_dirty || getenv("CE_DS_CLEAR_ALL")) {
+    fl.r[fl.n++] = {d->add.as<uint32_t>(), cap * 2ull, 0u};
+    fl.r[fl.n++] = {d->kill.as<uint32_t>(), cap * 2ull, 0u};
+    fl.r[fl.n++] = {d->oth.as<uint32_t>(), cap * 2ull, 0u};
+    fl.r[fl.n++] = {d->hold.as<uint32_t>(), cap * 2ull, 0u};
+    c->path_counts["ds_clear_scratch"]++;
+  }
   if (extra) fl.r[fl.n++] = *extra;
   if ((e = launch_fill(ctx->stream, fl))) return ctx->hip_fail(e, "dot-set tables");
+  d->scratch_dirty = false;
   d->used_pairs = 0;
   d->live_pairs = 0;
   d->used_members = 0;
@@ -635,6 +646,7 @@ int orswot_fold(ce_core* c, const Counts& k, uint64_t kill_bound) {
     if ((e = d->deferred_flags.reserve(nr + n0 + 64))) return ctx->hip_fail(e, "finalize");
   } else {
     const int tp = ctx->tbegin("ds_add_pairs");
+    d->scratch_dirty = true;
     if ((e = launch_ds_add_pairs(s, tables(d), o, d->applied.as<uint8_t>(), na)) ||
         (e = launch_ds_clock(s, clock_keys, clock_ctr, d->excl.as<unsigned long long>(),
                              d->clock.as<unsigned long long>(), na)))
@@ -654,6 +666,7 @@ int orswot_fold(ce_core* c, const Counts& k, uint64_t kill_bound) {
       return ctx->hip_fail(e, "finalize");
     const int t = ctx->tbegin("ds_finalize");
     if ((e = launch_ds_finalize(s, tables(d)))) return ctx->hip_fail(e, "finalize");
+    d->scratch_dirty = false;
     ctx->tend(t);
     c->path_counts["ds_fold_global"]++;
   }
@@ -1435,10 +1448,12 @@ int orswot_merge_cols(ce_core* c, const IdDots& oclock,
     // no deferred removals on either side: merge + finalize in one pass over the pairs, then
     // the clock; the counts come back only for the merge the caller reads them after
     const int tm = ctx->tbegin("ds_merge");
+    d->scratch_dirty = true;
     if ((e = launch_ds_put_other(s, tables(d), ocols.member, ocols.actor, ocols.value, n, true)) ||
         (e = launch_ds_merge_finalize(s, tables(d), d->clock.as<unsigned long long>(), oclk)) ||
         (e = launch_merge_max(s, d->clock.as<unsigned long long>(), oclk, cap)))
       return ctx->hip_fail(e, "merge");
+    d->scratch_dirty = false;  // merge_finalize cleared oth / add / kill
     ctx->tend(tm);
     if (want_live && (e = hipMemcpyAsync(live_async, d->live.p, 16, hipMemcpyDeviceToHost, s)))
       return ctx->hip_fail(e, "finalize");
@@ -1447,6 +1462,7 @@ int orswot_merge_cols(ce_core* c, const IdDots& oclock,
     return CE_OK;
   }
   const int tm = ctx->tbegin("ds_merge");
+  d->scratch_dirty = true;
   if ((e = launch_ds_put_other(s, tables(d), ocols.member, ocols.actor, ocols.value, n)) ||
       (e = launch_ds_merge(s, tables(d), d->clock.as<unsigned long long>(), d->oclock.as<unsigned long long>())))
     return ctx->hip_fail(e, "merge");
@@ -1460,6 +1476,7 @@ int orswot_merge_cols(ce_core* c, const IdDots& oclock,
       (e = launch_merge_max(s, d->clock.as<unsigned long long>(), d->oclock.as<unsigned long long>(), cap)))
     return ctx->hip_fail(e, "merge");
   if ((rc = finalize(c))) return rc;
+  d->scratch_dirty = false;  // merge cleared oth, finalize add / kill
   std::vector<uint8_t> fl;
   if ((rc = flags_for(c, d->d0[0].as<uint32_t>(), d->d0[2].as<uint32_t>(), d->d0[3].as<unsigned long long>(), nr, &fl)))
     return rc;
@@ -1902,6 +1919,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     }
     // no host wait: the merged counts land in pinned memory for ds_settle (the next ingest's
     // first wait), like a fold's
+    d->scratch_dirty = true;
     if ((e = hipMemcpyAsync(d->rd_args_d.p, hs, n * sizeof(DsMergeSrc), hipMemcpyHostToDevice, s)) ||
         (e = launch_ds_kmerge(s, tables(d), d->rd_args_d.as<DsMergeSrc>(), hs, (uint32_t)n,
                               d->clock.as<unsigned long long>(), d->rd_oclocks.as<unsigned long long>(), ccap,
@@ -1909,6 +1927,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
         (e = hipMemcpyAsync(d->h_cnt.as<uint32_t>() + 56, d->live.p, 20, hipMemcpyDeviceToHost, s)))
       return ctx->hip_fail(e, "merge");
     c->path_counts["states_kway_merge"]++;
+    d->scratch_dirty = false;  // k_ds_kfinal cleared oth / hold
     d->settle_pending = true;
     d->settle_fold = false;
     d->settle_delta = false;

@@ -394,41 +394,71 @@ __global__ void k_rdm_dups(const OrswotReadArgs* fa) {
   }
 }
 
-// exclusive scan of ndots -> dbase, one 1024-thread block per file (a thread per contiguous run),
-// then the tail words (k_rd_tail) for the file's one download
-__global__ void __launch_bounds__(1024) k_rdm_scan_tail(const OrswotReadArgs* fa) {
-  const OrswotReadArgs a = fa[blockIdx.x];
-  __shared__ uint32_t part[16];
-  const uint32_t n = a.n_cand, t = threadIdx.x;
-  const uint32_t per = (n + 1023) / 1024;
-  const uint32_t b0 = min(n, t * per), b1 = min(n, b0 + per);
+// exclusive scan of ndots -> dbase over 2048-entry tiles, then the tail words (k_rd_tail) for
+// the file's one download.  k_rdm_tile_sums: tile totals into the repeat-check set's words (free
+// once k_rdm_dups is done); k_rdm_tile_scan: a tile's base from the totals before it, the tile
+// scanned in LDS, dbase written coalesced.  (One 1024-thread block per file walking contiguous
+// per-thread runs -- a load and a store per entry, each instruction touching 64 lines -- took
+// ~50 us at C3's 8 x 100k entries.)
+constexpr uint32_t kScanTile = kB * 8;
+
+__global__ void __launch_bounds__(kB) k_rdm_tile_sums(const OrswotReadArgs* fa) {
+  __shared__ uint32_t part[kB / 64];
+  const OrswotReadArgs& a = fa[blockIdx.y];
+  const uint32_t t0 = blockIdx.x * kScanTile;
+  if (t0 >= a.n_cand) return;
+  uint32_t v = 0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const uint32_t i = t0 + q * kB + threadIdx.x;
+    v += i < a.n_cand ? a.ndots[i] : 0u;
+  }
+  const uint32_t tot = block_sum(v, part);
+  if (threadIdx.x == 0) reinterpret_cast<uint32_t*>(a.msort)[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(kB) k_rdm_tile_scan(const OrswotReadArgs* fa) {
+  __shared__ uint32_t part[kB / 64];
+  __shared__ uint32_t run[kB];
+  const OrswotReadArgs& a = fa[blockIdx.y];
+  const uint32_t t0 = blockIdx.x * kScanTile;
+  if (t0 >= a.n_cand) return;
+  // the tile's base: the totals of the tiles before it
+  const uint32_t* tsum = reinterpret_cast<const uint32_t*>(a.msort);
+  uint32_t b = 0;
+  for (uint32_t x = threadIdx.x; x < blockIdx.x; x += kB) b += tsum[x];
+  const uint32_t base = block_sum(b, part);
+  // lane l owns entries t0 + 8 l .. + 7 (two 16-byte loads), a block scan of the lanes' sums
+  uint32_t v[8];
+  const uint32_t i0 = t0 + 8 * threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < 8; q++) v[q] = i0 + q < a.n_cand ? a.ndots[i0 + q] : 0u;
   uint32_t s = 0;
-  for (uint32_t i = b0; i < b1; i++) s += a.ndots[i];
-  // block exclusive scan of s
+#pragma unroll
+  for (int q = 0; q < 8; q++) s += v[q];
   uint32_t incl = s;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
-    if ((int)(t & 63) >= o) incl += y;
+    if ((int)(threadIdx.x & 63) >= o) incl += y;
   }
-  if ((t & 63) == 63) part[t >> 6] = incl;
+  if ((threadIdx.x & 63) == 63) run[threadIdx.x >> 6] = incl;
   __syncthreads();
   uint32_t wbase = 0;
-  for (uint32_t j = 0; j < (t >> 6); j++) wbase += part[j];
-  uint32_t run = wbase + incl - s;
-  for (uint32_t i = b0; i < b1; i++) {
-    a.dbase[i] = run;
-    run += a.ndots[i];
-  }
-  __syncthreads();
-  if (t == 0 && n && a.tail_out) {
-    uint32_t tot = 0;
-    for (int j = 0; j < 16; j++) tot += part[j];
-    const uint32_t l = n - 1;
-    a.tail_out[0] = a.end[l];
-    a.tail_out[1] = tot - a.ndots[l];  // dbase of the last entry
-    a.tail_out[2] = a.ndots[l];
-    a.tail_out[3] = *a.flags;
+  for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) wbase += run[w];
+  uint32_t r = base + wbase + incl - s;
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    if (i0 + q < a.n_cand) {
+      a.dbase[i0 + q] = r;
+      if (i0 + q == a.n_cand - 1 && a.tail_out) {
+        a.tail_out[0] = a.end[i0 + q];
+        a.tail_out[1] = r;  // dbase of the last entry
+        a.tail_out[2] = v[q];
+        a.tail_out[3] = *a.flags;
+      }
+    }
+    r += v[q];
   }
 }
 
@@ -489,7 +519,10 @@ hipError_t launch_orswot_read_multi(hipStream_t s, const OrswotReadArgs* d_args,
     hipLaunchKernelGGL(k_rdm_entry, dim3(gx, nf), dim3(kB), 0, s, d_args);
     hipLaunchKernelGGL(k_rdm_chain, dim3(gx, nf), dim3(kB), 0, s, d_args);
     hipLaunchKernelGGL(k_rdm_dups, dim3(gx, nf), dim3(kB), 0, s, d_args);
-    hipLaunchKernelGGL(k_rdm_scan_tail, dim3(nf), dim3(1024), 0, s, d_args);
+    uint32_t gt = 1;
+    for (uint32_t f = 0; f < nf; f++) gt = std::max(gt, (h_args[f].n_cand + kScanTile - 1) / kScanTile);
+    hipLaunchKernelGGL(k_rdm_tile_sums, dim3(gt, nf), dim3(kB), 0, s, d_args);
+    hipLaunchKernelGGL(k_rdm_tile_scan, dim3(gt, nf), dim3(kB), 0, s, d_args);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_rdm_emit, dim3(gx, nf), dim3(kB), 0, s, d_args);
