@@ -605,6 +605,12 @@ def main():
     dev_idx = 0 if os.environ.get("CE_BENCH_SHARE_GPU") == "1" else local
     torch.cuda.set_device(dev_idx)
     dev = torch.device("cuda", dev_idx)
+    # every host thread (launches, name hashing, host-buffer gathers) on the GPU's NUMA node:
+    # the C3 names ran 3.42 -> 2.60 ms/step pinned on the same box (CE_BENCH_NUMA_PIN=0: off)
+    if os.environ.get("CE_BENCH_NUMA_PIN", "1") == "1":
+        cpus = gpu_node_cpus(dev)
+        if cpus:
+            os.sched_setaffinity(0, cpus)
     if world > 1:
         backend = os.environ.get("CE_DIST_BACKEND", "nccl")
         if backend == "nccl":

@@ -1304,6 +1304,14 @@ def main():
     torch.cuda.set_stream(stream)
     ctx = crdtenc.Context(0)
     ctx.set_stream(stream.cuda_stream)
+    # every host thread on the GPU's NUMA node (bench.py does the same): the names' SHA3 threads
+    # 3.42 -> 2.60 ms/step with the names on one box (tools/c3_names_ab.sh, CE_BENCH_NUMA_PIN=0: off)
+    if os.environ.get("CE_BENCH_NUMA_PIN", "1") == "1":
+        sys.path.insert(0, REPO)
+        import bench
+        cpus = bench.gpu_node_cpus(dev)
+        if cpus:
+            os.sched_setaffinity(0, cpus)
     line = RUNNERS[args.config](args, ctx, dev)
     print(json.dumps(line), flush=True)
     ctx.close()
