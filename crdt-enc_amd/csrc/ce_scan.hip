@@ -3,9 +3,10 @@
 // hipCUB's DeviceScan (rocPRIM's look-back scan) queries the device properties on the host at
 // every call (to pick a sleep variant of its look-back state for one older chip); in the HIP
 // runtime torch loads that query costs tens of microseconds, which a C3 step paid ~5 times while
-// the GPU waited for the next launch (profiles/r04_c3_step.txt).  These scans are three plain
-// launches over 2048-item tiles: tile totals, one block scanning the totals, tiles rescanned
-// with their offsets.  Sizes come from the launch, nothing is read back.
+// the GPU waited for the next launch (profiles/r04_c3_step.txt).  These scans are plain launches
+// over 2048-item tiles: tile totals, then the tiles rescanned with their offsets (each block
+// sums the totals before its tile; past 4096 tiles one block scans the totals first).  Sizes
+// come from the launch, nothing is read back.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -82,6 +83,34 @@ __global__ void __launch_bounds__(kB) k_sum_apply(const uint32_t* in, uint32_t* 
     s += v[k];
   }
   uint32_t run = block_incl_sum(s, lds) - s + tile_off[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < kItems; k++) {
+    if (i0 + k < n) out[i0 + k] = run;
+    run += v[k];
+  }
+}
+
+// k_sum_apply with the tile's offset summed from the totals before it (no separate scan of the
+// totals: one launch less per scan; the reads grow as tiles^2 / 2, so only up to kApplyScanTiles)
+constexpr uint32_t kApplyScanTiles = 4096;
+__global__ void __launch_bounds__(kB) k_sum_apply_direct(const uint32_t* in, uint32_t* out, uint64_t n,
+                                                         const uint32_t* tile_sum) {
+  __shared__ uint32_t lds[kB / 64];
+  __shared__ uint32_t off;
+  uint32_t b = 0;
+  for (uint32_t x = threadIdx.x; x < blockIdx.x; x += kB) b += tile_sum[x];
+  b = block_incl_sum(b, lds);
+  if (threadIdx.x == kB - 1) off = b;
+  __syncthreads();
+  const uint64_t i0 = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * kItems;
+  uint32_t v[kItems];
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < kItems; k++) {
+    v[k] = i0 + k < n ? in[i0 + k] : 0u;
+    s += v[k];
+  }
+  uint32_t run = block_incl_sum(s, lds) - s + off;
 #pragma unroll
   for (int k = 0; k < kItems; k++) {
     if (i0 + k < n) out[i0 + k] = run;
@@ -264,6 +293,10 @@ hipError_t ds_excl_sum_u32(void* tmp, size_t& tb, const uint32_t* in, uint32_t* 
   if (n == 0) return hipSuccess;
   uint32_t* ts = static_cast<uint32_t*>(tmp);
   hipLaunchKernelGGL(k_sum_tiles, dim3(nt), dim3(kB), 0, s, in, (uint64_t)n, ts);
+  if (nt <= kApplyScanTiles && !getenv("CE_SCAN_3PASS")) {
+    hipLaunchKernelGGL(k_sum_apply_direct, dim3(nt), dim3(kB), 0, s, in, out, (uint64_t)n, ts);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_scan_tile_sums, dim3(1), dim3(kB), 0, s, ts, nt);
   hipLaunchKernelGGL(k_sum_apply, dim3(nt), dim3(kB), 0, s, in, out, (uint64_t)n, ts);
   return hipGetLastError();
