@@ -263,6 +263,45 @@ __global__ void __launch_bounds__(kB) k_seg_apply(const uint32_t* keys, const un
   }
 }
 
+// k_seg_apply with the carry into the tile combined from the tile summaries before it (a lane
+// folds a contiguous run of them in order, a block scan orders the lanes): no k_seg_carry launch
+// up to kApplyScanTiles tiles
+__global__ void __launch_bounds__(kB) k_seg_apply_direct(const uint32_t* keys, const unsigned long long* vals,
+                                                         unsigned long long* out, uint64_t n, const Seg* tile_seg) {
+  __shared__ Seg lds[kB / 64];
+  __shared__ Seg carry;
+  const uint32_t nb = blockIdx.x, per = (nb + kB - 1) / kB;
+  Seg agg;
+  agg.empty = 1;
+  agg.kf = agg.kl = 0;
+  agg.mx = 0;
+  agg.uni = 1;
+  for (uint32_t j = threadIdx.x * per; j < min(nb, (threadIdx.x + 1) * per); j++) agg = seg_combine(agg, tile_seg[j]);
+  const Seg ea = block_excl_seg(agg, lds);
+  if (threadIdx.x == kB - 1) carry = seg_combine(ea, agg);
+  __syncthreads();
+  const Seg tile_in = carry;
+  const uint64_t i0 = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * kItems;
+  const Seg s = thread_seg(keys, vals, i0, n);
+  const Seg c = seg_combine(tile_in, block_excl_seg(s, lds));
+  if (s.empty) return;
+  uint32_t rk = c.kl;
+  unsigned long long rm = c.empty ? 0ull : c.mx;
+  if (c.empty) rk = ~keys[i0];  // forces a new run at the first item
+#pragma unroll
+  for (int k = 0; k < kItems; k++) {
+    if (i0 + k >= n) break;
+    const uint32_t kk = keys[i0 + k];
+    const unsigned long long v = vals[i0 + k];
+    if (kk != rk) {
+      rk = kk;
+      rm = 0;
+    }
+    out[i0 + k] = rm;
+    rm = v > rm ? v : rm;
+  }
+}
+
 }  // namespace
 
 namespace {
@@ -322,6 +361,10 @@ hipError_t ds_excl_max_by_key(void* tmp, size_t& tb, const uint32_t* keys, const
   if (n == 0) return hipSuccess;
   Seg* ts = static_cast<Seg*>(tmp);
   hipLaunchKernelGGL(k_seg_tiles, dim3(nt), dim3(kB), 0, s, keys, vals, (uint64_t)n, ts);
+  if (nt <= kApplyScanTiles && !getenv("CE_SCAN_3PASS")) {
+    hipLaunchKernelGGL(k_seg_apply_direct, dim3(nt), dim3(kB), 0, s, keys, vals, out, (uint64_t)n, ts);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_seg_carry, dim3(1), dim3(kB), 0, s, ts, nt);
   hipLaunchKernelGGL(k_seg_apply, dim3(nt), dim3(kB), 0, s, keys, vals, out, (uint64_t)n, ts);
   return hipGetLastError();
