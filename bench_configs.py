@@ -165,12 +165,14 @@ def seal_op_files(ctx, key, actors, a_lo, a_hi, v_lo, v_hi, dev, seed):
 
 
 def name_threads():
-    """SHA3 name threads for the pipelined compactions: the job's CPU share less two (the
-    launching thread and the runtime's), at least 4; CE_NAME_THREADS overrides"""
+    """SHA3 name threads for the pipelined compactions: the job's CPU share less four (the
+    launching thread, the runtime's and the download waits: at share - 2 the cgroup quota was
+    exceeded and throttled, C3 3.27-3.39 ms/step against 2.58-2.67 at share - 4 on one box,
+    tools/c3_names_ab.sh), at least 4; CE_NAME_THREADS overrides"""
     if os.environ.get("CE_NAME_THREADS"):
         return max(1, int(os.environ["CE_NAME_THREADS"]))
     import bench
-    return max(4, bench.host_cpu()[2] - 2)
+    return max(4, bench.host_cpu()[2] - 4)
 
 
 def _lower_priority():
