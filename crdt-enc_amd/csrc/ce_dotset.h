@@ -60,6 +60,7 @@ struct DsTile {
   void* col[9];
   uint64_t npad;
   uint32_t total[5];
+  uint32_t max_rows;  // the largest per-file count of any column group (<= kTileMaxRows): LDS rows
 };
 
 struct DsDecodeArgs {

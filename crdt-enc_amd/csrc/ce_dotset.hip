@@ -534,7 +534,7 @@ __global__ void __launch_bounds__(kBlock) k_ds_emit(DsDecodeArgs a) {
 // writes the tile's contiguous output range with coalesced stores (each output index finds its
 // file among the tile's 65 bases by binary search in LDS).
 __global__ void __launch_bounds__(kBlock) k_ds_untile(DsDecodeArgs a) {
-  __shared__ unsigned long long tile[kTileMaxRows * 64];
+  extern __shared__ unsigned long long tile[];  // [tile.max_rows * 64]: sized at launch
   __shared__ uint32_t sb[65];
   __shared__ uint32_t tmax;
   const int c = blockIdx.y;
@@ -1540,7 +1540,9 @@ hipError_t launch_ds_emit(hipStream_t s, const DsDecodeArgs& a) {
   if (a.tile.npad) {
     if (decode_stage()) hipLaunchKernelGGL((k_ds_emit<true, true>), dim3(blocks_for(a.n)), dim3(kBlock), kStageLds, s, a);
     else hipLaunchKernelGGL((k_ds_emit<true, false>), dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
-    hipLaunchKernelGGL(k_ds_untile, dim3((a.n + 63) / 64, 9), dim3(kBlock), 0, s, a);
+    // LDS for the batch's largest per-file count, not kTileMaxRows: more blocks per CU
+    const uint32_t rows = a.tile.max_rows ? std::min<uint32_t>(a.tile.max_rows, kTileMaxRows) : kTileMaxRows;
+    hipLaunchKernelGGL(k_ds_untile, dim3((a.n + 63) / 64, 9), dim3(kBlock), (size_t)rows * 64 * 8, s, a);
   } else {
     if (decode_stage()) hipLaunchKernelGGL((k_ds_emit<false, true>), dim3(blocks_for(a.n)), dim3(kBlock), kStageLds, s, a);
     else hipLaunchKernelGGL((k_ds_emit<false, false>), dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);

@@ -1172,7 +1172,11 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
         a.tile.col[cc] = d->tile_col[cc].p;
       }
       a.tile.npad = npad;
-      for (int j = 0; j < kCntN; j++) a.tile.total[j] = (uint32_t)k.v[j];
+      a.tile.max_rows = 1;
+      for (int j = 0; j < kCntN; j++) {
+        a.tile.total[j] = (uint32_t)k.v[j];
+        a.tile.max_rows = std::max<uint32_t>(a.tile.max_rows, (uint32_t)kmax.v[j]);
+      }
       c->path_counts["ds_emit_tiled"]++;
     }
   }
