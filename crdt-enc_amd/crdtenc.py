@@ -49,7 +49,7 @@ EXPORTS = [
     "ce_core_register_actors", "ce_core_dense_capacity", "ce_core_export_dense",
     "ce_core_import_dense", "ce_vbuf_init", "ce_vbuf_remaining", "ce_vbuf_chunk",
     "ce_vbuf_advance", "ce_vbuf_chunks_vectored", "ce_ctx_set_timing", "ce_ctx_timing_read",
-    "ce_ctx_timing_reset", "ce_ctx_set_timing_only", "ce_core_reset", "ce_core_merge_state", "ce_core_dense_ready",
+    "ce_ctx_timing_reset", "ce_ctx_set_timing_only", "ce_core_reset", "ce_core_settle", "ce_core_merge_state", "ce_core_dense_ready",
     "ce_keys_decode", "ce_keys_from_remote_metas", "ce_keys_merge", "ce_keys_free",
     "ce_keys_count", "ce_keys_latest", "ce_keys_get", "ce_keys_at", "ce_core_set_keys",
     "ce_core_apply_ops_batch", "ce_core_ingest_ops_iov", "ce_core_ingest_states_iov", "ce_core_compact_ops_iov",
@@ -852,6 +852,11 @@ class Core:
 
     def reset(self):
         self.ctx.check(lib().ce_core_reset(self.p), "reset")
+
+    def settle(self):
+        """Wait for the queued device work; the status a fold / merge found after its call
+        returned (a dot-set table overflow, sticky until reset)."""
+        return lib().ce_core_settle(self.p)
 
     def merge_state(self, state_wrapper_msgpack):
         """read_remote_states' merge of one decrypted StateWrapper (lib.rs:447, 458-466)."""

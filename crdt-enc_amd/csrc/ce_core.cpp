@@ -2125,6 +2125,15 @@ int ce_core_reset(ce_core* c) {
   return CE_OK;
 }
 
+int ce_core_settle(ce_core* c) {
+  if (!c) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  if (is_dotset_kind(c->kind)) return ds_settle(c);
+  hipError_t e = hipStreamSynchronize(c->ctx->stream);
+  if (e) return c->ctx->hip_fail(e, "settle");
+  return CE_OK;
+}
+
 int ce_core_register_actors(ce_core* c, const uint8_t* actors, uint32_t m) {
   if (!c || (m && !actors)) return CE_ERR_INVALID_ARG;
   std::lock_guard<std::recursive_mutex> g(c->ctx->mu);

@@ -38,6 +38,10 @@ struct DsState {
   // flags have not been read yet: ds_settle reads them at the next host wait
   bool settle_pending = false, settle_fold = false;
   bool settle_delta = false;  // live[0..1] are changes (the partitioned fold), not totals
+  // a fold / merge overflowed a table: the tables and the deferred set no longer describe the
+  // state, so every later operation fails until ce_core_reset (sticky: the overflow is only seen
+  // at the settle after the call that caused it returned)
+  bool poisoned = false;
   uint32_t settle_nr = 0;
   uint64_t settle_rmc = 0, settle_rmm = 0;
   std::vector<std::pair<IdDots, std::vector<uint64_t>>> settle_d0;
@@ -216,7 +220,10 @@ int ensure_pairs(ce_core* c, uint64_t extra) {
   }
   uint32_t n_live = 0;
   if ((rc = collect(c, &n_live))) return rc;
-  const uint32_t cap = pow2_at_least(std::max<uint64_t>(4096, 2 * (n_live + extra) + 1));
+  uint32_t cap = pow2_at_least(std::max<uint64_t>(4096, 2 * (n_live + extra) + 1));
+  // test knob: a pair table that cannot grow past n slots, so an ingest overflows it
+  const uint32_t cap_max = getenv("CE_DS_TEST_PAIR_CAP") ? pow2_at_least(std::max(4096, atoi(getenv("CE_DS_TEST_PAIR_CAP")))) : 0;
+  if (cap_max && cap > cap_max) cap = std::max(cap_max, d->pcap);
   // the collected columns survive the reallocation of the tables
   if ((rc = tables_alloc(c, cap))) return rc;
   hipError_t e;
@@ -514,7 +521,10 @@ int finalize(ce_core* c) {
       (e = hipMemcpyAsync(h, d->live.p, 16, hipMemcpyDeviceToHost, c->ctx->stream)) ||
       (e = stream_wait(c->ctx->stream)))
     return c->ctx->hip_fail(e, "finalize");
-  if (h[2]) return c->ctx->fail(CE_ERR_DEVICE, "dot-set table overflow");
+  if (h[2]) {
+    d->poisoned = true;
+    return c->ctx->fail(CE_ERR_DEVICE, "dot-set table overflow");
+  }
   d->live_pairs = h[0];
   d->used_pairs = h[1];
   return CE_OK;
@@ -523,8 +533,10 @@ int finalize(ce_core* c) {
 // Orswot fold of a columnar batch in application order (k = counts); the removals of the
 // batch plus the current deferred set (re-applied by apply_deferred) set the thresholds.
 // kill_bound: an upper bound on the batch's removal items (sum over removals of members x clock
-// entries; ~0 = unknown: the global kernels)
-int orswot_fold(ce_core* c, const Counts& k, uint64_t kill_bound) {
+// entries; ~0 = unknown: the global kernels).  adds_contig: the emit that produced THESE columns
+// proved every actor's adds one contiguous run (only ds_ingest_ops can say so; any other caller
+// passes false, and the sorted path is always correct)
+int orswot_fold(ce_core* c, const Counts& k, uint64_t kill_bound, bool adds_contig) {
   DsState* d = c->ds;
   ce_ctx* ctx = c->ctx;
   hipStream_t s = ctx->stream;
@@ -540,7 +552,7 @@ int orswot_fold(ce_core* c, const Counts& k, uint64_t kill_bound) {
   // (set after the reserves below: a reserve may move the buffer)
   const uint32_t* clock_keys = nullptr;
   const unsigned long long* clock_ctr = nullptr;
-  if (na && d->adds_contig) {
+  if (na && adds_contig) {
     if ((e = d->excl.reserve(na * 8ull))) return ctx->hip_fail(e, "applied");
     unsigned long long* ex = d->excl.as<unsigned long long>();
     size_t t2 = 0;
@@ -694,14 +706,20 @@ int orswot_fold(ce_core* c, const Counts& k, uint64_t kill_bound) {
 // drained (usually it has: callers settle right after a host wait of their own)
 int ds_settle(ce_core* c) {
   DsState* d = c->ds;
-  if (!d || !d->settle_pending) return CE_OK;
+  if (!d) return CE_OK;
   ce_ctx* ctx = c->ctx;
+  if (d->poisoned) return ctx->fail(CE_ERR_DEVICE, "dot-set table overflow in an earlier operation (reset the core)");
+  if (!d->settle_pending) return CE_OK;
   hipStream_t s = ctx->stream;
   hipError_t e;
   if ((e = stream_wait(s))) return ctx->hip_fail(e, "settle");
   d->settle_pending = false;
   const uint32_t* hl = d->h_cnt.as<uint32_t>() + 56;
-  if (hl[2]) return ctx->fail(CE_ERR_DEVICE, "dot-set table overflow");
+  if (hl[2]) {
+    d->poisoned = true;
+    d->settle_d0.clear();
+    return ctx->fail(CE_ERR_DEVICE, "dot-set table overflow");
+  }
   if (d->settle_delta) {
     d->live_pairs += (int64_t)(int32_t)hl[0];
     d->used_pairs += hl[1];
@@ -1017,7 +1035,11 @@ int ds_init(ce_core* c) {
 
 int ds_reset(ce_core* c) {
   DsState* d = c->ds;
-  if (int rs = ds_settle(c)) return rs;
+  // an overflow poisons the core until here: the reset rebuilds every table from empty
+  if (int rs = ds_settle(c); rs && !d->poisoned) return rs;
+  d->poisoned = false;
+  d->settle_pending = false;
+  d->settle_d0.clear();
   d->deferred.clear();
   d->vals.clear();
   hipError_t e;
@@ -1237,7 +1259,8 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
   if (c->kind == CE_STATE_ORSWOT) {
     // removal items <= members x the largest per-file clock-entry count (a removal's clock is
     // part of one file)
-    rc = orswot_fold(c, tot, tot.v[kCntRmM] * std::max<uint64_t>(1, kmax.v[kCntRmC]));
+    rc = orswot_fold(c, tot, tot.v[kCntRmM] * std::max<uint64_t>(1, kmax.v[kCntRmC]), d->adds_contig);
+    d->adds_contig = false;  // describes this batch's columns only
   } else {
     rc = mvreg_commit(c, (uint32_t)base.v[kCntRm], (uint32_t)tot.v[kCntRm], true);
   }
@@ -2072,7 +2095,7 @@ int ds_apply_local_ops(ce_core* c, const uint8_t* ops, size_t len) {
       const uint64_t me = r + 1 < nr ? hc.rm_mbeg[r + 1] : hc.rm_mem.size();
       items += (ce - hc.rm_cbeg[r]) * (me - hc.rm_mbeg[r]);
     }
-    return orswot_fold(c, tot, items);
+    return orswot_fold(c, tot, items, false);
   }
   return mvreg_commit(c, (uint32_t)base.v[kCntRm], (uint32_t)tot.v[kCntRm], true);
 }

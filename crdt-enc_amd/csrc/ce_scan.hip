@@ -313,6 +313,12 @@ bool use_hipcub() {
   static const bool v = getenv("CE_HIPCUB_SCAN") != nullptr;
   return v;
 }
+// CE_SCAN_3PASS=1 (tests): the three-launch form (tile sums, one carry block, apply) at any size;
+// by default it only runs past kApplyScanTiles tiles
+bool three_pass() {
+  static const bool v = getenv("CE_SCAN_3PASS") != nullptr;
+  return v;
+}
 }  // namespace
 
 hipError_t ds_excl_sum_u32(void* tmp, size_t& tb, const uint32_t* in, uint32_t* out, uint32_t n, hipStream_t s) {
@@ -332,7 +338,7 @@ hipError_t ds_excl_sum_u32(void* tmp, size_t& tb, const uint32_t* in, uint32_t* 
   if (n == 0) return hipSuccess;
   uint32_t* ts = static_cast<uint32_t*>(tmp);
   hipLaunchKernelGGL(k_sum_tiles, dim3(nt), dim3(kB), 0, s, in, (uint64_t)n, ts);
-  if (nt <= kApplyScanTiles && !getenv("CE_SCAN_3PASS")) {
+  if (nt <= kApplyScanTiles && !three_pass()) {
     hipLaunchKernelGGL(k_sum_apply_direct, dim3(nt), dim3(kB), 0, s, in, out, (uint64_t)n, ts);
     return hipGetLastError();
   }
@@ -361,7 +367,7 @@ hipError_t ds_excl_max_by_key(void* tmp, size_t& tb, const uint32_t* keys, const
   if (n == 0) return hipSuccess;
   Seg* ts = static_cast<Seg*>(tmp);
   hipLaunchKernelGGL(k_seg_tiles, dim3(nt), dim3(kB), 0, s, keys, vals, (uint64_t)n, ts);
-  if (nt <= kApplyScanTiles && !getenv("CE_SCAN_3PASS")) {
+  if (nt <= kApplyScanTiles && !three_pass()) {
     hipLaunchKernelGGL(k_seg_apply_direct, dim3(nt), dim3(kB), 0, s, keys, vals, out, (uint64_t)n, ts);
     return hipGetLastError();
   }

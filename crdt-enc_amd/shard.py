@@ -273,6 +273,8 @@ def ingest_dotset_sharded(core, ingest, group=None, device="cpu", snapshot=True,
     empty after a reset) and restores it itself; a failure then raises.  Returns (rc, merges)."""
     s0 = core.state_bytes() if snapshot else None
     rc = ingest()
+    if rc == 0 and hasattr(core, "settle"):
+        rc = core.settle()  # a device table overflow is only seen once the fold has run
     code = torch.tensor([rc], dtype=torch.int64, device=device)
     all_reduce_(code, dist.ReduceOp.MAX, group=group)
     code = int(code.item())

@@ -257,6 +257,13 @@ int ce_core_state_bytes(ce_core *c, ce_buf *out);
 /* Back to the empty StateWrapper (Default, lib.rs:240-243), keeping registered actors and the
  * read key; used to compact the same batch repeatedly in benchmarks. */
 int ce_core_reset(ce_core *c);
+/* Wait for the core's queued device work and return its deferred status: CE_OK, or the error a
+ * fold / merge that already returned CE_OK found on the device (a dot-set table overflow).  Such
+ * an error is sticky: every later call fails with it until ce_core_reset.  Callers that must act
+ * on an ingest's exact status before the next call (the sharded ingest's all_reduce of statuses)
+ * settle first.  No reference counterpart: the reference's apply loop is synchronous
+ * (crdt-enc/src/lib.rs:533-535). */
+int ce_core_settle(ce_core *c);
 
 /* Storage-less ingest: what read_remote_ops does after Storage::load_ops (lib.rs:495-546).
  * files i = blob[offs[i], offs[i+1]) (outer version || cryptor box); the writer of file i is

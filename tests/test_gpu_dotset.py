@@ -938,3 +938,100 @@ def test_staged_decode_equals_global(ctx, kind, adversarial):
             os.environ.pop("CE_DS_DECODE_STAGE", None)
     assert got[False] == got[True]
     assert got[True][0] == want and got[True][1] == oc.serialize()
+
+
+def test_local_apply_after_contiguous_ingest(ctx):
+    """a load_ops-ordered ingest whose adds are one run per actor takes the
+    sort-free applied flags; a later local apply_ops with interleaved actors (Add(A), Add(B),
+    Add(A)) must not inherit that flag -- it takes the sorted path and equals the oracle."""
+    rng = random.Random(2024)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 6)
+    files, truth = G.well_formed_orswot(rng, actors, 3, 8, 200)
+    acts, clears, fa, fv = G.batch(files, "orswot", APP)
+    sealed = seal_files(ctx, key, clears)
+    core, oc = new_core(ctx, "orswot", key), C.Core("orswot")
+    assert core.ingest_ops(sealed, acts, fa, fv)[0] == 0
+    assert oc.read_remote_ops(key, [APP], sealed, [acts[i] for i in fa], fv)[0] == 0
+    assert core.path_count("ds_adds_contiguous") == 1
+    me = core.info_actor()
+    a, b = acts[0], acts[1]
+    ca, cb = oc.state.clock.get(a), oc.state.clock.get(b)
+    for rnd in range(3):
+        ops = [("Add", (a, ca + 1), [1000 + rnd]), ("Add", (b, cb + 1), [2000 + rnd]),
+               ("Add", (a, ca + 2), [3000 + rnd]), ("Add", (b, cb + 2), [1000 + rnd])]
+        ca, cb = ca + 2, cb + 2
+        assert core.apply_ops(C.enc_orswot_ops(ops)) == 0
+        for op in ops:
+            oc.state.apply(op)
+        oc.nov.apply(me, oc.nov.get(me) + 1)
+        assert core.state_bytes() == oc.serialize(), rnd
+    assert core.path_count("ds_adds_contiguous") == 1   # the local applies took the sort
+    core.close()
+
+
+def test_table_overflow_is_sticky_until_reset(ctx):
+    """a pair-table overflow is found on the device after the ingest
+    returned; it must not be lost.  With the pair table pinned at 4096 slots
+    (CE_DS_TEST_PAIR_CAP) an ingest of ~9k distinct (member, actor) pairs overflows: settle
+    reports CE_ERR_DEVICE, every later call fails the same way, and reset brings the core back
+    (a small batch then equals the oracle)."""
+    rng = random.Random(4242)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 9)
+    big = {a: [[("Add", (a, v * 500 + i + 1), [v * 500 + i]) for i in range(500)] for v in range(2)]
+           for a in actors}
+    acts, clears, fa, fv = G.batch(big, "orswot", APP)
+    sealed = seal_files(ctx, key, clears)
+    os.environ["CE_DS_TEST_PAIR_CAP"] = "4096"
+    try:
+        core = new_core(ctx, "orswot", key)
+        rc = core.ingest_ops(sealed, acts, fa, fv)[0]
+        assert rc in (0, 65), rc        # 0: found later (the fold closes without a wait)
+        assert core.settle() == 65      # CE_ERR_DEVICE
+        assert core.settle() == 65      # sticky
+        with pytest.raises(Exception):
+            core.state_bytes()
+        assert core.ingest_ops(sealed[:1], acts, fa[:1], fv[:1])[0] == 65
+    finally:
+        os.environ.pop("CE_DS_TEST_PAIR_CAP", None)
+    core.reset()
+    assert core.settle() == 0
+    small = {a: [[("Add", (a, 1), [7])]] for a in actors[:3]}
+    acts, clears, fa, fv = G.batch(small, "orswot", APP)
+    oc = C.Core("orswot")
+    assert check_ops(ctx, "orswot", key, core, oc, acts, clears, fa, fv) == 0
+    core.close()
+
+
+def test_scan_forms_equal(ctx):
+    """the dot-set scans (ce_scan.hip) in their default two-launch form, the
+    three-launch form (CE_SCAN_3PASS=1, otherwise only past 4096 tiles) and hipCUB's
+    (CE_HIPCUB_SCAN=1) give identical state bytes == the oracle, on an adversarial batch (the
+    sorted adds' segmented max scan, ragged actor runs across 2048-item tiles; the per-file
+    count scans over 4096 files).  The forms are chosen once per process, so each runs in its own
+    child process (tests/scan_modes_worker.py)."""
+    import hashlib
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    rng = random.Random(31337)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 256)
+    files = G.adversarial_orswot(rng, actors, 16, 6, 5000)
+    acts, clears, fa, fv = G.batch(files, "orswot", APP)
+    sealed = seal_files(ctx, key, clears)
+    oc = C.Core("orswot")
+    orc = oc.read_remote_ops(key, [APP], sealed, [acts[i] for i in fa], fv)[0]
+    want = "%d %s" % (orc, hashlib.sha256(oc.serialize()).hexdigest())
+    outs = {}
+    for mode, env in {"two": {}, "three": {"CE_SCAN_3PASS": "1"}, "hipcub": {"CE_HIPCUB_SCAN": "1"}}.items():
+        e = dict(os.environ)
+        e.pop("CE_SCAN_3PASS", None)
+        e.pop("CE_HIPCUB_SCAN", None)
+        e.update(env)
+        r = subprocess.run([sys.executable, os.path.join(here, "scan_modes_worker.py")], env=e,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs[mode] = r.stdout.strip().splitlines()[-1]
+    assert outs["two"] == outs["three"] == outs["hipcub"] == want, outs
