@@ -135,7 +135,7 @@ int device_open_setup(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs
 // single-page file idles half its lanes on a 2 KiB file (C3's op files)
 int device_open(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
                 uint64_t blob_len, bool outer, const KeyRef& key, uint8_t* d_out,
-                int32_t* d_status, bool sync_counters, bool small_lanes) {
+                int32_t* d_status, bool sync_counters, bool small_lanes, const DecodeArgs* ds) {
   uint32_t ec;
   int rc = reserve_batch(ctx, n, blob_len, &ec);
   if (rc) return rc;
@@ -156,6 +156,13 @@ int device_open(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint
     da.status = d_status;
     da.n = n;
     da.counters = ctx->counters.as<uint32_t>();
+    if (ds) {
+      da.ds = ds->ds;
+      da.supported = ds->supported;
+      da.n_supported = ds->n_supported;
+      da.table = ds->table;
+      da.mask = ds->mask;
+    }
     t = ctx->tbegin("open_small");
     if ((e = launch_open_small_v2(ctx->stream, da)) != hipSuccess) return ctx->hip_fail(e, "open small");
     ctx->tend(t);

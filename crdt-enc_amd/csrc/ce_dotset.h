@@ -82,9 +82,14 @@ struct DsDecodeArgs {
   uint4* miss_list;
   uint32_t miss_cap;
   DsTile tile;                  // emit: the tiled layout (npad 0: direct CSR stores)
+  // Orswot files the open already decoded (k_open_fold_v2's DS form): done[i] = 1 -> the count
+  // pass takes fuse.rawcnt, the emit skips the file, k_ds_untile reads its file-major rows
+  // (fuse.*) and writes the offsets columns as op index + base.  null: none.
+  const uint8_t* fdone;
+  DsFuse fuse;
 };
 hipError_t launch_ds_count(hipStream_t s, const DsDecodeArgs& a);
-hipError_t launch_ds_emit(hipStream_t s, const DsDecodeArgs& a);
+hipError_t launch_ds_emit(hipStream_t s, const DsDecodeArgs& a, bool emit_legacy = true);
 
 struct DsTables {
   unsigned long long* mkey;      // [smask + 1] primary, [mmask + 1] overflow, 1 reserved (member ~0)

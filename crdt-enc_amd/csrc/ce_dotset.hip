@@ -458,9 +458,19 @@ __global__ void __launch_bounds__(kBlock) k_ds_count(DsDecodeArgs a) {
     const uint32_t i = i0 + threadIdx.x;
     const bool in = i < a.n;
     int32_t st = in ? a.status[i] : CE_ERR_DECODE;
-    const uint8_t* sp = STAGE ? stage_files(a, i, in && st == CE_OK, stage_lds) : nullptr;
+    // decoded in the open (its tag verified): the counts it left, no parse
+    const bool fd = in && a.fdone && a.fdone[i];
+    const uint8_t* sp = STAGE ? stage_files(a, i, in && st == CE_OK && !fd, stage_lds) : nullptr;
     uint32_t c[kCntN] = {0, 0, 0, 0, 0};
-    if (in && st == CE_OK) {
+    if (fd) {
+#pragma unroll
+      for (int k = 0; k < kCntN; k++) c[k] = a.fuse.rawcnt[(size_t)k * a.n + i];
+    }
+    if (a.fdone) {  // files the open decoded (counters[5]: the host reads it with the totals)
+      const unsigned long long b = __ballot(fd);
+      if (b && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(b)) atomicAdd(a.counters + 5, (uint32_t)__popcll(b));
+    }
+    if (in && st == CE_OK && !fd) {
       const uint32_t len = a.params[i].len;
       if (STAGE && sp) {
         CountSinkT<true> cs;
@@ -519,7 +529,7 @@ __global__ void __launch_bounds__(kBlock) k_ds_emit(DsDecodeArgs a) {
   extern __shared__ uint8_t stage_lds[];
   for (uint32_t i0 = blockIdx.x * kBlock; i0 < a.n; i0 += gridDim.x * kBlock) {
     const uint32_t i = i0 + threadIdx.x;
-    const bool act = i < a.n && a.status[i] == CE_OK && a.apply[i];
+    const bool act = i < a.n && a.status[i] == CE_OK && a.apply[i] && !(a.fdone && a.fdone[i]);
     const uint8_t* sp = STAGE ? stage_files(a, i, act, stage_lds) : nullptr;
     if (act) {
       if (STAGE && sp) emit_file<TILE, true>(a, i, sp + 16);
@@ -533,9 +543,15 @@ __global__ void __launch_bounds__(kBlock) k_ds_emit(DsDecodeArgs a) {
 // column) stages the tile's rows (k < the tile's largest count) in LDS with coalesced reads, then
 // writes the tile's contiguous output range with coalesced stores (each output index finds its
 // file among the tile's 65 bases by binary search in LDS).
+// Files the open decoded (a.fdone) come from its file-major rows instead (a.fuse: op k of file f at
+// [f * rows + k]); their offsets columns are the op index plus the file's base in the member /
+// clock-entry column (one member, one clock entry per op).  Without the tiled emit (tile.npad 0:
+// the other files were stored directly) only the open's files are written.
 __global__ void __launch_bounds__(kBlock) k_ds_untile(DsDecodeArgs a) {
   extern __shared__ unsigned long long tile[];  // [tile.max_rows * 64]: sized at launch
   __shared__ uint32_t sb[65];
+  __shared__ uint32_t ob[64];     // fused files: the offsets column's base (add_mbeg / rm_cbeg / rm_mbeg)
+  __shared__ uint8_t sdone[64];
   __shared__ uint32_t tmax;
   const int c = blockIdx.y;
   const int g = c == 0 || c == 1 || c == 2 ? kCntAdd : c == 3 ? kCntAddM : c == 4 || c == 5 ? kCntRm
@@ -544,21 +560,48 @@ __global__ void __launch_bounds__(kBlock) k_ds_untile(DsDecodeArgs a) {
   void* const dst[9] = {a.ops.add_actor, a.ops.add_ctr, a.ops.add_mbeg, a.ops.add_mem, a.ops.rm_cbeg,
                         a.ops.rm_mbeg, a.ops.rmc_actor, a.ops.rmc_ctr, a.ops.rm_mem};
   const uint32_t i0 = blockIdx.x * 64;
+  // the offsets columns' base groups: add_mbeg -> add members, rm_cbeg -> clock entries, rm_mbeg
+  // -> removal members
+  const int og = c == 2 ? kCntAddM : c == 4 ? kCntRmC : kCntRmM;
+  const bool synth = c == 2 || c == 4 || c == 5;
   if (threadIdx.x == 0) tmax = 0;
   if (threadIdx.x <= 64) {
     const uint32_t i = i0 + threadIdx.x;
     sb[threadIdx.x] = i < a.n ? a.cnt[(size_t)g * a.n + i] - a.cnt[(size_t)g * a.n] + a.base_off[g]
                               : a.tile.total[g] + a.base_off[g];
+    if (threadIdx.x < 64) {
+      sdone[threadIdx.x] = i < a.n && a.fdone && a.fdone[i];
+      ob[threadIdx.x] = i < a.n ? a.cnt[(size_t)og * a.n + i] - a.cnt[(size_t)og * a.n] + a.base_off[og] : 0u;
+    }
   }
   __syncthreads();
   if (threadIdx.x < 64) atomicMax(&tmax, sb[threadIdx.x + 1] - sb[threadIdx.x]);
   __syncthreads();
   const uint32_t rows = tmax;  // <= kTileMaxRows (the host checked every column's largest count)
   const size_t npad = a.tile.npad;
-  for (uint32_t x = threadIdx.x; x < rows * 64; x += kBlock) {
-    const size_t idx = (size_t)(x >> 6) * npad + i0 + (x & 63);
-    tile[x] = wide ? reinterpret_cast<const unsigned long long*>(a.tile.col[c])[idx]
-                   : reinterpret_cast<const uint32_t*>(a.tile.col[c])[idx];
+  const bool legacy = npad != 0;  // the other files' rows are in tile.col (else: stored directly)
+  if (legacy) {
+    for (uint32_t x = threadIdx.x; x < rows * 64; x += kBlock) {
+      const size_t idx = (size_t)(x >> 6) * npad + i0 + (x & 63);
+      if (sdone[x & 63]) continue;
+      tile[x] = wide ? reinterpret_cast<const unsigned long long*>(a.tile.col[c])[idx]
+                     : reinterpret_cast<const uint32_t*>(a.tile.col[c])[idx];
+    }
+  }
+  if (a.fdone && rows) {
+    // file-major rows: a file's ops are contiguous (x -> file x / rows, op x % rows)
+    const void* fsrc = c == 0 ? (const void*)a.fuse.add_actor : c == 1 ? (const void*)a.fuse.add_ctr
+                       : c == 3 ? (const void*)a.fuse.add_mem : c == 6 ? (const void*)a.fuse.rm_actor
+                       : c == 7 ? (const void*)a.fuse.rm_ctr : (const void*)a.fuse.rm_mem;
+    const uint32_t R = a.fuse.rows;
+    for (uint32_t x = threadIdx.x; x < rows * 64; x += kBlock) {
+      const uint32_t l = x / rows, k = x - l * rows;
+      if (!sdone[l] || k >= R) continue;
+      const size_t idx = (size_t)(i0 + l) * R + k;
+      tile[k * 64 + l] = synth ? (unsigned long long)(ob[l] + k)
+                         : wide ? reinterpret_cast<const unsigned long long*>(fsrc)[idx]
+                                : reinterpret_cast<const uint32_t*>(fsrc)[idx];
+    }
   }
   __syncthreads();
   const uint32_t lo = sb[0], hi = sb[64];
@@ -567,6 +610,7 @@ __global__ void __launch_bounds__(kBlock) k_ds_untile(DsDecodeArgs a) {
 #pragma unroll
     for (uint32_t step = 32; step > 0; step >>= 1)
       if (sb[l + step] <= j) l += step;
+    if (!legacy && !sdone[l]) continue;  // stored by the direct emit
     const unsigned long long v = tile[(j - sb[l]) * 64 + l];
     if (wide) reinterpret_cast<unsigned long long*>(dst[c])[j] = v;
     else reinterpret_cast<uint32_t*>(dst[c])[j] = (uint32_t)v;
@@ -1477,6 +1521,7 @@ __global__ void __launch_bounds__(1024) k_ds_col_totals(const uint32_t* cnt, con
     out[k] = bases[cl] + cnt[cl] - bases[c0];
     out[8 + k] = maxima[k];
   }
+  if (clear8 && k == 5) out[19] = clear8[5];  // files the open decoded (k_ds_count's counters[5])
   if (gate_flags && k < 2) out[17 + k] = gate_flags[k];
   __syncthreads();
   if (clear8 && k < 8) clear8[k] = 0;  // the emit's counters (after the maxima above were read)
@@ -1535,17 +1580,25 @@ hipError_t launch_ds_count(hipStream_t s, const DsDecodeArgs& a) {
   return hipGetLastError();
 }
 
-hipError_t launch_ds_emit(hipStream_t s, const DsDecodeArgs& a) {
+// emit_legacy: some file is left to the lane-per-file emit (false: the open decoded every applied
+// file, only the untile runs)
+hipError_t launch_ds_emit(hipStream_t s, const DsDecodeArgs& a, bool emit_legacy) {
   if (a.n == 0) return hipSuccess;
   if (a.tile.npad) {
-    if (decode_stage()) hipLaunchKernelGGL((k_ds_emit<true, true>), dim3(blocks_for(a.n)), dim3(kBlock), kStageLds, s, a);
-    else hipLaunchKernelGGL((k_ds_emit<true, false>), dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
+    if (!emit_legacy) {
+    } else if (decode_stage()) {
+      hipLaunchKernelGGL((k_ds_emit<true, true>), dim3(blocks_for(a.n)), dim3(kBlock), kStageLds, s, a);
+    } else {
+      hipLaunchKernelGGL((k_ds_emit<true, false>), dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
+    }
+  } else if (emit_legacy) {
+    if (decode_stage()) hipLaunchKernelGGL((k_ds_emit<false, true>), dim3(blocks_for(a.n)), dim3(kBlock), kStageLds, s, a);
+    else hipLaunchKernelGGL((k_ds_emit<false, false>), dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
+  }
+  if (a.tile.npad || a.fdone) {
     // LDS for the batch's largest per-file count, not kTileMaxRows: more blocks per CU
     const uint32_t rows = a.tile.max_rows ? std::min<uint32_t>(a.tile.max_rows, kTileMaxRows) : kTileMaxRows;
     hipLaunchKernelGGL(k_ds_untile, dim3((a.n + 63) / 64, 9), dim3(kBlock), (size_t)rows * 64 * 8, s, a);
-  } else {
-    if (decode_stage()) hipLaunchKernelGGL((k_ds_emit<false, true>), dim3(blocks_for(a.n)), dim3(kBlock), kStageLds, s, a);
-    else hipLaunchKernelGGL((k_ds_emit<false, false>), dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
   }
   return hipGetLastError();
 }

@@ -71,6 +71,9 @@ struct DsState {
   bool adds_contig = false;  // this batch's adds: every actor's adds one contiguous run
   DevBuf seal_out;           // the compaction's sealed file (ds_compact_device)
   DevBuf tile_col[9];        // the tiled emit's file-minor scratch rows (k_ds_emit<true>)
+  // Orswot op files decoded in the open (k_open_fold_v2's DS form): raw counts, done flags and
+  // the file-major rows (add actor / counter / member, removal actor / counter / member)
+  DevBuf fz_cnt, fz_done, fz_col[6], fz_why;
   // device state reader (per state file: candidates, sorted heads, entry ends, Dot counts and
   // bases, members, sorted members [0..6]
   // and emitted (member, actor id, value) columns [7..9]), pinned staging for its downloads
@@ -1072,10 +1075,42 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
   if ((e = ctx->out.reserve(blob_len + 16ull * n + 128)) || (e = ctx->status.reserve(n * 4ull + 64)) ||
       (e = d->cnt.reserve(2ull * kCntN * n * 4 + 64)))
     return ctx->hip_fail(e, "ingest reserve");
-  // 1) open every file (lib.rs:501-502), plaintext -> HBM
+  // 1) open every file (lib.rs:501-502), plaintext -> HBM; Orswot op files of at most
+  //    kDsFuseRegion bytes are decoded inside the open instead (their plaintext stays in LDS:
+  //    ce_fused.hip ds_fused_decode; CE_DS_FUSED_DECODE=0 turns it off)
   HostPhase hpo("ops: open+gate+count");
+  const bool fused_off = getenv("CE_DS_FUSED_DECODE") && atoi(getenv("CE_DS_FUSED_DECODE")) == 0;  // (tests flip it)
+  const bool fused = c->kind == CE_STATE_ORSWOT && n > 0 && !fused_off;
+  DecodeArgs fz{};
+  if (fused) {
+    constexpr uint32_t kRows = 64;  // ops per file the rows hold (more: the lane-per-file decode)
+    static const uint32_t kEl[6] = {4, 8, 8, 4, 8, 8};
+    if ((e = d->fz_cnt.reserve(4ull * kCntN * n + 64)) || (e = d->fz_done.reserve(n + 64)))
+      return ctx->hip_fail(e, "fused decode");
+    for (int j = 0; j < 6; j++)
+      if ((e = d->fz_col[j].reserve((uint64_t)kRows * n * kEl[j] + 64))) return ctx->hip_fail(e, "fused decode");
+    fz.ds.on = 1;
+    fz.ds.rows = kRows;
+    fz.ds.rawcnt = d->fz_cnt.as<uint32_t>();
+    fz.ds.done = d->fz_done.as<uint8_t>();
+    fz.ds.add_actor = d->fz_col[0].as<uint32_t>();
+    fz.ds.add_ctr = d->fz_col[1].as<unsigned long long>();
+    fz.ds.add_mem = d->fz_col[2].as<unsigned long long>();
+    fz.ds.rm_actor = d->fz_col[3].as<uint32_t>();
+    fz.ds.rm_ctr = d->fz_col[4].as<unsigned long long>();
+    fz.ds.rm_mem = d->fz_col[5].as<unsigned long long>();
+    fz.supported = c->d_supported.as<uint8_t>();
+    fz.n_supported = (uint32_t)c->supported.size();
+    fz.table = c->d_table.as<ActorSlot>();
+    fz.mask = c->cap - 1;
+    if (getenv("CE_DS_FUSE_DEBUG")) {
+      if ((e = d->fz_why.reserve(4ull * n + 64)) || (e = hipMemsetAsync(d->fz_why.p, 0xff, 4ull * n + 4, ctx->stream)))
+        return ctx->hip_fail(e, "fused decode");
+      fz.ds.why = d->fz_why.as<uint32_t>();
+    }
+  }
   if ((rc = device_open(ctx, d_blob, d_offs, n, blob_len, true, key_of(c), ctx->out.as<uint8_t>(),
-                        ctx->status.as<int32_t>(), false, true)))
+                        ctx->status.as<int32_t>(), false, true, fused ? &fz : nullptr)))
     return rc;
   // 2) version gate -> apply flags (decode errors reject the batch whatever the gate says),
   // 3) data version + Vec<S::Op> decode, count pass, 4) bases: one exclusive scan over the kCntN
@@ -1090,6 +1125,10 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
   const FillRange count_counters{d->misses.as<uint32_t>(), 16, 0u};  // the count pass's counters
   if ((rc = gate_enqueue(c, d_fa, d_fv, n, m, wslot, &expect, &gj, &count_counters))) return rc;
   DsDecodeArgs a = decode_args(c, n);
+  if (fused) {
+    a.fdone = fz.ds.done;
+    a.fuse = fz.ds;
+  }
   if ((uint64_t)kCntN * n > 0x7fffffffull) return ctx->fail(CE_ERR_INVALID_ARG, "batch too large for one scan");
   uint32_t* cnt = d->cnt.as<uint32_t>();
   uint32_t* bases = cnt + (size_t)kCntN * n;
@@ -1103,7 +1142,7 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
   bool counters_clear = true;  // the gate's fill cleared them for the first pass
   auto count_pass = [&]() -> int {
     if (n == 0) {
-      std::memset(hsum, 0, 19 * 4);
+      std::memset(hsum, 0, 20 * 4);
       hsum[18] = 0xffffffffu;
       return CE_OK;
     }
@@ -1117,7 +1156,7 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
         (e = launch_ds_col_totals(ctx->stream, cnt, bases, n, d->misses.as<uint32_t>() + 8, ctx->status.as<int32_t>(),
                                   ctx->counters.as<uint32_t>() + 12, d->misses.as<uint32_t>(),
                                   d->cnt_tot.as<uint32_t>())) ||
-        (e = hipMemcpyAsync(hsum, d->cnt_tot.p, 19 * 4, hipMemcpyDeviceToHost, ctx->stream)))
+        (e = hipMemcpyAsync(hsum, d->cnt_tot.p, 20 * 4, hipMemcpyDeviceToHost, ctx->stream)))
       return ctx->hip_fail(e, "count");
     return CE_OK;
   };
@@ -1171,6 +1210,28 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
   // 5) emit (actor ids from the device table; unknown actors -> insert and emit again)
   a = decode_args(c, n);
   a.cnt = d->cnt.as<uint32_t>() + (size_t)kCntN * n;  // bases
+  const uint32_t n_fused = fused ? hsum[19] : 0;  // files the open decoded
+  if (fz.ds.why) {
+    std::vector<uint32_t> w(n + 1);
+    if (hipMemcpy(w.data(), fz.ds.why, 4ull * (n + 1), hipMemcpyDeviceToHost) == hipSuccess) {
+      std::map<uint32_t, uint32_t> h;
+      for (uint32_t i = 0; i < n; i++) h[w[i] & 0xffff]++;
+      fprintf(stderr, "[ds fused decode] n=%u fused=%u file0: cnt %u p0 %u nc %u; why:", n, n_fused, w[n] >> 16,
+              (w[n] >> 8) & 0xff, w[n] & 0xff);
+      for (auto& x : h) fprintf(stderr, " %x:%u", x.first, x.second);
+      fprintf(stderr, " (file 0 %08x)\n", w[0]);
+    }
+  }
+  if (n_fused) {
+    a.fdone = fz.ds.done;
+    a.fuse = fz.ds;
+    for (int j = 0; j < kCntN; j++) {  // the untile's last-tile bound and LDS rows
+      a.tile.total[j] = (uint32_t)k.v[j];
+      a.tile.max_rows = std::max<uint32_t>(a.tile.max_rows, (uint32_t)kmax.v[j]);
+    }
+    c->path_counts["ds_fused_decode"]++;
+    c->path_counts["ds_fused_files"] += n_fused;
+  }
   for (int j = 0; j < kCntN; j++) a.base_off[j] = (uint32_t)base.v[j];
   // Orswot: the tiled emit (file-minor scratch rows, then k_ds_untile) when every file's counts
   // fit its LDS tile and the rows cost at most ~2x the columns (files of similar shape, as op
@@ -1207,7 +1268,7 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
     // round 0: k_ds_col_totals (the last kernel of the count pass) cleared misses[0..8)
     if (round > 0 && (e = hipMemsetAsync(d->misses.p, 0, 64, ctx->stream))) return ctx->hip_fail(e, "emit");
     const int te = ctx->tbegin("ds_emit");
-    if ((e = launch_ds_emit(ctx->stream, a))) return ctx->hip_fail(e, "emit");
+    if ((e = launch_ds_emit(ctx->stream, a, n_fused < n))) return ctx->hip_fail(e, "emit");
     ctx->tend(te);
     // are every actor's adds one contiguous run (load_ops order, each writer adding its own
     // dots)?  Then the fold's applied flags need no sort (orswot_fold); the flag rides in

@@ -861,6 +861,267 @@ __device__ __forceinline__ FilePre2 load_pre2(const DecodeArgs& a, uint32_t f) {
   return p;
 }
 
+// ---- Orswot op files decoded in the open (k_open_fold_v2's DS form) ------------------------
+// C3's op files (~2 KiB of plaintext, 32 ops) used to go open -> plaintext in HBM -> a lane-per-
+// file count pass -> scan -> a lane-per-file emit, reading the plaintext twice.  In the DS form a
+// file of at most kDsFuseRegion bytes keeps its plaintext in LDS after the open and its 16 lanes
+// decode it there (read_remote_ops' from_slice, crdt-enc/src/lib.rs:507, of a Vec<orswot::Op>):
+//   1. the supported data version (lib.rs:504-505) and the Vec header (fixarray / array16 / 32);
+//   2. candidate op starts: every byte position whose word is Add's or Rm's first four bytes
+//      (81 a3 "Ad" / 81 a2 "Rm"), lane sub scanning dwords sub, sub + 16, ... (in order);
+//   3. a lane per candidate proves the canonical form ce_dotset.hip's fast_orswot_op accepts
+//      (one member; a one-entry clock; any uint width), resolves its actor (a one-entry cache,
+//      then the table), and writes its row: op k of file f at col[f * rows + k];
+//   4. the proven ops must be exactly the Vec's elements: as many as the header says, the first
+//      where the header ends, each starting where the previous one ends.  A spurious proven
+//      candidate inside an op, an op of another form, an unknown actor, a count past the rows,
+//      any of it: the file's plaintext goes to HBM and the lane-per-file decode takes it
+//      (done[f] = 0), so every file gets exactly the reference grammar's result.
+// The offsets columns (add_mbeg, rm_cbeg, rm_mbeg) are not written: with one member / one clock
+// entry per op they are the op's index plus the file's base (k_ds_untile adds it).
+static constexpr uint32_t kDsStride = kDsFuseRegion + 96;  // plaintext + the windows' over-reads
+static constexpr uint32_t kDsCandCap = 96;                  // candidate op starts per file
+static constexpr uint32_t kDsVCap = 64;                     // proven ops per file (>= 47 B each)
+static constexpr uint32_t kDsAuxHalves = kDsCandCap + 2 * kDsVCap;  // u16: cand, vpos, vlen
+static constexpr uint32_t kAddMagic = 0x6441a381u;  // 81 a3 'A' 'd'
+static constexpr uint32_t kRmMagic = 0x6d52a281u;   // 81 a2 'R' 'm'
+
+// N LE words at byte x of a dword-aligned LDS region L (any alignment of x): N + 1 aligned dword
+// reads shifted into place (indexed from L, so they stay LDS reads, not flat ones)
+template <int N>
+struct LdsWin {
+  uint32_t w[N];
+  __device__ __forceinline__ LdsWin(const uint32_t* L, uint32_t x) {
+    const uint32_t* b = L + (x >> 2);
+    const uint32_t sh = x & 3u;
+    uint32_t d[N + 1];
+#pragma unroll
+    for (int k = 0; k <= N; k++) d[k] = b[k];
+#pragma unroll
+    for (int k = 0; k < N; k++) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+  }
+  __device__ __forceinline__ uint32_t word(int b) const {  // bytes [b, b + 4), b compile-time
+    return (b & 3) ? __builtin_amdgcn_alignbyte(w[(b >> 2) + 1], w[b >> 2], b & 3) : w[b >> 2];
+  }
+  __device__ __forceinline__ uint32_t byte(int b) const { return (w[b >> 2] >> (8 * (b & 3))) & 0xffu; }
+  // msgpack uint at byte b (positive fixint, cc, cd, ce, cf); *len = its size, 0 for another form
+  __device__ __forceinline__ unsigned long long uint_at(int b, uint32_t* len) const {
+    const uint32_t m = byte(b);
+    const uint32_t x0 = __builtin_bswap32(word(b + 1)), x1 = __builtin_bswap32(word(b + 5));
+    *len = m < 0x80u ? 1u : m == 0xccu ? 2u : m == 0xcdu ? 3u : m == 0xceu ? 5u : m == 0xcfu ? 9u : 0u;
+    return m < 0x80u ? m : m == 0xccu ? x0 >> 24 : m == 0xcdu ? x0 >> 16 : m == 0xceu ? x0
+                                                       : ((unsigned long long)x0 << 32) | x1;
+  }
+};
+
+struct DsOp {
+  uint32_t kind;  // 1 Add, 2 Rm, 0 not proven
+  uint32_t len, u0, u1, u2, u3;
+  unsigned long long ctr, mem;
+};
+
+// the op at byte x of a file's plaintext in LDS (len bytes), in the forms rmp-serde's
+// to_vec_named writes for a one-member Add / a one-entry-clock Rm:
+//   Add: 81 a3"Add" 82 a3"dot" 82 a5"actor" c4 10 <uuid> a7"counter" <uint> a7"members" 91 <uint>
+//   Rm:  81 a2"Rm" 82 a5"clock" 81 a4"dots" 81 c4 10 <uuid> <uint> a7"members" 91 <uint>
+__device__ __forceinline__ DsOp ds_parse_fast(const uint32_t* L, uint32_t x, uint32_t len) {
+  DsOp o{};
+  const LdsWin<13> v(L, x);  // bytes x .. x + 51
+  uint32_t l = 0, y = 0;
+  if (v.w[0] == kAddMagic && v.w[1] == 0x64a38264u && v.w[2] == 0xa582746fu && v.w[3] == 0x6f746361u &&
+      (v.w[4] & 0xffffffu) == 0x10c472u && v.word(35) == 0x756f63a7u && v.word(39) == 0x7265746eu) {
+    o.ctr = v.uint_at(43, &l);
+    o.u0 = v.word(19); o.u1 = v.word(23); o.u2 = v.word(27); o.u3 = v.word(31);
+    y = 43 + l;
+    o.kind = l ? 1u : 0u;
+  } else if (v.w[0] == kRmMagic && v.w[1] == 0x6c63a582u && v.w[2] == 0x816b636fu && v.w[3] == 0x746f64a4u &&
+             v.w[4] == 0x10c48173u) {
+    o.ctr = v.uint_at(36, &l);
+    o.u0 = v.w[5]; o.u1 = v.w[6]; o.u2 = v.w[7]; o.u3 = v.w[8];
+    y = 36 + l;
+    o.kind = l ? 2u : 0u;
+  }
+  if (o.kind) {
+    const LdsWin<5> m(L, x + y);  // "a7 members 91" <uint>: bytes y .. y + 19
+    uint32_t lm = 0;
+    if (m.word(0) == 0x6d656da7u && m.word(4) == 0x73726562u && m.byte(8) == 0x91u) o.mem = m.uint_at(9, &lm);
+    o.len = y + 9 + lm;
+    if (!lm || x + o.len > len) o.kind = 0;
+  }
+  return o;
+}
+
+// the dot-set actor id (ActorSlot.pad[0]) of a UUID through a one-entry per-lane cache
+struct DsActorCache {
+  uint32_t k0 = 0, k1 = 0, k2 = 0, k3 = 0, id = 0xffffffffu;
+  uint4 pk = make_uint4(0, 0, 0, 0);  // prime: the first probe's slot of the first op's UUID
+  uint32_t pused = 0, pid = 0xffffffffu;
+  // the first op's UUID (bytes 19.. of an Add, 20.. of an Rm at p0) and its first table probe,
+  // loaded but not waited for; get() takes it when the slot holds that UUID
+  __device__ __forceinline__ void prime(const DecodeArgs& a, const uint32_t* L, uint32_t p0, uint32_t len) {
+    if (p0 + 40 > len) return;
+    const LdsWin<6> w(L, p0);
+    const uint32_t u = w.byte(1) == 0xa3u ? 19u : 20u;
+    const LdsWin<4> v(L, p0 + u);
+    k0 = v.w[0]; k1 = v.w[1]; k2 = v.w[2]; k3 = v.w[3];
+    const ActorSlot& sl = a.table[actor_hash(k0, k1, k2, k3) & a.mask];
+    pk = *reinterpret_cast<const uint4*>(sl.k);
+    pused = sl.used;
+    pid = sl.pad[0];
+  }
+  __device__ __forceinline__ uint32_t get(const DecodeArgs& a, const DsOp& o) {
+    if (pused && o.u0 == k0 && o.u1 == k1 && o.u2 == k2 && o.u3 == k3 && pk.x == k0 && pk.y == k1 && pk.z == k2 &&
+        pk.w == k3) {
+      pused = 0;
+      id = pid;
+    }
+    if (id != 0xffffffffu && o.u0 == k0 && o.u1 == k1 && o.u2 == k2 && o.u3 == k3) return id;
+    const uint32_t h = lookup_slot(a.table, a.mask, o.u0, o.u1, o.u2, o.u3);
+    if (h == 0xffffffffu) return h;
+    k0 = o.u0; k1 = o.u1; k2 = o.u2; k3 = o.u3;
+    id = a.table[h].pad[0];
+    return id;
+  }
+};
+
+// steps 1-4 above for the file of this lane group (act: its tag verified and its plaintext is
+// in LDS at fl); returns whether the file was decoded (group-uniform).  Wave-uniform control flow.
+template <int LPF>
+__device__ __forceinline__ bool ds_fused_decode(const DecodeArgs& a, const SupVers& sup, const uint8_t* fl,
+                                                uint16_t* aux, uint32_t len, bool act, uint32_t f, uint32_t grp,
+                                                uint32_t sub) {
+  DsActorCache cache;  // per file (a file's ops are mostly its writer's)
+  static_assert(LPF <= 32, "group ballots are taken as 32-bit masks");
+  const DsFuse& x = a.ds;
+  const uint32_t* L = reinterpret_cast<const uint32_t*>(fl);
+  const uint32_t lt = (1u << sub) - 1u;
+  auto gb = [&](bool p) { return (uint32_t)grp_bits<LPF>(p, grp); };
+  __syncthreads();  // the open's plaintext stores (one wave per workgroup)
+  // 1) data version and Vec header
+  bool ok = act && len >= 17;
+  uint32_t cnt = 0, p0 = 0;
+  if (ok) {
+    const uint4 dv = *reinterpret_cast<const uint4*>(fl);
+    const uint32_t w4 = L[4], w5 = L[5];
+    const uint32_t h = w4 & 0xffu;
+    ok = sup.has(a, dv);
+    if ((h & 0xf0u) == 0x90u) {
+      cnt = h & 15u;
+      p0 = 17;
+    } else if (h == 0xdcu) {
+      cnt = (((w4 >> 8) & 0xffu) << 8) | ((w4 >> 16) & 0xffu);
+      p0 = 19;
+    } else if (h == 0xddu) {
+      cnt = __builtin_bswap32(__builtin_amdgcn_alignbyte(w5, w4, 1));
+      p0 = 21;
+    } else {
+      ok = false;
+    }
+    ok = ok && p0 <= len && cnt <= kDsVCap;
+  }
+  // the first op's actor (the file's writer, usually every op's): its first table probe issued now,
+  // so the load lands during the scan (DsActorCache::prime)
+  if (ok) cache.prime(a, L, p0, len);
+  // 2) candidate op starts, in position order: positions whose bytes are 81 a2 / 81 a3 (an Add's or
+  //    Rm's first two bytes; the proof in step 3 checks the rest).  Branch-free SWAR over two dwords
+  //    per lane per round: g's byte j is zero iff byte j == 0x81 and byte j + 1 is a2 / a3, found
+  //    exactly (no borrow between bytes); a dword holds at most two such positions (a member's
+  //    last bytes can spell 81 a2 just before the next op).  Positions before p0 or past len are
+  //    left to step 3 and the chain check (nothing there proves, or the chain fails and the lane
+  //    decode takes the file).
+  uint16_t* cand = aux;
+  uint32_t nc = 0;
+  const uint32_t dbeg = p0 >> 2, dend = (len + 3) >> 2;
+  auto zbytes = [](uint32_t A, uint32_t B) {  // bit 8j + 7: bytes (j, j + 1) = 81, a2|a3
+    const uint32_t g = (A ^ 0x81818181u) | ((__builtin_amdgcn_alignbyte(B, A, 1) ^ 0xa2a2a2a2u) & 0xfefefefeu);
+    return ~(((g & 0x7f7f7f7fu) + 0x7f7f7f7fu) | g) & 0x80808080u;
+  };
+  for (uint32_t r = 0; __any(ok && dbeg + r < dend); r += 2 * LPF) {
+    const uint32_t d = dbeg + r + 2 * sub;
+    unsigned long long m = 0;
+    if (ok && d < dend) {
+      const uint32_t A = L[d], B = L[d + 1], Cw = L[d + 2];
+      m = ((unsigned long long)zbytes(B, Cw) << 32) | zbytes(A, B);
+    }
+    // this lane's candidates (0..4) go after every lower lane's: a group prefix sum by bit planes
+    const uint32_t c = (uint32_t)__popcll(m);
+    const uint32_t b0 = gb(c & 1u), b1 = gb(c & 2u), b2 = gb(c & 4u);
+    uint32_t idx = nc + __popc(b0 & lt) + 2 * __popc(b1 & lt) + 4 * __popc(b2 & lt);
+    while (m) {
+      if (idx < kDsCandCap) cand[idx] = (uint16_t)(4 * d + ((uint32_t)__builtin_ctzll(m) >> 3));
+      idx++;
+      m &= m - 1;
+    }
+    nc += __popc(b0) + 2 * __popc(b1) + 4 * __popc(b2);
+  }
+  ok = ok && nc <= kDsCandCap;
+  __syncthreads();
+  // 3) prove the candidates, rank the proven ones, write their rows
+  uint16_t* vpos = aux + kDsCandCap;
+  uint16_t* vlen = vpos + kDsVCap;
+  uint32_t nv = 0, na = 0, nr = 0;
+  bool miss = false;
+  const size_t row0 = (size_t)f * x.rows;
+  for (uint32_t r = 0; __any(ok && r < nc); r += LPF) {
+    const uint32_t i = r + sub;
+    DsOp o{};
+    uint32_t pos = 0;
+    if (ok && i < nc) {
+      pos = cand[i];
+      o = ds_parse_fast(L, pos, len);
+    }
+    const bool v = o.kind != 0;
+    const uint32_t vb = gb(v), ab = gb(o.kind == 1), rb = gb(o.kind == 2);
+    const uint32_t k = nv + __popc(vb & lt), ka = na + __popc(ab & lt), kr = nr + __popc(rb & lt);
+    if (v) {
+      if (k < kDsVCap) {
+        vpos[k] = (uint16_t)pos;
+        vlen[k] = (uint16_t)o.len;
+      }
+      const uint32_t id = cache.get(a, o);
+      miss = miss || id == 0xffffffffu;
+      if (o.kind == 1 && ka < x.rows) {
+        x.add_actor[row0 + ka] = id;
+        x.add_ctr[row0 + ka] = o.ctr;
+        x.add_mem[row0 + ka] = o.mem;
+      } else if (o.kind == 2 && kr < x.rows) {
+        x.rm_actor[row0 + kr] = id;
+        x.rm_ctr[row0 + kr] = o.ctr;
+        x.rm_mem[row0 + kr] = o.mem;
+      }
+    }
+    nv += __popc(vb);
+    na += __popc(ab);
+    nr += __popc(rb);
+  }
+  __syncthreads();
+  // 4) the proven ops are the Vec's elements, back to back from the header
+  bool chain = ok && nv == cnt && na <= x.rows && nr <= x.rows && gb(miss) == 0;
+  for (uint32_t r = 0; __any(chain && r < nv); r += LPF) {
+    const uint32_t k = r + sub;
+    bool bad = false;
+    if (chain && k < nv) {
+      const uint32_t e = (uint32_t)vpos[k] + vlen[k];
+      bad = (k == 0 && vpos[0] != p0) || (k + 1 < nv && vpos[k + 1] != e) || e > len;
+    }
+    chain = chain && gb(bad) == 0;
+  }
+  if (x.why && sub == 0 && act) {
+    x.why[f] = !ok ? 1u + (nc > kDsCandCap) : nv != cnt ? 3u + (nv > cnt) * 0x100u + (nv << 16) : na > x.rows || nr > x.rows ? 4u
+               : gb(miss) ? 5u : chain ? 0u : 6u;
+    if (f == 0) x.why[a.n] = (cnt << 16) | (p0 << 8) | nc;
+  }
+  if (chain && sub == 0) {
+    const size_t n = a.n;
+    x.rawcnt[f] = na;
+    x.rawcnt[n + f] = na;
+    x.rawcnt[2 * n + f] = nr;
+    x.rawcnt[3 * n + f] = nr;
+    x.rawcnt[4 * n + f] = nr;
+  }
+  return chain;
+}
+
 // W = waves per SIMD the VGPR budget is sized for (LDS allows 2.5 at LPF 16, 5 at LPF 32).
 // OPT bits: 1 = rot16 as two SDWA xors (ce_device.h xor_rotl16_t), 2 = the next iteration's
 // ciphertext loads issued inside this iteration's decode (after its first round, with the
@@ -871,9 +1132,13 @@ __device__ __forceinline__ FilePre2 load_pre2(const DecodeArgs& a, uint32_t f) {
 // DEC = false: open only (EncHandler::decrypt, xchacha lib.rs:73-101) -- plaintext pieces go to
 // HBM at the file's out_off instead of LDS, the tag check sets the status, nothing is decoded
 // (the dot-set ingest decodes the plaintext afterwards).
-template <int LPF, int W, bool JIT, int OPT = 3, bool DEC = true>
+// DS (with DEC = false): Orswot op files of at most kDsFuseRegion bytes keep their plaintext in LDS
+// and are decoded there (ds_fused_decode); larger ones, and any the decode does not prove, get
+// their plaintext in HBM as in the open-only form.
+template <int LPF, int W, bool JIT, int OPT = 3, bool DEC = true, bool DS = false>
 __global__ __launch_bounds__(64, W)
 void k_open_fold_v2(DecodeArgs a) {
+  static_assert(!(DEC && DS), "the DS form is an open-only form");
 #if !CE_FUSED_DIAG
   static_assert((OPT & ~3) == 0, "k_open_fold_v2 diagnostics variants exist only in the diagnostics build");
 #endif
@@ -890,10 +1155,12 @@ void k_open_fold_v2(DecodeArgs a) {
   using C = V2Cfg<LPF>;
   constexpr int F = C::F;
   constexpr int BPL = C::BPL;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[DEC ? (F - 1) * kRegionStride2 + kRegion2 + 64 : 16];
+  __shared__ __attribute__((aligned(16))) uint8_t
+      lds[DEC ? (F - 1) * kRegionStride2 + kRegion2 + 64 : DS ? F * kDsStride + F * kDsAuxHalves * 2 : 16];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t grp = lane / LPF, sub = lane % LPF;
-  uint8_t* fl = lds + grp * kRegionStride2;
+  uint8_t* fl = lds + grp * (DS ? kDsStride : kRegionStride2);
+  uint16_t* aux = DS ? reinterpret_cast<uint16_t*>(lds + F * kDsStride) + grp * kDsAuxHalves : nullptr;
   const uint32_t ngroups = (a.n + F - 1) / F;
   const uint32_t stride = gridDim.x;
   uint32_t g = bcast(blockIdx.x);
@@ -963,6 +1230,7 @@ void k_open_fold_v2(DecodeArgs a) {
     if (PF1 && !DP) nx = load_pre2(a, (g + stride) * F + grp);  // issued before this iteration's loads
     const bool act = cur.ok && cur.len <= kSmallMax;
     const uint32_t len = act ? cur.len : 0u;
+    const bool dsl = DS && act && len <= kDsFuseRegion;  // DS: plaintext into LDS
     const uint32_t npc = (len + 15) >> 4;             // ciphertext Poly1305 blocks
     const int32_t nblk = (int32_t)((len + 63) >> 6);  // ChaCha20 blocks
     const FileParams* Pp = a.params + (act ? f : 0);
@@ -1053,6 +1321,8 @@ void k_open_fold_v2(DecodeArgs a) {
         if (DEC) {
           const uint32_t st_off = has ? q * 16u : kRegion2 - 16u;
           *reinterpret_cast<uint4*>(fl + st_off) = pv;
+        } else if (dsl) {
+          if (has) *reinterpret_cast<uint4*>(fl + q * 16u) = pv;  // q < 4 nblk <= 128
         } else if (act && has && q * 16u < len) {
           // out_off is 16-aligned and the next file's plaintext starts >= 99 B past this one's
           // end (its header, envelope and tag), so the zero-padded tail piece is a whole store
@@ -1159,6 +1429,16 @@ void k_open_fold_v2(DecodeArgs a) {
     // 4) data-version check, decode from LDS, fold; the next iteration's parameters are loaded
     //    inside (their latency hides under the decode)
     if (!DEC) {
+      if (DS) {
+        bool done = false;
+        if (__any(dsl && ok)) done = ds_fused_decode<LPF>(a, sup, fl, aux, len, dsl && ok, f, grp, sub);
+        if (dsl && ok && !done) {  // the lane-per-file decode reads it from HBM
+          for (uint32_t q = sub; q * 16u < len; q += LPF)
+            *reinterpret_cast<uint4*>(gout + q * 16u) = *reinterpret_cast<const uint4*>(fl + q * 16u);
+        }
+        if (sub == 0 && f < a.n) a.ds.done[f] = done ? 1 : 0;
+        __syncthreads();  // the next iteration's plaintext overwrites the regions
+      }
       (void)ok;
       nx = load_pre2(a, (g + stride) * F + grp);
     } else
@@ -1191,15 +1471,15 @@ void k_open_fold_v2(DecodeArgs a) {
 #endif
 }
 
-template <int LPF, int W, bool JIT, int OPT = 3, bool DEC = true>
+template <int LPF, int W, bool JIT, int OPT = 3, bool DEC = true, bool DS = false>
 static void launch_v2(hipStream_t s, const DecodeArgs& a, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr) {
-  static const uint32_t res = resident_blocks(k_open_fold_v2<LPF, W, JIT, OPT, DEC>, 64);
+  static const uint32_t res = resident_blocks(k_open_fold_v2<LPF, W, JIT, OPT, DEC, DS>, 64);
   const uint32_t groups = (a.n + 64 / LPF - 1) / (64 / LPF);
   const dim3 grid(std::min<uint32_t>(groups, res));
   if (t0) {  // the launch's own start / end timestamps: no marker packets around the kernel
-    hipExtLaunchKernelGGL((k_open_fold_v2<LPF, W, JIT, OPT, DEC>), grid, dim3(64), 0, s, t0, t1, 0u, a);
+    hipExtLaunchKernelGGL((k_open_fold_v2<LPF, W, JIT, OPT, DEC, DS>), grid, dim3(64), 0, s, t0, t1, 0u, a);
   } else {
-    hipLaunchKernelGGL((k_open_fold_v2<LPF, W, JIT, OPT, DEC>), grid, dim3(64), 0, s, a);
+    hipLaunchKernelGGL((k_open_fold_v2<LPF, W, JIT, OPT, DEC, DS>), grid, dim3(64), 0, s, a);
   }
 }
 
@@ -1207,7 +1487,11 @@ static void launch_v2(hipStream_t s, const DecodeArgs& a, hipEvent_t t0 = nullpt
 // a.only / a.apply unused.  Larger files: k_segments with skip_small (their setup's list).
 hipError_t launch_open_small_v2(hipStream_t s, const DecodeArgs& a) {
   if (a.n == 0) return hipSuccess;
-  launch_v2<16, 3, false, 1, false>(s, a);
+  // the DS form's VGPR budget: CE_DS_FUSED_W=3 (same-box A/B) or 2 waves per SIMD
+  static const int dsw = getenv("CE_DS_FUSED_W") ? atoi(getenv("CE_DS_FUSED_W")) : 3;
+  if (a.ds.on && dsw == 3) launch_v2<16, 3, false, 1, false, true>(s, a);
+  else if (a.ds.on) launch_v2<16, 2, false, 1, false, true>(s, a);
+  else launch_v2<16, 3, false, 1, false>(s, a);
   return hipGetLastError();
 }
 

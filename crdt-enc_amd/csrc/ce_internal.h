@@ -221,7 +221,10 @@ int device_open_setup(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs
 SegScratch segscratch(ce_ctx* ctx, uint32_t extra_cap);
 int device_open(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,
                 uint64_t blob_len, bool outer, const KeyRef& key, uint8_t* d_out,
-                int32_t* d_status, bool sync_counters, bool small_lanes = false);
+                int32_t* d_status, bool sync_counters, bool small_lanes = false,
+                const DecodeArgs* ds = nullptr);
+// (ds: small_lanes only -- Orswot op files decoded in the open: ds->ds, supported / n_supported,
+// table / mask are taken from it; ce_fused.hip ds_fused_decode)
 
 // Seal n clear texts resident in HBM.  d_out_offs[i] = output start of file i.
 // counters_ready: the caller's kernel already reset ctx's counter block (k_compact_prologue)

@@ -97,6 +97,26 @@ hipError_t launch_finalize_multi(hipStream_t s, bool seal, uint8_t* out, const F
 
 // decode Vec<Dot<Uuid>> of every opened file and max-fold the dots of applied files into
 // batch_counters (dense by actor slot).  One wavefront per file.
+// Orswot op files decoded inside the open (k_open_fold_v2's DS form; ce_fused.hip
+// ds_fused_decode): a file of at most kDsFuseRegion plaintext bytes whose ops are all the
+// canonical one-member Add / one-entry-clock Rm forms has its op columns written as file-major
+// rows (op k of file f at col[f * rows + k]) and its counts into rawcnt; any other file has its
+// plaintext stored to HBM for the lane-per-file decode (done[f] = 0).
+static constexpr uint32_t kDsFuseRegion = 2048;
+struct DsFuse {
+  int on;
+  uint32_t rows;                 // rows per file (<= 96)
+  uint32_t* rawcnt;              // [5][n]: adds, add members, removals, removal clock entries, removal members
+  uint8_t* done;                 // [n]
+  uint32_t* add_actor;           // dot-set actor ids (ActorSlot.pad[0])
+  unsigned long long* add_ctr;
+  unsigned long long* add_mem;
+  uint32_t* rm_actor;
+  unsigned long long* rm_ctr;
+  unsigned long long* rm_mem;
+  uint32_t* why;                 // diagnostics (CE_DS_FUSE_DEBUG=1): per file, the step that declined it
+};
+
 struct DecodeArgs {
   const uint8_t* pt;            // plaintext blob (FileParams.out_off / len)
   const FileParams* params;
@@ -122,6 +142,7 @@ struct DecodeArgs {
   uint8_t* redo;                // k_segdec_apply: files left to the whole-file decode
   int nil_actor;                // the nil UUID is in the actor table: lookups take the two-load
                                 // probe (lookup_slot1)
+  DsFuse ds;                    // launch_open_small_v2: Orswot ops decoded in the open (ds.on)
 };
 hipError_t launch_decode_dots(hipStream_t s, const DecodeArgs& a, uint32_t grid_waves);
 // diagnostics: shader clock vs the reference clock (ce_ctx_clock_probe)

@@ -592,7 +592,7 @@ def test_orswot_op_fast_path_boundaries(ctx, case):
     windows (ce_dotset.hip fast_orswot_op) and hands every other form to the grammar from the
     same op on: each uint width, multi-member / multi-entry ops between fast ones, a signed
     marker, a field-name near miss and a file cut inside its last op -- all == oracle."""
-    rng = random.Random(hash(case) & 0xffff)
+    rng = random.Random(sum(map(ord, case)))
     key = rng.randbytes(32)
     actors = sorted(rng.randbytes(16) for _ in range(3))
     widths = ["fix", "cc", "cd", "ce", "cf"]
@@ -1035,3 +1035,103 @@ def test_scan_forms_equal(ctx):
         assert r.returncode == 0, r.stderr[-2000:]
         outs[mode] = r.stdout.strip().splitlines()[-1]
     assert outs["two"] == outs["three"] == outs["hipcub"] == want, outs
+
+
+def _canonical_orswot(rng, actors, n_versions, ops_per_file, members, widths=(1, 2, 3, 5, 9), p_rm=0.2):
+    """Op files whose ops are all the forms the open's decode proves: one-member Adds of the
+    writer's own dots, removals with a one-entry clock {writer: an earlier counter}; counters and
+    members drawn from every msgpack uint width (fixint, cc, cd, ce, cf)."""
+    lim = {1: (0, 127), 2: (128, 255), 3: (256, 65535), 5: (65536, (1 << 32) - 1), 9: (1 << 32, (1 << 64) - 1)}
+    files = {a: [] for a in actors}
+    ctr = {a: 0 for a in actors}
+    for _ in range(n_versions):
+        for a in actors:
+            ops = []
+            for _ in range(ops_per_file):
+                w = rng.choice(widths)
+                lo, hi = lim[w]
+                if ctr[a] and rng.random() < p_rm:
+                    ops.append(("Rm", C.VClock({a: rng.randint(1, ctr[a])}), [rng.randrange(members)]))
+                else:
+                    ctr[a] = max(ctr[a] + 1, rng.randint(lo, hi))
+                    mem = rng.randrange(members) if rng.random() < 0.5 else rng.randint(*lim[rng.choice(widths)])
+                    ops.append(("Add", (a, ctr[a]), [mem]))
+            files[a].append(ops)
+    return files
+
+
+@pytest.mark.parametrize("case", ["canonical", "well_formed", "adversarial", "large_files", "spurious_magic",
+                                  "foreign_actor", "trailing", "bad_version", "tampered"])
+def test_orswot_fused_decode_equals_lane_decode(ctx, case):
+    """Orswot op files decoded inside the open (k_open_fold_v2's DS form: the plaintext stays in
+    LDS, 16 lanes per file prove the canonical ops and write their rows) == the lane-per-file
+    decode from HBM (CE_DS_FUSED_DECODE=0) == the oracle: statuses, return code and state bytes.
+    The cases mix files the open proves with files it must hand to the lane decode: removals
+    with several clock entries and several members (well_formed / adversarial), files past
+    kDsFuseRegion (large_files), member values whose bytes spell an op's first word (a candidate
+    the decode must drop), ops naming actors outside the table (foreign_actor: the emit's miss
+    rounds), bytes after the Vec (ignored by from_slice), an unsupported data version and a
+    flipped tag bit."""
+    rng = random.Random(sum(map(ord, case)))
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 12)
+    if case == "canonical":
+        files = _canonical_orswot(rng, actors, 6, 24, 300)
+    elif case == "well_formed":
+        files = G.well_formed_orswot(rng, actors, 5, 20, 200, max_members=1)[0]
+    elif case == "adversarial":
+        files = gen("orswot", rng, actors, 5, 12, 200, True)
+    elif case == "large_files":
+        files = _canonical_orswot(rng, actors, 3, 60, 300)          # ~3.5 KiB: past the LDS region
+        files.update(_canonical_orswot(rng, actors[:4], 3, 20, 300))
+    elif case == "spurious_magic":
+        files = _canonical_orswot(rng, actors, 4, 16, 300)
+        a = actors[0]
+        # ce members 0x81a34164 / 0x81a2526d: bytes 81 a3 41 64 / 81 a2 52 6d inside an op
+        files[a][1][2] = ("Add", (a, 10 ** 9), [0x81A34164])
+        files[a][2][3] = ("Add", (a, 10 ** 9 + 1), [0x81A2526D])
+        files[a][3] = [op if op[0] == "Rm" else ("Add", op[1], [0x81A34164A3646F74]) for op in files[a][3]]
+        # members ending in 81 a2 / 81 a3 right before the next op: two prefixes in one dword
+        b = actors[1]
+        files[b][0] = [op if op[0] == "Rm" else ("Add", op[1], [rng.choice([0x123481A2, 0x81A3, 0x81A2])])
+                       for op in files[b][0]]
+    elif case == "foreign_actor":
+        files = _canonical_orswot(rng, actors, 4, 16, 300)
+        stranger = rng.randbytes(16)
+        files[actors[2]][1][0] = ("Add", (stranger, 5), [42])
+        files[actors[3]][2][1] = ("Rm", C.VClock({stranger: 3}), [42])
+    else:
+        files = _canonical_orswot(rng, actors, 4, 16, 300)
+    acts, clears, fa, fv = G.batch(files, "orswot", APP)
+    if case == "trailing":
+        clears = [c + rng.randbytes(rng.randint(1, 90)) if i % 3 == 0 else c for i, c in enumerate(clears)]
+    if case == "bad_version":
+        clears[7] = bytes(16) + clears[7][16:]
+    sealed = seal_files(ctx, key, clears)
+    if case == "tampered":
+        b = bytearray(sealed[5])
+        b[-1] ^= 1
+        sealed[5] = bytes(b)
+    oc = C.Core("orswot")
+    want = oc.read_remote_ops(key, [APP], sealed, [acts[i] for i in fa], fv)
+    got = {}
+    for fused in (True, False):
+        os.environ["CE_DS_FUSED_DECODE"] = "1" if fused else "0"
+        try:
+            core = new_core(ctx, "orswot", key)
+            got[fused] = (core.ingest_ops(sealed, acts, fa, fv), core.state_bytes(), core.path_count("ds_fused_files"))
+            core.close()
+        finally:
+            os.environ.pop("CE_DS_FUSED_DECODE", None)
+    assert got[True][:2] == got[False][:2]
+    assert got[True][0] == want and got[True][1] == oc.serialize()
+    assert got[False][2] == 0
+    n = len(sealed)
+    if case in ("canonical", "trailing", "spurious_magic"):
+        assert got[True][2] == n          # every file proven in the open
+    elif case in ("bad_version", "tampered"):
+        assert want[0] != 0
+    elif case == "large_files":
+        assert 0 < got[True][2] < n
+    elif case in ("well_formed", "foreign_actor"):
+        assert 0 < got[True][2] < n
