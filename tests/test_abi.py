@@ -103,10 +103,12 @@ def test_product_library_has_no_diagnostic_kernel_variants():
     status 77) -- live only in libcrdtenc_prof.so (CE_FUSED_DIAG), so no environment variable
     can select them from the product."""
     raw = open(os.path.join(REPO, "crdt-enc_amd", "libcrdtenc.so"), "rb").read()
-    found = set(re.findall(rb"k_open_fold_v2ILi(\d+)ELi(\d+)ELb([01])ELi(\d+)ELb([01])E", raw))
+    found = set(re.findall(rb"k_open_fold_v2ILi(\d+)ELi(\d+)ELb([01])ELi(\d+)ELb([01])ELb([01])E", raw))
     assert found, "no k_open_fold_v2 instantiation found in the product library"
-    opts = {(int(l), int(w), int(j), int(o), int(d)) for l, w, j, o, d in found}
-    assert opts <= {(16, 2, 0, 1, 1), (32, 3, 0, 3, 1), (16, 3, 0, 1, 0)}, sorted(opts)
+    opts = {tuple(int(x) for x in t) for t in found}
+    # (LPF, waves, JIT, OPT, DEC, DS): the C2 kernel, its 2-files-per-wave form, the open-only
+    # form and the open-only form with the Orswot op decode (DS)
+    assert opts <= {(16, 2, 0, 1, 1, 0), (32, 3, 0, 3, 1, 0), (16, 3, 0, 1, 0, 0), (16, 3, 0, 1, 0, 1)}, sorted(opts)
     assert not re.search(rb"decode_foldILi\d+ELi[1-9]", raw)
 
 
