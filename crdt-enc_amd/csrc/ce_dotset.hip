@@ -574,7 +574,28 @@ __global__ void __launch_bounds__(kBlock) k_ds_untile(DsDecodeArgs a) {
       ob[threadIdx.x] = i < a.n ? a.cnt[(size_t)og * a.n + i] - a.cnt[(size_t)og * a.n] + a.base_off[og] : 0u;
     }
   }
-  __syncthreads();
+  // every file of the tile decoded in the open (the usual case when any was): each output entry
+  // reads its file's row directly -- a file's entries are contiguous there -- no staging
+  const bool alldone = __syncthreads_and(threadIdx.x >= 64 || i0 + threadIdx.x >= a.n || sdone[threadIdx.x]);
+  const void* fsrc = c == 0 ? (const void*)a.fuse.add_actor : c == 1 ? (const void*)a.fuse.add_ctr
+                     : c == 3 ? (const void*)a.fuse.add_mem : c == 6 ? (const void*)a.fuse.rm_actor
+                     : c == 7 ? (const void*)a.fuse.rm_ctr : (const void*)a.fuse.rm_mem;
+  const uint32_t R = a.fuse.rows;
+  if (a.fdone && alldone) {
+    const uint32_t lo = sb[0], hi = sb[64];
+    for (uint32_t j = lo + threadIdx.x; j < hi; j += kBlock) {
+      uint32_t l = 0;  // last file whose base <= j
+#pragma unroll
+      for (uint32_t step = 32; step > 0; step >>= 1)
+        if (sb[l + step] <= j) l += step;
+      const uint32_t k = j - sb[l];
+      const size_t idx = (size_t)(i0 + l) * R + k;
+      if (synth) reinterpret_cast<uint32_t*>(dst[c])[j] = ob[l] + k;
+      else if (wide) reinterpret_cast<unsigned long long*>(dst[c])[j] = reinterpret_cast<const unsigned long long*>(fsrc)[idx];
+      else reinterpret_cast<uint32_t*>(dst[c])[j] = reinterpret_cast<const uint32_t*>(fsrc)[idx];
+    }
+    return;
+  }
   if (threadIdx.x < 64) atomicMax(&tmax, sb[threadIdx.x + 1] - sb[threadIdx.x]);
   __syncthreads();
   const uint32_t rows = tmax;  // <= kTileMaxRows (the host checked every column's largest count)
@@ -590,10 +611,6 @@ __global__ void __launch_bounds__(kBlock) k_ds_untile(DsDecodeArgs a) {
   }
   if (a.fdone && rows) {
     // file-major rows: a file's ops are contiguous (x -> file x / rows, op x % rows)
-    const void* fsrc = c == 0 ? (const void*)a.fuse.add_actor : c == 1 ? (const void*)a.fuse.add_ctr
-                       : c == 3 ? (const void*)a.fuse.add_mem : c == 6 ? (const void*)a.fuse.rm_actor
-                       : c == 7 ? (const void*)a.fuse.rm_ctr : (const void*)a.fuse.rm_mem;
-    const uint32_t R = a.fuse.rows;
     for (uint32_t x = threadIdx.x; x < rows * 64; x += kBlock) {
       const uint32_t l = x / rows, k = x - l * rows;
       if (!sdone[l] || k >= R) continue;
