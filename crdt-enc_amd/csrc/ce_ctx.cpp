@@ -98,12 +98,13 @@ SegScratch segscratch(ce_ctx* ctx, uint32_t extra_cap) {
   return sc;
 }
 
+// the counter block: [5] (first failing index, atomicMin) and [13] (the gate's first gap) start at
+// UINT32_MAX, the rest at 0 -- one k_fill launch (two runtime fills were two blit dispatches)
 static hipError_t reset_counters(ce_ctx* ctx) {
-  hipError_t e = hipMemsetAsync(ctx->counters.p, 0, 64, ctx->stream);
-  if (e != hipSuccess) return e;
-  // counters[5] = first failing index (atomicMin) starts at UINT32_MAX
-  return hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ctx->counters.as<uint32_t>() + 5),
-                           0xffffffffu, 1, ctx->stream);
+  FillArgs fl{};
+  fl.n = 0;
+  fl.counters = ctx->counters.as<uint32_t>();
+  return launch_fill(ctx->stream, fl);
 }
 
 int device_open_setup(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint32_t n,

@@ -178,7 +178,10 @@ hipError_t launch_ds_part_apply(hipStream_t s, const DsPartArgs& a);
 // some removal is deferred
 hipError_t launch_ds_deferred(hipStream_t s, const uint32_t* cbeg, const uint32_t* c_actor,
                               const unsigned long long* c_ctr, const unsigned long long* clock,
-                              uint8_t* deferred, uint32_t n_rm, uint32_t* any = nullptr);
+                              uint8_t* deferred, uint32_t n_rm, uint32_t* any = nullptr,
+                              const uint32_t* pub_src = nullptr, uint32_t* pub_dst = nullptr, uint32_t pub_words = 0);
+// (pub_dst: the grid's last block copies pub_src[0..pub_words) -- the fold's live counters, pub_src
+// = DsTables.live, live[7] counting the blocks -- into the caller's pinned memory)
 // state merge: insert the other state's entries with oth = value, then the per-pair merge rule
 hipError_t launch_ds_put_other(hipStream_t s, DsTables t, const unsigned long long* member,
                                const uint32_t* actor, const unsigned long long* value, uint32_t n,
@@ -199,14 +202,16 @@ struct DsMergeSrc {
 // hold = a zeroed u64 per pair slot (left zeroed); live[0..1] = live / used pairs after
 hipError_t launch_ds_kmerge(hipStream_t s, DsTables t, const DsMergeSrc* d_src, const DsMergeSrc* h_src, uint32_t nf,
                             unsigned long long* clock, const unsigned long long* oclocks, uint32_t ccap,
-                            unsigned long long* hold);
+                            unsigned long long* hold, uint32_t* pub_dst = nullptr);  // pub_dst: live[0..5) -> pinned
 hipError_t launch_ds_merge_finalize(hipStream_t s, DsTables t, const unsigned long long* clock,
                                    const unsigned long long* oclock);
 // live pairs -> (member, actor, value) columns (any order); n_out[0] (zeroed beforehand) = their
 // count, n_out[2..3] = the largest member; bmax: kCollectBlocks words of scratch
 static constexpr uint32_t kCollectBlocks = 2048;
 hipError_t launch_ds_collect(hipStream_t s, DsTables t, unsigned long long* member, uint32_t* actor,
-                             unsigned long long* value, uint32_t* n_out, unsigned long long* bmax);
+                             unsigned long long* value, uint32_t* n_out, unsigned long long* bmax, uint32_t* host_out,
+                             unsigned long long* extra_dst = nullptr, const unsigned long long* extra_src = nullptr,
+                             uint32_t extra_words = 0);
 // rebuild: insert (member, actor, value) into fresh (cleared) tables as cur
 hipError_t launch_ds_reinsert(hipStream_t s, DsTables t, const unsigned long long* member,
                               const uint32_t* actor, const unsigned long long* value, uint32_t n);
@@ -232,7 +237,8 @@ hipError_t ds_excl_sum_u32(void* tmp, size_t& tb, const uint32_t* in, uint32_t* 
 // the gate's two flags [17..19) (gate_flags may be null); then clear8[0..8) = 0 (may be null)
 hipError_t launch_ds_col_totals(hipStream_t s, const uint32_t* cnt, const uint32_t* bases, uint32_t n,
                                 const uint32_t* maxima, const int32_t* status, const uint32_t* gate_flags,
-                                uint32_t* clear8, uint32_t* out);
+                                uint32_t* clear8, uint32_t* out, const unsigned long long* nn_src = nullptr,
+                                uint32_t nn_m = 0, unsigned long long* nn_dst = nullptr);
 hipError_t launch_ds_set3(hipStream_t s, uint32_t* p0, uint32_t v0, uint32_t* p1, uint32_t v1, uint32_t* p2,
                           uint32_t v2);
 

@@ -1075,9 +1075,33 @@ __global__ void __launch_bounds__(kApplyThreads) k_ds_part_apply(DsPartArgs a) {
   }
 }
 
+// the last block of a grid to finish copies words [0, pub.words) of pub.src (device counters the
+// grid and the kernels before it produced) into pub.dst (the caller's pinned memory), so the host
+// reads them after its next wait without a runtime copy; pub.done (zero between uses) counts blocks
+struct DsPublish {
+  const uint32_t* src;
+  uint32_t* dst;
+  uint32_t words;
+  uint32_t* done;
+};
+
+__device__ __forceinline__ void publish_last(const DsPublish& pub) {
+  if (!pub.dst) return;
+  __shared__ bool last;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(pub.done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  if (threadIdx.x < pub.words)
+    pub.dst[threadIdx.x] = __hip_atomic_load(pub.src + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) *pub.done = 0;
+}
+
 __global__ void k_ds_deferred(const uint32_t* cbeg, const uint32_t* c_actor,
                               const unsigned long long* c_ctr, const unsigned long long* clock,
-                              uint8_t* deferred, uint32_t n, uint32_t* any) {
+                              uint8_t* deferred, uint32_t n, uint32_t* any, DsPublish pub) {
   bool some = false;
   for (uint32_t r = blockIdx.x * kBlock + threadIdx.x; r < n; r += gridDim.x * kBlock) {
     bool d = false;
@@ -1090,6 +1114,7 @@ __global__ void k_ds_deferred(const uint32_t* cbeg, const uint32_t* c_actor,
     const unsigned long long b = __ballot(some);
     if (b && (threadIdx.x & 63) == (uint32_t)(__ffsll(b) - 1)) atomicOr(any, 1u);
   }
+  publish_last(pub);
 }
 
 __global__ void __launch_bounds__(kBlock) k_ds_put_other(DsTables t, const unsigned long long* member,
@@ -1181,10 +1206,17 @@ __global__ void __launch_bounds__(kBlock) k_ds_merge_finalize(DsTables t, const 
 // not hold exactly M has a clock below it: M > C_Y[a] -- a condition independent of the order.
 // k_ds_kput: pairs inserted, oth = max over the files; k_ds_khold: bit f of hold = file f holds
 // that max; k_ds_kfinal: the test above, then finalize's add / kill as k_ds_merge_finalize.
-__global__ void __launch_bounds__(kBlock) k_ds_kput(DsTables t, const DsMergeSrc* src) {
-  const DsMergeSrc x = src[blockIdx.y];
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2) t.live[threadIdx.x] = 0;  // k_ds_kfinal counts
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 2) t.live[4] = 0;
+// (sources by value, kMergeInline files per launch: an uploaded descriptor array was a runtime copy)
+constexpr uint32_t kMergeInline = 16;
+struct DsMergeSrcs {
+  DsMergeSrc f[kMergeInline];
+  uint32_t f0;  // the first file's index in the merge (its hold bit)
+};
+
+__global__ void __launch_bounds__(kBlock) k_ds_kput(DsTables t, DsMergeSrcs src) {
+  const DsMergeSrc x = src.f[blockIdx.y];
+  if (src.f0 == 0 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2) t.live[threadIdx.x] = 0;  // k_ds_kfinal counts
+  if (src.f0 == 0 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 2) t.live[4] = 0;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < x.n; i += gridDim.x * kBlock) {
     const unsigned long long h = member_find(t, x.member[i], true);
     if (h == kDsEmpty) continue;
@@ -1193,15 +1225,16 @@ __global__ void __launch_bounds__(kBlock) k_ds_kput(DsTables t, const DsMergeSrc
   }
 }
 
-__global__ void __launch_bounds__(kBlock) k_ds_khold(DsTables t, const DsMergeSrc* src, unsigned long long* hold) {
-  const DsMergeSrc x = src[blockIdx.y];
+__global__ void __launch_bounds__(kBlock) k_ds_khold(DsTables t, DsMergeSrcs src, unsigned long long* hold) {
+  const DsMergeSrc x = src.f[blockIdx.y];
+  const uint32_t fb = src.f0 + blockIdx.y;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < x.n; i += gridDim.x * kBlock) {
     const unsigned long long h = member_find(t, x.member[i], false);
     if (h == kDsEmpty) continue;
     const unsigned long long b = pair_find(t, pair_key(h, x.actor[i]), false);
     if (b == kDsEmpty) continue;
     const unsigned long long c = t.cur[b], o = t.oth[b];
-    if (x.value[i] == (c > o ? c : o)) atomicOr(&hold[b], 1ull << blockIdx.y);
+    if (x.value[i] == (c > o ? c : o)) atomicOr(&hold[b], 1ull << fb);
   }
 }
 
@@ -1284,7 +1317,10 @@ __global__ void __launch_bounds__(kBlock) k_ds_kfinal(DsTables t, const unsigned
 }
 
 // clock = max(clock, every file's clock)
-__global__ void k_ds_kclock(unsigned long long* clock, const unsigned long long* oclocks, uint32_t ccap, uint32_t nf) {
+// (pub_dst: the k-way merge's live counters, final since k_ds_kfinal, into the caller's pinned memory)
+__global__ void k_ds_kclock(unsigned long long* clock, const unsigned long long* oclocks, uint32_t ccap, uint32_t nf,
+                            const uint32_t* pub_src, uint32_t* pub_dst, uint32_t pub_words) {
+  if (pub_dst && blockIdx.x == 0 && threadIdx.x < pub_words) pub_dst[threadIdx.x] = pub_src[threadIdx.x];
   for (uint32_t a = blockIdx.x * kBlock + threadIdx.x; a < ccap; a += gridDim.x * kBlock) {
     unsigned long long v = clock[a];
     for (uint32_t f = 0; f < nf; f++) {
@@ -1359,18 +1395,30 @@ __global__ void __launch_bounds__(kBlock) k_ds_collect(DsTables t, unsigned long
   }
 }
 
-__global__ void __launch_bounds__(kBlock) k_ds_collect_max(const unsigned long long* bmax, uint32_t nb, uint32_t* n_out) {
+// ... and the results straight into the caller's pinned memory (host_out: [0] count, [2..3] the
+// largest member; extra: one more device range copied alongside, the compaction's clock), then the
+// output counter back to zero for the next collect: no runtime fill or copy around the pair
+__global__ void __launch_bounds__(kBlock) k_ds_collect_max(const unsigned long long* bmax, uint32_t nb, uint32_t* n_out,
+                                                           uint32_t* host_out, unsigned long long* extra_dst,
+                                                           const unsigned long long* extra_src, uint32_t extra_words) {
   __shared__ unsigned long long lmax[kBlock / 64];
   unsigned long long mx = 0;
   for (uint32_t i = threadIdx.x; i < nb; i += kBlock) mx = bmax[i] > mx ? bmax[i] : mx;
   mx = wave_max64(mx);
   if ((threadIdx.x & 63) == 0) lmax[threadIdx.x >> 6] = mx;
+  for (uint32_t i = threadIdx.x; i < extra_words; i += kBlock) extra_dst[i] = extra_src[i];
   __syncthreads();
   if (threadIdx.x == 0) {
     unsigned long long m = 0;
     for (int w = 0; w < kBlock / 64; w++) m = lmax[w] > m ? lmax[w] : m;
     n_out[2] = (uint32_t)m;
     n_out[3] = (uint32_t)(m >> 32);
+    if (host_out) {
+      host_out[0] = n_out[0];
+      host_out[2] = (uint32_t)m;
+      host_out[3] = (uint32_t)(m >> 32);
+      n_out[0] = 0;
+    }
   }
 }
 
@@ -1528,7 +1576,11 @@ hipError_t ds_sort_pairs_u64(void* tmp, size_t& tb, const unsigned long long* ki
 // version gate's flags (gate_flags, when given); then clear8[0..8) = 0 (the emit's counters)
 __global__ void __launch_bounds__(1024) k_ds_col_totals(const uint32_t* cnt, const uint32_t* bases, uint32_t n,
                                                         const uint32_t* maxima, const int32_t* status,
-                                                        const uint32_t* gate_flags, uint32_t* clear8, uint32_t* out) {
+                                                        const uint32_t* gate_flags, uint32_t* clear8, uint32_t* out,
+                                                        const unsigned long long* nn_src, uint32_t nn_m,
+                                                        unsigned long long* nn_dst) {
+  // the version gate's next versions per writer too (out and nn_dst: the caller's pinned memory)
+  for (uint32_t i = threadIdx.x; nn_dst && i < nn_m; i += blockDim.x) nn_dst[i] = nn_src[i];
   __shared__ uint32_t acc[4];
   const uint32_t k = threadIdx.x;
   if (k < 3) acc[k] = 0;
@@ -1564,10 +1616,11 @@ __global__ void __launch_bounds__(1024) k_ds_col_totals(const uint32_t* cnt, con
 
 hipError_t launch_ds_col_totals(hipStream_t s, const uint32_t* cnt, const uint32_t* bases, uint32_t n,
                                 const uint32_t* maxima, const int32_t* status, const uint32_t* gate_flags,
-                                uint32_t* clear8, uint32_t* out) {
+                                uint32_t* clear8, uint32_t* out, const unsigned long long* nn_src, uint32_t nn_m,
+                                unsigned long long* nn_dst) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_ds_col_totals, dim3(1), dim3(1024), 0, s, cnt, bases, n, maxima, status, gate_flags,
-                     clear8, out);
+                     clear8, out, nn_src, nn_m, nn_dst);
   return hipGetLastError();
 }
 
@@ -1709,10 +1762,13 @@ hipError_t launch_ds_part_apply(hipStream_t s, const DsPartArgs& a) {
 
 hipError_t launch_ds_deferred(hipStream_t s, const uint32_t* cbeg, const uint32_t* c_actor,
                               const unsigned long long* c_ctr, const unsigned long long* clock,
-                              uint8_t* deferred, uint32_t n_rm, uint32_t* any) {
-  if (n_rm == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ds_deferred, dim3(blocks_for(n_rm)), dim3(kBlock), 0, s, cbeg, c_actor, c_ctr,
-                     clock, deferred, n_rm, any);
+                              uint8_t* deferred, uint32_t n_rm, uint32_t* any, const uint32_t* pub_src,
+                              uint32_t* pub_dst, uint32_t pub_words) {
+  if (n_rm == 0 && !pub_dst) return hipSuccess;
+  // (publishing: live[7] counts the blocks, zero between uses)
+  const DsPublish pub{pub_src, pub_dst, pub_words, pub_dst ? const_cast<uint32_t*>(pub_src) + 7 : nullptr};
+  hipLaunchKernelGGL(k_ds_deferred, dim3(std::max<uint32_t>(1, blocks_for(n_rm))), dim3(kBlock), 0, s, cbeg, c_actor,
+                     c_ctr, clock, deferred, n_rm, any, pub);
   return hipGetLastError();
 }
 
@@ -1734,15 +1790,25 @@ hipError_t launch_ds_merge_finalize(hipStream_t s, DsTables t, const unsigned lo
 
 hipError_t launch_ds_kmerge(hipStream_t s, DsTables t, const DsMergeSrc* d_src, const DsMergeSrc* h_src, uint32_t nf,
                             unsigned long long* clock, const unsigned long long* oclocks, uint32_t ccap,
-                            unsigned long long* hold) {
+                            unsigned long long* hold, uint32_t* pub_dst) {
+  (void)d_src;
   uint32_t nmax = 0;
   for (uint32_t f = 0; f < nf; f++) nmax = h_src[f].n > nmax ? h_src[f].n : nmax;
   const uint32_t gx = nmax ? blocks_for(nmax) : 1;
-  hipLaunchKernelGGL(k_ds_kput, dim3(gx, nf), dim3(kBlock), 0, s, t, d_src);
-  hipLaunchKernelGGL(k_ds_khold, dim3(gx, nf), dim3(kBlock), 0, s, t, d_src, hold);
+  auto srcs = [&](uint32_t c0) {
+    DsMergeSrcs m{};
+    m.f0 = c0;
+    for (uint32_t i = 0; i < kMergeInline && c0 + i < nf; i++) m.f[i] = h_src[c0 + i];
+    return m;
+  };
+  for (uint32_t c0 = 0; c0 < nf; c0 += kMergeInline)
+    hipLaunchKernelGGL(k_ds_kput, dim3(gx, std::min(kMergeInline, nf - c0)), dim3(kBlock), 0, s, t, srcs(c0));
+  for (uint32_t c0 = 0; c0 < nf; c0 += kMergeInline)
+    hipLaunchKernelGGL(k_ds_khold, dim3(gx, std::min(kMergeInline, nf - c0)), dim3(kBlock), 0, s, t, srcs(c0), hold);
   hipLaunchKernelGGL(k_ds_kfinal, dim3(blocks_for((uint64_t)t.pmask + 1, 1024)), dim3(kBlock), 0, s, t, clock, oclocks,
                      ccap, nf, hold);
-  hipLaunchKernelGGL(k_ds_kclock, dim3(blocks_for(ccap)), dim3(kBlock), 0, s, clock, oclocks, ccap, nf);
+  hipLaunchKernelGGL(k_ds_kclock, dim3(std::max<uint32_t>(1, blocks_for(ccap))), dim3(kBlock), 0, s, clock, oclocks,
+                     ccap, nf, t.live, pub_dst, 5u);
   return hipGetLastError();
 }
 
@@ -1753,10 +1819,12 @@ hipError_t launch_ds_merge(hipStream_t s, DsTables t, const unsigned long long* 
 }
 
 hipError_t launch_ds_collect(hipStream_t s, DsTables t, unsigned long long* member, uint32_t* actor,
-                             unsigned long long* value, uint32_t* n_out, unsigned long long* bmax) {
+                             unsigned long long* value, uint32_t* n_out, unsigned long long* bmax, uint32_t* host_out,
+                             unsigned long long* extra_dst, const unsigned long long* extra_src, uint32_t extra_words) {
   const uint32_t nb = blocks_for((uint64_t)t.pmask + 1, kCollectBlocks);
   hipLaunchKernelGGL(k_ds_collect, dim3(nb), dim3(kBlock), 0, s, t, member, actor, value, n_out, bmax);
-  hipLaunchKernelGGL(k_ds_collect_max, dim3(1), dim3(kBlock), 0, s, bmax, nb, n_out);
+  hipLaunchKernelGGL(k_ds_collect_max, dim3(1), dim3(kBlock), 0, s, bmax, nb, n_out, host_out, extra_dst, extra_src,
+                     extra_words);
   return hipGetLastError();
 }
 

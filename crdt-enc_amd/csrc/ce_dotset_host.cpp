@@ -74,6 +74,8 @@ struct DsState {
   // Orswot op files decoded in the open (k_open_fold_v2's DS form): raw counts, done flags and
   // the file-major rows (add actor / counter / member, removal actor / counter / member)
   DevBuf fz_cnt, fz_done, fz_col[6], fz_why;
+  DevBuf ser_cnt, ser_off;  // the serializer's counting sort (per-member counts, their scan)
+  void* col5_zeroed = nullptr;  // col[5] (the collect counter) was cleared at this address
   // device state reader (per state file: candidates, sorted heads, entry ends, Dot counts and
   // bases, members, sorted members [0..6]
   // and emitted (member, actor id, value) columns [7..9]), pinned staging for its downloads
@@ -174,6 +176,17 @@ int ensure_clock(ce_core* c) {
   return CE_OK;
 }
 
+// the device address of pinned host memory (kernels write their small results straight into it:
+// no runtime copy, which the HIP runtime issues as a blit dispatch)
+void* host_dev_ptr(void* h) {
+  void* dp = nullptr;
+  if (hipHostGetDevicePointer(&dp, h, 0) != hipSuccess || !dp) {
+    (void)hipGetLastError();
+    return h;
+  }
+  return dp;
+}
+
 // live entries -> (member, actor id, value) columns in d->col[0..2]; returns the count and
 // (max_member) the largest live member.  extra_dl: one more download (dst, src, bytes) queued
 // before the one wait (the compaction's clock)
@@ -189,12 +202,19 @@ int collect(ce_core* c, uint32_t* n_live, unsigned long long* max_member = nullp
     return ctx->hip_fail(e, "collect");
   uint32_t* cnt = d->col[5].as<uint32_t>();
   uint32_t* hc = d->h_cnt.as<uint32_t>() + 48;  // pinned: [0] count, [2..3] max member
-  if ((e = hipMemsetAsync(cnt, 0, 16, ctx->stream)) ||
-      (e = launch_ds_collect(ctx->stream, tables(d), d->col[0].as<unsigned long long>(),
+  // the output counter is zero between collects (k_ds_collect_max resets it): cleared only when new
+  if (d->col5_zeroed != d->col[5].p) {
+    if ((e = hipMemsetAsync(cnt, 0, 16, ctx->stream))) return ctx->hip_fail(e, "collect");
+    d->col5_zeroed = d->col[5].p;
+  }
+  // the count, largest member and the extra range (8-byte words) land in pinned memory from the
+  // collect's last kernel
+  if ((e = launch_ds_collect(ctx->stream, tables(d), d->col[0].as<unsigned long long>(),
                              d->col[1].as<uint32_t>(), d->col[2].as<unsigned long long>(), cnt,
-                             reinterpret_cast<unsigned long long*>(d->col[5].as<uint8_t>() + 64))) ||
-      (e = hipMemcpyAsync(hc, cnt, 16, hipMemcpyDeviceToHost, ctx->stream)) ||
-      (extra_bytes && (e = hipMemcpyAsync(extra_dst, extra_src, extra_bytes, hipMemcpyDeviceToHost, ctx->stream))) ||
+                             reinterpret_cast<unsigned long long*>(d->col[5].as<uint8_t>() + 64),
+                             static_cast<uint32_t*>(host_dev_ptr(hc)),
+                             extra_bytes ? static_cast<unsigned long long*>(host_dev_ptr(extra_dst)) : nullptr,
+                             static_cast<const unsigned long long*>(extra_src), (uint32_t)(extra_bytes / 8))) ||
       (e = stream_wait(ctx->stream)))
     return ctx->hip_fail(e, "collect");
   *n_live = hc[0];
@@ -214,9 +234,10 @@ int ensure_pairs(ce_core* c, uint64_t extra) {
     if ((e = d->h_cnt.reserve(512))) return c->ctx->hip_fail(e, "members");
     uint32_t* hm = d->h_cnt.as<uint32_t>() + 40;
     if ((e = d->col[5].reserve(64 + 8ull * kCollectBlocks)) ||
-        (e = hipMemsetAsync(d->col[5].p, 0, 4, c->ctx->stream)) ||
-        (e = launch_ds_count_members(c->ctx->stream, tables(d), d->col[5].as<uint32_t>())) ||
-        (e = hipMemcpyAsync(hm, d->col[5].p, 4, hipMemcpyDeviceToHost, c->ctx->stream)) ||
+        // (word 4: words 0..3 are the collect's counters, kept zero between collects)
+        (e = hipMemsetAsync(d->col[5].as<uint32_t>() + 4, 0, 4, c->ctx->stream)) ||
+        (e = launch_ds_count_members(c->ctx->stream, tables(d), d->col[5].as<uint32_t>() + 4)) ||
+        (e = hipMemcpyAsync(hm, d->col[5].as<uint32_t>() + 4, 4, hipMemcpyDeviceToHost, c->ctx->stream)) ||
         (e = stream_wait(c->ctx->stream)))
       return c->ctx->hip_fail(e, "members");
     d->mcap_s = pow2_at_least(std::max<uint64_t>(4096, std::min<uint64_t>(1u << 27, hm[0] * 5ull / 2)));
@@ -685,12 +706,14 @@ int orswot_fold(ce_core* c, const Counts& k, uint64_t kill_bound, bool adds_cont
     ctx->tend(t);
     c->path_counts["ds_fold_global"]++;
   }
+  // the last deferred-flags launch publishes live[0..5) into the pinned h_cnt[56..61) (ds_settle)
   uint8_t* fl = d->deferred_flags.as<uint8_t>();
-  if ((e = launch_ds_deferred(s, o.rm_cbeg, o.rmc_actor, o.rmc_ctr, d->clock.as<unsigned long long>(), fl, nr, live + 3)) ||
+  uint32_t* pub = static_cast<uint32_t*>(host_dev_ptr(d->h_cnt.as<uint32_t>() + 56));
+  if ((e = launch_ds_deferred(s, o.rm_cbeg, o.rmc_actor, o.rmc_ctr, d->clock.as<unsigned long long>(), fl, nr, live + 3,
+                              live, n0 ? nullptr : pub, 5)) ||
       (n0 && (e = launch_ds_deferred(s, d->d0[0].as<uint32_t>(), d->d0[2].as<uint32_t>(),
                                      d->d0[3].as<unsigned long long>(), d->clock.as<unsigned long long>(), fl + nr,
-                                     n0, live + 3))) ||
-      (e = hipMemcpyAsync(d->h_cnt.as<uint32_t>() + 56, live, 20, hipMemcpyDeviceToHost, s)))
+                                     n0, live + 3, live, pub, 5))))
     return ctx->hip_fail(e, "finalize");
   d->settle_pending = true;
   d->settle_fold = true;
@@ -921,8 +944,9 @@ int gate_enqueue(ce_core* c, const uint32_t* d_fa, const uint64_t* d_fv, uint32_
   ctx->tend(t);
   // the flags come back with the caller's next download when it passes `extra` (k_ds_col_totals
   // copies them), else here
-  if ((!extra && (e = hipMemcpyAsync(job->hf, ga.flags, 8, hipMemcpyDeviceToHost, ctx->stream))) ||
-      (e = hipMemcpyAsync(job->hnn, ga.newnov, m * 8ull, hipMemcpyDeviceToHost, ctx->stream)))
+  // (with `extra`, k_ds_col_totals also copies the next versions into job->hnn)
+  if (!extra && ((e = hipMemcpyAsync(job->hf, ga.flags, 8, hipMemcpyDeviceToHost, ctx->stream)) ||
+                 (e = hipMemcpyAsync(job->hnn, ga.newnov, m * 8ull, hipMemcpyDeviceToHost, ctx->stream))))
     return ctx->hip_fail(e, "gate");
   return CE_OK;
 }
@@ -1144,6 +1168,7 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
     if (n == 0) {
       std::memset(hsum, 0, 20 * 4);
       hsum[18] = 0xffffffffu;
+      std::memset(gj.hnn, 0, 8ull * m);  // (the gate's fill zeroed the device copy)
       return CE_OK;
     }
     size_t t = d->cub_tmp.cap;
@@ -1155,8 +1180,8 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
     if ((e = ds_excl_sum_u32(d->cub_tmp.p, t, cnt, bases, kCntN * n, ctx->stream)) ||
         (e = launch_ds_col_totals(ctx->stream, cnt, bases, n, d->misses.as<uint32_t>() + 8, ctx->status.as<int32_t>(),
                                   ctx->counters.as<uint32_t>() + 12, d->misses.as<uint32_t>(),
-                                  d->cnt_tot.as<uint32_t>())) ||
-        (e = hipMemcpyAsync(hsum, d->cnt_tot.p, 20 * 4, hipMemcpyDeviceToHost, ctx->stream)))
+                                  static_cast<uint32_t*>(host_dev_ptr(hsum)), gj.ga.newnov, m,
+                                  static_cast<unsigned long long*>(host_dev_ptr(gj.hnn)))))
       return ctx->hip_fail(e, "count");
     return CE_OK;
   };
@@ -1736,8 +1761,8 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
   if (d->rd.size() < n) d->rd.resize(n);
   // pinned words: [0, 2n) candidate counts / flags, [2n, 6n) entry tails, [6n, 10n) live counts
   // device words: [0, 2n) candidate counts / flags, [2n, 6n) entry tails (k_rd_tail)
-  if ((e = d->rd_misc.reserve(24ull * n + 64)) || (e = d->rd_small.reserve(40ull * n + 64)) ||
-      (e = hipMemsetAsync(d->rd_misc.p, 0, 8ull * n, s)))
+  // (rd_misc's candidate counts are cleared with the reader's chunk counter, one fill launch)
+  if ((e = d->rd_misc.reserve(24ull * n + 64)) || (e = d->rd_small.reserve(40ull * n + 64)))
     return ctx->hip_fail(e, "state reader");
   uint32_t* small = d->rd_small.as<uint32_t>();
   static const bool rd_debug = getenv("CE_RD_DEBUG") != nullptr;  // which stage declined a file
@@ -1831,7 +1856,6 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
         (e = d->rd_args_d.reserve(3 * na * sizeof(OrswotReadArgs))))
       return ctx->hip_fail(e, "state reader");
     OrswotReadArgs* hA = d->rd_args_h.as<OrswotReadArgs>();
-    OrswotReadArgs* dA = d->rd_args_d.as<OrswotReadArgs>();
     uint32_t nch = 0;
     for (size_t k = 0; k < dev.size(); k++) {
       const size_t i = dev[k];
@@ -1856,9 +1880,9 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     uint32_t* chunk_scan = chunk_cnt + nch + 1;
     h2 = std::make_unique<HostPhase>("   rd.c launch");
     if (!dev.empty() &&
-        ((e = hipMemsetAsync(chunk_cnt + nch, 0, 4, s)) ||
-         (e = hipMemcpyAsync(dA, hA, dev.size() * sizeof(OrswotReadArgs), hipMemcpyHostToDevice, s)) ||
-         (e = launch_orswot_read_multi(s, dA, hA, (uint32_t)dev.size(), 0, chunk_cnt, chunk_scan, d->rd_tmp.p,
+        ((e = launch_fill(s, FillArgs{{FillRange{chunk_cnt + nch, 1, 0u}, FillRange{d->rd_misc.as<uint32_t>(), 2ull * n, 0u}},
+                                      2, nullptr})) ||
+         (e = launch_orswot_read_multi(s, nullptr, hA, (uint32_t)dev.size(), 0, chunk_cnt, chunk_scan, d->rd_tmp.p,
                                        d->rd_tmp.cap))))
       return ctx->hip_fail(e, "state reader");
     h2 = std::make_unique<HostPhase>("   rd.d sync");
@@ -1885,8 +1909,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
       dev2.push_back(i);
     }
     if (!dev2.empty() &&
-        ((e = hipMemcpyAsync(dA + na, hA2, dev2.size() * sizeof(OrswotReadArgs), hipMemcpyHostToDevice, s)) ||
-         (e = launch_orswot_read_multi(s, dA + na, hA2, (uint32_t)dev2.size(), 1, nullptr, nullptr, nullptr, 0))))
+        (e = launch_orswot_read_multi(s, nullptr, hA2, (uint32_t)dev2.size(), 1, nullptr, nullptr, nullptr, 0)))
       return ctx->hip_fail(e, "state reader");
     // every file's tail words in one download
     if (!dev2.empty() && ((e = hipMemcpyAsync(small + 2 * n, d->rd_misc.as<uint32_t>() + 2 * n, 16ull * n,
@@ -1955,8 +1978,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
       hA4[k] = a;
     }
     if (!dev4.empty() &&
-        ((e = hipMemcpyAsync(dA + 2 * na, hA4, dev4.size() * sizeof(OrswotReadArgs), hipMemcpyHostToDevice, s)) ||
-         (e = launch_orswot_read_multi(s, dA + 2 * na, hA4, (uint32_t)dev4.size(), 2, nullptr, nullptr, nullptr, 0)) ||
+        ((e = launch_orswot_read_multi(s, nullptr, hA4, (uint32_t)dev4.size(), 2, nullptr, nullptr, nullptr, 0)) ||
          (e = hipMemcpyAsync(small, d->rd_misc.p, 8ull * n, hipMemcpyDeviceToHost, s))))
       return ctx->hip_fail(e, "state reader");
     if (!dev4.empty() && (rc = sync("state reader"))) return rc;
@@ -2008,11 +2030,10 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     // no host wait: the merged counts land in pinned memory for ds_settle (the next ingest's
     // first wait), like a fold's
     d->scratch_dirty = true;
-    if ((e = hipMemcpyAsync(d->rd_args_d.p, hs, n * sizeof(DsMergeSrc), hipMemcpyHostToDevice, s)) ||
-        (e = launch_ds_kmerge(s, tables(d), d->rd_args_d.as<DsMergeSrc>(), hs, (uint32_t)n,
+    if ((e = launch_ds_kmerge(s, tables(d), nullptr, hs, (uint32_t)n,
                               d->clock.as<unsigned long long>(), d->rd_oclocks.as<unsigned long long>(), ccap,
-                              d->hold.as<unsigned long long>())) ||
-        (e = hipMemcpyAsync(d->h_cnt.as<uint32_t>() + 56, d->live.p, 20, hipMemcpyDeviceToHost, s)))
+                              d->hold.as<unsigned long long>(),
+                              static_cast<uint32_t*>(host_dev_ptr(d->h_cnt.as<uint32_t>() + 56)))))
       return ctx->hip_fail(e, "merge");
     c->path_counts["states_kway_merge"]++;
     d->scratch_dirty = false;  // k_ds_kfinal cleared oth / hold
@@ -2231,11 +2252,18 @@ static int ds_serialize_dev(ce_core* c, ce_ctx* x, const uint8_t* outer, const u
   cph = std::make_unique<HostPhase>("  cd: sort enqueue");
   for (int k = 0; k < 15; k++) {
     // 0-3 u32 sort keys / perms, 4-6 u64 keys / sorted members / values, 7-10 actors, heads,
-    // ranks, lengths, 11 entry CSR (n + 1), 12 byte offsets
-    const size_t sz = k >= 4 && k <= 6 ? 8ull * nl + 64 : k <= 12 ? 4ull * nl + 68 : 64;
+    // ranks, lengths, 11 entry CSR (n + 1), 12 byte offsets, 13 u64 values (counting sort)
+    const size_t sz = (k >= 4 && k <= 6) || k == 13 ? 8ull * nl + 64 : k <= 12 ? 4ull * nl + 68 : 64;
     if ((e = d->ser[k].reserve(sz))) return x->hip_fail(e, "ds compact reserve");
   }
-  if ((e = d->ser[15].reserve(orswot_ser_tmp_bytes(std::max<uint32_t>(nl, 1))))) return x->hip_fail(e, "ds compact reserve");
+  if ((e = d->ser[15].reserve(std::max<size_t>(orswot_ser_tmp_bytes(std::max<uint32_t>(nl, 1)),
+                                               4ull * (((1u << kSerCountBits) + 2) / 2048 + 2) + 256))))
+    return x->hip_fail(e, "ds compact reserve");
+  if (!d->ser_cnt.p) {  // the counting sort's per-member counts: zero once, kept zero by the scatter
+    if ((e = d->ser_cnt.reserve(4ull * ((1u << kSerCountBits) + 2))) || (e = d->ser_off.reserve(4ull * ((1u << kSerCountBits) + 2))) ||
+        (e = hipMemsetAsync(d->ser_cnt.p, 0, 4ull * ((1u << kSerCountBits) + 2), s)))
+      return x->hip_fail(e, "ds compact reserve");
+  }
   OrswotSerScratch sc{};
   sc.member_in = d->col[0].as<unsigned long long>();
   sc.actor_in = d->col[1].as<uint32_t>();
@@ -2259,6 +2287,9 @@ static int ds_serialize_dev(ce_core* c, ce_ctx* x, const uint8_t* outer, const u
   sc.pos = d->ser[12].as<uint32_t>();
   sc.tmp = d->ser[15].p;
   sc.tmp_bytes = d->ser[15].cap;
+  sc.bucket_count = d->ser_cnt.as<uint32_t>();
+  sc.bucket_off = d->ser_off.as<uint32_t>();
+  sc.t_value = d->ser[13].as<unsigned long long>();
   const int t = x->tbegin("ds_serialize");
   if ((e = launch_orswot_ser_sort(s, sc, nl))) return x->hip_fail(e, "ds serialize");
   const unsigned long long* ck = d->h_clock.as<unsigned long long>();

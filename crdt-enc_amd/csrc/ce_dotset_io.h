@@ -47,7 +47,13 @@ struct OrswotSerScratch {
   uint32_t* seg;                         // n + 1
   void* tmp;
   size_t tmp_bytes;
+  // counting sort (members below 2^kSerCountBits): per-member counts, zero between calls (the
+  // scatter counts them back down), their exclusive scan, and a u64 value scratch (n)
+  uint32_t* bucket_count;                // [2^kSerCountBits + 1]
+  uint32_t* bucket_off;                  // [2^kSerCountBits + 2]
+  unsigned long long* t_value;
 };
+static constexpr int kSerCountBits = 20;
 hipError_t launch_orswot_ser(hipStream_t s, OrswotSerScratch& sc, const OrswotSerArgs& a);
 // the same in two halves: the sorts and scans over the n collected pairs (no host input), then the
 // writer (needs the host-built prefix / suffix) -- the host builds them while the sorts run
@@ -78,6 +84,11 @@ struct OrswotReadArgs {
   uint32_t* col_actor;
   unsigned long long* col_value;
   uint32_t chunk0, nchunks;    // multi-file reader: this file's 4 KiB chunks in the count array
+};
+// kRdInline descriptors per launch, passed by value (launch_orswot_read_multi)
+static constexpr uint32_t kRdInline = 16;
+struct RdFiles {
+  OrswotReadArgs f[kRdInline];
 };
 // the reader over nf files at once (d_args / h_args: the same descriptors in HBM and on the
 // host): stage 0 = entry heads in position order into `cand` and their count into *n_cand_dev

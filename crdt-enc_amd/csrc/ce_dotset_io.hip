@@ -105,6 +105,40 @@ __global__ void k_ser_unpack(const K* key, int rank_bits, const uint32_t* id_of_
   }
 }
 
+// Counting sort of the live pairs by (member, actor rank) when every member is below
+// 2^kSerCountBits (C3: 100k members): per-member counts, their exclusive scan, a scatter into each
+// member's slice (any order inside it; the counts go back to zero), then each pair's place in
+// its slice = the pairs of the slice with a smaller rank (a member has at most one pair per
+// actor: slices hold <= the actor count, ~12 at C3).  Four launches instead of a radix sort's
+// passes and their runtime fills, but slower at C3 (opt-in CE_SER_COUNT=1, launch_orswot_ser_sort).
+__global__ void k_ser_hist(const unsigned long long* member, uint32_t* count, uint32_t n) {
+  for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < n; i += gridDim.x * kB) atomicAdd(count + (uint32_t)member[i], 1u);
+}
+
+__global__ void k_ser_scatter(OrswotSerScratch sc, uint32_t n) {
+  for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < n; i += gridDim.x * kB) {
+    const uint32_t m = (uint32_t)sc.member_in[i], a = sc.actor_in[i];
+    const uint32_t p = sc.bucket_off[m] + atomicSub(sc.bucket_count + m, 1u) - 1u;
+    sc.k64a[p] = m;
+    sc.k32a[p] = sc.rank_of_id[a];
+    sc.p32a[p] = a;
+    sc.t_value[p] = sc.value_in[i];
+  }
+}
+
+__global__ void k_ser_slice_rank(OrswotSerScratch sc, uint32_t n) {
+  for (uint32_t p = blockIdx.x * kB + threadIdx.x; p < n; p += gridDim.x * kB) {
+    const uint32_t m = (uint32_t)sc.k64a[p], rk = sc.k32a[p];
+    const uint32_t b0 = sc.bucket_off[m], b1 = sc.bucket_off[m + 1];
+    uint32_t r = 0;
+    for (uint32_t q = b0; q < b1; q++) r += sc.k32a[q] < rk;
+    const uint32_t o = b0 + r;
+    sc.member_sorted[o] = m;
+    sc.actor_sorted[o] = sc.p32a[p];
+    sc.value_sorted[o] = sc.t_value[p];
+  }
+}
+
 // head[i] = pair i starts a member's entry
 __global__ void k_ser_head(const unsigned long long* member, uint32_t* head, uint32_t n) {
   for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < n; i += gridDim.x * kB)
@@ -276,9 +310,9 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* part) {
   return t;
 }
 
-__global__ void __launch_bounds__(kB) k_rdm_count(const OrswotReadArgs* fa, uint32_t* cnt) {
+__global__ void __launch_bounds__(kB) k_rdm_count(RdFiles fa, uint32_t* cnt) {
   __shared__ uint32_t part[kB / 64];
-  const OrswotReadArgs& a = fa[blockIdx.y];
+  const OrswotReadArgs a = fa.f[blockIdx.y];
   if (blockIdx.x >= a.nchunks) return;
   const uint64_t c0 = a.lo + (uint64_t)blockIdx.x * kFindChunk;
   uint32_t n = 0;
@@ -292,9 +326,9 @@ __global__ void __launch_bounds__(kB) k_rdm_count(const OrswotReadArgs* fa, uint
 }
 
 // chunk heads in position order: cand[scan(chunk) - scan(file's first chunk) + rank]
-__global__ void __launch_bounds__(kB) k_rdm_write(const OrswotReadArgs* fa, const uint32_t* scan) {
+__global__ void __launch_bounds__(kB) k_rdm_write(RdFiles fa, const uint32_t* scan) {
   __shared__ uint32_t part[kB / 64];
-  const OrswotReadArgs& a = fa[blockIdx.y];
+  const OrswotReadArgs a = fa.f[blockIdx.y];
   if (blockIdx.x >= a.nchunks) return;
   const uint64_t c0 = a.lo + (uint64_t)blockIdx.x * kFindChunk;
   uint32_t at = scan[a.chunk0 + blockIdx.x] - scan[a.chunk0];
@@ -320,13 +354,13 @@ __global__ void __launch_bounds__(kB) k_rdm_write(const OrswotReadArgs* fa, cons
   }
 }
 
-__global__ void k_rdm_found(const OrswotReadArgs* fa, const uint32_t* scan, uint32_t nf) {
+__global__ void k_rdm_found(RdFiles fa, const uint32_t* scan, uint32_t nf) {
   const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f < nf) *fa[f].n_cand_dev = scan[fa[f].chunk0 + fa[f].nchunks] - scan[fa[f].chunk0];
+  if (f < nf) *fa.f[f].n_cand_dev = scan[fa.f[f].chunk0 + fa.f[f].nchunks] - scan[fa.f[f].chunk0];
 }
 
-__global__ void k_rdm_entry(const OrswotReadArgs* fa) {
-  const OrswotReadArgs a = fa[blockIdx.y];
+__global__ void k_rdm_entry(RdFiles fa) {
+  const OrswotReadArgs a = fa.f[blockIdx.y];
   const uint8_t* base = a.s + a.lo;
   const uint8_t* end = a.s + a.hi;
   for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < a.n_cand; i += gridDim.x * kB) {
@@ -361,8 +395,8 @@ __global__ void k_rdm_entry(const OrswotReadArgs* fa) {
 
 // the chain check (k_rd_chain) and the repeat set's clearing in one pass: the set is cleared
 // here and filled by k_rdm_dups, the next launch
-__global__ void k_rdm_chain(const OrswotReadArgs* fa) {
-  const OrswotReadArgs a = fa[blockIdx.y];
+__global__ void k_rdm_chain(RdFiles fa) {
+  const OrswotReadArgs a = fa.f[blockIdx.y];
   const uint8_t* base = a.s + a.lo;
   for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < a.n_cand; i += gridDim.x * kB) {
     const uint32_t start = i == 0 ? 0u : a.end[i - 1];
@@ -375,8 +409,8 @@ __global__ void k_rdm_chain(const OrswotReadArgs* fa) {
   for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < a.dset_mask + 2u; i += gridDim.x * kB) a.msort[i] = ~0ull;
 }
 
-__global__ void k_rdm_dups(const OrswotReadArgs* fa) {
-  const OrswotReadArgs a = fa[blockIdx.y];
+__global__ void k_rdm_dups(RdFiles fa) {
+  const OrswotReadArgs a = fa.f[blockIdx.y];
   constexpr unsigned long long kEmpty = ~0ull;
   for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < a.n_cand; i += gridDim.x * kB) {
     const unsigned long long m = a.member[i];
@@ -402,9 +436,9 @@ __global__ void k_rdm_dups(const OrswotReadArgs* fa) {
 // ~50 us at C3's 8 x 100k entries.)
 constexpr uint32_t kScanTile = kB * 8;
 
-__global__ void __launch_bounds__(kB) k_rdm_tile_sums(const OrswotReadArgs* fa) {
+__global__ void __launch_bounds__(kB) k_rdm_tile_sums(RdFiles fa) {
   __shared__ uint32_t part[kB / 64];
-  const OrswotReadArgs& a = fa[blockIdx.y];
+  const OrswotReadArgs a = fa.f[blockIdx.y];
   const uint32_t t0 = blockIdx.x * kScanTile;
   if (t0 >= a.n_cand) return;
   uint32_t v = 0;
@@ -417,10 +451,10 @@ __global__ void __launch_bounds__(kB) k_rdm_tile_sums(const OrswotReadArgs* fa) 
   if (threadIdx.x == 0) reinterpret_cast<uint32_t*>(a.msort)[blockIdx.x] = tot;
 }
 
-__global__ void __launch_bounds__(kB) k_rdm_tile_scan(const OrswotReadArgs* fa) {
+__global__ void __launch_bounds__(kB) k_rdm_tile_scan(RdFiles fa) {
   __shared__ uint32_t part[kB / 64];
   __shared__ uint32_t run[kB];
-  const OrswotReadArgs& a = fa[blockIdx.y];
+  const OrswotReadArgs a = fa.f[blockIdx.y];
   const uint32_t t0 = blockIdx.x * kScanTile;
   if (t0 >= a.n_cand) return;
   // the tile's base: the totals of the tiles before it
@@ -462,8 +496,8 @@ __global__ void __launch_bounds__(kB) k_rdm_tile_scan(const OrswotReadArgs* fa) 
   }
 }
 
-__global__ void k_rdm_emit(const OrswotReadArgs* fa) {
-  const OrswotReadArgs a = fa[blockIdx.y];
+__global__ void k_rdm_emit(RdFiles fa) {
+  const OrswotReadArgs a = fa.f[blockIdx.y];
   const uint8_t* base = a.s + a.lo;
   for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < a.n_cand; i += gridDim.x * kB) {
     const uint8_t* p = base + a.cand[i] + 6;
@@ -495,37 +529,55 @@ __global__ void k_rdm_emit(const OrswotReadArgs* fa) {
 
 }  // namespace
 
-hipError_t launch_orswot_read_multi(hipStream_t s, const OrswotReadArgs* d_args, const OrswotReadArgs* h_args,
+// The descriptors go to the kernels as launch arguments, kRdInline files per launch (a
+// descriptor array uploaded with hipMemcpyAsync was a runtime copy -- a blit dispatch -- per stage).
+hipError_t launch_orswot_read_multi(hipStream_t s, const OrswotReadArgs* /*d_args*/, const OrswotReadArgs* h_args,
                                     uint32_t nf, int stage, uint32_t* chunk_cnt, uint32_t* chunk_scan,
                                     void* tmp, size_t tmp_bytes) {
   if (nf == 0) return hipSuccess;
-  uint32_t gx = 1;
+  auto files = [&](uint32_t c0) {
+    RdFiles r{};
+    for (uint32_t i = 0; i < kRdInline && c0 + i < nf; i++) r.f[i] = h_args[c0 + i];
+    return r;
+  };
+  auto part = [&](uint32_t c0) { return std::min<uint32_t>(kRdInline, nf - c0); };
   if (stage == 0) {
     uint32_t nchunks = 0;
-    for (uint32_t f = 0; f < nf; f++) {
-      gx = std::max(gx, h_args[f].nchunks);
-      nchunks = std::max(nchunks, h_args[f].chunk0 + h_args[f].nchunks);
-    }
-    hipLaunchKernelGGL(k_rdm_count, dim3(gx, nf), dim3(kB), 0, s, d_args, chunk_cnt);
+    for (uint32_t f = 0; f < nf; f++) nchunks = std::max(nchunks, h_args[f].chunk0 + h_args[f].nchunks);
+    auto gx_of = [&](uint32_t c0) {
+      uint32_t g = 1;
+      for (uint32_t f = c0; f < c0 + part(c0); f++) g = std::max(g, h_args[f].nchunks);
+      return g;
+    };
+    for (uint32_t c0 = 0; c0 < nf; c0 += kRdInline)
+      hipLaunchKernelGGL(k_rdm_count, dim3(gx_of(c0), part(c0)), dim3(kB), 0, s, files(c0), chunk_cnt);
     size_t tb = tmp_bytes;
     hipError_t e = ds_excl_sum_u32(tmp, tb, chunk_cnt, chunk_scan, nchunks + 1, s);
     if (e) return e;
-    hipLaunchKernelGGL(k_rdm_write, dim3(gx, nf), dim3(kB), 0, s, d_args, chunk_scan);
-    hipLaunchKernelGGL(k_rdm_found, dim3((nf + 63) / 64), dim3(64), 0, s, d_args, chunk_scan, nf);
+    for (uint32_t c0 = 0; c0 < nf; c0 += kRdInline) {
+      const RdFiles r = files(c0);
+      hipLaunchKernelGGL(k_rdm_write, dim3(gx_of(c0), part(c0)), dim3(kB), 0, s, r, chunk_scan);
+      hipLaunchKernelGGL(k_rdm_found, dim3(1), dim3(64), 0, s, r, chunk_scan, part(c0));
+    }
     return hipGetLastError();
   }
-  for (uint32_t f = 0; f < nf; f++) gx = std::max(gx, nblk(std::max<uint64_t>(h_args[f].n_cand, h_args[f].dset_mask + 2ull)));
-  if (stage == 1) {
-    hipLaunchKernelGGL(k_rdm_entry, dim3(gx, nf), dim3(kB), 0, s, d_args);
-    hipLaunchKernelGGL(k_rdm_chain, dim3(gx, nf), dim3(kB), 0, s, d_args);
-    hipLaunchKernelGGL(k_rdm_dups, dim3(gx, nf), dim3(kB), 0, s, d_args);
-    uint32_t gt = 1;
-    for (uint32_t f = 0; f < nf; f++) gt = std::max(gt, (h_args[f].n_cand + kScanTile - 1) / kScanTile);
-    hipLaunchKernelGGL(k_rdm_tile_sums, dim3(gt, nf), dim3(kB), 0, s, d_args);
-    hipLaunchKernelGGL(k_rdm_tile_scan, dim3(gt, nf), dim3(kB), 0, s, d_args);
-    return hipGetLastError();
+  for (uint32_t c0 = 0; c0 < nf; c0 += kRdInline) {
+    const RdFiles r = files(c0);
+    const uint32_t k = part(c0);
+    uint32_t gx = 1;
+    for (uint32_t f = c0; f < c0 + k; f++) gx = std::max(gx, nblk(std::max<uint64_t>(h_args[f].n_cand, h_args[f].dset_mask + 2ull)));
+    if (stage == 1) {
+      hipLaunchKernelGGL(k_rdm_entry, dim3(gx, k), dim3(kB), 0, s, r);
+      hipLaunchKernelGGL(k_rdm_chain, dim3(gx, k), dim3(kB), 0, s, r);
+      hipLaunchKernelGGL(k_rdm_dups, dim3(gx, k), dim3(kB), 0, s, r);
+      uint32_t gt = 1;
+      for (uint32_t f = c0; f < c0 + k; f++) gt = std::max(gt, (h_args[f].n_cand + kScanTile - 1) / kScanTile);
+      hipLaunchKernelGGL(k_rdm_tile_sums, dim3(gt, k), dim3(kB), 0, s, r);
+      hipLaunchKernelGGL(k_rdm_tile_scan, dim3(gt, k), dim3(kB), 0, s, r);
+    } else {
+      hipLaunchKernelGGL(k_rdm_emit, dim3(gx, k), dim3(kB), 0, s, r);
+    }
   }
-  hipLaunchKernelGGL(k_rdm_emit, dim3(gx, nf), dim3(kB), 0, s, d_args);
   return hipGetLastError();
 }
 
@@ -550,7 +602,18 @@ hipError_t launch_orswot_ser_sort(hipStream_t s, OrswotSerScratch& sc, uint32_t 
   // rank, then stably by member, LSD order), gather
   hipError_t e;
   const int kb = sc.member_bits + sc.rank_bits;
-  if (n && kb <= 64 && !getenv("CE_SER_TWO_SORTS")) {
+  // CE_SER_COUNT=1: the counting sort (measured slower at C3: 200 us for hist + scatter + ranks
+  // against 112 us for the radix sort -- its per-member counters are device-scope atomics on
+  // random addresses, which the XCDs' separate L2s cannot keep; r05)
+  const bool count = getenv("CE_SER_COUNT") != nullptr;  // (the tests flip it)
+  if (n && sc.member_bits <= kSerCountBits && sc.bucket_count && count && !getenv("CE_SER_TWO_SORTS")) {
+    const uint32_t nb = (1u << sc.member_bits) + 1;  // buckets: every member value < 2^member_bits, one past
+    size_t tb = sc.tmp_bytes;
+    hipLaunchKernelGGL(k_ser_hist, dim3(nblk(n)), dim3(kB), 0, s, sc.member_in, sc.bucket_count, n);
+    if ((e = ds_excl_sum_u32(sc.tmp, tb, sc.bucket_count, sc.bucket_off, nb, s))) return e;
+    hipLaunchKernelGGL(k_ser_scatter, dim3(nblk(n)), dim3(kB), 0, s, sc, n);
+    hipLaunchKernelGGL(k_ser_slice_rank, dim3(nblk(n)), dim3(kB), 0, s, sc, n);
+  } else if (n && kb <= 64 && !getenv("CE_SER_TWO_SORTS")) {
     // (member, rank) in one key: one radix sort over member_bits + rank_bits
     size_t tb = sc.tmp_bytes;
     if (kb <= 32) {

@@ -879,16 +879,22 @@ def test_orswot_partitioned_fold_equals_global(ctx, adversarial):
     assert got["global"][1:] == (0, len(batches))
 
 
-@pytest.mark.parametrize("n_members", [300, 1 << 40, (1 << 64) - 1])
+@pytest.mark.parametrize("n_members", [300, 1 << 20, 1 << 40, (1 << 64) - 1, "shared"])
 def test_orswot_serializer_one_sort_equals_two(ctx, n_members):
-    """The device serializer sorts the live (member, actor) pairs by one packed key when member
-    bits + actor-rank bits fit 32 (u32 keys) or 64 (u64 keys), else by rank then stably by member;
-    the packed sort == the two-sort form (CE_SER_TWO_SORTS=1) == the oracle's bytes, for small,
-    40-bit and full 64-bit members."""
-    rng = random.Random(929 + n_members % 1000)
+    """The device serializer orders the live (member, actor) pairs by (member, actor UUID rank):
+    by one radix sort of the packed key when member bits + actor-rank bits fit 64, else by rank
+    then stably by member, or (opt-in) by a counting sort over member values below 2^20.  Each
+    form (default, CE_SER_COUNT=1, CE_SER_TWO_SORTS=1) == the oracle's bytes, for
+    small, 20-bit (one past the counting range), 40-bit and full 64-bit members, and for members
+    every one of 300 actors adds (slices of 300 pairs)."""
+    rng = random.Random(929 + (n_members % 1000 if isinstance(n_members, int) else 7))
     key = rng.randbytes(32)
-    actors = G.actors_for(rng, 7)
-    files = G.well_formed_orswot(rng, actors, 3, 8, n_members)[0]
+    if n_members == "shared":
+        actors = G.actors_for(rng, 300)
+        files = {a: [[("Add", (a, 1), [5, 77, 1000 + i % 3])]] for i, a in enumerate(actors)}
+    else:
+        actors = G.actors_for(rng, 7)
+        files = G.well_formed_orswot(rng, actors, 3, 8, n_members)[0]
     acts, clears, fa, fv = G.batch(files, "orswot", APP)
     sealed = seal_files(ctx, key, clears)
     oc = C.Core("orswot")
@@ -896,9 +902,9 @@ def test_orswot_serializer_one_sort_equals_two(ctx, n_members):
     import torch
     want = oc.serialize()
     got = []
-    for two in (False, True):
-        if two:
-            os.environ["CE_SER_TWO_SORTS"] = "1"
+    for mode in (None, "CE_SER_COUNT", "CE_SER_TWO_SORTS"):
+        if mode:
+            os.environ[mode] = "1"
         try:
             core = new_core(ctx, "orswot", key)
             assert core.ingest_ops(sealed, acts, fa, fv)[0] == 0
@@ -909,8 +915,9 @@ def test_orswot_serializer_one_sort_equals_two(ctx, n_members):
             got.append(bytes(buf[:n].cpu().numpy().tobytes()))
             core.close()
         finally:
-            os.environ.pop("CE_SER_TWO_SORTS", None)
-    assert got[0] == got[1] == want
+            if mode:
+                os.environ.pop(mode, None)
+    assert got[0] == got[1] == got[2] == want
 
 
 @pytest.mark.parametrize("kind", ["orswot", "mvreg"])
@@ -1135,3 +1142,27 @@ def test_orswot_fused_decode_equals_lane_decode(ctx, case):
         assert 0 < got[True][2] < n
     elif case in ("well_formed", "foreign_actor"):
         assert 0 < got[True][2] < n
+
+
+def test_orswot_member_table_growth_then_compaction(ctx):
+    """The primary member table grows past half full (ensure_pairs counts the members, rebuilds the
+    tables from a collect of the live pairs) batch after batch; the collect's output counter stays
+    zero between collects (k_ds_collect_max resets it; the member count uses another word), so
+    every rebuild and the device serializer see exactly the live pairs == the oracle."""
+    rng = random.Random(5150)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 16)
+    files = G.well_formed_orswot(rng, actors, 6, 60, 40000, p_rm=0.1, max_members=3)[0]
+    core, oc = new_core(ctx, "orswot", key), C.Core("orswot")
+    import torch
+    for lo in range(0, 6, 2):
+        part = {a: files[a][: lo + 2] for a in files}
+        acts, clears, fa, fv = G.batch(part, "orswot", APP, start={a: lo for a in files})
+        assert check_ops(ctx, "orswot", key, core, oc, acts, clears, fa, fv) == 0
+        want = oc.serialize()
+        buf = torch.zeros(len(want) + 4096, dtype=torch.uint8, device="cuda:0")
+        rc, n = core.state_bytes_device(buf.data_ptr(), buf.numel())
+        assert rc == 0
+        torch.cuda.synchronize()
+        assert bytes(buf[:n].cpu().numpy().tobytes()) == want
+    core.close()
