@@ -1767,8 +1767,10 @@ hipError_t launch_ds_deferred(hipStream_t s, const uint32_t* cbeg, const uint32_
   if (n_rm == 0 && !pub_dst) return hipSuccess;
   // (publishing: live[7] counts the blocks, zero between uses)
   const DsPublish pub{pub_src, pub_dst, pub_words, pub_dst ? const_cast<uint32_t*>(pub_src) + 7 : nullptr};
-  hipLaunchKernelGGL(k_ds_deferred, dim3(std::max<uint32_t>(1, blocks_for(n_rm))), dim3(kBlock), 0, s, cbeg, c_actor,
-                     c_ctr, clock, deferred, n_rm, any, pub);
+  // publishing: a grid of at most 128 blocks (grid-stride), so its last-block count is 128 atomics
+  // on one word -- same-address atomics from every XCD cost ~60 ns each (1600 blocks: 95 us)
+  const uint32_t nb = std::max<uint32_t>(1, pub_dst ? std::min<uint32_t>(128, blocks_for(n_rm)) : blocks_for(n_rm));
+  hipLaunchKernelGGL(k_ds_deferred, dim3(nb), dim3(kBlock), 0, s, cbeg, c_actor, c_ctr, clock, deferred, n_rm, any, pub);
   return hipGetLastError();
 }
 

@@ -264,24 +264,3 @@ void destroy_uploader(ce_ctx* ctx);
 void host_parallel_for(ce_ctx* ctx, uint32_t n, const std::function<void(uint32_t)>& fn);
 
 }  // namespace ce
-
-// TEMP (call-site map of runtime copies / fills): CE_TRACE_COPIES=1
-#include <cstdio>
-namespace ce {
-inline bool trace_copies() { static const bool v = getenv("CE_TRACE_COPIES") != nullptr; return v; }
-inline hipError_t traced_memcpy_async(const char* f, int l, void* d, const void* s, size_t n, hipMemcpyKind k, hipStream_t st = nullptr) {
-  if (trace_copies()) fprintf(stderr, "[op] copy %s:%d %zu k%d\n", f, l, n, (int)k);
-  return hipMemcpyAsync(d, s, n, k, st);
-}
-inline hipError_t traced_memset_async(const char* f, int l, void* d, int v, size_t n, hipStream_t st = nullptr) {
-  if (trace_copies()) fprintf(stderr, "[op] fill %s:%d %zu\n", f, l, n);
-  return hipMemsetAsync(d, v, n, st);
-}
-inline hipError_t traced_memsetd32_async(const char* f, int l, hipDeviceptr_t d, int v, size_t n, hipStream_t st = nullptr) {
-  if (trace_copies()) fprintf(stderr, "[op] fill32 %s:%d %zu\n", f, l, n);
-  return hipMemsetD32Async(d, v, n, st);
-}
-}  // namespace ce
-#define hipMemcpyAsync(...) ::ce::traced_memcpy_async(__FILE__, __LINE__, __VA_ARGS__)
-#define hipMemsetAsync(...) ::ce::traced_memset_async(__FILE__, __LINE__, __VA_ARGS__)
-#define hipMemsetD32Async(...) ::ce::traced_memsetd32_async(__FILE__, __LINE__, __VA_ARGS__)
