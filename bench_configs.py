@@ -1011,12 +1011,15 @@ def run_c3_multi(args, ctx, dev, world, rank):
     k_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in
             ((k, ctx.timing(k)) for k in ("open_setup", "open_small", "segments_open", "gate", "ds_count",
                                          "ds_emit", "ds_applied", "ds_add_pairs", "ds_kill", "ds_finalize",
-                                         "ds_merge", "seal_setup", "segments_seal")) if v[1]}
+                                         "ds_merge", "cols_export", "cols_merge", "seal_setup",
+                                         "segments_seal")) if v[1]}
     # per-hop exchange figures: mean over the timed steps on each rank, max over ranks
     def mean(key_):
         v = [h[key_] for h in hops if key_ in h]
         return sum(v) / len(v) if v else 0.0
-    hop = {k: round(_max_over_ranks(mean(k), dev), 3) for k in ("serialize_ms", "send_ms", "recv_ms", "merge_ms")}
+    hop = {k: round(_max_over_ranks(mean(k), dev), 3)
+           for k in ("serialize_ms", "export_ms", "send_ms", "recv_ms", "merge_ms")}
+    hop["exchange"] = "columns" if core.path_count("columns_merge") or core.path_count("columns_export") else "state bytes"
     hop_bytes = int(_max_over_ranks(max([h["bytes"] for h in hops] or [0]), dev))
     tot = torch.tensor([n + len(my_states)], dtype=torch.int64, device=dev)
     shard.all_reduce_(tot, dist.ReduceOp.SUM)
@@ -1052,11 +1055,15 @@ def run_c3_multi(args, ctx, dev, world, rank):
                                "ranks by writer" % (N_MEMBERS, N_ACTORS, V0, N_ACTORS * V, V, PT_LEN, world),
                    "files_total": n_total, "entries": entries,
                    "parallelism": "writer shards (shard.actor_range) with their 512-writer state groups; "
-                                  "statuses all_reduce(MAX); partial StateWrappers reduced along a binomial "
-                                  "tree to rank 0 in HBM (ce_core_state_bytes_device -> %s send/recv -> "
-                                  "ce_core_merge_state_device); compaction + content name on rank 0"
-                                  % ("RCCL" if comm != "cpu" else "gloo (host-staged)")},
-        "exchange": {"hops_per_step": world - 1, "tree_depth": (world - 1).bit_length(),
+                                  "statuses all_reduce(MAX); %s; compaction + content name on rank 0"
+                                  % (("partial Orswots as columns gathered to rank 0 in HBM "
+                                      "(ce_core_export_columns_device -> %s send/recv -> one "
+                                      "ce_core_merge_columns_device)" if hop["exchange"] == "columns" else
+                                      "partial StateWrappers reduced along a binomial tree to rank 0 in HBM "
+                                      "(ce_core_state_bytes_device -> %s send/recv -> ce_core_merge_state_device)")
+                                     % ("RCCL" if comm != "cpu" else "gloo (host-staged)"))},
+        "exchange": {"hops_per_step": world - 1,
+                     "tree_depth": 1 if hop["exchange"] == "columns" else (world - 1).bit_length(),
                      "max_state_bytes_per_hop": hop_bytes, "per_hop_ms_max_over_ranks": hop},
         "kernels_ms_per_step_rank0": k_ms,
         "phases_ms_per_step_rank0": {k: round(v / args.steps, 3) for k, v in phase.items()},

@@ -58,7 +58,8 @@ EXPORTS = [
     "ce_core_shard_window", "ce_core_ingest_ops_device_sharded", "ce_core_pending_export",
     "ce_core_pending_commit", "ce_core_writer_versions", "ce_shard_stats_host",
     "ce_shard_window_host", "ce_shard_window_exact", "ce_core_compact_ops_device_into",
-    "ce_core_state_bytes_device", "ce_core_merge_state_device", "ce_core_ingest_states_device",
+    "ce_core_state_bytes_device", "ce_core_merge_state_device", "ce_core_export_columns_device",
+    "ce_core_merge_columns_device", "ce_core_ingest_states_device",
     "ce_core_compact_into_async", "ce_core_compact_wait", "ce_host_alloc", "ce_host_free", "ce_content_names",
 ]
 
@@ -615,6 +616,7 @@ class Core:
     def __init__(self, ctx, kind=STATE_GCOUNTER, supported=(), current_data_version=None,
                  local_path=None, remote_path=None, flags=0):
         self.ctx = ctx
+        self.kind = kind
         sup = b"".join(supported)
         cdv = current_data_version or (supported[0] if supported else bytes(16))
         self._keep = [sup, cdv]
@@ -862,6 +864,27 @@ class Core:
         """read_remote_states' merge of one decrypted StateWrapper (lib.rs:447, 458-466)."""
         return lib().ce_core_merge_state(self.p, _cbuf(state_wrapper_msgpack),
                                          ctypes.c_size_t(len(state_wrapper_msgpack)))
+
+    def export_columns_device(self, d_dst, cap):
+        """The column form of an Orswot for the multi-GPU exchange, into device memory d_dst (cap
+        bytes): (rc, length); rc INVALID_ARG with the needed length when cap is too small, with
+        length 0 when the state has no column form (deferred removals: use state_bytes_device)."""
+        n = ctypes.c_uint64(0)
+        rc = lib().ce_core_export_columns_device(self.p, ctypes.c_void_p(d_dst), ctypes.c_uint64(cap), ctypes.byref(n))
+        return rc, n.value
+
+    def columns_ready(self):
+        """the state has a column form now (an Orswot without deferred removals)"""
+        n = ctypes.c_uint64(0)
+        lib().ce_core_export_columns_device(self.p, None, ctypes.c_uint64(0), ctypes.byref(n))
+        return n.value != 0
+
+    def merge_columns_device(self, d_parts, lens):
+        """Merge column partials (device pointers, byte lengths) into the state at once."""
+        k = len(d_parts)
+        ptrs = (ctypes.c_void_p * max(k, 1))(*d_parts)
+        ls = (ctypes.c_uint64 * max(k, 1))(*lens)
+        return lib().ce_core_merge_columns_device(self.p, ptrs, ls, ctypes.c_uint32(k))
 
     def state_bytes_device(self, d_dst, cap):
         """StateWrapper bytes written into device memory d_dst (cap bytes): (rc, length); rc

@@ -2255,6 +2255,25 @@ int ce_core_merge_state_device(ce_core* c, const uint8_t* d_sw, uint64_t len) {
   return ce_core_merge_state(c, h.data(), len);
 }
 
+int ce_core_export_columns_device(ce_core* c, uint8_t* d_dst, uint64_t cap, uint64_t* len) {
+  if (!c || !len || (cap && !d_dst)) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  (void)hipSetDevice(c->ctx->device);
+  *len = 0;
+  if (c->kind != CE_STATE_ORSWOT || c->host_compact)
+    return c->ctx->fail(CE_ERR_INVALID_ARG, "no column form for this state kind: use the state bytes");
+  return ds_export_columns_device(c, d_dst, cap, len);
+}
+
+int ce_core_merge_columns_device(ce_core* c, const uint8_t* const* d_parts, const uint64_t* lens, uint32_t k) {
+  if (!c || (k && (!d_parts || !lens))) return CE_ERR_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->ctx->mu);
+  (void)hipSetDevice(c->ctx->device);
+  if (c->kind != CE_STATE_ORSWOT || c->host_compact)
+    return c->ctx->fail(CE_ERR_INVALID_ARG, "no column form for this state kind: use the state bytes");
+  return ds_merge_columns_device(c, d_parts, lens, k);
+}
+
 void* ce_host_alloc(size_t bytes) {
   void* p = nullptr;
   return hipHostMalloc(&p, bytes ? bytes : 1, 0) == hipSuccess ? p : nullptr;

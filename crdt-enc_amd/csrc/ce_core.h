@@ -243,6 +243,8 @@ int ds_download_fence(ce_core* c, hipStream_t s, bool device);
 // the last fold's / k-way merge's closing counts and deferred set (waits for the stream)
 int ds_settle(ce_core* c);
 int ds_state_bytes_device(ce_core* c, ce_ctx* x, uint8_t* dst, uint64_t cap, uint64_t* len);
+int ds_export_columns_device(ce_core* c, uint8_t* dst, uint64_t cap, uint64_t* len);
+int ds_merge_columns_device(ce_core* c, const uint8_t* const* parts, const uint64_t* lens, uint32_t k);
 // Core::apply_ops for a local Vec<S::Op> (already validated by ds_check_ops)
 int ds_check_ops(ce_core* c, const uint8_t* ops, size_t len);
 int ds_apply_local_ops(ce_core* c, const uint8_t* ops, size_t len);

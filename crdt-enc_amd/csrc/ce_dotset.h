@@ -196,6 +196,7 @@ struct DsMergeSrc {
   const uint32_t* actor;
   const unsigned long long* value;
   uint32_t n;
+  uint32_t* slot;  // optional, n words: k_ds_kput records each pair's slot for k_ds_khold
 };
 // Orswot::merge of nf state files at once (no deferred removals on any side): d_src / h_src the
 // same descriptors in HBM and on the host, oclocks = the files' dense clocks at stride ccap,
@@ -203,6 +204,21 @@ struct DsMergeSrc {
 hipError_t launch_ds_kmerge(hipStream_t s, DsTables t, const DsMergeSrc* d_src, const DsMergeSrc* h_src, uint32_t nf,
                             unsigned long long* clock, const unsigned long long* oclocks, uint32_t ccap,
                             unsigned long long* hold, uint32_t* pub_dst = nullptr);  // pub_dst: live[0..5) -> pinned
+// one column partial of the multi-GPU exchange (ds_merge_columns_device): its actor column and
+// clock remapped to the receiving core's ids
+struct DsColsRemap {
+  const uint32_t* actor;          // np partial-local actor indices
+  uint32_t* ids;                  // np receiver ids (out)
+  const uint32_t* map;            // na: partial-local index -> receiver id (device)
+  const unsigned long long* clock;  // na: the partial's clock by its indices
+  unsigned long long* oclock;     // ccap: dense by receiver id (zeroed; out)
+  uint32_t np, na;
+};
+static constexpr uint32_t kColsInline = 16;
+struct DsColsRemaps {
+  DsColsRemap f[kColsInline];
+};
+hipError_t launch_cols_remap(hipStream_t s, const DsColsRemap* parts, uint32_t k);
 hipError_t launch_ds_merge_finalize(hipStream_t s, DsTables t, const unsigned long long* clock,
                                    const unsigned long long* oclock);
 // live pairs -> (member, actor, value) columns (any order); n_out[0] (zeroed beforehand) = their

@@ -1219,9 +1219,9 @@ __global__ void __launch_bounds__(kBlock) k_ds_kput(DsTables t, DsMergeSrcs src)
   if (src.f0 == 0 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 2) t.live[4] = 0;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < x.n; i += gridDim.x * kBlock) {
     const unsigned long long h = member_find(t, x.member[i], true);
-    if (h == kDsEmpty) continue;
-    const unsigned long long b = pair_find(t, pair_key(h, x.actor[i]), true);
+    const unsigned long long b = h == kDsEmpty ? kDsEmpty : pair_find(t, pair_key(h, x.actor[i]), true);
     if (b != kDsEmpty) atomicMax(&t.oth[b], x.value[i]);
+    if (x.slot) x.slot[i] = b == kDsEmpty ? ~0u : (uint32_t)b;
   }
 }
 
@@ -1229,10 +1229,17 @@ __global__ void __launch_bounds__(kBlock) k_ds_khold(DsTables t, DsMergeSrcs src
   const DsMergeSrc x = src.f[blockIdx.y];
   const uint32_t fb = src.f0 + blockIdx.y;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < x.n; i += gridDim.x * kBlock) {
-    const unsigned long long h = member_find(t, x.member[i], false);
-    if (h == kDsEmpty) continue;
-    const unsigned long long b = pair_find(t, pair_key(h, x.actor[i]), false);
-    if (b == kDsEmpty) continue;
+    unsigned long long b;
+    if (x.slot) {  // recorded by k_ds_kput: no second probe of the member and pair tables
+      const uint32_t r = x.slot[i];
+      if (r == ~0u) continue;
+      b = r;
+    } else {
+      const unsigned long long h = member_find(t, x.member[i], false);
+      if (h == kDsEmpty) continue;
+      b = pair_find(t, pair_key(h, x.actor[i]), false);
+      if (b == kDsEmpty) continue;
+    }
     const unsigned long long c = t.cur[b], o = t.oth[b];
     if (x.value[i] == (c > o ? c : o)) atomicOr(&hold[b], 1ull << fb);
   }
@@ -1811,6 +1818,29 @@ hipError_t launch_ds_kmerge(hipStream_t s, DsTables t, const DsMergeSrc* d_src, 
                      ccap, nf, hold);
   hipLaunchKernelGGL(k_ds_kclock, dim3(std::max<uint32_t>(1, blocks_for(ccap))), dim3(kBlock), 0, s, clock, oclocks,
                      ccap, nf, t.live, pub_dst, 5u);
+  return hipGetLastError();
+}
+
+// Column partials (ds_merge_columns_device): each part's actor column holds indices into its own
+// actor list; map[i] is that actor's id in the receiving core.  ids[j] = map[actor[j]] and the
+// part's clock scattered densely by receiver id into oclock (zeroed beforehand by the caller's fill).
+__global__ void __launch_bounds__(kBlock) k_cols_remap(DsColsRemaps r) {
+  const DsColsRemap x = r.f[blockIdx.y];
+  for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < x.np; j += gridDim.x * kBlock) x.ids[j] = x.map[x.actor[j]];
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < x.na; i += gridDim.x * kBlock) x.oclock[x.map[i]] = x.clock[i];
+}
+
+hipError_t launch_cols_remap(hipStream_t s, const DsColsRemap* parts, uint32_t k) {
+  for (uint32_t c0 = 0; c0 < k; c0 += kColsInline) {
+    DsColsRemaps r{};
+    uint32_t mx = 1;
+    const uint32_t kk = std::min(kColsInline, k - c0);
+    for (uint32_t i = 0; i < kk; i++) {
+      r.f[i] = parts[c0 + i];
+      mx = std::max(mx, std::max(r.f[i].np, r.f[i].na));
+    }
+    hipLaunchKernelGGL(k_cols_remap, dim3(std::min<uint32_t>(blocks_for(mx), 2048), kk), dim3(kBlock), 0, s, r);
+  }
   return hipGetLastError();
 }
 

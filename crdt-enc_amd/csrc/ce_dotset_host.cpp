@@ -18,6 +18,7 @@
 #include <thread>
 
 #include <memory>
+#include <optional>
 
 #include "ce_core.h"
 #include "ce_dotset.h"
@@ -75,12 +76,17 @@ struct DsState {
   // the file-major rows (add actor / counter / member, removal actor / counter / member)
   DevBuf fz_cnt, fz_done, fz_col[6], fz_why;
   DevBuf ser_cnt, ser_off;  // the serializer's counting sort (per-member counts, their scan)
+  // the multi-GPU column exchange (ds_export_columns_device / ds_merge_columns_device)
+  HostBuf cx_host, cx_heads, cx_map;
+  DevBuf cx_mapd, cx_ids, cx_slot;
+  std::vector<uint32_t> cx_idslot;  // actor id -> table slot, as of table_gen cx_idslot_gen
+  uint64_t cx_idslot_gen = ~0ull;
   void* col5_zeroed = nullptr;  // col[5] (the collect counter) was cleared at this address
   // device state reader (per state file: candidates, sorted heads, entry ends, Dot counts and
   // bases, members, sorted members [0..6]
   // and emitted (member, actor id, value) columns [7..9]), pinned staging for its downloads
   std::vector<std::array<DevBuf, 10>> rd;
-  DevBuf rd_tmp, rd_misc, ser[16], uuid_of_id, rank_of_id, id_of_rank, rd_oclocks, cnt_tot, rd_args_d, rd_chunks, rd_gather;
+  DevBuf rd_tmp, rd_misc, ser[16], uuid_of_id, rank_of_id, id_of_rank, rd_oclocks, cnt_tot, rd_args_d, rd_chunks;
   HostBuf rd_host, rd_small, rd_clock, rd_args_h, h_clock;
   uint64_t uuid_ids = ~0ull;  // id count uuid_of_id / rank_of_id (and id_rank / rank_id) were built for
   std::vector<uint32_t> id_rank, rank_id;  // UUID-order rank of each stable id, and its inverse
@@ -1699,12 +1705,11 @@ hipError_t dl(void* dst, const void* src, size_t n, hipStream_t s) {
 // its own blit dispatch with its own gap on the box.  Not synchronised.
 hipError_t gather_download(DsState* d, hipStream_t s, uint8_t* hb, const std::vector<GatherRange>& r,
                            uint64_t total) {
+  // hb is pinned (a HostBuf): the gather kernel writes it through its device address, no staging
+  // copy and no runtime copy launch
+  (void)d;
   if (total == 0) return hipSuccess;
-  hipError_t e;
-  if ((e = d->rd_gather.reserve(total + 64)) ||
-      (e = launch_gather_ranges(s, d->rd_gather.as<uint8_t>(), r.data(), (uint32_t)r.size())))
-    return e;
-  return hipMemcpyAsync(hb, d->rd_gather.p, total, hipMemcpyDeviceToHost, s);
+  return launch_gather_ranges(s, static_cast<uint8_t*>(host_dev_ptr(hb)), r.data(), (uint32_t)r.size());
 }
 
 // the repeat-check set of a file with n entries: a power of two >= 2 n words (mask = size - 1)
@@ -2022,10 +2027,14 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     HostPhase hk("  merge: k-way");
     if ((e = d->rd_args_h.reserve(n * sizeof(DsMergeSrc) + 64)) || (e = d->rd_args_d.reserve(n * sizeof(DsMergeSrc) + 64)))
       return ctx->hip_fail(e, "merge");
+    uint64_t dots = 0;
+    for (size_t i = 0; i < n; i++) dots += ds[i].n_dots;
+    if ((e = d->cx_slot.reserve(4 * dots + 64))) return ctx->hip_fail(e, "merge");
     auto* hs = d->rd_args_h.as<DsMergeSrc>();
-    for (size_t i = 0; i < n; i++) {
+    for (size_t i = 0, q = 0; i < n; q += ds[i].n_dots, i++) {
       auto& b = d->rd[i];
-      hs[i] = DsMergeSrc{b[7].as<unsigned long long>(), b[8].as<uint32_t>(), b[9].as<unsigned long long>(), ds[i].n_dots};
+      hs[i] = DsMergeSrc{b[7].as<unsigned long long>(), b[8].as<uint32_t>(), b[9].as<unsigned long long>(), ds[i].n_dots,
+                         d->cx_slot.as<uint32_t>() + q};
     }
     // no host wait: the merged counts land in pinned memory for ds_settle (the next ingest's
     // first wait), like a fold's
@@ -2514,6 +2523,230 @@ int ds_state_bytes_device(ce_core* c, ce_ctx* x, uint8_t* dst, uint64_t cap, uin
   // complete on return, like the direct write: the caller's collective runs on another stream
   if (n && ((e = hipMemcpyAsync(dst, clear, n, hipMemcpyDeviceToDevice, s)) || (e = stream_wait(s))))
     return x->hip_fail(e, "state bytes");
+  return CE_OK;
+}
+
+// ---- the multi-GPU exchange as columns (include/crdtenc.h ce_core_export_columns_device) ----
+// A rank's partial Orswot goes to the compacting rank as columns -- the live (member, actor,
+// counter) pairs straight from the collect, its clock and next_op_versions, its actor UUIDs --
+// instead of a serialized StateWrapper that the receiver parses back (read_remote_states' merge,
+// crdt-enc/src/lib.rs:458-466, of every rank's partial).  Layout (byte offsets, 8-aligned):
+//   0 u32 magic 'CECL' | u32 version 1 | u64 pairs np | u32 actors na | u32 flags | u64 0
+//   32 uuid[16 na] | clock u64[na] | nov u64[na] | member u64[np] | value u64[np] | actor u32[np]
+// (actor = an index into the partial's own UUID list).  Deferred removals have no column form:
+// such a state is refused (*len = 0) and goes as state bytes.
+namespace {
+constexpr uint32_t kColsMagic = 0x4c434543u;  // "CECL"
+struct ColsHeader {
+  uint32_t magic, version;
+  uint64_t np;
+  uint32_t na, flags;
+  uint64_t reserved;
+};
+static_assert(sizeof(ColsHeader) == 32, "column partial header");
+uint64_t cols_len(uint64_t na, uint64_t np) { return 32 + 32 * na + 20 * np; }
+}  // namespace
+
+int ds_export_columns_device(ce_core* c, uint8_t* dst, uint64_t cap, uint64_t* len) {
+  if (int rs = ds_settle(c)) return rs;
+  DsState* d = c->ds;
+  ce_ctx* ctx = c->ctx;
+  hipStream_t s = ctx->stream;
+  *len = 0;
+  if (c->kind != CE_STATE_ORSWOT || !d->deferred.empty())
+    return ctx->fail(CE_ERR_INVALID_ARG, "no column form (deferred removals or not an Orswot): use the state bytes");
+  if (!dst && cap == 0) {  // the query form: *len = 1, the state has a column form
+    *len = 1;
+    return CE_ERR_INVALID_ARG;
+  }
+  int rc;
+  hipError_t e;
+  if ((rc = ensure_clock(c))) return rc;
+  uint32_t nl = 0;
+  if ((rc = collect(c, &nl))) return rc;
+  const uint32_t na = (uint32_t)c->id_actor.size();
+  const uint64_t need = cols_len(na, nl);
+  *len = need;
+  if (need > cap) return ctx->fail(CE_ERR_INVALID_ARG, "device buffer too small for the columns");
+  // header, UUIDs and next versions by id: built in pinned memory, read by the copy launch
+  if ((e = d->cx_host.reserve(32 + 24ull * na + 64))) return ctx->hip_fail(e, "columns");
+  uint8_t* h = d->cx_host.as<uint8_t>();
+  const ColsHeader hd{kColsMagic, 1u, nl, na, 0u, 0ull};
+  std::memcpy(h, &hd, 32);
+  for (uint32_t i = 0; i < na; i++) std::memcpy(h + 32 + 16ull * i, c->id_actor[i].data(), 16);
+  uint64_t* hn = reinterpret_cast<uint64_t*>(h + 32 + 16ull * na);
+  std::fill(hn, hn + na, 0ull);
+  for (uint32_t sl = 0; sl < c->cap; sl++)
+    if (c->h_table[sl].used && c->nov[sl]) hn[actor_id_of_slot(c, sl)] = c->nov[sl];
+  const uint32_t* hdev = static_cast<const uint32_t*>(host_dev_ptr(h));
+  const uint64_t o_clock = 32 + 16ull * na, o_nov = o_clock + 8ull * na, o_mem = o_nov + 8ull * na,
+                 o_val = o_mem + 8ull * nl, o_act = o_val + 8ull * nl;
+  auto w = [&](uint64_t o) { return reinterpret_cast<uint32_t*>(dst + o); };
+  FillArgs fl{};
+  fl.r[fl.n++] = {w(0), (32 + 16ull * na) / 4, 0u, hdev};
+  fl.r[fl.n++] = {w(o_clock), 2ull * na, 0u, d->clock.as<uint32_t>()};
+  fl.r[fl.n++] = {w(o_nov), 2ull * na, 0u, hdev + (32 + 16ull * na) / 4};
+  fl.r[fl.n++] = {w(o_mem), 2ull * nl, 0u, d->col[0].as<uint32_t>()};
+  fl.r[fl.n++] = {w(o_val), 2ull * nl, 0u, d->col[2].as<uint32_t>()};
+  fl.r[fl.n++] = {w(o_act), nl, 0u, d->col[1].as<uint32_t>()};
+  // complete on return, as the state-bytes export: the caller's collective runs on another stream
+  const int tx = ctx->tbegin("cols_export");
+  if ((e = launch_fill(s, fl))) return ctx->hip_fail(e, "columns");
+  ctx->tend(tx);
+  if ((e = stream_wait(s))) return ctx->hip_fail(e, "columns");
+  c->path_counts["columns_export"]++;
+  return CE_OK;
+}
+
+int ds_merge_columns_device(ce_core* c, const uint8_t* const* parts, const uint64_t* lens, uint32_t k) {
+  if (int rs = ds_settle(c)) return rs;
+  DsState* d = c->ds;
+  ce_ctx* ctx = c->ctx;
+  hipStream_t s = ctx->stream;
+  if (c->kind != CE_STATE_ORSWOT || !d->deferred.empty())
+    return ctx->fail(CE_ERR_INVALID_ARG, "no column merge (deferred removals or not an Orswot): use the state bytes");
+  if (k == 0) return CE_OK;
+  if (k > 64) return ctx->fail(CE_ERR_INVALID_ARG, "at most 64 column partials per merge");
+  hipError_t e;
+  int rc;
+  std::optional<HostPhase> ph;  // CE_HOST_PROF
+  ph.emplace("  cols: download");
+  // 1) every part's header, UUIDs, clock and next versions in one gathered download, sized for
+  //    as many actors as this core knows (a second one only for parts naming more)
+  const uint64_t guess = 32 + 32ull * std::max<uint64_t>(c->id_actor.size(), 64);
+  std::vector<uint64_t> pre(k), poff(k);
+  uint64_t tot = 0;
+  for (uint32_t f = 0; f < k; f++) {
+    if (lens[f] < 32) return ctx->fail(CE_ERR_DECODE, "not a column partial");
+    pre[f] = std::min<uint64_t>(lens[f], guess) & ~7ull;
+    poff[f] = tot;
+    tot += pre[f];
+  }
+  if ((e = d->cx_host.reserve(tot + 64))) return ctx->hip_fail(e, "columns");
+  {
+    std::vector<GatherRange> gr;
+    for (uint32_t f = 0; f < k; f++) gr.push_back({parts[f], poff[f], pre[f]});
+    if ((e = gather_download(d, s, d->cx_host.as<uint8_t>(), gr, tot)) || (e = stream_wait(s)))
+      return ctx->hip_fail(e, "columns");
+  }
+  std::vector<ColsHeader> hd(k);
+  std::vector<const uint8_t*> base(k);
+  uint64_t np_tot = 0, more = 0;
+  for (uint32_t f = 0; f < k; f++) {
+    base[f] = d->cx_host.as<uint8_t>() + poff[f];
+    std::memcpy(&hd[f], base[f], 32);
+    if (hd[f].magic != kColsMagic || hd[f].version != 1 || hd[f].flags ||
+        cols_len(hd[f].na, hd[f].np) != lens[f] || hd[f].np >= (1ull << 31))
+      return ctx->fail(CE_ERR_DECODE, "not a column partial");
+    np_tot += hd[f].np;
+    if (32 + 32ull * hd[f].na > pre[f]) more += 32 + 32ull * hd[f].na;
+  }
+  if (more) {
+    if ((e = d->cx_heads.reserve(more + 64))) return ctx->hip_fail(e, "columns");
+    std::vector<GatherRange> gr;
+    uint64_t o = 0;
+    for (uint32_t f = 0; f < k; f++)
+      if (32 + 32ull * hd[f].na > pre[f]) {
+        gr.push_back({parts[f], o, 32 + 32ull * hd[f].na});
+        base[f] = d->cx_heads.as<uint8_t>() + o;
+        o += 32 + 32ull * hd[f].na;
+      }
+    if ((e = gather_download(d, s, d->cx_heads.as<uint8_t>(), gr, more)) || (e = stream_wait(s)))
+      return ctx->hip_fail(e, "columns");
+  }
+  ph.emplace("  cols: actors");
+  // 2) every part's actors in this core's table (ids), next_op_versions merged (VClock::merge).
+  //    A part whose UUID list is this core's id order (every rank registered the same actors)
+  //    maps by identity, its next versions through the cached id -> slot list.
+  auto idslot = [&]() {
+    if (d->cx_idslot_gen != c->table_gen || d->cx_idslot.size() != c->id_actor.size()) {
+      d->cx_idslot.assign(c->id_actor.size(), 0u);
+      for (uint32_t sl = 0; sl < c->cap; sl++)
+        if (c->h_table[sl].used) d->cx_idslot[actor_id_of_slot(c, sl)] = sl;
+      d->cx_idslot_gen = c->table_gen;
+    }
+  };
+  uint64_t maps = 0;
+  for (uint32_t f = 0; f < k; f++) maps += hd[f].na;
+  if ((e = d->cx_map.reserve(4 * maps + 64)) || (e = d->cx_mapd.reserve(4 * maps + 64)) ||
+      (e = d->cx_ids.reserve(4 * np_tot + 64)) || (e = d->cx_slot.reserve(4 * np_tot + 64)))
+    return ctx->hip_fail(e, "columns");
+  uint32_t* hmap = d->cx_map.as<uint32_t>();
+  {
+    uint64_t m = 0;
+    for (uint32_t f = 0; f < k; f++) {
+      const uint32_t na = hd[f].na;
+      const uint8_t* u = base[f] + 32;
+      const uint64_t* nv = reinterpret_cast<const uint64_t*>(u + 24ull * na);
+      const bool ident = na <= c->id_actor.size() && (na == 0 || std::memcmp(u, c->id_actor.data(), 16ull * na) == 0);
+      if (ident) {
+        idslot();  // (an earlier part's new actors may have moved the slots)
+        for (uint32_t i = 0; i < na; i++) {
+          hmap[m + i] = i;
+          if (nv[i]) {
+            uint64_t& x = c->nov[d->cx_idslot[i]];
+            x = std::max(x, nv[i]);
+          }
+        }
+      } else {
+        for (uint32_t i = 0; i < na; i++) {
+          Uuid id;
+          std::memcpy(id.data(), u + 16ull * i, 16);
+          uint32_t sl;
+          if ((rc = insert_actor(c, id, &sl))) return rc;
+          hmap[m + i] = actor_id_of_slot(c, sl);
+          if (nv[i]) c->nov[sl] = std::max(c->nov[sl], nv[i]);
+        }
+      }
+      m += na;
+    }
+  }
+  ph.emplace("  cols: tables");
+  if ((rc = table_upload(c)) || (rc = ensure_clock(c)) || (rc = ensure_pairs(c, np_tot))) return rc;
+  ph.emplace("  cols: launch");
+  // 3) maps uploaded and the dense other-clocks zeroed in one launch, then the remap
+  const uint32_t ccap = d->clock_cap;
+  if ((e = d->rd_oclocks.reserve(8ull * ccap * k + 64))) return ctx->hip_fail(e, "columns");
+  FillArgs fl{};
+  fl.r[fl.n++] = {d->cx_mapd.as<uint32_t>(), maps, 0u, static_cast<const uint32_t*>(host_dev_ptr(hmap))};
+  fl.r[fl.n++] = {d->rd_oclocks.as<uint32_t>(), 2ull * ccap * k, 0u};
+  std::vector<DsColsRemap> rm(k);
+  std::vector<DsMergeSrc> src(k);
+  {
+    uint64_t m = 0, q = 0;
+    for (uint32_t f = 0; f < k; f++) {
+      const uint64_t na = hd[f].na, np = hd[f].np;
+      const uint8_t* b = parts[f];
+      const uint64_t o_clock = 32 + 16 * na, o_mem = o_clock + 16 * na, o_val = o_mem + 8 * np, o_act = o_val + 8 * np;
+      rm[f] = DsColsRemap{reinterpret_cast<const uint32_t*>(b + o_act), d->cx_ids.as<uint32_t>() + q,
+                          d->cx_mapd.as<uint32_t>() + m, reinterpret_cast<const unsigned long long*>(b + o_clock),
+                          d->rd_oclocks.as<unsigned long long>() + (size_t)ccap * f, (uint32_t)np, (uint32_t)na};
+      src[f] = DsMergeSrc{reinterpret_cast<const unsigned long long*>(b + o_mem), d->cx_ids.as<uint32_t>() + q,
+                          reinterpret_cast<const unsigned long long*>(b + o_val), (uint32_t)np,
+                          d->cx_slot.as<uint32_t>() + q};
+      m += na;
+      q += np;
+    }
+  }
+  // 4) one k-way merge of every part into the state (launch_ds_kmerge; the live counts land in
+  //    pinned memory for ds_settle, like the state files' merge)
+  d->scratch_dirty = true;
+  const int tm = ctx->tbegin("cols_merge");
+  if ((e = launch_fill(s, fl)) || (e = launch_cols_remap(s, rm.data(), k)) ||
+      (e = launch_ds_kmerge(s, tables(d), nullptr, src.data(), k, d->clock.as<unsigned long long>(),
+                            d->rd_oclocks.as<unsigned long long>(), ccap, d->hold.as<unsigned long long>(),
+                            static_cast<uint32_t*>(host_dev_ptr(d->h_cnt.as<uint32_t>() + 56)))))
+    return ctx->hip_fail(e, "columns");
+  ctx->tend(tm);
+  d->scratch_dirty = false;
+  d->settle_pending = true;
+  d->settle_fold = false;
+  d->settle_delta = false;
+  d->settle_members = true;
+  c->path_counts["columns_merge"]++;
+  // the parts may be reused by the caller after the return: the merge reads them
+  ph.emplace("  cols: settle");
+  if ((rc = ds_settle(c))) return rc;
   return CE_OK;
 }
 

@@ -29,6 +29,8 @@ the merged state everywhere).  Sharding by writer keeps every actor's ops on one
 partial state is an op-based replica of that shard and the merge equals one fold over all files
 (SURVEY.md §8e).
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -169,6 +171,14 @@ class StateBuffer:
 _ERR_INVALID_ARG = 64
 
 
+def _on_comm_device(t, comm_device):
+    """t already lives where the collectives run (a plain "cuda" means the current device)"""
+    d = torch.device(comm_device)
+    if d.type == "cuda" and d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return t.device == d
+
+
 def _send_state_device(core, buf, dst, group, comm_device, timing):
     """core's StateWrapper serialized into HBM (ce_core_state_bytes_device: the device writer,
     complete on return) -> dist.send.  With RCCL the bytes go GPU to GPU; gloo stages them
@@ -185,7 +195,10 @@ def _send_state_device(core, buf, dst, group, comm_device, timing):
     t1 = time.perf_counter()
     dist.send(torch.tensor([n], dtype=torch.int64, device=comm_device), dst, group=group)
     if n:
-        dist.send(t[:n] if t.device == torch.device(comm_device) else t[:n].to(comm_device), dst, group=group)
+        dist.send(t[:n] if _on_comm_device(t, comm_device) else t[:n].to(comm_device), dst, group=group)
+        # the buffer is written again by the next export on the core's stream: the send (queued on
+        # torch's stream under RCCL) must have read it first
+        torch.cuda.current_stream(t.device).synchronize()
     if timing is not None:
         timing.append({"send": True, "bytes": n, "serialize_ms": round((t1 - t0) * 1e3, 3),
                        "send_ms": round((time.perf_counter() - t1) * 1e3, 3)})
@@ -202,7 +215,7 @@ def _recv_merge_device(core, buf, src, group, comm_device, timing):
     if not n:
         raise RuntimeError("rank %d sent an empty state" % src)
     t = buf.ensure(n)
-    if t.device == torch.device(comm_device):
+    if _on_comm_device(t, comm_device):
         dist.recv(t[:n], src, group=group)
         # the receive completes on torch's stream; the core reads on its own stream
         torch.cuda.current_stream(t.device).synchronize()
@@ -218,6 +231,76 @@ def _recv_merge_device(core, buf, src, group, comm_device, timing):
     if timing is not None:
         timing.append({"recv": True, "bytes": n, "recv_ms": round((t1 - t0) * 1e3, 3),
                        "merge_ms": round((time.perf_counter() - t1) * 1e3, 3)})
+
+
+def _columns_ok(core, group, device):
+    """every rank can exchange its partial as columns (no deferred removals anywhere): one
+    all_reduce(MAX) of a refusal flag, so all ranks take the same path"""
+    flag = torch.tensor([0 if core.columns_ready() else 1], dtype=torch.int64, device=device)
+    all_reduce_(flag, dist.ReduceOp.MAX, group=group)
+    return int(flag.item()) == 0
+
+
+def gather_dotset_columns(core, group=None, device="cpu", dst=0, buf=None, timing=None):
+    """Merge the partial Orswots of all ranks into rank `dst`'s `core` in ONE k-way merge: every
+    other rank exports its state as columns (ce_core_export_columns_device: the live pairs, clock,
+    next versions and actor UUIDs straight from the device, no msgpack) and sends them to `dst`,
+    which merges all N - 1 partials at once (ce_core_merge_columns_device; read_remote_states'
+    merge, crdt-enc/src/lib.rs:458-466, of every partial, in one pass).  RCCL moves device tensors
+    GPU to GPU; gloo stages them through the host.  Returns the merges this rank ran (1 on dst)."""
+    import time
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    if buf is None:
+        buf = StateBuffer(torch.device("cuda", core.ctx.device))
+    if rank != dst:
+        t0 = time.perf_counter()
+        t = buf.ensure(1 << 20)
+        rc, n = core.export_columns_device(t.data_ptr(), t.numel())
+        if rc == _ERR_INVALID_ARG and n > t.numel():
+            t = buf.ensure(n)
+            rc, n = core.export_columns_device(t.data_ptr(), t.numel())
+        if rc:
+            raise RuntimeError("export_columns_device failed: %d" % rc)
+        t1 = time.perf_counter()
+        peer = _global(group, dst)
+        dist.send(torch.tensor([n], dtype=torch.int64, device=device), peer, group=group)
+        dist.send(t[:n] if _on_comm_device(t, device) else t[:n].to(device), peer, group=group)
+        torch.cuda.current_stream(t.device).synchronize()  # the next export rewrites the buffer
+        if timing is not None:
+            timing.append({"send": True, "bytes": n, "export_ms": round((t1 - t0) * 1e3, 3),
+                           "send_ms": round((time.perf_counter() - t1) * 1e3, 3)})
+        return 0
+    t0 = time.perf_counter()
+    parts = getattr(buf, "parts", None)
+    if parts is None:
+        parts = buf.parts = {}
+    ptrs, lens = [], []
+    for r in range(world):
+        if r == dst:
+            continue
+        peer = _global(group, r)
+        hdr = torch.zeros(1, dtype=torch.int64, device=device)
+        dist.recv(hdr, peer, group=group)
+        n = int(hdr.item())
+        pb = parts.setdefault(r, StateBuffer(buf.device))
+        t = pb.ensure(n)
+        if _on_comm_device(t, device):
+            dist.recv(t[:n], peer, group=group)
+        else:
+            h = torch.empty(n, dtype=torch.uint8, device=device)
+            dist.recv(h, peer, group=group)
+            t[:n].copy_(h)
+        ptrs.append(t.data_ptr())
+        lens.append(n)
+    torch.cuda.current_stream(buf.device).synchronize()  # the receives land on torch's stream
+    t1 = time.perf_counter()
+    rc = core.merge_columns_device(ptrs, lens)
+    if rc:
+        raise RuntimeError("merge_columns_device failed: %d" % rc)
+    if timing is not None:
+        timing.append({"recv": True, "parts": len(lens), "bytes": sum(lens), "recv_ms": round((t1 - t0) * 1e3, 3),
+                       "merge_ms": round((time.perf_counter() - t1) * 1e3, 3)})
+    return 1
 
 
 def reduce_dotset(core, group=None, device="cpu", dst=0, buf=None, timing=None):
@@ -237,6 +320,11 @@ def reduce_dotset(core, group=None, device="cpu", dst=0, buf=None, timing=None):
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     rel = (rank - dst) % world
     on_device = hasattr(core, "state_bytes_device")
+    # device Orswot cores: the partials as columns, one k-way merge on dst (CE_DS_EXCHANGE=tree:
+    # the binomial tree of serialized partials below, for A/B)
+    if (on_device and world > 1 and hasattr(core, "export_columns_device") and getattr(core, "kind", None) == 2
+            and os.environ.get("CE_DS_EXCHANGE") != "tree" and _columns_ok(core, group, device)):
+        return gather_dotset_columns(core, group=group, device=device, dst=dst, buf=buf, timing=timing)
     if on_device and buf is None:
         buf = StateBuffer(torch.device("cuda", core.ctx.device))
     merges, step = 0, 1

@@ -52,7 +52,7 @@ def workload(mode, seed=77, n_actors=6, versions=5):
     return key, actors, files, fa, fv
 
 
-def workload_orswot(seed=88, n_actors=8, versions=4):
+def workload_orswot(seed=88, n_actors=8, versions=4, p_rm=0.2):
     """Seeded well-formed Orswot op files (tests/dotset_gen.py), sealed with the oracle, in
     load_ops order: removals may name other writers' adds, so a rank's partial state carries
     deferred removals the exchange has to resolve."""
@@ -62,7 +62,7 @@ def workload_orswot(seed=88, n_actors=8, versions=4):
     rng = random.Random(seed)
     key = rng.randbytes(32)
     actors = G.actors_for(rng, n_actors)
-    files = G.well_formed_orswot(rng, actors, versions, 6, 30)[0]
+    files = G.well_formed_orswot(rng, actors, versions, 6, 30, p_rm=p_rm)[0]
     acts, clears, fa, fv = G.batch(files, "orswot", APP)
     sealed = []
     for c in clears:
@@ -72,10 +72,10 @@ def workload_orswot(seed=88, n_actors=8, versions=4):
     return key, acts, sealed, fa, fv
 
 
-def main_orswot(rank, world, out, tree=False):
+def main_orswot(rank, world, out, tree=False, p_rm=0.2):
     import crdtenc
     import shard
-    key, actors, files, fa, fv = workload_orswot()
+    key, actors, files, fa, fv = workload_orswot(p_rm=p_rm)
     ctx = crdtenc.Context(0)
     core = crdtenc.Core(ctx, kind=crdtenc.STATE_ORSWOT, supported=[APP], current_data_version=APP)
     core.set_latest_key(key)
@@ -89,7 +89,7 @@ def main_orswot(rank, world, out, tree=False):
     if tree:   # the binomial-tree reduce to rank 0 (shard.ingest_dotset_sharded)
         rc, merges = shard.ingest_dotset_sharded(core, ingest)
         assert rc == 0, rc
-        tag = b"tree %d" % merges
+        tag = b"tree %d %d" % (merges, core.path_count("columns_merge"))
     else:
         rc = ingest()
         assert rc == 0, rc
@@ -152,8 +152,9 @@ def main():
     import shard
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        if mode in ("orswot", "orswot_tree"):
-            main_orswot(rank, world, out, tree=mode == "orswot_tree")
+        if mode in ("orswot", "orswot_tree", "orswot_adds"):
+            # orswot_adds: adds only, no deferred removal -- the column exchange
+            main_orswot(rank, world, out, tree=mode != "orswot", p_rm=0.0 if mode == "orswot_adds" else 0.2)
             return
         if mode.startswith("sharded:"):
             main_sharded(rank, world, mode.split(":", 1)[1], out)

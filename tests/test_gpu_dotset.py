@@ -1166,3 +1166,60 @@ def test_orswot_member_table_growth_then_compaction(ctx):
         torch.cuda.synchronize()
         assert bytes(buf[:n].cpu().numpy().tobytes()) == want
     core.close()
+
+
+def test_columns_export_merge_equals_state_merge(ctx):
+    """The column form of the multi-GPU exchange through the C ABI: writer shards folded on
+    separate cores, the others' states exported as columns into HBM and merged into the first in
+    one k-way merge == merging their StateWrappers one by one == one core over every file == the
+    oracle; a state with a deferred removal has no column form (*len = 0) and the receiver with
+    one refuses the merge."""
+    import torch
+    rng = random.Random(6060)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 12)
+    files = G.well_formed_orswot(rng, actors, 4, 10, 500, p_rm=0.0)[0]
+    acts, clears, fa, fv = G.batch(files, "orswot", APP)
+    sealed = seal_files(ctx, key, clears)
+    oc = C.Core("orswot")
+    assert oc.read_remote_ops(key, [APP], sealed, [acts[i] for i in fa], fv)[0] == 0
+    shards = []
+    for r in range(4):
+        idx = [i for i in range(len(fa)) if fa[i] % 4 == r]
+        core = new_core(ctx, "orswot", key)
+        assert core.ingest_ops([sealed[i] for i in idx], acts, [fa[i] for i in idx], [fv[i] for i in idx])[0] == 0
+        shards.append(core)
+    bufs, lens = [], []
+    for core in shards[1:]:
+        assert core.columns_ready()
+        rc, n = core.export_columns_device(0, 0)
+        assert rc == 64 and n == 1                  # the query form
+        t = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda:0")
+        rc, n = core.export_columns_device(t.data_ptr(), 64)
+        assert rc == 64 and n > 64                  # too small: the needed length
+        t = torch.zeros(n + 128, dtype=torch.uint8, device="cuda:0")
+        rc, n2 = core.export_columns_device(t.data_ptr(), t.numel())
+        assert rc == 0 and n2 == n
+        bufs.append(t)
+        lens.append(n)
+    seq = new_core(ctx, "orswot", key)
+    assert seq.merge_state(shards[0].state_bytes()) == 0
+    for core in shards[1:]:
+        assert seq.merge_state(core.state_bytes()) == 0
+    assert shards[0].merge_columns_device([t.data_ptr() for t in bufs], lens) == 0
+    assert shards[0].state_bytes() == seq.state_bytes() == oc.serialize()
+    assert shards[0].path_count("columns_merge") == 1
+    # not a column partial: refused, state unchanged
+    bad = torch.zeros(256, dtype=torch.uint8, device="cuda:0")
+    assert shards[1].merge_columns_device([bad.data_ptr()], [256]) == 12
+    # deferred removals: no column form
+    dfiles = {acts[0]: [[("Rm", C.VClock({acts[1]: 99}), [7])]]}
+    dacts, dclears, dfa, dfv = G.batch(dfiles, "orswot", APP, start={acts[0]: 0})
+    d = new_core(ctx, "orswot", key)
+    assert d.ingest_ops(seal_files(ctx, key, dclears), dacts, dfa, dfv)[0] == 0
+    assert not d.columns_ready()
+    rc, n = d.export_columns_device(bufs[0].data_ptr(), bufs[0].numel())
+    assert rc == 64 and n == 0
+    assert d.merge_columns_device([bufs[0].data_ptr()], [lens[0]]) == 64
+    for core in shards + [seq, d]:
+        core.close()

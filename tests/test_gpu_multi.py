@@ -46,6 +46,8 @@ def test_bench_two_ranks_share_gpu():
         assert cl["checks"] and all(cl["checks"].values()), (c, cl["checks"])
     assert line["configs"]["c3"]["exchange"]["hops_per_step"] == 1
     assert line["configs"]["c3"]["exchange"]["max_state_bytes_per_hop"] > 0
+    # C3's removals name the writer's own adds: no deferred removal, the partials go as columns
+    assert line["configs"]["c3"]["exchange"]["per_hop_ms_max_over_ranks"]["exchange"] == "columns"
     assert line["configs"]["c5"]["config"]["path"] == "rejected"
 
 
@@ -111,7 +113,40 @@ def test_reduce_dotset_two_processes(tmp_path):
     assert [p.wait(timeout=180) for p in procs] == [0, 0]
     with open(out + ".0", "rb") as f:
         tag, state = f.read().split(b"\n", 1)
-    assert tag == b"tree 1" and state == oc.serialize()
+    # (this workload's partials carry deferred removals: the serialized tree, not the columns)
+    assert tag == b"tree 1 0" and state == oc.serialize()
     with open(out + ".1", "rb") as f:
-        assert f.read().split(b"\n", 1)[0] == b"tree 0"
+        assert f.read().split(b"\n", 1)[0] == b"tree 0 0"
+
+
+@pytest.mark.parametrize("world,exchange", [(3, "columns"), (3, "tree")])
+def test_reduce_dotset_columns_three_processes(tmp_path, world, exchange):
+    """The column exchange (no deferred removal on any rank): ranks 1..N-1 export their partial
+    Orswot as columns (ce_core_export_columns_device), rank 0 merges all of them in one k-way merge
+    (ce_core_merge_columns_device) and holds the oracle's single fold; CE_DS_EXCHANGE=tree takes
+    the serialized binomial tree for the same files, with the same result."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import multi_rank_worker as W
+    from oracle import crdts as C
+    key, actors, files, fa, fv = W.workload_orswot(p_rm=0.0)
+    oc = C.Core("orswot")
+    assert oc.read_remote_ops(key, [APP], files, [actors[i] for i in fa], fv)[0] == 0
+    out = str(tmp_path / "t")
+    port = str(_port())
+    env = dict(os.environ)
+    if exchange == "tree":
+        env["CE_DS_EXCHANGE"] = "tree"
+    procs = [subprocess.Popen([sys.executable, os.path.join(REPO, "tests", "multi_rank_worker.py"),
+                               str(r), str(world), port, "orswot_adds", out], env=env) for r in range(world)]
+    assert [p.wait(timeout=180) for p in procs] == [0] * world
+    with open(out + ".0", "rb") as f:
+        tag, state = f.read().split(b"\n", 1)
+    assert state == oc.serialize()
+    if exchange == "columns":
+        assert tag == b"tree 1 1"          # one merge, the column form
+        for r in range(1, world):
+            with open("%s.%d" % (out, r), "rb") as f:
+                assert f.read().split(b"\n", 1)[0] == b"tree 0 0"
+    else:
+        assert tag == b"tree 2 0"          # ceil(log2 3) serialized merges
 
