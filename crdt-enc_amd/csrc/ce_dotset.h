@@ -116,7 +116,7 @@ hipError_t launch_ds_applied(hipStream_t s, const uint32_t* keys_sorted, const u
 // flag |= 1 unless every actor's adds are one contiguous run (marks: u32[n_marks] holding older
 // generations only; gen = a fresh nonzero value per check)
 hipError_t launch_ds_contig(hipStream_t s, const uint32_t* actor, uint32_t n, uint32_t* marks, uint32_t n_marks,
-                            uint32_t gen, uint32_t* flag);
+                            uint32_t gen, uint32_t* flag, const uint32_t* miss_src = nullptr, uint32_t* pub = nullptr);
 // clock[a] = max(clock[a], counter) for every add
 hipError_t launch_ds_clock(hipStream_t s, const uint32_t* keys_sorted, const unsigned long long* ctr_sorted,
                            const unsigned long long* excl_max, unsigned long long* clock, uint32_t n_add);
@@ -131,18 +131,24 @@ hipError_t launch_ds_kill(hipStream_t s, DsTables t, const uint32_t* cbeg, const
 hipError_t launch_ds_finalize(hipStream_t s, DsTables t);
 
 // The partitioned fold (adds + removals + finalize of one Orswot batch; the global kernels above
-// remain for batches outside its limits).  Every (pair key, value) item is bucketed by its
-// pair-table partition, then one workgroup per partition loads the partition's keys into LDS,
-// inserts the adds / max-merges their counters and the removal thresholds there, and writes back
-// only the slots that changed:
-//   launch_ds_part_count   K1: adds (member insert, pair key per add member, per-block partition
-//                          histogram), then removals (member lookup, histogram) -- two launches,
-//                          so a removal's lookup sees every member the batch's adds inserted
-//   ds_excl_sum_u32        hist -> off (the bases of every (partition, block) run)
-//   launch_ds_part_apply   K3 scatter of the items by partition, K4 one workgroup per partition
-// live[0] += change of the live-pair count (two's complement), live[1] += pairs inserted; K1
-// zeroes live[0], live[1] and live[3].
-static constexpr uint32_t kDsPartChunk = 8192;      // adds / removals per K1 / K3 block
+// remain for batches outside its limits).  Every (pair key, value) item goes to its pair-table
+// partition's run, then one workgroup per partition loads the partition's keys into LDS, inserts
+// the adds / max-merges their counters and the removal thresholds there, and writes back only the
+// slots that changed:
+//   launch_ds_part_count   K1: adds (member insert, pair key per add member), then removals
+//                          (member lookup) -- two launches, so a removal's lookup sees every member
+//                          the batch's adds inserted.  Each block counts its items per partition in
+//                          LDS, reserves its share of every partition's run with one returning add
+//                          per partition on pcnt (contiguous counters: 256 B per wave instruction),
+//                          and writes its items there: no histogram, scan or scatter pass
+//   launch_ds_part_apply   K4 one workgroup per partition over its runs
+// A partition's run holds cap items (the batch's expected share x the host's factor); the items of
+// a block whose reservation passes it go to the overflow list, which every apply workgroup then
+// filters for its partition (correct at any skew; the host widens the runs after one).  pcnt is
+// zeroed by the apply that reads it; ovf_n by parity (the apply of fold g zeroes fold g + 1's).
+// live[0] += change of the live-pair count (two's complement), live[1] += pairs inserted, live[5]
+// = items that overflowed; K1 zeroes live[0], live[1], live[3] and live[4].
+static constexpr uint32_t kDsPartChunk = 8192;      // adds / removals per K1 block (one trip)
 static constexpr uint32_t kDsPartMaxParts = 16384;  // LDS histogram bound (64 KB)
 struct DsKillSrc {
   const uint32_t* cbeg;
@@ -150,7 +156,7 @@ struct DsKillSrc {
   const uint32_t* c_actor;
   const unsigned long long* c_ctr;
   const unsigned long long* mem;
-  unsigned long long* hk;       // K1 -> K3: member handle per removal member (kDsEmpty: absent)
+  unsigned long long* hk;       // K1: member handle per removal member of a removal with several items
   uint32_t n;
 };
 struct DsPartArgs {
@@ -158,17 +164,20 @@ struct DsPartArgs {
   DsOps o;
   const uint8_t* applied;
   uint32_t n_add;
-  unsigned long long* akey;     // K1 -> K3: pair key per add member (kDsEmpty: not inserted)
+  unsigned long long* akey;     // K1: pair key per member of an add with several members
   DsKillSrc ks[2];              // the batch's removals, the deferred set
   uint32_t ba, bk0, bk;         // add blocks, blocks of ks[0], all removal blocks
   uint32_t parts;               // (pmask + 1) >> kDsPartBits
-  uint32_t chunk;               // adds per K1 / K3 block (kDsPartChunk)
-  uint32_t kchunk;              // removals per K1 / K3 block (fewer items: smaller blocks' worth)
-  uint32_t* hist;               // parts * (ba + bk) + 1 counts: [p * ba + b], then [parts * ba + p * bk + b]
-  const uint32_t* off;          // exclusive scan of hist
-  unsigned long long* items;    // (key, value) pairs, partition-major: adds, then removals
+  uint32_t chunk;               // adds per K1 block (kDsPartChunk)
+  uint32_t kchunk;              // removals per K1 block (fewer items: smaller blocks' worth)
+  uint32_t cap[2];              // run length per partition: adds, removals
+  uint32_t* pcnt;               // [2 parts]: items reserved per partition (adds, then removals)
+  unsigned long long* items;    // (key, value) pairs: parts x cap[0] adds, then parts x cap[1] removals
+  unsigned long long* ovf[2];   // overflow lists (key, value): adds, removals
+  uint32_t ovf_cap[2];
+  uint32_t* ovf_n;              // [4]: [2 par + 0 / 1] overflow counts of adds / removals
+  uint32_t par;                 // this fold's parity
 };
-__host__ __device__ inline uint64_t ds_part_hist_len(const DsPartArgs& a) { return (uint64_t)a.parts * (a.ba + a.bk) + 1; }
 hipError_t launch_ds_part_count(hipStream_t s, const DsPartArgs& a);
 // out[0] += members held (primary + overflow); out zeroed beforehand
 hipError_t launch_ds_count_members(hipStream_t s, DsTables t, uint32_t* out);

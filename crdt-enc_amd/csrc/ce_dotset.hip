@@ -661,8 +661,11 @@ __global__ void k_ds_applied(const uint32_t* keys, const uint32_t* perm,
 
 // flag |= 1 unless every actor's adds form one contiguous run: a run head stamps its actor's
 // mark with this check's generation; a second head of the same actor finds the stamp
+// (pub: pinned words -- [0] the emit's miss count copied from miss_src, [1] the flag, set by a
+// plain store; the host zeroes it before the launch)
 __global__ void k_ds_contig(const uint32_t* actor, uint32_t n, uint32_t* marks, uint32_t n_marks, uint32_t gen,
-                            uint32_t* flag) {
+                            uint32_t* flag, const uint32_t* miss_src, uint32_t* pub) {
+  if (pub && blockIdx.x == 0 && threadIdx.x == 0) pub[0] = *miss_src;  // (the emit is done)
   bool bad = false;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
     const uint32_t a = actor[i];
@@ -670,7 +673,10 @@ __global__ void k_ds_contig(const uint32_t* actor, uint32_t n, uint32_t* marks, 
     if (a >= n_marks) { bad = true; continue; }
     bad |= atomicExch(marks + a, gen) == gen;
   }
-  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+  if (__any(bad) && (threadIdx.x & 63) == 0) {
+    if (pub) pub[1] = 1u;
+    else atomicOr(flag, 1u);
+  }
 }
 
 // clock[a] = max(clock[a], every counter of actor a in the batch), from the actor-sorted adds:
@@ -775,59 +781,107 @@ __device__ __forceinline__ unsigned long long member_handle(const DsTables& t, u
 }
 
 constexpr int kPartBatch = 8;  // items per lane whose loads are issued before any is used
+static_assert(kDsPartChunk == kPartThreads * kPartBatch, "K1 walks its chunk in one trip");
+
+// K1 after its count: lh[p] (this block's items of partition p) -> the base of its reservation in
+// p's run, one returning add per partition with items (64 contiguous counters per wave instruction)
+__device__ __forceinline__ void part_reserve(uint32_t* lh, uint32_t parts, uint32_t* pcnt) {
+  __syncthreads();
+  for (uint32_t p = threadIdx.x; p < parts; p += kPartThreads) {
+    const uint32_t n = lh[p];
+    if (n) lh[p] = atomicAdd(pcnt + p, n);
+  }
+  __syncthreads();
+}
+
+// one item to its place in partition p's run (pos from the block's LDS cursor), or to the overflow
+// list past the run's end
+__device__ __forceinline__ void part_put(const DsPartArgs& a, int side, uint32_t p, uint32_t pos,
+                                         unsigned long long key, unsigned long long v) {
+  unsigned long long* dst;
+  if (pos < a.cap[side]) {
+    dst = a.items + 2ull * (((size_t)side * a.parts * a.cap[0]) + (size_t)p * a.cap[side] + pos);
+  } else {
+    const uint32_t o = atomicAdd(a.ovf_n + 2 * a.par + side, 1u);
+    if (o >= a.ovf_cap[side]) {  // (sized for every item of the batch: not reached)
+      atomicAdd(a.t.live + 2, 1u);
+      return;
+    }
+    dst = a.ovf[side] + 2ull * o;
+  }
+  *reinterpret_cast<ulonglong2*>(dst) = make_ulonglong2(key, v);
+}
 
 __global__ void __launch_bounds__(kPartThreads) k_ds_part_adds(DsPartArgs a) {
-  extern __shared__ uint32_t lh[];  // [parts]
+  extern __shared__ uint32_t lh[];  // [parts]: counts, then the block's cursors in every run
   for (uint32_t p = threadIdx.x; p < a.parts; p += kPartThreads) lh[p] = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     a.t.live[0] = 0;
     a.t.live[1] = 0;
     a.t.live[3] = 0;
     a.t.live[4] = 0;
-    a.hist[ds_part_hist_len(a) - 1] = 0;
   }
   __syncthreads();
-  const uint32_t k0 = blockIdx.x * a.chunk;
-  const uint32_t k1 = min(a.n_add, k0 + a.chunk);
-  for (uint32_t kb = k0 + threadIdx.x; kb < k1; kb += kPartThreads * kPartBatch) {
-    uint32_t j0[kPartBatch], j1[kPartBatch], aid[kPartBatch];
-    unsigned long long m[kPartBatch], g[kPartBatch];
+  const uint32_t k1 = min(a.n_add, blockIdx.x * a.chunk + a.chunk);
+  // an add with one member keeps its pair key and counter in registers; one with several leaves
+  // its members' keys in akey for the write below
+  uint32_t j0[kPartBatch], j1[kPartBatch], aid[kPartBatch];
+  unsigned long long m[kPartBatch], g[kPartBatch], c[kPartBatch], key[kPartBatch];
 #pragma unroll
-    for (int q = 0; q < kPartBatch; q++) {
-      const uint32_t k = kb + q * kPartThreads;
-      j0[q] = j1[q] = 0;
-      m[q] = g[q] = 0;
-      if (k < k1) {
-        j0[q] = a.o.add_mbeg[k];
-        j1[q] = a.o.add_mbeg[k + 1];
-        aid[q] = a.o.add_actor[k];
-        if (!a.applied[k]) {
-          for (uint32_t j = j0[q]; j < j1[q]; j++) a.akey[j] = kDsEmpty;
-          j1[q] = j0[q];
-        } else if (j1[q] == j0[q] + 1) {
-          m[q] = a.o.add_mem[j0[q]];
-          g[q] = a.t.mkey[(uint32_t)mix64(m[q]) & a.t.smask];
-        }
+  for (int q = 0; q < kPartBatch; q++) {
+    const uint32_t k = blockIdx.x * a.chunk + threadIdx.x + q * kPartThreads;
+    j0[q] = j1[q] = 0;
+    m[q] = g[q] = c[q] = 0;
+    if (k < k1 && a.applied[k]) {
+      j0[q] = a.o.add_mbeg[k];
+      j1[q] = a.o.add_mbeg[k + 1];
+      aid[q] = a.o.add_actor[k];
+      c[q] = a.o.add_ctr[k];
+      if (j1[q] == j0[q] + 1) {
+        m[q] = a.o.add_mem[j0[q]];
+        g[q] = a.t.mkey[(uint32_t)mix64(m[q]) & a.t.smask];
       }
     }
+  }
 #pragma unroll
-    for (int q = 0; q < kPartBatch; q++) {
+  for (int q = 0; q < kPartBatch; q++) {
+    key[q] = kDsEmpty;
+    if (j1[q] == j0[q] + 1) {
+      const unsigned long long h = member_handle(a.t, m[q], g[q], true);
+      if (h != kDsEmpty) {
+        key[q] = pair_key(h, aid[q]);
+        atomicAdd(&lh[pair_part(a.t, key[q])], 1u);
+      }
+    } else {
       for (uint32_t j = j0[q]; j < j1[q]; j++) {
-        const unsigned long long mm = j1[q] == j0[q] + 1 ? m[q] : a.o.add_mem[j];
-        const unsigned long long h = member_handle(a.t, mm, j1[q] == j0[q] + 1 ? g[q] : ~mm, true);
-        const unsigned long long key = h == kDsEmpty ? kDsEmpty : pair_key(h, aid[q]);
-        a.akey[j] = key;
-        if (key != kDsEmpty) atomicAdd(&lh[pair_part(a.t, key)], 1u);
+        const unsigned long long h = member_find(a.t, a.o.add_mem[j], true);
+        const unsigned long long kj = h == kDsEmpty ? kDsEmpty : pair_key(h, aid[q]);
+        a.akey[j] = kj;
+        if (kj != kDsEmpty) atomicAdd(&lh[pair_part(a.t, kj)], 1u);
       }
     }
   }
-  __syncthreads();
-  if (blockIdx.x < a.ba)  // (one block with no adds still runs for the clears above)
-    for (uint32_t p = threadIdx.x; p < a.parts; p += kPartThreads) a.hist[(size_t)p * a.ba + blockIdx.x] = lh[p];
+  part_reserve(lh, a.parts, a.pcnt);
+#pragma unroll
+  for (int q = 0; q < kPartBatch; q++) {
+    if (j1[q] == j0[q] + 1) {
+      if (key[q] == kDsEmpty) continue;
+      const uint32_t p = pair_part(a.t, key[q]);
+      part_put(a, 0, p, atomicAdd(&lh[p], 1u), key[q], c[q]);
+    } else {
+      for (uint32_t j = j0[q]; j < j1[q]; j++) {
+        const unsigned long long kj = a.akey[j];
+        if (kj == kDsEmpty) continue;
+        const uint32_t p = pair_part(a.t, kj);
+        part_put(a, 0, p, atomicAdd(&lh[p], 1u), kj, c[q]);
+      }
+    }
+  }
 }
 
 // removal r kills (m, a_e) for every member m and clock entry e (k_ds_kill); a member absent after
-// the adds has no pair to kill
+// the adds has no pair to kill.  A removal with one member and one clock entry (one item) keeps it
+// in registers; others leave their member handles in hk for the write below.
 __global__ void __launch_bounds__(kPartThreads) k_ds_part_kills(DsPartArgs a) {
   extern __shared__ uint32_t lh[];
   for (uint32_t p = threadIdx.x; p < a.parts; p += kPartThreads) lh[p] = 0;
@@ -836,97 +890,64 @@ __global__ void __launch_bounds__(kPartThreads) k_ds_part_kills(DsPartArgs a) {
   const DsKillSrc& x = a.ks[b < a.bk0 ? 0 : 1];
   const uint32_t r0 = (b < a.bk0 ? b : b - a.bk0) * a.kchunk;
   const uint32_t r1 = min(x.n, r0 + a.kchunk);
-  for (uint32_t rb = r0 + threadIdx.x; rb < r1; rb += kPartThreads * kPartBatch) {
-    uint32_t c0[kPartBatch], c1[kPartBatch], j0[kPartBatch], j1[kPartBatch];
-    unsigned long long m[kPartBatch], g[kPartBatch];
+  uint32_t c0[kPartBatch], c1[kPartBatch], j0[kPartBatch], j1[kPartBatch];
+  unsigned long long m[kPartBatch], g[kPartBatch], key[kPartBatch], v[kPartBatch];
+  uint32_t ca[kPartBatch];
 #pragma unroll
-    for (int q = 0; q < kPartBatch; q++) {
-      const uint32_t r = rb + q * kPartThreads;
-      c0[q] = c1[q] = j0[q] = j1[q] = 0;
-      m[q] = g[q] = 0;
-      if (r < r1) {
-        c0[q] = x.cbeg[r];
-        c1[q] = x.cbeg[r + 1];
-        j0[q] = x.mbeg[r];
-        j1[q] = x.mbeg[r + 1];
-        if (c0[q] == c1[q]) {  // an empty clock kills nothing
-          for (uint32_t j = j0[q]; j < j1[q]; j++) x.hk[j] = kDsEmpty;
-          j1[q] = j0[q];
-        } else if (j1[q] == j0[q] + 1) {
-          m[q] = x.mem[j0[q]];
-          g[q] = a.t.mkey[(uint32_t)mix64(m[q]) & a.t.smask];
-        }
+  for (int q = 0; q < kPartBatch; q++) {
+    const uint32_t r = r0 + threadIdx.x + q * kPartThreads;
+    c0[q] = c1[q] = j0[q] = j1[q] = 0;
+    m[q] = g[q] = v[q] = 0;
+    ca[q] = 0;
+    if (r < r1) {
+      c0[q] = x.cbeg[r];
+      c1[q] = x.cbeg[r + 1];
+      j0[q] = x.mbeg[r];
+      j1[q] = x.mbeg[r + 1];
+      if (c0[q] == c1[q]) {  // an empty clock kills nothing
+        j1[q] = j0[q];
+      } else if (j1[q] == j0[q] + 1 && c1[q] == c0[q] + 1) {
+        m[q] = x.mem[j0[q]];
+        g[q] = a.t.mkey[(uint32_t)mix64(m[q]) & a.t.smask];
+        ca[q] = x.c_actor[c0[q]];
+        v[q] = x.c_ctr[c0[q]];
       }
     }
+  }
 #pragma unroll
-    for (int q = 0; q < kPartBatch; q++) {
+  for (int q = 0; q < kPartBatch; q++) {
+    key[q] = kDsEmpty;
+    if (j1[q] == j0[q] + 1 && c1[q] == c0[q] + 1) {
+      const unsigned long long h = member_handle(a.t, m[q], g[q], false);
+      if (h != kDsEmpty) {
+        key[q] = pair_key(h, ca[q]);
+        atomicAdd(&lh[pair_part(a.t, key[q])], 1u);
+      }
+    } else {
       for (uint32_t j = j0[q]; j < j1[q]; j++) {
-        const bool one = j1[q] == j0[q] + 1;
-        const unsigned long long mm = one ? m[q] : x.mem[j];
-        const unsigned long long h = member_handle(a.t, mm, one ? g[q] : ~mm, false);
+        const unsigned long long h = member_find(a.t, x.mem[j], false);
         x.hk[j] = h;
         if (h == kDsEmpty) continue;
         for (uint32_t e = c0[q]; e < c1[q]; e++) atomicAdd(&lh[pair_part(a.t, pair_key(h, x.c_actor[e]))], 1u);
       }
     }
   }
-  __syncthreads();
-  const size_t col = (size_t)a.parts * a.ba;
-  for (uint32_t p = threadIdx.x; p < a.parts; p += kPartThreads) a.hist[col + (size_t)p * a.bk + b] = lh[p];
-}
-
-// K3: the same items as K1, block by block, each to its (partition, block) run
-__global__ void __launch_bounds__(kPartThreads) k_ds_part_scatter(DsPartArgs a) {
-  extern __shared__ uint32_t lc[];  // [parts] cursors
-  const uint32_t b = blockIdx.x;
-  const bool adds = b < a.ba;
-  const uint32_t kb = adds ? 0 : b - a.ba;
-  for (uint32_t p = threadIdx.x; p < a.parts; p += kPartThreads)
-    lc[p] = adds ? a.off[(size_t)p * a.ba + b] : a.off[(size_t)a.parts * a.ba + (size_t)p * a.bk + kb];
-  __syncthreads();
-  if (adds) {
-    const uint32_t k0 = b * a.chunk;
-    const uint32_t k1 = min(a.n_add, k0 + a.chunk);
-    for (uint32_t kq = k0 + threadIdx.x; kq < k1; kq += kPartThreads * kPartBatch) {
-      uint32_t j0[kPartBatch], j1[kPartBatch];
-      unsigned long long c[kPartBatch], key1[kPartBatch];
+  part_reserve(lh, a.parts, a.pcnt + a.parts);
 #pragma unroll
-      for (int q = 0; q < kPartBatch; q++) {
-        const uint32_t k = kq + q * kPartThreads;
-        j0[q] = j1[q] = 0;
-        c[q] = key1[q] = 0;
-        if (k < k1) {
-          j0[q] = a.o.add_mbeg[k];
-          j1[q] = a.o.add_mbeg[k + 1];
-          c[q] = a.o.add_ctr[k];
-          if (j1[q] == j0[q] + 1) key1[q] = a.akey[j0[q]];
+  for (int q = 0; q < kPartBatch; q++) {
+    if (j1[q] == j0[q] + 1 && c1[q] == c0[q] + 1) {
+      if (key[q] == kDsEmpty) continue;
+      const uint32_t p = pair_part(a.t, key[q]);
+      part_put(a, 1, p, atomicAdd(&lh[p], 1u), key[q], v[q]);
+    } else {
+      for (uint32_t j = j0[q]; j < j1[q]; j++) {
+        const unsigned long long h = x.hk[j];
+        if (h == kDsEmpty) continue;
+        for (uint32_t e = c0[q]; e < c1[q]; e++) {
+          const unsigned long long kj = pair_key(h, x.c_actor[e]);
+          const uint32_t p = pair_part(a.t, kj);
+          part_put(a, 1, p, atomicAdd(&lh[p], 1u), kj, x.c_ctr[e]);
         }
-      }
-#pragma unroll
-      for (int q = 0; q < kPartBatch; q++) {
-        for (uint32_t j = j0[q]; j < j1[q]; j++) {
-          const unsigned long long key = j1[q] == j0[q] + 1 ? key1[q] : a.akey[j];
-          if (key == kDsEmpty) continue;
-          const uint32_t pos = atomicAdd(&lc[pair_part(a.t, key)], 1u);
-          *reinterpret_cast<ulonglong2*>(a.items + 2ull * pos) = make_ulonglong2(key, c[q]);
-        }
-      }
-    }
-    return;
-  }
-  const DsKillSrc& x = a.ks[kb < a.bk0 ? 0 : 1];
-  const uint32_t r0 = (kb < a.bk0 ? kb : kb - a.bk0) * a.kchunk;
-  const uint32_t r1 = min(x.n, r0 + a.kchunk);
-  for (uint32_t r = r0 + threadIdx.x; r < r1; r += kPartThreads) {
-    const uint32_t c0 = x.cbeg[r], c1 = x.cbeg[r + 1];
-    if (c0 == c1) continue;
-    for (uint32_t j = x.mbeg[r]; j < x.mbeg[r + 1]; j++) {
-      const unsigned long long h = x.hk[j];
-      if (h == kDsEmpty) continue;
-      for (uint32_t e = c0; e < c1; e++) {
-        const unsigned long long key = pair_key(h, x.c_actor[e]);
-        const uint32_t pos = atomicAdd(&lc[pair_part(a.t, key)], 1u);
-        *reinterpret_cast<ulonglong2*>(a.items + 2ull * pos) = make_ulonglong2(key, x.c_ctr[e]);
       }
     }
   }
@@ -972,6 +993,14 @@ __global__ void __launch_bounds__(kApplyThreads) k_ds_part_apply(DsPartArgs a) {
   __shared__ int part[3][kApplyThreads / 64];
   int dl = 0, du = 0, dm = 0;
   const uint32_t tid = threadIdx.x;
+  // this fold's overflow counts (usually 0); the next fold's zeroed; live[5] = the items that
+  // overflowed, for the host's run sizing
+  const uint32_t no_a = min(a.ovf_n[2 * a.par], a.ovf_cap[0]), no_k = min(a.ovf_n[2 * a.par + 1], a.ovf_cap[1]);
+  if (blockIdx.x == 0 && tid == 0) {
+    a.ovf_n[2 * (a.par ^ 1)] = 0;
+    a.ovf_n[2 * (a.par ^ 1) + 1] = 0;
+    a.t.live[5] = no_a + no_k;
+  }
   // a grid of a few workgroups per CU walks the partitions
   for (uint32_t p = blockIdx.x; p < a.parts; p += gridDim.x) {
     const size_t base = (size_t)p << kDsPartBits;
@@ -986,14 +1015,15 @@ __global__ void __launch_bounds__(kApplyThreads) k_ds_part_apply(DsPartArgs a) {
       kill[i] = 0;
     }
     __syncthreads();
-    // adds: insert, max-merge the counter
-    const uint32_t ia0 = a.off[(size_t)p * a.ba], ia1 = a.off[(size_t)(p + 1) * a.ba];
-    for (uint32_t i0 = ia0; i0 < ia1; i0 += kApplyThreads * kApplyItemBatch) {
+    // adds: insert, max-merge the counter (the partition's run, then its overflowed items)
+    const uint32_t na_p = min(a.pcnt[p], a.cap[0]), nk_p = min(a.pcnt[a.parts + p], a.cap[1]);
+    const unsigned long long* ra = a.items + 2ull * ((size_t)p * a.cap[0]);
+    for (uint32_t i0 = 0; i0 < na_p; i0 += kApplyThreads * kApplyItemBatch) {
       ulonglong2 it[kApplyItemBatch];
 #pragma unroll
       for (int b = 0; b < kApplyItemBatch; b++) {
         const uint32_t i = i0 + tid + b * kApplyThreads;
-        it[b] = i < ia1 ? *reinterpret_cast<const ulonglong2*>(a.items + 2ull * i) : make_ulonglong2(kDsEmpty, 0);
+        it[b] = i < na_p ? *reinterpret_cast<const ulonglong2*>(ra + 2ull * i) : make_ulonglong2(kDsEmpty, 0);
       }
 #pragma unroll
       for (int b = 0; b < kApplyItemBatch; b++) {
@@ -1003,16 +1033,22 @@ __global__ void __launch_bounds__(kApplyThreads) k_ds_part_apply(DsPartArgs a) {
         else atomicAdd(a.t.live + 2, 1u);  // partition full (tables sized to <= 50% load)
       }
     }
+    for (uint32_t i = tid; i < no_a; i += kApplyThreads) {
+      const ulonglong2 it = *reinterpret_cast<const ulonglong2*>(a.ovf[0] + 2ull * i);
+      if (pair_part(a.t, it.x) != p) continue;
+      const uint32_t h = lds_insert(key, it.x);
+      if (h != ~0u) atomicMax(&add[h], it.y);
+      else atomicAdd(a.t.live + 2, 1u);
+    }
     __syncthreads();
     // removals: thresholds of existing pairs
-    const size_t kcol = (size_t)a.parts * a.ba;
-    const uint32_t ik0 = a.off[kcol + (size_t)p * a.bk], ik1 = a.off[kcol + (size_t)(p + 1) * a.bk];
-    for (uint32_t i0 = ik0; i0 < ik1; i0 += kApplyThreads * kApplyItemBatch) {
+    const unsigned long long* rk = a.items + 2ull * ((size_t)a.parts * a.cap[0] + (size_t)p * a.cap[1]);
+    for (uint32_t i0 = 0; i0 < nk_p; i0 += kApplyThreads * kApplyItemBatch) {
       ulonglong2 it[kApplyItemBatch];
 #pragma unroll
       for (int b = 0; b < kApplyItemBatch; b++) {
         const uint32_t i = i0 + tid + b * kApplyThreads;
-        it[b] = i < ik1 ? *reinterpret_cast<const ulonglong2*>(a.items + 2ull * i) : make_ulonglong2(kDsEmpty, 0);
+        it[b] = i < nk_p ? *reinterpret_cast<const ulonglong2*>(rk + 2ull * i) : make_ulonglong2(kDsEmpty, 0);
       }
 #pragma unroll
       for (int b = 0; b < kApplyItemBatch; b++) {
@@ -1021,8 +1057,18 @@ __global__ void __launch_bounds__(kApplyThreads) k_ds_part_apply(DsPartArgs a) {
         if (h != ~0u) atomicMax(&kill[h], it[b].y);
       }
     }
+    for (uint32_t i = tid; i < no_k; i += kApplyThreads) {
+      const ulonglong2 it = *reinterpret_cast<const ulonglong2*>(a.ovf[1] + 2ull * i);
+      if (pair_part(a.t, it.x) != p) continue;
+      const uint32_t h = lds_lookup(key, it.x);
+      if (h != ~0u) atomicMax(&kill[h], it.y);
+    }
     dm += (int)primary_used(a.t, p, a.parts);
     __syncthreads();
+    if (tid == 0) {  // every lane has read the counts (barriers above): the next fold's are zero
+      a.pcnt[p] = 0;
+      a.pcnt[a.parts + p] = 0;
+    }
     // finalize the touched slots: the current values they need, all loads first
     unsigned long long ad[kApplySlotsPerLane], kl[kApplySlotsPerLane], c[kApplySlotsPerLane];
     bool fresh[kApplySlotsPerLane];
@@ -1704,9 +1750,10 @@ hipError_t launch_ds_applied(hipStream_t s, const uint32_t* keys_sorted, const u
 }
 
 hipError_t launch_ds_contig(hipStream_t s, const uint32_t* actor, uint32_t n, uint32_t* marks, uint32_t n_marks,
-                            uint32_t gen, uint32_t* flag) {
+                            uint32_t gen, uint32_t* flag, const uint32_t* miss_src, uint32_t* pub) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ds_contig, dim3(blocks_for(n)), dim3(kBlock), 0, s, actor, n, marks, n_marks, gen, flag);
+  hipLaunchKernelGGL(k_ds_contig, dim3(blocks_for(n)), dim3(kBlock), 0, s, actor, n, marks, n_marks, gen, flag,
+                     miss_src, pub);
   return hipGetLastError();
 }
 
@@ -1761,7 +1808,6 @@ hipError_t launch_ds_part_count(hipStream_t s, const DsPartArgs& a) {
 }
 
 hipError_t launch_ds_part_apply(hipStream_t s, const DsPartArgs& a) {
-  if (a.ba + a.bk) hipLaunchKernelGGL(k_ds_part_scatter, dim3(a.ba + a.bk), dim3(kPartThreads), (size_t)a.parts * 4, s, a);
   static const uint32_t grid = getenv("CE_DS_APPLY_GRID") ? (uint32_t)atoi(getenv("CE_DS_APPLY_GRID")) : 768u;
   hipLaunchKernelGGL(k_ds_part_apply, dim3(grid && grid < a.parts ? grid : a.parts), dim3(kApplyThreads), 0, s, a);
   return hipGetLastError();

@@ -64,7 +64,11 @@ struct DsState {
   DevBuf cnt, ops[10], applied, sort_keys, sort_perm, sort_keys2, sort_perm2, ctr_sorted, excl,
       cub_tmp, deferred_flags, d0[5], col[6], mv[6], other[4], oclock;
   DevBuf misses;
-  DevBuf part_akey, part_hk[2], part_hist, part_items;  // the partitioned fold (DsPartArgs)
+  DevBuf part_akey, part_hk[2], part_items, part_ovf[2];  // the partitioned fold (DsPartArgs)
+  DevBuf part_cnt;              // pcnt[2 parts] + ovf_n[4]: zero between folds (each apply zeroes them)
+  uint32_t part_cnt_parts = 0;  // partitions part_cnt was zeroed for (0: zero it again)
+  uint32_t part_gen = 0;        // partitioned folds so far (the parity of ovf_n)
+  uint32_t part_factor = 3;     // run length = the expected share x part_factor / 2 (+64)
   HostBuf h_cnt;
   // run-contiguity marks of the adds' actors (k_ds_contig: a generation per check, no clearing)
   DevBuf contig_marks;
@@ -75,7 +79,9 @@ struct DsState {
   // Orswot op files decoded in the open (k_open_fold_v2's DS form): raw counts, done flags and
   // the file-major rows (add actor / counter / member, removal actor / counter / member)
   DevBuf fz_cnt, fz_done, fz_col[6], fz_why;
-  DevBuf ser_cnt, ser_off;  // the serializer's counting sort (per-member counts, their scan)
+  DevBuf ser_sort;               // the serializer's radix-sort state (ce_ser_sort.hip), zeroed once
+  size_t ser_sort_words = 0;
+  uint32_t ser_sort_gen = 0;     // sorts so far (the state's histogram parity)
   // the multi-GPU column exchange (ds_export_columns_device / ds_merge_columns_device)
   HostBuf cx_host, cx_heads, cx_map;
   DevBuf cx_mapd, cx_ids, cx_slot;
@@ -86,7 +92,7 @@ struct DsState {
   // bases, members, sorted members [0..6]
   // and emitted (member, actor id, value) columns [7..9]), pinned staging for its downloads
   std::vector<std::array<DevBuf, 10>> rd;
-  DevBuf rd_tmp, rd_misc, ser[16], uuid_of_id, rank_of_id, id_of_rank, rd_oclocks, cnt_tot, rd_args_d, rd_chunks;
+  DevBuf rd_tmp, rd_misc, ser[17], uuid_of_id, rank_of_id, id_of_rank, rd_oclocks, cnt_tot, rd_args_d, rd_chunks;
   HostBuf rd_host, rd_small, rd_clock, rd_args_h, h_clock;
   uint64_t uuid_ids = ~0ull;  // id count uuid_of_id / rank_of_id (and id_rank / rank_id) were built for
   std::vector<uint32_t> id_rank, rank_id;  // UUID-order rank of each stable id, and its inverse
@@ -644,25 +650,35 @@ int orswot_fold(ce_core* c, const Counts& k, uint64_t kill_bound, bool adds_cont
   uint32_t* live = d->live.as<uint32_t>();
   DsPartArgs pa{};
   pa.parts = d->pcap >> kDsPartBits;
-  static const uint32_t chunk = getenv("CE_DS_PART_CHUNK") ? (uint32_t)std::max(1024, atoi(getenv("CE_DS_PART_CHUNK")))
-                                                          : kDsPartChunk;
-  pa.chunk = chunk;
-  pa.kchunk = std::max<uint32_t>(1024, chunk / 4);  // removals are ~1/4 of C3's ops: as many blocks
-  pa.ba = (uint32_t)((na + chunk - 1) / chunk);
+  pa.chunk = kDsPartChunk;
+  pa.kchunk = kDsPartChunk / 4;  // removals are ~1/4 of C3's ops: as many blocks
+  pa.ba = (uint32_t)((na + pa.chunk - 1) / pa.chunk);
   pa.bk0 = (uint32_t)((nr + pa.kchunk - 1) / pa.kchunk);
   pa.bk = pa.bk0 + (uint32_t)((n0 + pa.kchunk - 1) / pa.kchunk);
   const uint64_t kill_items = kill_bound == ~0ull ? ~0ull : kill_bound + kb0;
+  // runs: the expected share of a partition x part_factor / 2, + 64 (C3: ~12 sigma of slack);
+  // what passes it goes to the overflow lists (sized for the whole batch)
+  const uint64_t cap_a = pa.parts ? k.v[kCntAddM] / pa.parts * d->part_factor / 2 + 64 : 0,
+                 cap_k = pa.parts && kill_items != ~0ull ? kill_items / pa.parts * d->part_factor / 2 + 64 : 0;
   const bool part = !getenv("CE_DS_FOLD_GLOBAL") && pa.parts >= 1 && pa.parts <= kDsPartMaxParts &&
                     kill_items <= 4 * (k.v[kCntRmM] + k.v[kCntRmC] + kb0) + (1ull << 20) &&
-                    ds_part_hist_len(pa) < (1ull << 31) && k.v[kCntAddM] + kill_items < (1ull << 31);
+                    k.v[kCntAddM] + kill_items < (1ull << 31) && (uint64_t)pa.parts * (cap_a + cap_k) < (1ull << 31);
   if (part) {
-    const uint64_t hl = ds_part_hist_len(pa);
-    size_t tb = 0;
+    pa.cap[0] = (uint32_t)cap_a;
+    pa.cap[1] = (uint32_t)cap_k;
+    pa.ovf_cap[0] = (uint32_t)k.v[kCntAddM];
+    pa.ovf_cap[1] = (uint32_t)kill_items;
     if ((e = d->part_akey.reserve(8 * k.v[kCntAddM] + 64)) || (e = d->part_hk[0].reserve(8 * k.v[kCntRmM] + 64)) ||
-        (e = d->part_hk[1].reserve(8 * m0 + 64)) || (e = d->part_hist.reserve(8 * hl + 64)) ||
-        (e = d->part_items.reserve(16 * (k.v[kCntAddM] + kill_items) + 64)) ||
-        (e = ds_excl_sum_u32(nullptr, tb, nullptr, nullptr, (uint32_t)hl, s)) || (e = d->cub_tmp.reserve(tb + 256)))
+        (e = d->part_hk[1].reserve(8 * m0 + 64)) ||
+        (e = d->part_items.reserve(16ull * pa.parts * (cap_a + cap_k) + 64)) ||
+        (e = d->part_ovf[0].reserve(16 * k.v[kCntAddM] + 64)) || (e = d->part_ovf[1].reserve(16 * kill_items + 64)))
       return ctx->hip_fail(e, "fold");
+    if (d->part_cnt_parts < pa.parts) {  // new (or larger) counters: zeroed once, then by the applies
+      if ((e = d->part_cnt.reserve(8ull * pa.parts + 64)) ||
+          (e = hipMemsetAsync(d->part_cnt.p, 0, 8ull * pa.parts + 64, s)))
+        return ctx->hip_fail(e, "fold");
+      d->part_cnt_parts = pa.parts;
+    }
     pa.t = tables(d);
     pa.o = o;
     pa.applied = d->applied.as<uint8_t>();
@@ -672,14 +688,14 @@ int orswot_fold(ce_core* c, const Counts& k, uint64_t kill_bound, bool adds_cont
     pa.ks[1] = {d->d0[0].as<uint32_t>(), d->d0[1].as<uint32_t>(), d->d0[2].as<uint32_t>(),
                 d->d0[3].as<unsigned long long>(), d->d0[4].as<unsigned long long>(),
                 d->part_hk[1].as<unsigned long long>(), n0};
-    pa.hist = d->part_hist.as<uint32_t>();
-    pa.off = pa.hist + hl;
+    pa.pcnt = d->part_cnt.as<uint32_t>();
+    pa.ovf_n = pa.pcnt + 2ull * d->part_cnt_parts;
     pa.items = d->part_items.as<unsigned long long>();
-    tb = d->cub_tmp.cap;
+    pa.ovf[0] = d->part_ovf[0].as<unsigned long long>();
+    pa.ovf[1] = d->part_ovf[1].as<unsigned long long>();
+    pa.par = d->part_gen++ & 1u;
     const int tp = ctx->tbegin("ds_part_fold");
-    if ((e = launch_ds_part_count(s, pa)) ||
-        (e = ds_excl_sum_u32(d->cub_tmp.p, tb, pa.hist, pa.hist + hl, (uint32_t)hl, s)) ||
-        (e = launch_ds_part_apply(s, pa)) ||
+    if ((e = launch_ds_part_count(s, pa)) || (e = launch_ds_part_apply(s, pa)) ||
         (e = launch_ds_clock(s, clock_keys, clock_ctr, d->excl.as<unsigned long long>(),
                              d->clock.as<unsigned long long>(), na)))
       return ctx->hip_fail(e, "fold");
@@ -712,14 +728,14 @@ int orswot_fold(ce_core* c, const Counts& k, uint64_t kill_bound, bool adds_cont
     ctx->tend(t);
     c->path_counts["ds_fold_global"]++;
   }
-  // the last deferred-flags launch publishes live[0..5) into the pinned h_cnt[56..61) (ds_settle)
+  // the last deferred-flags launch publishes live[0..6) into the pinned h_cnt[56..62) (ds_settle)
   uint8_t* fl = d->deferred_flags.as<uint8_t>();
   uint32_t* pub = static_cast<uint32_t*>(host_dev_ptr(d->h_cnt.as<uint32_t>() + 56));
   if ((e = launch_ds_deferred(s, o.rm_cbeg, o.rmc_actor, o.rmc_ctr, d->clock.as<unsigned long long>(), fl, nr, live + 3,
-                              live, n0 ? nullptr : pub, 5)) ||
+                              live, n0 ? nullptr : pub, 6)) ||
       (n0 && (e = launch_ds_deferred(s, d->d0[0].as<uint32_t>(), d->d0[2].as<uint32_t>(),
                                      d->d0[3].as<unsigned long long>(), d->clock.as<unsigned long long>(), fl + nr,
-                                     n0, live + 3, live, pub, 5))))
+                                     n0, live + 3, live, pub, 6))))
     return ctx->hip_fail(e, "finalize");
   d->settle_pending = true;
   d->settle_fold = true;
@@ -755,6 +771,11 @@ int ds_settle(ce_core* c) {
   if (d->settle_delta) {
     d->live_pairs += (int64_t)(int32_t)hl[0];
     d->used_pairs += hl[1];
+    // items past their partition's run (folded from the overflow lists): longer runs next time
+    if (d->settle_fold && hl[5]) {
+      d->part_factor = std::min<uint32_t>(64, std::max<uint32_t>(1, d->part_factor) * 2);
+      c->path_counts["ds_fold_run_overflow"]++;
+    }
   } else {
     d->live_pairs = hl[0];
     d->used_pairs = hl[1];
@@ -1057,6 +1078,8 @@ int ds_init(ce_core* c) {
     c->ds->mcap_s = pow2_at_least(std::max(32, atoi(ps)));
     c->ds->primary_fixed = true;
   }
+  if (const char* pf = getenv("CE_DS_PART_FACTOR"))  // tests: short partition runs (overflow lists)
+    c->ds->part_factor = (uint32_t)std::max(0, atoi(pf));
   c->ds->kind = c->kind;
   hipError_t e;
   if ((e = c->ds->misses.reserve(64 + kMissCap * 16ull)) || (e = c->ds->h_cnt.reserve(512)))
@@ -1319,13 +1342,20 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
         if ((e = hipMemsetAsync(d->contig_marks.p, 0, 4ull * d->contig_cap, ctx->stream))) return ctx->hip_fail(e, "contig");
         d->contig_gen = 1;
       }
+      // the miss count and the flag come back in pinned h_cnt[62..64), written by the contig launch
+      uint32_t* hp = d->h_cnt.as<uint32_t>() + 62;
+      hp[0] = hp[1] = 0;
       if ((e = launch_ds_contig(ctx->stream, a.ops.add_actor, n_add, d->contig_marks.as<uint32_t>(), d->contig_cap,
-                                d->contig_gen, a.counters + 3)))
+                                d->contig_gen, a.counters + 3, d->misses.as<uint32_t>() + 2,
+                                static_cast<uint32_t*>(host_dev_ptr(hp)))))
         return ctx->hip_fail(e, "contig");
-    }
-    if ((e = hipMemcpyAsync(hm, d->misses.p, 16, hipMemcpyDeviceToHost, ctx->stream)) ||
-        (e = stream_wait(ctx->stream)))
+      if ((e = stream_wait(ctx->stream))) return ctx->hip_fail(e, "emit");
+      hm[2] = hp[0];
+      hm[3] = hp[1];
+    } else if ((e = hipMemcpyAsync(hm, d->misses.p, 16, hipMemcpyDeviceToHost, ctx->stream)) ||
+               (e = stream_wait(ctx->stream))) {
       return ctx->hip_fail(e, "emit");
+    }
     d->adds_contig = check && hm[3] == 0 && !getenv("CE_DS_SORT_ADDS");
     if (hm[2] == 0) break;
     if (round > 64) return ctx->fail(CE_ERR_DEVICE, "actor table did not converge");
@@ -1726,7 +1756,8 @@ OrswotReadArgs read_args(ce_core* c, DsState* d, size_t f, const DevState& ds, c
   a.lo = ds.body;
   a.hi = ds.len;
   auto& b = d->rd[f];
-  a.n_cand_dev = d->rd_misc.as<uint32_t>() + 2 * f;
+  // (the count straight into the pinned small words the host reads after stage 0)
+  a.n_cand_dev = static_cast<uint32_t*>(host_dev_ptr(d->rd_small.as<uint32_t>())) + 2 * f;
   a.flags = d->rd_misc.as<uint32_t>() + 2 * f + 1;
   a.cap = cap;
   a.n_cand = ds.n_entries;
@@ -1891,8 +1922,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
                                        d->rd_tmp.cap))))
       return ctx->hip_fail(e, "state reader");
     h2 = std::make_unique<HostPhase>("   rd.d sync");
-    if (!dev.empty() && ((e = hipMemcpyAsync(small, d->rd_misc.p, 8ull * n, hipMemcpyDeviceToHost, s)) ||
-                         (rc = sync("state reader")))) return rc ? rc : ctx->hip_fail(e, "state reader");
+    if (!dev.empty() && (rc = sync("state reader"))) return rc;  // (k_rdm_found wrote the counts into small)
     h2.reset();
     // 3) the first N heads in position order are the entries: parse, chain, repeats, scan
     ph = std::make_unique<HostPhase>("  rd: entries");
@@ -1909,17 +1939,15 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
       }
       OrswotReadArgs a = hA[k];
       a.n_cand = x.n_entries;
-      a.tail_out = d->rd_misc.as<uint32_t>() + 2 * n + 4 * i;
+      a.tail_out = static_cast<uint32_t*>(host_dev_ptr(small)) + 2 * n + 4 * i;  // pinned: no download
       hA2[dev2.size()] = a;
       dev2.push_back(i);
     }
     if (!dev2.empty() &&
         (e = launch_orswot_read_multi(s, nullptr, hA2, (uint32_t)dev2.size(), 1, nullptr, nullptr, nullptr, 0)))
       return ctx->hip_fail(e, "state reader");
-    // every file's tail words in one download
-    if (!dev2.empty() && ((e = hipMemcpyAsync(small + 2 * n, d->rd_misc.as<uint32_t>() + 2 * n, 16ull * n,
-                                              hipMemcpyDeviceToHost, s)) ||
-                          (rc = sync("state reader")))) return rc ? rc : ctx->hip_fail(e, "state reader");
+    // every file's tail words (k_rdm_tile_scan wrote them into small)
+    if (!dev2.empty() && (rc = sync("state reader"))) return rc;
     // 4) the deferred maps after the entries, on the host
     ph = std::make_unique<HostPhase>("  rd: tails");
     std::vector<uint64_t> toff(n + 1, 0), eend(n, 0);
@@ -2259,19 +2287,21 @@ static int ds_serialize_dev(ce_core* c, ce_ctx* x, const uint8_t* outer, const u
   // the sorts and scans over the collected pairs first (they need nothing from the host): the
   // head and tail bytes below are built while they run
   cph = std::make_unique<HostPhase>("  cd: sort enqueue");
-  for (int k = 0; k < 15; k++) {
+  for (int k = 0; k < 17; k++) {
     // 0-3 u32 sort keys / perms, 4-6 u64 keys / sorted members / values, 7-10 actors, heads,
-    // ranks, lengths, 11 entry CSR (n + 1), 12 byte offsets, 13 u64 values (counting sort)
-    const size_t sz = (k >= 4 && k <= 6) || k == 13 ? 8ull * nl + 64 : k <= 12 ? 4ull * nl + 68 : 64;
+    // ranks, lengths, 11 entry CSR (n + 1), 12 byte offsets, 13-14 u64 values and 16 u64 keys
+    // (the radix sort's ping-pong), 15 the scans' scratch (below)
+    if (k == 15) continue;
+    const size_t sz = (k >= 4 && k <= 6) || k >= 13 ? 8ull * nl + 64 : 4ull * nl + 68;
     if ((e = d->ser[k].reserve(sz))) return x->hip_fail(e, "ds compact reserve");
   }
-  if ((e = d->ser[15].reserve(std::max<size_t>(orswot_ser_tmp_bytes(std::max<uint32_t>(nl, 1)),
-                                               4ull * (((1u << kSerCountBits) + 2) / 2048 + 2) + 256))))
-    return x->hip_fail(e, "ds compact reserve");
-  if (!d->ser_cnt.p) {  // the counting sort's per-member counts: zero once, kept zero by the scatter
-    if ((e = d->ser_cnt.reserve(4ull * ((1u << kSerCountBits) + 2))) || (e = d->ser_off.reserve(4ull * ((1u << kSerCountBits) + 2))) ||
-        (e = hipMemsetAsync(d->ser_cnt.p, 0, 4ull * ((1u << kSerCountBits) + 2), s)))
+  if ((e = d->ser[15].reserve(orswot_ser_tmp_bytes(std::max<uint32_t>(nl, 1))))) return x->hip_fail(e, "ds compact reserve");
+  if (ser_sort_state_words(nl) > d->ser_sort_words) {  // (zero once; the sorts keep it so)
+    const size_t w = ser_sort_state_words(std::max<uint32_t>(nl, 1u << 20));
+    if ((e = d->ser_sort.reserve(4 * w + 64)) || (e = hipMemsetAsync(d->ser_sort.p, 0, 4 * w + 64, s)))
       return x->hip_fail(e, "ds compact reserve");
+    d->ser_sort_words = w;
+    d->ser_sort_gen = 0;
   }
   OrswotSerScratch sc{};
   sc.member_in = d->col[0].as<unsigned long long>();
@@ -2296,9 +2326,11 @@ static int ds_serialize_dev(ce_core* c, ce_ctx* x, const uint8_t* outer, const u
   sc.pos = d->ser[12].as<uint32_t>();
   sc.tmp = d->ser[15].p;
   sc.tmp_bytes = d->ser[15].cap;
-  sc.bucket_count = d->ser_cnt.as<uint32_t>();
-  sc.bucket_off = d->ser_off.as<uint32_t>();
-  sc.t_value = d->ser[13].as<unsigned long long>();
+  sc.sort_state = d->ser_sort.as<uint32_t>();
+  sc.sort_gen = &d->ser_sort_gen;
+  sc.v64a = d->ser[13].as<unsigned long long>();
+  sc.v64b = d->ser[14].as<unsigned long long>();
+  sc.k64b = d->ser[16].as<unsigned long long>();
   const int t = x->tbegin("ds_serialize");
   if ((e = launch_orswot_ser_sort(s, sc, nl))) return x->hip_fail(e, "ds serialize");
   const unsigned long long* ck = d->h_clock.as<unsigned long long>();

@@ -47,13 +47,41 @@ struct OrswotSerScratch {
   uint32_t* seg;                         // n + 1
   void* tmp;
   size_t tmp_bytes;
-  // counting sort (members below 2^kSerCountBits): per-member counts, zero between calls (the
-  // scatter counts them back down), their exclusive scan, and a u64 value scratch (n)
-  uint32_t* bucket_count;                // [2^kSerCountBits + 1]
-  uint32_t* bucket_off;                  // [2^kSerCountBits + 2]
-  unsigned long long* t_value;
+  // the radix sort (launch_ser_sort): its state words and parity, and the ping-pong key / value
+  // buffers of its passes (n each; k64b / v64a / v64b u64)
+  uint32_t* sort_state;
+  uint32_t* sort_gen;                    // sorts so far (host): the state's histogram parity
+  unsigned long long *k64b, *v64a, *v64b;
 };
-static constexpr int kSerCountBits = 20;
+
+// the serializer's LSD radix sort (ce_ser_sort.hip): pairs (member_in, actor_in, value_in) in
+// collect order -> member_out / actor_out / value_out ordered by key = member << rank_bits | rank
+// (key_bits <= 64).  State (u32 words, zero before the first sort; the sorts keep it so):
+// hist [2][kSortMaxPlaces][256] | ticket [kSortMaxPlaces] | look [places][tiles][256]
+static constexpr uint32_t kSortMaxPlaces = 8;
+struct SerSortArgs {
+  const unsigned long long* member_in;
+  const uint32_t* actor_in;
+  const unsigned long long* value_in;
+  const uint32_t* rank_of_id;
+  const uint32_t* id_of_rank;
+  int rank_bits, key_bits;
+  uint32_t n, tiles, places, par;
+  uint32_t *hist, *ticket, *look;
+  const void* keys_in;
+  void* keys_out;
+  const unsigned long long* vals_in;
+  unsigned long long* vals_out;
+  unsigned long long* member_out;
+  uint32_t* actor_out;
+  unsigned long long* value_out;
+};
+uint32_t ser_sort_tiles(uint32_t n);
+inline size_t ser_sort_state_words(uint32_t n) {
+  return 2ull * kSortMaxPlaces * 256 + kSortMaxPlaces + (size_t)kSortMaxPlaces * ser_sort_tiles(n) * 256;
+}
+// kbuf: two key buffers of n (u32 when key_bits <= 32, else u64), vbuf: two u64 buffers of n
+hipError_t launch_ser_sort(hipStream_t s, const SerSortArgs& a, void* const kbuf[2], unsigned long long* const vbuf[2]);
 hipError_t launch_orswot_ser(hipStream_t s, OrswotSerScratch& sc, const OrswotSerArgs& a);
 // the same in two halves: the sorts and scans over the n collected pairs (no host input), then the
 // writer (needs the host-built prefix / suffix) -- the host builds them while the sorts run

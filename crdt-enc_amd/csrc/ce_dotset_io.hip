@@ -105,40 +105,6 @@ __global__ void k_ser_unpack(const K* key, int rank_bits, const uint32_t* id_of_
   }
 }
 
-// Counting sort of the live pairs by (member, actor rank) when every member is below
-// 2^kSerCountBits (C3: 100k members): per-member counts, their exclusive scan, a scatter into each
-// member's slice (any order inside it; the counts go back to zero), then each pair's place in
-// its slice = the pairs of the slice with a smaller rank (a member has at most one pair per
-// actor: slices hold <= the actor count, ~12 at C3).  Four launches instead of a radix sort's
-// passes and their runtime fills, but slower at C3 (opt-in CE_SER_COUNT=1, launch_orswot_ser_sort).
-__global__ void k_ser_hist(const unsigned long long* member, uint32_t* count, uint32_t n) {
-  for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < n; i += gridDim.x * kB) atomicAdd(count + (uint32_t)member[i], 1u);
-}
-
-__global__ void k_ser_scatter(OrswotSerScratch sc, uint32_t n) {
-  for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < n; i += gridDim.x * kB) {
-    const uint32_t m = (uint32_t)sc.member_in[i], a = sc.actor_in[i];
-    const uint32_t p = sc.bucket_off[m] + atomicSub(sc.bucket_count + m, 1u) - 1u;
-    sc.k64a[p] = m;
-    sc.k32a[p] = sc.rank_of_id[a];
-    sc.p32a[p] = a;
-    sc.t_value[p] = sc.value_in[i];
-  }
-}
-
-__global__ void k_ser_slice_rank(OrswotSerScratch sc, uint32_t n) {
-  for (uint32_t p = blockIdx.x * kB + threadIdx.x; p < n; p += gridDim.x * kB) {
-    const uint32_t m = (uint32_t)sc.k64a[p], rk = sc.k32a[p];
-    const uint32_t b0 = sc.bucket_off[m], b1 = sc.bucket_off[m + 1];
-    uint32_t r = 0;
-    for (uint32_t q = b0; q < b1; q++) r += sc.k32a[q] < rk;
-    const uint32_t o = b0 + r;
-    sc.member_sorted[o] = m;
-    sc.actor_sorted[o] = sc.p32a[p];
-    sc.value_sorted[o] = sc.t_value[p];
-  }
-}
-
 // head[i] = pair i starts a member's entry
 __global__ void k_ser_head(const unsigned long long* member, uint32_t* head, uint32_t n) {
   for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < n; i += gridDim.x * kB)
@@ -168,6 +134,138 @@ __global__ void k_ser_len(const unsigned long long* member, const unsigned long 
       l += ulen(member[i]) + 6u + maplen(seg[e + 1] - seg[e]);
     }
     len[i] = l;
+  }
+}
+
+// The entry bookkeeping over the sorted pairs in two scans of 2048-pair tiles, each a tile-sums
+// launch and an apply launch that sums the tiles before its own (no separate scan of the sums):
+//   k_ser_head_tiles / k_ser_head_apply: head[i] (pair i starts a member's entry), hrank = its
+//     exclusive scan, seg[] = the entries' CSR over pairs (seg[e] = head position, seg[e + 1]
+//     written by the entry's last pair, seg[n_members] = n)
+//   k_ser_len_tiles / k_ser_len_apply: len[i] = bytes of pair i (its Dot, plus at a head the entry
+//     head: member uint, 81 a4 "dots", map header of the entry's Dot count) and pos = its scan
+// (four launches where head, scan, seg, len, scan were seven)
+constexpr uint32_t kSerItems = 8, kSerTile = kB * kSerItems;
+
+__device__ __forceinline__ uint32_t ser_block_incl(uint32_t v, uint32_t* lds) {
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(v, o);
+    if (lane >= (uint32_t)o) v += y;
+  }
+  if (lane == 63) lds[w] = v;
+  __syncthreads();
+  uint32_t add = 0;
+  for (uint32_t k = 0; k < w; k++) add += lds[k];
+  __syncthreads();
+  return v + add;
+}
+
+// the sum of tile_sum[0 .. blockIdx.x), every lane
+__device__ __forceinline__ uint32_t ser_tiles_before(const uint32_t* tile_sum, uint32_t* lds, uint32_t* off) {
+  uint32_t b = 0;
+  for (uint32_t x = threadIdx.x; x < blockIdx.x; x += kB) b += tile_sum[x];
+  b = ser_block_incl(b, lds);
+  if (threadIdx.x == kB - 1) *off = b;
+  __syncthreads();
+  return *off;
+}
+
+__global__ void __launch_bounds__(kB) k_ser_head_tiles(const unsigned long long* member, uint32_t n, uint32_t* tile_sum) {
+  __shared__ uint32_t lds[kB / 64];
+  const uint32_t i0 = blockIdx.x * kSerTile + threadIdx.x * kSerItems;
+  uint32_t s = 0;
+  unsigned long long prev = i0 > 0 && i0 < n ? member[i0 - 1] : 0ull;
+#pragma unroll
+  for (int k = 0; k < (int)kSerItems; k++) {
+    const uint32_t i = i0 + k;
+    if (i < n) {
+      const unsigned long long m = member[i];
+      s += i == 0 || m != prev;
+      prev = m;
+    }
+  }
+  s = ser_block_incl(s, lds);
+  if (threadIdx.x == kB - 1) tile_sum[blockIdx.x] = s;
+}
+
+__global__ void __launch_bounds__(kB) k_ser_head_apply(const unsigned long long* member, uint32_t n, const uint32_t* tile_sum,
+                                                       uint32_t* head, uint32_t* hrank, uint32_t* seg) {
+  __shared__ uint32_t lds[kB / 64];
+  __shared__ uint32_t off;
+  const uint32_t base = ser_tiles_before(tile_sum, lds, &off);
+  const uint32_t i0 = blockIdx.x * kSerTile + threadIdx.x * kSerItems;
+  unsigned long long m[kSerItems + 2];
+  m[0] = i0 > 0 && i0 <= n ? member[i0 - 1] : 0ull;
+#pragma unroll
+  for (int k = 0; k <= (int)kSerItems; k++) m[k + 1] = i0 + k < n ? member[i0 + k] : 0ull;
+  uint32_t h[kSerItems], s = 0;
+#pragma unroll
+  for (int k = 0; k < (int)kSerItems; k++) {
+    h[k] = i0 + k < n && (i0 + k == 0 || m[k + 1] != m[k]);
+    s += h[k];
+  }
+  uint32_t run = ser_block_incl(s, lds) - s + base;
+#pragma unroll
+  for (int k = 0; k < (int)kSerItems; k++) {
+    const uint32_t i = i0 + k;
+    if (i < n) {
+      head[i] = h[k];
+      hrank[i] = run;
+      const uint32_t e = run + h[k] - 1;  // entry of pair i
+      if (h[k]) seg[e] = i;
+      if (i + 1 == n || m[k + 2] != m[k + 1]) seg[e + 1] = i + 1;
+    }
+    run += h[k];
+  }
+}
+
+__device__ __forceinline__ uint32_t ser_len_of(const unsigned long long* member, const unsigned long long* value,
+                                               const uint32_t* head, const uint32_t* hrank, const uint32_t* seg,
+                                               uint32_t i) {
+  uint32_t l = 18u + ulen(value[i]);
+  if (head[i]) {
+    const uint32_t e = hrank[i];
+    l += ulen(member[i]) + 6u + maplen(seg[e + 1] - seg[e]);
+  }
+  return l;
+}
+
+__global__ void __launch_bounds__(kB) k_ser_len_tiles(const unsigned long long* member, const unsigned long long* value,
+                                                      const uint32_t* head, const uint32_t* hrank, const uint32_t* seg,
+                                                      uint32_t n, uint32_t* tile_sum) {
+  __shared__ uint32_t lds[kB / 64];
+  const uint32_t i0 = blockIdx.x * kSerTile + threadIdx.x * kSerItems;
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < (int)kSerItems; k++)
+    if (i0 + k < n) s += ser_len_of(member, value, head, hrank, seg, i0 + k);
+  s = ser_block_incl(s, lds);
+  if (threadIdx.x == kB - 1) tile_sum[blockIdx.x] = s;
+}
+
+__global__ void __launch_bounds__(kB) k_ser_len_apply(const unsigned long long* member, const unsigned long long* value,
+                                                      const uint32_t* head, const uint32_t* hrank, const uint32_t* seg,
+                                                      uint32_t n, const uint32_t* tile_sum, uint32_t* len, uint32_t* pos) {
+  __shared__ uint32_t lds[kB / 64];
+  __shared__ uint32_t off;
+  const uint32_t base = ser_tiles_before(tile_sum, lds, &off);
+  const uint32_t i0 = blockIdx.x * kSerTile + threadIdx.x * kSerItems;
+  uint32_t l[kSerItems], s = 0;
+#pragma unroll
+  for (int k = 0; k < (int)kSerItems; k++) {
+    l[k] = i0 + k < n ? ser_len_of(member, value, head, hrank, seg, i0 + k) : 0u;
+    s += l[k];
+  }
+  uint32_t run = ser_block_incl(s, lds) - s + base;
+#pragma unroll
+  for (int k = 0; k < (int)kSerItems; k++) {
+    if (i0 + k < n) {
+      len[i0 + k] = l[k];
+      pos[i0 + k] = run;
+    }
+    run += l[k];
   }
 }
 
@@ -597,24 +695,36 @@ hipError_t launch_orswot_ser(hipStream_t s, OrswotSerScratch& sc, const OrswotSe
 }
 
 hipError_t launch_orswot_ser_sort(hipStream_t s, OrswotSerScratch& sc, uint32_t n) {
-  // pairs (member, actor id, value) in collect order -> sorted by (member, rank): one sort of the
-  // packed (member, rank) key when it fits 64 bits (CE_SER_TWO_SORTS=1: the general form -- sort by
-  // rank, then stably by member, LSD order), gather
+  // pairs (member, actor id, value) in collect order -> sorted by (member, rank): the hand-written
+  // radix sort of the packed (member, rank) key when it fits 64 bits (ce_ser_sort.hip; CE_SER_CUB=1:
+  // hipCUB's sort of the same key, for A/B), else (or CE_SER_TWO_SORTS=1) the general form -- sort
+  // by rank, then stably by member, LSD order -- and a gather
   hipError_t e;
   const int kb = sc.member_bits + sc.rank_bits;
-  // CE_SER_COUNT=1: the counting sort (measured slower at C3: 200 us for hist + scatter + ranks
-  // against 112 us for the radix sort -- its per-member counters are device-scope atomics on
-  // random addresses, which the XCDs' separate L2s cannot keep; r05)
-  const bool count = getenv("CE_SER_COUNT") != nullptr;  // (the tests flip it)
-  if (n && sc.member_bits <= kSerCountBits && sc.bucket_count && count && !getenv("CE_SER_TWO_SORTS")) {
-    const uint32_t nb = (1u << sc.member_bits) + 1;  // buckets: every member value < 2^member_bits, one past
-    size_t tb = sc.tmp_bytes;
-    hipLaunchKernelGGL(k_ser_hist, dim3(nblk(n)), dim3(kB), 0, s, sc.member_in, sc.bucket_count, n);
-    if ((e = ds_excl_sum_u32(sc.tmp, tb, sc.bucket_count, sc.bucket_off, nb, s))) return e;
-    hipLaunchKernelGGL(k_ser_scatter, dim3(nblk(n)), dim3(kB), 0, s, sc, n);
-    hipLaunchKernelGGL(k_ser_slice_rank, dim3(nblk(n)), dim3(kB), 0, s, sc, n);
-  } else if (n && kb <= 64 && !getenv("CE_SER_TWO_SORTS")) {
-    // (member, rank) in one key: one radix sort over member_bits + rank_bits
+  static const bool cub = getenv("CE_SER_CUB") != nullptr;
+  const bool two = getenv("CE_SER_TWO_SORTS") != nullptr;  // (the tests flip it)
+  if (n && kb <= 64 && !two && !cub && n < (1u << 30)) {
+    SerSortArgs a{};
+    a.member_in = sc.member_in;
+    a.actor_in = sc.actor_in;
+    a.value_in = sc.value_in;
+    a.rank_of_id = sc.rank_of_id;
+    a.id_of_rank = sc.id_of_rank;
+    a.rank_bits = sc.rank_bits;
+    a.key_bits = kb;
+    a.n = n;
+    a.par = (*sc.sort_gen)++ & 1u;
+    a.hist = sc.sort_state;
+    a.ticket = a.hist + 2 * kSortMaxPlaces * 256;
+    a.look = a.ticket + kSortMaxPlaces;
+    a.member_out = sc.member_sorted;
+    a.actor_out = sc.actor_sorted;
+    a.value_out = sc.value_sorted;
+    void* kbuf[2] = {kb <= 32 ? (void*)sc.k32a : (void*)sc.k64a, kb <= 32 ? (void*)sc.k32b : (void*)sc.k64b};
+    unsigned long long* vbuf[2] = {sc.v64a, sc.v64b};
+    if ((e = launch_ser_sort(s, a, kbuf, vbuf))) return e;
+  } else if (n && kb <= 64 && !two) {
+    // (member, rank) in one key: hipCUB's radix sort over member_bits + rank_bits
     size_t tb = sc.tmp_bytes;
     if (kb <= 32) {
       hipLaunchKernelGGL(k_ser_key<uint32_t>, dim3(nblk(n)), dim3(kB), 0, s, sc.actor_in, sc.rank_of_id, sc.member_in,
@@ -648,7 +758,17 @@ hipError_t launch_orswot_ser_sort(hipStream_t s, OrswotSerScratch& sc, uint32_t 
     hipLaunchKernelGGL(k_ser_gather2, dim3(nblk(n)), dim3(kB), 0, s, sc.p32a, sc.actor_in, sc.value_in,
                        sc.actor_sorted, sc.value_sorted, n);
   }
-  if (n) {
+  const uint32_t nt = (n + kSerTile - 1) / kSerTile;
+  if (n && nt <= 4096 && 8ull * nt <= sc.tmp_bytes) {
+    // (an apply block sums the tile totals before it: up to 4096 tiles, 8M pairs)
+    uint32_t* ts = static_cast<uint32_t*>(sc.tmp);
+    hipLaunchKernelGGL(k_ser_head_tiles, dim3(nt), dim3(kB), 0, s, sc.member_sorted, n, ts);
+    hipLaunchKernelGGL(k_ser_head_apply, dim3(nt), dim3(kB), 0, s, sc.member_sorted, n, ts, sc.head, sc.hrank, sc.seg);
+    hipLaunchKernelGGL(k_ser_len_tiles, dim3(nt), dim3(kB), 0, s, sc.member_sorted, sc.value_sorted, sc.head, sc.hrank,
+                       sc.seg, n, ts + nt);
+    hipLaunchKernelGGL(k_ser_len_apply, dim3(nt), dim3(kB), 0, s, sc.member_sorted, sc.value_sorted, sc.head, sc.hrank,
+                       sc.seg, n, ts + nt, sc.len, sc.pos);
+  } else if (n) {
     size_t tb = sc.tmp_bytes;
     hipLaunchKernelGGL(k_ser_head, dim3(nblk(n)), dim3(kB), 0, s, sc.member_sorted, sc.head, n);
     tb = sc.tmp_bytes;

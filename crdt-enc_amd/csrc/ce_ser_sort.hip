@@ -1,0 +1,246 @@
+// ce_ser_sort.hip -- the Orswot serializer's sort: the live (member, actor, counter) pairs of a
+// collect ordered by (member, actor UUID rank), as the StateWrapper's entries map is written
+// (crdts Orswot's BTreeMap<M, VClock> -> rmp-serde; crdt-enc/src/lib.rs:332-380).
+//
+// An LSD radix sort over the packed key member << rank_bits | rank (unique per pair), 8-bit
+// digits, one kernel per digit place and one histogram kernel before them -- no runtime fills:
+//   k_sort_hist   every place's digit counts (LDS per block, then one no-return add per digit
+//                 into hist[par]); zeroes what the passes need zero: their lookback words and tile
+//                 tickets, and the other parity's histogram (the next sort's)
+//   k_sort_pass   one 4096-item tile per workgroup, tiles in ticket order: the tile's items
+//                 ranked stably per digit (per-wave match on the digit bits, wave counters in
+//                 LDS), the tile's digit counts published for the tiles after it and its prefix
+//                 found by looking back over the tiles before it (decoupled look-back; the words
+//                 are agent-scope atomics), then the tile reordered in LDS and written out as
+//                 contiguous digit runs.  The first pass builds the key from the collect columns
+//                 (member, actor id -> rank); the last writes the serializer's sorted member /
+//                 actor id / counter columns directly.
+// Stability: a wave owns 1024 consecutive items and walks them 64 at a time in order, the waves'
+// counts are prefixed in wave order and the tiles' in ticket order, so equal digits keep their
+// input order, as LSD needs.
+#include "ce_dotset_io.h"
+
+namespace ce {
+namespace {
+
+constexpr int kSortThreads = 256;
+constexpr int kSortWaves = kSortThreads / 64;
+constexpr int kSortPerLane = 16;
+constexpr uint32_t kSortTile = kSortThreads * kSortPerLane;  // 4096
+constexpr int kDigitBits = 8;
+constexpr uint32_t kDigits = 1u << kDigitBits;
+constexpr uint32_t kFlagAgg = 1u << 30, kFlagInc = 2u << 30, kCountMask = (1u << 30) - 1;
+static_assert(kDigits == kSortThreads, "one lane per digit in the tile bookkeeping");
+
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <typename K>
+__device__ __forceinline__ K pair_key(const SerSortArgs& a, uint32_t i) {
+  return ((K)a.member_in[i] << a.rank_bits) | (K)a.rank_of_id[a.actor_in[i]];
+}
+
+// block-wide exclusive scan of one value per lane (256 lanes); returns the lane's prefix and
+// *total the sum
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t* total) {
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint32_t before = 0, all = 0;
+#pragma unroll
+  for (int k = 0; k < kSortWaves; k++) {
+    before += (uint32_t)k < w ? wsum[k] : 0u;
+    all += wsum[k];
+  }
+  __syncthreads();
+  *total = all;
+  return before + x - v;
+}
+
+template <typename K>
+__global__ void __launch_bounds__(kSortThreads) k_sort_hist(SerSortArgs a) {
+  __shared__ uint32_t lh[kSortMaxPlaces][kDigits];
+  const uint32_t t = threadIdx.x;
+  // zero what this sort's passes need zero, and the next sort's histogram
+  const uint32_t nz = a.places * a.tiles * kDigits;
+  for (uint32_t i = blockIdx.x * kSortThreads + t; i < nz; i += gridDim.x * kSortThreads) a.look[i] = 0;
+  if (blockIdx.x == 0) {
+    if (t < kSortMaxPlaces) a.ticket[t] = 0;
+    for (uint32_t i = t; i < kSortMaxPlaces * kDigits; i += kSortThreads)
+      a.hist[(size_t)(a.par ^ 1) * kSortMaxPlaces * kDigits + i] = 0;
+  }
+  for (uint32_t p = 0; p < a.places; p++) lh[p][t] = 0;
+  __syncthreads();
+  const uint32_t i0 = blockIdx.x * kSortTile;
+#pragma unroll 4
+  for (int k = 0; k < kSortPerLane; k++) {
+    const uint32_t i = i0 + k * kSortThreads + t;
+    if (i >= a.n) break;
+    const K key = pair_key<K>(a, i);
+    for (uint32_t p = 0; p < a.places; p++) atomicAdd(&lh[p][(uint32_t)(key >> (p * kDigitBits)) & (kDigits - 1)], 1u);
+  }
+  __syncthreads();
+  uint32_t* h = a.hist + (size_t)a.par * kSortMaxPlaces * kDigits;
+  for (uint32_t p = 0; p < a.places; p++)
+    if (lh[p][t]) atomicAdd(h + p * kDigits + t, lh[p][t]);
+}
+
+template <typename K, bool FIRST, bool LAST>
+__global__ void __launch_bounds__(kSortThreads) k_sort_pass(SerSortArgs a, uint32_t place) {
+  __shared__ K lkey[kSortTile];
+  __shared__ unsigned long long lval[kSortTile];
+  __shared__ uint32_t wcnt[kSortWaves][kDigits];  // per wave: items of each digit so far
+  __shared__ uint32_t tstart[kDigits], gofs[kDigits], wsum[kSortWaves], tile_s;
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t == 0) tile_s = atomicAdd(a.ticket + place, 1u);  // tiles in dispatch order (look-back)
+#pragma unroll
+  for (int k = 0; k < kSortWaves; k++) wcnt[k][t] = 0;
+  __syncthreads();
+  const uint32_t tile = tile_s, base = tile * kSortTile;
+  const uint32_t shift = place * kDigitBits;
+  // wave w's items: base + 1024 w + 64 k + lane, k = 0..15 (in input order)
+  K key[kSortPerLane];
+  unsigned long long val[kSortPerLane];
+  uint32_t rk[kSortPerLane];
+#pragma unroll
+  for (int k = 0; k < kSortPerLane; k++) {
+    const uint32_t i = base + w * (64 * kSortPerLane) + k * 64 + lane;
+    key[k] = 0;
+    val[k] = 0;
+    if (i < a.n) {
+      if (FIRST) {
+        key[k] = pair_key<K>(a, i);
+        val[k] = a.value_in[i];
+      } else {
+        key[k] = reinterpret_cast<const K*>(a.keys_in)[i];
+        val[k] = a.vals_in[i];
+      }
+    }
+  }
+  const unsigned long long lt = (1ull << lane) - 1;
+#pragma unroll
+  for (int k = 0; k < kSortPerLane; k++) {
+    const uint32_t i = base + w * (64 * kSortPerLane) + k * 64 + lane;
+    const bool ok = i < a.n;
+    const uint32_t d = (uint32_t)(key[k] >> shift) & (kDigits - 1);
+    // lanes holding the same digit: the digit's bits matched by ballots
+    unsigned long long peers = __ballot(ok);
+#pragma unroll
+    for (int b = 0; b < kDigitBits; b++) {
+      const unsigned long long m = __ballot((d >> b) & 1u);
+      peers &= ((d >> b) & 1u) ? m : ~m;
+    }
+    const uint32_t before = wcnt[w][d];  // every peer reads the count before the leader adds
+    rk[k] = before + (uint32_t)__popcll(peers & lt);
+    if (ok && (peers & lt) == 0) wcnt[w][d] = before + (uint32_t)__popcll(peers);
+  }
+  __syncthreads();
+  // digit t: the tile's count, the waves' bases inside it, the tile-local start of the digit
+  uint32_t tot = 0, wb[kSortWaves];
+#pragma unroll
+  for (int k = 0; k < kSortWaves; k++) {
+    wb[k] = tot;
+    tot += wcnt[k][t];
+  }
+  // publish the tile's count of digit t, then its prefix over the tiles before (look-back)
+  uint32_t* look = a.look + ((size_t)place * a.tiles) * kDigits;
+  uint32_t prefix = 0;
+  if (tile == 0) {
+    st_agent(look + t, tot | kFlagInc);
+  } else {
+    st_agent(look + (size_t)tile * kDigits + t, tot | kFlagAgg);
+    for (int32_t j = (int32_t)tile - 1; j >= 0;) {
+      const uint32_t v = ld_agent(look + (size_t)j * kDigits + t);
+      if (v == 0) {
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      prefix += v & kCountMask;
+      if (v & kFlagInc) break;
+      j--;
+    }
+    st_agent(look + (size_t)tile * kDigits + t, (prefix + tot) | kFlagInc);
+  }
+  const uint32_t* h = a.hist + (size_t)a.par * kSortMaxPlaces * kDigits + place * kDigits;
+  uint32_t all;
+  const uint32_t hx = block_excl_scan(h[t], wsum, &all);
+  gofs[t] = hx + prefix;
+  const uint32_t ts = block_excl_scan(tot, wsum, &all);
+  tstart[t] = ts;
+#pragma unroll
+  for (int k = 0; k < kSortWaves; k++) wcnt[k][t] = wb[k] + ts;  // tile-local base of (wave k, digit t)
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kSortPerLane; k++) {
+    const uint32_t i = base + w * (64 * kSortPerLane) + k * 64 + lane;
+    if (i >= a.n) continue;
+    const uint32_t d = (uint32_t)(key[k] >> shift) & (kDigits - 1);
+    const uint32_t lp = wcnt[w][d] + rk[k];
+    lkey[lp] = key[k];
+    lval[lp] = val[k];
+  }
+  __syncthreads();
+  // the tile in digit order: consecutive lanes write consecutive places of a digit's run
+  const uint32_t tn = min(kSortTile, a.n - base);
+  for (uint32_t lp = t; lp < tn; lp += kSortThreads) {
+    const K kk = lkey[lp];
+    const uint32_t d = (uint32_t)(kk >> shift) & (kDigits - 1);
+    const uint32_t g = gofs[d] + (lp - tstart[d]);
+    if (LAST) {
+      a.member_out[g] = (unsigned long long)(kk >> a.rank_bits);
+      a.actor_out[g] = a.id_of_rank[(uint32_t)kk & ((1u << a.rank_bits) - 1)];
+      a.value_out[g] = lval[lp];
+    } else {
+      reinterpret_cast<K*>(a.keys_out)[g] = kk;
+      a.vals_out[g] = lval[lp];
+    }
+  }
+}
+
+template <typename K, bool FIRST, bool LAST>
+void pass_launch(hipStream_t s, const SerSortArgs& a, uint32_t p) {
+  hipLaunchKernelGGL((k_sort_pass<K, FIRST, LAST>), dim3(a.tiles), dim3(kSortThreads), 0, s, a, p);
+}
+
+template <typename K>
+hipError_t sort_typed(hipStream_t s, SerSortArgs a, void* const kbuf[2], unsigned long long* const vbuf[2]) {
+  hipLaunchKernelGGL(k_sort_hist<K>, dim3(a.tiles), dim3(kSortThreads), 0, s, a);
+  for (uint32_t p = 0; p < a.places; p++) {
+    const bool first = p == 0, last = p + 1 == a.places;
+    a.keys_in = kbuf[(p + 1) & 1];
+    a.vals_in = vbuf[(p + 1) & 1];
+    a.keys_out = kbuf[p & 1];
+    a.vals_out = vbuf[p & 1];
+    if (first && last) pass_launch<K, true, true>(s, a, p);
+    else if (first) pass_launch<K, true, false>(s, a, p);
+    else if (last) pass_launch<K, false, true>(s, a, p);
+    else pass_launch<K, false, false>(s, a, p);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace
+
+uint32_t ser_sort_tiles(uint32_t n) { return (n + kSortTile - 1) / kSortTile; }
+
+hipError_t launch_ser_sort(hipStream_t s, const SerSortArgs& in, void* const kbuf[2],
+                           unsigned long long* const vbuf[2]) {
+  SerSortArgs a = in;
+  if (a.n == 0) return hipSuccess;
+  a.tiles = ser_sort_tiles(a.n);
+  a.places = (uint32_t)((a.key_bits + kDigitBits - 1) / kDigitBits);
+  if (a.places == 0) a.places = 1;
+  return a.key_bits <= 32 ? sort_typed<uint32_t>(s, a, kbuf, vbuf) : sort_typed<unsigned long long>(s, a, kbuf, vbuf);
+}
+
+}  // namespace ce

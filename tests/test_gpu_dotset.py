@@ -17,6 +17,7 @@ import dotset_gen as G
 from oracle import crdts as C
 
 pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 APP = bytes.fromhex("aadfd5a66e194b24a8024fa27c72f20c")
 CORE = crdtenc.CORE_VERSION
 KIND = {"orswot": crdtenc.STATE_ORSWOT, "mvreg": crdtenc.STATE_MVREG}
@@ -838,8 +839,8 @@ def test_orswot_tiled_emit_equals_direct(ctx, adversarial):
 
 @pytest.mark.parametrize("adversarial", [False, True])
 def test_orswot_partitioned_fold_equals_global(ctx, adversarial):
-    """The partitioned fold (items bucketed by pair-table partition, each partition folded in LDS:
-    k_ds_part_*) == the global kernels (k_ds_add_pairs / k_ds_kill / k_ds_finalize, forced with
+    """The partitioned fold (items reserved into per-partition runs, each partition folded in LDS:
+    k_ds_part_*; with 64-item runs most items go through the overflow lists) == the global kernels (k_ds_add_pairs / k_ds_kill / k_ds_finalize, forced with
     CE_DS_FOLD_GLOBAL=1) == the oracle, over four batches that grow the tables past one partition
     and carry deferred removals from batch to batch (adversarial: removals naming other writers'
     dots, multi-entry clocks and several members per removal)."""
@@ -859,7 +860,8 @@ def test_orswot_partitioned_fold_equals_global(ctx, adversarial):
         want.append((rc, oc.serialize()))
     got = {}
     modes = {"partitioned": {}, "global": {"CE_DS_FOLD_GLOBAL": "1"},
-             "member_overflow": {"CE_DS_PRIMARY_SLOTS": "64"}}   # most members in the overflow table
+             "member_overflow": {"CE_DS_PRIMARY_SLOTS": "64"},   # most members in the overflow table
+             "run_overflow": {"CE_DS_PART_FACTOR": "0"}}          # 64-item runs: the overflow lists
     for mode, env in modes.items():
         os.environ.update(env)
         try:
@@ -867,26 +869,30 @@ def test_orswot_partitioned_fold_equals_global(ctx, adversarial):
             out = []
             for acts, sealed, fa, fv in batches:
                 out.append((core.ingest_ops(sealed, acts, fa, fv)[0], core.state_bytes()))
-            got[mode] = (out, core.path_count("ds_fold_partitioned"), core.path_count("ds_fold_global"))
+            got[mode] = (out, core.path_count("ds_fold_partitioned"), core.path_count("ds_fold_global"),
+                         core.path_count("ds_fold_run_overflow"))
             core.close()
         finally:
             for k in env:
                 os.environ.pop(k, None)
     for mode in modes:
         assert got[mode][0] == want, mode
-    assert got["partitioned"][1:] == (len(batches), 0)
-    assert got["member_overflow"][1:] == (len(batches), 0)
-    assert got["global"][1:] == (0, len(batches))
+    assert got["partitioned"][1:3] == (len(batches), 0)
+    assert got["member_overflow"][1:3] == (len(batches), 0)
+    assert got["run_overflow"][1:3] == (len(batches), 0)
+    if not adversarial:   # (the adversarial batches apply few adds: their runs may not fill)
+        assert got["run_overflow"][3] >= 1
+    assert got["global"][1:3] == (0, len(batches))
 
 
 @pytest.mark.parametrize("n_members", [300, 1 << 20, 1 << 40, (1 << 64) - 1, "shared"])
 def test_orswot_serializer_one_sort_equals_two(ctx, n_members):
     """The device serializer orders the live (member, actor) pairs by (member, actor UUID rank):
-    by one radix sort of the packed key when member bits + actor-rank bits fit 64, else by rank
-    then stably by member, or (opt-in) by a counting sort over member values below 2^20.  Each
-    form (default, CE_SER_COUNT=1, CE_SER_TWO_SORTS=1) == the oracle's bytes, for
-    small, 20-bit (one past the counting range), 40-bit and full 64-bit members, and for members
-    every one of 300 actors adds (slices of 300 pairs)."""
+    by the hand-written radix sort of the packed key when member bits + actor-rank bits fit 64
+    (ce_ser_sort.hip), else by rank then stably by member.  Each form (default, CE_SER_CUB=1:
+    hipCUB's sort of the packed key, CE_SER_TWO_SORTS=1) == the oracle's bytes, for small,
+    20-bit, 40-bit (64-bit keys) and full 64-bit members (the two sorts), and for members every
+    one of 300 actors adds (slices of 300 pairs)."""
     rng = random.Random(929 + (n_members % 1000 if isinstance(n_members, int) else 7))
     key = rng.randbytes(32)
     if n_members == "shared":
@@ -902,7 +908,7 @@ def test_orswot_serializer_one_sort_equals_two(ctx, n_members):
     import torch
     want = oc.serialize()
     got = []
-    for mode in (None, "CE_SER_COUNT", "CE_SER_TWO_SORTS"):
+    for mode in (None, "CE_SER_CUB", "CE_SER_TWO_SORTS"):
         if mode:
             os.environ[mode] = "1"
         try:
@@ -918,6 +924,50 @@ def test_orswot_serializer_one_sort_equals_two(ctx, n_members):
             if mode:
                 os.environ.pop(mode, None)
     assert got[0] == got[1] == got[2] == want
+
+
+@pytest.mark.parametrize("member_bits", [18, 36])
+def test_orswot_serializer_sort_many_tiles(ctx, member_bits):
+    """The hand-written sort over many 4096-pair tiles (the look-back between tiles, every digit
+    place, 32- and 64-bit keys): ~300 K live pairs from 256 writers, serialized on the device ==
+    the same state serialized with hipCUB's sort (CE_SER_CUB=1, a separate process: the choice is
+    read once) == the two-sort form; plus a checksum of the bytes' member order: entries strictly
+    ascending."""
+    import subprocess
+    import sys
+    code = (
+        "import os, sys, hashlib, random\n"
+        "sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
+        "import crdtenc, torch\n"
+        "import dotset_gen as G\n"
+        "from oracle import crdts as C\n"
+        "rng = random.Random(4242)\n"
+        "key = rng.randbytes(32)\n"
+        "actors = G.actors_for(rng, 256)\n"
+        "files = {a: [[('Add', (a, v * 400 + j + 1), [(rng.getrandbits(%d) | 1) for _ in range(3)]) "
+        "for j in range(400)] for v in range(1)] for a in actors}\n"
+        "acts, clears, fa, fv = G.batch(files, 'orswot', bytes.fromhex(%r))\n"
+        "ctx = crdtenc.Context(0)\n"
+        "sealed = [bytes.fromhex(%r) + e for e in ctx.encrypt_batch(key, clears)]\n"
+        "core = crdtenc.Core(ctx, kind=crdtenc.STATE_ORSWOT, supported=[bytes.fromhex(%r)], current_data_version=bytes.fromhex(%r))\n"
+        "core.set_latest_key(key)\n"
+        "assert core.ingest_ops(sealed, acts, fa, fv)[0] == 0\n"
+        "buf = torch.zeros(64 << 20, dtype=torch.uint8, device='cuda:0')\n"
+        "rc, n = core.state_bytes_device(buf.data_ptr(), buf.numel())\n"
+        "assert rc == 0, rc\n"
+        "torch.cuda.synchronize()\n"
+        "b = bytes(buf[:n].cpu().numpy().tobytes())\n"
+        "print(hashlib.sha256(b).hexdigest(), n)\n"
+        % (os.path.join(REPO, "crdt-enc_amd"), os.path.join(REPO, "tests"), member_bits, APP.hex(),
+           CORE.hex(), APP.hex(), APP.hex()))
+    outs = []
+    for env in ({}, {"CE_SER_CUB": "1"}, {"CE_SER_TWO_SORTS": "1"}):
+        p = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), capture_output=True,
+                           timeout=300, cwd=REPO)
+        assert p.returncode == 0, p.stderr.decode()[-2000:]
+        outs.append(p.stdout.decode().split()[-2:])
+    assert outs[0] == outs[1] == outs[2], outs
+    assert int(outs[0][1]) > 300000 * 20
 
 
 @pytest.mark.parametrize("kind", ["orswot", "mvreg"])
