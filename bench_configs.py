@@ -493,8 +493,8 @@ def run_c3(args, ctx, dev):
                         "what": "the same step with the 8 state files uploaded from per-file host "
                                 "buffers each step (ce_core_ingest_states_iov: pinned staging + DMA)"}
     names = ("open_setup", "open_small", "segments_open", "finalize_open", "gate", "ds_count", "ds_emit",
-             "ds_applied", "ds_add_pairs", "ds_kill", "ds_finalize", "ds_part_fold", "ds_merge", "seal_setup",
-             "segments_seal")
+             "ds_contig", "ds_applied", "ds_add_pairs", "ds_kill", "ds_finalize", "ds_part_fold", "ds_merge",
+             "seal_setup", "segments_seal")
     kern = {k: ctx.timing(k) for k in names}
     sb = core.state_bytes()
     t_n = time.perf_counter()
@@ -574,7 +574,8 @@ def run_c3(args, ctx, dev):
     fold_bytes = n_add * (4 + 8 + 4 + 8 + 32) + n_rm * (8 + 12 + 8 + 24)
     # (the partitioned fold: applied flags + ds_part_fold = member probes, bucketing, the LDS fold
     # with finalize, the clock; the global kernels: applied + add_pairs + kill, finalize apart)
-    fold_ms = sum(k_ms.get(x, 0) for x in ("ds_applied", "ds_add_pairs", "ds_kill", "ds_part_fold"))
+    # (ds_contig: the contiguity check, which also writes the applied flags of increasing runs)
+    fold_ms = sum(k_ms.get(x, 0) for x in ("ds_applied", "ds_contig", "ds_add_pairs", "ds_kill", "ds_part_fold"))
     line = {
         "metric": "C3 op+state files compacted/sec (Orswot<u64,Uuid>)",
         "value": round((n + n_state) / (ms / 1e3), 1), "unit": "files/s", "n_gpus": 1,
@@ -597,8 +598,9 @@ def run_c3(args, ctx, dev):
                               "hashed on %d host threads; timed up to the last download; ms_per_step "
                               "above adds the names still being hashed then (drain / steps)" % name_threads()},
         "aead_open_GBps": round(ct / (open_ms / 1e3) / 1e9, 1) if open_ms else None,
-        "fold": {"kernels": "ds_applied + ds_part_fold (member probes, bucketing by pair-table partition, LDS "
-                            "fold + finalize, clock)" if "ds_part_fold" in k_ms else "ds_applied + ds_add_pairs + ds_kill",
+        "fold": {"kernels": "applied flags (ds_contig for increasing runs, else ds_applied) + ds_part_fold (member "
+                            "probes, items into per-partition runs, LDS fold + finalize, clock)" if "ds_part_fold" in k_ms
+                 else "ds_applied + ds_add_pairs + ds_kill",
                  "ms": round(fold_ms, 4),
                  "algorithmic_bytes": fold_bytes,
                  "achieved_GBps": round(fold_bytes / (fold_ms / 1e3) / 1e9, 1) if fold_ms else None,

@@ -115,8 +115,18 @@ hipError_t launch_ds_applied(hipStream_t s, const uint32_t* keys_sorted, const u
                              uint8_t* applied, uint32_t n);
 // flag |= 1 unless every actor's adds are one contiguous run (marks: u32[n_marks] holding older
 // generations only; gen = a fresh nonzero value per check)
+// the contiguity check's optional second job (k_ds_contig): applied flags and exclusive maxima of
+// strictly increasing runs (ctr null: off)
+struct DsMono {
+  const unsigned long long* ctr;
+  const unsigned long long* clock;
+  uint32_t ccap;
+  uint8_t* applied;
+  unsigned long long* excl;
+};
 hipError_t launch_ds_contig(hipStream_t s, const uint32_t* actor, uint32_t n, uint32_t* marks, uint32_t n_marks,
-                            uint32_t gen, uint32_t* flag, const uint32_t* miss_src = nullptr, uint32_t* pub = nullptr);
+                            uint32_t gen, uint32_t* flag, const uint32_t* miss_src = nullptr, uint32_t* pub = nullptr,
+                            DsMono mono = DsMono{});
 // clock[a] = max(clock[a], counter) for every add
 hipError_t launch_ds_clock(hipStream_t s, const uint32_t* keys_sorted, const unsigned long long* ctr_sorted,
                            const unsigned long long* excl_max, unsigned long long* clock, uint32_t n_add);
@@ -149,6 +159,7 @@ hipError_t launch_ds_finalize(hipStream_t s, DsTables t);
 // live[0] += change of the live-pair count (two's complement), live[1] += pairs inserted, live[5]
 // = items that overflowed; K1 zeroes live[0], live[1], live[3] and live[4].
 static constexpr uint32_t kDsPartChunk = 8192;      // adds / removals per K1 block (one trip)
+static constexpr uint32_t kDsPartReps = 8;          // sub-runs per partition and side (K1 block % 8)
 static constexpr uint32_t kDsPartMaxParts = 16384;  // LDS histogram bound (64 KB)
 struct DsKillSrc {
   const uint32_t* cbeg;
@@ -170,9 +181,9 @@ struct DsPartArgs {
   uint32_t parts;               // (pmask + 1) >> kDsPartBits
   uint32_t chunk;               // adds per K1 block (kDsPartChunk)
   uint32_t kchunk;              // removals per K1 block (fewer items: smaller blocks' worth)
-  uint32_t cap[2];              // run length per partition: adds, removals
-  uint32_t* pcnt;               // [2 parts]: items reserved per partition (adds, then removals)
-  unsigned long long* items;    // (key, value) pairs: parts x cap[0] adds, then parts x cap[1] removals
+  uint32_t cap[2];              // sub-run length: adds, removals
+  uint32_t* pcnt;               // [2][kDsPartReps][parts]: items reserved per sub-run (adds, removals)
+  unsigned long long* items;    // (key, value) pairs: [parts][kDsPartReps][cap[0]] adds, then the removals
   unsigned long long* ovf[2];   // overflow lists (key, value): adds, removals
   uint32_t ovf_cap[2];
   uint32_t* ovf_n;              // [4]: [2 par + 0 / 1] overflow counts of adds / removals

@@ -660,16 +660,28 @@ __global__ void k_ds_applied(const uint32_t* keys, const uint32_t* perm,
 }
 
 // flag |= 1 unless every actor's adds form one contiguous run: a run head stamps its actor's
-// mark with this check's generation; a second head of the same actor finds the stamp
-// (pub: pinned words -- [0] the emit's miss count copied from miss_src, [1] the flag, set by a
-// plain store; the host zeroes it before the launch)
+// mark with this check's generation; a second head of the same actor finds the stamp.
+// With mono (the pinned form): also the applied flags and exclusive maxima of runs whose counters
+// strictly increase (load_ops order of a writer's own op files): the exclusive max of add i is
+// then its predecessor's counter, so add i applies iff ctr > max(ctr[i - 1], C0[a]) (C0 = clock
+// before the batch; ids past ccap are new actors, C0 = 0).  pub: pinned words -- [0] the emit's
+// miss count copied from miss_src, [1] the contiguity flag, [2] set when a run does not
+// strictly increase (then the fold takes the segmented scan); plain stores, zeroed by the host.
 __global__ void k_ds_contig(const uint32_t* actor, uint32_t n, uint32_t* marks, uint32_t n_marks, uint32_t gen,
-                            uint32_t* flag, const uint32_t* miss_src, uint32_t* pub) {
+                            uint32_t* flag, const uint32_t* miss_src, uint32_t* pub, DsMono mono) {
   if (pub && blockIdx.x == 0 && threadIdx.x == 0) pub[0] = *miss_src;  // (the emit is done)
-  bool bad = false;
+  bool bad = false, rise = true;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
     const uint32_t a = actor[i];
-    if (i > 0 && actor[i - 1] == a) continue;
+    const bool head = i == 0 || actor[i - 1] != a;
+    if (mono.ctr) {
+      const unsigned long long c = mono.ctr[i], prev = head ? 0ull : mono.ctr[i - 1];
+      if (!head && c <= prev) rise = false;
+      const unsigned long long c0 = a < mono.ccap ? mono.clock[a] : 0ull;
+      mono.excl[i] = prev;
+      mono.applied[i] = c > (prev > c0 ? prev : c0);
+    }
+    if (!head) continue;
     if (a >= n_marks) { bad = true; continue; }
     bad |= atomicExch(marks + a, gen) == gen;
   }
@@ -677,6 +689,7 @@ __global__ void k_ds_contig(const uint32_t* actor, uint32_t n, uint32_t* marks, 
     if (pub) pub[1] = 1u;
     else atomicOr(flag, 1u);
   }
+  if (pub && __any(!rise) && (threadIdx.x & 63) == 0) pub[2] = 1u;
 }
 
 // clock[a] = max(clock[a], every counter of actor a in the batch), from the actor-sorted adds:
@@ -785,11 +798,14 @@ static_assert(kDsPartChunk == kPartThreads * kPartBatch, "K1 walks its chunk in 
 
 // K1 after its count: lh[p] (this block's items of partition p) -> the base of its reservation in
 // p's run, one returning add per partition with items (64 contiguous counters per wave instruction)
+// (block b reserves in sub-run b % kDsPartReps of every partition: a counter then takes
+// ~blocks / 8 same-address adds -- one counter per partition took ~200, ~60 ns each across XCDs)
 __device__ __forceinline__ void part_reserve(uint32_t* lh, uint32_t parts, uint32_t* pcnt) {
   __syncthreads();
+  uint32_t* c = pcnt + (size_t)(blockIdx.x % kDsPartReps) * parts;
   for (uint32_t p = threadIdx.x; p < parts; p += kPartThreads) {
     const uint32_t n = lh[p];
-    if (n) lh[p] = atomicAdd(pcnt + p, n);
+    if (n) lh[p] = atomicAdd(c + p, n);
   }
   __syncthreads();
 }
@@ -800,7 +816,9 @@ __device__ __forceinline__ void part_put(const DsPartArgs& a, int side, uint32_t
                                          unsigned long long key, unsigned long long v) {
   unsigned long long* dst;
   if (pos < a.cap[side]) {
-    dst = a.items + 2ull * (((size_t)side * a.parts * a.cap[0]) + (size_t)p * a.cap[side] + pos);
+    const uint32_t r = blockIdx.x % kDsPartReps;
+    dst = a.items + 2ull * ((size_t)side * a.parts * kDsPartReps * a.cap[0] +
+                            ((size_t)p * kDsPartReps + r) * a.cap[side] + pos);
   } else {
     const uint32_t o = atomicAdd(a.ovf_n + 2 * a.par + side, 1u);
     if (o >= a.ovf_cap[side]) {  // (sized for every item of the batch: not reached)
@@ -932,7 +950,7 @@ __global__ void __launch_bounds__(kPartThreads) k_ds_part_kills(DsPartArgs a) {
       }
     }
   }
-  part_reserve(lh, a.parts, a.pcnt + a.parts);
+  part_reserve(lh, a.parts, a.pcnt + (size_t)kDsPartReps * a.parts);
 #pragma unroll
   for (int q = 0; q < kPartBatch; q++) {
     if (j1[q] == j0[q] + 1 && c1[q] == c0[q] + 1) {
@@ -1016,14 +1034,29 @@ __global__ void __launch_bounds__(kApplyThreads) k_ds_part_apply(DsPartArgs a) {
     }
     __syncthreads();
     // adds: insert, max-merge the counter (the partition's run, then its overflowed items)
-    const uint32_t na_p = min(a.pcnt[p], a.cap[0]), nk_p = min(a.pcnt[a.parts + p], a.cap[1]);
-    const unsigned long long* ra = a.items + 2ull * ((size_t)p * a.cap[0]);
+    // the partition's kDsPartReps sub-runs of each side, as one index space
+    uint32_t pa_[kDsPartReps + 1], pk_[kDsPartReps + 1];
+    pa_[0] = pk_[0] = 0;
+#pragma unroll
+    for (int r = 0; r < (int)kDsPartReps; r++) {
+      pa_[r + 1] = pa_[r] + min(a.pcnt[(size_t)r * a.parts + p], a.cap[0]);
+      pk_[r + 1] = pk_[r] + min(a.pcnt[(size_t)(kDsPartReps + r) * a.parts + p], a.cap[1]);
+    }
+    const uint32_t na_p = pa_[kDsPartReps], nk_p = pk_[kDsPartReps];
+    const unsigned long long* ra = a.items + 2ull * ((size_t)p * kDsPartReps * a.cap[0]);
+    auto at = [](const uint32_t* pre, uint32_t cap, uint32_t i) {  // item i's slot in the sub-runs
+      uint32_t r = 0;
+#pragma unroll
+      for (int q = 1; q < (int)kDsPartReps; q++) r += i >= pre[q];
+      return r * cap + (i - pre[r]);
+    };
     for (uint32_t i0 = 0; i0 < na_p; i0 += kApplyThreads * kApplyItemBatch) {
       ulonglong2 it[kApplyItemBatch];
 #pragma unroll
       for (int b = 0; b < kApplyItemBatch; b++) {
         const uint32_t i = i0 + tid + b * kApplyThreads;
-        it[b] = i < na_p ? *reinterpret_cast<const ulonglong2*>(ra + 2ull * i) : make_ulonglong2(kDsEmpty, 0);
+        it[b] = i < na_p ? *reinterpret_cast<const ulonglong2*>(ra + 2ull * at(pa_, a.cap[0], i))
+                         : make_ulonglong2(kDsEmpty, 0);
       }
 #pragma unroll
       for (int b = 0; b < kApplyItemBatch; b++) {
@@ -1042,13 +1075,15 @@ __global__ void __launch_bounds__(kApplyThreads) k_ds_part_apply(DsPartArgs a) {
     }
     __syncthreads();
     // removals: thresholds of existing pairs
-    const unsigned long long* rk = a.items + 2ull * ((size_t)a.parts * a.cap[0] + (size_t)p * a.cap[1]);
+    const unsigned long long* rk =
+        a.items + 2ull * ((size_t)a.parts * kDsPartReps * a.cap[0] + (size_t)p * kDsPartReps * a.cap[1]);
     for (uint32_t i0 = 0; i0 < nk_p; i0 += kApplyThreads * kApplyItemBatch) {
       ulonglong2 it[kApplyItemBatch];
 #pragma unroll
       for (int b = 0; b < kApplyItemBatch; b++) {
         const uint32_t i = i0 + tid + b * kApplyThreads;
-        it[b] = i < nk_p ? *reinterpret_cast<const ulonglong2*>(rk + 2ull * i) : make_ulonglong2(kDsEmpty, 0);
+        it[b] = i < nk_p ? *reinterpret_cast<const ulonglong2*>(rk + 2ull * at(pk_, a.cap[1], i))
+                         : make_ulonglong2(kDsEmpty, 0);
       }
 #pragma unroll
       for (int b = 0; b < kApplyItemBatch; b++) {
@@ -1065,10 +1100,8 @@ __global__ void __launch_bounds__(kApplyThreads) k_ds_part_apply(DsPartArgs a) {
     }
     dm += (int)primary_used(a.t, p, a.parts);
     __syncthreads();
-    if (tid == 0) {  // every lane has read the counts (barriers above): the next fold's are zero
-      a.pcnt[p] = 0;
-      a.pcnt[a.parts + p] = 0;
-    }
+    if (tid < 2 * kDsPartReps)  // every lane has read the counts (barriers above): the next fold's are zero
+      a.pcnt[(size_t)tid * a.parts + p] = 0;
     // finalize the touched slots: the current values they need, all loads first
     unsigned long long ad[kApplySlotsPerLane], kl[kApplySlotsPerLane], c[kApplySlotsPerLane];
     bool fresh[kApplySlotsPerLane];
@@ -1750,10 +1783,10 @@ hipError_t launch_ds_applied(hipStream_t s, const uint32_t* keys_sorted, const u
 }
 
 hipError_t launch_ds_contig(hipStream_t s, const uint32_t* actor, uint32_t n, uint32_t* marks, uint32_t n_marks,
-                            uint32_t gen, uint32_t* flag, const uint32_t* miss_src, uint32_t* pub) {
+                            uint32_t gen, uint32_t* flag, const uint32_t* miss_src, uint32_t* pub, DsMono mono) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_ds_contig, dim3(blocks_for(n)), dim3(kBlock), 0, s, actor, n, marks, n_marks, gen, flag,
-                     miss_src, pub);
+                     miss_src, pub, mono);
   return hipGetLastError();
 }
 

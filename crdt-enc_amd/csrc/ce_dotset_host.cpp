@@ -74,6 +74,9 @@ struct DsState {
   DevBuf contig_marks;
   uint32_t contig_cap = 0, contig_gen = 0;
   bool adds_contig = false;  // this batch's adds: every actor's adds one contiguous run
+  bool adds_mono = false;    // ... and each run's counters strictly increase: k_ds_contig wrote the
+                             // applied flags and exclusive maxima (applied, excl) of adds_mono_n adds
+  uint32_t adds_mono_n = 0;
   DevBuf seal_out;           // the compaction's sealed file (ds_compact_device)
   DevBuf tile_col[9];        // the tiled emit's file-minor scratch rows (k_ds_emit<true>)
   // Orswot op files decoded in the open (k_open_fold_v2's DS form): raw counts, done flags and
@@ -588,7 +591,12 @@ int orswot_fold(ce_core* c, const Counts& k, uint64_t kill_bound, bool adds_cont
   // (set after the reserves below: a reserve may move the buffer)
   const uint32_t* clock_keys = nullptr;
   const unsigned long long* clock_ctr = nullptr;
-  if (na && adds_contig) {
+  if (na && adds_contig && d->adds_mono && d->adds_mono_n == na) {
+    // k_ds_contig already wrote the applied flags and exclusive maxima (strictly increasing runs)
+    clock_keys = o.add_actor;
+    clock_ctr = o.add_ctr;
+    c->path_counts["ds_adds_monotone"]++;
+  } else if (na && adds_contig) {
     if ((e = d->excl.reserve(na * 8ull))) return ctx->hip_fail(e, "applied");
     unsigned long long* ex = d->excl.as<unsigned long long>();
     size_t t2 = 0;
@@ -658,11 +666,12 @@ int orswot_fold(ce_core* c, const Counts& k, uint64_t kill_bound, bool adds_cont
   const uint64_t kill_items = kill_bound == ~0ull ? ~0ull : kill_bound + kb0;
   // runs: the expected share of a partition x part_factor / 2, + 64 (C3: ~12 sigma of slack);
   // what passes it goes to the overflow lists (sized for the whole batch)
-  const uint64_t cap_a = pa.parts ? k.v[kCntAddM] / pa.parts * d->part_factor / 2 + 64 : 0,
-                 cap_k = pa.parts && kill_items != ~0ull ? kill_items / pa.parts * d->part_factor / 2 + 64 : 0;
+  const uint64_t sub = (uint64_t)pa.parts * kDsPartReps;  // sub-runs per side
+  const uint64_t cap_a = pa.parts ? k.v[kCntAddM] / sub * d->part_factor / 2 + 32 : 0,
+                 cap_k = pa.parts && kill_items != ~0ull ? kill_items / sub * d->part_factor / 2 + 32 : 0;
   const bool part = !getenv("CE_DS_FOLD_GLOBAL") && pa.parts >= 1 && pa.parts <= kDsPartMaxParts &&
                     kill_items <= 4 * (k.v[kCntRmM] + k.v[kCntRmC] + kb0) + (1ull << 20) &&
-                    k.v[kCntAddM] + kill_items < (1ull << 31) && (uint64_t)pa.parts * (cap_a + cap_k) < (1ull << 31);
+                    k.v[kCntAddM] + kill_items < (1ull << 31) && sub * (cap_a + cap_k) < (1ull << 31);
   if (part) {
     pa.cap[0] = (uint32_t)cap_a;
     pa.cap[1] = (uint32_t)cap_k;
@@ -670,12 +679,12 @@ int orswot_fold(ce_core* c, const Counts& k, uint64_t kill_bound, bool adds_cont
     pa.ovf_cap[1] = (uint32_t)kill_items;
     if ((e = d->part_akey.reserve(8 * k.v[kCntAddM] + 64)) || (e = d->part_hk[0].reserve(8 * k.v[kCntRmM] + 64)) ||
         (e = d->part_hk[1].reserve(8 * m0 + 64)) ||
-        (e = d->part_items.reserve(16ull * pa.parts * (cap_a + cap_k) + 64)) ||
+        (e = d->part_items.reserve(16ull * sub * (cap_a + cap_k) + 64)) ||
         (e = d->part_ovf[0].reserve(16 * k.v[kCntAddM] + 64)) || (e = d->part_ovf[1].reserve(16 * kill_items + 64)))
       return ctx->hip_fail(e, "fold");
     if (d->part_cnt_parts < pa.parts) {  // new (or larger) counters: zeroed once, then by the applies
-      if ((e = d->part_cnt.reserve(8ull * pa.parts + 64)) ||
-          (e = hipMemsetAsync(d->part_cnt.p, 0, 8ull * pa.parts + 64, s)))
+      if ((e = d->part_cnt.reserve(8ull * kDsPartReps * pa.parts + 64)) ||
+          (e = hipMemsetAsync(d->part_cnt.p, 0, 8ull * kDsPartReps * pa.parts + 64, s)))
         return ctx->hip_fail(e, "fold");
       d->part_cnt_parts = pa.parts;
     }
@@ -689,7 +698,7 @@ int orswot_fold(ce_core* c, const Counts& k, uint64_t kill_bound, bool adds_cont
                 d->d0[3].as<unsigned long long>(), d->d0[4].as<unsigned long long>(),
                 d->part_hk[1].as<unsigned long long>(), n0};
     pa.pcnt = d->part_cnt.as<uint32_t>();
-    pa.ovf_n = pa.pcnt + 2ull * d->part_cnt_parts;
+    pa.ovf_n = pa.pcnt + 2ull * kDsPartReps * d->part_cnt_parts;
     pa.items = d->part_items.as<unsigned long long>();
     pa.ovf[0] = d->part_ovf[0].as<unsigned long long>();
     pa.ovf[1] = d->part_ovf[1].as<unsigned long long>();
@@ -1342,21 +1351,34 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
         if ((e = hipMemsetAsync(d->contig_marks.p, 0, 4ull * d->contig_cap, ctx->stream))) return ctx->hip_fail(e, "contig");
         d->contig_gen = 1;
       }
-      // the miss count and the flag come back in pinned h_cnt[62..64), written by the contig launch
-      uint32_t* hp = d->h_cnt.as<uint32_t>() + 62;
-      hp[0] = hp[1] = 0;
+      // the miss count and the flags come back in pinned h_cnt[88..91), written by the contig
+      // launch, which also computes the fold's applied flags when the runs strictly increase
+      uint32_t* hp = d->h_cnt.as<uint32_t>() + 88;
+      hp[0] = hp[1] = hp[2] = 0;
+      DsMono mono{};
+      if (!getenv("CE_DS_SORT_ADDS") && !getenv("CE_DS_NO_MONO")) {
+        if ((e = d->applied.reserve(n_add + 64)) || (e = d->excl.reserve(n_add * 8ull)))
+          return ctx->hip_fail(e, "applied");
+        mono = DsMono{a.ops.add_ctr, d->clock.as<unsigned long long>(), d->clock_cap, d->applied.as<uint8_t>(),
+                      d->excl.as<unsigned long long>()};
+      }
+      const int tc = ctx->tbegin("ds_contig");  // (with mono: the fold's applied flags)
       if ((e = launch_ds_contig(ctx->stream, a.ops.add_actor, n_add, d->contig_marks.as<uint32_t>(), d->contig_cap,
                                 d->contig_gen, a.counters + 3, d->misses.as<uint32_t>() + 2,
-                                static_cast<uint32_t*>(host_dev_ptr(hp)))))
+                                static_cast<uint32_t*>(host_dev_ptr(hp)), mono)))
         return ctx->hip_fail(e, "contig");
+      ctx->tend(tc);
       if ((e = stream_wait(ctx->stream))) return ctx->hip_fail(e, "emit");
       hm[2] = hp[0];
       hm[3] = hp[1];
+      d->adds_mono = mono.ctr && hp[2] == 0;
+      d->adds_mono_n = n_add;
     } else if ((e = hipMemcpyAsync(hm, d->misses.p, 16, hipMemcpyDeviceToHost, ctx->stream)) ||
                (e = stream_wait(ctx->stream))) {
       return ctx->hip_fail(e, "emit");
     }
     d->adds_contig = check && hm[3] == 0 && !getenv("CE_DS_SORT_ADDS");
+    if (!check) d->adds_mono = false;
     if (hm[2] == 0) break;
     if (round > 64) return ctx->fail(CE_ERR_DEVICE, "actor table did not converge");
     const uint32_t nm = std::min<uint32_t>(hm[2], kMissCap);

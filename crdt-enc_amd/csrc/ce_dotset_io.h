@@ -57,8 +57,10 @@ struct OrswotSerScratch {
 // the serializer's LSD radix sort (ce_ser_sort.hip): pairs (member_in, actor_in, value_in) in
 // collect order -> member_out / actor_out / value_out ordered by key = member << rank_bits | rank
 // (key_bits <= 64).  State (u32 words, zero before the first sort; the sorts keep it so):
-// hist [2][kSortMaxPlaces][256] | ticket [kSortMaxPlaces] | look [places][tiles][256]
+// hist [2][8 replicas][kSortMaxPlaces][256] | ticket [kSortMaxPlaces] | pad, then from word
+// kSortStateHead: look [places][tiles][256]
 static constexpr uint32_t kSortMaxPlaces = 8;
+static constexpr uint32_t kSortStateHead = 2 * 8 * kSortMaxPlaces * 256 + 64;
 struct SerSortArgs {
   const unsigned long long* member_in;
   const uint32_t* actor_in;
@@ -78,7 +80,7 @@ struct SerSortArgs {
 };
 uint32_t ser_sort_tiles(uint32_t n);
 inline size_t ser_sort_state_words(uint32_t n) {
-  return 2ull * kSortMaxPlaces * 256 + kSortMaxPlaces + (size_t)kSortMaxPlaces * ser_sort_tiles(n) * 256;
+  return kSortStateHead + (size_t)kSortMaxPlaces * ser_sort_tiles(n) * 256;
 }
 // kbuf: two key buffers of n (u32 when key_bits <= 32, else u64), vbuf: two u64 buffers of n
 hipError_t launch_ser_sort(hipStream_t s, const SerSortArgs& a, void* const kbuf[2], unsigned long long* const vbuf[2]);

@@ -715,8 +715,8 @@ hipError_t launch_orswot_ser_sort(hipStream_t s, OrswotSerScratch& sc, uint32_t 
     a.n = n;
     a.par = (*sc.sort_gen)++ & 1u;
     a.hist = sc.sort_state;
-    a.ticket = a.hist + 2 * kSortMaxPlaces * 256;
-    a.look = a.ticket + kSortMaxPlaces;
+    a.ticket = a.hist + 2 * 8 * kSortMaxPlaces * 256;
+    a.look = a.hist + kSortStateHead;
     a.member_out = sc.member_sorted;
     a.actor_out = sc.actor_sorted;
     a.value_out = sc.value_sorted;

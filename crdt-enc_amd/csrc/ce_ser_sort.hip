@@ -31,6 +31,12 @@ constexpr int kDigitBits = 8;
 constexpr uint32_t kDigits = 1u << kDigitBits;
 constexpr uint32_t kFlagAgg = 1u << 30, kFlagInc = 2u << 30, kCountMask = (1u << 30) - 1;
 static_assert(kDigits == kSortThreads, "one lane per digit in the tile bookkeeping");
+constexpr int kLookWindow = 16;
+// the histogram in kHistReps replicas (block b adds into replica b % kHistReps, ~ its XCD): a
+// digit's count is then ~tiles / 8 same-address adds per replica (~60 ns each across XCDs: one
+// copy took ~24 us at C3's 406 tiles); the passes sum the replicas
+constexpr uint32_t kHistReps = 8;
+static_assert(kHistReps * kSortMaxPlaces * kDigits * 2 + kSortMaxPlaces <= kSortStateHead, "state layout");
 
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -76,21 +82,17 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_hist(SerSortArgs a) {
   for (uint32_t i = blockIdx.x * kSortThreads + t; i < nz; i += gridDim.x * kSortThreads) a.look[i] = 0;
   if (blockIdx.x == 0) {
     if (t < kSortMaxPlaces) a.ticket[t] = 0;
-    for (uint32_t i = t; i < kSortMaxPlaces * kDigits; i += kSortThreads)
-      a.hist[(size_t)(a.par ^ 1) * kSortMaxPlaces * kDigits + i] = 0;
+    for (uint32_t i = t; i < kHistReps * kSortMaxPlaces * kDigits; i += kSortThreads)
+      a.hist[(size_t)(a.par ^ 1) * kHistReps * kSortMaxPlaces * kDigits + i] = 0;
   }
   for (uint32_t p = 0; p < a.places; p++) lh[p][t] = 0;
   __syncthreads();
-  const uint32_t i0 = blockIdx.x * kSortTile;
-#pragma unroll 4
-  for (int k = 0; k < kSortPerLane; k++) {
-    const uint32_t i = i0 + k * kSortThreads + t;
-    if (i >= a.n) break;
+  for (uint32_t i = blockIdx.x * kSortTile + t; i < min(a.n, (blockIdx.x + 1) * kSortTile); i += kSortThreads) {
     const K key = pair_key<K>(a, i);
     for (uint32_t p = 0; p < a.places; p++) atomicAdd(&lh[p][(uint32_t)(key >> (p * kDigitBits)) & (kDigits - 1)], 1u);
   }
   __syncthreads();
-  uint32_t* h = a.hist + (size_t)a.par * kSortMaxPlaces * kDigits;
+  uint32_t* h = a.hist + ((size_t)a.par * kHistReps + blockIdx.x % kHistReps) * kSortMaxPlaces * kDigits;
   for (uint32_t p = 0; p < a.places; p++)
     if (lh[p][t]) atomicAdd(h + p * kDigits + t, lh[p][t]);
 }
@@ -159,21 +161,34 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_pass(SerSortArgs a, uint3
     st_agent(look + t, tot | kFlagInc);
   } else {
     st_agent(look + (size_t)tile * kDigits + t, tot | kFlagAgg);
+    // kLookWindow predecessors' words per round, their loads in flight together (a cross-XCD
+    // load is ~1 us: one at a time, a walk over a few dozen aggregates cost tens of us)
     for (int32_t j = (int32_t)tile - 1; j >= 0;) {
-      const uint32_t v = ld_agent(look + (size_t)j * kDigits + t);
-      if (v == 0) {
-        __builtin_amdgcn_s_sleep(1);
-        continue;
+      uint32_t v[kLookWindow];
+#pragma unroll
+      for (int q = 0; q < kLookWindow; q++) v[q] = j - q >= 0 ? ld_agent(look + (size_t)(j - q) * kDigits + t) : kFlagInc;
+      int q = 0;
+      bool found = false;
+      for (; q < kLookWindow; q++) {
+        if (v[q] == 0) break;  // not published yet: poll again from there
+        prefix += v[q] & kCountMask;
+        if (v[q] & kFlagInc) {
+          found = true;
+          break;
+        }
       }
-      prefix += v & kCountMask;
-      if (v & kFlagInc) break;
-      j--;
+      if (found) break;
+      j -= q;
+      if (q < kLookWindow) __builtin_amdgcn_s_sleep(1);
     }
     st_agent(look + (size_t)tile * kDigits + t, (prefix + tot) | kFlagInc);
   }
-  const uint32_t* h = a.hist + (size_t)a.par * kSortMaxPlaces * kDigits + place * kDigits;
+  const uint32_t* h = a.hist + (size_t)a.par * kHistReps * kSortMaxPlaces * kDigits + place * kDigits;
+  uint32_t hv = 0;
+#pragma unroll
+  for (uint32_t r = 0; r < kHistReps; r++) hv += h[(size_t)r * kSortMaxPlaces * kDigits + t];
   uint32_t all;
-  const uint32_t hx = block_excl_scan(h[t], wsum, &all);
+  const uint32_t hx = block_excl_scan(hv, wsum, &all);
   gofs[t] = hx + prefix;
   const uint32_t ts = block_excl_scan(tot, wsum, &all);
   tstart[t] = ts;

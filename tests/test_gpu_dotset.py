@@ -751,19 +751,45 @@ def test_orswot_adds_without_sort(ctx, adversarial):
     oc = C.Core("orswot")
     assert oc.read_remote_ops(key, [APP], sealed, [acts[i] for i in fa], fv)[0] == 0
     got = {}
-    for forced in (False, True):
-        if forced:
-            os.environ["CE_DS_SORT_ADDS"] = "1"
+    for mode in (None, "CE_DS_NO_MONO", "CE_DS_SORT_ADDS"):
+        if mode:
+            os.environ[mode] = "1"
         try:
             core = new_core(ctx, "orswot", key)
             assert core.ingest_ops(sealed, acts, fa, fv)[0] == 0
-            got[forced] = (core.state_bytes(), core.path_count("ds_adds_contiguous"))
+            got[mode] = (core.state_bytes(), core.path_count("ds_adds_contiguous"), core.path_count("ds_adds_monotone"))
             core.close()
         finally:
-            os.environ.pop("CE_DS_SORT_ADDS", None)
-    assert got[False][0] == got[True][0] == oc.serialize()
-    assert got[True][1] == 0
-    assert got[False][1] == (0 if adversarial else 1)
+            if mode:
+                os.environ.pop(mode, None)
+    assert got[None][0] == got["CE_DS_NO_MONO"][0] == got["CE_DS_SORT_ADDS"][0] == oc.serialize()
+    assert got["CE_DS_SORT_ADDS"][1:] == (0, 0)
+    # well-formed: contiguous, strictly increasing runs -> the applied flags from k_ds_contig
+    assert got[None][1:] == ((0, 0) if adversarial else (0, 1))
+    assert got["CE_DS_NO_MONO"][1:] == ((0, 0) if adversarial else (1, 0))
+
+
+def test_orswot_adds_contiguous_not_increasing(ctx):
+    """A writer's adds contiguous (its own dots) but their counters not strictly increasing: a
+    repeated and a lower counter inside the run.  k_ds_contig flags the run, the fold takes the
+    segmented max scan (ds_adds_contiguous, not ds_adds_monotone), and the state == the oracle's
+    (the lower / repeated counters do not apply)."""
+    rng = random.Random(5151)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 3)
+    files = {actors[0]: [[("Add", (actors[0], 5), [1]), ("Add", (actors[0], 3), [2]), ("Add", (actors[0], 5), [3]),
+                          ("Add", (actors[0], 9), [4])]],
+             actors[1]: [[("Add", (actors[1], 2), [1]), ("Add", (actors[1], 4), [5])]],
+             actors[2]: [[("Add", (actors[2], 7), [6]), ("Add", (actors[2], 7), [7])]]}
+    acts, clears, fa, fv = G.batch(files, "orswot", APP)
+    sealed = seal_files(ctx, key, clears)
+    oc = C.Core("orswot")
+    assert oc.read_remote_ops(key, [APP], sealed, [acts[i] for i in fa], fv)[0] == 0
+    core = new_core(ctx, "orswot", key)
+    assert core.ingest_ops(sealed, acts, fa, fv)[0] == 0
+    assert core.state_bytes() == oc.serialize()
+    assert core.path_count("ds_adds_contiguous") == 1 and core.path_count("ds_adds_monotone") == 0
+    core.close()
 
 
 def test_compact_into_async_overlaps_next_ingest(ctx):
@@ -1010,7 +1036,8 @@ def test_local_apply_after_contiguous_ingest(ctx):
     core, oc = new_core(ctx, "orswot", key), C.Core("orswot")
     assert core.ingest_ops(sealed, acts, fa, fv)[0] == 0
     assert oc.read_remote_ops(key, [APP], sealed, [acts[i] for i in fa], fv)[0] == 0
-    assert core.path_count("ds_adds_contiguous") == 1
+    # (contiguous, strictly increasing runs: the applied flags come from k_ds_contig)
+    assert core.path_count("ds_adds_monotone") == 1 and core.path_count("ds_adds_contiguous") == 0
     me = core.info_actor()
     a, b = acts[0], acts[1]
     ca, cb = oc.state.clock.get(a), oc.state.clock.get(b)
@@ -1023,7 +1050,8 @@ def test_local_apply_after_contiguous_ingest(ctx):
             oc.state.apply(op)
         oc.nov.apply(me, oc.nov.get(me) + 1)
         assert core.state_bytes() == oc.serialize(), rnd
-    assert core.path_count("ds_adds_contiguous") == 1   # the local applies took the sort
+    # the local applies took the sort
+    assert core.path_count("ds_adds_monotone") == 1 and core.path_count("ds_adds_contiguous") == 0
     core.close()
 
 
