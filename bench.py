@@ -844,7 +844,7 @@ def main():
 def rocprof_frac(sa, n):
     """the same fraction with the committed rocprofv3 averages of the two kernels (the verdict's
     recomputation uses these), None without this round's profile"""
-    f = rocprof_avg_ms("ce::k_open_fold_v2<16, 2, false, 1, true>")
+    f = rocprof_avg_ms("ce::k_open_fold_v2<16, 2, false, 1, true, false>")
     s = rocprof_avg_ms("ce::k_open_setup")
     if not f or not s:
         return None
