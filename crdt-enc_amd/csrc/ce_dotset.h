@@ -159,6 +159,8 @@ hipError_t launch_ds_finalize(hipStream_t s, DsTables t);
 // live[0] += change of the live-pair count (two's complement), live[1] += pairs inserted, live[5]
 // = items that overflowed; K1 zeroes live[0], live[1], live[3] and live[4].
 static constexpr uint32_t kDsPartChunk = 8192;      // adds / removals per K1 block (one trip)
+static constexpr uint32_t kDsPartThreadsSmall = 512;  // the half-size K1 blocks (CE_DS_PART_SMALL)
+static constexpr uint32_t kDsPartChunkSmall = 4096;
 static constexpr uint32_t kDsPartReps = 8;          // sub-runs per partition and side (K1 block % 8)
 static constexpr uint32_t kDsPartMaxParts = 16384;  // LDS histogram bound (64 KB)
 struct DsKillSrc {

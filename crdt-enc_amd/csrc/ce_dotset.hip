@@ -782,7 +782,7 @@ __global__ void __launch_bounds__(kBlock) k_ds_finalize(DsTables t) {
 // add slot's atomic) plus two full passes over the 4M-slot table (finalize); here the items are
 // bucketed by partition first (two streaming passes), then each partition's 2048 keys and the
 // counters / thresholds of its items meet in LDS, and only changed slots go back to HBM.
-constexpr int kPartThreads = 1024;     // K1 / K3
+constexpr int kPartThreads = 1024;     // K1 (the 512-thread form: kDsPartThreadsSmall)
 constexpr int kApplyThreads = 512;     // K4
 
 // member handle of m when its first probe holds it (g = mkey[that bucket], read ahead of time
@@ -795,15 +795,17 @@ __device__ __forceinline__ unsigned long long member_handle(const DsTables& t, u
 
 constexpr int kPartBatch = 8;  // items per lane whose loads are issued before any is used
 static_assert(kDsPartChunk == kPartThreads * kPartBatch, "K1 walks its chunk in one trip");
+static_assert(kDsPartChunkSmall == kDsPartThreadsSmall * kPartBatch, "K1 walks its chunk in one trip");
 
 // K1 after its count: lh[p] (this block's items of partition p) -> the base of its reservation in
 // p's run, one returning add per partition with items (64 contiguous counters per wave instruction)
 // (block b reserves in sub-run b % kDsPartReps of every partition: a counter then takes
 // ~blocks / 8 same-address adds -- one counter per partition took ~200, ~60 ns each across XCDs)
+template <int T>
 __device__ __forceinline__ void part_reserve(uint32_t* lh, uint32_t parts, uint32_t* pcnt) {
   __syncthreads();
   uint32_t* c = pcnt + (size_t)(blockIdx.x % kDsPartReps) * parts;
-  for (uint32_t p = threadIdx.x; p < parts; p += kPartThreads) {
+  for (uint32_t p = threadIdx.x; p < parts; p += T) {
     const uint32_t n = lh[p];
     if (n) lh[p] = atomicAdd(c + p, n);
   }
@@ -830,9 +832,10 @@ __device__ __forceinline__ void part_put(const DsPartArgs& a, int side, uint32_t
   *reinterpret_cast<ulonglong2*>(dst) = make_ulonglong2(key, v);
 }
 
-__global__ void __launch_bounds__(kPartThreads) k_ds_part_adds(DsPartArgs a) {
+template <int T>
+__global__ void __launch_bounds__(T) k_ds_part_adds(DsPartArgs a) {
   extern __shared__ uint32_t lh[];  // [parts]: counts, then the block's cursors in every run
-  for (uint32_t p = threadIdx.x; p < a.parts; p += kPartThreads) lh[p] = 0;
+  for (uint32_t p = threadIdx.x; p < a.parts; p += T) lh[p] = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     a.t.live[0] = 0;
     a.t.live[1] = 0;
@@ -847,7 +850,7 @@ __global__ void __launch_bounds__(kPartThreads) k_ds_part_adds(DsPartArgs a) {
   unsigned long long m[kPartBatch], g[kPartBatch], c[kPartBatch], key[kPartBatch];
 #pragma unroll
   for (int q = 0; q < kPartBatch; q++) {
-    const uint32_t k = blockIdx.x * a.chunk + threadIdx.x + q * kPartThreads;
+    const uint32_t k = blockIdx.x * a.chunk + threadIdx.x + q * T;
     j0[q] = j1[q] = 0;
     m[q] = g[q] = c[q] = 0;
     if (k < k1 && a.applied[k]) {
@@ -879,7 +882,7 @@ __global__ void __launch_bounds__(kPartThreads) k_ds_part_adds(DsPartArgs a) {
       }
     }
   }
-  part_reserve(lh, a.parts, a.pcnt);
+  part_reserve<T>(lh, a.parts, a.pcnt);
 #pragma unroll
   for (int q = 0; q < kPartBatch; q++) {
     if (j1[q] == j0[q] + 1) {
@@ -900,9 +903,10 @@ __global__ void __launch_bounds__(kPartThreads) k_ds_part_adds(DsPartArgs a) {
 // removal r kills (m, a_e) for every member m and clock entry e (k_ds_kill); a member absent after
 // the adds has no pair to kill.  A removal with one member and one clock entry (one item) keeps it
 // in registers; others leave their member handles in hk for the write below.
-__global__ void __launch_bounds__(kPartThreads) k_ds_part_kills(DsPartArgs a) {
+template <int T>
+__global__ void __launch_bounds__(T) k_ds_part_kills(DsPartArgs a) {
   extern __shared__ uint32_t lh[];
-  for (uint32_t p = threadIdx.x; p < a.parts; p += kPartThreads) lh[p] = 0;
+  for (uint32_t p = threadIdx.x; p < a.parts; p += T) lh[p] = 0;
   __syncthreads();
   const uint32_t b = blockIdx.x;
   const DsKillSrc& x = a.ks[b < a.bk0 ? 0 : 1];
@@ -913,7 +917,7 @@ __global__ void __launch_bounds__(kPartThreads) k_ds_part_kills(DsPartArgs a) {
   uint32_t ca[kPartBatch];
 #pragma unroll
   for (int q = 0; q < kPartBatch; q++) {
-    const uint32_t r = r0 + threadIdx.x + q * kPartThreads;
+    const uint32_t r = r0 + threadIdx.x + q * T;
     c0[q] = c1[q] = j0[q] = j1[q] = 0;
     m[q] = g[q] = v[q] = 0;
     ca[q] = 0;
@@ -950,7 +954,7 @@ __global__ void __launch_bounds__(kPartThreads) k_ds_part_kills(DsPartArgs a) {
       }
     }
   }
-  part_reserve(lh, a.parts, a.pcnt + (size_t)kDsPartReps * a.parts);
+  part_reserve<T>(lh, a.parts, a.pcnt + (size_t)kDsPartReps * a.parts);
 #pragma unroll
   for (int q = 0; q < kPartBatch; q++) {
     if (j1[q] == j0[q] + 1 && c1[q] == c0[q] + 1) {
@@ -1835,8 +1839,13 @@ hipError_t launch_ds_count_members(hipStream_t s, DsTables t, uint32_t* out) {
 
 hipError_t launch_ds_part_count(hipStream_t s, const DsPartArgs& a) {
   const size_t lds = (size_t)a.parts * 4;
-  hipLaunchKernelGGL(k_ds_part_adds, dim3(a.ba ? a.ba : 1), dim3(kPartThreads), lds, s, a);
-  if (a.bk) hipLaunchKernelGGL(k_ds_part_kills, dim3(a.bk), dim3(kPartThreads), lds, s, a);
+  if (a.chunk == kDsPartChunkSmall) {
+    hipLaunchKernelGGL(k_ds_part_adds<kDsPartThreadsSmall>, dim3(a.ba ? a.ba : 1), dim3(kDsPartThreadsSmall), lds, s, a);
+    if (a.bk) hipLaunchKernelGGL(k_ds_part_kills<kDsPartThreadsSmall>, dim3(a.bk), dim3(kDsPartThreadsSmall), lds, s, a);
+  } else {
+    hipLaunchKernelGGL(k_ds_part_adds<kPartThreads>, dim3(a.ba ? a.ba : 1), dim3(kPartThreads), lds, s, a);
+    if (a.bk) hipLaunchKernelGGL(k_ds_part_kills<kPartThreads>, dim3(a.bk), dim3(kPartThreads), lds, s, a);
+  }
   return hipGetLastError();
 }
 

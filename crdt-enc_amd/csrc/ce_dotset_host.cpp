@@ -658,8 +658,9 @@ int orswot_fold(ce_core* c, const Counts& k, uint64_t kill_bound, bool adds_cont
   uint32_t* live = d->live.as<uint32_t>();
   DsPartArgs pa{};
   pa.parts = d->pcap >> kDsPartBits;
-  pa.chunk = kDsPartChunk;
-  pa.kchunk = kDsPartChunk / 4;  // removals are ~1/4 of C3's ops: as many blocks
+  static const bool small_k1 = getenv("CE_DS_PART_SMALL") && atoi(getenv("CE_DS_PART_SMALL")) != 0;
+  pa.chunk = small_k1 ? kDsPartChunkSmall : kDsPartChunk;
+  pa.kchunk = pa.chunk / 4;  // removals are ~1/4 of C3's ops: as many blocks
   pa.ba = (uint32_t)((na + pa.chunk - 1) / pa.chunk);
   pa.bk0 = (uint32_t)((nr + pa.kchunk - 1) / pa.kchunk);
   pa.bk = pa.bk0 + (uint32_t)((n0 + pa.kchunk - 1) / pa.kchunk);

@@ -252,8 +252,9 @@ def gather_dotset_columns(core, group=None, device="cpu", dst=0, buf=None, timin
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     if buf is None:
         buf = StateBuffer(torch.device("cuda", core.ctx.device))
+    t0 = time.perf_counter()
+    n = 0
     if rank != dst:
-        t0 = time.perf_counter()
         t = buf.ensure(1 << 20)
         rc, n = core.export_columns_device(t.data_ptr(), t.numel())
         if rc == _ERR_INVALID_ARG and n > t.numel():
@@ -261,45 +262,51 @@ def gather_dotset_columns(core, group=None, device="cpu", dst=0, buf=None, timin
             rc, n = core.export_columns_device(t.data_ptr(), t.numel())
         if rc:
             raise RuntimeError("export_columns_device failed: %d" % rc)
-        t1 = time.perf_counter()
+    t1 = time.perf_counter()
+    # every partial's length in one all_gather, then every transfer posted at once: each peer's
+    # partial comes over its own xGMI link instead of one after another
+    got = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(world)]
+    dist.all_gather(got, torch.tensor([n], dtype=torch.int64, device=device), group=group)
+    lens_all = [int(x.item()) for x in got]
+    if rank != dst:
         peer = _global(group, dst)
-        dist.send(torch.tensor([n], dtype=torch.int64, device=device), peer, group=group)
-        dist.send(t[:n] if _on_comm_device(t, device) else t[:n].to(device), peer, group=group)
+        src = t[:n] if _on_comm_device(t, device) else t[:n].to(device)
+        dist.isend(src, peer, group=group).wait()
         torch.cuda.current_stream(t.device).synchronize()  # the next export rewrites the buffer
         if timing is not None:
             timing.append({"send": True, "bytes": n, "export_ms": round((t1 - t0) * 1e3, 3),
                            "send_ms": round((time.perf_counter() - t1) * 1e3, 3)})
         return 0
-    t0 = time.perf_counter()
     parts = getattr(buf, "parts", None)
     if parts is None:
         parts = buf.parts = {}
-    ptrs, lens = [], []
+    ptrs, lens, reqs, staged = [], [], [], []
     for r in range(world):
         if r == dst:
             continue
-        peer = _global(group, r)
-        hdr = torch.zeros(1, dtype=torch.int64, device=device)
-        dist.recv(hdr, peer, group=group)
-        n = int(hdr.item())
+        n = lens_all[r]
         pb = parts.setdefault(r, StateBuffer(buf.device))
         t = pb.ensure(n)
         if _on_comm_device(t, device):
-            dist.recv(t[:n], peer, group=group)
+            reqs.append(dist.irecv(t[:n], _global(group, r), group=group))
         else:
             h = torch.empty(n, dtype=torch.uint8, device=device)
-            dist.recv(h, peer, group=group)
-            t[:n].copy_(h)
+            reqs.append(dist.irecv(h, _global(group, r), group=group))
+            staged.append((t, h, n))
         ptrs.append(t.data_ptr())
         lens.append(n)
+    for q in reqs:
+        q.wait()
+    for t, h, n in staged:
+        t[:n].copy_(h)
     torch.cuda.current_stream(buf.device).synchronize()  # the receives land on torch's stream
-    t1 = time.perf_counter()
+    t2 = time.perf_counter()
     rc = core.merge_columns_device(ptrs, lens)
     if rc:
         raise RuntimeError("merge_columns_device failed: %d" % rc)
     if timing is not None:
-        timing.append({"recv": True, "parts": len(lens), "bytes": sum(lens), "recv_ms": round((t1 - t0) * 1e3, 3),
-                       "merge_ms": round((time.perf_counter() - t1) * 1e3, 3)})
+        timing.append({"recv": True, "parts": len(lens), "bytes": sum(lens), "recv_ms": round((t2 - t1) * 1e3, 3),
+                       "merge_ms": round((time.perf_counter() - t2) * 1e3, 3)})
     return 1
 
 
