@@ -221,10 +221,11 @@ struct DsMergeSrc {
   uint32_t* slot;  // optional, n words: k_ds_kput records each pair's slot for k_ds_khold
 };
 // Orswot::merge of nf state files at once (no deferred removals on any side): d_src / h_src the
-// same descriptors in HBM and on the host, oclocks = the files' dense clocks at stride ccap,
+// same descriptors in HBM and on the host, oclocks = the files' dense clocks actor-major
+// (oclocks[a * ostride + f], ostride = ds_oclock_stride(nf), the padding zero),
 // hold = a zeroed u64 per pair slot (left zeroed); live[0..1] = live / used pairs after
 hipError_t launch_ds_kmerge(hipStream_t s, DsTables t, const DsMergeSrc* d_src, const DsMergeSrc* h_src, uint32_t nf,
-                            unsigned long long* clock, const unsigned long long* oclocks, uint32_t ccap,
+                            unsigned long long* clock, const unsigned long long* oclocks, uint32_t ccap, uint32_t ostride,
                             unsigned long long* hold, uint32_t* pub_dst = nullptr);  // pub_dst: live[0..5) -> pinned
 // one column partial of the multi-GPU exchange (ds_merge_columns_device): its actor column and
 // clock remapped to the receiving core's ids
@@ -233,9 +234,11 @@ struct DsColsRemap {
   uint32_t* ids;                  // np receiver ids (out)
   const uint32_t* map;            // na: partial-local index -> receiver id (device)
   const unsigned long long* clock;  // na: the partial's clock by its indices
-  unsigned long long* oclock;     // ccap: dense by receiver id (zeroed; out)
-  uint32_t np, na;
+  unsigned long long* oclock;     // dense by receiver id at stride ostride (zeroed; out)
+  uint32_t np, na, ostride;
 };
+// the actor-major stride of nf files' dense clocks (launch_ds_kmerge): a multiple of 8, >= nf
+inline uint32_t ds_oclock_stride(uint32_t nf) { return nf <= 8 ? 8u : (nf + 7u) & ~7u; }
 static constexpr uint32_t kColsInline = 16;
 struct DsColsRemaps {
   DsColsRemap f[kColsInline];

@@ -1328,8 +1328,11 @@ __global__ void __launch_bounds__(kBlock) k_ds_khold(DsTables t, DsMergeSrcs src
   }
 }
 
+// oclocks: the files' dense clocks actor-major, oclocks[a * ostride + f] (ostride a multiple of 8
+// >= nf, the padding zero): a slot's first eight files' clocks are one 64-byte line, four 16-byte
+// loads (file-major, eight gathers from lines 32 KiB apart took ~70 us at C3's 8 state files)
 __global__ void __launch_bounds__(kBlock) k_ds_kfinal(DsTables t, const unsigned long long* clock,
-                                                      const unsigned long long* oclocks, uint32_t ccap,
+                                                      const unsigned long long* oclocks, uint32_t ostride,
                                                       uint32_t nf, unsigned long long* hold) {
   const uint32_t cap = t.pmask + 1;
   uint32_t n_used = 0, n_live = 0, n_mem = primary_used(t, blockIdx.x, gridDim.x);
@@ -1357,9 +1360,16 @@ __global__ void __launch_bounds__(kBlock) k_ds_kfinal(DsTables t, const unsigned
     for (int q = 0; q < kKQ; q++) {
       const uint32_t a = (uint32_t)(key[q] & ((1u << kDsActorBits) - 1));
       ck[q] = key[q] != kDsEmpty ? clock[a] : 0ull;
+      const uint4* op = reinterpret_cast<const uint4*>(oclocks + (size_t)a * ostride);
+#pragma unroll
+      for (int i = 0; i < kKF / 2; i++) {
+        const uint4 w = key[q] != kDsEmpty && (uint32_t)(2 * i) < nf ? op[i] : make_uint4(0, 0, 0, 0);
+        oc[q][2 * i] = ((unsigned long long)w.y << 32) | w.x;
+        oc[q][2 * i + 1] = ((unsigned long long)w.w << 32) | w.z;
+      }
 #pragma unroll
       for (int f = 0; f < kKF; f++)
-        oc[q][f] = key[q] != kDsEmpty && (uint32_t)f < nf && !((hm[q] >> f) & 1ull) ? oclocks[(size_t)f * ccap + a] : 0ull;
+        if ((hm[q] >> f) & 1ull) oc[q][f] = 0ull;  // a holder does not kill (m > 0)
     }
 #pragma unroll
     for (int q = 0; q < kKQ; q++) {
@@ -1372,7 +1382,7 @@ __global__ void __launch_bounds__(kBlock) k_ds_kfinal(DsTables t, const unsigned
 #pragma unroll
       for (int f = 0; f < kKF; f++) keep = keep && m > oc[q][f];  // (0 for a holder: m > 0)
       for (uint32_t f = kKF; f < nf && keep; f++)
-        if (!((hm[q] >> f) & 1ull)) keep = m > oclocks[(size_t)f * ccap + a];
+        if (!((hm[q] >> f) & 1ull)) keep = m > oclocks[(size_t)a * ostride + f];
       const unsigned long long v = keep ? m : 0ull;
       if (v != s[q]) t.cur[b] = v;
       if (o[q]) t.oth[b] = 0;
@@ -1408,13 +1418,14 @@ __global__ void __launch_bounds__(kBlock) k_ds_kfinal(DsTables t, const unsigned
 
 // clock = max(clock, every file's clock)
 // (pub_dst: the k-way merge's live counters, final since k_ds_kfinal, into the caller's pinned memory)
-__global__ void k_ds_kclock(unsigned long long* clock, const unsigned long long* oclocks, uint32_t ccap, uint32_t nf,
-                            const uint32_t* pub_src, uint32_t* pub_dst, uint32_t pub_words) {
+__global__ void k_ds_kclock(unsigned long long* clock, const unsigned long long* oclocks, uint32_t ccap,
+                            uint32_t ostride, uint32_t nf, const uint32_t* pub_src, uint32_t* pub_dst,
+                            uint32_t pub_words) {
   if (pub_dst && blockIdx.x == 0 && threadIdx.x < pub_words) pub_dst[threadIdx.x] = pub_src[threadIdx.x];
   for (uint32_t a = blockIdx.x * kBlock + threadIdx.x; a < ccap; a += gridDim.x * kBlock) {
     unsigned long long v = clock[a];
     for (uint32_t f = 0; f < nf; f++) {
-      const unsigned long long w = oclocks[(size_t)f * ccap + a];
+      const unsigned long long w = oclocks[(size_t)a * ostride + f];
       v = w > v ? w : v;
     }
     clock[a] = v;
@@ -1886,7 +1897,7 @@ hipError_t launch_ds_merge_finalize(hipStream_t s, DsTables t, const unsigned lo
 }
 
 hipError_t launch_ds_kmerge(hipStream_t s, DsTables t, const DsMergeSrc* d_src, const DsMergeSrc* h_src, uint32_t nf,
-                            unsigned long long* clock, const unsigned long long* oclocks, uint32_t ccap,
+                            unsigned long long* clock, const unsigned long long* oclocks, uint32_t ccap, uint32_t ostride,
                             unsigned long long* hold, uint32_t* pub_dst) {
   (void)d_src;
   uint32_t nmax = 0;
@@ -1903,9 +1914,9 @@ hipError_t launch_ds_kmerge(hipStream_t s, DsTables t, const DsMergeSrc* d_src, 
   for (uint32_t c0 = 0; c0 < nf; c0 += kMergeInline)
     hipLaunchKernelGGL(k_ds_khold, dim3(gx, std::min(kMergeInline, nf - c0)), dim3(kBlock), 0, s, t, srcs(c0), hold);
   hipLaunchKernelGGL(k_ds_kfinal, dim3(blocks_for((uint64_t)t.pmask + 1, 1024)), dim3(kBlock), 0, s, t, clock, oclocks,
-                     ccap, nf, hold);
+                     ostride, nf, hold);
   hipLaunchKernelGGL(k_ds_kclock, dim3(std::max<uint32_t>(1, blocks_for(ccap))), dim3(kBlock), 0, s, clock, oclocks,
-                     ccap, nf, t.live, pub_dst, 5u);
+                     ccap, ostride, nf, t.live, pub_dst, 5u);
   return hipGetLastError();
 }
 
@@ -1915,7 +1926,8 @@ hipError_t launch_ds_kmerge(hipStream_t s, DsTables t, const DsMergeSrc* d_src, 
 __global__ void __launch_bounds__(kBlock) k_cols_remap(DsColsRemaps r) {
   const DsColsRemap x = r.f[blockIdx.y];
   for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < x.np; j += gridDim.x * kBlock) x.ids[j] = x.map[x.actor[j]];
-  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < x.na; i += gridDim.x * kBlock) x.oclock[x.map[i]] = x.clock[i];
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < x.na; i += gridDim.x * kBlock)
+    x.oclock[(size_t)x.map[i] * x.ostride] = x.clock[i];
 }
 
 hipError_t launch_cols_remap(hipStream_t s, const DsColsRemap* parts, uint32_t k) {

@@ -2057,24 +2057,33 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     if (ds[i].device) dev_dots += ds[i].n_dots;
   if ((rc = ensure_pairs(c, dev_dots))) return rc;
   uint32_t* live = small + 6 * n;
-  // dense other-clocks in pinned memory, so the queued merges never wait on a pageable copy
-  const uint32_t ccap = d->clock_cap;
-  if ((e = d->rd_clock.reserve(8ull * ccap * n + 64))) return ctx->hip_fail(e, "merge");
-  auto* hclk = d->rd_clock.as<unsigned long long>();
-  for (size_t i = 0; i < n; i++)
-    if (ds[i].device) {
-      std::memset(hclk + (size_t)ccap * i, 0, 8ull * ccap);
-      for (auto& y : ds[i].oclock) hclk[(size_t)ccap * i + y.first] = y.second;
-    }
-  // every file's dense other-clock in HBM with one copy
-  if ((e = d->rd_oclocks.reserve(8ull * ccap * n + 64)) ||
-      (e = hipMemcpyAsync(d->rd_oclocks.p, hclk, 8ull * ccap * n, hipMemcpyHostToDevice, s)))
-    return ctx->hip_fail(e, "merge");
   // every file read on the device and no deferred removal anywhere: all merges in one pass
   // (launch_ds_kmerge; the order-free form of the merges below)
-  bool kway = n >= 2 && n <= 64 && d->deferred.empty();
+  bool kway = n >= 2 && n <= 64 && d->deferred.empty() && !getenv("CE_NO_KMERGE");
   for (size_t i = 0; i < n && kway; i++) kway = ds[i].device && ds[i].od.empty();
-  if (kway && !getenv("CE_NO_KMERGE")) {
+  // dense other-clocks in pinned memory, so the queued merges never wait on a pageable copy:
+  // actor-major at stride ostride for the k-way merge, file-major for the merges one by one
+  const uint32_t ccap = d->clock_cap;
+  const uint32_t ostride = ds_oclock_stride((uint32_t)n);
+  const size_t oc_words = kway ? (size_t)ccap * ostride : (size_t)ccap * n;
+  if ((e = d->rd_clock.reserve(8ull * oc_words + 64))) return ctx->hip_fail(e, "merge");
+  auto* hclk = d->rd_clock.as<unsigned long long>();
+  if (kway) {
+    std::memset(hclk, 0, 8ull * oc_words);
+    for (size_t i = 0; i < n; i++)
+      for (auto& y : ds[i].oclock) hclk[(size_t)y.first * ostride + i] = y.second;
+  } else {
+    for (size_t i = 0; i < n; i++)
+      if (ds[i].device) {
+        std::memset(hclk + (size_t)ccap * i, 0, 8ull * ccap);
+        for (auto& y : ds[i].oclock) hclk[(size_t)ccap * i + y.first] = y.second;
+      }
+  }
+  // every file's dense other-clock in HBM with one copy
+  if ((e = d->rd_oclocks.reserve(8ull * oc_words + 64)) ||
+      (e = hipMemcpyAsync(d->rd_oclocks.p, hclk, 8ull * oc_words, hipMemcpyHostToDevice, s)))
+    return ctx->hip_fail(e, "merge");
+  if (kway) {
     HostPhase hk("  merge: k-way");
     if ((e = d->rd_args_h.reserve(n * sizeof(DsMergeSrc) + 64)) || (e = d->rd_args_d.reserve(n * sizeof(DsMergeSrc) + 64)))
       return ctx->hip_fail(e, "merge");
@@ -2091,7 +2100,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     // first wait), like a fold's
     d->scratch_dirty = true;
     if ((e = launch_ds_kmerge(s, tables(d), nullptr, hs, (uint32_t)n,
-                              d->clock.as<unsigned long long>(), d->rd_oclocks.as<unsigned long long>(), ccap,
+                              d->clock.as<unsigned long long>(), d->rd_oclocks.as<unsigned long long>(), ccap, ostride,
                               d->hold.as<unsigned long long>(),
                               static_cast<uint32_t*>(host_dev_ptr(d->h_cnt.as<uint32_t>() + 56)))))
       return ctx->hip_fail(e, "merge");
@@ -2760,11 +2769,11 @@ int ds_merge_columns_device(ce_core* c, const uint8_t* const* parts, const uint6
   if ((rc = table_upload(c)) || (rc = ensure_clock(c)) || (rc = ensure_pairs(c, np_tot))) return rc;
   ph.emplace("  cols: launch");
   // 3) maps uploaded and the dense other-clocks zeroed in one launch, then the remap
-  const uint32_t ccap = d->clock_cap;
-  if ((e = d->rd_oclocks.reserve(8ull * ccap * k + 64))) return ctx->hip_fail(e, "columns");
+  const uint32_t ccap = d->clock_cap, ostride = ds_oclock_stride(k);
+  if ((e = d->rd_oclocks.reserve(8ull * ccap * ostride + 64))) return ctx->hip_fail(e, "columns");
   FillArgs fl{};
   fl.r[fl.n++] = {d->cx_mapd.as<uint32_t>(), maps, 0u, static_cast<const uint32_t*>(host_dev_ptr(hmap))};
-  fl.r[fl.n++] = {d->rd_oclocks.as<uint32_t>(), 2ull * ccap * k, 0u};
+  fl.r[fl.n++] = {d->rd_oclocks.as<uint32_t>(), 2ull * ccap * ostride, 0u};
   std::vector<DsColsRemap> rm(k);
   std::vector<DsMergeSrc> src(k);
   {
@@ -2775,7 +2784,7 @@ int ds_merge_columns_device(ce_core* c, const uint8_t* const* parts, const uint6
       const uint64_t o_clock = 32 + 16 * na, o_mem = o_clock + 16 * na, o_val = o_mem + 8 * np, o_act = o_val + 8 * np;
       rm[f] = DsColsRemap{reinterpret_cast<const uint32_t*>(b + o_act), d->cx_ids.as<uint32_t>() + q,
                           d->cx_mapd.as<uint32_t>() + m, reinterpret_cast<const unsigned long long*>(b + o_clock),
-                          d->rd_oclocks.as<unsigned long long>() + (size_t)ccap * f, (uint32_t)np, (uint32_t)na};
+                          d->rd_oclocks.as<unsigned long long>() + f, (uint32_t)np, (uint32_t)na, ostride};
       src[f] = DsMergeSrc{reinterpret_cast<const unsigned long long*>(b + o_mem), d->cx_ids.as<uint32_t>() + q,
                           reinterpret_cast<const unsigned long long*>(b + o_val), (uint32_t)np,
                           d->cx_slot.as<uint32_t>() + q};
@@ -2789,7 +2798,7 @@ int ds_merge_columns_device(ce_core* c, const uint8_t* const* parts, const uint6
   const int tm = ctx->tbegin("cols_merge");
   if ((e = launch_fill(s, fl)) || (e = launch_cols_remap(s, rm.data(), k)) ||
       (e = launch_ds_kmerge(s, tables(d), nullptr, src.data(), k, d->clock.as<unsigned long long>(),
-                            d->rd_oclocks.as<unsigned long long>(), ccap, d->hold.as<unsigned long long>(),
+                            d->rd_oclocks.as<unsigned long long>(), ccap, ostride, d->hold.as<unsigned long long>(),
                             static_cast<uint32_t*>(host_dev_ptr(d->h_cnt.as<uint32_t>() + 56)))))
     return ctx->hip_fail(e, "columns");
   ctx->tend(tm);
