@@ -87,7 +87,13 @@ struct DsDecodeArgs {
   // (fuse.*) and writes the offsets columns as op index + base.  null: none.
   const uint8_t* fdone;
   DsFuse fuse;
+  // count pass: per block [8 words]: the largest count of each column and the files the open
+  // decoded, reduced by k_ds_col_totals (same-address atomics from every block serialised across
+  // the XCDs, ~60 ns each).  null: the atomics into counters[5] / counters[8 + k]
+  uint32_t* bpart;
 };
+// k_ds_count's grid for n files (its bpart rows)
+uint32_t ds_count_blocks(uint32_t n);
 hipError_t launch_ds_count(hipStream_t s, const DsDecodeArgs& a);
 hipError_t launch_ds_emit(hipStream_t s, const DsDecodeArgs& a, bool emit_legacy = true);
 
@@ -277,7 +283,8 @@ hipError_t ds_excl_sum_u32(void* tmp, size_t& tb, const uint32_t* in, uint32_t* 
 // out (19 words): column totals [0..kCntN), column maxima [8..8+kCntN), status summary [13..17),
 // the gate's two flags [17..19) (gate_flags may be null); then clear8[0..8) = 0 (may be null)
 hipError_t launch_ds_col_totals(hipStream_t s, const uint32_t* cnt, const uint32_t* bases, uint32_t n,
-                                const uint32_t* maxima, const int32_t* status, const uint32_t* gate_flags,
+                                const uint32_t* maxima, const uint32_t* bpart, uint32_t nb,
+                                const int32_t* status, const uint32_t* gate_flags,
                                 uint32_t* clear8, uint32_t* out, const unsigned long long* nn_src = nullptr,
                                 uint32_t nn_m = 0, unsigned long long* nn_dst = nullptr);
 hipError_t launch_ds_set3(hipStream_t s, uint32_t* p0, uint32_t v0, uint32_t* p1, uint32_t v1, uint32_t* p2,

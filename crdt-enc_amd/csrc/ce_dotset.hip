@@ -447,8 +447,9 @@ __device__ __forceinline__ int32_t count_file(const DsDecodeArgs& a, const uint8
 template <bool STAGE>
 __global__ void __launch_bounds__(kBlock) k_ds_count(DsDecodeArgs a) {
   extern __shared__ uint8_t stage_lds[];
-  __shared__ uint32_t smax[kCntN];
+  __shared__ uint32_t smax[kCntN], sfused;
   if (threadIdx.x < kCntN) smax[threadIdx.x] = 0;
+  if (threadIdx.x == 0) sfused = 0;
   __syncthreads();
   uint32_t mx[kCntN];
 #pragma unroll
@@ -466,9 +467,12 @@ __global__ void __launch_bounds__(kBlock) k_ds_count(DsDecodeArgs a) {
 #pragma unroll
       for (int k = 0; k < kCntN; k++) c[k] = a.fuse.rawcnt[(size_t)k * a.n + i];
     }
-    if (a.fdone) {  // files the open decoded (counters[5]: the host reads it with the totals)
+    if (a.fdone) {  // files the open decoded (the host reads the count with the totals)
       const unsigned long long b = __ballot(fd);
-      if (b && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(b)) atomicAdd(a.counters + 5, (uint32_t)__popcll(b));
+      if (b && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(b)) {
+        if (a.bpart) atomicAdd(&sfused, (uint32_t)__popcll(b));
+        else atomicAdd(a.counters + 5, (uint32_t)__popcll(b));
+      }
     }
     if (in && st == CE_OK && !fd) {
       const uint32_t len = a.params[i].len;
@@ -503,7 +507,12 @@ __global__ void __launch_bounds__(kBlock) k_ds_count(DsDecodeArgs a) {
     if ((threadIdx.x & 63) == 0 && m) atomicMax(&smax[k], m);
   }
   __syncthreads();
-  if (threadIdx.x < kCntN && smax[threadIdx.x]) atomicMax(a.counters + 8 + threadIdx.x, smax[threadIdx.x]);
+  if (a.bpart) {
+    if (threadIdx.x < kCntN) a.bpart[8 * blockIdx.x + threadIdx.x] = smax[threadIdx.x];
+    if (threadIdx.x == kCntN) a.bpart[8 * blockIdx.x + 5] = sfused;
+  } else if (threadIdx.x < kCntN && smax[threadIdx.x]) {
+    atomicMax(a.counters + 8 + threadIdx.x, smax[threadIdx.x]);
+  }
 }
 
 template <bool TILE, bool ST>
@@ -1676,33 +1685,60 @@ hipError_t ds_sort_pairs_u64(void* tmp, size_t& tb, const unsigned long long* ki
 // left to the host op decoder; out[16] the first file not OK (0xffffffff: none); out[17..19) the
 // version gate's flags (gate_flags, when given); then clear8[0..8) = 0 (the emit's counters)
 __global__ void __launch_bounds__(1024) k_ds_col_totals(const uint32_t* cnt, const uint32_t* bases, uint32_t n,
-                                                        const uint32_t* maxima, const int32_t* status,
+                                                        const uint32_t* maxima, const uint32_t* bpart, uint32_t nb,
+                                                        const int32_t* status,
                                                         const uint32_t* gate_flags, uint32_t* clear8, uint32_t* out,
                                                         const unsigned long long* nn_src, uint32_t nn_m,
                                                         unsigned long long* nn_dst) {
   // the version gate's next versions per writer too (out and nn_dst: the caller's pinned memory)
   for (uint32_t i = threadIdx.x; nn_dst && i < nn_m; i += blockDim.x) nn_dst[i] = nn_src[i];
-  __shared__ uint32_t acc[4];
+  __shared__ uint32_t acc[4], pmax[kCntN + 1];
   const uint32_t k = threadIdx.x;
   if (k < 3) acc[k] = 0;
   if (k == 3) acc[3] = 0xffffffffu;
+  if (k <= kCntN) pmax[k] = 0;
+  __syncthreads();
+  if (bpart) {  // the count pass's per-block maxima and decoded-file counts
+    uint32_t m[kCntN + 1] = {0, 0, 0, 0, 0, 0};
+    for (uint32_t b = k; b < nb; b += blockDim.x) {
+#pragma unroll
+      for (int j = 0; j < kCntN; j++) m[j] = max(m[j], bpart[8 * b + j]);
+      m[kCntN] += bpart[8 * b + 5];
+    }
+#pragma unroll
+    for (int j = 0; j < kCntN; j++)
+      if (m[j]) atomicMax(&pmax[j], m[j]);
+    if (m[kCntN]) atomicAdd(&pmax[kCntN], m[kCntN]);
+  }
+  __syncthreads();
   if (k < kCntN) {
     const size_t c0 = (size_t)k * n, cl = c0 + n - 1;
     out[k] = bases[cl] + cnt[cl] - bases[c0];
-    out[8 + k] = maxima[k];
+    out[8 + k] = bpart ? pmax[k] : maxima[k];
   }
-  if (clear8 && k == 5) out[19] = clear8[5];  // files the open decoded (k_ds_count's counters[5])
+  if (k == 5) out[19] = bpart ? pmax[kCntN] : clear8 ? clear8[5] : 0u;  // files the open decoded
   if (gate_flags && k < 2) out[17 + k] = gate_flags[k];
   __syncthreads();
   if (clear8 && k < 8) clear8[k] = 0;  // the emit's counters (after the maxima above were read)
   uint32_t bad = 0, hp = 0, hd = 0, first = 0xffffffffu;
-  for (uint32_t i = k; i < n; i += blockDim.x) {
-    const int32_t st = status[i];
-    if (st != CE_OK) {
-      bad++;
-      hp += st == kStatusHostParse;
-      hd += st == kStatusHostDecode;
-      first = min(first, i);
+  // 16 statuses per lane in flight per trip (one block: a load at a time was one latency each)
+  constexpr int kSt = 16;
+  for (uint32_t i0 = k; i0 < n; i0 += kSt * blockDim.x) {
+    int32_t v[kSt];
+#pragma unroll
+    for (int q = 0; q < kSt; q++) {
+      const uint32_t i = i0 + q * blockDim.x;
+      v[q] = i < n ? status[i] : CE_OK;
+    }
+#pragma unroll
+    for (int q = 0; q < kSt; q++) {
+      const int32_t st = v[q];
+      if (st != CE_OK) {
+        bad++;
+        hp += st == kStatusHostParse;
+        hd += st == kStatusHostDecode;
+        first = min(first, i0 + q * blockDim.x);
+      }
     }
   }
   if (bad) {
@@ -1716,11 +1752,12 @@ __global__ void __launch_bounds__(1024) k_ds_col_totals(const uint32_t* cnt, con
 }
 
 hipError_t launch_ds_col_totals(hipStream_t s, const uint32_t* cnt, const uint32_t* bases, uint32_t n,
-                                const uint32_t* maxima, const int32_t* status, const uint32_t* gate_flags,
+                                const uint32_t* maxima, const uint32_t* bpart, uint32_t nb,
+                                const int32_t* status, const uint32_t* gate_flags,
                                 uint32_t* clear8, uint32_t* out, const unsigned long long* nn_src, uint32_t nn_m,
                                 unsigned long long* nn_dst) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ds_col_totals, dim3(1), dim3(1024), 0, s, cnt, bases, n, maxima, status, gate_flags,
+  hipLaunchKernelGGL(k_ds_col_totals, dim3(1), dim3(1024), 0, s, cnt, bases, n, maxima, bpart, nb, status, gate_flags,
                      clear8, out, nn_src, nn_m, nn_dst);
   return hipGetLastError();
 }
@@ -1744,10 +1781,12 @@ static bool decode_stage() {
   return v && atoi(v) != 0;
 }
 
+uint32_t ds_count_blocks(uint32_t n) { return blocks_for(n); }
+
 hipError_t launch_ds_count(hipStream_t s, const DsDecodeArgs& a) {
   if (a.n == 0) return hipSuccess;
-  if (decode_stage()) hipLaunchKernelGGL(k_ds_count<true>, dim3(blocks_for(a.n)), dim3(kBlock), kStageLds, s, a);
-  else hipLaunchKernelGGL(k_ds_count<false>, dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
+  if (decode_stage()) hipLaunchKernelGGL(k_ds_count<true>, dim3(ds_count_blocks(a.n)), dim3(kBlock), kStageLds, s, a);
+  else hipLaunchKernelGGL(k_ds_count<false>, dim3(ds_count_blocks(a.n)), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 

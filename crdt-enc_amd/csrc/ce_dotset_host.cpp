@@ -95,6 +95,7 @@ struct DsState {
   // bases, members, sorted members [0..6]
   // and emitted (member, actor id, value) columns [7..9]), pinned staging for its downloads
   std::vector<std::array<DevBuf, 10>> rd;
+  DevBuf cnt_part;  // the count pass's per-block maxima / decoded-file counts (DsDecodeArgs::bpart)
   DevBuf rd_tmp, rd_misc, ser[17], uuid_of_id, rank_of_id, id_of_rank, rd_oclocks, cnt_tot, rd_args_d, rd_chunks;
   HostBuf rd_host, rd_small, rd_clock, rd_args_h, h_clock;
   uint64_t uuid_ids = ~0ull;  // id count uuid_of_id / rank_of_id (and id_rank / rank_id) were built for
@@ -1192,6 +1193,9 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
     a.fdone = fz.ds.done;
     a.fuse = fz.ds;
   }
+  const uint32_t cnt_nb = ds_count_blocks(n);
+  if ((e = d->cnt_part.reserve(32ull * cnt_nb + 64))) return ctx->hip_fail(e, "count");
+  a.bpart = d->cnt_part.as<uint32_t>();
   if ((uint64_t)kCntN * n > 0x7fffffffull) return ctx->fail(CE_ERR_INVALID_ARG, "batch too large for one scan");
   uint32_t* cnt = d->cnt.as<uint32_t>();
   uint32_t* bases = cnt + (size_t)kCntN * n;
@@ -1217,7 +1221,8 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
     if ((e = launch_ds_count(ctx->stream, a))) return ctx->hip_fail(e, "count");
     ctx->tend(tc);
     if ((e = ds_excl_sum_u32(d->cub_tmp.p, t, cnt, bases, kCntN * n, ctx->stream)) ||
-        (e = launch_ds_col_totals(ctx->stream, cnt, bases, n, d->misses.as<uint32_t>() + 8, ctx->status.as<int32_t>(),
+        (e = launch_ds_col_totals(ctx->stream, cnt, bases, n, d->misses.as<uint32_t>() + 8, a.bpart, cnt_nb,
+                                  ctx->status.as<int32_t>(),
                                   ctx->counters.as<uint32_t>() + 12, d->misses.as<uint32_t>(),
                                   static_cast<uint32_t*>(host_dev_ptr(hsum)), gj.ga.newnov, m,
                                   static_cast<unsigned long long*>(host_dev_ptr(gj.hnn)))))
