@@ -92,8 +92,11 @@ struct DsDecodeArgs {
   // the XCDs, ~60 ns each).  null: the atomics into counters[5] / counters[8 + k]
   uint32_t* bpart;
 };
-// k_ds_count's grid for n files (its bpart rows)
+// k_ds_count's grid for n files (its bpart rows: kDsCountPart words each -- [0, 5) column
+// maxima, [5] files the open decoded, [8] files not OK, [9] left to the host envelope parser,
+// [10] left to the host op decoder, [11] the first not OK)
 uint32_t ds_count_blocks(uint32_t n);
+static constexpr uint32_t kDsCountPart = 16;
 hipError_t launch_ds_count(hipStream_t s, const DsDecodeArgs& a);
 hipError_t launch_ds_emit(hipStream_t s, const DsDecodeArgs& a, bool emit_legacy = true);
 

@@ -447,13 +447,15 @@ __device__ __forceinline__ int32_t count_file(const DsDecodeArgs& a, const uint8
 template <bool STAGE>
 __global__ void __launch_bounds__(kBlock) k_ds_count(DsDecodeArgs a) {
   extern __shared__ uint8_t stage_lds[];
-  __shared__ uint32_t smax[kCntN], sfused;
+  __shared__ uint32_t smax[kCntN], sfused, sst[4];
   if (threadIdx.x < kCntN) smax[threadIdx.x] = 0;
   if (threadIdx.x == 0) sfused = 0;
+  if (threadIdx.x < 4) sst[threadIdx.x] = threadIdx.x == 3 ? 0xffffffffu : 0u;
   __syncthreads();
   uint32_t mx[kCntN];
 #pragma unroll
   for (int k = 0; k < kCntN; k++) mx[k] = 0;
+  uint32_t nbad = 0, nhp = 0, nhd = 0, first_bad = 0xffffffffu;
   // (STAGE: the trip count is uniform over the block -- every lane reaches the barriers)
   for (uint32_t i0 = blockIdx.x * kBlock; i0 < a.n; i0 += gridDim.x * kBlock) {
     const uint32_t i = i0 + threadIdx.x;
@@ -494,6 +496,12 @@ __global__ void __launch_bounds__(kBlock) k_ds_count(DsDecodeArgs a) {
       for (int k = 0; k < kCntN; k++) a.cnt[(size_t)k * a.n + i] = keep ? c[k] : 0u;
 #pragma unroll
       for (int k = 0; k < kCntN; k++) mx[k] = max(mx[k], keep ? c[k] : 0u);
+      if (st != CE_OK) {  // the status summary (final statuses: the parse above may have failed)
+        nbad++;
+        nhp += st == kStatusHostParse;
+        nhd += st == kStatusHostDecode;
+        first_bad = min(first_bad, i);
+      }
     }
     if (STAGE) __syncthreads();  // the next trip's staging overwrites the region
   }
@@ -506,10 +514,17 @@ __global__ void __launch_bounds__(kBlock) k_ds_count(DsDecodeArgs a) {
     for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
     if ((threadIdx.x & 63) == 0 && m) atomicMax(&smax[k], m);
   }
+  if (nbad) {
+    atomicAdd(&sst[0], nbad);
+    if (nhp) atomicAdd(&sst[1], nhp);
+    if (nhd) atomicAdd(&sst[2], nhd);
+    atomicMin(&sst[3], first_bad);
+  }
   __syncthreads();
   if (a.bpart) {
-    if (threadIdx.x < kCntN) a.bpart[8 * blockIdx.x + threadIdx.x] = smax[threadIdx.x];
-    if (threadIdx.x == kCntN) a.bpart[8 * blockIdx.x + 5] = sfused;
+    if (threadIdx.x < kCntN) a.bpart[kDsCountPart * blockIdx.x + threadIdx.x] = smax[threadIdx.x];
+    if (threadIdx.x == kCntN) a.bpart[kDsCountPart * blockIdx.x + 5] = sfused;
+    if (threadIdx.x >= 8 && threadIdx.x < 12) a.bpart[kDsCountPart * blockIdx.x + threadIdx.x] = sst[threadIdx.x - 8];
   } else if (threadIdx.x < kCntN && smax[threadIdx.x]) {
     atomicMax(a.counters + 8 + threadIdx.x, smax[threadIdx.x]);
   }
@@ -1177,17 +1192,38 @@ struct DsPublish {
   uint32_t* done;
 };
 
-__device__ __forceinline__ void publish_last(const DsPublish& pub) {
+// The last block of the grid copies pub.src[0..words) (counters earlier kernels produced) into
+// pub.dst, with word any_word (>= 0) OR'ed with "some block of this grid had `some`".  Found in
+// two levels: block b adds 1 (+ 1 << 16 when `some`) into done[1 + b % 8], the block completing
+// its replica adds its replica's verdict into done[0] -- ~blocks / 8 same-address adds per word,
+// ~60 ns each across XCDs, and the flag travels in the same atomics, so no block needs a fence
+// (an agent-scope fence per block writes back its XCD's L2: ~20 us over 128 blocks).
+// done[0..8] are zero between uses.
+__device__ __forceinline__ void publish_last(const DsPublish& pub, bool some, int any_word) {
   if (!pub.dst) return;
   __shared__ bool last;
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(pub.done, 1u) == gridDim.x - 1;
+  __shared__ uint32_t any_all;
+  const bool bsome = __syncthreads_or(some) != 0;
+  if (threadIdx.x == 0) {
+    const uint32_t r = blockIdx.x & 7u, reps = min(gridDim.x, 8u);
+    const uint32_t in_r = (gridDim.x - r + 7u) / 8u;  // blocks counting into replica r
+    last = false;
+    const uint32_t o = atomicAdd(pub.done + 1 + r, 1u + (bsome ? 0x10000u : 0u));
+    if ((o & 0xffffu) == in_r - 1) {
+      pub.done[1 + r] = 0;
+      const bool rsome = (o >> 16) != 0 || bsome;
+      const uint32_t o2 = atomicAdd(pub.done, 1u + (rsome ? 0x10000u : 0u));
+      last = (o2 & 0xffffu) == reps - 1;
+      any_all = ((o2 >> 16) != 0 || rsome) ? 1u : 0u;
+    }
+  }
   __syncthreads();
   if (!last) return;
-  __threadfence();
-  if (threadIdx.x < pub.words)
-    pub.dst[threadIdx.x] = __hip_atomic_load(pub.src + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x < pub.words) {
+    uint32_t v = __hip_atomic_load(pub.src + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((int)threadIdx.x == any_word) v |= any_all;
+    pub.dst[threadIdx.x] = v;
+  }
   if (threadIdx.x == 0) *pub.done = 0;
 }
 
@@ -1195,18 +1231,40 @@ __global__ void k_ds_deferred(const uint32_t* cbeg, const uint32_t* c_actor,
                               const unsigned long long* c_ctr, const unsigned long long* clock,
                               uint8_t* deferred, uint32_t n, uint32_t* any, DsPublish pub) {
   bool some = false;
-  for (uint32_t r = blockIdx.x * kBlock + threadIdx.x; r < n; r += gridDim.x * kBlock) {
-    bool d = false;
-    for (uint32_t e = cbeg[r]; e < cbeg[r + 1] && !d; e++) d = c_ctr[e] > clock[c_actor[e]];
-    deferred[r] = d;  // !(clock <= self.clock)
-    some = some || d;
+  // four removals per lane and trip, their loads issued together (one-entry clocks: C3's); longer
+  // clocks walk the rest
+  constexpr int kQ = 4;
+  for (uint32_t r0 = blockIdx.x * kBlock + threadIdx.x; r0 < n; r0 += gridDim.x * kBlock * kQ) {
+    uint32_t e0[kQ], e1[kQ], ca[kQ];
+    unsigned long long cc[kQ];
+#pragma unroll
+    for (int q = 0; q < kQ; q++) {
+      const uint32_t r = r0 + q * gridDim.x * kBlock;
+      e0[q] = r < n ? cbeg[r] : 0u;
+      e1[q] = r < n ? cbeg[r + 1] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < kQ; q++) {
+      ca[q] = e0[q] < e1[q] ? c_actor[e0[q]] : 0u;
+      cc[q] = e0[q] < e1[q] ? c_ctr[e0[q]] : 0ull;
+    }
+#pragma unroll
+    for (int q = 0; q < kQ; q++) {
+      const uint32_t r = r0 + q * gridDim.x * kBlock;
+      if (r >= n) continue;
+      bool d = e0[q] < e1[q] && cc[q] > clock[ca[q]];
+      for (uint32_t e = e0[q] + 1; e < e1[q] && !d; e++) d = c_ctr[e] > clock[c_actor[e]];
+      deferred[r] = d;  // !(clock <= self.clock)
+      some = some || d;
+    }
   }
-  // any[0] = 1 when some removal is deferred (one atomic per wave that has one; rare)
-  if (any) {
+  // any[0] = 1 when some removal is deferred (one atomic per wave that has one; rare); a
+  // publishing launch carries it in its last-block count instead (publish_last)
+  if (any && !pub.dst) {
     const unsigned long long b = __ballot(some);
     if (b && (threadIdx.x & 63) == (uint32_t)(__ffsll(b) - 1)) atomicOr(any, 1u);
   }
-  publish_last(pub);
+  publish_last(pub, some, any && pub.dst ? (int)(any - pub.src) : -1);
 }
 
 __global__ void __launch_bounds__(kBlock) k_ds_put_other(DsTables t, const unsigned long long* member,
@@ -1698,17 +1756,29 @@ __global__ void __launch_bounds__(1024) k_ds_col_totals(const uint32_t* cnt, con
   if (k == 3) acc[3] = 0xffffffffu;
   if (k <= kCntN) pmax[k] = 0;
   __syncthreads();
-  if (bpart) {  // the count pass's per-block maxima and decoded-file counts
+  if (bpart) {  // the count pass's per-block maxima, decoded-file counts and status summaries
     uint32_t m[kCntN + 1] = {0, 0, 0, 0, 0, 0};
+    uint32_t bad = 0, hp = 0, hd = 0, first = 0xffffffffu;
     for (uint32_t b = k; b < nb; b += blockDim.x) {
+      const uint32_t* r = bpart + kDsCountPart * b;
 #pragma unroll
-      for (int j = 0; j < kCntN; j++) m[j] = max(m[j], bpart[8 * b + j]);
-      m[kCntN] += bpart[8 * b + 5];
+      for (int j = 0; j < kCntN; j++) m[j] = max(m[j], r[j]);
+      m[kCntN] += r[5];
+      bad += r[8];
+      hp += r[9];
+      hd += r[10];
+      first = min(first, r[11]);
     }
 #pragma unroll
     for (int j = 0; j < kCntN; j++)
       if (m[j]) atomicMax(&pmax[j], m[j]);
     if (m[kCntN]) atomicAdd(&pmax[kCntN], m[kCntN]);
+    if (bad) {
+      atomicAdd(&acc[0], bad);
+      if (hp) atomicAdd(&acc[1], hp);
+      if (hd) atomicAdd(&acc[2], hd);
+      atomicMin(&acc[3], first);
+    }
   }
   __syncthreads();
   if (k < kCntN) {
@@ -1721,9 +1791,9 @@ __global__ void __launch_bounds__(1024) k_ds_col_totals(const uint32_t* cnt, con
   __syncthreads();
   if (clear8 && k < 8) clear8[k] = 0;  // the emit's counters (after the maxima above were read)
   uint32_t bad = 0, hp = 0, hd = 0, first = 0xffffffffu;
-  // 16 statuses per lane in flight per trip (one block: a load at a time was one latency each)
+  // (without bpart) 16 statuses per lane in flight per trip
   constexpr int kSt = 16;
-  for (uint32_t i0 = k; i0 < n; i0 += kSt * blockDim.x) {
+  for (uint32_t i0 = k; !bpart && i0 < n; i0 += kSt * blockDim.x) {
     int32_t v[kSt];
 #pragma unroll
     for (int q = 0; q < kSt; q++) {
@@ -1910,11 +1980,12 @@ hipError_t launch_ds_deferred(hipStream_t s, const uint32_t* cbeg, const uint32_
                               uint8_t* deferred, uint32_t n_rm, uint32_t* any, const uint32_t* pub_src,
                               uint32_t* pub_dst, uint32_t pub_words) {
   if (n_rm == 0 && !pub_dst) return hipSuccess;
-  // (publishing: live[7] counts the blocks, zero between uses)
+  // (publishing: live[7..16) count the blocks in two levels, zero between uses)
   const DsPublish pub{pub_src, pub_dst, pub_words, pub_dst ? const_cast<uint32_t*>(pub_src) + 7 : nullptr};
-  // publishing: a grid of at most 128 blocks (grid-stride), so its last-block count is 128 atomics
-  // on one word -- same-address atomics from every XCD cost ~60 ns each (1600 blocks: 95 us)
-  const uint32_t nb = std::max<uint32_t>(1, pub_dst ? std::min<uint32_t>(128, blocks_for(n_rm)) : blocks_for(n_rm));
+  // publishing: at most 512 blocks (grid-stride, four removals per lane and trip): the two-level
+  // count is then ~64 same-address atomics per word (one word for 1600 blocks took 95 us)
+  const uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(pub_dst ? 512 : 8192, blocks_for((n_rm + 3) / 4)));
+  if (nb > 0xffffu * 8u) return hipErrorInvalidValue;  // (the 16-bit block counts)
   hipLaunchKernelGGL(k_ds_deferred, dim3(nb), dim3(kBlock), 0, s, cbeg, c_actor, c_ctr, clock, deferred, n_rm, any, pub);
   return hipGetLastError();
 }

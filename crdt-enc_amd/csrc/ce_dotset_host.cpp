@@ -975,14 +975,19 @@ int gate_enqueue(ce_core* c, const uint32_t* d_fa, const uint64_t* d_fv, uint32_
   fl.r[fl.n++] = {reinterpret_cast<uint32_t*>(gbase + 8ull * m), 4ull * m, 0u};
   fl.r[fl.n++] = {ga.flags, 1, 0u};
   fl.r[fl.n++] = {ga.flags + 1, 1, 0xffffffffu};
-  if (extra) fl.r[fl.n++] = *extra;
+  if (extra) {
+    fl.r[fl.n++] = *extra;
+    // the next versions straight into the pinned words the host reads (no copy after the count)
+    std::memset(job->hnn, 0, 8ull * m);
+    ga.newnov_host = static_cast<unsigned long long*>(host_dev_ptr(job->hnn));
+  }
   if ((e = launch_fill(ctx->stream, fl))) return ctx->hip_fail(e, "gate");
   const int t = ctx->tbegin("gate");
   if ((e = launch_gate(ctx->stream, ga))) return ctx->hip_fail(e, "gate");
   ctx->tend(t);
   // the flags come back with the caller's next download when it passes `extra` (k_ds_col_totals
   // copies them), else here
-  // (with `extra`, k_ds_col_totals also copies the next versions into job->hnn)
+  // (with `extra`, k_gate_apply writes the next versions into job->hnn itself)
   if (!extra && ((e = hipMemcpyAsync(job->hf, ga.flags, 8, hipMemcpyDeviceToHost, ctx->stream)) ||
                  (e = hipMemcpyAsync(job->hnn, ga.newnov, m * 8ull, hipMemcpyDeviceToHost, ctx->stream))))
     return ctx->hip_fail(e, "gate");
@@ -1194,7 +1199,7 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
     a.fuse = fz.ds;
   }
   const uint32_t cnt_nb = ds_count_blocks(n);
-  if ((e = d->cnt_part.reserve(32ull * cnt_nb + 64))) return ctx->hip_fail(e, "count");
+  if ((e = d->cnt_part.reserve(4ull * kDsCountPart * cnt_nb + 64))) return ctx->hip_fail(e, "count");
   a.bpart = d->cnt_part.as<uint32_t>();
   if ((uint64_t)kCntN * n > 0x7fffffffull) return ctx->fail(CE_ERR_INVALID_ARG, "batch too large for one scan");
   uint32_t* cnt = d->cnt.as<uint32_t>();
@@ -1224,8 +1229,7 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
         (e = launch_ds_col_totals(ctx->stream, cnt, bases, n, d->misses.as<uint32_t>() + 8, a.bpart, cnt_nb,
                                   ctx->status.as<int32_t>(),
                                   ctx->counters.as<uint32_t>() + 12, d->misses.as<uint32_t>(),
-                                  static_cast<uint32_t*>(host_dev_ptr(hsum)), gj.ga.newnov, m,
-                                  static_cast<unsigned long long*>(host_dev_ptr(gj.hnn)))))
+                                  static_cast<uint32_t*>(host_dev_ptr(hsum)), nullptr, 0, nullptr)))
       return ctx->hip_fail(e, "count");
     return CE_OK;
   };

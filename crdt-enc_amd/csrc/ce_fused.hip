@@ -1576,7 +1576,10 @@ __global__ void k_gate_apply(GateArgs g) {
     // versions are consecutive inside a run: only the run's last applied file bumps
     // next_op_versions (one atomic per actor instead of one per file)
     const bool last = i + 1 == g.n || g.fa[i + 1] != a || i + 1 >= gap;
-    if (ap && last) atomicMax(&g.newnov[a], (unsigned long long)(g.fv[i] + 1));
+    if (ap && last) {
+      atomicMax(&g.newnov[a], (unsigned long long)(g.fv[i] + 1));
+      if (g.newnov_host) g.newnov_host[a] = g.fv[i] + 1;
+    }
   }
   g.apply[i] = ap ? 1 : 0;
 }

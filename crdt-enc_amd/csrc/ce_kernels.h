@@ -189,6 +189,8 @@ struct GateArgs {
   uint32_t* flags;         // [0] not grouped/consecutive, [1] first gap (min file index)
   unsigned long long* newnov;  // [m] max(v + 1) over applied files
   uint8_t* apply;          // [n]
+  unsigned long long* newnov_host;  // optional mapped pinned copy of newnov (zeroed by the host;
+                                    // exact when flags[0] stays 0: one run per actor)
 };
 hipError_t launch_gate(hipStream_t s, const GateArgs& g);
 
