@@ -97,7 +97,7 @@ struct DsState {
   std::vector<std::array<DevBuf, 10>> rd;
   DevBuf cnt_part;  // the count pass's per-block maxima / decoded-file counts (DsDecodeArgs::bpart)
   DevBuf rd_tmp, rd_misc, ser[17], uuid_of_id, rank_of_id, id_of_rank, rd_oclocks, cnt_tot, rd_args_d, rd_chunks;
-  HostBuf rd_host, rd_small, rd_clock, rd_args_h, h_clock;
+  HostBuf rd_host, rd_small, rd_clock, rd_args_h, h_clock, rd_tailh;
   uint64_t uuid_ids = ~0ull;  // id count uuid_of_id / rank_of_id (and id_rank / rank_id) were built for
   std::vector<uint32_t> id_rank, rank_id;  // UUID-order rank of each stable id, and its inverse
 };
@@ -1791,6 +1791,7 @@ OrswotReadArgs read_args(ce_core* c, DsState* d, size_t f, const DevState& ds, c
   // (the count straight into the pinned small words the host reads after stage 0)
   a.n_cand_dev = static_cast<uint32_t*>(host_dev_ptr(d->rd_small.as<uint32_t>())) + 2 * f;
   a.flags = d->rd_misc.as<uint32_t>() + 2 * f + 1;
+  a.skip = d->rd_misc.as<uint32_t>() + 2 * f;
   a.cap = cap;
   a.n_cand = ds.n_entries;
   a.cand = b[1].as<uint32_t>();
@@ -1850,6 +1851,34 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
   };
   auto sync = [&](const char* what) { return (e = stream_wait(s)) ? ctx->hip_fail(e, what) : CE_OK; };
   int first = CE_OK;
+  // dense other-clocks in pinned memory, so the queued merges never wait on a pageable copy:
+  // actor-major at stride ostride for the k-way merge, file-major for the merges one by one;
+  // every file's in HBM with one copy
+  const uint32_t ostride = ds_oclock_stride((uint32_t)n);
+  unsigned long long* hclk = nullptr;
+  bool oclk_pre = false;
+  uint32_t oclk_cap = 0;
+  auto upload_oclocks = [&](bool kway) -> int {
+    const uint32_t ccap = oclk_cap = d->clock_cap;
+    const size_t oc_words = kway ? (size_t)ccap * ostride : (size_t)ccap * n;
+    if ((e = d->rd_clock.reserve(8ull * oc_words + 64))) return ctx->hip_fail(e, "merge");
+    hclk = d->rd_clock.as<unsigned long long>();
+    if (kway) {
+      std::memset(hclk, 0, 8ull * oc_words);
+      for (size_t i = 0; i < n; i++)
+        for (auto& y : ds[i].oclock) hclk[(size_t)y.first * ostride + i] = y.second;
+    } else {
+      for (size_t i = 0; i < n; i++)
+        if (ds[i].device) {
+          std::memset(hclk + (size_t)ccap * i, 0, 8ull * ccap);
+          for (auto& y : ds[i].oclock) hclk[(size_t)ccap * i + y.first] = y.second;
+        }
+    }
+    if ((e = d->rd_oclocks.reserve(8ull * oc_words + 64)) ||
+        (e = hipMemcpyAsync(d->rd_oclocks.p, hclk, 8ull * oc_words, hipMemcpyHostToDevice, s)))
+      return ctx->hip_fail(e, "merge");
+    return CE_OK;
+  };
   {
     HostPhase hp("states: device read");
     // 1) the heads on the host: a prefix of every file long enough for next_op_versions and
@@ -1866,7 +1895,48 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
         if (poff[i + 1] > poff[i]) gr.push_back({out + off[i], poff[i], poff[i + 1] - poff[i]});
       if ((e = gather_download(d, s, hb, gr, poff[n]))) return ctx->hip_fail(e, "state head");
     }
-    if ((rc = sync("state head"))) return rc;
+    hipEvent_t heads_ev = nullptr;
+    if ((e = stream_mark(s, &heads_ev))) return ctx->hip_fail(e, "state head");
+    // 1b) queued behind the heads, stage 0 over each whole file -- the entry-head candidates in
+    //     position order (count, scan, write) -- runs while the host parses the heads; the
+    //     candidates before the entries (the clocks' own "dots" maps) are skipped on the device
+    //     once the host knows where the entries start (k_rdm_skip)
+    auto h2 = std::make_unique<HostPhase>("   rd.b stage 0");
+    constexpr uint32_t kTailWin = 4096;
+    std::vector<size_t> dev0;
+    std::vector<OrswotReadArgs> A0;
+    std::vector<int32_t> k0_of(n, -1);
+    uint32_t nch = 0;
+    for (size_t i = 0; i < n; i++) {
+      if (st[i] != CE_OK || len[i] < 8 || len[i] > 0xffffffffull) continue;
+      DevState& x = ds[i];
+      x.pt = off[i];
+      x.len = len[i];
+      x.body = 0;
+      x.n_entries = 0;
+      x.cap = (uint32_t)(len[i] / 7 + 1);  // (a head takes >= 7 bytes)
+      if ((e = d->rd[i][1].reserve(4ull * x.cap + 64))) return ctx->hip_fail(e, "state reader");
+      OrswotReadArgs a = read_args(c, d, i, x, out, x.cap);
+      a.chunk0 = nch;
+      a.nchunks = orswot_read_chunks(a.lo, a.hi);
+      nch += a.nchunks;
+      k0_of[i] = (int32_t)A0.size();
+      A0.push_back(a);
+      dev0.push_back(i);
+    }
+    if ((e = d->rd_chunks.reserve(8ull * (nch + 1) + 64)) ||
+        (e = d->rd_tmp.reserve(orswot_read_multi_tmp_bytes(nch))))
+      return ctx->hip_fail(e, "state reader");
+    uint32_t* chunk_cnt = d->rd_chunks.as<uint32_t>();
+    uint32_t* chunk_scan = chunk_cnt + nch + 1;
+    if (!A0.empty() &&
+        ((e = launch_fill(s, FillArgs{{FillRange{chunk_cnt + nch, 1, 0u}, FillRange{d->rd_misc.as<uint32_t>(), 2ull * n, 0u}},
+                                      2, nullptr})) ||
+         (e = launch_orswot_read_multi(s, nullptr, A0.data(), (uint32_t)A0.size(), 0, chunk_cnt, chunk_scan, d->rd_tmp.p,
+                                       d->rd_tmp.cap))))
+      return ctx->hip_fail(e, "state reader");
+    h2.reset();
+    if ((e = mark_wait(heads_ev))) return ctx->hip_fail(e, "state head");
     ph = std::make_unique<HostPhase>("  rd: heads parse");
     std::vector<size_t> dev;
     uint64_t head_max = 0;
@@ -1884,7 +1954,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
         if ((e = dl(pre.data(), out + off[i], want, s))) return ctx->hip_fail(e, "state head");
         pr = parse_state_prefix(pre.data(), want, want == len[i], &x.hs, &body, &ne);
       }
-      if (pr != 0 || ne == 0 || ne > (1ull << 30) || len[i] > 0xffffffffull) {  // (the repeat-check set needs 2 ne < 2^32)
+      if (pr != 0 || ne == 0 || ne > (1ull << 30) || k0_of[i] < 0) {  // (the repeat-check set needs 2 ne < 2^32)
         decline_stage = 1;
         if ((rc = host_parse(i))) return rc;
         continue;
@@ -1892,7 +1962,6 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
       x.body = body;
       head_max = std::max<uint64_t>(head_max, body);
       x.n_entries = (uint32_t)ne;
-      x.cap = (uint32_t)std::min<uint64_t>(ne + 65536, len[i] / 7 + 1);
       dev.push_back(i);
     }
     if (head_max) {
@@ -1900,9 +1969,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
       while (h < head_max + head_max / 4 + 1024 && h < (1u << 18)) h <<= 1;
       d->head_hint = h;
     }
-    // 2) the states' actors into the table (the emitted columns carry their ids), then the
-    //    entry-head search over every file (it covers the deferred map too: its VClock keys
-    //    look alike)
+    // 2) the states' actors into the table (the emitted columns carry their ids)
     ph = std::make_unique<HostPhase>("  rd: actors + search");
     // clocks -> actor ids: read-only lookups on the host threads; a file naming an actor
     // outside the table inserts it below, in file order (the order the ids are handed out in)
@@ -1915,51 +1982,59 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
       for (size_t i : dev)
         if (need_insert[i] && (rc = id_dots(c, ds[i].hs.clock, &ds[i].oclock))) return rc;
     }
-    auto h2 = std::make_unique<HostPhase>("   rd.b reserve");
-    // every stage below is one launch per kind for all device files (launch_orswot_read_multi:
-    // descriptors in HBM, gridDim.y = file); the descriptors of the three stages sit in separate
-    // thirds of one pinned buffer (each upload is ordered before the host rewrites its third)
-    const size_t na = std::max<size_t>(dev.size(), 1);
-    if ((e = d->rd_args_h.reserve(3 * na * sizeof(OrswotReadArgs))) ||
-        (e = d->rd_args_d.reserve(3 * na * sizeof(OrswotReadArgs))))
-      return ctx->hip_fail(e, "state reader");
-    OrswotReadArgs* hA = d->rd_args_h.as<OrswotReadArgs>();
-    uint32_t nch = 0;
+    h2 = std::make_unique<HostPhase>("   rd.b reserve");
+    // stages 1 and 2 are one launch per kind for all device files (launch_orswot_read_multi:
+    // descriptors as launch arguments, gridDim.y = file), queued back to back behind stage 0 (a
+    // file failing a stage is skipped by the later ones on the device), so the reader waits once
+    // more: head counts, tail words, the deferred maps' bytes and the flags come back in pinned
+    // memory together.  The columns are sized for the most Dots the entries' bytes can hold (a
+    // non-zero Dot takes >= 19 of them).
+    if ((e = d->rd_tailh.reserve((uint64_t)kTailWin * n + 64))) return ctx->hip_fail(e, "state reader");
+    uint8_t* tailh = d->rd_tailh.as<uint8_t>();
+    std::vector<OrswotReadArgs> hA(dev.size());
     for (size_t k = 0; k < dev.size(); k++) {
       const size_t i = dev[k];
       DevState& x = ds[i];
       const uint64_t ne = x.n_entries;
+      const uint64_t dots_max = (x.len - std::min<uint64_t>(x.len, x.body)) / 19 + 1;
       auto& b = d->rd[i];
-      if ((e = b[1].reserve(4ull * x.cap + 64)) || (e = b[2].reserve(4ull * ne + 64)) ||
-          (e = b[3].reserve(4ull * ne + 64)) || (e = b[4].reserve(4ull * ne + 64)) ||
-          (e = b[5].reserve(8ull * ne + 64)) || (e = b[6].reserve(8ull * (dset_mask_for(ne) + 2) + 64)))
+      if ((e = b[2].reserve(4ull * ne + 64)) || (e = b[3].reserve(4ull * ne + 64)) ||
+          (e = b[4].reserve(4ull * ne + 64)) || (e = b[5].reserve(8ull * ne + 64)) ||
+          (e = b[6].reserve(8ull * (dset_mask_for(ne) + 2) + 64)) || (e = b[7].reserve(8ull * dots_max + 8)) ||
+          (e = b[8].reserve(4ull * dots_max + 4)) || (e = b[9].reserve(8ull * dots_max + 8)))
         return ctx->hip_fail(e, "state reader");
       OrswotReadArgs a = read_args(c, d, i, x, out, x.cap);
-      a.chunk0 = nch;
-      a.nchunks = orswot_read_chunks(a.lo, a.hi);
-      nch += a.nchunks;
+      a.tail_out = static_cast<uint32_t*>(host_dev_ptr(small)) + 2 * n + 4 * i;  // pinned: no download
+      a.tail_host = static_cast<uint8_t*>(host_dev_ptr(tailh)) + (uint64_t)kTailWin * i;
+      a.tail_cap = kTailWin;
+      a.col_member = b[7].as<unsigned long long>();
+      a.col_actor = b[8].as<uint32_t>();
+      a.col_value = b[9].as<unsigned long long>();
       hA[k] = a;
     }
     if ((rc = table_upload(c)) || (rc = ensure_clock(c))) return rc;
-    if ((e = d->rd_chunks.reserve(8ull * (nch + 1) + 64)) ||
-        (e = d->rd_tmp.reserve(orswot_read_multi_tmp_bytes(nch))))
-      return ctx->hip_fail(e, "state reader");
-    uint32_t* chunk_cnt = d->rd_chunks.as<uint32_t>();
-    uint32_t* chunk_scan = chunk_cnt + nch + 1;
+    for (auto& a : hA) {  // (the upload may have moved the table)
+      a.table = c->d_table.as<ActorSlot>();
+      a.mask = c->cap - 1;
+    }
     h2 = std::make_unique<HostPhase>("   rd.c launch");
-    if (!dev.empty() &&
-        ((e = launch_fill(s, FillArgs{{FillRange{chunk_cnt + nch, 1, 0u}, FillRange{d->rd_misc.as<uint32_t>(), 2ull * n, 0u}},
-                                      2, nullptr})) ||
-         (e = launch_orswot_read_multi(s, nullptr, hA, (uint32_t)dev.size(), 0, chunk_cnt, chunk_scan, d->rd_tmp.p,
-                                       d->rd_tmp.cap))))
+    const uint32_t nd = (uint32_t)dev.size();
+    if (nd && ((e = launch_orswot_read_multi(s, nullptr, hA.data(), nd, 1, nullptr, nullptr, nullptr, 0)) ||
+               (e = launch_orswot_read_multi(s, nullptr, hA.data(), nd, 2, nullptr, nullptr, nullptr, 0))))
       return ctx->hip_fail(e, "state reader");
+    // the k-way merge's dense other-clocks (below), built and uploaded while stages 1-2 run when
+    // every file is still on the device path (else they are rebuilt for the merges one by one)
+    oclk_pre = n >= 2 && n <= 64 && dev.size() == n && d->deferred.empty() && !getenv("CE_NO_KMERGE");
+    if (oclk_pre && (rc = upload_oclocks(true))) return rc;
     h2 = std::make_unique<HostPhase>("   rd.d sync");
-    if (!dev.empty() && (rc = sync("state reader"))) return rc;  // (k_rdm_found wrote the counts into small)
+    // (also when no file is left for stage 1: stage 0 may still be running over the candidates)
+    if (!A0.empty() && (rc = sync("state reader"))) return rc;
     h2.reset();
-    // 3) the first N heads in position order are the entries: parse, chain, repeats, scan
+    // 3) the first N heads in position order are the entries (count in small[2i]); the tail words
+    //    (end, dbase, Dots of the last entry, flags after stage 1) in small[2n + 4i]
     ph = std::make_unique<HostPhase>("  rd: entries");
-    std::vector<size_t> dev2;
-    OrswotReadArgs* hA2 = hA + na;
+    std::vector<uint64_t> toff(n + 1, 0), eend(n, 0);
+    std::vector<size_t> dev3;
     for (size_t k = 0; k < dev.size(); k++) {
       const size_t i = dev[k];
       const uint32_t found = small[2 * i];
@@ -1969,47 +2044,35 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
         if ((rc = host_parse(i))) return rc;
         continue;
       }
-      OrswotReadArgs a = hA[k];
-      a.n_cand = x.n_entries;
-      a.tail_out = static_cast<uint32_t*>(host_dev_ptr(small)) + 2 * n + 4 * i;  // pinned: no download
-      hA2[dev2.size()] = a;
-      dev2.push_back(i);
-    }
-    if (!dev2.empty() &&
-        (e = launch_orswot_read_multi(s, nullptr, hA2, (uint32_t)dev2.size(), 1, nullptr, nullptr, nullptr, 0)))
-      return ctx->hip_fail(e, "state reader");
-    // every file's tail words (k_rdm_tile_scan wrote them into small)
-    if (!dev2.empty() && (rc = sync("state reader"))) return rc;
-    // 4) the deferred maps after the entries, on the host
-    ph = std::make_unique<HostPhase>("  rd: tails");
-    std::vector<uint64_t> toff(n + 1, 0), eend(n, 0);
-    std::vector<size_t> dev3;
-    std::vector<const OrswotReadArgs*> args_of(n, nullptr);
-    for (size_t k = 0; k < dev2.size(); k++) args_of[dev2[k]] = &hA2[k];
-    for (size_t i : dev2) {
       const uint32_t* tail = small + 2 * n + 4 * i;
-      eend[i] = ds[i].body + (uint64_t)tail[0];
+      eend[i] = x.body + (uint64_t)tail[0];
       if (tail[3] == 0 && tail[0] != 0xffffffffu && eend[i] <= len[i]) {
-        ds[i].n_dots = tail[1] + tail[2];
+        x.n_dots = tail[1] + tail[2];
         dev3.push_back(i);
       } else if ((decline_stage = 3) && (rc = host_parse(i))) {
         return rc;
       }
     }
+    // 4) the deferred maps after the entries, on the host: from the pinned window (k_rdm_tail),
+    //    or downloaded when longer
+    ph = std::make_unique<HostPhase>("  rd: tails");
     uint64_t ttot = 0;
-    for (size_t i : dev3) { toff[i] = ttot; ttot += len[i] - eend[i]; }
-    if ((e = d->rd_host.reserve(ttot + 64))) return ctx->hip_fail(e, "state tail");
-    hb = d->rd_host.as<uint8_t>();
-    {
+    for (size_t i : dev3)
+      if (len[i] - eend[i] > kTailWin) { toff[i] = ttot; ttot += len[i] - eend[i]; }
+    if (ttot) {
+      if ((e = d->rd_host.reserve(ttot + 64))) return ctx->hip_fail(e, "state tail");
+      hb = d->rd_host.as<uint8_t>();
       std::vector<GatherRange> gr;
       for (size_t i : dev3)
-        if (len[i] > eend[i]) gr.push_back({out + off[i] + eend[i], toff[i], len[i] - eend[i]});
+        if (len[i] - eend[i] > kTailWin) gr.push_back({out + off[i] + eend[i], toff[i], len[i] - eend[i]});
       if ((e = gather_download(d, s, hb, gr, ttot))) return ctx->hip_fail(e, "state tail");
+      if ((rc = sync("state tail"))) return rc;
     }
-    if (ttot && (rc = sync("state tail"))) return rc;
     std::vector<size_t> dev4;
     for (size_t i : dev3) {
-      if (parse_state_tail(hb + toff[i], len[i] - eend[i], &ds[i].hs)) {
+      const uint64_t tl = len[i] - eend[i];
+      const uint8_t* tp = tl > kTailWin ? hb + toff[i] : tailh + (uint64_t)kTailWin * i;
+      if (parse_state_tail(tp, tl, &ds[i].hs)) {
         DevState& x = ds[i];
         x.od.clear();
         for (auto& y : x.hs.deferred) {
@@ -2022,31 +2085,10 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
         return rc;
       }
     }
-    // 5) (member, actor id, value) columns of every entry Dot; an actor outside the table (not
-    //    in the state's clock) flags the file for the host parser
+    // 5) the emitted (member, actor id, value) columns of every entry Dot; an actor outside the
+    //    table (not in the state's clock) flagged the file for the host parser (small[2i + 1])
     ph = std::make_unique<HostPhase>("  rd: emit");
-    if ((rc = table_upload(c))) return rc;
-    OrswotReadArgs* hA4 = hA + 2 * na;
-    for (size_t k = 0; k < dev4.size(); k++) {
-      const size_t i = dev4[k];
-      DevState& x = ds[i];
-      auto& b = d->rd[i];
-      if ((e = b[7].reserve(8ull * x.n_dots + 8)) || (e = b[8].reserve(4ull * x.n_dots + 4)) ||
-          (e = b[9].reserve(8ull * x.n_dots + 8)))
-        return ctx->hip_fail(e, "state reader");
-      OrswotReadArgs a = *args_of[i];
-      a.table = c->d_table.as<ActorSlot>();  // the table may have grown above
-      a.mask = c->cap - 1;
-      a.col_member = b[7].as<unsigned long long>();
-      a.col_actor = b[8].as<uint32_t>();
-      a.col_value = b[9].as<unsigned long long>();
-      hA4[k] = a;
-    }
-    if (!dev4.empty() &&
-        ((e = launch_orswot_read_multi(s, nullptr, hA4, (uint32_t)dev4.size(), 2, nullptr, nullptr, nullptr, 0)) ||
-         (e = hipMemcpyAsync(small, d->rd_misc.p, 8ull * n, hipMemcpyDeviceToHost, s))))
-      return ctx->hip_fail(e, "state reader");
-    if (!dev4.empty() && (rc = sync("state reader"))) return rc;
+    if ((rc = table_upload(c))) return rc;  // (the deferred maps' actors)
     for (size_t i : dev4) {
       if (small[2 * i + 1] == 0) {
         ds[i].device = true;
@@ -2070,28 +2112,8 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
   // (launch_ds_kmerge; the order-free form of the merges below)
   bool kway = n >= 2 && n <= 64 && d->deferred.empty() && !getenv("CE_NO_KMERGE");
   for (size_t i = 0; i < n && kway; i++) kway = ds[i].device && ds[i].od.empty();
-  // dense other-clocks in pinned memory, so the queued merges never wait on a pageable copy:
-  // actor-major at stride ostride for the k-way merge, file-major for the merges one by one
   const uint32_t ccap = d->clock_cap;
-  const uint32_t ostride = ds_oclock_stride((uint32_t)n);
-  const size_t oc_words = kway ? (size_t)ccap * ostride : (size_t)ccap * n;
-  if ((e = d->rd_clock.reserve(8ull * oc_words + 64))) return ctx->hip_fail(e, "merge");
-  auto* hclk = d->rd_clock.as<unsigned long long>();
-  if (kway) {
-    std::memset(hclk, 0, 8ull * oc_words);
-    for (size_t i = 0; i < n; i++)
-      for (auto& y : ds[i].oclock) hclk[(size_t)y.first * ostride + i] = y.second;
-  } else {
-    for (size_t i = 0; i < n; i++)
-      if (ds[i].device) {
-        std::memset(hclk + (size_t)ccap * i, 0, 8ull * ccap);
-        for (auto& y : ds[i].oclock) hclk[(size_t)ccap * i + y.first] = y.second;
-      }
-  }
-  // every file's dense other-clock in HBM with one copy
-  if ((e = d->rd_oclocks.reserve(8ull * oc_words + 64)) ||
-      (e = hipMemcpyAsync(d->rd_oclocks.p, hclk, 8ull * oc_words, hipMemcpyHostToDevice, s)))
-    return ctx->hip_fail(e, "merge");
+  if (!(kway && oclk_pre && oclk_cap == ccap) && (rc = upload_oclocks(kway))) return rc;
   if (kway) {
     HostPhase hk("  merge: k-way");
     if ((e = d->rd_args_h.reserve(n * sizeof(DsMergeSrc) + 64)) || (e = d->rd_args_d.reserve(n * sizeof(DsMergeSrc) + 64)))

@@ -95,10 +95,12 @@ size_t orswot_ser_tmp_bytes(uint32_t n);
 struct OrswotReadArgs {
   const uint8_t* s;
   uint64_t lo, hi;
-  uint32_t* n_cand_dev;  // stage 0: entry heads found
+  uint32_t* n_cand_dev;  // stage 0: entry heads found (pinned; stage 1: those from lo on)
+  uint32_t* skip;        // device word: stage 0 the heads found, stage 1 (k_rdm_skip) the heads
+                         // before lo (stage 0 runs with lo = 0, before the host knows lo)
   uint32_t cap;          // room in cand
   uint32_t n_cand;       // stage >= 1: the entries (the first n_cand heads; host-checked)
-  uint32_t* cand;        // entry heads in position order
+  uint32_t* cand;        // entry heads in position order (positions from the file's start)
   uint32_t* end;        // entry end (relative to lo), n_cand
   uint32_t* ndots;      // non-zero Dots per entry
   uint32_t* dbase;      // exclusive scan of ndots
@@ -107,7 +109,10 @@ struct OrswotReadArgs {
                                // words (all ones = empty; the last word counts all-ones members)
   uint32_t dset_mask;          // power of two minus one, >= 2 n_cand - 1
   uint32_t* tail_out;          // stage 1: end, dbase, ndots of the last entry and the flags word
-  uint32_t* flags;      // 1 non-canonical entry, 2 broken chain, 4 unknown actor, 8 repeated member
+  uint8_t* tail_host;          // stage 1: the bytes after the entries (the deferred map) when they
+  uint32_t tail_cap;           //   fit tail_cap (pinned; else the host downloads them)
+  uint32_t* flags;      // 1 non-canonical entry, 2 broken chain, 4 unknown actor, 8 repeated member,
+                        // 16 heads found outside [n_cand, cap] (stages 1-2 skip the file)
   const ActorSlot* table;
   uint32_t mask;
   unsigned long long* col_member;
@@ -123,7 +128,9 @@ struct RdFiles {
 // the reader over nf files at once (d_args / h_args: the same descriptors in HBM and on the
 // host): stage 0 = entry heads in position order into `cand` and their count into *n_cand_dev
 // (chunk_cnt / chunk_scan: sum of nchunks + 1 words); 1 = entry parse, chain check, repeated
-// members, Dot scan and tail words; 2 = emit columns
+// members, Dot scan, tail words and tail bytes; 2 = emit columns, then each file's flags word into
+// n_cand_dev[1].  The stages are queued back to back: a file whose earlier stage failed is skipped
+// by the later ones (its flags word), so one host wait covers all three
 hipError_t launch_orswot_read_multi(hipStream_t s, const OrswotReadArgs* d_args, const OrswotReadArgs* h_args,
                                     uint32_t nf, int stage, uint32_t* chunk_cnt, uint32_t* chunk_scan,
                                     void* tmp, size_t tmp_bytes);

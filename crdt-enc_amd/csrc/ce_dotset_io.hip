@@ -452,17 +452,59 @@ __global__ void __launch_bounds__(kB) k_rdm_write(RdFiles fa, const uint32_t* sc
   }
 }
 
+// the heads found; a count outside [n_cand, cap] (fewer heads than entries, or cand overflowed)
+// flags the file so that stages 1 and 2, queued behind without a host wait, skip it
 __global__ void k_rdm_found(RdFiles fa, const uint32_t* scan, uint32_t nf) {
   const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f < nf) *fa.f[f].n_cand_dev = scan[fa.f[f].chunk0 + fa.f[f].nchunks] - scan[fa.f[f].chunk0];
+  if (f >= nf) return;
+  const OrswotReadArgs& a = fa.f[f];
+  const uint32_t found = scan[a.chunk0 + a.nchunks] - scan[a.chunk0];
+  *a.n_cand_dev = found;
+  *a.skip = found;
+}
+
+// stage 1's first launch, block per file, once the host knows where the entries start (lo): the
+// heads before lo (the clocks' own "dots" maps: a couple) are skipped, the count from lo on goes
+// to the host, and a count outside [n_cand, cap] flags the file for the later stages to skip
+__global__ void __launch_bounds__(256) k_rdm_skip(RdFiles fa) {
+  const OrswotReadArgs a = fa.f[blockIdx.x];
+  const uint32_t found = *reinterpret_cast<volatile const uint32_t*>(a.skip);
+  const uint32_t m = min(found, a.cap);
+  const uint32_t t = threadIdx.x;
+  const int before = __syncthreads_count(t < m && (uint64_t)a.cand[t] < a.lo);
+  if (t != 0) return;
+  uint32_t k = (uint32_t)before;
+  if (k == 256u && m > 256u) {  // (many heads before lo: binary search the rest)
+    uint32_t l = 256u, h = m;
+    while (l < h) {
+      const uint32_t mid = (l + h) / 2;
+      if ((uint64_t)a.cand[mid] < a.lo) l = mid + 1;
+      else h = mid;
+    }
+    k = l;
+  }
+  *a.skip = k;
+  *a.n_cand_dev = found - k;
+  if (found - k < a.n_cand || found > a.cap) atomicOr(a.flags, 16u);
+}
+
+__device__ __forceinline__ bool rdm_skip(const OrswotReadArgs& a) {
+  return (*reinterpret_cast<volatile const uint32_t*>(a.flags) & 16u) != 0;
+}
+
+// entry i's head, relative to lo (stage 1 on: the heads before lo skipped)
+__device__ __forceinline__ uint32_t rdm_head(const OrswotReadArgs& a, uint32_t sk, uint32_t i) {
+  return a.cand[sk + i] - (uint32_t)a.lo;
 }
 
 __global__ void k_rdm_entry(RdFiles fa) {
   const OrswotReadArgs a = fa.f[blockIdx.y];
+  if (rdm_skip(a)) return;
+  const uint32_t sk = *a.skip;
   const uint8_t* base = a.s + a.lo;
   const uint8_t* end = a.s + a.hi;
   for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < a.n_cand; i += gridDim.x * kB) {
-    const uint8_t* p = base + a.cand[i] + 6;
+    const uint8_t* p = base + rdm_head(a, sk, i) + 6;
     uint32_t k;
     bool ok = true;
     if ((p[0] & 0xf0) == 0x80) { k = p[0] & 15u; p += 1; }
@@ -495,10 +537,12 @@ __global__ void k_rdm_entry(RdFiles fa) {
 // here and filled by k_rdm_dups, the next launch
 __global__ void k_rdm_chain(RdFiles fa) {
   const OrswotReadArgs a = fa.f[blockIdx.y];
+  if (rdm_skip(a)) return;
+  const uint32_t sk = *a.skip;
   const uint8_t* base = a.s + a.lo;
   for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < a.n_cand; i += gridDim.x * kB) {
     const uint32_t start = i == 0 ? 0u : a.end[i - 1];
-    const uint32_t head = a.cand[i];
+    const uint32_t head = rdm_head(a, sk, i);
     unsigned long long m = 0;
     const uint32_t ul = start <= head ? rd_uint(base + start, base + head, &m) : 0u;
     if (!ul || start + ul != head || a.end[i] == 0xffffffffu) atomicOr(a.flags, 2u);
@@ -509,6 +553,7 @@ __global__ void k_rdm_chain(RdFiles fa) {
 
 __global__ void k_rdm_dups(RdFiles fa) {
   const OrswotReadArgs a = fa.f[blockIdx.y];
+  if (rdm_skip(a)) return;
   constexpr unsigned long long kEmpty = ~0ull;
   for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < a.n_cand; i += gridDim.x * kB) {
     const unsigned long long m = a.member[i];
@@ -538,7 +583,7 @@ __global__ void __launch_bounds__(kB) k_rdm_tile_sums(RdFiles fa) {
   __shared__ uint32_t part[kB / 64];
   const OrswotReadArgs a = fa.f[blockIdx.y];
   const uint32_t t0 = blockIdx.x * kScanTile;
-  if (t0 >= a.n_cand) return;
+  if (t0 >= a.n_cand || rdm_skip(a)) return;
   uint32_t v = 0;
 #pragma unroll
   for (int q = 0; q < 8; q++) {
@@ -554,7 +599,7 @@ __global__ void __launch_bounds__(kB) k_rdm_tile_scan(RdFiles fa) {
   __shared__ uint32_t run[kB];
   const OrswotReadArgs a = fa.f[blockIdx.y];
   const uint32_t t0 = blockIdx.x * kScanTile;
-  if (t0 >= a.n_cand) return;
+  if (t0 >= a.n_cand || rdm_skip(a)) return;
   // the tile's base: the totals of the tiles before it
   const uint32_t* tsum = reinterpret_cast<const uint32_t*>(a.msort);
   uint32_t b = 0;
@@ -594,11 +639,26 @@ __global__ void __launch_bounds__(kB) k_rdm_tile_scan(RdFiles fa) {
   }
 }
 
+// the bytes after the last entry (the deferred map) into pinned memory, block per file, when the
+// entries parsed and the tail fits the window
+__global__ void __launch_bounds__(kB) k_rdm_tail(RdFiles fa) {
+  const OrswotReadArgs a = fa.f[blockIdx.x];
+  if (!a.tail_host || *reinterpret_cast<volatile const uint32_t*>(a.flags)) return;
+  const uint32_t e = a.end[a.n_cand - 1];
+  if (e == 0xffffffffu || a.lo + e > a.hi || a.hi - (a.lo + e) > a.tail_cap) return;
+  const uint8_t* src = a.s + a.lo + e;
+  const uint32_t n = (uint32_t)(a.hi - (a.lo + e));
+  for (uint32_t j = threadIdx.x; j < n; j += kB) a.tail_host[j] = src[j];
+}
+
+// emit: only files whose entries all parsed (flags 0 after stage 1; the host checks the rest)
 __global__ void k_rdm_emit(RdFiles fa) {
   const OrswotReadArgs a = fa.f[blockIdx.y];
+  if (*reinterpret_cast<volatile const uint32_t*>(a.flags)) return;
+  const uint32_t sk = *a.skip;
   const uint8_t* base = a.s + a.lo;
   for (uint32_t i = blockIdx.x * kB + threadIdx.x; i < a.n_cand; i += gridDim.x * kB) {
-    const uint8_t* p = base + a.cand[i] + 6;
+    const uint8_t* p = base + rdm_head(a, sk, i) + 6;
     uint32_t k;
     if ((p[0] & 0xf0) == 0x80) { k = p[0] & 15u; p += 1; }
     else if (p[0] == 0xde) { k = ((uint32_t)p[1] << 8) | p[2]; p += 3; }
@@ -623,6 +683,12 @@ __global__ void k_rdm_emit(RdFiles fa) {
       p += 18 + ul;
     }
   }
+}
+
+// each file's flags word next to its head count in pinned memory (after the emit)
+__global__ void k_rdm_flags(RdFiles fa, uint32_t nf) {
+  const uint32_t f = threadIdx.x;
+  if (f < nf) fa.f[f].n_cand_dev[1] = *fa.f[f].flags;
 }
 
 }  // namespace
@@ -665,6 +731,7 @@ hipError_t launch_orswot_read_multi(hipStream_t s, const OrswotReadArgs* /*d_arg
     uint32_t gx = 1;
     for (uint32_t f = c0; f < c0 + k; f++) gx = std::max(gx, nblk(std::max<uint64_t>(h_args[f].n_cand, h_args[f].dset_mask + 2ull)));
     if (stage == 1) {
+      hipLaunchKernelGGL(k_rdm_skip, dim3(k), dim3(256), 0, s, r);
       hipLaunchKernelGGL(k_rdm_entry, dim3(gx, k), dim3(kB), 0, s, r);
       hipLaunchKernelGGL(k_rdm_chain, dim3(gx, k), dim3(kB), 0, s, r);
       hipLaunchKernelGGL(k_rdm_dups, dim3(gx, k), dim3(kB), 0, s, r);
@@ -672,8 +739,10 @@ hipError_t launch_orswot_read_multi(hipStream_t s, const OrswotReadArgs* /*d_arg
       for (uint32_t f = c0; f < c0 + k; f++) gt = std::max(gt, (h_args[f].n_cand + kScanTile - 1) / kScanTile);
       hipLaunchKernelGGL(k_rdm_tile_sums, dim3(gt, k), dim3(kB), 0, s, r);
       hipLaunchKernelGGL(k_rdm_tile_scan, dim3(gt, k), dim3(kB), 0, s, r);
+      hipLaunchKernelGGL(k_rdm_tail, dim3(k), dim3(kB), 0, s, r);
     } else {
       hipLaunchKernelGGL(k_rdm_emit, dim3(gx, k), dim3(kB), 0, s, r);
+      hipLaunchKernelGGL(k_rdm_flags, dim3(1), dim3(64), 0, s, r, k);
     }
   }
   return hipGetLastError();

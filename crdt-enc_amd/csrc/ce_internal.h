@@ -95,6 +95,28 @@ inline hipError_t stream_wait(hipStream_t s) {
   return e;
 }
 
+// A point on `s` to wait for later while the work queued after it keeps running (stream_mark),
+// and the wait (mark_wait: the same polling as stream_wait).  One mark per thread and device is
+// live at a time.
+inline hipError_t stream_mark(hipStream_t s, hipEvent_t* out) {
+  thread_local hipEvent_t evs[64] = {};
+  int dev = 0;
+  hipError_t e;
+  if ((e = hipGetDevice(&dev))) return e;
+  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+  hipEvent_t& ev = evs[dev];
+  if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming))) return e;
+  *out = ev;
+  return hipEventRecord(ev, s);
+}
+
+inline hipError_t mark_wait(hipEvent_t ev) {
+  hipError_t e;
+  for (unsigned i = 0; (e = hipEventQuery(ev)) == hipErrorNotReady; i++)
+    if (i >= 32) sched_yield();
+  return e;
+}
+
 struct KeyRef {
   const uint8_t* version;  // 16
   const uint8_t* key;

@@ -424,6 +424,40 @@ def test_orswot_state_reader_forms(ctx, seed):
                 os.environ.pop("CE_HOST_STATES", None)
 
 
+def test_orswot_state_reader_long_deferred(ctx):
+    """A state whose deferred map is longer than the reader's 4 KiB pinned tail window
+    (k_rdm_tail) is read on the device with the map downloaded instead; beside it a state with
+    an empty map takes the window.  Both give the oracle's state."""
+    rng = random.Random(77)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 24)
+    part = C.Core("orswot")
+    files = G.adversarial_orswot(rng, actors, 2, 40, 60)
+    # removals far past every add: each stays deferred under its own clock (~9 KiB of map)
+    files[actors[0]].append([("Rm", C.VClock({actors[j % 24]: 1000 + j}), [j % 60, (7 * j) % 60])
+                             for j in range(300)])
+    acts, clears, fa, fv = G.batch(files, "orswot", APP)
+    f = [CORE + C._oc.cryptor_encrypt(key, bytes(24), c)[1] for c in clears]
+    assert part.read_remote_ops(key, [APP], f, [acts[i] for i in fa], fv)[0] == 0
+    big = part.serialize()
+    assert len(_raw_deferred(big)) > 4096
+    small_part = C.Core("orswot")
+    wf = G.well_formed_orswot(rng, actors[:4], 2, 6, 30)[0]
+    acts, clears, fa, fv = G.batch(wf, "orswot", APP)
+    f = [CORE + C._oc.cryptor_encrypt(key, bytes(24), c)[1] for c in clears]
+    assert small_part.read_remote_ops(key, [APP], f, [acts[i] for i in fa], fv)[0] == 0
+    for bodies in ([big], [small_part.serialize(), big]):
+        sf = seal_files(ctx, key, [APP + b for b in bodies])
+        oc = C.Core("orswot")
+        assert oc.read_remote_states(key, [APP], sf)[0] == 0
+        core = new_core(ctx, "orswot", key)
+        rc, st = core.ingest_states(sf)
+        assert rc == 0 and list(st) == [0] * len(bodies)
+        assert core.state_bytes() == oc.serialize()
+        assert core.path_count("states_device_read") == len(bodies)
+        core.close()
+
+
 def test_orswot_device_compaction_bytes(ctx):
     """Core::compact for Orswot writes the clear text on the device (ce_dotset_io.hip writer):
     the sealed file opens to exactly data_version || the canonical StateWrapper (host writer ==
