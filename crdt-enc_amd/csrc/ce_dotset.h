@@ -228,6 +228,8 @@ struct DsMergeSrc {
   const unsigned long long* value;
   uint32_t n;
   uint32_t* slot;  // optional, n words: k_ds_kput records each pair's slot for k_ds_khold
+  const uint32_t* n_dev;  // optional: the pair count is n_dev[1] + n_dev[2] (the reader's device
+                          // tail words), n only sizes the grid
 };
 // Orswot::merge of nf state files at once (no deferred removals on any side): d_src / h_src the
 // same descriptors in HBM and on the host, oclocks = the files' dense clocks actor-major
@@ -235,7 +237,8 @@ struct DsMergeSrc {
 // hold = a zeroed u64 per pair slot (left zeroed); live[0..1] = live / used pairs after
 hipError_t launch_ds_kmerge(hipStream_t s, DsTables t, const DsMergeSrc* d_src, const DsMergeSrc* h_src, uint32_t nf,
                             unsigned long long* clock, const unsigned long long* oclocks, uint32_t ccap, uint32_t ostride,
-                            unsigned long long* hold, uint32_t* pub_dst = nullptr);  // pub_dst: live[0..5) -> pinned
+                            unsigned long long* hold, uint32_t* pub_dst = nullptr,  // pub_dst: live[0..5) -> pinned
+                            const uint32_t* go = nullptr);  // go: every kernel does nothing unless *go
 // one column partial of the multi-GPU exchange (ds_merge_columns_device): its actor column and
 // clock remapped to the receiving core's ids
 struct DsColsRemap {

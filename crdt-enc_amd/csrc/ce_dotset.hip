@@ -1361,13 +1361,24 @@ constexpr uint32_t kMergeInline = 16;
 struct DsMergeSrcs {
   DsMergeSrc f[kMergeInline];
   uint32_t f0;  // the first file's index in the merge (its hold bit)
+  const uint32_t* go;  // optional: nothing happens unless *go (a merge queued before the host
+                       // knows that every file was read on the device, ds_merge_states_device)
 };
 
+__device__ __forceinline__ bool kmerge_off(const uint32_t* go) {
+  return go && *reinterpret_cast<volatile const uint32_t*>(go) == 0;
+}
+__device__ __forceinline__ uint32_t kmerge_n(const DsMergeSrc& x) {
+  return x.n_dev ? x.n_dev[1] + x.n_dev[2] : x.n;
+}
+
 __global__ void __launch_bounds__(kBlock) k_ds_kput(DsTables t, DsMergeSrcs src) {
+  if (kmerge_off(src.go)) return;
   const DsMergeSrc x = src.f[blockIdx.y];
   if (src.f0 == 0 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2) t.live[threadIdx.x] = 0;  // k_ds_kfinal counts
   if (src.f0 == 0 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 2) t.live[4] = 0;
-  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < x.n; i += gridDim.x * kBlock) {
+  const uint32_t n = kmerge_n(x);
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
     const unsigned long long h = member_find(t, x.member[i], true);
     const unsigned long long b = h == kDsEmpty ? kDsEmpty : pair_find(t, pair_key(h, x.actor[i]), true);
     if (b != kDsEmpty) atomicMax(&t.oth[b], x.value[i]);
@@ -1376,9 +1387,11 @@ __global__ void __launch_bounds__(kBlock) k_ds_kput(DsTables t, DsMergeSrcs src)
 }
 
 __global__ void __launch_bounds__(kBlock) k_ds_khold(DsTables t, DsMergeSrcs src, unsigned long long* hold) {
+  if (kmerge_off(src.go)) return;
   const DsMergeSrc x = src.f[blockIdx.y];
   const uint32_t fb = src.f0 + blockIdx.y;
-  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < x.n; i += gridDim.x * kBlock) {
+  const uint32_t n = kmerge_n(x);
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
     unsigned long long b;
     if (x.slot) {  // recorded by k_ds_kput: no second probe of the member and pair tables
       const uint32_t r = x.slot[i];
@@ -1400,7 +1413,8 @@ __global__ void __launch_bounds__(kBlock) k_ds_khold(DsTables t, DsMergeSrcs src
 // loads (file-major, eight gathers from lines 32 KiB apart took ~70 us at C3's 8 state files)
 __global__ void __launch_bounds__(kBlock) k_ds_kfinal(DsTables t, const unsigned long long* clock,
                                                       const unsigned long long* oclocks, uint32_t ostride,
-                                                      uint32_t nf, unsigned long long* hold) {
+                                                      uint32_t nf, unsigned long long* hold, const uint32_t* go) {
+  if (kmerge_off(go)) return;
   const uint32_t cap = t.pmask + 1;
   uint32_t n_used = 0, n_live = 0, n_mem = primary_used(t, blockIdx.x, gridDim.x);
   // kKQ slots per lane and trip, every load of a trip issued before any is used
@@ -1487,7 +1501,8 @@ __global__ void __launch_bounds__(kBlock) k_ds_kfinal(DsTables t, const unsigned
 // (pub_dst: the k-way merge's live counters, final since k_ds_kfinal, into the caller's pinned memory)
 __global__ void k_ds_kclock(unsigned long long* clock, const unsigned long long* oclocks, uint32_t ccap,
                             uint32_t ostride, uint32_t nf, const uint32_t* pub_src, uint32_t* pub_dst,
-                            uint32_t pub_words) {
+                            uint32_t pub_words, const uint32_t* go) {
+  if (kmerge_off(go)) return;
   if (pub_dst && blockIdx.x == 0 && threadIdx.x < pub_words) pub_dst[threadIdx.x] = pub_src[threadIdx.x];
   for (uint32_t a = blockIdx.x * kBlock + threadIdx.x; a < ccap; a += gridDim.x * kBlock) {
     unsigned long long v = clock[a];
@@ -2008,7 +2023,7 @@ hipError_t launch_ds_merge_finalize(hipStream_t s, DsTables t, const unsigned lo
 
 hipError_t launch_ds_kmerge(hipStream_t s, DsTables t, const DsMergeSrc* d_src, const DsMergeSrc* h_src, uint32_t nf,
                             unsigned long long* clock, const unsigned long long* oclocks, uint32_t ccap, uint32_t ostride,
-                            unsigned long long* hold, uint32_t* pub_dst) {
+                            unsigned long long* hold, uint32_t* pub_dst, const uint32_t* go) {
   (void)d_src;
   uint32_t nmax = 0;
   for (uint32_t f = 0; f < nf; f++) nmax = h_src[f].n > nmax ? h_src[f].n : nmax;
@@ -2016,6 +2031,7 @@ hipError_t launch_ds_kmerge(hipStream_t s, DsTables t, const DsMergeSrc* d_src, 
   auto srcs = [&](uint32_t c0) {
     DsMergeSrcs m{};
     m.f0 = c0;
+    m.go = go;
     for (uint32_t i = 0; i < kMergeInline && c0 + i < nf; i++) m.f[i] = h_src[c0 + i];
     return m;
   };
@@ -2024,9 +2040,9 @@ hipError_t launch_ds_kmerge(hipStream_t s, DsTables t, const DsMergeSrc* d_src, 
   for (uint32_t c0 = 0; c0 < nf; c0 += kMergeInline)
     hipLaunchKernelGGL(k_ds_khold, dim3(gx, std::min(kMergeInline, nf - c0)), dim3(kBlock), 0, s, t, srcs(c0), hold);
   hipLaunchKernelGGL(k_ds_kfinal, dim3(blocks_for((uint64_t)t.pmask + 1, 1024)), dim3(kBlock), 0, s, t, clock, oclocks,
-                     ostride, nf, hold);
+                     ostride, nf, hold, go);
   hipLaunchKernelGGL(k_ds_kclock, dim3(std::max<uint32_t>(1, blocks_for(ccap))), dim3(kBlock), 0, s, clock, oclocks,
-                     ccap, ostride, nf, t.live, pub_dst, 5u);
+                     ccap, ostride, nf, t.live, pub_dst, 5u, go);
   return hipGetLastError();
 }
 

@@ -1856,8 +1856,9 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
   // every file's in HBM with one copy
   const uint32_t ostride = ds_oclock_stride((uint32_t)n);
   unsigned long long* hclk = nullptr;
-  bool oclk_pre = false;
+  bool oclk_pre = false, spec = false;
   uint32_t oclk_cap = 0;
+  hipEvent_t pre_ev = nullptr;  // (set: the upload goes on the side stream, after this point of s)
   auto upload_oclocks = [&](bool kway) -> int {
     const uint32_t ccap = oclk_cap = d->clock_cap;
     const size_t oc_words = kway ? (size_t)ccap * ostride : (size_t)ccap * n;
@@ -1874,8 +1875,16 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
           for (auto& y : ds[i].oclock) hclk[(size_t)ccap * i + y.first] = y.second;
         }
     }
-    if ((e = d->rd_oclocks.reserve(8ull * oc_words + 64)) ||
-        (e = hipMemcpyAsync(d->rd_oclocks.p, hclk, 8ull * oc_words, hipMemcpyHostToDevice, s)))
+    if ((e = d->rd_oclocks.reserve(8ull * oc_words + 64))) return ctx->hip_fail(e, "merge");
+    if (pre_ev) {  // beside the reader's stages (an SDMA copy); s waits for it before the merge
+      if ((e = hipStreamWaitEvent(ctx->side, pre_ev, 0)) ||
+          (e = hipMemcpyAsync(d->rd_oclocks.p, hclk, 8ull * oc_words, hipMemcpyHostToDevice, ctx->side)) ||
+          (e = hipEventRecord(ctx->up_ev, ctx->side)) || (e = hipStreamWaitEvent(s, ctx->up_ev, 0)))
+        return ctx->hip_fail(e, "merge");
+      pre_ev = nullptr;
+      return CE_OK;
+    }
+    if ((e = hipMemcpyAsync(d->rd_oclocks.p, hclk, 8ull * oc_words, hipMemcpyHostToDevice, s)))
       return ctx->hip_fail(e, "merge");
     return CE_OK;
   };
@@ -1930,7 +1939,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     uint32_t* chunk_cnt = d->rd_chunks.as<uint32_t>();
     uint32_t* chunk_scan = chunk_cnt + nch + 1;
     if (!A0.empty() &&
-        ((e = launch_fill(s, FillArgs{{FillRange{chunk_cnt + nch, 1, 0u}, FillRange{d->rd_misc.as<uint32_t>(), 2ull * n, 0u}},
+        ((e = launch_fill(s, FillArgs{{FillRange{chunk_cnt + nch, 1, 0u}, FillRange{d->rd_misc.as<uint32_t>(), 6ull * n + 1, 0u}},
                                       2, nullptr})) ||
          (e = launch_orswot_read_multi(s, nullptr, A0.data(), (uint32_t)A0.size(), 0, chunk_cnt, chunk_scan, d->rd_tmp.p,
                                        d->rd_tmp.cap))))
@@ -1991,12 +2000,21 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     // non-zero Dot takes >= 19 of them).
     if ((e = d->rd_tailh.reserve((uint64_t)kTailWin * n + 64))) return ctx->hip_fail(e, "state reader");
     uint8_t* tailh = d->rd_tailh.as<uint8_t>();
+    // every file still on the device path, no deferred removal held: the k-way merge is queued
+    // behind stage 2 before the host wait, on the reader's device words (pair counts, a go flag
+    // that is 1 only when every file was read without a flag and with an empty deferred map --
+    // otherwise its kernels do nothing and the host merges below as before)
+    spec = n >= 2 && n <= kRdInline && dev.size() == n && d->deferred.empty() && !getenv("CE_NO_KMERGE") &&
+           !getenv("CE_NO_KMERGE_EARLY");
+    uint32_t* misc = d->rd_misc.as<uint32_t>();
     std::vector<OrswotReadArgs> hA(dev.size());
+    std::vector<uint64_t> dmax(n, 0);
     for (size_t k = 0; k < dev.size(); k++) {
       const size_t i = dev[k];
       DevState& x = ds[i];
       const uint64_t ne = x.n_entries;
       const uint64_t dots_max = (x.len - std::min<uint64_t>(x.len, x.body)) / 19 + 1;
+      dmax[i] = dots_max;
       auto& b = d->rd[i];
       if ((e = b[2].reserve(4ull * ne + 64)) || (e = b[3].reserve(4ull * ne + 64)) ||
           (e = b[4].reserve(4ull * ne + 64)) || (e = b[5].reserve(8ull * ne + 64)) ||
@@ -2010,6 +2028,11 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
       a.col_member = b[7].as<unsigned long long>();
       a.col_actor = b[8].as<uint32_t>();
       a.col_value = b[9].as<unsigned long long>();
+      a.tail_dev = misc + 2 * n + 4 * i;
+      if (spec && k == 0) {
+        a.go = misc + 6 * n;
+        a.go_host = static_cast<uint32_t*>(host_dev_ptr(small)) + 10 * n;
+      }
       hA[k] = a;
     }
     if ((rc = table_upload(c)) || (rc = ensure_clock(c))) return rc;
@@ -2019,6 +2042,14 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     }
     h2 = std::make_unique<HostPhase>("   rd.c launch");
     const uint32_t nd = (uint32_t)dev.size();
+    if (nd == n && n >= 2 && n <= 64 && d->deferred.empty()) {  // (the other-clocks' upload, below)
+      if ((!ctx->side && (e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking))) ||
+          (!ctx->up_ev && (e = hipEventCreateWithFlags(&ctx->up_ev, hipEventDisableTiming))) ||
+          (!ctx->side_ev && (e = hipEventCreateWithFlags(&ctx->side_ev, hipEventDisableTiming))) ||
+          (e = hipEventRecord(ctx->side_ev, s)))
+        return ctx->hip_fail(e, "state reader");
+      pre_ev = ctx->side_ev;
+    }
     if (nd && ((e = launch_orswot_read_multi(s, nullptr, hA.data(), nd, 1, nullptr, nullptr, nullptr, 0)) ||
                (e = launch_orswot_read_multi(s, nullptr, hA.data(), nd, 2, nullptr, nullptr, nullptr, 0))))
       return ctx->hip_fail(e, "state reader");
@@ -2026,9 +2057,31 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
     // every file is still on the device path (else they are rebuilt for the merges one by one)
     oclk_pre = n >= 2 && n <= 64 && dev.size() == n && d->deferred.empty() && !getenv("CE_NO_KMERGE");
     if (oclk_pre && (rc = upload_oclocks(true))) return rc;
+    // the reader's wait is for the stages only, not for the merge queued behind them
+    hipEvent_t stages_ev = nullptr;
+    if (!A0.empty() && (e = stream_mark(s, &stages_ev))) return ctx->hip_fail(e, "state reader");
+    if (spec) {
+      uint64_t bound = 0;
+      for (size_t i = 0; i < n; i++) bound += dmax[i];
+      if ((rc = ensure_pairs(c, bound))) return rc;
+      if ((e = d->cx_slot.reserve(4 * bound + 64))) return ctx->hip_fail(e, "merge");
+      std::vector<DsMergeSrc> hs(n);
+      for (size_t i = 0, q = 0; i < n; q += dmax[i], i++) {
+        auto& b = d->rd[i];
+        hs[i] = DsMergeSrc{b[7].as<unsigned long long>(), b[8].as<uint32_t>(), b[9].as<unsigned long long>(),
+                           (uint32_t)dmax[i], d->cx_slot.as<uint32_t>() + q, misc + 2 * n + 4 * i};
+      }
+      d->scratch_dirty = true;
+      if ((e = launch_ds_kmerge(s, tables(d), nullptr, hs.data(), (uint32_t)n, d->clock.as<unsigned long long>(),
+                                d->rd_oclocks.as<unsigned long long>(), d->clock_cap, ostride,
+                                d->hold.as<unsigned long long>(),
+                                static_cast<uint32_t*>(host_dev_ptr(d->h_cnt.as<uint32_t>() + 56)), misc + 6 * n)))
+        return ctx->hip_fail(e, "merge");
+      d->scratch_dirty = false;  // (k_ds_kfinal cleared oth / hold, or nothing ran)
+    }
     h2 = std::make_unique<HostPhase>("   rd.d sync");
     // (also when no file is left for stage 1: stage 0 may still be running over the candidates)
-    if (!A0.empty() && (rc = sync("state reader"))) return rc;
+    if (!A0.empty() && (e = mark_wait(stages_ev))) return ctx->hip_fail(e, "state reader");
     h2.reset();
     // 3) the first N heads in position order are the entries (count in small[2i]); the tail words
     //    (end, dbase, Dots of the last entry, flags after stage 1) in small[2n + 4i]
@@ -2103,38 +2156,43 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
   if (status_out) std::memcpy(status_out, st, n * 4);
   if (first != CE_OK) return first;  // nothing merged (lib.rs:431-456)
   HostPhase hp("states: merge");
-  uint64_t dev_dots = 0;
-  for (size_t i = 0; i < n; i++)
-    if (ds[i].device) dev_dots += ds[i].n_dots;
-  if ((rc = ensure_pairs(c, dev_dots))) return rc;
-  uint32_t* live = small + 6 * n;
   // every file read on the device and no deferred removal anywhere: all merges in one pass
   // (launch_ds_kmerge; the order-free form of the merges below)
   bool kway = n >= 2 && n <= 64 && d->deferred.empty() && !getenv("CE_NO_KMERGE");
   for (size_t i = 0; i < n && kway; i++) kway = ds[i].device && ds[i].od.empty();
+  const bool early = spec && small[10 * n] != 0;  // the k-way merge queued before the wait ran
+  if (early && !kway) return ctx->fail(CE_ERR_DEVICE, "state reader: early merge for a declined file");
+  uint64_t dev_dots = 0;
+  for (size_t i = 0; i < n; i++)
+    if (ds[i].device) dev_dots += ds[i].n_dots;
+  if (!early && (rc = ensure_pairs(c, dev_dots))) return rc;
+  uint32_t* live = small + 6 * n;
   const uint32_t ccap = d->clock_cap;
-  if (!(kway && oclk_pre && oclk_cap == ccap) && (rc = upload_oclocks(kway))) return rc;
+  if (!early && !(kway && oclk_pre && oclk_cap == ccap) && (rc = upload_oclocks(kway))) return rc;
+  if (early) c->path_counts["states_kway_early"]++;
   if (kway) {
     HostPhase hk("  merge: k-way");
-    if ((e = d->rd_args_h.reserve(n * sizeof(DsMergeSrc) + 64)) || (e = d->rd_args_d.reserve(n * sizeof(DsMergeSrc) + 64)))
-      return ctx->hip_fail(e, "merge");
-    uint64_t dots = 0;
-    for (size_t i = 0; i < n; i++) dots += ds[i].n_dots;
-    if ((e = d->cx_slot.reserve(4 * dots + 64))) return ctx->hip_fail(e, "merge");
-    auto* hs = d->rd_args_h.as<DsMergeSrc>();
-    for (size_t i = 0, q = 0; i < n; q += ds[i].n_dots, i++) {
-      auto& b = d->rd[i];
-      hs[i] = DsMergeSrc{b[7].as<unsigned long long>(), b[8].as<uint32_t>(), b[9].as<unsigned long long>(), ds[i].n_dots,
-                         d->cx_slot.as<uint32_t>() + q};
+    if (!early) {  // (else queued before the reader's wait, on its device words)
+      if ((e = d->rd_args_h.reserve(n * sizeof(DsMergeSrc) + 64)) || (e = d->rd_args_d.reserve(n * sizeof(DsMergeSrc) + 64)))
+        return ctx->hip_fail(e, "merge");
+      uint64_t dots = 0;
+      for (size_t i = 0; i < n; i++) dots += ds[i].n_dots;
+      if ((e = d->cx_slot.reserve(4 * dots + 64))) return ctx->hip_fail(e, "merge");
+      auto* hs = d->rd_args_h.as<DsMergeSrc>();
+      for (size_t i = 0, q = 0; i < n; q += ds[i].n_dots, i++) {
+        auto& b = d->rd[i];
+        hs[i] = DsMergeSrc{b[7].as<unsigned long long>(), b[8].as<uint32_t>(), b[9].as<unsigned long long>(), ds[i].n_dots,
+                           d->cx_slot.as<uint32_t>() + q};
+      }
+      // no host wait: the merged counts land in pinned memory for ds_settle (the next ingest's
+      // first wait), like a fold's
+      d->scratch_dirty = true;
+      if ((e = launch_ds_kmerge(s, tables(d), nullptr, hs, (uint32_t)n,
+                                d->clock.as<unsigned long long>(), d->rd_oclocks.as<unsigned long long>(), ccap, ostride,
+                                d->hold.as<unsigned long long>(),
+                                static_cast<uint32_t*>(host_dev_ptr(d->h_cnt.as<uint32_t>() + 56)))))
+        return ctx->hip_fail(e, "merge");
     }
-    // no host wait: the merged counts land in pinned memory for ds_settle (the next ingest's
-    // first wait), like a fold's
-    d->scratch_dirty = true;
-    if ((e = launch_ds_kmerge(s, tables(d), nullptr, hs, (uint32_t)n,
-                              d->clock.as<unsigned long long>(), d->rd_oclocks.as<unsigned long long>(), ccap, ostride,
-                              d->hold.as<unsigned long long>(),
-                              static_cast<uint32_t*>(host_dev_ptr(d->h_cnt.as<uint32_t>() + 56)))))
-      return ctx->hip_fail(e, "merge");
     c->path_counts["states_kway_merge"]++;
     d->scratch_dirty = false;  // k_ds_kfinal cleared oth / hold
     d->settle_pending = true;

@@ -109,6 +109,11 @@ struct OrswotReadArgs {
                                // words (all ones = empty; the last word counts all-ones members)
   uint32_t dset_mask;          // power of two minus one, >= 2 n_cand - 1
   uint32_t* tail_out;          // stage 1: end, dbase, ndots of the last entry and the flags word
+  uint32_t* tail_dev;          // optional device words: end, dbase, ndots of the last entry (as
+                               // tail_out) and [3] = 1 when the tail is exactly an empty deferred
+                               // map (k_rdm_tail) -- what a merge queued before the host wait reads
+  uint32_t* go;                // optional (stage 2, one launch): device word and go[1] pinned --
+  uint32_t* go_host;           //   1 when every file of the launch is flag-free with an empty map
   uint8_t* tail_host;          // stage 1: the bytes after the entries (the deferred map) when they
   uint32_t tail_cap;           //   fit tail_cap (pinned; else the host downloads them)
   uint32_t* flags;      // 1 non-canonical entry, 2 broken chain, 4 unknown actor, 8 repeated member,

@@ -458,6 +458,47 @@ def test_orswot_state_reader_long_deferred(ctx):
         core.close()
 
 
+@pytest.mark.parametrize("form", ["canonical", "map16_empty_deferred", "no_early"])
+def test_orswot_kway_merge_queued_early(ctx, form):
+    """With several state files and no deferred removal held, the k-way merge is queued behind
+    the reader before the host wait and runs only if every file read cleanly with its deferred
+    map in the one canonical empty form (k_rdm_flags' go word); a map16 {} -- accepted, but not
+    that form -- leaves the early merge idle and the host queues the same merge after the wait.
+    CE_NO_KMERGE_EARLY=1 turns the early merge off.  All three equal the oracle."""
+    import os
+    rng = random.Random(4242)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 8)
+    bodies = []
+    for k in range(3):
+        part = C.Core("orswot")
+        wf = G.well_formed_orswot(rng, actors, 2, 5, 50)[0]
+        acts, clears, fa, fv = G.batch(wf, "orswot", APP)
+        f = [CORE + C._oc.cryptor_encrypt(key, bytes(24), c)[1] for c in clears]
+        assert part.read_remote_ops(key, [APP], f, [acts[i] for i in fa], fv)[0] == 0
+        sw = part.serialize()
+        assert sw.endswith(b"\xa8deferred\x80")
+        bodies.append(sw)
+    if form == "map16_empty_deferred":
+        bodies[1] = bodies[1][:-1] + b"\xde\x00\x00"
+    sf = seal_files(ctx, key, [APP + b for b in bodies])
+    oc = C.Core("orswot")
+    assert oc.read_remote_states(key, [APP], sf)[0] == 0
+    if form == "no_early":
+        os.environ["CE_NO_KMERGE_EARLY"] = "1"
+    try:
+        core = new_core(ctx, "orswot", key)
+        rc, st = core.ingest_states(sf)
+        assert rc == 0 and list(st) == [0, 0, 0]
+        assert core.state_bytes() == oc.serialize()
+        assert core.path_count("states_device_read") == 3
+        assert core.path_count("states_kway_merge") == 1
+        assert core.path_count("states_kway_early") == (1 if form == "canonical" else 0)
+        core.close()
+    finally:
+        os.environ.pop("CE_NO_KMERGE_EARLY", None)
+
+
 def test_orswot_device_compaction_bytes(ctx):
     """Core::compact for Orswot writes the clear text on the device (ce_dotset_io.hip writer):
     the sealed file opens to exactly data_version || the canonical StateWrapper (host writer ==
