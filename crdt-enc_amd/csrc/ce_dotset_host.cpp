@@ -1508,8 +1508,7 @@ bool id_dots_lookup(const ce_core* c, const Dots& d, IdDots* out) {
     if (it == c->slot_of.end()) return false;
     out->push_back({actor_id_of_slot(c, it->second), x.second});
   }
-  std::sort(out->begin(), out->end());
-  return true;
+  return true;  // (in the clock's order: its users scatter it by id)
 }
 
 int id_dots(ce_core* c, Dots d, IdDots* out) {
@@ -1946,17 +1945,33 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
       return ctx->hip_fail(e, "state reader");
     h2.reset();
     if ((e = mark_wait(heads_ev))) return ctx->hip_fail(e, "state head");
-    ph = std::make_unique<HostPhase>("  rd: heads parse");
+    // the heads parsed and their clocks' actors looked up (read-only) on the host threads, a file
+    // per task; a head longer than its prefix, a declined file and actors outside the table are
+    // then handled in file order (the order the ids are handed out in)
+    ph = std::make_unique<HostPhase>("  rd: heads parse + lookups");
+    std::vector<int> pres(n, -1);
+    std::vector<uint64_t> pbody(n, 0), pne(n, 0);
+    std::vector<uint8_t> need_insert(n, 0);
+    std::vector<uint32_t> todo;
+    for (size_t i = 0; i < n; i++)
+      if (st[i] == CE_OK) todo.push_back((uint32_t)i);
+    host_parallel_for(ctx, (uint32_t)todo.size(), [&](uint32_t k) {
+      const size_t i = todo[k];
+      DevState& x = ds[i];
+      const uint64_t want = poff[i + 1] - poff[i];
+      pres[i] = parse_state_prefix(hb + poff[i], want, want == len[i], &x.hs, &pbody[i], &pne[i]);
+      if (pres[i] == 0 && !id_dots_lookup(c, x.hs.clock, &x.oclock)) need_insert[i] = 1;
+    });
     std::vector<size_t> dev;
     uint64_t head_max = 0;
-    for (size_t i = 0; i < n; i++) {
-      if (st[i] != CE_OK) continue;
+    for (size_t i : todo) {
       DevState& x = ds[i];
       x.pt = off[i];
       x.len = len[i];
-      uint64_t want = poff[i + 1] - poff[i], body = 0, ne = 0;
-      int pr = parse_state_prefix(hb + poff[i], want, want == len[i], &x.hs, &body, &ne);
+      uint64_t want = poff[i + 1] - poff[i], body = pbody[i], ne = pne[i];
+      int pr = pres[i];
       std::vector<uint8_t> pre;
+      const bool longer = pr == 2;
       while (pr == 2) {
         want = std::min<uint64_t>(len[i], want * 4);
         pre.resize(want);
@@ -1968,6 +1983,7 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
         if ((rc = host_parse(i))) return rc;
         continue;
       }
+      if (longer && !id_dots_lookup(c, x.hs.clock, &x.oclock)) need_insert[i] = 1;
       x.body = body;
       head_max = std::max<uint64_t>(head_max, body);
       x.n_entries = (uint32_t)ne;
@@ -1979,18 +1995,9 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
       d->head_hint = h;
     }
     // 2) the states' actors into the table (the emitted columns carry their ids)
-    ph = std::make_unique<HostPhase>("  rd: actors + search");
-    // clocks -> actor ids: read-only lookups on the host threads; a file naming an actor
-    // outside the table inserts it below, in file order (the order the ids are handed out in)
-    std::vector<uint8_t> need_insert(n, 0);
-    {
-      HostPhase h1("   rd.a lookups");
-      host_parallel_for(ctx, (uint32_t)dev.size(), [&](uint32_t k) {
-        if (!id_dots_lookup(c, ds[dev[k]].hs.clock, &ds[dev[k]].oclock)) need_insert[dev[k]] = 1;
-      });
-      for (size_t i : dev)
-        if (need_insert[i] && (rc = id_dots(c, ds[i].hs.clock, &ds[i].oclock))) return rc;
-    }
+    ph = std::make_unique<HostPhase>("  rd: actors");
+    for (size_t i : dev)
+      if (need_insert[i] && (rc = id_dots(c, ds[i].hs.clock, &ds[i].oclock))) return rc;
     h2 = std::make_unique<HostPhase>("   rd.b reserve");
     // stages 1 and 2 are one launch per kind for all device files (launch_orswot_read_multi:
     // descriptors as launch arguments, gridDim.y = file), queued back to back behind stage 0 (a
