@@ -69,6 +69,8 @@ struct SerSortArgs {
   const uint32_t* id_of_rank;
   int rank_bits, key_bits;
   uint32_t n, tiles, places, par;
+  uint32_t ticketed;  // tiles ordered by an atomic ticket (when they do not all fit on the GPU at
+                      // once), else by blockIdx
   uint32_t *hist, *ticket, *look;
   const void* keys_in;
   void* keys_out;

@@ -104,7 +104,11 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_pass(SerSortArgs a, uint3
   __shared__ uint32_t wcnt[kSortWaves][kDigits];  // per wave: items of each digit so far
   __shared__ uint32_t tstart[kDigits], gofs[kDigits], wsum[kSortWaves], tile_s;
   const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
-  if (t == 0) tile_s = atomicAdd(a.ticket + place, 1u);  // tiles in dispatch order (look-back)
+  // the look-back waits only on earlier tiles: in dispatch order (an atomic ticket) when the tiles
+  // do not all fit on the GPU at once, else by blockIdx -- every tile is resident, so each one's
+  // predecessors run; the ticket is a same-address atomic per tile, ~60 ns each across XCDs
+  // (~25 us per pass at C3's 415 tiles)
+  if (t == 0) tile_s = a.ticketed ? atomicAdd(a.ticket + place, 1u) : blockIdx.x;
 #pragma unroll
   for (int k = 0; k < kSortWaves; k++) wcnt[k][t] = 0;
   __syncthreads();
@@ -223,7 +227,17 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_pass(SerSortArgs a, uint3
 }
 
 template <typename K, bool FIRST, bool LAST>
-void pass_launch(hipStream_t s, const SerSortArgs& a, uint32_t p) {
+void pass_launch(hipStream_t s, SerSortArgs a, uint32_t p) {
+  // resident workgroups of this pass on the whole GPU (the occupancy calculator: LDS-bound)
+  static const uint32_t res = [] {
+    int dev = 0, per_cu = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sort_pass<K, FIRST, LAST>, kSortThreads, 0) != hipSuccess)
+      return 0u;
+    return (uint32_t)(per_cu > 0 ? per_cu : 0) * (uint32_t)(cus > 0 ? cus : 0);
+  }();
+  static const bool force_ticket = getenv("CE_SORT_TICKET") != nullptr;  // (tests / A/B)
+  a.ticketed = force_ticket || a.tiles > res ? 1u : 0u;
   hipLaunchKernelGGL((k_sort_pass<K, FIRST, LAST>), dim3(a.tiles), dim3(kSortThreads), 0, s, a, p);
 }
 

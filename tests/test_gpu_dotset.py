@@ -1031,9 +1031,9 @@ def test_orswot_serializer_one_sort_equals_two(ctx, n_members):
 def test_orswot_serializer_sort_many_tiles(ctx, member_bits):
     """The hand-written sort over many 4096-pair tiles (the look-back between tiles, every digit
     place, 32- and 64-bit keys): ~300 K live pairs from 256 writers, serialized on the device ==
-    the same state serialized with hipCUB's sort (CE_SER_CUB=1, a separate process: the choice is
-    read once) == the two-sort form; plus a checksum of the bytes' member order: entries strictly
-    ascending."""
+    the same state serialized with the tiles ordered by an atomic ticket (CE_SORT_TICKET=1; by
+    blockIdx otherwise, when every tile is resident), with hipCUB's sort (CE_SER_CUB=1; separate
+    processes: the choices are read once) and with the two-sort form."""
     import subprocess
     import sys
     code = (
@@ -1062,12 +1062,12 @@ def test_orswot_serializer_sort_many_tiles(ctx, member_bits):
         % (os.path.join(REPO, "crdt-enc_amd"), os.path.join(REPO, "tests"), member_bits, APP.hex(),
            CORE.hex(), APP.hex(), APP.hex()))
     outs = []
-    for env in ({}, {"CE_SER_CUB": "1"}, {"CE_SER_TWO_SORTS": "1"}):
+    for env in ({}, {"CE_SORT_TICKET": "1"}, {"CE_SER_CUB": "1"}, {"CE_SER_TWO_SORTS": "1"}):
         p = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), capture_output=True,
                            timeout=300, cwd=REPO)
         assert p.returncode == 0, p.stderr.decode()[-2000:]
         outs.append(p.stdout.decode().split()[-2:])
-    assert outs[0] == outs[1] == outs[2], outs
+    assert outs[0] == outs[1] == outs[2] == outs[3], outs
     assert int(outs[0][1]) > 300000 * 20
 
 
