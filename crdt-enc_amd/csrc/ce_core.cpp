@@ -814,6 +814,7 @@ int ingest_ops_dev_once(ce_core* c, const uint8_t* d_blob, const uint64_t* d_off
   da.pt = ctx->out.as<uint8_t>();
   da.blob = d_blob;
   da.params = ctx->params.as<FileParams>();
+  da.aux = ctx->poly_aux.as<PolyAux>();  // written by device_open_setup above
   da.status = ctx->status.as<int32_t>();
   da.n = n;
   da.supported = c->d_supported.as<uint8_t>();

@@ -123,9 +123,12 @@ int device_open_setup(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs
   // the setup then runs straight into the kernel that consumes it
   if (after_fill && (rc = (*after_fill)())) return rc;
   SegScratch sc = segscratch(ctx, *extra_cap);
+  if ((e = ctx->poly_aux.reserve((size_t)n * sizeof(PolyAux))) != hipSuccess)
+    return ctx->hip_fail(e, "reserve poly aux");
   const int t = ctx->tbegin("open_setup");
   if ((e = launch_open_setup(ctx->stream, d_blob, d_offs, n, outer, dev_key(key), key_status(key),
-                             ctx->params.as<FileParams>(), d_status, sc)) != hipSuccess)
+                             ctx->params.as<FileParams>(), d_status, sc,
+                             ctx->poly_aux.as<PolyAux>())) != hipSuccess)
     return ctx->hip_fail(e, "open setup");
   ctx->tend(t);
   return CE_OK;

@@ -314,6 +314,62 @@ __device__ __forceinline__ void key_schedule_w(const DevKey& key, const uint32_t
   }
 }
 
+// PolyAux of an opened file whose FileParams (rpow, len, s, tag) are set (lane per file)
+__device__ __forceinline__ void poly_aux(const FileParams& P, PolyAux& X) {
+  const L5 r = load_l5(P.rpow[0]), r2 = load_l5(P.rpow[1]), r4 = load_l5(P.rpow[2]);
+  const L5 r3 = mulmod(r2, r);
+  const L5 r12 = mulmod(load_l5(P.rpow[3]), r4);
+  const L5 r48 = mulmod(load_l5(P.rpow[5]), load_l5(P.rpow[4]));
+  const uint32_t npc = (P.len + 15) >> 4, nblk = (P.len + 63) >> 6;
+  const uint32_t delta = 4 * nblk - npc;  // 0..3
+  const L5 r5 = mulmod(r4, r), r6 = mulmod(r4, r2);
+  const L5 e6 = delta == 0 ? r6 : delta == 1 ? r5 : delta == 2 ? r4 : r3;
+  const L5 lr = mulmod(block_limbs(0u, 0u, P.len, 0u), r);  // le64(0) || le64(len), pad bit
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    X.r3[i] = r3.v[i]; X.r12[i] = r12.v[i]; X.r48[i] = r48.v[i];
+    X.e6[i] = e6.v[i]; X.lr[i] = lr.v[i];
+  }
+  uint64_t b = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint64_t d = (uint64_t)P.tag[i] - P.s[i] - b;
+    X.ts[i] = (uint32_t)d;
+    b = (d >> 32) & 1;
+  }
+  X.pad[0] = X.pad[1] = X.pad[2] = 0;
+}
+
+// h (limbs < 2^31, v[1] < 2^31) fully reduced mod p, its low 128 bits == ts (the expected tag
+// less s, mod 2^128): the tag check of (h + s) mod 2^128 == tag without the 128-bit add
+__device__ __forceinline__ bool poly_check(L5 h, const uint32_t (&ts)[4]) {
+  uint32_t c;
+  c = h.v[0] >> 26; h.v[0] &= M26; h.v[1] += c;
+  c = h.v[1] >> 26; h.v[1] &= M26; h.v[2] += c;
+  c = h.v[2] >> 26; h.v[2] &= M26; h.v[3] += c;
+  c = h.v[3] >> 26; h.v[3] &= M26; h.v[4] += c;
+  c = h.v[4] >> 26; h.v[4] &= M26; h.v[0] += c * 5;
+  c = h.v[0] >> 26; h.v[0] &= M26; h.v[1] += c;
+  c = h.v[1] >> 26; h.v[1] &= M26; h.v[2] += c;
+  c = h.v[2] >> 26; h.v[2] &= M26; h.v[3] += c;
+  c = h.v[3] >> 26; h.v[3] &= M26; h.v[4] += c;
+  // limbs 0..3 < 2^26, h4 <= 2^26 (+small): g = h + 5 - 2^130, kept when non-negative (h >= p)
+  uint32_t g[5];
+  g[0] = h.v[0] + 5; c = g[0] >> 26; g[0] &= M26;
+  g[1] = h.v[1] + c; c = g[1] >> 26; g[1] &= M26;
+  g[2] = h.v[2] + c; c = g[2] >> 26; g[2] &= M26;
+  g[3] = h.v[3] + c; c = g[3] >> 26; g[3] &= M26;
+  g[4] = h.v[4] + c - (1u << 26);
+  const uint32_t mask = (g[4] >> 31) - 1;  // all ones when g >= 0
+#pragma unroll
+  for (int i = 0; i < 5; i++) h.v[i] = (h.v[i] & ~mask) | (g[i] & mask);
+  const uint32_t w0 = h.v[0] | (h.v[1] << 26);
+  const uint32_t w1 = (h.v[1] >> 6) | (h.v[2] << 20);
+  const uint32_t w2 = (h.v[2] >> 12) | (h.v[3] << 14);
+  const uint32_t w3 = (h.v[3] >> 18) | (h.v[4] << 8);
+  return ((w0 ^ ts[0]) | (w1 ^ ts[1]) | (w2 ^ ts[2]) | (w3 ^ ts[3])) == 0;
+}
+
 __device__ __forceinline__ void key_schedule(const DevKey& key, const uint8_t* nonce, FileParams& P) {
   uint32_t nw[6];
 #pragma unroll

@@ -1471,6 +1471,212 @@ void k_open_fold_v2(DecodeArgs a) {
 #endif
 }
 
+// ----------------------------------------------------------------------------------------
+// k_open_fold_v3: k_open_fold_v2<16, 2, false, 1> (the C2 kernel) with its Poly1305 rebuilt
+// around the setup's per-file constants (PolyAux, ce_kernels.h), so that every Poly1305 step
+// of a lane is a four-product column sum reduced once, and the cross-lane combination is sums:
+//   - the full blocks: acc r^64 + m0 r^3 + m1 r^2 + m2 r + m3 (r^3 from the setup; the first
+//     block has no acc term);
+//   - the file's last block (lane 0, k = 0) in the same four-product form: its Poly1305
+//     pieces are loaded shifted by delta (the pieces it lacks, 4 nblk - npc), so the absent ones
+//     are the leading zeros of the Horner form and the sum is G' itself; the partial piece's
+//     bytes past the ciphertext (the tag's) are masked;
+//   - lane s's chain sits at tree position q = s - 1 (lane 0's at 15) with weight r^(4q) =
+//     r^(4 (q & 3)) r^(16 (q >> 2)): two multiplications per lane, then a DPP sum of the 16
+//     lanes (v2: a four-level tree, one multiplication per level);
+//   - T = U r^(6 - delta) + G' r^2 + L r (r^(6 - delta) and L r from the setup) and the check
+//     against (tag - s) mod 2^128 (xchacha lib.rs:92-97).
+// The plaintext past the ciphertext (the last piece's tag bytes XOR keystream) is not masked:
+// the decode reads nothing past len.  ChaCha20, the LDS plaintext and the decode are v2's.
+// ----------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64, 2)
+void k_open_fold_v3(DecodeArgs a) {
+  constexpr int LPF = 16, F = 4, BPL = 4;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[(F - 1) * kRegionStride2 + kRegion2 + 64];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t grp = lane / LPF, sub = lane % LPF;
+  uint8_t* fl = lds + grp * kRegionStride2;
+  const uint32_t ngroups = (a.n + F - 1) / F;
+  const uint32_t stride = gridDim.x;
+  uint32_t g = bcast(blockIdx.x);
+  FilePre2 nx = load_pre2(a, g * F + grp);
+  const SupVers sup(a);
+  DecState S{38, 0, 0, 0, 0, 0xffffffffu};
+  AuthFails fails;
+  // this lane's tree weight r^(4q), q = (sub + 15) & 15: X = r^(4 (q & 3)) in {1, r^4, r^8,
+  // r^12}, Y = r^(16 (q >> 2)) in {1, r^16, r^32, r^48}, read from FileParams.rpow / PolyAux
+  const uint32_t qpos = (sub + 15u) & 15u;
+  const uint32_t qx = qpos & 3u, qy = qpos >> 2;
+  const bool x_one = qx == 0, y_one = qy == 0, x_aux = qx == 3, y_aux = qy == 3;
+  const uint32_t x_off = x_aux ? (uint32_t)offsetof(PolyAux, r12) : 80u + 20u * (qx + 1u);
+  const uint32_t y_off = y_aux ? (uint32_t)offsetof(PolyAux, r48) : 80u + 20u * (qy + 3u);
+  static_assert(offsetof(FileParams, rpow) == 80, "rpow offset");
+
+  uint4 ct[BPL][4];
+  for (; g < ngroups; g += stride) {
+    const uint32_t f = g * F + grp;
+    const FilePre2 cur = nx;
+    const bool act = cur.ok && cur.len <= kSmallMax;
+    const uint32_t len = act ? cur.len : 0u;
+    const uint32_t npc = (len + 15) >> 4;             // ciphertext Poly1305 pieces
+    const int32_t nblk = (int32_t)((len + 63) >> 6);  // ChaCha20 blocks
+    const FileParams* Pp = a.params + (act ? f : 0);
+    const PolyAux* Xp = a.aux + (act ? f : 0);
+    const uint8_t* src = act ? a.blob + (((uint64_t)cur.in_hi << 32) | cur.in_off)
+                             : reinterpret_cast<const uint8_t*>(a.params);
+    // 1) ciphertext -> registers, every block up front.  Block k of the lane is b = nblk - 1 -
+    //    sub - 16 k; all but the file's last (lane 0, k = 0) are whole, so their four pieces are
+    //    one address + immediate offsets.  A lane without the block reads the params rows (any
+    //    64 readable bytes); the last block clamps its pieces to the last one (the 16-byte tag
+    //    follows the ciphertext: a load at any piece < npc stays inside the file).
+#pragma unroll
+    for (int k = BPL - 1; k >= 0; k--) {
+      const int32_t b = nblk - 1 - (int32_t)sub - LPF * k;
+      if (k > 0) {
+        const uint8_t* bp = b >= 0 ? src + 64u * (uint32_t)b : reinterpret_cast<const uint8_t*>(a.params);
+#pragma unroll
+        for (int j = 0; j < 4; j++) ct[k][j] = *reinterpret_cast<const uint4*>(bp + 16 * j);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint32_t q = (uint32_t)(4 * b + j);
+          const uint32_t off = b >= 0 ? 16u * (q < npc ? q : npc - 1u) : 0u;
+          ct[0][j] = *reinterpret_cast<const uint4*>(src + off);
+        }
+      }
+    }
+    // the multipliers: r, r^2, r^3 (the four-product step), r^64 (the chain step)
+    L5 R1, RC, R2, R3;
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      R1.v[i] = cur.R1[i];
+      RC.v[i] = cur.R64[i];
+      R2.v[i] = Pp->rpow[1][i];
+      R3.v[i] = Xp->r3[i];
+    }
+    const ChachaPre cpre = chacha_pre(cur.key, 0u, cur.n2a, cur.n2b);
+    L5 acc{{0, 0, 0, 0, 0}}, glast{{0, 0, 0, 0, 0}};
+    L5 X, Y, E6, LR;
+    uint32_t ts[4];
+    uint4 pc[4];  // lane 0: the last block's Poly1305 pieces, shifted by delta
+    // lane 0's shift and its last piece's valid bytes (others: 0 and 16)
+    const uint32_t dl = sub == 0 ? (uint32_t)(4 * nblk) - npc : 0u;
+    const uint32_t rb = sub == 0 && npc ? len - 16u * (npc - 1u) : 16u;
+
+#pragma unroll
+    for (int k = BPL - 1; k >= 0; k--) {
+      const int32_t b = nblk - 1 - (int32_t)sub - LPF * k;
+      const bool has = b >= 0;
+      if (k == 0) {
+        // issued before the last block's ChaCha20 (latency hidden under it; the other blocks'
+        // ciphertext registers are free by now): the shifted pieces, the tree weights, the tail
+        const uint8_t* pb = has ? src + 16 * (int64_t)(4 * b - (int32_t)dl) : src;
+#pragma unroll
+        for (int j = 0; j < 4; j++) pc[j] = *reinterpret_cast<const uint4*>(pb + 16 * j);
+        const uint32_t* xs = reinterpret_cast<const uint32_t*>(
+            (x_aux ? reinterpret_cast<const uint8_t*>(Xp) : reinterpret_cast<const uint8_t*>(Pp)) + x_off);
+        const uint32_t* ys = reinterpret_cast<const uint32_t*>(
+            (y_aux ? reinterpret_cast<const uint8_t*>(Xp) : reinterpret_cast<const uint8_t*>(Pp)) + y_off);
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+          X.v[i] = xs[i];
+          Y.v[i] = ys[i];
+          E6.v[i] = Xp->e6[i];
+          LR.v[i] = Xp->lr[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) ts[i] = Xp->ts[i];
+      }
+      uint32_t kb[16];
+      chacha_block_pre<true, 9>(cpre, cur.key, 1u + (uint32_t)b, 0u, cur.n2a, cur.n2b, kb);
+      L5 m[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t q = (uint32_t)(4 * b + j);
+        const uint4 c = ct[k][j];
+        const uint4 pv = make_uint4(c.x ^ kb[4 * j], c.y ^ kb[4 * j + 1], c.z ^ kb[4 * j + 2], c.w ^ kb[4 * j + 3]);
+        // a lane without a block stores to bytes 4080..4095: past the end of any file that has
+        // absent blocks (nblk < 64)
+        *reinterpret_cast<uint4*>(fl + (has ? q * 16u : kRegion2 - 16u)) = pv;
+        if (k > 0) {
+          m[j] = block_limbs(c.x, c.y, c.z, c.w);
+        } else {
+          // position j holds piece 4 b + j - dl (none when j < dl); the last position's bytes
+          // past the ciphertext are zeroed
+          uint32_t w[4] = {pc[j].x, pc[j].y, pc[j].z, pc[j].w};
+          const bool pres = (uint32_t)j >= dl;
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            if (j == 3) {
+              const int32_t cb = (int32_t)rb - 4 * i;  // valid bytes of the word
+              const uint32_t keep = cb >= 4 ? ~0u : cb <= 0 ? 0u : ((1u << (8 * cb)) - 1u);
+              w[i] &= keep;
+            } else {
+              w[i] = pres ? w[i] : 0u;
+            }
+          }
+          m[j] = block_limbs(w[0], w[1], w[2], w[3]);
+          if (j < 3) m[j].v[4] = pres ? m[j].v[4] : 0u;
+        }
+      }
+      // acc r^64 + m0 r^3 + m1 r^2 + m2 r + m3 as four (five) products into one set of column
+      // sums, carried once.  Lane 0's last block starts from zero and is kept apart (G').
+      uint64_t d[5] = {m[3].v[0], m[3].v[1], m[3].v[2], m[3].v[3], m[3].v[4]};
+      if (k < BPL - 1) {  // the lane's first block has no acc term
+        L5 ain = acc;
+        if (k == 0) {
+#pragma unroll
+          for (int i = 0; i < 5; i++) ain.v[i] = sub == 0 ? 0u : acc.v[i];
+        }
+        mac5(d, ain, mul_r(RC));
+      }
+      mac5(d, m[0], mul_r(R3));
+      mac5(d, m[1], mul_r(R2));
+      mac5(d, m[2], mul_r(R1));
+      const L5 an = reduce5(d);
+      const bool to_acc = has && !(k == 0 && sub == 0);
+#pragma unroll
+      for (int i = 0; i < 5; i++) acc.v[i] = to_acc ? an.v[i] : acc.v[i];
+      if (k == 0) {
+#pragma unroll
+        for (int i = 0; i < 5; i++) glast.v[i] = has && sub == 0 ? an.v[i] : 0u;
+      }
+    }
+
+    // 2) U = sum_q v_q r^(4q): each chain times its weight, then the group's sum into lane 0
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      X.v[i] = x_one ? (i == 0 ? 1u : 0u) : X.v[i];
+      Y.v[i] = y_one ? (i == 0 ? 1u : 0u) : Y.v[i];
+    }
+    L5 v = mulmod(mulmod(acc, X), Y);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+#pragma unroll
+      for (int i = 0; i < 5; i++) v.v[i] += row_down(v.v[i], 1 << k);  // limbs < 2^31
+    }
+    // 3) T = U r^(6 - delta) + G' r^2 + L r, checked against (tag - s) mod 2^128
+    uint64_t d[5] = {LR.v[0], LR.v[1], LR.v[2], LR.v[3], LR.v[4]};
+    mac5(d, v, mul_r(E6));
+    mac5(d, glast, mul_r(R2));
+    const L5 tot = reduce5(d);
+    bool tag_ok = false;
+    if (act && sub == 0) {
+      tag_ok = poly_check(tot, ts);
+      if (!tag_ok) a.status[f] = CE_ERR_AUTH;
+    }
+    fails.add(act && sub == 0 && !tag_ok, f);
+    const bool ok = grp_bits<LPF>(tag_ok, grp) != 0;
+
+    // 4) data-version check, decode from LDS, fold; the next iteration's parameters are loaded
+    //    inside (their latency hides under the decode)
+    decode_fold<LPF>(a, sup, fl, len, act && ok, cur.apply != 0, f, grp, sub, S,
+                     [&] { nx = load_pre2(a, (g + stride) * F + grp); });
+    __builtin_amdgcn_wave_barrier();
+  }
+  fails.flush(a);
+}
+
 template <int LPF, int W, bool JIT, int OPT = 3, bool DEC = true, bool DS = false>
 static void launch_v2(hipStream_t s, const DecodeArgs& a, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr) {
   static const uint32_t res = resident_blocks(k_open_fold_v2<LPF, W, JIT, OPT, DEC, DS>, 64);
@@ -1497,6 +1703,15 @@ hipError_t launch_open_small_v2(hipStream_t s, const DecodeArgs& a) {
 hipError_t launch_open_fold_v2(hipStream_t s, const DecodeArgs& a, int files_per_wave, hipEvent_t t0,
                                hipEvent_t t1) {
   if (a.n == 0) return hipSuccess;
+  // the v3 Poly1305 form (needs the setup's PolyAux rows); CE_FUSED_V2=1 keeps v2 for A/B
+  static const bool force_v2 = getenv("CE_FUSED_V2") != nullptr;
+  if (files_per_wave == 4 && a.aux && !force_v2) {
+    static const uint32_t res = resident_blocks(k_open_fold_v3, 64);
+    const dim3 grid(std::min<uint32_t>((a.n + 3) / 4, res));
+    if (t0) hipExtLaunchKernelGGL(k_open_fold_v3, grid, dim3(64), 0, s, t0, t1, 0u, a);
+    else hipLaunchKernelGGL(k_open_fold_v3, grid, dim3(64), 0, s, a);
+    return hipGetLastError();
+  }
 #if CE_FUSED_DIAG
   // diagnostics build only (libcrdtenc_prof.so): same-box A/B variants.  Several of them are
   // NOT correct (OPT 129/385 skip the actor lookups, 513/1025 may write status 77), so none is

@@ -148,7 +148,8 @@ struct ce_ctx {
   std::string last_error;
   // batch scratch (device)
   ce::DevBuf params, status, counters, extra, multi, partials, large, out, apply, refold, miss,
-      supported, blob, offs, nonces, out_offs, outer_ver, batch_counters, split, segrec, redo, heads;
+      supported, blob, offs, nonces, out_offs, outer_ver, batch_counters, split, segrec, redo, heads,
+      poly_aux;  // PolyAux rows of the fused open (device_open_setup)
   ce::HostBuf h_counters, h_apply, h_stage, h_stage2, h_heads;
   uint32_t publish_gen = 0;  // k_publish_words generations (the setup's counters, C2 path)
   // marks the setup kernel's counter snapshot (h_counters + 128) as landed on the host

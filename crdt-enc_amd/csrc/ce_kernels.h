@@ -32,6 +32,22 @@ struct alignas(16) FileParams {
 };
 static_assert(sizeof(FileParams) == 256, "FileParams layout");
 
+// Per-file constants of the single-page fused open (k_open_fold_v3), written by the open setup
+// (lane per file) so the kernel's 16-lane groups do not each recompute them.  With delta =
+// 4 ceil(len / 64) - ceil(len / 16) pieces missing from the last ChaCha20 block, the tag
+// polynomial is T = U r^(6 - delta) + G' r^2 + L r (U: the lanes' chains, G': the last block's
+// pieces, L: the length block le64(0) || le64(len) + 2^128).
+struct alignas(16) PolyAux {
+  uint32_t r3[5];   // r^3 (the full blocks' four-product step)
+  uint32_t r12[5];  // r^12, r^48: the chains' weights r^(4q) = r^(4 (q & 3)) r^(16 (q >> 2))
+  uint32_t r48[5];
+  uint32_t e6[5];   // r^(6 - delta)
+  uint32_t lr[5];   // L r mod p
+  uint32_t ts[4];   // (tag - s) mod 2^128: T mod p must equal it (xchacha lib.rs:92-97)
+  uint32_t pad[3];
+};
+static_assert(sizeof(PolyAux) == 128, "PolyAux layout");
+
 struct DevKey {
   uint32_t k[8];
 };
@@ -80,7 +96,8 @@ hipError_t launch_publish_sealed_len(hipStream_t s, const uint64_t* clear_len_at
 // file-level open: outer version check (when outer), envelope parse, key schedule.
 hipError_t launch_open_setup(hipStream_t s, const uint8_t* blob, const uint64_t* offs,
                              uint32_t n, bool outer, DevKey key, int32_t key_status,
-                             FileParams* params, int32_t* status, SegScratch sc);
+                             FileParams* params, int32_t* status, SegScratch sc,
+                             PolyAux* aux = nullptr);
 // seal setup: header write + key schedule; out_offs[i] = start of output i.
 hipError_t launch_seal_setup(hipStream_t s, const uint8_t* clear, const uint64_t* offs,
                              uint32_t n, const uint8_t* outer_version /* device, or null */,
@@ -143,6 +160,7 @@ struct DecodeArgs {
   int nil_actor;                // the nil UUID is in the actor table: lookups take the two-load
                                 // probe (lookup_slot1)
   DsFuse ds;                    // launch_open_small_v2: Orswot ops decoded in the open (ds.on)
+  const PolyAux* aux;           // fused open (k_open_fold_v3): the setup's per-file constants
 };
 hipError_t launch_decode_dots(hipStream_t s, const DecodeArgs& a, uint32_t grid_waves);
 // diagnostics: shader clock vs the reference clock (ce_ctx_clock_probe)

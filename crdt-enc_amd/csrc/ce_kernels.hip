@@ -25,10 +25,12 @@ __global__ __launch_bounds__(256) void k_open_setup(const uint8_t* __restrict__ 
                                                     const uint64_t* __restrict__ offs, uint32_t n,
                                                     int outer, DevKey key, int32_t key_status,
                                                     FileParams* __restrict__ params,
-                                                    int32_t* __restrict__ status, SegScratch sc) {
+                                                    int32_t* __restrict__ status, SegScratch sc,
+                                                    PolyAux* __restrict__ aux) {
   // parameters are staged in LDS, 128 B per lane per half (16-B columns XOR-swizzled by the
   // lane), and stored as the block's contiguous rows: a per-lane 256-B struct store touches 64
-  // lines per instruction.  32 KiB keeps 5 workgroups per CU.
+  // lines per instruction.  32 KiB keeps 5 workgroups per CU.  The PolyAux rows (when asked
+  // for) go the same way as a third half.
   __shared__ uint4 stage[256 * 8];
   const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = f < n;
@@ -108,22 +110,34 @@ __global__ __launch_bounds__(256) void k_open_setup(const uint8_t* __restrict__ 
     if (P.len > kSmallMax) sc.large_list[atomicAdd(&sc.counters[9], 1u)] = f;
   }
   reserve_segments(P, f, sc, st == CE_OK);  // the whole wave (long files are filled together)
+  PolyAux X;
+  if (aux) {  // block-uniform
+    if (st == CE_OK) poly_aux(P, X);
+    else X = PolyAux{};
+  }
   {
     const uint4* pv = reinterpret_cast<const uint4*>(&P);
+    const uint4* xv = reinterpret_cast<const uint4*>(&X);
     const uint32_t f0 = blockIdx.x * blockDim.x;
     const uint32_t nrow = min(n - f0, (uint32_t)blockDim.x);
     uint4* dstp = reinterpret_cast<uint4*>(params + f0);
+    uint4* dsta = aux ? reinterpret_cast<uint4*>(aux + f0) : nullptr;
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
+    for (int h = 0; h < 3; h++) {
+      if (h == 2 && !aux) break;
       if (h) __syncthreads();
 #pragma unroll
-      for (int i = 0; i < 8; i++) stage[threadIdx.x * 8 + (i ^ (threadIdx.x & 7))] = pv[8 * h + i];
+      for (int i = 0; i < 8; i++) stage[threadIdx.x * 8 + (i ^ (threadIdx.x & 7))] = h < 2 ? pv[8 * h + i] : xv[i];
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < 8; k++) {
         const uint32_t j = threadIdx.x + 256u * k;
         const uint32_t row = j >> 3, col = j & 7;
-        if (row < nrow) dstp[row * 16 + 8 * h + col] = stage[row * 8 + (col ^ (row & 7))];
+        if (row < nrow) {
+          const uint4 v = stage[row * 8 + (col ^ (row & 7))];
+          if (h < 2) dstp[row * 16 + 8 * h + col] = v;
+          else dsta[row * 8 + col] = v;
+        }
       }
     }
   }
@@ -1259,10 +1273,10 @@ __global__ __launch_bounds__(1024) void k_serialize_vclock(
 // ----------------------------------------------------------------------------------------
 hipError_t launch_open_setup(hipStream_t s, const uint8_t* blob, const uint64_t* offs, uint32_t n,
                              bool outer, DevKey key, int32_t key_status, FileParams* params,
-                             int32_t* status, SegScratch sc) {
+                             int32_t* status, SegScratch sc, PolyAux* aux) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_open_setup, dim3((n + 255) / 256), dim3(256), 0, s, blob, offs, n,
-                     outer ? 1 : 0, key, key_status, params, status, sc);
+                     outer ? 1 : 0, key, key_status, params, status, sc, aux);
   return hipGetLastError();
 }
 
