@@ -166,7 +166,27 @@ __device__ __forceinline__ FilePre load_pre(const DecodeArgs& a, uint32_t f) {
 struct DecState {
   uint32_t Ls;
   uint32_t ck0, ck1, ck2, ck3, cslot;
+  // CARRY (k_open_fold_v3): the lane's pending (slot, max) carried from file to file -- a wave
+  // takes a contiguous run of files, a writer's run, so one flush per writer instead of per file
+  uint32_t pslot = 0xffffffffu;
+  unsigned long long pbest = 0;
 };
+
+// one atomicMax per lane group when the group's pending slots agree, else one per lane
+template <int LPF>
+__device__ __forceinline__ void flush_pending(const DecodeArgs& a, uint32_t sub, uint32_t pslot,
+                                              unsigned long long pbest) {
+  const uint32_t hi = pslot == 0xffffffffu ? 0u : pslot + 1;
+  const uint32_t lo = pslot == 0xffffffffu ? 0xffffffffu : pslot + 1;
+  const uint32_t mx = grp_reduce<LPF>(hi, [](uint32_t x, uint32_t y) { return x > y ? x : y; });
+  const uint32_t mn = grp_reduce<LPF>(lo, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
+  const unsigned long long b = grp_max64<LPF>(pslot == 0xffffffffu ? 0ull : pbest);
+  if (mx != 0 && mn == mx) {
+    if (sub == 0) batch_max(&a.batch[mx - 1], b);
+  } else if (pslot != 0xffffffffu) {
+    batch_max(&a.batch[pslot], pbest);
+  }
+}
 
 // Steps 5-6 of the fused kernels for the file of this lane group whose plaintext sits in LDS at
 // fl: VersionBytes data-version check (crdt-enc/src/lib.rs:504-505), rmp-serde Vec<Dot<Uuid>>
@@ -196,7 +216,7 @@ struct SupVers {
 // its read, 4 = one extra ChaCha20 block's double rounds spread over the fast rounds (one per
 // round, the rest after the loop), 8 = the same extra block after the decode loops (4 vs 8:
 // how much independent VALU work the decode's stalls could absorb)
-template <int LPF, int DOPT = 0, typename Pf>
+template <int LPF, int DOPT = 0, bool CARRY = false, typename Pf>
 __device__ __forceinline__ void decode_fold(const DecodeArgs& a, const SupVers& sup, const uint8_t* fl,
                                             uint32_t len, bool live, bool apply, uint32_t f,
                                             uint32_t grp, uint32_t sub, DecState& S, Pf&& prefetch) {
@@ -232,9 +252,10 @@ __device__ __forceinline__ void decode_fold(const DecodeArgs& a, const SupVers& 
     else { remaining = count; pos = (uint32_t)r.i; }
   }
   const bool do_fold = live && st == CE_OK && apply;
-  // pending max per lane: flushed with atomicMax when the lane's actor changes
-  uint32_t pslot = 0xffffffffu;
-  unsigned long long pbest = 0;
+  // pending max per lane: flushed with atomicMax when the lane's actor changes (CARRY: from
+  // the previous file on, and the caller flushes after its last file)
+  uint32_t pslot = CARRY ? S.pslot : 0xffffffffu;
+  unsigned long long pbest = CARRY ? S.pbest : 0ull;
   auto fold_slot = [&](uint32_t slot, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3,
                        unsigned long long ctr) {
     if (slot == 0xffffffffu) {
@@ -512,7 +533,10 @@ __device__ __forceinline__ void decode_fold(const DecodeArgs& a, const SupVers& 
     }
   }
   // flush: one atomicMax per file when the group's pending actors agree
-  {
+  if (CARRY) {
+    S.pslot = pslot;
+    S.pbest = pbest;
+  } else {
     const uint32_t hi = pslot == 0xffffffffu ? 0u : pslot + 1;
     const uint32_t lo = pslot == 0xffffffffu ? 0xffffffffu : pslot + 1;
     const uint32_t mx = grp_reduce<LPF>(hi, [](uint32_t x, uint32_t y) { return x > y ? x : y; });
@@ -1496,9 +1520,11 @@ void k_open_fold_v3(DecodeArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t grp = lane / LPF, sub = lane % LPF;
   uint8_t* fl = lds + grp * kRegionStride2;
+  // a wave takes a contiguous run of file groups (load_ops order: a writer's files are adjacent,
+  // so the lane's actor cache and pending max carry over from file to file)
   const uint32_t ngroups = (a.n + F - 1) / F;
-  const uint32_t stride = gridDim.x;
-  uint32_t g = bcast(blockIdx.x);
+  const uint32_t g_end = (uint32_t)(((uint64_t)(blockIdx.x + 1) * ngroups) / gridDim.x);
+  uint32_t g = bcast((uint32_t)(((uint64_t)blockIdx.x * ngroups) / gridDim.x));
   FilePre2 nx = load_pre2(a, g * F + grp);
   const SupVers sup(a);
   DecState S{38, 0, 0, 0, 0, 0xffffffffu};
@@ -1513,7 +1539,7 @@ void k_open_fold_v3(DecodeArgs a) {
   static_assert(offsetof(FileParams, rpow) == 80, "rpow offset");
 
   uint4 ct[BPL][4];
-  for (; g < ngroups; g += stride) {
+  for (; g < g_end; g++) {
     const uint32_t f = g * F + grp;
     const FilePre2 cur = nx;
     const bool act = cur.ok && cur.len <= kSmallMax;
@@ -1670,10 +1696,11 @@ void k_open_fold_v3(DecodeArgs a) {
 
     // 4) data-version check, decode from LDS, fold; the next iteration's parameters are loaded
     //    inside (their latency hides under the decode)
-    decode_fold<LPF>(a, sup, fl, len, act && ok, cur.apply != 0, f, grp, sub, S,
-                     [&] { nx = load_pre2(a, (g + stride) * F + grp); });
+    decode_fold<LPF, 0, true>(a, sup, fl, len, act && ok, cur.apply != 0, f, grp, sub, S,
+                              [&] { nx = load_pre2(a, (g + 1) * F + grp); });
     __builtin_amdgcn_wave_barrier();
   }
+  flush_pending<LPF>(a, sub, S.pslot, S.pbest);
   fails.flush(a);
 }
 

@@ -6,7 +6,8 @@ import csv, glob, json, os, sys
 
 out = sys.argv[1]
 repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {"k_open_fold_v2": "fused", "k_open_setup": "setup"}
+KERNELS = {"k_open_fold_v": "fused", "k_open_setup": "setup"}
+names = {}
 acc = {}    # short -> counter -> [per-dispatch sums]
 durs = {}   # short -> [ns]
 for p in sorted(glob.glob(os.path.join(out, "pass*"))):
@@ -17,6 +18,7 @@ for p in sorted(glob.glob(os.path.join(out, "pass*"))):
         for row in csv.DictReader(open(fn)):
             short = next((v for k, v in KERNELS.items() if k in row["Kernel_Name"]), None)
             if short:
+                names[short] = row["Kernel_Name"].split("(")[0]
                 key = (short, row["Dispatch_Id"], row["Counter_Name"])
                 per[key] = per.get(key, 0.0) + float(row["Counter_Value"])
     for (short, _, cn), v in per.items():
@@ -46,7 +48,7 @@ for short, cs in acc.items():
                                                                    "SQ_WAIT_ANY") if k in d}
     res[short] = r
 if "fused" in res:
-    res["fused"]["kernel"] = "k_open_fold_v2<16>"   # bench.py only uses a record of its own kernel
+    res["fused"]["kernel"] = names.get("fused", "k_open_fold_v3")
 print(json.dumps(res, indent=1))
 with open(os.path.join(out, "summary.json"), "w") as f:
     json.dump(res, f, indent=1)
