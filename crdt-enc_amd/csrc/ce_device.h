@@ -124,6 +124,45 @@ __device__ __forceinline__ void chacha_block_pre(const ChachaPre& pre, const uin
   out[12] = x[12] + ctr; out[13] = x[13] + n0; out[14] = x[14] + n1; out[15] = x[15] + n2;
 }
 
+// two chacha_block_pre blocks (counters ca, cb) with their quarter rounds interleaved: eight
+// independent ARX chains per round instead of four
+__device__ __forceinline__ void chacha_block_pre2(const ChachaPre& pre, const uint32_t (&k)[8],
+                                                  uint32_t ca, uint32_t cb, uint32_t n0, uint32_t n1,
+                                                  uint32_t n2, uint32_t (&oa)[16], uint32_t (&ob)[16]) {
+  uint32_t x[16], y[16];
+  x[1] = pre.c[0]; x[5] = pre.c[1]; x[9] = pre.c[2]; x[13] = pre.c[3];
+  x[2] = pre.c[4]; x[6] = pre.c[5]; x[10] = pre.c[6]; x[14] = pre.c[7];
+  x[3] = pre.c[8]; x[7] = pre.c[9]; x[11] = pre.c[10]; x[15] = pre.c[11];
+#pragma unroll
+  for (int i = 1; i < 16; i++) y[i] = x[i];
+  x[0] = pre.a0; x[4] = k[0]; x[8] = k[4]; x[12] = ca;
+  y[0] = pre.a0; y[4] = k[0]; y[8] = k[4]; y[12] = cb;
+  x[12] = xor_rotl16_t<true>(x[12], x[0]); y[12] = xor_rotl16_t<true>(y[12], y[0]);
+  x[8] += x[12]; y[8] += y[12]; x[4] ^= x[8]; y[4] ^= y[8];
+  x[4] = rotl32(x[4], 12); y[4] = rotl32(y[4], 12);
+  x[0] += x[4]; y[0] += y[4]; x[12] ^= x[0]; y[12] ^= y[0];
+  x[12] = rotl32(x[12], 8); y[12] = rotl32(y[12], 8);
+  x[8] += x[12]; y[8] += y[12]; x[4] ^= x[8]; y[4] ^= y[8];
+  x[4] = rotl32(x[4], 7); y[4] = rotl32(y[4], 7);
+#define CE_QR2(a, b, c, d) CE_QR_T(true, x[a], x[b], x[c], x[d]); CE_QR_T(true, y[a], y[b], y[c], y[d]);
+  CE_QR2(0, 5, 10, 15); CE_QR2(1, 6, 11, 12); CE_QR2(2, 7, 8, 13); CE_QR2(3, 4, 9, 14);
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    CE_QR2(0, 4, 8, 12); CE_QR2(1, 5, 9, 13); CE_QR2(2, 6, 10, 14); CE_QR2(3, 7, 11, 15);
+    CE_QR2(0, 5, 10, 15); CE_QR2(1, 6, 11, 12); CE_QR2(2, 7, 8, 13); CE_QR2(3, 4, 9, 14);
+  }
+#undef CE_QR2
+  const uint32_t c4[4] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u};
+#pragma unroll
+  for (int i = 0; i < 4; i++) { oa[i] = x[i] + c4[i]; ob[i] = y[i] + c4[i]; }
+#pragma unroll
+  for (int i = 0; i < 8; i++) { oa[4 + i] = x[4 + i] + k[i]; ob[4 + i] = y[4 + i] + k[i]; }
+  oa[12] = x[12] + ca; ob[12] = y[12] + cb;
+  oa[13] = x[13] + n0; ob[13] = y[13] + n0;
+  oa[14] = x[14] + n1; ob[14] = y[14] + n1;
+  oa[15] = x[15] + n2; ob[15] = y[15] + n2;
+}
+
 __device__ __forceinline__ void hchacha20(const uint32_t (&k)[8], const uint32_t (&n)[4],
                                           uint32_t (&sub)[8]) {
   uint32_t x[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, k[0], k[1], k[2], k[3],

@@ -2168,7 +2168,12 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
   bool kway = n >= 2 && n <= 64 && d->deferred.empty() && !getenv("CE_NO_KMERGE");
   for (size_t i = 0; i < n && kway; i++) kway = ds[i].device && ds[i].od.empty();
   const bool early = spec && small[10 * n] != 0;  // the k-way merge queued before the wait ran
-  if (early && !kway) return ctx->fail(CE_ERR_DEVICE, "state reader: early merge for a declined file");
+  if (early && !kway) {
+    // the early merge already changed the pair table and the clock: later calls must fail until
+    // ce_core_reset (all-or-nothing, lib.rs:431-456), as after a table overflow
+    d->poisoned = true;
+    return ctx->fail(CE_ERR_DEVICE, "state reader: early merge for a declined file");
+  }
   uint64_t dev_dots = 0;
   for (size_t i = 0; i < n; i++)
     if (ds[i].device) dev_dots += ds[i].n_dots;
@@ -2691,20 +2696,24 @@ int ds_state_bytes_device(ce_core* c, ce_ctx* x, uint8_t* dst, uint64_t cap, uin
 // counter) pairs straight from the collect, its clock and next_op_versions, its actor UUIDs --
 // instead of a serialized StateWrapper that the receiver parses back (read_remote_states' merge,
 // crdt-enc/src/lib.rs:458-466, of every rank's partial).  Layout (byte offsets, 8-aligned):
-//   0 u32 magic 'CECL' | u32 version 1 | u64 pairs np | u32 actors na | u32 flags | u64 0
+//   0 u32 magic 'CECL' | u32 version 1 | u64 pairs np | u32 actors na | u32 flags | u64 dlen
 //   32 uuid[16 na] | clock u64[na] | nov u64[na] | member u64[np] | value u64[np] | actor u32[np]
-// (actor = an index into the partial's own UUID list).  Deferred removals have no column form:
-// such a state is refused (*len = 0) and goes as state bytes.
+//   then, when flags bit 0 (the partial holds deferred removals), at the next 8-byte boundary the
+//   deferred map as dlen bytes of u64 words: n, then per removal nc, nm, (actor, counter) x nc,
+//   member x nm
+// (actor = an index into the partial's own UUID list).
 namespace {
 constexpr uint32_t kColsMagic = 0x4c434543u;  // "CECL"
+constexpr uint32_t kColsDeferred = 1u;        // flags: a deferred section follows the columns
 struct ColsHeader {
   uint32_t magic, version;
   uint64_t np;
   uint32_t na, flags;
-  uint64_t reserved;
+  uint64_t dlen;  // bytes of the deferred section (0 without one)
 };
 static_assert(sizeof(ColsHeader) == 32, "column partial header");
 uint64_t cols_len(uint64_t na, uint64_t np) { return 32 + 32 * na + 20 * np; }
+uint64_t cols_def_off(uint64_t na, uint64_t np) { return (cols_len(na, np) + 7) & ~7ull; }
 }  // namespace
 
 int ds_export_columns_device(ce_core* c, uint8_t* dst, uint64_t cap, uint64_t* len) {
@@ -2713,8 +2722,8 @@ int ds_export_columns_device(ce_core* c, uint8_t* dst, uint64_t cap, uint64_t* l
   ce_ctx* ctx = c->ctx;
   hipStream_t s = ctx->stream;
   *len = 0;
-  if (c->kind != CE_STATE_ORSWOT || !d->deferred.empty())
-    return ctx->fail(CE_ERR_INVALID_ARG, "no column form (deferred removals or not an Orswot): use the state bytes");
+  if (c->kind != CE_STATE_ORSWOT)
+    return ctx->fail(CE_ERR_INVALID_ARG, "no column form (not an Orswot): use the state bytes");
   if (!dst && cap == 0) {  // the query form: *len = 1, the state has a column form
     *len = 1;
     return CE_ERR_INVALID_ARG;
@@ -2725,13 +2734,26 @@ int ds_export_columns_device(ce_core* c, uint8_t* dst, uint64_t cap, uint64_t* l
   uint32_t nl = 0;
   if ((rc = collect(c, &nl))) return rc;
   const uint32_t na = (uint32_t)c->id_actor.size();
-  const uint64_t need = cols_len(na, nl);
+  // the deferred map (small, on the host) as u64 words by this core's actor ids
+  std::vector<uint64_t> dw;
+  if (!d->deferred.empty()) {
+    dw.push_back(d->deferred.size());
+    for (auto& x : d->deferred) {
+      dw.push_back(x.first.size());
+      dw.push_back(x.second.size());
+      for (auto& y : x.first) { dw.push_back(y.first); dw.push_back(y.second); }
+      for (uint64_t m : x.second) dw.push_back(m);
+    }
+  }
+  const uint64_t o_def = cols_def_off(na, nl), dlen = 8ull * dw.size();
+  const uint64_t need = dw.empty() ? cols_len(na, nl) : o_def + dlen;
   *len = need;
   if (need > cap) return ctx->fail(CE_ERR_INVALID_ARG, "device buffer too small for the columns");
-  // header, UUIDs and next versions by id: built in pinned memory, read by the copy launch
-  if ((e = d->cx_host.reserve(32 + 24ull * na + 64))) return ctx->hip_fail(e, "columns");
+  // header, UUIDs, next versions by id and the deferred words: built in pinned memory, read by
+  // the copy launch
+  if ((e = d->cx_host.reserve(32 + 24ull * na + dlen + 64))) return ctx->hip_fail(e, "columns");
   uint8_t* h = d->cx_host.as<uint8_t>();
-  const ColsHeader hd{kColsMagic, 1u, nl, na, 0u, 0ull};
+  const ColsHeader hd{kColsMagic, 1u, nl, na, dw.empty() ? 0u : kColsDeferred, dlen};
   std::memcpy(h, &hd, 32);
   for (uint32_t i = 0; i < na; i++) std::memcpy(h + 32 + 16ull * i, c->id_actor[i].data(), 16);
   uint64_t* hn = reinterpret_cast<uint64_t*>(h + 32 + 16ull * na);
@@ -2749,6 +2771,10 @@ int ds_export_columns_device(ce_core* c, uint8_t* dst, uint64_t cap, uint64_t* l
   fl.r[fl.n++] = {w(o_mem), 2ull * nl, 0u, d->col[0].as<uint32_t>()};
   fl.r[fl.n++] = {w(o_val), 2ull * nl, 0u, d->col[2].as<uint32_t>()};
   fl.r[fl.n++] = {w(o_act), nl, 0u, d->col[1].as<uint32_t>()};
+  if (!dw.empty()) {
+    std::memcpy(h + 32 + 24ull * na, dw.data(), dlen);
+    fl.r[fl.n++] = {w(o_def), dlen / 4, 0u, hdev + (32 + 24ull * na) / 4};
+  }
   // complete on return, as the state-bytes export: the caller's collective runs on another stream
   const int tx = ctx->tbegin("cols_export");
   if ((e = launch_fill(s, fl))) return ctx->hip_fail(e, "columns");
@@ -2763,8 +2789,8 @@ int ds_merge_columns_device(ce_core* c, const uint8_t* const* parts, const uint6
   DsState* d = c->ds;
   ce_ctx* ctx = c->ctx;
   hipStream_t s = ctx->stream;
-  if (c->kind != CE_STATE_ORSWOT || !d->deferred.empty())
-    return ctx->fail(CE_ERR_INVALID_ARG, "no column merge (deferred removals or not an Orswot): use the state bytes");
+  if (c->kind != CE_STATE_ORSWOT)
+    return ctx->fail(CE_ERR_INVALID_ARG, "no column merge (not an Orswot): use the state bytes");
   if (k == 0) return CE_OK;
   if (k > 64) return ctx->fail(CE_ERR_INVALID_ARG, "at most 64 column partials per merge");
   hipError_t e;
@@ -2795,8 +2821,11 @@ int ds_merge_columns_device(ce_core* c, const uint8_t* const* parts, const uint6
   for (uint32_t f = 0; f < k; f++) {
     base[f] = d->cx_host.as<uint8_t>() + poff[f];
     std::memcpy(&hd[f], base[f], 32);
-    if (hd[f].magic != kColsMagic || hd[f].version != 1 || hd[f].flags ||
-        cols_len(hd[f].na, hd[f].np) != lens[f] || hd[f].np >= (1ull << 31))
+    const bool hasdef = hd[f].flags == kColsDeferred;
+    const uint64_t want = hasdef ? cols_def_off(hd[f].na, hd[f].np) + hd[f].dlen : cols_len(hd[f].na, hd[f].np);
+    if (hd[f].magic != kColsMagic || hd[f].version != 1 || (hd[f].flags & ~kColsDeferred) ||
+        (hasdef ? (hd[f].dlen < 8 || (hd[f].dlen & 7)) : hd[f].dlen != 0) || want != lens[f] ||
+        hd[f].np >= (1ull << 31))
       return ctx->fail(CE_ERR_DECODE, "not a column partial");
     np_tot += hd[f].np;
     if (32 + 32ull * hd[f].na > pre[f]) more += 32 + 32ull * hd[f].na;
@@ -2861,6 +2890,57 @@ int ds_merge_columns_device(ce_core* c, const uint8_t* const* parts, const uint6
       m += na;
     }
   }
+  // the parts' deferred maps (Orswot::merge merges other.deferred, lib.rs:458-466): downloaded in
+  // one gather, their actors mapped to this core's ids; applied after the k-way merge below
+  std::vector<std::pair<IdDots, std::vector<uint64_t>>> pdef;
+  {
+    std::vector<GatherRange> gr;
+    uint64_t o = 0;
+    for (uint32_t f = 0; f < k; f++)
+      if (hd[f].flags & kColsDeferred) {
+        gr.push_back({parts[f] + cols_def_off(hd[f].na, hd[f].np), o, hd[f].dlen});
+        o += hd[f].dlen;
+      }
+    if (o) {
+      ph.emplace("  cols: deferred");
+      if ((e = d->cx_heads.reserve(o + 64))) return ctx->hip_fail(e, "columns");
+      if ((e = gather_download(d, s, d->cx_heads.as<uint8_t>(), gr, o)) || (e = stream_wait(s)))
+        return ctx->hip_fail(e, "columns");
+      const uint64_t* q = d->cx_heads.as<uint64_t>();
+      uint64_t m = 0, qi = 0;
+      for (uint32_t f = 0; f < k; f++) {
+        const uint64_t na = hd[f].na;
+        if (hd[f].flags & kColsDeferred) {
+          const uint64_t end = qi + hd[f].dlen / 8;
+          auto take = [&](uint64_t* v) {
+            if (qi >= end) return false;
+            *v = q[qi++];
+            return true;
+          };
+          uint64_t nr = 0;
+          if (!take(&nr) || nr > hd[f].dlen / 24) return ctx->fail(CE_ERR_DECODE, "column partial: deferred map");
+          for (uint64_t r = 0; r < nr; r++) {
+            uint64_t nc = 0, nm = 0;
+            if (!take(&nc) || !take(&nm) || nc + nm > end - qi) return ctx->fail(CE_ERR_DECODE, "column partial: deferred map");
+            IdDots ck;
+            for (uint64_t j = 0; j < nc; j++) {
+              uint64_t a = 0, v = 0;
+              take(&a);
+              take(&v);
+              if (a >= na) return ctx->fail(CE_ERR_DECODE, "column partial: deferred actor");
+              if (v) ck.push_back({hmap[m + a], v});
+            }
+            std::sort(ck.begin(), ck.end());
+            std::vector<uint64_t> ms(nm);
+            for (uint64_t j = 0; j < nm; j++) take(&ms[j]);
+            pdef.push_back({std::move(ck), std::move(ms)});
+          }
+          if (qi != end) return ctx->fail(CE_ERR_DECODE, "column partial: deferred map");
+        }
+        m += na;
+      }
+    }
+  }
   ph.emplace("  cols: tables");
   if ((rc = table_upload(c)) || (rc = ensure_clock(c)) || (rc = ensure_pairs(c, np_tot))) return rc;
   ph.emplace("  cols: launch");
@@ -2907,6 +2987,30 @@ int ds_merge_columns_device(ce_core* c, const uint8_t* const* parts, const uint6
   // the parts may be reused by the caller after the return: the merge reads them
   ph.emplace("  cols: settle");
   if ((rc = ds_settle(c))) return rc;
+  // 5) deferred removals (ours and the parts'): every removal's thresholds over the merged pairs
+  //    (apply_rm's reset_remove), finalize, and the removals the merged clock does not cover stay
+  //    deferred (apply_deferred) -- order-free, as the merge rule above
+  if (!pdef.empty() || !d->deferred.empty()) {
+    ph.emplace("  cols: apply deferred");
+    auto rms = deferred_list(d);
+    rms.insert(rms.end(), pdef.begin(), pdef.end());
+    if ((rc = upload_removals(c, rms))) return rc;
+    const uint32_t nr = (uint32_t)rms.size();
+    if ((e = launch_ds_kill(s, tables(d), d->d0[0].as<uint32_t>(), d->d0[1].as<uint32_t>(), d->d0[2].as<uint32_t>(),
+                            d->d0[3].as<unsigned long long>(), d->d0[4].as<unsigned long long>(), nr)))
+      return ctx->hip_fail(e, "columns");
+    d->scratch_dirty = true;
+    if ((rc = finalize(c))) return rc;
+    d->scratch_dirty = false;
+    std::vector<uint8_t> fl2;
+    if ((rc = flags_for(c, d->d0[0].as<uint32_t>(), d->d0[2].as<uint32_t>(), d->d0[3].as<unsigned long long>(), nr, &fl2)))
+      return rc;
+    std::map<IdDots, std::set<uint64_t>> nd;
+    for (uint32_t i = 0; i < nr; i++)
+      if (fl2[i]) nd[rms[i].first].insert(rms[i].second.begin(), rms[i].second.end());
+    d->deferred = std::move(nd);
+    c->path_counts["columns_merge_deferred"]++;
+  }
   return CE_OK;
 }
 

@@ -1513,6 +1513,9 @@ void k_open_fold_v2(DecodeArgs a) {
 // The plaintext past the ciphertext (the last piece's tag bytes XOR keystream) is not masked:
 // the decode reads nothing past len.  ChaCha20, the LDS plaintext and the decode are v2's.
 // ----------------------------------------------------------------------------------------
+// PAIR: the lane's blocks' keystreams two at a time (chacha_block_pre2); EARLY: the next file's
+// parameters loaded when this one starts (a whole iteration of latency) instead of in the decode
+template <bool PAIR, bool EARLY>
 __global__ __launch_bounds__(64, 2)
 void k_open_fold_v3(DecodeArgs a) {
   constexpr int LPF = 16, F = 4, BPL = 4;
@@ -1542,6 +1545,7 @@ void k_open_fold_v3(DecodeArgs a) {
   for (; g < g_end; g++) {
     const uint32_t f = g * F + grp;
     const FilePre2 cur = nx;
+    if (EARLY) nx = load_pre2(a, (g + 1) * F + grp);
     const bool act = cur.ok && cur.len <= kSmallMax;
     const uint32_t len = act ? cur.len : 0u;
     const uint32_t npc = (len + 15) >> 4;             // ciphertext Poly1305 pieces
@@ -1588,15 +1592,17 @@ void k_open_fold_v3(DecodeArgs a) {
     // lane 0's shift and its last piece's valid bytes (others: 0 and 16)
     const uint32_t dl = sub == 0 ? (uint32_t)(4 * nblk) - npc : 0u;
     const uint32_t rb = sub == 0 && npc ? len - 16u * (npc - 1u) : 16u;
+    uint32_t kbn[16];  // PAIR: the keystream of block k - 1 (b + 16), computed with block k's
 
 #pragma unroll
     for (int k = BPL - 1; k >= 0; k--) {
       const int32_t b = nblk - 1 - (int32_t)sub - LPF * k;
       const bool has = b >= 0;
-      if (k == 0) {
+      if (k == (PAIR ? 1 : 0)) {
         // issued before the last block's ChaCha20 (latency hidden under it; the other blocks'
         // ciphertext registers are free by now): the shifted pieces, the tree weights, the tail
-        const uint8_t* pb = has ? src + 16 * (int64_t)(4 * b - (int32_t)dl) : src;
+        const int32_t b0 = nblk - 1 - (int32_t)sub;  // the lane's block k = 0
+        const uint8_t* pb = b0 >= 0 ? src + 16 * (int64_t)(4 * b0 - (int32_t)dl) : src;
 #pragma unroll
         for (int j = 0; j < 4; j++) pc[j] = *reinterpret_cast<const uint4*>(pb + 16 * j);
         const uint32_t* xs = reinterpret_cast<const uint32_t*>(
@@ -1614,7 +1620,16 @@ void k_open_fold_v3(DecodeArgs a) {
         for (int i = 0; i < 4; i++) ts[i] = Xp->ts[i];
       }
       uint32_t kb[16];
-      chacha_block_pre<true, 9>(cpre, cur.key, 1u + (uint32_t)b, 0u, cur.n2a, cur.n2b, kb);
+      if (!PAIR) {
+        chacha_block_pre<true, 9>(cpre, cur.key, 1u + (uint32_t)b, 0u, cur.n2a, cur.n2b, kb);
+      } else {
+        if (k & 1) chacha_block_pre2(cpre, cur.key, 1u + (uint32_t)b, 1u + (uint32_t)(b + LPF), 0u,
+                                     cur.n2a, cur.n2b, kb, kbn);
+        else {
+#pragma unroll
+          for (int i = 0; i < 16; i++) kb[i] = kbn[i];
+        }
+      }
       L5 m[4];
 #pragma unroll
       for (int j = 0; j < 4; j++) {
@@ -1696,8 +1711,9 @@ void k_open_fold_v3(DecodeArgs a) {
 
     // 4) data-version check, decode from LDS, fold; the next iteration's parameters are loaded
     //    inside (their latency hides under the decode)
-    decode_fold<LPF, 0, true>(a, sup, fl, len, act && ok, cur.apply != 0, f, grp, sub, S,
-                              [&] { nx = load_pre2(a, (g + 1) * F + grp); });
+    decode_fold<LPF, 0, true>(a, sup, fl, len, act && ok, cur.apply != 0, f, grp, sub, S, [&] {
+      if (!EARLY) nx = load_pre2(a, (g + 1) * F + grp);
+    });
     __builtin_amdgcn_wave_barrier();
   }
   flush_pending<LPF>(a, sub, S.pslot, S.pbest);
@@ -1733,10 +1749,24 @@ hipError_t launch_open_fold_v2(hipStream_t s, const DecodeArgs& a, int files_per
   // the v3 Poly1305 form (needs the setup's PolyAux rows); CE_FUSED_V2=1 keeps v2 for A/B
   static const bool force_v2 = getenv("CE_FUSED_V2") != nullptr;
   if (files_per_wave == 4 && a.aux && !force_v2) {
-    static const uint32_t res = resident_blocks(k_open_fold_v3, 64);
-    const dim3 grid(std::min<uint32_t>((a.n + 3) / 4, res));
-    if (t0) hipExtLaunchKernelGGL(k_open_fold_v3, grid, dim3(64), 0, s, t0, t1, 0u, a);
-    else hipLaunchKernelGGL(k_open_fold_v3, grid, dim3(64), 0, s, a);
+    // CE_V3=<bits> (A/B of correct variants): 1 = PAIR, 2 = EARLY; default 2 (same box, two runs
+    // each: EARLY 2.899 / 2.859 ms against 2.913 / 2.893, PAIR 2.961 / 2.922)
+    static const int v3 = [] {
+      const char* e = getenv("CE_V3");
+      return e ? atoi(e) : 2;
+    }();
+    auto go = [&](auto kern) {
+      const uint32_t res = resident_blocks(kern, 64);
+      const dim3 grid(std::min<uint32_t>((a.n + 3) / 4, res));
+      if (t0) hipExtLaunchKernelGGL(kern, grid, dim3(64), 0, s, t0, t1, 0u, a);
+      else hipLaunchKernelGGL(kern, grid, dim3(64), 0, s, a);
+    };
+    switch (v3 & 3) {
+      case 1: go(k_open_fold_v3<true, false>); break;
+      case 2: go(k_open_fold_v3<false, true>); break;
+      case 3: go(k_open_fold_v3<true, true>); break;
+      default: go(k_open_fold_v3<false, false>); break;
+    }
     return hipGetLastError();
   }
 #if CE_FUSED_DIAG

@@ -233,9 +233,15 @@ def _recv_merge_device(core, buf, src, group, comm_device, timing):
                        "merge_ms": round((time.perf_counter() - t1) * 1e3, 3)})
 
 
+_MAX_COLUMN_PARTS = 64  # ce_core_merge_columns_device merges at most 64 partials per call
+
+
 def _columns_ok(core, group, device):
-    """every rank can exchange its partial as columns (no deferred removals anywhere): one
+    """every rank can exchange its partial as columns (an Orswot core; deferred removals travel in
+    the columns' deferred section) and the receiver can merge all of them in one call: one
     all_reduce(MAX) of a refusal flag, so all ranks take the same path"""
+    if dist.get_world_size(group) - 1 > _MAX_COLUMN_PARTS:
+        return False
     flag = torch.tensor([0 if core.columns_ready() else 1], dtype=torch.int64, device=device)
     all_reduce_(flag, dist.ReduceOp.MAX, group=group)
     return int(flag.item()) == 0
@@ -253,7 +259,7 @@ def gather_dotset_columns(core, group=None, device="cpu", dst=0, buf=None, timin
     if buf is None:
         buf = StateBuffer(torch.device("cuda", core.ctx.device))
     t0 = time.perf_counter()
-    n = 0
+    n, err = 0, 0
     if rank != dst:
         t = buf.ensure(1 << 20)
         rc, n = core.export_columns_device(t.data_ptr(), t.numel())
@@ -261,13 +267,18 @@ def gather_dotset_columns(core, group=None, device="cpu", dst=0, buf=None, timin
             t = buf.ensure(n)
             rc, n = core.export_columns_device(t.data_ptr(), t.numel())
         if rc:
-            raise RuntimeError("export_columns_device failed: %d" % rc)
+            # the failure goes into the length exchange below (n = -rc), so every rank raises
+            # together instead of the others waiting in the collectives for this one
+            n, err = -abs(rc), rc
     t1 = time.perf_counter()
     # every partial's length in one all_gather, then every transfer posted at once: each peer's
     # partial comes over its own xGMI link instead of one after another
     got = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(world)]
     dist.all_gather(got, torch.tensor([n], dtype=torch.int64, device=device), group=group)
     lens_all = [int(x.item()) for x in got]
+    bad = [(r, -x) for r, x in enumerate(lens_all) if x < 0]
+    if bad:
+        raise RuntimeError("export_columns_device failed on rank(s) %s" % ", ".join("%d (%d)" % b for b in bad))
     if rank != dst:
         peer = _global(group, dst)
         src = t[:n] if _on_comm_device(t, device) else t[:n].to(device)

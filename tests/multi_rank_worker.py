@@ -72,7 +72,7 @@ def workload_orswot(seed=88, n_actors=8, versions=4, p_rm=0.2):
     return key, acts, sealed, fa, fv
 
 
-def main_orswot(rank, world, out, tree=False, p_rm=0.2):
+def main_orswot(rank, world, out, tree=False, p_rm=0.2, device="cpu"):
     import crdtenc
     import shard
     key, actors, files, fa, fv = workload_orswot(p_rm=p_rm)
@@ -87,7 +87,7 @@ def main_orswot(rank, world, out, tree=False, p_rm=0.2):
                                [fv[i] for i in sel])[0]
 
     if tree:   # the binomial-tree reduce to rank 0 (shard.ingest_dotset_sharded)
-        rc, merges = shard.ingest_dotset_sharded(core, ingest)
+        rc, merges = shard.ingest_dotset_sharded(core, ingest, device=device)
         assert rc == 0, rc
         tag = b"tree %d %d" % (merges, core.path_count("columns_merge"))
     else:
@@ -150,11 +150,18 @@ def main():
     import torch.distributed as dist
     import crdtenc
     import shard
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # CE_TEST_BACKEND=nccl: RCCL (one rank per device; the one-GPU box runs world 1), the
+    # collectives on device tensors
+    backend = os.environ.get("CE_TEST_BACKEND", "gloo")
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+    dist.init_process_group(backend, rank=rank, world_size=world)
+    cdev = "cuda:0" if backend == "nccl" else "cpu"
     try:
         if mode in ("orswot", "orswot_tree", "orswot_adds"):
             # orswot_adds: adds only, no deferred removal -- the column exchange
-            main_orswot(rank, world, out, tree=mode != "orswot", p_rm=0.0 if mode == "orswot_adds" else 0.2)
+            main_orswot(rank, world, out, tree=mode != "orswot", p_rm=0.0 if mode == "orswot_adds" else 0.2,
+                        device=cdev)
             return
         if mode.startswith("sharded:"):
             main_sharded(rank, world, mode.split(":", 1)[1], out)

@@ -1325,8 +1325,7 @@ def test_columns_export_merge_equals_state_merge(ctx):
     """The column form of the multi-GPU exchange through the C ABI: writer shards folded on
     separate cores, the others' states exported as columns into HBM and merged into the first in
     one k-way merge == merging their StateWrappers one by one == one core over every file == the
-    oracle; a state with a deferred removal has no column form (*len = 0) and the receiver with
-    one refuses the merge."""
+    oracle; a state with a deferred removal exports its deferred map with the columns."""
     import torch
     rng = random.Random(6060)
     key = rng.randbytes(32)
@@ -1365,14 +1364,75 @@ def test_columns_export_merge_equals_state_merge(ctx):
     # not a column partial: refused, state unchanged
     bad = torch.zeros(256, dtype=torch.uint8, device="cuda:0")
     assert shards[1].merge_columns_device([bad.data_ptr()], [256]) == 12
-    # deferred removals: no column form
+    # a deferred removal travels in the columns' deferred section: either side may hold one
     dfiles = {acts[0]: [[("Rm", C.VClock({acts[1]: 99}), [7])]]}
     dacts, dclears, dfa, dfv = G.batch(dfiles, "orswot", APP, start={acts[0]: 0})
     d = new_core(ctx, "orswot", key)
     assert d.ingest_ops(seal_files(ctx, key, dclears), dacts, dfa, dfv)[0] == 0
-    assert not d.columns_ready()
+    assert d.columns_ready()
     rc, n = d.export_columns_device(bufs[0].data_ptr(), bufs[0].numel())
-    assert rc == 64 and n == 0
-    assert d.merge_columns_device([bufs[0].data_ptr()], [lens[0]]) == 64
-    for core in shards + [seq, d]:
+    assert rc == 0 and n > 0
+    dbuf = bufs[0][:n].clone()
+    seq2 = new_core(ctx, "orswot", key)
+    assert seq2.merge_state(shards[1].state_bytes()) == 0 and seq2.merge_state(d.state_bytes()) == 0
+    assert shards[1].merge_columns_device([dbuf.data_ptr()], [n]) == 0       # theirs deferred
+    assert shards[1].state_bytes() == seq2.state_bytes()
+    assert shards[1].path_count("columns_merge_deferred") == 1
+    seq3 = new_core(ctx, "orswot", key)
+    assert seq3.merge_state(d.state_bytes()) == 0 and seq3.merge_state(shards[2].state_bytes()) == 0
+    assert d.merge_columns_device([bufs[1].data_ptr()], [lens[1]]) == 0       # ours deferred
+    assert d.state_bytes() == seq3.state_bytes()
+    for core in shards + [seq, seq2, seq3, d]:
+        core.close()
+
+
+@pytest.mark.parametrize("shape", ["writers", "overlap"])
+def test_columns_merge_deferred_and_covered_removals(ctx, shape):
+    """Column partials that hold deferred removals and removals covering each other's dots:
+    well-formed histories whose removals carry the member's whole read context (crdts
+    rm(member, read_ctx)).  "writers": writer shards, so a shard defers a removal that names
+    another writer's dots; "overlap": every shard folds three consecutive writers, so the
+    partials' clocks overlap and one partial's removals cover pairs another still holds (the
+    kill side of the merge rule through k_cols_remap's remapped clocks).  One k-way merge of the
+    exported columns == merging the StateWrappers one by one == one core over every file == the
+    oracle (crdt-enc/src/lib.rs:457-465, Orswot::merge with other.deferred)."""
+    import torch
+    rng = random.Random(7171 if shape == "writers" else 7272)
+    key = rng.randbytes(32)
+    actors = G.actors_for(rng, 9)
+    files = G.well_formed_orswot(rng, actors, 5, 8, 60, p_rm=0.35)[0]
+    acts, clears, fa, fv = G.batch(files, "orswot", APP)
+    sealed = seal_files(ctx, key, clears)
+    oc = C.Core("orswot")
+    assert oc.read_remote_ops(key, [APP], sealed, [acts[i] for i in fa], fv)[0] == 0
+    ns = 3
+    shards = []
+    for r in range(ns):
+        if shape == "writers":
+            ws = {a for a in range(len(acts)) if a % ns == r}
+        else:
+            ws = {(3 * r + j) % len(acts) for j in range(5)}
+        idx = [i for i in range(len(fa)) if fa[i] in ws]
+        core = new_core(ctx, "orswot", key)
+        assert core.ingest_ops([sealed[i] for i in idx], acts, [fa[i] for i in idx], [fv[i] for i in idx])[0] == 0
+        shards.append(core)
+    seq = new_core(ctx, "orswot", key)
+    for core in shards:
+        assert seq.merge_state(core.state_bytes()) == 0
+    bufs, lens = [], []
+    for core in shards[1:]:
+        rc, n = core.export_columns_device(0, 0)
+        assert rc == 64 and n == 1
+        t = torch.zeros(1 << 21, dtype=torch.uint8, device="cuda:0")
+        rc, n = core.export_columns_device(t.data_ptr(), t.numel())
+        assert rc == 0 and n > 0
+        bufs.append(t)
+        lens.append(n)
+    assert shards[0].merge_columns_device([t.data_ptr() for t in bufs], lens) == 0
+    got = shards[0].state_bytes()
+    assert got == seq.state_bytes() == oc.serialize()
+    assert shards[0].path_count("columns_merge") == 1
+    # the workload exercises what it says: some partial held a deferred removal
+    assert shards[0].path_count("columns_merge_deferred") == 1
+    for core in shards + [seq]:
         core.close()

@@ -108,27 +108,30 @@ def test_reduce_dotset_two_processes(tmp_path):
     assert oc.read_remote_ops(key, [APP], files, [actors[i] for i in fa], fv)[0] == 0
     out = str(tmp_path / "t")
     port = str(_port())
+    env = dict(os.environ, CE_DS_EXCHANGE="tree")
     procs = [subprocess.Popen([sys.executable, os.path.join(REPO, "tests", "multi_rank_worker.py"),
-                               str(r), "2", port, "orswot_tree", out]) for r in range(2)]
+                               str(r), "2", port, "orswot_tree", out], env=env) for r in range(2)]
     assert [p.wait(timeout=180) for p in procs] == [0, 0]
     with open(out + ".0", "rb") as f:
         tag, state = f.read().split(b"\n", 1)
-    # (this workload's partials carry deferred removals: the serialized tree, not the columns)
+    # (CE_DS_EXCHANGE=tree: the serialized tree for partials with deferred removals)
     assert tag == b"tree 1 0" and state == oc.serialize()
     with open(out + ".1", "rb") as f:
         assert f.read().split(b"\n", 1)[0] == b"tree 0 0"
 
 
-@pytest.mark.parametrize("world,exchange", [(3, "columns"), (3, "tree")])
-def test_reduce_dotset_columns_three_processes(tmp_path, world, exchange):
-    """The column exchange (no deferred removal on any rank): ranks 1..N-1 export their partial
-    Orswot as columns (ce_core_export_columns_device), rank 0 merges all of them in one k-way merge
+@pytest.mark.parametrize("world,exchange,p_rm", [(3, "columns", 0.0), (3, "tree", 0.0), (3, "columns", 0.2)])
+def test_reduce_dotset_columns_three_processes(tmp_path, world, exchange, p_rm):
+    """The column exchange: ranks 1..N-1 export their partial Orswot as columns
+    (ce_core_export_columns_device), rank 0 merges all of them in one k-way merge
     (ce_core_merge_columns_device) and holds the oracle's single fold; CE_DS_EXCHANGE=tree takes
-    the serialized binomial tree for the same files, with the same result."""
+    the serialized binomial tree for the same files, with the same result.  p_rm 0.2: removals
+    with the member's read context, so ranks hold deferred removals (the columns' deferred
+    section)."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import multi_rank_worker as W
     from oracle import crdts as C
-    key, actors, files, fa, fv = W.workload_orswot(p_rm=0.0)
+    key, actors, files, fa, fv = W.workload_orswot(p_rm=p_rm)
     oc = C.Core("orswot")
     assert oc.read_remote_ops(key, [APP], files, [actors[i] for i in fa], fv)[0] == 0
     out = str(tmp_path / "t")
@@ -137,7 +140,8 @@ def test_reduce_dotset_columns_three_processes(tmp_path, world, exchange):
     if exchange == "tree":
         env["CE_DS_EXCHANGE"] = "tree"
     procs = [subprocess.Popen([sys.executable, os.path.join(REPO, "tests", "multi_rank_worker.py"),
-                               str(r), str(world), port, "orswot_adds", out], env=env) for r in range(world)]
+                               str(r), str(world), port, "orswot_adds" if p_rm == 0.0 else "orswot_tree", out],
+                              env=env) for r in range(world)]
     assert [p.wait(timeout=180) for p in procs] == [0] * world
     with open(out + ".0", "rb") as f:
         tag, state = f.read().split(b"\n", 1)
