@@ -563,11 +563,14 @@ def ops_fused(pt):
     return ops_8d(pt) - 992 - 960
 
 
+PROFILE_ROUND = "r06"
+
+
 def rocprof_avg_ms(name):
     """average duration of the kernel whose name starts with `name` in this round's committed
-    rocprofv3 --kernel-trace --stats summary of the bench (profiles/r05_kernel_stats.csv), or None"""
+    rocprofv3 --kernel-trace --stats summary of the bench (profiles/<round>_kernel_stats.csv), or None"""
     import csv
-    f = os.path.join(REPO, "profiles", "r05_kernel_stats.csv")
+    f = os.path.join(REPO, "profiles", PROFILE_ROUND + "_kernel_stats.csv")
     if not os.path.exists(f):
         return None
     with open(f) as fh:
@@ -613,7 +616,7 @@ def main():
     ap.add_argument("--no-clock", action="store_true", help="skip the shader-clock probe")
     ap.add_argument("--no-host-buffers", action="store_true",
                     help="skip the end-to-end run from host buffers (H2D over PCIe)")
-    ap.add_argument("--configs", default="c3,c4,c5",
+    ap.add_argument("--configs", default="c3,c3r,c4,c5",
                     help="N=1: also run these BASELINE configs (bench_configs.py runners) and report "
                          "them under the line's `configs` key ('' = none)")
     ap.add_argument("--no-strong", action="store_true", help="N > 1: skip the strong-scaling C2 leg")
@@ -715,8 +718,9 @@ def main():
             # C3: 120 steps (~0.4 s) -- every step's 35 MB file is named by a ~48 ms SHA3 on a host
             # thread, so the timed region (which ends when the last name is done) approaches the
             # steady state only over many steps: the last name's latency weighs ~0.4 ms a step here
-            steps_c = {"c3": 120, "c4": 10, "c5": 10}[c]
-            extra = {"c3": ["--versions", "2", "--state-versions", "1"], "c4": ["--c4-versions", "2"],
+            steps_c = {"c3": 120, "c3r": 40, "c4": 10, "c5": 10}[c]
+            extra = {"c3": ["--versions", "2", "--state-versions", "1"],
+                     "c3r": ["--versions", "2", "--state-versions", "1"], "c4": ["--c4-versions", "2"],
                      "c5": ["--c5-versions", "4"]}[c] if args.quick else []
             ns = bench_configs.make_parser().parse_args(
                 ["--config", c, "--steps", str(2 if args.quick else steps_c), "--warmup", "1", "--no-clock"] +
@@ -735,9 +739,15 @@ def main():
     if rank == 0:
         fused = os.environ.get("CE_FUSED", str(DEFAULT_FUSED))
         lpf = 64 // int(os.environ.get("CE_FILES_PER_WAVE", "4"))
-        kname = ("k_open_fold_v2<%d> (XChaCha20-Poly1305 open + Vec<Dot> decode + fold, "
+        v3 = fused == "2" and lpf == 16 and not os.environ.get("CE_FUSED_V2")
+        v3b = int(os.environ.get("CE_V3", "2"))
+        kname = ("k_open_fold_v3<%s, %s> (XChaCha20-Poly1305 open + Vec<Dot> decode + fold, lane-owned "
+                 "ChaCha20 blocks, Poly1305 as four-product column sums)"
+                 % ("true" if v3b & 1 else "false", "true" if v3b & 2 else "false") if v3 else
+                 "k_open_fold_v2<%d> (XChaCha20-Poly1305 open + Vec<Dot> decode + fold, "
                  "lane-owned ChaCha20 blocks)" % lpf if fused == "2" and lpf != 64 else
                  "k_open_fold_small<%d> (XChaCha20-Poly1305 open + Vec<Dot> decode + fold)" % lpf)
+        kshort = kname.split(" (")[0]
         traffic = None
         tf = os.path.join(REPO, "profiles", "traffic_open_fold_small.json")
         if os.path.exists(tf):
@@ -753,7 +763,7 @@ def main():
             with open(vf) as f:
                 rec = json.load(f).get("fused", {})
             ipf = rec.get("valu_instr_per_file_per_lane")
-            if ipf and rec.get("kernel", "") in kname:
+            if ipf and rec.get("kernel", "").replace("ce::", "") == kshort:
                 t = wa_n(args, world) * ipf / (sa["avg_launch_ms"] / 1e3) / 1e12
                 valu_pmc = {"instr_per_file": ipf, "achieved_tops": round(t, 2),
                             "frac_of_peak": round(t / VALU_PEAK_TOPS, 4),
@@ -805,7 +815,7 @@ def main():
                 "fused_only": {"ops_per_file": sa["ops_per_file_fused"], "achieved": sa["valu_tops_fused_only"],
                                "frac": sa["valu_frac_fused_only"],
                                "note": "the fused kernel alone: §8d less the setup's 1,952 ops per file"},
-                "rocprof": rocprof_frac(sa, wa_n(args, world)),
+                "rocprof": rocprof_frac(sa, wa_n(args, world), kshort),
                 "measured_chacha20_ceiling": {
                     "tops": round(VALU_CHACHA_TOPS, 1), "keystream_TBps": CHACHA_KS_TBPS,
                     "frac": round(sa["valu_tops"] / VALU_CHACHA_TOPS, 4),
@@ -841,16 +851,26 @@ def main():
         sys.exit(3)
 
 
-def rocprof_frac(sa, n):
+def rocprof_frac(sa, n, kshort):
     """the same fraction with the committed rocprofv3 averages of the two kernels (the verdict's
-    recomputation uses these), None without this round's profile"""
-    f = rocprof_avg_ms("ce::k_open_fold_v2<16, 2, false, 1, true, false>")
+    recomputation uses these) -- only when the profile is of the kernel this run launched, over
+    the same files per launch (its .meta.json, written with it), else None"""
+    meta = os.path.join(REPO, "profiles", PROFILE_ROUND + "_kernel_stats.meta.json")
+    if not os.path.exists(meta):
+        return None
+    with open(meta) as fh:
+        m = json.load(fh)
+    if m.get("files_per_launch") != n or m.get("fused_kernel", "").replace("ce::", "") != kshort:
+        return None
+    f = rocprof_avg_ms("ce::" + kshort)
     s = rocprof_avg_ms("ce::k_open_setup")
     if not f or not s:
         return None
     t = n * sa["ops_per_file"] / ((f + s) / 1e3) / 1e12
     return {"fused_avg_ms": round(f, 4), "setup_avg_ms": round(s, 4), "achieved": round(t, 2),
-            "frac": round(t / VALU_PEAK_TOPS, 4), "source": "profiles/r05_kernel_stats.csv"}
+            "frac": round(t / VALU_PEAK_TOPS, 4), "files_per_launch": m["files_per_launch"],
+            "kernel": m["fused_kernel"], "command": m.get("command"),
+            "source": "profiles/%s_kernel_stats.csv" % PROFILE_ROUND}
 
 
 def wa_n(args, world):

@@ -137,8 +137,75 @@ def orswot_clears(actors, a_idx, v, dev):
     return out
 
 
-def seal_op_files(ctx, key, actors, a_lo, a_hi, v_lo, v_hi, dev, seed):
-    """op files of actors [a_lo, a_hi) x versions [v_lo, v_hi), actor-major (load_ops order)"""
+_READ_CTX = {}
+READ_CTX_STATS = {}  # the last read-ctx batch: plaintext bytes, removal clock entries
+
+
+def read_ctx_table(V0):
+    """What every writer has read from the state files when its op versions start: per member, the
+    (actor, largest counter) of the adds of versions [0, V0) listing it, actors ascending (a
+    VClock's BTreeMap order; the actor table is sorted by UUID bytes) -- CSR by member."""
+    if V0 in _READ_CTX:
+        return _READ_CTX[V0]
+    a = torch.arange(N_ACTORS, dtype=torch.int64).repeat_interleave(V0 * N_ADD)
+    v = torch.arange(V0, dtype=torch.int64).repeat_interleave(N_ADD).repeat(N_ACTORS)
+    j = torch.arange(N_ADD, dtype=torch.int64).repeat(N_ACTORS * V0)
+    m = member_of(a, v, j).numpy()
+    a, ctr = a.numpy(), (v * N_ADD + j + 1).numpy()
+    o = np.lexsort((ctr, a, m))
+    m, a, ctr = m[o], a[o], ctr[o]
+    last = np.ones(len(m), bool)  # the last (largest counter) of each (member, actor) run
+    last[:-1] = (m[1:] != m[:-1]) | (a[1:] != a[:-1])
+    m, a, ctr = m[last], a[last], ctr[last]
+    beg = np.searchsorted(m, np.arange(N_MEMBERS + 1))
+    _READ_CTX[V0] = (beg, a, ctr)
+    return _READ_CTX[V0]
+
+
+def orswot_clears_read_ctx(actors, a_idx, v, V0):
+    """orswot_clears with every Rm carrying the removed member's read context in place of the
+    one-entry clock {writer: its own earlier counter}: Rm{clock: the member's entry clock as writer
+    a reads it -- the state files' adds of m (read_ctx_table) and a's own removed add --, members:
+    [m]}, crdts' rm(member, read_ctx), fixed-width uints.  Clocks name other writers' dots, so a
+    writer shard defers them ("Rm ops with read-ctx clocks").  -> plaintexts"""
+    base = orswot_clears(actors, a_idx.cpu(), v.cpu(), "cpu").numpy()
+    beg, ta, tc = read_ctx_table(V0)
+    beg, ta, tc = beg.tolist(), ta.tolist(), tc.tolist()
+    ent_b = [b"\xc4\x10" + actors[x].tobytes() + b"\xce" for x in range(N_ACTORS)]
+    cut = len(HDR) + N_ADD * len(ADD_T)
+    vv = torch.where(v > 0, v - 1, v).cpu()
+    k = torch.arange(N_RM, dtype=torch.int64)
+    jv = (k * 5 + 3) % N_ADD
+    mm = member_of(a_idx.cpu()[:, None], vv[:, None], jv[None, :]).tolist()
+    own = (vv[:, None] * N_ADD + jv[None, :] + 1).tolist()
+    out = []
+    n_ent = 0
+    for i, ai in enumerate(a_idx.tolist()):
+        parts = [base[i, :cut].tobytes()]
+        for r in range(N_RM):
+            m = mm[i][r]
+            b0, b1 = beg[m], beg[m + 1]
+            ent = dict(zip(ta[b0:b1], tc[b0:b1]))
+            oc = own[i][r]
+            if ent.get(ai, 0) < oc:
+                ent[ai] = oc
+            e = len(ent)
+            n_ent += e
+            parts.append(b"\x81\xa2Rm\x82\xa5clock\x81\xa4dots")
+            parts.append(bytes([0x80 | e]) if e <= 15 else b"\xde" + e.to_bytes(2, "big"))
+            for x in sorted(ent):
+                parts.append(ent_b[x] + ent[x].to_bytes(4, "big"))
+            parts.append(b"\xa7members\x91\xce" + m.to_bytes(4, "big"))
+        out.append(b"".join(parts))
+    READ_CTX_STATS["clock_entries"] = n_ent
+    return out
+
+
+def seal_op_files(ctx, key, actors, a_lo, a_hi, v_lo, v_hi, dev, seed, rm_ctx="own", V0=None):
+    """op files of actors [a_lo, a_hi) x versions [v_lo, v_hi), actor-major (load_ops order).
+    rm_ctx "read": removals carry read contexts (orswot_clears_read_ctx; variable file lengths)"""
+    if rm_ctx == "read":
+        return _seal_op_files_read_ctx(ctx, key, actors, a_lo, a_hi, v_lo, v_hi, dev, seed, V0)
     na, nv = a_hi - a_lo, v_hi - v_lo
     n = na * nv
     flen = 16 + crdtenc.sealed_len(PT_LEN)
@@ -162,6 +229,37 @@ def seal_op_files(ctx, key, actors, a_lo, a_hi, v_lo, v_hi, dev, seed):
     fa = torch.arange(na, dtype=torch.int32, device=dev).repeat_interleave(nv)
     fv = torch.arange(v_lo, v_hi, dtype=torch.int64, device=dev).repeat(na)
     return files, offs, n, n * flen, fa, fv
+
+
+def _seal_op_files_read_ctx(ctx, key, actors, a_lo, a_hi, v_lo, v_hi, dev, seed, V0):
+    na, nv = a_hi - a_lo, v_hi - v_lo
+    n = na * nv
+    idx = torch.arange(n, dtype=torch.int64)
+    a_idx, v = a_lo + idx // nv, v_lo + idx % nv
+    clears = orswot_clears_read_ctx(actors, a_idx, v, V0 if V0 is not None else v_lo)
+    clen = np.array([len(c) for c in clears], np.int64)
+    READ_CTX_STATS.update(plaintext_bytes=int(clen.sum()), files=n, mean_file_plaintext=round(float(clen.mean()), 1),
+                          max_file_plaintext=int(clen.max()))
+    flen = np.array([16 + crdtenc.sealed_len(int(x)) for x in clen], np.int64)
+    fo = np.zeros(n + 1, np.int64)
+    fo[1:] = np.cumsum(flen)
+    co = np.zeros(n + 1, np.int64)
+    co[1:] = np.cumsum(clen)
+    clear = torch.from_numpy(np.frombuffer(b"".join(clears), np.uint8).copy()).to(dev)
+    files = torch.empty(int(fo[-1]) + 64, dtype=torch.uint8, device=dev)
+    coffs = torch.from_numpy(co).to(dev)
+    ooffs = torch.from_numpy(fo[:-1].copy()).to(dev)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed)
+    nonces = torch.randint(0, 256, (n, 24), dtype=torch.uint8, device=dev, generator=gen)
+    torch.cuda.current_stream().synchronize()
+    ctx.encrypt_batch_device(key, clear.data_ptr(), coffs.data_ptr(), n, nonces.data_ptr(),
+                             files.data_ptr(), ooffs.data_ptr(), outer_version=CORE)
+    ctx.synchronize()
+    offs = torch.from_numpy(fo).to(dev)
+    fa = torch.arange(na, dtype=torch.int32, device=dev).repeat_interleave(nv)
+    fv = torch.arange(v_lo, v_hi, dtype=torch.int64, device=dev).repeat(na)
+    return files, offs, n, int(fo[-1]), fa, fv
 
 
 def name_threads():
@@ -386,6 +484,7 @@ def run_c3(args, ctx, dev):
     actors = actors_table()
     key = bytes(np.random.default_rng(7).integers(0, 256, 32, dtype=np.uint8))
     V0, V = args.state_versions, args.versions
+    rm_ctx = getattr(args, "rm_ctx", "own")
     t0 = time.time()
     # state files: compaction (ingest-readable format) of 512 actors' versions [0, V0) each
     states = []
@@ -401,7 +500,9 @@ def run_c3(args, ctx, dev):
         states.append(sc.compact_to_buffer(nonce=bytes(24))[0])
         sc.close()
         del f, o
-    files, offs, n, blob_len, fa, fv = seal_op_files(ctx, key, actors, 0, N_ACTORS, V0, V0 + V, dev, 1234)
+    files, offs, n, blob_len, fa, fv = seal_op_files(ctx, key, actors, 0, N_ACTORS, V0, V0 + V, dev, 1234,
+                                                     rm_ctx=rm_ctx, V0=V0)
+    rc_stats = dict(READ_CTX_STATS) if rm_ctx == "read" else None
     all_actors = b"".join(bytes(a) for a in actors)
     log("c3: %d state files (%.1f MB), %d op files (%.2f GB) in %.1f s" % (
         len(states), sum(map(len, states)) / 1e6, n, blob_len / 1e9, time.time() - t0))
@@ -537,11 +638,11 @@ def run_c3(args, ctx, dev):
         lo, hi = r * N_ACTORS // 2, (r + 1) * N_ACTORS // 2
         for sw_i in range(8 * r // 2, 8 * (r + 1) // 2):
             assert p.ingest_states([states[sw_i]])[0] == 0
-        flen = blob_len // n
         f0, f1 = lo * V, hi * V
-        sub = files[f0 * flen: f1 * flen]
-        so = offs[: f1 - f0 + 1]
-        rc = p.ingest_ops_device(sub.data_ptr(), so.data_ptr(), f1 - f0, (f1 - f0) * flen,
+        b0, b1 = int(offs[f0]), int(offs[f1])
+        sub = files[b0:b1]
+        so = (offs[f0:f1 + 1] - b0).contiguous()
+        rc = p.ingest_ops_device(sub.data_ptr(), so.data_ptr(), f1 - f0, b1 - b0,
                                  b"".join(bytes(a) for a in actors[lo:hi]),
                                  (fa[f0:f1] - lo).contiguous().data_ptr(), fv[f0:f1].contiguous().data_ptr())
         assert rc == 0, rc
@@ -565,25 +666,33 @@ def run_c3(args, ctx, dev):
 
     k_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in kern.items() if v[1]}
     n_state = len(states)
-    ct = n * PT_LEN + sum(len(s) for s in states)
+    pt_ops = rc_stats["plaintext_bytes"] if rc_stats else n * PT_LEN
+    ct = pt_ops + sum(len(s) for s in states)
     open_ms = sum(k_ms.get(x, 0) for x in ("open_setup", "open_small", "segments_open", "finalize_open"))
     # fold roofline: algorithmic bytes of the columnar fold per step -- adds: actor 4 + counter 8
     # + mbeg 4 + member 8 + pair key/value RMW 32; removals: cbeg/mbeg 8 + clock entry 12 +
     # member 8 + pair key/kill 24
     n_add, n_rm = n * N_ADD, n * N_RM
-    fold_bytes = n_add * (4 + 8 + 4 + 8 + 32) + n_rm * (8 + 12 + 8 + 24)
+    n_rmc = rc_stats["clock_entries"] if rc_stats else n_rm   # removal clock entries
+    fold_bytes = n_add * (4 + 8 + 4 + 8 + 32) + n_rm * (8 + 8) + n_rmc * (12 + 24)
     # (the partitioned fold: applied flags + ds_part_fold = member probes, bucketing, the LDS fold
     # with finalize, the clock; the global kernels: applied + add_pairs + kill, finalize apart)
     # (ds_contig: the contiguity check, which also writes the applied flags of increasing runs)
     fold_ms = sum(k_ms.get(x, 0) for x in ("ds_applied", "ds_contig", "ds_add_pairs", "ds_kill", "ds_part_fold"))
+    shape = ("26 Add + 6 Rm, %d B" % PT_LEN if not rc_stats else
+             "26 Add + 6 Rm whose clocks are the removed member's read context (the state files' adds "
+             "of it + the writer's own: %.2f entries per clock), %.0f B mean, %d B max"
+             % (n_rmc / n_rm, rc_stats["mean_file_plaintext"], rc_stats["max_file_plaintext"]))
     line = {
-        "metric": "C3 op+state files compacted/sec (Orswot<u64,Uuid>)",
+        "metric": "C3 op+state files compacted/sec (Orswot<u64,Uuid>)" + (
+            ", read-context removals" if rc_stats else ""),
         "value": round((n + n_state) / (ms / 1e3), 1), "unit": "files/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
         "higher_is_better": True, "dtype": "u32/u64", "data": "synthetic (GPU-sealed, seeded)",
         "config": {"workload": "C3: Orswot, %d members, %d actors; %d state files (512 actors x %d "
-                               "versions each) + %d op files (4096 x %d versions, 26 Add + 6 Rm, %d B), "
-                               "all resident in HBM" % (N_MEMBERS, N_ACTORS, n_state, V0, n, V, PT_LEN),
+                               "versions each) + %d op files (4096 x %d versions, %s), "
+                               "all resident in HBM" % (N_MEMBERS, N_ACTORS, n_state, V0, n, V, shape),
+                   "rm_ctx": rm_ctx, "removal_clock_entries": n_rmc,
                    "ops": n * (N_ADD + N_RM), "entries": entries,
                    "state_file_bytes": int(len(out["file"])), "name_ms": name_ms},
         "single_compact_latency": single_call,
@@ -952,7 +1061,9 @@ def run_c3_multi(args, ctx, dev, world, rank):
     mine = [j for j in range(8) if lo <= j * per < hi]
     states = _state_files_c3(ctx, key, actors, V0, dev, mine)
     my_states = [states[j] for j in mine]
-    files, offs, n, blob_len, fa, fv = seal_op_files(ctx, key, actors, lo, hi, V0, V0 + V, dev, 1234 + rank)
+    rm_ctx = getattr(args, "rm_ctx", "own")
+    files, offs, n, blob_len, fa, fv = seal_op_files(ctx, key, actors, lo, hi, V0, V0 + V, dev, 1234 + rank,
+                                                     rm_ctx=rm_ctx, V0=V0)
     writers = b"".join(bytes(a) for a in actors[lo:hi])
     log("c3 rank %d: writers [%d, %d), %d state files, %d op files in %.1f s" % (
         rank, lo, hi, len(my_states), n, time.time() - t0))
@@ -1037,7 +1148,8 @@ def run_c3_multi(args, ctx, dev, world, rank):
         entries = len(d[b"state"][b"entries"])
         # the single-core fold of every file, untimed
         all_states = _state_files_c3(ctx, key, actors, V0, dev, range(8))
-        fw, ow, nw, bw, faw, fvw = seal_op_files(ctx, key, actors, 0, N_ACTORS, V0, V0 + V, dev, 4321)
+        fw, ow, nw, bw, faw, fvw = seal_op_files(ctx, key, actors, 0, N_ACTORS, V0, V0 + V, dev, 4321,
+                                                 rm_ctx=rm_ctx, V0=V0)
         whole = new_core(ctx, key)
         assert whole.ingest_states([all_states[j] for j in range(8)])[0] == 0
         rc = whole.ingest_ops_device(fw.data_ptr(), ow.data_ptr(), nw, bw, b"".join(bytes(a) for a in actors),
@@ -1048,14 +1160,15 @@ def run_c3_multi(args, ctx, dev, world, rank):
         pipe.close()
     ok_clock, ok_whole = _all_true(ok_clock, dev), _all_true(ok_whole, dev)
     line = {
-        "metric": "C3 op+state files compacted/sec (Orswot<u64,Uuid>)",
+        "metric": "C3 op+state files compacted/sec (Orswot<u64,Uuid>)" + (
+            ", read-context removals" if rm_ctx == "read" else ""),
         "value": round(n_total / (ms / 1e3), 1), "unit": "files/s", "n_gpus": world, "scaling": "strong",
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
         "higher_is_better": True, "dtype": "u32/u64", "data": "synthetic (GPU-sealed, seeded)",
         "config": {"workload": "C3: Orswot, %d members, %d actors; 8 state files (512 actors x %d versions "
                                "each) + %d op files (4096 x %d versions, 26 Add + 6 Rm, %d B), split over %d "
                                "ranks by writer" % (N_MEMBERS, N_ACTORS, V0, N_ACTORS * V, V, PT_LEN, world),
-                   "files_total": n_total, "entries": entries,
+                   "files_total": n_total, "entries": entries, "rm_ctx": rm_ctx,
                    "parallelism": "writer shards (shard.actor_range) with their 512-writer state groups; "
                                   "statuses all_reduce(MAX); %s; compaction + content name on rank 0"
                                   % (("partial Orswots as columns gathered to rank 0 in HBM "
@@ -1276,7 +1389,10 @@ def run_c5_multi(args, ctx, dev, world, rank):
 
 def make_parser():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="c3", choices=["c3", "c4", "c5"])
+    ap.add_argument("--config", default="c3", choices=["c3", "c3r", "c4", "c5"])
+    ap.add_argument("--rm-ctx", default="own", choices=["own", "read"],
+                    help="C3 removals: 'own' = one-entry clock {writer: its own earlier counter}; 'read' = "
+                         "the removed member's read context (config c3r)")
     ap.add_argument("--c4-versions", type=int, default=32, help="C4 versions per actor (1024 actors)")
     ap.add_argument("--c5-versions", type=int, default=256, help="C5 versions per actor (4096 actors)")
     ap.add_argument("--c5-clean", action="store_true",
@@ -1293,8 +1409,16 @@ def make_parser():
     return ap
 
 
-RUNNERS = {"c3": run_c3, "c4": run_c4, "c5": run_c5}
-RUNNERS_MULTI = {"c3": run_c3_multi, "c4": run_c4_multi, "c5": run_c5_multi}
+def _read_ctx(run):
+    """config c3r: C3 with read-context removals (SURVEY.md §8d's op shape)"""
+    def go(args, *a):
+        args.rm_ctx = "read"
+        return run(args, *a)
+    return go
+
+
+RUNNERS = {"c3": run_c3, "c3r": _read_ctx(run_c3), "c4": run_c4, "c5": run_c5}
+RUNNERS_MULTI = {"c3": run_c3_multi, "c3r": _read_ctx(run_c3_multi), "c4": run_c4_multi, "c5": run_c5_multi}
 
 
 def run_config(name, args, ctx, dev, world=1, rank=0):
@@ -1308,7 +1432,7 @@ def run_config(name, args, ctx, dev, world=1, rank=0):
 def main():
     args = make_parser().parse_args()
     if args.steps is None:
-        args.steps = 120 if args.config == "c3" else 20
+        args.steps = 120 if args.config == "c3" else 40 if args.config == "c3r" else 20
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     stream = torch.cuda.Stream(device=dev)

@@ -9,10 +9,10 @@
 
 #include <cstdlib>
 
-#include <hipcub/hipcub.hpp>
 
 #include "ce_dotset.h"
 #include "ce_dotset_codec.h"
+#include "ce_dotset_io.h"
 
 namespace ce {
 namespace {
@@ -1737,15 +1737,16 @@ struct MaxOp {
 };
 }  // namespace
 
+// the stable pair sorts: the hand-written LSD radix sort of ce_ser_sort.hip (no hipCUB)
 hipError_t ds_sort_pairs_u32(void* tmp, size_t& tb, const uint32_t* kin, uint32_t* kout,
                              const uint32_t* vin, uint32_t* vout, uint32_t n, int bits, hipStream_t s) {
-  return hipcub::DeviceRadixSort::SortPairs(tmp, tb, kin, kout, vin, vout, (int)n, 0, bits, s);
+  return sort_pairs_u32(tmp, tb, kin, kout, vin, vout, n, bits, s);
 }
 
 hipError_t ds_sort_pairs_u64(void* tmp, size_t& tb, const unsigned long long* kin,
                              unsigned long long* kout, const uint32_t* vin, uint32_t* vout,
                              uint32_t n, hipStream_t s) {
-  return hipcub::DeviceRadixSort::SortPairs(tmp, tb, kin, kout, vin, vout, (int)n, 0, 64, s);
+  return sort_pairs_u64(tmp, tb, kin, kout, vin, vout, n, 64, s);
 }
 
 // ds_excl_max_by_key / ds_excl_sum_u32: ce_scan.hip (no hipCUB: its scans query the device

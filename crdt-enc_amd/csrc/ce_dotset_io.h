@@ -79,6 +79,13 @@ struct SerSortArgs {
   unsigned long long* member_out;
   uint32_t* actor_out;
   unsigned long long* value_out;
+  // generic (sort_pairs_*): the first pass reads keys gk_in / u32 values gv_in, the last writes
+  // gk_out / gv_out (the serializer's key build and column unpack are off)
+  int generic;
+  const void* gk_in;
+  void* gk_out;
+  const uint32_t* gv_in;
+  uint32_t* gv_out;
 };
 uint32_t ser_sort_tiles(uint32_t n);
 inline size_t ser_sort_state_words(uint32_t n) {
@@ -86,6 +93,13 @@ inline size_t ser_sort_state_words(uint32_t n) {
 }
 // kbuf: two key buffers of n (u32 when key_bits <= 32, else u64), vbuf: two u64 buffers of n
 hipError_t launch_ser_sort(hipStream_t s, const SerSortArgs& a, void* const kbuf[2], unsigned long long* const vbuf[2]);
+// Stable LSD radix sort of (key, u32 value) pairs over the key's low `bits` bits (the same
+// kernels as the serializer's sort; hipCUB's DeviceRadixSort::SortPairs interface: tmp == null ->
+// *tb = the scratch bytes needed).  kin / vin are not modified; kout / vout may not alias them.
+hipError_t sort_pairs_u32(void* tmp, size_t& tb, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
+                          uint32_t* vout, uint32_t n, int bits, hipStream_t s);
+hipError_t sort_pairs_u64(void* tmp, size_t& tb, const unsigned long long* kin, unsigned long long* kout,
+                          const uint32_t* vin, uint32_t* vout, uint32_t n, int bits, hipStream_t s);
 hipError_t launch_orswot_ser(hipStream_t s, OrswotSerScratch& sc, const OrswotSerArgs& a);
 // the same in two halves: the sorts and scans over the n collected pairs (no host input), then the
 // writer (needs the host-built prefix / suffix) -- the host builds them while the sorts run

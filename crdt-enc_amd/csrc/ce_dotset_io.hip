@@ -19,7 +19,9 @@
 #include <cstdlib>
 
 #include <algorithm>
+#if CE_FUSED_DIAG  // hipCUB only for the diagnostics build's A/B (CE_SER_CUB)
 #include <hipcub/hipcub.hpp>
+#endif
 #include <map>
 #include <mutex>
 
@@ -792,7 +794,11 @@ hipError_t launch_orswot_ser_sort(hipStream_t s, OrswotSerScratch& sc, uint32_t 
   // by rank, then stably by member, LSD order -- and a gather
   hipError_t e;
   const int kb = sc.member_bits + sc.rank_bits;
-  static const bool cub = getenv("CE_SER_CUB") != nullptr;
+#if CE_FUSED_DIAG
+  static const bool cub = getenv("CE_SER_CUB") != nullptr;  // diagnostics build: hipCUB's sort, A/B
+#else
+  constexpr bool cub = false;
+#endif
   const bool two = getenv("CE_SER_TWO_SORTS") != nullptr;  // (the tests flip it)
   if (n && kb <= 64 && !two && !cub && n < (1u << 30)) {
     SerSortArgs a{};
@@ -814,6 +820,7 @@ hipError_t launch_orswot_ser_sort(hipStream_t s, OrswotSerScratch& sc, uint32_t 
     void* kbuf[2] = {kb <= 32 ? (void*)sc.k32a : (void*)sc.k64a, kb <= 32 ? (void*)sc.k32b : (void*)sc.k64b};
     unsigned long long* vbuf[2] = {sc.v64a, sc.v64b};
     if ((e = launch_ser_sort(s, a, kbuf, vbuf))) return e;
+#if CE_FUSED_DIAG
   } else if (n && kb <= 64 && !two) {
     // (member, rank) in one key: hipCUB's radix sort over member_bits + rank_bits
     size_t tb = sc.tmp_bytes;
@@ -834,17 +841,19 @@ hipError_t launch_orswot_ser_sort(hipStream_t s, OrswotSerScratch& sc, uint32_t 
       hipLaunchKernelGGL(k_ser_unpack<unsigned long long>, dim3(nblk(n)), dim3(kB), 0, s, sc.member_sorted,
                          sc.rank_bits, sc.id_of_rank, sc.member_sorted, sc.actor_sorted, n);
     }
+#endif
   } else if (n) {
+    // the general form (keys past 64 bits, CE_SER_TWO_SORTS): two stable pair sorts of the
+    // hand-written radix sort (ce_ser_sort.hip), by rank, then by member
     size_t tb = sc.tmp_bytes;
     hipLaunchKernelGGL(k_ser_rank, dim3(nblk(n)), dim3(kB), 0, s, sc.actor_in, sc.rank_of_id, sc.k32a, n);
     hipLaunchKernelGGL(k_ser_iota, dim3(nblk(n)), dim3(kB), 0, s, sc.p32a, n);
-    if ((e = hipcub::DeviceRadixSort::SortPairs(sc.tmp, tb, sc.k32a, sc.k32b, sc.p32a, sc.p32b, (int)n, 0,
-                                                 sc.rank_bits, s)))
+    if ((e = sort_pairs_u32(sc.tmp, tb, sc.k32a, sc.k32b, sc.p32a, sc.p32b, n, sc.rank_bits, s)))
       return e;
     hipLaunchKernelGGL(k_ser_gather_member, dim3(nblk(n)), dim3(kB), 0, s, sc.p32b, sc.member_in, sc.k64a, n);
     tb = sc.tmp_bytes;
-    if ((e = hipcub::DeviceRadixSort::SortPairs(sc.tmp, tb, sc.k64a, sc.member_sorted, sc.p32b, sc.p32a,
-                                                 (int)n, 0, sc.member_bits > 0 && sc.member_bits <= 64 ? sc.member_bits : 64, s)))
+    if ((e = sort_pairs_u64(sc.tmp, tb, sc.k64a, sc.member_sorted, sc.p32b, sc.p32a, n,
+                            sc.member_bits > 0 && sc.member_bits <= 64 ? sc.member_bits : 64, s)))
       return e;
     hipLaunchKernelGGL(k_ser_gather2, dim3(nblk(n)), dim3(kB), 0, s, sc.p32a, sc.actor_in, sc.value_in,
                        sc.actor_sorted, sc.value_sorted, n);
@@ -905,17 +914,16 @@ static size_t cached_tmp_bytes(uint32_t n, size_t (*raw)(uint32_t), std::map<uin
 
 static size_t ser_tmp_bytes_raw(uint32_t n) {
   size_t a = 0, b = 0, c = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                           (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 32);
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, (unsigned long long*)nullptr,
-                                           (unsigned long long*)nullptr, (uint32_t*)nullptr,
-                                           (uint32_t*)nullptr, (int)n, 0, 64);
+  (void)sort_pairs_u32(nullptr, a, nullptr, nullptr, nullptr, nullptr, n, 32, nullptr);
+  (void)sort_pairs_u64(nullptr, b, nullptr, nullptr, nullptr, nullptr, n, 64, nullptr);
   (void)ds_excl_sum_u32(nullptr, c, nullptr, nullptr, n, nullptr);
-  size_t d = 0, e = 0;  // the packed-key sorts: u64 values
+  size_t d = 0, e = 0;
+#if CE_FUSED_DIAG  // CE_SER_CUB: the packed-key sorts through hipCUB, u64 values
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, d, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                            (unsigned long long*)nullptr, (unsigned long long*)nullptr, (int)n, 0, 32);
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, e, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                            (unsigned long long*)nullptr, (unsigned long long*)nullptr, (int)n, 0, 64);
+#endif
   return std::max(std::max(a, b), std::max(c, std::max(d, e))) + 256;
 }
 

@@ -10,7 +10,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#if CE_FUSED_DIAG  // hipCUB only for the diagnostics build's A/B (CE_HIPCUB_SCAN)
 #include <hipcub/hipcub.hpp>
+#endif
 
 #include <algorithm>
 #include <cstdlib>
@@ -308,10 +310,14 @@ namespace {
 struct MaxOp {
   __device__ __host__ unsigned long long operator()(unsigned long long a, unsigned long long b) const { return a > b ? a : b; }
 };
-// CE_HIPCUB_SCAN=1 (diagnostics): hipCUB's scans instead, for same-box A/B
+// CE_HIPCUB_SCAN=1 (diagnostics build only): hipCUB's scans instead, for same-box A/B
 bool use_hipcub() {
+#if CE_FUSED_DIAG
   static const bool v = getenv("CE_HIPCUB_SCAN") != nullptr;
   return v;
+#else
+  return false;
+#endif
 }
 // CE_SCAN_3PASS=1 (tests): the three-launch form (tile sums, one carry block, apply) at any size;
 // by default it only runs past kApplyScanTiles tiles
@@ -322,12 +328,14 @@ bool three_pass() {
 }  // namespace
 
 hipError_t ds_excl_sum_u32(void* tmp, size_t& tb, const uint32_t* in, uint32_t* out, uint32_t n, hipStream_t s) {
+#if CE_FUSED_DIAG
   if (use_hipcub()) {
     size_t need = 0;
     hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, need, in, out, (int)n, s);
     if (!tmp) { tb = std::max<size_t>(need, 4ull * (tiles_for(n) + 1) + 64); return e; }
     return hipcub::DeviceScan::ExclusiveSum(tmp, tb, in, out, (int)n, s);
   }
+#endif
   const uint32_t nt = tiles_for(n);
   const size_t need = 4ull * (nt + 1) + 64;
   if (!tmp) {
@@ -349,6 +357,7 @@ hipError_t ds_excl_sum_u32(void* tmp, size_t& tb, const uint32_t* in, uint32_t* 
 
 hipError_t ds_excl_max_by_key(void* tmp, size_t& tb, const uint32_t* keys, const unsigned long long* vals,
                               unsigned long long* out, uint32_t n, hipStream_t s) {
+#if CE_FUSED_DIAG
   if (use_hipcub()) {
     size_t need = 0;
     hipError_t e = hipcub::DeviceScan::ExclusiveScanByKey(nullptr, need, keys, vals, out, MaxOp(), 0ull, (int)n,
@@ -357,6 +366,7 @@ hipError_t ds_excl_max_by_key(void* tmp, size_t& tb, const uint32_t* keys, const
     return hipcub::DeviceScan::ExclusiveScanByKey(tmp, tb, keys, vals, out, MaxOp(), 0ull, (int)n,
                                                   hipcub::Equality(), s);
   }
+#endif
   const uint32_t nt = tiles_for(n);
   const size_t need = sizeof(Seg) * (nt + 1) + 64;
   if (!tmp) {

@@ -47,6 +47,7 @@ __device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
 
 template <typename K>
 __device__ __forceinline__ K pair_key(const SerSortArgs& a, uint32_t i) {
+  if (a.generic) return reinterpret_cast<const K*>(a.gk_in)[i];
   return ((K)a.member_in[i] << a.rank_bits) | (K)a.rank_of_id[a.actor_in[i]];
 }
 
@@ -126,7 +127,7 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_pass(SerSortArgs a, uint3
     if (i < a.n) {
       if (FIRST) {
         key[k] = pair_key<K>(a, i);
-        val[k] = a.value_in[i];
+        val[k] = a.generic ? (unsigned long long)a.gv_in[i] : a.value_in[i];
       } else {
         key[k] = reinterpret_cast<const K*>(a.keys_in)[i];
         val[k] = a.vals_in[i];
@@ -215,7 +216,10 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_pass(SerSortArgs a, uint3
     const K kk = lkey[lp];
     const uint32_t d = (uint32_t)(kk >> shift) & (kDigits - 1);
     const uint32_t g = gofs[d] + (lp - tstart[d]);
-    if (LAST) {
+    if (LAST && a.generic) {
+      reinterpret_cast<K*>(a.gk_out)[g] = kk;
+      a.gv_out[g] = (uint32_t)lval[lp];
+    } else if (LAST) {
       a.member_out[g] = (unsigned long long)(kk >> a.rank_bits);
       a.actor_out[g] = a.id_of_rank[(uint32_t)kk & ((1u << a.rank_bits) - 1)];
       a.value_out[g] = lval[lp];
@@ -258,7 +262,61 @@ hipError_t sort_typed(hipStream_t s, SerSortArgs a, void* const kbuf[2], unsigne
   return hipGetLastError();
 }
 
+// the generic sorts' state is scratch, not kept across sorts: this sort's histogram and tickets
+// start at zero (the serializer's persistent state has k_sort_hist zero the next sort's instead)
+__global__ void __launch_bounds__(kSortThreads) k_sort_zero(uint32_t* hist) {
+  for (uint32_t i = blockIdx.x * kSortThreads + threadIdx.x; i < kSortStateHead; i += gridDim.x * kSortThreads) hist[i] = 0;
+}
+
+template <typename K>
+hipError_t sort_pairs_t(void* tmp, size_t& tb, const K* kin, K* kout, const uint32_t* vin, uint32_t* vout,
+                        uint32_t n, int bits, hipStream_t s) {
+  // scratch: sort state | keys x 2 | u64 values x 2 (the passes' ping-pong buffers)
+  const uint32_t tiles = (n + kSortTile - 1) / kSortTile;
+  const size_t sw = ((size_t)kSortStateHead + (size_t)kSortMaxPlaces * tiles * kDigits) * 4;
+  const size_t a0 = (sw + 255) & ~(size_t)255, kb = ((size_t)n * sizeof(K) + 255) & ~(size_t)255,
+               vb = ((size_t)n * 8 + 255) & ~(size_t)255;
+  const size_t need = a0 + 2 * kb + 2 * vb + 256;
+  if (!tmp) {
+    tb = need;
+    return hipSuccess;
+  }
+  if (tb < need) return hipErrorInvalidValue;
+  if (n == 0) return hipSuccess;
+  uint8_t* base = static_cast<uint8_t*>(tmp);
+  SerSortArgs a{};
+  a.generic = 1;
+  a.gk_in = kin;
+  a.gk_out = kout;
+  a.gv_in = vin;
+  a.gv_out = vout;
+  a.n = n;
+  a.key_bits = bits > 0 ? bits : (int)(8 * sizeof(K));
+  a.par = 0;
+  a.hist = reinterpret_cast<uint32_t*>(base);
+  a.ticket = a.hist + 2 * 8 * kSortMaxPlaces * 256;
+  a.look = a.hist + kSortStateHead;
+  a.tiles = tiles;
+  a.places = (uint32_t)((a.key_bits + kDigitBits - 1) / kDigitBits);
+  if (a.places == 0) a.places = 1;
+  void* kbuf[2] = {base + a0, base + a0 + kb};
+  unsigned long long* vbuf[2] = {reinterpret_cast<unsigned long long*>(base + a0 + 2 * kb),
+                                 reinterpret_cast<unsigned long long*>(base + a0 + 2 * kb + vb)};
+  hipLaunchKernelGGL(k_sort_zero, dim3(16), dim3(kSortThreads), 0, s, a.hist);
+  return sort_typed<K>(s, a, kbuf, vbuf);
+}
+
 }  // namespace
+
+hipError_t sort_pairs_u32(void* tmp, size_t& tb, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
+                          uint32_t* vout, uint32_t n, int bits, hipStream_t s) {
+  return sort_pairs_t<uint32_t>(tmp, tb, kin, kout, vin, vout, n, bits > 32 ? 32 : bits, s);
+}
+
+hipError_t sort_pairs_u64(void* tmp, size_t& tb, const unsigned long long* kin, unsigned long long* kout,
+                          const uint32_t* vin, uint32_t* vout, uint32_t n, int bits, hipStream_t s) {
+  return sort_pairs_t<unsigned long long>(tmp, tb, kin, kout, vin, vout, n, bits > 64 ? 64 : bits, s);
+}
 
 uint32_t ser_sort_tiles(uint32_t n) { return (n + kSortTile - 1) / kSortTile; }
 

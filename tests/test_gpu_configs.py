@@ -196,3 +196,23 @@ def test_multi_key_opt_in(ctx, oracle, tamper):
                                    [actors[i] for i in fa], fv)[0] == 0
         assert core.state_bytes() == ref.serialize()
     core.close()
+
+
+def test_c3_read_context_removals(ctx):
+    """C3 with SURVEY.md §8d's removal shape (bench config c3r): every Rm carries the removed
+    member's read context -- the state files' adds of it and the writer's own (crdts'
+    rm(member, read_ctx)), so op files pass the 2 KiB fused-decode region and removals name
+    other writers' dots.  At a small size, through bench_configs' own runner: the closed-form
+    clock, the writer-sharded fold + merge_state == the whole fold, and the C restatement's state
+    bytes over the same files == the GPU's (crdt-enc/src/lib.rs:457-465, 533-535)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench_configs as B
+    ns = B.make_parser().parse_args(["--config", "c3r", "--steps", "2", "--warmup", "1", "--versions", "2",
+                                     "--state-versions", "1"])
+    line = B.RUNNERS["c3r"](ns, ctx, torch.device("cuda", 0))
+    assert line["config"]["rm_ctx"] == "read"
+    assert line["config"]["removal_clock_entries"] > 2 * 4096 * 2 * B.N_RM   # multi-entry clocks
+    assert all(line["checks"].values()), line["checks"]
+    assert line["cpu_baseline"]["same_result_as_gpu"], line["cpu_baseline"]

@@ -990,8 +990,9 @@ def test_orswot_partitioned_fold_equals_global(ctx, adversarial):
 def test_orswot_serializer_one_sort_equals_two(ctx, n_members):
     """The device serializer orders the live (member, actor) pairs by (member, actor UUID rank):
     by the hand-written radix sort of the packed key when member bits + actor-rank bits fit 64
-    (ce_ser_sort.hip), else by rank then stably by member.  Each form (default, CE_SER_CUB=1:
-    hipCUB's sort of the packed key, CE_SER_TWO_SORTS=1) == the oracle's bytes, for small,
+    (ce_ser_sort.hip), else by rank then stably by member (two pair sorts of the same kernels).
+    Each form (default, CE_SER_TWO_SORTS=1) and the host serializer (state_bytes, its own
+    pair sort) == the oracle's bytes, for small,
     20-bit, 40-bit (64-bit keys) and full 64-bit members (the two sorts), and for members every
     one of 300 actors adds (slices of 300 pairs)."""
     rng = random.Random(929 + (n_members % 1000 if isinstance(n_members, int) else 7))
@@ -1009,7 +1010,7 @@ def test_orswot_serializer_one_sort_equals_two(ctx, n_members):
     import torch
     want = oc.serialize()
     got = []
-    for mode in (None, "CE_SER_CUB", "CE_SER_TWO_SORTS"):
+    for mode in (None, "CE_SER_TWO_SORTS"):
         if mode:
             os.environ[mode] = "1"
         try:
@@ -1020,11 +1021,12 @@ def test_orswot_serializer_one_sort_equals_two(ctx, n_members):
             assert rc == 0
             torch.cuda.synchronize()
             got.append(bytes(buf[:n].cpu().numpy().tobytes()))
+            got.append(core.state_bytes())
             core.close()
         finally:
             if mode:
                 os.environ.pop(mode, None)
-    assert got[0] == got[1] == got[2] == want
+    assert got[0] == got[1] == got[2] == got[3] == want
 
 
 @pytest.mark.parametrize("member_bits", [18, 36])
@@ -1032,13 +1034,14 @@ def test_orswot_serializer_sort_many_tiles(ctx, member_bits):
     """The hand-written sort over many 4096-pair tiles (the look-back between tiles, every digit
     place, 32- and 64-bit keys): ~300 K live pairs from 256 writers, serialized on the device ==
     the same state serialized with the tiles ordered by an atomic ticket (CE_SORT_TICKET=1; by
-    blockIdx otherwise, when every tile is resident), with hipCUB's sort (CE_SER_CUB=1; separate
-    processes: the choices are read once) and with the two-sort form."""
+    blockIdx otherwise, when every tile is resident; separate processes: the choices are read
+    once), with the two-sort form and by the host serializer, and == the C restatement's bytes
+    over the same files (oracle/ce_oracle.c)."""
     import subprocess
     import sys
     code = (
         "import os, sys, hashlib, random\n"
-        "sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
+        "sys.path.insert(0, %r); sys.path.insert(0, %r); sys.path.insert(0, os.path.dirname(sys.path[0]))\n"
         "import crdtenc, torch\n"
         "import dotset_gen as G\n"
         "from oracle import crdts as C\n"
@@ -1058,16 +1061,23 @@ def test_orswot_serializer_sort_many_tiles(ctx, member_bits):
         "assert rc == 0, rc\n"
         "torch.cuda.synchronize()\n"
         "b = bytes(buf[:n].cpu().numpy().tobytes())\n"
+        "assert core.state_bytes() == b\n"
+        "if os.environ.get('CE_T_ORACLE'):\n"
+        "    import numpy as np, oracle\n"
+        "    offs = np.zeros(len(sealed) + 1, np.uint64); offs[1:] = np.cumsum([len(x) for x in sealed])\n"
+        "    err, ser, _, _ = oracle.compact_orswot_best(key, bytes.fromhex(%r), [], b''.join(sealed), offs,\n"
+        "        np.frombuffer(b''.join(acts[i] for i in fa), np.uint8).reshape(-1, 16), np.array(fv, np.uint64), 8, seal=False)\n"
+        "    assert err == 0 and ser == b, 'C oracle differs'\n"
         "print(hashlib.sha256(b).hexdigest(), n)\n"
         % (os.path.join(REPO, "crdt-enc_amd"), os.path.join(REPO, "tests"), member_bits, APP.hex(),
-           CORE.hex(), APP.hex(), APP.hex()))
+           CORE.hex(), APP.hex(), APP.hex(), APP.hex()))
     outs = []
-    for env in ({}, {"CE_SORT_TICKET": "1"}, {"CE_SER_CUB": "1"}, {"CE_SER_TWO_SORTS": "1"}):
+    for env in ({"CE_T_ORACLE": "1"}, {"CE_SORT_TICKET": "1"}, {"CE_SER_TWO_SORTS": "1"}):
         p = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), capture_output=True,
                            timeout=300, cwd=REPO)
         assert p.returncode == 0, p.stderr.decode()[-2000:]
         outs.append(p.stdout.decode().split()[-2:])
-    assert outs[0] == outs[1] == outs[2] == outs[3], outs
+    assert outs[0] == outs[1] == outs[2], outs
     assert int(outs[0][1]) > 300000 * 20
 
 
@@ -1166,8 +1176,8 @@ def test_table_overflow_is_sticky_until_reset(ctx):
 
 def test_scan_forms_equal(ctx):
     """the dot-set scans (ce_scan.hip) in their default two-launch form, the
-    three-launch form (CE_SCAN_3PASS=1, otherwise only past 4096 tiles) and hipCUB's
-    (CE_HIPCUB_SCAN=1) give identical state bytes == the oracle, on an adversarial batch (the
+    three-launch form (CE_SCAN_3PASS=1, otherwise only past 4096 tiles) give identical state
+    bytes == the oracle, on an adversarial batch (the
     sorted adds' segmented max scan, ragged actor runs across 2048-item tiles; the per-file
     count scans over 4096 files).  The forms are chosen once per process, so each runs in its own
     child process (tests/scan_modes_worker.py)."""
@@ -1185,7 +1195,7 @@ def test_scan_forms_equal(ctx):
     orc = oc.read_remote_ops(key, [APP], sealed, [acts[i] for i in fa], fv)[0]
     want = "%d %s" % (orc, hashlib.sha256(oc.serialize()).hexdigest())
     outs = {}
-    for mode, env in {"two": {}, "three": {"CE_SCAN_3PASS": "1"}, "hipcub": {"CE_HIPCUB_SCAN": "1"}}.items():
+    for mode, env in {"two": {}, "three": {"CE_SCAN_3PASS": "1"}}.items():
         e = dict(os.environ)
         e.pop("CE_SCAN_3PASS", None)
         e.pop("CE_HIPCUB_SCAN", None)
@@ -1194,7 +1204,7 @@ def test_scan_forms_equal(ctx):
                            capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
         outs[mode] = r.stdout.strip().splitlines()[-1]
-    assert outs["two"] == outs["three"] == outs["hipcub"] == want, outs
+    assert outs["two"] == outs["three"] == want, outs
 
 
 def _canonical_orswot(rng, actors, n_versions, ops_per_file, members, widths=(1, 2, 3, 5, 9), p_rm=0.2):
