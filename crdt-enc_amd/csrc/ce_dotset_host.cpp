@@ -1140,6 +1140,7 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
     if ((rc = insert_actor(c, u, &wslot[a]))) return rc;
   }
   if (c->table_gen != gen0) refresh_slots(c, actors, m, &wslot);  // a growth moved them
+  const uint64_t gen1 = c->table_gen;
   if ((rc = table_upload(c)) || (rc = ensure_supported(c))) return rc;
   if ((e = ctx->out.reserve(blob_len + 16ull * n + 128)) || (e = ctx->status.reserve(n * 4ull + 64)) ||
       (e = d->cnt.reserve(2ull * kCntN * n * 4 + 64)))
@@ -1419,7 +1420,10 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
     rc = mvreg_commit(c, (uint32_t)base.v[kCntRm], (uint32_t)tot.v[kCntRm], true);
   }
   if (rc) return rc;
-  // 7) next_op_versions (lib.rs:537-538) and the gap error (lib.rs:527-531)
+  // 7) next_op_versions (lib.rs:537-538) and the gap error (lib.rs:527-531).  The decode's misses
+  //    (actors the ops name that the table did not hold: removal clocks naming other writers)
+  //    may have grown the table since the writers got their slots: refreshed first
+  if (c->table_gen != gen1) refresh_slots(c, actors, m, &wslot);
   for (uint32_t w = 0; w < m; w++) c->nov[wslot[w]] = std::max(c->nov[wslot[w]], expect[w]);
   if (first_gap < n) {
     if (status_out) status_out[first_gap] = CE_ERR_OP_VERSION;

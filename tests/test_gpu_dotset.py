@@ -1446,3 +1446,26 @@ def test_columns_merge_deferred_and_covered_removals(ctx, shape):
     assert shards[0].path_count("columns_merge_deferred") == 1
     for core in shards + [seq]:
         core.close()
+
+
+def test_orswot_writer_versions_after_table_growth(ctx):
+    """Removal clocks naming more actors than the actor table holds (2,100 strangers, the writer
+    shard of C3 with read-context removals): the decode's misses grow the table inside the
+    ingest, and every writer's next_op_versions must still land on its own slot afterwards
+    (lib.rs:537-538) -- the state, next versions included, == the oracle's."""
+    rng = random.Random(8080)
+    key = rng.randbytes(32)
+    writers = G.actors_for(rng, 3)
+    strangers = G.actors_for(rng, 2100)
+    files = {}
+    for i, w in enumerate(writers):
+        files[w] = [[("Add", (w, v + 1), [100 * i + v]),
+                     ("Rm", C.VClock({s: 5 for s in strangers[700 * i:700 * (i + 1)]}), [7])] for v in range(3)]
+    acts, clears, fa, fv = G.batch(files, "orswot", APP)
+    sealed = seal_files(ctx, key, clears)
+    oc = C.Core("orswot")
+    assert oc.read_remote_ops(key, [APP], sealed, [acts[i] for i in fa], fv)[0] == 0
+    core = new_core(ctx, "orswot", key)
+    assert core.ingest_ops(sealed, acts, fa, fv)[0] == 0
+    assert core.state_bytes() == oc.serialize()
+    core.close()

@@ -83,18 +83,35 @@ def main():
     seq = B.new_core(ctx, key)
     assert seq.merge_state(gparts[0]) == 0 and seq.merge_state(gparts[1]) == 0
     out["gpu_seq_merge_eq_c_merge"] = seq.state_bytes() == cmerged
-    if cmerged != gm:  # where: the members whose entries differ
+    if cmerged != cw:  # where: the members whose entries differ (merge of the shards vs the whole)
+        gm = cmerged
+        cmerged = cw
         import msgpack
         a = msgpack.unpackb(cmerged, raw=True, strict_map_key=False)[b"state"]
         b = msgpack.unpackb(gm, raw=True, strict_map_key=False)[b"state"]
         ea, eb = a[b"entries"], b[b"entries"]
         diff = [m for m in set(ea) | set(eb) if ea.get(m) != eb.get(m)]
-        out["entries_c_gpu"] = [len(ea), len(eb)]
+        out["entries_whole_merged"] = [len(ea), len(eb)]
         out["n_diff_members"] = len(diff)
         out["clock_eq"] = a[b"clock"] == b[b"clock"]
-        out["deferred_c_gpu"] = [len(a[b"deferred"]), len(b[b"deferred"])]
-        for m in diff[:3]:
-            print("member", m, "c:", ea.get(m), "gpu:", eb.get(m), flush=True)
+        out["deferred_whole_merged"] = [len(a[b"deferred"]), len(b[b"deferred"])]
+        ta = msgpack.unpackb(cmerged, raw=True, strict_map_key=False)
+        tb = msgpack.unpackb(gm, raw=True, strict_map_key=False)
+        out["nov_eq"] = ta[b"next_op_versions"] == tb[b"next_op_versions"]
+        na_, nb_ = ta[b"next_op_versions"][b"dots"], tb[b"next_op_versions"][b"dots"]
+        dn = [k for k in set(na_) | set(nb_) if na_.get(k) != nb_.get(k)]
+        out["nov_diff"] = [(na_.get(k), nb_.get(k)) for k in dn[:5]]
+        out["nov_len"] = [len(na_), len(nb_)]
+        i = next((i for i in range(min(len(cmerged), len(gm))) if cmerged[i] != gm[i]), None)
+        out["first_diff_byte"] = i
+        if i is not None:
+            out["ctx_whole"] = cmerged[max(0, i - 24):i + 24].hex()
+            out["ctx_merged"] = gm[max(0, i - 24):i + 24].hex()
+        act_ix = {bytes(x): i for i, x in enumerate(actors)}
+        for m in diff[:4]:
+            fmt = lambda e: None if e is None else {act_ix.get(k, -1): v for k, v in e[b"dots"].items()}
+            print("member", m, "whole:", fmt(ea.get(m)), "merged:", fmt(eb.get(m)), flush=True)
+        print(out, flush=True)
     os.environ["CE_NO_KMERGE"] = "1"
     print(out, flush=True)
 
