@@ -147,9 +147,14 @@ int device_open(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint
   if ((e = reset_counters(ctx)) != hipSuccess) return ctx->hip_fail(e, "memset counters");
   SegScratch sc = segscratch(ctx, ec);
   FileParams* P = ctx->params.as<FileParams>();
+  // the DS form's 8-lane kernel reads the setup's PolyAux rows (k_open_ds8)
+  static const bool ds8_on = getenv("CE_DS8") && atoi(getenv("CE_DS8")) == 1;  // (ce_fused.hip)
+  const bool want_aux = small_lanes && ds && ds->ds.on && ds->ds.big && ds8_on;
+  if (want_aux && (e = ctx->poly_aux.reserve((size_t)n * sizeof(PolyAux))) != hipSuccess)
+    return ctx->hip_fail(e, "reserve poly aux");
   int t = ctx->tbegin("open_setup");
   if ((e = launch_open_setup(ctx->stream, d_blob, d_offs, n, outer, dev_key(key), key_status(key),
-                             P, d_status, sc)) != hipSuccess)
+                             P, d_status, sc, want_aux ? ctx->poly_aux.as<PolyAux>() : nullptr)) != hipSuccess)
     return ctx->hip_fail(e, "open setup");
   ctx->tend(t);
   if (small_lanes) {
@@ -162,6 +167,7 @@ int device_open(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint
     da.counters = ctx->counters.as<uint32_t>();
     if (ds) {
       da.ds = ds->ds;
+      da.aux = want_aux ? ctx->poly_aux.as<PolyAux>() : nullptr;
       da.supported = ds->supported;
       da.n_supported = ds->n_supported;
       da.table = ds->table;

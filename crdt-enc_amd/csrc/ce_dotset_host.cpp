@@ -81,7 +81,7 @@ struct DsState {
   DevBuf tile_col[9];        // the tiled emit's file-minor scratch rows (k_ds_emit<true>)
   // Orswot op files decoded in the open (k_open_fold_v2's DS form): raw counts, done flags and
   // the file-major rows (add actor / counter / member, removal actor / counter / member)
-  DevBuf fz_cnt, fz_done, fz_col[6], fz_why;
+  DevBuf fz_cnt, fz_done, fz_col[6], fz_why, fz_big;
   DevBuf ser_sort;               // the serializer's radix-sort state (ce_ser_sort.hip), zeroed once
   size_t ser_sort_words = 0;
   uint32_t ser_sort_gen = 0;     // sorts so far (the state's histogram parity)
@@ -1155,7 +1155,8 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
   if (fused) {
     constexpr uint32_t kRows = 64;  // ops per file the rows hold (more: the lane-per-file decode)
     static const uint32_t kEl[6] = {4, 8, 8, 4, 8, 8};
-    if ((e = d->fz_cnt.reserve(4ull * kCntN * n + 64)) || (e = d->fz_done.reserve(n + 64)))
+    if ((e = d->fz_cnt.reserve(4ull * kCntN * n + 64)) || (e = d->fz_done.reserve(n + 64)) ||
+        (e = d->fz_big.reserve(n + 64)))
       return ctx->hip_fail(e, "fused decode");
     for (int j = 0; j < 6; j++)
       if ((e = d->fz_col[j].reserve((uint64_t)kRows * n * kEl[j] + 64))) return ctx->hip_fail(e, "fused decode");
@@ -1163,6 +1164,7 @@ int ds_ingest_ops(ce_core* c, const uint8_t* d_blob, const uint64_t* d_offs, uin
     fz.ds.rows = kRows;
     fz.ds.rawcnt = d->fz_cnt.as<uint32_t>();
     fz.ds.done = d->fz_done.as<uint8_t>();
+    fz.ds.big = d->fz_big.as<uint8_t>();
     fz.ds.add_actor = d->fz_col[0].as<uint32_t>();
     fz.ds.add_ctr = d->fz_col[1].as<unsigned long long>();
     fz.ds.add_mem = d->fz_col[2].as<unsigned long long>();

@@ -1188,6 +1188,8 @@ void k_open_fold_v2(DecodeArgs a) {
   const uint32_t ngroups = (a.n + F - 1) / F;
   const uint32_t stride = gridDim.x;
   uint32_t g = bcast(blockIdx.x);
+  // k_open_ds8's pass over the files it left: none (counters[10], counted by it) -> done
+  if (DS && a.only && *reinterpret_cast<volatile const uint32_t*>(a.counters + 10) == 0) return;
   FilePre2 nx = load_pre2(a, g * F + grp);
   const SupVers sup(a);
   DecState S{38, 0, 0, 0, 0, 0xffffffffu};
@@ -1252,6 +1254,10 @@ void k_open_fold_v2(DecodeArgs a) {
     const FilePre2 cur = nx;
     if (PF || DP) nx = nn;
     if (PF1 && !DP) nx = load_pre2(a, (g + stride) * F + grp);  // issued before this iteration's loads
+    if (DS && a.only && !__any(cur.ok)) {  // a masked pass (k_open_ds8's big files): nothing here
+      nx = load_pre2(a, (g + stride) * F + grp);
+      continue;
+    }
     const bool act = cur.ok && cur.len <= kSmallMax;
     const uint32_t len = act ? cur.len : 0u;
     const bool dsl = DS && act && len <= kDsFuseRegion;  // DS: plaintext into LDS
@@ -1460,7 +1466,7 @@ void k_open_fold_v2(DecodeArgs a) {
           for (uint32_t q = sub; q * 16u < len; q += LPF)
             *reinterpret_cast<uint4*>(gout + q * 16u) = *reinterpret_cast<const uint4*>(fl + q * 16u);
         }
-        if (sub == 0 && f < a.n) a.ds.done[f] = done ? 1 : 0;
+        if (sub == 0 && f < a.n && (!a.only || cur.ok)) a.ds.done[f] = done ? 1 : 0;
         __syncthreads();  // the next iteration's plaintext overwrites the regions
       }
       (void)ok;
@@ -1720,6 +1726,210 @@ void k_open_fold_v3(DecodeArgs a) {
   fails.flush(a);
 }
 
+// ----------------------------------------------------------------------------------------
+// k_open_ds8: the DS form (Orswot op files decoded in LDS, ds_fused_decode) with 8 lanes per
+// file and 8 files per wave.  C3's op files (~2 KiB, 31 ChaCha20 blocks) filled two of a 16-lane
+// group's four block slots per lane, so every per-file cost of an iteration (parameters, the
+// Poly1305 combination and tag, the decode's setup) was paid over half a lane's work; here a lane
+// owns four blocks b = nblk - 1 - sub - 8 k of a file of at most kDsFuseRegion bytes.  Poly1305
+// as k_open_fold_v3 (four-product column sums, the setup's PolyAux, weights r^(4q) =
+// r^(4 (q & 3)) r^(16 (q >> 2)), q < 8, a DPP sum over the group).  A single-page file past
+// kDsFuseRegion is not opened here: big[f] = 1, and the 16-lane DS kernel opens it in a second
+// pass over that mask.
+// ----------------------------------------------------------------------------------------
+// PF: the next file's ciphertext loaded before this one's decode (into the registers the open no
+// longer needs), so it lands while the decode runs instead of at the next iteration's first XOR
+template <bool PF>
+__global__ __launch_bounds__(64, 2)
+void k_open_ds8(DecodeArgs a) {
+  constexpr int LPF = 8, F = 8, BPL = 4;
+  // 64 B of over-read room past a region (the decode's windows read at most 52 B past a candidate
+  // below len): 8 x (2112 + 448) B = 20 KiB, two waves per SIMD as the VGPRs allow
+  constexpr uint32_t kStride = kDsFuseRegion + 64;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[F * kStride + F * kDsAuxHalves * 2];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t grp = lane / LPF, sub = lane % LPF;
+  uint8_t* fl = lds + grp * kStride;
+  uint16_t* aux = reinterpret_cast<uint16_t*>(lds + F * kStride) + grp * kDsAuxHalves;
+  const uint32_t ngroups = (a.n + F - 1) / F;
+  const uint32_t g_end = (uint32_t)(((uint64_t)(blockIdx.x + 1) * ngroups) / gridDim.x);
+  uint32_t g = bcast((uint32_t)(((uint64_t)blockIdx.x * ngroups) / gridDim.x));
+  FilePre2 nx = load_pre2(a, g * F + grp);
+  const SupVers sup(a);
+  AuthFails fails;
+  const uint32_t qpos = (sub + 7u) & 7u;
+  const uint32_t qx = qpos & 3u;
+  const bool x_one = qx == 0, y_one = (qpos >> 2) == 0, x_aux = qx == 3;
+  const uint32_t x_off = x_aux ? (uint32_t)offsetof(PolyAux, r12) : 80u + 20u * (qx + 1u);
+  uint4 ct[BPL][4];
+  // a file's ciphertext -> ct: block k of the lane is b = nblk - 1 - sub - 8 k, whole but for the
+  // file's last (lane 0, k = 0); a lane without the block reads the params rows
+  auto load_ct = [&](const FilePre2& p) {
+    const bool ac = p.ok && p.len <= kDsFuseRegion;
+    const uint32_t ln = ac ? p.len : 0u;
+    const uint32_t np = (ln + 15) >> 4;
+    const int32_t nb = (int32_t)((ln + 63) >> 6);
+    const uint8_t* sr = ac ? a.blob + (((uint64_t)p.in_hi << 32) | p.in_off) : reinterpret_cast<const uint8_t*>(a.params);
+#pragma unroll
+    for (int k = BPL - 1; k >= 0; k--) {
+      const int32_t b = nb - 1 - (int32_t)sub - LPF * k;
+      if (k > 0) {
+        const uint8_t* bp = b >= 0 ? sr + 64u * (uint32_t)b : reinterpret_cast<const uint8_t*>(a.params);
+#pragma unroll
+        for (int j = 0; j < 4; j++) ct[k][j] = *reinterpret_cast<const uint4*>(bp + 16 * j);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint32_t q = (uint32_t)(4 * b + j);
+          const uint32_t off = b >= 0 ? 16u * (q < np ? q : np - 1u) : 0u;
+          ct[0][j] = *reinterpret_cast<const uint4*>(sr + off);
+        }
+      }
+    }
+  };
+  if (PF) load_ct(nx);
+  for (; g < g_end; g++) {
+    const uint32_t f = g * F + grp;
+    const FilePre2 cur = nx;
+    nx = load_pre2(a, (g + 1) * F + grp);
+    const bool act0 = cur.ok && cur.len <= kSmallMax;
+    const bool big = act0 && cur.len > kDsFuseRegion;
+    const bool act = act0 && !big;
+    const uint32_t len = act ? cur.len : 0u;
+    const uint32_t npc = (len + 15) >> 4;
+    const int32_t nblk = (int32_t)((len + 63) >> 6);  // <= 32
+    const FileParams* Pp = a.params + (act ? f : 0);
+    const PolyAux* Xp = a.aux + (act ? f : 0);
+    const uint8_t* src = act ? a.blob + (((uint64_t)cur.in_hi << 32) | cur.in_off)
+                             : reinterpret_cast<const uint8_t*>(a.params);
+    uint8_t* gout = const_cast<uint8_t*>(a.pt) + Pp->out_off;
+    if (!PF) load_ct(cur);
+    L5 R1, RC, R2, R3;
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      R1.v[i] = cur.R1[i];
+      RC.v[i] = Pp->rpow[5][i];  // the chain step r^(4 LPF) = r^32
+      R2.v[i] = Pp->rpow[1][i];
+      R3.v[i] = Xp->r3[i];
+    }
+    const ChachaPre cpre = chacha_pre(cur.key, 0u, cur.n2a, cur.n2b);
+    L5 acc{{0, 0, 0, 0, 0}}, glast{{0, 0, 0, 0, 0}};
+    L5 X, Y, E6, LR;
+    uint32_t ts[4];
+    uint4 pc[4];
+    const uint32_t dl = sub == 0 ? (uint32_t)(4 * nblk) - npc : 0u;
+    const uint32_t rb = sub == 0 && npc ? len - 16u * (npc - 1u) : 16u;
+#pragma unroll
+    for (int k = BPL - 1; k >= 0; k--) {
+      const int32_t b = nblk - 1 - (int32_t)sub - LPF * k;
+      const bool has = b >= 0;
+      // block slots no file of the wave has are skipped (slot 0 always has the file's last block)
+      if (k > 0 && !__any(has)) continue;
+      if (k == 0) {
+        const uint8_t* pb = has ? src + 16 * (int64_t)(4 * b - (int32_t)dl) : src;
+#pragma unroll
+        for (int j = 0; j < 4; j++) pc[j] = *reinterpret_cast<const uint4*>(pb + 16 * j);
+        const uint32_t* xs = reinterpret_cast<const uint32_t*>(
+            (x_aux ? reinterpret_cast<const uint8_t*>(Xp) : reinterpret_cast<const uint8_t*>(Pp)) + x_off);
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+          X.v[i] = xs[i];
+          Y.v[i] = Pp->rpow[4][i];  // r^16
+          E6.v[i] = Xp->e6[i];
+          LR.v[i] = Xp->lr[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) ts[i] = Xp->ts[i];
+      }
+      uint32_t kb[16];
+      chacha_block_pre<true, 9>(cpre, cur.key, 1u + (uint32_t)b, 0u, cur.n2a, cur.n2b, kb);
+      L5 m[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t q = (uint32_t)(4 * b + j);
+        const uint4 c = ct[k][j];
+        const uint4 pv = make_uint4(c.x ^ kb[4 * j], c.y ^ kb[4 * j + 1], c.z ^ kb[4 * j + 2], c.w ^ kb[4 * j + 3]);
+        if (has) *reinterpret_cast<uint4*>(fl + q * 16u) = pv;  // q < 4 nblk <= 128
+        if (k > 0) {
+          m[j] = block_limbs(c.x, c.y, c.z, c.w);
+        } else {
+          uint32_t w[4] = {pc[j].x, pc[j].y, pc[j].z, pc[j].w};
+          const bool pres = (uint32_t)j >= dl;
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            if (j == 3) {
+              const int32_t cb = (int32_t)rb - 4 * i;
+              const uint32_t keep = cb >= 4 ? ~0u : cb <= 0 ? 0u : ((1u << (8 * cb)) - 1u);
+              w[i] &= keep;
+            } else {
+              w[i] = pres ? w[i] : 0u;
+            }
+          }
+          m[j] = block_limbs(w[0], w[1], w[2], w[3]);
+          if (j < 3) m[j].v[4] = pres ? m[j].v[4] : 0u;
+        }
+      }
+      uint64_t d[5] = {m[3].v[0], m[3].v[1], m[3].v[2], m[3].v[3], m[3].v[4]};
+      L5 ain = acc;
+      if (k == 0) {
+#pragma unroll
+        for (int i = 0; i < 5; i++) ain.v[i] = sub == 0 ? 0u : acc.v[i];
+      }
+      mac5(d, ain, mul_r(RC));  // (acc is zero before the lane's first block)
+      mac5(d, m[0], mul_r(R3));
+      mac5(d, m[1], mul_r(R2));
+      mac5(d, m[2], mul_r(R1));
+      const L5 an = reduce5(d);
+      const bool to_acc = has && !(k == 0 && sub == 0);
+#pragma unroll
+      for (int i = 0; i < 5; i++) acc.v[i] = to_acc ? an.v[i] : acc.v[i];
+      if (k == 0) {
+#pragma unroll
+        for (int i = 0; i < 5; i++) glast.v[i] = has && sub == 0 ? an.v[i] : 0u;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      X.v[i] = x_one ? (i == 0 ? 1u : 0u) : X.v[i];
+      Y.v[i] = y_one ? (i == 0 ? 1u : 0u) : Y.v[i];
+    }
+    L5 v = mulmod(mulmod(acc, X), Y);
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+#pragma unroll
+      for (int i = 0; i < 5; i++) v.v[i] += row_down(v.v[i], 1 << k);
+    }
+    uint64_t d[5] = {LR.v[0], LR.v[1], LR.v[2], LR.v[3], LR.v[4]};
+    mac5(d, v, mul_r(E6));
+    mac5(d, glast, mul_r(R2));
+    const L5 tot = reduce5(d);
+    bool tag_ok = false;
+    if (act && sub == 0) {
+      tag_ok = poly_check(tot, ts);
+      if (!tag_ok) a.status[f] = CE_ERR_AUTH;
+    }
+    fails.add(act && sub == 0 && !tag_ok, f);
+    const bool ok = grp_bits<LPF>(tag_ok, grp) != 0;
+    if (PF) load_ct(nx);
+    bool done = false;
+    if (__any(act && ok)) done = ds_fused_decode<LPF>(a, sup, fl, aux, len, act && ok, f, grp, sub);
+    if (act && ok && !done) {  // the lane-per-file decode reads it from HBM
+      for (uint32_t q = sub; q * 16u < len; q += LPF)
+        *reinterpret_cast<uint4*>(gout + q * 16u) = *reinterpret_cast<const uint4*>(fl + q * 16u);
+    }
+    if (sub == 0 && f < a.n) {
+      a.ds.done[f] = done ? 1 : 0;
+      a.ds.big[f] = big ? 1 : 0;
+    }
+    // big files counted (counters[10], zeroed with the block before the open): the 16-lane pass
+    // over them returns at once when there are none
+    const unsigned long long bb = __ballot(big && sub == 0);
+    if (bb && lane == (uint32_t)__builtin_ctzll(bb)) atomicAdd(&a.counters[10], (uint32_t)__builtin_popcountll(bb));
+    __syncthreads();  // the next iteration's plaintext overwrites the regions
+  }
+  fails.flush(a);
+}
+
 template <int LPF, int W, bool JIT, int OPT = 3, bool DEC = true, bool DS = false>
 static void launch_v2(hipStream_t s, const DecodeArgs& a, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr) {
   static const uint32_t res = resident_blocks(k_open_fold_v2<LPF, W, JIT, OPT, DEC, DS>, 64);
@@ -1736,10 +1946,32 @@ static void launch_v2(hipStream_t s, const DecodeArgs& a, hipEvent_t t0 = nullpt
 // a.only / a.apply unused.  Larger files: k_segments with skip_small (their setup's list).
 hipError_t launch_open_small_v2(hipStream_t s, const DecodeArgs& a) {
   if (a.n == 0) return hipSuccess;
-  // the DS form at a 3-wave VGPR budget (168, a few spills): same-box A/B against 2 waves (191
-  // VGPRs, none): 155 vs 162 us at C3 (r05)
-  if (a.ds.on) launch_v2<16, 3, false, 1, false, true>(s, a);
-  else launch_v2<16, 3, false, 1, false>(s, a);
+  // CE_DS8=1 (opt-in A/B): 8 lanes per file for files of at most kDsFuseRegion bytes
+  // (k_open_ds8, with the setup's PolyAux), then the 16-lane DS form over the files it left
+  // (a.only = big; it returns at once when there are none).  Measured at C3 (r06, same box,
+  // rocprofv3): 65.0K VALU lane-instr per file against 79.7K, but 153-155 us against 159-162 us
+  // for the 16-lane form, plus 6 us for the second pass: at 2 waves per SIMD (206 VGPRs, 20 KiB of
+  // LDS per wave) the decode's LDS and table latencies stay exposed, so it is not the default.
+  // The 16-lane DS form at a 3-wave VGPR budget (168, a few spills): same-box A/B against 2 waves
+  // (191 VGPRs, none): 155 vs 162 us at C3 (r05)
+  static const bool ds8_on = getenv("CE_DS8") && atoi(getenv("CE_DS8")) == 1;
+  if (a.ds.on && a.aux && a.ds.big && ds8_on) {
+    static const bool pf = !(getenv("CE_DS8_PF") && atoi(getenv("CE_DS8_PF")) == 0);
+    if (pf) {
+      static const uint32_t res = resident_blocks(k_open_ds8<true>, 64);
+      hipLaunchKernelGGL(k_open_ds8<true>, dim3(std::min<uint32_t>((a.n + 7) / 8, res)), dim3(64), 0, s, a);
+    } else {
+      static const uint32_t res = resident_blocks(k_open_ds8<false>, 64);
+      hipLaunchKernelGGL(k_open_ds8<false>, dim3(std::min<uint32_t>((a.n + 7) / 8, res)), dim3(64), 0, s, a);
+    }
+    DecodeArgs b = a;
+    b.only = a.ds.big;
+    launch_v2<16, 3, false, 1, false, true>(s, b);
+  } else if (a.ds.on) {
+    launch_v2<16, 3, false, 1, false, true>(s, a);
+  } else {
+    launch_v2<16, 3, false, 1, false>(s, a);
+  }
   return hipGetLastError();
 }
 

@@ -132,6 +132,8 @@ struct DsFuse {
   unsigned long long* rm_ctr;
   unsigned long long* rm_mem;
   uint32_t* why;                 // diagnostics (CE_DS_FUSE_DEBUG=1): per file, the step that declined it
+  uint8_t* big;                  // [n] k_open_ds8: 1 = a single-page file past kDsFuseRegion, left
+                                 // to the 16-lane DS kernel's pass over that mask (a.only)
 };
 
 struct DecodeArgs {
