@@ -256,6 +256,10 @@ struct DsColsRemaps {
   DsColsRemap f[kColsInline];
 };
 hipError_t launch_cols_remap(hipStream_t s, const DsColsRemap* parts, uint32_t k);
+// a column partial's deferred CSR section checked in place (offsets ordered and in range, actor
+// indices < na): *bad (zeroed beforehand) = 1 when it is not
+hipError_t launch_ds_csr_check(hipStream_t s, const uint32_t* cbeg, const uint32_t* mbeg, const uint32_t* act,
+                               uint32_t n_rm, uint32_t n_ent, uint32_t n_mem, uint32_t na, uint32_t* bad);
 hipError_t launch_ds_merge_finalize(hipStream_t s, DsTables t, const unsigned long long* clock,
                                    const unsigned long long* oclock);
 // live pairs -> (member, actor, value) columns (any order); n_out[0] (zeroed beforehand) = their

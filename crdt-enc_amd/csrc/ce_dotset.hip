@@ -2057,6 +2057,33 @@ __global__ void __launch_bounds__(kBlock) k_cols_remap(DsColsRemaps r) {
     x.oclock[(size_t)x.map[i] * x.ostride] = x.clock[i];
 }
 
+// a column partial's deferred section (CSR: cbeg / mbeg n_rm + 1 offsets, act n_ent indices into
+// the partial's na actors) checked before the remap and the kill kernels walk it: *bad = 1 on any
+// offset out of order or past its array, or an actor index >= na
+__global__ void __launch_bounds__(kBlock) k_ds_csr_check(const uint32_t* cbeg, const uint32_t* mbeg, const uint32_t* act,
+                                                         uint32_t n_rm, uint32_t n_ent, uint32_t n_mem, uint32_t na,
+                                                         uint32_t* bad) {
+  const uint32_t nt = gridDim.x * kBlock;
+  bool b = false;
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i <= n_rm; i += nt) {
+    const uint32_t c = cbeg[i], m = mbeg[i];
+    if (i == 0) b |= c != 0 || m != 0;
+    else b |= c < cbeg[i - 1] || m < mbeg[i - 1];
+    if (i == n_rm) b |= c != n_ent || m != n_mem;
+    b |= c > n_ent || m > n_mem;
+  }
+  for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < n_ent; j += nt) b |= act[j] >= na;
+  if (b) *bad = 1u;
+}
+
+hipError_t launch_ds_csr_check(hipStream_t s, const uint32_t* cbeg, const uint32_t* mbeg, const uint32_t* act,
+                               uint32_t n_rm, uint32_t n_ent, uint32_t n_mem, uint32_t na, uint32_t* bad) {
+  const uint32_t mx = std::max(n_rm + 1, n_ent);
+  hipLaunchKernelGGL(k_ds_csr_check, dim3(std::min<uint32_t>(blocks_for(mx), 1024)), dim3(kBlock), 0, s, cbeg, mbeg, act,
+                     n_rm, n_ent, n_mem, na, bad);
+  return hipGetLastError();
+}
+
 hipError_t launch_cols_remap(hipStream_t s, const DsColsRemap* parts, uint32_t k) {
   for (uint32_t c0 = 0; c0 < k; c0 += kColsInline) {
     DsColsRemaps r{};

@@ -86,8 +86,8 @@ struct DsState {
   size_t ser_sort_words = 0;
   uint32_t ser_sort_gen = 0;     // sorts so far (the state's histogram parity)
   // the multi-GPU column exchange (ds_export_columns_device / ds_merge_columns_device)
-  HostBuf cx_host, cx_heads, cx_map;
-  DevBuf cx_mapd, cx_ids, cx_slot;
+  HostBuf cx_host, cx_heads, cx_map, cx_dheads;
+  DevBuf cx_mapd, cx_ids, cx_slot, cx_defact, cx_defflag;
   std::vector<uint32_t> cx_idslot;  // actor id -> table slot, as of table_gen cx_idslot_gen
   uint64_t cx_idslot_gen = ~0ull;
   void* col5_zeroed = nullptr;  // col[5] (the collect counter) was cleared at this address
@@ -524,6 +524,33 @@ int upload_removals(ce_core* c, const std::vector<std::pair<IdDots, std::vector<
   if ((e = up(d->d0[0].as<uint32_t>(), cbeg, s)) || (e = up(d->d0[1].as<uint32_t>(), mbeg, s)) ||
       (e = up(d->d0[2].as<uint32_t>(), act, s)) || (e = up(d->d0[3].as<unsigned long long>(), ctr, s)) ||
       (e = up(d->d0[4].as<unsigned long long>(), mem, s)) || (e = stream_wait(s)))
+    return c->ctx->hip_fail(e, "removals");
+  return CE_OK;
+}
+
+// removals as CSR arrays on the host (the column merge's: hundreds of thousands of deferred
+// removals at N = 8 with read-context clocks, without a heap object per removal)
+struct RmCsr {
+  std::vector<uint32_t> cbeg{0}, mbeg{0}, act;
+  std::vector<unsigned long long> ctr, mem;
+  uint32_t size() const { return (uint32_t)cbeg.size() - 1; }
+  void close() {
+    cbeg.push_back((uint32_t)act.size());
+    mbeg.push_back((uint32_t)mem.size());
+  }
+};
+
+int upload_removals_csr(ce_core* c, const RmCsr& r) {
+  DsState* d = c->ds;
+  hipError_t e;
+  if ((e = d->d0[0].reserve(r.cbeg.size() * 4)) || (e = d->d0[1].reserve(r.mbeg.size() * 4)) ||
+      (e = d->d0[2].reserve(r.act.size() * 4 + 4)) || (e = d->d0[3].reserve(r.ctr.size() * 8 + 8)) ||
+      (e = d->d0[4].reserve(r.mem.size() * 8 + 8)))
+    return c->ctx->hip_fail(e, "removals");
+  hipStream_t s = c->ctx->stream;
+  if ((e = up(d->d0[0].as<uint32_t>(), r.cbeg, s)) || (e = up(d->d0[1].as<uint32_t>(), r.mbeg, s)) ||
+      (e = up(d->d0[2].as<uint32_t>(), r.act, s)) || (e = up(d->d0[3].as<unsigned long long>(), r.ctr, s)) ||
+      (e = up(d->d0[4].as<unsigned long long>(), r.mem, s)) || (e = stream_wait(s)))
     return c->ctx->hip_fail(e, "removals");
   return CE_OK;
 }
@@ -2705,8 +2732,9 @@ int ds_state_bytes_device(ce_core* c, ce_ctx* x, uint8_t* dst, uint64_t cap, uin
 //   0 u32 magic 'CECL' | u32 version 1 | u64 pairs np | u32 actors na | u32 flags | u64 dlen
 //   32 uuid[16 na] | clock u64[na] | nov u64[na] | member u64[np] | value u64[np] | actor u32[np]
 //   then, when flags bit 0 (the partial holds deferred removals), at the next 8-byte boundary the
-//   deferred map as dlen bytes of u64 words: n, then per removal nc, nm, (actor, counter) x nc,
-//   member x nm
+//   deferred map as dlen bytes of CSR arrays (what the kill / deferred-flag kernels read in place):
+//   u64 n_rm, n_ent, n_mem, 0 | cbeg u32[n_rm + 1] | mbeg u32[n_rm + 1] | pad8 | actor u32[n_ent] |
+//   pad8 | counter u64[n_ent] | member u64[n_mem]
 // (actor = an index into the partial's own UUID list).
 namespace {
 constexpr uint32_t kColsMagic = 0x4c434543u;  // "CECL"
@@ -2720,6 +2748,19 @@ struct ColsHeader {
 static_assert(sizeof(ColsHeader) == 32, "column partial header");
 uint64_t cols_len(uint64_t na, uint64_t np) { return 32 + 32 * na + 20 * np; }
 uint64_t cols_def_off(uint64_t na, uint64_t np) { return (cols_len(na, np) + 7) & ~7ull; }
+uint64_t al8(uint64_t x) { return (x + 7) & ~7ull; }
+// byte offsets inside a deferred section (from its start)
+struct DefLayout {
+  uint64_t cbeg, mbeg, act, ctr, mem, len;
+  DefLayout(uint64_t n_rm, uint64_t n_ent, uint64_t n_mem) {
+    cbeg = 32;
+    mbeg = cbeg + 4 * (n_rm + 1);
+    act = al8(mbeg + 4 * (n_rm + 1));
+    ctr = al8(act + 4 * n_ent);
+    mem = ctr + 8 * n_ent;
+    len = mem + 8 * n_mem;
+  }
+};
 }  // namespace
 
 int ds_export_columns_device(ce_core* c, uint8_t* dst, uint64_t cap, uint64_t* len) {
@@ -2740,18 +2781,39 @@ int ds_export_columns_device(ce_core* c, uint8_t* dst, uint64_t cap, uint64_t* l
   uint32_t nl = 0;
   if ((rc = collect(c, &nl))) return rc;
   const uint32_t na = (uint32_t)c->id_actor.size();
-  // the deferred map (small, on the host) as u64 words by this core's actor ids
-  std::vector<uint64_t> dw;
+  // the deferred map (on the host) as CSR arrays by this core's actor ids
+  std::vector<uint8_t> dw;
   if (!d->deferred.empty()) {
-    dw.push_back(d->deferred.size());
+    uint64_t ne = 0, nm = 0;
     for (auto& x : d->deferred) {
-      dw.push_back(x.first.size());
-      dw.push_back(x.second.size());
-      for (auto& y : x.first) { dw.push_back(y.first); dw.push_back(y.second); }
-      for (uint64_t m : x.second) dw.push_back(m);
+      ne += x.first.size();
+      nm += x.second.size();
+    }
+    const uint64_t nr = d->deferred.size();
+    const DefLayout L(nr, ne, nm);
+    dw.assign(L.len, 0);
+    uint64_t* hdr = reinterpret_cast<uint64_t*>(dw.data());
+    hdr[0] = nr;
+    hdr[1] = ne;
+    hdr[2] = nm;
+    uint32_t* cb = reinterpret_cast<uint32_t*>(dw.data() + L.cbeg);
+    uint32_t* mb = reinterpret_cast<uint32_t*>(dw.data() + L.mbeg);
+    uint32_t* ac = reinterpret_cast<uint32_t*>(dw.data() + L.act);
+    uint64_t* ct = reinterpret_cast<uint64_t*>(dw.data() + L.ctr);
+    uint64_t* me = reinterpret_cast<uint64_t*>(dw.data() + L.mem);
+    uint32_t r = 0, e = 0, q = 0;
+    cb[0] = mb[0] = 0;
+    for (auto& x : d->deferred) {
+      for (auto& y : x.first) {
+        ac[e] = y.first;
+        ct[e++] = y.second;
+      }
+      for (uint64_t m : x.second) me[q++] = m;
+      cb[++r] = e;
+      mb[r] = q;
     }
   }
-  const uint64_t o_def = cols_def_off(na, nl), dlen = 8ull * dw.size();
+  const uint64_t o_def = cols_def_off(na, nl), dlen = dw.size();
   const uint64_t need = dw.empty() ? cols_len(na, nl) : o_def + dlen;
   *len = need;
   if (need > cap) return ctx->fail(CE_ERR_INVALID_ARG, "device buffer too small for the columns");
@@ -2778,7 +2840,7 @@ int ds_export_columns_device(ce_core* c, uint8_t* dst, uint64_t cap, uint64_t* l
   fl.r[fl.n++] = {w(o_val), 2ull * nl, 0u, d->col[2].as<uint32_t>()};
   fl.r[fl.n++] = {w(o_act), nl, 0u, d->col[1].as<uint32_t>()};
   if (!dw.empty()) {
-    std::memcpy(h + 32 + 24ull * na, dw.data(), dlen);
+    std::memcpy(h + 32 + 24ull * na, dw.data(), dlen);  // (32 + 24 na: 8-aligned)
     fl.r[fl.n++] = {w(o_def), dlen / 4, 0u, hdev + (32 + 24ull * na) / 4};
   }
   // complete on return, as the state-bytes export: the caller's collective runs on another stream
@@ -2830,7 +2892,7 @@ int ds_merge_columns_device(ce_core* c, const uint8_t* const* parts, const uint6
     const bool hasdef = hd[f].flags == kColsDeferred;
     const uint64_t want = hasdef ? cols_def_off(hd[f].na, hd[f].np) + hd[f].dlen : cols_len(hd[f].na, hd[f].np);
     if (hd[f].magic != kColsMagic || hd[f].version != 1 || (hd[f].flags & ~kColsDeferred) ||
-        (hasdef ? (hd[f].dlen < 8 || (hd[f].dlen & 7)) : hd[f].dlen != 0) || want != lens[f] ||
+        (hasdef ? (hd[f].dlen < 40 || (hd[f].dlen & 7)) : hd[f].dlen != 0) || want != lens[f] ||
         hd[f].np >= (1ull << 31))
       return ctx->fail(CE_ERR_DECODE, "not a column partial");
     np_tot += hd[f].np;
@@ -2848,6 +2910,74 @@ int ds_merge_columns_device(ce_core* c, const uint8_t* const* parts, const uint6
       }
     if ((e = gather_download(d, s, d->cx_heads.as<uint8_t>(), gr, more)) || (e = stream_wait(s)))
       return ctx->hip_fail(e, "columns");
+  }
+  // the parts' deferred maps (Orswot::merge merges other.deferred, lib.rs:458-466): only their
+  // 32-byte heads come to the host; the CSR arrays are read in place by the kill and deferred-flag
+  // kernels after the k-way merge below, their actors mapped to this core's ids on the device
+  struct PartDef {
+    uint32_t f;
+    uint64_t n_rm, n_ent, n_mem, ent0, rm0;
+    const uint8_t* base;
+    DefLayout L{0, 0, 0};
+  };
+  std::vector<PartDef> pdef;
+  uint64_t def_ent = 0, def_rm = 0;
+  {
+    std::vector<GatherRange> gr;
+    uint64_t o = 0;
+    for (uint32_t f = 0; f < k; f++)
+      if (hd[f].flags & kColsDeferred) {
+        gr.push_back({parts[f] + cols_def_off(hd[f].na, hd[f].np), o, 32});
+        o += 32;
+      }
+    if (o) {
+      ph.emplace("  cols: deferred heads");
+      if ((e = d->cx_dheads.reserve(o + 64))) return ctx->hip_fail(e, "columns");
+      if ((e = gather_download(d, s, d->cx_dheads.as<uint8_t>(), gr, o)) || (e = stream_wait(s)))
+        return ctx->hip_fail(e, "columns");
+      const uint64_t* q = d->cx_dheads.as<uint64_t>();
+      uint32_t qi = 0;
+      for (uint32_t f = 0; f < k; f++) {
+        if (!(hd[f].flags & kColsDeferred)) continue;
+        PartDef x;
+        x.f = f;
+        x.n_rm = q[4 * qi];
+        x.n_ent = q[4 * qi + 1];
+        x.n_mem = q[4 * qi + 2];
+        qi++;
+        if (x.n_rm > hd[f].dlen || x.n_ent > hd[f].dlen || x.n_mem > hd[f].dlen)
+          return ctx->fail(CE_ERR_DECODE, "column partial: deferred map");
+        x.L = DefLayout(x.n_rm, x.n_ent, x.n_mem);
+        if (x.L.len != hd[f].dlen) return ctx->fail(CE_ERR_DECODE, "column partial: deferred map");
+        x.base = parts[f] + cols_def_off(hd[f].na, hd[f].np);
+        x.ent0 = def_ent;
+        x.rm0 = def_rm;
+        def_ent += x.n_ent;
+        def_rm += x.n_rm;
+        pdef.push_back(x);
+      }
+    }
+  }
+  // every deferred section checked on the device (offsets ordered and in range, actor indices in
+  // the part's list) before this core's state or the remap and kill kernels touch anything
+  if (!pdef.empty()) {
+    if ((e = d->cx_defact.reserve(4 * def_ent + 64)) || (e = d->cx_defflag.reserve(def_rm + 64 + 4 * (uint64_t)k)))
+      return ctx->hip_fail(e, "columns");
+    uint32_t* bad = reinterpret_cast<uint32_t*>(d->cx_defflag.as<uint8_t>() + ((def_rm + 3) & ~3ull));
+    std::vector<uint32_t> hb(pdef.size());
+    if ((e = hipMemsetAsync(bad, 0, 4 * hb.size(), s))) return ctx->hip_fail(e, "columns");
+    for (size_t i = 0; i < pdef.size(); i++) {
+      const PartDef& x = pdef[i];
+      if ((e = launch_ds_csr_check(s, reinterpret_cast<const uint32_t*>(x.base + x.L.cbeg),
+                                   reinterpret_cast<const uint32_t*>(x.base + x.L.mbeg),
+                                   reinterpret_cast<const uint32_t*>(x.base + x.L.act), (uint32_t)x.n_rm,
+                                   (uint32_t)x.n_ent, (uint32_t)x.n_mem, hd[x.f].na, bad + i)))
+        return ctx->hip_fail(e, "columns");
+    }
+    if ((e = hipMemcpyAsync(hb.data(), bad, 4 * hb.size(), hipMemcpyDeviceToHost, s)) || (e = stream_wait(s)))
+      return ctx->hip_fail(e, "columns");
+    for (uint32_t b : hb)
+      if (b) return ctx->fail(CE_ERR_DECODE, "column partial: deferred map");
   }
   ph.emplace("  cols: actors");
   // 2) every part's actors in this core's table (ids), next_op_versions merged (VClock::merge).
@@ -2896,57 +3026,6 @@ int ds_merge_columns_device(ce_core* c, const uint8_t* const* parts, const uint6
       m += na;
     }
   }
-  // the parts' deferred maps (Orswot::merge merges other.deferred, lib.rs:458-466): downloaded in
-  // one gather, their actors mapped to this core's ids; applied after the k-way merge below
-  std::vector<std::pair<IdDots, std::vector<uint64_t>>> pdef;
-  {
-    std::vector<GatherRange> gr;
-    uint64_t o = 0;
-    for (uint32_t f = 0; f < k; f++)
-      if (hd[f].flags & kColsDeferred) {
-        gr.push_back({parts[f] + cols_def_off(hd[f].na, hd[f].np), o, hd[f].dlen});
-        o += hd[f].dlen;
-      }
-    if (o) {
-      ph.emplace("  cols: deferred");
-      if ((e = d->cx_heads.reserve(o + 64))) return ctx->hip_fail(e, "columns");
-      if ((e = gather_download(d, s, d->cx_heads.as<uint8_t>(), gr, o)) || (e = stream_wait(s)))
-        return ctx->hip_fail(e, "columns");
-      const uint64_t* q = d->cx_heads.as<uint64_t>();
-      uint64_t m = 0, qi = 0;
-      for (uint32_t f = 0; f < k; f++) {
-        const uint64_t na = hd[f].na;
-        if (hd[f].flags & kColsDeferred) {
-          const uint64_t end = qi + hd[f].dlen / 8;
-          auto take = [&](uint64_t* v) {
-            if (qi >= end) return false;
-            *v = q[qi++];
-            return true;
-          };
-          uint64_t nr = 0;
-          if (!take(&nr) || nr > hd[f].dlen / 24) return ctx->fail(CE_ERR_DECODE, "column partial: deferred map");
-          for (uint64_t r = 0; r < nr; r++) {
-            uint64_t nc = 0, nm = 0;
-            if (!take(&nc) || !take(&nm) || nc + nm > end - qi) return ctx->fail(CE_ERR_DECODE, "column partial: deferred map");
-            IdDots ck;
-            for (uint64_t j = 0; j < nc; j++) {
-              uint64_t a = 0, v = 0;
-              take(&a);
-              take(&v);
-              if (a >= na) return ctx->fail(CE_ERR_DECODE, "column partial: deferred actor");
-              if (v) ck.push_back({hmap[m + a], v});
-            }
-            std::sort(ck.begin(), ck.end());
-            std::vector<uint64_t> ms(nm);
-            for (uint64_t j = 0; j < nm; j++) take(&ms[j]);
-            pdef.push_back({std::move(ck), std::move(ms)});
-          }
-          if (qi != end) return ctx->fail(CE_ERR_DECODE, "column partial: deferred map");
-        }
-        m += na;
-      }
-    }
-  }
   ph.emplace("  cols: tables");
   if ((rc = table_upload(c)) || (rc = ensure_clock(c)) || (rc = ensure_pairs(c, np_tot))) return rc;
   ph.emplace("  cols: launch");
@@ -2974,11 +3053,26 @@ int ds_merge_columns_device(ce_core* c, const uint8_t* const* parts, const uint6
       q += np;
     }
   }
+  // the deferred sections' actors: part-local -> this core's ids (k_cols_remap, no clock), and a
+  // check of their CSR bounds on the device before any kernel walks them
+  if (!pdef.empty()) {
+    uint64_t mo = 0;
+    std::vector<uint64_t> moff(k);
+    for (uint32_t f = 0; f < k; f++) {
+      moff[f] = mo;
+      mo += hd[f].na;
+    }
+    for (size_t i = 0; i < pdef.size(); i++) {
+      const PartDef& x = pdef[i];
+      rm.push_back(DsColsRemap{reinterpret_cast<const uint32_t*>(x.base + x.L.act), d->cx_defact.as<uint32_t>() + x.ent0,
+                               d->cx_mapd.as<uint32_t>() + moff[x.f], nullptr, nullptr, (uint32_t)x.n_ent, 0u, 0u});
+    }
+  }
   // 4) one k-way merge of every part into the state (launch_ds_kmerge; the live counts land in
   //    pinned memory for ds_settle, like the state files' merge)
   d->scratch_dirty = true;
   const int tm = ctx->tbegin("cols_merge");
-  if ((e = launch_fill(s, fl)) || (e = launch_cols_remap(s, rm.data(), k)) ||
+  if ((fl.n && (e = launch_fill(s, fl))) || (e = launch_cols_remap(s, rm.data(), (uint32_t)rm.size())) ||
       (e = launch_ds_kmerge(s, tables(d), nullptr, src.data(), k, d->clock.as<unsigned long long>(),
                             d->rd_oclocks.as<unsigned long long>(), ccap, ostride, d->hold.as<unsigned long long>(),
                             static_cast<uint32_t*>(host_dev_ptr(d->h_cnt.as<uint32_t>() + 56)))))
@@ -2998,22 +3092,73 @@ int ds_merge_columns_device(ce_core* c, const uint8_t* const* parts, const uint6
   //    deferred (apply_deferred) -- order-free, as the merge rule above
   if (!pdef.empty() || !d->deferred.empty()) {
     ph.emplace("  cols: apply deferred");
-    auto rms = deferred_list(d);
-    rms.insert(rms.end(), pdef.begin(), pdef.end());
-    if ((rc = upload_removals(c, rms))) return rc;
-    const uint32_t nr = (uint32_t)rms.size();
-    if ((e = launch_ds_kill(s, tables(d), d->d0[0].as<uint32_t>(), d->d0[1].as<uint32_t>(), d->d0[2].as<uint32_t>(),
-                            d->d0[3].as<unsigned long long>(), d->d0[4].as<unsigned long long>(), nr)))
+    RmCsr own;  // this core's deferred removals (uploaded), then the parts' in place
+    std::vector<const std::pair<const IdDots, std::set<uint64_t>>*> ownp;
+    for (auto& x : d->deferred) {
+      for (auto& y : x.first) {
+        own.act.push_back(y.first);
+        own.ctr.push_back(y.second);
+      }
+      for (uint64_t mv : x.second) own.mem.push_back(mv);
+      own.close();
+      ownp.push_back(&x);
+    }
+    const uint32_t no = own.size();
+    if (no && (rc = upload_removals_csr(c, own))) return rc;
+    if (no && (e = launch_ds_kill(s, tables(d), d->d0[0].as<uint32_t>(), d->d0[1].as<uint32_t>(), d->d0[2].as<uint32_t>(),
+                                  d->d0[3].as<unsigned long long>(), d->d0[4].as<unsigned long long>(), no)))
       return ctx->hip_fail(e, "columns");
+    for (auto& x : pdef) {
+      if ((e = launch_ds_kill(s, tables(d), reinterpret_cast<const uint32_t*>(x.base + x.L.cbeg),
+                              reinterpret_cast<const uint32_t*>(x.base + x.L.mbeg), d->cx_defact.as<uint32_t>() + x.ent0,
+                              reinterpret_cast<const unsigned long long*>(x.base + x.L.ctr),
+                              reinterpret_cast<const unsigned long long*>(x.base + x.L.mem), (uint32_t)x.n_rm)))
+        return ctx->hip_fail(e, "columns");
+    }
     d->scratch_dirty = true;
     if ((rc = finalize(c))) return rc;
     d->scratch_dirty = false;
-    std::vector<uint8_t> fl2;
-    if ((rc = flags_for(c, d->d0[0].as<uint32_t>(), d->d0[2].as<uint32_t>(), d->d0[3].as<unsigned long long>(), nr, &fl2)))
+    // which removals the merged clock does not cover (they stay deferred): the parts' flags on the
+    // device, one download
+    std::vector<uint8_t> fo, fp(def_rm);
+    if ((rc = flags_for(c, d->d0[0].as<uint32_t>(), d->d0[2].as<uint32_t>(), d->d0[3].as<unsigned long long>(), no, &fo)))
       return rc;
+    for (auto& x : pdef)
+      if (x.n_rm && (e = launch_ds_deferred(s, reinterpret_cast<const uint32_t*>(x.base + x.L.cbeg),
+                                            d->cx_defact.as<uint32_t>() + x.ent0,
+                                            reinterpret_cast<const unsigned long long*>(x.base + x.L.ctr),
+                                            d->clock.as<unsigned long long>(), d->cx_defflag.as<uint8_t>() + x.rm0,
+                                            (uint32_t)x.n_rm)))
+        return ctx->hip_fail(e, "columns");
+    if (def_rm && ((e = hipMemcpyAsync(fp.data(), d->cx_defflag.p, def_rm, hipMemcpyDeviceToHost, s)) || (e = stream_wait(s))))
+      return ctx->hip_fail(e, "columns");
     std::map<IdDots, std::set<uint64_t>> nd;
-    for (uint32_t i = 0; i < nr; i++)
-      if (fl2[i]) nd[rms[i].first].insert(rms[i].second.begin(), rms[i].second.end());
+    for (uint32_t i = 0; i < no; i++)
+      if (fo[i]) nd[ownp[i]->first].insert(ownp[i]->second.begin(), ownp[i]->second.end());
+    for (auto& x : pdef) {  // (usually none: the merged clock covers what the partials deferred)
+      bool any = false;
+      for (uint64_t i = 0; i < x.n_rm && !any; i++) any = fp[x.rm0 + i] != 0;
+      if (!any) continue;
+      std::vector<uint8_t> sec(x.L.len);
+      std::vector<uint32_t> ids(x.n_ent);
+      if ((e = hipMemcpyAsync(sec.data(), x.base, x.L.len, hipMemcpyDeviceToHost, s)) ||
+          (x.n_ent && (e = hipMemcpyAsync(ids.data(), d->cx_defact.as<uint32_t>() + x.ent0, 4 * x.n_ent,
+                                          hipMemcpyDeviceToHost, s))) ||
+          (e = stream_wait(s)))
+        return ctx->hip_fail(e, "columns");
+      const uint32_t* cb = reinterpret_cast<const uint32_t*>(sec.data() + x.L.cbeg);
+      const uint32_t* mb = reinterpret_cast<const uint32_t*>(sec.data() + x.L.mbeg);
+      const uint64_t* ct = reinterpret_cast<const uint64_t*>(sec.data() + x.L.ctr);
+      const uint64_t* me = reinterpret_cast<const uint64_t*>(sec.data() + x.L.mem);
+      for (uint64_t i = 0; i < x.n_rm; i++) {
+        if (!fp[x.rm0 + i]) continue;
+        IdDots kk;
+        for (uint32_t j = cb[i]; j < cb[i + 1]; j++)
+          if (ct[j]) kk.push_back({ids[j], ct[j]});
+        std::sort(kk.begin(), kk.end());
+        nd[kk].insert(me + mb[i], me + mb[i + 1]);
+      }
+    }
     d->deferred = std::move(nd);
     c->path_counts["columns_merge_deferred"]++;
   }

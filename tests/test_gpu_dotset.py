@@ -7,6 +7,7 @@ itself is unpinned: the oracle restates its published source.
 """
 import os
 import random
+import struct
 
 import msgpack
 import numpy as np
@@ -1383,6 +1384,21 @@ def test_columns_export_merge_equals_state_merge(ctx):
     rc, n = d.export_columns_device(bufs[0].data_ptr(), bufs[0].numel())
     assert rc == 0 and n > 0
     dbuf = bufs[0][:n].clone()
+    # a deferred section the device check refuses (an actor index past the partial's actors, then
+    # removal offsets out of order): CE_ERR_DECODE, the receiver's state unchanged
+    hb = dbuf.cpu().numpy().tobytes()
+    np_, na_ = struct.unpack_from("<QI", hb, 8)
+    dof = (32 + 32 * na_ + 20 * np_ + 7) & ~7
+    n_rm, n_ent, n_mem = struct.unpack_from("<QQQ", hb, dof)
+    assert (n_rm, n_ent, n_mem) == (1, 1, 1)
+    act_off = dof + ((32 + 8 * (n_rm + 1) + 7) & ~7)
+    before = shards[1].state_bytes()
+    for off, val in ((act_off, na_ + 3), (dof + 36, 5)):
+        bad = bytearray(hb)
+        struct.pack_into("<I", bad, off, val)
+        tb = torch.frombuffer(bytes(bad), dtype=torch.uint8).to("cuda:0")
+        assert shards[1].merge_columns_device([tb.data_ptr()], [n]) == 12
+        assert shards[1].state_bytes() == before
     seq2 = new_core(ctx, "orswot", key)
     assert seq2.merge_state(shards[1].state_bytes()) == 0 and seq2.merge_state(d.state_bytes()) == 0
     assert shards[1].merge_columns_device([dbuf.data_ptr()], [n]) == 0       # theirs deferred

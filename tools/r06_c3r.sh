@@ -11,3 +11,7 @@ l = json.loads(open("gpurun_out/c3r.json").read().strip().splitlines()[-1])
 print(json.dumps({k: l.get(k) for k in ("ms_per_step", "value", "checks", "config", "fold", "kernels_ms_per_step", "phases_ms_per_step", "pipelined")}, indent=0)[:4000])
 print("cpu", json.dumps(l.get("cpu_baseline"))[:600])
 PY
+for rc in own read; do
+  timeout -k 10 400 python -u tools/cols_bench.py --parts 7 --rm-ctx $rc --steps 10 > gpurun_out/cols_k7_$rc.json 2> gpurun_out/cols_k7_$rc.err || { tail -20 gpurun_out/cols_k7_$rc.err; exit 1; }
+  tail -1 gpurun_out/cols_k7_$rc.json
+done
