@@ -1501,6 +1501,16 @@ void k_open_fold_v2(DecodeArgs a) {
 #endif
 }
 
+#ifndef CE_V3_UNR
+#define CE_V3_UNR 1  // ChaCha20 double rounds per trip of chacha_block_pre's 9-trip loop: 1 keeps
+#endif                // the kernel's code inside the instruction cache (9, straight-line: +2% time)
+#ifndef CE_V3_PRIO
+#define CE_V3_PRIO 2  // wave priority over the decode (s_setprio): the decode's short dependent
+#endif                // chains issue ahead of the other wave's ChaCha20 (C2-B -10%, C2 flat)
+// the Poly1305 value 1 in radix-2^26 limbs (k_open_fold_v3's weight of the lanes at q & 3 = 0 /
+// q >> 2 = 0, read like the other weights)
+__device__ const uint32_t kPolyOne[8] = {1u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+
 // ----------------------------------------------------------------------------------------
 // k_open_fold_v3: k_open_fold_v2<16, 2, false, 1> (the C2 kernel) with its Poly1305 rebuilt
 // around the setup's per-file constants (PolyAux, ce_kernels.h), so that every Poly1305 step
@@ -1540,12 +1550,22 @@ void k_open_fold_v3(DecodeArgs a) {
   AuthFails fails;
   // this lane's tree weight r^(4q), q = (sub + 15) & 15: X = r^(4 (q & 3)) in {1, r^4, r^8,
   // r^12}, Y = r^(16 (q >> 2)) in {1, r^16, r^32, r^48}, read from FileParams.rpow / PolyAux
+  // As per-lane (base, stride) address pairs, X at base + f stride (stride 0: the constant 1),
+  // so the loop holds no per-lane selects or lane masks for them
   const uint32_t qpos = (sub + 15u) & 15u;
   const uint32_t qx = qpos & 3u, qy = qpos >> 2;
-  const bool x_one = qx == 0, y_one = qy == 0, x_aux = qx == 3, y_aux = qy == 3;
-  const uint32_t x_off = x_aux ? (uint32_t)offsetof(PolyAux, r12) : 80u + 20u * (qx + 1u);
-  const uint32_t y_off = y_aux ? (uint32_t)offsetof(PolyAux, r48) : 80u + 20u * (qy + 3u);
   static_assert(offsetof(FileParams, rpow) == 80, "rpow offset");
+  auto wsrc = [&](uint32_t q, uint32_t aux_off, uint32_t rp_idx, const uint8_t*& base, uint32_t& stride) {
+    base = q == 0 ? reinterpret_cast<const uint8_t*>(kPolyOne)
+         : q == 3 ? reinterpret_cast<const uint8_t*>(a.aux) + aux_off
+                  : reinterpret_cast<const uint8_t*>(a.params) + 80u + 20u * rp_idx;
+    stride = q == 0 ? 0u : q == 3 ? (uint32_t)sizeof(PolyAux) : (uint32_t)sizeof(FileParams);
+  };
+  const uint8_t* x_base;
+  const uint8_t* y_base;
+  uint32_t x_stride, y_stride;
+  wsrc(qx, (uint32_t)offsetof(PolyAux, r12), qx + 1u, x_base, x_stride);
+  wsrc(qy, (uint32_t)offsetof(PolyAux, r48), qy + 3u, y_base, y_stride);
 
   uint4 ct[BPL][4];
   for (; g < g_end; g++) {
@@ -1611,10 +1631,9 @@ void k_open_fold_v3(DecodeArgs a) {
         const uint8_t* pb = b0 >= 0 ? src + 16 * (int64_t)(4 * b0 - (int32_t)dl) : src;
 #pragma unroll
         for (int j = 0; j < 4; j++) pc[j] = *reinterpret_cast<const uint4*>(pb + 16 * j);
-        const uint32_t* xs = reinterpret_cast<const uint32_t*>(
-            (x_aux ? reinterpret_cast<const uint8_t*>(Xp) : reinterpret_cast<const uint8_t*>(Pp)) + x_off);
-        const uint32_t* ys = reinterpret_cast<const uint32_t*>(
-            (y_aux ? reinterpret_cast<const uint8_t*>(Xp) : reinterpret_cast<const uint8_t*>(Pp)) + y_off);
+        const uint32_t fi = act ? f : 0u;
+        const uint32_t* xs = reinterpret_cast<const uint32_t*>(x_base + (uint64_t)fi * x_stride);
+        const uint32_t* ys = reinterpret_cast<const uint32_t*>(y_base + (uint64_t)fi * y_stride);
 #pragma unroll
         for (int i = 0; i < 5; i++) {
           X.v[i] = xs[i];
@@ -1627,7 +1646,7 @@ void k_open_fold_v3(DecodeArgs a) {
       }
       uint32_t kb[16];
       if (!PAIR) {
-        chacha_block_pre<true, 9>(cpre, cur.key, 1u + (uint32_t)b, 0u, cur.n2a, cur.n2b, kb);
+        chacha_block_pre<true, CE_V3_UNR>(cpre, cur.key, 1u + (uint32_t)b, 0u, cur.n2a, cur.n2b, kb);
       } else {
         if (k & 1) chacha_block_pre2(cpre, cur.key, 1u + (uint32_t)b, 1u + (uint32_t)(b + LPF), 0u,
                                      cur.n2a, cur.n2b, kb, kbn);
@@ -1691,11 +1710,6 @@ void k_open_fold_v3(DecodeArgs a) {
     }
 
     // 2) U = sum_q v_q r^(4q): each chain times its weight, then the group's sum into lane 0
-#pragma unroll
-    for (int i = 0; i < 5; i++) {
-      X.v[i] = x_one ? (i == 0 ? 1u : 0u) : X.v[i];
-      Y.v[i] = y_one ? (i == 0 ? 1u : 0u) : Y.v[i];
-    }
     L5 v = mulmod(mulmod(acc, X), Y);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -1717,9 +1731,11 @@ void k_open_fold_v3(DecodeArgs a) {
 
     // 4) data-version check, decode from LDS, fold; the next iteration's parameters are loaded
     //    inside (their latency hides under the decode)
+    if (CE_V3_PRIO) __builtin_amdgcn_s_setprio(CE_V3_PRIO);  // the decode's short dependent chains first
     decode_fold<LPF, 0, true>(a, sup, fl, len, act && ok, cur.apply != 0, f, grp, sub, S, [&] {
       if (!EARLY) nx = load_pre2(a, (g + 1) * F + grp);
     });
+    if (CE_V3_PRIO) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_wave_barrier();
   }
   flush_pending<LPF>(a, sub, S.pslot, S.pbest);
