@@ -1146,6 +1146,12 @@ __device__ __forceinline__ bool ds_fused_decode(const DecodeArgs& a, const SupVe
   return chain;
 }
 
+#ifndef CE_V2_OPEN_UNR
+#define CE_V2_OPEN_UNR 1  // the open-only / DS forms' ChaCha20 loop (C3 open 159 -> 158 us, half the code)
+#endif
+#ifndef CE_DS_PRIO
+#define CE_DS_PRIO 2
+#endif
 // W = waves per SIMD the VGPR budget is sized for (LDS allows 2.5 at LPF 16, 5 at LPF 32).
 // OPT bits: 1 = rot16 as two SDWA xors (ce_device.h xor_rotl16_t), 2 = the next iteration's
 // ciphertext loads issued inside this iteration's decode (after its first round, with the
@@ -1168,7 +1174,8 @@ void k_open_fold_v2(DecodeArgs a) {
 #endif
   constexpr bool SD = (OPT & 1) != 0;
   constexpr bool PF = (OPT & 2) != 0 && !JIT;
-  constexpr int UNR = (OPT & 4) ? 1 : (OPT & 8) ? 3 : 9;  // ChaCha20 double rounds per loop trip
+  // ChaCha20 double rounds per loop trip (the open-only and DS forms: CE_V2_OPEN_UNR)
+  constexpr int UNR = (OPT & 4) ? 1 : (OPT & 8) ? 3 : DEC ? 9 : CE_V2_OPEN_UNR;
   // OPT 16: the first-processed block (k = BPL - 1) of the NEXT iteration is loaded as soon as
   // this iteration has consumed its own (its parameters are loaded at this iteration's start)
   constexpr bool PF1 = (OPT & 16) != 0 && !PF && !JIT;
@@ -1461,7 +1468,11 @@ void k_open_fold_v2(DecodeArgs a) {
     if (!DEC) {
       if (DS) {
         bool done = false;
-        if (__any(dsl && ok)) done = ds_fused_decode<LPF>(a, sup, fl, aux, len, dsl && ok, f, grp, sub);
+        if (__any(dsl && ok)) {
+          if (CE_DS_PRIO) __builtin_amdgcn_s_setprio(CE_DS_PRIO);  // as k_open_fold_v3's decode
+          done = ds_fused_decode<LPF>(a, sup, fl, aux, len, dsl && ok, f, grp, sub);
+          if (CE_DS_PRIO) __builtin_amdgcn_s_setprio(0);
+        }
         if (dsl && ok && !done) {  // the lane-per-file decode reads it from HBM
           for (uint32_t q = sub; q * 16u < len; q += LPF)
             *reinterpret_cast<uint4*>(gout + q * 16u) = *reinterpret_cast<const uint4*>(fl + q * 16u);
