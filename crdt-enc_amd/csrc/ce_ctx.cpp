@@ -148,7 +148,7 @@ int device_open(ce_ctx* ctx, const uint8_t* d_blob, const uint64_t* d_offs, uint
   SegScratch sc = segscratch(ctx, ec);
   FileParams* P = ctx->params.as<FileParams>();
   // the DS form's 8-lane kernel reads the setup's PolyAux rows (k_open_ds8)
-  static const bool ds8_on = getenv("CE_DS8") && atoi(getenv("CE_DS8")) == 1;  // (ce_fused.hip)
+  static const bool ds8_on = !(getenv("CE_DS8") && atoi(getenv("CE_DS8")) == 0);  // (ce_fused.hip)
   const bool want_aux = small_lanes && ds && ds->ds.on && ds->ds.big && ds8_on;
   if (want_aux && (e = ctx->poly_aux.reserve((size_t)n * sizeof(PolyAux))) != hipSuccess)
     return ctx->hip_fail(e, "reserve poly aux");

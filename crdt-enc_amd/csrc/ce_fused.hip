@@ -1869,7 +1869,7 @@ void k_open_ds8(DecodeArgs a) {
         for (int i = 0; i < 4; i++) ts[i] = Xp->ts[i];
       }
       uint32_t kb[16];
-      chacha_block_pre<true, 9>(cpre, cur.key, 1u + (uint32_t)b, 0u, cur.n2a, cur.n2b, kb);
+      chacha_block_pre<true, CE_V2_OPEN_UNR>(cpre, cur.key, 1u + (uint32_t)b, 0u, cur.n2a, cur.n2b, kb);
       L5 m[4];
 #pragma unroll
       for (int j = 0; j < 4; j++) {
@@ -1939,7 +1939,11 @@ void k_open_ds8(DecodeArgs a) {
     const bool ok = grp_bits<LPF>(tag_ok, grp) != 0;
     if (PF) load_ct(nx);
     bool done = false;
-    if (__any(act && ok)) done = ds_fused_decode<LPF>(a, sup, fl, aux, len, act && ok, f, grp, sub);
+    if (__any(act && ok)) {
+      if (CE_DS_PRIO) __builtin_amdgcn_s_setprio(CE_DS_PRIO);
+      done = ds_fused_decode<LPF>(a, sup, fl, aux, len, act && ok, f, grp, sub);
+      if (CE_DS_PRIO) __builtin_amdgcn_s_setprio(0);
+    }
     if (act && ok && !done) {  // the lane-per-file decode reads it from HBM
       for (uint32_t q = sub; q * 16u < len; q += LPF)
         *reinterpret_cast<uint4*>(gout + q * 16u) = *reinterpret_cast<const uint4*>(fl + q * 16u);
@@ -1973,15 +1977,15 @@ static void launch_v2(hipStream_t s, const DecodeArgs& a, hipEvent_t t0 = nullpt
 // a.only / a.apply unused.  Larger files: k_segments with skip_small (their setup's list).
 hipError_t launch_open_small_v2(hipStream_t s, const DecodeArgs& a) {
   if (a.n == 0) return hipSuccess;
-  // CE_DS8=1 (opt-in A/B): 8 lanes per file for files of at most kDsFuseRegion bytes
-  // (k_open_ds8, with the setup's PolyAux), then the 16-lane DS form over the files it left
-  // (a.only = big; it returns at once when there are none).  Measured at C3 (r06, same box,
-  // rocprofv3): 65.0K VALU lane-instr per file against 79.7K, but 153-155 us against 159-162 us
-  // for the 16-lane form, plus 6 us for the second pass: at 2 waves per SIMD (206 VGPRs, 20 KiB of
-  // LDS per wave) the decode's LDS and table latencies stay exposed, so it is not the default.
-  // The 16-lane DS form at a 3-wave VGPR budget (168, a few spills): same-box A/B against 2 waves
-  // (191 VGPRs, none): 155 vs 162 us at C3 (r05)
-  static const bool ds8_on = getenv("CE_DS8") && atoi(getenv("CE_DS8")) == 1;
+  // The DS form: 8 lanes per file for files of at most kDsFuseRegion bytes (k_open_ds8, with the
+  // setup's PolyAux), then the 16-lane DS form over the files it left (a.only = big; it returns
+  // at once when there are none).  CE_DS8=0: the 16-lane form for every file (A/B).  Measured at
+  // C3 (r06, same box, rocprofv3): 65.0K VALU lane-instr per file against 79.7K; with both
+  // kernels' ChaCha20 rolled and the decode at raised wave priority, 143.5 us against 150.8 us
+  // (before: 153-155 against 159-162, the decode's LDS and table latencies exposed at 2 waves per
+  // SIMD).  The 16-lane DS form at a 3-wave VGPR budget (168, a few spills): same-box A/B against
+  // 2 waves (191 VGPRs, none): 155 vs 162 us at C3 (r05)
+  static const bool ds8_on = !(getenv("CE_DS8") && atoi(getenv("CE_DS8")) == 0);
   if (a.ds.on && a.aux && a.ds.big && ds8_on) {
     static const bool pf = !(getenv("CE_DS8_PF") && atoi(getenv("CE_DS8_PF")) == 0);
     if (pf) {
