@@ -28,6 +28,7 @@ with merge_state (the multi-GPU exchange) serializes to the same bytes.
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -359,11 +360,12 @@ class CompactPipe:
         self.order = []         # name futures in step order
         self.i = 0
         self.last_file = None
+        self.names = not NO_NAMES
 
     def _name(self, k, ln, tk):
         ln = self.core.compact_wait(tk) if tk else ln
         self.last_file = self.obuf[k][:ln]
-        if NO_NAMES:    # diagnostics only: the step without the host's SHA3 load beside it
+        if not self.names:    # diagnostics only: the step without the host's SHA3 load beside it
             return
         self.fut[k] = (self.namer.submit(self.last_file) if isinstance(self.namer, BatchNamer)
                        else self.namer.submit(crdtenc.content_name, self.last_file))
@@ -590,6 +592,22 @@ def run_c3(args, ctx, dev):
     th1 = time.perf_counter()
     pipe.drain()
     host_states[0] = False
+    # diagnostic leg: the same pipelined step with the content names off (the host's SHA3 load
+    # beside the device pipeline removed; never the line's value)
+    pipe.names = False
+    step()
+    pipe.flush()
+    torch.cuda.synchronize()
+    tn0 = time.perf_counter()
+    nn = max(10, args.steps // 2)
+    for _ in range(nn):
+        step()
+    pipe.flush()
+    torch.cuda.synchronize()
+    no_names = {"ms_per_step": round((time.perf_counter() - tn0) * 1e3 / nn, 3), "steps": nn,
+                "what": "diagnostic: the same pipelined step (downloads included) without the SHA3-256 "
+                        "content names, i.e. without the host hashing load beside the device pipeline"}
+    pipe.names = not NO_NAMES
     states_from_host = {"pipelined_ms_per_step": round((th1 - th0) * 1e3 / nh, 3), "steps": nh,
                         "what": "the same step with the 8 state files uploaded from per-file host "
                                 "buffers each step (ce_core_ingest_states_iov: pinned staging + DMA)"}
@@ -679,6 +697,20 @@ def run_c3(args, ctx, dev):
     # with finalize, the clock; the global kernels: applied + add_pairs + kill, finalize apart)
     # (ds_contig: the contiguity check, which also writes the applied flags of increasing runs)
     fold_ms = sum(k_ms.get(x, 0) for x in ("ds_applied", "ds_contig", "ds_add_pairs", "ds_kill", "ds_part_fold"))
+    # the op open's VALU roofline: SURVEY §8(d)'s int32 lane-ops per file at the op files' mean
+    # plaintext length, over the open kernels' time (setup + the fused DS open) against the
+    # 78.6 T lane-op/s slot peak (bench.py roofline)
+    mean_pt = pt_ops / n
+    ops_file = 992 * math.ceil(mean_pt / 64) + 992 + 960 + 48 * (math.ceil(mean_pt / 16) + 1)
+    op_open_ms = sum(k_ms.get(x, 0) for x in ("open_setup", "open_small"))
+    open_roofline = None
+    if op_open_ms:
+        ach = ops_file * n / (op_open_ms / 1e3) / 1e12
+        open_roofline = {"bound": "valu", "ops_per_file": ops_file, "files": n,
+                         "ms": round(op_open_ms, 4), "achieved": round(ach, 2), "peak": 78.6,
+                         "unit": "T int32 lane-ops/s", "frac": round(ach / 78.6, 4),
+                         "note": "ops at the op files' mean plaintext (%.0f B); open_setup covers the state "
+                                 "files' setup as well" % mean_pt}
     shape = ("26 Add + 6 Rm, %d B" % PT_LEN if not rc_stats else
              "26 Add + 6 Rm whose clocks are the removed member's read context (the state files' adds "
              "of it + the writer's own: %.2f entries per clock), %.0f B mean, %d B max"
@@ -706,7 +738,9 @@ def run_c3(args, ctx, dev):
                               "step on the device (ce_core_compact_into_async) and its content name "
                               "hashed on %d host threads; timed up to the last download; ms_per_step "
                               "above adds the names still being hashed then (drain / steps)" % name_threads()},
+        "no_names": no_names,
         "aead_open_GBps": round(ct / (open_ms / 1e3) / 1e9, 1) if open_ms else None,
+        "open_roofline": open_roofline,
         "fold": {"kernels": "applied flags (ds_contig for increasing runs, else ds_applied) + ds_part_fold (member "
                             "probes, items into per-partition runs, LDS fold + finalize, clock)" if "ds_part_fold" in k_ms
                  else "ds_applied + ds_add_pairs + ds_kill",

@@ -371,19 +371,21 @@ int ce_core_merge_state_device(ce_core *c, const uint8_t *d_sw, uint64_t len);
 
 /* The multi-GPU dot-set exchange as columns: an Orswot's live (member, actor, counter) pairs, its
  * clock, next_op_versions and actor UUIDs written into device memory d_dst (cap bytes) -- no
- * msgpack, no parse on the receiving side.  *len = the bytes written, or needed when cap is too
- * small (CE_ERR_INVALID_ARG).  A state with deferred removals (or another kind) has no column form:
- * CE_ERR_INVALID_ARG with *len = 0, and the caller exchanges ce_core_state_bytes_device instead.
+ * msgpack, no parse on the receiving side -- and, when the state holds deferred removals, its
+ * deferred map as a final section of CSR arrays (removal clocks by the partial's actor index and
+ * their members; format in INTEGRATION.md).  *len = the bytes written, or needed when cap is too
+ * small (CE_ERR_INVALID_ARG).  Another kind than Orswot has no column form: CE_ERR_INVALID_ARG
+ * with *len = 0, and the caller exchanges ce_core_state_bytes_device instead.
  * d_dst NULL with cap 0 is a query: CE_ERR_INVALID_ARG with *len = 1 when the state has a column
  * form, 0 when not (nothing is collected).
  * Complete on return.  Replaces, for the exchange only, the serialize -> parse round trip of
  * read_remote_states' merge (crdt-enc/src/lib.rs:458-466). */
 int ce_core_export_columns_device(ce_core *c, uint8_t *d_dst, uint64_t cap, uint64_t *len);
-/* Merge k column partials (device pointers d_parts[i], lens[i] bytes) into the state at once:
- * Orswot::merge of every part (the same result as merging their StateWrappers one by one, in
- * any order), next_op_versions max-merged.  Complete on return (the parts may be reused).
- * CE_ERR_DECODE when a part is not a column partial; CE_ERR_INVALID_ARG when this state has
- * deferred removals (merge state bytes instead). */
+/* Merge k <= 64 column partials (device pointers d_parts[i], lens[i] bytes) into the state at once:
+ * Orswot::merge of every part, deferred removals on either side included (the same result as
+ * merging their StateWrappers one by one, in any order), next_op_versions max-merged.  Complete
+ * on return (the parts may be reused).  CE_ERR_DECODE when a part is not a column partial or its
+ * deferred section is malformed (checked on the device before this state is touched). */
 int ce_core_merge_columns_device(ce_core *c, const uint8_t *const *d_parts, const uint64_t *lens, uint32_t k);
 
 /* Dense state exchange for multi-GPU merges (one process per GPU): actors registered in the
