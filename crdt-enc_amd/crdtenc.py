@@ -867,20 +867,22 @@ class Core:
 
     def export_columns_device(self, d_dst, cap):
         """The column form of an Orswot for the multi-GPU exchange, into device memory d_dst (cap
-        bytes): (rc, length); rc INVALID_ARG with the needed length when cap is too small, with
-        length 0 when the state has no column form (deferred removals: use state_bytes_device)."""
+        bytes), deferred removals as its final section: (rc, length); rc INVALID_ARG with the
+        needed length when cap is too small, with length 0 when the state has no column form
+        (not an Orswot: use state_bytes_device)."""
         n = ctypes.c_uint64(0)
         rc = lib().ce_core_export_columns_device(self.p, ctypes.c_void_p(d_dst), ctypes.c_uint64(cap), ctypes.byref(n))
         return rc, n.value
 
     def columns_ready(self):
-        """the state has a column form now (an Orswot without deferred removals)"""
+        """the state has a column form (an Orswot, deferred removals included)"""
         n = ctypes.c_uint64(0)
         lib().ce_core_export_columns_device(self.p, None, ctypes.c_uint64(0), ctypes.byref(n))
         return n.value != 0
 
     def merge_columns_device(self, d_parts, lens):
-        """Merge column partials (device pointers, byte lengths) into the state at once."""
+        """Merge column partials (device pointers, byte lengths; at most 64) into the state at once,
+        their deferred removals and this state's applied after the k-way merge."""
         k = len(d_parts)
         ptrs = (ctypes.c_void_p * max(k, 1))(*d_parts)
         ls = (ctypes.c_uint64 * max(k, 1))(*lens)
