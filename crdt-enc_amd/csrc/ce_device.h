@@ -126,6 +126,7 @@ __device__ __forceinline__ void chacha_block_pre(const ChachaPre& pre, const uin
 
 // two chacha_block_pre blocks (counters ca, cb) with their quarter rounds interleaved: eight
 // independent ARX chains per round instead of four
+template <int UNR = 9>
 __device__ __forceinline__ void chacha_block_pre2(const ChachaPre& pre, const uint32_t (&k)[8],
                                                   uint32_t ca, uint32_t cb, uint32_t n0, uint32_t n1,
                                                   uint32_t n2, uint32_t (&oa)[16], uint32_t (&ob)[16]) {
@@ -146,10 +147,16 @@ __device__ __forceinline__ void chacha_block_pre2(const ChachaPre& pre, const ui
   x[4] = rotl32(x[4], 7); y[4] = rotl32(y[4], 7);
 #define CE_QR2(a, b, c, d) CE_QR_T(true, x[a], x[b], x[c], x[d]); CE_QR_T(true, y[a], y[b], y[c], y[d]);
   CE_QR2(0, 5, 10, 15); CE_QR2(1, 6, 11, 12); CE_QR2(2, 7, 8, 13); CE_QR2(3, 4, 9, 14);
-#pragma unroll
-  for (int i = 0; i < 9; i++) {
+  auto dround2 = [&] {
     CE_QR2(0, 4, 8, 12); CE_QR2(1, 5, 9, 13); CE_QR2(2, 6, 10, 14); CE_QR2(3, 7, 11, 15);
     CE_QR2(0, 5, 10, 15); CE_QR2(1, 6, 11, 12); CE_QR2(2, 7, 8, 13); CE_QR2(3, 4, 9, 14);
+  };
+  if constexpr (UNR == 1) {
+#pragma unroll 1
+    for (int i = 0; i < 9; i++) dround2();
+  } else {
+#pragma unroll
+    for (int i = 0; i < 9; i++) dround2();
   }
 #undef CE_QR2
   const uint32_t c4[4] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u};

@@ -1659,7 +1659,7 @@ void k_open_fold_v3(DecodeArgs a) {
       if (!PAIR) {
         chacha_block_pre<true, CE_V3_UNR>(cpre, cur.key, 1u + (uint32_t)b, 0u, cur.n2a, cur.n2b, kb);
       } else {
-        if (k & 1) chacha_block_pre2(cpre, cur.key, 1u + (uint32_t)b, 1u + (uint32_t)(b + LPF), 0u,
+        if (k & 1) chacha_block_pre2<CE_V3_UNR>(cpre, cur.key, 1u + (uint32_t)b, 1u + (uint32_t)(b + LPF), 0u,
                                      cur.n2a, cur.n2b, kb, kbn);
         else {
 #pragma unroll
