@@ -238,7 +238,8 @@ struct DsMergeSrc {
 hipError_t launch_ds_kmerge(hipStream_t s, DsTables t, const DsMergeSrc* d_src, const DsMergeSrc* h_src, uint32_t nf,
                             unsigned long long* clock, const unsigned long long* oclocks, uint32_t ccap, uint32_t ostride,
                             unsigned long long* hold, uint32_t* pub_dst = nullptr,  // pub_dst: live[0..5) -> pinned
-                            const uint32_t* go = nullptr);  // go: every kernel does nothing unless *go
+                            const uint32_t* go = nullptr,  // go: every kernel does nothing unless *go
+                            bool fresh = false);  // the table holds no pair: the current values are not read
 // one column partial of the multi-GPU exchange (ds_merge_columns_device): its actor column and
 // clock remapped to the receiving core's ids
 struct DsColsRemap {

@@ -1361,6 +1361,7 @@ constexpr uint32_t kMergeInline = 16;
 struct DsMergeSrcs {
   DsMergeSrc f[kMergeInline];
   uint32_t f0;  // the first file's index in the merge (its hold bit)
+  uint32_t fresh;  // the table held no pair before the merge: every cur is 0 (not read)
   const uint32_t* go;  // optional: nothing happens unless *go (a merge queued before the host
                        // knows that every file was read on the device, ds_merge_states_device)
 };
@@ -1386,7 +1387,9 @@ __global__ void __launch_bounds__(kBlock) k_ds_kput(DsTables t, DsMergeSrcs src)
   }
 }
 
-__global__ void __launch_bounds__(kBlock) k_ds_khold(DsTables t, DsMergeSrcs src, unsigned long long* hold) {
+// H: the hold word (u32 when the merge has at most 32 sources: half the bytes of k_ds_kfinal's read)
+template <typename H>
+__global__ void __launch_bounds__(kBlock) k_ds_khold(DsTables t, DsMergeSrcs src, H* hold) {
   if (kmerge_off(src.go)) return;
   const DsMergeSrc x = src.f[blockIdx.y];
   const uint32_t fb = src.f0 + blockIdx.y;
@@ -1403,17 +1406,18 @@ __global__ void __launch_bounds__(kBlock) k_ds_khold(DsTables t, DsMergeSrcs src
       b = pair_find(t, pair_key(h, x.actor[i]), false);
       if (b == kDsEmpty) continue;
     }
-    const unsigned long long c = t.cur[b], o = t.oth[b];
-    if (x.value[i] == (c > o ? c : o)) atomicOr(&hold[b], 1ull << fb);
+    const unsigned long long c = src.fresh ? 0ull : t.cur[b], o = t.oth[b];
+    if (x.value[i] == (c > o ? c : o)) atomicOr(&hold[b], (H)1 << fb);
   }
 }
 
 // oclocks: the files' dense clocks actor-major, oclocks[a * ostride + f] (ostride a multiple of 8
 // >= nf, the padding zero): a slot's first eight files' clocks are one 64-byte line, four 16-byte
 // loads (file-major, eight gathers from lines 32 KiB apart took ~70 us at C3's 8 state files)
+template <typename H>
 __global__ void __launch_bounds__(kBlock) k_ds_kfinal(DsTables t, const unsigned long long* clock,
                                                       const unsigned long long* oclocks, uint32_t ostride,
-                                                      uint32_t nf, unsigned long long* hold, const uint32_t* go) {
+                                                      uint32_t nf, H* hold, const uint32_t* go, uint32_t fresh) {
   if (kmerge_off(go)) return;
   const uint32_t cap = t.pmask + 1;
   uint32_t n_used = 0, n_live = 0, n_mem = primary_used(t, blockIdx.x, gridDim.x);
@@ -1429,7 +1433,7 @@ __global__ void __launch_bounds__(kBlock) k_ds_kfinal(DsTables t, const unsigned
       if (key[q] == kDsEmpty) continue;
       // (add / kill are zero here: every fold's finalize clears what it set, so a state merge never
       // meets a batch's scratch -- not read, 64 MB less per pass at C3)
-      s[q] = t.cur[b0 + q * kBlock];
+      s[q] = fresh ? 0ull : t.cur[b0 + q * kBlock];
       o[q] = t.oth[b0 + q * kBlock];
       hm[q] = hold[b0 + q * kBlock];
     }
@@ -2024,7 +2028,7 @@ hipError_t launch_ds_merge_finalize(hipStream_t s, DsTables t, const unsigned lo
 
 hipError_t launch_ds_kmerge(hipStream_t s, DsTables t, const DsMergeSrc* d_src, const DsMergeSrc* h_src, uint32_t nf,
                             unsigned long long* clock, const unsigned long long* oclocks, uint32_t ccap, uint32_t ostride,
-                            unsigned long long* hold, uint32_t* pub_dst, const uint32_t* go) {
+                            unsigned long long* hold, uint32_t* pub_dst, const uint32_t* go, bool fresh) {
   (void)d_src;
   uint32_t nmax = 0;
   for (uint32_t f = 0; f < nf; f++) nmax = h_src[f].n > nmax ? h_src[f].n : nmax;
@@ -2033,15 +2037,26 @@ hipError_t launch_ds_kmerge(hipStream_t s, DsTables t, const DsMergeSrc* d_src, 
     DsMergeSrcs m{};
     m.f0 = c0;
     m.go = go;
+    m.fresh = fresh ? 1u : 0u;
     for (uint32_t i = 0; i < kMergeInline && c0 + i < nf; i++) m.f[i] = h_src[c0 + i];
     return m;
   };
   for (uint32_t c0 = 0; c0 < nf; c0 += kMergeInline)
     hipLaunchKernelGGL(k_ds_kput, dim3(gx, std::min(kMergeInline, nf - c0)), dim3(kBlock), 0, s, t, srcs(c0));
-  for (uint32_t c0 = 0; c0 < nf; c0 += kMergeInline)
-    hipLaunchKernelGGL(k_ds_khold, dim3(gx, std::min(kMergeInline, nf - c0)), dim3(kBlock), 0, s, t, srcs(c0), hold);
-  hipLaunchKernelGGL(k_ds_kfinal, dim3(blocks_for((uint64_t)t.pmask + 1, 1024)), dim3(kBlock), 0, s, t, clock, oclocks,
-                     ostride, nf, hold, go);
+  const dim3 gf(blocks_for((uint64_t)t.pmask + 1, 1024));
+  if (nf <= 32) {  // (the buffer is zero as u64 words: its u32 view too)
+    uint32_t* h32 = reinterpret_cast<uint32_t*>(hold);
+    for (uint32_t c0 = 0; c0 < nf; c0 += kMergeInline)
+      hipLaunchKernelGGL(k_ds_khold<uint32_t>, dim3(gx, std::min(kMergeInline, nf - c0)), dim3(kBlock), 0, s, t, srcs(c0), h32);
+    hipLaunchKernelGGL(k_ds_kfinal<uint32_t>, gf, dim3(kBlock), 0, s, t, clock, oclocks, ostride, nf, h32, go,
+                       fresh ? 1u : 0u);
+  } else {
+    for (uint32_t c0 = 0; c0 < nf; c0 += kMergeInline)
+      hipLaunchKernelGGL(k_ds_khold<unsigned long long>, dim3(gx, std::min(kMergeInline, nf - c0)), dim3(kBlock), 0, s, t,
+                         srcs(c0), hold);
+    hipLaunchKernelGGL(k_ds_kfinal<unsigned long long>, gf, dim3(kBlock), 0, s, t, clock, oclocks, ostride, nf, hold, go,
+                       fresh ? 1u : 0u);
+  }
   hipLaunchKernelGGL(k_ds_kclock, dim3(std::max<uint32_t>(1, blocks_for(ccap))), dim3(kBlock), 0, s, clock, oclocks,
                      ccap, ostride, nf, t.live, pub_dst, 5u, go);
   return hipGetLastError();

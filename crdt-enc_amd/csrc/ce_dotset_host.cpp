@@ -2111,11 +2111,15 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
         hs[i] = DsMergeSrc{b[7].as<unsigned long long>(), b[8].as<uint32_t>(), b[9].as<unsigned long long>(),
                            (uint32_t)dmax[i], d->cx_slot.as<uint32_t>() + q, misc + 2 * n + 4 * i};
       }
+      // no pair in the table yet (read_remote after a reset: C3's state files): the merge reads no
+      // current values
+      const bool fresh = d->used_pairs == 0 && !d->settle_pending;
       d->scratch_dirty = true;
       if ((e = launch_ds_kmerge(s, tables(d), nullptr, hs.data(), (uint32_t)n, d->clock.as<unsigned long long>(),
                                 d->rd_oclocks.as<unsigned long long>(), d->clock_cap, ostride,
                                 d->hold.as<unsigned long long>(),
-                                static_cast<uint32_t*>(host_dev_ptr(d->h_cnt.as<uint32_t>() + 56)), misc + 6 * n)))
+                                static_cast<uint32_t*>(host_dev_ptr(d->h_cnt.as<uint32_t>() + 56)), misc + 6 * n,
+                                fresh)))
         return ctx->hip_fail(e, "merge");
       d->scratch_dirty = false;  // (k_ds_kfinal cleared oth / hold, or nothing ran)
     }
@@ -2231,11 +2235,12 @@ int ds_merge_states_device(ce_core* c, const uint8_t* out, const std::vector<uin
       }
       // no host wait: the merged counts land in pinned memory for ds_settle (the next ingest's
       // first wait), like a fold's
+      const bool fresh = d->used_pairs == 0 && !d->settle_pending;
       d->scratch_dirty = true;
       if ((e = launch_ds_kmerge(s, tables(d), nullptr, hs, (uint32_t)n,
                                 d->clock.as<unsigned long long>(), d->rd_oclocks.as<unsigned long long>(), ccap, ostride,
                                 d->hold.as<unsigned long long>(),
-                                static_cast<uint32_t*>(host_dev_ptr(d->h_cnt.as<uint32_t>() + 56)))))
+                                static_cast<uint32_t*>(host_dev_ptr(d->h_cnt.as<uint32_t>() + 56)), nullptr, fresh)))
         return ctx->hip_fail(e, "merge");
     }
     c->path_counts["states_kway_merge"]++;

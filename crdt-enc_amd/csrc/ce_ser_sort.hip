@@ -240,6 +240,11 @@ void pass_launch(hipStream_t s, SerSortArgs a, uint32_t p) {
       return 0u;
     return (uint32_t)(per_cu > 0 ? per_cu : 0) * (uint32_t)(cus > 0 ? cus : 0);
   }();
+  // Without the ticket the look-back relies on in-order workgroup dispatch: the command processor
+  // hands out a grid's workgroups in blockIdx order, so every tile a tile waits on was dispatched
+  // before it and holds a CU -- even when other streams' kernels (RCCL, the side stream) occupy
+  // part of the GPU and not every tile is resident at once.  CE_SORT_TICKET=1 takes the ticket
+  // (dispatch order made explicit) on any grid.
   static const bool force_ticket = getenv("CE_SORT_TICKET") != nullptr;  // (tests / A/B)
   a.ticketed = force_ticket || a.tiles > res ? 1u : 0u;
   hipLaunchKernelGGL((k_sort_pass<K, FIRST, LAST>), dim3(a.tiles), dim3(kSortThreads), 0, s, a, p);

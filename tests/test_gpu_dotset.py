@@ -235,15 +235,19 @@ def _kway_state_merge(ctx, p_rm):
             sws.append(part.serialize())
     rng.shuffle(sws)
     kway_runs = 0
-    for batch in (sws[:9], sws[9:], list(reversed(sws))):
+    # (into an empty state: the k-way merge reads no current values; 40 files: 64-bit hold words)
+    wide = (sws * 3)[:40]
+    for batch, first in ((sws[:9], True), (sws[9:], True), (list(reversed(sws)), True), (sws[:9], False),
+                         (wide, False), (wide, True)):
         got = []
         for env in (None, "1"):
             if env:
                 os.environ["CE_NO_KMERGE"] = env
             try:
                 core, oc = new_core(ctx, "orswot", key), C.Core("orswot")
-                pre = seal_states(ctx, key, [sws[0]])          # a non-empty state first
-                assert core.ingest_states(pre)[0] == oc.read_remote_states(key, [APP], pre)[0] == 0
+                if first:
+                    pre = seal_states(ctx, key, [sws[0]])          # a non-empty state first
+                    assert core.ingest_states(pre)[0] == oc.read_remote_states(key, [APP], pre)[0] == 0
                 sf = seal_states(ctx, key, batch)
                 rc, st = core.ingest_states(sf)
                 orc, ost = oc.read_remote_states(key, [APP], sf)
