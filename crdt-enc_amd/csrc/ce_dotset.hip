@@ -2043,7 +2043,8 @@ hipError_t launch_ds_kmerge(hipStream_t s, DsTables t, const DsMergeSrc* d_src, 
   };
   for (uint32_t c0 = 0; c0 < nf; c0 += kMergeInline)
     hipLaunchKernelGGL(k_ds_kput, dim3(gx, std::min(kMergeInline, nf - c0)), dim3(kBlock), 0, s, t, srcs(c0));
-  const dim3 gf(blocks_for((uint64_t)t.pmask + 1, 1024));
+  static const uint32_t kf_cap = getenv("CE_KFINAL_BLOCKS") ? (uint32_t)atoi(getenv("CE_KFINAL_BLOCKS")) : 1024u;
+  const dim3 gf(blocks_for((uint64_t)t.pmask + 1, kf_cap));
   if (nf <= 32) {  // (the buffer is zero as u64 words: its u32 view too)
     uint32_t* h32 = reinterpret_cast<uint32_t*>(hold);
     for (uint32_t c0 = 0; c0 < nf; c0 += kMergeInline)
