@@ -807,8 +807,10 @@ int ds_settle(ce_core* c) {
     return ctx->fail(CE_ERR_DEVICE, "dot-set table overflow");
   }
   if (d->settle_delta) {
+    // (k_ds_part_apply adds both words as one 64-bit value: a negative live change borrowed one
+    // from the used count's word)
     d->live_pairs += (int64_t)(int32_t)hl[0];
-    d->used_pairs += hl[1];
+    d->used_pairs += hl[1] + ((int32_t)hl[0] < 0 ? 1u : 0u);
     // items past their partition's run (folded from the overflow lists): longer runs next time
     if (d->settle_fold && hl[5]) {
       d->part_factor = std::min<uint32_t>(64, std::max<uint32_t>(1, d->part_factor) * 2);
