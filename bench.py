@@ -763,7 +763,7 @@ def main():
             with open(vf) as f:
                 rec = json.load(f).get("fused", {})
             ipf = rec.get("valu_instr_per_file_per_lane")
-            if ipf and rec.get("kernel", "").replace("ce::", "") == kshort:
+            if ipf and rec.get("kernel", "").replace("void ", "").replace("ce::", "") == kshort:
                 t = wa_n(args, world) * ipf / (sa["avg_launch_ms"] / 1e3) / 1e12
                 valu_pmc = {"instr_per_file": ipf, "achieved_tops": round(t, 2),
                             "frac_of_peak": round(t / VALU_PEAK_TOPS, 4),
