@@ -1986,7 +1986,10 @@ hipError_t launch_ds_count_members(hipStream_t s, DsTables t, uint32_t* out) {
 
 hipError_t launch_ds_part_count(hipStream_t s, const DsPartArgs& a) {
   const size_t lds = (size_t)a.parts * 4;
-  if (a.chunk == kDsPartChunkSmall) {
+  if (a.chunk == 256 * kPartBatch) {
+    hipLaunchKernelGGL(k_ds_part_adds<256>, dim3(a.ba ? a.ba : 1), dim3(256), lds, s, a);
+    if (a.bk) hipLaunchKernelGGL(k_ds_part_kills<256>, dim3(a.bk), dim3(256), lds, s, a);
+  } else if (a.chunk == kDsPartChunkSmall) {
     hipLaunchKernelGGL(k_ds_part_adds<kDsPartThreadsSmall>, dim3(a.ba ? a.ba : 1), dim3(kDsPartThreadsSmall), lds, s, a);
     if (a.bk) hipLaunchKernelGGL(k_ds_part_kills<kDsPartThreadsSmall>, dim3(a.bk), dim3(kDsPartThreadsSmall), lds, s, a);
   } else {
