@@ -116,6 +116,29 @@ __device__ unsigned long long pair_find(const DsTables& t, unsigned long long ke
   return kDsEmpty;
 }
 
+// pair_find(insert = true) that also says whether this call inserted the key (its compare-and-swap
+// won): exactly one caller per new pair does
+__device__ unsigned long long pair_find_ins(const DsTables& t, unsigned long long key, bool* ins) {
+  uint32_t h = (uint32_t)mix64(key) & t.pmask;
+  const uint32_t lo = h & ~(kDsPartSlots - 1);
+  *ins = false;
+  for (uint32_t probe = 0; probe < kDsPartSlots; probe++) {
+    const unsigned long long k = ld_volatile(t.pkey + h);
+    if (k == key) return h;
+    if (k == kDsEmpty) {
+      const unsigned long long prev = atomicCAS(t.pkey + h, kDsEmpty, key);
+      if (prev == kDsEmpty) {
+        *ins = true;
+        return h;
+      }
+      if (prev == key) return h;
+    }
+    h = lo | ((h + 1) & (kDsPartSlots - 1));
+  }
+  atomicAdd(t.live + 2, 1u);
+  return kDsEmpty;
+}
+
 __device__ __forceinline__ unsigned long long pair_key(unsigned long long handle, uint32_t aid) {
   return (handle << kDsActorBits) | aid;
 }
@@ -1364,6 +1387,16 @@ __global__ void __launch_bounds__(kBlock) k_ds_merge_finalize(DsTables t, const 
 // that max; k_ds_kfinal: the test above, then finalize's add / kill as k_ds_merge_finalize.
 // (sources by value, kMergeInline files per launch: an uploaded descriptor array was a runtime copy)
 constexpr uint32_t kMergeInline = 16;
+constexpr uint32_t kSlotOwner = 0x80000000u;  // DsMergeSrc.slot: this row inserted the pair
+// the k-way merge's live / used / member counts: each block of its final pass adds into one of
+// kLiveReps replicas (t.live[16 + 16 r ..], 64 B apart: same-address atomics serialise in L2, one
+// chain per replica instead of one for the grid), k_ds_kclock sums them into live[0], [1], [4]
+constexpr uint32_t kLiveReps = 16;
+__device__ __forceinline__ void kmerge_count(const DsTables& t, uint32_t block, uint32_t l, uint32_t u, uint32_t mm) {
+  uint32_t* r = t.live + 16 + 16 * (block % kLiveReps);
+  if (l | u) atomicAdd(reinterpret_cast<unsigned long long*>(r), ((unsigned long long)u << 32) | l);
+  if (mm) atomicAdd(r + 2, mm);
+}
 struct DsMergeSrcs {
   DsMergeSrc f[kMergeInline];
   uint32_t f0;  // the first file's index in the merge (its hold bit)
@@ -1384,12 +1417,15 @@ __global__ void __launch_bounds__(kBlock) k_ds_kput(DsTables t, DsMergeSrcs src)
   const DsMergeSrc x = src.f[blockIdx.y];
   if (src.f0 == 0 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2) t.live[threadIdx.x] = 0;  // k_ds_kfinal counts
   if (src.f0 == 0 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 2) t.live[4] = 0;
+  if (src.f0 == 0 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 16 * kLiveReps) t.live[16 + threadIdx.x] = 0;
   const uint32_t n = kmerge_n(x);
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
     const unsigned long long h = member_find(t, x.member[i], true);
-    const unsigned long long b = h == kDsEmpty ? kDsEmpty : pair_find(t, pair_key(h, x.actor[i]), true);
+    bool ins = false;
+    const unsigned long long b = h == kDsEmpty ? kDsEmpty : pair_find_ins(t, pair_key(h, x.actor[i]), &ins);
     if (b != kDsEmpty) atomicMax(&t.oth[b], x.value[i]);
-    if (x.slot) x.slot[i] = b == kDsEmpty ? ~0u : (uint32_t)b;
+    // the slot, bit 31 = this row inserted the pair (its owner for k_ds_kfinal_rows)
+    if (x.slot) x.slot[i] = b == kDsEmpty ? ~0u : (uint32_t)b | (ins ? kSlotOwner : 0u);
   }
 }
 
@@ -1405,7 +1441,7 @@ __global__ void __launch_bounds__(kBlock) k_ds_khold(DsTables t, DsMergeSrcs src
     if (x.slot) {  // recorded by k_ds_kput: no second probe of the member and pair tables
       const uint32_t r = x.slot[i];
       if (r == ~0u) continue;
-      b = r;
+      b = r & ~kSlotOwner;
     } else {
       const unsigned long long h = member_find(t, x.member[i], false);
       if (h == kDsEmpty) continue;
@@ -1503,8 +1539,73 @@ __global__ void __launch_bounds__(kBlock) k_ds_kfinal(DsTables t, const unsigned
     }
     // live[0] (live pairs) and live[1] (used slots) in one 64-bit add: same-address atomics
     // serialise in L2 (~60 ns each across XCDs), one per block instead of two
-    if (l | u) atomicAdd(reinterpret_cast<unsigned long long*>(t.live), ((unsigned long long)u << 32) | l);
-    if (mm) atomicAdd(t.live + 4, mm);  // (zeroed by k_ds_kput)
+    kmerge_count(t, blockIdx.x, l, u, mm);  // (replicas zeroed by k_ds_kput)
+  }
+}
+
+// k_ds_kfinal over the merge's rows instead of the table's slots, for a merge into an empty table
+// (fresh: every used slot was inserted by exactly one row, its owner -- k_ds_kput's slot bit 31):
+// the owner row applies the rule to its slot (the current value is 0), so the pass reads the rows'
+// slots and the touched slots' words, not the whole table's keys (C3: 0.41M rows, 4M slots).
+// Grid (x, y) as k_ds_kput's, sources y of this launch (f0 + y); the primary member table's used
+// slots are counted in slices over every block of every launch (live[4]).
+template <typename H>
+__global__ void __launch_bounds__(kBlock) k_ds_kfinal_rows(DsTables t, DsMergeSrcs src, const unsigned long long* clock,
+                                                           const unsigned long long* oclocks, uint32_t ostride,
+                                                           uint32_t nf, H* hold, uint32_t blocks_total) {
+  if (kmerge_off(src.go)) return;
+  const DsMergeSrc x = src.f[blockIdx.y];
+  const uint32_t n = kmerge_n(x);
+  const uint32_t bl = (src.f0 + blockIdx.y) * gridDim.x + blockIdx.x;  // this block among all
+  uint32_t n_used = 0, n_live = 0, n_mem = primary_used(t, bl, blocks_total);
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+    const uint32_t r = x.slot[i];
+    if (r == ~0u || !(r & kSlotOwner)) continue;
+    const uint32_t b = r & ~kSlotOwner;
+    const unsigned long long key = t.pkey[b], m = t.oth[b], hm = hold[b];
+    const uint32_t a = (uint32_t)(key & ((1u << kDsActorBits) - 1));
+    const unsigned long long ck = clock[a];
+    const uint4* op = reinterpret_cast<const uint4*>(oclocks + (size_t)a * ostride);
+    constexpr int kKF = 8;
+    unsigned long long oc[kKF];
+#pragma unroll
+    for (int q = 0; q < kKF / 2; q++) {
+      const uint4 w = (uint32_t)(2 * q) < nf ? op[q] : make_uint4(0, 0, 0, 0);
+      oc[2 * q] = ((unsigned long long)w.y << 32) | w.x;
+      oc[2 * q + 1] = ((unsigned long long)w.w << 32) | w.z;
+    }
+    n_used++;
+    bool keep = m != 0 && m > ck;  // (the current value is 0: "ours" is never the max)
+#pragma unroll
+    for (int f = 0; f < kKF; f++) keep = keep && (((hm >> f) & 1ull) || m > oc[f]);
+    for (uint32_t f = kKF; f < nf && keep; f++)
+      if (!((hm >> f) & 1ull)) keep = m > oclocks[(size_t)a * ostride + f];
+    if (keep) t.cur[b] = m;
+    t.oth[b] = 0;
+    if (hm) hold[b] = 0;
+    n_live += keep;
+  }
+#pragma unroll
+  for (int q = 32; q > 0; q >>= 1) {
+    n_used += __shfl_xor(n_used, q);
+    n_live += __shfl_xor(n_live, q);
+    n_mem += __shfl_xor(n_mem, q);
+  }
+  __shared__ uint32_t part[3][kBlock / 64];
+  if ((threadIdx.x & 63) == 0) {
+    part[0][threadIdx.x >> 6] = n_live;
+    part[1][threadIdx.x >> 6] = n_used;
+    part[2][threadIdx.x >> 6] = n_mem;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t l = 0, u = 0, mm = 0;
+    for (int w = 0; w < kBlock / 64; w++) {
+      l += part[0][w];
+      u += part[1][w];
+      mm += part[2][w];
+    }
+    kmerge_count(t, bl, l, u, mm);
   }
 }
 
@@ -1514,7 +1615,20 @@ __global__ void k_ds_kclock(unsigned long long* clock, const unsigned long long*
                             uint32_t ostride, uint32_t nf, const uint32_t* pub_src, uint32_t* pub_dst,
                             uint32_t pub_words, const uint32_t* go) {
   if (kmerge_off(go)) return;
-  if (pub_dst && blockIdx.x == 0 && threadIdx.x < pub_words) pub_dst[threadIdx.x] = pub_src[threadIdx.x];
+  if (blockIdx.x == 0) {
+    // the final pass's replicated counts summed into live[0], [1], [4] (pub_src = t.live), then
+    // live[0..pub_words) into the caller's pinned memory
+    uint32_t* live = const_cast<uint32_t*>(pub_src);
+    const uint32_t w = threadIdx.x;
+    if (w == 0 || w == 1 || w == 4) {  // replica words 0, 1, 2
+      uint32_t v = 0;
+      for (uint32_t r = 0; r < kLiveReps; r++) v += live[16 + 16 * r + (w == 4 ? 2u : w)];
+      live[w] = v;
+      if (pub_dst && w < pub_words) pub_dst[w] = v;
+    } else if (pub_dst && w < pub_words) {
+      pub_dst[w] = pub_src[w];
+    }
+  }
   for (uint32_t a = blockIdx.x * kBlock + threadIdx.x; a < ccap; a += gridDim.x * kBlock) {
     unsigned long long v = clock[a];
     for (uint32_t f = 0; f < nf; f++) {
@@ -2057,19 +2171,28 @@ hipError_t launch_ds_kmerge(hipStream_t s, DsTables t, const DsMergeSrc* d_src, 
   // 512 60.5, 256 73.1, 4096 148)
   static const uint32_t kf_cap = getenv("CE_KFINAL_BLOCKS") ? (uint32_t)atoi(getenv("CE_KFINAL_BLOCKS")) : 512u;
   const dim3 gf(blocks_for((uint64_t)t.pmask + 1, kf_cap));
-  if (nf <= 32) {  // (the buffer is zero as u64 words: its u32 view too)
-    uint32_t* h32 = reinterpret_cast<uint32_t*>(hold);
+  // into an empty table with every row's slot recorded: the final rule over the rows' owners
+  // (k_ds_kfinal_rows) instead of a scan of the whole table (CE_KFINAL_ROWS=0: the scan)
+  static const bool rows_env = !(getenv("CE_KFINAL_ROWS") && atoi(getenv("CE_KFINAL_ROWS")) == 0);
+  bool rows = rows_env && fresh && t.pmask < kSlotOwner;
+  for (uint32_t f = 0; f < nf && rows; f++) rows = h_src[f].slot != nullptr;
+  uint32_t nlaunch = 0;
+  for (uint32_t c0 = 0; c0 < nf; c0 += kMergeInline) nlaunch += std::min(kMergeInline, nf - c0);
+  const uint32_t blocks_total = gx * nlaunch;
+  auto go_hold = [&](auto* hp) {
+    using H = std::remove_pointer_t<decltype(hp)>;
     for (uint32_t c0 = 0; c0 < nf; c0 += kMergeInline)
-      hipLaunchKernelGGL(k_ds_khold<uint32_t>, dim3(gx, std::min(kMergeInline, nf - c0)), dim3(kBlock), 0, s, t, srcs(c0), h32);
-    hipLaunchKernelGGL(k_ds_kfinal<uint32_t>, gf, dim3(kBlock), 0, s, t, clock, oclocks, ostride, nf, h32, go,
-                       fresh ? 1u : 0u);
-  } else {
-    for (uint32_t c0 = 0; c0 < nf; c0 += kMergeInline)
-      hipLaunchKernelGGL(k_ds_khold<unsigned long long>, dim3(gx, std::min(kMergeInline, nf - c0)), dim3(kBlock), 0, s, t,
-                         srcs(c0), hold);
-    hipLaunchKernelGGL(k_ds_kfinal<unsigned long long>, gf, dim3(kBlock), 0, s, t, clock, oclocks, ostride, nf, hold, go,
-                       fresh ? 1u : 0u);
-  }
+      hipLaunchKernelGGL(k_ds_khold<H>, dim3(gx, std::min(kMergeInline, nf - c0)), dim3(kBlock), 0, s, t, srcs(c0), hp);
+    if (rows) {
+      for (uint32_t c0 = 0; c0 < nf; c0 += kMergeInline)
+        hipLaunchKernelGGL(k_ds_kfinal_rows<H>, dim3(gx, std::min(kMergeInline, nf - c0)), dim3(kBlock), 0, s, t,
+                           srcs(c0), clock, oclocks, ostride, nf, hp, blocks_total);
+    } else {
+      hipLaunchKernelGGL(k_ds_kfinal<H>, gf, dim3(kBlock), 0, s, t, clock, oclocks, ostride, nf, hp, go, fresh ? 1u : 0u);
+    }
+  };
+  if (nf <= 32) go_hold(reinterpret_cast<uint32_t*>(hold));  // (the buffer is zero as u64 words: its u32 view too)
+  else go_hold(hold);
   hipLaunchKernelGGL(k_ds_kclock, dim3(std::max<uint32_t>(1, blocks_for(ccap))), dim3(kBlock), 0, s, clock, oclocks,
                      ccap, ostride, nf, t.live, pub_dst, 5u, go);
   return hipGetLastError();

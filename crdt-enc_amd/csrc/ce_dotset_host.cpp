@@ -144,7 +144,7 @@ int tables_alloc(ce_core* c, uint32_t cap, const FillRange* extra = nullptr) {
   if ((e = d->mkey.reserve(mslots * 8)) || (e = d->pkey.reserve(cap * 8ull)) ||
       (e = d->cur.reserve(cap * 8ull)) || (e = d->add.reserve(cap * 8ull)) ||
       (e = d->kill.reserve(cap * 8ull)) || (e = d->oth.reserve(cap * 8ull)) ||
-      (e = d->hold.reserve(cap * 8ull)) || (e = d->live.reserve(64)))
+      (e = d->hold.reserve(cap * 8ull)) || (e = d->live.reserve(64 + 64 * 16)))  // (+ the k-way merge's count replicas)
     return ctx->hip_fail(e, "dot-set tables");
   d->pcap = cap;
   // every table cleared by one launch (eight blit fills cost a dispatch gap each)
