@@ -705,8 +705,11 @@ int orswot_fold(ce_core* c, const Counts& k, uint64_t kill_bound, bool adds_cont
   const uint64_t sub = (uint64_t)pa.parts * kDsPartReps;  // sub-runs per side
   const uint64_t cap_a = pa.parts ? k.v[kCntAddM] / sub * d->part_factor / 2 + 32 : 0,
                  cap_k = pa.parts && kill_items != ~0ull ? kill_items / sub * d->part_factor / 2 + 32 : 0;
+  // (the removal-item bound is loose for multi-entry clocks -- members x the largest file's clock
+  // entries: C3 read-context 23.6M for 2.1M actual items -- so it only caps the scratch: up to 64M
+  // items, ~1 GB of runs and overflow list, the partitioned fold takes it)
   const bool part = !getenv("CE_DS_FOLD_GLOBAL") && pa.parts >= 1 && pa.parts <= kDsPartMaxParts &&
-                    kill_items <= 4 * (k.v[kCntRmM] + k.v[kCntRmC] + kb0) + (1ull << 20) &&
+                    (kill_items <= 4 * (k.v[kCntRmM] + k.v[kCntRmC] + kb0) + (1ull << 20) || kill_items <= (1ull << 26)) &&
                     k.v[kCntAddM] + kill_items < (1ull << 31) && sub * (cap_a + cap_k) < (1ull << 31);
   if (part) {
     pa.cap[0] = (uint32_t)cap_a;
