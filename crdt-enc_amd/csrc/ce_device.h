@@ -282,7 +282,7 @@ __device__ __forceinline__ L5 block_limbs(uint32_t w0, uint32_t w1, uint32_t w2,
   m.v[1] = __builtin_amdgcn_alignbit(w1, w0, 26) & M26;
   m.v[2] = __builtin_amdgcn_alignbit(w2, w1, 20) & M26;
   m.v[3] = __builtin_amdgcn_alignbit(w3, w2, 14) & M26;
-  m.v[4] = (w3 >> 8) | (1u << 24);
+  m.v[4] = __builtin_amdgcn_alignbit(1u, w3, 8);  // (w3 >> 8) | 2^24 in one instruction
   return m;
 }
 
