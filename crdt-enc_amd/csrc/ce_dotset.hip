@@ -362,6 +362,45 @@ __device__ __forceinline__ bool fast_orswot_op(const uint8_t* p, uint64_t n, uin
     i += 43 + l + lm;
     return true;
   }
+  if (v.w[0] == 0x6d52a281u && v.w[1] == 0x6c63a582u && v.w[2] == 0x816b636fu && v.w[3] == 0x746f64a4u &&
+      (v.w[4] & 0xf0ffu) == 0x8073u && (v.w[4] & 0x0f00u) >= 0x0200u) {
+    // Rm whose clock has 2..15 entries (fixmap; crdts rm(member, read_ctx) carries the member's
+    // whole read context): each entry "c4 10 <uuid> <uint>" from its own 64-byte window, the
+    // entries' actors strictly ascending as ds_vclock requires (else the grammar takes the op and
+    // reports it for the host parse).  Proven in full first, then the sink calls ds_orswot_op
+    // would make, in the same order.
+    const uint32_t ne = (v.w[4] >> 8) & 15u;
+    uint64_t off = 18;
+    uint32_t p0 = 0, p1 = 0, p2 = 0, p3 = 0;  // the previous actor, big-endian words
+    for (uint32_t e = 0; e < ne; e++) {
+      if (off + 27 > n - i + 64) return false;  // (the window stays inside the buffer's slack)
+      const Win64<ST> w(q + off);
+      if (w.byte(0) != 0xc4u || w.byte(1) != 0x10u) return false;
+      const uint32_t u0 = __builtin_bswap32(w.word(2)), u1 = __builtin_bswap32(w.word(6)),
+                     u2 = __builtin_bswap32(w.word(10)), u3 = __builtin_bswap32(w.word(14));
+      if (e && !(u0 > p0 || (u0 == p0 && (u1 > p1 || (u1 == p1 && (u2 > p2 || (u2 == p2 && u3 > p3)))))))
+        return false;
+      p0 = u0; p1 = u1; p2 = u2; p3 = u3;
+      w.uint_at(18, &l);
+      if (!l) return false;
+      off += 18 + l;
+      if (off > n - i) return false;
+    }
+    lm = fast_members1<ST>(q + off, &mem);
+    if (!lm || off + lm > n - i) return false;
+    sink.rm_begin();
+    off = 18;
+    for (uint32_t e = 0; e < ne; e++) {
+      const Win64<ST> w(q + off);
+      ctr = w.uint_at(18, &l);
+      sink.rm_dot(i + off + 2, ctr);
+      off += 18 + l;
+    }
+    sink.rm_member(mem);
+    sink.rm_end();
+    i += off + lm;
+    return true;
+  }
   if (v.w[0] == 0x6d52a281u && v.w[1] == 0x6c63a582u && v.w[2] == 0x816b636fu &&
       v.w[3] == 0x746f64a4u && v.w[4] == 0x10c48173u) {  // Rm with a one-entry clock
     ctr = v.uint_at(36, &l);

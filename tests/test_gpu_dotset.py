@@ -708,6 +708,50 @@ def test_orswot_op_fast_path_boundaries(ctx, case):
     core.close()
 
 
+@pytest.mark.parametrize("case", ["ascending", "unordered", "repeated", "cut", "signed"])
+def test_orswot_multi_entry_clock_fast_path(ctx, case):
+    """Removals whose clock carries the member's read context (2..15 entries, crdts
+    rm(member, read_ctx)) are proven by the lane decode's window path (fast_orswot_op) -- every
+    uint width, entry counts 2..15 -- and anything it must not take goes to the grammar from the
+    same op: actors out of order or repeated (ds_vclock reports those for the host parse), a file
+    cut inside an entry, a signed counter marker.  All == the oracle."""
+    rng = random.Random(sum(map(ord, case)) + 77)
+    key = rng.randbytes(32)
+    actors = sorted(rng.randbytes(16) for _ in range(16))
+    widths = ["fix", "cc", "cd", "ce", "cf"]
+    lim = {"fix": 128, "cc": 256, "cd": 65536, "ce": 1 << 32, "cf": 1 << 64}
+    clears, fa, fv = [], [], []
+    for a in range(4):
+        for v in range(4):
+            ops = []
+            for j in range(12):
+                cw = widths[(j + v + a) % 5]
+                if j % 3 == 0:
+                    ops.append(_add(actors[a], 64 * v + j + 1, [rng.randrange(0, 40)], "cc", "fix"))
+                    continue
+                ne = 2 + (j * 5 + v + a) % 14
+                sel = sorted(rng.sample(range(16), ne))
+                clock = [(actors[k], rng.randrange(1, lim[cw])) for k in sel]
+                if case == "unordered" and j == 4 and v % 2 == 0:
+                    clock[0], clock[-1] = clock[-1], clock[0]
+                if case == "repeated" and j == 5 and v % 2 == 1:
+                    clock[1] = (clock[0][0], clock[1][1])
+                op = _rm(clock, [rng.randrange(0, 40)], cw, "fix")
+                if case == "signed" and j == 7:
+                    op = op.replace(b"\xc4\x10" + clock[1][0] + _u(clock[1][1], cw),
+                                    b"\xc4\x10" + clock[1][0] + b"\xd2" + (5).to_bytes(4, "big"), 1)
+                ops.append(op)
+            body = _arr(len(ops)) + b"".join(ops)
+            if case == "cut" and a == 2 and v == 1:
+                body = body[:-25]
+            clears.append(APP + body)
+            fa.append(a)
+            fv.append(v)
+    core, oc = new_core(ctx, "orswot", key), C.Core("orswot")
+    check_ops(ctx, "orswot", key, core, oc, actors[:4], clears, fa, fv)
+    core.close()
+
+
 @pytest.mark.parametrize("kind", ["orswot", "mvreg", "gcounter"])
 def test_state_bytes_and_merge_device(ctx, kind):
     """The dot-set exchange without a host hop (shard.reduce_dotset): ce_core_state_bytes_device
