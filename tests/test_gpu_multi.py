@@ -26,7 +26,7 @@ def _port():
 
 def test_bench_two_ranks_share_gpu():
     """bench.py --gpus 2 as the driver's scaling run would start it (here: gloo, both ranks on
-    the one GPU): the weak C2 line, the strong C2 leg, and C3 / C4 / C5 at N = 2 under `configs`,
+    the one GPU): the weak C2 line, the strong C2 leg, and C3 / C3r / C4 / C5 at N = 2 under `configs`,
     each with every check true (small sizes: --quick)."""
     env = dict(os.environ, CE_BENCH_SHARE_GPU="1", CE_DIST_BACKEND="gloo")
     env.pop("WORLD_SIZE", None)
@@ -40,7 +40,7 @@ def test_bench_two_ranks_share_gpu():
     assert "dense" in line["config"]["parallelism"]
     st = line["strong"]
     assert st["scaling"] == "strong" and st["state_check"].endswith("ok") and st["files_total"] == 4096 * 2
-    for c in ("c3", "c4", "c5"):
+    for c in ("c3", "c3r", "c4", "c5"):
         cl = line["configs"][c]
         assert cl["n_gpus"] == 2 and cl["scaling"] == "strong", (c, cl)
         assert cl["checks"] and all(cl["checks"].values()), (c, cl["checks"])
@@ -49,6 +49,9 @@ def test_bench_two_ranks_share_gpu():
     # C3's removals name the writer's own adds: no deferred removal, the partials go as columns
     assert line["configs"]["c3"]["exchange"]["per_hop_ms_max_over_ranks"]["exchange"] == "columns"
     assert line["configs"]["c5"]["config"]["path"] == "rejected"
+    # read-context removals (c3r): writer shards defer removals naming the other shard's dots;
+    # they travel in the columns' deferred section, still one merge on rank 0
+    assert line["configs"]["c3r"]["exchange"]["per_hop_ms_max_over_ranks"]["exchange"] == "columns"
 
 
 @pytest.mark.parametrize("mode,path", [("registered", "dense"), ("unregistered", "bytes")])
