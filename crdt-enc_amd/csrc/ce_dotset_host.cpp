@@ -2962,7 +2962,8 @@ int ds_merge_columns_device(ce_core* c, const uint8_t* const* parts, const uint6
         x.n_ent = q[4 * qi + 1];
         x.n_mem = q[4 * qi + 2];
         qi++;
-        if (x.n_rm > hd[f].dlen || x.n_ent > hd[f].dlen || x.n_mem > hd[f].dlen)
+        if (x.n_rm > hd[f].dlen || x.n_ent > hd[f].dlen || x.n_mem > hd[f].dlen || x.n_rm >= (1ull << 31) ||
+            x.n_ent >= (1ull << 31) || x.n_mem >= (1ull << 31))  // (the kernels index them in 32 bits)
           return ctx->fail(CE_ERR_DECODE, "column partial: deferred map");
         x.L = DefLayout(x.n_rm, x.n_ent, x.n_mem);
         if (x.L.len != hd[f].dlen) return ctx->fail(CE_ERR_DECODE, "column partial: deferred map");
