@@ -167,9 +167,14 @@ hipError_t launch_ds_finalize(hipStream_t s, DsTables t);
 // zeroed by the apply that reads it; ovf_n by parity (the apply of fold g zeroes fold g + 1's).
 // live[0] += change of the live-pair count (two's complement), live[1] += pairs inserted, live[5]
 // = items that overflowed; K1 zeroes live[0], live[1], live[3] and live[4].
-static constexpr uint32_t kDsPartChunk = 8192;      // adds / removals per K1 block (one trip)
+#ifndef CE_PART_BATCH
+#define CE_PART_BATCH 4  // K1 items per lane whose loads are issued before any is used (same box
+                         // at C3: 8 -> 4 k_ds_part_adds 62.7 -> 49.7 us, more lanes in flight; 2: 48.8
+                         // but the rest of the fold slower)
+#endif
+static constexpr uint32_t kDsPartChunk = 1024 * CE_PART_BATCH;  // adds / removals per 1024-thread K1 block
 static constexpr uint32_t kDsPartThreadsSmall = 512;  // the half-size K1 blocks (CE_DS_PART_SMALL)
-static constexpr uint32_t kDsPartChunkSmall = 4096;
+static constexpr uint32_t kDsPartChunkSmall = 512 * CE_PART_BATCH;
 static constexpr uint32_t kDsPartReps = 8;          // sub-runs per partition and side (K1 block % 8)
 static constexpr uint32_t kDsPartMaxParts = 16384;  // LDS histogram bound (64 KB)
 struct DsKillSrc {

@@ -880,7 +880,7 @@ __device__ __forceinline__ unsigned long long member_handle(const DsTables& t, u
   return member_find(t, m, insert);
 }
 
-constexpr int kPartBatch = 8;  // items per lane whose loads are issued before any is used
+constexpr int kPartBatch = CE_PART_BATCH;  // items per lane whose loads are issued before any is used
 static_assert(kDsPartChunk == kPartThreads * kPartBatch, "K1 walks its chunk in one trip");
 static_assert(kDsPartChunkSmall == kDsPartThreadsSmall * kPartBatch, "K1 walks its chunk in one trip");
 

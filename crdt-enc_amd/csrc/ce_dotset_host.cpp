@@ -686,15 +686,15 @@ int orswot_fold(ce_core* c, const Counts& k, uint64_t kill_bound, bool adds_cont
   uint32_t* live = d->live.as<uint32_t>();
   DsPartArgs pa{};
   pa.parts = d->pcap >> kDsPartBits;
-  // K1 block size (CE_DS_PART_THREADS: 1024, 512 or 256; 8 items per thread): 512 by default --
-  // C3's 1.7M adds are then ~415 blocks, every CU busy (1024: ~207 blocks on 256 CUs; same box
-  // k_ds_part_adds 80 -> 62 us)
+  // K1 block size (CE_DS_PART_THREADS: 1024, 512 or 256; CE_PART_BATCH items per thread): 512 by
+  // default -- with 8 items per thread C3's 1.7M adds were ~415 blocks, every CU busy (1024: ~207
+  // blocks on 256 CUs; same box k_ds_part_adds 80 -> 62 us), with 4 ~830 blocks (49.7 us)
   static const uint32_t k1_threads = [] {
     const char* v = getenv("CE_DS_PART_THREADS");
     const uint32_t t = v ? (uint32_t)atoi(v) : (getenv("CE_DS_PART_SMALL") && atoi(getenv("CE_DS_PART_SMALL")) == 0 ? 1024u : 512u);
     return t == 1024u || t == 256u ? t : 512u;
   }();
-  pa.chunk = k1_threads == 1024u ? kDsPartChunk : k1_threads == 512u ? kDsPartChunkSmall : 256u * 8u;
+  pa.chunk = k1_threads == 1024u ? kDsPartChunk : k1_threads == 512u ? kDsPartChunkSmall : 256u * CE_PART_BATCH;
   pa.kchunk = pa.chunk / 4;  // removals are ~1/4 of C3's ops: as many blocks
   pa.ba = (uint32_t)((na + pa.chunk - 1) / pa.chunk);
   pa.bk0 = (uint32_t)((nr + pa.kchunk - 1) / pa.kchunk);
