@@ -219,6 +219,20 @@ def test_orswot_kway_state_merge(ctx, p_rm, primary):
         os.environ.pop("CE_DS_PRIMARY_SLOTS", None)
 
 
+def test_orswot_kway_final_rows_form():
+    """The k-way merge's opt-in final pass over the rows' pair owners (CE_KFINAL_ROWS=1,
+    k_ds_kfinal_rows: taken for merges into an empty table) == the oracle, through the same
+    k-way test in a child process (the switch is read once per process)."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, CE_KFINAL_ROWS="1")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", "-m", "gpu",
+                        "tests/test_gpu_dotset.py::test_orswot_kway_state_merge"], cwd=repo, env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "passed" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
+
+
 def _kway_state_merge(ctx, p_rm):
     rng = random.Random(91 + int(p_rm * 100))
     key = rng.randbytes(32)

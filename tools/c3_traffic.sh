@@ -16,7 +16,7 @@ python3 - $O <<'PY'
 import csv, glob, json, sys
 o = sys.argv[1]
 names = ("k_ds_applied", "k_ds_add_pairs", "k_ds_kill", "k_ds_emit", "k_ds_count", "k_ds_collect", "k_ds_finalize",
-         "k_ds_contig", "k_ser_write", "k_ds_kfinal", "k_ds_kput", "k_ds_khold", "k_ds_untile", "k_fill",
+         "k_ds_contig", "k_ser_write", "k_ds_kfinal_rows", "k_ds_kfinal", "k_ds_kput", "k_ds_khold", "k_ds_untile", "k_fill",
          "k_ds_part_adds", "k_ds_part_kills", "k_ds_part_scatter", "k_ds_part_apply", "k_ds_clock",
          "k_open_fold_v2", "k_open_setup", "k_ser_key", "k_ser_unpack", "k_ser_len", "k_rdm_count", "k_rdm_write",
          "k_sort_hist", "k_sort_pass", "k_ser_head_tiles", "k_ser_head_apply")
